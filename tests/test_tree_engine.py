@@ -1,0 +1,115 @@
+"""Tree engine: host kernels vs a brute-force reference, and HIP kernels vs host kernels."""
+import numpy as np
+import pytest
+import torch
+
+from transmogrifai_amd.models import tree_engine as te
+
+
+def _data(N=3000, F=10, B=32, seed=0, missing=False):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randint(0, B - (1 if missing else 0), (N, F), dtype=torch.uint8, generator=g)
+    if missing:
+        m = torch.rand(N, F, generator=g) < 0.2
+        X[m] = B - 1
+    y = ((X[:, 0].float() + 0.5 * X[:, 3].float() + 3 * torch.randn(N, generator=g)) > 20).float()
+    return X, y
+
+
+def _brute_root(X, y, B):
+    best = (-1, None, None)
+    N, F = X.shape
+    tot = np.array([(y == 0).sum(), (y == 1).sum()], float)
+    gini = lambda c: 1 - ((c / c.sum()) ** 2).sum() if c.sum() > 0 else 0
+    pg = gini(tot)
+    for f in range(F):
+        for b in range(B - 1):
+            left = X[:, f] <= b
+            lc = np.array([((y == 0) & left).sum(), ((y == 1) & left).sum()], float)
+            rc = tot - lc
+            if lc.sum() < 1 or rc.sum() < 1:
+                continue
+            g = pg - lc.sum() / N * gini(lc) - rc.sum() / N * gini(rc)
+            if g > best[0] + 1e-12:
+                best = (g, f, b)
+    return best
+
+
+def test_root_split_matches_bruteforce():
+    X, y = _data()
+    jobs = [te.TreeJob(0, te.TreeParams(max_depth=1), torch.arange(X.shape[0]))]
+    f = te.grow_forest(X, np.full(X.shape[1], 32), jobs, mode=te.MODE_CLS, kind=te.KIND_GINI, y=y, B=32)
+    g, bf, bb = _brute_root(X.numpy(), y.numpy(), 32)
+    assert f.nodes[0, 0] == bf and f.nodes[0, 1] == bb
+    assert abs(f.gain[0] - g) < 1e-6
+
+
+def test_predict_consistency_and_leaf_rows():
+    X, y = _data(N=2000)
+    jobs = [te.TreeJob(0, te.TreeParams(max_depth=5, min_instances=3), torch.arange(2000))]
+    f = te.grow_forest(X, np.full(X.shape[1], 32), jobs, mode=te.MODE_CLS, kind=te.KIND_GINI, y=y, B=32)
+    p = te.forest_predict(f, X, [None], [[0]])[0]
+    assert p.shape == (2000, 2)
+    assert torch.allclose(p.sum(1), torch.ones(2000))
+    # the leaf distribution equals the empirical label mix of the rows routed there
+    nodes = f.nodes
+    leaf = np.zeros(2000, np.int64)
+    Xn = X.numpy()
+    for i in range(2000):
+        k = 0
+        while nodes[k, 2] >= 0:
+            k = nodes[k, 2] if Xn[i, nodes[k, 0]] <= nodes[k, 1] else nodes[k, 3]
+        leaf[i] = k
+    for k in np.unique(leaf):
+        m = leaf == k
+        assert abs(y.numpy()[m].mean() - f.value[k, 1]) < 1e-5
+
+
+def test_min_instances_respected():
+    X, y = _data(N=1500)
+    jobs = [te.TreeJob(0, te.TreeParams(max_depth=8, min_instances=50), torch.arange(1500))]
+    f = te.grow_forest(X, np.full(X.shape[1], 32), jobs, mode=te.MODE_CLS, kind=te.KIND_GINI, y=y, B=32)
+    assert (f.cover >= 50 - 1e-6).all()
+
+
+def _grow_all(dev, mode, missing=False, subset=None, n_models=2):
+    X, y = _data(missing=missing)
+    N = X.shape[0]
+    B = 32
+    g = torch.Generator().manual_seed(1)
+    t1 = torch.round(torch.randn(n_models, N, generator=g) * 8) / 8
+    t2 = torch.full((n_models, N), 0.25)
+    jobs = []
+    for m in range(n_models):
+        rows = torch.arange(N)[torch.arange(N) % (m + 2) != 0]
+        w = torch.randint(0, 3, (rows.numel(),), generator=g) if mode == te.MODE_CLS else None
+        jobs.append(te.TreeJob(m, te.TreeParams(max_depth=6, min_instances=2, reg_lambda=1.0,
+                                                min_child_weight=0.5, feature_subset=subset), rows, w))
+    kind = {te.MODE_CLS: te.KIND_GINI, te.MODE_VAR: te.KIND_VARIANCE, te.MODE_GH: te.KIND_NEWTON}[mode]
+    f = te.grow_forest(X.to(dev), np.full(X.shape[1], B - 1 if missing else B), [
+        te.TreeJob(j.model, j.params, j.rows.to(dev), None if j.weights is None else j.weights.to(dev)) for j in jobs],
+        mode=mode, kind=kind, y=y.to(dev), t1=t1.to(dev), t2=t2.to(dev), B=B,
+        missing_bin=(B - 1) if missing else -1, rng_seed=3, chunk_rows=512)
+    preds = te.forest_predict(f, X.to(dev), [None, torch.arange(0, N, 3).to(dev)], [[0], [1]])
+    return f, [p.cpu() for p in preds]
+
+
+@pytest.mark.parametrize("mode", [te.MODE_CLS, te.MODE_VAR, te.MODE_GH])
+def test_cpu_engine_runs_all_modes(mode):
+    f, preds = _grow_all("cpu", mode, missing=(mode == te.MODE_GH))
+    assert f.n_trees == 2 and len(f.nodes) > 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,missing,subset", [(te.MODE_CLS, False, None), (te.MODE_CLS, False, 4),
+                                                 (te.MODE_VAR, False, None), (te.MODE_GH, True, None)])
+def test_hip_engine_matches_host(mode, missing, subset):
+    fc, pc = _grow_all("cpu", mode, missing, subset)
+    fg, pg = _grow_all("cuda", mode, missing, subset)
+    np.testing.assert_array_equal(fc.tree_off, fg.tree_off)
+    np.testing.assert_array_equal(fc.nodes, fg.nodes)
+    np.testing.assert_allclose(fc.value, fg.value, rtol=1e-5, atol=1e-5)
+    for a, b in zip(pc, pg):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+    from transmogrifai_amd.ops import _native
+    assert _native.hip_loaded()

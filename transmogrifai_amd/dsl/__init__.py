@@ -1,0 +1,52 @@
+"""Feature DSL: typed methods available on features (``core/.../dsl/Rich*Feature.scala``).
+
+Methods are registered per feature type and resolved dynamically by ``FeatureLike.__getattr__``, so
+``age.fill_missing_with_mean().z_normalize()``, ``sex.pivot()``, ``label.sanity_check(vec)`` work as in
+the reference DSL. Collection helpers (``transmogrify``, ``combine``) are module-level functions.
+"""
+_REGISTRY = {}
+_loaded = False
+
+
+def register(types, name):
+    def deco(fn):
+        for t in (types if isinstance(types, (list, tuple)) else [types]):
+            _REGISTRY.setdefault(name, []).append((t, fn))
+        return fn
+    return deco
+
+
+def _ensure():
+    global _loaded
+    if not _loaded:
+        _loaded = True
+        from . import core  # noqa: F401
+
+
+def lookup(wtype, name):
+    if name.startswith("__"):
+        return None
+    _ensure()
+    for t, fn in _REGISTRY.get(name, []):
+        if issubclass(wtype, t):
+            return fn
+    return None
+
+
+def binary_op(a, b, op, reverse=False):
+    _ensure()
+    from .core import _binary_op
+    return _binary_op(a, b, op, reverse)
+
+
+def transmogrify(features, label=None, defaults=None):
+    from ..stages.feature.transmogrifier import TransmogrifierDefaults, transmogrify_combined
+    return transmogrify_combined(list(features), label, defaults or TransmogrifierDefaults)
+
+
+def combine(*vectors):
+    from ..stages.feature.vectorizers import VectorsCombiner
+    vs = []
+    for v in vectors:
+        vs.extend(v if isinstance(v, (list, tuple)) else [v])
+    return VectorsCombiner().set_input(vs).get_output()

@@ -1,0 +1,369 @@
+"""DSL method implementations (``RichNumericFeature``, ``RichTextFeature``, ``RichDateFeature``,
+``RichListFeature``, ``RichSetFeature``, ``RichMapFeature``, ``RichVectorFeature``, ``RichLocationFeature``)."""
+from __future__ import annotations
+
+from typing import Callable, Optional, Sequence
+
+from ..features import types as T
+from ..features.feature import FeatureLike
+from ..stages.base import BinaryTransformer, UnaryTransformer
+from ..stages.feature import math_stages as M
+from ..stages.feature import text_stages as TS
+from ..stages.feature import vectorizers as V
+from ..stages.feature.transmogrifier import TransmogrifierDefaults as D
+from . import register
+
+NUM = (T.OPNumeric,)
+
+
+def _others(f, others):
+    return [f] + list(others or [])
+
+
+# ------------------------------------------------------------------------------------- generic
+@register(T.FeatureType, "map")
+def _map(self: FeatureLike, fn: Callable, output_type=T.Text, operation_name: str = "map"):
+    st = UnaryTransformer(lambda v: fn(v), operation_name=operation_name, output_type=output_type)
+    return st.set_input(self).get_output()
+
+
+@register(T.FeatureType, "alias")
+def _alias(self, name: str):
+    st = UnaryTransformer(lambda v: v, operation_name="alias", output_type=self.wtype)
+    st.set_input(self)
+    st.set_output_feature_name(name)
+    return st.get_output()
+
+
+@register(T.FeatureType, "exists")
+def _exists(self, fn: Callable):
+    st = UnaryTransformer(lambda v: None if v is None else bool(fn(v)), operation_name="exists",
+                          output_type=T.Binary)
+    return st.set_input(self).get_output()
+
+
+@register(T.FeatureType, "filter")
+def _filter(self, fn: Callable, default=None):
+    st = UnaryTransformer(lambda v: v if (v is not None and fn(v)) else default, operation_name="filter",
+                          output_type=self.wtype)
+    return st.set_input(self).get_output()
+
+
+@register(T.FeatureType, "replace_with")
+def _replace(self, old, new):
+    st = UnaryTransformer(lambda v: new if v == old else v, operation_name="replaceWith", output_type=self.wtype)
+    return st.set_input(self).get_output()
+
+
+@register(T.FeatureType, "to_occur")
+def _to_occur(self, match_fn: Optional[Callable] = None):
+    def occ(v):
+        if match_fn is not None:
+            return 1.0 if (v is not None and match_fn(v)) else 0.0
+        if v is None:
+            return 0.0
+        if isinstance(v, (list, set, frozenset, dict)):
+            return 1.0 if len(v) else 0.0
+        if isinstance(v, (int, float)) and not isinstance(v, bool):
+            return 1.0 if v > 0 else 0.0
+        if isinstance(v, bool):
+            return 1.0 if v else 0.0
+        return 1.0 if str(v) else 0.0
+    st = UnaryTransformer(occ, operation_name="toOccur", output_type=T.RealNN)
+    return st.set_input(self).get_output()
+
+
+# ------------------------------------------------------------------------------------- numeric
+def _binary_op(a, b, op, reverse=False):
+    if isinstance(b, FeatureLike):
+        x, y = (b, a) if reverse else (a, b)
+        return M.BinaryMathTransformer(op).set_input(x, y).get_output()
+    return M.ScalarMathTransformer(op, float(b), reverse).set_input(a).get_output()
+
+
+for _op in ("abs", "ceil", "floor", "round", "exp", "sqrt"):
+    def _mk(op):
+        def f(self):
+            return M.UnaryMathTransformer(op).set_input(self).get_output()
+        return f
+    register(NUM, _op)(_mk(_op))
+
+
+@register(NUM, "log")
+def _log(self, base: float = 2.718281828459045):
+    return M.UnaryMathTransformer("log", base=base).set_input(self).get_output()
+
+
+@register(NUM, "power")
+def _power(self, p: float):
+    return M.ScalarMathTransformer("power", p).set_input(self).get_output()
+
+
+@register(NUM, "round_digits")
+def _round_digits(self, digits: int):
+    return M.UnaryMathTransformer("roundDigits", digits=digits).set_input(self).get_output()
+
+
+@register(NUM, "fill_missing_with_mean")
+def _fill_mean(self, default: float = 0.0):
+    return M.FillMissingWithMean(default_value=default).set_input(self).get_output()
+
+
+@register(NUM, "z_normalize")
+def _znorm(self):
+    return M.OpScalarStandardScaler().set_input(self).get_output()
+
+
+@register(NUM, "to_percentile")
+def _pct(self, buckets: int = 100):
+    return M.PercentileCalibrator(expected_num_buckets=buckets).set_input(self).get_output()
+
+
+@register(NUM, "scale")
+def _scale(self, scaling_type: str = "Linear", slope: float = 1.0, intercept: float = 0.0):
+    return M.ScalerTransformer(scaling_type=scaling_type, slope=slope, intercept=intercept).set_input(self).get_output()
+
+
+@register(NUM, "bucketize")
+def _bucketize(self, splits: Sequence[float], track_nulls: bool = True, track_invalid: bool = False,
+               split_inclusion: str = "Left", bucket_labels=None):
+    return M.NumericBucketizer(splits=list(splits), track_nulls=track_nulls, track_invalid=track_invalid,
+                               split_inclusion=split_inclusion, bucket_labels=bucket_labels).set_input(self).get_output()
+
+
+@register(NUM, "auto_bucketize")
+def _auto_bucketize(self, label: FeatureLike, track_nulls: bool = True, track_invalid: bool = False,
+                    min_info_gain: float = 0.01):
+    from ..stages.feature.bucketizers import DecisionTreeNumericBucketizer
+    return DecisionTreeNumericBucketizer(track_nulls=track_nulls, track_invalid=track_invalid,
+                                         min_info_gain=min_info_gain).set_input(label, self).get_output()
+
+
+@register(T.RealNN, "to_isotonic_calibrated")
+def _iso(self, label: FeatureLike, isotonic: bool = True):
+    return M.IsotonicRegressionCalibrator(isotonic=isotonic).set_input(label, self).get_output()
+
+
+@register((T.Real, T.Currency, T.Percent), "vectorize")
+def _vec_real(self, fill_value: float = 0.0, fill_with_mean: bool = True, track_nulls: bool = True, others=(),
+              label: Optional[FeatureLike] = None, **kw):
+    if self.wtype is T.RealNN and not others:
+        return V.RealNNVectorizer().set_input(self).get_output()
+    st = V.RealVectorizer(track_nulls=track_nulls, fill_value=float(fill_value))
+    if fill_with_mean:
+        st.set_fill_with_mean()
+    out = st.set_input(_others(self, others)).get_output()
+    if label is None:
+        return out
+    from ..stages.feature.bucketizers import DecisionTreeNumericBucketizer
+    bs = [DecisionTreeNumericBucketizer(track_nulls=track_nulls).set_input(label, f).get_output()
+          for f in _others(self, others)]
+    return V.VectorsCombiner().set_input([out] + bs).get_output()
+
+
+@register(T.RealNN, "vectorize")
+def _vec_realnn(self, others=(), **kw):
+    return V.RealNNVectorizer().set_input(_others(self, others)).get_output()
+
+
+@register(T.Integral, "vectorize")
+def _vec_int(self, fill_value: float = 0.0, fill_with_mode: bool = True, track_nulls: bool = True, others=(),
+             label=None, **kw):
+    st = V.IntegralVectorizer(track_nulls=track_nulls, fill_value=float(fill_value))
+    if fill_with_mode:
+        st.set_fill_with_mode()
+    return st.set_input(_others(self, others)).get_output()
+
+
+@register(T.Binary, "vectorize")
+def _vec_bin(self, fill_value: bool = False, track_nulls: bool = True, others=(), **kw):
+    return V.BinaryVectorizer(fill_value=fill_value, track_nulls=track_nulls).set_input(_others(self, others)).get_output()
+
+
+@register(T.RealNN, "sanity_check")
+def _sanity(self, features: FeatureLike, check_sample: float = 1.0, sample_seed: int = 42,
+            sample_lower_limit: int = 1000, sample_upper_limit: int = 1_000_000, max_correlation: float = 0.95,
+            min_correlation: float = 0.0, min_variance: float = 1e-5, max_cramers_v: float = 0.95,
+            remove_bad_features: bool = False, remove_feature_group: bool = True,
+            protect_text_shared_hash: bool = False, max_rule_confidence: float = 1.0,
+            min_required_rule_support: float = 1.0, correlation_type: str = "pearson",
+            feature_feature_corr_level: str = "Computed", categorical_label: Optional[bool] = None,
+            max_feature_correlation: float = 0.99, correlation_exclusion: str = "NoExclusion"):
+    from ..stages.preparators.sanity_checker import SanityChecker
+    st = SanityChecker(check_sample=check_sample, sample_seed=sample_seed, sample_lower_limit=sample_lower_limit,
+                       sample_upper_limit=sample_upper_limit, max_correlation=max_correlation,
+                       min_correlation=min_correlation, min_variance=min_variance, max_cramers_v=max_cramers_v,
+                       remove_bad_features=remove_bad_features, remove_feature_group=remove_feature_group,
+                       protect_text_shared_hash=protect_text_shared_hash, max_rule_confidence=max_rule_confidence,
+                       min_required_rule_support=min_required_rule_support, correlation_type=correlation_type,
+                       feature_feature_corr_level=feature_feature_corr_level, categorical_label=categorical_label,
+                       max_feature_correlation=max_feature_correlation, correlation_exclusion=correlation_exclusion)
+    return st.set_input(self, features).get_output()
+
+
+# ---------------------------------------------------------------------------------------- text
+@register(T.Text, "pivot")
+def _pivot(self, others=(), top_k: int = 20, min_support: int = 10, clean_text: bool = True,
+           track_nulls: bool = True, max_pct_cardinality: float = 1.0, unseen_name: str = "OTHER"):
+    return V.OpTextPivotVectorizer(top_k=top_k, min_support=min_support, clean_text=clean_text,
+                                   track_nulls=track_nulls, max_pct_cardinality=max_pct_cardinality,
+                                   unseen_name=unseen_name).set_input(_others(self, others)).get_output()
+
+
+@register(T.Text, "smart_vectorize")
+def _smart(self, max_categorical_cardinality: int = 30, num_hashes: int = 512, track_nulls: bool = True,
+           others=(), hash_space_strategy: str = "auto", min_token_length: int = 1, to_lowercase: bool = True,
+           prepend_feature_name: bool = True, track_text_len: bool = False, **kw):
+    return V.SmartTextVectorizer(max_cardinality=max_categorical_cardinality, num_features=num_hashes,
+                                 track_nulls=track_nulls, hash_space_strategy=hash_space_strategy,
+                                 min_token_length=min_token_length, to_lowercase=to_lowercase,
+                                 prepend_feature_name=prepend_feature_name, track_text_len=track_text_len
+                                 ).set_input(_others(self, others)).get_output()
+
+
+@register(T.Text, "vectorize")
+def _vec_text(self, num_terms: int = 512, binary: bool = False, others=(), auto_detect_language: bool = False,
+              min_token_length: int = 1, to_lowercase: bool = True, hash_space_strategy: str = "auto",
+              prepend_feature_name: bool = True, top_k: int = 20, min_support: int = 10, clean_text: bool = True,
+              track_nulls: bool = True, **kw):
+    if self.wtype in (T.Text, T.TextArea):
+        toks = [TS.TextTokenizer(min_token_length=min_token_length, to_lowercase=to_lowercase)
+                .set_input(f).get_output() for f in _others(self, others)]
+        return V.OPCollectionHashingVectorizer(num_features=num_terms, binary_freq=binary,
+                                               hash_space_strategy=hash_space_strategy,
+                                               prepend_feature_name=prepend_feature_name).set_input(toks).get_output()
+    return _pivot(self, others, top_k, min_support, clean_text, track_nulls)
+
+
+@register(T.Text, "tokenize")
+def _tokenize(self, to_lowercase: bool = True, min_token_length: int = 1, strip_html: bool = False, **kw):
+    return TS.TextTokenizer(to_lowercase=to_lowercase, min_token_length=min_token_length,
+                            strip_html=strip_html).set_input(self).get_output()
+
+
+@register(T.Email, "to_email_domain")
+def _email_domain(self):
+    return TS.TextMapTransformer("EmailDomainToPickList", T.Text).set_input(self).get_output()
+
+
+@register(T.Email, "to_email_prefix")
+def _email_prefix(self):
+    return TS.TextMapTransformer("EmailPrefixToText", T.Text).set_input(self).get_output()
+
+
+@register(T.Email, "is_valid_email")
+def _valid_email(self):
+    return TS.ValidEmailTransformer().set_input(self).get_output()
+
+
+@register(T.URL, "to_domain")
+def _url_domain(self):
+    return TS.TextMapTransformer("URLDomainToText", T.Text).set_input(self).get_output()
+
+
+@register(T.URL, "to_protocol")
+def _url_proto(self):
+    return TS.TextMapTransformer("URLProtocolToText", T.Text).set_input(self).get_output()
+
+
+@register(T.Phone, "is_valid_phone_default_country")
+def _phone_valid(self, default_region: str = "US", is_strict: bool = False):
+    return TS.PhoneValidator(default_region=default_region, strict=is_strict).set_input(self).get_output()
+
+
+@register(T.Base64, "detect_mime_types")
+def _mime(self):
+    return TS.TextMapTransformer("MimeTypeDetector", T.Text).set_input(self).get_output()
+
+
+@register(T.Text, "text_len")
+def _text_len(self, others=()):
+    return TS.TextLenTransformer().set_input(_others(self, others)).get_output()
+
+
+@register(T.Text, "indexed")
+def _indexed(self, unseen_name: str = "UnseenLabel", handle_invalid: str = "NoFilter"):
+    from ..stages.feature.indexers import OpStringIndexerNoFilter
+    return OpStringIndexerNoFilter(unseen_name=unseen_name).set_input(self).get_output()
+
+
+# --------------------------------------------------------------------------------- collections
+@register(T.TextList, "tf")
+def _tf(self, num_terms: int = 512, binary: bool = False):
+    return TS.OpHashingTF(num_features=num_terms, binary=binary).set_input(self).get_output()
+
+
+@register(T.TextList, "tfidf")
+def _tfidf(self, num_terms: int = 512, binary: bool = False, min_doc_freq: int = 0):
+    return TS.IDF(min_doc_freq=min_doc_freq).set_input(_tf(self, num_terms, binary)).get_output()
+
+
+@register(T.TextList, "vectorize")
+def _vec_tl(self, num_terms: int = 512, binary: bool = False, min_doc_freq: int = 0, others=()):
+    vs = [_tfidf(f, num_terms, binary, min_doc_freq) for f in _others(self, others)]
+    return V.VectorsCombiner().set_input(vs).get_output() if len(vs) > 1 else vs[0]
+
+
+@register((T.OPList, T.OPSet, T.OPMap), "hash_vectorize")
+def _hash_vec(self, num_terms: int = 512, binary: bool = False, others=()):
+    return V.OPCollectionHashingVectorizer(num_features=num_terms, binary_freq=binary).set_input(
+        _others(self, others)).get_output()
+
+
+@register(T.MultiPickList, "vectorize")
+def _vec_mpl(self, top_k: int = 20, min_support: int = 10, clean_text: bool = True, track_nulls: bool = True,
+             others=(), **kw):
+    return V.OpSetVectorizer(top_k=top_k, min_support=min_support, clean_text=clean_text,
+                             track_nulls=track_nulls).set_input(_others(self, others)).get_output()
+
+
+@register(T.MultiPickList, "pivot")
+def _pivot_mpl(self, **kw):
+    return _vec_mpl(self, **kw)
+
+
+@register((T.Date, T.DateList), "vectorize")
+def _vec_date(self, date_list_pivot: str = "SinceLast", reference_date=None, track_nulls: bool = True,
+              circular_date_reps=D.CircularDateRepresentations, others=()):
+    fs = _others(self, others)
+    since = V.DateListVectorizer(pivot=date_list_pivot, reference_date=reference_date,
+                                 track_nulls=track_nulls).set_input(fs).get_output()
+    if issubclass(self.wtype, T.DateList) or not circular_date_reps:
+        return since
+    circ = [V.DateToUnitCircleTransformer(time_period=p).set_input(fs).get_output() for p in circular_date_reps]
+    return V.VectorsCombiner().set_input(circ + [since]).get_output()
+
+
+@register(T.Date, "to_unit_circle")
+def _unit_circle(self, time_period: str = "HourOfDay", others=()):
+    return V.DateToUnitCircleTransformer(time_period=time_period).set_input(_others(self, others)).get_output()
+
+
+@register(T.Geolocation, "vectorize")
+def _vec_geo(self, fill_with_mean: bool = True, track_nulls: bool = True, others=(), **kw):
+    return V.GeolocationVectorizer(fill_with_constant=not fill_with_mean, track_nulls=track_nulls).set_input(
+        _others(self, others)).get_output()
+
+
+@register(T.OPMap, "vectorize")
+def _vec_map(self, others=(), **kw):
+    from ..stages.feature.maps import map_vectorize
+    return map_vectorize(self.wtype, _others(self, others), None, D)[0]
+
+
+@register(T.OPVector, "drop_indices_by")
+def _drop_indices_by(self, match_fn: Callable):
+    from ..stages.feature.vector_stages import DropIndicesByTransformer
+    return DropIndicesByTransformer(match_fn).set_input(self).get_output()
+
+
+@register(T.OPVector, "filter_min_variance")
+def _min_var(self, min_variance: float = 1e-5, remove_bad_features: bool = True):
+    from ..stages.preparators.min_variance import MinVarianceFilter
+    return MinVarianceFilter(min_variance=min_variance, remove_bad_features=remove_bad_features).set_input(
+        self).get_output()
+
+
+@register(T.OPVector, "combine")
+def _combine(self, *others):
+    return V.VectorsCombiner().set_input([self] + list(others)).get_output()

@@ -1,0 +1,273 @@
+"""Evaluators and the ``Evaluators`` factory.
+
+Reference: ``core/.../evaluators/Evaluators.scala:51-319`` (factory), ``OpBinaryClassificationEvaluator``
+(``:56-174``), ``OpBinScoreEvaluator`` (``:60-173``), ``OpMultiClassificationEvaluator``,
+``OpRegressionEvaluator``, ``OpForecastEvaluator`` and ``OPLogLoss``. An evaluator reads the label
+and ``Prediction`` columns of a dataset (or raw arrays, which is how the model selector calls it)
+and returns a metrics dict; ``evaluate`` returns the single selection metric.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, Optional
+
+import torch
+
+from ..data.columns import PredictionColumn
+from . import metrics as M
+
+
+class OpEvaluatorBase:
+    name = "evaluator"
+    default_metric = ""
+    larger_better = True
+
+    def __init__(self, metric: Optional[str] = None, uid: Optional[str] = None, **kw):
+        from ..uid import make_uid
+        self.uid = uid or make_uid(type(self).__name__)
+        self.metric = metric or self.default_metric
+        self.label_col = None
+        self.prediction_col = None
+        self.params = kw
+
+    def set_label_col(self, f):
+        self.label_col = f.name if hasattr(f, "name") else f
+        return self
+
+    def set_prediction_col(self, f):
+        self.prediction_col = f.name if hasattr(f, "name") else f
+        return self
+
+    @property
+    def is_larger_better(self) -> bool:
+        return self.larger_better
+
+    def _arrays(self, ds):
+        y = ds[self.label_col].values.to(torch.float64)
+        p: PredictionColumn = ds[self.prediction_col]
+        return y, p.prediction, p.raw, p.probability
+
+    def evaluate_all(self, ds) -> Dict:
+        return self.evaluate_arrays(*self._arrays(ds))
+
+    def evaluate(self, ds) -> float:
+        return self.metric_value(self.evaluate_all(ds))
+
+    def metric_value(self, metrics: Dict) -> float:
+        return float(metrics[self.metric])
+
+    def evaluate_arrays(self, y, pred, raw, prob) -> Dict:
+        raise NotImplementedError
+
+    def selection_metric(self, y, pred, raw, prob) -> float:
+        """Metric used by the model selector on a validation fold."""
+        return self.metric_value(self.evaluate_arrays(y, pred, raw, prob))
+
+    def to_json(self):
+        return {"className": type(self).__name__, "uid": self.uid, "metric": self.metric, "name": self.name}
+
+
+def _score(raw, prob, pred):
+    if prob is not None and prob.numel() and prob.shape[1] >= 2:
+        return prob[:, 1]
+    if raw is not None and raw.numel() and raw.shape[1] >= 2:
+        return raw[:, 1]
+    return pred
+
+
+class OpBinaryClassificationEvaluator(OpEvaluatorBase):
+    name = "binEval"
+    default_metric = "AuROC"
+
+    def __init__(self, metric=None, num_bins: int = 100, **kw):
+        super().__init__(metric, **kw)
+        self.num_bins = num_bins
+        self.larger_better = self.metric not in ("Error",)
+
+    def evaluate_arrays(self, y, pred, raw, prob):
+        return M.binary_classification_metrics(pred, _score(None, prob, pred), y, self.num_bins)
+
+    def selection_metric(self, y, pred, raw, prob):
+        # BinaryClassificationEvaluator on rawPrediction, exact curve (numBins = 0)
+        if self.metric in ("AuPR", "AuROC"):
+            s = raw[:, 1] if (raw is not None and raw.numel() and raw.shape[1] >= 2) else _score(raw, prob, pred)
+            c = M.binary_curves(s, y, 0)
+            return c[self.metric]
+        if self.metric == "Error":
+            tp, tn, fp, fn = M.confusion_at(pred, y)
+            return (fp + fn) / max(1.0, tp + tn + fp + fn)
+        return self.metric_value(self.evaluate_arrays(y, pred, raw, prob))
+
+
+class OpBinScoreEvaluator(OpEvaluatorBase):
+    name = "binScoreEval"
+    default_metric = "BrierScore"
+    larger_better = False
+
+    def __init__(self, metric=None, num_bins: int = 100, **kw):
+        super().__init__(metric, **kw)
+        self.num_bins = num_bins
+
+    def evaluate_arrays(self, y, pred, raw, prob):
+        return M.bin_score_metrics(_score(None, prob, pred), y, self.num_bins)
+
+
+class OpMultiClassificationEvaluator(OpEvaluatorBase):
+    name = "multiEval"
+    default_metric = "F1"
+
+    def __init__(self, metric=None, **kw):
+        super().__init__(metric, **kw)
+        self.larger_better = self.metric not in ("Error",)
+
+    def evaluate_arrays(self, y, pred, raw, prob):
+        return M.multiclass_metrics(pred, y, prob)
+
+
+class OpRegressionEvaluator(OpEvaluatorBase):
+    name = "regEval"
+    default_metric = "RootMeanSquaredError"
+    larger_better = False
+
+    def __init__(self, metric=None, **kw):
+        super().__init__(metric, **kw)
+        self.larger_better = self.metric == "R2"
+
+    def evaluate_arrays(self, y, pred, raw, prob):
+        return M.regression_metrics(pred, y)
+
+
+class OpForecastEvaluator(OpEvaluatorBase):
+    name = "forecastEval"
+    default_metric = "SMAPE"
+    larger_better = False
+
+    def __init__(self, metric=None, seasonal_window: int = 1, **kw):
+        super().__init__(metric, **kw)
+        self.seasonal_window = seasonal_window
+
+    def evaluate_arrays(self, y, pred, raw, prob):
+        return M.forecast_metrics(pred, y, self.seasonal_window)
+
+
+class OpLogLossEvaluator(OpEvaluatorBase):
+    name = "logLoss"
+    default_metric = "LogLoss"
+    larger_better = False
+
+    def evaluate_arrays(self, y, pred, raw, prob):
+        return {"LogLoss": M.log_loss(prob, y)}
+
+
+class CustomEvaluator(OpEvaluatorBase):
+    """``Evaluators.*.custom(metricName, isLargerBetter, evaluateFn)``."""
+
+    def __init__(self, metric_name: str, is_larger_better: bool, fn: Callable, **kw):
+        super().__init__(metric_name, **kw)
+        self.larger_better = is_larger_better
+        self.fn = fn
+
+    def evaluate_arrays(self, y, pred, raw, prob):
+        return {self.metric: float(self.fn(y, pred, raw, prob))}
+
+
+class Evaluators:
+    """Factory mirroring ``Evaluators.scala``."""
+
+    class BinaryClassification:
+        @staticmethod
+        def __call__():
+            return OpBinaryClassificationEvaluator()
+
+        @staticmethod
+        def auPR():
+            return OpBinaryClassificationEvaluator("AuPR")
+
+        @staticmethod
+        def auROC():
+            return OpBinaryClassificationEvaluator("AuROC")
+
+        @staticmethod
+        def precision():
+            return OpBinaryClassificationEvaluator("Precision")
+
+        @staticmethod
+        def recall():
+            return OpBinaryClassificationEvaluator("Recall")
+
+        @staticmethod
+        def f1():
+            return OpBinaryClassificationEvaluator("F1")
+
+        @staticmethod
+        def error():
+            return OpBinaryClassificationEvaluator("Error")
+
+        @staticmethod
+        def brierScore():
+            return OpBinScoreEvaluator("BrierScore")
+
+        @staticmethod
+        def custom(metric_name, is_larger_better, evaluate_fn):
+            return CustomEvaluator(metric_name, is_larger_better, evaluate_fn)
+
+    class MultiClassification:
+        @staticmethod
+        def f1():
+            return OpMultiClassificationEvaluator("F1")
+
+        @staticmethod
+        def precision():
+            return OpMultiClassificationEvaluator("Precision")
+
+        @staticmethod
+        def recall():
+            return OpMultiClassificationEvaluator("Recall")
+
+        @staticmethod
+        def error():
+            return OpMultiClassificationEvaluator("Error")
+
+        @staticmethod
+        def logLoss():
+            return OpLogLossEvaluator()
+
+        @staticmethod
+        def custom(metric_name, is_larger_better, evaluate_fn):
+            return CustomEvaluator(metric_name, is_larger_better, evaluate_fn)
+
+    class Regression:
+        @staticmethod
+        def rmse():
+            return OpRegressionEvaluator("RootMeanSquaredError")
+
+        @staticmethod
+        def mse():
+            return OpRegressionEvaluator("MeanSquaredError")
+
+        @staticmethod
+        def mae():
+            return OpRegressionEvaluator("MeanAbsoluteError")
+
+        @staticmethod
+        def r2():
+            return OpRegressionEvaluator("R2")
+
+        @staticmethod
+        def custom(metric_name, is_larger_better, evaluate_fn):
+            return CustomEvaluator(metric_name, is_larger_better, evaluate_fn)
+
+    class Forecast:
+        @staticmethod
+        def smape():
+            return OpForecastEvaluator("SMAPE")
+
+        @staticmethod
+        def mase(seasonal_window=1):
+            return OpForecastEvaluator("MASE", seasonal_window)
+
+
+def evaluator_from_json(d) -> OpEvaluatorBase:
+    cls = {c.__name__: c for c in (OpBinaryClassificationEvaluator, OpBinScoreEvaluator,
+                                   OpMultiClassificationEvaluator, OpRegressionEvaluator, OpForecastEvaluator,
+                                   OpLogLossEvaluator)}[d["className"]]
+    return cls(d.get("metric"), uid=d.get("uid"))

@@ -1,0 +1,240 @@
+"""Evaluation metric kernels (device-resident).
+
+Binary curves follow Spark ``BinaryClassificationMetrics`` (used by ``OpBinaryClassificationEvaluator.scala:67-135``
+and the selector's ``BinaryClassificationEvaluator`` metric at ``:149-155``): distinct scores sorted
+descending, optional down-sampling into ``numBins`` groups (each group keyed by its first score),
+cumulative confusion counts, PR curve prefixed with ``(0, precision_first)``, ROC with ``(0,0)`` and
+``(1,1)`` end points, trapezoidal areas. Everything runs as sort + segmented reductions on the
+tensors' device.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+
+def _curve_counts(scores: torch.Tensor, labels: torch.Tensor, num_bins: int = 0, weights=None):
+    s = scores.to(torch.float64).reshape(-1)
+    y = labels.to(torch.float64).reshape(-1)
+    w = torch.ones_like(s) if weights is None else weights.to(torch.float64)
+    order = torch.argsort(s, descending=True, stable=True)
+    s, y, w = s[order], y[order], w[order]
+    uniq, inv = torch.unique_consecutive(s, return_inverse=True)
+    n_u = uniq.numel()
+    pos = torch.zeros(n_u, dtype=torch.float64, device=s.device).index_add_(0, inv, w * (y > 0.5))
+    neg = torch.zeros(n_u, dtype=torch.float64, device=s.device).index_add_(0, inv, w * (y <= 0.5))
+    thr = uniq
+    if num_bins > 0:
+        grouping = n_u // num_bins
+        if grouping >= 2:
+            gid = torch.arange(n_u, device=s.device) // grouping
+            ng = int(gid[-1].item()) + 1
+            pos = torch.zeros(ng, dtype=torch.float64, device=s.device).index_add_(0, gid, pos)
+            neg = torch.zeros(ng, dtype=torch.float64, device=s.device).index_add_(0, gid, neg)
+            thr = uniq[torch.arange(ng, device=s.device) * grouping]
+    tp = torch.cumsum(pos, 0)
+    fp = torch.cumsum(neg, 0)
+    return thr, tp, fp, float(pos.sum()), float(neg.sum())
+
+
+def _trapz(x, y):
+    if x.numel() < 2:
+        return 0.0
+    return float(((x[1:] - x[:-1]) * (y[1:] + y[:-1]) / 2.0).sum())
+
+
+def binary_curves(scores, labels, num_bins: int = 0, weights=None) -> Dict[str, object]:
+    thr, tp, fp, P, Nn = _curve_counts(scores, labels, num_bins, weights)
+    prec = torch.where(tp + fp > 0, tp / (tp + fp).clamp_min(1e-300), torch.ones_like(tp))
+    rec = tp / P if P > 0 else torch.zeros_like(tp)
+    fpr = fp / Nn if Nn > 0 else torch.zeros_like(fp)
+    dev = tp.device
+    pr_x = torch.cat([torch.zeros(1, dtype=torch.float64, device=dev), rec])
+    pr_y = torch.cat([prec[:1] if prec.numel() else torch.ones(1, dtype=torch.float64, device=dev), prec])
+    roc_x = torch.cat([torch.zeros(1, dtype=torch.float64, device=dev), fpr,
+                       torch.ones(1, dtype=torch.float64, device=dev)])
+    roc_y = torch.cat([torch.zeros(1, dtype=torch.float64, device=dev), rec,
+                       torch.ones(1, dtype=torch.float64, device=dev)])
+    return {"thresholds": thr, "tp": tp, "fp": fp, "P": P, "N": Nn, "precision": prec, "recall": rec, "fpr": fpr,
+            "AuPR": _trapz(pr_x, pr_y), "AuROC": _trapz(roc_x, roc_y)}
+
+
+def au_pr(scores, labels, num_bins: int = 0) -> float:
+    return binary_curves(scores, labels, num_bins)["AuPR"]
+
+
+def au_roc(scores, labels, num_bins: int = 0) -> float:
+    return binary_curves(scores, labels, num_bins)["AuROC"]
+
+
+def binned_aupr(scores: torch.Tensor, labels: torch.Tensor, bins: int = 1 << 16) -> float:
+    """O(N) histogram approximation of AuPR for scores in [0, 1] (early-stopping monitor)."""
+    s = scores.to(torch.float32).clamp(0, 1)
+    b = (s * (bins - 1)).to(torch.int64)
+    y = labels > 0.5
+    pos = torch.bincount(b[y], minlength=bins).flip(0).to(torch.float64)
+    neg = torch.bincount(b[~y], minlength=bins).flip(0).to(torch.float64)
+    keep = (pos + neg) > 0
+    pos, neg = pos[keep], neg[keep]
+    tp, fp = torch.cumsum(pos, 0), torch.cumsum(neg, 0)
+    P = float(pos.sum())
+    if P == 0:
+        return 0.0
+    prec = tp / (tp + fp)
+    rec = tp / P
+    x = torch.cat([torch.zeros(1, dtype=torch.float64, device=rec.device), rec])
+    yv = torch.cat([prec[:1], prec])
+    return _trapz(x, yv)
+
+
+def confusion_at(pred: torch.Tensor, labels: torch.Tensor):
+    p = pred.to(torch.float64) > 0.5
+    y = labels.to(torch.float64) > 0.5
+    tp = float((p & y).sum())
+    tn = float((~p & ~y).sum())
+    fp = float((p & ~y).sum())
+    fn = float((~p & y).sum())
+    return tp, tn, fp, fn
+
+
+def binary_classification_metrics(pred, prob1, labels, num_bins: int = 100) -> Dict[str, object]:
+    """``OpBinaryClassificationEvaluator.evaluateAll`` (``OpBinaryClassificationEvaluator.scala:67-135``)."""
+    n = int(labels.numel())
+    if n == 0:
+        z = {k: 0.0 for k in ("Precision", "Recall", "F1", "AuROC", "AuPR", "Error", "TP", "TN", "FP", "FN")}
+        z["ThresholdMetrics"] = {"thresholds": [], "precisionByThreshold": [], "recallByThreshold": [],
+                                 "falsePositiveRateByThreshold": [], "truePositivesByThreshold": [],
+                                 "falsePositivesByThreshold": [], "trueNegativesByThreshold": [],
+                                 "falseNegativesByThreshold": []}
+        return z
+    labs = torch.unique(labels.to(torch.float64))
+    if labs.numel() == 2 or True:
+        tp, tn, fp, fn = confusion_at(pred, labels)
+    precision = 0.0 if tp + fp == 0 else tp / (tp + fp)
+    recall = 0.0 if tp + fn == 0 else tp / (tp + fn)
+    f1 = 0.0 if precision + recall == 0 else 2 * precision * recall / (precision + recall)
+    error = 0.0 if n == 0 else (fp + fn) / n
+    c = binary_curves(prob1, labels, num_bins)
+    P, Nn = c["P"], c["N"]
+    tpt, fpt = c["tp"], c["fp"]
+    return {"Precision": precision, "Recall": recall, "F1": f1, "AuROC": c["AuROC"], "AuPR": c["AuPR"],
+            "Error": error, "TP": tp, "TN": tn, "FP": fp, "FN": fn,
+            "ThresholdMetrics": {
+                "thresholds": c["thresholds"].tolist(), "precisionByThreshold": c["precision"].tolist(),
+                "recallByThreshold": c["recall"].tolist(), "falsePositiveRateByThreshold": c["fpr"].tolist(),
+                "truePositivesByThreshold": tpt.tolist(), "falsePositivesByThreshold": fpt.tolist(),
+                "trueNegativesByThreshold": (Nn - fpt).tolist(), "falseNegativesByThreshold": (P - tpt).tolist()}}
+
+
+def bin_score_metrics(prob1, labels, num_bins: int = 100) -> Dict[str, object]:
+    """``OpBinScoreEvaluator.evaluateScoreAndLabels`` (``OpBinScoreEvaluator.scala:60-173``): Brier score + bins."""
+    s = prob1.to(torch.float64)
+    y = labels.to(torch.float64)
+    if s.numel() == 0:
+        return {"BrierScore": 0.0, "binSize": 0.0, "binCenters": [], "numberOfDataPoints": [],
+                "numberOfPositiveLabels": [], "averageScore": [], "averageConversionRate": []}
+    mx = max(1.0, float(s.max()))
+    mn = min(0.0, float(s.min()))
+    diff = mx - mn
+    idx = torch.clamp((num_bins * (s - mn) / diff).to(torch.int64), max=num_bins - 1)
+    cnt = torch.bincount(idx, minlength=num_bins).to(torch.float64)
+    ssum = torch.zeros(num_bins, dtype=torch.float64, device=s.device).index_add_(0, idx, s)
+    psum = torch.zeros(num_bins, dtype=torch.float64, device=s.device).index_add_(0, idx, (y > 0).to(torch.float64))
+    brier = float(((s - y) ** 2).sum() / s.numel())
+    avg_s = torch.where(cnt > 0, ssum / cnt.clamp_min(1), torch.zeros_like(cnt))
+    avg_c = torch.where(cnt > 0, psum / cnt.clamp_min(1), torch.zeros_like(cnt))
+    centers = [mn + diff * i / num_bins + diff / (2 * num_bins) for i in range(num_bins)]
+    return {"BrierScore": brier, "binSize": diff / num_bins, "binCenters": centers,
+            "numberOfDataPoints": cnt.to(torch.int64).tolist(), "numberOfPositiveLabels": psum.to(torch.int64).tolist(),
+            "averageScore": avg_s.tolist(), "averageConversionRate": avg_c.tolist()}
+
+
+def multiclass_metrics(pred, labels, prob=None, top_ns=(1, 3), thresholds=None) -> Dict[str, object]:
+    """``OpMultiClassificationEvaluator.evaluateAll``: error, weighted precision / recall, F1 (+ threshold metrics)."""
+    p = pred.to(torch.int64).reshape(-1)
+    y = labels.to(torch.int64).reshape(-1)
+    n = y.numel()
+    if n == 0:
+        return {"Precision": 0.0, "Recall": 0.0, "F1": 0.0, "Error": 0.0}
+    K = int(max(p.max(), y.max()).item()) + 1
+    cm = torch.zeros(K, K, dtype=torch.float64, device=y.device)
+    cm.index_put_((y, p), torch.ones(n, dtype=torch.float64, device=y.device), accumulate=True)
+    tp = cm.diag()
+    actual = cm.sum(1)
+    predicted = cm.sum(0)
+    prec_c = torch.where(predicted > 0, tp / predicted.clamp_min(1), torch.zeros_like(tp))
+    rec_c = torch.where(actual > 0, tp / actual.clamp_min(1), torch.zeros_like(tp))
+    wts = actual / n
+    precision = float((prec_c * wts).sum())
+    recall = float((rec_c * wts).sum())
+    f1 = 0.0 if precision + recall == 0 else 2 * precision * recall / (precision + recall)
+    out = {"Precision": precision, "Recall": recall, "F1": f1, "Error": 1.0 - float(tp.sum()) / n}
+    if prob is not None and prob.numel() and prob.dim() == 2:
+        th = thresholds if thresholds is not None else [i / 100 for i in range(101)]
+        pr = prob.to(torch.float64)
+        top = torch.argsort(pr, 1, descending=True)
+        topscore = pr.gather(1, top[:, :1])[:, 0]
+        res = {"topNs": list(top_ns), "thresholds": list(th), "correctCounts": {}, "incorrectCounts": {},
+               "noPredictionCounts": {}}
+        tht = torch.as_tensor(th, dtype=torch.float64, device=pr.device)
+        for t in top_ns:
+            hit = (top[:, :min(t, pr.shape[1])] == y[:, None]).any(1)
+            truescore = pr.gather(1, y.clamp(max=pr.shape[1] - 1)[:, None])[:, 0]
+            above_true = truescore[None, :] >= tht[:, None]
+            above_top = topscore[None, :] >= tht[:, None]
+            correct = (above_true & hit[None, :]).sum(1)
+            incorrect = (above_top & ~(above_true & hit[None, :])).sum(1)
+            res["correctCounts"][str(t)] = correct.tolist()
+            res["incorrectCounts"][str(t)] = incorrect.tolist()
+            res["noPredictionCounts"][str(t)] = (n - correct - incorrect).tolist()
+        out["ThresholdMetrics"] = res
+    return out
+
+
+def regression_metrics(pred, labels, bins=(-1e9, -100, -10, 0, 10, 100, 1e9), scaled_error_cutoff=1e-3) -> Dict:
+    """``OpRegressionEvaluator``: RMSE, MSE, MAE, R2 and signed percentage-error histogram."""
+    p = pred.to(torch.float64).reshape(-1)
+    y = labels.to(torch.float64).reshape(-1)
+    n = y.numel()
+    if n == 0:
+        return {"RootMeanSquaredError": 0.0, "MeanSquaredError": 0.0, "R2": 0.0, "MeanAbsoluteError": 0.0}
+    e = p - y
+    mse = float((e * e).mean())
+    ss_tot = float(((y - y.mean()) ** 2).sum())
+    r2 = 1.0 - float((e * e).sum()) / ss_tot if ss_tot > 0 else 0.0
+    den = torch.where(y.abs() > scaled_error_cutoff, y.abs(), torch.full_like(y, scaled_error_cutoff))
+    pct = 100.0 * e / den
+    edges = torch.as_tensor(list(bins), dtype=torch.float64, device=y.device)
+    idx = torch.clamp(torch.searchsorted(edges, pct, right=True) - 1, 0, len(bins) - 2)
+    hist = torch.bincount(idx, minlength=len(bins) - 1)
+    return {"RootMeanSquaredError": math.sqrt(mse), "MeanSquaredError": mse, "R2": r2,
+            "MeanAbsoluteError": float(e.abs().mean()),
+            "SignedPercentageErrorHistogram": {"bins": list(bins), "counts": hist.tolist()}}
+
+
+def forecast_metrics(pred, labels, seasonal_window: int = 1) -> Dict:
+    """``OpForecastEvaluator``: SMAPE and MASE."""
+    p = pred.to(torch.float64).reshape(-1)
+    y = labels.to(torch.float64).reshape(-1)
+    n = y.numel()
+    if n == 0:
+        return {"SMAPE": 0.0, "SeasonalError": 0.0, "MASE": 0.0}
+    den = p.abs() + y.abs()
+    smape = float(torch.where(den > 0, 2 * (p - y).abs() / den.clamp_min(1e-300), torch.zeros_like(den)).mean())
+    if n > seasonal_window:
+        se = float((y[seasonal_window:] - y[:-seasonal_window]).abs().mean())
+    else:
+        se = 0.0
+    mae = float((p - y).abs().mean())
+    return {"SMAPE": smape, "SeasonalError": se, "MASE": mae / se if se > 0 else 0.0}
+
+
+def log_loss(prob, labels) -> float:
+    """Multiclass log loss (``stages/impl/evaluator/OPLogLoss.scala``)."""
+    pr = prob.to(torch.float64)
+    y = labels.to(torch.int64)
+    p = pr.gather(1, y[:, None])[:, 0].clamp(1e-15, 1 - 1e-15)
+    return float(-torch.log(p).mean())

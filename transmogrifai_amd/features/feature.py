@@ -1,0 +1,262 @@
+"""Typed feature DAG nodes.
+
+Reference: ``FeatureLike`` (``features/.../features/FeatureLike.scala:43-466``: ``transformWith``
+``:210-279``, ``traverse`` ``:309-325``, ``parentStages`` ``:363-437``), ``Feature``
+(``Feature.scala:40-130``) and ``FeatureUID`` (``Feature.scala:115-130``).
+
+A feature is an immutable node: name, uid, value type, response flag, the stage that produces it
+and the parent features that stage consumes. ``parent_stages`` topologically layers the graph
+(edges child -> parent) and returns ``{stage: distance}`` where distance is the layer index of
+the stage's output counted from this feature -- the workflow fits the deepest layers first.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+from ..data.vector_metadata import FeatureHistory
+from ..uid import from_string
+from . import types as T
+
+
+class FeatureCycleException(Exception):
+    pass
+
+
+def feature_uid(wtype, stage_uid: str) -> str:
+    """``<ShortTypeName>_<stage uid suffix>`` (``Feature.scala:124-128``)."""
+    _, suffix = from_string(stage_uid)
+    return f"{wtype.short_name()}_{suffix}"
+
+
+class FeatureLike:
+    __slots__ = ("name", "uid", "wtype", "is_response", "origin_stage", "parents", "distributions")
+
+    def __init__(self, name: str, wtype, is_response: bool, origin_stage, parents: Sequence["FeatureLike"] = (),
+                 uid: Optional[str] = None, distributions=()):
+        self.name = name
+        self.wtype = wtype
+        self.is_response = bool(is_response)
+        self.origin_stage = origin_stage
+        self.parents = list(parents)
+        self.uid = uid if uid is not None else feature_uid(wtype, origin_stage.uid)
+        self.distributions = list(distributions)
+
+    # ---------------------------------------------------------------------------------- identity
+    @property
+    def is_raw(self) -> bool:
+        return len(self.parents) == 0
+
+    @property
+    def type_name(self) -> str:
+        return self.wtype.type_name()
+
+    def is_subtype_of(self, t) -> bool:
+        return issubclass(self.wtype, t)
+
+    def same_origin(self, other) -> bool:
+        if not isinstance(other, FeatureLike):
+            return False
+        if self.is_response != other.is_response or self.wtype is not other.wtype:
+            return False
+        a, b = self.origin_stage, other.origin_stage
+        if a is None or b is None:
+            return a is None and b is None
+        return a.uid == b.uid
+
+    def __eq__(self, other):
+        return (isinstance(other, FeatureLike) and self.name == other.name and self.same_origin(other)
+                and [p.uid for p in self.parents] == [p.uid for p in other.parents])
+
+    def __hash__(self):
+        return hash(self.uid)
+
+    def __repr__(self):
+        os_uid = None if self.origin_stage is None else self.origin_stage.uid
+        return (f"Feature(name = {self.name}, uid = {self.uid}, isResponse = {self.is_response}, "
+                f"originStage = {os_uid}, parents = [{','.join(p.uid for p in self.parents)}])")
+
+    # ------------------------------------------------------------------------------ construction
+    def as_response(self) -> "FeatureLike":
+        return self._with_response(True)
+
+    def as_predictor(self) -> "FeatureLike":
+        return self._with_response(False)
+
+    def _with_response(self, r: bool) -> "FeatureLike":
+        if not self.is_raw:
+            raise ValueError("only raw features can change their response flag")
+        st = self.origin_stage
+        if st is not None and hasattr(st, "output_is_response"):
+            st.output_is_response = r
+            st._output = None
+            return st.get_output()
+        return FeatureLike(self.name, self.wtype, r, st, self.parents, self.uid)
+
+    def transform_with(self, stage, *others):
+        """Apply ``stage`` with this feature as the first input (``FeatureLike.scala:210-279``)."""
+        return stage.set_input(self, *others).get_output()
+
+    def with_distributions(self, distributions) -> "FeatureLike":
+        return FeatureLike(self.name, self.wtype, self.is_response, self.origin_stage, self.parents,
+                           self.uid, distributions)
+
+    # ----------------------------------------------------------------------------------- traversal
+    def traverse(self) -> List["FeatureLike"]:
+        """All features reachable through ``parents`` (DFS, including self)."""
+        seen: Dict[str, FeatureLike] = {}
+        stack = [self]
+        while stack:
+            f = stack.pop()
+            if f.uid in seen:
+                continue
+            seen[f.uid] = f
+            stack.extend(p for p in f.parents if p.uid not in seen)
+        return list(seen.values())
+
+    def all_features(self) -> List["FeatureLike"]:
+        return self.traverse()
+
+    def raw_features(self) -> List["FeatureLike"]:
+        out = {f.uid: f for f in self.traverse() if f.is_raw}
+        return sorted(out.values(), key=lambda f: f.name)
+
+    def parent_stages(self) -> Dict[object, int]:
+        """``{stage: distance}`` for every non-generator stage upstream (``FeatureLike.scala:363-437``)."""
+        feats = {f.uid: f for f in self.traverse()}
+        # validate origin stage inputs match parents
+        for f in feats.values():
+            if f.is_raw or f.origin_stage is None:
+                continue
+            ins = {t.uid for t in f.origin_stage.get_input_features()}
+            if not ins.issubset({p.uid for p in f.parents}) and ins != {p.uid for p in f.parents}:
+                raise ValueError("Some of your features had parent features that did not match the inputs to their "
+                                 "origin stage. All stages must be a new instance when used to transform features")
+        # Kahn layering over edges child -> parent
+        indeg = {u: 0 for u in feats}
+        for f in feats.values():
+            for p in f.parents:
+                indeg[p.uid] += 1
+        layer = {u: 0 for u in feats}
+        frontier = [u for u, d in indeg.items() if d == 0]
+        processed = 0
+        depth = 0
+        while frontier:
+            nxt = []
+            for u in frontier:
+                layer[u] = depth
+                processed += 1
+                for p in feats[u].parents:
+                    indeg[p.uid] -= 1
+                    if indeg[p.uid] == 0:
+                        nxt.append(p.uid)
+            frontier = nxt
+            depth += 1
+        if processed != len(feats):
+            bad = next(u for u, d in indeg.items() if d > 0)
+            raise FeatureCycleException(f"Cycle detected from {self.uid} to {bad}")
+        from ..stages.generator import FeatureGeneratorStage
+        out: Dict[object, int] = {}
+        for u, f in feats.items():
+            st = f.origin_stage
+            if st is None or isinstance(st, FeatureGeneratorStage):
+                continue
+            d = layer[u]
+            if st not in out or out[st] < d:
+                out[st] = d
+        return out
+
+    def history(self) -> FeatureHistory:
+        origins = sorted({f.name for f in self.raw_features()})
+        stages = sorted(((-d, s.stage_name()) for s, d in self.parent_stages().items()))
+        return FeatureHistory(tuple(origins), tuple(n for _, n in stages))
+
+    def pretty_parent_stages(self) -> str:
+        lines = []
+        stack = [(0, self)]
+        while stack:
+            lvl, f = stack.pop()
+            if f.origin_stage is not None:
+                lines.append(f"{'|    ' * lvl}+-- {f.origin_stage.operation_name}")
+                for p in f.parents:
+                    stack.append((lvl + 1, p))
+        return "\n".join(lines) + ("\n" if lines else "")
+
+    # ------------------------------------------------------------------------------------ json
+    def to_json(self) -> dict:
+        """``FeatureJsonHelper`` shape (``features/.../FeatureJsonHelper.scala:57-140``)."""
+        return {"typeName": self.type_name, "uid": self.uid, "name": self.name, "isResponse": self.is_response,
+                "originStage": None if self.origin_stage is None else self.origin_stage.uid,
+                "parents": [p.uid for p in self.parents],
+                "distributions": [d.to_json() if hasattr(d, "to_json") else d for d in self.distributions]}
+
+    # -------------------------------------------------------------------------- DSL hook points
+    def __getattr__(self, item):
+        # DSL methods (transmogrify, pivot, vectorize, ...) are registered in transmogrifai_amd.dsl
+        from ..dsl import lookup
+        fn = lookup(self.wtype, item)
+        if fn is None:
+            raise AttributeError(f"'{self.wtype.__name__}' feature has no attribute '{item}'")
+        return fn.__get__(self, FeatureLike)
+
+    def _binop(self, other, op, reverse=False):
+        from ..dsl import binary_op
+        return binary_op(self, other, op, reverse)
+
+    def __add__(self, o):
+        return self._binop(o, "plus")
+
+    def __radd__(self, o):
+        return self._binop(o, "plus", True)
+
+    def __sub__(self, o):
+        return self._binop(o, "minus")
+
+    def __rsub__(self, o):
+        return self._binop(o, "minus", True)
+
+    def __mul__(self, o):
+        return self._binop(o, "multiply")
+
+    def __rmul__(self, o):
+        return self._binop(o, "multiply", True)
+
+    def __truediv__(self, o):
+        return self._binop(o, "divide")
+
+    def __rtruediv__(self, o):
+        return self._binop(o, "divide", True)
+
+
+Feature = FeatureLike
+
+
+class TransientFeature:
+    """Serializable lightweight feature reference used as a stage param
+    (``features/.../features/TransientFeature.scala``)."""
+
+    def __init__(self, name, uid, is_response, is_raw, type_name, origin_features, stages):
+        self.name = name
+        self.uid = uid
+        self.is_response = is_response
+        self.is_raw = is_raw
+        self.type_name = type_name
+        self.origin_features = list(origin_features)
+        self.stages = list(stages)
+
+    @staticmethod
+    def of(f: FeatureLike) -> "TransientFeature":
+        h = f.history()
+        return TransientFeature(f.name, f.uid, f.is_response, f.is_raw, f.type_name, h.origin_features, h.stages)
+
+    def to_json(self):
+        return {"name": self.name, "isResponse": self.is_response, "isRaw": self.is_raw, "uid": self.uid,
+                "typeName": self.type_name, "originFeatures": self.origin_features, "stages": self.stages}
+
+    @staticmethod
+    def from_json(d):
+        return TransientFeature(d["name"], d["uid"], d["isResponse"], d.get("isRaw", False), d["typeName"],
+                                d.get("originFeatures", []), d.get("stages", []))
+
+    @property
+    def wtype(self):
+        return T.feature_type_from_name(self.type_name)

@@ -1,0 +1,614 @@
+"""Batched level-wise histogram tree engine.
+
+One engine serves every tree learner of the reference: Spark ``DecisionTree`` / ``RandomForest``
+/ ``GBT`` (``OpDecisionTreeClassifier.scala:47-115``, ``OpRandomForestClassifier.scala:59-154``,
+``OpGBTClassifier.scala:47-142`` and the regressors) and XGBoost (``OpXGBoostClassifier.scala:47-403``),
+i.e. SURVEY.md kernels K23-K25 and K29.
+
+MI355X-first design: instead of training one tree per Spark job, *all* trees of a batch -- every
+tree of every (hyper-parameter config x CV fold) -- grow together, level by level. Per level there
+is one histogram launch (work items = node row-chunks x feature groups), one split-scan launch,
+one partition-count launch, a single device->host sync to collect the split decisions, and one
+stable-scatter launch. Rows live in one packed ``uint32`` buffer (row id | bootstrap weight << 24)
+partitioned by node, so a level touches only the rows of the nodes still being split. The same
+orchestration drives the C++ host kernels when the data lives on the CPU.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..ops import _native as N
+
+MODE_CLS, MODE_VAR, MODE_GH = 0, 1, 2
+KIND_GINI, KIND_ENTROPY, KIND_VARIANCE, KIND_NEWTON = 0, 1, 2, 3
+KINDS = {"gini": KIND_GINI, "entropy": KIND_ENTROPY, "variance": KIND_VARIANCE, "newton": KIND_NEWTON}
+
+HIST_ITEM = np.dtype([("node", "<i4"), ("fg0", "<i4"), ("nf", "<i4"), ("excl", "<i4"),
+                      ("begin", "<i8"), ("count", "<i8")])
+PART_ITEM = np.dtype([("node", "<i4"), ("pad", "<i4"), ("begin", "<i8"), ("count", "<i8"),
+                      ("out_left", "<i8"), ("out_right", "<i8")])
+assert HIST_ITEM.itemsize == 32 and PART_ITEM.itemsize == 40
+
+ROW_MASK = 0xFFFFFF
+MAX_ROWS = 1 << 24
+
+
+@dataclass
+class TreeParams:
+    max_depth: int = 5
+    min_instances: float = 1.0
+    min_info_gain: float = 0.0
+    min_child_weight: float = 0.0
+    reg_lambda: float = 0.0
+    gamma: float = 0.0
+    eta: float = 1.0
+    feature_subset: Optional[int] = None   # features sampled per node (None = all)
+    split_eps: float = 0.0                 # split only if gain > split_eps
+
+
+@dataclass
+class TreeJob:
+    model: int                      # index into t1/t2 model axis
+    params: TreeParams
+    rows: torch.Tensor              # int64 row ids of the root (on the engine device)
+    weights: Optional[torch.Tensor] = None   # optional integer weights per root row (bootstrap)
+    seed: int = 0
+
+
+@dataclass
+class Forest:
+    """Flat node arrays for a set of trees (children indices are global into the arrays)."""
+    tree_off: np.ndarray            # int64 [T+1]
+    nodes: np.ndarray               # int32 [n, 4] (feat, bin, left, right), left < 0 => leaf
+    default_left: np.ndarray        # uint8 [n]
+    value: np.ndarray               # float32 [n, K]
+    gain: np.ndarray                # float32 [n]
+    cover: np.ndarray               # float32 [n]  (weighted count / hessian)
+    tree_model: np.ndarray          # int32 [T]   job.model for each tree
+    missing_bin: int = -1
+
+    @property
+    def n_trees(self):
+        return len(self.tree_off) - 1
+
+    @property
+    def K(self):
+        return self.value.shape[1]
+
+    def tree(self, t: int) -> "Forest":
+        a, b = int(self.tree_off[t]), int(self.tree_off[t + 1])
+        nodes = self.nodes[a:b].copy()
+        nodes[:, 2:] = np.where(nodes[:, 2:] >= 0, nodes[:, 2:] - a, -1)
+        return Forest(np.array([0, b - a], np.int64), nodes, self.default_left[a:b].copy(),
+                      self.value[a:b].copy(), self.gain[a:b].copy(), self.cover[a:b].copy(),
+                      self.tree_model[t:t + 1].copy(), self.missing_bin)
+
+    @staticmethod
+    def concat(forests: Sequence["Forest"]) -> "Forest":
+        offs, nodes, dls, vals, gains, covs, tms = [0], [], [], [], [], [], []
+        base = 0
+        for f in forests:
+            nd = f.nodes.copy()
+            nd[:, 2:] = np.where(nd[:, 2:] >= 0, nd[:, 2:] + base, -1)
+            nodes.append(nd)
+            dls.append(f.default_left)
+            vals.append(f.value)
+            gains.append(f.gain)
+            covs.append(f.cover)
+            tms.append(f.tree_model)
+            for t in range(f.n_trees):
+                offs.append(base + int(f.tree_off[t + 1]))
+            base += len(f.nodes)
+        return Forest(np.asarray(offs, np.int64), np.concatenate(nodes), np.concatenate(dls),
+                      np.concatenate(vals), np.concatenate(gains), np.concatenate(covs),
+                      np.concatenate(tms), forests[0].missing_bin if forests else -1)
+
+    def to_state(self) -> dict:
+        return {"tree_off": self.tree_off, "nodes": self.nodes, "default_left": self.default_left,
+                "value": self.value, "gain": self.gain, "cover": self.cover, "tree_model": self.tree_model,
+                "missing_bin": int(self.missing_bin)}
+
+    @staticmethod
+    def from_state(d) -> "Forest":
+        return Forest(np.asarray(d["tree_off"], np.int64), np.asarray(d["nodes"], np.int32).reshape(-1, 4),
+                      np.asarray(d["default_left"], np.uint8), np.asarray(d["value"], np.float32).reshape(
+                          len(np.asarray(d["default_left"])), -1),
+                      np.asarray(d["gain"], np.float32), np.asarray(d["cover"], np.float32),
+                      np.asarray(d["tree_model"], np.int32), int(d.get("missing_bin", -1)))
+
+    def feature_importance(self, n_features: int) -> np.ndarray:
+        """Total gain per feature, normalized per tree then averaged (Spark ``featureImportances``)."""
+        imp = np.zeros(n_features)
+        for t in range(self.n_trees):
+            a, b = int(self.tree_off[t]), int(self.tree_off[t + 1])
+            ti = np.zeros(n_features)
+            nd = self.nodes[a:b]
+            internal = nd[:, 2] >= 0
+            np.add.at(ti, nd[internal, 0], (self.gain[a:b][internal] * self.cover[a:b][internal]).astype(np.float64))
+            s = ti.sum()
+            if s > 0:
+                imp += ti / s
+        s = imp.sum()
+        return imp / s if s > 0 else imp
+
+
+def pack_rows(rows: torch.Tensor, weights: Optional[torch.Tensor]) -> torch.Tensor:
+    """Pack ``row | weight << 24`` into an int32 tensor (bit pattern read as uint32 by the kernels)."""
+    r = rows.to(torch.int64)
+    w = torch.ones_like(r) if weights is None else weights.to(torch.int64).clamp(0, 255)
+    e = r | (w << 24)
+    e = torch.where(e >= (1 << 31), e - (1 << 32), e)
+    return e.to(torch.int32)
+
+
+class _Grow:
+    """Growable host arrays for the created nodes."""
+
+    def __init__(self, S):
+        self.S = S
+        self.n = 0
+        cap = 1024
+        self.tree = np.zeros(cap, np.int64)
+        self.feat = np.full(cap, -1, np.int64)
+        self.bin = np.full(cap, -1, np.int64)
+        self.dl = np.zeros(cap, np.uint8)
+        self.gain = np.zeros(cap, np.float64)
+        self.tot = np.zeros((cap, S), np.float64)
+        self.left = np.full(cap, -1, np.int64)
+        self.right = np.full(cap, -1, np.int64)
+
+    def add(self, trees: np.ndarray) -> np.ndarray:
+        k = trees.size
+        need = self.n + k
+        if need > self.tree.size:
+            cap = max(need, 2 * self.tree.size)
+            for name, fill in (("tree", 0), ("feat", -1), ("bin", -1), ("dl", 0), ("gain", 0.0),
+                               ("left", -1), ("right", -1)):
+                a = getattr(self, name)
+                b = np.full(cap, fill, a.dtype)
+                b[:a.size] = a
+                setattr(self, name, b)
+            t = np.zeros((cap, self.S))
+            t[:self.tot.shape[0]] = self.tot
+            self.tot = t
+        ids = np.arange(self.n, need, dtype=np.int64)
+        self.tree[ids] = trees
+        self.n = need
+        return ids
+
+
+def _feature_subsets(n_nodes: int, F: int, k: np.ndarray, dev, gen) -> tuple:
+    """Per node j, ``k[j]`` distinct uniformly sampled features, sorted ascending.
+
+    Returns ``(feat_list int32 [sum k], offsets int32 [n], nfeat int32 [n])``. Sampling is the
+    "k smallest of F uniform keys" construction, done in node chunks with a seeded generator.
+    """
+    parts = [None] * n_nodes
+    out = torch.empty(int(k.sum()), dtype=torch.int32, device=dev)
+    offs = np.zeros(n_nodes, np.int64)
+    if n_nodes > 1:
+        offs[1:] = np.cumsum(k[:-1])
+    for kv in np.unique(k):
+        idx = np.nonzero(k == kv)[0]
+        kv = int(kv)
+        step = max(1, (1 << 24) // max(F, 1))
+        for a in range(0, idx.size, step):
+            sub = idx[a:a + step]
+            keys = torch.rand((sub.size, F), generator=gen).to(dev)
+            sel = torch.sort(torch.topk(keys, kv, dim=1, largest=False).indices, dim=1).values.to(torch.int32)
+            pos = torch.as_tensor(offs[sub], device=dev)[:, None] + torch.arange(kv, device=dev)[None, :]
+            out[pos.reshape(-1)] = sel.reshape(-1)
+    del parts
+    return out, offs.astype(np.int32), k.astype(np.int32)
+
+
+def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *, mode: int, kind: int,
+                n_classes: int = 2, y: Optional[torch.Tensor] = None, t1: Optional[torch.Tensor] = None,
+                t2: Optional[torch.Tensor] = None, B: int = 32, missing_bin: int = -1,
+                subtract: bool = True, chunk_rows: int = 4096, rng_seed: int = 0) -> Forest:
+    """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``."""
+    dev = Xb.device
+    on_gpu = dev.type == "cuda"
+    Nrows, F = int(Xb.shape[0]), int(Xb.shape[1])
+    if Nrows >= MAX_ROWS:
+        raise ValueError(f"tree engine supports < {MAX_ROWS} rows per training set, got {Nrows}")
+    S = n_classes if mode == MODE_CLS else (3 if mode == MODE_VAR else 2)
+    K = n_classes if mode == MODE_CLS else 1
+    if missing_bin >= B:
+        raise ValueError("missing_bin must be < B")
+    n_bins_t = torch.as_tensor(np.asarray(n_bins, np.int32), device=dev)
+    stride = int(t1.shape[1]) if (t1 is not None and t1.dim() == 2) else 0
+    yf = y.to(device=dev, dtype=torch.float32).contiguous() if y is not None else None
+    t1f = t1.to(device=dev, dtype=torch.float32).contiguous() if t1 is not None else None
+    t2f = t2.to(device=dev, dtype=torch.float32).contiguous() if t2 is not None else None
+    Xb = Xb.contiguous()
+    T = len(jobs)
+    P_depth = np.array([j.params.max_depth for j in jobs], np.int64)
+    P_inst = np.array([j.params.min_instances for j in jobs], np.float64)
+    P_gain = np.array([j.params.min_info_gain for j in jobs], np.float64)
+    P_mcw = np.array([j.params.min_child_weight for j in jobs], np.float64)
+    P_lam = np.array([j.params.reg_lambda for j in jobs], np.float64)
+    P_eps = np.array([j.params.split_eps for j in jobs], np.float64)
+    P_sub = np.array([F if (j.params.feature_subset is None or j.params.feature_subset >= F)
+                      else max(1, int(j.params.feature_subset)) for j in jobs], np.int64)
+    use_subset = bool(np.any(P_sub < F))
+    all_feats = torch.arange(F, dtype=torch.int32, device=dev)
+    gen = torch.Generator(device="cpu")
+    gen.manual_seed(int(rng_seed))
+    G = _Grow(S)
+
+    # ---- roots
+    packs, counts = [], []
+    for j in jobs:
+        r = j.rows.to(dev)
+        w = None if j.weights is None else j.weights.to(dev)
+        if w is not None:
+            keep = w > 0
+            r, w = r[keep], w[keep]
+        packs.append(pack_rows(r, w))
+        counts.append(int(r.numel()))
+    rows = torch.cat(packs) if packs else torch.zeros(0, dtype=torch.int32, device=dev)
+    rows_alt = torch.empty_like(rows)
+    lv_tree = np.arange(T, dtype=np.int64)
+    lv_gid = G.add(lv_tree)
+    lv_count = np.asarray(counts, np.int64)
+    lv_begin = np.zeros(T, np.int64)
+    if T:
+        lv_begin[1:] = np.cumsum(lv_count[:-1])
+    max_depth = int(P_depth.max()) if T else 0
+
+    prev_hist = None          # previous level's histogram buffer
+    pair_parent_off = None    # per sibling pair: parent's offset in prev_hist
+    for depth in range(max_depth + 1):
+        n = lv_gid.size
+        if n == 0:
+            break
+        can = (depth < P_depth[lv_tree]) & (lv_count >= 2) & (lv_count >= 2 * P_inst[lv_tree] - 1e-9)
+        need = can | (depth == 0)
+        hist_nodes = np.nonzero(need)[0]
+        if hist_nodes.size == 0:
+            break
+        m = hist_nodes.size
+        h_tree = lv_tree[hist_nodes]
+        if use_subset:
+            feat_list, feat_off, nfeat = _feature_subsets(m, F, P_sub[h_tree], dev, gen)
+        else:
+            feat_list, feat_off, nfeat = all_feats, np.zeros(m, np.int32), np.full(m, F, np.int32)
+        hsz = nfeat.astype(np.int64) * B * S
+        hoff = np.zeros(m, np.int64)
+        if m > 1:
+            hoff[1:] = np.cumsum(hsz[:-1])
+        hist = torch.zeros(int(hsz.sum()), dtype=torch.float32, device=dev)
+        loc = np.full(n, -1, np.int64)
+        loc[hist_nodes] = np.arange(m)
+
+        # subtraction trick: children come in (left, right) pairs at positions (2q, 2q+1)
+        derive_big = np.zeros(0, np.int64)
+        derive_small = np.zeros(0, np.int64)
+        derive_poff = np.zeros(0, np.int64)
+        if subtract and not use_subset and prev_hist is not None and depth > 0:
+            lidx = np.arange(0, n, 2)
+            both = need[lidx] & need[lidx + 1]
+            q = np.nonzero(both)[0]
+            li, ri = lidx[q], lidx[q] + 1
+            left_big = lv_count[li] >= lv_count[ri]
+            big = np.where(left_big, li, ri)
+            small = np.where(left_big, ri, li)
+            derive_big, derive_small, derive_poff = loc[big], loc[small], pair_parent_off[q]
+        build = np.ones(m, bool)
+        build[derive_big] = False
+        build_local = np.nonzero(build)[0]
+
+        node_model = np.array([jobs[t].model for t in h_tree], np.int32) if T else np.zeros(0, np.int32)
+        nb_ = torch.as_tensor(lv_begin[hist_nodes], device=dev)
+        nc_ = torch.as_tensor(lv_count[hist_nodes], device=dev)
+        nfo = torch.as_tensor(feat_off, device=dev)
+        nnf = torch.as_tensor(nfeat, device=dev)
+        nmd = torch.as_tensor(node_model, device=dev)
+        nho = torch.as_tensor(hoff, device=dev)
+        if on_gpu:
+            items = _hist_items(build_local, lv_begin[hist_nodes], lv_count[hist_nodes], nfeat, chunk_rows)
+            if len(items):
+                it_t = torch.as_tensor(items.view(np.uint8), device=dev)
+                N.check(N.hip().tmog_hip_hist_build(
+                    N.ptr(Xb), F, N.ptr(rows), N.ptr(it_t), len(items), N.ptr(nfo), N.ptr(feat_list),
+                    N.ptr(nmd), N.ptr(nho), N.ptr(hist), B, mode, S, N.ptr(yf), N.ptr(t1f), N.ptr(t2f),
+                    stride, N.stream(dev)), "hist_build")
+            if derive_big.size:
+                par = torch.as_tensor(derive_poff, device=dev)
+                sm = torch.as_tensor(hoff[derive_small], device=dev)
+                oo = torch.as_tensor(hoff[derive_big], device=dev)
+                sz = torch.as_tensor(hsz[derive_big], device=dev)
+                N.check(N.hip().tmog_hip_hist_subtract(
+                    N.ptr(hist), N.ptr(prev_hist), N.ptr(par), N.ptr(sm), N.ptr(oo), N.ptr(sz), int(derive_big.size),
+                    int(hsz[derive_big].max()), N.stream(dev)), "hist_subtract")
+        else:
+            if build_local.size:
+                sel = torch.as_tensor(build_local, device=dev)
+                keep = [nb_[sel].contiguous(), nc_[sel].contiguous(), nfo[sel].contiguous(), nnf[sel].contiguous(),
+                        nmd[sel].contiguous(), nho[sel].contiguous()]
+                N.check(N.host().tmog_hist_build_cpu(
+                    N.ptr(Xb), Nrows, F, N.ptr(rows), int(build_local.size), N.ptr(keep[0]), N.ptr(keep[1]),
+                    N.ptr(keep[2]), N.ptr(keep[3]), N.ptr(feat_list), N.ptr(keep[4]), N.ptr(keep[5]), N.ptr(hist), B,
+                    mode, S, N.ptr(yf), N.ptr(t1f), N.ptr(t2f), stride), "hist_build_cpu")
+            for b_, s_, p_ in zip(derive_big, derive_small, derive_poff):
+                sz = int(hsz[b_])
+                hist[hoff[b_]:hoff[b_] + sz] = prev_hist[p_:p_ + sz] - hist[hoff[s_]:hoff[s_] + sz]
+
+        # ---- split scan
+        params = np.zeros((m, 8), np.float32)
+        params[:, 0] = P_inst[h_tree]
+        params[:, 1] = P_gain[h_tree]
+        params[:, 2] = P_mcw[h_tree]
+        params[:, 3] = P_lam[h_tree]
+        params[:, 5] = 1.0 if missing_bin >= 0 else 0.0
+        par_t = torch.as_tensor(params, device=dev)
+        s_feat = torch.empty(m, dtype=torch.int32, device=dev)
+        s_bin = torch.empty(m, dtype=torch.int32, device=dev)
+        s_gain = torch.empty(m, dtype=torch.float32, device=dev)
+        s_dl = torch.empty(m, dtype=torch.uint8, device=dev)
+        s_left = torch.empty(m * S, dtype=torch.float32, device=dev)
+        s_tot = torch.empty(m * S, dtype=torch.float32, device=dev)
+        fn = N.hip().tmog_hip_split_find if on_gpu else N.host().tmog_split_find_cpu
+        extra = (N.stream(dev),) if on_gpu else ()
+        N.check(fn(N.ptr(hist), m, N.ptr(nho), N.ptr(nnf), N.ptr(nfo), N.ptr(feat_list), N.ptr(n_bins_t), B, S,
+                   kind, N.ptr(par_t), missing_bin, N.ptr(s_feat), N.ptr(s_bin), N.ptr(s_gain), N.ptr(s_dl),
+                   N.ptr(s_left), N.ptr(s_tot), *extra), "split_find")
+        eps = torch.as_tensor(P_eps[h_tree].astype(np.float32), device=dev)
+        can_t = torch.as_tensor(can[hist_nodes], device=dev)
+        ok = can_t & (s_feat >= 0) & (s_gain > eps)
+        s_feat = torch.where(ok, s_feat, torch.full_like(s_feat, -1))
+
+        # ---- partition count (GPU), then one sync for every decision of the level
+        if on_gpu:
+            citems = _part_items(np.arange(m), lv_begin[hist_nodes], lv_count[hist_nodes], chunk_rows)
+            cit = torch.as_tensor(citems.view(np.uint8), device=dev)
+            chunk_left = torch.zeros(len(citems), dtype=torch.int64, device=dev)
+            N.check(N.hip().tmog_hip_partition_count(
+                N.ptr(Xb), F, N.ptr(rows), N.ptr(cit), len(citems), N.ptr(s_feat), N.ptr(s_bin), N.ptr(s_dl),
+                missing_bin, N.ptr(chunk_left), N.stream(dev)), "partition_count")
+            h_chunk_left = chunk_left.cpu().numpy()
+        h_feat = s_feat.cpu().numpy().astype(np.int64)
+        h_bin = s_bin.cpu().numpy().astype(np.int64)
+        h_gain = s_gain.cpu().numpy().astype(np.float64)
+        h_dl = s_dl.cpu().numpy()
+        h_left = s_left.cpu().numpy().reshape(m, S).astype(np.float64)
+        h_tot = s_tot.cpu().numpy().reshape(m, S).astype(np.float64)
+
+        g_h = lv_gid[hist_nodes]
+        G.tot[g_h] = h_tot
+        spl = h_feat >= 0
+        sl = np.nonzero(spl)[0]
+        if sl.size == 0:
+            break
+        gs = g_h[sl]
+        G.feat[gs], G.bin[gs], G.dl[gs], G.gain[gs] = h_feat[sl], h_bin[sl], h_dl[sl], h_gain[sl]
+
+        counts_sl = lv_count[hist_nodes[sl]]
+        out_begin = np.zeros(sl.size, np.int64)
+        out_begin[1:] = np.cumsum(counts_sl[:-1])
+        if on_gpu:
+            nl, sitems = _scatter_items(citems, h_chunk_left, sl, m, out_begin)
+            sit = torch.as_tensor(sitems.view(np.uint8), device=dev)
+            N.check(N.hip().tmog_hip_partition_scatter(
+                N.ptr(Xb), F, N.ptr(rows), N.ptr(rows_alt), N.ptr(sit), len(sitems), N.ptr(s_feat), N.ptr(s_bin),
+                N.ptr(s_dl), missing_bin, N.stream(dev)), "partition_scatter")
+        else:
+            lsel = torch.as_tensor(sl, device=dev)
+            ob = torch.as_tensor(out_begin, device=dev)
+            nl_t = torch.zeros(sl.size, dtype=torch.int64, device=dev)
+            keep = [nb_[lsel].contiguous(), nc_[lsel].contiguous(), s_feat[lsel].contiguous(),
+                    s_bin[lsel].contiguous(), s_dl[lsel].contiguous()]
+            N.check(N.host().tmog_partition_cpu(
+                N.ptr(Xb), F, N.ptr(rows), N.ptr(rows_alt), int(sl.size), N.ptr(keep[0]), N.ptr(keep[1]),
+                N.ptr(keep[2]), N.ptr(keep[3]), N.ptr(keep[4]), missing_bin, N.ptr(ob), N.ptr(nl_t)),
+                "partition_cpu")
+            nl = nl_t.numpy()
+
+        # ---- next level: children pairs (left, right) interleaved
+        ptree = lv_tree[hist_nodes[sl]]
+        ch_tree = np.repeat(ptree, 2)
+        ch = G.add(ch_tree)
+        gl, gr = ch[0::2], ch[1::2]
+        G.left[gs], G.right[gs] = gl, gr
+        G.tot[gl] = h_left[sl]
+        G.tot[gr] = h_tot[sl] - h_left[sl]
+        nlv = np.asarray(nl, np.int64)
+        new_begin = np.empty(2 * sl.size, np.int64)
+        new_begin[0::2] = out_begin
+        new_begin[1::2] = out_begin + nlv
+        new_count = np.empty(2 * sl.size, np.int64)
+        new_count[0::2] = nlv
+        new_count[1::2] = counts_sl - nlv
+        pair_parent_off = hoff[sl]
+        prev_hist = hist
+        rows, rows_alt = rows_alt, rows
+        lv_tree, lv_gid, lv_begin, lv_count = ch_tree, ch, new_begin, new_count
+
+    return _finalize(jobs, G, mode, kind, K, S, missing_bin)
+
+
+def _hist_items(build_local, begin, count, nfeat, chunk_rows):
+    if build_local.size == 0:
+        return np.zeros(0, HIST_ITEM)
+    cnt = count[build_local]
+    nf = nfeat[build_local].astype(np.int64)
+    ng = np.maximum(1, -(-nf // 64))
+    fg = -(-nf // ng)
+    nch = np.maximum(1, -(-cnt // chunk_rows))
+    rep = nch * ng
+    tot = int(rep.sum())
+    starts = np.zeros(build_local.size, np.int64)
+    starts[1:] = np.cumsum(rep[:-1])
+    within = np.arange(tot, dtype=np.int64) - np.repeat(starts, rep)
+    ngr, fgr, nfr = np.repeat(ng, rep), np.repeat(fg, rep), np.repeat(nf, rep)
+    c = within // ngr
+    g = within % ngr
+    a = np.zeros(tot, HIST_ITEM)
+    a["node"] = np.repeat(build_local, rep)
+    a["fg0"] = g * fgr
+    a["nf"] = np.minimum(fgr, nfr - g * fgr)
+    a["excl"] = np.repeat((nch == 1).astype(np.int64), rep)
+    a["begin"] = np.repeat(begin[build_local], rep) + c * chunk_rows
+    a["count"] = np.minimum(chunk_rows, np.repeat(cnt, rep) - c * chunk_rows)
+    return a
+
+
+def _part_items(local, begin, count, chunk_rows):
+    cnt = count[local]
+    nch = np.maximum(1, -(-cnt // chunk_rows))
+    tot = int(nch.sum())
+    starts = np.zeros(local.size, np.int64)
+    if local.size > 1:
+        starts[1:] = np.cumsum(nch[:-1])
+    within = np.arange(tot, dtype=np.int64) - np.repeat(starts, nch)
+    a = np.zeros(tot, PART_ITEM)
+    a["node"] = np.repeat(local, nch)
+    a["begin"] = np.repeat(begin[local], nch) + within * chunk_rows
+    a["count"] = np.minimum(chunk_rows, np.repeat(cnt, nch) - within * chunk_rows)
+    return a
+
+
+def _scatter_items(citems, chunk_left, split_local, m, out_begin):
+    """Per-chunk output offsets (stable scatter) for the splitting nodes; returns (left counts, items)."""
+    pos = np.full(m, -1, np.int64)
+    pos[split_local] = np.arange(split_local.size)
+    q = pos[citems["node"]]
+    keep = q >= 0
+    ci = citems[keep]
+    q = q[keep]
+    cl = chunk_left[keep].astype(np.int64)
+    cr = ci["count"] - cl
+    nl = np.bincount(q, weights=cl, minlength=split_local.size).astype(np.int64)
+    # exclusive running sums within each node's (contiguous) chunk run
+    cum_l = np.cumsum(cl) - cl
+    cum_r = np.cumsum(cr) - cr
+    first = np.ones(q.size, bool)
+    first[1:] = q[1:] != q[:-1]
+    run_id = np.cumsum(first) - 1
+    base_l = cum_l[first][run_id]
+    base_r = cum_r[first][run_id]
+    a = np.zeros(q.size, PART_ITEM)
+    a["node"] = ci["node"]
+    a["begin"] = ci["begin"]
+    a["count"] = ci["count"]
+    a["out_left"] = out_begin[q] + (cum_l - base_l)
+    a["out_right"] = out_begin[q] + nl[q] + (cum_r - base_r)
+    return nl, a
+
+
+def _finalize(jobs, G: _Grow, mode, kind, K, S, missing_bin):
+    n = G.n
+    tot = G.tot[:n]
+    left = G.left[:n].copy()
+    right = G.right[:n].copy()
+    feat = G.feat[:n].copy()
+    gain = G.gain[:n]
+    tree = G.tree[:n]
+    if mode == MODE_CLS:
+        s = tot.sum(1, keepdims=True)
+        value = np.where(s > 0, tot / np.maximum(s, 1e-300), 0.0)
+        cover = s[:, 0]
+    elif mode == MODE_VAR:
+        value = np.where(tot[:, :1] > 0, tot[:, 1:2] / np.maximum(tot[:, :1], 1e-300), 0.0)
+        cover = tot[:, 0]
+    else:
+        lam = np.array([j.params.reg_lambda for j in jobs])[tree]
+        eta = np.array([j.params.eta for j in jobs])[tree]
+        value = (-tot[:, 0] / (tot[:, 1] + lam) * eta)[:, None]
+        cover = tot[:, 1]
+    if kind == KIND_NEWTON:
+        gam = np.array([j.params.gamma for j in jobs])[tree]
+        while True:
+            idx = np.nonzero(left >= 0)[0]
+            if idx.size == 0:
+                break
+            leafy = (left[left[idx]] < 0) & (left[right[idx]] < 0)
+            prune = idx[leafy & (gain[idx] < gam[idx])]
+            if prune.size == 0:
+                break
+            left[prune] = -1
+            right[prune] = -1
+            feat[prune] = -1
+    # BFS renumbering per tree (drops pruned descendants); nodes of a tree are created in BFS order
+    # already, so a stable filter of reachable nodes preserves it.
+    reach = np.zeros(n, bool)
+    T = len(jobs)
+    roots = np.arange(T, dtype=np.int64)          # roots were created first, one per job
+    reach[roots] = True
+    # propagate reachability in creation order (parents precede children)
+    internal = np.nonzero(left >= 0)[0]
+    for g in internal:                             # creation order == topological order
+        if reach[g]:
+            reach[left[g]] = True
+            reach[right[g]] = True
+    keep = np.nonzero(reach)[0]
+    # group by tree, keeping creation order inside a tree
+    order = keep[np.argsort(tree[keep], kind="stable")]
+    new_id = np.full(n, -1, np.int64)
+    new_id[order] = np.arange(order.size)
+    tree_off = np.zeros(T + 1, np.int64)
+    tree_off[1:] = np.cumsum(np.bincount(tree[order], minlength=T))
+    isint = left[order] >= 0
+    nodes = np.zeros((order.size, 4), np.int32)
+    nodes[:, 0] = np.where(isint, feat[order], 0)
+    nodes[:, 1] = np.where(isint, G.bin[:n][order], 0)
+    nodes[:, 2] = np.where(isint, new_id[np.maximum(left[order], 0)], -1)
+    nodes[:, 3] = np.where(isint, new_id[np.maximum(right[order], 0)], -1)
+    return Forest(tree_off, nodes, np.where(isint, G.dl[:n][order], 0).astype(np.uint8),
+                  value[order].astype(np.float32).reshape(order.size, K),
+                  np.where(isint, gain[order], 0).astype(np.float32), cover[order].astype(np.float32),
+                  np.array([j.model for j in jobs], np.int32), missing_bin)
+
+
+def forest_predict(forest: Forest, Xb: torch.Tensor, model_rows: Sequence[Optional[torch.Tensor]],
+                   model_trees: Sequence[Sequence[int]], tree_weight: Optional[np.ndarray] = None,
+                   n_rows: Optional[int] = None) -> List[torch.Tensor]:
+    """Evaluate groups of trees ("models") on row subsets of ``Xb``.
+
+    ``model_rows[m]`` = row ids (or None for all rows); ``model_trees[m]`` = tree indices of the
+    forest that form model m. Returns one ``float32 [n_m, K]`` tensor per model: the weighted sum
+    of leaf values over the model's trees.
+    """
+    dev = Xb.device
+    Xb = Xb.contiguous()
+    Nrows, F = int(Xb.shape[0]), int(Xb.shape[1])
+    K = forest.K
+    # reorder trees so each model's trees are contiguous
+    order = [t for ts in model_trees for t in ts]
+    mto = np.zeros(len(model_trees) + 1, np.int64)
+    mto[1:] = np.cumsum([len(ts) for ts in model_trees])
+    tw = np.ones(forest.n_trees, np.float32) if tree_weight is None else np.asarray(tree_weight, np.float32)
+    t_off = torch.as_tensor(forest.tree_off[:-1][order].astype(np.int64), device=dev)
+    t_w = torch.as_tensor(tw[order], device=dev)
+    nodes = torch.as_tensor(np.ascontiguousarray(forest.nodes), device=dev)
+    dl = torch.as_tensor(forest.default_left, device=dev)
+    lv = torch.as_tensor(np.ascontiguousarray(forest.value), device=dev)
+    counts = [Nrows if r is None else int(r.numel()) for r in model_rows]
+    mro = np.zeros(len(model_rows) + 1, np.int64)
+    mro[1:] = np.cumsum(counts)
+    if all(r is None for r in model_rows):
+        row_list = None
+        if len(model_rows) > 1:
+            row_list = torch.cat([torch.arange(Nrows, device=dev, dtype=torch.int32)] * len(model_rows))
+    else:
+        row_list = torch.cat([(torch.arange(Nrows, device=dev) if r is None else r.to(dev)).to(torch.int32)
+                              for r in model_rows])
+    out = torch.zeros(int(mro[-1]), K, dtype=torch.float32, device=dev)
+    mro_t = torch.as_tensor(mro, device=dev)
+    mto_t = torch.as_tensor(mto, device=dev)
+    if dev.type == "cuda":
+        N.check(N.hip().tmog_hip_forest_predict(
+            N.ptr(Xb), F, len(model_rows), N.ptr(mro_t), N.ptr(row_list), max(counts) if counts else 0,
+            N.ptr(mto_t), N.ptr(t_off), N.ptr(t_w), N.ptr(nodes), N.ptr(dl), forest.missing_bin, N.ptr(lv), K,
+            N.ptr(out), N.stream(dev)), "forest_predict")
+    else:
+        N.check(N.host().tmog_forest_predict_cpu(
+            N.ptr(Xb), F, len(model_rows), N.ptr(mro_t), N.ptr(row_list), N.ptr(mto_t), N.ptr(t_off), N.ptr(t_w),
+            N.ptr(nodes), N.ptr(dl), forest.missing_bin, N.ptr(lv), K, N.ptr(out)), "forest_predict_cpu")
+    return [out[int(mro[m]):int(mro[m + 1])] for m in range(len(model_rows))]

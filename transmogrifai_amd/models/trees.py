@@ -1,0 +1,502 @@
+"""Tree learners on the batched histogram engine.
+
+Reference learners: ``OpDecisionTreeClassifier`` (``OpDecisionTreeClassifier.scala:47-115``),
+``OpRandomForestClassifier`` (``OpRandomForestClassifier.scala:59-154``), ``OpGBTClassifier`` (``OpGBTClassifier.scala:47-142``),
+``OpXGBoostClassifier`` (``OpXGBoostClassifier.scala:47-403``) and the regression counterparts. Spark MLlib
+semantics reproduced: quantile split candidates (``maxBins``), Poisson(1) bootstrap per tree when
+``numTrees > 1``, per-node feature subsets (``featureSubsetStrategy``: auto = sqrt / onethird),
+``minInstancesPerNode``, ``minInfoGain``, gini / entropy / variance impurity, RF probability = mean of
+normalized leaf distributions, GBT log-loss boosting on {-1, +1} labels with ``1/(1+exp(-2F))``.
+XGBoost: second-order gain, ``min_child_weight``, ``lambda``, ``gamma`` post-pruning, ``eta``-scaled
+leaves, learned default direction for missing values (``missing`` = 0.0 by default in the
+reference grid), early stopping on the training ``aucpr``.
+
+Every (config x fold x tree) of a learner grows in the same level-synchronous forest; boosting
+learners advance all their models one round per engine call.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import tree_engine as TE
+from .base import FitJob, Learner, OpPredictor, probability_outputs, register_learner
+from .binning import BinSpec, find_splits, quantize
+from ..stages.base import register_stage
+
+
+# --------------------------------------------------------------------------------------- context
+class TreeContext:
+    """Caches quantized matrices of one design matrix ``X`` per binning configuration."""
+
+    def __init__(self, X: torch.Tensor, rows: Optional[torch.Tensor] = None):
+        self.X = X
+        self.rows = rows
+        self._cache: Dict[tuple, tuple] = {}
+
+    def binned(self, max_bins: int, missing_value: Optional[float] = None, reserve_missing: bool = False):
+        key = (max_bins, missing_value, reserve_missing)
+        if key not in self._cache:
+            spec = find_splits(self.X, max_bins, missing_value=missing_value, reserve_missing=reserve_missing,
+                               rows=self.rows)
+            self._cache[key] = (spec, quantize(self.X, spec))
+        return self._cache[key]
+
+
+def _ctx(X, context):
+    if isinstance(context, TreeContext) and context.X is X:
+        return context
+    if isinstance(context, dict):
+        c = context.get("tree")
+        if c is None or c.X is not X:
+            c = TreeContext(X)
+            context["tree"] = c
+        return c
+    return TreeContext(X)
+
+
+def _subset_size(strategy, F: int, classification: bool, num_trees: int) -> int:
+    s = str(strategy).lower()
+    if s == "auto":
+        if num_trees == 1:
+            return F
+        s = "sqrt" if classification else "onethird"
+    if s == "all":
+        return F
+    if s == "sqrt":
+        return int(math.ceil(math.sqrt(F)))
+    if s == "log2":
+        return max(1, int(math.ceil(math.log2(F))))
+    if s == "onethird":
+        return int(math.ceil(F / 3.0))
+    try:
+        v = float(s)
+    except ValueError:
+        raise ValueError(f"bad featureSubsetStrategy {strategy}")
+    if v >= 1.0 and float(v).is_integer():
+        return min(F, int(v))
+    return max(1, int(math.ceil(v * F)))
+
+
+def _rows(job: FitJob, N, dev):
+    return torch.arange(N, device=dev) if job.rows is None else job.rows.to(dev)
+
+
+def _model_rows_forest_predict(forest, Xb, rows_list, trees_list, tree_weight=None):
+    return TE.forest_predict(forest, Xb, rows_list, trees_list, tree_weight)
+
+
+# ------------------------------------------------------------------------------------ RF / DT
+class _ForestLearner(Learner):
+    classification = True
+    default_trees = 20
+    is_forest = True
+
+    def _num_classes(self, y):
+        return max(2, int(y.max().item()) + 1) if y.numel() else 2
+
+    def fit_batch(self, X, y, jobs, context=None):
+        if not jobs:
+            return []
+        ctx = _ctx(X, context)
+        dev = X.device
+        N, F = X.shape
+        out: List[Optional[dict]] = [None] * len(jobs)
+        # group jobs by binning
+        groups: Dict[int, List[int]] = {}
+        for i, j in enumerate(jobs):
+            groups.setdefault(int(j.params.get("max_bins", 32)), []).append(i)
+        K = self._num_classes(y) if self.classification else 1
+        for mb, idxs in groups.items():
+            spec, Xb = ctx.binned(mb)
+            tjobs, owner = [], []
+            for i in idxs:
+                p = jobs[i].params
+                nt = int(p.get("num_trees", self.default_trees)) if self.is_forest else 1
+                rows = _rows(jobs[i], N, dev)
+                sub = _subset_size(p.get("feature_subset_strategy", "auto"), F, self.classification, nt)
+                tp = TE.TreeParams(max_depth=int(p.get("max_depth", 5)),
+                                   min_instances=float(p.get("min_instances_per_node", 1)),
+                                   min_info_gain=float(p.get("min_info_gain", 0.0)), feature_subset=sub)
+                seed = int(p.get("seed", 0)) + 7919 * i
+                rate = float(p.get("subsampling_rate", 1.0))
+                g = torch.Generator(device="cpu").manual_seed(seed)
+                for t in range(nt):
+                    if nt > 1:
+                        w = torch.poisson(torch.full((rows.numel(),), rate), generator=g).to(torch.int64).to(dev)
+                    elif rate < 1.0:
+                        w = (torch.rand(rows.numel(), generator=g) < rate).to(torch.int64).to(dev)
+                    else:
+                        w = jobs[i].weights.to(dev).round().to(torch.int64) if jobs[i].weights is not None else None
+                    tjobs.append(TE.TreeJob(0, tp, rows, w, seed + t))
+                    owner.append(i)
+            if self.classification:
+                forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_CLS,
+                                        kind=TE.KINDS[jobs[idxs[0]].params.get("impurity", "gini")], n_classes=K,
+                                        y=y, B=mb, rng_seed=int(jobs[idxs[0]].params.get("seed", 0)))
+            else:
+                forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_VAR, kind=TE.KIND_VARIANCE,
+                                        t1=y.to(torch.float32)[None, :], B=mb,
+                                        rng_seed=int(jobs[idxs[0]].params.get("seed", 0)))
+            owner = np.asarray(owner)
+            for i in idxs:
+                ts = np.nonzero(owner == i)[0]
+                sub = Forest_subset(forest, ts)
+                out[i] = {"forest": sub.to_state(), "bins": spec.to_state(), "n_classes": K,
+                          "num_trees": len(ts), "max_bins": mb, "n_features": F}
+        return out
+
+    # -- prediction
+    def _forest(self, state):
+        if "_forest" not in state:
+            state["_forest"] = TE.Forest.from_state(state["forest"])
+            state["_bins"] = BinSpec.from_state(state["bins"])
+        return state["_forest"], state["_bins"]
+
+    def _binned(self, state, X, context):
+        forest, spec = self._forest(state)
+        if context is not None:
+            ctx = _ctx(X, context)
+            key = (int(state["max_bins"]), spec.missing_value, spec.missing_bin >= 0)
+            if key in ctx._cache and np.array_equal(ctx._cache[key][0].thresholds, spec.thresholds):
+                return forest, ctx._cache[key][1]
+        return forest, quantize(X, spec)
+
+    def raw_sum(self, state, X, rows=None, context=None):
+        forest, Xb = self._binned(state, X, context)
+        return TE.forest_predict(forest, Xb, [rows], [list(range(forest.n_trees))])[0].to(torch.float64)
+
+    def predict(self, state, X, context=None):
+        return self._outputs(state, self.raw_sum(state, X, None, context))
+
+    def predict_batch(self, states, X, rows, context=None):
+        if not states:
+            return []
+        # one traversal launch for all models that share a binning
+        groups: Dict[int, List[int]] = {}
+        for i, s in enumerate(states):
+            groups.setdefault(int(s["max_bins"]), []).append(i)
+        res = [None] * len(states)
+        for mb, idxs in groups.items():
+            forests = [self._forest(states[i])[0] for i in idxs]
+            _, Xb = self._binned(states[idxs[0]], X, context)
+            big = TE.Forest.concat(forests)
+            off = np.cumsum([0] + [f.n_trees for f in forests])
+            raws = TE.forest_predict(big, Xb, [rows[i] for i in idxs],
+                                     [list(range(off[k], off[k + 1])) for k in range(len(idxs))])
+            for k, i in enumerate(idxs):
+                res[i] = self._outputs(states[i], raws[k].to(torch.float64))
+        return res
+
+    def _outputs(self, state, raw):
+        if not self.classification:
+            nt = max(1, int(state.get("num_trees", 1)))
+            p = raw[:, 0] / (nt if self.is_forest else 1)
+            e = torch.zeros(p.shape[0], 0, dtype=torch.float64, device=p.device)
+            return p, e, e
+        s = raw.sum(1, keepdim=True)
+        prob = torch.where(s > 0, raw / s.clamp_min(1e-300), torch.full_like(raw, 1.0 / raw.shape[1]))
+        if not self.is_forest:
+            raw = raw  # DT raw = leaf distribution (normalized counts)
+        pred = torch.argmax(raw, 1).to(torch.float64)
+        return pred, raw, prob
+
+    def feature_contributions(self, state, d):
+        forest, _ = self._forest(state)
+        return forest.feature_importance(d)
+
+
+def Forest_subset(forest: TE.Forest, trees: np.ndarray) -> TE.Forest:
+    return TE.Forest.concat([forest.tree(int(t)) for t in trees]) if len(trees) else forest
+
+
+@register_learner
+class RandomForestClassifierLearner(_ForestLearner):
+    name = "OpRandomForestClassifier"
+    problem = "multiclass"
+    defaults = {"max_depth": 5, "max_bins": 32, "min_instances_per_node": 1, "min_info_gain": 0.0,
+                "num_trees": 20, "impurity": "gini", "subsampling_rate": 1.0, "feature_subset_strategy": "auto",
+                "seed": 0}
+
+
+@register_learner
+class DecisionTreeClassifierLearner(_ForestLearner):
+    name = "OpDecisionTreeClassifier"
+    problem = "multiclass"
+    is_forest = False
+    defaults = {"max_depth": 5, "max_bins": 32, "min_instances_per_node": 1, "min_info_gain": 0.0,
+                "impurity": "gini", "seed": 0}
+
+
+@register_learner
+class RandomForestRegressorLearner(_ForestLearner):
+    name = "OpRandomForestRegressor"
+    problem = "regression"
+    classification = False
+    defaults = {"max_depth": 5, "max_bins": 32, "min_instances_per_node": 1, "min_info_gain": 0.0,
+                "num_trees": 20, "impurity": "variance", "subsampling_rate": 1.0,
+                "feature_subset_strategy": "auto", "seed": 0}
+
+
+@register_learner
+class DecisionTreeRegressorLearner(_ForestLearner):
+    name = "OpDecisionTreeRegressor"
+    problem = "regression"
+    classification = False
+    is_forest = False
+    defaults = {"max_depth": 5, "max_bins": 32, "min_instances_per_node": 1, "min_info_gain": 0.0,
+                "impurity": "variance", "seed": 0}
+
+
+# -------------------------------------------------------------------------------- boosting
+class _BoostLearner(Learner):
+    """Shared boosting loop: all jobs advance one round per engine call."""
+    classification = True
+
+    def _rounds(self, p):
+        raise NotImplementedError
+
+    def fit_batch(self, X, y, jobs, context=None):
+        if not jobs:
+            return []
+        ctx = _ctx(X, context)
+        dev = X.device
+        N, F = X.shape
+        out = [None] * len(jobs)
+        groups: Dict[tuple, List[int]] = {}
+        for i, j in enumerate(jobs):
+            groups.setdefault(self._bin_key(j.params), []).append(i)
+        for key, idxs in groups.items():
+            spec, Xb = ctx.binned(*key)
+            res = self._boost(Xb, spec, y.to(dev), [jobs[i] for i in idxs], N, F, dev, key[0])
+            for k, i in enumerate(idxs):
+                out[i] = res[k]
+        return out
+
+    def _bin_key(self, p):
+        return (int(p.get("max_bins", 32)), None, False)
+
+    def _forest(self, state):
+        if "_forest" not in state:
+            state["_forest"] = TE.Forest.from_state(state["forest"])
+            state["_bins"] = BinSpec.from_state(state["bins"])
+        return state["_forest"], state["_bins"]
+
+    def margin(self, state, X, rows=None, context=None):
+        forest, spec = self._forest(state)
+        Xb = None
+        if context is not None:
+            ctx = _ctx(X, context)
+            for (k, v) in ctx._cache.items():
+                if np.array_equal(v[0].thresholds, spec.thresholds) and v[0].missing_bin == spec.missing_bin:
+                    Xb = v[1]
+        if Xb is None:
+            Xb = quantize(X, spec)
+        m = TE.forest_predict(forest, Xb, [rows], [list(range(forest.n_trees))],
+                              np.asarray(state["tree_weights"], np.float32))[0][:, 0].to(torch.float64)
+        return m + float(state.get("base_margin", 0.0))
+
+    def predict(self, state, X, context=None):
+        return self._outputs(state, self.margin(state, X, None, context))
+
+    def predict_batch(self, states, X, rows, context=None):
+        return [self._outputs(s, self.margin(s, X, r, context)) for s, r in zip(states, rows)]
+
+    def feature_contributions(self, state, d):
+        forest, _ = self._forest(state)
+        return forest.feature_importance(d)
+
+
+@register_learner
+class GBTClassifierLearner(_BoostLearner):
+    """Spark GBT with log loss (``OpGBTClassifier.scala:47-142``)."""
+    name = "OpGBTClassifier"
+    defaults = {"max_depth": 5, "max_bins": 32, "min_instances_per_node": 1, "min_info_gain": 0.0, "max_iter": 20,
+                "step_size": 0.1, "subsampling_rate": 1.0, "impurity": "variance", "loss_type": "logistic",
+                "seed": 0}
+
+    def _target(self, yy, Fm, first):
+        ys = 2 * yy - 1
+        if first:
+            return ys
+        return 4 * ys / (1 + torch.exp(2 * ys * Fm))
+
+    def _boost(self, Xb, spec, y, jobs, N, F, dev, mb):
+        P = len(jobs)
+        rows = [_rows(j, N, dev) for j in jobs]
+        iters = [int(j.params.get("max_iter", 20)) for j in jobs]
+        Fm = torch.zeros(P, N, dtype=torch.float64, device=dev)
+        yy = y.to(torch.float64)
+        forests, weights = [[] for _ in range(P)], [[] for _ in range(P)]
+        for it in range(max(iters)):
+            act = [p for p in range(P) if it < iters[p]]
+            t1 = torch.stack([self._target(yy, Fm[p], it == 0) for p in range(P)]).to(torch.float32)
+            tjobs = []
+            for p in act:
+                pr = jobs[p].params
+                tp = TE.TreeParams(max_depth=int(pr.get("max_depth", 5)),
+                                   min_instances=float(pr.get("min_instances_per_node", 1)),
+                                   min_info_gain=float(pr.get("min_info_gain", 0.0)))
+                r = rows[p]
+                rate = float(pr.get("subsampling_rate", 1.0))
+                w = None
+                if rate < 1.0:
+                    g = torch.Generator().manual_seed(int(pr.get("seed", 0)) + 131 * it + p)
+                    w = (torch.rand(r.numel(), generator=g) < rate).to(torch.int64).to(dev)
+                tjobs.append(TE.TreeJob(p, tp, r, w))
+            forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_VAR, kind=TE.KIND_VARIANCE, t1=t1, B=mb)
+            preds = TE.forest_predict(forest, Xb, [None] * len(act), [[k] for k in range(len(act))])
+            for k, p in enumerate(act):
+                wgt = 1.0 if it == 0 else float(jobs[p].params.get("step_size", 0.1))
+                Fm[p] += wgt * preds[k][:, 0].to(torch.float64)
+                forests[p].append(forest.tree(k))
+                weights[p].append(wgt)
+        return [{"forest": TE.Forest.concat(forests[p]).to_state(), "bins": spec.to_state(),
+                 "tree_weights": np.asarray(weights[p], np.float32), "n_classes": 2, "max_bins": mb,
+                 "num_trees": len(forests[p])} for p in range(P)]
+
+    def _outputs(self, state, m):
+        p1 = 1.0 / (1.0 + torch.exp(-2.0 * m))
+        raw = torch.stack([-m, m], 1)
+        prob = torch.stack([1 - p1, p1], 1)
+        return (p1 > 0.5).to(torch.float64), raw, prob
+
+
+@register_learner
+class GBTRegressorLearner(GBTClassifierLearner):
+    name = "OpGBTRegressor"
+    problem = "regression"
+    classification = False
+    defaults = {"max_depth": 5, "max_bins": 32, "min_instances_per_node": 1, "min_info_gain": 0.0, "max_iter": 20,
+                "step_size": 0.1, "subsampling_rate": 1.0, "impurity": "variance", "loss_type": "squared",
+                "seed": 0}
+
+    def _target(self, yy, Fm, first):
+        if first:
+            return yy
+        return 2 * (yy - Fm)   # -gradient of squared error (Spark SquaredError)
+
+    def _outputs(self, state, m):
+        e = torch.zeros(m.shape[0], 0, dtype=torch.float64, device=m.device)
+        return m, e, e
+
+
+@register_learner
+class XGBoostClassifierLearner(_BoostLearner):
+    """Newton boosting with XGBoost semantics (binary:logistic)."""
+    name = "OpXGBoostClassifier"
+    defaults = {"num_round": 100, "eta": 0.3, "gamma": 0.0, "max_depth": 6, "min_child_weight": 1.0,
+                "reg_lambda": 1.0, "missing": float("nan"), "max_bins": 64, "num_early_stopping_rounds": 0,
+                "eval_metric": "aucpr", "maximize_evaluation_metrics": True, "objective": "binary:logistic",
+                "base_score": 0.5, "subsample": 1.0, "colsample_bytree": 1.0, "seed": 0}
+
+    def _bin_key(self, p):
+        miss = p.get("missing", float("nan"))
+        mv = None if (miss is None or (isinstance(miss, float) and math.isnan(miss))) else float(miss)
+        return (int(p.get("max_bins", 64)), mv, True)
+
+    def _grad(self, yy, Fm):
+        p = torch.sigmoid(Fm)
+        return p - yy, (p * (1 - p)).clamp_min(1e-16)
+
+    def _base_margin(self, bs):
+        bs = min(max(bs, 1e-12), 1 - 1e-12)
+        return math.log(bs / (1 - bs))
+
+    def _boost(self, Xb, spec, y, jobs, N, F, dev, mb):
+        from ..evaluators.metrics import binned_aupr
+        P = len(jobs)
+        rows = [_rows(j, N, dev) for j in jobs]
+        rounds = [int(j.params.get("num_round", 100)) for j in jobs]
+        esr = [int(j.params.get("num_early_stopping_rounds", 0)) for j in jobs]
+        base = [self._base_margin(float(j.params.get("base_score", 0.5))) for j in jobs]
+        Fm = torch.tensor(base, dtype=torch.float64, device=dev)[:, None].repeat(1, N)
+        yy = y.to(torch.float64)
+        forests, weights = [[] for _ in range(P)], [[] for _ in range(P)]
+        best = [-float("inf")] * P
+        best_round = [0] * P
+        stopped = [False] * P
+        for it in range(max(rounds)):
+            act = [p for p in range(P) if it < rounds[p] and not stopped[p]]
+            if not act:
+                break
+            G = torch.empty(P, N, dtype=torch.float32, device=dev)
+            H = torch.empty(P, N, dtype=torch.float32, device=dev)
+            for p in act:
+                g, h = self._grad(yy, Fm[p])
+                G[p], H[p] = g.to(torch.float32), h.to(torch.float32)
+            tjobs = []
+            for p in act:
+                pr = jobs[p].params
+                tp = TE.TreeParams(max_depth=int(pr.get("max_depth", 6)),
+                                   min_child_weight=float(pr.get("min_child_weight", 1.0)),
+                                   reg_lambda=float(pr.get("reg_lambda", 1.0)), gamma=float(pr.get("gamma", 0.0)),
+                                   eta=float(pr.get("eta", 0.3)), split_eps=1e-6)
+                r = rows[p]
+                w = None
+                ss = float(pr.get("subsample", 1.0))
+                if ss < 1.0:
+                    gen = torch.Generator().manual_seed(int(pr.get("seed", 0)) + 17 * it + p)
+                    w = (torch.rand(r.numel(), generator=gen) < ss).to(torch.int64).to(dev)
+                tjobs.append(TE.TreeJob(p, tp, r, w))
+            forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
+                                    missing_bin=spec.missing_bin)
+            preds = TE.forest_predict(forest, Xb, [None] * len(act), [[k] for k in range(len(act))])
+            for k, p in enumerate(act):
+                Fm[p] += preds[k][:, 0].to(torch.float64)
+                forests[p].append(forest.tree(k))
+                weights[p].append(1.0)
+            # early stopping on the training metric (the reference sets no eval set)
+            need = [p for p in act if esr[p] > 0]
+            if need and self.classification:
+                scores = torch.stack([torch.sigmoid(Fm[p][rows[p]]) for p in need]) if \
+                    len({rows[p].numel() for p in need}) == 1 else None
+                for k, p in enumerate(need):
+                    s = scores[k] if scores is not None else torch.sigmoid(Fm[p][rows[p]])
+                    v = binned_aupr(s, yy[rows[p]])
+                    if v > best[p] + 1e-12:
+                        best[p], best_round[p] = v, it
+                    elif it - best_round[p] >= esr[p]:
+                        stopped[p] = True
+        res = []
+        for p in range(P):
+            keep = len(forests[p]) if not stopped[p] else best_round[p] + 1
+            res.append({"forest": TE.Forest.concat(forests[p][:keep]).to_state(), "bins": spec.to_state(),
+                        "tree_weights": np.asarray(weights[p][:keep], np.float32), "n_classes": 2,
+                        "max_bins": mb, "base_margin": base[p], "num_trees": keep})
+        return res
+
+    def _outputs(self, state, m):
+        return probability_outputs(m)
+
+
+@register_learner
+class XGBoostRegressorLearner(XGBoostClassifierLearner):
+    name = "OpXGBoostRegressor"
+    problem = "regression"
+    classification = False
+    defaults = dict(XGBoostClassifierLearner.defaults, objective="reg:squarederror", eval_metric="rmse",
+                    maximize_evaluation_metrics=False)
+
+    def _grad(self, yy, Fm):
+        return Fm - yy, torch.ones_like(Fm)
+
+    def _base_margin(self, bs):
+        return float(bs)
+
+    def _outputs(self, state, m):
+        e = torch.zeros(m.shape[0], 0, dtype=torch.float64, device=m.device)
+        return m, e, e
+
+
+for _name, _cls in [("OpRandomForestClassifier", RandomForestClassifierLearner),
+                    ("OpDecisionTreeClassifier", DecisionTreeClassifierLearner),
+                    ("OpRandomForestRegressor", RandomForestRegressorLearner),
+                    ("OpDecisionTreeRegressor", DecisionTreeRegressorLearner),
+                    ("OpGBTClassifier", GBTClassifierLearner), ("OpGBTRegressor", GBTRegressorLearner),
+                    ("OpXGBoostClassifier", XGBoostClassifierLearner),
+                    ("OpXGBoostRegressor", XGBoostRegressorLearner)]:
+    globals()[_name] = register_stage(type(_name, (OpPredictor,), {"operation_name": _name, "learner_cls": _cls}))

@@ -1,0 +1,110 @@
+"""ctypes bindings to the in-tree native libraries.
+
+The HIP library must be loaded *after* ``torch`` so that it binds to the HIP runtime torch has
+already mapped (same ``libamdhip64.so.7`` soname): kernels then run on torch's device/streams and
+take ``torch.cuda.current_stream().cuda_stream`` as their ``hipStream_t``.
+
+Device kernels fail loudly: if a CUDA tensor reaches an op and ``libtmog_hip.so`` cannot be built
+or loaded, :func:`hip` raises instead of silently falling back to a slower path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+from . import build
+
+_lock = threading.Lock()
+_host = None
+_hip = None
+
+P = C.c_void_p
+I32 = C.c_int32
+I64 = C.c_int64
+F32 = C.c_float
+
+_HOST_SIGS = {
+    "tmog_hist_build_cpu": [P, I64, I32, P, I32, P, P, P, P, P, P, P, P, I32, I32, I32, P, P, P, I64],
+    "tmog_split_find_cpu": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P],
+    "tmog_partition_cpu": [P, I32, P, P, I32, P, P, P, P, P, I32, P, P],
+    "tmog_forest_predict_cpu": [P, I32, I32, P, P, P, P, P, P, P, I32, P, I32, P],
+    "tmog_find_splits_cpu": [P, I64, I32, I32, P, P],
+    "tmog_murmur3_batch": [P, P, I64, I32, P],
+    "tmog_hash_index_batch": [P, P, I64, I32, I32, P],
+    "tmog_col_stats_cpu": [P, P, I64, I32, I64, P],
+    "tmog_tokenize_batch": [P, P, I64, I32, I32, P, P, P, I64],
+}
+
+_HIP_SIGS = {
+    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P],
+    "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
+    "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, P],
+    "tmog_hip_partition_count": [P, I32, P, P, I32, P, P, P, I32, P, P],
+    "tmog_hip_partition_scatter": [P, I32, P, P, P, I32, P, P, P, I32, P],
+    "tmog_hip_forest_predict": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P],
+    "tmog_hip_col_stats": [P, P, I64, I32, I64, P, P],
+    "tmog_hip_vectorize_numeric": [P, P, P, I64, I32, P, P, P, P, I64, I32, P],
+    "tmog_hip_onehot_pivot": [P, I64, I32, P, P, P, P, I64, I32, P],
+    "tmog_hip_quantize": [P, I64, I32, I64, P, P, P, I32, P, I64, P],
+    "tmog_hip_gram_f32": [P, I64, I32, I64, P, I32, P],
+    "tmog_hip_logistic_grad": [P, P, P, I64, I32, P],
+    "tmog_hip_label_colsum": [P, P, I64, I32, I64, I32, P, P],
+}
+
+
+def _declare(lib, sigs):
+    for name, args in sigs.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = args
+        fn.restype = C.c_int
+
+
+def host():
+    global _host
+    if _host is None:
+        with _lock:
+            if _host is None:
+                path = build.build_host()
+                lib = C.CDLL(str(path))
+                _declare(lib, _HOST_SIGS)
+                _host = lib
+    return _host
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        with _lock:
+            if _hip is None:
+                if os.environ.get("TMOG_DISABLE_HIP") == "1":
+                    raise RuntimeError("HIP kernels disabled by TMOG_DISABLE_HIP=1 but a device tensor was passed")
+                path = build.build_hip()
+                torch.cuda.init()
+                lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+                _declare(lib, _HIP_SIGS)
+                _hip = lib
+    return _hip
+
+
+def hip_loaded() -> bool:
+    return _hip is not None
+
+
+def ptr(t) -> int:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError(f"native kernel {name} failed with code {rc}")

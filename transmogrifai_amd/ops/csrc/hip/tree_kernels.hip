@@ -1,0 +1,498 @@
+// Histogram tree engine kernels for CDNA4 (gfx950).
+//
+// Replaces the per-level statistics aggregation of Spark MLlib trees (DTStatsAggregator, used by
+// OpRandomForestClassifier.scala:59-154 / OpGBTClassifier.scala:47-142 / DT) and XGBoost4J's
+// hist updater (OpXGBoostClassifier.scala:47-403): SURVEY.md kernels K23 (histogram, split scan,
+// partition), K24/K25 (GBT / Newton stats) and K29 (ensemble traversal).
+//
+// Layout contract (identical to ../host/tree_cpu.cpp, orchestrated by models/tree_engine.py):
+//   Xb    uint8 [N][F] row-major bins          rows  uint32 (row | weight<<24)
+//   hist  float, node j at node_hist_off[j], index ((fl * B) + bin) * S + s
+//
+// Histogram kernel mapping (wave64-first): a wave-instruction covers R = 64 / FG rows x FG
+// features -- lane (r, f) handles feature f of row r. Lanes of one instruction therefore touch
+// distinct LDS histogram rows (feature-major, padded by one word so bank = f + bin*S + s spreads),
+// and the R row-slots get private LDS copies, so no two lanes of an instruction ever hit the same
+// address. Per-row data (row id, weight, label / gradients) is loaded once per lane group. All
+// waves of the workgroup share the LDS copies through ds_add_f32. The R copies are folded on the
+// way out; a node covered by one row-chunk stores with plain stores, otherwise float atomics.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#define TM_MAX_S 16
+
+namespace {
+
+struct HistItem {
+  int32_t node;     // node slot
+  int32_t fg0;      // first local feature of this group
+  int32_t nf;       // features in this group (<= 64)
+  int32_t excl;     // 1 => this item alone covers node rows for its features (plain stores)
+  int64_t begin;    // first row entry
+  int64_t count;    // row entries in this chunk
+};
+
+template <int MODE>
+__device__ __forceinline__ void row_stats(int64_t r, float w, int64_t model, int64_t stride, const float* __restrict__ y,
+                                          const float* __restrict__ t1, const float* __restrict__ t2, int S, int cls_lane,
+                                          float* st) {
+  if (MODE == 0) {
+    // classification: only the label slot is non-zero; kept as (class, w)
+    st[0] = w;
+    st[1] = y[r];
+  } else if (MODE == 1) {
+    const float t = t1[model * stride + r];
+    st[0] = w; st[1] = w * t; st[2] = w * t * t;
+  } else {
+    st[0] = w * t1[model * stride + r];
+    st[1] = w * t2[model * stride + r];
+  }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) hist_build_kernel(
+    const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const HistItem* __restrict__ items,
+    const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
+    const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, float* __restrict__ hist, int B,
+    int S, const float* __restrict__ y, const float* __restrict__ t1, const float* __restrict__ t2, int64_t stride) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const HistItem it = items[blockIdx.x];
+  const int FG = it.nf;
+  const int R = 64 / FG;
+  const int rowstride = B * S + 1;            // padded feature row
+  const int ncopy_words = R * FG * rowstride;  // <= 64 * rowstride
+  for (int i = threadIdx.x; i < ncopy_words; i += blockDim.x) lds[i] = 0.f;
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nwaves = blockDim.x >> 6;
+  const int rsub = lane / FG;
+  const int fidx = lane - rsub * FG;
+  const bool active = rsub < R;
+  const int feat = active ? feat_list[node_feat_off[it.node] + it.fg0 + fidx] : 0;
+  const int64_t model = node_model ? node_model[it.node] : 0;
+  float* my = lds + (rsub * FG + fidx) * rowstride;
+  const uint32_t* rp = rows + it.begin;
+  const int64_t cnt = it.count;
+  const int64_t step = (int64_t)nwaves * R;
+
+  // 4 rows in flight per lane to overlap the dependent (entry -> bin) gathers
+  int64_t i = (int64_t)wave * R + rsub;
+  for (; i + 3 * step < cnt; i += 4 * step) {
+    uint32_t e[4];
+    int bin[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) e[u] = active ? rp[i + u * step] : 0u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bin[u] = active ? (int)Xb[(int64_t)(e[u] & 0xFFFFFFu) * F + feat] : 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!active) continue;
+      const int64_t r = e[u] & 0xFFFFFFu;
+      const float w = (float)(e[u] >> 24);
+      float st[3];
+      row_stats<MODE>(r, w, model, stride, y, t1, t2, S, 0, st);
+      if (MODE == 0) {
+        atomicAdd(my + bin[u] * S + (int)st[1], st[0]);
+      } else if (MODE == 1) {
+        float* hb = my + bin[u] * 3;
+        atomicAdd(hb, st[0]); atomicAdd(hb + 1, st[1]); atomicAdd(hb + 2, st[2]);
+      } else {
+        float* hb = my + bin[u] * 2;
+        atomicAdd(hb, st[0]); atomicAdd(hb + 1, st[1]);
+      }
+    }
+  }
+  for (; i < cnt; i += step) {
+    if (!active) continue;
+    const uint32_t e = rp[i];
+    const int64_t r = e & 0xFFFFFFu;
+    const int bin = Xb[r * F + feat];
+    const float w = (float)(e >> 24);
+    float st[3];
+    row_stats<MODE>(r, w, model, stride, y, t1, t2, S, 0, st);
+    if (MODE == 0) {
+      atomicAdd(my + bin * S + (int)st[1], st[0]);
+    } else if (MODE == 1) {
+      float* hb = my + bin * 3;
+      atomicAdd(hb, st[0]); atomicAdd(hb + 1, st[1]); atomicAdd(hb + 2, st[2]);
+    } else {
+      float* hb = my + bin * 2;
+      atomicAdd(hb, st[0]); atomicAdd(hb + 1, st[1]);
+    }
+  }
+  __syncthreads();
+
+  // fold the R private copies and write the node histogram of this feature group
+  float* out = hist + node_hist_off[it.node] + (int64_t)it.fg0 * B * S;
+  const int words = FG * B * S;
+  for (int k = threadIdx.x; k < words; k += blockDim.x) {
+    const int f = k / (B * S);
+    const int rem = k - f * (B * S);
+    float acc = 0.f;
+    for (int r = 0; r < R; ++r) acc += lds[(r * FG + f) * rowstride + rem];
+    if (it.excl) out[k] = acc;
+    else if (acc != 0.f) atomicAdd(out + k, acc);
+  }
+}
+
+// sibling = parent - small (histogram subtraction trick), size words each
+__global__ void hist_subtract_kernel(float* __restrict__ hist, const float* __restrict__ parent,
+                                     const int64_t* __restrict__ parent_off, const int64_t* __restrict__ small_off,
+                                     const int64_t* __restrict__ out_off, const int64_t* __restrict__ size, int n) {
+  const int j = blockIdx.y;
+  if (j >= n) return;
+  const int64_t sz = size[j];
+  const float* p = parent + parent_off[j];
+  const float* s = hist + small_off[j];
+  float* o = hist + out_off[j];
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += (int64_t)gridDim.x * blockDim.x)
+    o[k] = p[k] - s[k];
+}
+
+// ------------------------------------------------------------------------------- split finding
+__device__ __forceinline__ double impurity_dev(const double* st, int S, int kind, double* cnt) {
+  if (kind == 0 || kind == 1) {
+    double n = 0;
+    for (int s = 0; s < S; ++s) n += st[s];
+    *cnt = n;
+    if (n <= 0) return 0.0;
+    double imp = kind == 0 ? 1.0 : 0.0;
+    for (int s = 0; s < S; ++s) {
+      const double p = st[s] / n;
+      if (kind == 0) imp -= p * p;
+      else if (p > 0) imp -= p * log2(p);
+    }
+    return imp;
+  }
+  if (kind == 2) {
+    const double n = st[0];
+    *cnt = n;
+    if (n <= 0) return 0.0;
+    const double m = st[1] / n;
+    return st[2] / n - m * m;
+  }
+  *cnt = st[1];
+  return 0.0;
+}
+
+struct Best {
+  double gain;
+  int f;    // local feature index (tie-break)
+  int b;
+  int dl;
+};
+
+__device__ __forceinline__ bool better(const Best& a, const Best& b) {
+  if (a.gain != b.gain) return a.gain > b.gain;
+  if (a.f != b.f) return a.f < b.f;
+  if (a.dl != b.dl) return a.dl < b.dl;
+  return a.b < b.b;
+}
+
+// One workgroup (4 waves) per node; each wave scans features (lane = bin, B <= 64) with a
+// double-precision wave prefix sum, then the block reduces the best (gain, f, dl, b).
+__global__ void __launch_bounds__(256) split_find_kernel(
+    const float* __restrict__ hist, const int64_t* __restrict__ node_hist_off, const int32_t* __restrict__ node_nfeat,
+    const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
+    const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
+    int missing_bin, int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin, float* __restrict__ out_gain,
+    uint8_t* __restrict__ out_dl, float* __restrict__ out_left, float* __restrict__ out_total) {
+  const int j = blockIdx.x;
+  const float* h = hist + node_hist_off[j];
+  const int nf = node_nfeat[j];
+  const int32_t* fl = feat_list + node_feat_off[j];
+  const float* P = node_params + (int64_t)j * 8;
+  const double min_inst = P[0], min_gain = P[1], mcw = P[2], lambda = P[3];
+  const bool allow_missing = P[5] > 0.5f && missing_bin >= 0;
+  __shared__ double s_tot[TM_MAX_S];
+  __shared__ Best s_best[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x < S) {
+    double t = 0;
+    for (int b = 0; b < B; ++b) t += h[b * S + threadIdx.x];
+    s_tot[threadIdx.x] = t;
+    out_total[(int64_t)j * S + threadIdx.x] = (float)t;
+  }
+  __syncthreads();
+  double tot[TM_MAX_S];
+  for (int s = 0; s < S; ++s) tot[s] = s_tot[s];
+  double tcount;
+  const double pimp = impurity_dev(tot, S, kind, &tcount);
+  const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
+
+  Best best{-INFINITY, 0x7fffffff, 0, 0};
+  for (int f = wave; f < nf; f += 4) {
+    const int nb = feat_nbins[fl[f]];
+    const float* hf = h + (int64_t)f * B * S;
+    double v[TM_MAX_S], miss[TM_MAX_S];
+    for (int s = 0; s < S; ++s) {
+      v[s] = (lane < nb - 1) ? (double)hf[lane * S + s] : 0.0;
+      miss[s] = allow_missing ? (double)hf[missing_bin * S + s] : 0.0;
+    }
+    // inclusive wave prefix over bins
+    for (int off = 1; off < 64; off <<= 1) {
+      for (int s = 0; s < S; ++s) {
+        const double o = __shfl_up(v[s], off, 64);
+        if (lane >= off) v[s] += o;
+      }
+    }
+    if (lane < nb - 1) {
+      for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
+        double left[TM_MAX_S], right[TM_MAX_S];
+        for (int s = 0; s < S; ++s) {
+          left[s] = v[s] + (dl ? miss[s] : 0.0);
+          right[s] = tot[s] - left[s];
+        }
+        double gain;
+        bool ok = true;
+        if (kind == 3) {
+          if (left[1] < mcw || right[1] < mcw) ok = false;
+          gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
+        } else {
+          double lc, rc;
+          const double li = impurity_dev(left, S, kind, &lc);
+          const double ri = impurity_dev(right, S, kind, &rc);
+          if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) ok = false;
+          gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
+          if (gain < min_gain) ok = false;
+        }
+        if (ok) {
+          Best c{gain, f, lane, dl};
+          if (better(c, best)) best = c;
+        }
+      }
+    }
+  }
+  // wave reduce
+  for (int off = 32; off > 0; off >>= 1) {
+    Best o;
+    o.gain = __shfl_xor(best.gain, off, 64);
+    o.f = __shfl_xor(best.f, off, 64);
+    o.b = __shfl_xor(best.b, off, 64);
+    o.dl = __shfl_xor(best.dl, off, 64);
+    if (better(o, best)) best = o;
+  }
+  if (lane == 0) s_best[wave] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Best b = s_best[0];
+    for (int w = 1; w < 4; ++w)
+      if (better(s_best[w], b)) b = s_best[w];
+    const bool found = b.f != 0x7fffffff && b.gain > -INFINITY;
+    out_feat[j] = found ? fl[b.f] : -1;
+    out_bin[j] = found ? b.b : -1;
+    out_gain[j] = found ? (float)b.gain : -INFINITY;
+    out_dl[j] = (uint8_t)(found ? b.dl : 0);
+    s_best[0] = b;
+  }
+  __syncthreads();
+  // left stats of the winner (recomputed in double from the histogram)
+  const Best b = s_best[0];
+  if (threadIdx.x < S) {
+    const int s = threadIdx.x;
+    double acc = 0;
+    if (b.f != 0x7fffffff) {
+      const float* hf = h + (int64_t)b.f * B * S;
+      for (int k = 0; k <= b.b; ++k) acc += hf[k * S + s];
+      if (b.dl) acc += hf[missing_bin * S + s];
+    }
+    out_left[(int64_t)j * S + s] = (float)acc;
+  }
+}
+
+// ----------------------------------------------------------------------------------- partition
+struct PartItem {
+  int32_t node;
+  int32_t pad;
+  int64_t begin;      // absolute position of the chunk in rows_in
+  int64_t count;
+  int64_t out_left;   // absolute output position for this chunk's first left row
+  int64_t out_right;  // absolute output position for this chunk's first right row
+};
+
+__device__ __forceinline__ bool goes_left(uint8_t bin, int sb, bool dl, int missing_bin) {
+  return (missing_bin >= 0 && bin == missing_bin) ? dl : ((int)bin <= sb);
+}
+
+__global__ void __launch_bounds__(256) partition_count_kernel(
+    const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const PartItem* __restrict__ items,
+    const int32_t* __restrict__ split_feat, const int32_t* __restrict__ split_bin, const uint8_t* __restrict__ dl,
+    int missing_bin, int64_t* __restrict__ chunk_left) {
+  const PartItem it = items[blockIdx.x];
+  const int f = split_feat[it.node], sb = split_bin[it.node];
+  const bool d = dl[it.node] != 0;
+  if (f < 0) {
+    if (threadIdx.x == 0) chunk_left[blockIdx.x] = 0;
+    return;
+  }
+  int c = 0;
+  for (int64_t i = threadIdx.x; i < it.count; i += blockDim.x) {
+    const uint32_t e = rows[it.begin + i];
+    c += goes_left(Xb[(int64_t)(e & 0xFFFFFFu) * F + f], sb, d, missing_bin);
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  __shared__ int s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) chunk_left[blockIdx.x] = (int64_t)s[0] + s[1] + s[2] + s[3];
+}
+
+// stable scatter: block-wide exclusive scan of the left flags, 256 rows per step
+__global__ void __launch_bounds__(256) partition_scatter_kernel(
+    const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows_in, uint32_t* __restrict__ rows_out,
+    const PartItem* __restrict__ items, const int32_t* __restrict__ split_feat, const int32_t* __restrict__ split_bin,
+    const uint8_t* __restrict__ dl, int missing_bin) {
+  const PartItem it = items[blockIdx.x];
+  const int f = split_feat[it.node], sb = split_bin[it.node];
+  const bool d = dl[it.node] != 0;
+  if (f < 0) return;
+  __shared__ int s_wave[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t nl = 0, nr = 0;
+  for (int64_t base = 0; base < it.count; base += blockDim.x) {
+    const int64_t i = base + threadIdx.x;
+    const bool valid = i < it.count;
+    uint32_t e = 0;
+    bool left = false;
+    if (valid) {
+      e = rows_in[it.begin + i];
+      left = goes_left(Xb[(int64_t)(e & 0xFFFFFFu) * F + f], sb, d, missing_bin);
+    }
+    const unsigned long long m = __ballot(valid && left);
+    const int wpre = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wave[wave] = __popcll(m);
+    __syncthreads();
+    int before = 0, tot = 0;
+    for (int w = 0; w < 4; ++w) {
+      if (w < wave) before += s_wave[w];
+      tot += s_wave[w];
+    }
+    const int64_t nvalid = min((int64_t)blockDim.x, it.count - base);
+    if (valid) {
+      const int lpos = before + wpre;
+      if (left) rows_out[it.out_left + nl + lpos] = e;
+      else rows_out[it.out_right + nr + ((int)threadIdx.x - lpos)] = e;
+    }
+    nl += tot;
+    nr += nvalid - tot;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------- predict
+// grid.y = model; each thread walks every tree of its model for one of the model's rows.
+__global__ void __launch_bounds__(256) forest_predict_kernel(
+    const uint8_t* __restrict__ Xb, int F, const int64_t* __restrict__ model_row_off,
+    const int32_t* __restrict__ row_list, const int64_t* __restrict__ model_tree_off,
+    const int64_t* __restrict__ tree_off, const float* __restrict__ tree_weight, const int4* __restrict__ nodes,
+    const uint8_t* __restrict__ default_left, int missing_bin, const float* __restrict__ leaf_value, int K,
+    float* __restrict__ out) {
+  const int m = blockIdx.y;
+  const int64_t r0 = model_row_off[m], r1 = model_row_off[m + 1];
+  const int64_t i = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= r1) return;
+  const int64_t row = row_list ? row_list[i] : (i - r0);
+  const uint8_t* xr = Xb + row * F;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t t = model_tree_off[m]; t < model_tree_off[m + 1]; ++t) {
+    int64_t k = tree_off[t];
+    int4 nd = nodes[k];  // (feat, bin, left, right)
+    while (nd.z >= 0) {
+      const uint8_t b = xr[nd.x];
+      const bool gl = (missing_bin >= 0 && b == missing_bin) ? (default_left[k] != 0) : ((int)b <= nd.y);
+      k = gl ? nd.z : nd.w;
+      nd = nodes[k];
+    }
+    const float w = tree_weight[t];
+    for (int c = 0; c < K && c < 8; ++c) acc[c] += w * leaf_value[k * K + c];
+  }
+  float* o = out + i * K;
+  for (int c = 0; c < K && c < 8; ++c) o[c] = acc[c];
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------- C ABI
+extern "C" {
+
+int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
+                        const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
+                        const int64_t* node_hist_off, float* hist, int B, int mode, int S, const float* y,
+                        const float* t1, const float* t2, int64_t stride, hipStream_t stream) {
+  if (n_items == 0) return 0;
+  const size_t lds = (size_t)64 * (B * S + 1) * sizeof(float);
+  if (lds > 160 * 1024) return -2;
+  const HistItem* it = (const HistItem*)items;
+  dim3 grid(n_items), block(256);
+  if (mode == 0)
+    hipLaunchKernelGGL(hist_build_kernel<0>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride);
+  else if (mode == 1)
+    hipLaunchKernelGGL(hist_build_kernel<1>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride);
+  else
+    hipLaunchKernelGGL(hist_build_kernel<2>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride);
+  return (int)hipGetLastError();
+}
+
+int tmog_hip_hist_subtract(float* hist, const float* parent, const int64_t* parent_off, const int64_t* small_off,
+                           const int64_t* out_off, const int64_t* size, int n, int64_t max_size, hipStream_t stream) {
+  if (n == 0) return 0;
+  int gx = (int)((max_size + 255) / 256);
+  if (gx > 1024) gx = 1024;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(hist_subtract_kernel, dim3(gx, n), dim3(256), 0, stream, hist, parent, parent_off, small_off,
+                     out_off, size, n);
+  return (int)hipGetLastError();
+}
+
+int tmog_hip_split_find(const float* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
+                        const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
+                        int S, int kind, const float* node_params, int missing_bin, int32_t* out_feat,
+                        int32_t* out_bin, float* out_gain, uint8_t* out_dl, float* out_left, float* out_total,
+                        hipStream_t stream) {
+  if (n_nodes == 0) return 0;
+  if (S > TM_MAX_S || B > 64) return -2;
+  hipLaunchKernelGGL(split_find_kernel, dim3(n_nodes), dim3(256), 0, stream, hist, node_hist_off, node_nfeat,
+                     node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin, out_feat, out_bin,
+                     out_gain, out_dl, out_left, out_total);
+  return (int)hipGetLastError();
+}
+
+int tmog_hip_partition_count(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
+                             const int32_t* split_feat, const int32_t* split_bin, const uint8_t* dl, int missing_bin,
+                             int64_t* chunk_left, hipStream_t stream) {
+  if (n_items == 0) return 0;
+  hipLaunchKernelGGL(partition_count_kernel, dim3(n_items), dim3(256), 0, stream, Xb, F, rows,
+                     (const PartItem*)items, split_feat, split_bin, dl, missing_bin, chunk_left);
+  return (int)hipGetLastError();
+}
+
+int tmog_hip_partition_scatter(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out,
+                               const void* items, int n_items, const int32_t* split_feat, const int32_t* split_bin,
+                               const uint8_t* dl, int missing_bin, hipStream_t stream) {
+  if (n_items == 0) return 0;
+  hipLaunchKernelGGL(partition_scatter_kernel, dim3(n_items), dim3(256), 0, stream, Xb, F, rows_in, rows_out,
+                     (const PartItem*)items, split_feat, split_bin, dl, missing_bin);
+  return (int)hipGetLastError();
+}
+
+int tmog_hip_forest_predict(const uint8_t* Xb, int F, int n_models, const int64_t* model_row_off,
+                            const int32_t* row_list, int64_t max_rows, const int64_t* model_tree_off,
+                            const int64_t* tree_off, const float* tree_weight, const int32_t* nodes,
+                            const uint8_t* default_left, int missing_bin, const float* leaf_value, int K, float* out,
+                            hipStream_t stream) {
+  if (n_models == 0 || max_rows == 0) return 0;
+  if (K > 8) return -2;
+  dim3 grid((unsigned)((max_rows + 255) / 256), n_models);
+  hipLaunchKernelGGL(forest_predict_kernel, grid, dim3(256), 0, stream, Xb, F, model_row_off, row_list,
+                     model_tree_off, tree_off, tree_weight, (const int4*)nodes, default_left, missing_bin, leaf_value,
+                     K, out);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+// Fused vectorizer kernels: the layer transform of RealVectorizer /
+// IntegralVectorizer / BinaryVectorizer (RealVectorizer.scala:108-119) written straight into the
+// row-major feature matrix -- fill + null indicator + column->row transpose in one HBM pass.
+//
+// Each workgroup owns a 64-row x 32-column tile: phase 1 reads every input column with 64
+// consecutive rows per wave (256 B coalesced), phase 2 writes whole 64/32-float output row
+// segments through LDS (padded by one word to avoid bank conflicts on the transpose).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int TR = 64;   // rows per tile
+constexpr int TC = 32;   // input columns per tile
+
+__global__ void __launch_bounds__(256) vectorize_numeric_kernel(const float* const* __restrict__ vals,
+                                                                const uint8_t* const* __restrict__ valid,
+                                                                const float* __restrict__ fills, int64_t n, int F,
+                                                                float* __restrict__ out, int64_t W, int track) {
+  __shared__ float tile[TR][2 * TC + 1];
+  const int64_t row0 = (int64_t)blockIdx.x * TR;
+  const int c0 = blockIdx.y * TC;
+  const int per = track ? 2 : 1;
+  for (int k = threadIdx.x; k < TR * TC; k += blockDim.x) {
+    const int r = k % TR, cj = k / TR, c = c0 + cj;
+    const int64_t row = row0 + r;
+    if (c < F && row < n) {
+      const bool ok = valid[c][row] != 0;
+      const float v = ok ? vals[c][row] : fills[c];
+      tile[r][per * cj] = v;
+      if (track) tile[r][per * cj + 1] = ok ? 0.f : 1.f;
+    }
+  }
+  __syncthreads();
+  const int ncols = min(TC, F - c0) * per;
+  for (int k = threadIdx.x; k < TR * TC * per; k += blockDim.x) {
+    const int r = k / (TC * per), oc = k % (TC * per);
+    const int64_t row = row0 + r;
+    if (oc < ncols && row < n) out[row * W + (int64_t)c0 * per + oc] = tile[r][oc];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int tmog_hip_vectorize_numeric(const void* vals, const void* valid, const float* fills, int64_t n, int F,
+                               const void* r1, const void* r2, const void* r3, float* out, int64_t W, int track,
+                               hipStream_t stream) {
+  (void)r1; (void)r2; (void)r3;
+  if (n == 0 || F == 0) return 0;
+  dim3 grid((unsigned)((n + TR - 1) / TR), (unsigned)((F + TC - 1) / TC));
+  hipLaunchKernelGGL(vectorize_numeric_kernel, grid, dim3(256), 0, stream, (const float* const*)vals,
+                     (const uint8_t* const*)valid, fills, n, F, out, W, track);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

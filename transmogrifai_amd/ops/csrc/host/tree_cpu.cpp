@@ -1,0 +1,279 @@
+// CPU reference implementation of the histogram tree engine kernels.
+//
+// These are the host twins of the HIP kernels in ../hip/tree_kernels.hip and share their
+// data layout exactly (see transmogrifai_amd/models/tree_engine.py for the orchestration):
+//
+//   Xb        uint8 [N][F] row-major binned feature matrix
+//   rows      uint32 packed row entries: (row & 0xFFFFFF) | (weight << 24)
+//   nodes     j = 0..n_nodes-1 : [node_begin[j], node_begin[j]+node_count[j]) slice of `rows`
+//   features  node j histograms features feat_list[node_feat_off[j] + 0 .. node_nfeat[j]-1]
+//   hist      float [node_hist_off[j] + (fl * B + bin) * S + s]
+//
+// Stat modes (S = stats per bin):
+//   0 CLS : S = n_classes, contribution w at class y[row]                  (gini / entropy trees)
+//   1 VAR : S = 3, (w, w*t, w*t*t), t = t1[model*stride + row]              (variance trees, GBT)
+//   2 GH  : S = 2, (w*g, w*h), g = t1[model*stride + row], h = t2[...]      (Newton / XGBoost-style)
+//
+// Reference hot loops being replaced: Spark MLlib DecisionTree/RandomForest/GBT per-level
+// DTStatsAggregator (K23-K25 in SURVEY.md) and XGBoost4J hist building.
+#include <cstdint>
+#include <cstring>
+#include <cmath>
+#include <vector>
+#include <algorithm>
+#include <omp.h>
+
+extern "C" {
+
+static inline float stat_target(const float* t, int64_t model, int64_t stride, int64_t row) {
+  return t[model * stride + row];
+}
+
+int tmog_hist_build_cpu(const uint8_t* Xb, int64_t N, int F, const uint32_t* rows, int n_nodes,
+                        const int64_t* node_begin, const int64_t* node_count, const int32_t* node_feat_off,
+                        const int32_t* node_nfeat, const int32_t* feat_list, const int32_t* node_model,
+                        const int64_t* node_hist_off, float* hist, int B, int mode, int S, const float* y,
+                        const float* t1, const float* t2, int64_t model_stride) {
+  (void)N;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int j = 0; j < n_nodes; ++j) {
+    const int nf = node_nfeat[j];
+    const int32_t* fl = feat_list + node_feat_off[j];
+    float* h = hist + node_hist_off[j];
+    std::memset(h, 0, sizeof(float) * (size_t)nf * B * S);
+    const int64_t b0 = node_begin[j], cnt = node_count[j];
+    const int64_t model = node_model ? node_model[j] : 0;
+    for (int64_t i = 0; i < cnt; ++i) {
+      const uint32_t e = rows[b0 + i];
+      const int64_t r = e & 0xFFFFFFu;
+      const float w = (float)(e >> 24);
+      float st[16];
+      if (mode == 0) {
+        for (int s = 0; s < S; ++s) st[s] = 0.f;
+        st[(int)y[r]] = w;
+      } else if (mode == 1) {
+        const float t = stat_target(t1, model, model_stride, r);
+        st[0] = w; st[1] = w * t; st[2] = w * t * t;
+      } else {
+        st[0] = w * stat_target(t1, model, model_stride, r);
+        st[1] = w * stat_target(t2, model, model_stride, r);
+      }
+      const uint8_t* xr = Xb + r * (int64_t)F;
+      for (int f = 0; f < nf; ++f) {
+        const int bin = xr[fl[f]];
+        float* hb = h + ((int64_t)f * B + bin) * S;
+        for (int s = 0; s < S; ++s) hb[s] += st[s];
+      }
+    }
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------- split finding
+// Impurity kinds: 0 gini, 1 entropy, 2 variance, 3 newton (xgboost gain).
+static inline double impurity(const double* st, int S, int kind, double* count_out) {
+  if (kind == 0 || kind == 1) {
+    double n = 0;
+    for (int s = 0; s < S; ++s) n += st[s];
+    *count_out = n;
+    if (n <= 0) return 0.0;
+    double imp = kind == 0 ? 1.0 : 0.0;
+    for (int s = 0; s < S; ++s) {
+      const double p = st[s] / n;
+      if (kind == 0) imp -= p * p;
+      else if (p > 0) imp -= p * std::log2(p);
+    }
+    return imp;
+  }
+  if (kind == 2) {
+    const double n = st[0];
+    *count_out = n;
+    if (n <= 0) return 0.0;
+    const double m = st[1] / n;
+    return st[2] / n - m * m;
+  }
+  *count_out = st[1];
+  return 0.0;
+}
+
+// params per node (float): [0] min_instances, [1] min_info_gain, [2] min_child_weight, [3] lambda,
+// [4] alpha (unused), [5] allow_missing (xgb default-direction search)
+int tmog_split_find_cpu(const float* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
+                        const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
+                        int S, int kind, const float* node_params, int missing_bin, int32_t* out_feat,
+                        int32_t* out_bin, float* out_gain, uint8_t* out_default_left, float* out_left,
+                        float* out_total) {
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int j = 0; j < n_nodes; ++j) {
+    const float* h = hist + node_hist_off[j];
+    const int nf = node_nfeat[j];
+    const int32_t* fl = feat_list + node_feat_off[j];
+    const float* P = node_params + (int64_t)j * 8;
+    const double min_inst = P[0], min_gain = P[1], mcw = P[2], lambda = P[3];
+    const bool allow_missing = P[5] > 0.5f && missing_bin >= 0;
+    double tot[16] = {0};
+    // totals from feature 0 (every row is counted once per feature, including the missing bin)
+    for (int b = 0; b < B; ++b)
+      for (int s = 0; s < S; ++s) tot[s] += h[(int64_t)b * S + s];
+    for (int s = 0; s < S; ++s) out_total[(int64_t)j * S + s] = (float)tot[s];
+    double tcount;
+    const double pimp = impurity(tot, S, kind, &tcount);
+    const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
+    double best = -INFINITY;
+    int bf = -1, bb = -1, bdl = 0;
+    double bleft[16] = {0};
+    for (int f = 0; f < nf; ++f) {
+      const int gf = fl[f];
+      const int nb = feat_nbins[gf];
+      const float* hf = h + (int64_t)f * B * S;
+      double miss[16] = {0};
+      if (allow_missing)
+        for (int s = 0; s < S; ++s) miss[s] = hf[(int64_t)missing_bin * S + s];
+      for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
+        double left[16];
+        for (int s = 0; s < S; ++s) left[s] = dl ? miss[s] : 0.0;
+        for (int b = 0; b + 1 < nb; ++b) {
+          for (int s = 0; s < S; ++s) left[s] += hf[(int64_t)b * S + s];
+          double right[16];
+          for (int s = 0; s < S; ++s) right[s] = tot[s] - left[s];
+          double gain;
+          if (kind == 3) {
+            if (left[1] < mcw || right[1] < mcw) continue;
+            gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
+          } else {
+            double lc, rc;
+            const double li = impurity(left, S, kind, &lc);
+            const double ri = impurity(right, S, kind, &rc);
+            if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) continue;
+            gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
+            if (gain < min_gain) continue;
+          }
+          if (gain > best) {
+            best = gain; bf = gf; bb = b; bdl = dl;
+            for (int s = 0; s < S; ++s) bleft[s] = left[s];
+          }
+        }
+      }
+    }
+    out_feat[j] = bf;
+    out_bin[j] = bb;
+    out_gain[j] = bf >= 0 ? (float)best : -INFINITY;
+    out_default_left[j] = (uint8_t)bdl;
+    for (int s = 0; s < S; ++s) out_left[(int64_t)j * S + s] = (float)bleft[s];
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------- partition
+// Stable partition of every splitting node's rows into [left | right] written at out_begin[j].
+// out_left_count[j] receives the number of left rows. Nodes with split_feat < 0 are skipped.
+int tmog_partition_cpu(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, int n_nodes,
+                       const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
+                       const int32_t* split_bin, const uint8_t* default_left, int missing_bin,
+                       const int64_t* out_begin, int64_t* out_left_count) {
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int j = 0; j < n_nodes; ++j) {
+    if (split_feat[j] < 0) { out_left_count[j] = 0; continue; }
+    const int f = split_feat[j], sb = split_bin[j];
+    const bool dl = default_left[j] != 0;
+    const uint32_t* in = rows_in + node_begin[j];
+    const int64_t cnt = node_count[j];
+    int64_t nl = 0;
+    for (int64_t i = 0; i < cnt; ++i) {
+      const int bin = Xb[(int64_t)(in[i] & 0xFFFFFFu) * F + f];
+      const bool left = (missing_bin >= 0 && bin == missing_bin) ? dl : (bin <= sb);
+      nl += left;
+    }
+    uint32_t* out = rows_out + out_begin[j];
+    int64_t li = 0, ri = nl;
+    for (int64_t i = 0; i < cnt; ++i) {
+      const int bin = Xb[(int64_t)(in[i] & 0xFFFFFFu) * F + f];
+      const bool left = (missing_bin >= 0 && bin == missing_bin) ? dl : (bin <= sb);
+      if (left) out[li++] = in[i]; else out[ri++] = in[i];
+    }
+    out_left_count[j] = nl;
+  }
+  return 0;
+}
+
+// -------------------------------------------------------------------------------------- predict
+// Flat forest: model m owns trees [model_tree_off[m], model_tree_off[m+1]) and rows
+// row_list[model_row_off[m] .. model_row_off[m+1]) (row_list == nullptr => rows 0..n_m-1).
+// Tree t starts at node tree_off[t]; nodes are int4 (feat, bin, left, right) with global child
+// indices, left < 0 marks a leaf. out[i][K] = sum_t w_t * leaf_value[leaf(t, row_i)].
+int tmog_forest_predict_cpu(const uint8_t* Xb, int F, int n_models, const int64_t* model_row_off,
+                            const int32_t* row_list, const int64_t* model_tree_off, const int64_t* tree_off,
+                            const float* tree_weight, const int32_t* nodes, const uint8_t* default_left,
+                            int missing_bin, const float* leaf_value, int K, float* out) {
+  for (int m = 0; m < n_models; ++m) {
+    const int64_t r0 = model_row_off[m], r1 = model_row_off[m + 1];
+#pragma omp parallel for schedule(static)
+    for (int64_t i = r0; i < r1; ++i) {
+      const int64_t row = row_list ? row_list[i] : (i - r0);
+      const uint8_t* xr = Xb + row * (int64_t)F;
+      float* o = out + i * K;
+      for (int c = 0; c < K; ++c) o[c] = 0.f;
+      for (int64_t t = model_tree_off[m]; t < model_tree_off[m + 1]; ++t) {
+        int64_t k = tree_off[t];
+        while (nodes[4 * k + 2] >= 0) {
+          const int b = xr[nodes[4 * k]];
+          const bool gl = (missing_bin >= 0 && b == missing_bin) ? (default_left[k] != 0) : (b <= nodes[4 * k + 1]);
+          k = gl ? nodes[4 * k + 2] : nodes[4 * k + 3];
+        }
+        const float w = tree_weight[t];
+        for (int c = 0; c < K; ++c) o[c] += w * leaf_value[k * K + c];
+      }
+    }
+  }
+  return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------- split finding
+// Spark MLlib RandomForest.findSplitsForContinuousFeature (2.4) on a row sample, per feature:
+// distinct values + counts, then midpoints chosen by the greedy stride rule. sample is [S][F]
+// row-major; out is [F][max_splits] padded with +inf; n_out[f] = number of thresholds.
+extern "C" int tmog_find_splits_cpu(const double* sample, int64_t S, int F, int max_splits, double* out,
+                                    int32_t* n_out) {
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int f = 0; f < F; ++f) {
+    std::vector<double> v;
+    v.reserve(S);
+    for (int64_t i = 0; i < S; ++i) {
+      const double x = sample[i * F + f];
+      if (!std::isnan(x)) v.push_back(x);
+    }
+    double* o = out + (int64_t)f * max_splits;
+    for (int k = 0; k < max_splits; ++k) o[k] = INFINITY;
+    n_out[f] = 0;
+    if (v.empty()) continue;
+    std::sort(v.begin(), v.end());
+    std::vector<double> vals;
+    std::vector<int64_t> cnts;
+    for (size_t i = 0; i < v.size(); ++i) {
+      if (vals.empty() || v[i] != vals.back()) { vals.push_back(v[i]); cnts.push_back(1); }
+      else cnts.back()++;
+    }
+    const int64_t possible = (int64_t)vals.size() - 1;
+    const int64_t num_samples = (int64_t)v.size();
+    int n = 0;
+    if (possible <= 0) {
+      n = 0;
+    } else if (possible <= max_splits) {
+      for (int64_t i = 1; i <= possible; ++i) o[n++] = (vals[i - 1] + vals[i]) / 2.0;
+    } else {
+      const double stride = (double)num_samples / (max_splits + 1);
+      int64_t cur = cnts[0];
+      double target = stride;
+      for (size_t i = 1; i < vals.size() && n < max_splits; ++i) {
+        const int64_t prev = cur;
+        cur += cnts[i];
+        const double pg = std::fabs((double)prev - target), cg = std::fabs((double)cur - target);
+        if (pg < cg) { o[n++] = (vals[i - 1] + vals[i]) / 2.0; target += stride; }
+      }
+    }
+    n_out[f] = n;
+  }
+  return 0;
+}

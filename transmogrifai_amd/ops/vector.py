@@ -1,0 +1,107 @@
+"""Vectorizer column kernels (fill / null-indicator blocks, one-hot scatter, hashed TF scatter).
+
+Device tensors go to the fused HIP kernels in ``csrc/hip/vector_kernels.hip`` when they are
+available for the shape; host tensors use the torch reference path, which is also the numerics
+spec the HIP kernels are tested against.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import numpy as np
+import torch
+
+from ..data.columns import NumericColumn
+from . import _native as N
+
+
+def column_means(cols: Sequence[NumericColumn]) -> List[float]:
+    """Mean of non-null values per column; 0 when a column is all null (``MeanSeqNullNum``)."""
+    out = []
+    for c in cols:
+        v = c.values.to(torch.float64)
+        ok = c.valid
+        s = torch.where(ok, v, torch.zeros_like(v)).sum()
+        n = ok.sum()
+        out.append(float(s / n) if int(n) > 0 else float(s))
+    return out
+
+
+def column_modes(cols: Sequence[NumericColumn]) -> List[float]:
+    """Mode of non-null values per column, ties -> smallest value, 0 if empty (``ModeSeqNullInt``)."""
+    out = []
+    for c in cols:
+        v = c.values[c.valid]
+        if v.numel() == 0:
+            out.append(0.0)
+            continue
+        u, cnt = torch.unique(v, return_counts=True)
+        out.append(float(u[int(torch.argmax(cnt))]))
+    return out
+
+
+def fill_and_track(cols: Sequence[NumericColumn], fills: Sequence[float], track_nulls: bool,
+                   dtype: torch.dtype) -> torch.Tensor:
+    """``[N, F]`` (or ``[N, 2F]`` interleaved with null flags) filled value block."""
+    if not cols:
+        return torch.zeros(0, 0, dtype=dtype)
+    dev = cols[0].values.device
+    n = len(cols[0])
+    F = len(cols)
+    W = F * (2 if track_nulls else 1)
+    if dev.type == "cuda" and dtype == torch.float32 and n > 0:
+        out = torch.empty(n, W, dtype=dtype, device=dev)
+        vals = [c.values.to(torch.float32).contiguous() for c in cols]
+        oks = [c.valid.contiguous() for c in cols]
+        vp = torch.tensor([t.data_ptr() for t in vals], dtype=torch.int64, device=dev)
+        op = torch.tensor([t.data_ptr() for t in oks], dtype=torch.int64, device=dev)
+        fl = torch.tensor(list(fills), dtype=torch.float32, device=dev)
+        N.check(N.hip().tmog_hip_vectorize_numeric(
+            N.ptr(vp), N.ptr(op), N.ptr(fl), n, F, None, None, None, N.ptr(out), W, int(track_nulls),
+            N.stream(dev)), "vectorize_numeric")
+        del vals, oks
+        return out
+    vals = torch.stack([c.values.to(dtype) for c in cols], 1)
+    ok = torch.stack([c.valid for c in cols], 1)
+    fill = torch.tensor(list(fills), dtype=dtype, device=dev)[None, :]
+    filled = torch.where(ok, vals, fill)
+    if not track_nulls:
+        return filled.contiguous()
+    return torch.stack([filled, (~ok).to(dtype)], 2).reshape(n, W)
+
+
+def onehot_scatter(out: torch.Tensor, codes: torch.Tensor, lut: torch.Tensor, off: int) -> None:
+    """``out[r, off + lut[codes[r]]] += 1`` (code -1 uses the last lut entry; slot -1 = skip)."""
+    n = codes.shape[0]
+    if n == 0:
+        return
+    idx = torch.where(codes >= 0, codes.long(), torch.full_like(codes.long(), lut.numel() - 1))
+    slot = lut[idx]
+    rows = torch.arange(n, device=codes.device)
+    m = slot >= 0
+    out.index_put_((rows[m], slot[m] + off), torch.ones(int(m.sum()), dtype=out.dtype, device=out.device),
+                   accumulate=True)
+
+
+def csr_rows_scatter_add(out: torch.Tensor, codes: torch.Tensor, indptr: np.ndarray, idx: np.ndarray,
+                         vals: np.ndarray) -> None:
+    """For each row r with code c >= 0 add the sparse vector ``c`` (CSR) into ``out[r]``."""
+    dev = out.device
+    if idx.size == 0:
+        return
+    ip = torch.as_tensor(indptr, device=dev)
+    ix = torch.as_tensor(idx, device=dev)
+    vx = torch.as_tensor(vals, dtype=out.dtype, device=dev)
+    c = codes.long()
+    ok = c >= 0
+    rows = torch.arange(codes.shape[0], device=dev)[ok]
+    c = c[ok]
+    starts = ip[c]
+    cnt = ip[c + 1] - starts
+    total = int(cnt.sum())
+    if total == 0:
+        return
+    r_rep = torch.repeat_interleave(rows, cnt)
+    base = torch.repeat_interleave(starts - (torch.cumsum(cnt, 0) - cnt), cnt)
+    g = base + torch.arange(total, device=dev)
+    out.index_put_((r_rep, ix[g]), vx[g], accumulate=True)

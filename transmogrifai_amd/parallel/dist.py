@@ -1,0 +1,129 @@
+"""Process-group helpers: one rank per GPU, ``torch.distributed`` over RCCL (``nccl`` backend on ROCm)
+or ``gloo`` on the host.
+
+Replaces the reference's Spark ``treeAggregate``/``reduce``/``fold``/``collect`` reductions and XGBoost's
+Rabit allreduce. Statistics of one fit stage are packed into a single
+flat buffer and reduced in one collective (``bucketed_all_reduce``): the payloads are small and
+latency-bound on xGMI, so one call per stage beats one call per statistic.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+def is_dist() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def rank() -> int:
+    return dist.get_rank() if is_dist() else 0
+
+
+def world() -> int:
+    return dist.get_world_size() if is_dist() else 1
+
+
+def barrier():
+    if is_dist():
+        dist.barrier()
+
+
+def init_from_env(backend: str = None, device_id: int = None):
+    """Initialize from torchrun env vars (RANK, WORLD_SIZE, MASTER_ADDR/PORT); no-op when single-process."""
+    if is_dist():
+        return
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1:
+        return
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kw = {}
+    if backend == "nccl" and device_id is not None:
+        kw["device_id"] = torch.device("cuda", device_id)
+    dist.init_process_group(backend=backend, **kw)
+
+
+def _comm_device(t: torch.Tensor):
+    if is_dist() and dist.get_backend() == "nccl" and t.device.type != "cuda":
+        return torch.device("cuda", torch.cuda.current_device())
+    return t.device
+
+
+def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    if not is_dist():
+        return t
+    dev = _comm_device(t)
+    x = t.to(dev)
+    o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+    dist.all_reduce(x, op=o)
+    return x.to(t.device)
+
+
+def bucketed_all_reduce(tensors: Sequence[torch.Tensor], op: str = "sum") -> List[torch.Tensor]:
+    """Flatten, reduce once, unflatten (same dtype required per bucket; mixed dtypes go via float64)."""
+    if not is_dist() or not tensors:
+        return list(tensors)
+    dt = torch.float64
+    flat = torch.cat([t.reshape(-1).to(dt) for t in tensors])
+    flat = all_reduce(flat, op)
+    out, off = [], 0
+    for t in tensors:
+        n = t.numel()
+        out.append(flat[off:off + n].reshape(t.shape).to(t.dtype))
+        off += n
+    return out
+
+
+def all_gather_object(obj) -> list:
+    if not is_dist():
+        return [obj]
+    out = [None] * world()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def broadcast_object(obj, src: int = 0):
+    if not is_dist():
+        return obj
+    box = [obj]
+    dist.broadcast_object_list(box, src=src)
+    return box[0]
+
+
+def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
+    """Concatenate a row-sharded tensor from every rank (variable row counts)."""
+    if not is_dist():
+        return t
+    dev = _comm_device(t)
+    x = t.to(dev).contiguous()
+    n = torch.tensor([x.shape[0]], device=dev, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(world())]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    mx = max(sizes)
+    pad = torch.zeros((mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=dev)
+    pad[:x.shape[0]] = x
+    if x.dtype == torch.bool:
+        pad = pad.to(torch.uint8)
+    bufs = [torch.empty_like(pad) for _ in range(world())]
+    dist.all_gather(bufs, pad)
+    out = torch.cat([b[:s] for b, s in zip(bufs, sizes)])
+    if x.dtype == torch.bool:
+        out = out.to(torch.bool)
+    return out.to(t.device)
+
+
+def lpt_assign(costs: Sequence[float], n_workers: int) -> List[int]:
+    """Longest-processing-time-first assignment of tasks to workers; returns worker per task."""
+    order = sorted(range(len(costs)), key=lambda i: -costs[i])
+    load = [0.0] * n_workers
+    owner = [0] * len(costs)
+    for i in order:
+        w = min(range(n_workers), key=lambda k: load[k])
+        owner[i] = w
+        load[w] += costs[i]
+    return owner

@@ -1,0 +1,128 @@
+"""File readers: CSV (explicit schema or headers), CSV with schema inference, Parquet, Avro.
+
+Reference: ``CSVReaders.scala:54-122``, ``CSVAutoReaders.scala:57-142``, ``ParquetProductReader.scala:47-90``,
+``AvroReaders.scala:55-134`` and the ``DataReaders`` factory (``DataReaders.scala:44-278``). Parsing goes
+through pandas/pyarrow's native CSV/Parquet engines into a DataFrame, then column-wise into the
+columnar dataset (see :mod:`.base`). Avro container files are decoded by :mod:`.avro`.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Tuple
+
+from .base import DataReader
+
+
+class CSVReader(DataReader):
+    """CSV with column names from ``schema`` (``[(name, kind)]`` or names) or the file header."""
+
+    def __init__(self, path: Optional[str] = None, schema: Optional[Sequence] = None, has_header: bool = False,
+                 key: Optional[Callable] = None, device=None, separator: str = ","):
+        super().__init__(key, device)
+        self.path = path
+        self.schema = schema
+        self.has_header = has_header
+        self.separator = separator
+
+    def _names(self):
+        if self.schema is None:
+            return None
+        return [s[0] if isinstance(s, (tuple, list)) else s for s in self.schema]
+
+    def read_frame(self, params=None):
+        import pandas as pd
+        path = self.path
+        if params is not None and getattr(params, "path", None):
+            path = params.path
+        if path is None:
+            raise ValueError("CSV reader requires a path")
+        names = self._names()
+        dtype = None
+        if self.schema is not None and all(isinstance(s, (tuple, list)) for s in self.schema):
+            m = {"string": str, "text": str}
+            dtype = {n: m[k] for n, k in self.schema if k in m}
+        df = pd.read_csv(path, header=0 if self.has_header else None, names=names, sep=self.separator,
+                         dtype=dtype, keep_default_na=True, skipinitialspace=False)
+        return df
+
+
+class CSVAutoReader(CSVReader):
+    """CSV with a header row and schema inference (``CSVAutoReaders``)."""
+
+    def __init__(self, path=None, key=None, device=None, separator=","):
+        super().__init__(path, None, True, key, device, separator)
+
+
+class ParquetReader(DataReader):
+    def __init__(self, path: Optional[str] = None, key=None, device=None):
+        super().__init__(key, device)
+        self.path = path
+
+    def read_frame(self, params=None):
+        import pandas as pd
+        path = params.path if (params is not None and getattr(params, "path", None)) else self.path
+        return pd.read_parquet(path)
+
+
+class AvroReader(DataReader):
+    def __init__(self, path: Optional[str] = None, key=None, device=None):
+        super().__init__(key, device)
+        self.path = path
+
+    def read_records(self, params=None):
+        from .avro import read_avro
+        path = params.path if (params is not None and getattr(params, "path", None)) else self.path
+        return read_avro(path)
+
+
+class DataReaders:
+    """``DataReaders.Simple`` / ``.Aggregate`` / ``.Conditional`` factories."""
+
+    class Simple:
+        @staticmethod
+        def csv(path=None, schema=None, key=None, has_header=False, device=None):
+            return CSVReader(path, schema, has_header, key, device)
+
+        @staticmethod
+        def csv_case(path=None, schema=None, key=None, device=None):
+            return CSVReader(path, schema, False, key, device)
+
+        @staticmethod
+        def csv_auto(path=None, key=None, device=None):
+            return CSVAutoReader(path, key, device)
+
+        @staticmethod
+        def parquet(path=None, key=None, device=None):
+            return ParquetReader(path, key, device)
+
+        @staticmethod
+        def avro(path=None, key=None, device=None):
+            return AvroReader(path, key, device)
+
+        @staticmethod
+        def custom(data, key=None, device=None):
+            from .base import InMemoryReader
+            return InMemoryReader(data, key, device)
+
+    class Aggregate:
+        @staticmethod
+        def csv(path=None, schema=None, key=None, aggregate_params=None, has_header=False, device=None):
+            from .aggregate import AggregateReader
+            return AggregateReader(CSVReader(path, schema, has_header, None, device), key, aggregate_params)
+
+        @staticmethod
+        def custom(data, key=None, aggregate_params=None, device=None):
+            from .aggregate import AggregateReader
+            from .base import InMemoryReader
+            return AggregateReader(InMemoryReader(data, None, device), key, aggregate_params)
+
+    class Conditional:
+        @staticmethod
+        def csv(path=None, schema=None, key=None, conditional_params=None, has_header=False, device=None):
+            from .aggregate import ConditionalReader
+            return ConditionalReader(CSVReader(path, schema, has_header, None, device), key, conditional_params)
+
+        @staticmethod
+        def custom(data, key=None, conditional_params=None, device=None):
+            from .aggregate import ConditionalReader
+            from .base import InMemoryReader
+            return ConditionalReader(InMemoryReader(data, None, device), key, conditional_params)

@@ -1,0 +1,127 @@
+"""Model selector stage and its fitted ``SelectedModel``.
+
+Reference: ``ModelSelector`` (``core/.../stages/impl/selector/ModelSelector.scala:72-264``: validate grid,
+refit the winner on the prepared full training set, train evaluation, ``ModelSelectorSummary``
+metadata, ``SelectedModel``), ``ModelSelectorSummary`` (``ModelSelectorSummary.scala:55-309``) and the
+hold-out evaluation of ``HasTestEval`` (``ModelSelectorNames.scala:73-123``).
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..data.columns import PredictionColumn
+from ..features import types as T
+from ..models.base import FitJob, OpPredictorModel, learner_class
+from ..stages.base import BinaryEstimator, register_stage
+from ..tuning.splitters import Splitter
+from ..tuning.validators import OpValidator
+
+log = logging.getLogger(__name__)
+
+SUMMARY_KEY = "summary"
+
+
+def problem_type_of(metrics: Dict) -> str:
+    if "AuROC" in metrics or "AuPR" in metrics:
+        return "BinaryClassification"
+    if "F1" in metrics:
+        return "MultiClassification"
+    return "Regression"
+
+
+@register_stage
+class SelectedModel(OpPredictorModel):
+    operation_name = "modelSelection"
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.evaluators = []
+
+    def evaluate_model(self, ds) -> Dict:
+        """Hold-out evaluation (``HasTestEval.evaluateModel``): fills ``holdoutEvaluation``."""
+        lab = ds[self._inputs[0].name].values.to(torch.float64)
+        vec = ds[self._inputs[1].name].values
+        pred, raw, prob = self.learner.predict(self.state, vec)
+        res = {}
+        for ev in self.evaluators:
+            res.update(ev.evaluate_arrays(lab, pred, raw, prob))
+        if SUMMARY_KEY in self.metadata:
+            self.metadata[SUMMARY_KEY]["holdoutEvaluation"] = res
+        return res
+
+
+@register_stage
+class ModelSelector(BinaryEstimator):
+    """Estimator (label: RealNN, features: OPVector) -> Prediction choosing the best learner + params."""
+    operation_name = "modelSelection"
+    output_type = T.Prediction
+    allow_label_as_input = True
+
+    def __init__(self, validator: OpValidator = None, splitter: Optional[Splitter] = None,
+                 models: Sequence[Tuple[str, Sequence[Dict]]] = (), evaluators: Sequence = (),
+                 uid: Optional[str] = None):
+        super().__init__(uid=uid)
+        self.validator = validator
+        self.splitter = splitter
+        self.models = [(n, [dict(g) for g in grid]) for n, grid in models]
+        self.evaluators = list(evaluators)
+        self.best: Optional[Any] = None
+
+    def fit_columns(self, label_col, vec_col, ds=None):
+        X = vec_col.values
+        y = label_col.values.to(X.dtype)
+        row_ids = ds.row_ids.to(X.device) if ds is not None else torch.arange(X.shape[0], device=X.device)
+        t0 = time.time()
+        split_summary = None
+        if self.splitter is not None:
+            split_summary = self.splitter.pre_validation_prepare(y)
+        ctx: Dict[str, Any] = {}
+        res = self.validator.validate(self.models, X, y, row_ids, self.splitter, context=ctx)
+        self.best = res
+        # refit the winner on the prepared full training set
+        learner = learner_class(res.best_learner)()
+        params = dict(learner.defaults, **res.best_params)
+        if self.splitter is not None:
+            if hasattr(self.splitter, "weights"):
+                w = self.splitter.weights(row_ids, y, stream=5)
+                rows = torch.nonzero(w > 0).reshape(-1)
+                job = FitJob(params, rows, w[rows])
+            else:
+                rows = torch.nonzero(self.splitter.validation_prepare(row_ids, y, stream=5)).reshape(-1)
+                job = FitJob(params, rows)
+        else:
+            rows = None
+            job = FitJob(params)
+        state = learner.fit_batch(X, y, [job], context=ctx)[0]
+        # training evaluation on the prepared data
+        Xr = X if rows is None else X[rows]
+        yr = y if rows is None else y[rows]
+        pred, raw, prob = learner.predict(state, Xr)
+        train_eval: Dict = {}
+        for ev in self.evaluators:
+            train_eval.update(ev.evaluate_arrays(yr.to(torch.float64), pred, raw, prob))
+        summary = {
+            "validationType": self.validator.validation_type,
+            "validationParameters": self.validator.params(),
+            "dataPrepParameters": self.splitter.params() if self.splitter is not None else {},
+            "dataPrepResults": split_summary,
+            "evaluationMetric": self.validator.evaluator.metric,
+            "problemType": problem_type_of(train_eval),
+            "bestModelUID": f"{res.best_learner}_{self.uid.split('_')[-1]}",
+            "bestModelName": res.best_learner,
+            "bestModelType": res.best_learner,
+            "bestModelParameters": params,
+            "validationResults": [e.to_json() for e in res.evaluations],
+            "trainEvaluation": train_eval,
+            "holdoutEvaluation": None,
+            "failures": res.failures,
+            "timings": dict(res.timings, selector_total=time.time() - t0),
+        }
+        self.metadata[SUMMARY_KEY] = summary
+        m = SelectedModel(res.best_learner, state, params)
+        m.evaluators = list(self.evaluators)
+        return m

@@ -1,0 +1,259 @@
+"""Map vectorizers: one block of columns per (map feature, key).
+
+Reference: ``OPMapVectorizer`` family (``core/.../impl/feature/OPMapVectorizer.scala:60-468``: RealMap / IntegralMap /
+BinaryMap / DateMap / TextMapHashing; key discovery, per-key mean / mode / constant fill and null
+tracking), ``TextMapPivotVectorizer`` (``:53-145``), ``MultiPickListMapVectorizer`` (``:49-122``),
+``SmartTextMapVectorizer`` (``:57-418``), ``GeolocationMapVectorizer`` (``:42-129``) and
+``DateMapToUnitCircleVectorizer`` (``:63-134``). Maps are ragged host data (COO of row, key, value);
+every key becomes a dense device column block.
+"""
+from __future__ import annotations
+
+from collections import Counter
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ...config import vector_dtype
+from ...data.columns import ObjectColumn
+from ...data.vector_metadata import NULL_STRING, OTHER_STRING, OpVectorColumnMetadata
+from ...features import types as T
+from ...utils import text as TU
+from ..base import SequenceEstimator, SequenceTransformer, register_stage
+from .vectorizers import VectorizerMixin, top_values
+
+
+def _clean_key(k, clean):
+    return TU.clean_string(k) if clean else k
+
+
+def _kind_of(t) -> str:
+    if issubclass(t, T.BinaryMap):
+        return "binary"
+    if issubclass(t, T.DateMap):
+        return "date"
+    if issubclass(t, T.IntegralMap):
+        return "integral"
+    if issubclass(t, T.RealMap):
+        return "real"
+    if issubclass(t, T.MultiPickListMap):
+        return "set"
+    if issubclass(t, T.GeolocationMap):
+        return "geo"
+    if issubclass(t, (T.TextMap, T.TextAreaMap)) and t in (T.TextMap, T.TextAreaMap):
+        return "smarttext"
+    return "pivot"
+
+
+@register_stage
+class MapVectorizerModel(VectorizerMixin, SequenceTransformer):
+    operation_name = "vecMap"
+
+    def __init__(self, kind="real", keys=None, fills=None, tops=None, clean_keys=False, clean_text=True,
+                 track_nulls=True, reference_date=None, methods=None, num_features=512, uid=None, **kw):
+        super().__init__(uid=uid, **kw)
+        self.kind = kind
+        self.keys = [list(k) for k in (keys or [])]
+        self.fills = [list(f) for f in (fills or [])]
+        self.tops = [[list(t) for t in tt] for tt in (tops or [])]
+        self.clean_keys = clean_keys
+        self.clean_text = clean_text
+        self.track_nulls = track_nulls
+        self.reference_date = reference_date
+        self.methods = [list(m) for m in (methods or [])]
+        self.num_features = num_features
+
+    def transform_columns(self, *cols, ds=None):
+        n = len(cols[0]) if cols else 0
+        blocks = []
+        for ci, c in enumerate(cols):
+            vals = c.values if isinstance(c, ObjectColumn) else np.array(c.to_list(), dtype=object)
+            keys = self.keys[ci]
+            kidx = {k: i for i, k in enumerate(keys)}
+            if self.kind in ("real", "integral", "binary", "date"):
+                per = 2 if self.track_nulls else 1
+                b = np.zeros((n, len(keys) * per))
+                seen = np.zeros((n, len(keys)), bool)
+                for r, m in enumerate(vals):
+                    for k, v in (m or {}).items():
+                        j = kidx.get(_clean_key(k, self.clean_keys))
+                        if j is None or v is None:
+                            continue
+                        if self.kind == "date":
+                            v = float((int(self.reference_date) - int(v)) // 86400000)
+                        elif self.kind == "binary":
+                            v = 1.0 if v else 0.0
+                        b[r, j * per] = float(v)
+                        seen[r, j] = True
+                for j in range(len(keys)):
+                    miss = ~seen[:, j]
+                    b[miss, j * per] = self.fills[ci][j]
+                    if self.track_nulls:
+                        b[:, j * per + 1] = miss.astype(np.float64)
+                blocks.append(b)
+            elif self.kind == "geo":
+                per = 4 if self.track_nulls else 3
+                b = np.zeros((n, len(keys) * per))
+                for j in range(len(keys)):
+                    b[:, j * per:j * per + 3] = self.fills[ci][j] if self.fills[ci][j] else [0.0, 0.0, 0.0]
+                    if self.track_nulls:
+                        b[:, j * per + 3] = 1.0
+                for r, m in enumerate(vals):
+                    for k, v in (m or {}).items():
+                        j = kidx.get(_clean_key(k, self.clean_keys))
+                        if j is None or not v:
+                            continue
+                        b[r, j * per:j * per + 3] = v
+                        if self.track_nulls:
+                            b[r, j * per + 3] = 0.0
+                blocks.append(b)
+            else:  # pivot / set / smarttext (pivot or hash per key)
+                parts = []
+                for j, k in enumerate(keys):
+                    method = self.methods[ci][j] if self.methods else "pivot"
+                    top = self.tops[ci][j]
+                    if method == "hash":
+                        w = self.num_features + (1 if self.track_nulls else 0)
+                        bb = np.zeros((n, w))
+                        for r, m in enumerate(vals):
+                            v = _get(m, k, self.clean_keys)
+                            toks = TU.tokenize(v) if isinstance(v, str) else []
+                            if toks:
+                                idx = TU.hash_terms(toks, self.num_features)
+                                np.add.at(bb[r], idx, 1.0)
+                            elif self.track_nulls:
+                                bb[r, -1] = 1.0
+                        parts.append(bb)
+                        continue
+                    w = len(top) + 1 + (1 if self.track_nulls else 0)
+                    bb = np.zeros((n, w))
+                    ix = {v: i for i, v in enumerate(top)}
+                    for r, m in enumerate(vals):
+                        v = _get(m, k, self.clean_keys)
+                        items = ([] if v is None else (list(v) if isinstance(v, (set, frozenset, list)) else [v]))
+                        if not items:
+                            if self.track_nulls:
+                                bb[r, -1] = 1.0
+                            continue
+                        for it in items:
+                            s = TU.clean_string(str(it)) if self.clean_text else str(it)
+                            bb[r, ix.get(s, len(top))] += 1.0
+                    parts.append(bb)
+                blocks.append(np.concatenate(parts, 1) if parts else np.zeros((n, 0)))
+        dev = cols[0].device if cols else torch.device("cpu")
+        out = np.concatenate(blocks, 1) if blocks else np.zeros((n, 0))
+        return self._vec(torch.as_tensor(out, dtype=vector_dtype(dev), device=dev))
+
+    def ctor_args(self):
+        return {"kind": self.kind, "keys": self.keys, "fills": self.fills, "tops": self.tops,
+                "cleanKeys": self.clean_keys, "cleanText": self.clean_text, "trackNulls": self.track_nulls,
+                "referenceDate": self.reference_date, "methods": self.methods, "numFeatures": self.num_features}
+
+    def load_ctor_args(self, a):
+        self.__init__(a["kind"], a["keys"], a["fills"], a["tops"], a["cleanKeys"], a["cleanText"], a["trackNulls"],
+                      a.get("referenceDate"), a.get("methods"), a.get("numFeatures", 512), uid=self.uid)
+
+
+def _get(m, k, clean):
+    if not m:
+        return None
+    if k in m:
+        return m[k]
+    if clean:
+        for kk, v in m.items():
+            if TU.clean_string(kk) == k:
+                return v
+    return None
+
+
+@register_stage
+class MapVectorizer(VectorizerMixin, SequenceEstimator):
+    operation_name = "vecMap"
+    _defaults = {"kind": "real", "clean_keys": False, "clean_text": True, "track_nulls": True,
+                 "fill_with_mean": True, "fill_with_mode": True, "fill_value": 0.0, "top_k": 20, "min_support": 10,
+                 "reference_date": None, "max_cardinality": 30, "num_features": 512, "allow_keys": None,
+                 "block_keys": None}
+
+    def fit_columns(self, *cols, ds=None):
+        from ...utils.dates import now_ms
+        p = self.params
+        kind = p["kind"]
+        ref = p["reference_date"] or now_ms()
+        self.params["reference_date"] = ref
+        all_keys, fills, tops, methods = [], [], [], []
+        colsm = []
+        for c, t in zip(cols, self.get_transient_features()):
+            vals = c.values if isinstance(c, ObjectColumn) else c.to_list()
+            per_key: Dict[str, list] = {}
+            for m in vals:
+                for k, v in (m or {}).items():
+                    if v is None:
+                        continue
+                    per_key.setdefault(_clean_key(k, p["clean_keys"]), []).append(v)
+            keys = sorted(per_key)
+            if p["allow_keys"]:
+                keys = [k for k in keys if k in set(p["allow_keys"])]
+            if p["block_keys"]:
+                keys = [k for k in keys if k not in set(p["block_keys"])]
+            all_keys.append(keys)
+            f_col, t_col, m_col = [], [], []
+            for k in keys:
+                vs = per_key[k]
+                if kind == "real":
+                    f_col.append(float(np.mean(vs)) if p["fill_with_mean"] else float(p["fill_value"]))
+                elif kind == "integral":
+                    if p["fill_with_mode"]:
+                        cnt = Counter(int(v) for v in vs)
+                        f_col.append(float(min(cnt.items(), key=lambda kv: (-kv[1], kv[0]))[0]))
+                    else:
+                        f_col.append(float(p["fill_value"]))
+                elif kind in ("binary", "date"):
+                    f_col.append(float(p["fill_value"]))
+                elif kind == "geo":
+                    from ...features.aggregators import Event, GeolocationMidpoint
+                    f_col.append(GeolocationMidpoint().aggregate(Event(0, v) for v in vs))
+                else:
+                    cnt: Counter = Counter()
+                    for v in vs:
+                        items = list(v) if isinstance(v, (set, frozenset, list)) else [v]
+                        cnt.update(TU.clean_string(str(i)) if p["clean_text"] else str(i) for i in items)
+                    method = "pivot"
+                    if kind == "smarttext" and len(cnt) > p["max_cardinality"]:
+                        method = "hash"
+                    m_col.append(method)
+                    t_col.append(top_values(cnt, p["top_k"], p["min_support"]) if method == "pivot" else [])
+            fills.append(f_col)
+            tops.append(t_col)
+            methods.append(m_col)
+            for j, k in enumerate(keys):
+                base = dict(parent_feature_name=(t.name,), parent_feature_type=(t.type_name,), grouping=k)
+                if kind in ("real", "integral", "binary", "date"):
+                    colsm.append(OpVectorColumnMetadata(**base))
+                    if p["track_nulls"]:
+                        colsm.append(OpVectorColumnMetadata(indicator_value=NULL_STRING, **base))
+                elif kind == "geo":
+                    colsm += [OpVectorColumnMetadata(descriptor_value=d, **base) for d in ("lat", "lon", "accuracy")]
+                    if p["track_nulls"]:
+                        colsm.append(OpVectorColumnMetadata(indicator_value=NULL_STRING, **base))
+                elif m_col[j] == "hash":
+                    colsm += [OpVectorColumnMetadata(**base) for _ in range(p["num_features"])]
+                    if p["track_nulls"]:
+                        colsm.append(OpVectorColumnMetadata(indicator_value=NULL_STRING, **base))
+                else:
+                    vals2 = t_col[j] + [OTHER_STRING] + ([NULL_STRING] if p["track_nulls"] else [])
+                    colsm += [OpVectorColumnMetadata(indicator_value=v, **base) for v in vals2]
+        self.metadata["vector_metadata"] = self.vector_metadata(colsm)
+        return MapVectorizerModel(kind, all_keys, fills, tops, p["clean_keys"], p["clean_text"], p["track_nulls"],
+                                  ref, methods, p["num_features"])
+
+
+def map_vectorize(t, feats, label, D) -> list:
+    kind = _kind_of(t)
+    if t is T.PhoneMap or t is T.EmailMap or t is T.URLMap or t is T.Base64Map:
+        kind = "pivot"
+    st = MapVectorizer(kind=kind, clean_keys=D.CleanKeys, clean_text=D.CleanText, track_nulls=D.TrackNulls,
+                       top_k=D.TopK, min_support=D.MinSupport, reference_date=D.ReferenceDate,
+                       max_cardinality=D.MaxCategoricalCardinality, num_features=D.DefaultNumOfFeatures,
+                       fill_value=float(D.FillValue))
+    return [st.set_input(feats).get_output()]

@@ -1,0 +1,455 @@
+"""Numeric transformers: arithmetic, unary math, scaling, filling, bucketizing, calibration.
+
+Reference: ``MathTransformers.scala:50-393`` (plus / minus / multiply / divide, scalar variants, abs, ceil,
+floor, round, exp, sqrt, log, power, roundDigits), ``FillMissingWithMean.scala:47``,
+``OpScalarStandardScaler.scala:49``, ``ScalerTransformer.scala:144`` / ``DescalerTransformer.scala:56-92``,
+``PercentileCalibrator.scala:48``, ``NumericBucketizer.scala:54-300`` (binary search over splits,
+one-hot + invalid + null slots) and ``IsotonicRegressionCalibrator.scala:44-63``. All ops are
+whole-column tensor expressions (validity masks carried alongside values).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ...config import vector_dtype
+from ...data.columns import NumericColumn, VectorColumn
+from ...data.vector_metadata import NULL_STRING, OTHER_STRING, OpVectorColumnMetadata, OpVectorMetadata
+from ...features import types as T
+from ..base import (BinaryEstimator, BinaryTransformer, OpTransformer, UnaryEstimator, UnaryTransformer,
+                    register_stage)
+
+
+def _f64(c: NumericColumn):
+    return c.values.to(torch.float64), c.valid
+
+
+def _finite(v):
+    return ~(torch.isnan(v) | torch.isinf(v))
+
+
+@register_stage
+class BinaryMathTransformer(BinaryTransformer):
+    """plus / minus / multiply / divide of two numeric columns -> Real."""
+    output_type = T.Real
+    _defaults = {"op": "plus"}
+
+    def __init__(self, op: str = "plus", uid=None, **kw):
+        super().__init__(None, uid=uid, operation_name=op, op=op, **kw)
+
+    def transform_columns(self, a, b, ds=None):
+        x, xa = _f64(a)
+        y, ya = _f64(b)
+        op = self.params["op"]
+        if op == "plus":
+            v = torch.where(xa & ya, x + y, torch.where(xa, x, y))
+            ok = xa | ya
+        elif op == "minus":
+            v = torch.where(xa & ya, x - y, torch.where(xa, x, -y))
+            ok = xa | ya
+        elif op == "multiply":
+            v = x * y
+            ok = xa & ya & _finite(v)
+        elif op == "divide":
+            v = x / y
+            ok = xa & ya & _finite(v)
+        else:
+            raise ValueError(op)
+        return NumericColumn(T.Real, torch.where(ok, v, torch.zeros_like(v)), ok)
+
+    def transform_row(self, a, b):
+        col = self.transform_columns(NumericColumn.from_values(T.Real, [a]), NumericColumn.from_values(T.Real, [b]))
+        return col.row(0)
+
+
+@register_stage
+class ScalarMathTransformer(UnaryTransformer):
+    """``x op scalar`` (or ``scalar op x`` when reversed) -> Real."""
+    output_type = T.Real
+    _defaults = {"op": "plus", "scalar": 0.0, "reverse": False}
+
+    def __init__(self, op: str = "plus", scalar: float = 0.0, reverse: bool = False, uid=None, **kw):
+        super().__init__(None, uid=uid, operation_name=op + "S", op=op, scalar=float(scalar), reverse=reverse, **kw)
+
+    def transform_columns(self, a, ds=None):
+        x, ok = _f64(a)
+        s = self.params["scalar"]
+        op = self.params["op"]
+        rev = self.params["reverse"]
+        if op == "plus":
+            v = x + s
+        elif op == "minus":
+            v = (s - x) if rev else (x - s)
+        elif op == "multiply":
+            v = x * s
+        elif op == "divide":
+            v = (s / x) if rev else (x / s)
+        elif op == "power":
+            v = torch.pow(torch.full_like(x, s), x) if rev else torch.pow(x, s)
+        else:
+            raise ValueError(op)
+        ok = ok & _finite(v)
+        return NumericColumn(T.Real, torch.where(ok, v, torch.zeros_like(v)), ok)
+
+    def transform_row(self, a):
+        return self.transform_columns(NumericColumn.from_values(T.Real, [a])).row(0)
+
+
+_UNARY = {"abs": torch.abs, "ceil": torch.ceil, "floor": torch.floor, "round": torch.round, "exp": torch.exp,
+          "sqrt": torch.sqrt, "log": None, "sigmoid": torch.sigmoid}
+
+
+@register_stage
+class UnaryMathTransformer(UnaryTransformer):
+    output_type = T.Real
+    _defaults = {"op": "abs", "base": math.e, "digits": 0}
+
+    def __init__(self, op: str = "abs", uid=None, **kw):
+        super().__init__(None, uid=uid, operation_name=op, op=op, **kw)
+        if op in ("ceil", "floor", "round"):
+            self.output_type = T.Integral
+
+    def transform_columns(self, a, ds=None):
+        x, ok = _f64(a)
+        op = self.params["op"]
+        if op == "log":
+            v = torch.log(x) / math.log(self.params["base"])
+        elif op == "roundDigits":
+            f = 10.0 ** self.params["digits"]
+            v = torch.round(x * f) / f
+        else:
+            v = _UNARY[op](x)
+        ok = ok & _finite(v)
+        if op in ("ceil", "floor", "round"):
+            return NumericColumn(T.Integral, torch.where(ok, v, torch.zeros_like(v)).to(torch.int64), ok)
+        return NumericColumn(T.Real, torch.where(ok, v, torch.zeros_like(v)), ok)
+
+    def transform_row(self, a):
+        return self.transform_columns(NumericColumn.from_values(T.Real, [a])).row(0)
+
+
+# ---------------------------------------------------------------------------------------- fills
+@register_stage
+class FillMissingWithMeanModel(UnaryTransformer):
+    operation_name = "fillWithMean"
+    output_type = T.RealNN
+
+    def __init__(self, mean: float = 0.0, uid=None, **kw):
+        super().__init__(None, uid=uid, **kw)
+        self.mean = mean
+
+    def transform_columns(self, a, ds=None):
+        x, ok = _f64(a)
+        return NumericColumn(T.RealNN, torch.where(ok, x, torch.full_like(x, self.mean)),
+                             torch.ones_like(ok))
+
+    def transform_row(self, a):
+        return float(a) if a is not None else self.mean
+
+    def ctor_args(self):
+        return {"mean": self.mean}
+
+    def load_ctor_args(self, a):
+        self.mean = a["mean"]
+
+
+@register_stage
+class FillMissingWithMean(UnaryEstimator):
+    operation_name = "fillWithMean"
+    output_type = T.RealNN
+    _defaults = {"default_value": 0.0}
+
+    def fit_columns(self, a, ds=None):
+        x, ok = _f64(a)
+        n = int(ok.sum())
+        m = float(x[ok].mean()) if n > 0 else float(self.params["default_value"])
+        return FillMissingWithMeanModel(m)
+
+
+@register_stage
+class OpScalarStandardScalerModel(UnaryTransformer):
+    operation_name = "stdScaled"
+    output_type = T.RealNN
+
+    def __init__(self, mean: float = 0.0, std: float = 1.0, with_mean=True, with_std=True, uid=None, **kw):
+        super().__init__(None, uid=uid, **kw)
+        self.mean, self.std, self.with_mean, self.with_std = mean, std, with_mean, with_std
+
+    def transform_columns(self, a, ds=None):
+        x, ok = _f64(a)
+        v = x - self.mean if self.with_mean else x
+        if self.with_std:
+            v = v / self.std if self.std != 0 else torch.zeros_like(v)
+        return NumericColumn(T.RealNN, torch.where(ok, v, torch.zeros_like(v)), torch.ones_like(ok))
+
+    def transform_row(self, a):
+        return self.transform_columns(NumericColumn.from_values(T.Real, [a])).row(0)
+
+    def ctor_args(self):
+        return {"mean": self.mean, "std": self.std, "withMean": self.with_mean, "withStd": self.with_std}
+
+    def load_ctor_args(self, a):
+        self.mean, self.std, self.with_mean, self.with_std = a["mean"], a["std"], a["withMean"], a["withStd"]
+
+
+@register_stage
+class OpScalarStandardScaler(UnaryEstimator):
+    """z-normalization (``RichNumericFeature.zNormalize``)."""
+    operation_name = "stdScaled"
+    output_type = T.RealNN
+    _defaults = {"with_mean": True, "with_std": True}
+
+    def fit_columns(self, a, ds=None):
+        x, ok = _f64(a)
+        v = x[ok]
+        mean = float(v.mean()) if v.numel() else 0.0
+        std = float(v.std(unbiased=True)) if v.numel() > 1 else 0.0
+        return OpScalarStandardScalerModel(mean, std, self.params["with_mean"], self.params["with_std"])
+
+
+@register_stage
+class ScalerTransformer(UnaryTransformer):
+    """Linear (``slope * x + intercept``) or log scaling with stored args (``ScalerTransformer.scala``)."""
+    operation_name = "scaler"
+    output_type = T.Real
+    _defaults = {"scaling_type": "Linear", "slope": 1.0, "intercept": 0.0}
+
+    def transform_columns(self, a, ds=None):
+        x, ok = _f64(a)
+        if self.params["scaling_type"] == "Logarithmic":
+            v = torch.log(x)
+        else:
+            v = self.params["slope"] * x + self.params["intercept"]
+        ok = ok & _finite(v)
+        return NumericColumn(T.Real, torch.where(ok, v, torch.zeros_like(v)), ok)
+
+    def transform_row(self, a):
+        return self.transform_columns(NumericColumn.from_values(T.Real, [a])).row(0)
+
+
+@register_stage
+class DescalerTransformer(BinaryTransformer):
+    """Inverse of the scaling recorded in the metadata of the second input's origin ``ScalerTransformer``."""
+    operation_name = "descaler"
+    output_type = T.Real
+    _defaults = {"scaling_type": "Linear", "slope": 1.0, "intercept": 0.0}
+
+    def transform_columns(self, a, b=None, ds=None):
+        x, ok = _f64(a)
+        if self.params["scaling_type"] == "Logarithmic":
+            v = torch.exp(x)
+        else:
+            v = (x - self.params["intercept"]) / self.params["slope"]
+        ok = ok & _finite(v)
+        return NumericColumn(T.Real, torch.where(ok, v, torch.zeros_like(v)), ok)
+
+
+# ------------------------------------------------------------------------------------ bucketizer
+def java_double(v: float) -> str:
+    """Java ``Double.toString`` formatting (bucket labels must match the reference)."""
+    v = float(v)
+    if math.isinf(v):
+        return "Infinity" if v > 0 else "-Infinity"
+    if math.isnan(v):
+        return "NaN"
+    if v == 0:
+        return "0.0" if math.copysign(1, v) > 0 else "-0.0"
+    if 1e-3 <= abs(v) < 1e7:
+        return repr(v)
+    m, e = np.format_float_scientific(v, unique=True, trim="-").split("e")
+    if "." not in m:
+        m += ".0"
+    return f"{m}E{int(e)}"
+
+
+def bucket_labels(splits: Sequence[float], inclusion: str = "Left") -> List[str]:
+    pre, suf = ("[", ")") if inclusion == "Left" else ("(", "]")
+    return [f"{pre}{java_double(a)}-{java_double(b)}{suf}" for a, b in zip(splits[:-1], splits[1:])]
+
+
+def check_splits(splits: Sequence[float]) -> bool:
+    if len(splits) < 3:
+        return False
+    return all(a < b and not math.isnan(a) for a, b in zip(splits[:-1], splits[1:]))
+
+
+def bucketize_column(x: torch.Tensor, ok: torch.Tensor, splits: Sequence[float], track_nulls: bool,
+                     track_invalid: bool, inclusion: str, dtype) -> torch.Tensor:
+    """One-hot bucket index via binary search (``NumericBucketizer.bucketize:219-265``)."""
+    nb = len(splits) - 1
+    n = x.shape[0]
+    width = nb + (1 if track_invalid else 0) + (1 if track_nulls else 0)
+    out = torch.zeros(n, width, dtype=dtype, device=x.device)
+    s = torch.as_tensor(list(splits), dtype=torch.float64, device=x.device)
+    if inclusion == "Left":
+        idx = torch.searchsorted(s, x, right=True) - 1          # splits[i] <= x < splits[i+1]
+    else:
+        idx = torch.searchsorted(s, x, right=False) - 1         # splits[i] < x <= splits[i+1]
+    invalid = (idx < 0) | (idx >= nb) | ~_finite(x)
+    if invalid[ok].any() and not track_invalid:
+        bad = x[ok & invalid][0].item()
+        raise ValueError(f"Numeric value {bad} falls outside the bounds of the specified buckets")
+    rows = torch.arange(n, device=x.device)
+    good = ok & ~invalid
+    out[rows[good], idx[good]] = 1.0
+    if track_invalid:
+        m = ok & invalid
+        out[rows[m], nb] = 1.0
+    if track_nulls:
+        out[rows[~ok], width - 1] = 1.0
+    return out
+
+
+def bucket_metadata(tf, labels, track_nulls, track_invalid) -> List[OpVectorColumnMetadata]:
+    base = dict(parent_feature_name=(tf.name,), parent_feature_type=(tf.type_name,), grouping=tf.name)
+    cols = [OpVectorColumnMetadata(indicator_value=l, **base) for l in labels]
+    if track_invalid:
+        cols.append(OpVectorColumnMetadata(indicator_value=OTHER_STRING, **base))
+    if track_nulls:
+        cols.append(OpVectorColumnMetadata(indicator_value=NULL_STRING, **base))
+    return cols
+
+
+@register_stage
+class NumericBucketizer(OpTransformer):
+    operation_name = "numBuck"
+    output_type = T.OPVector
+    arity = 1
+    _defaults = {"splits": [float("-inf"), 0.0, float("inf")], "bucket_labels": None, "track_nulls": True,
+                 "track_invalid": False, "split_inclusion": "Left"}
+
+    def transform_columns(self, a, ds=None):
+        p = self.params
+        splits = [float(v) for v in p["splits"]]
+        x, ok = _f64(a)
+        labels = p["bucket_labels"] or bucket_labels(splits, p["split_inclusion"])
+        if self._inputs:
+            t = self.get_transient_features()[0]
+            self.metadata["vector_metadata"] = OpVectorMetadata(
+                self.get_output_feature_name(), bucket_metadata(t, labels, p["track_nulls"], p["track_invalid"]),
+                {t.name: __import__("transmogrifai_amd.data.vector_metadata", fromlist=["FeatureHistory"])
+                 .FeatureHistory(tuple(t.origin_features), tuple(t.stages) + (self.stage_name(),))})
+        out = bucketize_column(x, ok, splits, p["track_nulls"], p["track_invalid"], p["split_inclusion"],
+                               vector_dtype(x.device))
+        return VectorColumn(out, self.metadata.get("vector_metadata"))
+
+
+@register_stage
+class PercentileCalibratorModel(UnaryTransformer):
+    operation_name = "percentCalibrator"
+    output_type = T.RealNN
+
+    def __init__(self, splits=None, uid=None, **kw):
+        super().__init__(None, uid=uid, **kw)
+        self.splits = list(splits or [])
+
+    def transform_columns(self, a, ds=None):
+        x, ok = _f64(a)
+        s = torch.as_tensor(self.splits, dtype=torch.float64, device=x.device)
+        b = torch.searchsorted(s, x, right=False).clamp(max=max(len(self.splits) - 1, 0)).to(torch.float64)
+        scale = 99.0 / max(len(self.splits) - 1, 1)
+        v = b * scale
+        return NumericColumn(T.RealNN, torch.where(ok, v, torch.zeros_like(v)), torch.ones_like(ok))
+
+    def ctor_args(self):
+        return {"splits": self.splits}
+
+    def load_ctor_args(self, a):
+        self.splits = list(a["splits"])
+
+
+@register_stage
+class PercentileCalibrator(UnaryEstimator):
+    """Map a score to its percentile bucket (0..99) using quantile splits (``PercentileCalibrator.scala``)."""
+    operation_name = "percentCalibrator"
+    output_type = T.RealNN
+    _defaults = {"expected_num_buckets": 100}
+
+    def fit_columns(self, a, ds=None):
+        x, ok = _f64(a)
+        v = x[ok]
+        k = self.params["expected_num_buckets"]
+        if v.numel() == 0:
+            return PercentileCalibratorModel([0.0])
+        q = torch.quantile(v, torch.linspace(0, 1, k + 1, dtype=torch.float64, device=v.device)[1:])
+        return PercentileCalibratorModel(torch.unique(q).tolist())
+
+
+@register_stage
+class IsotonicRegressionCalibratorModel(BinaryTransformer):
+    operation_name = "isotonic"
+    output_type = T.RealNN
+    allow_label_as_input = True
+
+    def __init__(self, boundaries=None, predictions=None, uid=None, **kw):
+        super().__init__(None, uid=uid, **kw)
+        self.boundaries = list(boundaries or [])
+        self.predictions = list(predictions or [])
+
+    def transform_columns(self, label, a, ds=None):
+        x, ok = _f64(a)
+        bx = torch.as_tensor(self.boundaries, dtype=torch.float64, device=x.device)
+        by = torch.as_tensor(self.predictions, dtype=torch.float64, device=x.device)
+        v = _interp(x, bx, by)
+        return NumericColumn(T.RealNN, torch.where(ok, v, torch.zeros_like(v)), torch.ones_like(ok))
+
+    def ctor_args(self):
+        return {"boundaries": self.boundaries, "predictions": self.predictions}
+
+    def load_ctor_args(self, a):
+        self.boundaries, self.predictions = list(a["boundaries"]), list(a["predictions"])
+
+
+def _interp(x, bx, by):
+    if bx.numel() == 0:
+        return torch.zeros_like(x)
+    if bx.numel() == 1:
+        return torch.full_like(x, float(by[0]))
+    i = torch.searchsorted(bx, x).clamp(1, bx.numel() - 1)
+    x0, x1, y0, y1 = bx[i - 1], bx[i], by[i - 1], by[i]
+    t = torch.where(x1 > x0, (x - x0) / (x1 - x0), torch.zeros_like(x))
+    v = y0 + t * (y1 - y0)
+    v = torch.where(x <= bx[0], by[0], v)
+    return torch.where(x >= bx[-1], by[-1], v)
+
+
+def pava(x: np.ndarray, y: np.ndarray, w: Optional[np.ndarray] = None, increasing: bool = True):
+    """Pool-adjacent-violators isotonic fit; returns (boundaries, predictions) like Spark."""
+    order = np.lexsort((y, x))
+    x, y = x[order], y[order]
+    w = np.ones_like(y) if w is None else w[order]
+    if not increasing:
+        y = -y
+    vals, wts, lo, hi = [], [], [], []
+    for i in range(len(x)):
+        vals.append(y[i]); wts.append(w[i]); lo.append(x[i]); hi.append(x[i])
+        while len(vals) > 1 and vals[-2] > vals[-1]:
+            v = (vals[-2] * wts[-2] + vals[-1] * wts[-1]) / (wts[-2] + wts[-1])
+            wt = wts[-2] + wts[-1]
+            l2 = lo[-2]
+            vals.pop(); wts.pop(); lo.pop(); hi.pop()
+            vals[-1], wts[-1], lo[-1] = v, wt, l2
+    bnd, pred = [], []
+    for v, l, h in zip(vals, lo, hi):
+        vv = v if increasing else -v
+        bnd.append(l); pred.append(vv)
+        if h != l:
+            bnd.append(h); pred.append(vv)
+    return bnd, pred
+
+
+@register_stage
+class IsotonicRegressionCalibrator(BinaryEstimator):
+    operation_name = "isotonic"
+    output_type = T.RealNN
+    allow_label_as_input = True
+    _defaults = {"isotonic": True}
+
+    def fit_columns(self, label, a, ds=None):
+        x, ok = _f64(a)
+        y = label.values.to(torch.float64)
+        b, p = pava(x[ok].cpu().numpy(), y[ok].cpu().numpy(), increasing=self.params["isotonic"])
+        return IsotonicRegressionCalibratorModel(b, p)

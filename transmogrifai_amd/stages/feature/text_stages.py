@@ -1,0 +1,294 @@
+"""Text transformers: value maps, tokenizer, hashing TF / IDF, validators, detectors.
+
+Reference: ``TextTokenizer`` (``core/.../impl/feature/TextTokenizer.scala:125-234``), ``OpHashingTF``
+and ``IDF`` Spark wrappers (``RichListFeature.scala:57-80``, ``RichVectorFeature.scala:57-60``),
+``EmailDomainToPickList`` / ``URLDomainToPickList`` map functions (``RichTextFeature.scala:617-680``),
+``ValidEmailTransformer``, ``MimeTypeDetector`` (Tika, ``RichTextFeature.scala:712-731``),
+``PhoneNumberParser.isValidPhoneDefaultCountry`` (``PhoneNumberParser.scala:143-255``),
+``TextLenTransformer`` (``TextLenTransformer.scala:45``), ``TextListNullTransformer`` (``:48``).
+
+Text maps run once per *distinct* value of a dictionary-encoded column (``TextColumn.map_vocab``).
+"""
+from __future__ import annotations
+
+import base64
+import re
+from typing import Callable, Dict, Optional
+
+import numpy as np
+import torch
+
+from ...config import vector_dtype
+from ...data.columns import NumericColumn, ObjectColumn, TextColumn, VectorColumn, column_from_values
+from ...data.vector_metadata import OpVectorColumnMetadata
+from ...features import types as T
+from ...utils import text as TU
+from ..base import (OpEstimator, OpTransformer, SequenceTransformer, UnaryEstimator, UnaryTransformer,
+                    register_stage)
+from .vectorizers import (HashingParams, VectorizerMixin, _terms_csr, hash_metadata, col_meta)
+from ...ops import vector as V
+
+# ------------------------------------------------------------------------------- named value maps
+VALUE_FNS: Dict[str, Callable] = {}
+
+
+def value_fn(name):
+    def deco(fn):
+        VALUE_FNS[name] = fn
+        return fn
+    return deco
+
+
+@value_fn("EmailDomainToPickList")
+def _email_domain(s):
+    return TU.email_domain(s)
+
+
+@value_fn("EmailPrefixToText")
+def _email_prefix(s):
+    return TU.email_prefix(s)
+
+
+@value_fn("URLDomainToPickList")
+def _url_domain_valid(s):
+    return TU.url_domain(s) if TU.is_valid_url(s) else None
+
+
+@value_fn("URLDomainToText")
+def _url_domain(s):
+    return TU.url_domain(s)
+
+
+@value_fn("URLProtocolToText")
+def _url_protocol(s):
+    return TU.url_protocol(s)
+
+
+@value_fn("Identity")
+def _ident(s):
+    return s
+
+
+@value_fn("CleanText")
+def _clean(s):
+    return TU.clean_string(s)
+
+
+_MAGIC = [(b"%PDF", "application/pdf"), (b"\x89PNG", "image/png"), (b"\xff\xd8\xff", "image/jpeg"),
+          (b"GIF8", "image/gif"), (b"PK\x03\x04", "application/zip"), (b"ID3", "audio/mpeg"),
+          (b"RIFF", "audio/x-wav"), (b"<?xml", "application/xml"), (b"\x1f\x8b", "application/gzip"),
+          (b"BM", "image/bmp"), (b"OggS", "audio/ogg"), (b"fLaC", "audio/x-flac"), (b"<html", "text/html"),
+          (b"<!DOCTYPE html", "text/html")]
+
+
+@value_fn("MimeTypeDetector")
+def detect_mime(s):
+    """Magic-byte MIME detection of base64 content (Tika replacement; parity unpinned)."""
+    if s is None:
+        return None
+    try:
+        raw = base64.b64decode(s, validate=False)
+    except Exception:
+        return None
+    if not raw:
+        return None
+    for sig, mime in _MAGIC:
+        if raw[:len(sig)].lower() == sig.lower():
+            return mime
+    try:
+        raw[:512].decode("utf-8")
+        return "text/plain"
+    except UnicodeDecodeError:
+        return "application/octet-stream"
+
+
+_PHONE_DIGITS = re.compile(r"\d")
+
+
+def is_valid_phone(s: Optional[str], region: str = "US", strict: bool = False) -> Optional[bool]:
+    """NANP validity for the default region (libphonenumber replacement; parity unpinned)."""
+    if s is None:
+        return None
+    digits = "".join(_PHONE_DIGITS.findall(s))
+    if s.strip().startswith("+") and not digits.startswith("1"):
+        return 7 <= len(digits) <= 15
+    if len(digits) == 11 and digits[0] == "1":
+        digits = digits[1:]
+    if len(digits) != 10:
+        return False
+    return digits[0] in "23456789" and digits[3] in "23456789"
+
+
+@register_stage
+class TextMapTransformer(UnaryTransformer):
+    """Applies a named value function to each distinct text value (map[PickList] etc.)."""
+    operation_name = "map"
+
+    def __init__(self, fn_name: str = "Identity", output_type=T.Text, uid=None, operation_name=None, **kw):
+        super().__init__(None, uid=uid, operation_name=operation_name or fn_name, output_type=output_type, **kw)
+        self.fn_name = fn_name
+
+    def transform_fn(self, v):
+        return VALUE_FNS[self.fn_name](v)
+
+    def transform_columns(self, *cols, ds=None):
+        c = cols[0]
+        if isinstance(c, TextColumn) and issubclass(self.output_type, T.Text):
+            return c.map_vocab(VALUE_FNS[self.fn_name], self.output_type)
+        return super().transform_columns(*cols, ds=ds)
+
+    def ctor_args(self):
+        return {"fnName": self.fn_name, "tto": self.output_type.__name__}
+
+    def load_ctor_args(self, a):
+        self.fn_name = a["fnName"]
+        self.output_type = T.feature_type_from_name(a["tto"])
+
+
+@register_stage
+class ValidEmailTransformer(UnaryTransformer):
+    operation_name = "isValidEmail"
+    output_type = T.Binary
+
+    def transform_fn(self, v):
+        return None if v is None else TU.is_valid_email(v)
+
+
+@register_stage
+class PhoneValidator(UnaryTransformer):
+    operation_name = "isValidPhoneDefaultCountry"
+    output_type = T.Binary
+    _defaults = {"default_region": "US", "strict": False}
+
+    def transform_fn(self, v):
+        return is_valid_phone(v, self.params["default_region"], self.params["strict"])
+
+    def transform_columns(self, *cols, ds=None):
+        c = cols[0]
+        if isinstance(c, TextColumn):
+            lut = np.array([1.0 if is_valid_phone(s) else 0.0 for s in c.vocab] + [0.0])
+            ok = c.codes >= 0
+            idx = torch.where(ok, c.codes.long(), torch.full_like(c.codes.long(), len(c.vocab)))
+            vals = torch.as_tensor(lut, device=c.codes.device)[idx] > 0.5
+            return NumericColumn(T.Binary, vals, ok)
+        return super().transform_columns(*cols, ds=ds)
+
+
+@register_stage
+class TextTokenizer(UnaryTransformer):
+    """Lowercase + StandardAnalyzer tokenization + min token length -> TextList."""
+    operation_name = "textToken"
+    output_type = T.TextList
+    _defaults = {"to_lowercase": True, "min_token_length": 1, "auto_detect_language": False,
+                 "strip_html": False, "default_language": "Unknown"}
+
+    def transform_fn(self, v):
+        if v is None:
+            return []
+        s = TU.strip_html(v) if self.params["strip_html"] else v
+        return TU.tokenize(s, self.params["to_lowercase"], self.params["min_token_length"])
+
+    def transform_columns(self, *cols, ds=None):
+        c = cols[0]
+        if isinstance(c, TextColumn):
+            toks = [self.transform_fn(s) for s in c.vocab]
+            codes = c.codes.cpu().numpy()
+            out = np.empty(len(codes), dtype=object)
+            for i, k in enumerate(codes):
+                out[i] = list(toks[k]) if k >= 0 else []
+            return ObjectColumn(T.TextList, out)
+        return super().transform_columns(*cols, ds=ds)
+
+
+@register_stage
+class TextLenTransformer(VectorizerMixin, SequenceTransformer):
+    operation_name = "textLen"
+
+    def transform_columns(self, *cols, ds=None):
+        tfs = self.get_transient_features()
+        self.metadata["vector_metadata"] = self.vector_metadata(
+            [col_meta(t, descriptor="TextLenValue") for t in tfs])
+        dev = cols[0].device
+        parts = []
+        for c in cols:
+            if isinstance(c, TextColumn):
+                lens = torch.as_tensor([float(sum(len(t) for t in TU.tokenize(s))) for s in c.vocab] + [0.0],
+                                       device=dev)
+                idx = torch.where(c.codes >= 0, c.codes.long(), torch.full_like(c.codes.long(), len(c.vocab)))
+                parts.append(lens[idx])
+            else:
+                parts.append(torch.as_tensor([float(sum(len(x) for x in (v or []))) for v in c.to_list()],
+                                             device=dev))
+        return self._vec(torch.stack(parts, 1).to(vector_dtype(dev)))
+
+
+@register_stage
+class TextListNullTransformer(VectorizerMixin, SequenceTransformer):
+    operation_name = "textListNull"
+
+    def transform_columns(self, *cols, ds=None):
+        tfs = self.get_transient_features()
+        self.metadata["vector_metadata"] = self.vector_metadata([col_meta(t, is_null=True) for t in tfs])
+        dev = cols[0].device
+        parts = [c.null_mask().to(dev).to(torch.float64) for c in cols]
+        return self._vec(torch.stack(parts, 1).to(vector_dtype(dev)))
+
+
+@register_stage
+class OpHashingTF(VectorizerMixin, OpTransformer):
+    """Hashing term frequency of a TextList (Spark ``HashingTF``, murmur3 seed 42, no name prefix)."""
+    operation_name = "hashingTF"
+    arity = 1
+    _defaults = {"num_features": 512, "binary": False}
+
+    def transform_columns(self, *cols, ds=None):
+        c = cols[0]
+        hp = HashingParams(self.params["num_features"], 1, 1 << 30, self.params["binary"], False, "separate")
+        tfs = self.get_transient_features()
+        self.metadata["vector_metadata"] = self.vector_metadata(hash_metadata(tfs, hp))
+        lists = [[str(x) for x in (v or [])] for v in c.to_list()]
+        indptr, idx, vals = _terms_csr(lists, None, hp)
+        dev = c.device
+        out = torch.zeros(len(lists), hp.num_features, dtype=vector_dtype(dev), device=dev)
+        V.csr_rows_scatter_add(out, torch.arange(len(lists), device=dev, dtype=torch.int32), indptr,
+                               idx.astype(np.int64), vals)
+        return self._vec(out)
+
+
+@register_stage
+class IDFModel(VectorizerMixin, OpTransformer):
+    operation_name = "idf"
+    arity = 1
+
+    def __init__(self, idf=None, uid=None, **kw):
+        super().__init__(uid=uid, **kw)
+        self.idf = None if idf is None else np.asarray(idf, np.float64)
+
+    def transform_columns(self, *cols, ds=None):
+        c = cols[0]
+        w = torch.as_tensor(self.idf, dtype=c.values.dtype, device=c.values.device)
+        return VectorColumn(c.values * w[None, :], c.metadata if self.metadata.get("vector_metadata") is None
+                            else self.metadata["vector_metadata"])
+
+    def ctor_args(self):
+        return {"idf": self.idf.tolist()}
+
+    def load_ctor_args(self, a):
+        self.idf = np.asarray(a["idf"], np.float64)
+
+
+@register_stage
+class IDF(VectorizerMixin, UnaryEstimator):
+    """Spark IDF: ``log((m + 1) / (df + 1))``, zeroed for terms with df < minDocFreq."""
+    operation_name = "idf"
+    _defaults = {"min_doc_freq": 0}
+
+    def fit_columns(self, *cols, ds=None):
+        x = cols[0].values
+        m = x.shape[0]
+        df = (x != 0).sum(0).to(torch.float64).cpu().numpy()
+        idf = np.log((m + 1.0) / (df + 1.0))
+        idf[df < self.params["min_doc_freq"]] = 0.0
+        if cols[0].metadata is not None:
+            self.metadata["vector_metadata"] = cols[0].metadata.with_name(self.get_output_feature_name())
+        return IDFModel(idf)

@@ -1,0 +1,181 @@
+"""Hold-out reservation and training-set preparation.
+
+Reference: ``Splitter`` (``core/.../stages/impl/tuning/Splitter.scala:58-182``; reserve 0.1, maxTrainingSample 1e6),
+``DataSplitter`` (``DataSplitter.scala:73-98``: downsample to ``maxTrainingSample``), ``DataBalancer``
+(``DataBalancer.scala:84-303``: up/down-sample the minority class to ``sampleFraction``) and ``DataCutter``
+(``DataCutter.scala:78-334``: keep at most ``maxLabelCategories`` labels above ``minLabelFraction``).
+
+Splitters work on row-index tensors (no data copies): sampling masks come from a seeded
+counter-based RNG so every rank of a sharded dataset draws the same decision for a global row id.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..uid import make_uid
+
+
+def row_uniform(row_ids: torch.Tensor, seed: int, stream: int = 0) -> torch.Tensor:
+    """Deterministic U[0,1) per global row id (splitmix64 hash), identical on any device / shard."""
+    x = row_ids.to(torch.int64) * 0x1E3779B97F4A7C15 + (int(seed) * 0x632BE59BD9B4E019 + stream * 0x2545F4914F6CDD1D)
+    x = x & 0x7FFFFFFFFFFFFFFF
+    x = (x ^ (x >> 30)) * 0x2F58476D1CE4E5B9 & 0x7FFFFFFFFFFFFFFF
+    x = (x ^ (x >> 27)) * 0x14C3124B4B69A5C5 & 0x7FFFFFFFFFFFFFFF
+    x = x ^ (x >> 31)
+    return (x >> 10).to(torch.float64) / float(1 << 53)
+
+
+class Splitter:
+    reserve_test_fraction = 0.1
+
+    def __init__(self, seed: Optional[int] = None, reserve_test_fraction: float = 0.1,
+                 max_training_sample: int = 1_000_000, uid: Optional[str] = None):
+        self.uid = uid or make_uid(type(self).__name__)
+        self.seed = int(np.random.randint(0, 2 ** 31 - 1)) if seed is None else int(seed)
+        self.reserve_test_fraction = reserve_test_fraction
+        self.max_training_sample = max_training_sample
+        self.down_sample_fraction = 1.0
+        self.summary: Optional[Dict] = None
+
+    def split(self, row_ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(train mask, test mask) of ``randomSplit([1 - f, f])``."""
+        u = row_uniform(row_ids, self.seed, 1)
+        test = u < self.reserve_test_fraction
+        return ~test, test
+
+    def pre_validation_prepare(self, y: torch.Tensor, n_total: Optional[int] = None) -> Dict:
+        raise NotImplementedError
+
+    def validation_prepare(self, row_ids: torch.Tensor, y: torch.Tensor, stream: int = 7) -> torch.Tensor:
+        """Boolean mask of rows kept for training."""
+        return torch.ones(row_ids.shape[0], dtype=torch.bool, device=row_ids.device)
+
+    def params(self) -> Dict:
+        return {"seed": self.seed, "reserveTestFraction": self.reserve_test_fraction,
+                "maxTrainingSample": self.max_training_sample}
+
+    def to_json(self):
+        return {"className": type(self).__name__, "uid": self.uid, "params": self.params()}
+
+
+class DataSplitter(Splitter):
+    def pre_validation_prepare(self, y, n_total=None):
+        n = int(y.shape[0]) if n_total is None else int(n_total)
+        self.down_sample_fraction = min(self.max_training_sample / max(n, 1), 1.0)
+        self.summary = {"className": "com.salesforce.op.stages.impl.tuning.DataSplitterSummary",
+                        "preSplitterDataCount": n, "downSamplingFraction": self.down_sample_fraction}
+        return self.summary
+
+    def validation_prepare(self, row_ids, y, stream=7):
+        if self.down_sample_fraction >= 1.0:
+            return torch.ones(row_ids.shape[0], dtype=torch.bool, device=row_ids.device)
+        return row_uniform(row_ids, self.seed, stream) < self.down_sample_fraction
+
+
+class DataBalancer(Splitter):
+    """Rebalance a binary label: minority up-sampled (with replacement) and majority down-sampled so the
+    minority fraction reaches ``sample_fraction`` and the total stays <= ``max_training_sample``."""
+
+    def __init__(self, sample_fraction: float = 0.1, **kw):
+        super().__init__(**kw)
+        self.sample_fraction = sample_fraction
+        self.up_fraction = 1.0
+        self.already_balanced = False
+        self.positive_is_small = True
+
+    def pre_validation_prepare(self, y, n_total=None):
+        pos = float((y > 0.5).sum())
+        neg = float((y <= 0.5).sum())
+        small, big = (pos, neg) if pos < neg else (neg, pos)
+        self.positive_is_small = pos < neg
+        total = small + big
+        f = self.sample_fraction
+        mx = self.max_training_sample
+        if small / max(total, 1) >= f:
+            self.already_balanced = True
+            self.down_sample_fraction = min(mx / max(total, 1), 1.0)
+            self.up_fraction = 1.0
+        else:
+            # getProportions (DataBalancer.scala:84-122)
+            def fits(mult):
+                return mult * small * (1 - f) < f * big and mx * f > small * mult
+            if small < mx * f:
+                up = next((float(m) for m in (100, 50, 10, 5, 4, 3, 2) if fits(m)), 1.0)
+                down = (small * up / f - small * up) / big
+            else:
+                up = (mx * f) / small
+                down = (1 - f) * mx / big
+            self.up_fraction, self.down_sample_fraction = up, min(down, 1.0)
+        self.summary = {"className": "com.salesforce.op.stages.impl.tuning.DataBalancerSummary",
+                        "positiveLabels": int(pos), "negativeLabels": int(neg), "desiredFraction": f,
+                        "upSamplingFraction": self.up_fraction, "downSamplingFraction": self.down_sample_fraction}
+        return self.summary
+
+    def validation_prepare(self, row_ids, y, stream=7):
+        """Boolean keep-mask; up-sampling is expressed as integer weights via :meth:`weights`."""
+        return self.weights(row_ids, y, stream) > 0
+
+    def weights(self, row_ids, y, stream=7) -> torch.Tensor:
+        u = row_uniform(row_ids, self.seed, stream)
+        if self.already_balanced:
+            return (u < self.down_sample_fraction).to(torch.int64)
+        small_mask = (y > 0.5) if self.positive_is_small else (y <= 0.5)
+        big_keep = (u < self.down_sample_fraction).to(torch.int64)
+        # Poisson(up) for the minority class via inverse CDF on the same uniform stream
+        lam = self.up_fraction
+        u2 = row_uniform(row_ids, self.seed, stream + 101)
+        k = torch.zeros_like(u2, dtype=torch.int64)
+        p = torch.exp(torch.tensor(-lam, dtype=torch.float64))
+        cdf = p.clone()
+        pk = p.clone()
+        for i in range(1, 64):
+            k += (u2 >= cdf).to(torch.int64)
+            pk = pk * lam / i
+            cdf = cdf + pk
+        return torch.where(small_mask, k, big_keep)
+
+    def params(self):
+        d = super().params()
+        d["sampleFraction"] = self.sample_fraction
+        return d
+
+
+class DataCutter(Splitter):
+    """Multiclass preparation: keep the most frequent labels (<= ``max_label_categories``, each with
+    fraction >= ``min_label_fraction``) and down-sample to ``max_training_sample``."""
+
+    def __init__(self, max_label_categories: int = 100, min_label_fraction: float = 0.0, **kw):
+        super().__init__(**kw)
+        self.max_label_categories = max_label_categories
+        self.min_label_fraction = min_label_fraction
+        self.labels_kept = None
+
+    def pre_validation_prepare(self, y, n_total=None):
+        vals, cnt = torch.unique(y.to(torch.float64), return_counts=True)
+        tot = float(cnt.sum())
+        order = sorted(zip(vals.tolist(), cnt.tolist()), key=lambda vc: (-vc[1], vc[0]))
+        kept = [v for v, c in order if c / tot >= self.min_label_fraction][:self.max_label_categories]
+        dropped = [v for v, _ in order if v not in set(kept)]
+        self.labels_kept = sorted(kept)
+        n_kept = sum(c for v, c in order if v in set(kept))
+        self.down_sample_fraction = min(self.max_training_sample / max(n_kept, 1), 1.0)
+        self.summary = {"className": "com.salesforce.op.stages.impl.tuning.DataCutterSummary",
+                        "preSplitterDataCount": int(tot), "downSamplingFraction": self.down_sample_fraction,
+                        "labelsKept": self.labels_kept, "labelsDropped": sorted(dropped),
+                        "labelsDroppedTotal": int(tot - n_kept)}
+        return self.summary
+
+    def validation_prepare(self, row_ids, y, stream=7):
+        keep = torch.isin(y.to(torch.float64), torch.as_tensor(self.labels_kept, dtype=torch.float64, device=y.device))
+        if self.down_sample_fraction < 1.0:
+            keep &= row_uniform(row_ids, self.seed, stream) < self.down_sample_fraction
+        return keep
+
+    def params(self):
+        d = super().params()
+        d.update(maxLabelCategories=self.max_label_categories, minLabelFraction=self.min_label_fraction)
+        return d

@@ -1,0 +1,228 @@
+"""Cross-validation and train/validation split over (learner x grid) candidates.
+
+Reference: ``OpValidator`` (``core/.../stages/impl/tuning/OpValidator.scala:94-380``; Future pool over grid
+points, failures dropped, ``maxWait``), ``OpCrossValidation`` (``OpCrossValidation.scala:63-202``: k folds
+via ``MLUtils.kFold``, optional stratification, per-grid metric averaged over folds, best grid per
+estimator, best estimator overall) and ``OpTrainValidationSplit`` (``OpTrainValidationSplit.scala:35-143``).
+
+MI355X execution model: instead of a thread pool of Spark jobs, every learner trains *all* of its
+(grid point x fold) models in one batched device program (``Learner.fit_batch``), then scores all
+of them on their validation folds in one traversal / GEMM (``Learner.predict_batch``). With several
+ranks (one per GPU) the (learner, grid, fold) jobs are sharded across ranks by estimated cost
+(LPT) over a replicated training table -- no per-iteration collectives -- and only the metrics are
+exchanged (one ``all_gather_object``).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..models.base import FitJob, learner_class
+from ..parallel import dist as D
+from .splitters import Splitter, row_uniform
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class ModelEvaluation:
+    model_uid: str
+    model_name: str
+    model_type: str
+    metric_values: Dict[str, float]
+    model_parameters: Dict[str, Any]
+
+    def to_json(self):
+        return {"modelUID": self.model_uid, "modelName": self.model_name, "modelType": self.model_type,
+                "metricValues": self.metric_values, "modelParameters": self.model_parameters}
+
+
+@dataclass
+class ValidationResult:
+    best_learner: str
+    best_params: Dict[str, Any]
+    best_metric: float
+    evaluations: List[ModelEvaluation]
+    failures: List[str] = field(default_factory=list)
+    timings: Dict[str, float] = field(default_factory=dict)
+
+
+def _job_cost(learner: str, params: Dict, n: int, d: int) -> float:
+    if "LogisticRegression" in learner or "SVC" in learner or "LinearRegression" in learner:
+        return 2.0 * n * d * params.get("max_iter", 100) * 0.05
+    depth = params.get("max_depth", 5)
+    if "RandomForest" in learner:
+        k = math.sqrt(d)
+        return params.get("num_trees", 20) * n * depth * k
+    if "GBT" in learner:
+        return params.get("max_iter", 20) * n * depth * d * 0.5
+    if "XGBoost" in learner:
+        return params.get("num_round", 100) * n * params.get("max_depth", 6) * d * 0.5
+    if "DecisionTree" in learner:
+        return n * depth * d
+    return float(n * d)
+
+
+class OpValidator:
+    validation_type = "CrossValidation"
+
+    def __init__(self, evaluator, seed: Optional[int] = None, stratify: bool = False, parallelism: int = 8,
+                 max_wait: float = 86400.0, is_classification: bool = True):
+        self.evaluator = evaluator
+        self.seed = int(np.random.randint(0, 2 ** 31 - 1)) if seed is None else int(seed)
+        self.stratify = stratify
+        self.parallelism = parallelism
+        self.max_wait = max_wait
+        self.is_classification = is_classification
+
+    # -- splits ---------------------------------------------------------------------------------
+    def make_splits(self, row_ids: torch.Tensor, y: torch.Tensor) -> List[Tuple[torch.Tensor, torch.Tensor]]:
+        raise NotImplementedError
+
+    def params(self) -> Dict[str, Any]:
+        raise NotImplementedError
+
+    # -- validation -----------------------------------------------------------------------------
+    def validate(self, models: Sequence[Tuple[str, Sequence[Dict]]], X: torch.Tensor, y: torch.Tensor,
+                 row_ids: torch.Tensor, splitter: Optional[Splitter] = None, context=None) -> ValidationResult:
+        t0 = time.time()
+        splits = self.make_splits(row_ids, y)
+        train_rows, val_rows = [], []
+        for k, (tr, va) in enumerate(splits):
+            keep = tr
+            weights = None
+            if splitter is not None:
+                if hasattr(splitter, "weights"):
+                    w = splitter.weights(row_ids, y, stream=11 + k)
+                    keep = tr & (w > 0)
+                    weights = w
+                else:
+                    keep = tr & splitter.validation_prepare(row_ids, y, stream=11 + k)
+            idx = torch.nonzero(keep).reshape(-1)
+            train_rows.append((idx, None if weights is None else weights[idx]))
+            val_rows.append(torch.nonzero(va).reshape(-1))
+        # all (learner, grid, fold) jobs
+        jobs = []
+        for li, (lname, grid) in enumerate(models):
+            for gi, p in enumerate(grid):
+                for k in range(len(splits)):
+                    jobs.append((li, gi, k))
+        n_tr = max(1, int(train_rows[0][0].numel())) if train_rows else 1
+        costs = [_job_cost(models[li][0], models[li][1][gi], n_tr, X.shape[1]) for li, gi, k in jobs]
+        owner = D.lpt_assign(costs, D.world())
+        me = D.rank()
+        ctx = context if context is not None else {}
+        results: Dict[Tuple[int, int, int], float] = {}
+        failures = []
+        timings = {}
+        for li, (lname, grid) in enumerate(models):
+            mine = [(j, (l, g, k)) for j, (l, g, k) in enumerate(jobs) if l == li and owner[j] == me]
+            if not mine:
+                continue
+            t1 = time.time()
+            learner = learner_class(lname)()
+            fjobs = [FitJob(dict(learner.defaults, **grid[g]), train_rows[k][0], train_rows[k][1])
+                     for _, (_, g, k) in mine]
+            try:
+                states = learner.fit_batch(X, y, fjobs, context=ctx)
+                preds = learner.predict_batch(states, X, [val_rows[k] for _, (_, g, k) in mine], context=ctx)
+                for (j, (l, g, k)), (pred, raw, prob) in zip(mine, preds):
+                    yv = y[val_rows[k]]
+                    results[(l, g, k)] = float(self.evaluator.selection_metric(yv, pred, raw, prob))
+            except Exception as e:  # failed models are dropped, as in OpValidator.getSummary
+                log.warning("Model %s failed in model selector: %r", lname, e)
+                failures.append(f"{lname}: {e!r}")
+            timings[lname] = time.time() - t1
+        # exchange metrics between ranks
+        gathered = D.all_gather_object((results, failures, timings))
+        allres: Dict[Tuple[int, int, int], float] = {}
+        allfail: List[str] = []
+        for r, f, tm in gathered:
+            allres.update(r)
+            allfail.extend(f)
+            for k, v in tm.items():
+                timings[k] = max(timings.get(k, 0.0), v)
+        return self._select(models, allres, len(splits), allfail, timings, t0)
+
+    def _select(self, models, results, n_folds, failures, timings, t0) -> ValidationResult:
+        larger = self.evaluator.is_larger_better
+        evals: List[ModelEvaluation] = []
+        best = None
+        for li, (lname, grid) in enumerate(models):
+            # grids evaluated on the max number of folds (OpCrossValidation.findBestModel)
+            per = {}
+            for gi in range(len(grid)):
+                ms = [results[(li, gi, k)] for k in range(n_folds) if (li, gi, k) in results]
+                if ms:
+                    per[gi] = ms
+            if not per:
+                continue
+            max_f = max(len(v) for v in per.values())
+            for gi, ms in per.items():
+                if len(ms) != max_f:
+                    continue
+                m = float(np.nansum(ms) / max_f)
+                evals.append(ModelEvaluation(f"{lname}_{li:03d}", lname, lname,
+                                             {self.evaluator.metric: m}, dict(grid[gi])))
+                better = best is None or (m > best[2] if larger else m < best[2])
+                if better and not math.isnan(m):
+                    best = (lname, dict(grid[gi]), m)
+        if best is None:
+            raise RuntimeError("All models failed model selector! Models tried were: " +
+                               ", ".join(f"{m[0]} -> {len(m[1])} grid points" for m in models) +
+                               (f"; failures: {failures}" if failures else ""))
+        timings["total"] = time.time() - t0
+        return ValidationResult(best[0], best[1], best[2], evals, failures, timings)
+
+
+class OpCrossValidation(OpValidator):
+    validation_type = "CrossValidation"
+
+    def __init__(self, num_folds: int = 3, **kw):
+        super().__init__(**kw)
+        if num_folds < 2:
+            raise ValueError("numFolds must be >= 2")
+        self.num_folds = num_folds
+
+    def make_splits(self, row_ids, y):
+        u = row_uniform(row_ids, self.seed, 2)
+        if self.stratify and self.is_classification:
+            fold = torch.empty(row_ids.shape[0], dtype=torch.int64, device=row_ids.device)
+            for c in torch.unique(y):
+                m = y == c
+                # per class, rank the uniforms and deal folds round-robin (balanced per class)
+                idx = torch.nonzero(m).reshape(-1)
+                order = torch.argsort(u[idx])
+                f = torch.empty_like(order)
+                f[order] = torch.arange(order.numel(), device=order.device) % self.num_folds
+                fold[idx] = f
+        else:
+            fold = torch.clamp((u * self.num_folds).to(torch.int64), max=self.num_folds - 1)
+        return [(fold != k, fold == k) for k in range(self.num_folds)]
+
+    def params(self):
+        return {"numFolds": self.num_folds, "seed": self.seed, "evaluator": self.evaluator.metric,
+                "stratify": self.stratify, "parallelism": self.parallelism}
+
+
+class OpTrainValidationSplit(OpValidator):
+    validation_type = "TrainValidationSplit"
+
+    def __init__(self, train_ratio: float = 0.75, **kw):
+        super().__init__(**kw)
+        self.train_ratio = train_ratio
+
+    def make_splits(self, row_ids, y):
+        u = row_uniform(row_ids, self.seed, 3)
+        tr = u < self.train_ratio
+        return [(tr, ~tr)]
+
+    def params(self):
+        return {"trainRatio": self.train_ratio, "seed": self.seed, "evaluator": self.evaluator.metric,
+                "stratify": self.stratify, "parallelism": self.parallelism}

@@ -1,0 +1,169 @@
+"""Text utilities: cleaning, tokenization and Spark-compatible murmur3 hashing.
+
+* :func:`clean_string` -- ``TextUtils.cleanString`` (``utils/.../text/TextUtils.scala:39-46``).
+* :func:`tokenize` -- ``TextTokenizer.tokenizeString`` (``core/.../TextTokenizer.scala:160-188``) with the
+  default analyzer ``StandardAnalyzer(english snowball stopwords)``
+  (``core/.../utils/text/LuceneTextAnalyzer.scala:160-166``): a UAX#29-style word tokenizer
+  (letters/digits/underscore words, ``'`` and ``.`` joining letters, ``.`` and ``,`` joining digits),
+  lowercasing and stopword removal, max token length 255.
+* :func:`hash_terms` -- bit-exact Spark ``HashingTF`` murmur3 indices (native host library).
+"""
+from __future__ import annotations
+
+import re
+from typing import Iterable, List, Optional, Sequence
+from urllib.parse import urlparse
+
+import numpy as np
+
+_PUNCT = re.compile(r"[!\"#$%&'()*+,\-./:;<=>?@\[\\\]^_`{|}~]")
+_SPACES = re.compile(" +")
+
+
+def clean_string(raw: str, split_on: str = " ") -> str:
+    s = raw.lower()
+    s = _PUNCT.sub(split_on, s)
+    s = re.sub(re.escape(split_on) + "+", split_on, s)
+    parts = s.split(split_on)
+    # Java's String.split drops trailing empty strings; capitalize() of "" is ""
+    return "".join(p[:1].upper() + p[1:] for p in parts)
+
+
+def clean_opt(raw: Optional[str], should_clean: bool = True) -> Optional[str]:
+    if raw is None:
+        return None
+    return clean_string(raw) if should_clean else raw
+
+
+# Snowball English stop words (Lucene's english_stop.txt, used by LuceneTextAnalyzer.DefaultAnalyzer)
+ENGLISH_STOPWORDS = frozenset("""
+i me my myself we our ours ourselves you your yours yourself yourselves he him his himself she her hers
+herself it its itself they them their theirs themselves what which who whom this that these those am is
+are was were be been being have has had having do does did doing would should could ought i'm you're
+he's she's it's we're they're i've you've we've they've i'd you'd he'd she'd we'd they'd i'll you'll he'll
+she'll we'll they'll isn't aren't wasn't weren't hasn't haven't hadn't doesn't don't didn't won't wouldn't
+shan't shouldn't can't cannot couldn't mustn't let's that's who's what's here's there's when's where's
+why's how's a an the and but if or because as until while of at by for with about against between into
+through during before after above below to from up down in out on off over under again further then once
+here there when where why how all any both each few more most other some such no nor not only own same so
+than too very
+""".split())
+
+# word = runs of letters/digits/underscore, letters may be joined by ' or . , digits by . or ,
+_WORD = re.compile(
+    r"[^\W\d_](?:[\w]|['.](?=[^\W\d_]))*"          # letter-led word (may contain digits)
+    r"|\d(?:[\w]|[.,](?=\d))*"                      # number-led token
+    r"|_+\w*",
+    re.UNICODE)
+_CJK = re.compile(r"[぀-ヿ㐀-䶿一-鿿가-힯]")
+
+
+def analyze(text: str, stopwords=ENGLISH_STOPWORDS, max_len: int = 255) -> List[str]:
+    """StandardAnalyzer-style analysis (lowercase + stop filter) of an already lowercased or raw string."""
+    out = []
+    for m in _WORD.finditer(text):
+        tok = m.group(0)
+        if _CJK.search(tok):
+            out.extend(c for c in tok)
+            continue
+        tok = tok.lower()
+        if len(tok) > max_len:
+            continue
+        if tok in stopwords:
+            continue
+        out.append(tok)
+    return out
+
+
+def tokenize(text: Optional[str], to_lowercase: bool = True, min_token_length: int = 1,
+             stopwords=ENGLISH_STOPWORDS) -> List[str]:
+    if text is None:
+        return []
+    s = text.lower() if to_lowercase else text
+    return [t for t in analyze(s, stopwords) if len(t) >= min_token_length]
+
+
+def strip_html(text: str) -> str:
+    return re.sub(r"<[^>]*>", " ", text)
+
+
+def hash_terms(terms: Sequence[str], num_features: int, seed: int = 42) -> np.ndarray:
+    """``nonNegativeMod(murmur3_x86_32(utf8(term), 42), num_features)`` for every term (Spark HashingTF)."""
+    from ..ops import _native as N
+    n = len(terms)
+    if n == 0:
+        return np.zeros(0, np.int32)
+    enc = [t.encode("utf-8") for t in terms]
+    lens = np.fromiter((len(e) for e in enc), dtype=np.int64, count=n)
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    buf = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8)
+    out = np.empty(n, np.int32)
+    N.check(N.host().tmog_hash_index_batch(buf.ctypes.data, offs.ctypes.data, n, seed, num_features,
+                                            out.ctypes.data), "hash_index_batch")
+    return out
+
+
+def murmur3(terms: Sequence[str], seed: int = 42) -> np.ndarray:
+    from ..ops import _native as N
+    n = len(terms)
+    enc = [t.encode("utf-8") for t in terms]
+    lens = np.fromiter((len(e) for e in enc), dtype=np.int64, count=n)
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    buf = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8)
+    out = np.empty(n, np.int32)
+    N.check(N.host().tmog_murmur3_batch(buf.ctypes.data, offs.ctypes.data, n, seed, out.ctypes.data), "murmur3")
+    return out
+
+
+# ------------------------------------------------------------------------------ email / url helpers
+_EMAIL = re.compile(r"^[A-Za-z0-9.!#$%&'*+/=?^_`{|}~-]+@[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?"
+                    r"(?:\.[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?)+$")
+
+
+def is_valid_email(s: Optional[str]) -> bool:
+    return s is not None and bool(_EMAIL.match(s))
+
+
+def email_domain(s: Optional[str]) -> Optional[str]:
+    if s is None or s.count("@") != 1:
+        return None
+    d = s.split("@")[1]
+    return d or None
+
+
+def email_prefix(s: Optional[str]) -> Optional[str]:
+    if s is None or s.count("@") != 1:
+        return None
+    p = s.split("@")[0]
+    return p or None
+
+
+def is_valid_url(s: Optional[str], schemes=("http", "https", "ftp")) -> bool:
+    if not s:
+        return False
+    try:
+        u = urlparse(s)
+    except ValueError:
+        return False
+    return u.scheme in schemes and bool(u.netloc) and "." in u.netloc and " " not in s
+
+
+def url_domain(s: Optional[str]) -> Optional[str]:
+    if not s:
+        return None
+    try:
+        u = urlparse(s)
+    except ValueError:
+        return None
+    return u.hostname or None
+
+
+def url_protocol(s: Optional[str]) -> Optional[str]:
+    if not s:
+        return None
+    try:
+        return urlparse(s).scheme or None
+    except ValueError:
+        return None

@@ -1,0 +1,133 @@
+"""DAG computation and layer-by-layer fit / transform.
+
+Reference: ``FitStagesUtil`` (``core/.../utils/stages/FitStagesUtil.scala:51-369``): ``computeDAG`` (stages layered by
+distance, deepest first, each stage once, ``:173-198``), ``fitAndTransformDAG`` / ``fitAndTransformLayer``
+(``:212-290``: fit the estimators of a layer on train, evaluate ``HasTestEval`` models on the hold-out,
+then apply every transformer of the layer to train and test) and ``cutDAG`` (``:302-355``) for
+workflow-level CV. A layer's transformers write new device columns into the columnar dataset -- no
+row materialization.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from ..data.dataset import Dataset
+from ..stages.base import OpEstimator, OpTransformer
+
+log = logging.getLogger(__name__)
+
+Layer = List[Tuple[object, int]]
+
+
+def compute_dag(features) -> List[Layer]:
+    by_dist: Dict[int, list] = {}
+    for f in features:
+        for st, d in f.parent_stages().items():
+            by_dist.setdefault(d, []).append((st, d))
+    layers = []
+    seen = set()
+    for d in sorted(by_dist, reverse=True):
+        layer = []
+        for st, dd in sorted(by_dist[d], key=lambda sd: sd[0].get_output_feature_name()):
+            if id(st) in seen:
+                continue
+            seen.add(id(st))
+            layer.append((st, dd))
+        if layer:
+            layers.append(layer)
+    return layers
+
+
+def fit_and_transform_layer(layer: Layer, train: Dataset, test: Optional[Dataset], timings: Optional[dict] = None):
+    fitted = []
+    for st, _ in layer:
+        t0 = time.time()
+        if isinstance(st, OpEstimator):
+            m = st.fit(train)
+            if test is not None and len(test) > 0 and hasattr(m, "evaluate_model"):
+                test_in = test
+                m.evaluate_model(test_in)
+            fitted.append(m)
+        else:
+            fitted.append(st)
+        if timings is not None:
+            timings[f"fit:{st.stage_name()}"] = time.time() - t0
+    for m in fitted:
+        t0 = time.time()
+        train = m.transform(train)
+        if test is not None and len(test) > 0:
+            test = m.transform(test)
+        if timings is not None:
+            timings[f"transform:{m.stage_name()}"] = time.time() - t0
+    return train, test, fitted
+
+
+def fit_and_transform_dag(dag: Sequence[Layer], train: Dataset, test: Optional[Dataset] = None,
+                          timings: Optional[dict] = None):
+    fitted_all = []
+    for layer in dag:
+        # a hold-out must be transformed before a HasTestEval model of the next layer evaluates on it
+        train, test, fitted = _fit_layer_with_eval(layer, train, test, timings)
+        fitted_all.extend(fitted)
+    return train, test, fitted_all
+
+
+def _fit_layer_with_eval(layer, train, test, timings):
+    fitted = []
+    for st, _ in layer:
+        t0 = time.time()
+        if isinstance(st, OpEstimator):
+            m = st.fit(train)
+            if test is not None and len(test) > 0 and hasattr(m, "evaluate_model"):
+                m.evaluate_model(test)
+            fitted.append(m)
+        else:
+            fitted.append(st)
+        if timings is not None:
+            timings[f"fit:{st.stage_name()}"] = time.time() - t0
+    for m in fitted:
+        t0 = time.time()
+        train = m.transform(train)
+        if test is not None and len(test) > 0:
+            test = m.transform(test)
+        if timings is not None:
+            timings[f"transform:{m.stage_name()}"] = time.time() - t0
+    return train, test, fitted
+
+
+def apply_transformations_dag(data: Dataset, dag: Sequence[Layer]) -> Dataset:
+    """Score path: apply already-fitted transformers layer by layer (``OpWorkflowCore.scala:324-348``)."""
+    for layer in dag:
+        for st, _ in layer:
+            if isinstance(st, OpEstimator):
+                raise ValueError(f"stage {st.uid} is not fitted")
+            data = st.transform(data)
+    return data
+
+
+def cut_dag(dag: Sequence[Layer]):
+    """Split a DAG around its model selector for workflow-level CV (``FitStagesUtil.cutDAG``)."""
+    from ..selector.model_selector import ModelSelector
+    sels = [(st, d) for layer in dag for st, d in layer if isinstance(st, ModelSelector)]
+    if not sels:
+        return None, list(dag), [], []
+    if len(sels) > 1:
+        raise ValueError(f"OpWorkflow can contain at most 1 Model Selector. Found {len(sels)}")
+    ms, dist = sels[0]
+    after = [layer for layer in dag if any(d < dist for _, d in layer)]
+    before = [layer for layer in dag if not any(d < dist for _, d in layer)]
+    ms_dag = compute_dag([ms.get_output()])[:-1]
+    ms_dag = [[(st, d + len(after)) for st, d in layer] for layer in ms_dag]
+    non_ms = [[(st, d) for st, d in layer if st is not ms] for layer in before]
+    non_ms = [l for l in non_ms if l]
+    first = next((i for i, layer in enumerate(ms_dag)
+                  if any(any(t.is_response for t in st.get_input_features()) and
+                         any(not t.is_response for t in st.get_input_features()) for st, _ in layer)), -1)
+    if first == -1:
+        return ms, non_ms, [], after
+    during = ms_dag[first:]
+    flat = {id(st) for layer in during for st, _ in layer}
+    before2 = [[(st, d) for st, d in layer if id(st) not in flat] for layer in non_ms]
+    return ms, [l for l in before2 if l], during, after

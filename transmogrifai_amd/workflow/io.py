@@ -1,0 +1,206 @@
+"""Model checkpoint writer / reader: the ``op-model.json`` format.
+
+Reference: ``OpWorkflowModelWriter`` (``core/.../OpWorkflowModelWriter.scala:58-183``: fields uid,
+resultFeaturesUids, blocklisted*, stages, allFeatures, parameters, trainParameters,
+rawFeatureFilterResults; written gzip-compressed as ``op-model.json/part-00000.gz``), the stage writer
+(``features/.../stages/OpPipelineStageWriter.scala:67-88``: class, uid, paramMap, ctorArgs) and
+``OpWorkflowModelReader`` (``OpWorkflowModelReader.scala:97-266``: falls back through ``part-00000.gz``,
+``part-00000`` and the raw path; accepts the legacy ``blacklisted*`` field names). Learned tensors are
+stored inline as base64 arrays (:mod:`transmogrifai_amd.utils.serde`); nothing is unpickled on load.
+"""
+from __future__ import annotations
+
+import gzip
+import json
+import os
+import shutil
+import time
+from typing import Dict, List, Optional
+
+from ..data.vector_metadata import OpVectorMetadata
+from ..features import types as T
+from ..features.feature import FeatureLike, TransientFeature
+from ..stages.base import OpPipelineStage, stage_class
+from ..stages.generator import FeatureGeneratorStage
+from ..utils.serde import decode, encode
+from .params import OpParams
+
+MODEL_DIR = "op-model.json"
+PART = "part-00000"
+
+
+def _meta_to_json(meta: Dict) -> Dict:
+    out = {}
+    for k, v in meta.items():
+        if isinstance(v, OpVectorMetadata):
+            out[k] = {"__vector_metadata__": v.name, **v.to_json()}
+        else:
+            out[k] = encode(v)
+    return out
+
+
+def _meta_from_json(d: Dict) -> Dict:
+    out = {}
+    for k, v in (d or {}).items():
+        if isinstance(v, dict) and "__vector_metadata__" in v:
+            out[k] = OpVectorMetadata.from_json(v["__vector_metadata__"], v)
+        else:
+            out[k] = decode(v)
+    return out
+
+
+def stage_to_json(st: OpPipelineStage) -> Dict:
+    params = {k: encode(v) for k, v in st.params.items()}
+    params["inputFeatures"] = [t.to_json() for t in st.get_transient_features()] if st._inputs else []
+    params["outputFeatureName"] = st.get_output_feature_name() if (st._inputs or isinstance(
+        st, FeatureGeneratorStage)) else None
+    params["outputMetadata"] = _meta_to_json(st.metadata)
+    return {"class": f"{type(st).__module__}.{type(st).__qualname__}", "uid": st.uid,
+            "operationName": st.operation_name, "outputType": st.output_type.type_name(),
+            "timestamp": int(time.time() * 1000), "paramMap": params, "defaultParamMap": {},
+            "ctorArgs": encode(st.ctor_args())}
+
+
+def model_to_json(model) -> Dict:
+    gens = {}
+    for f in model.raw_features:
+        gens[f.origin_stage.uid] = f.origin_stage
+    stages = [stage_to_json(s) for s in gens.values()] + [stage_to_json(s) for s in model.stages]
+    feats = {}
+    for f in model.result_features:
+        for x in f.traverse():
+            feats[x.uid] = x
+    all_features = []
+    for x in feats.values():
+        j = x.to_json()
+        j.pop("distributions", None)
+        all_features.append(j)
+    rff = model.raw_feature_filter_results
+    return {
+        "uid": model.uid,
+        "resultFeaturesUids": [f.uid for f in model.result_features],
+        "blocklistedFeaturesUids": [f.uid for f in model.blocklist],
+        "blocklistedMapKeys": model.blocklist_map_keys,
+        "blocklistedStages": [],
+        "stages": stages,
+        "allFeatures": all_features,
+        "parameters": model.parameters.to_string(),
+        "trainParameters": model.train_parameters.to_string(),
+        "rawFeatureFilterResults": json.dumps(encode(rff.to_json() if hasattr(rff, "to_json") else (rff or {}))),
+        "trainTimings": encode(getattr(model, "train_timings", {})),
+    }
+
+
+def save_model(model, path: str, overwrite: bool = True) -> None:
+    d = os.path.join(path, MODEL_DIR)
+    if os.path.exists(path):
+        if not overwrite:
+            raise FileExistsError(path)
+        if os.path.isdir(d):
+            shutil.rmtree(d)
+    os.makedirs(d, exist_ok=True)
+    data = json.dumps(model_to_json(model), default=str).encode("utf-8")
+    with gzip.open(os.path.join(d, PART + ".gz"), "wb") as f:
+        f.write(data)
+
+
+def _read_text(path: str) -> str:
+    cands = [os.path.join(path, MODEL_DIR, PART + ".gz"), os.path.join(path, MODEL_DIR, PART),
+             os.path.join(path, PART + ".gz"), os.path.join(path, PART), path]
+    for c in cands:
+        if os.path.isfile(c):
+            if c.endswith(".gz"):
+                with gzip.open(c, "rb") as f:
+                    return f.read().decode("utf-8")
+            with open(c) as f:
+                return f.read()
+    raise FileNotFoundError(f"no model found at {path}")
+
+
+def _build_stage(sj: Dict) -> OpPipelineStage:
+    cls = stage_class(sj["class"])
+    pm = sj.get("paramMap", {})
+    args = decode(sj.get("ctorArgs", {}))
+    if cls is FeatureGeneratorStage:
+        st = FeatureGeneratorStage(args.get("outputName") or pm.get("outputFeatureName"),
+                                   T.feature_type_from_name(args.get("tto", sj.get("outputType", "Text"))),
+                                   None, None, args.get("aggregateWindow"), bool(args.get("outputIsResponse")),
+                                   args.get("extractSource"), uid=sj["uid"],
+                                   column=(args.get("extractFn") or {}).get("column"))
+        return st
+    from .. import uid as _uid
+    c0 = _uid.count()
+    try:
+        st = cls()
+    except TypeError:
+        st = cls.__new__(cls)
+        OpPipelineStage.__init__(st, uid=sj["uid"])
+    _uid.reset(c0)
+    st.uid = sj["uid"]
+    st.operation_name = sj.get("operationName", st.operation_name)
+    if sj.get("outputType"):
+        st.output_type = T.feature_type_from_name(sj["outputType"])
+    for k, v in pm.items():
+        if k in ("inputFeatures", "outputFeatureName", "outputMetadata"):
+            continue
+        st.params[k] = decode(v)
+    st.metadata = _meta_from_json(pm.get("outputMetadata", {}))
+    st._output_name = pm.get("outputFeatureName")
+    st.load_ctor_args(args)
+    return st
+
+
+def load_model(path: str, workflow=None):
+    from .workflow import OpWorkflowModel
+    j = json.loads(_read_text(path))
+    stages_j = j["stages"]
+    by_uid: Dict[str, OpPipelineStage] = {}
+    order: List[OpPipelineStage] = []
+    for sj in stages_j:
+        st = _build_stage(sj)
+        by_uid[st.uid] = st
+        order.append(st)
+    # features
+    fjs = {f["uid"]: f for f in j["allFeatures"]}
+    built: Dict[str, FeatureLike] = {}
+
+    def build(uid):
+        if uid in built:
+            return built[uid]
+        fj = fjs[uid]
+        parents = [build(p) for p in fj.get("parents", [])]
+        st = by_uid.get(fj.get("originStage"))
+        f = FeatureLike(fj["name"], T.feature_type_from_name(fj["typeName"]), fj.get("isResponse", False), st,
+                        parents, uid=fj["uid"])
+        built[uid] = f
+        return f
+
+    for u in fjs:
+        build(u)
+    # wire stage inputs / outputs
+    for sj in stages_j:
+        st = by_uid[sj["uid"]]
+        ins = sj.get("paramMap", {}).get("inputFeatures", [])
+        if ins:
+            st._inputs = [built[t["uid"]] for t in ins]
+            st._transient = [TransientFeature.from_json(t) for t in ins]
+        out = next((f for f in built.values() if f.origin_stage is st), None)
+        if out is not None:
+            st._output = out
+    gens = [s for s in order if isinstance(s, FeatureGeneratorStage)]
+    fitted = [s for s in order if not isinstance(s, FeatureGeneratorStage)]
+    model = OpWorkflowModel(j.get("uid"), OpParams.from_string(j.get("parameters", "{}")))
+    model.train_parameters = OpParams.from_string(j.get("trainParameters", "{}"))
+    model.stages = fitted
+    model.result_features = [built[u] for u in j["resultFeaturesUids"]]
+    model.raw_features = sorted([built[f.uid] for f in built.values() if f.is_raw and f.origin_stage in gens],
+                                key=lambda f: f.name)
+    bl = j.get("blocklistedFeaturesUids", j.get("blacklistedFeaturesUids", []))
+    model.blocklist = [built[u] for u in bl if u in built]
+    model.blocklist_map_keys = j.get("blocklistedMapKeys", j.get("blacklistedMapKeys", {}))
+    rff = j.get("rawFeatureFilterResults")
+    model.raw_feature_filter_results = decode(json.loads(rff)) if isinstance(rff, str) and rff else rff
+    model.train_timings = decode(j.get("trainTimings", {}))
+    if workflow is not None:
+        model.reader = workflow.reader
+    return model

@@ -1,0 +1,324 @@
+"""``OpWorkflow`` (train) and ``OpWorkflowModel`` (score / evaluate / summarize / save / load).
+
+Reference: ``OpWorkflowCore`` (``core/.../OpWorkflowCore.scala:53-361``), ``OpWorkflow`` (``OpWorkflow.scala:61-592``:
+``setResultFeatures:90-110``, parameter injection ``:179-201``, validation ``:331-338``, ``train:347-365``,
+``fitStages:376-455``, ``withRawFeatureFilter:537-578``) and ``OpWorkflowModel`` (``OpWorkflowModel.scala:60-473``:
+``score:259-273``, ``scoreAndEvaluate:296-314``, ``summaryJson/summary/summaryPretty:187-215``,
+``modelInsights:167-180``, ``save:223-225``, ``load:470-471``).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import time
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ..data.dataset import Dataset
+from ..features.feature import FeatureLike
+from ..stages.base import OpEstimator, OpPipelineStage
+from ..stages.generator import FeatureGeneratorStage
+from ..uid import make_uid
+from .dag import apply_transformations_dag, compute_dag, cut_dag, fit_and_transform_dag
+from .params import OpParams
+
+log = logging.getLogger(__name__)
+
+
+class OpStep:
+    """Job-phase labels (``utils/.../spark/OpStep.scala:35-46``) used for run metrics."""
+    DataReadingAndFiltering = "DataReadingAndFiltering"
+    FeatureEngineering = "FeatureEngineering"
+    CrossValidation = "CrossValidation"
+    ModelIO = "ModelIO"
+    Scoring = "Scoring"
+    ResultsSaving = "ResultsSaving"
+
+
+class _Timer:
+    def __init__(self, sink: Dict[str, float], name: str):
+        self.sink, self.name = sink, name
+
+    def __enter__(self):
+        self.t = time.time()
+
+    def __exit__(self, *a):
+        self.sink[self.name] = self.sink.get(self.name, 0.0) + time.time() - self.t
+
+
+class OpWorkflowCore:
+    def __init__(self, uid: Optional[str] = None):
+        self.uid = uid or make_uid("OpWorkflow")
+        self.result_features: List[FeatureLike] = []
+        self.raw_features: List[FeatureLike] = []
+        self.blocklist: List[FeatureLike] = []
+        self.blocklist_map_keys: Dict[str, List[str]] = {}
+        self.stages: List[OpPipelineStage] = []
+        self.parameters = OpParams()
+        self.reader = None
+        self.input_dataset = None
+        self.raw_feature_filter_results = None
+        self.workflow_cv = False
+        self.timings: Dict[str, float] = {}
+
+    def set_reader(self, reader):
+        self.reader = reader
+        return self
+
+    def set_input_dataset(self, data, key=None):
+        """Records, a pandas DataFrame or a columnar :class:`Dataset` (``setInputDataset``)."""
+        from ..readers.base import InMemoryReader
+        self.reader = InMemoryReader(data, key)
+        return self
+
+    set_input_rdd = set_input_dataset
+
+    def with_workflow_cv(self):
+        self.workflow_cv = True
+        return self
+
+    def get_parameters(self) -> OpParams:
+        return self.parameters
+
+    def generate_raw_data(self, params: Optional[OpParams] = None) -> Dataset:
+        if self.reader is None:
+            raise ValueError("Data reader must be set (set_reader or set_input_dataset)")
+        rp = None
+        if params is not None and params.reader_params:
+            rp = next(iter(params.reader_params.values()))
+        raws = [f for f in self.raw_features if f not in self.blocklist]
+        ds = self.reader.generate_dataset(raws, rp)
+        return ds
+
+
+class OpWorkflow(OpWorkflowCore):
+    def set_result_features(self, *features) -> "OpWorkflow":
+        fs = []
+        for f in features:
+            fs.extend(f if isinstance(f, (list, tuple)) else [f])
+        self.result_features = fs
+        dag = compute_dag(fs)
+        self.stages = [st for layer in dag for st, _ in layer]
+        raws = {}
+        for f in fs:
+            for r in f.raw_features():
+                raws[r.uid] = r
+        self.raw_features = sorted(raws.values(), key=lambda f: f.name)
+        self._validate_stages()
+        return self
+
+    def _validate_stages(self):
+        uids = [s.uid for s in self.stages]
+        if len(uids) != len(set(uids)):
+            dup = sorted({u for u in uids if uids.count(u) > 1})
+            raise ValueError(f"Duplicate stage uids in workflow: {dup}")
+
+    def set_parameters(self, params: OpParams) -> "OpWorkflow":
+        """Inject ``stageParams`` by stage class simple name or uid (``OpWorkflow.scala:179-201``)."""
+        self.parameters = params
+        for st in self.stages:
+            for key in (type(st).__name__, st.uid):
+                for k, v in (params.stage_params.get(key) or {}).items():
+                    name = _snake(k)
+                    if name in st.params or st._accepts_param(name):
+                        st.set(name, v)
+                    elif hasattr(st, name):
+                        setattr(st, name, v)
+                    else:
+                        raise ValueError(f"stage {st.uid} has no param '{k}'")
+        return self
+
+    def with_raw_feature_filter(self, training_reader=None, scoring_reader=None, **kw) -> "OpWorkflow":
+        from ..filters.raw_feature_filter import RawFeatureFilter
+        self.rff = RawFeatureFilter(training_reader or self.reader, scoring_reader, **kw)
+        return self
+
+    def train(self, params: Optional[OpParams] = None) -> "OpWorkflowModel":
+        timings: Dict[str, float] = {}
+        t0 = time.time()
+        with _Timer(timings, OpStep.DataReadingAndFiltering):
+            raw = self.generate_raw_data(params or self.parameters)
+            if getattr(self, "rff", None) is not None:
+                raw, blocked, results = self.rff.filter(raw, self.raw_features, self.result_features)
+                self.blocklist = blocked
+                self.raw_feature_filter_results = results
+        fitted = self.fit_stages(raw, timings)
+        model = OpWorkflowModel(self.uid, self.parameters)
+        model.stages = fitted
+        model.result_features = list(self.result_features)
+        model.raw_features = list(self.raw_features)
+        model.blocklist = list(self.blocklist)
+        model.blocklist_map_keys = dict(self.blocklist_map_keys)
+        model.raw_feature_filter_results = self.raw_feature_filter_results
+        model.reader = self.reader
+        model.train_parameters = self.parameters
+        timings["total"] = time.time() - t0
+        model.train_timings = timings
+        return model
+
+    def _holdout_split(self, data: Dataset):
+        from ..selector.model_selector import ModelSelector
+        sps = [s.splitter for s in self.stages if isinstance(s, ModelSelector) and s.splitter is not None]
+        if not sps:
+            return data, None
+        sp = max(sps, key=lambda s: s.reserve_test_fraction)
+        if sp.reserve_test_fraction <= 0:
+            return data, None
+        tr, te = sp.split(data.row_ids)
+        ti = torch.nonzero(tr).reshape(-1)
+        hi = torch.nonzero(te).reshape(-1)
+        return data.take(ti), data.take(hi)
+
+    def fit_stages(self, data: Dataset, timings: Dict[str, float]) -> List[OpPipelineStage]:
+        with _Timer(timings, "HoldoutSplit"):
+            train, test = self._holdout_split(data)
+        dag = [[(st, d) for st, d in layer if st in self.stages] for layer in compute_dag(self.result_features)]
+        dag = [l for l in dag if l]
+        stage_t: Dict[str, float] = {}
+        if not self.workflow_cv:
+            with _Timer(timings, OpStep.FeatureEngineering):
+                _, _, fitted = fit_and_transform_dag(dag, train, test, stage_t)
+        else:
+            ms, before, during, after = cut_dag(dag)
+            with _Timer(timings, OpStep.FeatureEngineering):
+                tr2, te2, fb = fit_and_transform_dag(before, train, test, stage_t)
+            fitted = list(fb)
+            if ms is not None:
+                with _Timer(timings, OpStep.CrossValidation):
+                    ms.during_dag = during
+                rest = list(during) + [[(ms, 0)]] + list(after)
+                with _Timer(timings, OpStep.FeatureEngineering):
+                    _, _, fr = fit_and_transform_dag(rest, tr2, te2, stage_t)
+                fitted += fr
+        timings["stages"] = stage_t
+        return fitted
+
+    def compute_data_up_to(self, feature: FeatureLike, params: Optional[OpParams] = None) -> Dataset:
+        raw = self.generate_raw_data(params or self.parameters)
+        dag = compute_dag([feature])
+        dag = [[(st, d) for st, d in layer if st is not feature.origin_stage] for layer in dag]
+        dag = [l for l in dag if l]
+        out, _, _ = fit_and_transform_dag(dag, raw, None)
+        return out
+
+    def load_model(self, path: str) -> "OpWorkflowModel":
+        from .io import load_model
+        m = load_model(path, self)
+        m.reader = self.reader
+        return m
+
+    def with_model_stages(self, model: "OpWorkflowModel") -> "OpWorkflow":
+        """Reuse fitted stages of a model (``OpWorkflow.scala:468-472``)."""
+        by_uid = {s.uid: s for s in model.stages}
+        self.stages = [by_uid.get(s.uid, s) for s in self.stages]
+        return self
+
+
+class OpWorkflowModel(OpWorkflowCore):
+    PersistEveryKStages = 5
+
+    def __init__(self, uid: Optional[str] = None, parameters: Optional[OpParams] = None):
+        super().__init__(uid)
+        self.parameters = parameters or OpParams()
+        self.train_parameters = self.parameters
+        self.train_timings: Dict[str, float] = {}
+
+    # ---------------------------------------------------------------------------------- scoring
+    def _fitted_dag(self, features: Sequence[FeatureLike]):
+        by_uid = {s.uid: s for s in self.stages}
+        dag = compute_dag(features)
+        out = []
+        for layer in dag:
+            l2 = []
+            for st, d in layer:
+                fs = by_uid.get(st.uid)
+                if fs is None:
+                    raise ValueError(f"stage {st.uid} ({type(st).__name__}) was not fitted in this model")
+                l2.append((fs, d))
+            out.append(l2)
+        return out
+
+    def transform_dataset(self, raw: Dataset, features=None) -> Dataset:
+        return apply_transformations_dag(raw, self._fitted_dag(features or self.result_features))
+
+    def score(self, data=None, keep_raw_features: bool = False, keep_intermediate_features: bool = False,
+              params: Optional[OpParams] = None) -> Dataset:
+        """Score a reader's / dataset's rows: raw -> all fitted stages -> result features."""
+        if data is not None:
+            self.set_input_dataset(data)
+        raw = self.generate_raw_data(params or self.parameters)
+        out = self.transform_dataset(raw)
+        keep = [f.name for f in self.result_features]
+        if keep_intermediate_features:
+            return out
+        if keep_raw_features:
+            keep = [f.name for f in self.raw_features if f.name in out] + keep
+        return out.select([k for k in dict.fromkeys(keep)])
+
+    def score_and_evaluate(self, evaluator, data=None, **kw):
+        scores = self.score(data, keep_raw_features=True, **kw)
+        return scores, self.evaluate_scores(evaluator, scores)
+
+    def evaluate(self, evaluator, data=None):
+        return self.score_and_evaluate(evaluator, data)[1]
+
+    def evaluate_scores(self, evaluator, scores: Dataset) -> Dict:
+        if evaluator.label_col not in scores:
+            raise ValueError(f"label column {evaluator.label_col} not in scored data")
+        return evaluator.evaluate_all(scores)
+
+    # -------------------------------------------------------------------------------- summaries
+    def model_insights(self, feature: Optional[FeatureLike] = None):
+        from ..insights.model_insights import extract_model_insights
+        feat = feature or next((f for f in self.result_features if f.wtype.__name__ == "Prediction"), None)
+        return extract_model_insights(self, feat)
+
+    def summary_json(self) -> Dict:
+        from ..selector.model_selector import ModelSelector
+        out = {}
+        for st in self.stages:
+            if "summary" in st.metadata:
+                out[st.uid] = st.metadata["summary"]
+        return out
+
+    def summary(self) -> str:
+        return json.dumps(self.summary_json(), indent=2, default=_json_default)
+
+    def summary_pretty(self) -> str:
+        from ..insights.pretty import summary_pretty
+        return summary_pretty(self)
+
+    # ------------------------------------------------------------------------------------ io
+    def save(self, path: str, overwrite: bool = True) -> None:
+        from .io import save_model
+        save_model(self, path, overwrite)
+
+    @staticmethod
+    def load(path: str, workflow: Optional[OpWorkflow] = None) -> "OpWorkflowModel":
+        from .io import load_model
+        return load_model(path, workflow)
+
+    def score_function(self):
+        """Spark-free per-record scoring function (``local/.../OpWorkflowModelLocal.scala:79-122``)."""
+        from ..local.scoring import score_function
+        return score_function(self)
+
+    def get_origin_stage_of(self, feature: FeatureLike):
+        return next(s for s in self.stages if s.uid == feature.origin_stage.uid)
+
+
+def _snake(k: str) -> str:
+    import re
+    return re.sub(r"(?<!^)(?=[A-Z])", "_", k).lower()
+
+
+def _json_default(o):
+    import numpy as np
+    if isinstance(o, (np.floating, np.integer)):
+        return o.item()
+    if isinstance(o, np.ndarray):
+        return o.tolist()
+    if isinstance(o, torch.Tensor):
+        return o.tolist()
+    return str(o)
