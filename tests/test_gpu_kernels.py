@@ -1,0 +1,70 @@
+"""HIP kernels vs plain fp64/fp32 PyTorch references, and an end-to-end workflow on the device."""
+import numpy as np
+import pytest
+import torch
+
+from transmogrifai_amd.data.columns import NumericColumn
+from transmogrifai_amd.features import types as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _native_loaded():
+    from transmogrifai_amd.ops import _native
+    return _native.hip_loaded()
+
+
+def test_col_stats_matches_fp64():
+    from transmogrifai_amd.ops import stats as ST
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(100_003, 37, generator=g) * 3 + 1
+    X[:, 5] = 0
+    X[::7, 9] = 0
+    ref = ST.col_stats(X.to(torch.float64))
+    got = ST.col_stats(X.cuda())
+    for k in ("mean", "variance", "min", "max", "numNonzeros"):
+        torch.testing.assert_close(got[k].cpu(), ref[k], rtol=1e-6, atol=1e-6)
+    assert _native_loaded()
+
+
+def test_vectorize_numeric_matches_host():
+    from transmogrifai_amd.ops import vector as V
+    g = torch.Generator().manual_seed(1)
+    n = 50_001
+    cols_h, cols_d = [], []
+    for j in range(5):
+        v = torch.randn(n, generator=g, dtype=torch.float64)
+        ok = torch.rand(n, generator=g) > 0.2
+        cols_h.append(NumericColumn(T.Real, v.to(torch.float32), ok))
+        cols_d.append(NumericColumn(T.Real, v.to(torch.float32).cuda(), ok.cuda()))
+    fills = [0.5, -1.0, 2.0, 0.0, 3.25]
+    for track in (True, False):
+        ref = V.fill_and_track(cols_h, fills, track, torch.float32)
+        got = V.fill_and_track(cols_d, fills, track, torch.float32)
+        torch.testing.assert_close(got.cpu(), ref)
+    assert _native_loaded()
+
+
+def test_workflow_end_to_end_on_device():
+    from transmogrifai_amd import config as CFG
+    from transmogrifai_amd.testkit.synthetic import binary_table
+    from transmogrifai_amd.dsl import transmogrify
+    from transmogrifai_amd.readers.base import InMemoryReader
+    from transmogrifai_amd.selector.factories import BinaryClassificationModelSelector
+    from transmogrifai_amd.workflow.workflow import OpWorkflow
+    dev = torch.device("cuda:0")
+    old = CFG.default_device()
+    CFG.set_default_device(dev)
+    try:
+        ds, label, preds = binary_table(20_000, n_real=10, n_int=3, n_pick=3, seed=5, device=dev)
+        vec = transmogrify(preds)
+        checked = label.sanity_check(vec, remove_bad_features=True)
+        pred = BinaryClassificationModelSelector.with_cross_validation(
+            num_folds=2, seed=3, model_types_to_use=["OpLogisticRegression", "OpRandomForestClassifier"]
+        ).set_input(label, checked).get_output()
+        model = OpWorkflow().set_result_features(label, pred).set_reader(InMemoryReader(ds)).train()
+        summ = model.get_origin_stage_of(pred).metadata["summary"]
+        assert summ["holdoutEvaluation"]["AuPR"] > 0.5
+        assert _native_loaded()
+    finally:
+        CFG.set_default_device(old)

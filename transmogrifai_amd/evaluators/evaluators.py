@@ -174,8 +174,7 @@ class Evaluators:
     """Factory mirroring ``Evaluators.scala``."""
 
     class BinaryClassification:
-        @staticmethod
-        def __call__():
+        def __new__(cls):
             return OpBinaryClassificationEvaluator()
 
         @staticmethod
@@ -211,6 +210,9 @@ class Evaluators:
             return CustomEvaluator(metric_name, is_larger_better, evaluate_fn)
 
     class MultiClassification:
+        def __new__(cls):
+            return OpMultiClassificationEvaluator()
+
         @staticmethod
         def f1():
             return OpMultiClassificationEvaluator("F1")
@@ -236,6 +238,9 @@ class Evaluators:
             return CustomEvaluator(metric_name, is_larger_better, evaluate_fn)
 
     class Regression:
+        def __new__(cls):
+            return OpRegressionEvaluator()
+
         @staticmethod
         def rmse():
             return OpRegressionEvaluator("RootMeanSquaredError")
@@ -257,6 +262,9 @@ class Evaluators:
             return CustomEvaluator(metric_name, is_larger_better, evaluate_fn)
 
     class Forecast:
+        def __new__(cls):
+            return OpForecastEvaluator()
+
         @staticmethod
         def smape():
             return OpForecastEvaluator("SMAPE")

@@ -37,7 +37,13 @@ def register_learner(cls):
     return cls
 
 
+def _load_all():
+    from . import linear, trees  # noqa: F401  (registers every learner)
+
+
 def learner_class(name: str):
+    if name not in _LEARNERS:
+        _load_all()
     if name not in _LEARNERS:
         raise ValueError(f"unknown learner {name}")
     return _LEARNERS[name]

@@ -190,6 +190,13 @@ class SanityChecker(BinaryEstimator):
         cat_stats = []
         if cat_label is not False and (cat_label is True or labels_u.numel() < min(100.0, count * 0.1)):
             cat_stats = self._categorical_tests(X, y, cols)
+        label_dist = None
+        if labels_u.numel() <= 100:
+            lu, lc = torch.unique(y, return_counts=True)
+            label_dist = {"domain": [_label_str(v) for v in lu.cpu().tolist()],
+                          "prob": (lc.to(torch.float64) / max(int(lc.sum()), 1)).cpu().tolist()}
+            for s in cat_stats:
+                s["labels"] = label_dist["domain"]
         stats = self._column_statistics(cols, cs, label_col, d, corr_label, corr_idx, cat_stats, C)
         to_drop = []
         if p["remove_bad_features"]:
@@ -210,6 +217,7 @@ class SanityChecker(BinaryEstimator):
             "featuresStatistics": {"count": float(count), "mean": cs["mean"].tolist(), "max": cs["max"].tolist(),
                                    "min": cs["min"].tolist(), "variance": cs["variance"].tolist(),
                                    "sampleFraction": frac},
+            "labelDistribution": label_dist,
             "names": [c.make_col_name() for c in cols] + [self._inputs[0].name],
             "categoricalStats": [dict(s, contingencyMatrix=s.get("contingency")) for s in cat_stats],
             "columnStatistics": [{k: v for k, v in s.items() if k != "column"} for s in stats],
@@ -376,6 +384,11 @@ class SanityChecker(BinaryEstimator):
                 R.append(f"correlation {pc} for something in parent feature set higher than max correlation "
                          f"{p['max_correlation']}")
         return R
+
+
+def _label_str(v) -> str:
+    f = float(v)
+    return str(int(f)) if f.is_integer() else repr(f)
 
 
 def _is_text_shared_hash(c) -> bool:

@@ -19,12 +19,22 @@ import torch
 from ..uid import make_uid
 
 
+def _s64(c: int) -> int:
+    """Reinterpret an unsigned 64-bit constant as the signed int64 torch arithmetic wraps with."""
+    c &= (1 << 64) - 1
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+_M63 = 0x7FFFFFFFFFFFFFFF
+
+
 def row_uniform(row_ids: torch.Tensor, seed: int, stream: int = 0) -> torch.Tensor:
-    """Deterministic U[0,1) per global row id (splitmix64 hash), identical on any device / shard."""
-    x = row_ids.to(torch.int64) * 0x1E3779B97F4A7C15 + (int(seed) * 0x632BE59BD9B4E019 + stream * 0x2545F4914F6CDD1D)
-    x = x & 0x7FFFFFFFFFFFFFFF
-    x = (x ^ (x >> 30)) * 0x2F58476D1CE4E5B9 & 0x7FFFFFFFFFFFFFFF
-    x = (x ^ (x >> 27)) * 0x14C3124B4B69A5C5 & 0x7FFFFFFFFFFFFFFF
+    """Deterministic U[0,1) per global row id (splitmix64-style hash), identical on any device / shard."""
+    off = _s64(int(seed) * 0x632BE59BD9B4E019 + stream * 0x2545F4914F6CDD1D)
+    x = row_ids.to(torch.int64) * _s64(0x1E3779B97F4A7C15) + off
+    x = x & _M63
+    x = ((x ^ (x >> 30)) * _s64(0x2F58476D1CE4E5B9)) & _M63
+    x = ((x ^ (x >> 27)) * _s64(0x14C3124B4B69A5C5)) & _M63
     x = x ^ (x >> 31)
     return (x >> 10).to(torch.float64) / float(1 << 53)
 
