@@ -22,22 +22,28 @@ def _curve_counts(scores: torch.Tensor, labels: torch.Tensor, num_bins: int = 0,
     w = torch.ones_like(s) if weights is None else weights.to(torch.float64)
     order = torch.argsort(s, descending=True, stable=True)
     s, y, w = s[order], y[order], w[order]
-    uniq, inv = torch.unique_consecutive(s, return_inverse=True)
+    # segmented sums over runs of equal scores without atomics: the input is sorted, so the per-run
+    # totals are differences of the running sums at the run ends
+    uniq, cnt = torch.unique_consecutive(s, return_counts=True)
     n_u = uniq.numel()
-    pos = torch.zeros(n_u, dtype=torch.float64, device=s.device).index_add_(0, inv, w * (y > 0.5))
-    neg = torch.zeros(n_u, dtype=torch.float64, device=s.device).index_add_(0, inv, w * (y <= 0.5))
+    ends = torch.cumsum(cnt, 0) - 1
+    cpos = torch.cumsum(w * (y > 0.5), 0)
+    cneg = torch.cumsum(w * (y <= 0.5), 0)
+    tp_end, fp_end = cpos[ends], cneg[ends]
     thr = uniq
     if num_bins > 0:
         grouping = n_u // num_bins
         if grouping >= 2:
-            gid = torch.arange(n_u, device=s.device) // grouping
-            ng = int(gid[-1].item()) + 1
-            pos = torch.zeros(ng, dtype=torch.float64, device=s.device).index_add_(0, gid, pos)
-            neg = torch.zeros(ng, dtype=torch.float64, device=s.device).index_add_(0, gid, neg)
-            thr = uniq[torch.arange(ng, device=s.device) * grouping]
-    tp = torch.cumsum(pos, 0)
-    fp = torch.cumsum(neg, 0)
-    return thr, tp, fp, float(pos.sum()), float(neg.sum())
+            # groups of ``grouping`` consecutive distinct scores, keyed by their first score
+            last = torch.arange(grouping - 1, n_u, grouping, device=s.device)
+            if last.numel() == 0 or int(last[-1]) != n_u - 1:
+                last = torch.cat([last, torch.tensor([n_u - 1], device=s.device)])
+            thr = uniq[torch.arange(last.numel(), device=s.device) * grouping]
+            tp_end, fp_end = tp_end[last], fp_end[last]
+    tp, fp = tp_end, fp_end
+    P = float(tp[-1]) if tp.numel() else 0.0
+    Nn = float(fp[-1]) if fp.numel() else 0.0
+    return thr, tp, fp, P, Nn
 
 
 def _trapz(x, y):

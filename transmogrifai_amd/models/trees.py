@@ -26,6 +26,7 @@ from . import tree_engine as TE
 from .base import FitJob, Learner, OpPredictor, probability_outputs, register_learner
 from .binning import BinSpec, find_splits, quantize
 from ..stages.base import register_stage
+from ..tuning.splitters import row_uniform
 
 
 # --------------------------------------------------------------------------------------- context
@@ -81,6 +82,26 @@ def _subset_size(strategy, F: int, classification: bool, num_trees: int) -> int:
     return max(1, int(math.ceil(v * F)))
 
 
+def bootstrap_weights(rows: torch.Tensor, seed: int, rate: float) -> torch.Tensor:
+    """Poisson(``rate``) bootstrap multiplicity per row (Spark RF ``BaggedPoint`` with replacement).
+
+    Drawn on the rows' device from a counter-based per-(seed, row id) uniform and the inverse Poisson
+    CDF, so the draw is identical on every device/rank and costs one elementwise pass instead of a
+    host RNG stream per tree.
+    """
+    u = row_uniform(rows, seed, 23)
+    k = torch.zeros(rows.shape[0], dtype=torch.int64, device=rows.device)
+    p = math.exp(-rate)
+    cdf = p
+    for i in range(1, 40):
+        k += (u >= cdf).to(torch.int64)
+        p = p * rate / i
+        cdf += p
+        if 1.0 - cdf < 1e-12:
+            break
+    return k
+
+
 def _rows(job: FitJob, N, dev):
     return torch.arange(N, device=dev) if job.rows is None else job.rows.to(dev)
 
@@ -123,12 +144,11 @@ class _ForestLearner(Learner):
                                    min_info_gain=float(p.get("min_info_gain", 0.0)), feature_subset=sub)
                 seed = int(p.get("seed", 0)) + 7919 * i
                 rate = float(p.get("subsampling_rate", 1.0))
-                g = torch.Generator(device="cpu").manual_seed(seed)
                 for t in range(nt):
                     if nt > 1:
-                        w = torch.poisson(torch.full((rows.numel(),), rate), generator=g).to(torch.int64).to(dev)
+                        w = bootstrap_weights(rows, seed * 1009 + t, rate)
                     elif rate < 1.0:
-                        w = (torch.rand(rows.numel(), generator=g) < rate).to(torch.int64).to(dev)
+                        w = (row_uniform(rows, seed * 1009 + t, 17) < rate).to(torch.int64)
                     else:
                         w = jobs[i].weights.to(dev).round().to(torch.int64) if jobs[i].weights is not None else None
                     tjobs.append(TE.TreeJob(0, tp, rows, w, seed + t))
