@@ -133,11 +133,22 @@ class _ForestLearner(Learner):
         K = self._num_classes(y) if self.classification else 1
         for mb, idxs in groups.items():
             spec, Xb = ctx.binned(mb)
+            yg = y
+            jrows = {i: _rows(jobs[i], N, dev) for i in idxs}
+            if all(jobs[i].rows is not None for i in idxs):
+                # grow over the union of the training rows only (smaller gather footprint, and the
+                # packed 24-bit row ids then index the compacted matrix)
+                U, inv = torch.unique(torch.cat([jrows[i] for i in idxs]), return_inverse=True)
+                if U.numel() < N:
+                    Xb = Xb.index_select(0, U)
+                    yg = y.to(dev).index_select(0, U)
+                    parts = torch.split(inv, [int(jrows[i].numel()) for i in idxs])
+                    jrows = {i: r for i, r in zip(idxs, parts)}
             tjobs, owner = [], []
             for i in idxs:
                 p = jobs[i].params
                 nt = int(p.get("num_trees", self.default_trees)) if self.is_forest else 1
-                rows = _rows(jobs[i], N, dev)
+                rows = jrows[i]
                 sub = _subset_size(p.get("feature_subset_strategy", "auto"), F, self.classification, nt)
                 tp = TE.TreeParams(max_depth=int(p.get("max_depth", 5)),
                                    min_instances=float(p.get("min_instances_per_node", 1)),
@@ -156,10 +167,10 @@ class _ForestLearner(Learner):
             if self.classification:
                 forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_CLS,
                                         kind=TE.KINDS[jobs[idxs[0]].params.get("impurity", "gini")], n_classes=K,
-                                        y=y, B=mb, rng_seed=int(jobs[idxs[0]].params.get("seed", 0)))
+                                        y=yg, B=mb, rng_seed=int(jobs[idxs[0]].params.get("seed", 0)))
             else:
                 forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_VAR, kind=TE.KIND_VARIANCE,
-                                        t1=y.to(torch.float32)[None, :], B=mb,
+                                        t1=yg.to(torch.float32)[None, :], B=mb,
                                         rng_seed=int(jobs[idxs[0]].params.get("seed", 0)))
             owner = np.asarray(owner)
             for i in idxs:
@@ -291,7 +302,20 @@ class _BoostLearner(Learner):
             groups.setdefault(self._bin_key(j.params), []).append(i)
         for key, idxs in groups.items():
             spec, Xb = ctx.binned(*key)
-            res = self._boost(Xb, spec, y.to(dev), [jobs[i] for i in idxs], N, F, dev, key[0])
+            gjobs = [jobs[i] for i in idxs]
+            yd = y.to(dev)
+            NU = N
+            if all(j.rows is not None for j in gjobs):
+                # boost only over the union of the jobs' training rows: gradients, margins and the
+                # per-round prediction pass then scale with the (down-sampled) training sets, not N
+                U, inv = torch.unique(torch.cat([j.rows.to(dev) for j in gjobs]), return_inverse=True)
+                if U.numel() < N:
+                    Xb = Xb.index_select(0, U)
+                    yd = yd.index_select(0, U)
+                    NU = int(U.numel())
+                    parts = torch.split(inv, [int(j.rows.numel()) for j in gjobs])
+                    gjobs = [FitJob(j.params, r, j.weights) for j, r in zip(gjobs, parts)]
+            res = self._boost(Xb, spec, yd, gjobs, NU, F, dev, key[0])
             for k, i in enumerate(idxs):
                 out[i] = res[k]
         return out
