@@ -271,6 +271,8 @@ class UnaryTransformer(OpTransformer):
         return column_from_values(self.output_type, out, cols[0].device)
 
     def transform_row(self, *values):
+        if self.fn is None and type(self).transform_fn is UnaryTransformer.transform_fn:
+            return OpTransformer.transform_row(self, *values)   # columnar-only model: one-row batch
         return _unwrap(self.transform_fn(values[0]))
 
 
@@ -290,6 +292,8 @@ class BinaryTransformer(OpTransformer):
         return column_from_values(self.output_type, out, cols[0].device)
 
     def transform_row(self, *values):
+        if self.fn is None and type(self).transform_fn is BinaryTransformer.transform_fn:
+            return OpTransformer.transform_row(self, *values)
         return _unwrap(self.transform_fn(values[0], values[1]))
 
 

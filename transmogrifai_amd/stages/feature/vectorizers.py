@@ -644,7 +644,7 @@ def _date_reduce(c, first: bool, dev):
     if isinstance(c, NumericColumn):
         return c.values.to(torch.int64), c.valid
     vals = c.to_list()
-    ok = np.array([bool(v) for v in vals])
+    ok = np.array([bool(v) for v in vals], dtype=bool)
     d = np.array([(min(v) if first else max(v)) if v else 0 for v in vals], np.int64)
     return torch.as_tensor(d, device=dev), torch.as_tensor(ok, device=dev)
 
