@@ -237,6 +237,8 @@ def extract_model_insights(model, pred_feature=None) -> ModelInsights:
                     fi = feats[o] = FeatureInsights(o, raw_types.get(o, c.parent_feature_type[0]), [])
                 fi.derivedFeatures.append(ins)
     rff = getattr(model, "raw_feature_filter_results", None)
+    if rff is not None and hasattr(rff, "to_json"):
+        rff = rff.to_json()
     if rff:
         for m in rff.get("rawFeatureFilterMetrics", []):
             n = m.get("name")

@@ -52,6 +52,8 @@ _HIP_SIGS = {
     "tmog_hip_gram_f32": [P, I64, I32, I64, P, I32, P],
     "tmog_hip_logistic_grad": [P, P, P, I64, I32, P],
     "tmog_hip_label_colsum": [P, P, I64, I32, I64, I32, P, P],
+    "tmog_hip_rff_summary": [P, P, P, I64, I32, P, I32, P, P],
+    "tmog_hip_rff_hist": [P, P, P, I64, I32, P, P, I32, P, P],
 }
 
 

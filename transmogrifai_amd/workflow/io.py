@@ -63,11 +63,13 @@ def stage_to_json(st: OpPipelineStage) -> Dict:
 
 def model_to_json(model) -> Dict:
     gens = {}
-    for f in model.raw_features:
-        gens[f.origin_stage.uid] = f.origin_stage
+    for f in list(model.raw_features) + list(model.blocklist):
+        for r in (f.raw_features() if not f.is_raw else [f]):
+            gens[r.origin_stage.uid] = r.origin_stage
     stages = [stage_to_json(s) for s in gens.values()] + [stage_to_json(s) for s in model.stages]
+    # raw + blocklisted + every stage output (OpWorkflowModelWriter allFeatures)
     feats = {}
-    for f in model.result_features:
+    for f in list(model.result_features) + list(model.blocklist):
         for x in f.traverse():
             feats[x.uid] = x
     all_features = []

@@ -130,9 +130,61 @@ class OpWorkflow(OpWorkflowCore):
         return self
 
     def with_raw_feature_filter(self, training_reader=None, scoring_reader=None, **kw) -> "OpWorkflow":
+        """Attach a :class:`RawFeatureFilter` (``OpWorkflow.withRawFeatureFilter``, ``OpWorkflow.scala:537-578``)."""
         from ..filters.raw_feature_filter import RawFeatureFilter
-        self.rff = RawFeatureFilter(training_reader or self.reader, scoring_reader, **kw)
+        training = training_reader or self.reader
+        if training is None:
+            raise ValueError("Reader for training data must be provided either in with_raw_feature_filter or "
+                             "directly as the reader for the workflow")
+        self.rff = RawFeatureFilter(training, scoring_reader, **kw)
+        if self.reader is None:
+            self.reader = training
         return self
+
+    def set_blocklist(self, features: Sequence[FeatureLike], distributions=()) -> None:
+        """Remove blocklisted raw features from every stage's inputs and rebuild the DAG
+        (``OpWorkflow.setBlocklist``, ``OpWorkflow.scala:118-168``)."""
+        policy = getattr(getattr(self, "rff", None), "result_feature_retention_policy", "Strict")
+        self.blocklist = list(features)
+        if not self.blocklist:
+            return
+        blocked: List[FeatureLike] = list(self.blocklist)
+        updated: List[FeatureLike] = []
+        initial_results = list(self.result_features)
+
+        def check_results():
+            if policy == "Strict":
+                for f in initial_results:
+                    if any(b.same_origin(f) for b in blocked):
+                        raise ValueError(f"Blocklist of features ({', '.join(b.name for b in blocked)}) from "
+                                         f"RawFeatureFilter contained the result feature {f.name}")
+            elif policy == "AtLeastOne":
+                if all(any(b.same_origin(f) for b in blocked) for f in initial_results):
+                    raise ValueError("Blocklist of features from RawFeatureFilter removed all result features")
+            else:
+                raise ValueError(f"result feature retention policy {policy} not supported")
+
+        check_results()
+        dist_by_name: Dict[str, list] = {}
+        for d in distributions or ():
+            dist_by_name.setdefault(d.name, []).append(d)
+        for stg in list(self.stages):
+            ins = [f for f in stg.get_input_features() if not any(b.same_origin(f) for b in blocked)]
+            ins = [f.with_distributions(dist_by_name.get(f.name, [])) if f.is_raw else f for f in ins]
+            ins = [next((u for u in updated if u.same_origin(f)), f) for f in ins]
+            old = stg.get_output()
+            try:
+                if not ins:
+                    raise ValueError("no inputs left")
+                out = stg.set_input(*ins).set_output_feature_name(old.name).get_output()
+                updated.append(out)
+            except Exception as e:   # the stage cannot run without the blocklisted inputs
+                log.info("Issue updating inputs for stage %s: %s", stg, e)
+                blocked.append(old)
+                check_results()
+        new_results = [next((u for u in updated if u.same_origin(f)), f) for f in initial_results
+                       if not any(b.same_origin(f) for b in blocked)]
+        self.set_result_features(*new_results)
 
     def train(self, params: Optional[OpParams] = None) -> "OpWorkflowModel":
         timings: Dict[str, float] = {}
@@ -140,9 +192,14 @@ class OpWorkflow(OpWorkflowCore):
         with _Timer(timings, OpStep.DataReadingAndFiltering):
             raw = self.generate_raw_data(params or self.parameters)
             if getattr(self, "rff", None) is not None:
-                raw, blocked, results = self.rff.filter(raw, self.raw_features, self.result_features)
-                self.blocklist = blocked
+                rp = None
+                pp = params or self.parameters
+                if pp is not None and pp.reader_params:
+                    rp = next(iter(pp.reader_params.values()))
+                raw, to_drop, drop_keys, results = self.rff.generate_filtered_raw(self.raw_features, rp, raw)
                 self.raw_feature_filter_results = results
+                self.set_blocklist(to_drop, results.rawFeatureDistributions)
+                self.blocklist_map_keys = {k: sorted(v) for k, v in drop_keys.items()}
         fitted = self.fit_stages(raw, timings)
         model = OpWorkflowModel(self.uid, self.parameters)
         model.stages = fitted
