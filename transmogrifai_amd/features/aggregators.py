@@ -107,6 +107,9 @@ class ConcatText(MonoidAggregator):
             return a
         return f"{a}{self.separator}{b}"
 
+    def to_json(self):
+        return {"name": self.name, "separator": self.separator}
+
 
 class ModePickList(MonoidAggregator):
     name = "ModePickList"
@@ -288,3 +291,23 @@ def filter_by_date_with_cutoff(date: int, cutoff: CutOffTime, is_response: bool,
     if is_response:
         return c <= date <= c + window
     return c - window <= date < c
+
+
+def aggregator_from_json(d) -> Optional[MonoidAggregator]:
+    """Rebuild a (default-family) aggregator from its serialized ``{"className", "value": {"name"}}`` form."""
+    if not d:
+        return None
+    name = (d.get("value") or {}).get("name") or d.get("className")
+    simple = {c.name: c for c in (SumNumeric, MaxNumeric, MinNumeric, MeanNumeric, LogicalOr, ModePickList,
+                                  ConcatList, UnionSet, GeolocationMidpoint, CombineVector)}
+    if name in simple:
+        return simple[name]()
+    if name == "ConcatText":
+        return ConcatText((d.get("value") or {}).get("separator", ","))
+    probe = {"UnionMeanPrediction": T.Prediction, "UnionMultiPickListMap": T.MultiPickListMap,
+             "UnionGeolocationMidpointMap": T.GeolocationMap, "UnionBinaryMap": T.BinaryMap,
+             "UnionMaxDateMap": T.DateMap, "UnionMeanPercentMap": T.PercentMap, "UnionSumMap": T.RealMap,
+             "UnionConcatTextMap": T.TextMap}
+    if name in probe:
+        return default_aggregator(probe[name])
+    return None

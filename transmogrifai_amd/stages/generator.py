@@ -43,12 +43,13 @@ class FeatureGeneratorStage(OpPipelineStage):
 
     def extract(self, record) -> Any:
         """Apply the extract function to a record (dict, object or pandas row)."""
+        col = self.column if self.column is not None else self.name
         if self.extract_fn is not None:
             v = self.extract_fn(record)
         elif isinstance(record, dict):
-            v = record.get(self.column)
+            v = record.get(col)
         else:
-            v = getattr(record, self.column, None)
+            v = getattr(record, col, None)
         if isinstance(v, T.FeatureType):
             v = v.value
         return v
@@ -59,9 +60,41 @@ class FeatureGeneratorStage(OpPipelineStage):
             agg = {"className": type(self.aggregator).__name__, "value": getattr(self.aggregator, "to_json",
                                                                                lambda: {})()}
         return {"tti": "Record", "tto": self.output_type.type_name(), "aggregator": agg,
-                "extractFn": {"className": "ColumnExtract" if self.extract_fn is None else "PythonFunction",
-                              "column": self.column},
+                "extractFn": {"className": _fn_name(self.extract_fn), "column": self.column},
                 "outputName": self.name, "uid": self.uid,
                 "extractSource": self.extract_source or "",
                 "outputIsResponse": self.output_is_response,
                 "aggregateWindow": self.aggregate_window}
+
+
+def _fn_name(fn) -> str:
+    """Importable ``module.qualname`` of a module-level extract function (reloaded on model load, the
+    analogue of the reference's reflective ``extractFn`` class instances); ``ColumnExtract`` for
+    column extraction; ``PythonFunction`` for lambdas / closures, which cannot be restored."""
+    if fn is None:
+        return "ColumnExtract"
+    mod, qn = getattr(fn, "__module__", None), getattr(fn, "__qualname__", "")
+    if mod and qn and "<" not in qn:
+        return f"{mod}.{qn}"
+    return "PythonFunction"
+
+
+def load_extract_fn(name: Optional[str]):
+    if not name or name in ("ColumnExtract", "PythonFunction"):
+        return None
+    import importlib
+    mod, _, qn = name.rpartition(".")
+    while mod:
+        try:
+            obj = importlib.import_module(mod)
+            break
+        except ImportError:
+            mod, _, head = mod.rpartition(".")
+            qn = head + "." + qn
+    else:
+        return None
+    for part in qn.split("."):
+        obj = getattr(obj, part, None)
+        if obj is None:
+            return None
+    return obj if callable(obj) else None

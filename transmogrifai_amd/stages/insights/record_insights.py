@@ -1,0 +1,318 @@
+"""Per-record explanations: leave-one-column-out (LOCO) and score/feature correlation insights.
+
+Reference: ``RecordInsightsLOCO`` (``core/.../stages/impl/insights/RecordInsightsLOCO.scala:100-347``: top-K
+by |score change| or top-K positive + negative, text / date column groups aggregated by ``Avg`` or
+``LeaveOutVector``), ``RecordInsightsCorr`` (``RecordInsightsCorr.scala:55-220``: per-feature
+correlation with each score column times the normalized feature value) and ``RecordInsightsParser``
+(``insightToText`` / ``parseInsights``). SURVEY.md K30.
+
+Device design: LOCO is computed for a whole block of records at once. Every (record, non-zero
+column) perturbation becomes one row of a perturbed batch scored by the model's vectorized predict
+(for linear models the batch is never materialized: the perturbed margin is ``m_i - w_j x_ij``, an
+elementwise [rows, d] tensor op); top-K selection per record is ``torch.topk`` over the
+[rows, candidates] score-change matrix. Only the final ``TextMap`` strings are built on the host.
+"""
+from __future__ import annotations
+
+import json
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ...data.columns import ObjectColumn, PredictionColumn, VectorColumn
+from ...features import types as T
+from ..base import BinaryEstimator, BinaryTransformer, UnaryTransformer, register_stage
+
+TEXT_TYPES = {"Text", "TextArea", "TextList", "TextMap", "TextAreaMap"}
+DATE_TYPES = {"Date", "DateTime", "DateMap", "DateTimeMap"}
+TIME_PERIODS = ("DayOfMonth", "DayOfWeek", "DayOfYear", "HourOfDay", "MonthOfYear", "WeekOfMonth", "WeekOfYear")
+
+
+# ------------------------------------------------------------------------------------------- parser
+def insight_to_text(column_info: str, score_diffs) -> Tuple[str, str]:
+    scores = [[i, float(s)] for i, s in enumerate(score_diffs)]
+    return column_info, json.dumps(scores, separators=(",", ":"))
+
+
+def parse_insights(insights: Dict[str, str]) -> Dict[str, List[Tuple[int, float]]]:
+    """``RecordInsightsParser.parseInsights``: column-history JSON -> [(score index, value)]."""
+    out = {}
+    for k, v in (insights or {}).items():
+        hist = json.loads(k)
+        key = hist.get("columnName", k)
+        out[key] = [(int(a), float(b)) for a, b in json.loads(v)]
+    return out
+
+
+def _short(t: str) -> str:
+    return t.rsplit(".", 1)[-1]
+
+
+def _history_json(h: dict) -> str:
+    return json.dumps(h, separators=(",", ":"), sort_keys=False)
+
+
+# ---------------------------------------------------------------------------------------------- LOCO
+@register_stage
+class RecordInsightsLOCO(UnaryTransformer):
+    """Unary (OPVector -> TextMap) transformer wrapping a fitted prediction model stage."""
+    operation_name = "recordInsightsLOCO"
+    output_type = T.TextMap
+    _defaults = {"top_k": 20, "top_k_strategy": "abs", "vector_aggregation_strategy": "Avg"}
+
+    def __init__(self, model=None, uid=None, **kw):
+        super().__init__(None, uid=uid, **kw)
+        self.model = model
+        self.histories: Optional[List[dict]] = None
+        self.chunk_elems = 1 << 22
+
+    # -- model access
+    def _learner_state(self):
+        m = self.model
+        return m.learner, m.state
+
+    def _scores(self, X: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(score matrix [n, C], predicted class [n])."""
+        learner, state = self._learner_state()
+        pred, raw, prob = learner.predict(state, X)
+        if prob.shape[1] > 0:
+            s = prob
+        else:
+            s = pred.reshape(-1, 1)
+        return s.to(torch.float64), pred.reshape(-1)
+
+    # -- groups of columns aggregated as one insight (text hashes, date unit circles)
+    def _groups(self, hist: List[dict]):
+        groups: Dict[str, List[int]] = {}
+        for j, h in enumerate(hist):
+            types = {_short(t) for t in h.get("parentFeatureType", [])}
+            is_text = bool(types & TEXT_TYPES) and h.get("indicatorValue") is None and h.get("descriptorValue") is None
+            is_date = bool(types & DATE_TYPES) and h.get("descriptorValue") is not None
+            if not (is_text or is_date):
+                continue
+            origins = h.get("parentFeatureOrigins") or h.get("parentFeatureName") or [""]
+            name = origins[0] + ("_" + h["grouping"] if h.get("grouping") else "")
+            if is_date:
+                tp = str(h.get("descriptorValue")).split("_")[-1]
+                if tp.lower() in {p.lower() for p in TIME_PERIODS}:
+                    name += "_" + next(p for p in TIME_PERIODS if p.lower() == tp.lower())
+            groups.setdefault(name, []).append(j)
+        return groups
+
+    def _loco_block(self, X: torch.Tensor, hist: List[dict]):
+        """Score changes for one block of records: returns per record a list of (col, value, diffs)."""
+        n, d = X.shape
+        base, pred_cls = self._scores(X)
+        C = base.shape[1]
+        if C == 0:
+            raise RuntimeError("model does not produce scores for insights")
+        if C == 1:
+            ex = torch.zeros(n, dtype=torch.long, device=X.device)
+        elif C == 2:
+            ex = torch.ones(n, dtype=torch.long, device=X.device)
+        else:
+            ex = pred_cls.to(torch.long)
+        groups = self._groups(hist)
+        in_group = torch.zeros(d, dtype=torch.bool)
+        for cols in groups.values():
+            in_group[cols] = True
+        nz = X != 0
+        rows, cols = torch.nonzero(nz, as_tuple=True)
+        diffs = torch.zeros(rows.numel(), C, dtype=torch.float64, device=X.device)
+        # one perturbed copy per (record, non-zero column), scored in bounded chunks
+        step = max(1, self.chunk_elems // max(d, 1))
+        for a in range(0, rows.numel(), step):
+            r, c = rows[a:a + step], cols[a:a + step]
+            Xp = X.index_select(0, r).clone()
+            Xp[torch.arange(r.numel(), device=X.device), c] = 0
+            s, _ = self._scores(Xp)
+            diffs[a:a + step] = base.index_select(0, r) - s
+        D = torch.zeros(n, d, C, dtype=torch.float64, device=X.device)
+        D[rows, cols] = diffs
+        strategy = self.params["vector_aggregation_strategy"]
+        cand_vals = []       # [n] tensors of diffs (all classes) per candidate
+        cand_cols = []
+        plain = [j for j in range(d) if not bool(in_group[j])]
+        for j in plain:
+            cand_cols.append(torch.full((n,), j, dtype=torch.long, device=X.device))
+            cand_vals.append(D[:, j, :])
+        for name, gc in groups.items():
+            gct = torch.as_tensor(gc, device=X.device)
+            active = nz[:, gct]
+            has = active.any(1)
+            first = torch.where(has, gct[active.to(torch.int8).argmax(1)], torch.full((n,), -1, device=X.device))
+            if strategy == "Avg":
+                v = D[:, gct, :].sum(1) / len(gc)
+            else:   # LeaveOutVector: zero every active column of the group at once
+                Xp = X.clone()
+                Xp[:, gct] = 0
+                s, _ = self._scores(Xp)
+                v = torch.where(has[:, None], base - s, torch.zeros_like(base))
+            cand_cols.append(first)
+            cand_vals.append(v)
+        if not cand_vals:
+            return [[] for _ in range(n)]
+        V = torch.stack(cand_vals, 1)                      # [n, m, C]
+        Cc = torch.stack(cand_cols, 1)                     # [n, m]
+        val = V.gather(2, ex.view(n, 1, 1).expand(n, V.shape[1], 1)).squeeze(2)
+        valid = (Cc >= 0) & (val != 0)
+        k = int(self.params["top_k"])
+        kk = min(k, val.shape[1])
+        pos = torch.where(valid & (val > 0), val, torch.full_like(val, -float("inf")))
+        neg = torch.where(valid & (val < 0), -val, torch.full_like(val, -float("inf")))
+        pv, pi = torch.topk(pos, kk, dim=1)
+        nv, ni = torch.topk(neg, kk, dim=1)
+        out = []
+        pv, pi, nv, ni = pv.cpu(), pi.cpu(), nv.cpu(), ni.cpu()
+        Vc, Cc_, valc = V.cpu(), Cc.cpu(), val.cpu()
+        for i in range(n):
+            items = [(int(Cc_[i, m]), float(valc[i, m]), Vc[i, m].tolist())
+                     for m, v in zip(pi[i].tolist(), pv[i].tolist()) if v != -float("inf")]
+            items += [(int(Cc_[i, m]), float(valc[i, m]), Vc[i, m].tolist())
+                      for m, v in zip(ni[i].tolist(), nv[i].tolist()) if v != -float("inf")]
+            if self.params["top_k_strategy"] == "abs":
+                items.sort(key=lambda t: -abs(t[1]))
+                items = items[:k]
+            else:
+                items.sort(key=lambda t: -t[1])
+                items = items[:2 * k]
+            out.append(items)
+        return out
+
+    def transform_columns(self, *cols, ds=None):
+        vec: VectorColumn = cols[0]
+        if vec.metadata is not None:
+            self.histories = vec.metadata.column_history()
+        hist = self.histories
+        if hist is None:
+            raise ValueError("RecordInsightsLOCO needs the input vector metadata (column histories)")
+        X = vec.values
+        n = X.shape[0]
+        res = []
+        block = max(1, self.chunk_elems // max(X.shape[1] * max(X.shape[1], 1), 1))
+        block = max(block, 64)
+        for a in range(0, n, block):
+            res.extend(self._loco_block(X[a:a + block], hist))
+        texts = []
+        for items in res:
+            texts.append(dict(insight_to_text(_history_json(hist[c]), diffs) for c, _, diffs in items))
+        return ObjectColumn(T.TextMap, texts)
+
+    def transform_row(self, *values):
+        x = torch.as_tensor(np.asarray(values[0], np.float64))[None, :]
+        if self.histories is None:
+            raise ValueError("RecordInsightsLOCO has not seen vector metadata yet")
+        items = self._loco_block(x, self.histories)[0]
+        return dict(insight_to_text(_history_json(self.histories[c]), diffs) for c, _, diffs in items)
+
+    def ctor_args(self):
+        from ...workflow.io import stage_to_json
+        return {"model": stage_to_json(self.model) if self.model is not None else None,
+                "histories": self.histories}
+
+    def load_ctor_args(self, a):
+        from ...workflow.io import _build_stage
+        self.model = _build_stage(a["model"]) if a.get("model") else None
+        self.histories = a.get("histories")
+
+
+# ---------------------------------------------------------------------------------------------- Corr
+def _pred_matrix(col) -> torch.Tensor:
+    if isinstance(col, PredictionColumn):
+        if col.probability.shape[1] > 0:
+            return col.probability.to(torch.float64)
+        return col.prediction.reshape(-1, 1).to(torch.float64)
+    return col.values.to(torch.float64)
+
+
+@register_stage
+class RecordInsightsCorrModel(BinaryTransformer):
+    operation_name = "recordInsightsCorr"
+    output_type = T.TextMap
+    allow_label_as_input = True
+
+    def __init__(self, top_k=20, score_corr=None, norm=None, histories=None, uid=None, **kw):
+        super().__init__(None, uid=uid, **kw)
+        self.top_k = top_k
+        self.score_corr = None if score_corr is None else np.asarray(score_corr, np.float64)
+        self.norm = norm or {}
+        self.histories = histories
+
+    def _normalize(self, X: torch.Tensor) -> torch.Tensor:
+        a = torch.as_tensor(self.norm["a"], dtype=torch.float64, device=X.device)
+        b = torch.as_tensor(self.norm["b"], dtype=torch.float64, device=X.device)
+        off = float(self.norm["offset"])
+        Xd = X.to(torch.float64)
+        return torch.where(b == 0, torch.zeros_like(Xd), (Xd - a) / torch.where(b == 0, torch.ones_like(b), b) - off)
+
+    def _rows(self, X: torch.Tensor) -> List[Dict[str, str]]:
+        d = X.shape[1]
+        if self.histories is not None and len(self.histories) != d:
+            raise ValueError("feature metadata size does not match feature size")
+        Z = self._normalize(X)
+        S = torch.as_tensor(np.nan_to_num(self.score_corr, nan=0.0), dtype=torch.float64, device=X.device)
+        imp = Z[:, None, :] * S[None, :, :]                  # [n, P, d]
+        k = min(int(self.top_k), d)
+        _, idx = torch.topk(imp.abs(), k, dim=2)
+        vals = imp.gather(2, idx)
+        idx, vals = idx.cpu().numpy(), vals.cpu().numpy()
+        out = []
+        for i in range(X.shape[0]):
+            acc: Dict[int, list] = {}
+            for p in range(idx.shape[1]):
+                for j, v in zip(idx[i, p], vals[i, p]):
+                    acc.setdefault(int(j), []).append([p, float(v)])
+            out.append({_history_json(self.histories[j]): json.dumps(v, separators=(",", ":"))
+                        for j, v in acc.items()})
+        return out
+
+    def transform_columns(self, pred, vec, ds=None):
+        return ObjectColumn(T.TextMap, self._rows(vec.values))
+
+    def transform_row(self, *values):
+        x = torch.as_tensor(np.asarray(values[1], np.float64))[None, :]
+        return self._rows(x)[0]
+
+    def ctor_args(self):
+        return {"topK": self.top_k, "scoreCorr": None if self.score_corr is None else self.score_corr.tolist(),
+                "norm": self.norm, "histories": self.histories}
+
+    def load_ctor_args(self, a):
+        self.top_k = a["topK"]
+        self.score_corr = None if a["scoreCorr"] is None else np.asarray(a["scoreCorr"], np.float64)
+        self.norm = a["norm"]
+        self.histories = a["histories"]
+
+
+@register_stage
+class RecordInsightsCorr(BinaryEstimator):
+    """(prediction, feature vector) -> TextMap of the top-K correlation-weighted features per record."""
+    operation_name = "recordInsightsCorr"
+    output_type = T.TextMap
+    allow_label_as_input = True
+    _defaults = {"norm_type": "minMax", "correlation_type": "pearson", "top_k": 20}
+
+    def fit_columns(self, pred, vec, ds=None):
+        from ...ops import stats as ST
+        if vec.metadata is None:
+            raise ValueError("second input feature must be a feature vector with OpVectorMetadata")
+        P = _pred_matrix(pred)
+        X = vec.values.to(torch.float64)
+        psize, fsize = P.shape[1], X.shape[1]
+        comb = torch.cat([X, P.to(X.device)], 1)
+        C = ST.corr_matrix(comb, self.params["correlation_type"]).cpu().numpy()
+        score_corr = C[fsize:fsize + psize, :fsize]
+        cs = ST.col_stats(X)
+        nt = self.params["norm_type"]
+        mn, mx = cs["min"].cpu().numpy(), cs["max"].cpu().numpy()
+        if nt == "minMax":
+            norm = {"a": mn.tolist(), "b": (mx - mn).tolist(), "offset": 0.0, "name": nt}
+        elif nt == "zNorm":
+            norm = {"a": cs["mean"].cpu().numpy().tolist(), "b": np.sqrt(cs["variance"].cpu().numpy()).tolist(),
+                    "offset": 0.0, "name": nt}
+        elif nt == "minMaxCentered":
+            norm = {"a": mn.tolist(), "b": ((mx - mn) / 2.0).tolist(), "offset": 1.0, "name": nt}
+        else:
+            raise ValueError(f"unknown norm type {nt}")
+        return RecordInsightsCorrModel(self.params["top_k"], score_corr, norm, vec.metadata.column_history())

@@ -54,6 +54,8 @@ def decode(obj):
         return {k: decode(v) for k, v in obj.items()}
     if isinstance(obj, list):
         return [decode(x) for x in obj]
+    if not isinstance(obj, str):     # already-decoded values (decode is idempotent)
+        return obj
     if obj == "NaN":
         return float("nan")
     if obj == "Infinity":

@@ -124,11 +124,15 @@ def _build_stage(sj: Dict) -> OpPipelineStage:
     pm = sj.get("paramMap", {})
     args = decode(sj.get("ctorArgs", {}))
     if cls is FeatureGeneratorStage:
-        st = FeatureGeneratorStage(args.get("outputName") or pm.get("outputFeatureName"),
-                                   T.feature_type_from_name(args.get("tto", sj.get("outputType", "Text"))),
-                                   None, None, args.get("aggregateWindow"), bool(args.get("outputIsResponse")),
-                                   args.get("extractSource"), uid=sj["uid"],
-                                   column=(args.get("extractFn") or {}).get("column"))
+        from ..features.aggregators import aggregator_from_json, default_aggregator
+        from ..stages.generator import load_extract_fn
+        ef = args.get("extractFn") or {}
+        tto = T.feature_type_from_name(args.get("tto", sj.get("outputType", "Text")))
+        agg = aggregator_from_json(args.get("aggregator")) or default_aggregator(tto)
+        st = FeatureGeneratorStage(args.get("outputName") or pm.get("outputFeatureName"), tto,
+                                   load_extract_fn(ef.get("className")), agg, args.get("aggregateWindow"),
+                                   bool(args.get("outputIsResponse")), args.get("extractSource"), uid=sj["uid"],
+                                   column=ef.get("column"))
         return st
     from .. import uid as _uid
     c0 = _uid.count()
