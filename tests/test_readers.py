@@ -1,0 +1,107 @@
+"""Readers: CSV / Avro / Parquet / aggregate / conditional / joined / streaming (``readers/src/test``)."""
+import os
+
+import numpy as np
+import pytest
+
+from transmogrifai_amd.features import types as T
+from transmogrifai_amd.features.builder import FeatureBuilder
+from transmogrifai_amd.features.aggregators import CutOffTime
+from transmogrifai_amd.readers.files import CSVReader, DataReaders
+from transmogrifai_amd.readers.aggregate import AggregateParams, ConditionalParams, TimeStampToKeep
+
+REF = "/root/reference/test-data"
+have_ref = pytest.mark.skipif(not os.path.isdir(REF), reason="reference test data not mounted")
+
+
+@have_ref
+def test_avro_matches_csv():
+    age = FeatureBuilder.Real("Age").as_predictor()
+    name = FeatureBuilder.Text("Name").as_predictor()
+    surv = FeatureBuilder.Integral("Survived").as_response()
+    a = DataReaders.Simple.avro(f"{REF}/PassengerDataAll.avro", key=lambda r: r["PassengerId"])
+    ds = a.generate_dataset([age, name, surv])
+    assert len(ds) == 891
+    c = DataReaders.Simple.csv_auto(f"{REF}/PassengerDataAllWithHeader.csv")
+    import pandas as pd
+    df = pd.read_csv(f"{REF}/PassengerDataAllWithHeader.csv")
+    assert ds["Name"].to_list()[:5] == list(df["Name"][:5])
+    ages = ds["Age"].to_list()
+    assert sum(v is None for v in ages) == int(df["Age"].isna().sum())
+
+
+@have_ref
+def test_parquet_reader():
+    p = DataReaders.Simple.parquet(f"{REF}/PassengerDataAll.parquet")
+    f = FeatureBuilder.Real("Fare").as_predictor() if False else None
+    frame = p.read_frame()
+    assert len(frame) == 891
+
+
+def _events():
+    # key, time, amount, label flag
+    day = 86_400_000
+    return [{"k": "a", "t": 1 * day, "amt": 1.0, "buy": False}, {"k": "a", "t": 2 * day, "amt": 2.0, "buy": False},
+            {"k": "a", "t": 5 * day, "amt": 4.0, "buy": True}, {"k": "b", "t": 1 * day, "amt": 10.0, "buy": False},
+            {"k": "b", "t": 9 * day, "amt": 20.0, "buy": False}]
+
+
+def test_aggregate_reader_cutoff():
+    day = 86_400_000
+    amt = FeatureBuilder.Real("amt").as_predictor()
+    buy = FeatureBuilder.Binary("buy").as_response()
+    r = DataReaders.Aggregate.custom(_events(), key=lambda e: e["k"],
+                                     aggregate_params=AggregateParams(lambda e: e["t"], CutOffTime.unix_epoch(3 * day)))
+    ds = r.generate_dataset([amt, buy])
+    got = dict(zip(ds.key, zip(ds["amt"].to_list(), ds["buy"].to_list())))
+    assert got["a"] == (3.0, True)      # predictors before cutoff summed; response after cutoff OR-ed
+    assert got["b"] == (10.0, False)
+
+
+def test_conditional_reader():
+    day = 86_400_000
+    amt = FeatureBuilder.Real("amt").as_predictor()
+    buy = FeatureBuilder.Binary("buy").as_response()
+    cp = ConditionalParams(lambda e: e["t"], lambda e: e["buy"], response_window_ms=2 * day,
+                           predictor_window_ms=10 * day, timestamp_to_keep=TimeStampToKeep.Min,
+                           drop_if_target_condition_not_met=True)
+    r = DataReaders.Conditional.custom(_events(), key=lambda e: e["k"], conditional_params=cp)
+    ds = r.generate_dataset([amt, buy])
+    assert list(ds.key) == ["a"]
+    assert ds["amt"].to_list() == [3.0] and ds["buy"].to_list() == [True]
+
+
+def test_joined_reader():
+    from transmogrifai_amd.readers.base import InMemoryReader
+    from transmogrifai_amd.readers.joined import JoinedReader, JoinTypes
+    left = InMemoryReader([{"id": 1, "x": 1.0}, {"id": 2, "x": 2.0}, {"id": 3, "x": 3.0}], key=lambda r: r["id"])
+    right = InMemoryReader([{"id": 2, "y": "b"}, {"id": 4, "y": "d"}], key=lambda r: r["id"])
+    x = FeatureBuilder.Real("x").as_predictor()
+    y = FeatureBuilder.PickList("y").as_predictor()
+    for jt, keys, ys in [(JoinTypes.Inner, ["2"], ["b"]), (JoinTypes.LeftOuter, ["1", "2", "3"], [None, "b", None]),
+                         (JoinTypes.Outer, ["1", "2", "3", "4"], [None, "b", None, "d"])]:
+        ds = JoinedReader(left, right, jt, right_features=["y"]).generate_dataset([x, y])
+        assert list(ds.key) == keys and ds["y"].to_list() == ys
+
+
+def test_streaming_readers(tmp_path):
+    import pandas as pd
+    from transmogrifai_amd.readers.streaming import FileStreamingReader, IterableStreamingReader
+    batches = list(IterableStreamingReader(({"a": i} for i in range(25)), batch_size=10).stream())
+    assert [len(b) for b in batches] == [10, 10, 5]
+    for i in range(3):
+        pd.DataFrame({"a": [i, i + 1]}).to_csv(tmp_path / f"b{i}.csv", index=False)
+    frames = list(FileStreamingReader(str(tmp_path), "*.csv").stream())
+    assert len(frames) == 3 and list(frames[2]["a"]) == [2, 3]
+
+
+def test_avro_roundtrip(tmp_path):
+    from transmogrifai_amd.readers.avro import read_avro, write_avro
+    schema = {"type": "record", "name": "R", "fields": [
+        {"name": "a", "type": ["null", "long"]}, {"name": "b", "type": ["null", "string"]},
+        {"name": "c", "type": {"type": "array", "items": "double"}},
+        {"name": "m", "type": {"type": "map", "values": "string"}}, {"name": "f", "type": "boolean"}]}
+    recs = [{"a": 1, "b": None, "c": [1.5, 2.0], "m": {"k": "v"}, "f": True},
+            {"a": None, "b": "x", "c": [], "m": {}, "f": False}]
+    write_avro(str(tmp_path / "r.avro"), schema, recs)
+    assert read_avro(str(tmp_path / "r.avro")) == recs

@@ -252,11 +252,11 @@ class OpWorkflow(OpWorkflowCore):
         return fitted
 
     def compute_data_up_to(self, feature: FeatureLike, params: Optional[OpParams] = None) -> Dataset:
+        """Raw data plus every feature up to and including ``feature`` (``OpWorkflow.scala:491-504``)."""
         raw = self.generate_raw_data(params or self.parameters)
-        dag = compute_dag([feature])
-        dag = [[(st, d) for st, d in layer if st is not feature.origin_stage] for layer in dag]
-        dag = [l for l in dag if l]
-        out, _, _ = fit_and_transform_dag(dag, raw, None)
+        if feature.is_raw:
+            return raw
+        out, _, _ = fit_and_transform_dag(compute_dag([feature]), raw, None)
         return out
 
     def load_model(self, path: str) -> "OpWorkflowModel":
