@@ -23,54 +23,100 @@ def _others(f, others):
 # ------------------------------------------------------------------------------------- generic
 @register(T.FeatureType, "map")
 def _map(self: FeatureLike, fn: Callable, output_type=T.Text, operation_name: str = "map"):
-    st = UnaryTransformer(lambda v: fn(v), operation_name=operation_name, output_type=output_type)
-    return st.set_input(self).get_output()
+    from ..stages.feature.misc_stages import MapTransformer
+    return MapTransformer(fn, output_type, operation_name).set_input(self).get_output()
 
 
 @register(T.FeatureType, "alias")
 def _alias(self, name: str):
-    st = UnaryTransformer(lambda v: v, operation_name="alias", output_type=self.wtype)
-    st.set_input(self)
-    st.set_output_feature_name(name)
-    return st.get_output()
+    from ..stages.feature.misc_stages import AliasTransformer
+    return AliasTransformer(name).set_input(self).get_output()
 
 
 @register(T.FeatureType, "exists")
 def _exists(self, fn: Callable):
-    st = UnaryTransformer(lambda v: None if v is None else bool(fn(v)), operation_name="exists",
-                          output_type=T.Binary)
-    return st.set_input(self).get_output()
+    from ..stages.feature.misc_stages import ExistsTransformer
+    return ExistsTransformer(fn).set_input(self).get_output()
 
 
 @register(T.FeatureType, "filter")
 def _filter(self, fn: Callable, default=None):
-    st = UnaryTransformer(lambda v: v if (v is not None and fn(v)) else default, operation_name="filter",
-                          output_type=self.wtype)
-    return st.set_input(self).get_output()
+    from ..stages.feature.misc_stages import FilterTransformer
+    return FilterTransformer(fn, default).set_input(self).get_output()
 
 
 @register(T.FeatureType, "replace_with")
 def _replace(self, old, new):
-    st = UnaryTransformer(lambda v: new if v == old else v, operation_name="replaceWith", output_type=self.wtype)
-    return st.set_input(self).get_output()
+    from ..stages.feature.misc_stages import ReplaceTransformer
+    return ReplaceTransformer(old_value=old, new_value=new).set_input(self).get_output()
 
 
 @register(T.FeatureType, "to_occur")
 def _to_occur(self, match_fn: Optional[Callable] = None):
-    def occ(v):
-        if match_fn is not None:
-            return 1.0 if (v is not None and match_fn(v)) else 0.0
-        if v is None:
-            return 0.0
-        if isinstance(v, (list, set, frozenset, dict)):
-            return 1.0 if len(v) else 0.0
-        if isinstance(v, (int, float)) and not isinstance(v, bool):
-            return 1.0 if v > 0 else 0.0
-        if isinstance(v, bool):
-            return 1.0 if v else 0.0
-        return 1.0 if str(v) else 0.0
-    st = UnaryTransformer(occ, operation_name="toOccur", output_type=T.RealNN)
-    return st.set_input(self).get_output()
+    from ..stages.feature.misc_stages import ToOccurTransformer
+    return ToOccurTransformer(match_fn).set_input(self).get_output()
+
+
+@register(T.Text, "is_substring")
+def _substring(self, full: FeatureLike, to_lowercase: bool = True):
+    """``self`` is contained in ``full`` (``RichTextFeature.isSubstring``)."""
+    from ..stages.feature.misc_stages import SubstringTransformer
+    return SubstringTransformer(to_lowercase=to_lowercase).set_input(self, full).get_output()
+
+
+@register(T.Text, "to_n_gram_similarity")
+def _ngram_text(self, other: FeatureLike, n_gram_size: int = 3, to_lowercase: bool = True):
+    from ..stages.feature.misc_stages import TextNGramSimilarity
+    return TextNGramSimilarity(n_gram_size=n_gram_size, to_lowercase=to_lowercase).set_input(self, other).get_output()
+
+
+@register(T.MultiPickList, "to_n_gram_similarity")
+def _ngram_set(self, other: FeatureLike, n_gram_size: int = 3, to_lowercase: bool = True):
+    from ..stages.feature.misc_stages import SetNGramSimilarity
+    return SetNGramSimilarity(n_gram_size=n_gram_size, to_lowercase=to_lowercase).set_input(self, other).get_output()
+
+
+@register(T.MultiPickList, "jaccard_similarity")
+def _jaccard(self, other: FeatureLike):
+    from ..stages.feature.misc_stages import JaccardSimilarity
+    return JaccardSimilarity().set_input(self, other).get_output()
+
+
+@register(T.Date, "to_time_period")
+def _time_period(self, period: str):
+    from ..stages.feature.misc_stages import TimePeriodTransformer
+    return TimePeriodTransformer(period=period).set_input(self).get_output()
+
+
+@register(T.DateList, "to_time_period")
+def _time_period_list(self, period: str):
+    from ..stages.feature.misc_stages import TimePeriodListTransformer
+    return TimePeriodListTransformer(period=period).set_input(self).get_output()
+
+
+@register(T.DateMap, "to_time_period")
+def _time_period_map(self, period: str):
+    from ..stages.feature.misc_stages import TimePeriodMapTransformer
+    return TimePeriodMapTransformer(period=period).set_input(self).get_output()
+
+
+@register(T.OPMap, "filter_keys")
+def _filter_map(self, allow_list_keys=(), block_list_keys=(), clean_keys: bool = False, clean_text: bool = False):
+    from ..stages.feature.misc_stages import FilterMap
+    return FilterMap(allow_list_keys=list(allow_list_keys), block_list_keys=list(block_list_keys),
+                     clean_keys=clean_keys, clean_text=clean_text).set_input(self).get_output()
+
+
+@register(T.EmailMap, "to_email_domains")
+def _email_map(self):
+    from ..stages.feature.misc_stages import EmailToPickListMapTransformer
+    return EmailToPickListMapTransformer().set_input(self).get_output()
+
+
+@register(T.URLMap, "to_domains")
+def _url_map(self):
+    from ..stages.feature.misc_stages import UrlMapToPickListMapTransformer
+    return UrlMapToPickListMapTransformer().set_input(self).get_output()
 
 
 # ------------------------------------------------------------------------------------- numeric
