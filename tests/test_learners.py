@@ -1,0 +1,128 @@
+"""Learners: batched fits match single fits, expected numerics vs numpy/sklearn-free references
+(``core/src/test/.../classification/*Test.scala``, ``regression/*Test.scala``)."""
+import numpy as np
+import pytest
+import torch
+
+from transmogrifai_amd.models.base import FitJob, learner_class
+
+
+def _bin(n=600, d=5, seed=0):
+    g = np.random.default_rng(seed)
+    X = g.normal(size=(n, d))
+    w = g.normal(size=d)
+    y = (X @ w + 0.3 * g.normal(size=n) > 0).astype(float)
+    return torch.as_tensor(X), torch.as_tensor(y), w
+
+
+def test_logistic_regression_batched_equals_single():
+    X, y, _ = _bin()
+    L = learner_class("OpLogisticRegression")()
+    jobs = [FitJob({"reg_param": r, "elastic_net_param": e, "max_iter": 100}, torch.arange(0, 600, k))
+            for r, e, k in [(0.01, 0.0, 1), (0.1, 0.5, 2), (0.0, 0.0, 3)]]
+    batch = L.fit_batch(X, y, jobs)
+    for j, b in zip(jobs, batch):
+        s = L.fit_batch(X, y, [j])[0]
+        np.testing.assert_allclose(s["coefficients"], b["coefficients"], atol=1e-6)
+
+
+def test_logistic_regression_unregularized_matches_newton():
+    X, y, _ = _bin(seed=1)
+    L = learner_class("OpLogisticRegression")()
+    st = L.fit(X, y, params={"reg_param": 0.0, "max_iter": 300, "tol": 1e-12})
+    # Newton reference in fp64
+    Xa = np.hstack([X.numpy(), np.ones((600, 1))])
+    b = np.zeros(Xa.shape[1])
+    for _ in range(50):
+        p = 1 / (1 + np.exp(-Xa @ b))
+        H = Xa.T @ (Xa * (p * (1 - p))[:, None])
+        b -= np.linalg.solve(H, Xa.T @ (p - y.numpy()))
+    np.testing.assert_allclose(st["coefficients"], b[:-1], rtol=1e-3, atol=1e-3)
+    assert st["intercept"] == pytest.approx(b[-1], abs=1e-3)
+
+
+def test_multinomial_logistic_regression():
+    g = np.random.default_rng(2)
+    X = g.normal(size=(900, 4))
+    y = np.argmax(X[:, :3] * 2 + g.normal(scale=0.3, size=(900, 3)), 1).astype(float)
+    L = learner_class("OpLogisticRegression")()
+    st = L.fit(torch.as_tensor(X), torch.as_tensor(y), params={"reg_param": 0.001})
+    pred, raw, prob = L.predict(st, torch.as_tensor(X))
+    assert prob.shape == (900, 3) and (pred.numpy() == y).mean() > 0.85
+    assert abs(st["intercepts"].sum()) < 1e-9
+
+
+def test_linear_regression_matches_lstsq():
+    g = np.random.default_rng(3)
+    X = g.normal(size=(500, 4))
+    y = X @ np.array([1.0, -2.0, 0.5, 3.0]) + 4.0 + 0.01 * g.normal(size=500)
+    L = learner_class("OpLinearRegression")()
+    st = L.fit(torch.as_tensor(X), torch.as_tensor(y), params={"reg_param": 0.0, "max_iter": 200, "tol": 1e-12})
+    ref = np.linalg.lstsq(np.hstack([X, np.ones((500, 1))]), y, rcond=None)[0]
+    np.testing.assert_allclose(st["coefficients"], ref[:4], atol=1e-3)
+
+
+@pytest.mark.parametrize("family,link", [("gaussian", None), ("poisson", None), ("binomial", "logit"),
+                                         ("gamma", "log")])
+def test_glm_families(family, link):
+    g = np.random.default_rng(4)
+    X = g.normal(size=(800, 3)) * 0.5
+    eta = X @ np.array([0.5, -0.3, 0.2]) + 0.4
+    if family == "gaussian":
+        y = eta + 0.05 * g.normal(size=800)
+    elif family == "poisson":
+        y = g.poisson(np.exp(eta)).astype(float)
+    elif family == "binomial":
+        y = (g.random(800) < 1 / (1 + np.exp(-eta))).astype(float)
+    else:
+        y = g.gamma(5.0, np.exp(eta) / 5.0)
+    L = learner_class("OpGeneralizedLinearRegression")()
+    st = L.fit(torch.as_tensor(X), torch.as_tensor(y), params={"family": family, "link": link})
+    np.testing.assert_allclose(st["coefficients"], [0.5, -0.3, 0.2], atol=0.2)
+    mu, _, _ = L.predict(st, torch.as_tensor(X))
+    assert torch.isfinite(mu).all()
+
+
+def test_glm_invalid_link_fails():
+    X, y, _ = _bin()
+    with pytest.raises(ValueError):
+        learner_class("OpGeneralizedLinearRegression")().fit(X, y, params={"family": "poisson", "link": "logit"})
+
+
+def test_mlp_learns_xor_like():
+    g = np.random.default_rng(5)
+    X = g.uniform(-1, 1, size=(400, 2))
+    y = ((X[:, 0] > 0) ^ (X[:, 1] > 0)).astype(float)
+    L = learner_class("OpMultilayerPerceptronClassifier")()
+    st = L.fit(torch.as_tensor(X, dtype=torch.float32), torch.as_tensor(y),
+               params={"layers": [2, 8, 2], "max_iter": 300, "seed": 1})
+    pred, raw, prob = L.predict(st, torch.as_tensor(X, dtype=torch.float32))
+    assert (pred.numpy() == y).mean() > 0.9
+
+
+@pytest.mark.parametrize("name", ["OpRandomForestClassifier", "OpGBTClassifier", "OpDecisionTreeClassifier",
+                                  "OpXGBoostClassifier", "OpNaiveBayes", "OpLinearSVC"])
+def test_classifiers_beat_chance(name):
+    X, y, _ = _bin(n=800, seed=6)
+    if name == "OpNaiveBayes":   # multinomial NB needs count features with class-dependent rates
+        g = np.random.default_rng(6)
+        lam = np.where(y.numpy()[:, None] > 0, [5.0, 1.0, 3.0], [1.0, 5.0, 3.0])
+        X = torch.as_tensor(g.poisson(lam).astype(float))
+    L = learner_class(name)()
+    tr, te = torch.arange(0, 600), torch.arange(600, 800)
+    st = L.fit_batch(X, y, [FitJob(dict(L.defaults), tr)])[0]
+    pred, raw, prob = L.predict(st, X[te])
+    assert (pred.numpy() == y[te].numpy()).mean() > 0.7
+
+
+@pytest.mark.parametrize("name", ["OpRandomForestRegressor", "OpGBTRegressor", "OpDecisionTreeRegressor",
+                                  "OpXGBoostRegressor"])
+def test_regressors_fit(name):
+    g = np.random.default_rng(7)
+    X = torch.as_tensor(g.normal(size=(800, 3)))
+    y = torch.as_tensor(np.sin(X[:, 0].numpy()) * 2 + X[:, 1].numpy())
+    L = learner_class(name)()
+    st = L.fit_batch(X, y, [FitJob(dict(L.defaults), torch.arange(600))])[0]
+    pred, _, _ = L.predict(st, X[600:])
+    r2 = 1 - ((pred - y[600:]) ** 2).sum() / ((y[600:] - y[600:].mean()) ** 2).sum()
+    assert float(r2) > 0.6

@@ -38,7 +38,7 @@ def register_learner(cls):
 
 
 def _load_all():
-    from . import linear, trees  # noqa: F401  (registers every learner)
+    from . import glm, linear, mlp, trees  # noqa: F401  (registers every learner)
 
 
 def learner_class(name: str):

@@ -84,6 +84,66 @@ class BatchedObjective:
         return f, g
 
 
+class MultinomialObjective:
+    """Softmax cross-entropy of P problems with K classes; ``U`` is ``[(d+1)*K, P]`` laid out as
+    ``[d+1, K]`` blocks (class-major coefficient columns), so the batched OWL-QN is reused unchanged.
+    One GEMM ``X [N,d] @ V [d, P*K]`` produces every problem's class margins."""
+
+    def __init__(self, X, y, W, inv_std, l2, fit_intercept, K):
+        self.X, self.W, self.K = X, W, K
+        self.Y = torch.nn.functional.one_hot(y.to(torch.int64), K).to(X.dtype)      # [N, K]
+        self.wsum = W.sum(0).to(torch.float64).clamp_min(1e-300)
+        self.inv_std = inv_std      # [d, P]
+        self.l2, self.fi = l2, fit_intercept
+        self.d = X.shape[1]
+        self.passes = 0
+
+    def _split(self, U):
+        d, K = self.d, self.K
+        P = U.shape[1]
+        B = U.reshape(d + 1, K, P)
+        V = B[:d] * self.inv_std[:, None, :]                                       # [d, K, P]
+        b = torch.where(self.fi[None, :], B[d], torch.zeros_like(B[d]))            # [K, P]
+        return B, V, b
+
+    def margins(self, U):
+        B, V, b = self._split(U)
+        P = U.shape[1]
+        M = LK.gemm(self.X, V.permute(0, 2, 1).reshape(self.d, P * self.K).to(self.X.dtype))
+        self.passes += 1
+        return M.reshape(-1, P, self.K) + b.t()[None, :, :].to(M.dtype)          # [N, P, K]
+
+    def _loss(self, M):
+        lse = torch.logsumexp(M, 2)                                                # [N, P]
+        l = lse - (M * self.Y[:, None, :]).sum(2)
+        return l, lse
+
+    def value(self, U):
+        M = self.margins(U)
+        l, _ = self._loss(M)
+        f = (l * self.W).sum(0).to(torch.float64) / self.wsum
+        B = U.reshape(self.d + 1, self.K, -1)
+        return f + 0.5 * self.l2 * (B[:self.d] ** 2).sum((0, 1))
+
+    def value_grad(self, U):
+        M = self.margins(U)
+        l, lse = self._loss(M)
+        Pr = torch.exp(M - lse[:, :, None])
+        R = (Pr - self.Y[:, None, :]) * self.W[:, :, None]                        # [N, P, K]
+        P = U.shape[1]
+        f = (l * self.W).sum(0).to(torch.float64) / self.wsum
+        G = LK.gemm_t(self.X, R.reshape(-1, P * self.K)).to(torch.float64).reshape(self.d, P, self.K)
+        G = G.permute(0, 2, 1) / self.wsum[None, None, :]                          # [d, K, P]
+        self.passes += 1
+        B = U.reshape(self.d + 1, self.K, P)
+        g = torch.zeros_like(B)
+        g[:self.d] = G * self.inv_std[:, None, :] + self.l2[None, None, :] * B[:self.d]
+        gb = R.sum(0).to(torch.float64).t() / self.wsum[None, :]                  # [K, P]
+        g[self.d] = torch.where(self.fi[None, :], gb, torch.zeros_like(gb))
+        f = f + 0.5 * self.l2 * (B[:self.d] ** 2).sum((0, 1))
+        return f, g.reshape(U.shape)
+
+
 def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max_iter: torch.Tensor,
                   tol: torch.Tensor, m: int = 10, max_ls: int = 30):
     """Batched OWL-QN (L-BFGS when ``l1 == 0``) over the columns of ``U``.
@@ -220,12 +280,39 @@ class LogisticRegressionLearner(_LinearBase):
                 "standardization": True, "tol": 1e-6, "threshold": 0.5}
     loss = "logistic"
 
+    def _fit_multinomial(self, X, y, jobs, K):
+        """Spark ``family=multinomial`` (chosen by ``auto`` when there are more than 2 classes)."""
+        dev = X.device
+        N, d = X.shape
+        P = len(jobs)
+        W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs)
+        l2 = reg * (1 - en)
+        obj = MultinomialObjective(X, y, W, inv_std, l2, fi, K)
+        U0 = torch.zeros(d + 1, K, P, dtype=torch.float64, device=dev)
+        cnt = torch.stack([(W * (y == k)[:, None].to(W.dtype)).sum(0) for k in range(K)]).to(torch.float64)
+        pri = (cnt / cnt.sum(0, keepdim=True).clamp_min(1e-300)).clamp_min(1e-12)
+        lp = torch.log(pri)
+        U0[d] = torch.where(fi[None, :], lp - lp.mean(0, keepdim=True), torch.zeros_like(lp))
+        l1 = torch.zeros(d + 1, K, P, dtype=torch.float64, device=dev)
+        l1[:d] = (reg * en)[None, None, :]
+        U, iters, F = owlqn_batched(obj, U0.reshape(-1, P), l1.reshape(-1, P), max_iter, tol)
+        B = U.reshape(d + 1, K, P)
+        coef = (B[:d] * inv_std[:, None, :]).permute(2, 1, 0).cpu().numpy()          # [P, K, d]
+        icpt = torch.where(fi[None, :], B[d], torch.zeros_like(B[d]))
+        icpt = (icpt - icpt.mean(0, keepdim=True)).t().cpu().numpy()                 # centered, [P, K]
+        it = iters.cpu().numpy()
+        return [{"coefficient_matrix": coef[p].copy(), "intercepts": icpt[p].copy(), "n_iter": int(it[p]),
+                 "n_classes": K} for p in range(P)]
+
     def fit_batch(self, X, y, jobs, context=None):
         dev = X.device
         N, d = X.shape
         P = len(jobs)
         if P == 0:
             return []
+        K = int(y.max().item()) + 1 if y.numel() else 2
+        if self.loss == "logistic" and K > 2:
+            return self._fit_multinomial(X, y, jobs, K)
         W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs)
         l2 = reg * (1 - en)
         l1v = reg * en
@@ -249,12 +336,24 @@ class LogisticRegressionLearner(_LinearBase):
         c = torch.as_tensor(state["coefficients"], dtype=X.dtype, device=X.device)
         return (X @ c).to(torch.float64) + state["intercept"]
 
+    @staticmethod
+    def _multinomial_outputs(state, X):
+        C = torch.as_tensor(state["coefficient_matrix"], dtype=X.dtype, device=X.device)     # [K, d]
+        b = torch.as_tensor(state["intercepts"], dtype=torch.float64, device=X.device)
+        raw = (X @ C.t()).to(torch.float64) + b[None, :]
+        prob = torch.softmax(raw, 1)
+        return torch.argmax(raw, 1).to(torch.float64), raw, prob
+
     def predict(self, state, X, context=None):
+        if "coefficient_matrix" in state:
+            return self._multinomial_outputs(state, X)
         return probability_outputs(self.margin(state, X), threshold=state.get("threshold", 0.5))
 
     def predict_batch(self, states, X, rows, context=None):
         if not states:
             return []
+        if any("coefficient_matrix" in s for s in states):
+            return Learner.predict_batch(self, states, X, rows, context)
         C = torch.as_tensor(np.stack([s["coefficients"] for s in states], 1), dtype=X.dtype, device=X.device)
         b = torch.as_tensor([s["intercept"] for s in states], dtype=torch.float64, device=X.device)
         M = LK.gemm(X, C).to(torch.float64) + b[None, :]
@@ -265,6 +364,8 @@ class LogisticRegressionLearner(_LinearBase):
         return out
 
     def feature_contributions(self, state, d):
+        if "coefficient_matrix" in state:
+            return np.asarray(state["coefficient_matrix"], np.float64)
         return np.asarray(state["coefficients"], np.float64)
 
 
