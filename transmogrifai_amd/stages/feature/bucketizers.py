@@ -100,3 +100,73 @@ class DecisionTreeNumericBucketizer(BinaryEstimator):
             self.get_output_feature_name(), cols,
             {t.name: FeatureHistory(tuple(t.origin_features), tuple(t.stages) + (self.stage_name(),))})
         return DecisionTreeNumericBucketizerModel(should, final, p["track_nulls"], should and p["track_invalid"])
+
+
+# ------------------------------------------------------------------------------------ map variant
+@register_stage
+class DecisionTreeNumericMapBucketizerModel(BinaryTransformer):
+    operation_name = "dtNumMapBuck"
+    output_type = T.OPVector
+    allow_label_as_input = True
+
+    def __init__(self, keys=None, splits=None, track_nulls=True, uid=None, **kw):
+        super().__init__(None, uid=uid, **kw)
+        self.keys = list(keys or [])
+        self.splits = [list(s) for s in (splits or [])]
+        self.track_nulls = track_nulls
+
+    def transform_columns(self, label, m, ds=None):
+        vals = m.to_list()
+        dtype = vector_dtype(torch.device("cpu"))
+        blocks = []
+        for k, sp in zip(self.keys, self.splits):
+            x = torch.as_tensor([float(r[k]) if (r and r.get(k) is not None) else 0.0 for r in vals],
+                                dtype=torch.float64)
+            ok = torch.as_tensor([bool(r) and r.get(k) is not None for r in vals], dtype=torch.bool)
+            if sp:
+                blocks.append(bucketize_column(x, ok, sp, self.track_nulls, False, "Right", dtype))
+            elif self.track_nulls:
+                blocks.append((~ok).to(dtype)[:, None])
+        out = torch.cat(blocks, 1) if blocks else torch.zeros(len(vals), 0, dtype=dtype)
+        return VectorColumn(out, self.metadata.get("vector_metadata"))
+
+    def ctor_args(self):
+        return {"keys": self.keys, "splits": self.splits, "trackNulls": self.track_nulls}
+
+    def load_ctor_args(self, a):
+        self.keys, self.splits, self.track_nulls = list(a["keys"]), [list(s) for s in a["splits"]], a["trackNulls"]
+
+
+@register_stage
+class DecisionTreeNumericMapBucketizer(BinaryEstimator):
+    """One label-aware tree per numeric map key (``DecisionTreeNumericMapBucketizer.scala:56-170``)."""
+    operation_name = "dtNumMapBuck"
+    output_type = T.OPVector
+    allow_label_as_input = True
+    _defaults = dict(DecisionTreeNumericBucketizer._defaults)
+
+    def fit_columns(self, label, m, ds=None):
+        from ...data.vector_metadata import OpVectorColumnMetadata, NULL_STRING
+        p = self.params
+        vals = m.to_list()
+        y_all = label.values.to(torch.float64).cpu()
+        keys = sorted({k for r in vals for k, v in (r or {}).items() if v is not None})
+        t = self.get_transient_features()[1]
+        splits, cols = [], []
+        for k in keys:
+            rows = [i for i, r in enumerate(vals) if r and r.get(k) is not None]
+            x = torch.as_tensor([float(vals[i][k]) for i in rows], dtype=torch.float64)
+            sp = tree_splits(x, y_all[rows], p["max_depth"], p["max_bins"], p["min_instances_per_node"],
+                             p["min_info_gain"], p["impurity"])
+            full = [float("-inf")] + sp + [float("inf")]
+            ok = check_splits(full)
+            splits.append(full if ok else [])
+            if ok:
+                for lab in bucket_labels(full, "Right"):
+                    cols.append(OpVectorColumnMetadata((t.name,), (t.type_name,), k, lab))
+            if p["track_nulls"]:
+                cols.append(OpVectorColumnMetadata((t.name,), (t.type_name,), k, NULL_STRING))
+        self.metadata["vector_metadata"] = OpVectorMetadata(
+            self.get_output_feature_name(), cols,
+            {t.name: FeatureHistory(tuple(t.origin_features), tuple(t.stages) + (self.stage_name(),))})
+        return DecisionTreeNumericMapBucketizerModel(keys, splits, p["track_nulls"])

@@ -257,3 +257,164 @@ def map_vectorize(t, feats, label, D) -> list:
                        max_cardinality=D.MaxCategoricalCardinality, num_features=D.DefaultNumOfFeatures,
                        fill_value=float(D.FillValue))
     return [st.set_input(feats).get_output()]
+
+
+# ---------------------------------------------------------------------- named map vectorizers (catalog)
+def _named(name: str, op: str, kind: str):
+    cls = type(name, (MapVectorizer,), {"operation_name": op, "_defaults": dict(MapVectorizer._defaults, kind=kind),
+                                        "__doc__": f"``{name}`` (kind={kind!r}) of ``OPMapVectorizer.scala``."})
+    return register_stage(cls)
+
+
+RealMapVectorizer = _named("RealMapVectorizer", "vecRealMap", "real")
+IntegralMapVectorizer = _named("IntegralMapVectorizer", "vecIntMap", "integral")
+BinaryMapVectorizer = _named("BinaryMapVectorizer", "vecBinMap", "binary")
+DateMapVectorizer = _named("DateMapVectorizer", "vecDateMap", "date")
+TextMapPivotVectorizer = _named("TextMapPivotVectorizer", "vecPivotTextMap", "pivot")
+SmartTextMapVectorizer = _named("SmartTextMapVectorizer", "smartTxtMapVec", "smarttext")
+MultiPickListMapVectorizer = _named("MultiPickListMapVectorizer", "vecCatMap", "set")
+GeolocationMapVectorizer = _named("GeolocationMapVectorizer", "vecGeoMap", "geo")
+
+
+@register_stage
+class TextMapHashingVectorizer(MapVectorizer):
+    """Hash every key's tokens (``TextMapHashingVectorizer`` of ``OPMapVectorizer.scala``)."""
+    operation_name = "vecHashTextMap"
+    _defaults = dict(MapVectorizer._defaults, kind="smarttext", max_cardinality=-1)
+
+
+# ------------------------------------------------------------------------ date map unit circle
+@register_stage
+class DateMapToUnitCircleVectorizerModel(VectorizerMixin, SequenceTransformer):
+    operation_name = "dateMapToUnitCircle"
+
+    def __init__(self, keys=None, time_period="HourOfDay", uid=None, **kw):
+        super().__init__(uid=uid, **kw)
+        self.keys = [list(k) for k in (keys or [])]
+        self.time_period = time_period
+
+    def transform_columns(self, *cols, ds=None):
+        from ...utils.dates import period_values
+        n = len(cols[0]) if cols else 0
+        blocks = []
+        for ci, c in enumerate(cols):
+            vals = c.to_list()
+            keys = self.keys[ci]
+            b = np.zeros((n, 2 * len(keys)))
+            for j, k in enumerate(keys):
+                rows = [r for r, m in enumerate(vals) if m and m.get(k) is not None]
+                if not rows:
+                    continue
+                ms = torch.as_tensor([int(vals[r][k]) for r in rows], dtype=torch.int64)
+                v, size = period_values(ms, self.time_period)
+                rad = 2 * np.pi * v.to(torch.float64).numpy() / size
+                b[rows, 2 * j] = np.cos(rad)
+                b[rows, 2 * j + 1] = np.sin(rad)
+            blocks.append(b)
+        dev = cols[0].device if cols else torch.device("cpu")
+        out = np.concatenate(blocks, 1) if blocks else np.zeros((n, 0))
+        return self._vec(torch.as_tensor(out, dtype=vector_dtype(dev), device=dev))
+
+    def ctor_args(self):
+        return {"keys": self.keys, "timePeriod": self.time_period}
+
+    def load_ctor_args(self, a):
+        self.keys, self.time_period = [list(k) for k in a["keys"]], a["timePeriod"]
+
+
+@register_stage
+class DateMapToUnitCircleVectorizer(VectorizerMixin, SequenceEstimator):
+    """(cos, sin) of a time period per map key (``DateMapToUnitCircleVectorizer.scala:63-134``)."""
+    operation_name = "dateMapToUnitCircle"
+    _defaults = {"time_period": "HourOfDay", "clean_keys": False}
+
+    def fit_columns(self, *cols, ds=None):
+        all_keys, colsm = [], []
+        tp = self.params["time_period"]
+        for c, t in zip(cols, self.get_transient_features()):
+            keys = sorted({k for m in c.to_list() for k, v in (m or {}).items() if v is not None})
+            all_keys.append(keys)
+            for k in keys:
+                for d in ("x", "y"):
+                    colsm.append(OpVectorColumnMetadata((t.name,), (t.type_name,), k, None, f"{d}_{tp}"))
+        self.metadata["vector_metadata"] = self.vector_metadata(colsm)
+        return DateMapToUnitCircleVectorizerModel(all_keys, tp)
+
+
+# ------------------------------------------------------------------------ text map length / null
+@register_stage
+class TextMapLenModel(VectorizerMixin, SequenceTransformer):
+    operation_name = "textMapLen"
+
+    def __init__(self, keys=None, clean_keys=False, uid=None, **kw):
+        super().__init__(uid=uid, **kw)
+        self.keys = [list(k) for k in (keys or [])]
+        self.clean_keys = clean_keys
+
+    def _block(self, ci, vals, fn):
+        keys = self.keys[ci]
+        b = np.zeros((len(vals), len(keys)))
+        for r, m in enumerate(vals):
+            for j, k in enumerate(keys):
+                b[r, j] = fn(_get(m, k, self.clean_keys))
+        return b
+
+    def _len(self, v):
+        return float(sum(len(t) for t in TU.tokenize(v))) if isinstance(v, str) else 0.0
+
+    def transform_columns(self, *cols, ds=None):
+        n = len(cols[0]) if cols else 0
+        blocks = [self._block(ci, c.to_list(), self._len) for ci, c in enumerate(cols)]
+        dev = cols[0].device if cols else torch.device("cpu")
+        out = np.concatenate(blocks, 1) if blocks else np.zeros((n, 0))
+        return self._vec(torch.as_tensor(out, dtype=vector_dtype(dev), device=dev))
+
+    def ctor_args(self):
+        return {"keys": self.keys, "cleanKeys": self.clean_keys}
+
+    def load_ctor_args(self, a):
+        self.keys, self.clean_keys = [list(k) for k in a["keys"]], a["cleanKeys"]
+
+
+@register_stage
+class TextMapNullModel(TextMapLenModel):
+    operation_name = "textMapNull"
+
+    def _len(self, v):
+        return 0.0 if isinstance(v, str) and v else 1.0
+
+
+class _TextMapKeysEstimator(VectorizerMixin, SequenceEstimator):
+    model_cls = TextMapLenModel
+    descriptor = "TextLen"
+    _defaults = {"clean_keys": False}
+
+    def fit_columns(self, *cols, ds=None):
+        all_keys, colsm = [], []
+        for c, t in zip(cols, self.get_transient_features()):
+            keys = sorted({_clean_key(k, self.params["clean_keys"]) for m in c.to_list()
+                           for k, v in (m or {}).items() if v is not None})
+            all_keys.append(keys)
+            for k in keys:
+                if self.descriptor == "TextLen":
+                    colsm.append(OpVectorColumnMetadata((t.name,), (t.type_name,), k, None, "TextLen"))
+                else:
+                    colsm.append(OpVectorColumnMetadata((t.name,), (t.type_name,), k, NULL_STRING))
+        self.metadata["vector_metadata"] = self.vector_metadata(colsm)
+        return self.model_cls(all_keys, self.params["clean_keys"])
+
+
+@register_stage
+class TextMapLenEstimator(_TextMapKeysEstimator):
+    """Token-length per text-map key (``TextMapLenEstimator.scala``)."""
+    operation_name = "textMapLen"
+    model_cls = TextMapLenModel
+    descriptor = "TextLen"
+
+
+@register_stage
+class TextMapNullEstimator(_TextMapKeysEstimator):
+    """Null indicator per text-map key (``TextMapNullEstimator.scala``)."""
+    operation_name = "textMapNull"
+    model_cls = TextMapNullModel
+    descriptor = "Null"
