@@ -33,23 +33,50 @@ struct HistItem {
   int64_t count;    // row entries in this chunk
 };
 
+// Per-row statistics staged for the whole wave: (entry bits, s0, s1, s2)
+//   MODE 0 (class counts):   s0 = w, s1 = class
+//   MODE 1 (variance stats): s0 = w, s1 = w*t, s2 = w*t*t
+//   MODE 2 (grad / hess):    s0 = w*g, s1 = w*h
 template <int MODE>
-__device__ __forceinline__ void row_stats(int64_t r, float w, int64_t model, int64_t stride, const float* __restrict__ y,
-                                          const float* __restrict__ t1, const float* __restrict__ t2, int S, int cls_lane,
-                                          float* st) {
+__device__ __forceinline__ float4 stage_row(uint32_t e, int64_t model, int64_t stride, const float* __restrict__ y,
+                                            const float* __restrict__ t1, const float* __restrict__ t2) {
+  const int64_t r = e & 0xFFFFFFu;
+  const float w = (float)(e >> 24);
+  float4 s;
+  s.x = __uint_as_float(e);
   if (MODE == 0) {
-    // classification: only the label slot is non-zero; kept as (class, w)
-    st[0] = w;
-    st[1] = y[r];
+    s.y = w; s.z = y[r]; s.w = 0.f;
   } else if (MODE == 1) {
     const float t = t1[model * stride + r];
-    st[0] = w; st[1] = w * t; st[2] = w * t * t;
+    s.y = w; s.z = w * t; s.w = w * t * t;
   } else {
-    st[0] = w * t1[model * stride + r];
-    st[1] = w * t2[model * stride + r];
+    s.y = w * t1[model * stride + r]; s.z = w * t2[model * stride + r]; s.w = 0.f;
+  }
+  return s;
+}
+
+template <int MODE>
+__device__ __forceinline__ void add_row(float* my, int bin, int S, const float4& st) {
+  if (MODE == 0) {
+    atomicAdd(my + bin * S + (int)st.z, st.y);
+  } else if (MODE == 1) {
+    float* hb = my + bin * 3;
+    atomicAdd(hb, st.y); atomicAdd(hb + 1, st.z); atomicAdd(hb + 2, st.w);
+  } else {
+    float* hb = my + bin * 2;
+    atomicAdd(hb, st.y); atomicAdd(hb + 1, st.z);
   }
 }
 
+// Histogram build. Latency structure (the kernel is gather-latency bound, not LDS bound):
+//  1. each wave takes 64 row entries at once -- one coalesced load of the packed (row, weight) list --
+//     and every lane gathers the statistics of *its* row (64 independent gathers in flight);
+//  2. the 64 (entry, stats) records are staged in a wave-private LDS slot (one ds_write_b128 per lane);
+//  3. lane (row-slot rsub, feature fidx) then walks the staged rows R at a time, 8 rows unrolled:
+//     8 broadcast ds_read_b128 of the records, 8 *independent* bin gathers Xb[row*F + feat] in flight,
+//     then the LDS atomics into the lane's private (row-slot, feature) histogram row.
+// Lanes of one atomic instruction always address different histogram rows (distinct features or
+// row slots), so the atomics never conflict.
 template <int MODE>
 __global__ void __launch_bounds__(256) hist_build_kernel(
     const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const HistItem* __restrict__ items,
@@ -62,12 +89,13 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   const int R = 64 / FG;
   const int rowstride = B * S + 1;            // padded feature row
   const int ncopy_words = R * FG * rowstride;  // <= 64 * rowstride
-  for (int i = threadIdx.x; i < ncopy_words; i += blockDim.x) lds[i] = 0.f;
-  __syncthreads();
-
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
+  float4* stage = reinterpret_cast<float4*>(lds + ((ncopy_words + 3) & ~3)) + wave * 64;
+  for (int i = threadIdx.x; i < ncopy_words; i += blockDim.x) lds[i] = 0.f;
+  __syncthreads();
+
   const int rsub = lane / FG;
   const int fidx = lane - rsub * FG;
   const bool active = rsub < R;
@@ -76,52 +104,29 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   float* my = lds + (rsub * FG + fidx) * rowstride;
   const uint32_t* rp = rows + it.begin;
   const int64_t cnt = it.count;
-  const int64_t step = (int64_t)nwaves * R;
 
-  // 4 rows in flight per lane to overlap the dependent (entry -> bin) gathers
-  int64_t i = (int64_t)wave * R + rsub;
-  for (; i + 3 * step < cnt; i += 4 * step) {
-    uint32_t e[4];
-    int bin[4];
+  // Loads are never predicated (a masked "load or skip" makes hipcc branch around every load and wait
+  // vmcnt(0) per element): out-of-range slots read a valid dummy record and are masked at the atomic.
+  for (int64_t base = (int64_t)wave * 64; base < cnt; base += (int64_t)nwaves * 64) {
+    const int64_t ri = min(base + lane, cnt - 1);
+    const int nrows = (int)min((int64_t)64, cnt - base);
+    float4 mine = stage_row<MODE>(rp[ri], model, stride, y, t1, t2);
+    stage[lane] = mine;
+    __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0): staged records visible to the wave
+    __builtin_amdgcn_wave_barrier();
+    for (int j0 = 0; j0 < nrows; j0 += R * 8) {
+      float4 st[8];
+      int bin[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) e[u] = active ? rp[i + u * step] : 0u;
+      for (int u = 0; u < 8; ++u) st[u] = stage[min(j0 + u * R + rsub, 63)];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) bin[u] = active ? (int)Xb[(int64_t)(e[u] & 0xFFFFFFu) * F + feat] : 0;
+      for (int u = 0; u < 8; ++u)
+        bin[u] = (int)Xb[(int64_t)(__float_as_uint(st[u].x) & 0xFFFFFFu) * F + feat];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (!active) continue;
-      const int64_t r = e[u] & 0xFFFFFFu;
-      const float w = (float)(e[u] >> 24);
-      float st[3];
-      row_stats<MODE>(r, w, model, stride, y, t1, t2, S, 0, st);
-      if (MODE == 0) {
-        atomicAdd(my + bin[u] * S + (int)st[1], st[0]);
-      } else if (MODE == 1) {
-        float* hb = my + bin[u] * 3;
-        atomicAdd(hb, st[0]); atomicAdd(hb + 1, st[1]); atomicAdd(hb + 2, st[2]);
-      } else {
-        float* hb = my + bin[u] * 2;
-        atomicAdd(hb, st[0]); atomicAdd(hb + 1, st[1]);
-      }
+      for (int u = 0; u < 8; ++u)
+        if (active && j0 + u * R + rsub < nrows) add_row<MODE>(my, bin[u], S, st[u]);
     }
-  }
-  for (; i < cnt; i += step) {
-    if (!active) continue;
-    const uint32_t e = rp[i];
-    const int64_t r = e & 0xFFFFFFu;
-    const int bin = Xb[r * F + feat];
-    const float w = (float)(e >> 24);
-    float st[3];
-    row_stats<MODE>(r, w, model, stride, y, t1, t2, S, 0, st);
-    if (MODE == 0) {
-      atomicAdd(my + bin * S + (int)st[1], st[0]);
-    } else if (MODE == 1) {
-      float* hb = my + bin * 3;
-      atomicAdd(hb, st[0]); atomicAdd(hb + 1, st[1]); atomicAdd(hb + 2, st[2]);
-    } else {
-      float* hb = my + bin * 2;
-      atomicAdd(hb, st[0]); atomicAdd(hb + 1, st[1]);
-    }
+    __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
 
@@ -423,7 +428,7 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, float* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, hipStream_t stream) {
   if (n_items == 0) return 0;
-  const size_t lds = (size_t)64 * (B * S + 1) * sizeof(float);
+  const size_t lds = (size_t)(((64 * (B * S + 1)) + 3) & ~3) * sizeof(float) + 4 * 64 * sizeof(float4);
   if (lds > 160 * 1024) return -2;
   const HistItem* it = (const HistItem*)items;
   dim3 grid(n_items), block(256);
