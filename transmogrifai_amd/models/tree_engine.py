@@ -262,6 +262,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         lv_begin[1:] = np.cumsum(lv_count[:-1])
     max_depth = int(P_depth.max()) if T else 0
 
+    qscale, qinv = _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev)
     prev_hist = None          # previous level's histogram buffer
     pair_parent_off = None    # per sibling pair: parent's offset in prev_hist
     for depth in range(max_depth + 1):
@@ -283,7 +284,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         hoff = np.zeros(m, np.int64)
         if m > 1:
             hoff[1:] = np.cumsum(hsz[:-1])
-        hist = torch.zeros(int(hsz.sum()), dtype=torch.float32, device=dev)
+        hist = torch.zeros(int(hsz.sum()), dtype=torch.int64, device=dev)
         loc = np.full(n, -1, np.int64)
         loc[hist_nodes] = np.arange(m)
 
@@ -318,7 +319,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 N.check(N.hip().tmog_hip_hist_build(
                     N.ptr(Xb), F, N.ptr(rows), N.ptr(it_t), len(items), N.ptr(nfo), N.ptr(feat_list),
                     N.ptr(nmd), N.ptr(nho), N.ptr(hist), B, mode, S, N.ptr(yf), N.ptr(t1f), N.ptr(t2f),
-                    stride, N.stream(dev)), "hist_build")
+                    stride, N.ptr(qscale), N.stream(dev)), "hist_build")
             if derive_big.size:
                 par = torch.as_tensor(derive_poff, device=dev)
                 sm = torch.as_tensor(hoff[derive_small], device=dev)
@@ -335,7 +336,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 N.check(N.host().tmog_hist_build_cpu(
                     N.ptr(Xb), Nrows, F, N.ptr(rows), int(build_local.size), N.ptr(keep[0]), N.ptr(keep[1]),
                     N.ptr(keep[2]), N.ptr(keep[3]), N.ptr(feat_list), N.ptr(keep[4]), N.ptr(keep[5]), N.ptr(hist), B,
-                    mode, S, N.ptr(yf), N.ptr(t1f), N.ptr(t2f), stride), "hist_build_cpu")
+                    mode, S, N.ptr(yf), N.ptr(t1f), N.ptr(t2f), stride, N.ptr(qscale)), "hist_build_cpu")
             for b_, s_, p_ in zip(derive_big, derive_small, derive_poff):
                 sz = int(hsz[b_])
                 hist[hoff[b_]:hoff[b_] + sz] = prev_hist[p_:p_ + sz] - hist[hoff[s_]:hoff[s_] + sz]
@@ -357,7 +358,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         fn = N.hip().tmog_hip_split_find if on_gpu else N.host().tmog_split_find_cpu
         extra = (N.stream(dev),) if on_gpu else ()
         N.check(fn(N.ptr(hist), m, N.ptr(nho), N.ptr(nnf), N.ptr(nfo), N.ptr(feat_list), N.ptr(n_bins_t), B, S,
-                   kind, N.ptr(par_t), missing_bin, N.ptr(s_feat), N.ptr(s_bin), N.ptr(s_gain), N.ptr(s_dl),
+                   kind, N.ptr(par_t), missing_bin, N.ptr(nmd), N.ptr(qinv), N.ptr(s_feat), N.ptr(s_bin), N.ptr(s_gain), N.ptr(s_dl),
                    N.ptr(s_left), N.ptr(s_tot), *extra), "split_find")
         eps = torch.as_tensor(P_eps[h_tree].astype(np.float32), device=dev)
         can_t = torch.as_tensor(can[hist_nodes], device=dev)
@@ -431,6 +432,38 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         lv_tree, lv_gid, lv_begin, lv_count = ch_tree, ch, new_begin, new_count
 
     return _finalize(jobs, G, mode, kind, K, S, missing_bin)
+
+
+def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev):
+    """Per-(model, stat) power-of-two fixed-point scales for the int64 histograms (see the
+    "Fixed-point statistics" note in ops/csrc/hip/tree_kernels.hip). A row's contribution is
+    ``rint(v * scale)`` with ``|v * scale| <= qmax``, so a ``chunk_rows``-row LDS partial fits int32.
+    Computed on the device (no host sync); returns (float32 scales, float64 inverses), ``[n_models, S]``."""
+    n_models = max([j.model for j in jobs], default=0) + 1
+    if mode == MODE_CLS or rows.numel() == 0:
+        one = torch.ones(n_models, S, dtype=torch.float32, device=dev)
+        return one, one.to(torch.float64)
+    qmax = float(min(1 << 22, (2 ** 31 - 1) // max(1, int(chunk_rows)) - 1))
+    wmax = ((rows >> 24) & 0xFF).max().to(torch.float32)
+
+    def amax(t):
+        if t is None:
+            return torch.zeros(n_models, dtype=torch.float32, device=dev)
+        v = t.reshape(t.shape[0], -1) if t.dim() == 2 else t.reshape(1, -1)
+        m = v.abs().amax(1)
+        return m.expand(n_models) if m.numel() == 1 else m[:n_models]
+
+    def pow2(bound):
+        x = qmax / (bound * wmax).clamp_min(1e-30)
+        return torch.exp2(torch.floor(torch.log2(x))).clamp(2.0 ** -60, 2.0 ** 60)
+
+    if mode == MODE_VAR:
+        m1 = amax(t1f)
+        sc = torch.stack([torch.ones_like(m1), pow2(m1), pow2(m1 * m1)], 1)
+    else:
+        sc = torch.stack([pow2(amax(t1f)), pow2(amax(t2f))], 1)
+    sc = sc.to(torch.float32).contiguous()
+    return sc, (1.0 / sc.to(torch.float64)).contiguous()
 
 
 def _hist_items(build_local, begin, count, nfeat, chunk_rows):

@@ -27,8 +27,8 @@ I64 = C.c_int64
 F32 = C.c_float
 
 _HOST_SIGS = {
-    "tmog_hist_build_cpu": [P, I64, I32, P, I32, P, P, P, P, P, P, P, P, I32, I32, I32, P, P, P, I64],
-    "tmog_split_find_cpu": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P],
+    "tmog_hist_build_cpu": [P, I64, I32, P, I32, P, P, P, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P],
+    "tmog_split_find_cpu": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, P, P],
     "tmog_partition_cpu": [P, I32, P, P, I32, P, P, P, P, P, I32, P, P],
     "tmog_forest_predict_cpu": [P, I32, I32, P, P, P, P, P, P, P, I32, P, I32, P],
     "tmog_find_splits_cpu": [P, I64, I32, I32, P, P],
@@ -39,9 +39,9 @@ _HOST_SIGS = {
 }
 
 _HIP_SIGS = {
-    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P],
+    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, P],
     "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
-    "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, P],
+    "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, P, P, P],
     "tmog_hip_partition_count": [P, I32, P, P, I32, P, P, P, I32, P, P],
     "tmog_hip_partition_scatter": [P, I32, P, P, P, I32, P, P, P, I32, P],
     "tmog_hip_forest_predict": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P],

@@ -7,15 +7,14 @@
 //
 // Layout contract (identical to ../host/tree_cpu.cpp, orchestrated by models/tree_engine.py):
 //   Xb    uint8 [N][F] row-major bins          rows  uint32 (row | weight<<24)
-//   hist  float, node j at node_hist_off[j], index ((fl * B) + bin) * S + s
+//   hist  int64 fixed point, node j at node_hist_off[j], index ((fl * B) + bin) * S + s;
+//         value = hist * qinv[model][s] (see "Fixed-point statistics" below)
 //
 // Histogram kernel mapping (wave64-first): a wave-instruction covers R = 64 / FG rows x FG
-// features -- lane (r, f) handles feature f of row r. Lanes of one instruction therefore touch
-// distinct LDS histogram rows (feature-major, padded by one word so bank = f + bin*S + s spreads),
-// and the R row-slots get private LDS copies, so no two lanes of an instruction ever hit the same
-// address. Per-row data (row id, weight, label / gradients) is loaded once per lane group. All
-// waves of the workgroup share the LDS copies through ds_add_f32. The R copies are folded on the
-// way out; a node covered by one row-chunk stores with plain stores, otherwise float atomics.
+// features -- lane (r, f) handles feature f of row r, so lanes of one instruction touch distinct LDS
+// histogram rows (feature-major, padded by one word so bank = f + bin*S + s spreads). All waves of
+// the workgroup share the table through integer LDS atomics; the R copies are folded on the way out
+// and a node covered by one row-chunk stores with plain stores, otherwise 64-bit integer atomics.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
@@ -33,57 +32,72 @@ struct HistItem {
   int64_t count;    // row entries in this chunk
 };
 
-// Per-row statistics staged for the whole wave: (entry bits, s0, s1, s2)
-//   MODE 0 (class counts):   s0 = w, s1 = class
-//   MODE 1 (variance stats): s0 = w, s1 = w*t, s2 = w*t*t
-//   MODE 2 (grad / hess):    s0 = w*g, s1 = w*h
+// Fixed-point statistics. Every per-row contribution is quantised to an integer,
+//   q = rint(v * qscale[model][s]),  |q| <= qmax = (2^31 - 1) / chunk_rows - 1,
+// with power-of-two scales chosen on the device from the per-model max |v| (tree_engine._quant_scales).
+// Workgroup LDS partials are int32 (ds_add_u32: ~17x the throughput of ds_add_f32 on gfx950, see
+// benchmarks/lds_atomic_bench.hip) and cannot overflow for a chunk of <= chunk_rows rows; the
+// global histogram is int64, so sums, the subtraction trick and the split scan's prefix sums are
+// exact and order-independent -- GPU and CPU (../host/tree_cpu.cpp) histograms are bit-identical and
+// runs are deterministic. Class counts (MODE 0) and the variance count are integer weights (scale 1).
+//
+// Staged row record (entry bits, q0, q1, q2):
+//   MODE 0 (class counts):   q0 = w, q1 = class
+//   MODE 1 (variance stats): q0 = w, q1 = q(w*t), q2 = q(w*t*t)
+//   MODE 2 (grad / hess):    q0 = q(w*g), q1 = q(w*h)
 template <int MODE>
-__device__ __forceinline__ float4 stage_row(uint32_t e, int64_t model, int64_t stride, const float* __restrict__ y,
-                                            const float* __restrict__ t1, const float* __restrict__ t2) {
+__device__ __forceinline__ int4 stage_row(uint32_t e, int64_t model, int64_t stride, const float* __restrict__ y,
+                                          const float* __restrict__ t1, const float* __restrict__ t2,
+                                          const float* __restrict__ qs) {
   const int64_t r = e & 0xFFFFFFu;
   const float w = (float)(e >> 24);
-  float4 s;
-  s.x = __uint_as_float(e);
+  int4 s;
+  s.x = (int)e;
   if (MODE == 0) {
-    s.y = w; s.z = y[r]; s.w = 0.f;
+    s.y = (int)(e >> 24); s.z = (int)y[r]; s.w = 0;
   } else if (MODE == 1) {
     const float t = t1[model * stride + r];
-    s.y = w; s.z = w * t; s.w = w * t * t;
+    const float wt = w * t;
+    s.y = (int)(e >> 24);
+    s.z = (int)rintf(wt * qs[1]);
+    s.w = (int)rintf((wt * t) * qs[2]);
   } else {
-    s.y = w * t1[model * stride + r]; s.z = w * t2[model * stride + r]; s.w = 0.f;
+    s.y = (int)rintf((w * t1[model * stride + r]) * qs[0]);
+    s.z = (int)rintf((w * t2[model * stride + r]) * qs[1]);
+    s.w = 0;
   }
   return s;
 }
 
 template <int MODE>
-__device__ __forceinline__ void add_row(float* my, int bin, int S, const float4& st) {
+__device__ __forceinline__ void add_row(int* my, int bin, int S, const int4& st) {
   if (MODE == 0) {
-    atomicAdd(my + bin * S + (int)st.z, st.y);
+    atomicAdd(my + bin * S + st.z, st.y);
   } else if (MODE == 1) {
-    float* hb = my + bin * 3;
+    int* hb = my + bin * 3;
     atomicAdd(hb, st.y); atomicAdd(hb + 1, st.z); atomicAdd(hb + 2, st.w);
   } else {
-    float* hb = my + bin * 2;
+    int* hb = my + bin * 2;
     atomicAdd(hb, st.y); atomicAdd(hb + 1, st.z);
   }
 }
 
-// Histogram build. Latency structure (the kernel is gather-latency bound, not LDS bound):
-//  1. each wave takes 64 row entries at once -- one coalesced load of the packed (row, weight) list --
-//     and every lane gathers the statistics of *its* row (64 independent gathers in flight);
-//  2. the 64 (entry, stats) records are staged in a wave-private LDS slot (one ds_write_b128 per lane);
-//  3. lane (row-slot rsub, feature fidx) then walks the staged rows R at a time, 8 rows unrolled:
-//     8 broadcast ds_read_b128 of the records, 8 *independent* bin gathers Xb[row*F + feat] in flight,
-//     then the LDS atomics into the lane's private (row-slot, feature) histogram row.
-// Lanes of one atomic instruction always address different histogram rows (distinct features or
-// row slots), so the atomics never conflict.
+// Histogram build. Lane mapping (wave64): a wave-instruction covers R = 64 / FG rows x FG features;
+// lane (rsub, fidx) owns histogram row (rsub, fidx) of the workgroup's LDS table, shared by its 4
+// waves through integer LDS atomics -- lanes of one instruction never address the same word.
+//  1. each wave takes 64 row entries at once (one coalesced load of the packed (row, weight) list)
+//     and every lane gathers + quantises the statistics of *its* row (64 independent gathers);
+//  2. the 64 records are staged in a wave-private LDS slot (one ds_write_b128 per lane);
+//  3. lane (rsub, fidx) walks the staged rows R at a time, 8 rows unrolled: 8 broadcast ds_read_b128,
+//     8 independent bin gathers Xb[row*F + feat] in flight, then the ds_add_u32s.
 template <int MODE>
 __global__ void __launch_bounds__(256) hist_build_kernel(
     const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const HistItem* __restrict__ items,
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
-    const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, float* __restrict__ hist, int B,
-    int S, const float* __restrict__ y, const float* __restrict__ t1, const float* __restrict__ t2, int64_t stride) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
+    int B, int S, const float* __restrict__ y, const float* __restrict__ t1, const float* __restrict__ t2,
+    int64_t stride, const float* __restrict__ qscale) {
+  extern __shared__ __attribute__((aligned(16))) int lds[];
   const HistItem it = items[blockIdx.x];
   const int FG = it.nf;
   const int R = 64 / FG;
@@ -92,8 +106,8 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
-  float4* stage = reinterpret_cast<float4*>(lds + ((ncopy_words + 3) & ~3)) + wave * 64;
-  for (int i = threadIdx.x; i < ncopy_words; i += blockDim.x) lds[i] = 0.f;
+  int4* stage = reinterpret_cast<int4*>(lds + ((ncopy_words + 3) & ~3)) + wave * 64;
+  for (int i = threadIdx.x; i < ncopy_words; i += blockDim.x) lds[i] = 0;
   __syncthreads();
 
   const int rsub = lane / FG;
@@ -101,7 +115,8 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   const bool active = rsub < R;
   const int feat = active ? feat_list[node_feat_off[it.node] + it.fg0 + fidx] : 0;
   const int64_t model = node_model ? node_model[it.node] : 0;
-  float* my = lds + (rsub * FG + fidx) * rowstride;
+  const float* qs = qscale + model * S;
+  int* my = lds + (rsub * FG + fidx) * rowstride;
   const uint32_t* rp = rows + it.begin;
   const int64_t cnt = it.count;
 
@@ -110,18 +125,16 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   for (int64_t base = (int64_t)wave * 64; base < cnt; base += (int64_t)nwaves * 64) {
     const int64_t ri = min(base + lane, cnt - 1);
     const int nrows = (int)min((int64_t)64, cnt - base);
-    float4 mine = stage_row<MODE>(rp[ri], model, stride, y, t1, t2);
-    stage[lane] = mine;
+    stage[lane] = stage_row<MODE>(rp[ri], model, stride, y, t1, t2, qs);
     __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0): staged records visible to the wave
     __builtin_amdgcn_wave_barrier();
     for (int j0 = 0; j0 < nrows; j0 += R * 8) {
-      float4 st[8];
+      int4 st[8];
       int bin[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) st[u] = stage[min(j0 + u * R + rsub, 63)];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        bin[u] = (int)Xb[(int64_t)(__float_as_uint(st[u].x) & 0xFFFFFFu) * F + feat];
+      for (int u = 0; u < 8; ++u) bin[u] = (int)Xb[(int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F + feat];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         if (active && j0 + u * R + rsub < nrows) add_row<MODE>(my, bin[u], S, st[u]);
@@ -131,28 +144,28 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   __syncthreads();
 
   // fold the R private copies and write the node histogram of this feature group
-  float* out = hist + node_hist_off[it.node] + (int64_t)it.fg0 * B * S;
+  int64_t* out = hist + node_hist_off[it.node] + (int64_t)it.fg0 * B * S;
   const int words = FG * B * S;
   for (int k = threadIdx.x; k < words; k += blockDim.x) {
     const int f = k / (B * S);
     const int rem = k - f * (B * S);
-    float acc = 0.f;
+    int64_t acc = 0;
     for (int r = 0; r < R; ++r) acc += lds[(r * FG + f) * rowstride + rem];
     if (it.excl) out[k] = acc;
-    else if (acc != 0.f) atomicAdd(out + k, acc);
+    else if (acc != 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + k), (unsigned long long)acc);
   }
 }
 
 // sibling = parent - small (histogram subtraction trick), size words each
-__global__ void hist_subtract_kernel(float* __restrict__ hist, const float* __restrict__ parent,
+__global__ void hist_subtract_kernel(int64_t* __restrict__ hist, const int64_t* __restrict__ parent,
                                      const int64_t* __restrict__ parent_off, const int64_t* __restrict__ small_off,
                                      const int64_t* __restrict__ out_off, const int64_t* __restrict__ size, int n) {
   const int j = blockIdx.y;
   if (j >= n) return;
   const int64_t sz = size[j];
-  const float* p = parent + parent_off[j];
-  const float* s = hist + small_off[j];
-  float* o = hist + out_off[j];
+  const int64_t* p = parent + parent_off[j];
+  const int64_t* s = hist + small_off[j];
+  int64_t* o = hist + out_off[j];
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += (int64_t)gridDim.x * blockDim.x)
     o[k] = p[k] - s[k];
 }
@@ -197,33 +210,43 @@ __device__ __forceinline__ bool better(const Best& a, const Best& b) {
   return a.b < b.b;
 }
 
-// One workgroup (4 waves) per node; each wave scans features (lane = bin, B <= 64) with a
-// double-precision wave prefix sum, then the block reduces the best (gain, f, dl, b).
+// One workgroup (4 waves) per node; each wave scans features (lane = bin, B <= 64) with an exact
+// int64 wave prefix sum of the fixed-point histogram, converting to double only to evaluate gains
+// (identical arithmetic to tmog_split_find_cpu, so both pick the same split bit for bit). The block
+// then reduces the best (gain, f, dl, b). SM = compile-time bound on S (register arrays sized to it).
+template <int SM>
 __global__ void __launch_bounds__(256) split_find_kernel(
-    const float* __restrict__ hist, const int64_t* __restrict__ node_hist_off, const int32_t* __restrict__ node_nfeat,
+    const int64_t* __restrict__ hist, const int64_t* __restrict__ node_hist_off, const int32_t* __restrict__ node_nfeat,
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
-    int missing_bin, int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin, float* __restrict__ out_gain,
+    int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv,
+    int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin, float* __restrict__ out_gain,
     uint8_t* __restrict__ out_dl, float* __restrict__ out_left, float* __restrict__ out_total) {
   const int j = blockIdx.x;
-  const float* h = hist + node_hist_off[j];
+  const int64_t* h = hist + node_hist_off[j];
   const int nf = node_nfeat[j];
   const int32_t* fl = feat_list + node_feat_off[j];
   const float* P = node_params + (int64_t)j * 8;
+  const double* qi = qinv + (int64_t)(node_model ? node_model[j] : 0) * S;
   const double min_inst = P[0], min_gain = P[1], mcw = P[2], lambda = P[3];
   const bool allow_missing = P[5] > 0.5f && missing_bin >= 0;
-  __shared__ double s_tot[TM_MAX_S];
+  __shared__ int64_t s_tot[SM];
   __shared__ Best s_best[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (threadIdx.x < S) {
-    double t = 0;
+    int64_t t = 0;
     for (int b = 0; b < B; ++b) t += h[b * S + threadIdx.x];
     s_tot[threadIdx.x] = t;
-    out_total[(int64_t)j * S + threadIdx.x] = (float)t;
+    out_total[(int64_t)j * S + threadIdx.x] = (float)((double)t * qi[threadIdx.x]);
   }
   __syncthreads();
-  double tot[TM_MAX_S];
-  for (int s = 0; s < S; ++s) tot[s] = s_tot[s];
+  int64_t totq[SM];
+  double tot[SM], q[SM];
+  for (int s = 0; s < S; ++s) {
+    q[s] = qi[s];
+    totq[s] = s_tot[s];
+    tot[s] = (double)totq[s] * q[s];
+  }
   double tcount;
   const double pimp = impurity_dev(tot, S, kind, &tcount);
   const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
@@ -231,25 +254,26 @@ __global__ void __launch_bounds__(256) split_find_kernel(
   Best best{-INFINITY, 0x7fffffff, 0, 0};
   for (int f = wave; f < nf; f += 4) {
     const int nb = feat_nbins[fl[f]];
-    const float* hf = h + (int64_t)f * B * S;
-    double v[TM_MAX_S], miss[TM_MAX_S];
+    const int64_t* hf = h + (int64_t)f * B * S;
+    int64_t v[SM], miss[SM];
     for (int s = 0; s < S; ++s) {
-      v[s] = (lane < nb - 1) ? (double)hf[lane * S + s] : 0.0;
-      miss[s] = allow_missing ? (double)hf[missing_bin * S + s] : 0.0;
+      v[s] = (lane < nb - 1) ? hf[lane * S + s] : 0;
+      miss[s] = allow_missing ? hf[missing_bin * S + s] : 0;
     }
-    // inclusive wave prefix over bins
+    // inclusive wave prefix over bins (exact)
     for (int off = 1; off < 64; off <<= 1) {
       for (int s = 0; s < S; ++s) {
-        const double o = __shfl_up(v[s], off, 64);
+        const int64_t o = __shfl_up(v[s], off, 64);
         if (lane >= off) v[s] += o;
       }
     }
     if (lane < nb - 1) {
       for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
-        double left[TM_MAX_S], right[TM_MAX_S];
+        double left[SM], right[SM];
         for (int s = 0; s < S; ++s) {
-          left[s] = v[s] + (dl ? miss[s] : 0.0);
-          right[s] = tot[s] - left[s];
+          const int64_t lq = v[s] + (dl ? miss[s] : 0);
+          left[s] = (double)lq * q[s];
+          right[s] = (double)(totq[s] - lq) * q[s];
         }
         double gain;
         bool ok = true;
@@ -294,17 +318,17 @@ __global__ void __launch_bounds__(256) split_find_kernel(
     s_best[0] = b;
   }
   __syncthreads();
-  // left stats of the winner (recomputed in double from the histogram)
+  // left stats of the winner
   const Best b = s_best[0];
   if (threadIdx.x < S) {
     const int s = threadIdx.x;
-    double acc = 0;
+    int64_t acc = 0;
     if (b.f != 0x7fffffff) {
-      const float* hf = h + (int64_t)b.f * B * S;
+      const int64_t* hf = h + (int64_t)b.f * B * S;
       for (int k = 0; k <= b.b; ++k) acc += hf[k * S + s];
       if (b.dl) acc += hf[missing_bin * S + s];
     }
-    out_left[(int64_t)j * S + s] = (float)acc;
+    out_left[(int64_t)j * S + s] = (float)((double)acc * qi[s]);
   }
 }
 
@@ -425,26 +449,26 @@ extern "C" {
 
 int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
-                        const int64_t* node_hist_off, float* hist, int B, int mode, int S, const float* y,
-                        const float* t1, const float* t2, int64_t stride, hipStream_t stream) {
+                        const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
+                        const float* t1, const float* t2, int64_t stride, const float* qscale, hipStream_t stream) {
   if (n_items == 0) return 0;
-  const size_t lds = (size_t)(((64 * (B * S + 1)) + 3) & ~3) * sizeof(float) + 4 * 64 * sizeof(float4);
+  const size_t lds = (size_t)(((64 * (B * S + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4);
   if (lds > 160 * 1024) return -2;
   const HistItem* it = (const HistItem*)items;
   dim3 grid(n_items), block(256);
   if (mode == 0)
     hipLaunchKernelGGL(hist_build_kernel<0>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale);
   else if (mode == 1)
     hipLaunchKernelGGL(hist_build_kernel<1>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale);
   else
     hipLaunchKernelGGL(hist_build_kernel<2>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale);
   return (int)hipGetLastError();
 }
 
-int tmog_hip_hist_subtract(float* hist, const float* parent, const int64_t* parent_off, const int64_t* small_off,
+int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
                            const int64_t* out_off, const int64_t* size, int n, int64_t max_size, hipStream_t stream) {
   if (n == 0) return 0;
   int gx = (int)((max_size + 255) / 256);
@@ -455,16 +479,23 @@ int tmog_hip_hist_subtract(float* hist, const float* parent, const int64_t* pare
   return (int)hipGetLastError();
 }
 
-int tmog_hip_split_find(const float* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
+int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
-                        int S, int kind, const float* node_params, int missing_bin, int32_t* out_feat,
+                        int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
+                        const double* qinv, int32_t* out_feat,
                         int32_t* out_bin, float* out_gain, uint8_t* out_dl, float* out_left, float* out_total,
                         hipStream_t stream) {
   if (n_nodes == 0) return 0;
   if (S > TM_MAX_S || B > 64) return -2;
-  hipLaunchKernelGGL(split_find_kernel, dim3(n_nodes), dim3(256), 0, stream, hist, node_hist_off, node_nfeat,
-                     node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin, out_feat, out_bin,
-                     out_gain, out_dl, out_left, out_total);
+#define TM_SPLIT(SMV)                                                                                         \
+  hipLaunchKernelGGL(split_find_kernel<SMV>, dim3(n_nodes), dim3(256), 0, stream, hist, node_hist_off, node_nfeat, \
+                     node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin, node_model, qinv,  \
+                     out_feat, out_bin, out_gain, out_dl, out_left, out_total)
+  if (S <= 2) TM_SPLIT(2);
+  else if (S == 3) TM_SPLIT(3);
+  else if (S <= 4) TM_SPLIT(4);
+  else TM_SPLIT(TM_MAX_S);
+#undef TM_SPLIT
   return (int)hipGetLastError();
 }
 

@@ -7,7 +7,9 @@
 //   rows      uint32 packed row entries: (row & 0xFFFFFF) | (weight << 24)
 //   nodes     j = 0..n_nodes-1 : [node_begin[j], node_begin[j]+node_count[j]) slice of `rows`
 //   features  node j histograms features feat_list[node_feat_off[j] + 0 .. node_nfeat[j]-1]
-//   hist      float [node_hist_off[j] + (fl * B + bin) * S + s]
+//   hist      int64 fixed point [node_hist_off[j] + (fl * B + bin) * S + s]; value = hist * qinv[model][s]
+//             per-row contributions are rint(v * qscale[model][s]) exactly as in the HIP kernel, so the
+//             integer sums (and therefore every split) are bit-identical between the two paths
 //
 // Stat modes (S = stats per bin):
 //   0 CLS : S = n_classes, contribution w at class y[row]                  (gini / entropy trees)
@@ -32,36 +34,40 @@ static inline float stat_target(const float* t, int64_t model, int64_t stride, i
 int tmog_hist_build_cpu(const uint8_t* Xb, int64_t N, int F, const uint32_t* rows, int n_nodes,
                         const int64_t* node_begin, const int64_t* node_count, const int32_t* node_feat_off,
                         const int32_t* node_nfeat, const int32_t* feat_list, const int32_t* node_model,
-                        const int64_t* node_hist_off, float* hist, int B, int mode, int S, const float* y,
-                        const float* t1, const float* t2, int64_t model_stride) {
+                        const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
+                        const float* t1, const float* t2, int64_t model_stride, const float* qscale) {
   (void)N;
 #pragma omp parallel for schedule(dynamic, 1)
   for (int j = 0; j < n_nodes; ++j) {
     const int nf = node_nfeat[j];
     const int32_t* fl = feat_list + node_feat_off[j];
-    float* h = hist + node_hist_off[j];
-    std::memset(h, 0, sizeof(float) * (size_t)nf * B * S);
+    int64_t* h = hist + node_hist_off[j];
+    std::memset(h, 0, sizeof(int64_t) * (size_t)nf * B * S);
     const int64_t b0 = node_begin[j], cnt = node_count[j];
     const int64_t model = node_model ? node_model[j] : 0;
+    const float* qs = qscale + model * S;
     for (int64_t i = 0; i < cnt; ++i) {
       const uint32_t e = rows[b0 + i];
       const int64_t r = e & 0xFFFFFFu;
       const float w = (float)(e >> 24);
-      float st[16];
+      int64_t st[16];
       if (mode == 0) {
-        for (int s = 0; s < S; ++s) st[s] = 0.f;
-        st[(int)y[r]] = w;
+        for (int s = 0; s < S; ++s) st[s] = 0;
+        st[(int)y[r]] = (int64_t)(e >> 24);
       } else if (mode == 1) {
         const float t = stat_target(t1, model, model_stride, r);
-        st[0] = w; st[1] = w * t; st[2] = w * t * t;
+        const float wt = w * t;
+        st[0] = (int64_t)(e >> 24);
+        st[1] = (int64_t)(int)rintf(wt * qs[1]);
+        st[2] = (int64_t)(int)rintf((wt * t) * qs[2]);
       } else {
-        st[0] = w * stat_target(t1, model, model_stride, r);
-        st[1] = w * stat_target(t2, model, model_stride, r);
+        st[0] = (int64_t)(int)rintf((w * stat_target(t1, model, model_stride, r)) * qs[0]);
+        st[1] = (int64_t)(int)rintf((w * stat_target(t2, model, model_stride, r)) * qs[1]);
       }
       const uint8_t* xr = Xb + r * (int64_t)F;
       for (int f = 0; f < nf; ++f) {
         const int bin = xr[fl[f]];
-        float* hb = h + ((int64_t)f * B + bin) * S;
+        int64_t* hb = h + ((int64_t)f * B + bin) * S;
         for (int s = 0; s < S; ++s) hb[s] += st[s];
       }
     }
@@ -98,44 +104,52 @@ static inline double impurity(const double* st, int S, int kind, double* count_o
 
 // params per node (float): [0] min_instances, [1] min_info_gain, [2] min_child_weight, [3] lambda,
 // [4] alpha (unused), [5] allow_missing (xgb default-direction search)
-int tmog_split_find_cpu(const float* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
+int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
-                        int S, int kind, const float* node_params, int missing_bin, int32_t* out_feat,
-                        int32_t* out_bin, float* out_gain, uint8_t* out_default_left, float* out_left,
-                        float* out_total) {
+                        int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
+                        const double* qinv, int32_t* out_feat, int32_t* out_bin, float* out_gain,
+                        uint8_t* out_default_left, float* out_left, float* out_total) {
 #pragma omp parallel for schedule(dynamic, 4)
   for (int j = 0; j < n_nodes; ++j) {
-    const float* h = hist + node_hist_off[j];
+    const int64_t* h = hist + node_hist_off[j];
     const int nf = node_nfeat[j];
     const int32_t* fl = feat_list + node_feat_off[j];
     const float* P = node_params + (int64_t)j * 8;
+    const double* q = qinv + (int64_t)(node_model ? node_model[j] : 0) * S;
     const double min_inst = P[0], min_gain = P[1], mcw = P[2], lambda = P[3];
     const bool allow_missing = P[5] > 0.5f && missing_bin >= 0;
-    double tot[16] = {0};
+    int64_t totq[16] = {0};
+    double tot[16];
     // totals from feature 0 (every row is counted once per feature, including the missing bin)
     for (int b = 0; b < B; ++b)
-      for (int s = 0; s < S; ++s) tot[s] += h[(int64_t)b * S + s];
-    for (int s = 0; s < S; ++s) out_total[(int64_t)j * S + s] = (float)tot[s];
+      for (int s = 0; s < S; ++s) totq[s] += h[(int64_t)b * S + s];
+    for (int s = 0; s < S; ++s) {
+      tot[s] = (double)totq[s] * q[s];
+      out_total[(int64_t)j * S + s] = (float)tot[s];
+    }
     double tcount;
     const double pimp = impurity(tot, S, kind, &tcount);
     const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
     double best = -INFINITY;
     int bf = -1, bb = -1, bdl = 0;
-    double bleft[16] = {0};
+    int64_t bleft[16] = {0};
     for (int f = 0; f < nf; ++f) {
       const int gf = fl[f];
       const int nb = feat_nbins[gf];
-      const float* hf = h + (int64_t)f * B * S;
-      double miss[16] = {0};
+      const int64_t* hf = h + (int64_t)f * B * S;
+      int64_t miss[16] = {0};
       if (allow_missing)
         for (int s = 0; s < S; ++s) miss[s] = hf[(int64_t)missing_bin * S + s];
       for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
-        double left[16];
-        for (int s = 0; s < S; ++s) left[s] = dl ? miss[s] : 0.0;
+        int64_t lq[16];
+        for (int s = 0; s < S; ++s) lq[s] = dl ? miss[s] : 0;
         for (int b = 0; b + 1 < nb; ++b) {
-          for (int s = 0; s < S; ++s) left[s] += hf[(int64_t)b * S + s];
-          double right[16];
-          for (int s = 0; s < S; ++s) right[s] = tot[s] - left[s];
+          double left[16], right[16];
+          for (int s = 0; s < S; ++s) {
+            lq[s] += hf[(int64_t)b * S + s];
+            left[s] = (double)lq[s] * q[s];
+            right[s] = (double)(totq[s] - lq[s]) * q[s];
+          }
           double gain;
           if (kind == 3) {
             if (left[1] < mcw || right[1] < mcw) continue;
@@ -150,7 +164,7 @@ int tmog_split_find_cpu(const float* hist, int n_nodes, const int64_t* node_hist
           }
           if (gain > best) {
             best = gain; bf = gf; bb = b; bdl = dl;
-            for (int s = 0; s < S; ++s) bleft[s] = left[s];
+            for (int s = 0; s < S; ++s) bleft[s] = lq[s];
           }
         }
       }
@@ -159,7 +173,7 @@ int tmog_split_find_cpu(const float* hist, int n_nodes, const int64_t* node_hist
     out_bin[j] = bb;
     out_gain[j] = bf >= 0 ? (float)best : -INFINITY;
     out_default_left[j] = (uint8_t)bdl;
-    for (int s = 0; s < S; ++s) out_left[(int64_t)j * S + s] = (float)bleft[s];
+    for (int s = 0; s < S; ++s) out_left[(int64_t)j * S + s] = (float)((double)bleft[s] * q[s]);
   }
   return 0;
 }
