@@ -113,3 +113,33 @@ def test_hip_engine_matches_host(mode, missing, subset):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
     from transmogrifai_amd.ops import _native
     assert _native.hip_loaded()
+
+
+def _leaf_vs_walk(dev):
+    X, y = _data(N=4000, missing=True)
+    X = X.to(dev)
+    g = torch.Generator().manual_seed(3)
+    G = torch.randn(2, X.shape[0], generator=g).to(dev)
+    H = (torch.rand(2, X.shape[0], generator=g) * 0.25).to(dev)
+    rows = [torch.randperm(X.shape[0], generator=g)[:3000].sort().values.to(dev) for _ in range(2)]
+    jobs = [te.TreeJob(k, te.TreeParams(max_depth=6, min_child_weight=0.5, reg_lambda=1.0, gamma=2.0 * k,
+                                        split_eps=1e-6), rows[k]) for k in range(2)]
+    f = te.grow_forest(X, np.full(10, 32), jobs, mode=te.MODE_GH, kind=te.KIND_NEWTON, t1=G, t2=H, B=32,
+                       missing_bin=31, collect_leaves=True)
+    la = f.leaf_assign
+    assert la.rows.numel() == sum(r.numel() for r in rows)
+    walk = te.forest_predict(f, X, [None, None], [[0], [1]])
+    t, r, v = la.entry_tree(), la.row_ids(), la.entry_value()[:, 0]
+    for k in range(2):
+        m = t == k
+        assert torch.equal(r[m].sort().values, rows[k])
+        torch.testing.assert_close(v[m], walk[k][r[m], 0], rtol=0, atol=0)
+
+
+def test_leaf_assign_matches_tree_walk_cpu():
+    _leaf_vs_walk("cpu")
+
+
+@pytest.mark.gpu
+def test_leaf_assign_matches_tree_walk_gpu():
+    _leaf_vs_walk("cuda")

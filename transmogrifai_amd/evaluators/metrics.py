@@ -147,8 +147,10 @@ def bin_score_metrics(prob1, labels, num_bins: int = 100) -> Dict[str, object]:
     diff = mx - mn
     idx = torch.clamp((num_bins * (s - mn) / diff).to(torch.int64), max=num_bins - 1)
     cnt = torch.bincount(idx, minlength=num_bins).to(torch.float64)
-    ssum = torch.zeros(num_bins, dtype=torch.float64, device=s.device).index_add_(0, idx, s)
-    psum = torch.zeros(num_bins, dtype=torch.float64, device=s.device).index_add_(0, idx, (y > 0).to(torch.float64))
+    # weighted bincount accumulates per-workgroup in LDS first (fp64 index_add_ on 100 bins is a global
+    # atomic storm: 210 ms per call at 10M rows on MI355X, see profiles/README.md)
+    ssum = torch.bincount(idx, weights=s, minlength=num_bins)[:num_bins]
+    psum = torch.bincount(idx, weights=(y > 0).to(torch.float64), minlength=num_bins)[:num_bins]
     brier = float(((s - y) ** 2).sum() / s.numel())
     avg_s = torch.where(cnt > 0, ssum / cnt.clamp_min(1), torch.zeros_like(cnt))
     avg_c = torch.where(cnt > 0, psum / cnt.clamp_min(1), torch.zeros_like(cnt))

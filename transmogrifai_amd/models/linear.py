@@ -40,6 +40,18 @@ class BatchedObjective:
         self.y_scale = y_scale          # [P] label scale for squared loss
         self.d = X.shape[1]
         self.passes = 0
+        # fused one-pass HIP objective (ops/csrc/hip/linear_kernels.hip) when X is an fp32 device matrix
+        self.fused = LK.fused_objective_supported(X) and loss in LK.LOSS_CODES
+        if self.fused:
+            self.yf = y.to(device=X.device, dtype=torch.float32).contiguous()
+            self.Wf = W.to(torch.float32).contiguous()
+            self.ysf = None if y_scale is None else y_scale.to(device=X.device, dtype=torch.float32)
+
+    def _fused_pass(self, U, grad):
+        V = (U[:self.d] * self.inv_std).to(torch.float32)
+        b = torch.where(self.fi, U[self.d], torch.zeros_like(U[self.d])).to(torch.float32)
+        self.passes += 1
+        return LK.fused_objective(self.X, self.yf, self.Wf, V, b, self.loss, self.ysf, grad=grad)
 
     def margins(self, U):
         V = (U[:self.d] * self.inv_std).to(self.X.dtype)
@@ -65,12 +77,21 @@ class BatchedObjective:
         return l, d
 
     def value(self, U):
+        if self.fused:
+            f = self._fused_pass(U, False)[0] / self.wsum
+            return f + 0.5 * self.l2 * (U[:self.d] ** 2).sum(0)
         M = self.margins(U)
         l, _ = self._elem(M, False)
         f = (l * self.W).sum(0).to(torch.float64) / self.wsum
         return f + 0.5 * self.l2 * (U[:self.d] ** 2).sum(0)
 
     def value_grad(self, U):
+        if self.fused:
+            f, r, G = self._fused_pass(U, True)
+            g = torch.zeros_like(U)
+            g[:self.d] = (G / self.wsum[None, :]) * self.inv_std + self.l2[None, :] * U[:self.d]
+            g[self.d] = torch.where(self.fi, r / self.wsum, torch.zeros_like(self.wsum))
+            return f / self.wsum + 0.5 * self.l2 * (U[:self.d] ** 2).sum(0), g
         M = self.margins(U)
         l, dm = self._elem(M, True)
         R = dm * self.W

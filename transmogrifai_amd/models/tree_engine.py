@@ -32,7 +32,8 @@ HIST_ITEM = np.dtype([("node", "<i4"), ("fg0", "<i4"), ("nf", "<i4"), ("excl", "
                       ("begin", "<i8"), ("count", "<i8")])
 PART_ITEM = np.dtype([("node", "<i4"), ("pad", "<i4"), ("begin", "<i8"), ("count", "<i8"),
                       ("out_left", "<i8"), ("out_right", "<i8")])
-assert HIST_ITEM.itemsize == 32 and PART_ITEM.itemsize == 40
+LEAF_ITEM = np.dtype([("begin", "<i8"), ("count", "<i8"), ("out", "<i8"), ("gid", "<i4"), ("pad", "<i4")])
+assert HIST_ITEM.itemsize == 32 and PART_ITEM.itemsize == 40 and LEAF_ITEM.itemsize == 32
 
 ROW_MASK = 0xFFFFFF
 MAX_ROWS = 1 << 24
@@ -210,8 +211,12 @@ def _feature_subsets(n_nodes: int, F: int, k: np.ndarray, dev, gen) -> tuple:
 def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *, mode: int, kind: int,
                 n_classes: int = 2, y: Optional[torch.Tensor] = None, t1: Optional[torch.Tensor] = None,
                 t2: Optional[torch.Tensor] = None, B: int = 32, missing_bin: int = -1,
-                subtract: bool = True, chunk_rows: int = 4096, rng_seed: int = 0) -> Forest:
-    """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``."""
+                subtract: bool = True, chunk_rows: int = 4096, rng_seed: int = 0,
+                collect_leaves: bool = False) -> Forest:
+    """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``.
+
+    ``collect_leaves``: also return, as ``forest.leaf_assign``, the final leaf of every training entry
+    (see ``LeafAssign``) so boosting can update margins without re-walking the new trees."""
     dev = Xb.device
     on_gpu = dev.type == "cuda"
     Nrows, F = int(Xb.shape[0]), int(Xb.shape[1])
@@ -263,6 +268,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     max_depth = int(P_depth.max()) if T else 0
 
     qscale, qinv = _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev)
+    lc = _LeafCollector(int(rows.numel()), dev, chunk_rows) if collect_leaves else None
     prev_hist = None          # previous level's histogram buffer
     pair_parent_off = None    # per sibling pair: parent's offset in prev_hist
     for depth in range(max_depth + 1):
@@ -273,6 +279,8 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         need = can | (depth == 0)
         hist_nodes = np.nonzero(need)[0]
         if hist_nodes.size == 0:
+            if lc is not None:
+                lc.add(rows, lv_begin, lv_count, lv_gid)
             break
         m = hist_nodes.size
         h_tree = lv_tree[hist_nodes]
@@ -385,6 +393,11 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         G.tot[g_h] = h_tot
         spl = h_feat >= 0
         sl = np.nonzero(spl)[0]
+        if lc is not None:
+            leaf_mask = np.ones(n, bool)
+            leaf_mask[hist_nodes[sl]] = False
+            lf = np.nonzero(leaf_mask)[0]
+            lc.add(rows, lv_begin[lf], lv_count[lf], lv_gid[lf])
         if sl.size == 0:
             break
         gs = g_h[sl]
@@ -431,7 +444,72 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         rows, rows_alt = rows_alt, rows
         lv_tree, lv_gid, lv_begin, lv_count = ch_tree, ch, new_begin, new_count
 
-    return _finalize(jobs, G, mode, kind, K, S, missing_bin)
+    forest = _finalize(jobs, G, mode, kind, K, S, missing_bin, with_gid_values=lc is not None)
+    if lc is not None:
+        gid_value, gid_tree = forest._gid_value, forest._gid_tree
+        del forest._gid_value, forest._gid_tree
+        forest.leaf_assign = LeafAssign(lc.rows[:lc.pos], lc.gid[:lc.pos],
+                                        torch.as_tensor(gid_value, device=dev),
+                                        torch.as_tensor(gid_tree, device=dev))
+    return forest
+
+
+@dataclass
+class LeafAssign:
+    """Final leaf of every training entry of a ``grow_forest`` call: ``rows`` (packed entries, as
+    given to the trees), ``gid`` (node id per entry), ``value[gid]`` (leaf output, pruning applied),
+    ``tree[gid]`` (job index). ``per_tree_values`` turns it into margin updates."""
+    rows: torch.Tensor
+    gid: torch.Tensor
+    value: torch.Tensor
+    tree: torch.Tensor
+
+    def row_ids(self) -> torch.Tensor:
+        return (self.rows & 0xFFFFFF).to(torch.int64)
+
+    def entry_tree(self) -> torch.Tensor:
+        return self.tree[self.gid.to(torch.int64)]
+
+    def entry_value(self) -> torch.Tensor:
+        return self.value[self.gid.to(torch.int64)]
+
+
+class _LeafCollector:
+    def __init__(self, total, dev, chunk_rows):
+        self.rows = torch.empty(total, dtype=torch.int32, device=dev)
+        self.gid = torch.empty(total, dtype=torch.int32, device=dev)
+        self.pos = 0
+        self.dev = dev
+        self.chunk = int(chunk_rows)
+
+    def add(self, rows, begin, count, gid):
+        begin, count, gid = (np.asarray(a, np.int64) for a in (begin, count, gid))
+        nz = count > 0
+        begin, count, gid = begin[nz], count[nz], gid[nz]
+        if count.size == 0:
+            return
+        out = self.pos + np.concatenate([[0], np.cumsum(count[:-1])])
+        self.pos += int(count.sum())
+        if self.dev.type == "cuda":
+            nch = -(-count // self.chunk)
+            seg = np.repeat(np.arange(count.size), nch)
+            c = np.arange(seg.size) - np.repeat(np.cumsum(nch) - nch, nch)
+            a = np.zeros(seg.size, LEAF_ITEM)
+            a["begin"] = begin[seg] + c * self.chunk
+            a["count"] = np.minimum(self.chunk, count[seg] - c * self.chunk)
+            a["out"] = out[seg] + c * self.chunk
+            a["gid"] = gid[seg]
+            it = torch.as_tensor(a.view(np.uint8), device=self.dev)
+            N.check(N.hip().tmog_hip_leaf_collect(N.ptr(rows), N.ptr(it), len(a), N.ptr(self.rows), N.ptr(self.gid),
+                                                  N.stream(self.dev)), "leaf_collect")
+        else:
+            seg = np.repeat(np.arange(count.size), count)
+            starts = np.concatenate([[0], np.cumsum(count[:-1])])
+            within = np.arange(seg.size) - np.repeat(starts, count)
+            src = torch.as_tensor(begin[seg] + within)
+            dst = slice(int(out[0]), int(out[0]) + seg.size)
+            self.rows[dst] = rows[src]
+            self.gid[dst] = torch.as_tensor(gid[seg].astype(np.int32))
 
 
 def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev):
@@ -535,7 +613,7 @@ def _scatter_items(citems, chunk_left, split_local, m, out_begin):
     return nl, a
 
 
-def _finalize(jobs, G: _Grow, mode, kind, K, S, missing_bin):
+def _finalize(jobs, G: _Grow, mode, kind, K, S, missing_bin, with_gid_values: bool = False):
     n = G.n
     tot = G.tot[:n]
     left = G.left[:n].copy()
@@ -593,10 +671,23 @@ def _finalize(jobs, G: _Grow, mode, kind, K, S, missing_bin):
     nodes[:, 1] = np.where(isint, G.bin[:n][order], 0)
     nodes[:, 2] = np.where(isint, new_id[np.maximum(left[order], 0)], -1)
     nodes[:, 3] = np.where(isint, new_id[np.maximum(right[order], 0)], -1)
-    return Forest(tree_off, nodes, np.where(isint, G.dl[:n][order], 0).astype(np.uint8),
+    gid_value = None
+    if with_gid_values:
+        # leaf output per created node id: pruned descendants inherit their kept ancestor's leaf value
+        parent = np.full(n, -1, np.int64)
+        orig_int = np.nonzero(G.left[:n] >= 0)[0]
+        parent[G.left[:n][orig_int]] = orig_int
+        parent[G.right[:n][orig_int]] = orig_int
+        gid_value = value.astype(np.float32).reshape(n, K).copy()
+        for g in np.nonzero(~reach)[0]:
+            gid_value[g] = gid_value[parent[g]]
+    f = Forest(tree_off, nodes, np.where(isint, G.dl[:n][order], 0).astype(np.uint8),
                   value[order].astype(np.float32).reshape(order.size, K),
                   np.where(isint, gain[order], 0).astype(np.float32), cover[order].astype(np.float32),
                   np.array([j.model for j in jobs], np.int32), missing_bin)
+    if with_gid_values:
+        f._gid_value, f._gid_tree = gid_value, tree.astype(np.int64)
+    return f
 
 
 def forest_predict(forest: Forest, Xb: torch.Tensor, model_rows: Sequence[Optional[torch.Tensor]],

@@ -106,6 +106,29 @@ def _rows(job: FitJob, N, dev):
     return torch.arange(N, device=dev) if job.rows is None else job.rows.to(dev)
 
 
+def _add_tree_margins(Fm: torch.Tensor, forest: "TE.Forest", Xb, act: List[int], wgts: List[float],
+                      tjobs) -> None:
+    """``Fm[act[k]] += wgts[k] * tree_k(x)`` for the trees of one boosting round.
+
+    Trees grown with ``collect_leaves`` know the leaf of every training entry, so the update is a
+    gather of leaf values scattered into the margins (each (model, row) pair occurs once, no atomics).
+    Rows outside a tree's training entries (zero-weight subsampled rows) need the tree walk."""
+    la = getattr(forest, "leaf_assign", None)
+    if la is None or any(j.weights is not None for j in tjobs):
+        preds = TE.forest_predict(forest, Xb, [None] * len(act), [[k] for k in range(len(act))])
+        for k, p in enumerate(act):
+            Fm[p] += wgts[k] * preds[k][:, 0].to(torch.float64)
+        return
+    N = Fm.shape[1]
+    t = la.entry_tree()
+    p_of = torch.as_tensor(act, dtype=torch.int64, device=Fm.device)
+    w_of = torch.as_tensor(wgts, dtype=torch.float64, device=Fm.device)
+    idx = p_of[t] * N + la.row_ids()
+    val = la.entry_value()[:, 0].to(torch.float64) * w_of[t]
+    flat = Fm.view(-1)
+    flat[idx] = flat[idx] + val
+
+
 def _model_rows_forest_predict(forest, Xb, rows_list, trees_list, tree_weight=None):
     return TE.forest_predict(forest, Xb, rows_list, trees_list, tree_weight)
 
@@ -391,13 +414,13 @@ class GBTClassifierLearner(_BoostLearner):
                     g = torch.Generator().manual_seed(int(pr.get("seed", 0)) + 131 * it + p)
                     w = (torch.rand(r.numel(), generator=g) < rate).to(torch.int64).to(dev)
                 tjobs.append(TE.TreeJob(p, tp, r, w))
-            forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_VAR, kind=TE.KIND_VARIANCE, t1=t1, B=mb)
-            preds = TE.forest_predict(forest, Xb, [None] * len(act), [[k] for k in range(len(act))])
+            forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_VAR, kind=TE.KIND_VARIANCE, t1=t1, B=mb,
+                                    collect_leaves=True)
+            wgts = [1.0 if it == 0 else float(jobs[p].params.get("step_size", 0.1)) for p in act]
+            _add_tree_margins(Fm, forest, Xb, act, wgts, tjobs)
             for k, p in enumerate(act):
-                wgt = 1.0 if it == 0 else float(jobs[p].params.get("step_size", 0.1))
-                Fm[p] += wgt * preds[k][:, 0].to(torch.float64)
                 forests[p].append(forest.tree(k))
-                weights[p].append(wgt)
+                weights[p].append(wgts[k])
         return [{"forest": TE.Forest.concat(forests[p]).to_state(), "bins": spec.to_state(),
                  "tree_weights": np.asarray(weights[p], np.float32), "n_classes": 2, "max_bins": mb,
                  "num_trees": len(forests[p])} for p in range(P)]
@@ -487,10 +510,9 @@ class XGBoostClassifierLearner(_BoostLearner):
                     w = (torch.rand(r.numel(), generator=gen) < ss).to(torch.int64).to(dev)
                 tjobs.append(TE.TreeJob(p, tp, r, w))
             forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
-                                    missing_bin=spec.missing_bin)
-            preds = TE.forest_predict(forest, Xb, [None] * len(act), [[k] for k in range(len(act))])
+                                    missing_bin=spec.missing_bin, collect_leaves=True)
+            _add_tree_margins(Fm, forest, Xb, act, [1.0] * len(act), tjobs)
             for k, p in enumerate(act):
-                Fm[p] += preds[k][:, 0].to(torch.float64)
                 forests[p].append(forest.tree(k))
                 weights[p].append(1.0)
             # early stopping on the training metric (the reference sets no eval set)

@@ -44,6 +44,8 @@ _HIP_SIGS = {
     "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, P, P, P],
     "tmog_hip_partition_count": [P, I32, P, P, I32, P, P, P, I32, P, P],
     "tmog_hip_partition_scatter": [P, I32, P, P, P, I32, P, P, P, I32, P],
+    "tmog_hip_leaf_collect": [P, P, I32, P, P, P],
+    "tmog_hip_lr_objective": [P, I64, I32, P, P, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P],
     "tmog_hip_forest_predict": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P],
     "tmog_hip_col_stats": [P, P, I64, I32, I64, P, P],
     "tmog_hip_vectorize_numeric": [P, P, P, I64, I32, P, P, P, P, I64, I32, P],

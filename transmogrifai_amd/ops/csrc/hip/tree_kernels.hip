@@ -411,6 +411,29 @@ __global__ void __launch_bounds__(256) partition_scatter_kernel(
   }
 }
 
+// ----------------------------------------------------------------------------- leaf collection
+// When a node stops splitting, its row entries (still contiguous in the level's row buffer) are
+// copied out with the node id: after the last level every training entry sits in exactly one
+// (entry, leaf) pair, so boosting updates its margins by a gather instead of re-walking the tree.
+struct LeafItem {
+  int64_t begin;    // first entry in rows
+  int64_t count;
+  int64_t out;      // output position
+  int32_t gid;      // node id
+  int32_t pad;
+};
+
+__global__ void __launch_bounds__(256) leaf_collect_kernel(const uint32_t* __restrict__ rows,
+                                                           const LeafItem* __restrict__ items,
+                                                           uint32_t* __restrict__ out_rows,
+                                                           int32_t* __restrict__ out_gid) {
+  const LeafItem it = items[blockIdx.x];
+  for (int64_t i = threadIdx.x; i < it.count; i += blockDim.x) {
+    out_rows[it.out + i] = rows[it.begin + i];
+    out_gid[it.out + i] = it.gid;
+  }
+}
+
 // ------------------------------------------------------------------------------------- predict
 // grid.y = model; each thread walks every tree of its model for one of the model's rows.
 __global__ void __launch_bounds__(256) forest_predict_kernel(
@@ -514,6 +537,14 @@ int tmog_hip_partition_scatter(const uint8_t* Xb, int F, const uint32_t* rows_in
   if (n_items == 0) return 0;
   hipLaunchKernelGGL(partition_scatter_kernel, dim3(n_items), dim3(256), 0, stream, Xb, F, rows_in, rows_out,
                      (const PartItem*)items, split_feat, split_bin, dl, missing_bin);
+  return (int)hipGetLastError();
+}
+
+int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
+                          int32_t* out_gid, hipStream_t stream) {
+  if (n_items == 0) return 0;
+  hipLaunchKernelGGL(leaf_collect_kernel, dim3(n_items), dim3(256), 0, stream, rows, (const LeafItem*)items,
+                     out_rows, out_gid);
   return (int)hipGetLastError();
 }
 

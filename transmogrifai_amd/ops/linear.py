@@ -17,3 +17,60 @@ def gemm(X: torch.Tensor, V: torch.Tensor) -> torch.Tensor:
 def gemm_t(X: torch.Tensor, R: torch.Tensor) -> torch.Tensor:
     """``X^T [d, N] @ R [N, P]`` in X's dtype."""
     return X.t() @ R.to(X.dtype)
+
+
+LOSS_CODES = {"logistic": 0, "hinge": 1, "squared": 2}
+_LR_DMAX = 512
+_LR_PC = 32
+
+
+def fused_objective_supported(X: torch.Tensor) -> bool:
+    """The fused HIP objective handles fp32 ``X`` on the GPU with ``d <= 512`` columns."""
+    return X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and 1 <= X.shape[1] <= _LR_DMAX \
+        and X.is_contiguous()
+
+
+def _n_blocks(N: int) -> int:
+    props = torch.cuda.get_device_properties(torch.cuda.current_device())
+    return max(1, min((N + 31) // 32, 2 * props.multi_processor_count))
+
+
+def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.Tensor, bias: torch.Tensor,
+                    loss: str, yscale=None, grad: bool = True):
+    """One pass of the fused HIP objective (``ops/csrc/hip/linear_kernels.hip``) for P problems.
+
+    ``m = X V + bias``; returns ``(f [P], r [P], G [d, P] or None)`` in fp64 with ``f = sum_i W l(m)``,
+    ``r = sum_i W l'(m)``, ``G = X^T (W * l'(m))``. Problems are processed 32 per launch."""
+    from . import _native as N_
+    N, d = X.shape
+    P = W.shape[1]
+    dev = X.device
+    yf = y.to(device=dev, dtype=torch.float32).contiguous()
+    Wf = W.to(torch.float32).contiguous()
+    nblk = _n_blocks(N)
+    dpad = ((d + 31) // 32) * 32
+    f = torch.empty(P, dtype=torch.float64, device=dev)
+    r = torch.empty(P, dtype=torch.float64, device=dev)
+    G = torch.empty(d, P, dtype=torch.float64, device=dev) if grad else None
+    fp = torch.empty(nblk, _LR_PC, dtype=torch.float64, device=dev)
+    rp = torch.empty_like(fp)
+    gp = torch.empty(nblk, dpad, _LR_PC, dtype=torch.float32, device=dev) if grad else fp
+    for c0 in range(0, P, _LR_PC):
+        pc = min(_LR_PC, P - c0)
+        Vc = torch.zeros(d, _LR_PC, dtype=torch.float32, device=dev)
+        Vc[:, :pc] = V[:, c0:c0 + pc]
+        bc = torch.zeros(_LR_PC, dtype=torch.float32, device=dev)
+        bc[:pc] = bias[c0:c0 + pc]
+        ys = None
+        if yscale is not None:
+            ys = torch.ones(_LR_PC, dtype=torch.float32, device=dev)
+            ys[:pc] = yscale[c0:c0 + pc]
+        N_.check(N_.hip().tmog_hip_lr_objective(
+            N_.ptr(X), N, d, N_.ptr(yf), N_.ptr(Wf), P, c0, pc, N_.ptr(Vc), N_.ptr(bc), LOSS_CODES[loss],
+            N_.ptr(ys), int(grad), N_.ptr(fp), N_.ptr(rp), N_.ptr(gp) if grad else None, nblk, N_.stream(dev)),
+            "lr_objective")
+        f[c0:c0 + pc] = fp[:, :pc].sum(0)
+        r[c0:c0 + pc] = rp[:, :pc].sum(0)
+        if grad:
+            G[:, c0:c0 + pc] = gp[:, :d, :pc].to(torch.float64).sum(0)
+    return f, r, G
