@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc
 rm -rf $OUT
 if [ -n "$LIST" ]; then timeout -k 10 120 rocprofv3 --list-avail > gpurun_out/pmc_list.txt 2>&1; fi
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${PMC:-SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM} --output-format csv -d $OUT -o run -- python3 $GRAFT_REPO_ROOT/benchmarks/bench_trees.py --rounds 1 ${GH_ARGS} > $GRAFT_REPO_ROOT/gpurun_out/pmc.log 2>&1; rc=$?
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${PMC:-SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM} --output-format csv -d $OUT -o run -- python3 $GRAFT_REPO_ROOT/${PMC_PROG:-benchmarks/bench_trees.py --rounds 1} ${GH_ARGS} > $GRAFT_REPO_ROOT/gpurun_out/pmc.log 2>&1; rc=$?
 cd $GRAFT_REPO_ROOT
 python - <<'PY'
 import csv, glob, collections

@@ -5,34 +5,36 @@
 // LogisticAggregator / HingeAggregator / LeastSquaresAggregator: margins, loss and gradient summed
 // over rows) for P problems at once -- the (config, fold) grid of the model selector, SURVEY.md K22.
 //
-// Per 32-row tile of X (row-major [N][d] fp32, staged once in LDS):
-//   phase A  M[32, 32] = X_tile . V           v_mfma_f32_32x32x2_f32, K (= d) split across the 4 waves
-//   epilogue l, dl/dm per (row, problem), R = W * dl/dm, weighted loss sums   (fused, LDS resident)
-//   phase B  G[d, 32] += X_tile^T . R         v_mfma_f32_32x32x2_f32, d split across the waves
+// Per 64-row tile of X (row-major [N][d] fp32, copied verbatim into LDS with 16-byte loads that are
+// issued one tile ahead, so HBM latency overlaps the MFMA work of the current tile), 8 waves:
+//   phase A  M[64, 32] = X_tile . V     v_mfma_f32_16x16x4_f32; wave w owns the 16x16 output block
+//            (rows 16(w&3).., problems 16(w>>2)..) over all of d; V is staged once in LDS
+//   epilogue in registers: l, dl/dm per (row, problem), R = W * dl/dm, weighted loss sums
+//   phase B  G[d, 32] += X_tile^T . R   v_mfma_f32_16x16x4_f32; 16x16 output blocks round-robin
+//            over the waves, accumulators resident for the whole kernel
 // so X is read from HBM exactly once per evaluation (the torch path reads it twice and round-trips M
-// and R through HBM). Workgroups are persistent and keep their G partial in accumulator registers;
-// the per-workgroup partials are summed in fp64 on the host side (ops/linear.py).
-//
-// LDS tile rows use a stride ds = d rounded up to 2 mod 4: the 32 rows of a phase-A operand read
-// land on 32 distinct even banks and the k+1 half on the odd ones (conflict-free ds_read_b32).
+// and R through HBM). Workgroups are persistent; their G / loss partials are summed in fp64 on the
+// host side (ops/linear.py). Phase-A column order inside each 64-column block is k = s + 16q (lane
+// group q) so the four lane groups of an operand read land 16 banks apart; V rows are padded to 33.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int TM = 32;         // rows per tile
+constexpr int TM = 64;         // rows per tile
+constexpr int NT = 512;        // threads per workgroup (8 waves)
 constexpr int PC = 32;         // problem columns per launch
-constexpr int DMAX = 512;      // KSW = max phase-A k-steps (column pairs) per wave, GTW = max phase-B
-                               // 32-column d tiles per wave: instantiated for d <= 256 / 384 / 512
+constexpr int VS = 33;         // LDS row stride of V
+constexpr int DMAX = 384;      // LDS: 64*384*4 (X) + 384*33*4 (V) + 64*32*4 (R) = 155 KB
 
 __device__ __forceinline__ void loss_and_grad(int loss, float m, float y, float ysc, float* l, float* g) {
   if (loss == 0) {              // logistic
     const float am = fabsf(m);
-    *l = fmaxf(m, 0.f) + log1pf(expf(-am)) - y * m;
-    const float e = expf(-am);
+    const float e = __expf(-am);
+    *l = fmaxf(m, 0.f) + log1pf(e) - y * m;
     const float sig = m >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
     *g = sig - y;
   } else if (loss == 1) {       // hinge
@@ -47,142 +49,170 @@ __device__ __forceinline__ void loss_and_grad(int loss, float m, float y, float 
   }
 }
 
-template <bool GRAD, int KSW, int GTW>
-__global__ void __launch_bounds__(256) lr_objective_kernel(
-    const float* __restrict__ X, int64_t N, int d, int ds, const float* __restrict__ y,
+__device__ __forceinline__ int kcol(int s, int q) { return 64 * (s >> 4) + (s & 15) + 16 * q; }
+
+// GB = phase-B output blocks per wave, NPF = prefetch float4 slots per thread
+template <bool GRAD, int GB, int NPF>
+__global__ void __launch_bounds__(NT) lr_objective_kernel(
+    const float* __restrict__ X, int64_t N, int d, const float* __restrict__ y,
     const float* __restrict__ W, int ldw, int wcol0, int P, const float* __restrict__ V,
     const float* __restrict__ bias, int loss, const float* __restrict__ yscale, double* __restrict__ f_part,
     double* __restrict__ r_part, float* __restrict__ G_part, int dpad) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* Xs = lds;                          // [TM][ds]
-  float* Mp = Xs + TM * ds;                 // [4][TM][PC] phase-A partials
-  float* Rs = Mp + 4 * TM * PC;             // [TM][PC]
+  const int ks_full = (d >> 6) * 16;        // phase-A k-steps over full 64-column blocks
+  const int ks_tail = ((d & 63) + 3) >> 2;  // k-steps over the ragged last block
+  const int dk = ((d + 63) >> 6) * 64;      // d rounded up to 64
+  const int xs_words = (TM * d + 64 + 3) & ~3;
+  float* Xs = lds;                          // [TM][d] + 64 words of overrun (finite, times V = 0)
+  float* Vs = Xs + xs_words;                // [dk][VS], zero beyond d
+  float* Rs = Vs + dk * VS;                 // [TM][PC]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 5, c32 = lane & 31;
-  const int ksteps = (d + 1) >> 1;
-  const int dtiles = (d + 31) >> 5;
+  const int q = lane >> 4, c = lane & 15;
+  const int rb = wave & 3, pb = wave >> 2;
+  const int nob = 2 * ((d + 15) >> 4);
 
-  // phase-A B operand (V) for this wave's k-steps s = wave + 4i, held in registers for the whole kernel
-  float vreg[KSW];
-#pragma unroll
-  for (int i = 0; i < KSW; ++i) {
-    const int s = wave + 4 * i;
-    const int k = 2 * s + h;
-    vreg[i] = (s < ksteps && k < d) ? V[(int64_t)k * PC + c32] : 0.f;
+  for (int i = threadIdx.x; i < xs_words; i += NT) Xs[i] = 0.f;
+  for (int i = threadIdx.x; i < dk * VS; i += NT) {
+    const int k = i / VS, j = i - k * VS;
+    Vs[i] = (k < d && j < PC) ? V[(int64_t)k * PC + j] : 0.f;
   }
-  f32x16 gacc[GTW];
+  f32x4 gacc[GB];
 #pragma unroll
-  for (int c = 0; c < GTW; ++c)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) gacc[c][r] = 0.f;
+  for (int i = 0; i < GB; ++i) gacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // epilogue ownership: thread t handles problem column p = t & 31, rows (t >> 5) + 8 j
-  const int ep = threadIdx.x & 31;
-  const int er = threadIdx.x >> 5;
-  const float bp = bias[ep];
-  const float ysp = yscale ? yscale[ep] : 1.f;
+  const int p = 16 * pb + c;                // this lane's problem column in phase A / epilogue
+  const float bp = bias[p];
+  const float ysp = yscale ? yscale[p] : 1.f;
   double f_acc = 0.0, r_acc = 0.0;
 
   const int64_t ntiles = (N + TM - 1) / TM;
+  const int tile_f4 = (TM * d) >> 2;
+  // branch-free prefetch (a guarded load makes hipcc wait vmcnt(0) per slot): out-of-range slots
+  // re-read the tile's last float4 and are zeroed at the LDS store. Host guarantees N * d % 4 == 0.
+  // The epilogue's W / y values of the next tile ride along (rows clamped to N - 1, masked later).
+  f32x4 pf[NPF];
+  float pw[4], py[4];
+  int nval4 = 0;
+  auto prefetch = [&](int64_t tile) {
+    const int64_t r0 = tile * TM;
+    nval4 = (int)((min((int64_t)TM, N - r0) * d) >> 2);
+    const f32x4* src = reinterpret_cast<const f32x4*>(X + r0 * (int64_t)d);
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) pf[i] = src[min((int)threadIdx.x + NT * i, nval4 - 1)];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t gr = min(r0 + 16 * rb + 4 * q + j, N - 1);
+      pw[j] = W[gr * ldw + wcol0 + min(p, P - 1)];
+      py[j] = y[gr];
+    }
+  };
+  if ((int64_t)blockIdx.x < ntiles) prefetch(blockIdx.x);
+  __syncthreads();
+
+  const float* va = Vs + 16 * pb + c;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t r0 = tile * TM;
     const int nrows = (int)min((int64_t)TM, N - r0);
-    // ---- stage the tile (contiguous in global memory) into LDS with row stride ds
-    const float* src = X + r0 * (int64_t)d;
-    const int n = nrows * d;
-    for (int e = threadIdx.x; e < TM * ds; e += blockDim.x) {
-      const int row = e / ds, col = e - row * ds;
-      Xs[e] = (row < nrows && col < d) ? src[row * d + col] : 0.f;
+    // ---- land the prefetched tile in LDS, then start fetching the next one
+    f32x4* xs4 = reinterpret_cast<f32x4*>(Xs);
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int e4 = threadIdx.x + NT * i;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      if (e4 < tile_f4) xs4[e4] = e4 < nval4 ? pf[i] : z;
     }
-    (void)n;
+    float cw[4], cy[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { cw[j] = pw[j]; cy[j] = py[j]; }
     __syncthreads();
+    if (tile + gridDim.x < ntiles) prefetch(tile + gridDim.x);
 
-    // ---- phase A: partial margins over this wave's k-steps
-    f32x16 macc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) macc[r] = 0.f;
-#pragma unroll
-    for (int i = 0; i < KSW; ++i) {
-      const int s = wave + 4 * i;
-      if (s < ksteps) {
-        const float a = Xs[c32 * ds + 2 * s + h];
-        macc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, vreg[i], macc, 0, 0, 0);
-      }
+    // ---- phase A: this wave's 16x16 margin block over all of d (two accumulators hide the
+    // 40-cycle dependent-MFMA latency)
+    // Full 64-column blocks use the bank-spread order; the ragged tail block steps 4 columns at a time.
+    f32x4 macc = {0.f, 0.f, 0.f, 0.f}, macc2 = {0.f, 0.f, 0.f, 0.f};
+    const float* xa = Xs + (16 * rb + c) * d;
+#pragma unroll 4
+    for (int s = 0; s < ks_full; s += 2) {
+      const int k0 = kcol(s, q), k1 = kcol(s + 1, q);
+      macc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k0], va[k0 * VS], macc, 0, 0, 0);
+      macc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k1], va[k1 * VS], macc2, 0, 0, 0);
     }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      Mp[(wave * TM + row) * PC + c32] = macc[r];
+    for (int k = 4 * ks_full + q; k < 4 * ks_full + 4 * ks_tail; k += 8) {
+      macc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k], va[k * VS], macc, 0, 0, 0);
+      if (k + 4 < 4 * ks_full + 4 * ks_tail)
+        macc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k + 4], va[(k + 4) * VS], macc2, 0, 0, 0);
     }
-    __syncthreads();
+    macc += macc2;
 
-    // ---- fused epilogue: loss, derivative, weights
+    // ---- fused epilogue in registers: rows 16rb + 4q + j, problem p
 #pragma unroll
-    for (int j = 0; j < TM / 8; ++j) {
-      const int row = er + 8 * j;
-      const int idx = row * PC + ep;
-      const float m = Mp[idx] + Mp[TM * PC + idx] + Mp[2 * TM * PC + idx] + Mp[3 * TM * PC + idx] + bp;
+    for (int j = 0; j < 4; ++j) {
+      const int row = 16 * rb + 4 * q + j;
       float rv = 0.f;
-      if (row < nrows && ep < P) {
-        const int64_t gr = r0 + row;
-        const float w = W[gr * ldw + wcol0 + ep];
+      if (row < nrows && p < P) {
+        const float w = cw[j];
         float l, g;
-        loss_and_grad(loss, m, y[gr], ysp, &l, &g);
+        loss_and_grad(loss, macc[j] + bp, cy[j], ysp, &l, &g);
         f_acc += (double)(l * w);
         rv = g * w;
         r_acc += (double)rv;
       }
-      if (GRAD) Rs[idx] = rv;
+      if (GRAD) Rs[row * PC + p] = rv;
     }
     if (GRAD) {
       __syncthreads();
-      // ---- phase B: G[d-tile, p] += X_tile^T R over the 32 rows (16 k-steps of 2 rows)
+      // ---- phase B: G[16db.., 16pb'..] += X_tile^T R  (16 k-steps of 4 rows)
+#pragma unroll 2
+      for (int t = 0; t < TM / 4; ++t) {
+        const int row = 4 * t + q;
+        const float rv0 = Rs[row * PC + c], rv1 = Rs[row * PC + 16 + c];
+        const float* xr = Xs + row * d + c;
 #pragma unroll
-      for (int c = 0; c < GTW; ++c) {
-        const int dt = wave + 4 * c;
-        if (dt < dtiles) {
-          const int col = 32 * dt + c32;
-          const bool okc = col < d;
-#pragma unroll
-          for (int t = 0; t < TM / 2; ++t) {
-            const int row = 2 * t + h;
-            const float a = okc ? Xs[row * ds + col] : 0.f;
-            const float b = Rs[row * PC + c32];
-            gacc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, gacc[c], 0, 0, 0);
-          }
+        for (int i = 0; i < GB; ++i) {
+          const int ob = wave + 8 * i;
+          if (ob < nob)
+            gacc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[16 * (ob >> 1)], (ob & 1) ? rv1 : rv0, gacc[i], 0, 0, 0);
         }
       }
     }
-    __syncthreads();          // Xs / Mp / Rs reused by the next tile
+    __syncthreads();          // Xs / Rs are rewritten by the next tile
   }
 
   // ---- per-workgroup partials
   if (GRAD) {
     float* gp = G_part + (int64_t)blockIdx.x * dpad * PC;
 #pragma unroll
-    for (int c = 0; c < GTW; ++c) {
-      const int dt = wave + 4 * c;
-      if (dt < dtiles) {
+    for (int i = 0; i < GB; ++i) {
+      const int ob = wave + 8 * i;
+      if (ob < nob) {
+        const int db = ob >> 1, pbb = ob & 1;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int dcol = 32 * dt + (r & 3) + 8 * (r >> 2) + 4 * h;
-          gp[(int64_t)dcol * PC + c32] = gacc[c][r];
-        }
+        for (int j = 0; j < 4; ++j) gp[(int64_t)(16 * db + 4 * q + j) * PC + 16 * pbb + c] = gacc[i][j];
       }
     }
   }
-  double* sf = reinterpret_cast<double*>(lds);   // reuse LDS: [256] f, [256] r
-  sf[threadIdx.x] = f_acc;
-  sf[256 + threadIdx.x] = r_acc;
+  // lanes sharing a problem column: 4 lane groups x 4 row-block waves
+  f_acc += __shfl_xor(f_acc, 16, 64);
+  f_acc += __shfl_xor(f_acc, 32, 64);
+  r_acc += __shfl_xor(r_acc, 16, 64);
+  r_acc += __shfl_xor(r_acc, 32, 64);
+  double* sf = reinterpret_cast<double*>(lds);
+  __syncthreads();
+  if (q == 0) {
+    sf[wave * 16 + c] = f_acc;
+    sf[128 + wave * 16 + c] = r_acc;
+  }
   __syncthreads();
   if (threadIdx.x < PC) {
+    const int pp = threadIdx.x, pbw = pp >> 4, cc = pp & 15;
     double fs = 0.0, rs = 0.0;
-    for (int k = 0; k < 8; ++k) {
-      fs += sf[threadIdx.x + 32 * k];
-      rs += sf[256 + threadIdx.x + 32 * k];
+    for (int r = 0; r < 4; ++r) {             // waves 4pb + r
+      fs += sf[(4 * pbw + r) * 16 + cc];
+      rs += sf[128 + (4 * pbw + r) * 16 + cc];
     }
-    f_part[(int64_t)blockIdx.x * PC + threadIdx.x] = fs;
-    r_part[(int64_t)blockIdx.x * PC + threadIdx.x] = rs;
+    f_part[(int64_t)blockIdx.x * PC + pp] = fs;
+    r_part[(int64_t)blockIdx.x * PC + pp] = rs;
   }
 }
 
@@ -198,23 +228,19 @@ int tmog_hip_lr_objective(const float* X, int64_t N, int d, const float* y, cons
                           int P, const float* V, const float* bias, int loss, const float* yscale, int grad,
                           double* f_part, double* r_part, float* G_part, int nblk, hipStream_t stream) {
   if (d > DMAX || d < 1 || P > PC || P < 1 || nblk < 1) return -2;
-  int ds = d;
-  while (ds % 4 != 2) ++ds;
-  const int dpad = ((d + 31) / 32) * 32;
-  size_t lds = (size_t)(TM * ds + 5 * TM * PC) * sizeof(float);
-  if (lds < 512 * sizeof(double)) lds = 512 * sizeof(double);
-#define TM_LR(G, K, T)                                                                                     \
-  hipLaunchKernelGGL((lr_objective_kernel<G, K, T>), dim3(nblk), dim3(256), lds, stream, X, N, d, ds, y, W, ldw, \
-                     wcol0, P, V, bias, loss, yscale, f_part, r_part, G_part, dpad)
-  if (grad) {
-    if (d <= 256) TM_LR(true, 32, 2);
-    else if (d <= 384) TM_LR(true, 48, 3);
-    else TM_LR(true, 64, 4);
-  } else {
-    if (d <= 256) TM_LR(false, 32, 2);
-    else if (d <= 384) TM_LR(false, 48, 3);
-    else TM_LR(false, 64, 4);
-  }
+  if ((reinterpret_cast<uintptr_t>(X) & 15) != 0 || (N * d) % 4 != 0) return -3;
+  const int dpad = ((d + 15) / 16) * 16;
+  const int dk = ((d + 63) / 64) * 64;
+  const size_t lds = (size_t)(((TM * d + 64 + 3) & ~3) + dk * VS + TM * PC) * sizeof(float);
+#define TM_LR(G, GB, DM)                                                                                  \
+  hipLaunchKernelGGL((lr_objective_kernel<G, GB, (TM * DM / 4 + NT - 1) / NT>), dim3(nblk), dim3(NT), lds, \
+                     stream, X, N, d, y, W, ldw, wcol0, P, V, bias, loss, yscale, f_part, r_part, G_part, dpad)
+#define TM_LR_D(G)                                   \
+  if (d <= 128) TM_LR(G, 2, 128);                    \
+  else if (d <= 256) TM_LR(G, 4, 256);               \
+  else TM_LR(G, 6, 384);
+  if (grad) { TM_LR_D(true) } else { TM_LR_D(false) }
+#undef TM_LR_D
 #undef TM_LR
   return (int)hipGetLastError();
 }

@@ -20,19 +20,20 @@ def gemm_t(X: torch.Tensor, R: torch.Tensor) -> torch.Tensor:
 
 
 LOSS_CODES = {"logistic": 0, "hinge": 1, "squared": 2}
-_LR_DMAX = 512
+_LR_DMAX = 384
 _LR_PC = 32
 
 
 def fused_objective_supported(X: torch.Tensor) -> bool:
-    """The fused HIP objective handles fp32 ``X`` on the GPU with ``d <= 512`` columns."""
+    """The fused HIP objective handles fp32 ``X`` on the GPU with ``d <= 384`` columns."""
     return X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and 1 <= X.shape[1] <= _LR_DMAX \
         and X.is_contiguous()
 
 
 def _n_blocks(N: int) -> int:
+    # persistent workgroups: one per CU (the 64-row tile + V fill ~150 KB of the 160 KB LDS)
     props = torch.cuda.get_device_properties(torch.cuda.current_device())
-    return max(1, min((N + 31) // 32, 2 * props.multi_processor_count))
+    return max(1, min((N + 63) // 64, props.multi_processor_count))
 
 
 def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.Tensor, bias: torch.Tensor,
@@ -45,10 +46,21 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
     N, d = X.shape
     P = W.shape[1]
     dev = X.device
+    if (N * d) % 4 or X.data_ptr() % 16:
+        # the kernel streams X in 16-byte chunks: run the <= 3 trailing rows through torch
+        Nm = N - N % 4 if X.data_ptr() % 16 == 0 else 0
+        parts = []
+        if Nm:
+            parts.append(fused_objective(X[:Nm], y[:Nm], W[:Nm], V, bias, loss, yscale, grad))
+        parts.append(_torch_objective(X[Nm:], y[Nm:], W[Nm:], V, bias, loss, yscale, grad))
+        f = sum(q[0] for q in parts)
+        r = sum(q[1] for q in parts)
+        G = sum(q[2] for q in parts) if grad else None
+        return f, r, G
     yf = y.to(device=dev, dtype=torch.float32).contiguous()
     Wf = W.to(torch.float32).contiguous()
     nblk = _n_blocks(N)
-    dpad = ((d + 31) // 32) * 32
+    dpad = ((d + 15) // 16) * 16
     f = torch.empty(P, dtype=torch.float64, device=dev)
     r = torch.empty(P, dtype=torch.float64, device=dev)
     G = torch.empty(d, P, dtype=torch.float64, device=dev) if grad else None
@@ -74,3 +86,24 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
         if grad:
             G[:, c0:c0 + pc] = gp[:, :d, :pc].to(torch.float64).sum(0)
     return f, r, G
+
+
+def _torch_objective(X, y, W, V, bias, loss, yscale, grad):
+    """Reference / tail path of ``fused_objective`` (same outputs, fp64 sums)."""
+    M = X @ V.to(X.dtype) + bias.to(X.dtype)[None, :]
+    yy = y.to(M.dtype)[:, None]
+    if loss == "logistic":
+        l = torch.nn.functional.softplus(M) - yy * M
+        g = torch.sigmoid(M) - yy
+    elif loss == "hinge":
+        ys = 2 * yy - 1
+        l = torch.clamp(1 - ys * M, min=0)
+        g = torch.where(ys * M < 1, -ys, torch.zeros_like(M))
+    else:
+        r = M - yy / yscale.to(M.dtype)[None, :]
+        l = 0.5 * r * r
+        g = r
+    Wm = W.to(M.dtype)
+    R = g * Wm
+    G = (X.t() @ R).to(torch.float64) if grad else None
+    return (l * Wm).sum(0).to(torch.float64), R.sum(0).to(torch.float64), G
