@@ -10,7 +10,7 @@ tensors' device.
 from __future__ import annotations
 
 import math
-from typing import Dict, Optional
+from typing import Dict, Optional, Sequence
 
 import numpy as np
 import torch
@@ -94,6 +94,32 @@ def binned_aupr(scores: torch.Tensor, labels: torch.Tensor, bins: int = 1 << 16)
     x = torch.cat([torch.zeros(1, dtype=torch.float64, device=rec.device), rec])
     yv = torch.cat([prec[:1], prec])
     return _trapz(x, yv)
+
+
+def binned_aupr_multi(scores: Sequence[torch.Tensor], labels: Sequence[torch.Tensor],
+                      bins: int = 1 << 16) -> torch.Tensor:
+    """``binned_aupr`` of several (scores, labels) sets at once, on the device, without host syncs:
+    one bincount over (set, label, bin), cumulative counts per set, trapezoids. Returns fp64 ``[K]``."""
+    K = len(scores)
+    dev = scores[0].device
+    sid = torch.cat([torch.full((s.numel(),), k, dtype=torch.int64, device=dev) for k, s in enumerate(scores)])
+    s = torch.cat([x.reshape(-1) for x in scores]).to(torch.float32).clamp(0, 1)
+    y = torch.cat([x.reshape(-1) for x in labels]).to(dev) > 0.5
+    b = (s * (bins - 1)).to(torch.int64)
+    idx = (sid * 2 + y.to(torch.int64)) * bins + (bins - 1 - b)        # descending score order
+    h = torch.bincount(idx, minlength=K * 2 * bins).to(torch.float64).view(K, 2, bins)
+    neg, pos = h[:, 0], h[:, 1]
+    tp, fp = torch.cumsum(pos, 1), torch.cumsum(neg, 1)
+    P = tp[:, -1:]
+    cnt = tp + fp
+    prec = tp / cnt.clamp_min(1)
+    first = torch.argmax((cnt > 0).to(torch.int8), 1, keepdim=True)
+    prec = torch.where(cnt > 0, prec, prec.gather(1, first))        # empty leading bins: width-0 points
+    rec = tp / P.clamp_min(1)
+    x = torch.cat([torch.zeros(K, 1, dtype=torch.float64, device=dev), rec], 1)
+    yv = torch.cat([prec.gather(1, first), prec], 1)
+    area = ((x[:, 1:] - x[:, :-1]) * (yv[:, 1:] + yv[:, :-1]) * 0.5).sum(1)
+    return torch.where(P[:, 0] > 0, area, torch.zeros_like(area))
 
 
 def confusion_at(pred: torch.Tensor, labels: torch.Tensor):

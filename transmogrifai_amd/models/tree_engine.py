@@ -314,25 +314,36 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         build_local = np.nonzero(build)[0]
 
         node_model = np.array([jobs[t].model for t in h_tree], np.int32) if T else np.zeros(0, np.int32)
-        nb_ = torch.as_tensor(lv_begin[hist_nodes], device=dev)
-        nc_ = torch.as_tensor(lv_count[hist_nodes], device=dev)
-        nfo = torch.as_tensor(feat_off, device=dev)
-        nnf = torch.as_tensor(nfeat, device=dev)
-        nmd = torch.as_tensor(node_model, device=dev)
-        nho = torch.as_tensor(hoff, device=dev)
+        params = np.zeros((m, 8), np.float32)
+        params[:, 0] = P_inst[h_tree]
+        params[:, 1] = P_gain[h_tree]
+        params[:, 2] = P_mcw[h_tree]
+        params[:, 3] = P_lam[h_tree]
+        params[:, 5] = 1.0 if missing_bin >= 0 else 0.0
+        params[:, 6] = P_eps[h_tree]
+        params[:, 7] = can[hist_nodes]
+        # every host->device array of the level's first half travels in one staged copy
+        pk = _Pack(dev)
+        i_nb, i_nc = pk.add(lv_begin[hist_nodes]), pk.add(lv_count[hist_nodes])
+        i_nfo, i_nnf, i_nmd, i_nho = pk.add(feat_off), pk.add(nfeat), pk.add(node_model), pk.add(hoff)
+        i_par = pk.add(params)
         if on_gpu:
             items = _hist_items(build_local, lv_begin[hist_nodes], lv_count[hist_nodes], nfeat, chunk_rows)
+            citems = _part_items(np.arange(m), lv_begin[hist_nodes], lv_count[hist_nodes], chunk_rows)
+            i_it, i_cit = pk.add(items.view(np.uint8)), pk.add(citems.view(np.uint8))
+            if derive_big.size:
+                i_sub = [pk.add(derive_poff), pk.add(hoff[derive_small]), pk.add(hoff[derive_big]),
+                         pk.add(hsz[derive_big])]
+        dv = pk.ship()
+        nb_, nc_, nfo, nnf, nmd, nho, par_t = (dv[i] for i in (i_nb, i_nc, i_nfo, i_nnf, i_nmd, i_nho, i_par))
+        if on_gpu:
             if len(items):
-                it_t = torch.as_tensor(items.view(np.uint8), device=dev)
                 N.check(N.hip().tmog_hip_hist_build(
-                    N.ptr(Xb), F, N.ptr(rows), N.ptr(it_t), len(items), N.ptr(nfo), N.ptr(feat_list),
+                    N.ptr(Xb), F, N.ptr(rows), N.ptr(dv[i_it]), len(items), N.ptr(nfo), N.ptr(feat_list),
                     N.ptr(nmd), N.ptr(nho), N.ptr(hist), B, mode, S, N.ptr(yf), N.ptr(t1f), N.ptr(t2f),
                     stride, N.ptr(qscale), N.stream(dev)), "hist_build")
             if derive_big.size:
-                par = torch.as_tensor(derive_poff, device=dev)
-                sm = torch.as_tensor(hoff[derive_small], device=dev)
-                oo = torch.as_tensor(hoff[derive_big], device=dev)
-                sz = torch.as_tensor(hsz[derive_big], device=dev)
+                par, sm, oo, sz = (dv[i] for i in i_sub)
                 N.check(N.hip().tmog_hip_hist_subtract(
                     N.ptr(hist), N.ptr(prev_hist), N.ptr(par), N.ptr(sm), N.ptr(oo), N.ptr(sz), int(derive_big.size),
                     int(hsz[derive_big].max()), N.stream(dev)), "hist_subtract")
@@ -349,45 +360,29 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 sz = int(hsz[b_])
                 hist[hoff[b_]:hoff[b_] + sz] = prev_hist[p_:p_ + sz] - hist[hoff[s_]:hoff[s_] + sz]
 
-        # ---- split scan
-        params = np.zeros((m, 8), np.float32)
-        params[:, 0] = P_inst[h_tree]
-        params[:, 1] = P_gain[h_tree]
-        params[:, 2] = P_mcw[h_tree]
-        params[:, 3] = P_lam[h_tree]
-        params[:, 5] = 1.0 if missing_bin >= 0 else 0.0
-        par_t = torch.as_tensor(params, device=dev)
-        s_feat = torch.empty(m, dtype=torch.int32, device=dev)
-        s_bin = torch.empty(m, dtype=torch.int32, device=dev)
-        s_gain = torch.empty(m, dtype=torch.float32, device=dev)
-        s_dl = torch.empty(m, dtype=torch.uint8, device=dev)
-        s_left = torch.empty(m * S, dtype=torch.float32, device=dev)
-        s_tot = torch.empty(m * S, dtype=torch.float32, device=dev)
+        # ---- split scan + partition count write into one result buffer -> one device->host sync
+        ncit = len(citems) if on_gpu else 0
+        res = _LevelResult(m, S, ncit, dev)
         fn = N.hip().tmog_hip_split_find if on_gpu else N.host().tmog_split_find_cpu
         extra = (N.stream(dev),) if on_gpu else ()
         N.check(fn(N.ptr(hist), m, N.ptr(nho), N.ptr(nnf), N.ptr(nfo), N.ptr(feat_list), N.ptr(n_bins_t), B, S,
-                   kind, N.ptr(par_t), missing_bin, N.ptr(nmd), N.ptr(qinv), N.ptr(s_feat), N.ptr(s_bin), N.ptr(s_gain), N.ptr(s_dl),
-                   N.ptr(s_left), N.ptr(s_tot), *extra), "split_find")
-        eps = torch.as_tensor(P_eps[h_tree].astype(np.float32), device=dev)
-        can_t = torch.as_tensor(can[hist_nodes], device=dev)
-        ok = can_t & (s_feat >= 0) & (s_gain > eps)
-        s_feat = torch.where(ok, s_feat, torch.full_like(s_feat, -1))
-
-        # ---- partition count (GPU), then one sync for every decision of the level
+                   kind, N.ptr(par_t), missing_bin, N.ptr(nmd), N.ptr(qinv), N.ptr(res.feat), N.ptr(res.bin),
+                   N.ptr(res.gain), N.ptr(res.dl), N.ptr(res.left), N.ptr(res.tot), *extra), "split_find")
+        ok = (par_t[:, 7] > 0.5) & (res.feat >= 0) & (res.gain > par_t[:, 6])
+        res.feat.masked_fill_(~ok, -1)
+        s_feat, s_bin, s_dl = res.feat, res.bin, res.dl
         if on_gpu:
-            citems = _part_items(np.arange(m), lv_begin[hist_nodes], lv_count[hist_nodes], chunk_rows)
-            cit = torch.as_tensor(citems.view(np.uint8), device=dev)
-            chunk_left = torch.zeros(len(citems), dtype=torch.int64, device=dev)
             N.check(N.hip().tmog_hip_partition_count(
-                N.ptr(Xb), F, N.ptr(rows), N.ptr(cit), len(citems), N.ptr(s_feat), N.ptr(s_bin), N.ptr(s_dl),
-                missing_bin, N.ptr(chunk_left), N.stream(dev)), "partition_count")
-            h_chunk_left = chunk_left.cpu().numpy()
-        h_feat = s_feat.cpu().numpy().astype(np.int64)
-        h_bin = s_bin.cpu().numpy().astype(np.int64)
-        h_gain = s_gain.cpu().numpy().astype(np.float64)
-        h_dl = s_dl.cpu().numpy()
-        h_left = s_left.cpu().numpy().reshape(m, S).astype(np.float64)
-        h_tot = s_tot.cpu().numpy().reshape(m, S).astype(np.float64)
+                N.ptr(Xb), F, N.ptr(rows), N.ptr(dv[i_cit]), ncit, N.ptr(s_feat), N.ptr(s_bin), N.ptr(s_dl),
+                missing_bin, N.ptr(res.chunk_left), N.stream(dev)), "partition_count")
+        h = res.fetch()
+        h_chunk_left = h["chunk_left"]
+        h_feat = h["feat"].astype(np.int64)
+        h_bin = h["bin"].astype(np.int64)
+        h_gain = h["gain"].astype(np.float64)
+        h_dl = h["dl"]
+        h_left = h["left"].reshape(m, S).astype(np.float64)
+        h_tot = h["tot"].reshape(m, S).astype(np.float64)
 
         g_h = lv_gid[hist_nodes]
         G.tot[g_h] = h_tot
@@ -408,9 +403,11 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         out_begin[1:] = np.cumsum(counts_sl[:-1])
         if on_gpu:
             nl, sitems = _scatter_items(citems, h_chunk_left, sl, m, out_begin)
-            sit = torch.as_tensor(sitems.view(np.uint8), device=dev)
+            sit = _Pack(dev)
+            i_s = sit.add(sitems.view(np.uint8))
+            sit_t = sit.ship()[i_s]
             N.check(N.hip().tmog_hip_partition_scatter(
-                N.ptr(Xb), F, N.ptr(rows), N.ptr(rows_alt), N.ptr(sit), len(sitems), N.ptr(s_feat), N.ptr(s_bin),
+                N.ptr(Xb), F, N.ptr(rows), N.ptr(rows_alt), N.ptr(sit_t), len(sitems), N.ptr(s_feat), N.ptr(s_bin),
                 N.ptr(s_dl), missing_bin, N.stream(dev)), "partition_scatter")
         else:
             lsel = torch.as_tensor(sl, device=dev)
@@ -474,6 +471,93 @@ class LeafAssign:
         return self.value[self.gid.to(torch.int64)]
 
 
+_TORCH_OF_NP = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32,
+                np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+                np.dtype(np.uint8): torch.uint8, np.dtype(np.bool_): torch.bool}
+
+
+class _Pack:
+    """Ships several small host arrays with ONE host->device copy through a pinned staging ring
+    (each ``torch.as_tensor(a, device=cuda)`` is its own blocking hipMemcpy: ~10 per tree level)."""
+    _ring: dict = {}
+    _RING = 4
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.arrs: List[np.ndarray] = []
+
+    def add(self, a) -> int:
+        self.arrs.append(np.ascontiguousarray(a))
+        return len(self.arrs) - 1
+
+    def ship(self) -> List[torch.Tensor]:
+        if self.dev.type != "cuda":
+            return [torch.from_numpy(a) for a in self.arrs]
+        offs, tot = [], 0
+        for a in self.arrs:
+            offs.append(tot)
+            tot += (a.nbytes + 15) & ~15
+        tot = max(tot, 16)
+        key = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
+        slots = _Pack._ring.setdefault(key, {"i": 0, "bufs": [None] * self._RING, "ev": [None] * self._RING})
+        k = slots["i"] = (slots["i"] + 1) % self._RING
+        buf, ev = slots["bufs"][k], slots["ev"][k]
+        if ev is not None:
+            ev.synchronize()                 # the copy that last used this slot has finished
+        if buf is None or buf.numel() < tot:
+            buf = torch.empty(max(tot, 1 << 16), dtype=torch.uint8, pin_memory=True)
+            slots["bufs"][k] = buf
+        hb = buf.numpy()
+        for a, o in zip(self.arrs, offs):
+            hb[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
+        d = torch.empty(tot, dtype=torch.uint8, device=self.dev)
+        d.copy_(buf[:tot], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        slots["ev"][k] = ev
+        return [d[o:o + a.nbytes].view(_TORCH_OF_NP[a.dtype]).reshape(a.shape) if a.dtype in _TORCH_OF_NP
+                else d[o:o + a.nbytes] for a, o in zip(self.arrs, offs)]
+
+
+class _LevelResult:
+    """Split-scan and partition-count outputs of one level laid out in one int32 device buffer so
+    the host reads every decision of the level with a single device->host copy."""
+
+    def __init__(self, m, S, n_chunks, dev):
+        self.m, self.S, self.nc = m, S, n_chunks
+        words = 2 * n_chunks + 3 * m + 2 * m * S + (m + 3) // 4
+        self.buf = torch.empty(max(words, 1), dtype=torch.int32, device=dev)
+        o = 0
+        self.chunk_left = self.buf[o:o + 2 * n_chunks].view(torch.int64)
+        self.chunk_left.zero_()
+        o += 2 * n_chunks
+        self.feat = self.buf[o:o + m]
+        o += m
+        self.bin = self.buf[o:o + m]
+        o += m
+        self.gain = self.buf[o:o + m].view(torch.float32)
+        o += m
+        self.left = self.buf[o:o + m * S].view(torch.float32)
+        o += m * S
+        self.tot = self.buf[o:o + m * S].view(torch.float32)
+        o += m * S
+        self.dl = self.buf[o:o + (m + 3) // 4].view(torch.uint8)[:m]
+
+    def fetch(self) -> dict:
+        h = self.buf.cpu().numpy()
+        m, S, o = self.m, self.S, 2 * self.nc
+        out = {"chunk_left": h[:o].view(np.int64)}
+        out["feat"] = h[o:o + m]
+        out["bin"] = h[o + m:o + 2 * m]
+        out["gain"] = h[o + 2 * m:o + 3 * m].view(np.float32)
+        o += 3 * m
+        out["left"] = h[o:o + m * S].view(np.float32)
+        out["tot"] = h[o + m * S:o + 2 * m * S].view(np.float32)
+        o += 2 * m * S
+        out["dl"] = h[o:o + (m + 3) // 4].view(np.uint8)[:m]
+        return out
+
+
 class _LeafCollector:
     def __init__(self, total, dev, chunk_rows):
         self.rows = torch.empty(total, dtype=torch.int32, device=dev)
@@ -499,7 +583,9 @@ class _LeafCollector:
             a["count"] = np.minimum(self.chunk, count[seg] - c * self.chunk)
             a["out"] = out[seg] + c * self.chunk
             a["gid"] = gid[seg]
-            it = torch.as_tensor(a.view(np.uint8), device=self.dev)
+            pk = _Pack(self.dev)
+            i_a = pk.add(a.view(np.uint8))
+            it = pk.ship()[i_a]
             N.check(N.hip().tmog_hip_leaf_collect(N.ptr(rows), N.ptr(it), len(a), N.ptr(self.rows), N.ptr(self.gid),
                                                   N.stream(self.dev)), "leaf_collect")
         else:

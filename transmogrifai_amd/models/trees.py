@@ -474,7 +474,7 @@ class XGBoostClassifierLearner(_BoostLearner):
         return math.log(bs / (1 - bs))
 
     def _boost(self, Xb, spec, y, jobs, N, F, dev, mb):
-        from ..evaluators.metrics import binned_aupr
+        from ..evaluators.metrics import binned_aupr_multi
         P = len(jobs)
         rows = [_rows(j, N, dev) for j in jobs]
         rounds = [int(j.params.get("num_round", 100)) for j in jobs]
@@ -482,6 +482,7 @@ class XGBoostClassifierLearner(_BoostLearner):
         base = [self._base_margin(float(j.params.get("base_score", 0.5))) for j in jobs]
         Fm = torch.tensor(base, dtype=torch.float64, device=dev)[:, None].repeat(1, N)
         yy = y.to(torch.float64)
+        ylab = [yy[r] for r in rows]
         forests, weights = [[] for _ in range(P)], [[] for _ in range(P)]
         best = [-float("inf")] * P
         best_round = [0] * P
@@ -518,11 +519,9 @@ class XGBoostClassifierLearner(_BoostLearner):
             # early stopping on the training metric (the reference sets no eval set)
             need = [p for p in act if esr[p] > 0]
             if need and self.classification:
-                scores = torch.stack([torch.sigmoid(Fm[p][rows[p]]) for p in need]) if \
-                    len({rows[p].numel() for p in need}) == 1 else None
-                for k, p in enumerate(need):
-                    s = scores[k] if scores is not None else torch.sigmoid(Fm[p][rows[p]])
-                    v = binned_aupr(s, yy[rows[p]])
+                vals = binned_aupr_multi([torch.sigmoid(Fm[p][rows[p]]) for p in need],
+                                         [ylab[p] for p in need]).tolist()     # one sync per round
+                for p, v in zip(need, vals):
                     if v > best[p] + 1e-12:
                         best[p], best_round[p] = v, it
                     elif it - best_round[p] >= esr[p]:
