@@ -29,7 +29,8 @@ __global__ void __launch_bounds__(256) k(const uint32_t* __restrict__ seed, floa
       atomicAdd(p, 1u);
       atomicAdd(p + 1, 3u);
     } else if (V == 2) {
-      atomicAdd(reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(p) & ~uintptr_t(7))), 0x0000000300000001ull);
+      unsigned long long* t64 = reinterpret_cast<unsigned long long*>(&tab[0][0]);
+      atomicAdd(t64 + lane * 65 + bin, 0x0000000300000001ull);
     } else {
       float* q = reinterpret_cast<float*>(p);
       q[0] += 1.0f;

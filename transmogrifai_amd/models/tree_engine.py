@@ -212,8 +212,11 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 n_classes: int = 2, y: Optional[torch.Tensor] = None, t1: Optional[torch.Tensor] = None,
                 t2: Optional[torch.Tensor] = None, B: int = 32, missing_bin: int = -1,
                 subtract: bool = True, chunk_rows: int = 4096, rng_seed: int = 0,
-                collect_leaves: bool = False) -> Forest:
+                collect_leaves: bool = False, groups: Optional[int] = None) -> Forest:
     """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``.
+
+    Jobs are split into ``groups`` (default 2) contiguous groups grown as independent pipelines on
+    separate HIP streams; each group draws its feature subsets from its own seeded generator.
 
     ``collect_leaves``: also return, as ``forest.leaf_assign``, the final leaf of every training entry
     (see ``LeafAssign``) so boosting can update margins without re-walking the new trees."""
@@ -233,6 +236,74 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     t2f = t2.to(device=dev, dtype=torch.float32).contiguous() if t2 is not None else None
     Xb = Xb.contiguous()
     T = len(jobs)
+    all_feats = torch.arange(F, dtype=torch.int32, device=dev)
+    ng = groups if groups is not None else (2 if T >= 2 else 1)
+    ng = max(1, min(ng, T)) if T else 1
+    cuts = np.linspace(0, T, ng + 1).astype(np.int64)
+    gens = [_grow_group(Xb, n_bins_t, all_feats, list(jobs[cuts[g]:cuts[g + 1]]), mode, kind, S, K, B, missing_bin,
+                        yf, t1f, t2f, stride, subtract, chunk_rows,
+                        int(rng_seed) if ng == 1 else int(rng_seed) + 1000003 * g, collect_leaves)
+            for g in range(ng)]
+    results = [None] * ng
+    if on_gpu and ng > 1:
+        # two job groups on two streams: while the host reads one group's level and plans the next,
+        # the GPU works on the other group's kernels
+        cur = torch.cuda.current_stream(dev)
+        streams = _group_streams(dev, ng)
+        for st in streams:
+            st.wait_stream(cur)
+        alive = list(range(ng))
+        while alive:
+            for g in list(alive):
+                with torch.cuda.stream(streams[g]):
+                    try:
+                        next(gens[g])
+                    except StopIteration as e:
+                        results[g] = e.value
+                        alive.remove(g)
+        for st in streams:
+            cur.wait_stream(st)
+    else:
+        for g in range(ng):
+            while True:
+                try:
+                    next(gens[g])
+                except StopIteration as e:
+                    results[g] = e.value
+                    break
+    if ng == 1:
+        return results[0]
+    forest = Forest.concat(results)
+    if collect_leaves:
+        las = [f.leaf_assign for f in results]
+        goff = np.concatenate([[0], np.cumsum([int(la.value.shape[0]) for la in las])[:-1]])
+        forest.leaf_assign = LeafAssign(
+            torch.cat([la.rows for la in las]),
+            torch.cat([la.gid + int(o) for la, o in zip(las, goff)]),
+            torch.cat([la.value for la in las]),
+            torch.cat([la.tree + int(cuts[g]) for g, la in enumerate(las)]))
+    return forest
+
+
+_STREAMS: dict = {}
+
+
+def _group_streams(dev, n):
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    lst = _STREAMS.setdefault(key, [])
+    while len(lst) < n:
+        lst.append(torch.cuda.Stream(device=dev))
+    return lst[:n]
+
+
+def _grow_group(Xb, n_bins_t, all_feats, jobs, mode, kind, S, K, B, missing_bin, yf, t1f, t2f, stride,
+                subtract, chunk_rows, rng_seed, collect_leaves):
+    """Level-synchronous growth of one job group (generator: yields once per level, right before
+    the level's device->host read, so another group's kernels can be queued behind this group's)."""
+    dev = Xb.device
+    on_gpu = dev.type == "cuda"
+    Nrows, F = int(Xb.shape[0]), int(Xb.shape[1])
+    T = len(jobs)
     P_depth = np.array([j.params.max_depth for j in jobs], np.int64)
     P_inst = np.array([j.params.min_instances for j in jobs], np.float64)
     P_gain = np.array([j.params.min_info_gain for j in jobs], np.float64)
@@ -242,7 +313,6 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     P_sub = np.array([F if (j.params.feature_subset is None or j.params.feature_subset >= F)
                       else max(1, int(j.params.feature_subset)) for j in jobs], np.int64)
     use_subset = bool(np.any(P_sub < F))
-    all_feats = torch.arange(F, dtype=torch.int32, device=dev)
     gen = torch.Generator(device="cpu")
     gen.manual_seed(int(rng_seed))
     G = _Grow(S)
@@ -292,7 +362,8 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         hoff = np.zeros(m, np.int64)
         if m > 1:
             hoff[1:] = np.cumsum(hsz[:-1])
-        hist = torch.zeros(int(hsz.sum()), dtype=torch.int64, device=dev)
+        hist = torch.empty(int(hsz.sum()), dtype=torch.int64, device=dev) if on_gpu else \
+            torch.zeros(int(hsz.sum()), dtype=torch.int64, device=dev)
         loc = np.full(n, -1, np.int64)
         loc[hist_nodes] = np.arange(m)
 
@@ -331,12 +402,19 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
             items = _hist_items(build_local, lv_begin[hist_nodes], lv_count[hist_nodes], nfeat, chunk_rows)
             citems = _part_items(np.arange(m), lv_begin[hist_nodes], lv_count[hist_nodes], chunk_rows)
             i_it, i_cit = pk.add(items.view(np.uint8)), pk.add(citems.view(np.uint8))
+            multi = build_local[lv_count[hist_nodes[build_local]] > chunk_rows]
+            if multi.size:
+                i_z = (pk.add(hoff[multi]), pk.add(hsz[multi]))
             if derive_big.size:
                 i_sub = [pk.add(derive_poff), pk.add(hoff[derive_small]), pk.add(hoff[derive_big]),
                          pk.add(hsz[derive_big])]
         dv = pk.ship()
         nb_, nc_, nfo, nnf, nmd, nho, par_t = (dv[i] for i in (i_nb, i_nc, i_nfo, i_nnf, i_nmd, i_nho, i_par))
         if on_gpu:
+            if multi.size:
+                N.check(N.hip().tmog_hip_zero_segments(N.ptr(hist), N.ptr(dv[i_z[0]]), N.ptr(dv[i_z[1]]),
+                                                       int(multi.size), int(hsz[multi].max()), N.stream(dev)),
+                        "zero_segments")
             if len(items):
                 N.check(N.hip().tmog_hip_hist_build(
                     N.ptr(Xb), F, N.ptr(rows), N.ptr(dv[i_it]), len(items), N.ptr(nfo), N.ptr(feat_list),
@@ -363,11 +441,18 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         # ---- split scan + partition count write into one result buffer -> one device->host sync
         ncit = len(citems) if on_gpu else 0
         res = _LevelResult(m, S, ncit, dev)
-        fn = N.hip().tmog_hip_split_find if on_gpu else N.host().tmog_split_find_cpu
-        extra = (N.stream(dev),) if on_gpu else ()
-        N.check(fn(N.ptr(hist), m, N.ptr(nho), N.ptr(nnf), N.ptr(nfo), N.ptr(feat_list), N.ptr(n_bins_t), B, S,
-                   kind, N.ptr(par_t), missing_bin, N.ptr(nmd), N.ptr(qinv), N.ptr(res.feat), N.ptr(res.bin),
-                   N.ptr(res.gain), N.ptr(res.dl), N.ptr(res.left), N.ptr(res.tot), *extra), "split_find")
+        if on_gpu:
+            mx = int(nfeat.max())
+            cand = torch.empty(m * (-(-mx // 16)) * 24, dtype=torch.uint8, device=dev)   # Best[m][fb] workspace
+            N.check(N.hip().tmog_hip_split_find(
+                N.ptr(hist), m, N.ptr(nho), N.ptr(nnf), N.ptr(nfo), N.ptr(feat_list), N.ptr(n_bins_t), B, S, kind,
+                N.ptr(par_t), missing_bin, N.ptr(nmd), N.ptr(qinv), mx, N.ptr(cand), N.ptr(res.feat), N.ptr(res.bin),
+                N.ptr(res.gain), N.ptr(res.dl), N.ptr(res.left), N.ptr(res.tot), N.stream(dev)), "split_find")
+        else:
+            N.check(N.host().tmog_split_find_cpu(
+                N.ptr(hist), m, N.ptr(nho), N.ptr(nnf), N.ptr(nfo), N.ptr(feat_list), N.ptr(n_bins_t), B, S, kind,
+                N.ptr(par_t), missing_bin, N.ptr(nmd), N.ptr(qinv), N.ptr(res.feat), N.ptr(res.bin), N.ptr(res.gain),
+                N.ptr(res.dl), N.ptr(res.left), N.ptr(res.tot)), "split_find_cpu")
         ok = (par_t[:, 7] > 0.5) & (res.feat >= 0) & (res.gain > par_t[:, 6])
         res.feat.masked_fill_(~ok, -1)
         s_feat, s_bin, s_dl = res.feat, res.bin, res.dl
@@ -375,6 +460,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
             N.check(N.hip().tmog_hip_partition_count(
                 N.ptr(Xb), F, N.ptr(rows), N.ptr(dv[i_cit]), ncit, N.ptr(s_feat), N.ptr(s_bin), N.ptr(s_dl),
                 missing_bin, N.ptr(res.chunk_left), N.stream(dev)), "partition_count")
+        yield                                   # the other job group enqueues its level meanwhile
         h = res.fetch()
         h_chunk_left = h["chunk_left"]
         h_feat = h["feat"].astype(np.int64)
@@ -614,7 +700,10 @@ def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev):
         if t is None:
             return torch.zeros(n_models, dtype=torch.float32, device=dev)
         v = t.reshape(t.shape[0], -1) if t.dim() == 2 else t.reshape(1, -1)
-        m = v.abs().amax(1)
+        if v.shape[1] >= 1 << 16 and v.shape[1] % 256 == 0:   # row-wise amax of a few long rows: split them
+            m = v.abs().view(v.shape[0], 256, -1).amax(2).amax(1)
+        else:
+            m = v.abs().amax(1)
         return m.expand(n_models) if m.numel() == 1 else m[:n_models]
 
     def pow2(bound):

@@ -170,6 +170,18 @@ __global__ void hist_subtract_kernel(int64_t* __restrict__ hist, const int64_t* 
     o[k] = p[k] - s[k];
 }
 
+// zero the histograms of nodes built from several row chunks (their items accumulate atomically);
+// single-chunk and derived nodes are fully overwritten, so the level buffer is never memset whole
+__global__ void zero_segments_kernel(int64_t* __restrict__ hist, const int64_t* __restrict__ off,
+                                     const int64_t* __restrict__ size, int n) {
+  const int j = blockIdx.y;
+  if (j >= n) return;
+  int64_t* o = hist + off[j];
+  const int64_t sz = size[j];
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += (int64_t)gridDim.x * blockDim.x)
+    o[k] = 0;
+}
+
 // ------------------------------------------------------------------------------- split finding
 __device__ __forceinline__ double impurity_dev(const double* st, int S, int kind, double* cnt) {
   if (kind == 0 || kind == 1) {
@@ -210,92 +222,93 @@ __device__ __forceinline__ bool better(const Best& a, const Best& b) {
   return a.b < b.b;
 }
 
-// One workgroup (4 waves) per node; each wave scans features (lane = bin, B <= 64) with an exact
-// int64 wave prefix sum of the fixed-point histogram, converting to double only to evaluate gains
-// (identical arithmetic to tmog_split_find_cpu, so both pick the same split bit for bit). The block
-// then reduces the best (gain, f, dl, b). SM = compile-time bound on S (register arrays sized to it).
+// Split scan, two kernels. split_scan_kernel: grid (node, feature block of FPB = 16 features); each
+// of the 4 waves scans 4 features (lane = bin, B <= 64) with an exact int64 wave prefix sum of the
+// fixed-point histogram, converting to double only to evaluate gains (identical arithmetic to
+// tmog_split_find_cpu, so both pick the same split bit for bit); the block's best candidate goes to
+// cand[node][fb]. split_reduce_kernel: one wave per node picks the best candidate with the CPU's
+// tie-break (gain, then lowest feature, dl, bin) and sums the winner's left statistics. Spreading a
+// node over feature blocks fills the chip at the shallow levels (6 root nodes = 6 workgroups before).
+// SM = compile-time bound on S (register arrays sized to it).
+constexpr int FPB = 16;
+
 template <int SM>
-__global__ void __launch_bounds__(256) split_find_kernel(
+__global__ void __launch_bounds__(256) split_scan_kernel(
     const int64_t* __restrict__ hist, const int64_t* __restrict__ node_hist_off, const int32_t* __restrict__ node_nfeat,
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
-    int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv,
-    int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin, float* __restrict__ out_gain,
-    uint8_t* __restrict__ out_dl, float* __restrict__ out_left, float* __restrict__ out_total) {
-  const int j = blockIdx.x;
-  const int64_t* h = hist + node_hist_off[j];
-  const int nf = node_nfeat[j];
-  const int32_t* fl = feat_list + node_feat_off[j];
-  const float* P = node_params + (int64_t)j * 8;
-  const double* qi = qinv + (int64_t)(node_model ? node_model[j] : 0) * S;
-  const double min_inst = P[0], min_gain = P[1], mcw = P[2], lambda = P[3];
-  const bool allow_missing = P[5] > 0.5f && missing_bin >= 0;
-  __shared__ int64_t s_tot[SM];
-  __shared__ Best s_best[4];
+    int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
+    Best* __restrict__ cand) {
+  const int j = blockIdx.x / fbmax;
+  const int fb = blockIdx.x - j * fbmax;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x < S) {
-    int64_t t = 0;
-    for (int b = 0; b < B; ++b) t += h[b * S + threadIdx.x];
-    s_tot[threadIdx.x] = t;
-    out_total[(int64_t)j * S + threadIdx.x] = (float)((double)t * qi[threadIdx.x]);
-  }
-  __syncthreads();
-  int64_t totq[SM];
-  double tot[SM], q[SM];
-  for (int s = 0; s < S; ++s) {
-    q[s] = qi[s];
-    totq[s] = s_tot[s];
-    tot[s] = (double)totq[s] * q[s];
-  }
-  double tcount;
-  const double pimp = impurity_dev(tot, S, kind, &tcount);
-  const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
-
+  const int nf = node_nfeat[j];
+  __shared__ Best s_best[4];
   Best best{-INFINITY, 0x7fffffff, 0, 0};
-  for (int f = wave; f < nf; f += 4) {
-    const int nb = feat_nbins[fl[f]];
-    const int64_t* hf = h + (int64_t)f * B * S;
-    int64_t v[SM], miss[SM];
+  if (fb * FPB < nf) {
+    const int64_t* h = hist + node_hist_off[j];
+    const int32_t* fl = feat_list + node_feat_off[j];
+    const float* P = node_params + (int64_t)j * 8;
+    const double* qi = qinv + (int64_t)(node_model ? node_model[j] : 0) * S;
+    const double min_inst = P[0], min_gain = P[1], mcw = P[2], lambda = P[3];
+    const bool allow_missing = P[5] > 0.5f && missing_bin >= 0;
+    // node totals from feature 0 (every row is counted once per feature, including the missing bin)
+    int64_t totq[SM];
+    double tot[SM], q[SM];
     for (int s = 0; s < S; ++s) {
-      v[s] = (lane < nb - 1) ? hf[lane * S + s] : 0;
-      miss[s] = allow_missing ? hf[missing_bin * S + s] : 0;
+      int64_t v = lane < B ? h[lane * S + s] : 0;
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      totq[s] = v;
+      q[s] = qi[s];
+      tot[s] = (double)v * q[s];
     }
-    // inclusive wave prefix over bins (exact)
-    for (int off = 1; off < 64; off <<= 1) {
+    double tcount;
+    const double pimp = impurity_dev(tot, S, kind, &tcount);
+    const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
+    const int f_end = min(nf, (fb + 1) * FPB);
+    for (int f = fb * FPB + wave; f < f_end; f += 4) {
+      const int nb = feat_nbins[fl[f]];
+      const int64_t* hf = h + (int64_t)f * B * S;
+      int64_t v[SM], miss[SM];
       for (int s = 0; s < S; ++s) {
-        const int64_t o = __shfl_up(v[s], off, 64);
-        if (lane >= off) v[s] += o;
+        v[s] = (lane < nb - 1) ? hf[lane * S + s] : 0;
+        miss[s] = allow_missing ? hf[missing_bin * S + s] : 0;
       }
-    }
-    if (lane < nb - 1) {
-      for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
-        double left[SM], right[SM];
+      for (int off = 1; off < 64; off <<= 1) {
         for (int s = 0; s < S; ++s) {
-          const int64_t lq = v[s] + (dl ? miss[s] : 0);
-          left[s] = (double)lq * q[s];
-          right[s] = (double)(totq[s] - lq) * q[s];
+          const int64_t o = __shfl_up(v[s], off, 64);
+          if (lane >= off) v[s] += o;
         }
-        double gain;
-        bool ok = true;
-        if (kind == 3) {
-          if (left[1] < mcw || right[1] < mcw) ok = false;
-          gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
-        } else {
-          double lc, rc;
-          const double li = impurity_dev(left, S, kind, &lc);
-          const double ri = impurity_dev(right, S, kind, &rc);
-          if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) ok = false;
-          gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
-          if (gain < min_gain) ok = false;
-        }
-        if (ok) {
-          Best c{gain, f, lane, dl};
-          if (better(c, best)) best = c;
+      }
+      if (lane < nb - 1) {
+        for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
+          double left[SM], right[SM];
+          for (int s = 0; s < S; ++s) {
+            const int64_t lq = v[s] + (dl ? miss[s] : 0);
+            left[s] = (double)lq * q[s];
+            right[s] = (double)(totq[s] - lq) * q[s];
+          }
+          double gain;
+          bool ok = true;
+          if (kind == 3) {
+            if (left[1] < mcw || right[1] < mcw) ok = false;
+            gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
+          } else {
+            double lc, rc;
+            const double li = impurity_dev(left, S, kind, &lc);
+            const double ri = impurity_dev(right, S, kind, &rc);
+            if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) ok = false;
+            gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
+            if (gain < min_gain) ok = false;
+          }
+          if (ok) {
+            Best c{gain, f, lane, dl};
+            if (better(c, best)) best = c;
+          }
         }
       }
     }
   }
-  // wave reduce
   for (int off = 32; off > 0; off >>= 1) {
     Best o;
     o.gain = __shfl_xor(best.gain, off, 64);
@@ -310,25 +323,53 @@ __global__ void __launch_bounds__(256) split_find_kernel(
     Best b = s_best[0];
     for (int w = 1; w < 4; ++w)
       if (better(s_best[w], b)) b = s_best[w];
-    const bool found = b.f != 0x7fffffff && b.gain > -INFINITY;
-    out_feat[j] = found ? fl[b.f] : -1;
+    cand[blockIdx.x] = b;
+  }
+}
+
+__global__ void __launch_bounds__(64) split_reduce_kernel(
+    const int64_t* __restrict__ hist, const int64_t* __restrict__ node_hist_off, const int32_t* __restrict__ node_feat_off,
+    const int32_t* __restrict__ feat_list, int B, int S, int missing_bin, const int32_t* __restrict__ node_model,
+    const double* __restrict__ qinv, int fbmax, const Best* __restrict__ cand, int32_t* __restrict__ out_feat,
+    int32_t* __restrict__ out_bin, float* __restrict__ out_gain, uint8_t* __restrict__ out_dl,
+    float* __restrict__ out_left, float* __restrict__ out_total) {
+  const int j = blockIdx.x;
+  const int lane = threadIdx.x;
+  Best b{-INFINITY, 0x7fffffff, 0, 0};
+  if (lane < fbmax) b = cand[(int64_t)j * fbmax + lane];
+  for (int off = 32; off > 0; off >>= 1) {
+    Best o;
+    o.gain = __shfl_xor(b.gain, off, 64);
+    o.f = __shfl_xor(b.f, off, 64);
+    o.b = __shfl_xor(b.b, off, 64);
+    o.dl = __shfl_xor(b.dl, off, 64);
+    if (better(o, b)) b = o;
+  }
+  const bool found = b.f != 0x7fffffff && b.gain > -INFINITY;
+  const int64_t* h = hist + node_hist_off[j];
+  const double* qi = qinv + (int64_t)(node_model ? node_model[j] : 0) * S;
+  if (lane == 0) {
+    out_feat[j] = found ? feat_list[node_feat_off[j] + b.f] : -1;
     out_bin[j] = found ? b.b : -1;
     out_gain[j] = found ? (float)b.gain : -INFINITY;
     out_dl[j] = (uint8_t)(found ? b.dl : 0);
-    s_best[0] = b;
   }
-  __syncthreads();
-  // left stats of the winner
-  const Best b = s_best[0];
-  if (threadIdx.x < S) {
-    const int s = threadIdx.x;
-    int64_t acc = 0;
-    if (b.f != 0x7fffffff) {
+  for (int s = 0; s < S; ++s) {
+    int64_t t = lane < B ? h[lane * S + s] : 0;
+    int64_t l = 0;
+    if (found) {
       const int64_t* hf = h + (int64_t)b.f * B * S;
-      for (int k = 0; k <= b.b; ++k) acc += hf[k * S + s];
-      if (b.dl) acc += hf[missing_bin * S + s];
+      l = lane <= b.b ? hf[lane * S + s] : 0;
+      if (b.dl && lane == 0) l += hf[missing_bin * S + s];
     }
-    out_left[(int64_t)j * S + s] = (float)((double)acc * qi[s]);
+    for (int off = 32; off > 0; off >>= 1) {
+      t += __shfl_xor(t, off, 64);
+      l += __shfl_xor(l, off, 64);
+    }
+    if (lane == 0) {
+      out_total[(int64_t)j * S + s] = (float)((double)t * qi[s]);
+      out_left[(int64_t)j * S + s] = (float)((double)l * qi[s]);
+    }
   }
 }
 
@@ -505,21 +546,38 @@ int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* 
 int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
-                        const double* qinv, int32_t* out_feat,
-                        int32_t* out_bin, float* out_gain, uint8_t* out_dl, float* out_left, float* out_total,
-                        hipStream_t stream) {
+                        const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
+                        float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, hipStream_t stream) {
   if (n_nodes == 0) return 0;
   if (S > TM_MAX_S || B > 64) return -2;
-#define TM_SPLIT(SMV)                                                                                         \
-  hipLaunchKernelGGL(split_find_kernel<SMV>, dim3(n_nodes), dim3(256), 0, stream, hist, node_hist_off, node_nfeat, \
-                     node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin, node_model, qinv,  \
-                     out_feat, out_bin, out_gain, out_dl, out_left, out_total)
+  const int fbmax = (max_nfeat + FPB - 1) / FPB;
+  if (fbmax > 64) return -2;
+  Best* cand = (Best*)cand_ws;   // >= n_nodes * fbmax entries
+#define TM_SPLIT(SMV)                                                                                          \
+  hipLaunchKernelGGL(split_scan_kernel<SMV>, dim3(n_nodes * fbmax), dim3(256), 0, stream, hist, node_hist_off,  \
+                     node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin,    \
+                     node_model, qinv, fbmax, cand)
   if (S <= 2) TM_SPLIT(2);
   else if (S == 3) TM_SPLIT(3);
   else if (S <= 4) TM_SPLIT(4);
   else TM_SPLIT(TM_MAX_S);
 #undef TM_SPLIT
+  hipLaunchKernelGGL(split_reduce_kernel, dim3(n_nodes), dim3(64), 0, stream, hist, node_hist_off, node_feat_off,
+                     feat_list, B, S, missing_bin, node_model, qinv, fbmax, cand, out_feat, out_bin, out_gain, out_dl,
+                     out_left, out_total);
   return (int)hipGetLastError();
+}
+
+int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
+                           hipStream_t stream) {
+  if (n == 0) return 0;
+  int gx = (int)min((max_size + 255) / 256, (int64_t)1024);
+  hipLaunchKernelGGL(zero_segments_kernel, dim3(gx, n), dim3(256), 0, stream, hist, off, size, n);
+  return (int)hipGetLastError();
+}
+
+size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat) {
+  return (size_t)n_nodes * ((max_nfeat + FPB - 1) / FPB) * sizeof(Best);
 }
 
 int tmog_hip_partition_count(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
