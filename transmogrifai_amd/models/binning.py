@@ -50,8 +50,9 @@ def sample_rows(n: int, max_bins: int, seed: int = 0, device="cpu") -> torch.Ten
     k = max(max_bins * max_bins, 10000)
     if n <= k:
         return torch.arange(n, device=device)
-    g = torch.Generator().manual_seed(seed)
-    return torch.randperm(n, generator=g)[:k].sort().values.to(device)
+    # O(k) sampling without replacement (a full randperm of n rows costs ~0.3 s at n = 10M)
+    idx = np.sort(np.random.default_rng(seed).choice(n, size=k, replace=False))
+    return torch.as_tensor(idx, dtype=torch.int64, device=device)
 
 
 def find_splits(X: torch.Tensor, max_bins: int = 32, seed: int = 0, missing_value: Optional[float] = None,

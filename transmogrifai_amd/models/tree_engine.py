@@ -147,6 +147,34 @@ def pack_rows(rows: torch.Tensor, weights: Optional[torch.Tensor]) -> torch.Tens
     return e.to(torch.int32)
 
 
+def _root_rows(jobs, dev):
+    """Packed root entries of every job, zero-weight (out-of-bag) rows dropped for all weighted jobs
+    with one compaction (two host syncs per call instead of one per tree)."""
+    packs: List[Optional[torch.Tensor]] = [None] * len(jobs)
+    counts = [0] * len(jobs)
+    wj = [k for k, j in enumerate(jobs) if j.weights is not None]
+    for k, j in enumerate(jobs):
+        if j.weights is None:
+            packs[k] = pack_rows(j.rows.to(dev), None)
+            counts[k] = int(j.rows.numel())
+    if wj:
+        sizes = [int(jobs[k].rows.numel()) for k in wj]
+        R = torch.cat([jobs[k].rows.to(dev).to(torch.int64) for k in wj])
+        W = torch.cat([jobs[k].weights.to(dev).to(torch.int64) for k in wj])
+        keep = W > 0
+        ends = torch.as_tensor(np.cumsum(sizes) - 1, device=dev)
+        csum = keep.to(torch.int64).cumsum(0)
+        kc = csum[ends].cpu().numpy()
+        kcount = np.diff(np.concatenate([[0], kc]))
+        idx = keep.nonzero().squeeze(1)
+        packed = pack_rows(R[idx], W[idx])
+        for k, part, c in zip(wj, torch.split(packed, kcount.tolist()), kcount):
+            packs[k] = part
+            counts[k] = int(c)
+    rows = torch.cat(packs) if packs else torch.zeros(0, dtype=torch.int32, device=dev)
+    return rows, counts
+
+
 class _Grow:
     """Growable host arrays for the created nodes."""
 
@@ -318,16 +346,7 @@ def _grow_group(Xb, n_bins_t, all_feats, jobs, mode, kind, S, K, B, missing_bin,
     G = _Grow(S)
 
     # ---- roots
-    packs, counts = [], []
-    for j in jobs:
-        r = j.rows.to(dev)
-        w = None if j.weights is None else j.weights.to(dev)
-        if w is not None:
-            keep = w > 0
-            r, w = r[keep], w[keep]
-        packs.append(pack_rows(r, w))
-        counts.append(int(r.numel()))
-    rows = torch.cat(packs) if packs else torch.zeros(0, dtype=torch.int32, device=dev)
+    rows, counts = _root_rows(jobs, dev)
     rows_alt = torch.empty_like(rows)
     lv_tree = np.arange(T, dtype=np.int64)
     lv_gid = G.add(lv_tree)

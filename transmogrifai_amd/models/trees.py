@@ -26,7 +26,7 @@ from . import tree_engine as TE
 from .base import FitJob, Learner, OpPredictor, probability_outputs, register_learner
 from .binning import BinSpec, find_splits, quantize
 from ..stages.base import register_stage
-from ..tuning.splitters import row_uniform
+from ..tuning.splitters import row_uniform, row_uniform_multi
 
 
 # --------------------------------------------------------------------------------------- context
@@ -91,6 +91,21 @@ def bootstrap_weights(rows: torch.Tensor, seed: int, rate: float) -> torch.Tenso
     """
     u = row_uniform(rows, seed, 23)
     k = torch.zeros(rows.shape[0], dtype=torch.int64, device=rows.device)
+    p = math.exp(-rate)
+    cdf = p
+    for i in range(1, 40):
+        k += (u >= cdf).to(torch.int64)
+        p = p * rate / i
+        cdf += p
+        if 1.0 - cdf < 1e-12:
+            break
+    return k
+
+
+def bootstrap_weights_multi(rows: torch.Tensor, seeds, rate: float) -> torch.Tensor:
+    """``bootstrap_weights`` for several trees at once: ``int64 [len(seeds), n]`` (bit-identical per tree)."""
+    u = row_uniform_multi(rows, seeds, 23)
+    k = torch.zeros(u.shape, dtype=torch.int64, device=rows.device)
     p = math.exp(-rate)
     cdf = p
     for i in range(1, 40):
@@ -178,9 +193,10 @@ class _ForestLearner(Learner):
                                    min_info_gain=float(p.get("min_info_gain", 0.0)), feature_subset=sub)
                 seed = int(p.get("seed", 0)) + 7919 * i
                 rate = float(p.get("subsampling_rate", 1.0))
+                wall = bootstrap_weights_multi(rows, [seed * 1009 + t for t in range(nt)], rate) if nt > 1 else None
                 for t in range(nt):
                     if nt > 1:
-                        w = bootstrap_weights(rows, seed * 1009 + t, rate)
+                        w = wall[t]
                     elif rate < 1.0:
                         w = (row_uniform(rows, seed * 1009 + t, 17) < rate).to(torch.int64)
                     else:

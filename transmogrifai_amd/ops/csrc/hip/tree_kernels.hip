@@ -183,6 +183,9 @@ __global__ void zero_segments_kernel(int64_t* __restrict__ hist, const int64_t* 
 }
 
 // ------------------------------------------------------------------------------- split finding
+// No FMA contraction from here on: gains are evaluated with exactly the CPU twin's IEEE operation
+// sequence, so near-tied candidates resolve identically on both paths (hipcc contracts by default).
+#pragma clang fp contract(off)
 __device__ __forceinline__ double impurity_dev(const double* st, int S, int kind, double* cnt) {
   if (kind == 0 || kind == 1) {
     double n = 0;

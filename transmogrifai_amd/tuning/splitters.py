@@ -39,6 +39,18 @@ def row_uniform(row_ids: torch.Tensor, seed: int, stream: int = 0) -> torch.Tens
     return (x >> 10).to(torch.float64) / float(1 << 53)
 
 
+def row_uniform_multi(row_ids: torch.Tensor, seeds, stream: int = 0) -> torch.Tensor:
+    """``row_uniform`` for several seeds at once: ``[len(seeds), n]`` (one fused pass, no per-seed launches)."""
+    off = torch.tensor([_s64(int(sd) * 0x632BE59BD9B4E019 + stream * 0x2545F4914F6CDD1D) for sd in seeds],
+                       dtype=torch.int64, device=row_ids.device)[:, None]
+    x = row_ids.to(torch.int64)[None, :] * _s64(0x1E3779B97F4A7C15) + off
+    x = x & _M63
+    x = ((x ^ (x >> 30)) * _s64(0x2F58476D1CE4E5B9)) & _M63
+    x = ((x ^ (x >> 27)) * _s64(0x14C3124B4B69A5C5)) & _M63
+    x = x ^ (x >> 31)
+    return (x >> 10).to(torch.float64) / float(1 << 53)
+
+
 class Splitter:
     reserve_test_fraction = 0.1
 
