@@ -143,3 +143,19 @@ def test_leaf_assign_matches_tree_walk_cpu():
 @pytest.mark.gpu
 def test_leaf_assign_matches_tree_walk_gpu():
     _leaf_vs_walk("cuda")
+
+
+@pytest.mark.gpu
+def test_hip_predict_many_classes_matches_host():
+    """K = 11 classes: the HIP walk accumulates 8 outputs per pass, wider K runs in class chunks."""
+    g = torch.Generator().manual_seed(5)
+    N, F, K = 3000, 8, 11
+    X = torch.randint(0, 32, (N, F), dtype=torch.uint8, generator=g)
+    y = (X[:, 0].long() * K // 32).float()
+    jobs = [te.TreeJob(0, te.TreeParams(max_depth=5), torch.arange(N)) for _ in range(5)]
+    f = te.grow_forest(X, np.full(F, 32), jobs, mode=te.MODE_CLS, kind=te.KIND_GINI, n_classes=K, y=y, B=32)
+    rows = [torch.arange(0, N, 2), None]
+    pc = te.forest_predict(f, X, rows, [[0, 1, 2], [3, 4]])
+    pg = te.forest_predict(f, X.cuda(), [None if r is None else r.cuda() for r in rows], [[0, 1, 2], [3, 4]])
+    for a, b in zip(pc, pg):
+        torch.testing.assert_close(a, b.cpu(), rtol=1e-6, atol=1e-6)

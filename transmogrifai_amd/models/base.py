@@ -56,6 +56,23 @@ class FitJob:
     weights: Optional[torch.Tensor] = None    # optional per-training-row weights
 
 
+def compact_rows(X: torch.Tensor, y: torch.Tensor, jobs: Sequence[FitJob]):
+    """Restrict a batch of jobs to the union of their training rows.
+
+    Cross-validation folds of a down-sampled training set touch only part of ``X``; learners that
+    stream ``X`` every iteration (linear models: one pass per objective evaluation) then read the
+    union once instead of all ``N`` rows per pass. Returns ``(X_u, y_u, jobs_u)`` with row ids
+    remapped, or the inputs unchanged when a job uses every row or the union is all of ``X``."""
+    if not jobs or any(j.rows is None for j in jobs):
+        return X, y, list(jobs)
+    U, inv = torch.unique(torch.cat([j.rows.to(X.device) for j in jobs]), return_inverse=True)
+    if U.numel() >= X.shape[0]:
+        return X, y, list(jobs)
+    parts = torch.split(inv, [int(j.rows.numel()) for j in jobs])
+    return X.index_select(0, U), y.to(X.device).index_select(0, U), \
+        [FitJob(j.params, r, j.weights) for j, r in zip(jobs, parts)]
+
+
 class Learner:
     name = "Learner"
     problem = "binary"          # binary | multiclass | regression

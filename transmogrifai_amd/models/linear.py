@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from ..ops import linear as LK
-from .base import FitJob, Learner, OpPredictor, probability_outputs, register_learner
+from .base import FitJob, Learner, OpPredictor, compact_rows, probability_outputs, register_learner
 from ..stages.base import register_stage
 
 
@@ -326,6 +326,7 @@ class LogisticRegressionLearner(_LinearBase):
                  "n_classes": K} for p in range(P)]
 
     def fit_batch(self, X, y, jobs, context=None):
+        X, y, jobs = compact_rows(X, y, jobs)
         dev = X.device
         N, d = X.shape
         P = len(jobs)
@@ -418,6 +419,7 @@ class LinearRegressionLearner(_LinearBase):
     loss = "squared"
 
     def fit_batch(self, X, y, jobs, context=None):
+        X, y, jobs = compact_rows(X, y, jobs)
         dev = X.device
         N, d = X.shape
         P = len(jobs)

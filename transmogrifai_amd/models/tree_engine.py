@@ -719,8 +719,13 @@ def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev):
         if t is None:
             return torch.zeros(n_models, dtype=torch.float32, device=dev)
         v = t.reshape(t.shape[0], -1) if t.dim() == 2 else t.reshape(1, -1)
-        if v.shape[1] >= 1 << 16 and v.shape[1] % 256 == 0:   # row-wise amax of a few long rows: split them
-            m = v.abs().view(v.shape[0], 256, -1).amax(2).amax(1)
+        L = v.shape[1]
+        if L >= 1 << 16:        # row-wise amax of a few long rows: split each row into 256 segments
+            seg = -(-L // 256)
+            a = v.abs()
+            if seg * 256 != L:
+                a = torch.nn.functional.pad(a, (0, seg * 256 - L))
+            m = a.view(v.shape[0], 256, seg).amax(2).amax(1)
         else:
             m = v.abs().amax(1)
         return m.expand(n_models) if m.numel() == 1 else m[:n_models]
@@ -921,10 +926,17 @@ def forest_predict(forest: Forest, Xb: torch.Tensor, model_rows: Sequence[Option
     mro_t = torch.as_tensor(mro, device=dev)
     mto_t = torch.as_tensor(mto, device=dev)
     if dev.type == "cuda":
-        N.check(N.hip().tmog_hip_forest_predict(
-            N.ptr(Xb), F, len(model_rows), N.ptr(mro_t), N.ptr(row_list), max(counts) if counts else 0,
-            N.ptr(mto_t), N.ptr(t_off), N.ptr(t_w), N.ptr(nodes), N.ptr(dl), forest.missing_bin, N.ptr(lv), K,
-            N.ptr(out), N.stream(dev)), "forest_predict")
+        # the kernel accumulates up to 8 outputs per row in registers: wider K runs in class chunks
+        for c0 in range(0, K, 8):
+            kc = min(8, K - c0)
+            lvc = lv if kc == K else lv[:, c0:c0 + kc].contiguous()
+            oc = out if kc == K else torch.empty(int(mro[-1]), kc, dtype=torch.float32, device=dev)
+            N.check(N.hip().tmog_hip_forest_predict(
+                N.ptr(Xb), F, len(model_rows), N.ptr(mro_t), N.ptr(row_list), max(counts) if counts else 0,
+                N.ptr(mto_t), N.ptr(t_off), N.ptr(t_w), N.ptr(nodes), N.ptr(dl), forest.missing_bin, N.ptr(lvc), kc,
+                N.ptr(oc), N.stream(dev)), "forest_predict")
+            if kc != K:
+                out[:, c0:c0 + kc] = oc
     else:
         N.check(N.host().tmog_forest_predict_cpu(
             N.ptr(Xb), F, len(model_rows), N.ptr(mro_t), N.ptr(row_list), N.ptr(mto_t), N.ptr(t_off), N.ptr(t_w),

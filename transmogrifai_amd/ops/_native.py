@@ -35,6 +35,14 @@ _HOST_SIGS = {
     "tmog_murmur3_batch": [P, P, I64, I32, P],
     "tmog_hash_index_batch": [P, P, I64, I32, I32, P],
     "tmog_col_stats_cpu": [P, P, I64, I32, I64, P],
+    "tmog_shist_new": [I32, I32, I64],
+    "tmog_shist_free": [P],
+    "tmog_shist_update": [P, P, P, I64],
+    "tmog_shist_flush": [P],
+    "tmog_shist_merge": [P, P],
+    "tmog_shist_size": [P],
+    "tmog_shist_bins": [P, P, P],
+    "tmog_shist_sum": [P, C.c_double],
     "tmog_tokenize_batch": [P, P, I64, I32, I32, P, P, P, I64],
 }
 
@@ -60,13 +68,19 @@ _HIP_SIGS = {
 }
 
 
+_RESTYPES = {"tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
+             "tmog_shist_flush": None, "tmog_shist_merge": None, "tmog_shist_bins": None,
+             "tmog_shist_size": C.c_int64, "tmog_shist_sum": C.c_double,
+             "tmog_hip_split_cand_bytes": C.c_size_t}
+
+
 def _declare(lib, sigs):
     for name, args in sigs.items():
         fn = getattr(lib, name, None)
         if fn is None:
             continue
         fn.argtypes = args
-        fn.restype = C.c_int
+        fn.restype = _RESTYPES.get(name, C.c_int)
 
 
 def host():

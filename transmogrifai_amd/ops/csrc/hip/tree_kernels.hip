@@ -493,7 +493,38 @@ __global__ void __launch_bounds__(256) forest_predict_kernel(
   const int64_t row = row_list ? row_list[i] : (i - r0);
   const uint8_t* xr = Xb + row * F;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int64_t t = model_tree_off[m]; t < model_tree_off[m + 1]; ++t) {
+  const int64_t t_end = model_tree_off[m + 1];
+  int64_t t = model_tree_off[m];
+  // four trees walked together: four independent node-fetch -> bin-fetch chains in flight per lane
+  for (; t + 4 <= t_end; t += 4) {
+    int64_t k[4];
+    int4 nd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      k[u] = tree_off[t + u];
+      nd[u] = nodes[k[u]];
+    }
+    bool active = true;
+    while (active) {
+      active = false;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (nd[u].z >= 0) {
+          const uint8_t b = xr[nd[u].x];
+          const bool gl = (missing_bin >= 0 && b == missing_bin) ? (default_left[k[u]] != 0) : ((int)b <= nd[u].y);
+          k[u] = gl ? nd[u].z : nd[u].w;
+          nd[u] = nodes[k[u]];
+          active = true;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float w = tree_weight[t + u];
+      for (int c = 0; c < K && c < 8; ++c) acc[c] += w * leaf_value[k[u] * K + c];
+    }
+  }
+  for (; t < t_end; ++t) {
     int64_t k = tree_off[t];
     int4 nd = nodes[k];  // (feat, bin, left, right)
     while (nd.z >= 0) {
