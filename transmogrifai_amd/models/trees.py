@@ -136,8 +136,10 @@ def _add_tree_margins(Fm: torch.Tensor, forest: "TE.Forest", Xb, act: List[int],
         return
     N = Fm.shape[1]
     t = la.entry_tree()
-    p_of = torch.as_tensor(act, dtype=torch.int64, device=Fm.device)
-    w_of = torch.as_tensor(wgts, dtype=torch.float64, device=Fm.device)
+    pk = TE._Pack(Fm.device)
+    i_p, i_w = pk.add(np.asarray(act, np.int64)), pk.add(np.asarray(wgts, np.float64))
+    dv = pk.ship()
+    p_of, w_of = dv[i_p], dv[i_w]
     idx = p_of[t] * N + la.row_ids()
     val = la.entry_value()[:, 0].to(torch.float64) * w_of[t]
     flat = Fm.view(-1)

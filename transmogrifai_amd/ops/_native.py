@@ -35,6 +35,12 @@ _HOST_SIGS = {
     "tmog_murmur3_batch": [P, P, I64, I32, P],
     "tmog_hash_index_batch": [P, P, I64, I32, I32, P],
     "tmog_col_stats_cpu": [P, P, I64, I32, I64, P],
+    "tmog_grow_forest_cpu": [P],
+    "tmog_grow_status_cpu": [P, P, I32],
+    "tmog_grow_nodes_cpu": [P, I32],
+    "tmog_grow_leaf_count_cpu": [P, I32],
+    "tmog_grow_copy_cpu": [P, I32, P, P, P, P, P, P, P, P],
+    "tmog_grow_free_cpu": [P],
     "tmog_shist_new": [I32, I32, I64],
     "tmog_shist_free": [P],
     "tmog_shist_update": [P, P, P, I64],
@@ -53,6 +59,12 @@ _HIP_SIGS = {
     "tmog_hip_partition_count": [P, I32, P, P, I32, P, P, P, I32, P, P],
     "tmog_hip_partition_scatter": [P, I32, P, P, P, I32, P, P, P, I32, P],
     "tmog_hip_leaf_collect": [P, P, I32, P, P, P],
+    "tmog_hip_grow_forest": [P],
+    "tmog_hip_grow_status": [P, P, I32],
+    "tmog_hip_grow_nodes": [P, I32],
+    "tmog_hip_grow_leaf_count": [P, I32],
+    "tmog_hip_grow_copy": [P, I32, P, P, P, P, P, P, P, P],
+    "tmog_hip_grow_free": [P],
     "tmog_hip_zero_segments": [P, P, P, I32, I64, P],
     "tmog_hip_lr_objective": [P, I64, I32, P, P, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P],
     "tmog_hip_forest_predict": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P],
@@ -71,7 +83,12 @@ _HIP_SIGS = {
 _RESTYPES = {"tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
              "tmog_shist_flush": None, "tmog_shist_merge": None, "tmog_shist_bins": None,
              "tmog_shist_size": C.c_int64, "tmog_shist_sum": C.c_double,
-             "tmog_hip_split_cand_bytes": C.c_size_t}
+             "tmog_hip_split_cand_bytes": C.c_size_t,
+             "tmog_grow_forest_cpu": C.c_void_p, "tmog_hip_grow_forest": C.c_void_p,
+             "tmog_grow_nodes_cpu": C.c_int64, "tmog_hip_grow_nodes": C.c_int64,
+             "tmog_grow_leaf_count_cpu": C.c_int64, "tmog_hip_grow_leaf_count": C.c_int64,
+             "tmog_grow_copy_cpu": None, "tmog_hip_grow_copy": None,
+             "tmog_grow_free_cpu": None, "tmog_hip_grow_free": None}
 
 
 def _declare(lib, sigs):

@@ -1,0 +1,500 @@
+// Native level-synchronous tree grower (host orchestration), shared by the HIP and CPU backends.
+//
+// This is the runtime half of the histogram tree engine (replaces Spark MLlib's
+// per-level RandomForest.findBestSplits driver loop and XGBoost4J's hist updater, e.g.
+// OpRandomForestClassifier.scala:59-154, OpGBTClassifier.scala:47-142, OpXGBoostClassifier.scala:47-403).
+// One call grows one tree per job, all jobs of a group level by level. Per level the grower plans the
+// work items on the host, ships every host array in ONE staged copy, launches the level's kernels
+// (histogram, subtraction trick, split scan, partition count), reads every decision back with ONE
+// device->host copy, then launches the stable partition and the leaf collection. Job groups run on
+// their own host threads and HIP streams, so one group's planning overlaps the other's kernels.
+//
+// Backends (template parameter BK) provide memory, staging and the kernels:
+//   GPU  (hip/tree_grow_hip.hip)   : pinned staging + hipMemcpyAsync, tmog_hip_* launchers
+//   CPU  (host/tree_grow_cpu.cpp)  : host memory, tmog_*_cpu functions (bit-identical results)
+// Layout contracts are those of hip/tree_kernels.hip (packed rows, int64 fixed-point histograms).
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace tmog {
+
+struct GrowArgs {
+  const uint8_t* Xb;
+  int64_t N;
+  int32_t F, mode, kind, S, B, missing_bin;
+  int64_t chunk_rows;
+  int32_t subtract, collect_leaves;
+  const float* y;
+  const float* t1;
+  const float* t2;
+  int64_t stride;
+  const float* qscale;
+  const double* qinv;
+  const int32_t* n_bins;
+  int32_t T;
+  const int32_t* job_model;
+  const int32_t* job_depth;
+  const double* job_min_inst;
+  const double* job_min_gain;
+  const double* job_mcw;
+  const double* job_lambda;
+  const double* job_eps;
+  const int32_t* job_fsub;
+  const int64_t* job_count;   // root entries per job (job-major in rows)
+  uint32_t* rows;             // packed root entries (device / host), overwritten
+  uint32_t* rows_alt;         // scratch of the same size
+  uint32_t* leaf_rows;        // collect_leaves: final leaf of every entry (same size as rows)
+  int32_t* leaf_gid;
+  int32_t n_groups;
+  const int32_t* group_start;  // [n_groups + 1] job boundaries
+  int64_t rng_seed;
+  void* stream;               // GPU: caller's stream (groups wait on it; it waits on the groups)
+};
+
+struct GroupResult {
+  std::vector<int64_t> tree, feat, bin, left, right;
+  std::vector<uint8_t> dl;
+  std::vector<double> gain, tot;   // tot: n * S
+  int64_t leaf_count = 0;
+  int S = 1;
+
+  std::vector<int64_t> add(const std::vector<int64_t>& trees) {
+    std::vector<int64_t> ids(trees.size());
+    for (size_t i = 0; i < trees.size(); ++i) {
+      ids[i] = (int64_t)tree.size();
+      tree.push_back(trees[i]);
+      feat.push_back(-1);
+      bin.push_back(-1);
+      left.push_back(-1);
+      right.push_back(-1);
+      dl.push_back(0);
+      gain.push_back(0.0);
+      for (int s = 0; s < S; ++s) tot.push_back(0.0);
+    }
+    return ids;
+  }
+};
+
+struct GrowResult {
+  std::vector<GroupResult> groups;
+  int status = 0;
+  std::string error;
+};
+
+// item layouts shared with hip/tree_kernels.hip
+struct HistItemH {
+  int32_t node, fg0, nf, excl;
+  int64_t begin, count;
+};
+struct PartItemH {
+  int32_t node, pad;
+  int64_t begin, count, out_left, out_right;
+};
+struct LeafItemH {
+  int64_t begin, count, out;
+  int32_t gid, pad;
+};
+static_assert(sizeof(HistItemH) == 32 && sizeof(PartItemH) == 40 && sizeof(LeafItemH) == 32, "item layout");
+
+// splitmix64 stream for the per-node feature subsets (identical on both backends)
+struct SplitMix {
+  uint64_t s;
+  explicit SplitMix(uint64_t seed) : s(seed) {}
+  uint64_t next() {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  uint64_t below(uint64_t n) { return next() % n; }
+};
+
+// Host staging: arrays appended at 16-byte aligned offsets, shipped as one block by the backend.
+struct Staging {
+  std::vector<uint8_t> buf;
+  size_t add(const void* p, size_t bytes) {
+    const size_t off = (buf.size() + 15) & ~size_t(15);
+    buf.resize(off + ((bytes + 15) & ~size_t(15)));
+    if (bytes) std::memcpy(buf.data() + off, p, bytes);
+    return off;
+  }
+  template <class T>
+  size_t add(const std::vector<T>& v) { return add(v.data(), v.size() * sizeof(T)); }
+  void clear() { buf.clear(); }
+};
+
+template <class BK>
+void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
+  const int j0 = a.group_start[g], j1 = a.group_start[g + 1];
+  const int T = j1 - j0;
+  const int F = a.F, S = a.S, B = a.B;
+  R.S = S;
+  if (T <= 0) return;
+  int64_t entry0 = 0;
+  for (int j = 0; j < j0; ++j) entry0 += a.job_count[j];
+  int64_t total = 0;
+  for (int j = j0; j < j1; ++j) total += a.job_count[j];
+  uint32_t* rows = a.rows + entry0;
+  uint32_t* rows_alt = a.rows_alt + entry0;
+  uint32_t* leaf_rows = a.collect_leaves ? a.leaf_rows + entry0 : nullptr;
+  int32_t* leaf_gid = a.collect_leaves ? a.leaf_gid + entry0 : nullptr;
+  int64_t leaf_pos = 0;
+
+  std::vector<int32_t> fsub(T);
+  bool use_subset = false;
+  int max_depth = 0;
+  for (int t = 0; t < T; ++t) {
+    const int k = a.job_fsub[j0 + t];
+    fsub[t] = (k <= 0 || k >= F) ? F : k;
+    use_subset |= fsub[t] < F;
+    max_depth = std::max(max_depth, a.job_depth[j0 + t]);
+  }
+  SplitMix rng((uint64_t)a.rng_seed + 1000003ull * (uint64_t)g);
+
+  std::vector<int64_t> lv_tree(T), lv_begin(T), lv_count(T);
+  for (int t = 0; t < T; ++t) {
+    lv_tree[t] = t;
+    lv_count[t] = a.job_count[j0 + t];
+    lv_begin[t] = t ? lv_begin[t - 1] + lv_count[t - 1] : 0;
+  }
+  std::vector<int64_t> lv_gid = R.add(lv_tree);
+
+  const int32_t* all_feats = bk.all_features(F);
+  int64_t* hist = nullptr;
+  int64_t* prev_hist = nullptr;
+  int cur_slot = 0;          // the backend keeps two grow-only histogram buffers per group
+  std::vector<int64_t> pair_parent_off;
+  Staging st1, st2, st3;   // level arrays (slot 0), scatter items (slot 1), leaf items (slot 2)
+
+  auto collect = [&](const std::vector<int64_t>& idx) {
+    if (!a.collect_leaves) return;
+    std::vector<LeafItemH> items;
+    for (int64_t i : idx) {
+      const int64_t c = lv_count[i];
+      if (c <= 0) continue;
+      for (int64_t o = 0; o < c; o += a.chunk_rows) {
+        LeafItemH it;
+        it.begin = lv_begin[i] + o;
+        it.count = std::min(a.chunk_rows, c - o);
+        it.out = leaf_pos + o;
+        it.gid = (int32_t)lv_gid[i];
+        it.pad = 0;
+        items.push_back(it);
+      }
+      leaf_pos += c;
+    }
+    if (items.empty()) return;
+    st3.clear();
+    const size_t o = st3.add(items);
+    const uint8_t* d = bk.ship(st3, 2);
+    bk.leaf_collect(rows, d + o, (int)items.size(), leaf_rows, leaf_gid);
+  };
+
+  for (int depth = 0; depth <= max_depth; ++depth) {
+    const int64_t n = (int64_t)lv_gid.size();
+    if (n == 0) break;
+    std::vector<uint8_t> can(n), need(n);
+    std::vector<int64_t> hist_nodes;
+    for (int64_t i = 0; i < n; ++i) {
+      const int t = (int)lv_tree[i];
+      can[i] = depth < a.job_depth[j0 + t] && lv_count[i] >= 2 &&
+               (double)lv_count[i] >= 2 * a.job_min_inst[j0 + t] - 1e-9;
+      need[i] = can[i] || depth == 0;
+      if (need[i]) hist_nodes.push_back(i);
+    }
+    if (hist_nodes.empty()) {
+      std::vector<int64_t> all(n);
+      for (int64_t i = 0; i < n; ++i) all[i] = i;
+      collect(all);
+      break;
+    }
+    const int m = (int)hist_nodes.size();
+    // ---- per-node feature lists
+    std::vector<int32_t> feat_list, feat_off(m), nfeat(m);
+    if (use_subset) {
+      std::vector<int32_t> perm(F);
+      for (int j = 0; j < m; ++j) {
+        const int k = fsub[lv_tree[hist_nodes[j]]];
+        for (int f = 0; f < F; ++f) perm[f] = f;
+        for (int i = 0; i < k; ++i) std::swap(perm[i], perm[i + (int)rng.below((uint64_t)(F - i))]);
+        std::sort(perm.begin(), perm.begin() + k);
+        feat_off[j] = (int32_t)feat_list.size();
+        nfeat[j] = k;
+        feat_list.insert(feat_list.end(), perm.begin(), perm.begin() + k);
+      }
+    } else {
+      for (int j = 0; j < m; ++j) {
+        feat_off[j] = 0;
+        nfeat[j] = F;
+      }
+    }
+    std::vector<int64_t> hsz(m), hoff(m);
+    int64_t hwords = 0;
+    int max_nf = 0;
+    for (int j = 0; j < m; ++j) {
+      hsz[j] = (int64_t)nfeat[j] * B * S;
+      hoff[j] = hwords;
+      hwords += hsz[j];
+      max_nf = std::max(max_nf, (int)nfeat[j]);
+    }
+    hist = bk.hist_buffer(cur_slot, (size_t)hwords);
+    std::vector<int64_t> loc(n, -1);
+    for (int j = 0; j < m; ++j) loc[hist_nodes[j]] = j;
+    // ---- subtraction trick: children come in (left, right) pairs
+    std::vector<int64_t> d_big, d_small, d_poff;
+    if (a.subtract && !use_subset && prev_hist && depth > 0) {
+      for (int64_t q = 0; 2 * q + 1 < n; ++q) {
+        const int64_t li = 2 * q, ri = 2 * q + 1;
+        if (!(need[li] && need[ri])) continue;
+        const bool left_big = lv_count[li] >= lv_count[ri];
+        d_big.push_back(loc[left_big ? li : ri]);
+        d_small.push_back(loc[left_big ? ri : li]);
+        d_poff.push_back(pair_parent_off[q]);
+      }
+    }
+    std::vector<uint8_t> build(m, 1);
+    for (int64_t b : d_big) build[b] = 0;
+    std::vector<int64_t> nb(m), nc(m);
+    std::vector<int32_t> nmd(m);
+    std::vector<float> params((size_t)m * 8, 0.f);
+    for (int j = 0; j < m; ++j) {
+      const int64_t i = hist_nodes[j];
+      const int t = (int)lv_tree[i];
+      nb[j] = lv_begin[i];
+      nc[j] = lv_count[i];
+      nmd[j] = a.job_model[j0 + t];
+      float* P = &params[(size_t)j * 8];
+      P[0] = (float)a.job_min_inst[j0 + t];
+      P[1] = (float)a.job_min_gain[j0 + t];
+      P[2] = (float)a.job_mcw[j0 + t];
+      P[3] = (float)a.job_lambda[j0 + t];
+      P[5] = a.missing_bin >= 0 ? 1.f : 0.f;
+      P[6] = (float)a.job_eps[j0 + t];
+      P[7] = can[i] ? 1.f : 0.f;
+    }
+    // ---- work items (GPU) / built-node arrays (CPU)
+    std::vector<HistItemH> hitems;
+    std::vector<PartItemH> citems;
+    std::vector<int64_t> z_off, z_size;
+    std::vector<int64_t> b_nb, b_nc, b_nho;
+    std::vector<int32_t> b_nfo, b_nnf, b_nmd;
+    for (int j = 0; j < m; ++j) {
+      const int64_t cnt = nc[j];
+      const int64_t nch = std::max<int64_t>(1, (cnt + a.chunk_rows - 1) / a.chunk_rows);
+      for (int64_t c = 0; c < nch; ++c) {
+        PartItemH p;
+        p.node = j;
+        p.pad = 0;
+        p.begin = nb[j] + c * a.chunk_rows;
+        p.count = std::min(a.chunk_rows, cnt - c * a.chunk_rows);
+        p.out_left = p.out_right = 0;
+        citems.push_back(p);
+      }
+      if (!build[j]) continue;
+      b_nb.push_back(nb[j]);
+      b_nc.push_back(nc[j]);
+      b_nho.push_back(hoff[j]);
+      b_nfo.push_back(feat_off[j]);
+      b_nnf.push_back(nfeat[j]);
+      b_nmd.push_back(nmd[j]);
+      const int nf = nfeat[j];
+      const int ng = std::max(1, (nf + 63) / 64);
+      const int fg = (nf + ng - 1) / ng;
+      if (nch > 1) {
+        z_off.push_back(hoff[j]);
+        z_size.push_back(hsz[j]);
+      }
+      for (int64_t c = 0; c < nch; ++c)
+        for (int gi = 0; gi < ng; ++gi) {
+          HistItemH h;
+          h.node = j;
+          h.fg0 = gi * fg;
+          h.nf = std::min(fg, nf - gi * fg);
+          h.excl = nch == 1 ? 1 : 0;
+          h.begin = nb[j] + c * a.chunk_rows;
+          h.count = std::min(a.chunk_rows, cnt - c * a.chunk_rows);
+          hitems.push_back(h);
+        }
+    }
+    std::vector<int64_t> d_soff, d_ooff, d_size;
+    int64_t d_max = 0;
+    for (size_t q = 0; q < d_big.size(); ++q) {
+      d_soff.push_back(hoff[d_small[q]]);
+      d_ooff.push_back(hoff[d_big[q]]);
+      d_size.push_back(hsz[d_big[q]]);
+      d_max = std::max(d_max, hsz[d_big[q]]);
+    }
+    int64_t z_max = 0;
+    for (int64_t z : z_size) z_max = std::max(z_max, z);
+    // ---- ship everything in one copy
+    st1.clear();
+    const size_t o_nfo = st1.add(feat_off), o_nnf = st1.add(nfeat), o_nmd = st1.add(nmd), o_nho = st1.add(hoff);
+    const size_t o_par = st1.add(params);
+    const size_t o_fl = use_subset ? st1.add(feat_list) : 0;
+    const size_t o_hit = st1.add(hitems), o_cit = st1.add(citems);
+    const size_t o_zo = st1.add(z_off), o_zs = st1.add(z_size);
+    const size_t o_dp = st1.add(d_poff), o_ds = st1.add(d_soff), o_do = st1.add(d_ooff), o_dz = st1.add(d_size);
+    const size_t o_bnb = st1.add(b_nb), o_bnc = st1.add(b_nc), o_bnfo = st1.add(b_nfo), o_bnnf = st1.add(b_nnf);
+    const size_t o_bnmd = st1.add(b_nmd), o_bnho = st1.add(b_nho);
+    const uint8_t* d1 = bk.ship(st1, 0);
+#define TM_P(T_, off) ((T_*)(d1 + (off)))
+    const int32_t* flist = use_subset ? TM_P(const int32_t, o_fl) : all_feats;
+    // ---- histograms
+    bk.zero_segments(hist, TM_P(const int64_t, o_zo), TM_P(const int64_t, o_zs), (int)z_off.size(), z_max);
+    bk.hist_build(a, rows, hitems.size() ? (const void*)(d1 + o_hit) : nullptr, (int)hitems.size(),
+                  TM_P(const int32_t, o_nfo), flist, TM_P(const int32_t, o_nmd), TM_P(const int64_t, o_nho), hist,
+                  (int)b_nb.size(), TM_P(const int64_t, o_bnb), TM_P(const int64_t, o_bnc),
+                  TM_P(const int32_t, o_bnfo), TM_P(const int32_t, o_bnnf), TM_P(const int32_t, o_bnmd),
+                  TM_P(const int64_t, o_bnho));
+    if (!d_big.empty())
+      bk.hist_subtract(hist, prev_hist, TM_P(const int64_t, o_dp), TM_P(const int64_t, o_ds),
+                       TM_P(const int64_t, o_do), TM_P(const int64_t, o_dz), (int)d_big.size(), d_max);
+    // ---- split scan + partition count -> one result block
+    const int64_t ncit = (int64_t)citems.size();
+    const size_t r_cl = 0, r_feat = r_cl + 8 * ncit, r_bin = r_feat + 4 * (size_t)m, r_gain = r_bin + 4 * (size_t)m;
+    const size_t r_left = r_gain + 4 * (size_t)m, r_tot = r_left + 4 * (size_t)m * S, r_dl = r_tot + 4 * (size_t)m * S;
+    const size_t r_bytes = r_dl + (size_t)m;
+    uint8_t* res = bk.result_buffer(r_bytes);
+    bk.split_find(a, hist, m, TM_P(const int64_t, o_nho), TM_P(const int32_t, o_nnf), TM_P(const int32_t, o_nfo),
+                  flist, TM_P(const float, o_par), TM_P(const int32_t, o_nmd), max_nf, (int32_t*)(res + r_feat),
+                  (int32_t*)(res + r_bin), (float*)(res + r_gain), res + r_dl, (float*)(res + r_left),
+                  (float*)(res + r_tot));
+    bk.partition_count(a, rows, d1 + o_cit, (int)ncit, (const int32_t*)(res + r_feat),
+                       (const int32_t*)(res + r_bin), res + r_dl, (int64_t*)(res + r_cl));
+    const uint8_t* h = bk.fetch(res, r_bytes);
+    const int64_t* h_cl = (const int64_t*)(h + r_cl);
+    const int32_t* h_feat = (const int32_t*)(h + r_feat);
+    const int32_t* h_bin = (const int32_t*)(h + r_bin);
+    const float* h_gain = (const float*)(h + r_gain);
+    const float* h_left = (const float*)(h + r_left);
+    const float* h_tot = (const float*)(h + r_tot);
+    const uint8_t* h_dl = h + r_dl;
+    // ---- decisions
+    std::vector<int64_t> sl;
+    for (int j = 0; j < m; ++j) {
+      const int64_t gid = lv_gid[hist_nodes[j]];
+      for (int s = 0; s < S; ++s) R.tot[(size_t)gid * S + s] = (double)h_tot[(size_t)j * S + s];
+      const bool ok = params[(size_t)j * 8 + 7] > 0.5f && h_feat[j] >= 0 && h_gain[j] > params[(size_t)j * 8 + 6];
+      if (ok) sl.push_back(j);
+    }
+    {
+      std::vector<uint8_t> splits(n, 0);
+      for (int64_t j : sl) splits[hist_nodes[j]] = 1;
+      std::vector<int64_t> lf;
+      for (int64_t i = 0; i < n; ++i)
+        if (!splits[i]) lf.push_back(i);
+      collect(lf);
+    }
+    if (sl.empty()) break;
+    const int64_t ns = (int64_t)sl.size();
+    std::vector<int64_t> counts_sl(ns), out_begin(ns), nl(ns, 0);
+    for (int64_t q = 0; q < ns; ++q) {
+      const int64_t j = sl[q], gid = lv_gid[hist_nodes[j]];
+      R.feat[gid] = h_feat[j];
+      R.bin[gid] = h_bin[j];
+      R.dl[gid] = h_dl[j];
+      R.gain[gid] = (double)h_gain[j];
+      counts_sl[q] = nc[j];
+      out_begin[q] = q ? out_begin[q - 1] + counts_sl[q - 1] : 0;
+    }
+    // ---- stable partition of the splitting nodes' entries
+    if (BK::kGPU) {
+      std::vector<int64_t> pos(m, -1);
+      for (int64_t q = 0; q < ns; ++q) pos[sl[q]] = q;
+      std::vector<PartItemH> sitems;
+      std::vector<int64_t> run_l(ns, 0), run_r(ns, 0);
+      for (int64_t c = 0; c < ncit; ++c) {
+        const int64_t q = pos[citems[c].node];
+        if (q >= 0) nl[q] += h_cl[c];
+      }
+      for (int64_t c = 0; c < ncit; ++c) {
+        const int64_t q = pos[citems[c].node];
+        if (q < 0) continue;
+        PartItemH it = citems[c];
+        const int64_t cl = h_cl[c], cr = it.count - cl;
+        it.out_left = out_begin[q] + run_l[q];
+        it.out_right = out_begin[q] + nl[q] + run_r[q];
+        run_l[q] += cl;
+        run_r[q] += cr;
+        sitems.push_back(it);
+      }
+      st2.clear();
+      const size_t o_s = st2.add(sitems);
+      const uint8_t* d2 = bk.ship(st2, 1);
+      bk.partition_scatter(a, rows, rows_alt, d2 + o_s, (int)sitems.size(), (const int32_t*)(res + r_feat),
+                           (const int32_t*)(res + r_bin), res + r_dl);
+    } else {
+      std::vector<int64_t> s_nb(ns), s_nc(ns);
+      std::vector<int32_t> s_f(ns), s_b(ns);
+      std::vector<uint8_t> s_d(ns);
+      for (int64_t q = 0; q < ns; ++q) {
+        const int64_t j = sl[q];
+        s_nb[q] = nb[j];
+        s_nc[q] = nc[j];
+        s_f[q] = h_feat[j];
+        s_b[q] = h_bin[j];
+        s_d[q] = h_dl[j];
+      }
+      bk.partition_nodes(a, rows, rows_alt, (int)ns, s_nb.data(), s_nc.data(), s_f.data(), s_b.data(), s_d.data(),
+                         out_begin.data(), nl.data());
+    }
+    // ---- next level: (left, right) children pairs
+    std::vector<int64_t> ch_tree(2 * ns);
+    for (int64_t q = 0; q < ns; ++q) ch_tree[2 * q] = ch_tree[2 * q + 1] = lv_tree[hist_nodes[sl[q]]];
+    std::vector<int64_t> ch = R.add(ch_tree);
+    std::vector<int64_t> new_begin(2 * ns), new_count(2 * ns);
+    pair_parent_off.assign(ns, 0);
+    for (int64_t q = 0; q < ns; ++q) {
+      const int64_t j = sl[q], gid = lv_gid[hist_nodes[j]];
+      const int64_t gl = ch[2 * q], gr = ch[2 * q + 1];
+      R.left[gid] = gl;
+      R.right[gid] = gr;
+      for (int s = 0; s < S; ++s) {
+        const double lt = (double)h_left[(size_t)j * S + s];
+        const double tt = (double)h_tot[(size_t)j * S + s];
+        R.tot[(size_t)gl * S + s] = lt;
+        R.tot[(size_t)gr * S + s] = tt - lt;
+      }
+      new_begin[2 * q] = out_begin[q];
+      new_begin[2 * q + 1] = out_begin[q] + nl[q];
+      new_count[2 * q] = nl[q];
+      new_count[2 * q + 1] = counts_sl[q] - nl[q];
+      pair_parent_off[q] = hoff[j];
+    }
+#undef TM_P
+    std::swap(hist, prev_hist);
+    cur_slot ^= 1;
+    std::swap(rows, rows_alt);
+    lv_tree = ch_tree;
+    lv_gid = ch;
+    lv_begin = new_begin;
+    lv_count = new_count;
+  }
+  bk.finish();
+  R.leaf_count = leaf_pos;
+}
+
+// Result accessors shared by both C ABIs.
+inline int64_t result_nodes(const GrowResult* r, int g) { return (int64_t)r->groups[g].tree.size(); }
+
+inline void result_copy(const GrowResult* r, int g, int64_t* tree, int64_t* feat, int64_t* bin, uint8_t* dl,
+                        double* gain, double* tot, int64_t* left, int64_t* right) {
+  const GroupResult& R = r->groups[g];
+  const size_t n = R.tree.size();
+  std::memcpy(tree, R.tree.data(), n * 8);
+  std::memcpy(feat, R.feat.data(), n * 8);
+  std::memcpy(bin, R.bin.data(), n * 8);
+  std::memcpy(dl, R.dl.data(), n);
+  std::memcpy(gain, R.gain.data(), n * 8);
+  std::memcpy(tot, R.tot.data(), n * R.S * 8);
+  std::memcpy(left, R.left.data(), n * 8);
+  std::memcpy(right, R.right.data(), n * 8);
+}
+
+}  // namespace tmog

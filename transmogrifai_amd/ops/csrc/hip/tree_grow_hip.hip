@@ -1,0 +1,247 @@
+// HIP backend of the native tree grower (common/tree_grow.hpp): one host thread + one HIP stream per
+// job group, pinned staging buffers (three rotating slots per group) with hipMemcpyAsync, grow-only
+// device buffers kept across calls (stream-ordered hipMallocAsync when they grow), and the tmog_hip_* kernel launchers of
+// tree_kernels.hip. The only host<->device synchronisation is one result read per level and group.
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "common/tree_grow.hpp"
+
+extern "C" {
+int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
+                        const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
+                        const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
+                        const float* t1, const float* t2, int64_t stride, const float* qscale, hipStream_t stream);
+int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
+                           const int64_t* out_off, const int64_t* size, int n, int64_t max_size, hipStream_t stream);
+int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
+                        const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
+                        int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
+                        const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
+                        float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, hipStream_t stream);
+int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
+                           hipStream_t stream);
+size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat);
+int tmog_hip_partition_count(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
+                             const int32_t* split_feat, const int32_t* split_bin, const uint8_t* dl, int missing_bin,
+                             int64_t* chunk_left, hipStream_t stream);
+int tmog_hip_partition_scatter(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out,
+                               const void* items, int n_items, const int32_t* split_feat, const int32_t* split_bin,
+                               const uint8_t* dl, int missing_bin, hipStream_t stream);
+int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
+                          int32_t* out_gid, hipStream_t stream);
+}
+
+namespace {
+
+inline void hchk(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+inline void kchk(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string("kernel ") + what + " failed with code " + std::to_string(rc));
+}
+
+// per-(group slot) persistent resources: stream, pinned staging slots, device staging, result mirror
+struct GpuSlot {
+  hipStream_t stream = nullptr;
+  uint8_t* pin[3] = {nullptr, nullptr, nullptr};
+  size_t pin_cap[3] = {0, 0, 0};
+  uint8_t* dev[3] = {nullptr, nullptr, nullptr};
+  size_t dev_cap[3] = {0, 0, 0};
+  uint8_t* res_dev = nullptr;
+  size_t res_cap = 0;
+  uint8_t* res_pin = nullptr;
+  size_t res_pin_cap = 0;
+  uint8_t* cand = nullptr;
+  size_t cand_cap = 0;
+  int32_t* feats = nullptr;
+  int feats_n = 0;
+  uint8_t* hist[2] = {nullptr, nullptr};     // grow-only level histogram buffers (int64 words)
+  size_t hist_cap[2] = {0, 0};
+  int device = -1;
+};
+
+std::vector<GpuSlot>& slots() {
+  static std::vector<GpuSlot> s(8);
+  return s;
+}
+
+struct GpuBackend {
+  static constexpr bool kGPU = true;
+  GpuSlot& sl;
+  const tmog::GrowArgs& a;
+  GpuBackend(GpuSlot& s, const tmog::GrowArgs& args) : sl(s), a(args) {}
+
+  static void grow_dev(uint8_t*& p, size_t& cap, size_t need, hipStream_t s) {
+    if (need <= cap) return;
+    if (p) hchk(hipFreeAsync(p, s), "hipFreeAsync");
+    cap = need + need / 2 + 4096;
+    hchk(hipMallocAsync((void**)&p, cap, s), "hipMallocAsync");
+  }
+  static void grow_pin(uint8_t*& p, size_t& cap, size_t need, hipStream_t s) {
+    if (need <= cap) return;
+    if (p) {
+      hchk(hipStreamSynchronize(s), "sync before pinned realloc");
+      hchk(hipHostFree(p), "hipHostFree");
+    }
+    cap = need + need / 2 + 4096;
+    hchk(hipHostMalloc((void**)&p, cap, hipHostMallocDefault), "hipHostMalloc");
+  }
+  const int32_t* all_features(int F) {
+    if (sl.feats_n < F) {
+      if (sl.feats) hchk(hipFreeAsync(sl.feats, sl.stream), "hipFreeAsync");
+      std::vector<int32_t> h(F);
+      for (int i = 0; i < F; ++i) h[i] = i;
+      hchk(hipMallocAsync((void**)&sl.feats, sizeof(int32_t) * F, sl.stream), "hipMallocAsync");
+      hchk(hipMemcpyAsync(sl.feats, h.data(), sizeof(int32_t) * F, hipMemcpyHostToDevice, sl.stream), "copy feats");
+      hchk(hipStreamSynchronize(sl.stream), "sync feats");
+      sl.feats_n = F;
+    }
+    return sl.feats;
+  }
+  // Staged host arrays -> device in one async copy. A slot's previous copy is always complete here:
+  // every level performs a blocking result read after the copies of the previous level were queued.
+  const uint8_t* ship(const tmog::Staging& st, int k) {
+    const size_t n = st.buf.size() ? st.buf.size() : 16;
+    grow_pin(sl.pin[k], sl.pin_cap[k], n, sl.stream);
+    grow_dev(sl.dev[k], sl.dev_cap[k], n, sl.stream);
+    if (st.buf.size()) {
+      std::memcpy(sl.pin[k], st.buf.data(), st.buf.size());
+      hchk(hipMemcpyAsync(sl.dev[k], sl.pin[k], st.buf.size(), hipMemcpyHostToDevice, sl.stream), "stage copy");
+    }
+    return sl.dev[k];
+  }
+  int64_t* hist_buffer(int k, size_t words) {
+    grow_dev(sl.hist[k], sl.hist_cap[k], words * sizeof(int64_t), sl.stream);
+    return (int64_t*)sl.hist[k];
+  }
+  uint8_t* result_buffer(size_t bytes) {
+    grow_dev(sl.res_dev, sl.res_cap, bytes, sl.stream);
+    return sl.res_dev;
+  }
+  const uint8_t* fetch(const uint8_t* dev, size_t bytes) {
+    grow_pin(sl.res_pin, sl.res_pin_cap, bytes, sl.stream);
+    hchk(hipMemcpyAsync(sl.res_pin, dev, bytes, hipMemcpyDeviceToHost, sl.stream), "result copy");
+    hchk(hipStreamSynchronize(sl.stream), "result sync");
+    return sl.res_pin;
+  }
+  void zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t mx) {
+    kchk(tmog_hip_zero_segments(hist, off, size, n, mx, sl.stream), "zero_segments");
+  }
+  void hist_build(const tmog::GrowArgs& g, const uint32_t* rows, const void* items, int n_items, const int32_t* nfo,
+                  const int32_t* flist, const int32_t* nmd, const int64_t* nho, int64_t* hist, int, const int64_t*,
+                  const int64_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*) {
+    if (n_items)
+      kchk(tmog_hip_hist_build(g.Xb, g.F, rows, items, n_items, nfo, flist, nmd, nho, hist, g.B, g.mode, g.S, g.y,
+                               g.t1, g.t2, g.stride, g.qscale, sl.stream),
+           "hist_build");
+  }
+  void hist_subtract(int64_t* hist, const int64_t* prev, const int64_t* poff, const int64_t* soff,
+                     const int64_t* ooff, const int64_t* size, int n, int64_t mx) {
+    kchk(tmog_hip_hist_subtract(hist, prev, poff, soff, ooff, size, n, mx, sl.stream), "hist_subtract");
+  }
+  void split_find(const tmog::GrowArgs& g, const int64_t* hist, int m, const int64_t* nho, const int32_t* nnf,
+                  const int32_t* nfo, const int32_t* flist, const float* params, const int32_t* nmd, int max_nf,
+                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot) {
+    grow_dev(sl.cand, sl.cand_cap, tmog_hip_split_cand_bytes(m, max_nf), sl.stream);
+    kchk(tmog_hip_split_find(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd,
+                             g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, sl.stream),
+         "split_find");
+  }
+  void partition_count(const tmog::GrowArgs& g, const uint32_t* rows, const void* items, int n, const int32_t* feat,
+                       const int32_t* bin, const uint8_t* dl, int64_t* chunk_left) {
+    kchk(tmog_hip_partition_count(g.Xb, g.F, rows, items, n, feat, bin, dl, g.missing_bin, chunk_left, sl.stream),
+         "partition_count");
+  }
+  void partition_scatter(const tmog::GrowArgs& g, const uint32_t* rows, uint32_t* rows_alt, const void* items, int n,
+                         const int32_t* feat, const int32_t* bin, const uint8_t* dl) {
+    kchk(tmog_hip_partition_scatter(g.Xb, g.F, rows, rows_alt, items, n, feat, bin, dl, g.missing_bin, sl.stream),
+         "partition_scatter");
+  }
+  void partition_nodes(const tmog::GrowArgs&, const uint32_t*, uint32_t*, int, const int64_t*, const int64_t*,
+                       const int32_t*, const int32_t*, const uint8_t*, const int64_t*, int64_t*) {
+    throw std::logic_error("partition_nodes is the CPU backend's path");
+  }
+  void leaf_collect(const uint32_t* rows, const void* items, int n, uint32_t* out_rows, int32_t* out_gid) {
+    kchk(tmog_hip_leaf_collect(rows, items, n, out_rows, out_gid, sl.stream), "leaf_collect");
+  }
+  void finish() {}
+};
+
+}  // namespace
+
+extern "C" {
+
+void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
+  tmog::GrowResult* res = new tmog::GrowResult();
+  const tmog::GrowArgs& a = *args;
+  const int ng = a.n_groups;
+  res->groups.resize(ng);
+  try {
+    if (ng > (int)slots().size()) throw std::runtime_error("too many job groups");
+    int dev = 0;
+    hchk(hipGetDevice(&dev), "hipGetDevice");
+    hipStream_t base = (hipStream_t)a.stream;
+    hipEvent_t ready;
+    hchk(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event");
+    hchk(hipEventRecord(ready, base), "event record");
+    for (int g = 0; g < ng; ++g) {
+      GpuSlot& s = slots()[g];
+      if (s.stream == nullptr || s.device != dev) {
+        hchk(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "stream");
+        s.device = dev;
+      }
+      hchk(hipStreamWaitEvent(s.stream, ready, 0), "wait ready");
+    }
+    std::vector<std::string> errs(ng);
+    std::vector<std::thread> th;
+    for (int g = 0; g < ng; ++g) {
+      th.emplace_back([&, g]() {
+        try {
+          hchk(hipSetDevice(dev), "hipSetDevice");
+          GpuBackend bk(slots()[g], a);
+          tmog::grow_group(bk, a, g, res->groups[g]);
+        } catch (const std::exception& e) {
+          errs[g] = e.what();
+        }
+      });
+    }
+    for (auto& t : th) t.join();
+    for (int g = 0; g < ng; ++g) {
+      hipEvent_t done;
+      hchk(hipEventCreateWithFlags(&done, hipEventDisableTiming), "event");
+      hchk(hipEventRecord(done, slots()[g].stream), "event record");
+      hchk(hipStreamWaitEvent(base, done, 0), "base wait");
+      hchk(hipEventDestroy(done), "event destroy");
+    }
+    hchk(hipEventDestroy(ready), "event destroy");
+    for (int g = 0; g < ng; ++g)
+      if (!errs[g].empty()) throw std::runtime_error("group " + std::to_string(g) + ": " + errs[g]);
+  } catch (const std::exception& e) {
+    res->status = -1;
+    res->error = e.what();
+  }
+  return res;
+}
+
+int tmog_hip_grow_status(void* h, char* msg, int cap) {
+  tmog::GrowResult* r = (tmog::GrowResult*)h;
+  if (msg && cap > 0) {
+    std::strncpy(msg, r->error.c_str(), cap - 1);
+    msg[cap - 1] = 0;
+  }
+  return r->status;
+}
+int64_t tmog_hip_grow_nodes(void* h, int g) { return tmog::result_nodes((tmog::GrowResult*)h, g); }
+int64_t tmog_hip_grow_leaf_count(void* h, int g) { return ((tmog::GrowResult*)h)->groups[g].leaf_count; }
+void tmog_hip_grow_copy(void* h, int g, int64_t* tree, int64_t* feat, int64_t* bin, uint8_t* dl, double* gain,
+                        double* tot, int64_t* left, int64_t* right) {
+  tmog::result_copy((tmog::GrowResult*)h, g, tree, feat, bin, dl, gain, tot, left, right);
+}
+void tmog_hip_grow_free(void* h) { delete (tmog::GrowResult*)h; }
+
+}  // extern "C"
