@@ -68,3 +68,20 @@ def test_workflow_end_to_end_on_device():
         assert _native_loaded()
     finally:
         CFG.set_default_device(old)
+
+
+@pytest.mark.gpu
+def test_onehot_pivot_kernel_matches_host():
+    from transmogrifai_amd.ops import vector as V
+    g = torch.Generator().manual_seed(0)
+    n = 5000
+    codes = [torch.randint(-1, 7, (n,), generator=g, dtype=torch.int32), torch.randint(-1, 3, (n,), generator=g,
+                                                                                        dtype=torch.int32)]
+    luts = [np.array([0, 1, 2, 3, 3, 3, 3, 4]), np.array([1, 0, 2, -1])]
+    offs = [0, 5]
+    ref = torch.zeros(n, 8)
+    V.onehot_pivot(ref, codes, luts, offs)
+    out = torch.zeros(n, 8, device="cuda")
+    V.onehot_pivot(out, [c.cuda() for c in codes], luts, offs)
+    torch.testing.assert_close(out.cpu(), ref)
+    assert float(ref.sum()) > 0

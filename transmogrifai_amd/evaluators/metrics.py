@@ -20,13 +20,17 @@ def _curve_counts(scores: torch.Tensor, labels: torch.Tensor, num_bins: int = 0,
     s = scores.to(torch.float64).reshape(-1)
     y = labels.to(torch.float64).reshape(-1)
     w = torch.ones_like(s) if weights is None else weights.to(torch.float64)
-    order = torch.argsort(s, descending=True, stable=True)
-    s, y, w = s[order], y[order], w[order]
+    s, order = torch.sort(s, descending=True, stable=True)
+    y, w = y[order], w[order]
     # segmented sums over runs of equal scores without atomics: the input is sorted, so the per-run
-    # totals are differences of the running sums at the run ends
-    uniq, cnt = torch.unique_consecutive(s, return_counts=True)
+    # totals are differences of the running sums at the run ends (run ends found by a neighbour
+    # compare + one compaction; torch.unique_consecutive is ~10x slower on ROCm at 3M rows)
+    is_end = torch.ones(s.numel(), dtype=torch.bool, device=s.device)
+    if s.numel() > 1:
+        is_end[:-1] = s[1:] != s[:-1]
+    ends = is_end.nonzero().squeeze(1)
+    uniq = s[ends]
     n_u = uniq.numel()
-    ends = torch.cumsum(cnt, 0) - 1
     cpos = torch.cumsum(w * (y > 0.5), 0)
     cneg = torch.cumsum(w * (y <= 0.5), 0)
     tp_end, fp_end = cpos[ends], cneg[ends]

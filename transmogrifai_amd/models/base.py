@@ -65,12 +65,23 @@ def compact_rows(X: torch.Tensor, y: torch.Tensor, jobs: Sequence[FitJob]):
     remapped, or the inputs unchanged when a job uses every row or the union is all of ``X``."""
     if not jobs or any(j.rows is None for j in jobs):
         return X, y, list(jobs)
-    U, inv = torch.unique(torch.cat([j.rows.to(X.device) for j in jobs]), return_inverse=True)
+    U, parts = union_rows([j.rows for j in jobs], X.shape[0], X.device)
     if U.numel() >= X.shape[0]:
         return X, y, list(jobs)
-    parts = torch.split(inv, [int(j.rows.numel()) for j in jobs])
     return X.index_select(0, U), y.to(X.device).index_select(0, U), \
         [FitJob(j.params, r, j.weights) for j, r in zip(jobs, parts)]
+
+
+def union_rows(rows: Sequence[torch.Tensor], N: int, device):
+    """Sorted union ``U`` of several row-id sets over ``[0, N)`` and each set remapped to positions in
+    ``U``: a presence mask + prefix count (O(N), no sort; ``torch.unique`` sorts the concatenation)."""
+    cat = torch.cat([r.to(device) for r in rows]).to(torch.int64)
+    mask = torch.zeros(N, dtype=torch.bool, device=device)
+    mask[cat] = True
+    U = mask.nonzero().squeeze(1)
+    pos = torch.cumsum(mask, 0) - 1
+    parts = torch.split(pos[cat], [int(r.numel()) for r in rows])
+    return U, list(parts)
 
 
 class Learner:

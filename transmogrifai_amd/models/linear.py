@@ -22,6 +22,7 @@ import torch
 
 from ..ops import linear as LK
 from .base import FitJob, Learner, OpPredictor, compact_rows, probability_outputs, register_learner
+from ..ops.staging import to_device
 from ..stages.base import register_stage
 
 
@@ -284,12 +285,11 @@ class _LinearBase(Learner):
         for p, s in enumerate(stdz):
             if not s:
                 inv_std[:, p] = torch.where(std[:, p] > 0, torch.ones_like(std[:, p]), torch.zeros_like(std[:, p]))
-        reg = torch.tensor([float(j.params.get("reg_param", 0.0)) for j in jobs], dtype=torch.float64, device=dev)
-        en = torch.tensor([float(j.params.get("elastic_net_param", 0.0)) for j in jobs], dtype=torch.float64,
-                          device=dev)
-        fi = torch.tensor([bool(j.params.get("fit_intercept", True)) for j in jobs], device=dev)
-        max_iter = torch.tensor([int(j.params.get("max_iter", 100)) for j in jobs], device=dev)
-        tol = torch.tensor([float(j.params.get("tol", 1e-6)) for j in jobs], dtype=torch.float64, device=dev)
+        reg = to_device([float(j.params.get("reg_param", 0.0)) for j in jobs], dev, np.float64)
+        en = to_device([float(j.params.get("elastic_net_param", 0.0)) for j in jobs], dev, np.float64)
+        fi = to_device([bool(j.params.get("fit_intercept", True)) for j in jobs], dev, np.bool_)
+        max_iter = to_device([int(j.params.get("max_iter", 100)) for j in jobs], dev, np.int64)
+        tol = to_device([float(j.params.get("tol", 1e-6)) for j in jobs], dev, np.float64)
         return W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz
 
 

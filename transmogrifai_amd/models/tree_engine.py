@@ -321,52 +321,7 @@ class LeafAssign:
         return self.value[self.gid.to(torch.int64)]
 
 
-_TORCH_OF_NP = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32,
-                np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
-                np.dtype(np.uint8): torch.uint8, np.dtype(np.bool_): torch.bool}
-
-
-class _Pack:
-    """Ships several small host arrays with ONE host->device copy through a pinned staging ring
-    (each ``torch.as_tensor(a, device=cuda)`` is its own blocking hipMemcpy: ~10 per tree level)."""
-    _ring: dict = {}
-    _RING = 4
-
-    def __init__(self, dev):
-        self.dev = dev
-        self.arrs: List[np.ndarray] = []
-
-    def add(self, a) -> int:
-        self.arrs.append(np.ascontiguousarray(a))
-        return len(self.arrs) - 1
-
-    def ship(self) -> List[torch.Tensor]:
-        if self.dev.type != "cuda":
-            return [torch.from_numpy(a) for a in self.arrs]
-        offs, tot = [], 0
-        for a in self.arrs:
-            offs.append(tot)
-            tot += (a.nbytes + 15) & ~15
-        tot = max(tot, 16)
-        key = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
-        slots = _Pack._ring.setdefault(key, {"i": 0, "bufs": [None] * self._RING, "ev": [None] * self._RING})
-        k = slots["i"] = (slots["i"] + 1) % self._RING
-        buf, ev = slots["bufs"][k], slots["ev"][k]
-        if ev is not None:
-            ev.synchronize()                 # the copy that last used this slot has finished
-        if buf is None or buf.numel() < tot:
-            buf = torch.empty(max(tot, 1 << 16), dtype=torch.uint8, pin_memory=True)
-            slots["bufs"][k] = buf
-        hb = buf.numpy()
-        for a, o in zip(self.arrs, offs):
-            hb[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
-        d = torch.empty(tot, dtype=torch.uint8, device=self.dev)
-        d.copy_(buf[:tot], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.dev))
-        slots["ev"][k] = ev
-        return [d[o:o + a.nbytes].view(_TORCH_OF_NP[a.dtype]).reshape(a.shape) if a.dtype in _TORCH_OF_NP
-                else d[o:o + a.nbytes] for a, o in zip(self.arrs, offs)]
+from ..ops.staging import Pack as _Pack  # noqa: E402  (re-exported for the learners)
 
 
 _CONST: dict = {}

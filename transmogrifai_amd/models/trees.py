@@ -23,9 +23,10 @@ import numpy as np
 import torch
 
 from . import tree_engine as TE
-from .base import FitJob, Learner, OpPredictor, probability_outputs, register_learner
+from .base import FitJob, Learner, OpPredictor, probability_outputs, register_learner, union_rows
 from .binning import BinSpec, find_splits, quantize
 from ..stages.base import register_stage
+from ..ops.staging import to_device
 from ..tuning.splitters import row_uniform, row_uniform_multi
 
 
@@ -178,11 +179,10 @@ class _ForestLearner(Learner):
             if all(jobs[i].rows is not None for i in idxs):
                 # grow over the union of the training rows only (smaller gather footprint, and the
                 # packed 24-bit row ids then index the compacted matrix)
-                U, inv = torch.unique(torch.cat([jrows[i] for i in idxs]), return_inverse=True)
+                U, parts = union_rows([jrows[i] for i in idxs], N, dev)
                 if U.numel() < N:
                     Xb = Xb.index_select(0, U)
                     yg = y.to(dev).index_select(0, U)
-                    parts = torch.split(inv, [int(jrows[i].numel()) for i in idxs])
                     jrows = {i: r for i, r in zip(idxs, parts)}
             tjobs, owner = [], []
             for i in idxs:
@@ -349,12 +349,11 @@ class _BoostLearner(Learner):
             if all(j.rows is not None for j in gjobs):
                 # boost only over the union of the jobs' training rows: gradients, margins and the
                 # per-round prediction pass then scale with the (down-sampled) training sets, not N
-                U, inv = torch.unique(torch.cat([j.rows.to(dev) for j in gjobs]), return_inverse=True)
+                U, parts = union_rows([j.rows for j in gjobs], N, dev)
                 if U.numel() < N:
                     Xb = Xb.index_select(0, U)
                     yd = yd.index_select(0, U)
                     NU = int(U.numel())
-                    parts = torch.split(inv, [int(j.rows.numel()) for j in gjobs])
                     gjobs = [FitJob(j.params, r, j.weights) for j, r in zip(gjobs, parts)]
             res = self._boost(Xb, spec, yd, gjobs, NU, F, dev, key[0])
             for k, i in enumerate(idxs):
@@ -498,7 +497,7 @@ class XGBoostClassifierLearner(_BoostLearner):
         rounds = [int(j.params.get("num_round", 100)) for j in jobs]
         esr = [int(j.params.get("num_early_stopping_rounds", 0)) for j in jobs]
         base = [self._base_margin(float(j.params.get("base_score", 0.5))) for j in jobs]
-        Fm = torch.tensor(base, dtype=torch.float64, device=dev)[:, None].repeat(1, N)
+        Fm = to_device(base, dev, np.float64)[:, None].repeat(1, N)
         yy = y.to(torch.float64)
         ylab = [yy[r] for r in rows]
         forests, weights = [[] for _ in range(P)], [[] for _ in range(P)]

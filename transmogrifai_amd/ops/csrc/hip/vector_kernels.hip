@@ -40,9 +40,37 @@ __global__ void __launch_bounds__(256) vectorize_numeric_kernel(const float* con
   }
 }
 
+// One-hot pivot of several categorical columns at once (OpOneHotVectorizer transform,
+// OpOneHotVectorizer.scala:416-437): column c maps dictionary code -> slot through lut[c]
+// (code -1 = missing uses the lut's last entry, slot -1 = no output), writing 1.0 at
+// out[row, off[c] + slot]. out is zero-initialised by the caller; each (row, column) writes at most
+// one element, so plain stores suffice. grid.y = column.
+__global__ void __launch_bounds__(256) onehot_pivot_kernel(const int32_t* const* __restrict__ codes,
+                                                           const int32_t* const* __restrict__ luts,
+                                                           const int32_t* __restrict__ lut_n,
+                                                           const int64_t* __restrict__ off, int64_t n,
+                                                           float* __restrict__ out, int64_t W) {
+  const int c = blockIdx.y;
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const int32_t code = codes[c][r];
+  const int32_t ln = lut_n[c];
+  const int32_t slot = luts[c][(code >= 0 && code < ln - 1) ? code : ln - 1];
+  if (slot >= 0) out[r * W + off[c] + slot] = 1.f;
+}
+
 }  // namespace
 
 extern "C" {
+
+int tmog_hip_onehot_pivot(const void* codes, const void* luts, const int32_t* lut_n, const int64_t* off, int n_cols,
+                          int64_t n, float* out, int64_t W, hipStream_t stream) {
+  if (n == 0 || n_cols == 0) return 0;
+  dim3 grid((unsigned)((n + 255) / 256), (unsigned)n_cols);
+  hipLaunchKernelGGL(onehot_pivot_kernel, grid, dim3(256), 0, stream, (const int32_t* const*)codes,
+                     (const int32_t* const*)luts, lut_n, off, n, out, W);
+  return (int)hipGetLastError();
+}
 
 int tmog_hip_vectorize_numeric(const void* vals, const void* valid, const float* fills, int64_t n, int F,
                                const void* r1, const void* r2, const void* r3, float* out, int64_t W, int track,

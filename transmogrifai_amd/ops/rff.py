@@ -10,9 +10,11 @@ from __future__ import annotations
 
 from typing import Optional, Sequence
 
+import numpy as np
 import torch
 
 from . import _native as N
+from .staging import Pack
 
 NSTAT = 9
 _DT = {torch.float32: 0, torch.float64: 1, torch.int64: 2, torch.bool: 3, torch.uint8: 3}
@@ -37,9 +39,10 @@ def _prep(values: Sequence[torch.Tensor], valids: Sequence[Optional[torch.Tensor
             o = ok.to(torch.uint8).contiguous()
             keep.append(o)
             oks.append(o.data_ptr())
-    vp = torch.tensor(vals, dtype=torch.int64, device=dev)
-    op = torch.tensor(oks, dtype=torch.int64, device=dev)
-    dt = torch.tensor(dts, dtype=torch.int32, device=dev)
+    pk = Pack(dev)
+    i_v, i_o, i_d = pk.add(np.asarray(vals, np.int64)), pk.add(np.asarray(oks, np.int64)), pk.add(np.asarray(dts, np.int32))
+    d = pk.ship()
+    vp, op, dt = d[i_v], d[i_o], d[i_d]
     return vp, op, dt, keep
 
 

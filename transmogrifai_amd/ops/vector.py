@@ -13,6 +13,7 @@ import torch
 
 from ..data.columns import NumericColumn
 from . import _native as N
+from .staging import Pack, to_device
 
 
 def column_means(cols: Sequence[NumericColumn]) -> List[float]:
@@ -53,9 +54,12 @@ def fill_and_track(cols: Sequence[NumericColumn], fills: Sequence[float], track_
         out = torch.empty(n, W, dtype=dtype, device=dev)
         vals = [c.values.to(torch.float32).contiguous() for c in cols]
         oks = [c.valid.contiguous() for c in cols]
-        vp = torch.tensor([t.data_ptr() for t in vals], dtype=torch.int64, device=dev)
-        op = torch.tensor([t.data_ptr() for t in oks], dtype=torch.int64, device=dev)
-        fl = torch.tensor(list(fills), dtype=torch.float32, device=dev)
+        pk = Pack(dev)
+        i_v = pk.add(np.array([t.data_ptr() for t in vals], np.int64))
+        i_o = pk.add(np.array([t.data_ptr() for t in oks], np.int64))
+        i_f = pk.add(np.asarray(list(fills), np.float32))
+        d = pk.ship()
+        vp, op, fl = d[i_v], d[i_o], d[i_f]
         N.check(N.hip().tmog_hip_vectorize_numeric(
             N.ptr(vp), N.ptr(op), N.ptr(fl), n, F, None, None, None, N.ptr(out), W, int(track_nulls),
             N.stream(dev)), "vectorize_numeric")
@@ -63,11 +67,38 @@ def fill_and_track(cols: Sequence[NumericColumn], fills: Sequence[float], track_
         return out
     vals = torch.stack([c.values.to(dtype) for c in cols], 1)
     ok = torch.stack([c.valid for c in cols], 1)
-    fill = torch.tensor(list(fills), dtype=dtype, device=dev)[None, :]
+    fill = to_device(np.asarray(list(fills), np.float64), dev).to(dtype)[None, :]
     filled = torch.where(ok, vals, fill)
     if not track_nulls:
         return filled.contiguous()
     return torch.stack([filled, (~ok).to(dtype)], 2).reshape(n, W)
+
+
+def onehot_pivot(out: torch.Tensor, codes: Sequence[torch.Tensor], luts: Sequence[np.ndarray],
+                 offs: Sequence[int]) -> None:
+    """All categorical columns of a pivot block in one HIP launch (``onehot_pivot_kernel``) when ``out``
+    is an fp32 device matrix; otherwise column by column through ``onehot_scatter``."""
+    if not codes:
+        return
+    dev = out.device
+    if dev.type == "cuda" and out.dtype == torch.float32 and out.is_contiguous():
+        cs = [c.to(device=dev, dtype=torch.int32).contiguous() for c in codes]
+        ls = [np.ascontiguousarray(l, np.int32) for l in luts]
+        pk = Pack(dev)
+        i_l = [pk.add(l) for l in ls]
+        i_n, i_o = pk.add(np.array([l.size for l in ls], np.int32)), pk.add(np.asarray(offs, np.int64))
+        d = pk.ship()
+        lp = [d[i] for i in i_l]
+        pk2 = Pack(dev)
+        i_c, i_lp = pk2.add(np.array([c.data_ptr() for c in cs], np.int64)), pk2.add(
+            np.array([t.data_ptr() for t in lp], np.int64))
+        d2 = pk2.ship()
+        N.check(N.hip().tmog_hip_onehot_pivot(N.ptr(d2[i_c]), N.ptr(d2[i_lp]), N.ptr(d[i_n]), N.ptr(d[i_o]), len(cs),
+                                              int(out.shape[0]), N.ptr(out), int(out.shape[1]), N.stream(dev)),
+                "onehot_pivot")
+        return
+    for c, l, o in zip(codes, luts, offs):
+        onehot_scatter(out, c, torch.as_tensor(np.asarray(l, np.int64), device=dev), o)
 
 
 def onehot_scatter(out: torch.Tensor, codes: torch.Tensor, lut: torch.Tensor, off: int) -> None:

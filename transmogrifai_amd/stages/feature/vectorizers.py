@@ -215,6 +215,7 @@ def pivot_columns(cols, tops, clean, track_nulls, dtype) -> torch.Tensor:
     widths = [len(t) + 1 + (1 if track_nulls else 0) for t in tops]
     out = torch.zeros(n, sum(widths), dtype=dtype, device=dev)
     off = 0
+    p_codes, p_luts, p_offs = [], [], []     # dictionary-coded columns: one batched pivot launch
     for c, top, w in zip(cols, tops, widths):
         if isinstance(c, TextColumn):
             idx = {v: i for i, v in enumerate(top)}
@@ -223,7 +224,9 @@ def pivot_columns(cols, tops, clean, track_nulls, dtype) -> torch.Tensor:
                 k = TU.clean_string(s) if clean else s
                 lut[j] = idx.get(k, len(top))
             lut[-1] = len(top) + 1 if track_nulls else -1
-            V.onehot_scatter(out, c.codes, torch.as_tensor(lut, device=dev), off)
+            p_codes.append(c.codes)
+            p_luts.append(lut)
+            p_offs.append(off)
         else:
             vals = c.values if isinstance(c, ObjectColumn) else c.to_list()
             block = np.zeros((n, w))
@@ -238,6 +241,7 @@ def pivot_columns(cols, tops, clean, track_nulls, dtype) -> torch.Tensor:
                     block[r, idx.get(k, len(top))] += cnt
             out[:, off:off + w] = torch.as_tensor(block, dtype=dtype, device=dev)
         off += w
+    V.onehot_pivot(out, p_codes, p_luts, p_offs)
     return out
 
 
