@@ -9,10 +9,13 @@ One *step* is one complete ``OpWorkflow.train()``:
   (10% hold-out reserve, 1M max training sample as in ``Splitter.scala:176-178``), refit of the
   winner, train + hold-out evaluation.
 
-Multi-GPU (``torchrun``, one rank per GPU, RCCL): every rank holds the table in HBM (288 GB makes the
-replicated layout viable) and the (model, grid point, fold) fits are sharded across ranks by a
-cost model (``tuning/validators.py``); metrics are exchanged with one all-gather. Total work is
-fixed as N grows -> ``"scaling": "strong"``.
+Multi-GPU (``torchrun``, one rank per GPU, RCCL over xGMI): each rank holds a contiguous row shard of
+the table (``Dataset.shard``); transmogrify / SanityChecker fit statistics are all-reduced
+(``parallel/dp.py``), the model selector gathers the rows its CV folds and refit sample (the 1M
+``maxTrainingSample`` cap) to every rank and shards the (model, grid point, fold) fits across ranks by
+a cost model (``tuning/validators.py``); the hold-out is scored on the local shard and its
+(label, score) rows are all-gathered for the metrics. ``--layout replicated`` keeps the whole table on
+every rank instead. Total work is fixed as N grows -> ``"scaling": "strong"``.
 
 The value reported is the end-to-end wall-clock seconds of one AutoML train (lower is better); the
 hold-out AuPR of the selected model is reported next to it. The reference publishes no wall-clock
@@ -45,6 +48,9 @@ def parse():
                     help="comma list of learner names, or 'default' (LR, RF, XGBoost as the reference)")
     ap.add_argument("--folds", type=int, default=3)
     ap.add_argument("--device", default=None)
+    ap.add_argument("--layout", default="sharded", choices=["sharded", "replicated"],
+                    help="multi-GPU table layout: row shards with all-reduced fit statistics (data parallel), "
+                         "or the whole table on every rank")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -94,6 +100,10 @@ def main():
     def one_run():
         uid.reset(0)
         ds, label, preds = binary_table(args.rows, args.real, args.ints, args.pick, seed=7, device=dev)
+        if world > 1 and args.layout == "sharded":
+            ds = ds.shard(D.rank(), world)      # N / world rows per GPU; global row ids kept
+            if use_gpu:
+                torch.cuda.empty_cache()
         wf, pred = build_workflow(args, ds, label, preds)
         sync()
         t0 = time.perf_counter()
@@ -136,7 +146,8 @@ def main():
                                 ("LR,RF,XGB default grid" if args.models == "default" else args.models) + ")",
                        "rows": args.rows, "raw_columns": args.real + args.ints + args.pick,
                        "cv_folds": args.folds, "global_batch": args.rows, "seq_len": None,
-                       "parallelism": f"grid-shard{world}" if world > 1 else "single"},
+                       "parallelism": (f"dp{world}" if args.layout == "sharded" else f"grid-shard{world}")
+                       if world > 1 else "single"},
         }
         if args.verbose and summ:
             out["timings"] = summ.get("timings")

@@ -33,6 +33,9 @@ class Dataset:
         self.key = key
         # global row ids (stable across shards / subsets): drive every seeded per-row decision
         self._row_ids = row_ids
+        # True when this is one rank's row shard of a table split across a process group
+        # (parallel/dp.py): estimator fits then reduce their statistics over the ranks
+        self.sharded = False
 
     @property
     def row_ids(self) -> torch.Tensor:
@@ -69,7 +72,7 @@ class Dataset:
             raise ValueError(f"column '{name}' has {len(col)} rows, dataset has {self.n_rows}")
         cols = OrderedDict(self.columns)
         cols[name] = col
-        return Dataset(cols, self.key, self.n_rows, self._row_ids)
+        return self._like(Dataset(cols, self.key, self.n_rows, self._row_ids))
 
     def with_columns(self, new: Dict[str, Column]) -> "Dataset":
         cols = OrderedDict(self.columns)
@@ -77,15 +80,33 @@ class Dataset:
             if len(v) != self.n_rows:
                 raise ValueError(f"column '{k}' has {len(v)} rows, dataset has {self.n_rows}")
             cols[k] = v
-        return Dataset(cols, self.key, self.n_rows, self._row_ids)
+        return self._like(Dataset(cols, self.key, self.n_rows, self._row_ids))
 
     def select(self, names: Iterable[str]) -> "Dataset":
-        return Dataset(OrderedDict((n, self.columns[n]) for n in names), self.key, self.n_rows, self._row_ids)
+        return self._like(Dataset(OrderedDict((n, self.columns[n]) for n in names), self.key, self.n_rows,
+                                  self._row_ids))
 
     def drop(self, names: Iterable[str]) -> "Dataset":
         names = set(names)
-        return Dataset(OrderedDict((k, v) for k, v in self.columns.items() if k not in names), self.key, self.n_rows,
-                       self._row_ids)
+        return self._like(Dataset(OrderedDict((k, v) for k, v in self.columns.items() if k not in names), self.key,
+                                  self.n_rows, self._row_ids))
+
+    def _like(self, other: "Dataset") -> "Dataset":
+        other.sharded = self.sharded
+        return other
+
+    def shard(self, rank: int, world: int) -> "Dataset":
+        """Contiguous row shard ``rank`` of ``world`` with the global row ids kept, marked ``sharded``: the
+        data-parallel layout of SURVEY.md §2.8 (each GPU holds ``N / world`` rows, fit statistics are
+        all-reduced, see parallel/dp.py)."""
+        n = self.n_rows
+        a, b = (n * rank) // world, (n * (rank + 1)) // world
+        idx = torch.arange(a, b, device=self.row_ids.device)
+        cols = OrderedDict((k, v.take(idx)) for k, v in self.columns.items())
+        key = None if self.key is None else self.key[a:b]
+        out = Dataset(cols, key, b - a, self.row_ids[a:b])
+        out.sharded = world > 1
+        return out
 
     def take(self, idx) -> "Dataset":
         if isinstance(idx, torch.Tensor):
@@ -95,11 +116,11 @@ class Dataset:
         cols = OrderedDict((k, v.take(idx)) for k, v in self.columns.items())
         key = None if self.key is None else self.key[idx_np]
         rid = self.row_ids
-        return Dataset(cols, key, len(idx_np), rid[torch.as_tensor(idx_np, device=rid.device)])
+        return self._like(Dataset(cols, key, len(idx_np), rid[torch.as_tensor(idx_np, device=rid.device)]))
 
     def to(self, device) -> "Dataset":
-        return Dataset(OrderedDict((k, v.to(device)) for k, v in self.columns.items()), self.key, self.n_rows,
-                       None if self._row_ids is None else self._row_ids.to(device))
+        return self._like(Dataset(OrderedDict((k, v.to(device)) for k, v in self.columns.items()), self.key,
+                                  self.n_rows, None if self._row_ids is None else self._row_ids.to(device)))
 
     @staticmethod
     def concat(parts) -> "Dataset":

@@ -613,7 +613,14 @@ class RawFeatureFilter:
             train_ds = self.training_reader.generate_dataset(raw_features, params)
         if len(train_ds) == 0:
             raise ValueError("RawFeatureFilter cannot work with empty training data")
-        tinfo = self.compute_feature_stats(train_ds, raw_features, TRAINING)
+        stats_ds = train_ds
+        if getattr(train_ds, "sharded", False):
+            # row-sharded input: the distributions are computed on the gathered raw columns so every
+            # rank derives the identical blocklist (the filtered DAG must agree across ranks)
+            from ..parallel import dp
+            with dp.scope(True):
+                stats_ds = dp.gather_dataset(train_ds, [n for n in train_ds.names])
+        tinfo = self.compute_feature_stats(stats_ds, raw_features, TRAINING)
         sinfo = None
         if self.scoring_reader is not None:
             sds = self.scoring_reader.generate_dataset(raw_features, params)

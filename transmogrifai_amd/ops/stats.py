@@ -15,21 +15,38 @@ import torch
 from . import _native as N
 
 
-def col_stats(X: torch.Tensor) -> Dict[str, torch.Tensor]:
-    n = X.shape[0]
+def _col_partials(X: torch.Tensor):
+    """(sum, sum of squares, min, max, non-zeros) per column, fp64, in one pass (HIP kernel on fp32 device data)."""
+    n, d = X.shape[0], X.shape[1]
     if X.is_cuda and X.dtype == torch.float32 and n > 0 and X.is_contiguous():
-        d = X.shape[1]
         out = torch.empty(6, d, dtype=torch.float64, device=X.device)
         N.check(N.hip().tmog_hip_col_stats(N.ptr(X), None, n, d, d, N.ptr(out), N.stream(X.device)), "col_stats")
-        s1, s2, mn, mx, nnz = out[0], out[1], out[2], out[3], out[4]
-        mean = s1 / max(n, 1)
-        var = (s2 - n * mean * mean) / max(n - 1, 1)
-        return {"count": n, "mean": mean, "variance": var.clamp_min(0), "min": mn, "max": mx, "numNonzeros": nnz}
+        return out[0], out[1], out[2], out[3], out[4]
     Xd = X.to(torch.float64)
-    mean = Xd.mean(0) if n else torch.zeros(X.shape[1], dtype=torch.float64)
-    var = Xd.var(0, unbiased=True) if n > 1 else torch.zeros(X.shape[1], dtype=torch.float64)
-    return {"count": n, "mean": mean, "variance": var, "min": Xd.min(0).values if n else mean,
-            "max": Xd.max(0).values if n else mean, "numNonzeros": (Xd != 0).sum(0).to(torch.float64)}
+    if n == 0:
+        z = torch.zeros(d, dtype=torch.float64, device=X.device)
+        return z, z.clone(), torch.full_like(z, float("inf")), torch.full_like(z, float("-inf")), z.clone()
+    return Xd.sum(0), (Xd * Xd).sum(0), Xd.min(0).values, Xd.max(0).values, (Xd != 0).sum(0).to(torch.float64)
+
+
+def col_stats(X: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """Spark ``Statistics.colStats``. In a row-sharded fit the per-rank partials are all-reduced (one packed
+    SUM of count / sums / non-zeros plus a MIN and a MAX, ``SanityChecker.scala:407``)."""
+    from ..parallel import dp
+    s1, s2, mn, mx, nnz = _col_partials(X)
+    n_t = torch.tensor([float(X.shape[0])], dtype=torch.float64, device=s1.device)
+    if dp.active():
+        n_t, s1, s2, nnz = dp.sum_([n_t, s1, s2, nnz])
+        mn, mx = dp.min_(mn), dp.max_(mx)
+    n = int(n_t.item())
+    mean = s1 / max(n, 1)
+    if not dp.active() and not (X.is_cuda and X.dtype == torch.float32) and n > 1:
+        var = X.to(torch.float64).var(0, unbiased=True)      # host reference path: two-pass variance
+    else:
+        var = ((s2 - n * mean * mean) / max(n - 1, 1)).clamp_min(0)
+    if n == 0:
+        mn, mx = mean, mean
+    return {"count": n, "mean": mean, "variance": var, "min": mn, "max": mx, "numNonzeros": nnz}
 
 
 def _rank_columns(X: torch.Tensor) -> torch.Tensor:
@@ -49,15 +66,26 @@ def _rank_columns(X: torch.Tensor) -> torch.Tensor:
 
 
 def corr_matrix(X: torch.Tensor, method: str = "pearson", mean=None) -> torch.Tensor:
-    """``(d x d)`` correlation matrix; NaN where a column has zero variance (Spark semantics)."""
+    """``(d x d)`` correlation matrix; NaN where a column has zero variance (Spark semantics).
+
+    Row-sharded fits: Pearson centres every shard on the global mean and all-reduces the partial
+    Gramians (``SanityChecker.scala:468``, one ``(d x d)`` SUM); Spearman needs global ranks, so the
+    (already down-sampled) rows are gathered first."""
+    from ..parallel import dp
     if method == "spearman":
+        if dp.active():
+            X = dp.rows(X)
+            with dp.local_only():
+                return corr_matrix(X, method)
         X = _rank_columns(X)
         mean = None
-    n = X.shape[0]
+    n = dp.count(X.shape[0])
     if mean is None:
-        mean = X.to(torch.float64).mean(0)
+        s, = dp.sum_([X.to(torch.float64).sum(0)])
+        mean = s / max(n, 1)
     Xc = (X - mean.to(X.dtype)[None, :])
-    G = (Xc.t() @ Xc).to(torch.float64) / max(n - 1, 1)
+    G, = dp.sum_([(Xc.t() @ Xc).to(torch.float64)])
+    G = G / max(n - 1, 1)
     sd = torch.sqrt(torch.diag(G))
     C = G / (sd[:, None] * sd[None, :])
     C = torch.where((sd[:, None] == 0) | (sd[None, :] == 0), torch.full_like(C, float("nan")), C)
@@ -66,10 +94,14 @@ def corr_matrix(X: torch.Tensor, method: str = "pearson", mean=None) -> torch.Te
 
 
 def label_column_sums(X: torch.Tensor, y: torch.Tensor):
-    """(sorted distinct labels, ``[L, d]`` per-label column sums, ``[L]`` counts)."""
-    labels, inv = torch.unique(y.to(torch.float64), return_inverse=True)
+    """(sorted distinct labels, ``[L, d]`` per-label column sums, ``[L]`` counts): the skinny GEMM
+    ``onehot(y)^T X``. Row-sharded fits use the global label set and all-reduce the sums
+    (``SanityChecker.scala:272,280`` ``reduceByKey(label)``)."""
+    from ..parallel import dp
+    labels = dp.unique_values(y.to(torch.float64))
+    inv = torch.searchsorted(labels, y.to(torch.float64))
     L = labels.numel()
     oh = torch.zeros(X.shape[0], L, dtype=X.dtype, device=X.device)
     oh[torch.arange(X.shape[0], device=X.device), inv] = 1
-    sums = (oh.t() @ X).to(torch.float64)
-    return labels, sums, oh.sum(0).to(torch.float64)
+    sums, cnt = dp.sum_([(oh.t() @ X).to(torch.float64), oh.sum(0).to(torch.float64)])
+    return labels, sums, cnt

@@ -17,27 +17,43 @@ from .staging import Pack, to_device
 
 
 def column_means(cols: Sequence[NumericColumn]) -> List[float]:
-    """Mean of non-null values per column; 0 when a column is all null (``MeanSeqNullNum``)."""
-    out = []
-    for c in cols:
-        v = c.values.to(torch.float64)
-        ok = c.valid
-        s = torch.where(ok, v, torch.zeros_like(v)).sum()
-        n = ok.sum()
-        out.append(float(s / n) if int(n) > 0 else float(s))
-    return out
+    """Mean of non-null values per column; 0 when a column is all null (``MeanSeqNullNum``).
+
+    All columns reduce in one batched pass and one host read; in a row-sharded fit the (sum, count)
+    pairs of every column are all-reduced in one collective (``RealVectorizer.scala:84``)."""
+    from ..parallel import dp
+    if not cols:
+        return []
+    sums = torch.stack([torch.where(c.valid, c.values.to(torch.float64), torch.zeros((), dtype=torch.float64,
+                                                                                        device=c.values.device)).sum()
+                        for c in cols])
+    cnts = torch.stack([c.valid.sum().to(torch.float64) for c in cols])
+    sums, cnts = dp.sum_([sums, cnts])
+    s, n = sums.cpu().numpy(), cnts.cpu().numpy()
+    return [float(a / b) if b > 0 else float(a) for a, b in zip(s, n)]
 
 
 def column_modes(cols: Sequence[NumericColumn]) -> List[float]:
-    """Mode of non-null values per column, ties -> smallest value, 0 if empty (``ModeSeqNullInt``)."""
-    out = []
+    """Mode of non-null values per column, ties -> smallest value, 0 if empty (``ModeSeqNullInt``).
+    Row-sharded fits merge the per-rank (value, count) tables before the argmax."""
+    from ..parallel import dp
+    tables = []
     for c in cols:
         v = c.values[c.valid]
-        if v.numel() == 0:
+        u, cnt = torch.unique(v, return_counts=True)
+        tables.append((u.cpu().numpy(), cnt.cpu().numpy()))
+    parts = dp.objects(tables)
+    out = []
+    for j in range(len(cols)):
+        acc: dict = {}
+        for p in parts:
+            for val, k in zip(*p[j]):
+                acc[val.item()] = acc.get(val.item(), 0) + int(k)
+        if not acc:
             out.append(0.0)
             continue
-        u, cnt = torch.unique(v, return_counts=True)
-        out.append(float(u[int(torch.argmax(cnt))]))
+        best = max(acc.items(), key=lambda vc: (vc[1], -vc[0]))
+        out.append(float(best[0]))
     return out
 
 

@@ -89,7 +89,7 @@ def _select_raw(ds: Dataset, raw_features, dev) -> Dataset:
             raise KeyError(f"raw feature '{f.name}' (column '{name}') not in input dataset")
         c = ds[name]
         cols[f.name] = c if c.device == torch.device(dev) or c.device.type == "cpu" and dev.type == "cpu" else c.to(dev)
-    return Dataset(cols, ds.key, ds.n_rows, ds._row_ids)
+    return ds._like(Dataset(cols, ds.key, ds.n_rows, ds._row_ids))
 
 
 def dataset_from_frame(df, raw_features, dev, key_fn=None) -> Dataset:

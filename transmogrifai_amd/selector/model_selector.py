@@ -42,10 +42,14 @@ class SelectedModel(OpPredictorModel):
         self.evaluators = []
 
     def evaluate_model(self, ds) -> Dict:
-        """Hold-out evaluation (``HasTestEval.evaluateModel``): fills ``holdoutEvaluation``."""
+        """Hold-out evaluation (``HasTestEval.evaluateModel``): fills ``holdoutEvaluation``. A row-sharded
+        hold-out is scored locally and the (label, prediction) rows are all-gathered for the metrics
+        (SURVEY.md §2.7 C12)."""
+        from ..parallel import dp
         lab = ds[self._inputs[0].name].values.to(torch.float64)
         vec = ds[self._inputs[1].name].values
         pred, raw, prob = self.learner.predict(self.state, vec)
+        lab, pred, raw, prob = dp.rows_opt(lab, pred, raw, prob)
         res = {}
         for ev in self.evaluators:
             res.update(ev.evaluate_arrays(lab, pred, raw, prob))
@@ -71,14 +75,42 @@ class ModelSelector(BinaryEstimator):
         self.evaluators = list(evaluators)
         self.best: Optional[Any] = None
 
+    # Row-sharded fits: the splitter's global statistics come from one label gather, then every rank
+    # contributes the rows that any CV fold or the refit samples (masks are functions of the global
+    # row id) and the (learner x grid x fold) jobs are sharded over the ranks on that replicated
+    # sample (tuning/validators.py) -- the reference's maxTrainingSample cap keeps it small.
+    dp_aware = True
+
     def fit_columns(self, label_col, vec_col, ds=None):
+        from ..parallel import dp
         X = vec_col.values
         y = label_col.values.to(X.dtype)
         row_ids = ds.row_ids.to(X.device) if ds is not None else torch.arange(X.shape[0], device=X.device)
         t0 = time.time()
         split_summary = None
         if self.splitter is not None:
-            split_summary = self.splitter.pre_validation_prepare(y)
+            split_summary = self.splitter.pre_validation_prepare(dp.rows(y))
+        if dp.active():
+            X, y, row_ids = self._gather_candidates(X, y, row_ids)
+            with dp.local_only():
+                return self._fit(X, y, row_ids, split_summary, t0)
+        return self._fit(X, y, row_ids, split_summary, t0)
+
+    def _gather_candidates(self, X, y, row_ids):
+        """Every rank's rows that some CV fold or the refit may train on, gathered to all ranks."""
+        from ..parallel import dp
+        if self.splitter is None:
+            keep = torch.ones(row_ids.shape[0], dtype=torch.bool, device=row_ids.device)
+        else:
+            n_folds = getattr(self.validator, "num_folds", 1)
+            keep = self.splitter.validation_prepare(row_ids, y, stream=5)
+            for k in range(n_folds):
+                keep |= self.splitter.validation_prepare(row_ids, y, stream=11 + k)
+        idx = torch.nonzero(keep).reshape(-1)
+        return dp.rows(X.index_select(0, idx).contiguous()), dp.rows(y.index_select(0, idx)), \
+            dp.rows(row_ids.index_select(0, idx))
+
+    def _fit(self, X, y, row_ids, split_summary, t0):
         ctx: Dict[str, Any] = {}
         res = self.validator.validate(self.models, X, y, row_ids, self.splitter, context=ctx)
         self.best = res

@@ -227,11 +227,20 @@ class OpEstimator(OpPipelineStage):
 
     is_estimator = True
     model_class: type = None
+    # True when fit_columns reduces its own statistics over the ranks of a row-sharded fit
+    # (parallel/dp.py); other estimators see their inputs gathered from every rank
+    dp_aware = False
 
     def fit_columns(self, *cols: Column, ds: Optional[Dataset] = None) -> OpTransformer:
         raise NotImplementedError(type(self).__name__)
 
     def fit(self, ds: Dataset) -> OpTransformer:
+        from ..parallel import dp
+        if dp.active() and not self.dp_aware:
+            ds = dp.gather_dataset(ds, dict.fromkeys(f.name for f in self._inputs))
+            with dp.local_only():
+                model = self.fit_columns(*[ds[f.name] for f in self._inputs], ds=ds)
+            return self._finish_model(model)
         cols = [ds[f.name] for f in self._inputs]
         model = self.fit_columns(*cols, ds=ds)
         return self._finish_model(model)

@@ -92,6 +92,7 @@ class RealVectorizer(VectorizerMixin, SequenceEstimator):
     """Fill missing reals with the column mean (or a constant) plus a null indicator."""
     operation_name = "vecReal"
     _defaults = {"fill_value": 0.0, "fill_with_constant": True, "track_nulls": True}
+    dp_aware = True     # means / modes reduce over the ranks (ops/vector.py)
 
     def set_fill_with_mean(self):
         return self.set("fill_with_constant", False)
@@ -279,12 +280,15 @@ class OpTextPivotVectorizer(VectorizerMixin, SequenceEstimator):
         return _text_counts(c, self.params["clean_text"]) if isinstance(c, TextColumn) else \
             _set_counts(c, self.params["clean_text"])
 
+    dp_aware = True
+
     def fit_columns(self, *cols, ds=None):
+        from ...parallel import dp
         p = self.params
         tops = []
-        n = len(cols[0]) if cols else 0
-        for c in cols:
-            counts = self._counts(c)
+        n = dp.count(len(cols[0]) if cols else 0)
+        # per-rank value counts folded over the process group (OpOneHotVectorizer.scala:97)
+        for counts in dp.merge_counters([self._counts(c) for c in cols]):
             if p["max_pct_cardinality"] < 1.0 and n > 0 and len(counts) / n >= p["max_pct_cardinality"]:
                 counts = Counter()
             tops.append(top_values(counts, p["top_k"], p["min_support"]))
@@ -731,6 +735,7 @@ class VectorsCombinerModel(VectorizerMixin, SequenceTransformer):
 class VectorsCombiner(VectorizerMixin, SequenceEstimator):
     """Concatenate vectors and merge their column metadata (``VectorsCombiner.scala:51-89``)."""
     operation_name = "combVec"
+    dp_aware = True     # metadata only: nothing to reduce
 
     def fit_columns(self, *cols, ds=None):
         metas = []

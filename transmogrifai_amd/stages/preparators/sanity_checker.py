@@ -144,11 +144,16 @@ class SanityChecker(BinaryEstimator):
         mx = max(0.0, p["sample_upper_limit"] / max(total, 1))
         return max(min(p["check_sample"], mx), mn)
 
+    # row-sharded fits reduce every statistic over the ranks (ops/stats.py: colStats, Gramian,
+    # label contingency; sampling is by global row id, so the sample equals the single-process one)
+    dp_aware = True
+
     def fit_columns(self, label_col, vec_col, ds=None):
+        from ...parallel import dp
         p = self.params
         X = vec_col.values
         y = label_col.values
-        n_all = X.shape[0]
+        n_all = dp.count(X.shape[0])
         frac = self.fraction(n_all)
         if frac < 1.0:
             rid = ds.row_ids.to(X.device) if ds is not None else torch.arange(n_all, device=X.device)
@@ -176,25 +181,29 @@ class SanityChecker(BinaryEstimator):
         if p["feature_feature_corr_level"] == "Off":
             C = None
             Z = Xy.index_select(1, ci)
-            m = Z.to(torch.float64).mean(0)
+            m = cs["mean"].index_select(0, ci.to(cs["mean"].device)).to(Z.device)
             Zc = Z.to(torch.float64) - m
-            cov = (Zc * Zc[:, -1:]).sum(0) / max(count - 1, 1)
-            sd = Zc.pow(2).sum(0).div(max(count - 1, 1)).sqrt()
+            cov, ss = dp.sum_([(Zc * Zc[:, -1:]).sum(0), Zc.pow(2).sum(0)])
+            cov = cov / max(count - 1, 1)
+            sd = ss.div(max(count - 1, 1)).sqrt()
             corr_label = (cov / (sd * sd[-1])).cpu().numpy()
         else:
-            C = ST.corr_matrix(Xy.index_select(1, ci), p["correlation_type"]).cpu().numpy()
+            C = ST.corr_matrix(Xy.index_select(1, ci), p["correlation_type"],
+                               mean=None if p["correlation_type"] == "spearman" else
+                               cs["mean"].index_select(0, ci.to(cs["mean"].device)).to(Xy.device)).cpu().numpy()
             corr_label = C[:, -1]
         # categorical tests
-        labels_u = torch.unique(y)
+        labels_u = dp.unique_values(y)
         cat_label = p["categorical_label"]
         cat_stats = []
         if cat_label is not False and (cat_label is True or labels_u.numel() < min(100.0, count * 0.1)):
             cat_stats = self._categorical_tests(X, y, cols)
         label_dist = None
         if labels_u.numel() <= 100:
-            lu, lc = torch.unique(y, return_counts=True)
+            lu = labels_u
+            lc, = dp.sum_([(y[:, None] == lu[None, :]).sum(0).to(torch.float64)])
             label_dist = {"domain": [_label_str(v) for v in lu.cpu().tolist()],
-                          "prob": (lc.to(torch.float64) / max(int(lc.sum()), 1)).cpu().tolist()}
+                          "prob": (lc / max(float(lc.sum()), 1.0)).cpu().tolist()}
             for s in cat_stats:
                 s["labels"] = label_dist["domain"]
         stats = self._column_statistics(cols, cs, label_col, d, corr_label, corr_idx, cat_stats, C)

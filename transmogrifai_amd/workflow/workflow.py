@@ -228,6 +228,13 @@ class OpWorkflow(OpWorkflowCore):
         return data.take(ti), data.take(hi)
 
     def fit_stages(self, data: Dataset, timings: Dict[str, float]) -> List[OpPipelineStage]:
+        from ..parallel import dp
+        # a row-sharded input (Dataset.shard, one shard per rank) fits data-parallel: every estimator
+        # reduces its statistics over the process group (parallel/dp.py)
+        with dp.scope(getattr(data, "sharded", False)):
+            return self._fit_stages(data, timings)
+
+    def _fit_stages(self, data: Dataset, timings: Dict[str, float]) -> List[OpPipelineStage]:
         with _Timer(timings, "HoldoutSplit"):
             train, test = self._holdout_split(data)
         dag = [[(st, d) for st, d in layer if st in self.stages] for layer in compute_dag(self.result_features)]
