@@ -10,6 +10,6 @@ tail -15 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
 tail -5 gpurun_out/smoke.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 ${BENCH_T:-400} python bench.py --rows ${ROWS:-1000000} --warmup 0 --steps 1 --verbose > gpurun_out/bench.log 2>&1; rc=$?
+timeout -k 10 ${BENCH_T:-400} python bench.py --rows ${ROWS:-1000000} --warmup ${WARMUP:-1} --steps 1 --verbose > gpurun_out/bench.log 2>&1; rc=$?
 tail -5 gpurun_out/bench.log
 exit $rc

@@ -85,3 +85,36 @@ def test_onehot_pivot_kernel_matches_host():
     V.onehot_pivot(out, [c.cuda() for c in codes], luts, offs)
     torch.testing.assert_close(out.cpu(), ref)
     assert float(ref.sum()) > 0
+
+
+def test_xgb_fused_round_epilogue_matches_torch_path(monkeypatch):
+    """The fused boosting-round kernel (margins, gradients, AuPR counts) against the torch reference."""
+    from transmogrifai_amd.models.base import FitJob
+    from transmogrifai_amd.models.trees import XGBoostClassifierLearner
+    g = torch.Generator().manual_seed(3)
+    n, d = 20_000, 12
+    X = torch.randn(n, d, generator=g)
+    X[:, :3] = (X[:, :3] > 0.8).float()               # sparse 0/1 columns exercise the missing bin
+    y = ((X[:, 3] + X[:, 0] - 0.5 * X[:, 5] + 0.3 * torch.randn(n, generator=g)) > 0).float()
+    Xd, yd = X.cuda(), y.cuda()
+    params = dict(XGBoostClassifierLearner.defaults, num_round=15, max_depth=4, eta=0.3, missing=0.0,
+                  num_early_stopping_rounds=5)
+    rows = torch.arange(0, n, 2, device="cuda")
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TMOG_XGB_FUSED", flag)
+        st = XGBoostClassifierLearner().fit_batch(Xd, yd, [FitJob(params, rows)])[0]
+        outs.append(XGBoostClassifierLearner().predict(st, Xd)[2][:, 1].cpu())
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-5)
+    assert _native_loaded()
+
+
+def test_row_uniform_kernel_bit_identical():
+    from transmogrifai_amd.tuning import splitters as SP
+    rid = torch.randint(0, 1 << 40, (100_003,), dtype=torch.int64)
+    ref = SP.row_uniform(rid, 1234, 7)
+    got = SP.row_uniform(rid.cuda(), 1234, 7).cpu()
+    assert torch.equal(ref, got)
+    refm = SP.row_uniform_multi(rid, [1, 2, 3], 23)
+    gotm = SP.row_uniform_multi(rid.cuda(), [1, 2, 3], 23).cpu()
+    assert torch.equal(refm, gotm)

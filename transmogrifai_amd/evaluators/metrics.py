@@ -111,7 +111,16 @@ def binned_aupr_multi(scores: Sequence[torch.Tensor], labels: Sequence[torch.Ten
     y = torch.cat([x.reshape(-1) for x in labels]).to(dev) > 0.5
     b = (s * (bins - 1)).to(torch.int64)
     idx = (sid * 2 + y.to(torch.int64)) * bins + (bins - 1 - b)        # descending score order
-    h = torch.bincount(idx, minlength=K * 2 * bins).to(torch.float64).view(K, 2, bins)
+    h = torch.bincount(idx, minlength=K * 2 * bins).view(K, 2, bins)
+    return binned_aupr_from_counts(h)
+
+
+def binned_aupr_from_counts(h: torch.Tensor) -> torch.Tensor:
+    """AuPR of ``K`` score sets from their ``[K, 2 (label), bins]`` count tables, bins in descending
+    score order (as filled by :func:`binned_aupr_multi` or the fused boosting-round kernel)."""
+    K = h.shape[0]
+    dev = h.device
+    h = h.to(torch.float64)
     neg, pos = h[:, 0], h[:, 1]
     tp, fp = torch.cumsum(pos, 1), torch.cumsum(neg, 1)
     P = tp[:, -1:]

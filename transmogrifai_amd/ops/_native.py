@@ -53,11 +53,10 @@ _HOST_SIGS = {
 }
 
 _HIP_SIGS = {
-    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, P],
+    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P],
     "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
-    "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P],
-    "tmog_hip_partition_count": [P, I32, P, P, I32, P, P, P, I32, P, P],
-    "tmog_hip_partition_scatter": [P, I32, P, P, P, I32, P, P, P, I32, P],
+    "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P, P],
+    "tmog_hip_partition_fused": [P, I32, P, P, P, I32, P, P, P, P, P, P, P, I32, P, P],
     "tmog_hip_leaf_collect": [P, P, I32, P, P, P],
     "tmog_hip_grow_forest": [P],
     "tmog_hip_grow_status": [P, P, I32],
@@ -66,6 +65,8 @@ _HIP_SIGS = {
     "tmog_hip_grow_copy": [P, I32, P, P, P, P, P, P, P, P],
     "tmog_hip_grow_free": [P],
     "tmog_hip_zero_segments": [P, P, P, I32, I64, P],
+    "tmog_hip_boost_epilogue": [P, P, I64, P, P, P, I64, P, P, P, P, I32, P, I32, P],
+    "tmog_hip_row_uniform": [P, I64, P, I32, P, P],
     "tmog_hip_lr_objective": [P, I64, I32, P, P, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P],
     "tmog_hip_forest_predict": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P],
     "tmog_hip_col_stats": [P, P, I64, I32, I64, P, P],

@@ -342,6 +342,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     const size_t o_dp = st1.add(d_poff), o_ds = st1.add(d_soff), o_do = st1.add(d_ooff), o_dz = st1.add(d_size);
     const size_t o_bnb = st1.add(b_nb), o_bnc = st1.add(b_nc), o_bnfo = st1.add(b_nfo), o_bnnf = st1.add(b_nnf);
     const size_t o_bnmd = st1.add(b_nmd), o_bnho = st1.add(b_nho);
+    const size_t o_nb = st1.add(nb), o_nc = st1.add(nc);
     const uint8_t* d1 = bk.ship(st1, 0);
 #define TM_P(T_, off) ((T_*)(d1 + (off)))
     const int32_t* flist = use_subset ? TM_P(const int32_t, o_fl) : all_feats;
@@ -355,20 +356,22 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     if (!d_big.empty())
       bk.hist_subtract(hist, prev_hist, TM_P(const int64_t, o_dp), TM_P(const int64_t, o_ds),
                        TM_P(const int64_t, o_do), TM_P(const int64_t, o_dz), (int)d_big.size(), d_max);
-    // ---- split scan + partition count -> one result block
+    // ---- split scan + (GPU) one-pass partition -> one result block: decisions + per-node slot cursors
     const int64_t ncit = (int64_t)citems.size();
-    const size_t r_cl = 0, r_feat = r_cl + 8 * ncit, r_bin = r_feat + 4 * (size_t)m, r_gain = r_bin + 4 * (size_t)m;
+    const size_t r_cl = 0, r_feat = r_cl + 16 * (size_t)m, r_bin = r_feat + 4 * (size_t)m, r_gain = r_bin + 4 * (size_t)m;
     const size_t r_left = r_gain + 4 * (size_t)m, r_tot = r_left + 4 * (size_t)m * S, r_dl = r_tot + 4 * (size_t)m * S;
     const size_t r_bytes = r_dl + (size_t)m;
     uint8_t* res = bk.result_buffer(r_bytes);
     bk.split_find(a, hist, m, TM_P(const int64_t, o_nho), TM_P(const int32_t, o_nnf), TM_P(const int32_t, o_nfo),
                   flist, TM_P(const float, o_par), TM_P(const int32_t, o_nmd), max_nf, (int32_t*)(res + r_feat),
                   (int32_t*)(res + r_bin), (float*)(res + r_gain), res + r_dl, (float*)(res + r_left),
-                  (float*)(res + r_tot));
-    bk.partition_count(a, rows, d1 + o_cit, (int)ncit, (const int32_t*)(res + r_feat),
-                       (const int32_t*)(res + r_bin), res + r_dl, (int64_t*)(res + r_cl));
+                  (float*)(res + r_tot), (int64_t*)(res + r_cl));
+    if (BK::kGPU)   // partition in place of the node ranges, straight from the device decisions
+      bk.partition_fused(a, rows, rows_alt, d1 + o_cit, (int)ncit, TM_P(const int64_t, o_nb),
+                         TM_P(const int64_t, o_nc), (const int32_t*)(res + r_feat), (const int32_t*)(res + r_bin),
+                         res + r_dl, TM_P(const float, o_par), (const float*)(res + r_gain), (int64_t*)(res + r_cl));
     const uint8_t* h = bk.fetch(res, r_bytes);
-    const int64_t* h_cl = (const int64_t*)(h + r_cl);
+    const int64_t* h_cur = (const int64_t*)(h + r_cl);   // GPU: [left, right] entries per node
     const int32_t* h_feat = (const int32_t*)(h + r_feat);
     const int32_t* h_bin = (const int32_t*)(h + r_bin);
     const float* h_gain = (const float*)(h + r_gain);
@@ -403,32 +406,9 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
       counts_sl[q] = nc[j];
       out_begin[q] = q ? out_begin[q - 1] + counts_sl[q - 1] : 0;
     }
-    // ---- stable partition of the splitting nodes' entries
+    // ---- partition of the splitting nodes' entries
     if (BK::kGPU) {
-      std::vector<int64_t> pos(m, -1);
-      for (int64_t q = 0; q < ns; ++q) pos[sl[q]] = q;
-      std::vector<PartItemH> sitems;
-      std::vector<int64_t> run_l(ns, 0), run_r(ns, 0);
-      for (int64_t c = 0; c < ncit; ++c) {
-        const int64_t q = pos[citems[c].node];
-        if (q >= 0) nl[q] += h_cl[c];
-      }
-      for (int64_t c = 0; c < ncit; ++c) {
-        const int64_t q = pos[citems[c].node];
-        if (q < 0) continue;
-        PartItemH it = citems[c];
-        const int64_t cl = h_cl[c], cr = it.count - cl;
-        it.out_left = out_begin[q] + run_l[q];
-        it.out_right = out_begin[q] + nl[q] + run_r[q];
-        run_l[q] += cl;
-        run_r[q] += cr;
-        sitems.push_back(it);
-      }
-      st2.clear();
-      const size_t o_s = st2.add(sitems);
-      const uint8_t* d2 = bk.ship(st2, 1);
-      bk.partition_scatter(a, rows, rows_alt, d2 + o_s, (int)sitems.size(), (const int32_t*)(res + r_feat),
-                           (const int32_t*)(res + r_bin), res + r_dl);
+      for (int64_t q = 0; q < ns; ++q) nl[q] = h_cur[2 * sl[q]];
     } else {
       std::vector<int64_t> s_nb(ns), s_nc(ns);
       std::vector<int32_t> s_f(ns), s_b(ns);
@@ -461,8 +441,9 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
         R.tot[(size_t)gl * S + s] = lt;
         R.tot[(size_t)gr * S + s] = tt - lt;
       }
-      new_begin[2 * q] = out_begin[q];
-      new_begin[2 * q + 1] = out_begin[q] + nl[q];
+      const int64_t b0 = BK::kGPU ? nb[j] : out_begin[q];   // GPU children stay inside the parent's range
+      new_begin[2 * q] = b0;
+      new_begin[2 * q + 1] = b0 + nl[q];
       new_count[2 * q] = nl[q];
       new_count[2 * q + 1] = counts_sl[q] - nl[q];
       pair_parent_off[q] = hoff[j];

@@ -1,0 +1,91 @@
+// Boosting-round epilogue and counter-based row sampling for CDNA4 (gfx950).
+//
+// boost_epilogue_kernel -- one launch per boosting round replaces the ~60 small torch ops that
+// followed every XGBoost / GBT round (OpXGBoostClassifier.scala:47-403 drives 200 of them per config):
+// for every training entry of the round's trees (the leaf assignment the tree grower returns) it
+//   1. adds the entry's leaf value to the job's margin   F[p, r] += value[gid]          (fp64)
+//   2. writes next round's gradient / hessian            G[p, r], H[p, r]             (fp32)
+//      (binary:logistic: p = sigmoid(F), g = p - y, h = max(p (1 - p), 1e-16); squared error: g = F - y, h = 1)
+//   3. bins the new training score into the job's (label, score-bin) count table, from which the
+//      early-stopping AuPR on the training rows (eval_metric aucpr) is a cumulative sum.
+// Every (job, row) pair occurs exactly once among a round's entries, so the margin / gradient
+// stores need no atomics; the AuPR table uses integer atomics (exact, order-independent).
+//
+// row_uniform_kernel -- the splitmix64 per-(seed, stream, global row id) uniform of
+// tuning/splitters.row_uniform (hold-out split, CV folds, down-sampling, bootstrap, sanity-check
+// sample) as one fused pass instead of ~12 int64 elementwise torch kernels; bit-identical results.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+namespace {
+
+__global__ void __launch_bounds__(256) boost_epilogue_kernel(
+    const uint32_t* __restrict__ entries, const int32_t* __restrict__ gid, int64_t n_entries,
+    const float* __restrict__ gid_value, const int64_t* __restrict__ gid_tree, const int64_t* __restrict__ tree_job,
+    int64_t N, double* __restrict__ F, float* __restrict__ G, float* __restrict__ H, const float* __restrict__ y,
+    int objective, int32_t* __restrict__ auc_hist, int bins) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_entries) return;
+  const int64_t r = entries[e] & 0xFFFFFFu;
+  const int32_t g_id = gid[e];
+  const int64_t p = tree_job[gid_tree[g_id]];
+  const int64_t k = p * N + r;
+  const double m = F[k] + (double)gid_value[g_id];
+  F[k] = m;
+  const float yr = y[r];
+  if (objective == 0) {
+    const double pr = 1.0 / (1.0 + exp(-m));
+    G[k] = (float)(pr - (double)yr);
+    H[k] = (float)fmax(pr * (1.0 - pr), 1e-16);
+    if (auc_hist) {
+      const float s = fminf(fmaxf((float)pr, 0.f), 1.f);
+      const int b = (int)(s * (float)(bins - 1));
+      atomicAdd(auc_hist + (p * 2 + (yr > 0.5f ? 1 : 0)) * bins + (bins - 1 - b), 1);
+    }
+  } else {
+    G[k] = (float)(m - (double)yr);
+    H[k] = 1.f;
+  }
+}
+
+__global__ void __launch_bounds__(256) row_uniform_kernel(const int64_t* __restrict__ row_ids, int64_t n,
+                                                          const int64_t* __restrict__ offsets, int k_seeds,
+                                                          double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t M63 = 0x7FFFFFFFFFFFFFFFull;
+  const uint64_t rid = (uint64_t)row_ids[i];
+  for (int s = 0; s < k_seeds; ++s) {
+    uint64_t x = rid * 0x1E3779B97F4A7C15ull + (uint64_t)offsets[s];
+    x &= M63;
+    x = ((x ^ (x >> 30)) * 0x2F58476D1CE4E5B9ull) & M63;
+    x = ((x ^ (x >> 27)) * 0x14C3124B4B69A5C5ull) & M63;
+    x = x ^ (x >> 31);
+    out[(int64_t)s * n + i] = (double)(x >> 10) / 9007199254740992.0;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int tmog_hip_boost_epilogue(const uint32_t* entries, const int32_t* gid, int64_t n_entries, const float* gid_value,
+                            const int64_t* gid_tree, const int64_t* tree_job, int64_t N, double* F, float* G, float* H,
+                            const float* y, int objective, int32_t* auc_hist, int bins, hipStream_t stream) {
+  if (n_entries == 0) return 0;
+  if (N >= (1 << 24)) return -2;
+  hipLaunchKernelGGL(boost_epilogue_kernel, dim3((unsigned)((n_entries + 255) / 256)), dim3(256), 0, stream, entries,
+                     gid, n_entries, gid_value, gid_tree, tree_job, N, F, G, H, y, objective, auc_hist, bins);
+  return (int)hipGetLastError();
+}
+
+int tmog_hip_row_uniform(const int64_t* row_ids, int64_t n, const int64_t* offsets, int k_seeds, double* out,
+                         hipStream_t stream) {
+  if (n == 0 || k_seeds == 0) return 0;
+  hipLaunchKernelGGL(row_uniform_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, row_ids, n, offsets,
+                     k_seeds, out);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -15,23 +15,23 @@ extern "C" {
 int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
-                        const float* t1, const float* t2, int64_t stride, const float* qscale, hipStream_t stream);
+                        const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
+                        hipStream_t stream);
 int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
                            const int64_t* out_off, const int64_t* size, int n, int64_t max_size, hipStream_t stream);
 int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
                         const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
-                        float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, hipStream_t stream);
+                        float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors,
+                        hipStream_t stream);
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
                            hipStream_t stream);
 size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat);
-int tmog_hip_partition_count(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
-                             const int32_t* split_feat, const int32_t* split_bin, const uint8_t* dl, int missing_bin,
-                             int64_t* chunk_left, hipStream_t stream);
-int tmog_hip_partition_scatter(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out,
-                               const void* items, int n_items, const int32_t* split_feat, const int32_t* split_bin,
-                               const uint8_t* dl, int missing_bin, hipStream_t stream);
+int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, const void* items,
+                             int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
+                             const int32_t* split_bin, const uint8_t* dl, const float* node_params,
+                             const float* split_gain, int missing_bin, int64_t* cursors, hipStream_t stream);
 int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
                           int32_t* out_gid, hipStream_t stream);
 }
@@ -137,7 +137,7 @@ struct GpuBackend {
                   const int64_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*) {
     if (n_items)
       kchk(tmog_hip_hist_build(g.Xb, g.F, rows, items, n_items, nfo, flist, nmd, nho, hist, g.B, g.mode, g.S, g.y,
-                               g.t1, g.t2, g.stride, g.qscale, sl.stream),
+                               g.t1, g.t2, g.stride, g.qscale, g.mode == 2 ? g.missing_bin : -1, sl.stream),
            "hist_build");
   }
   void hist_subtract(int64_t* hist, const int64_t* prev, const int64_t* poff, const int64_t* soff,
@@ -146,21 +146,18 @@ struct GpuBackend {
   }
   void split_find(const tmog::GrowArgs& g, const int64_t* hist, int m, const int64_t* nho, const int32_t* nnf,
                   const int32_t* nfo, const int32_t* flist, const float* params, const int32_t* nmd, int max_nf,
-                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot) {
+                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t* cursors) {
     grow_dev(sl.cand, sl.cand_cap, tmog_hip_split_cand_bytes(m, max_nf), sl.stream);
     kchk(tmog_hip_split_find(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd,
-                             g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, sl.stream),
+                             g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, cursors, sl.stream),
          "split_find");
   }
-  void partition_count(const tmog::GrowArgs& g, const uint32_t* rows, const void* items, int n, const int32_t* feat,
-                       const int32_t* bin, const uint8_t* dl, int64_t* chunk_left) {
-    kchk(tmog_hip_partition_count(g.Xb, g.F, rows, items, n, feat, bin, dl, g.missing_bin, chunk_left, sl.stream),
-         "partition_count");
-  }
-  void partition_scatter(const tmog::GrowArgs& g, const uint32_t* rows, uint32_t* rows_alt, const void* items, int n,
-                         const int32_t* feat, const int32_t* bin, const uint8_t* dl) {
-    kchk(tmog_hip_partition_scatter(g.Xb, g.F, rows, rows_alt, items, n, feat, bin, dl, g.missing_bin, sl.stream),
-         "partition_scatter");
+  void partition_fused(const tmog::GrowArgs& g, const uint32_t* rows, uint32_t* rows_alt, const void* items, int n,
+                       const int64_t* nb, const int64_t* nc, const int32_t* feat, const int32_t* bin, const uint8_t* dl,
+                       const float* params, const float* gain, int64_t* cursors) {
+    kchk(tmog_hip_partition_fused(g.Xb, g.F, rows, rows_alt, items, n, nb, nc, feat, bin, dl, params, gain,
+                                  g.missing_bin, cursors, sl.stream),
+         "partition_fused");
   }
   void partition_nodes(const tmog::GrowArgs&, const uint32_t*, uint32_t*, int, const int64_t*, const int64_t*,
                        const int32_t*, const int32_t*, const uint8_t*, const int64_t*, int64_t*) {

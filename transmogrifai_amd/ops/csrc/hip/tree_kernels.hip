@@ -90,13 +90,21 @@ __device__ __forceinline__ void add_row(int* my, int bin, int S, const int4& st)
 //  2. the 64 records are staged in a wave-private LDS slot (one ds_write_b128 per lane);
 //  3. lane (rsub, fidx) walks the staged rows R at a time, 8 rows unrolled: 8 broadcast ds_read_b128,
 //     8 independent bin gathers Xb[row*F + feat] in flight, then the ds_add_u32s.
+//
+// Sparse missing bin (MODE 2, skip_bin >= 0; XGBoost's sparsity-aware histogram): entries whose bin is
+// the reserved missing bin (XGBoost ``missing`` = 0.0 in the reference grid, i.e. every zero of the
+// one-hot / null-indicator columns) issue no LDS atomic. Each wave instead folds its 64 staged rows'
+// (g, h) into the chunk total with two wave reductions, and before the write-out the missing bin of
+// every feature is recovered exactly as chunk total - sum of the other bins (integer arithmetic, so
+// the histogram stays bit-identical to the CPU twin). On the headline table this drops about half of
+// all ds_add_u32 (the kernel is LDS-atomic-throughput bound: benchmarks/lds_atomic_bench.hip).
 template <int MODE>
 __global__ void __launch_bounds__(256) hist_build_kernel(
     const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const HistItem* __restrict__ items,
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
     int B, int S, const float* __restrict__ y, const float* __restrict__ t1, const float* __restrict__ t2,
-    int64_t stride, const float* __restrict__ qscale) {
+    int64_t stride, const float* __restrict__ qscale, int skip_bin) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
   const HistItem it = items[blockIdx.x];
   const int FG = it.nf;
@@ -107,7 +115,10 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   const int wave = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
   int4* stage = reinterpret_cast<int4*>(lds + ((ncopy_words + 3) & ~3)) + wave * 64;
+  int* tot = lds + ((ncopy_words + 3) & ~3) + 4 * 64 * 4;     // chunk totals (sparse missing bin)
+  const bool sparse = MODE == 2 && skip_bin >= 0;
   for (int i = threadIdx.x; i < ncopy_words; i += blockDim.x) lds[i] = 0;
+  if (threadIdx.x < TM_MAX_S) tot[threadIdx.x] = 0;
   __syncthreads();
 
   const int rsub = lane / FG;
@@ -125,7 +136,20 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   for (int64_t base = (int64_t)wave * 64; base < cnt; base += (int64_t)nwaves * 64) {
     const int64_t ri = min(base + lane, cnt - 1);
     const int nrows = (int)min((int64_t)64, cnt - base);
-    stage[lane] = stage_row<MODE>(rp[ri], model, stride, y, t1, t2, qs);
+    const int4 mine = stage_row<MODE>(rp[ri], model, stride, y, t1, t2, qs);
+    stage[lane] = mine;
+    if (sparse) {
+      // chunk totals: one wave reduction of the 64 staged (g, h) records, one LDS add per wave
+      int a = lane < nrows ? mine.y : 0, b = lane < nrows ? mine.z : 0;
+      for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off, 64);
+        b += __shfl_xor(b, off, 64);
+      }
+      if (lane == 0) {
+        atomicAdd(tot, a);
+        atomicAdd(tot + 1, b);
+      }
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0): staged records visible to the wave
     __builtin_amdgcn_wave_barrier();
     for (int j0 = 0; j0 < nrows; j0 += R * 8) {
@@ -137,15 +161,43 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
       for (int u = 0; u < 8; ++u) bin[u] = (int)Xb[(int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F + feat];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (active && j0 + u * R + rsub < nrows) add_row<MODE>(my, bin[u], S, st[u]);
+        if (active && j0 + u * R + rsub < nrows && bin[u] != skip_bin) add_row<MODE>(my, bin[u], S, st[u]);
     }
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
 
-  // fold the R private copies and write the node histogram of this feature group
   int64_t* out = hist + node_hist_off[it.node] + (int64_t)it.fg0 * B * S;
   const int words = FG * B * S;
+  if (sparse) {
+    // fold the R copies into copy 0, then recover each feature's missing bin from the chunk totals
+    if (R > 1) {
+      for (int k = threadIdx.x; k < words; k += blockDim.x) {
+        const int f = k / (B * S);
+        const int rem = k - f * (B * S);
+        int acc = 0;
+        for (int r = 0; r < R; ++r) acc += lds[(r * FG + f) * rowstride + rem];
+        lds[f * rowstride + rem] = acc;
+      }
+      __syncthreads();
+    }
+    for (int t = threadIdx.x; t < FG * S; t += blockDim.x) {
+      const int f = t / S, s = t - (t / S) * S;
+      int* row = lds + f * rowstride;
+      int sum = 0;
+      for (int b = 0; b < B; ++b) sum += (b == skip_bin) ? 0 : row[b * S + s];
+      row[skip_bin * S + s] = tot[s] - sum;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < words; k += blockDim.x) {
+      const int f = k / (B * S);
+      const int64_t acc = lds[f * rowstride + (k - f * (B * S))];
+      if (it.excl) out[k] = acc;
+      else if (acc != 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + k), (unsigned long long)acc);
+    }
+    return;
+  }
+  // fold the R private copies and write the node histogram of this feature group
   for (int k = threadIdx.x; k < words; k += blockDim.x) {
     const int f = k / (B * S);
     const int rem = k - f * (B * S);
@@ -335,9 +387,10 @@ __global__ void __launch_bounds__(64) split_reduce_kernel(
     const int32_t* __restrict__ feat_list, int B, int S, int missing_bin, const int32_t* __restrict__ node_model,
     const double* __restrict__ qinv, int fbmax, const Best* __restrict__ cand, int32_t* __restrict__ out_feat,
     int32_t* __restrict__ out_bin, float* __restrict__ out_gain, uint8_t* __restrict__ out_dl,
-    float* __restrict__ out_left, float* __restrict__ out_total) {
+    float* __restrict__ out_left, float* __restrict__ out_total, unsigned long long* __restrict__ cursors) {
   const int j = blockIdx.x;
   const int lane = threadIdx.x;
+  if (cursors && lane < 2) cursors[2 * j + lane] = 0;   // partition_fused_kernel's per-node slot cursors
   Best b{-INFINITY, 0x7fffffff, 0, 0};
   if (lane < fbmax) b = cand[(int64_t)j * fbmax + lane];
   for (int off = 32; off > 0; off >>= 1) {
@@ -390,41 +443,29 @@ __device__ __forceinline__ bool goes_left(uint8_t bin, int sb, bool dl, int miss
   return (missing_bin >= 0 && bin == missing_bin) ? dl : ((int)bin <= sb);
 }
 
-__global__ void __launch_bounds__(256) partition_count_kernel(
-    const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const PartItem* __restrict__ items,
-    const int32_t* __restrict__ split_feat, const int32_t* __restrict__ split_bin, const uint8_t* __restrict__ dl,
-    int missing_bin, int64_t* __restrict__ chunk_left) {
-  const PartItem it = items[blockIdx.x];
-  const int f = split_feat[it.node], sb = split_bin[it.node];
-  const bool d = dl[it.node] != 0;
-  if (f < 0) {
-    if (threadIdx.x == 0) chunk_left[blockIdx.x] = 0;
-    return;
-  }
-  int c = 0;
-  for (int64_t i = threadIdx.x; i < it.count; i += blockDim.x) {
-    const uint32_t e = rows[it.begin + i];
-    c += goes_left(Xb[(int64_t)(e & 0xFFFFFFu) * F + f], sb, d, missing_bin);
-  }
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-  __shared__ int s[4];
-  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) chunk_left[blockIdx.x] = (int64_t)s[0] + s[1] + s[2] + s[3];
-}
-
-// stable scatter: block-wide exclusive scan of the left flags, 256 rows per step
-__global__ void __launch_bounds__(256) partition_scatter_kernel(
+// One-pass partition (replaces count + scatter): every chunk of every node reads its split decision
+// straight from split_find's device output (no host round trip before the partition), and each
+// 256-row step reserves its left / right output slots with two atomics on the node's cursors: left
+// entries fill the node's own range [begin, begin + nl) upward, right entries fill it downward from
+// the end. The order inside a child is not stable, which changes nothing downstream: histograms are
+// exact integer sums (order-independent) and leaf assignments are keyed by row id. Nodes that do not
+// split (feat < 0) are skipped; their ranges are collected as leaves from the input buffer.
+__global__ void __launch_bounds__(256) partition_fused_kernel(
     const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows_in, uint32_t* __restrict__ rows_out,
-    const PartItem* __restrict__ items, const int32_t* __restrict__ split_feat, const int32_t* __restrict__ split_bin,
-    const uint8_t* __restrict__ dl, int missing_bin) {
+    const PartItem* __restrict__ items, const int64_t* __restrict__ node_begin, const int64_t* __restrict__ node_count,
+    const int32_t* __restrict__ split_feat, const int32_t* __restrict__ split_bin, const uint8_t* __restrict__ dl,
+    const float* __restrict__ node_params, const float* __restrict__ split_gain, int missing_bin,
+    unsigned long long* __restrict__ cursors) {
   const PartItem it = items[blockIdx.x];
-  const int f = split_feat[it.node], sb = split_bin[it.node];
-  const bool d = dl[it.node] != 0;
-  if (f < 0) return;
+  const int j = it.node;
+  const int f = split_feat[j], sb = split_bin[j];
+  // the host's split decision, evaluated identically: splittable node, a split found, gain above eps
+  if (f < 0 || !(node_params[(int64_t)j * 8 + 7] > 0.5f) || !(split_gain[j] > node_params[(int64_t)j * 8 + 6])) return;
+  const bool d = dl[j] != 0;
+  const int64_t nb = node_begin[j], nend = nb + node_count[j];
   __shared__ int s_wave[4];
+  __shared__ unsigned long long s_base[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int64_t nl = 0, nr = 0;
   for (int64_t base = 0; base < it.count; base += blockDim.x) {
     const int64_t i = base + threadIdx.x;
     const bool valid = i < it.count;
@@ -443,14 +484,17 @@ __global__ void __launch_bounds__(256) partition_scatter_kernel(
       if (w < wave) before += s_wave[w];
       tot += s_wave[w];
     }
-    const int64_t nvalid = min((int64_t)blockDim.x, it.count - base);
+    const int nvalid = (int)min((int64_t)blockDim.x, it.count - base);
+    if (threadIdx.x == 0) {
+      s_base[0] = atomicAdd(cursors + 2 * j, (unsigned long long)tot);
+      s_base[1] = atomicAdd(cursors + 2 * j + 1, (unsigned long long)(nvalid - tot));
+    }
+    __syncthreads();
     if (valid) {
       const int lpos = before + wpre;
-      if (left) rows_out[it.out_left + nl + lpos] = e;
-      else rows_out[it.out_right + nr + ((int)threadIdx.x - lpos)] = e;
+      if (left) rows_out[nb + (int64_t)s_base[0] + lpos] = e;
+      else rows_out[nend - 1 - (int64_t)s_base[1] - ((int)threadIdx.x - lpos)] = e;
     }
-    nl += tot;
-    nr += nvalid - tot;
     __syncthreads();
   }
 }
@@ -479,6 +523,73 @@ __global__ void __launch_bounds__(256) leaf_collect_kernel(const uint32_t* __res
 }
 
 // ------------------------------------------------------------------------------------- predict
+// LDS-row variant (F <= 512): the workgroup first copies its 128 rows' bins (row-major, F bytes each)
+// into LDS with coalesced byte loads, then every lane walks its model's trees reading bins from LDS,
+// eight trees interleaved. Without it each tree step paid a dependent L2/Infinity-cache round trip for
+// a single byte (64 lanes = 64 different rows = 64 cache lines per step); now only the node fetch
+// (shared by the wave near the root, L2/L1 resident) stays global. grid.y = model.
+constexpr int PRED_ROWS = 128;
+constexpr int PRED_TU = 8;
+
+__global__ void __launch_bounds__(PRED_ROWS) forest_predict_lds_kernel(
+    const uint8_t* __restrict__ Xb, int F, const int64_t* __restrict__ model_row_off,
+    const int32_t* __restrict__ row_list, const int64_t* __restrict__ model_tree_off,
+    const int64_t* __restrict__ tree_off, const float* __restrict__ tree_weight, const int4* __restrict__ nodes,
+    const uint8_t* __restrict__ default_left, int missing_bin, const float* __restrict__ leaf_value, int K,
+    float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t srows[];
+  const int m = blockIdx.y;
+  const int64_t r0 = model_row_off[m], r1 = model_row_off[m + 1];
+  const int64_t blk0 = r0 + (int64_t)blockIdx.x * PRED_ROWS;
+  if (blk0 >= r1) return;                                   // whole workgroup out of range (uniform)
+  const int nrow = (int)min((int64_t)PRED_ROWS, r1 - blk0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int r = wave; r < nrow; r += PRED_ROWS / 64) {
+    const int64_t row = row_list ? row_list[blk0 + r] : (blk0 + r - r0);
+    const uint8_t* src = Xb + row * F;
+    for (int b = lane; b < F; b += 64) srows[r * F + b] = src[b];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x >= nrow) return;
+  const uint8_t* xr = srows + threadIdx.x * F;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t t_end = model_tree_off[m + 1];
+  int64_t t = model_tree_off[m];
+  for (; t < t_end; t += PRED_TU) {
+    const int nu = (int)min((int64_t)PRED_TU, t_end - t);
+    int64_t k[PRED_TU];
+    int4 nd[PRED_TU];
+#pragma unroll
+    for (int u = 0; u < PRED_TU; ++u) {
+      k[u] = u < nu ? tree_off[t + u] : tree_off[t];
+      nd[u] = nodes[k[u]];
+    }
+    bool active = true;
+    while (active) {
+      active = false;
+#pragma unroll
+      for (int u = 0; u < PRED_TU; ++u) {
+        if (nd[u].z >= 0) {
+          const uint8_t b = xr[nd[u].x];
+          const bool gl = (missing_bin >= 0 && b == missing_bin) ? (default_left[k[u]] != 0) : ((int)b <= nd[u].y);
+          k[u] = gl ? nd[u].z : nd[u].w;
+          nd[u] = nodes[k[u]];
+          active = true;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PRED_TU; ++u) {
+      if (u < nu) {
+        const float w = tree_weight[t + u];
+        for (int c = 0; c < K && c < 8; ++c) acc[c] += w * leaf_value[k[u] * K + c];
+      }
+    }
+  }
+  float* o = out + (blk0 + threadIdx.x) * K;
+  for (int c = 0; c < K && c < 8; ++c) o[c] = acc[c];
+}
+
 // grid.y = model; each thread walks every tree of its model for one of the model's rows.
 __global__ void __launch_bounds__(256) forest_predict_kernel(
     const uint8_t* __restrict__ Xb, int F, const int64_t* __restrict__ model_row_off,
@@ -548,21 +659,24 @@ extern "C" {
 int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
-                        const float* t1, const float* t2, int64_t stride, const float* qscale, hipStream_t stream) {
+                        const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
+                        hipStream_t stream) {
   if (n_items == 0) return 0;
-  const size_t lds = (size_t)(((64 * (B * S + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4);
+  const size_t lds = (size_t)(((64 * (B * S + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
+                     TM_MAX_S * sizeof(int);
   if (lds > 160 * 1024) return -2;
+  if (skip_bin >= B || (mode == 2 && skip_bin >= 0 && S != 2)) return -2;
   const HistItem* it = (const HistItem*)items;
   dim3 grid(n_items), block(256);
   if (mode == 0)
     hipLaunchKernelGGL(hist_build_kernel<0>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1);
   else if (mode == 1)
     hipLaunchKernelGGL(hist_build_kernel<1>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1);
   else
     hipLaunchKernelGGL(hist_build_kernel<2>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin);
   return (int)hipGetLastError();
 }
 
@@ -581,7 +695,8 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
                         const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
-                        float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, hipStream_t stream) {
+                        float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors,
+                        hipStream_t stream) {
   if (n_nodes == 0) return 0;
   if (S > TM_MAX_S || B > 64) return -2;
   const int fbmax = (max_nfeat + FPB - 1) / FPB;
@@ -598,7 +713,7 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
 #undef TM_SPLIT
   hipLaunchKernelGGL(split_reduce_kernel, dim3(n_nodes), dim3(64), 0, stream, hist, node_hist_off, node_feat_off,
                      feat_list, B, S, missing_bin, node_model, qinv, fbmax, cand, out_feat, out_bin, out_gain, out_dl,
-                     out_left, out_total);
+                     out_left, out_total, (unsigned long long*)cursors);
   return (int)hipGetLastError();
 }
 
@@ -614,21 +729,14 @@ size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat) {
   return (size_t)n_nodes * ((max_nfeat + FPB - 1) / FPB) * sizeof(Best);
 }
 
-int tmog_hip_partition_count(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
-                             const int32_t* split_feat, const int32_t* split_bin, const uint8_t* dl, int missing_bin,
-                             int64_t* chunk_left, hipStream_t stream) {
+int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, const void* items,
+                             int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
+                             const int32_t* split_bin, const uint8_t* dl, const float* node_params,
+                             const float* split_gain, int missing_bin, int64_t* cursors, hipStream_t stream) {
   if (n_items == 0) return 0;
-  hipLaunchKernelGGL(partition_count_kernel, dim3(n_items), dim3(256), 0, stream, Xb, F, rows,
-                     (const PartItem*)items, split_feat, split_bin, dl, missing_bin, chunk_left);
-  return (int)hipGetLastError();
-}
-
-int tmog_hip_partition_scatter(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out,
-                               const void* items, int n_items, const int32_t* split_feat, const int32_t* split_bin,
-                               const uint8_t* dl, int missing_bin, hipStream_t stream) {
-  if (n_items == 0) return 0;
-  hipLaunchKernelGGL(partition_scatter_kernel, dim3(n_items), dim3(256), 0, stream, Xb, F, rows_in, rows_out,
-                     (const PartItem*)items, split_feat, split_bin, dl, missing_bin);
+  hipLaunchKernelGGL(partition_fused_kernel, dim3(n_items), dim3(256), 0, stream, Xb, F, rows_in, rows_out,
+                     (const PartItem*)items, node_begin, node_count, split_feat, split_bin, dl, node_params,
+                     split_gain, missing_bin, (unsigned long long*)cursors);
   return (int)hipGetLastError();
 }
 
@@ -647,6 +755,13 @@ int tmog_hip_forest_predict(const uint8_t* Xb, int F, int n_models, const int64_
                             hipStream_t stream) {
   if (n_models == 0 || max_rows == 0) return 0;
   if (K > 8) return -2;
+  if ((size_t)PRED_ROWS * F <= 64 * 1024) {
+    dim3 g2((unsigned)((max_rows + PRED_ROWS - 1) / PRED_ROWS), n_models);
+    hipLaunchKernelGGL(forest_predict_lds_kernel, g2, dim3(PRED_ROWS), (size_t)PRED_ROWS * F, stream, Xb, F,
+                       model_row_off, row_list, model_tree_off, tree_off, tree_weight, (const int4*)nodes,
+                       default_left, missing_bin, leaf_value, K, out);
+    return (int)hipGetLastError();
+  }
   dim3 grid((unsigned)((max_rows + 255) / 256), n_models);
   hipLaunchKernelGGL(forest_predict_kernel, grid, dim3(256), 0, stream, Xb, F, model_row_off, row_list,
                      model_tree_off, tree_off, tree_weight, (const int4*)nodes, default_left, missing_bin, leaf_value,

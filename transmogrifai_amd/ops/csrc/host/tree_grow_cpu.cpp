@@ -69,15 +69,14 @@ struct CpuBackend {
   }
   void split_find(const tmog::GrowArgs& g, const int64_t* hist, int m, const int64_t* nho, const int32_t* nnf,
                   const int32_t* nfo, const int32_t* flist, const float* params, const int32_t* nmd, int,
-                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot) {
+                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t*) {
     tmog_split_find_cpu(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd, g.qinv,
                         feat, bin, gain, dl, left, tot);
   }
-  void partition_count(const tmog::GrowArgs&, const uint32_t*, const void*, int, const int32_t*, const int32_t*,
-                       const uint8_t*, int64_t*) {}
-  void partition_scatter(const tmog::GrowArgs&, const uint32_t*, uint32_t*, const void*, int, const int32_t*,
-                         const int32_t*, const uint8_t*) {
-    throw std::logic_error("partition_scatter is the GPU backend's path");
+  void partition_fused(const tmog::GrowArgs&, const uint32_t*, uint32_t*, const void*, int, const int64_t*,
+                       const int64_t*, const int32_t*, const int32_t*, const uint8_t*, const float*, const float*,
+                       int64_t*) {
+    throw std::logic_error("partition_fused is the GPU backend's path");
   }
   void partition_nodes(const tmog::GrowArgs& g, const uint32_t* rows, uint32_t* rows_alt, int ns, const int64_t* nb,
                        const int64_t* nc, const int32_t* f, const int32_t* b, const uint8_t* d, const int64_t* ob,

@@ -28,9 +28,23 @@ def _s64(c: int) -> int:
 _M63 = 0x7FFFFFFFFFFFFFFF
 
 
+def _row_uniform_hip(row_ids: torch.Tensor, offs) -> torch.Tensor:
+    """One fused HIP pass (ops/csrc/hip/boost_kernels.hip) for device row ids: ``[len(offs), n]``."""
+    from ..ops import _native as N
+    from ..ops.staging import to_device
+    rid = row_ids.to(torch.int64).contiguous()
+    out = torch.empty(len(offs), rid.shape[0], dtype=torch.float64, device=rid.device)
+    o = to_device(list(offs), rid.device, np.int64)
+    N.check(N.hip().tmog_hip_row_uniform(N.ptr(rid), rid.shape[0], N.ptr(o), len(offs), N.ptr(out),
+                                         N.stream(rid.device)), "row_uniform")
+    return out
+
+
 def row_uniform(row_ids: torch.Tensor, seed: int, stream: int = 0) -> torch.Tensor:
     """Deterministic U[0,1) per global row id (splitmix64-style hash), identical on any device / shard."""
     off = _s64(int(seed) * 0x632BE59BD9B4E019 + stream * 0x2545F4914F6CDD1D)
+    if row_ids.is_cuda and row_ids.numel():
+        return _row_uniform_hip(row_ids, [off])[0]
     x = row_ids.to(torch.int64) * _s64(0x1E3779B97F4A7C15) + off
     x = x & _M63
     x = ((x ^ (x >> 30)) * _s64(0x2F58476D1CE4E5B9)) & _M63
@@ -41,8 +55,10 @@ def row_uniform(row_ids: torch.Tensor, seed: int, stream: int = 0) -> torch.Tens
 
 def row_uniform_multi(row_ids: torch.Tensor, seeds, stream: int = 0) -> torch.Tensor:
     """``row_uniform`` for several seeds at once: ``[len(seeds), n]`` (one fused pass, no per-seed launches)."""
-    off = torch.tensor([_s64(int(sd) * 0x632BE59BD9B4E019 + stream * 0x2545F4914F6CDD1D) for sd in seeds],
-                       dtype=torch.int64, device=row_ids.device)[:, None]
+    offs = [_s64(int(sd) * 0x632BE59BD9B4E019 + stream * 0x2545F4914F6CDD1D) for sd in seeds]
+    if row_ids.is_cuda and row_ids.numel():
+        return _row_uniform_hip(row_ids, offs)
+    off = torch.tensor(offs, dtype=torch.int64, device=row_ids.device)[:, None]
     x = row_ids.to(torch.int64)[None, :] * _s64(0x1E3779B97F4A7C15) + off
     x = x & _M63
     x = ((x ^ (x >> 30)) * _s64(0x2F58476D1CE4E5B9)) & _M63
