@@ -187,7 +187,8 @@ class _GrowArgs(C.Structure):
                 ("job_lambda", C.c_void_p), ("job_eps", C.c_void_p), ("job_fsub", C.c_void_p),
                 ("job_count", C.c_void_p), ("rows", C.c_void_p), ("rows_alt", C.c_void_p),
                 ("leaf_rows", C.c_void_p), ("leaf_gid", C.c_void_p), ("n_groups", C.c_int32),
-                ("group_start", C.c_void_p), ("rng_seed", C.c_int64), ("stream", C.c_void_p)]
+                ("group_start", C.c_void_p), ("rng_seed", C.c_int64), ("stream", C.c_void_p),
+                ("n_bins_host", C.c_void_p)]
 
 
 class _Nodes:
@@ -254,13 +255,13 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         lam=np.array([j.params.reg_lambda for j in jobs], np.float64),
         eps=np.array([j.params.split_eps for j in jobs], np.float64),
         fsub=np.array([0 if j.params.feature_subset is None else int(j.params.feature_subset) for j in jobs], np.int32),
-        count=np.asarray(counts, np.int64), cuts=cuts)
+        count=np.asarray(counts, np.int64), cuts=cuts, nbins=np.ascontiguousarray(np.asarray(n_bins, np.int32)))
     hp = {k: v.ctypes.data for k, v in host.items()}
     a = _GrowArgs(N.ptr(Xb), Nrows, F, mode, kind, S, B, missing_bin, int(chunk_rows), int(bool(subtract)),
                   int(bool(collect_leaves)), N.ptr(yf), N.ptr(t1f), N.ptr(t2f), stride, N.ptr(qscale), N.ptr(qinv),
                   N.ptr(n_bins_t), T, hp["model"], hp["depth"], hp["inst"], hp["gain"], hp["mcw"], hp["lam"], hp["eps"],
                   hp["fsub"], hp["count"], N.ptr(rows), N.ptr(rows_alt), N.ptr(leaf_rows), N.ptr(leaf_gid), ng,
-                  hp["cuts"], int(rng_seed), N.stream(dev) if on_gpu else None)
+                  hp["cuts"], int(rng_seed), N.stream(dev) if on_gpu else None, hp["nbins"])
     lib = N.hip() if on_gpu else N.host()
     fn = (lambda name: getattr(lib, f"tmog_hip_{name}")) if on_gpu else (lambda name: getattr(lib, f"tmog_{name}_cpu"))
     h = fn("grow_forest")(C.byref(a))

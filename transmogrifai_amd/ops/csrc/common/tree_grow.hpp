@@ -55,6 +55,7 @@ struct GrowArgs {
   const int32_t* group_start;  // [n_groups + 1] job boundaries
   int64_t rng_seed;
   void* stream;               // GPU: caller's stream (groups wait on it; it waits on the groups)
+  const int32_t* n_bins_host; // host copy of n_bins (feature grouping for the histogram kernel), may be null
 };
 
 struct GroupResult {
@@ -129,6 +130,21 @@ struct Staging {
   void clear() { buf.clear(); }
 };
 
+struct FeatGroup {
+  int f0, nf;
+  bool reg;
+};
+
+// n features in near-equal groups of at most 64
+inline std::vector<FeatGroup> equal_groups(int n) {
+  std::vector<FeatGroup> out;
+  if (n <= 0) return out;
+  const int ng = std::max(1, (n + 63) / 64);
+  const int fg = (n + ng - 1) / ng;
+  for (int gi = 0; gi * fg < n; ++gi) out.push_back(FeatGroup{gi * fg, std::min(fg, n - gi * fg), false});
+  return out;
+}
+
 template <class BK>
 void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
   const int j0 = a.group_start[g], j1 = a.group_start[g + 1];
@@ -196,6 +212,22 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     bk.leaf_collect(rows, d + o, (int)items.size(), leaf_rows, leaf_gid);
   };
 
+  // Feature groups of the histogram kernel (<= 64 features each). Without per-node subsets the
+  // grouping is fixed: with a sparse missing bin (GPU, MODE 2) runs of one-present-bin columns
+  // (one-hot / null indicators) get groups of their own so the kernel accumulates them in registers.
+  std::vector<FeatGroup> full_groups;
+  {
+    const bool reg_ok = BK::kGPU && a.mode == 2 && a.missing_bin >= 0 && a.n_bins_host != nullptr;
+    int f = 0;
+    while (f < F) {
+      const bool one = reg_ok && a.n_bins_host[f] == 1;
+      int e = f;
+      while (e < F && (reg_ok && a.n_bins_host[e] == 1) == one) ++e;
+      if (!reg_ok) e = F;
+      for (const FeatGroup& g : equal_groups(e - f)) full_groups.push_back(FeatGroup{f + g.f0, g.nf, one});
+      f = e;
+    }
+  }
   for (int depth = 0; depth <= max_depth; ++depth) {
     const int64_t n = (int64_t)lv_gid.size();
     if (n == 0) break;
@@ -304,19 +336,18 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
       b_nnf.push_back(nfeat[j]);
       b_nmd.push_back(nmd[j]);
       const int nf = nfeat[j];
-      const int ng = std::max(1, (nf + 63) / 64);
-      const int fg = (nf + ng - 1) / ng;
       if (nch > 1) {
         z_off.push_back(hoff[j]);
         z_size.push_back(hsz[j]);
       }
+      const std::vector<FeatGroup>& grp = use_subset ? equal_groups(nf) : full_groups;
       for (int64_t c = 0; c < nch; ++c)
-        for (int gi = 0; gi < ng; ++gi) {
+        for (const FeatGroup& fgp : grp) {
           HistItemH h;
           h.node = j;
-          h.fg0 = gi * fg;
-          h.nf = std::min(fg, nf - gi * fg);
-          h.excl = nch == 1 ? 1 : 0;
+          h.fg0 = fgp.f0;
+          h.nf = fgp.nf;
+          h.excl = (nch == 1 ? 1 : 0) | (fgp.reg ? 2 : 0);
           h.begin = nb[j] + c * a.chunk_rows;
           h.count = std::min(a.chunk_rows, cnt - c * a.chunk_rows);
           hitems.push_back(h);

@@ -27,7 +27,8 @@ struct HistItem {
   int32_t node;     // node slot
   int32_t fg0;      // first local feature of this group
   int32_t nf;       // features in this group (<= 64)
-  int32_t excl;     // 1 => this item alone covers node rows for its features (plain stores)
+  int32_t excl;     // bit 0: this item alone covers node rows for its features (plain stores)
+                    // bit 1: every feature of the group has one present bin (register accumulation)
   int64_t begin;    // first row entry
   int64_t count;    // row entries in this chunk
 };
@@ -96,8 +97,16 @@ __device__ __forceinline__ void add_row(int* my, int bin, int S, const int4& st)
 // one-hot / null-indicator columns) issue no LDS atomic. Each wave instead folds its 64 staged rows'
 // (g, h) into the chunk total with two wave reductions, and before the write-out the missing bin of
 // every feature is recovered exactly as chunk total - sum of the other bins (integer arithmetic, so
-// the histogram stays bit-identical to the CPU twin). On the headline table this drops about half of
-// all ds_add_u32 (the kernel is LDS-atomic-throughput bound: benchmarks/lds_atomic_bench.hip).
+// the histogram stays bit-identical to the CPU twin). Masking lanes does not shorten an LDS atomic
+// wave-instruction, so this alone saves little; what it enables is the register path below.
+//
+// Register path (excl bit 1, sparse mode only): when every feature of the group has a single present
+// bin (one-hot and null-indicator columns under ``missing`` = 0: value 1 -> bin 0, value 0 -> missing
+// bin) a lane just sums the (g, h) of its rows with bin 0 in two registers -- no LDS atomics in the
+// row loop at all, one per lane at the end. The tree grower groups such columns together
+// (common/tree_grow.hpp), so on the headline table ~40 % of the feature groups skip the atomics.
+// PMC on the tree micro-benchmark: ~0.064 LDS wave-instructions per CU-cycle at ~11 cycles each for
+// a ds_add_u32 -> the LDS atomic unit is ~70 % busy; VALU ~12 % busy, so trading atomics for VALU pays.
 template <int MODE>
 __global__ void __launch_bounds__(256) hist_build_kernel(
     const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const HistItem* __restrict__ items,
@@ -117,6 +126,8 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   int4* stage = reinterpret_cast<int4*>(lds + ((ncopy_words + 3) & ~3)) + wave * 64;
   int* tot = lds + ((ncopy_words + 3) & ~3) + 4 * 64 * 4;     // chunk totals (sparse missing bin)
   const bool sparse = MODE == 2 && skip_bin >= 0;
+  const bool regacc = sparse && (it.excl & 2);
+  const bool excl = (it.excl & 1) != 0;
   for (int i = threadIdx.x; i < ncopy_words; i += blockDim.x) lds[i] = 0;
   if (threadIdx.x < TM_MAX_S) tot[threadIdx.x] = 0;
   __syncthreads();
@@ -131,6 +142,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   const uint32_t* rp = rows + it.begin;
   const int64_t cnt = it.count;
 
+  int racc0 = 0, racc1 = 0;     // register path sums (bin 0 of this lane's feature)
   // Loads are never predicated (a masked "load or skip" makes hipcc branch around every load and wait
   // vmcnt(0) per element): out-of-range slots read a valid dummy record and are masked at the atomic.
   for (int64_t base = (int64_t)wave * 64; base < cnt; base += (int64_t)nwaves * 64) {
@@ -152,6 +164,24 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0): staged records visible to the wave
     __builtin_amdgcn_wave_barrier();
+    if (regacc) {
+      for (int j0 = 0; j0 < nrows; j0 += R * 8) {
+        int4 st[8];
+        int bin[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) st[u] = stage[min(j0 + u * R + rsub, 63)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) bin[u] = (int)Xb[(int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F + feat];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const bool hit = j0 + u * R + rsub < nrows && bin[u] == 0;
+          racc0 += hit ? st[u].y : 0;
+          racc1 += hit ? st[u].z : 0;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
     for (int j0 = 0; j0 < nrows; j0 += R * 8) {
       int4 st[8];
       int bin[8];
@@ -169,6 +199,13 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
 
   int64_t* out = hist + node_hist_off[it.node] + (int64_t)it.fg0 * B * S;
   const int words = FG * B * S;
+  if (regacc) {
+    if (active) {
+      atomicAdd(my, racc0);
+      atomicAdd(my + 1, racc1);
+    }
+    __syncthreads();
+  }
   if (sparse) {
     // fold the R copies into copy 0, then recover each feature's missing bin from the chunk totals
     if (R > 1) {
@@ -192,7 +229,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     for (int k = threadIdx.x; k < words; k += blockDim.x) {
       const int f = k / (B * S);
       const int64_t acc = lds[f * rowstride + (k - f * (B * S))];
-      if (it.excl) out[k] = acc;
+      if (excl) out[k] = acc;
       else if (acc != 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + k), (unsigned long long)acc);
     }
     return;
@@ -203,7 +240,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     const int rem = k - f * (B * S);
     int64_t acc = 0;
     for (int r = 0; r < R; ++r) acc += lds[(r * FG + f) * rowstride + rem];
-    if (it.excl) out[k] = acc;
+    if (excl) out[k] = acc;
     else if (acc != 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + k), (unsigned long long)acc);
   }
 }
@@ -326,7 +363,7 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
       const int64_t* hf = h + (int64_t)f * B * S;
       int64_t v[SM], miss[SM];
       for (int s = 0; s < S; ++s) {
-        v[s] = (lane < nb - 1) ? hf[lane * S + s] : 0;
+        v[s] = (lane < nb) ? hf[lane * S + s] : 0;
         miss[s] = allow_missing ? hf[missing_bin * S + s] : 0;
       }
       for (int off = 1; off < 64; off <<= 1) {
@@ -335,8 +372,10 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
           if (lane >= off) v[s] += o;
         }
       }
-      if (lane < nb - 1) {
+      // candidates b < nb - 1; with a missing bin dl = 0 also b = nb - 1 (present left, missing right)
+      if (lane < nb - 1 + (allow_missing ? 1 : 0)) {
         for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
+          if (lane == nb - 1 && dl) continue;
           double left[SM], right[SM];
           for (int s = 0; s < S; ++s) {
             const int64_t lq = v[s] + (dl ? miss[s] : 0);

@@ -143,7 +143,10 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
       for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
         int64_t lq[16];
         for (int s = 0; s < S; ++s) lq[s] = dl ? miss[s] : 0;
-        for (int b = 0; b + 1 < nb; ++b) {
+        // with a missing bin, dl = 0 also tries b = nb - 1: every present value left, missing right
+        // (XGBoost's present-vs-missing split; the only candidate of a one-bin indicator column)
+        const int b_end = nb - 1 + ((allow_missing && dl == 0) ? 1 : 0);
+        for (int b = 0; b < b_end; ++b) {
           double left[16], right[16];
           for (int s = 0; s < S; ++s) {
             lq[s] += hf[(int64_t)b * S + s];
