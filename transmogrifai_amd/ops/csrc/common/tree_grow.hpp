@@ -215,18 +215,21 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
   // Feature groups of the histogram kernel (<= 64 features each). Without per-node subsets the
   // grouping is fixed: with a sparse missing bin (GPU, MODE 2) runs of one-present-bin columns
   // (one-hot / null indicators) get groups of their own so the kernel accumulates them in registers.
+  // The feature order is the same on both backends (stable: multi-bin columns first, then the
+  // one-present-bin columns), so split tie-breaks by local feature index stay identical GPU vs CPU.
   std::vector<FeatGroup> full_groups;
-  {
-    const bool reg_ok = BK::kGPU && a.mode == 2 && a.missing_bin >= 0 && a.n_bins_host != nullptr;
-    int f = 0;
-    while (f < F) {
-      const bool one = reg_ok && a.n_bins_host[f] == 1;
-      int e = f;
-      while (e < F && (reg_ok && a.n_bins_host[e] == 1) == one) ++e;
-      if (!reg_ok) e = F;
-      for (const FeatGroup& g : equal_groups(e - f)) full_groups.push_back(FeatGroup{f + g.f0, g.nf, one});
-      f = e;
-    }
+  std::vector<int32_t> perm_feats;
+  if (!use_subset && a.mode == 2 && a.missing_bin >= 0 && a.n_bins_host != nullptr) {
+    for (int f = 0; f < F; ++f)
+      if (a.n_bins_host[f] != 1) perm_feats.push_back(f);
+    const int n_multi = (int)perm_feats.size();
+    for (int f = 0; f < F; ++f)
+      if (a.n_bins_host[f] == 1) perm_feats.push_back(f);
+    for (const FeatGroup& g : equal_groups(n_multi)) full_groups.push_back(g);
+    for (const FeatGroup& g : equal_groups(F - n_multi))
+      full_groups.push_back(FeatGroup{n_multi + g.f0, g.nf, BK::kGPU});
+  } else {
+    full_groups = equal_groups(F);
   }
   for (int depth = 0; depth <= max_depth; ++depth) {
     const int64_t n = (int64_t)lv_gid.size();
@@ -265,6 +268,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
         feat_off[j] = 0;
         nfeat[j] = F;
       }
+      if (!perm_feats.empty()) feat_list = perm_feats;
     }
     std::vector<int64_t> hsz(m), hoff(m);
     int64_t hwords = 0;
@@ -367,7 +371,8 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     st1.clear();
     const size_t o_nfo = st1.add(feat_off), o_nnf = st1.add(nfeat), o_nmd = st1.add(nmd), o_nho = st1.add(hoff);
     const size_t o_par = st1.add(params);
-    const size_t o_fl = use_subset ? st1.add(feat_list) : 0;
+    const bool own_list = use_subset || !perm_feats.empty();
+    const size_t o_fl = own_list ? st1.add(feat_list) : 0;
     const size_t o_hit = st1.add(hitems), o_cit = st1.add(citems);
     const size_t o_zo = st1.add(z_off), o_zs = st1.add(z_size);
     const size_t o_dp = st1.add(d_poff), o_ds = st1.add(d_soff), o_do = st1.add(d_ooff), o_dz = st1.add(d_size);
@@ -376,7 +381,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     const size_t o_nb = st1.add(nb), o_nc = st1.add(nc);
     const uint8_t* d1 = bk.ship(st1, 0);
 #define TM_P(T_, off) ((T_*)(d1 + (off)))
-    const int32_t* flist = use_subset ? TM_P(const int32_t, o_fl) : all_feats;
+    const int32_t* flist = own_list ? TM_P(const int32_t, o_fl) : all_feats;
     // ---- histograms
     bk.zero_segments(hist, TM_P(const int64_t, o_zo), TM_P(const int64_t, o_zs), (int)z_off.size(), z_max);
     bk.hist_build(a, rows, hitems.size() ? (const void*)(d1 + o_hit) : nullptr, (int)hitems.size(),
