@@ -70,3 +70,33 @@ def test_label_joiners_and_filter_map():
     assert check_transformer(tj, ds)[1] == {"a": 0.5, "c": 0.4}
     ds3, (mp,) = TestFeatureBuilder.of(("mp", T.TextMap, [{"k1": "v", "k2": "w"}, {}]))
     check_transformer(M.FilterMap(block_list_keys=["k2"]).set_input(mp), ds3, expected=[{"k1": "v"}, {}])
+
+
+def test_prediction_descaler_inverts_scaler():
+    """``DescalerTransformerTest`` / ``PredictionDescalerTransformerTest``: descaling a scaled label (and a
+    prediction made on the scaled label) recovers the original scale."""
+    import torch
+    from transmogrifai_amd.data.columns import NumericColumn, PredictionColumn
+    from transmogrifai_amd.data.dataset import Dataset
+    from transmogrifai_amd.dsl.core import descale_prediction
+    from transmogrifai_amd.features import types as T
+    from transmogrifai_amd.features.builder import FeatureBuilder
+    from transmogrifai_amd.stages.feature.math_stages import PredictionDescaler
+    y = FeatureBuilder.Real("y").as_predictor()
+    scaled = y.scale("Linear", slope=2.0, intercept=1.0)
+    back = y.descale(scaled)
+    vals = torch.tensor([1.0, 2.5, -3.0], dtype=torch.float64)
+    ds = Dataset({"y": NumericColumn(T.Real, vals)})
+    ds = scaled.origin_stage.transform(ds)
+    assert torch.allclose(ds[scaled.name].values, 2 * vals + 1)
+    ds2 = back.origin_stage.transform(ds.with_column("y", NumericColumn(T.Real, ds[scaled.name].values)))
+    assert torch.allclose(ds2[back.name].values, vals)
+    # prediction descaler
+    pcol = PredictionColumn(2 * vals + 1, None, None)
+    pd = PredictionDescaler(scaling_type="Linear", slope=2.0, intercept=1.0)
+    out = pd.transform_columns(pcol, ds[scaled.name])
+    assert torch.allclose(out.values, vals)
+    assert pd.transform_row({"prediction": 7.0}, None) == 3.0
+    pred_feat = FeatureBuilder.Real("p").as_predictor()
+    d = descale_prediction(pred_feat, scaled)
+    assert isinstance(d.origin_stage, PredictionDescaler)

@@ -170,6 +170,24 @@ def _scale(self, scaling_type: str = "Linear", slope: float = 1.0, intercept: fl
     return M.ScalerTransformer(scaling_type=scaling_type, slope=slope, intercept=intercept).set_input(self).get_output()
 
 
+def _scaling_of(scaled):
+    st = scaled.origin_stage
+    if not isinstance(st, M.ScalerTransformer):
+        raise ValueError(f"feature '{scaled.name}' was not produced by a ScalerTransformer (scale())")
+    return {k: st.params[k] for k in ("scaling_type", "slope", "intercept")}
+
+
+@register(NUM, "descale")
+def _descale(self, scaled):
+    """Inverse of ``scaled``'s scaling applied to this feature (``RichNumericFeature.descale``)."""
+    return M.DescalerTransformer(**_scaling_of(scaled)).set_input(self, scaled).get_output()
+
+
+def descale_prediction(prediction, scaled):
+    """``PredictionDescaler``: a model's prediction back on the scale of the unscaled label."""
+    return M.PredictionDescaler(**_scaling_of(scaled)).set_input(prediction, scaled).get_output()
+
+
 @register(NUM, "bucketize")
 def _bucketize(self, splits: Sequence[float], track_nulls: bool = True, track_invalid: bool = False,
                split_inclusion: str = "Left", bucket_labels=None):

@@ -247,6 +247,30 @@ class DescalerTransformer(BinaryTransformer):
         return NumericColumn(T.Real, torch.where(ok, v, torch.zeros_like(v)), ok)
 
 
+@register_stage
+class PredictionDescaler(DescalerTransformer):
+    """Descale a model's ``Prediction`` back to the original label scale with the scaling of the second
+    input's ``ScalerTransformer`` (``DescalerTransformer.scala:92-112``): the prediction value of the
+    Prediction map goes through the inverse scaling; raw / probability are dropped."""
+    operation_name = "descaler"
+    output_type = T.Real
+
+    def transform_columns(self, a, b=None, ds=None):
+        from ...data.columns import PredictionColumn
+        if isinstance(a, PredictionColumn):
+            p = a.prediction.to(torch.float64)
+            a = NumericColumn(T.Real, p, torch.ones(p.shape[0], dtype=torch.bool, device=p.device))
+        return super().transform_columns(a, b, ds=ds)
+
+    def transform_row(self, *values):
+        v = values[0]
+        if isinstance(v, dict):
+            v = v.get("prediction")
+        elif isinstance(v, T.FeatureType):
+            v = v.value.get("prediction") if isinstance(v.value, dict) else v.value
+        return self.transform_columns(NumericColumn.from_values(T.Real, [v])).row(0)
+
+
 # ------------------------------------------------------------------------------------ bucketizer
 def java_double(v: float) -> str:
     """Java ``Double.toString`` formatting (bucket labels must match the reference)."""
