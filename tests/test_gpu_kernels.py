@@ -100,12 +100,15 @@ def test_xgb_fused_round_epilogue_matches_torch_path(monkeypatch):
     params = dict(XGBoostClassifierLearner.defaults, num_round=15, max_depth=4, eta=0.3, missing=0.0,
                   num_early_stopping_rounds=5)
     rows = torch.arange(0, n, 2, device="cuda")
+    rows2 = torch.arange(1, n, 3, device="cuda")
+    jobs = [FitJob(params, rows), FitJob(dict(params, max_depth=6), rows2), FitJob(dict(params, eta=0.1), rows)]
     outs = []
     for flag in ("1", "0"):
         monkeypatch.setenv("TMOG_XGB_FUSED", flag)
-        st = XGBoostClassifierLearner().fit_batch(Xd, yd, [FitJob(params, rows)])[0]
-        outs.append(XGBoostClassifierLearner().predict(st, Xd)[2][:, 1].cpu())
-    torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-5)
+        sts = XGBoostClassifierLearner().fit_batch(Xd, yd, jobs)
+        outs.append([XGBoostClassifierLearner().predict(st, Xd)[2][:, 1].cpu() for st in sts])
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
     assert _native_loaded()
 
 

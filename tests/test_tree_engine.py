@@ -72,10 +72,15 @@ def test_min_instances_respected():
     assert (f.cover >= 50 - 1e-6).all()
 
 
-def _grow_all(dev, mode, missing=False, subset=None, n_models=2):
+def _grow_all(dev, mode, missing=False, subset=None, n_models=2, onebin=False):
     X, y = _data(missing=missing)
     N = X.shape[0]
     B = 32
+    nbins = np.full(X.shape[1], B - 1 if missing else B)
+    if onebin:                                   # one-hot / null-indicator columns: bin 0 or missing
+        for c in (1, 4, 6, 7, 8, 9):
+            X[:, c] = torch.where(X[:, c] > 20, 0, B - 1).to(torch.uint8)
+            nbins[c] = 1
     g = torch.Generator().manual_seed(1)
     t1 = torch.round(torch.randn(n_models, N, generator=g) * 8) / 8
     t2 = torch.full((n_models, N), 0.25)
@@ -86,7 +91,7 @@ def _grow_all(dev, mode, missing=False, subset=None, n_models=2):
         jobs.append(te.TreeJob(m, te.TreeParams(max_depth=6, min_instances=2, reg_lambda=1.0,
                                                 min_child_weight=0.5, feature_subset=subset), rows, w))
     kind = {te.MODE_CLS: te.KIND_GINI, te.MODE_VAR: te.KIND_VARIANCE, te.MODE_GH: te.KIND_NEWTON}[mode]
-    f = te.grow_forest(X.to(dev), np.full(X.shape[1], B - 1 if missing else B), [
+    f = te.grow_forest(X.to(dev), nbins, [
         te.TreeJob(j.model, j.params, j.rows.to(dev), None if j.weights is None else j.weights.to(dev)) for j in jobs],
         mode=mode, kind=kind, y=y.to(dev), t1=t1.to(dev), t2=t2.to(dev), B=B,
         missing_bin=(B - 1) if missing else -1, rng_seed=3, chunk_rows=512)
@@ -100,12 +105,22 @@ def test_cpu_engine_runs_all_modes(mode):
     assert f.n_trees == 2 and len(f.nodes) > 3
 
 
+def test_cpu_engine_one_present_bin_columns():
+    """Permuted feature groups (one-present-bin columns last) still report original feature ids."""
+    f, _ = _grow_all("cpu", te.MODE_GH, missing=True, n_models=3, onebin=True)
+    used = set(int(v) for v in f.nodes[:, 0] if v >= 0)
+    assert used and used <= set(range(10))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode,missing,subset", [(te.MODE_CLS, False, None), (te.MODE_CLS, False, 4),
-                                                 (te.MODE_VAR, False, None), (te.MODE_GH, True, None)])
+                                                 (te.MODE_VAR, False, None), (te.MODE_GH, True, None),
+                                                 (te.MODE_GH, True, "onebin")])
 def test_hip_engine_matches_host(mode, missing, subset):
-    fc, pc = _grow_all("cpu", mode, missing, subset)
-    fg, pg = _grow_all("cuda", mode, missing, subset)
+    onebin = subset == "onebin"
+    subset = None if onebin else subset
+    fc, pc = _grow_all("cpu", mode, missing, subset, n_models=3 if onebin else 2, onebin=onebin)
+    fg, pg = _grow_all("cuda", mode, missing, subset, n_models=3 if onebin else 2, onebin=onebin)
     np.testing.assert_array_equal(fc.tree_off, fg.tree_off)
     np.testing.assert_array_equal(fc.nodes, fg.nodes)
     np.testing.assert_allclose(fc.value, fg.value, rtol=1e-5, atol=1e-5)

@@ -584,7 +584,7 @@ class XGBoostClassifierLearner(_BoostLearner):
         NV.check(NV.hip().tmog_hip_boost_epilogue(
             NV.ptr(la.rows), NV.ptr(la.gid), int(la.rows.numel()), NV.ptr(val), NV.ptr(la.tree.contiguous()),
             NV.ptr(tree_job), int(N), NV.ptr(Fm), NV.ptr(G), NV.ptr(H), NV.ptr(yf), self.objective_code,
-            NV.ptr(counts), int(bins), NV.stream(dev)), "boost_epilogue")
+            NV.ptr(counts), int(bins), int(val.shape[0]), len(act), int(P), NV.stream(dev)), "boost_epilogue")
         return counts
 
     def _outputs(self, state, m):

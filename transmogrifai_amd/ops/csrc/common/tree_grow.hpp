@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -444,7 +445,11 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     }
     // ---- partition of the splitting nodes' entries
     if (BK::kGPU) {
-      for (int64_t q = 0; q < ns; ++q) nl[q] = h_cur[2 * sl[q]];
+      for (int64_t q = 0; q < ns; ++q) {
+        nl[q] = h_cur[2 * sl[q]];
+        if (nl[q] < 0 || nl[q] + h_cur[2 * sl[q] + 1] != nc[sl[q]])
+          throw std::runtime_error("partition cursor mismatch at depth " + std::to_string(depth));
+      }
     } else {
       std::vector<int64_t> s_nb(ns), s_nc(ns);
       std::vector<int32_t> s_f(ns), s_b(ns);

@@ -24,12 +24,16 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
     const uint32_t* __restrict__ entries, const int32_t* __restrict__ gid, int64_t n_entries,
     const float* __restrict__ gid_value, const int64_t* __restrict__ gid_tree, const int64_t* __restrict__ tree_job,
     int64_t N, double* __restrict__ F, float* __restrict__ G, float* __restrict__ H, const float* __restrict__ y,
-    int objective, int32_t* __restrict__ auc_hist, int bins) {
+    int objective, int32_t* __restrict__ auc_hist, int bins, int64_t n_gid, int64_t n_trees, int64_t P) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n_entries) return;
   const int64_t r = entries[e] & 0xFFFFFFu;
   const int32_t g_id = gid[e];
-  const int64_t p = tree_job[gid_tree[g_id]];
+  if (g_id < 0 || g_id >= n_gid || r >= N) return;                 // defensive: never index out of range
+  const int64_t t = gid_tree[g_id];
+  if (t < 0 || t >= n_trees) return;
+  const int64_t p = tree_job[t];
+  if (p < 0 || p >= P) return;
   const int64_t k = p * N + r;
   const double m = F[k] + (double)gid_value[g_id];
   F[k] = m;
@@ -72,11 +76,13 @@ extern "C" {
 
 int tmog_hip_boost_epilogue(const uint32_t* entries, const int32_t* gid, int64_t n_entries, const float* gid_value,
                             const int64_t* gid_tree, const int64_t* tree_job, int64_t N, double* F, float* G, float* H,
-                            const float* y, int objective, int32_t* auc_hist, int bins, hipStream_t stream) {
+                            const float* y, int objective, int32_t* auc_hist, int bins, int64_t n_gid,
+                            int64_t n_trees, int64_t P, hipStream_t stream) {
   if (n_entries == 0) return 0;
   if (N >= (1 << 24)) return -2;
   hipLaunchKernelGGL(boost_epilogue_kernel, dim3((unsigned)((n_entries + 255) / 256)), dim3(256), 0, stream, entries,
-                     gid, n_entries, gid_value, gid_tree, tree_job, N, F, G, H, y, objective, auc_hist, bins);
+                     gid, n_entries, gid_value, gid_tree, tree_job, N, F, G, H, y, objective, auc_hist, bins, n_gid,
+                     n_trees, P);
   return (int)hipGetLastError();
 }
 

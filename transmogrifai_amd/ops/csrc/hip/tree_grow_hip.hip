@@ -52,6 +52,7 @@ struct GpuSlot {
   size_t pin_cap[3] = {0, 0, 0};
   uint8_t* dev[3] = {nullptr, nullptr, nullptr};
   size_t dev_cap[3] = {0, 0, 0};
+  hipEvent_t copied[3] = {nullptr, nullptr, nullptr};   // last H2D copy out of pin[k]
   uint8_t* res_dev = nullptr;
   size_t res_cap = 0;
   uint8_t* res_pin = nullptr;
@@ -103,15 +104,20 @@ struct GpuBackend {
     }
     return sl.feats;
   }
-  // Staged host arrays -> device in one async copy. A slot's previous copy is always complete here:
-  // every level performs a blocking result read after the copies of the previous level were queued.
+  // Staged host arrays -> device in one async copy. The pinned buffer is rewritten only after its
+  // previous copy has completed: a level's leaf items (slot 2) can be shipped twice with no blocking
+  // result read in between (leaves after the split read, then every node at the next level when
+  // none of them can split), so the wait is explicit instead of relying on the level's fetch.
   const uint8_t* ship(const tmog::Staging& st, int k) {
     const size_t n = st.buf.size() ? st.buf.size() : 16;
+    if (sl.copied[k]) hchk(hipEventSynchronize(sl.copied[k]), "stage copy wait");
+    else hchk(hipEventCreateWithFlags(&sl.copied[k], hipEventDisableTiming), "event create");
     grow_pin(sl.pin[k], sl.pin_cap[k], n, sl.stream);
     grow_dev(sl.dev[k], sl.dev_cap[k], n, sl.stream);
     if (st.buf.size()) {
       std::memcpy(sl.pin[k], st.buf.data(), st.buf.size());
       hchk(hipMemcpyAsync(sl.dev[k], sl.pin[k], st.buf.size(), hipMemcpyHostToDevice, sl.stream), "stage copy");
+      hchk(hipEventRecord(sl.copied[k], sl.stream), "event record");
     }
     return sl.dev[k];
   }

@@ -531,8 +531,11 @@ __global__ void __launch_bounds__(256) partition_fused_kernel(
     __syncthreads();
     if (valid) {
       const int lpos = before + wpre;
-      if (left) rows_out[nb + (int64_t)s_base[0] + lpos] = e;
-      else rows_out[nend - 1 - (int64_t)s_base[1] - ((int)threadIdx.x - lpos)] = e;
+      // guarded: a slot outside the node's range (impossible unless the cursors were not reset) is
+      // dropped; the host checks every node's left + right count against its size
+      const int64_t pos = left ? nb + (int64_t)s_base[0] + lpos
+                               : nend - 1 - (int64_t)s_base[1] - ((int)threadIdx.x - lpos);
+      if (pos >= nb && pos < nend) rows_out[pos] = e;
     }
     __syncthreads();
   }
