@@ -94,7 +94,8 @@ def _grow_all(dev, mode, missing=False, subset=None, n_models=2, onebin=False):
     f = te.grow_forest(X.to(dev), nbins, [
         te.TreeJob(j.model, j.params, j.rows.to(dev), None if j.weights is None else j.weights.to(dev)) for j in jobs],
         mode=mode, kind=kind, y=y.to(dev), t1=t1.to(dev), t2=t2.to(dev), B=B,
-        missing_bin=(B - 1) if missing else -1, rng_seed=3, chunk_rows=512)
+        missing_bin=(B - 1) if missing else -1, rng_seed=3, chunk_rows=512,
+        csr=te.onebin_csr(X.to(dev), nbins) if onebin else None)
     preds = te.forest_predict(f, X.to(dev), [None, torch.arange(0, N, 3).to(dev)], [[0], [1]])
     return f, [p.cpu() for p in preds]
 
@@ -103,6 +104,20 @@ def _grow_all(dev, mode, missing=False, subset=None, n_models=2, onebin=False):
 def test_cpu_engine_runs_all_modes(mode):
     f, preds = _grow_all("cpu", mode, missing=(mode == te.MODE_GH))
     assert f.n_trees == 2 and len(f.nodes) > 3
+
+
+def test_onebin_csr_lists_present_entries():
+    X, _ = _data(N=500, missing=True)
+    nbins = np.full(X.shape[1], 31)
+    for c in (2, 5, 7):
+        X[:, c] = torch.where(X[:, c] > 15, 0, 31).to(torch.uint8)
+        nbins[c] = 1
+    ptr, col, nf = te.onebin_csr(X, nbins, block_rows=128)
+    assert nf == 3 and ptr.numel() == 501 and col.dtype == torch.int16
+    for r in range(0, 500, 37):
+        got = col[ptr[r]:ptr[r + 1]].tolist()
+        want = [i for i, c in enumerate((2, 5, 7)) if int(X[r, c]) == 0]
+        assert got == want
 
 
 def test_cpu_engine_one_present_bin_columns():

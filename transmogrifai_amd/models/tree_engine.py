@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -188,7 +189,36 @@ class _GrowArgs(C.Structure):
                 ("job_count", C.c_void_p), ("rows", C.c_void_p), ("rows_alt", C.c_void_p),
                 ("leaf_rows", C.c_void_p), ("leaf_gid", C.c_void_p), ("n_groups", C.c_int32),
                 ("group_start", C.c_void_p), ("rng_seed", C.c_int64), ("stream", C.c_void_p),
-                ("n_bins_host", C.c_void_p)]
+                ("n_bins_host", C.c_void_p), ("csr_ptr", C.c_void_p), ("csr_col", C.c_void_p),
+                ("csr_nf", C.c_int32)]
+
+
+def onebin_csr(Xb: torch.Tensor, n_bins: np.ndarray, block_rows: int = 1 << 20):
+    """Row-wise CSR of the one-present-bin columns of ``Xb`` (``n_bins == 1``: one-hot / null indicator
+    columns under a sparse missing bin), for the histogram kernel's CSR path.
+
+    Returns ``(ptr int64 [N + 1], col int16 [max(nnz, 1)] (read as uint16), n_cols)``: the entries of
+    row ``r`` are ``col[ptr[r]:ptr[r + 1]]``, the ids (in ascending column order among the one-bin
+    columns) of its columns holding the present bin 0. None when there are none or ids do not fit."""
+    nb = np.asarray(n_bins)
+    one = np.nonzero(nb == 1)[0]
+    if one.size == 0 or one.size >= (1 << 16) or Xb.dim() != 2:
+        return None
+    dev = Xb.device
+    idx = torch.as_tensor(one, dtype=torch.int64, device=dev)
+    N = int(Xb.shape[0])
+    counts, cols = [], []
+    for r0 in range(0, N, block_rows):
+        nz = Xb[r0:r0 + block_rows].index_select(1, idx) == 0
+        counts.append(nz.sum(1))
+        cols.append(nz.nonzero()[:, 1].to(torch.int16))    # row-major: sorted by row, then column
+    ptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    if N:
+        torch.cumsum(torch.cat(counts), 0, out=ptr[1:])
+    col = torch.cat(cols) if cols else torch.empty(0, dtype=torch.int16, device=dev)
+    if col.numel() == 0:
+        col = torch.zeros(1, dtype=torch.int16, device=dev)
+    return ptr, col.contiguous(), int(one.size)
 
 
 class _Nodes:
@@ -210,13 +240,16 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 n_classes: int = 2, y: Optional[torch.Tensor] = None, t1: Optional[torch.Tensor] = None,
                 t2: Optional[torch.Tensor] = None, B: int = 32, missing_bin: int = -1,
                 subtract: bool = True, chunk_rows: int = 4096, rng_seed: int = 0,
-                collect_leaves: bool = False, groups: Optional[int] = None) -> Forest:
+                collect_leaves: bool = False, groups: Optional[int] = None, csr=None) -> Forest:
     """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``.
 
     The level loop runs natively (``ops/csrc/common/tree_grow.hpp``): on the GPU every job group gets
     its own host thread and HIP stream (default 2 groups) so one group's planning overlaps the other's
     kernels; the CPU backend grows the same groups with the same seeds, bit-identically. Per-node
     feature subsets come from a splitmix64 stream seeded with ``rng_seed + 1000003 * group``.
+
+    ``csr``: ``onebin_csr(Xb, n_bins)`` (GPU, ``MODE_GH`` with a missing bin): the one-present-bin
+    columns' histograms are then built from the rows' CSR lists (identical results, fewer loads).
 
     ``collect_leaves``: also return, as ``forest.leaf_assign``, the final leaf of every training entry
     (see ``LeafAssign``) so boosting can update margins without re-walking the new trees."""
@@ -257,11 +290,18 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         fsub=np.array([0 if j.params.feature_subset is None else int(j.params.feature_subset) for j in jobs], np.int32),
         count=np.asarray(counts, np.int64), cuts=cuts, nbins=np.ascontiguousarray(np.asarray(n_bins, np.int32)))
     hp = {k: v.ctypes.data for k, v in host.items()}
+    use_csr = (csr is not None and on_gpu and mode == MODE_GH and missing_bin > 0
+               and os.environ.get("TMOG_TREE_CSR") != "0")
+    if use_csr and (int(csr[0].numel()) != Nrows + 1 or csr[0].device != dev or csr[1].dtype != torch.int16):
+        raise ValueError("csr does not match Xb")
     a = _GrowArgs(N.ptr(Xb), Nrows, F, mode, kind, S, B, missing_bin, int(chunk_rows), int(bool(subtract)),
                   int(bool(collect_leaves)), N.ptr(yf), N.ptr(t1f), N.ptr(t2f), stride, N.ptr(qscale), N.ptr(qinv),
                   N.ptr(n_bins_t), T, hp["model"], hp["depth"], hp["inst"], hp["gain"], hp["mcw"], hp["lam"], hp["eps"],
                   hp["fsub"], hp["count"], N.ptr(rows), N.ptr(rows_alt), N.ptr(leaf_rows), N.ptr(leaf_gid), ng,
-                  hp["cuts"], int(rng_seed), N.stream(dev) if on_gpu else None, hp["nbins"])
+                  hp["cuts"], int(rng_seed), N.stream(dev) if on_gpu else None,
+                  None if os.environ.get("TMOG_TREE_PERM") == "0" else hp["nbins"],
+                  N.ptr(csr[0]) if use_csr else None, N.ptr(csr[1]) if use_csr else None,
+                  int(csr[2]) if use_csr else 0)
     lib = N.hip() if on_gpu else N.host()
     fn = (lambda name: getattr(lib, f"tmog_hip_{name}")) if on_gpu else (lambda name: getattr(lib, f"tmog_{name}_cpu"))
     h = fn("grow_forest")(C.byref(a))

@@ -511,6 +511,8 @@ class XGBoostClassifierLearner(_BoostLearner):
             os.environ.get("TMOG_XGB_FUSED", "1") != "0"
         AUC_BINS = 1 << 16
         G = H = None
+        # one-hot / null-indicator columns: histogram from the rows' CSR lists (tree_kernels.hip)
+        csr = TE.onebin_csr(Xb, spec.n_bins) if (dev.type == "cuda" and spec.missing_bin > 0) else None
         yf = yy.to(torch.float32).contiguous()
         for it in range(max(rounds)):
             act = [p for p in range(P) if it < rounds[p] and not stopped[p]]
@@ -538,7 +540,7 @@ class XGBoostClassifierLearner(_BoostLearner):
                     w = (torch.rand(r.numel(), generator=gen) < ss).to(torch.int64).to(dev)
                 tjobs.append(TE.TreeJob(p, tp, r, w))
             forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
-                                    missing_bin=spec.missing_bin, collect_leaves=True)
+                                    missing_bin=spec.missing_bin, collect_leaves=True, csr=csr)
             need = [p for p in act if esr[p] > 0]
             auc_counts = None
             if fused:

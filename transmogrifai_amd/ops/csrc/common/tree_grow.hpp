@@ -57,6 +57,11 @@ struct GrowArgs {
   int64_t rng_seed;
   void* stream;               // GPU: caller's stream (groups wait on it; it waits on the groups)
   const int32_t* n_bins_host; // host copy of n_bins (feature grouping for the histogram kernel), may be null
+  // GPU, sparse missing bin: CSR of the one-present-bin columns (row -> local ids, in n_bins order, of
+  // the columns whose bin is the present bin 0); null when absent
+  const int64_t* csr_ptr;     // [N + 1]
+  const uint16_t* csr_col;
+  int32_t csr_nf;             // number of one-present-bin columns the CSR indexes
 };
 
 struct GroupResult {
@@ -134,6 +139,7 @@ struct Staging {
 struct FeatGroup {
   int f0, nf;
   bool reg;
+  bool csr = false;
 };
 
 // n features in near-equal groups of at most 64
@@ -142,7 +148,7 @@ inline std::vector<FeatGroup> equal_groups(int n) {
   if (n <= 0) return out;
   const int ng = std::max(1, (n + 63) / 64);
   const int fg = (n + ng - 1) / ng;
-  for (int gi = 0; gi * fg < n; ++gi) out.push_back(FeatGroup{gi * fg, std::min(fg, n - gi * fg), false});
+  for (int gi = 0; gi * fg < n; ++gi) out.push_back(FeatGroup{gi * fg, std::min(fg, n - gi * fg), false, false});
   return out;
 }
 
@@ -214,8 +220,10 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
   };
 
   // Feature groups of the histogram kernel (<= 64 features each). Without per-node subsets the
-  // grouping is fixed: with a sparse missing bin (GPU, MODE 2) runs of one-present-bin columns
-  // (one-hot / null indicators) get groups of their own so the kernel accumulates them in registers.
+  // grouping is fixed: with a sparse missing bin (GPU, MODE 2) the one-present-bin columns (one-hot /
+  // null indicators) go last; given their row-wise CSR they form one group whose items walk only the
+  // present entries of each row (a few per row instead of one byte per column), otherwise groups of
+  // their own that the kernel accumulates in registers.
   // The feature order is the same on both backends (stable: multi-bin columns first, then the
   // one-present-bin columns), so split tie-breaks by local feature index stay identical GPU vs CPU.
   std::vector<FeatGroup> full_groups;
@@ -227,8 +235,12 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     for (int f = 0; f < F; ++f)
       if (a.n_bins_host[f] == 1) perm_feats.push_back(f);
     for (const FeatGroup& g : equal_groups(n_multi)) full_groups.push_back(g);
-    for (const FeatGroup& g : equal_groups(F - n_multi))
-      full_groups.push_back(FeatGroup{n_multi + g.f0, g.nf, BK::kGPU});
+    const int n_one = F - n_multi;
+    if (BK::kGPU && a.csr_ptr && a.csr_col && n_one > 0 && a.csr_nf == n_one && 2 * n_one + 2 <= 64 * (B * S + 1))
+      full_groups.push_back(FeatGroup{n_multi, n_one, false, true});   // one item walks the rows' CSR lists
+    else
+      for (const FeatGroup& g : equal_groups(n_one))
+        full_groups.push_back(FeatGroup{n_multi + g.f0, g.nf, BK::kGPU, false});
   } else {
     full_groups = equal_groups(F);
   }
@@ -352,7 +364,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
           h.node = j;
           h.fg0 = fgp.f0;
           h.nf = fgp.nf;
-          h.excl = (nch == 1 ? 1 : 0) | (fgp.reg ? 2 : 0);
+          h.excl = (nch == 1 ? 1 : 0) | (fgp.reg ? 2 : 0) | (fgp.csr ? 4 : 0);
           h.begin = nb[j] + c * a.chunk_rows;
           h.count = std::min(a.chunk_rows, cnt - c * a.chunk_rows);
           hitems.push_back(h);

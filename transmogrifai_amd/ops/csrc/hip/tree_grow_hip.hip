@@ -16,7 +16,7 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
-                        hipStream_t stream);
+                        const int64_t* csr_ptr, const uint16_t* csr_col, hipStream_t stream);
 int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
                            const int64_t* out_off, const int64_t* size, int n, int64_t max_size, hipStream_t stream);
 int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
@@ -143,7 +143,8 @@ struct GpuBackend {
                   const int64_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*) {
     if (n_items)
       kchk(tmog_hip_hist_build(g.Xb, g.F, rows, items, n_items, nfo, flist, nmd, nho, hist, g.B, g.mode, g.S, g.y,
-                               g.t1, g.t2, g.stride, g.qscale, g.mode == 2 ? g.missing_bin : -1, sl.stream),
+                               g.t1, g.t2, g.stride, g.qscale, g.mode == 2 ? g.missing_bin : -1, g.csr_ptr,
+                               g.csr_col, sl.stream),
            "hist_build");
   }
   void hist_subtract(int64_t* hist, const int64_t* prev, const int64_t* poff, const int64_t* soff,

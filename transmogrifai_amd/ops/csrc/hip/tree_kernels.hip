@@ -107,15 +107,118 @@ __device__ __forceinline__ void add_row(int* my, int bin, int S, const int4& st)
 // (common/tree_grow.hpp), so on the headline table ~40 % of the feature groups skip the atomics.
 // PMC on the tree micro-benchmark: ~0.064 LDS wave-instructions per CU-cycle at ~11 cycles each for
 // a ds_add_u32 -> the LDS atomic unit is ~70 % busy; VALU ~12 % busy, so trading atomics for VALU pays.
+// CSR path (excl bit 2, MODE 2 with a sparse missing bin): one item covers ALL one-present-bin columns
+// of a node row-chunk. Such a column's histogram has two non-zero bins -- the present bin 0 and the
+// missing bin -- and the missing bin is the chunk total minus bin 0, so only the entries with bin 0
+// matter: the row's CSR list (csr_ptr / csr_col, local column ids). The wave walks its 64 staged
+// rows one at a time with the lanes spread over that row's list (coalesced 2-byte id loads; the ids
+// of one row are distinct, so an LDS atomic wave-instruction never conflicts), four rows in flight.
+// On the headline table that is ~50 entries per row instead of ~530 byte gathers.
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
+  const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
+
+__device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t* __restrict__ rows,
+                                              const int32_t* __restrict__ node_model,
+                                              const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
+                                              int B, int S, const float* __restrict__ t1,
+                                              const float* __restrict__ t2, int64_t stride,
+                                              const float* __restrict__ qscale, int skip_bin,
+                                              const int64_t* __restrict__ csr_ptr,
+                                              const uint16_t* __restrict__ csr_col, int* lds) {
+  const int nf = it.nf;
+  int* a0 = lds;            // bin-0 sum of q(w g) per column
+  int* a1 = lds + nf;       // bin-0 sum of q(w h)
+  int* ctot = lds + 2 * nf; // chunk totals
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nwaves = blockDim.x >> 6;
+  for (int i = threadIdx.x; i < 2 * nf + 2; i += blockDim.x) lds[i] = 0;
+  __syncthreads();
+  const int64_t model = node_model ? node_model[it.node] : 0;
+  const float* qs = qscale + model * S;
+  const uint32_t* rp = rows + it.begin;
+  const int64_t cnt = it.count;
+  for (int64_t base = (int64_t)wave * 64; base < cnt; base += (int64_t)nwaves * 64) {
+    const int64_t ri = min(base + lane, cnt - 1);
+    const int nrows = (int)min((int64_t)64, cnt - base);
+    const int4 mine = stage_row<2>(rp[ri], model, stride, nullptr, t1, t2, qs);
+    const int64_t r = (uint32_t)mine.x & 0xFFFFFFu;
+    const int64_t q0 = csr_ptr[r];
+    const int64_t q1 = lane < nrows ? csr_ptr[r + 1] : q0;
+    int ta = lane < nrows ? mine.y : 0, tb = lane < nrows ? mine.z : 0;
+    for (int off = 32; off > 0; off >>= 1) {
+      ta += __shfl_xor(ta, off, 64);
+      tb += __shfl_xor(tb, off, 64);
+    }
+    if (lane == 0) {
+      atomicAdd(ctot, ta);
+      atomicAdd(ctot + 1, tb);
+    }
+    for (int j = 0; j < nrows; j += 4) {
+      int col[4], gq[4], hq[4];
+      bool ok[4];
+      int64_t e1[4], k0[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int jj = min(j + u, 63);            // rows past nrows have an empty list (q1 = q0)
+        k0[u] = readlane64(q0, jj);
+        e1[u] = readlane64(q1, jj);
+        gq[u] = __builtin_amdgcn_readlane(mine.y, jj);
+        hq[u] = __builtin_amdgcn_readlane(mine.z, jj);
+        const int64_t k = k0[u] + lane;
+        ok[u] = k < e1[u];
+        col[u] = csr_col[ok[u] ? k : k0[u] > 0 ? k0[u] - 1 : 0];   // unpredicated load of a valid id
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (ok[u]) {
+          atomicAdd(a0 + col[u], gq[u]);
+          atomicAdd(a1 + col[u], hq[u]);
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)      // lists longer than one wave
+        for (int64_t k = k0[u] + 64 + lane; k < e1[u]; k += 64) {
+          const int c = csr_col[k];
+          atomicAdd(a0 + c, gq[u]);
+          atomicAdd(a1 + c, hq[u]);
+        }
+    }
+  }
+  __syncthreads();
+  int64_t* out = hist + node_hist_off[it.node] + (int64_t)it.fg0 * B * S;
+  const int per = B * S;
+  const int words = nf * per;
+  const bool excl = (it.excl & 1) != 0;
+  for (int k = threadIdx.x; k < words; k += blockDim.x) {
+    const int f = k / per;
+    const int rem = k - f * per;
+    const int b = rem / S, s = rem - b * S;
+    int v = 0;
+    if (b == 0) v = s ? a1[f] : a0[f];
+    else if (b == skip_bin) v = ctot[s] - (s ? a1[f] : a0[f]);
+    if (excl) out[k] = v;
+    else if (v != 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + k), (unsigned long long)(int64_t)v);
+  }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(256) hist_build_kernel(
     const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const HistItem* __restrict__ items,
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
     int B, int S, const float* __restrict__ y, const float* __restrict__ t1, const float* __restrict__ t2,
-    int64_t stride, const float* __restrict__ qscale, int skip_bin) {
+    int64_t stride, const float* __restrict__ qscale, int skip_bin, const int64_t* __restrict__ csr_ptr,
+    const uint16_t* __restrict__ csr_col) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
   const HistItem it = items[blockIdx.x];
+  if (MODE == 2 && (it.excl & 4)) {
+    hist_csr_item(it, rows, node_model, node_hist_off, hist, B, S, t1, t2, stride, qscale, skip_bin, csr_ptr,
+                  csr_col, lds);
+    return;
+  }
   const int FG = it.nf;
   const int R = 64 / FG;
   const int rowstride = B * S + 1;            // padded feature row
@@ -702,23 +805,25 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
-                        hipStream_t stream) {
+                        const int64_t* csr_ptr, const uint16_t* csr_col, hipStream_t stream) {
   if (n_items == 0) return 0;
   const size_t lds = (size_t)(((64 * (B * S + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
                      TM_MAX_S * sizeof(int);
   if (lds > 160 * 1024) return -2;
   if (skip_bin >= B || (mode == 2 && skip_bin >= 0 && S != 2)) return -2;
+  if ((csr_ptr != nullptr) != (csr_col != nullptr) || (csr_ptr && (mode != 2 || skip_bin <= 0))) return -2;
   const HistItem* it = (const HistItem*)items;
   dim3 grid(n_items), block(256);
   if (mode == 0)
     hipLaunchKernelGGL(hist_build_kernel<0>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr);
   else if (mode == 1)
     hipLaunchKernelGGL(hist_build_kernel<1>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr);
   else
     hipLaunchKernelGGL(hist_build_kernel<2>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
+                       csr_col);
   return (int)hipGetLastError();
 }
 
