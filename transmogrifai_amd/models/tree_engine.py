@@ -271,7 +271,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     t2f = t2.to(device=dev, dtype=torch.float32).contiguous() if t2 is not None else None
     Xb = Xb.contiguous()
     T = len(jobs)
-    ng = groups if groups is not None else (2 if T >= 2 else 1)
+    ng = groups if groups is not None else min(T, max(1, min(8, int(os.environ.get("TMOG_TREE_GROUPS", "2")))))
     ng = max(1, min(ng, T)) if T else 1
     cuts = np.linspace(0, T, ng + 1).astype(np.int32)
     rows, counts = _root_rows(jobs, dev)

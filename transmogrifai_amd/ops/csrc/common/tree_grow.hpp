@@ -142,6 +142,8 @@ struct FeatGroup {
   bool csr = false;
 };
 
+constexpr int64_t kCsrRows = 1024;   // rows per CSR histogram item (GPU)
+
 // n features in near-equal groups of at most 64
 inline std::vector<FeatGroup> equal_groups(int n) {
   std::vector<FeatGroup> out;
@@ -353,22 +355,30 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
       b_nnf.push_back(nfeat[j]);
       b_nmd.push_back(nmd[j]);
       const int nf = nfeat[j];
-      if (nch > 1) {
+      const std::vector<FeatGroup>& grp = use_subset ? equal_groups(nf) : full_groups;
+      // CSR items take kCsrRows-row slices (each walks its rows one at a time, so shorter items keep
+      // more of them in flight); a node split over several items is zeroed and accumulated atomically
+      const int64_t ncsr = std::max<int64_t>(1, (cnt + kCsrRows - 1) / kCsrRows);
+      bool has_csr = false;
+      for (const FeatGroup& fgp : grp) has_csr |= fgp.csr;
+      if (nch > 1 || (has_csr && ncsr > 1)) {
         z_off.push_back(hoff[j]);
         z_size.push_back(hsz[j]);
       }
-      const std::vector<FeatGroup>& grp = use_subset ? equal_groups(nf) : full_groups;
-      for (int64_t c = 0; c < nch; ++c)
-        for (const FeatGroup& fgp : grp) {
+      for (const FeatGroup& fgp : grp) {
+        const int64_t step = fgp.csr ? kCsrRows : a.chunk_rows;
+        const int64_t nit = fgp.csr ? ncsr : nch;
+        for (int64_t c = 0; c < nit; ++c) {
           HistItemH h;
           h.node = j;
           h.fg0 = fgp.f0;
           h.nf = fgp.nf;
-          h.excl = (nch == 1 ? 1 : 0) | (fgp.reg ? 2 : 0) | (fgp.csr ? 4 : 0);
-          h.begin = nb[j] + c * a.chunk_rows;
-          h.count = std::min(a.chunk_rows, cnt - c * a.chunk_rows);
+          h.excl = (nit == 1 ? 1 : 0) | (fgp.reg ? 2 : 0) | (fgp.csr ? 4 : 0);
+          h.begin = nb[j] + c * step;
+          h.count = std::min(step, cnt - c * step);
           hitems.push_back(h);
         }
+      }
     }
     std::vector<int64_t> d_soff, d_ooff, d_size;
     int64_t d_max = 0;

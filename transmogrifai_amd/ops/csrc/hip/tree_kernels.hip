@@ -112,8 +112,10 @@ __device__ __forceinline__ void add_row(int* my, int bin, int S, const int4& st)
 // missing bin -- and the missing bin is the chunk total minus bin 0, so only the entries with bin 0
 // matter: the row's CSR list (csr_ptr / csr_col, local column ids). The wave walks its 64 staged
 // rows one at a time with the lanes spread over that row's list (coalesced 2-byte id loads; the ids
-// of one row are distinct, so an LDS atomic wave-instruction never conflicts), four rows in flight.
+// of one row are distinct, so an LDS atomic wave-instruction never conflicts), kCsrU rows in flight.
 // On the headline table that is ~50 entries per row instead of ~530 byte gathers.
+constexpr int kCsrU = 8;
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
   const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
@@ -157,12 +159,12 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
       atomicAdd(ctot, ta);
       atomicAdd(ctot + 1, tb);
     }
-    for (int j = 0; j < nrows; j += 4) {
-      int col[4], gq[4], hq[4];
-      bool ok[4];
-      int64_t e1[4], k0[4];
+    for (int j = 0; j < nrows; j += kCsrU) {
+      int col[kCsrU], gq[kCsrU], hq[kCsrU];
+      bool ok[kCsrU];
+      int64_t e1[kCsrU], k0[kCsrU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kCsrU; ++u) {
         const int jj = min(j + u, 63);            // rows past nrows have an empty list (q1 = q0)
         k0[u] = readlane64(q0, jj);
         e1[u] = readlane64(q1, jj);
@@ -173,13 +175,13 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
         col[u] = csr_col[ok[u] ? k : k0[u] > 0 ? k0[u] - 1 : 0];   // unpredicated load of a valid id
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < kCsrU; ++u)
         if (ok[u]) {
           atomicAdd(a0 + col[u], gq[u]);
           atomicAdd(a1 + col[u], hq[u]);
         }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)      // lists longer than one wave
+      for (int u = 0; u < kCsrU; ++u)      // lists longer than one wave
         for (int64_t k = k0[u] + 64 + lane; k < e1[u]; k += 64) {
           const int c = csr_col[k];
           atomicAdd(a0 + c, gq[u]);
@@ -461,9 +463,44 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     const double pimp = impurity_dev(tot, S, kind, &tcount);
     const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
     const int f_end = min(nf, (fb + 1) * FPB);
+    // one candidate (left statistics lq, bin b, missing direction dl) with the CPU twin's arithmetic
+    auto consider = [&](const int64_t* lq, int f, int b, int dl) {
+      double left[SM], right[SM];
+      for (int s = 0; s < S; ++s) {
+        left[s] = (double)lq[s] * q[s];
+        right[s] = (double)(totq[s] - lq[s]) * q[s];
+      }
+      double gain;
+      bool ok = true;
+      if (kind == 3) {
+        if (left[1] < mcw || right[1] < mcw) ok = false;
+        gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
+      } else {
+        double lc, rc;
+        const double li = impurity_dev(left, S, kind, &lc);
+        const double ri = impurity_dev(right, S, kind, &rc);
+        if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) ok = false;
+        gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
+        if (gain < min_gain) ok = false;
+      }
+      if (ok) {
+        Best c{gain, f, b, dl};
+        if (better(c, best)) best = c;
+      }
+    };
     for (int f = fb * FPB + wave; f < f_end; f += 4) {
       const int nb = feat_nbins[fl[f]];
       const int64_t* hf = h + (int64_t)f * B * S;
+      if (nb == 1) {
+        // one present bin (one-hot / null indicator): the only candidate is present-left,
+        // missing-right -- no scan, one lane
+        if (allow_missing && lane == 0) {
+          int64_t lq[SM];
+          for (int s = 0; s < S; ++s) lq[s] = hf[s];
+          consider(lq, f, 0, 0);
+        }
+        continue;
+      }
       int64_t v[SM], miss[SM];
       for (int s = 0; s < S; ++s) {
         v[s] = (lane < nb) ? hf[lane * S + s] : 0;
@@ -479,29 +516,9 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
       if (lane < nb - 1 + (allow_missing ? 1 : 0)) {
         for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
           if (lane == nb - 1 && dl) continue;
-          double left[SM], right[SM];
-          for (int s = 0; s < S; ++s) {
-            const int64_t lq = v[s] + (dl ? miss[s] : 0);
-            left[s] = (double)lq * q[s];
-            right[s] = (double)(totq[s] - lq) * q[s];
-          }
-          double gain;
-          bool ok = true;
-          if (kind == 3) {
-            if (left[1] < mcw || right[1] < mcw) ok = false;
-            gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
-          } else {
-            double lc, rc;
-            const double li = impurity_dev(left, S, kind, &lc);
-            const double ri = impurity_dev(right, S, kind, &rc);
-            if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) ok = false;
-            gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
-            if (gain < min_gain) ok = false;
-          }
-          if (ok) {
-            Best c{gain, f, lane, dl};
-            if (better(c, best)) best = c;
-          }
+          int64_t lq[SM];
+          for (int s = 0; s < S; ++s) lq[s] = v[s] + (dl ? miss[s] : 0);
+          consider(lq, f, lane, dl);
         }
       }
     }
