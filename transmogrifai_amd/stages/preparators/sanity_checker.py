@@ -138,6 +138,28 @@ class SanityChecker(BinaryEstimator):
                  "feature_feature_corr_level": "Computed", "correlation_exclusion": "NoExclusion",
                  "categorical_label": None, "sample_seed": 42}
 
+    # parameter domains (SanityChecker.scala param validators: ParamValidators.inRange / gtEq)
+    _ranges = {"check_sample": (0.0, 1.0, False), "min_correlation": (0.0, 1.0, True),
+               "max_correlation": (0.0, 1.0, True), "max_feature_correlation": (0.0, 1.0, True),
+               "max_cramers_v": (0.0, 1.0, True), "max_rule_confidence": (0.0, 1.0, True),
+               "min_required_rule_support": (0.0, 1.0, True)}
+
+    def set(self, name, value):
+        if name in self._ranges:
+            lo, hi, lo_incl = self._ranges[name]
+            v = float(value)
+            if not ((v >= lo if lo_incl else v > lo) and v <= hi):
+                raise ValueError(f"SanityChecker param {name} = {value} outside {'[' if lo_incl else '('}{lo}, {hi}]")
+        if name in ("sample_lower_limit", "sample_upper_limit", "min_variance") and float(value) < 0:
+            raise ValueError(f"SanityChecker param {name} must be >= 0, got {value}")
+        return super().set(name, value)
+
+    def set_input(self, *features):
+        flat = [g for f in features for g in (f if isinstance(f, (list, tuple)) else [f])]
+        if len(flat) == 2 and flat[1].is_response:
+            raise ValueError("The feature vector should not contain any response features.")
+        return super().set_input(*features)
+
     def fraction(self, total: int) -> float:
         p = self.params
         mn = min(1.0, p["sample_lower_limit"] / max(total, 1))
@@ -155,6 +177,8 @@ class SanityChecker(BinaryEstimator):
         y = label_col.values
         n_all = dp.count(X.shape[0])
         frac = self.fraction(n_all)
+        if frac <= 0.0 or n_all == 0:
+            raise ValueError("Sample size cannot be zero")
         if frac < 1.0:
             rid = ds.row_ids.to(X.device) if ds is not None else torch.arange(n_all, device=X.device)
             keep = row_uniform(rid, int(p["sample_seed"]), 9) < frac
@@ -213,7 +237,7 @@ class SanityChecker(BinaryEstimator):
         drop_names = {s["name"] for s, _ in to_drop}
         keep_idx = [c.index for c in cols if c.make_col_name() not in drop_names]
         if p["remove_bad_features"] and not keep_idx:
-            raise ValueError("The sanity checker dropped all features")
+            raise ValueError("The sanity checker has dropped all of your features, check your input data quality")
         new_meta = meta.select(keep_idx if p["remove_bad_features"] else range(d), self.get_output_feature_name())
         self.metadata["vector_metadata"] = new_meta
         self.metadata["summary"] = {
