@@ -121,3 +121,22 @@ def test_row_uniform_kernel_bit_identical():
     refm = SP.row_uniform_multi(rid, [1, 2, 3], 23)
     gotm = SP.row_uniform_multi(rid.cuda(), [1, 2, 3], 23).cpu()
     assert torch.equal(refm, gotm)
+
+
+def test_poisson_pack_kernel_matches_host():
+    """Fused bootstrap draw + root packing == the torch path, tree by tree (order-free)."""
+    from transmogrifai_amd.models import tree_engine as TE
+    from transmogrifai_amd.models.trees import bootstrap_weights_multi
+    rows = torch.arange(3, 200_003, 3, dtype=torch.int64)
+    seeds = [11, 12, 13, 14, 15]
+    pc, cc = TE.bootstrap_pack(rows, seeds, 1.0)
+    pg, cg = TE.bootstrap_pack(rows.cuda(), seeds, 1.0)
+    assert (cc == cg).all()
+    w = bootstrap_weights_multi(rows, seeds, 1.0)
+    assert (cc == (w > 0).sum(1).numpy()).all()
+    off = np.concatenate([[0], np.cumsum(cc)])
+    pg = pg.cpu()
+    for t in range(len(seeds)):
+        a, b = pc[off[t]:off[t + 1]], pg[off[t]:off[t + 1]]
+        assert torch.equal(a.sort().values, b.sort().values)
+    assert _native_loaded()

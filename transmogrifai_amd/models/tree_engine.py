@@ -149,6 +149,60 @@ def pack_rows(rows: torch.Tensor, weights: Optional[torch.Tensor]) -> torch.Tens
     return e.to(torch.int32)
 
 
+def poisson_cdf_table(rate: float) -> List[float]:
+    """Inverse-CDF steps of Poisson(rate) exactly as ``trees.bootstrap_weights_multi`` compares them."""
+    out = []
+    p = math.exp(-rate)
+    cdf = p
+    for i in range(1, 40):
+        out.append(cdf)
+        p = p * rate / i
+        cdf += p
+        if 1.0 - cdf < 1e-12:
+            break
+    return out
+
+
+def bootstrap_pack(rows: torch.Tensor, seeds: Sequence[int], rate: float):
+    """Poisson(``rate``) bootstrap of ``rows`` for one tree per seed, packed as tree-engine root
+    entries (``row | w << 24``, zero draws dropped): ``(int32 entries, int64 counts per tree)``.
+
+    Multiplicities are ``trees.bootstrap_weights_multi``'s (same per-row uniform, same CDF steps); on
+    the GPU one fused HIP kernel (``boost_kernels.hip: poisson_pack_kernel``) draws and packs."""
+    from ..tuning.splitters import row_uniform_multi, _s64
+    dev = rows.device
+    cdf = poisson_cdf_table(rate)
+    rid = rows.to(torch.int64).contiguous()
+    k, n = len(seeds), int(rid.numel())
+    if dev.type == "cuda" and n and k:
+        offs = np.asarray([_s64(int(sd) * 0x632BE59BD9B4E019 + 23 * 0x2545F4914F6CDD1D) for sd in seeds], np.int64)
+        pk = _Pack(dev)
+        i_o, i_c = pk.add(offs), pk.add(np.asarray(cdf, np.float64))
+        dv = pk.ship()
+        cnt = torch.zeros(k, dtype=torch.int64, device=dev)
+        lib = N.hip()
+        N.check(lib.tmog_hip_poisson_pack(N.ptr(rid), n, N.ptr(dv[i_o]), k, N.ptr(dv[i_c]), len(cdf), N.ptr(cnt),
+                                          None, None, N.stream(dev)), "poisson_pack count")
+        counts = cnt.cpu().numpy()
+        base = torch.as_tensor(np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64), device=dev)
+        out = torch.empty(max(int(counts.sum()), 1), dtype=torch.int32, device=dev)
+        cnt.zero_()
+        N.check(lib.tmog_hip_poisson_pack(N.ptr(rid), n, N.ptr(dv[i_o]), k, N.ptr(dv[i_c]), len(cdf), N.ptr(cnt),
+                                          N.ptr(base), N.ptr(out), N.stream(dev)), "poisson_pack")
+        return out[:int(counts.sum())], counts.astype(np.int64)
+    u = row_uniform_multi(rid, seeds, 23)
+    w = torch.zeros(u.shape, dtype=torch.int64, device=dev)
+    for c in cdf:
+        w += (u >= c).to(torch.int64)
+    parts, counts = [], []
+    for t in range(k):
+        keep = w[t] > 0
+        parts.append(pack_rows(rid[keep], w[t][keep]))
+        counts.append(int(keep.sum()))
+    out = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int32, device=dev)
+    return out, np.asarray(counts, np.int64)
+
+
 def _root_rows(jobs, dev):
     """Packed root entries of every job, zero-weight (out-of-bag) rows dropped for all weighted jobs
     with one compaction (two host syncs per call instead of one per tree)."""
@@ -240,13 +294,16 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 n_classes: int = 2, y: Optional[torch.Tensor] = None, t1: Optional[torch.Tensor] = None,
                 t2: Optional[torch.Tensor] = None, B: int = 32, missing_bin: int = -1,
                 subtract: bool = True, chunk_rows: int = 4096, rng_seed: int = 0,
-                collect_leaves: bool = False, groups: Optional[int] = None, csr=None) -> Forest:
+                collect_leaves: bool = False, groups: Optional[int] = None, csr=None, root=None) -> Forest:
     """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``.
 
     The level loop runs natively (``ops/csrc/common/tree_grow.hpp``): on the GPU every job group gets
     its own host thread and HIP stream (default 2 groups) so one group's planning overlaps the other's
     kernels; the CPU backend grows the same groups with the same seeds, bit-identically. Per-node
     feature subsets come from a splitmix64 stream seeded with ``rng_seed + 1000003 * group``.
+
+    ``root``: pre-packed root entries ``(int32 tensor, counts per job)`` (e.g. from ``bootstrap_pack``),
+    used instead of the jobs' rows / weights; the tensor is consumed (the grower partitions it in place).
 
     ``csr``: ``onebin_csr(Xb, n_bins)`` (GPU, ``MODE_GH`` with a missing bin): the one-present-bin
     columns' histograms are then built from the rows' CSR lists (identical results, fewer loads).
@@ -274,7 +331,12 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     ng = groups if groups is not None else min(T, max(1, min(8, int(os.environ.get("TMOG_TREE_GROUPS", "2")))))
     ng = max(1, min(ng, T)) if T else 1
     cuts = np.linspace(0, T, ng + 1).astype(np.int32)
-    rows, counts = _root_rows(jobs, dev)
+    if root is not None:
+        rows, counts = root[0].to(device=dev, dtype=torch.int32).contiguous(), [int(c) for c in root[1]]
+        if len(counts) != len(jobs) or sum(counts) != int(rows.numel()):
+            raise ValueError("root entries do not match the jobs")
+    else:
+        rows, counts = _root_rows(jobs, dev)
     rows_alt = torch.empty_like(rows)
     qscale, qinv = _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev)
     total = int(rows.numel())

@@ -186,6 +186,13 @@ class _ForestLearner(Learner):
                     yg = y.to(dev).index_select(0, U)
                     jrows = {i: r for i, r in zip(idxs, parts)}
             tjobs, owner = [], []
+            # Bootstraps are drawn per (training rows, seed): grid points of one CV fold share theirs,
+            # as Spark RF does for equal seeds on equal data (one draw per fold instead of per grid point)
+            forests_only = self.is_forest and all(
+                int(jobs[i].params.get("num_trees", self.default_trees)) > 1 for i in idxs)
+            boot: Dict[tuple, tuple] = {}
+            row_keys: Dict[tuple, int] = {}
+            root_parts, root_counts = [], []
             for i in idxs:
                 p = jobs[i].params
                 nt = int(p.get("num_trees", self.default_trees)) if self.is_forest else 1
@@ -194,8 +201,23 @@ class _ForestLearner(Learner):
                 tp = TE.TreeParams(max_depth=int(p.get("max_depth", 5)),
                                    min_instances=float(p.get("min_instances_per_node", 1)),
                                    min_info_gain=float(p.get("min_info_gain", 0.0)), feature_subset=sub)
-                seed = int(p.get("seed", 0)) + 7919 * i
                 rate = float(p.get("subsampling_rate", 1.0))
+                if forests_only:
+                    src = jobs[i].rows
+                    rk = ("all",) if src is None else (src.data_ptr(), int(src.numel()), str(src.device))
+                    seed = int(p.get("seed", 0)) + 7919 * row_keys.setdefault(rk, len(row_keys))
+                    key = (rk, seed, nt, rate)
+                    if key not in boot:
+                        packed, cnts = TE.bootstrap_pack(rows, [seed * 1009 + t for t in range(nt)], rate)
+                        boot[key] = (packed, cnts, np.concatenate([[0], np.cumsum(cnts)]))
+                    packed, cnts, offs = boot[key]
+                    for t in range(nt):
+                        root_parts.append(packed[int(offs[t]):int(offs[t + 1])])
+                        root_counts.append(int(cnts[t]))
+                        tjobs.append(TE.TreeJob(0, tp, rows, None, seed + t))
+                        owner.append(i)
+                    continue
+                seed = int(p.get("seed", 0)) + 7919 * i
                 wall = bootstrap_weights_multi(rows, [seed * 1009 + t for t in range(nt)], rate) if nt > 1 else None
                 for t in range(nt):
                     if nt > 1:
@@ -206,14 +228,15 @@ class _ForestLearner(Learner):
                         w = jobs[i].weights.to(dev).round().to(torch.int64) if jobs[i].weights is not None else None
                     tjobs.append(TE.TreeJob(0, tp, rows, w, seed + t))
                     owner.append(i)
+            root = (torch.cat(root_parts), root_counts) if forests_only and root_parts else None
             if self.classification:
                 forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_CLS,
                                         kind=TE.KINDS[jobs[idxs[0]].params.get("impurity", "gini")], n_classes=K,
-                                        y=yg, B=mb, rng_seed=int(jobs[idxs[0]].params.get("seed", 0)))
+                                        y=yg, B=mb, rng_seed=int(jobs[idxs[0]].params.get("seed", 0)), root=root)
             else:
                 forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_VAR, kind=TE.KIND_VARIANCE,
                                         t1=yg.to(torch.float32)[None, :], B=mb,
-                                        rng_seed=int(jobs[idxs[0]].params.get("seed", 0)))
+                                        rng_seed=int(jobs[idxs[0]].params.get("seed", 0)), root=root)
             owner = np.asarray(owner)
             for i in idxs:
                 ts = np.nonzero(owner == i)[0]

@@ -11,6 +11,14 @@
 // Every (job, row) pair occurs exactly once among a round's entries, so the margin / gradient
 // stores need no atomics; the AuPR table uses integer atomics (exact, order-independent).
 //
+// poisson_pack_kernel -- Poisson(rate) bootstrap multiplicities (Spark RF BaggedPoint with
+// replacement) for k trees over one row list, fused with the tree engine's root packing: the uniform
+// is row_uniform's, the count is the number of inverse-CDF steps it passes (the host ships the exact
+// CDF table of trees.bootstrap_weights_multi), rows drawn zero times are dropped and the rest written
+// as packed entries (row | w << 24) -- one pass instead of ~20 int64 [k, n] torch ops plus a
+// compaction per forest. Two launches: count (per-tree totals) and pack (block-reserved output slots;
+// the order inside a tree is not significant: histograms are exact integer sums).
+//
 // row_uniform_kernel -- the splitmix64 per-(seed, stream, global row id) uniform of
 // tuning/splitters.row_uniform (hold-out split, CV folds, down-sampling, bootstrap, sanity-check
 // sample) as one fused pass instead of ~12 int64 elementwise torch kernels; bit-identical results.
@@ -53,6 +61,53 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
   }
 }
 
+__device__ __forceinline__ double splitmix_uniform(uint64_t rid, uint64_t off) {
+  const uint64_t M63 = 0x7FFFFFFFFFFFFFFFull;
+  uint64_t x = rid * 0x1E3779B97F4A7C15ull + off;
+  x &= M63;
+  x = ((x ^ (x >> 30)) * 0x2F58476D1CE4E5B9ull) & M63;
+  x = ((x ^ (x >> 27)) * 0x14C3124B4B69A5C5ull) & M63;
+  x = x ^ (x >> 31);
+  return (double)(x >> 10) / 9007199254740992.0;
+}
+
+__global__ void __launch_bounds__(256) poisson_pack_kernel(const int64_t* __restrict__ rows, int64_t n,
+                                                           const int64_t* __restrict__ offsets,
+                                                           const double* __restrict__ cdf, int ncdf,
+                                                           unsigned long long* __restrict__ counts,
+                                                           const int64_t* __restrict__ base,
+                                                           int32_t* __restrict__ out) {
+  const int t = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int w = 0;
+  uint32_t r = 0;
+  if (i < n) {
+    r = (uint32_t)rows[i];
+    const double u = splitmix_uniform((uint64_t)rows[i], (uint64_t)offsets[t]);
+    for (int c = 0; c < ncdf; ++c) w += (u >= cdf[c]) ? 1 : 0;
+  }
+  const bool keep = w > 0;
+  const unsigned long long m = __ballot(keep);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int pre = __popcll(m & ((1ull << lane) - 1ull));
+  __shared__ int wtot[4];
+  __shared__ unsigned long long blk;
+  if (lane == 0) wtot[wv] = __popcll(m);
+  __syncthreads();
+  int wbase = 0, tot = 0;
+  for (int k = 0; k < 4; ++k) {
+    if (k < wv) wbase += wtot[k];
+    tot += wtot[k];
+  }
+  if (out == nullptr) {
+    if (threadIdx.x == 0 && tot) atomicAdd(counts + t, (unsigned long long)tot);
+    return;
+  }
+  if (threadIdx.x == 0) blk = tot ? atomicAdd(counts + t, (unsigned long long)tot) : 0ull;
+  __syncthreads();
+  if (keep) out[base[t] + (int64_t)blk + wbase + pre] = (int32_t)(r | ((uint32_t)min(w, 255) << 24));
+}
+
 __global__ void __launch_bounds__(256) row_uniform_kernel(const int64_t* __restrict__ row_ids, int64_t n,
                                                           const int64_t* __restrict__ offsets, int k_seeds,
                                                           double* __restrict__ out) {
@@ -83,6 +138,17 @@ int tmog_hip_boost_epilogue(const uint32_t* entries, const int32_t* gid, int64_t
   hipLaunchKernelGGL(boost_epilogue_kernel, dim3((unsigned)((n_entries + 255) / 256)), dim3(256), 0, stream, entries,
                      gid, n_entries, gid_value, gid_tree, tree_job, N, F, G, H, y, objective, auc_hist, bins, n_gid,
                      n_trees, P);
+  return (int)hipGetLastError();
+}
+
+// counts[k] must be zero. out == nullptr: count pass (counts = kept rows per tree); otherwise pack
+// pass with base[k] = first output slot of tree k (counts, re-zeroed, act as the slot cursors).
+int tmog_hip_poisson_pack(const int64_t* rows, int64_t n, const int64_t* offsets, int k, const double* cdf, int ncdf,
+                          unsigned long long* counts, const int64_t* base, int32_t* out, hipStream_t stream) {
+  if (n == 0 || k == 0) return 0;
+  if (n >= (1 << 24) || k > 65535 || ncdf > 64 || (out != nullptr && base == nullptr)) return -2;
+  hipLaunchKernelGGL(poisson_pack_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)k), dim3(256), 0, stream, rows,
+                     n, offsets, cdf, ncdf, counts, base, out);
   return (int)hipGetLastError();
 }
 
