@@ -686,14 +686,17 @@ __global__ void __launch_bounds__(256) leaf_collect_kernel(const uint32_t* __res
 
 // ------------------------------------------------------------------------------------- predict
 // LDS-row variant (F <= 512): the workgroup first copies its 128 rows' bins (row-major, F bytes each)
-// into LDS with coalesced byte loads, then every lane walks its model's trees reading bins from LDS,
-// eight trees interleaved. Without it each tree step paid a dependent L2/Infinity-cache round trip for
+// into LDS with coalesced byte loads, then four lanes per row each walk a quarter of the model's
+// trees (chunks of eight interleaved) reading bins from LDS, and the four partial sums are folded in a
+// fixed order. 512-thread workgroups keep 16 waves per CU busy on the dependent node-fetch chains
+// (128-thread groups left 4 waves per CU with the 64 KB of staged rows). Without it each tree step paid a dependent L2/Infinity-cache round trip for
 // a single byte (64 lanes = 64 different rows = 64 cache lines per step); now only the node fetch
 // (shared by the wave near the root, L2/L1 resident) stays global. grid.y = model.
 constexpr int PRED_ROWS = 128;
 constexpr int PRED_TU = 8;
+constexpr int PRED_TPR = 4;   // threads per row (tree slices), 512-thread workgroups sharing the staged rows
 
-__global__ void __launch_bounds__(PRED_ROWS) forest_predict_lds_kernel(
+__global__ void __launch_bounds__(PRED_ROWS * PRED_TPR) forest_predict_lds_kernel(
     const uint8_t* __restrict__ Xb, int F, const int64_t* __restrict__ model_row_off,
     const int32_t* __restrict__ row_list, const int64_t* __restrict__ model_tree_off,
     const int64_t* __restrict__ tree_off, const float* __restrict__ tree_weight, const int4* __restrict__ nodes,
@@ -705,51 +708,63 @@ __global__ void __launch_bounds__(PRED_ROWS) forest_predict_lds_kernel(
   const int64_t blk0 = r0 + (int64_t)blockIdx.x * PRED_ROWS;
   if (blk0 >= r1) return;                                   // whole workgroup out of range (uniform)
   const int nrow = (int)min((int64_t)PRED_ROWS, r1 - blk0);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int r = wave; r < nrow; r += PRED_ROWS / 64) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  for (int r = wave; r < nrow; r += nwaves) {
     const int64_t row = row_list ? row_list[blk0 + r] : (blk0 + r - r0);
     const uint8_t* src = Xb + row * F;
     for (int b = lane; b < F; b += 64) srows[r * F + b] = src[b];
   }
   __syncthreads();
-  if ((int)threadIdx.x >= nrow) return;
-  const uint8_t* xr = srows + threadIdx.x * F;
+  // thread (rr, q): row rr of the block, tree chunks q, q + PRED_TPR, ... of PRED_TU trees each
+  const int rr = threadIdx.x % PRED_ROWS, q = threadIdx.x / PRED_ROWS;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int64_t t_end = model_tree_off[m + 1];
-  int64_t t = model_tree_off[m];
-  for (; t < t_end; t += PRED_TU) {
-    const int nu = (int)min((int64_t)PRED_TU, t_end - t);
-    int64_t k[PRED_TU];
-    int4 nd[PRED_TU];
-#pragma unroll
-    for (int u = 0; u < PRED_TU; ++u) {
-      k[u] = u < nu ? tree_off[t + u] : tree_off[t];
-      nd[u] = nodes[k[u]];
-    }
-    bool active = true;
-    while (active) {
-      active = false;
+  if (rr < nrow) {
+    const uint8_t* xr = srows + rr * F;
+    const int64_t t_end = model_tree_off[m + 1];
+    for (int64_t t = model_tree_off[m] + (int64_t)q * PRED_TU; t < t_end; t += (int64_t)PRED_TU * PRED_TPR) {
+      const int nu = (int)min((int64_t)PRED_TU, t_end - t);
+      int64_t k[PRED_TU];
+      int4 nd[PRED_TU];
 #pragma unroll
       for (int u = 0; u < PRED_TU; ++u) {
-        if (nd[u].z >= 0) {
-          const uint8_t b = xr[nd[u].x];
-          const bool gl = (missing_bin >= 0 && b == missing_bin) ? (default_left[k[u]] != 0) : ((int)b <= nd[u].y);
-          k[u] = gl ? nd[u].z : nd[u].w;
-          nd[u] = nodes[k[u]];
-          active = true;
+        k[u] = u < nu ? tree_off[t + u] : tree_off[t];
+        nd[u] = nodes[k[u]];
+      }
+      bool active = true;
+      while (active) {
+        active = false;
+#pragma unroll
+        for (int u = 0; u < PRED_TU; ++u) {
+          if (nd[u].z >= 0) {
+            const uint8_t b = xr[nd[u].x];
+            const bool gl = (missing_bin >= 0 && b == missing_bin) ? (default_left[k[u]] != 0) : ((int)b <= nd[u].y);
+            k[u] = gl ? nd[u].z : nd[u].w;
+            nd[u] = nodes[k[u]];
+            active = true;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PRED_TU; ++u) {
+        if (u < nu) {
+          const float w = tree_weight[t + u];
+          for (int c = 0; c < K && c < 8; ++c) acc[c] += w * leaf_value[k[u] * K + c];
         }
       }
     }
-#pragma unroll
-    for (int u = 0; u < PRED_TU; ++u) {
-      if (u < nu) {
-        const float w = tree_weight[t + u];
-        for (int c = 0; c < K && c < 8; ++c) acc[c] += w * leaf_value[k[u] * K + c];
-      }
+  }
+  // fold the PRED_TPR partial sums in q order (deterministic)
+  float* red = reinterpret_cast<float*>(srows + ((PRED_ROWS * F + 15) & ~15));
+  for (int c = 0; c < 8; ++c) red[(q * PRED_ROWS + rr) * 8 + c] = acc[c];
+  __syncthreads();
+  if (q == 0 && rr < nrow) {
+    float* o = out + (blk0 + rr) * K;
+    for (int c = 0; c < K && c < 8; ++c) {
+      float v = red[rr * 8 + c];
+      for (int qq = 1; qq < PRED_TPR; ++qq) v += red[(qq * PRED_ROWS + rr) * 8 + c];
+      o[c] = v;
     }
   }
-  float* o = out + (blk0 + threadIdx.x) * K;
-  for (int c = 0; c < K && c < 8; ++c) o[c] = acc[c];
 }
 
 // grid.y = model; each thread walks every tree of its model for one of the model's rows.
@@ -921,7 +936,8 @@ int tmog_hip_forest_predict(const uint8_t* Xb, int F, int n_models, const int64_
   if (K > 8) return -2;
   if ((size_t)PRED_ROWS * F <= 64 * 1024) {
     dim3 g2((unsigned)((max_rows + PRED_ROWS - 1) / PRED_ROWS), n_models);
-    hipLaunchKernelGGL(forest_predict_lds_kernel, g2, dim3(PRED_ROWS), (size_t)PRED_ROWS * F, stream, Xb, F,
+    const size_t lds = (((size_t)PRED_ROWS * F + 15) & ~(size_t)15) + sizeof(float) * 8 * PRED_ROWS * PRED_TPR;
+    hipLaunchKernelGGL(forest_predict_lds_kernel, g2, dim3(PRED_ROWS * PRED_TPR), lds, stream, Xb, F,
                        model_row_off, row_list, model_tree_off, tree_off, tree_weight, (const int4*)nodes,
                        default_left, missing_bin, leaf_value, K, out);
     return (int)hipGetLastError();
