@@ -313,6 +313,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     dev = Xb.device
     on_gpu = dev.type == "cuda"
     Nrows, F = int(Xb.shape[0]), int(Xb.shape[1])
+    chunk_rows = int(os.environ.get("TMOG_TREE_CHUNK", chunk_rows))
     if Nrows >= MAX_ROWS:
         raise ValueError(f"tree engine supports < {MAX_ROWS} rows per training set, got {Nrows}")
     S = n_classes if mode == MODE_CLS else (3 if mode == MODE_VAR else 2)

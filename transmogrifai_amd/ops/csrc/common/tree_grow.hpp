@@ -143,6 +143,7 @@ struct FeatGroup {
 };
 
 constexpr int64_t kCsrRows = 1024;   // rows per CSR histogram item (GPU)
+constexpr int64_t kPartRows = 1024;  // rows per partition item (GPU)
 
 // n features in near-equal groups of at most 64
 inline std::vector<FeatGroup> equal_groups(int n) {
@@ -338,12 +339,13 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     for (int j = 0; j < m; ++j) {
       const int64_t cnt = nc[j];
       const int64_t nch = std::max<int64_t>(1, (cnt + a.chunk_rows - 1) / a.chunk_rows);
-      for (int64_t c = 0; c < nch; ++c) {
+      // partition items: short slices (each is a chain of 256-row steps with cursor atomics)
+      for (int64_t c = 0, npi = std::max<int64_t>(1, (cnt + kPartRows - 1) / kPartRows); c < npi; ++c) {
         PartItemH p;
         p.node = j;
         p.pad = 0;
-        p.begin = nb[j] + c * a.chunk_rows;
-        p.count = std::min(a.chunk_rows, cnt - c * a.chunk_rows);
+        p.begin = nb[j] + c * kPartRows;
+        p.count = std::min(kPartRows, cnt - c * kPartRows);
         p.out_left = p.out_right = 0;
         citems.push_back(p);
       }
