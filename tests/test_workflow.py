@@ -1,0 +1,96 @@
+"""Workflow-level integration (OpWorkflowTest.scala, OpWorkflowCVTest.scala:299-345, ModelInsightsTest.scala):
+model insights extraction + JSON round trip + pretty print, summaries, workflow-level CV, and
+``saveScores`` in every output format (Avro read back with the framework's own reader)."""
+import json
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from transmogrifai_amd.evaluators.evaluators import Evaluators
+from transmogrifai_amd.insights.model_insights import ModelInsights
+
+from test_local_scoring import _records, _workflow
+
+
+@pytest.fixture(scope="module")
+def trained():
+    recs = _records(n=400, seed=2)
+    wf, pred = _workflow()
+    model = wf.set_input_dataset(recs).train()
+    return model, pred, recs
+
+
+def test_model_insights_extract_roundtrip_and_pretty(trained):
+    model, pred, _ = trained
+    mi = model.model_insights(pred)
+    assert mi.label.labelName == "survived"
+    names = {f.featureName for f in mi.features}
+    assert {"age", "fare", "sex"} <= names
+    fare = next(f for f in mi.features if f.featureName == "fare")
+    assert fare.derivedFeatures and all(d.stagesApplied for d in fare.derivedFeatures)
+    assert any(d.corr is not None for d in fare.derivedFeatures)
+    assert mi.selectedModelInfo is not None
+    js = mi.to_json()
+    back = ModelInsights.from_json(js)
+    assert back.to_json_dict() == json.loads(js)
+    text = mi.pretty_print()
+    assert "fare" in text
+
+
+def test_summaries(trained):
+    model, pred, _ = trained
+    summ = model.summary_json()
+    assert summ and all(isinstance(v, dict) for v in summ.values())
+    assert json.loads(model.summary())
+    assert isinstance(model.summary_pretty(), str) and model.summary_pretty()
+
+
+@pytest.mark.parametrize("fmt", ["parquet", "csv", "json", "avro"])
+def test_save_scores_formats(trained, tmp_path, fmt):
+    model, pred, recs = trained
+    ev = Evaluators.BinaryClassification.auPR()
+    ev.set_label_col(model.result_features[0]).set_prediction_col(pred)
+    scores, metrics = model.save_scores(str(tmp_path / "scores"), recs, evaluator=ev,
+                                        metrics_path=str(tmp_path / "metrics.json"), fmt=fmt)
+    assert metrics["AuPR"] > 0.5 and json.load(open(tmp_path / "metrics.json"))["AuPR"] == metrics["AuPR"]
+    files = os.listdir(tmp_path / "scores")
+    assert len(files) == 1
+    path = str(tmp_path / "scores" / files[0])
+    if fmt == "parquet":
+        n = len(pd.read_parquet(path))
+    elif fmt == "csv":
+        n = len(pd.read_csv(path))
+    elif fmt == "json":
+        n = len(pd.read_json(path, lines=True))
+    else:
+        from transmogrifai_amd.readers.avro import read_avro
+        rows = read_avro(path)
+        n = len(rows)
+        first = json.loads(rows[0][pred.name])
+        assert "prediction" in first and "probability_1" in first
+    assert n == len(recs)
+
+
+def test_workflow_cv_trains_and_scores():
+    from transmogrifai_amd.dsl import transmogrify
+    from transmogrifai_amd.features.builder import FeatureBuilder
+    from transmogrifai_amd.selector.factories import BinaryClassificationModelSelector
+    from transmogrifai_amd.workflow.workflow import OpWorkflow
+    recs = _records(n=400, seed=5)
+    survived = FeatureBuilder.RealNN("survived").as_response()
+    feats = [FeatureBuilder.Real("age").as_predictor(), FeatureBuilder.Real("fare").as_predictor(),
+             FeatureBuilder.PickList("sex").as_predictor()]
+    vec = transmogrify(feats)
+    checked = survived.sanity_check(vec, remove_bad_features=True)
+    pred = BinaryClassificationModelSelector.with_cross_validation(
+        model_types_to_use=["OpLogisticRegression"], num_folds=3, seed=1).set_input(survived, checked).get_output()
+    wf = OpWorkflow().set_result_features(survived, pred).set_input_dataset(recs).with_workflow_cv()
+    model = wf.train()
+    out = model.score(recs)[pred.name].to_list()
+    probs = np.array([o["probability_1"] for o in out])
+    assert probs.shape == (400,) and ((probs >= 0) & (probs <= 1)).all()
+    ev = Evaluators.BinaryClassification.auROC()
+    ev.set_label_col(survived).set_prediction_col(pred)
+    assert model.evaluate(ev, recs)["AuROC"] > 0.6

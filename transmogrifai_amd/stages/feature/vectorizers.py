@@ -271,10 +271,16 @@ class OpOneHotVectorizerModel(VectorizerMixin, SequenceTransformer):
 
 @register_stage
 class OpTextPivotVectorizer(VectorizerMixin, SequenceEstimator):
-    """One-hot pivot of text/categorical values (topK by count with min support)."""
+    """One-hot pivot of text/categorical values (topK by count with min support).
+
+    ``max_pct_cardinality`` drops a column whose distinct-value count reaches that fraction of the rows
+    (OpOneHotVectorizer.scala:75-124). The reference estimates the cardinality with an Algebird
+    HyperLogLog of ``hll_bits`` bits (~1.04 / sqrt(2^bits) error); here the distinct count comes exactly
+    from the (all-reduced) value counts the fit already holds, so ``hll_bits`` is accepted for parity
+    and has no effect."""
     operation_name = "pivotText"
     _defaults = {"top_k": 20, "min_support": 10, "clean_text": True, "track_nulls": True,
-                 "unseen_name": OTHER_STRING, "max_pct_cardinality": 1.0}
+                 "unseen_name": OTHER_STRING, "max_pct_cardinality": 1.0, "hll_bits": 12}
 
     def _counts(self, c):
         return _text_counts(c, self.params["clean_text"]) if isinstance(c, TextColumn) else \

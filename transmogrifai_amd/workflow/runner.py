@@ -140,7 +140,7 @@ def _default(o):
 
 
 def save_dataset(ds, path: str, fmt: str = "parquet") -> str:
-    """Write a scored / computed dataset (key + columns) as Parquet, CSV or JSON lines."""
+    """Write a scored / computed dataset (key + columns) as Parquet, CSV, Avro or JSON lines."""
     os.makedirs(path, exist_ok=True)
     df = ds.to_pandas()
     for c in df.columns:
@@ -152,6 +152,26 @@ def save_dataset(ds, path: str, fmt: str = "parquet") -> str:
     elif fmt == "csv":
         out = os.path.join(path, "part-00000.csv")
         df.to_csv(out, index=False)
+    elif fmt == "avro":
+        # the reference's default score format (Avro container, deflate); complex values JSON-encoded
+        from ..readers.avro import write_avro
+        import numpy as np
+        fields, conv = [], []
+        for c in df.columns:
+            num = df[c].map(lambda v: v is None or isinstance(v, (int, float, bool, np.integer, np.floating))).all()
+            fields.append({"name": str(c), "type": ["null", "double" if num else "string"], "default": None})
+            conv.append(num)
+        recs = []
+        for row in df.itertuples(index=False):
+            r = {}
+            for f, num, v in zip(fields, conv, row):
+                if v is None or (isinstance(v, float) and v != v):
+                    r[f["name"]] = None
+                else:
+                    r[f["name"]] = float(v) if num else str(v)
+            recs.append(r)
+        out = os.path.join(path, "part-00000.avro")
+        write_avro(out, {"type": "record", "name": "OpScores", "fields": fields}, recs)
     else:
         out = os.path.join(path, "part-00000.json")
         df.to_json(out, orient="records", lines=True)

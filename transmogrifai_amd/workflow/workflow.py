@@ -324,6 +324,23 @@ class OpWorkflowModel(OpWorkflowCore):
         scores = self.score(data, keep_raw_features=True, **kw)
         return scores, self.evaluate_scores(evaluator, scores)
 
+    def save_scores(self, path: str, data=None, evaluator=None, metrics_path: Optional[str] = None,
+                    fmt: str = "parquet", keep_raw_features: bool = False):
+        """Score and write the result features to ``path`` (``OpWorkflowModel.saveScores``,
+        ``OpWorkflowModel.scala:381-428``); with ``evaluator`` also evaluate, writing the metrics JSON
+        to ``metrics_path`` when given. ``fmt``: parquet | csv | json | avro. Returns (scores, metrics)."""
+        from .runner import _write_json, save_dataset
+        if evaluator is not None:
+            scores, metrics = self.score_and_evaluate(evaluator, data)
+            if not keep_raw_features:
+                scores = scores.select([f.name for f in self.result_features if f.name in scores])
+        else:
+            scores, metrics = self.score(data, keep_raw_features=keep_raw_features), None
+        save_dataset(scores, path, fmt)
+        if metrics is not None and metrics_path:
+            _write_json(metrics_path, metrics)
+        return scores, metrics
+
     def evaluate(self, evaluator, data=None):
         return self.score_and_evaluate(evaluator, data)[1]
 
