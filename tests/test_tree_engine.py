@@ -189,3 +189,29 @@ def test_hip_predict_many_classes_matches_host():
     pg = te.forest_predict(f, X.cuda(), [None if r is None else r.cuda() for r in rows], [[0, 1, 2], [3, 4]])
     for a, b in zip(pc, pg):
         torch.testing.assert_close(a, b.cpu(), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", [te.MODE_CLS, te.MODE_VAR, te.MODE_GH])
+def test_native_finalize_matches_numpy(mode, monkeypatch):
+    """tmog_tree_finalize_cpu == _finalize_py array for array (values, gamma pruning, regrouping, gid values)."""
+    X, y = _data(N=3000, missing=(mode == te.MODE_GH))
+    g = torch.Generator().manual_seed(4)
+    G = torch.randn(3, X.shape[0], generator=g)
+    H = torch.rand(3, X.shape[0], generator=g) * 0.25
+    jobs = [te.TreeJob(k, te.TreeParams(max_depth=6, min_instances=3, reg_lambda=1.0 + k, gamma=1.5 * k, eta=0.3,
+                                        min_child_weight=0.5, split_eps=1e-6), torch.arange(k, 3000, 1 + k))
+            for k in range(3)]
+    kind = {te.MODE_CLS: te.KIND_GINI, te.MODE_VAR: te.KIND_VARIANCE, te.MODE_GH: te.KIND_NEWTON}[mode]
+    kw = dict(mode=mode, kind=kind, y=y, t1=G if mode != te.MODE_CLS else None, t2=H if mode == te.MODE_GH else None,
+              B=32, missing_bin=31 if mode == te.MODE_GH else -1, collect_leaves=(mode == te.MODE_GH))
+    if mode == te.MODE_VAR:
+        kw["t1"] = G[:1]
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TMOG_FINALIZE_PY", flag)
+        out.append(te.grow_forest(X, np.full(10, 31 if mode == te.MODE_GH else 32), jobs, **kw))
+    a, b = out
+    for name in ("tree_off", "nodes", "default_left", "value", "gain", "cover", "tree_model"):
+        np.testing.assert_array_equal(getattr(a, name), getattr(b, name), err_msg=name)
+    if mode == te.MODE_GH:
+        assert torch.equal(a.leaf_assign.value.cpu(), b.leaf_assign.value.cpu())

@@ -483,6 +483,37 @@ def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev):
 
 
 def _finalize(jobs, G: "_Nodes", mode, kind, K, S, missing_bin, with_gid_values: bool = False):
+    """Created nodes -> Forest (values, gamma pruning, per-tree regrouping): native
+    ``tmog_tree_finalize_cpu`` (ops/csrc/host/tree_cpu.cpp), array-identical to ``_finalize_py``."""
+    if os.environ.get("TMOG_FINALIZE_PY") == "1":
+        return _finalize_py(jobs, G, mode, kind, K, S, missing_bin, with_gid_values)
+    n = G.n
+    T = len(jobs)
+    lam = np.ascontiguousarray([j.params.reg_lambda for j in jobs], np.float64)
+    eta = np.ascontiguousarray([j.params.eta for j in jobs], np.float64)
+    gam = np.ascontiguousarray([j.params.gamma for j in jobs], np.float64)
+    tree_off = np.empty(T + 1, np.int64)
+    nodes = np.empty((max(n, 1), 4), np.int32)
+    dl = np.empty(max(n, 1), np.uint8)
+    value = np.empty((max(n, 1), K), np.float32)
+    gain = np.empty(max(n, 1), np.float32)
+    cover = np.empty(max(n, 1), np.float32)
+    gid_value = np.empty((max(n, 1), K), np.float32) if with_gid_values else None
+    tot = np.ascontiguousarray(G.tot[:n])
+    m = int(N.host().tmog_tree_finalize_cpu(
+        n, T, G.tree.ctypes.data, G.feat.ctypes.data, G.bin.ctypes.data, G.dl.ctypes.data, G.gain.ctypes.data,
+        tot.ctypes.data, S, G.left.ctypes.data, G.right.ctypes.data, mode, kind, K, lam.ctypes.data,
+        eta.ctypes.data, gam.ctypes.data, int(bool(with_gid_values)), tree_off.ctypes.data, nodes.ctypes.data,
+        dl.ctypes.data, value.ctypes.data, gain.ctypes.data, cover.ctypes.data,
+        gid_value.ctypes.data if with_gid_values else None))
+    f = Forest(tree_off, nodes[:m].copy(), dl[:m].copy(), value[:m].copy(), gain[:m].copy(), cover[:m].copy(),
+               np.array([j.model for j in jobs], np.int32), missing_bin)
+    if with_gid_values:
+        f._gid_value, f._gid_tree = gid_value[:n], G.tree[:n].astype(np.int64)
+    return f
+
+
+def _finalize_py(jobs, G: "_Nodes", mode, kind, K, S, missing_bin, with_gid_values: bool = False):
     n = G.n
     tot = G.tot[:n]
     left = G.left[:n].copy()

@@ -534,6 +534,7 @@ class XGBoostClassifierLearner(_BoostLearner):
             os.environ.get("TMOG_XGB_FUSED", "1") != "0"
         AUC_BINS = 1 << 16
         G = H = None
+        root_cache: Dict[tuple, tuple] = {}
         # one-hot / null-indicator columns: histogram from the rows' CSR lists (tree_kernels.hip)
         csr = TE.onebin_csr(Xb, spec.n_bins) if (dev.type == "cuda" and spec.missing_bin > 0) else None
         yf = yy.to(torch.float32).contiguous()
@@ -562,8 +563,17 @@ class XGBoostClassifierLearner(_BoostLearner):
                     gen = torch.Generator().manual_seed(int(pr.get("seed", 0)) + 17 * it + p)
                     w = (torch.rand(r.numel(), generator=gen) < ss).to(torch.int64).to(dev)
                 tjobs.append(TE.TreeJob(p, tp, r, w))
+            root = None
+            if all(j.weights is None for j in tjobs):
+                # the packed root entries only change when a job stops: pack once per active set
+                key = tuple(act)
+                if key not in root_cache:
+                    root_cache.clear()
+                    root_cache[key] = TE._root_rows(tjobs, dev)
+                packed, cnts = root_cache[key]
+                root = (packed.clone(), cnts)
             forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
-                                    missing_bin=spec.missing_bin, collect_leaves=True, csr=csr)
+                                    missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root)
             need = [p for p in act if esr[p] > 0]
             auc_counts = None
             if fused:

@@ -27,6 +27,8 @@ I64 = C.c_int64
 F32 = C.c_float
 
 _HOST_SIGS = {
+    "tmog_tree_finalize_cpu": [I64, I32, P, P, P, P, P, P, I32, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P,
+                               P, P],
     "tmog_hist_build_cpu": [P, I64, I32, P, I32, P, P, P, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P],
     "tmog_split_find_cpu": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, P, P],
     "tmog_partition_cpu": [P, I32, P, P, I32, P, P, P, P, P, I32, P, P],
@@ -82,7 +84,7 @@ _HIP_SIGS = {
 }
 
 
-_RESTYPES = {"tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
+_RESTYPES = {"tmog_tree_finalize_cpu": C.c_int64, "tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
              "tmog_shist_flush": None, "tmog_shist_merge": None, "tmog_shist_bins": None,
              "tmog_shist_size": C.c_int64, "tmog_shist_sum": C.c_double,
              "tmog_hip_split_cand_bytes": C.c_size_t,

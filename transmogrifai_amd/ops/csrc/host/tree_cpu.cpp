@@ -294,3 +294,94 @@ extern "C" int tmog_find_splits_cpu(const double* sample, int64_t S, int F, int 
   }
   return 0;
 }
+
+// Native twin of tree_engine._finalize_py (one job group's created nodes -> flat forest arrays):
+// leaf values (class frequencies / mean / Newton step -G/(H+lambda)*eta), XGBoost gamma pruning
+// (bottom-up: children are created after their parents, so a reverse sweep sees final children),
+// reachability from the roots, per-tree stable regrouping, child renumbering and (boosting) the leaf
+// value of every created node id (pruned descendants take their nearest kept ancestor's value).
+// Same float64 arithmetic and float32 roundings as the numpy version, so the arrays are identical.
+// Returns the kept node count; outputs are sized for n nodes.
+extern "C" int64_t tmog_tree_finalize_cpu(int64_t n, int T, const int64_t* tree, const int64_t* feat_in,
+                                          const int64_t* bin, const uint8_t* dl, const double* gain, const double* tot,
+                                          int S, const int64_t* left_in, const int64_t* right_in, int mode, int kind,
+                                          int K, const double* job_lam, const double* job_eta,
+                                          const double* job_gamma, int with_gid, int64_t* tree_off, int32_t* nodes,
+                                          uint8_t* dl_out, float* value_out, float* gain_out, float* cover_out,
+                                          float* gid_value) {
+  std::vector<double> value((size_t)n * K), cover(n);
+  for (int64_t i = 0; i < n; ++i) {
+    const double* t = tot + (size_t)i * S;
+    if (mode == 0) {
+      double s = 0;
+      for (int c = 0; c < S; ++c) s += t[c];
+      for (int c = 0; c < K; ++c) value[(size_t)i * K + c] = s > 0 ? t[c] / std::max(s, 1e-300) : 0.0;
+      cover[i] = s;
+    } else if (mode == 1) {
+      value[i] = t[0] > 0 ? t[1] / std::max(t[0], 1e-300) : 0.0;
+      cover[i] = t[0];
+    } else {
+      const int64_t j = tree[i];
+      value[i] = -t[0] / (t[1] + job_lam[j]) * job_eta[j];
+      cover[i] = t[1];
+    }
+  }
+  std::vector<int64_t> left(left_in, left_in + n), right(right_in, right_in + n), feat(feat_in, feat_in + n);
+  if (kind == 3) {   // KIND_NEWTON
+    for (int64_t i = n - 1; i >= 0; --i) {
+      if (left[i] < 0) continue;
+      if (left[left[i]] < 0 && left[right[i]] < 0 && gain[i] < job_gamma[tree[i]]) {
+        left[i] = right[i] = -1;
+        feat[i] = -1;
+      }
+    }
+  }
+  std::vector<uint8_t> reach(n, 0);
+  for (int t = 0; t < T && t < n; ++t) reach[t] = 1;
+  for (int64_t i = 0; i < n; ++i)
+    if (reach[i] && left[i] >= 0) reach[left[i]] = reach[right[i]] = 1;
+  std::vector<int64_t> cnt(T + 1, 0);
+  for (int64_t i = 0; i < n; ++i)
+    if (reach[i]) cnt[tree[i] + 1]++;
+  for (int t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+  for (int t = 0; t <= T; ++t) tree_off[t] = cnt[t];
+  std::vector<int64_t> new_id(n, -1), order(cnt[T]);
+  {
+    std::vector<int64_t> cur(cnt.begin(), cnt.end() - 1);
+    for (int64_t i = 0; i < n; ++i)
+      if (reach[i]) {
+        const int64_t p = cur[tree[i]]++;
+        order[p] = i;
+        new_id[i] = p;
+      }
+  }
+  const int64_t m = cnt[T];
+  for (int64_t p = 0; p < m; ++p) {
+    const int64_t i = order[p];
+    const bool isint = left[i] >= 0;
+    nodes[p * 4 + 0] = isint ? (int32_t)feat[i] : 0;
+    nodes[p * 4 + 1] = isint ? (int32_t)bin[i] : 0;
+    nodes[p * 4 + 2] = isint ? (int32_t)new_id[left[i]] : -1;
+    nodes[p * 4 + 3] = isint ? (int32_t)new_id[right[i]] : -1;
+    dl_out[p] = isint ? dl[i] : 0;
+    for (int c = 0; c < K; ++c) value_out[p * K + c] = (float)value[(size_t)i * K + c];
+    gain_out[p] = isint ? (float)gain[i] : 0.f;
+    cover_out[p] = (float)cover[i];
+  }
+  if (with_gid) {
+    std::vector<int64_t> parent(n, -1);
+    for (int64_t i = 0; i < n; ++i)
+      if (left_in[i] >= 0) {
+        parent[left_in[i]] = i;
+        parent[right_in[i]] = i;
+      }
+    for (int64_t i = 0; i < n; ++i) {
+      if (reach[i] || parent[i] < 0) {
+        for (int c = 0; c < K; ++c) gid_value[i * K + c] = (float)value[(size_t)i * K + c];
+      } else {
+        for (int c = 0; c < K; ++c) gid_value[i * K + c] = gid_value[parent[i] * K + c];
+      }
+    }
+  }
+  return m;
+}
