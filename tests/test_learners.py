@@ -126,3 +126,22 @@ def test_regressors_fit(name):
     pred, _, _ = L.predict(st, X[600:])
     r2 = 1 - ((pred - y[600:]) ** 2).sum() / ((y[600:] - y[600:].mean()) ** 2).sum()
     assert float(r2) > 0.6
+
+
+def test_xgb_column_permutation_leaves_trees_unchanged(monkeypatch):
+    """Boosting on the multi-bin-first column order grows the same trees (features mapped back)."""
+    from transmogrifai_amd.models.base import FitJob
+    from transmogrifai_amd.models.trees import XGBoostClassifierLearner
+    g = torch.Generator().manual_seed(9)
+    n, d = 3000, 10
+    X = torch.randn(n, d, generator=g)
+    X[:, 1::3] = (X[:, 1::3] > 0.7).float()          # interleaved 0/1 columns
+    y = ((X[:, 0] + X[:, 1] - X[:, 4] + 0.3 * torch.randn(n, generator=g)) > 0).float()
+    params = dict(XGBoostClassifierLearner.defaults, num_round=6, max_depth=4, missing=0.0)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TMOG_XGB_COLPERM", flag)
+        st = XGBoostClassifierLearner().fit_batch(X, y, [FitJob(params, torch.arange(0, n, 2))])[0]
+        outs.append(st)
+    np.testing.assert_array_equal(np.asarray(outs[0]["forest"]["nodes"]), np.asarray(outs[1]["forest"]["nodes"]))
+    np.testing.assert_array_equal(np.asarray(outs[0]["forest"]["value"]), np.asarray(outs[1]["forest"]["value"]))

@@ -535,8 +535,20 @@ class XGBoostClassifierLearner(_BoostLearner):
         AUC_BINS = 1 << 16
         G = H = None
         root_cache: Dict[tuple, tuple] = {}
+        # Column order for growth: multi-bin columns first, then the one-present-bin ones (one-hot /
+        # null indicators), physically -- the histogram kernel's multi-bin groups then gather contiguous
+        # row bytes. It is the order the grower would use anyway (common/tree_grow.hpp), so trees are
+        # unchanged; split features are mapped back to the original columns after each round.
+        Xg, n_bins_g, colperm = Xb, spec.n_bins, None
+        if spec.missing_bin > 0 and os.environ.get("TMOG_XGB_COLPERM") != "0":
+            nb_all = np.asarray(spec.n_bins)
+            order = np.concatenate([np.nonzero(nb_all != 1)[0], np.nonzero(nb_all == 1)[0]])
+            if not np.array_equal(order, np.arange(nb_all.size)):
+                colperm = order.astype(np.int64)
+                Xg = Xb.index_select(1, torch.as_tensor(colperm, device=dev)).contiguous()
+                n_bins_g = nb_all[colperm]
         # one-hot / null-indicator columns: histogram from the rows' CSR lists (tree_kernels.hip)
-        csr = TE.onebin_csr(Xb, spec.n_bins) if (dev.type == "cuda" and spec.missing_bin > 0) else None
+        csr = TE.onebin_csr(Xg, n_bins_g) if (dev.type == "cuda" and spec.missing_bin > 0) else None
         yf = yy.to(torch.float32).contiguous()
         for it in range(max(rounds)):
             act = [p for p in range(P) if it < rounds[p] and not stopped[p]]
@@ -572,8 +584,11 @@ class XGBoostClassifierLearner(_BoostLearner):
                     root_cache[key] = TE._root_rows(tjobs, dev)
                 packed, cnts = root_cache[key]
                 root = (packed.clone(), cnts)
-            forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
+            forest = TE.grow_forest(Xg, n_bins_g, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
                                     missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root)
+            if colperm is not None:
+                internal = forest.nodes[:, 2] >= 0
+                forest.nodes[internal, 0] = colperm[forest.nodes[internal, 0]]
             need = [p for p in act if esr[p] > 0]
             auc_counts = None
             if fused:
