@@ -231,10 +231,12 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
   // one-present-bin columns), so split tie-breaks by local feature index stay identical GPU vs CPU.
   std::vector<FeatGroup> full_groups;
   std::vector<int32_t> perm_feats;
+  int split_n_multi = -1;   // GPU split scan: local features [n_multi, F) have one present bin
   if (!use_subset && a.mode == 2 && a.missing_bin >= 0 && a.n_bins_host != nullptr) {
     for (int f = 0; f < F; ++f)
       if (a.n_bins_host[f] != 1) perm_feats.push_back(f);
     const int n_multi = (int)perm_feats.size();
+    split_n_multi = n_multi;
     for (int f = 0; f < F; ++f)
       if (a.n_bins_host[f] == 1) perm_feats.push_back(f);
     for (const FeatGroup& g : equal_groups(n_multi)) full_groups.push_back(g);
@@ -426,7 +428,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     bk.split_find(a, hist, m, TM_P(const int64_t, o_nho), TM_P(const int32_t, o_nnf), TM_P(const int32_t, o_nfo),
                   flist, TM_P(const float, o_par), TM_P(const int32_t, o_nmd), max_nf, (int32_t*)(res + r_feat),
                   (int32_t*)(res + r_bin), (float*)(res + r_gain), res + r_dl, (float*)(res + r_left),
-                  (float*)(res + r_tot), (int64_t*)(res + r_cl));
+                  (float*)(res + r_tot), (int64_t*)(res + r_cl), use_subset ? -1 : split_n_multi);
     if (BK::kGPU)   // partition in place of the node ranges, straight from the device decisions
       bk.partition_fused(a, rows, rows_alt, d1 + o_cit, (int)ncit, TM_P(const int64_t, o_nb),
                          TM_P(const int64_t, o_nc), (const int32_t*)(res + r_feat), (const int32_t*)(res + r_bin),

@@ -23,7 +23,7 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
                         const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
-                        float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors,
+                        float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors, int n_multi,
                         hipStream_t stream);
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
                            hipStream_t stream);
@@ -153,10 +153,11 @@ struct GpuBackend {
   }
   void split_find(const tmog::GrowArgs& g, const int64_t* hist, int m, const int64_t* nho, const int32_t* nnf,
                   const int32_t* nfo, const int32_t* flist, const float* params, const int32_t* nmd, int max_nf,
-                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t* cursors) {
+                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t* cursors,
+                  int n_multi) {
     grow_dev(sl.cand, sl.cand_cap, tmog_hip_split_cand_bytes(m, max_nf), sl.stream);
     kchk(tmog_hip_split_find(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd,
-                             g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, cursors, sl.stream),
+                             g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, cursors, n_multi, sl.stream),
          "split_find");
   }
   void partition_fused(const tmog::GrowArgs& g, const uint32_t* rows, uint32_t* rows_alt, const void* items, int n,

@@ -435,14 +435,19 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
     int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
-    Best* __restrict__ cand) {
+    Best* __restrict__ cand, int n_multi) {
   const int j = blockIdx.x / fbmax;
   const int fb = blockIdx.x - j * fbmax;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nf = node_nfeat[j];
+  // n_multi >= 0: local features [n_multi, nf) have one present bin; their blocks (fb >= fb_multi)
+  // take 256 features each, one thread per feature, instead of 16 per block through the scan
+  const int f_lim = n_multi >= 0 ? min(n_multi, nf) : nf;
+  const int fb_multi = n_multi >= 0 ? (n_multi + FPB - 1) / FPB : fbmax;
+  const bool one_blk = fb >= fb_multi;
   __shared__ Best s_best[4];
   Best best{-INFINITY, 0x7fffffff, 0, 0};
-  if (fb * FPB < nf) {
+  if (one_blk ? (n_multi + (fb - fb_multi) * 256 < nf) : (fb * FPB < f_lim)) {
     const int64_t* h = hist + node_hist_off[j];
     const int32_t* fl = feat_list + node_feat_off[j];
     const float* P = node_params + (int64_t)j * 8;
@@ -462,7 +467,7 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     double tcount;
     const double pimp = impurity_dev(tot, S, kind, &tcount);
     const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
-    const int f_end = min(nf, (fb + 1) * FPB);
+    const int f_end = one_blk ? 0 : min(f_lim, (fb + 1) * FPB);
     // one candidate (left statistics lq, bin b, missing direction dl) with the CPU twin's arithmetic
     auto consider = [&](const int64_t* lq, int f, int b, int dl) {
       double left[SM], right[SM];
@@ -488,6 +493,15 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
         if (better(c, best)) best = c;
       }
     };
+    if (one_blk) {
+      const int f = n_multi + (fb - fb_multi) * 256 + (int)threadIdx.x;
+      if (f < nf && allow_missing && feat_nbins[fl[f]] == 1) {
+        const int64_t* hf = h + (int64_t)f * B * S;
+        int64_t lq[SM];
+        for (int s = 0; s < S; ++s) lq[s] = hf[s];
+        consider(lq, f, 0, 0);
+      }
+    }
     for (int f = fb * FPB + wave; f < f_end; f += 4) {
       const int nb = feat_nbins[fl[f]];
       const int64_t* hf = h + (int64_t)f * B * S;
@@ -875,16 +889,18 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
                         const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
                         float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors,
-                        hipStream_t stream) {
+                        int n_multi, hipStream_t stream) {
   if (n_nodes == 0) return 0;
   if (S > TM_MAX_S || B > 64) return -2;
-  const int fbmax = (max_nfeat + FPB - 1) / FPB;
+  if (n_multi > max_nfeat) n_multi = -1;
+  const int fbmax = n_multi >= 0 ? (n_multi + FPB - 1) / FPB + (max_nfeat - n_multi + 255) / 256
+                                 : (max_nfeat + FPB - 1) / FPB;
   if (fbmax > 64) return -2;
   Best* cand = (Best*)cand_ws;   // >= n_nodes * fbmax entries
 #define TM_SPLIT(SMV)                                                                                          \
   hipLaunchKernelGGL(split_scan_kernel<SMV>, dim3(n_nodes * fbmax), dim3(256), 0, stream, hist, node_hist_off,  \
                      node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin,    \
-                     node_model, qinv, fbmax, cand)
+                     node_model, qinv, fbmax, cand, n_multi)
   if (S <= 2) TM_SPLIT(2);
   else if (S == 3) TM_SPLIT(3);
   else if (S <= 4) TM_SPLIT(4);

@@ -69,7 +69,7 @@ struct CpuBackend {
   }
   void split_find(const tmog::GrowArgs& g, const int64_t* hist, int m, const int64_t* nho, const int32_t* nnf,
                   const int32_t* nfo, const int32_t* flist, const float* params, const int32_t* nmd, int,
-                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t*) {
+                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t*, int) {
     tmog_split_find_cpu(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd, g.qinv,
                         feat, bin, gain, dl, left, tot);
   }
