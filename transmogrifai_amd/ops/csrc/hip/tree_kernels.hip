@@ -612,6 +612,8 @@ struct PartItem {
   int64_t out_right;  // absolute output position for this chunk's first right row
 };
 
+constexpr int PART_U = 4;
+
 __device__ __forceinline__ bool goes_left(uint8_t bin, int sb, bool dl, int missing_bin) {
   return (missing_bin >= 0 && bin == missing_bin) ? dl : ((int)bin <= sb);
 }
@@ -636,40 +638,59 @@ __global__ void __launch_bounds__(256) partition_fused_kernel(
   if (f < 0 || !(node_params[(int64_t)j * 8 + 7] > 0.5f) || !(split_gain[j] > node_params[(int64_t)j * 8 + 6])) return;
   const bool d = dl[j] != 0;
   const int64_t nb = node_begin[j], nend = nb + node_count[j];
-  __shared__ int s_wave[4];
+  // PART_U rows per thread per pass: their row / bin loads are all in flight together and one pair
+  // of cursor atomics reserves the slots of 256 * PART_U rows (the dependent load -> load -> atomic
+  // chain runs once per pass instead of once per 256 rows)
+  __shared__ int s_cnt[PART_U][4];
   __shared__ unsigned long long s_base[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int64_t base = 0; base < it.count; base += blockDim.x) {
-    const int64_t i = base + threadIdx.x;
-    const bool valid = i < it.count;
-    uint32_t e = 0;
-    bool left = false;
-    if (valid) {
-      e = rows_in[it.begin + i];
-      left = goes_left(Xb[(int64_t)(e & 0xFFFFFFu) * F + f], sb, d, missing_bin);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int64_t base = 0; base < it.count; base += (int64_t)blockDim.x * PART_U) {
+    uint32_t e[PART_U];
+    bool vd[PART_U], lf[PART_U];
+#pragma unroll
+    for (int u = 0; u < PART_U; ++u) {
+      const int64_t i = base + (int64_t)u * blockDim.x + threadIdx.x;
+      vd[u] = i < it.count;
+      e[u] = rows_in[it.begin + (vd[u] ? i : 0)];     // unpredicated: row 0 of the item is valid
     }
-    const unsigned long long m = __ballot(valid && left);
-    const int wpre = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) s_wave[wave] = __popcll(m);
+    uint8_t bn[PART_U];
+#pragma unroll
+    for (int u = 0; u < PART_U; ++u) bn[u] = Xb[(int64_t)(e[u] & 0xFFFFFFu) * F + f];
+    int wpre[PART_U];
+#pragma unroll
+    for (int u = 0; u < PART_U; ++u) {
+      lf[u] = vd[u] && goes_left(bn[u], sb, d, missing_bin);
+      const unsigned long long m = __ballot(lf[u]);
+      wpre[u] = __popcll(m & below);
+      if (lane == 0) s_cnt[u][wave] = __popcll(m);
+    }
     __syncthreads();
-    int before = 0, tot = 0;
-    for (int w = 0; w < 4; ++w) {
-      if (w < wave) before += s_wave[w];
-      tot += s_wave[w];
+    int tot = 0, before[PART_U];
+#pragma unroll
+    for (int u = 0; u < PART_U; ++u) {
+      int b = tot;
+      for (int w = 0; w < 4; ++w) {
+        if (w < wave) b += s_cnt[u][w];
+        tot += s_cnt[u][w];
+      }
+      before[u] = b;
     }
-    const int nvalid = (int)min((int64_t)blockDim.x, it.count - base);
+    const int nvalid = (int)min((int64_t)blockDim.x * PART_U, it.count - base);
     if (threadIdx.x == 0) {
       s_base[0] = atomicAdd(cursors + 2 * j, (unsigned long long)tot);
       s_base[1] = atomicAdd(cursors + 2 * j + 1, (unsigned long long)(nvalid - tot));
     }
     __syncthreads();
-    if (valid) {
-      const int lpos = before + wpre;
+#pragma unroll
+    for (int u = 0; u < PART_U; ++u) {
+      if (!vd[u]) continue;
+      const int lpos = before[u] + wpre[u];               // left rows before this one (row order)
+      const int idx = u * (int)blockDim.x + (int)threadIdx.x;  // rows before this one
       // guarded: a slot outside the node's range (impossible unless the cursors were not reset) is
       // dropped; the host checks every node's left + right count against its size
-      const int64_t pos = left ? nb + (int64_t)s_base[0] + lpos
-                               : nend - 1 - (int64_t)s_base[1] - ((int)threadIdx.x - lpos);
-      if (pos >= nb && pos < nend) rows_out[pos] = e;
+      const int64_t pos = lf[u] ? nb + (int64_t)s_base[0] + lpos : nend - 1 - (int64_t)s_base[1] - (idx - lpos);
+      if (pos >= nb && pos < nend) rows_out[pos] = e[u];
     }
     __syncthreads();
   }
