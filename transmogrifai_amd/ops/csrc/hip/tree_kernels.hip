@@ -206,6 +206,8 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
   }
 }
 
+constexpr int HIST_U = 16;   // row bins gathered per lane before their LDS atomics (loads in flight)
+
 template <int MODE>
 __global__ void __launch_bounds__(256) hist_build_kernel(
     const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const HistItem* __restrict__ items,
@@ -287,15 +289,15 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
       __builtin_amdgcn_wave_barrier();
       continue;
     }
-    for (int j0 = 0; j0 < nrows; j0 += R * 8) {
-      int4 st[8];
-      int bin[8];
+    for (int j0 = 0; j0 < nrows; j0 += R * HIST_U) {
+      int4 st[HIST_U];
+      int bin[HIST_U];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) st[u] = stage[min(j0 + u * R + rsub, 63)];
+      for (int u = 0; u < HIST_U; ++u) st[u] = stage[min(j0 + u * R + rsub, 63)];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) bin[u] = (int)Xb[(int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F + feat];
+      for (int u = 0; u < HIST_U; ++u) bin[u] = (int)Xb[(int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F + feat];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < HIST_U; ++u)
         if (active && j0 + u * R + rsub < nrows && bin[u] != skip_bin) add_row<MODE>(my, bin[u], S, st[u]);
     }
     __builtin_amdgcn_wave_barrier();
