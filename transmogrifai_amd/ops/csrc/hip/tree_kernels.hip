@@ -114,7 +114,7 @@ __device__ __forceinline__ void add_row(int* my, int bin, int S, const int4& st)
 // rows one at a time with the lanes spread over that row's list (coalesced 2-byte id loads; the ids
 // of one row are distinct, so an LDS atomic wave-instruction never conflicts), kCsrU rows in flight.
 // On the headline table that is ~50 entries per row instead of ~530 byte gathers.
-constexpr int kCsrU = 8;
+constexpr int kCsrU = 16;
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
