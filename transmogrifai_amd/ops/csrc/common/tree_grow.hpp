@@ -236,12 +236,15 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     for (int f = 0; f < F; ++f)
       if (a.n_bins_host[f] != 1) perm_feats.push_back(f);
     const int n_multi = (int)perm_feats.size();
-    split_n_multi = n_multi;
+    // node totals are read from local feature 0, which must be a multi-bin column: with no multi-bin
+    // column at all every histogram word stays written and scanned (no CSR / reduced write-out)
+    split_n_multi = n_multi > 0 ? n_multi : -1;
     for (int f = 0; f < F; ++f)
       if (a.n_bins_host[f] == 1) perm_feats.push_back(f);
     for (const FeatGroup& g : equal_groups(n_multi)) full_groups.push_back(g);
     const int n_one = F - n_multi;
-    if (BK::kGPU && a.csr_ptr && a.csr_col && n_one > 0 && a.csr_nf == n_one && 2 * n_one + 2 <= 64 * (B * S + 1))
+    if (BK::kGPU && a.csr_ptr && a.csr_col && n_multi > 0 && n_one > 0 && a.csr_nf == n_one &&
+        2 * n_one + 2 <= 64 * (B * S + 1))
       full_groups.push_back(FeatGroup{n_multi, n_one, false, true});   // one item walks the rows' CSR lists
     else
       for (const FeatGroup& g : equal_groups(n_one))

@@ -190,19 +190,21 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
     }
   }
   __syncthreads();
+  // Only bin 0 and the missing bin of these columns are written: the split scan evaluates a
+  // one-present-bin column from its bin 0 alone (and the node totals come from a multi-bin column),
+  // so bins 1 .. B-2 are never read -- 2 instead of B words per column and statistic.
   int64_t* out = hist + node_hist_off[it.node] + (int64_t)it.fg0 * B * S;
   const int per = B * S;
-  const int words = nf * per;
   const bool excl = (it.excl & 1) != 0;
-  for (int k = threadIdx.x; k < words; k += blockDim.x) {
-    const int f = k / per;
-    const int rem = k - f * per;
-    const int b = rem / S, s = rem - b * S;
-    int v = 0;
-    if (b == 0) v = s ? a1[f] : a0[f];
-    else if (b == skip_bin) v = ctot[s] - (s ? a1[f] : a0[f]);
-    if (excl) out[k] = v;
-    else if (v != 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + k), (unsigned long long)(int64_t)v);
+  for (int k = threadIdx.x; k < nf * 2 * S; k += blockDim.x) {
+    const int f = k / (2 * S);
+    const int rem = k - f * 2 * S;
+    const int which = rem / S, s = rem - which * S;
+    const int a = s ? a1[f] : a0[f];
+    const int v = which ? ctot[s] - a : a;
+    int64_t* w = out + (int64_t)f * per + (which ? skip_bin : 0) * S + s;
+    if (excl) *w = v;
+    else if (v != 0) atomicAdd(reinterpret_cast<unsigned long long*>(w), (unsigned long long)(int64_t)v);
   }
 }
 
