@@ -162,7 +162,7 @@ class BinaryVectorizer(VectorizerMixin, SequenceTransformer):
 
 @register_stage
 class RealNNVectorizer(VectorizerMixin, SequenceTransformer):
-    operation_name = "vecRealNN"
+    operation_name = "vecNum"   # RealNNVectorizer.scala:46
 
     def transform_columns(self, *cols, ds=None):
         self.metadata["vector_metadata"] = self.vector_metadata([col_meta(t) for t in self.get_transient_features()])
