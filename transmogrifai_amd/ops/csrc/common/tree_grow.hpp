@@ -232,6 +232,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
   std::vector<FeatGroup> full_groups;
   std::vector<int32_t> perm_feats;
   int split_n_multi = -1;   // GPU split scan: local features [n_multi, F) have one present bin
+  int64_t live_dense = -1;  // GPU zero / subtract: words past this prefix are live only at bin 0
   if (!use_subset && a.mode == 2 && a.missing_bin >= 0 && a.n_bins_host != nullptr) {
     for (int f = 0; f < F; ++f)
       if (a.n_bins_host[f] != 1) perm_feats.push_back(f);
@@ -239,6 +240,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     // node totals are read from local feature 0, which must be a multi-bin column: with no multi-bin
     // column at all every histogram word stays written and scanned (no CSR / reduced write-out)
     split_n_multi = n_multi > 0 ? n_multi : -1;
+    if (BK::kGPU && n_multi > 0) live_dense = (int64_t)n_multi * a.B * a.S;
     for (int f = 0; f < F; ++f)
       if (a.n_bins_host[f] == 1) perm_feats.push_back(f);
     for (const FeatGroup& g : equal_groups(n_multi)) full_groups.push_back(g);
@@ -413,7 +415,8 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
 #define TM_P(T_, off) ((T_*)(d1 + (off)))
     const int32_t* flist = own_list ? TM_P(const int32_t, o_fl) : all_feats;
     // ---- histograms
-    bk.zero_segments(hist, TM_P(const int64_t, o_zo), TM_P(const int64_t, o_zs), (int)z_off.size(), z_max);
+    bk.zero_segments(hist, TM_P(const int64_t, o_zo), TM_P(const int64_t, o_zs), (int)z_off.size(), z_max, live_dense,
+                     a.B * a.S, a.S);
     bk.hist_build(a, rows, hitems.size() ? (const void*)(d1 + o_hit) : nullptr, (int)hitems.size(),
                   TM_P(const int32_t, o_nfo), flist, TM_P(const int32_t, o_nmd), TM_P(const int64_t, o_nho), hist,
                   (int)b_nb.size(), TM_P(const int64_t, o_bnb), TM_P(const int64_t, o_bnc),
@@ -421,7 +424,8 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
                   TM_P(const int64_t, o_bnho));
     if (!d_big.empty())
       bk.hist_subtract(hist, prev_hist, TM_P(const int64_t, o_dp), TM_P(const int64_t, o_ds),
-                       TM_P(const int64_t, o_do), TM_P(const int64_t, o_dz), (int)d_big.size(), d_max);
+                       TM_P(const int64_t, o_do), TM_P(const int64_t, o_dz), (int)d_big.size(), d_max, live_dense,
+                       a.B * a.S, a.S);
     // ---- split scan + (GPU) one-pass partition -> one result block: decisions + per-node slot cursors
     const int64_t ncit = (int64_t)citems.size();
     const size_t r_cl = 0, r_feat = r_cl + 16 * (size_t)m, r_bin = r_feat + 4 * (size_t)m, r_gain = r_bin + 4 * (size_t)m;

@@ -18,7 +18,8 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, hipStream_t stream);
 int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
-                           const int64_t* out_off, const int64_t* size, int n, int64_t max_size, hipStream_t stream);
+                           const int64_t* out_off, const int64_t* size, int n, int64_t max_size, int64_t dense,
+                           int per, int S, hipStream_t stream);
 int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
@@ -26,7 +27,7 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors, int n_multi,
                         hipStream_t stream);
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
-                           hipStream_t stream);
+                           int64_t dense, int per, int S, hipStream_t stream);
 size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat);
 int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, const void* items,
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
@@ -135,8 +136,9 @@ struct GpuBackend {
     hchk(hipStreamSynchronize(sl.stream), "result sync");
     return sl.res_pin;
   }
-  void zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t mx) {
-    kchk(tmog_hip_zero_segments(hist, off, size, n, mx, sl.stream), "zero_segments");
+  void zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t mx, int64_t dense, int per,
+                     int S) {
+    kchk(tmog_hip_zero_segments(hist, off, size, n, mx, dense, per, S, sl.stream), "zero_segments");
   }
   void hist_build(const tmog::GrowArgs& g, const uint32_t* rows, const void* items, int n_items, const int32_t* nfo,
                   const int32_t* flist, const int32_t* nmd, const int64_t* nho, int64_t* hist, int, const int64_t*,
@@ -148,8 +150,8 @@ struct GpuBackend {
            "hist_build");
   }
   void hist_subtract(int64_t* hist, const int64_t* prev, const int64_t* poff, const int64_t* soff,
-                     const int64_t* ooff, const int64_t* size, int n, int64_t mx) {
-    kchk(tmog_hip_hist_subtract(hist, prev, poff, soff, ooff, size, n, mx, sl.stream), "hist_subtract");
+                     const int64_t* ooff, const int64_t* size, int n, int64_t mx, int64_t dense, int per, int S) {
+    kchk(tmog_hip_hist_subtract(hist, prev, poff, soff, ooff, size, n, mx, dense, per, S, sl.stream), "hist_subtract");
   }
   void split_find(const tmog::GrowArgs& g, const int64_t* hist, int m, const int64_t* nho, const int32_t* nnf,
                   const int32_t* nfo, const int32_t* flist, const float* params, const int32_t* nmd, int max_nf,

@@ -355,29 +355,45 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
 }
 
 // sibling = parent - small (histogram subtraction trick), size words each
+// Word k of a node's live region: with dense >= 0 the region is the first `dense` words (the multi-bin
+// columns, every bin) followed by bin 0 of each one-present-bin column -- the only words the split scan,
+// the split reduce and the next level's subtraction read of those columns (tree_grow.hpp orders the
+// multi-bin columns first), so ~530 of the headline table's ~730 columns move S words instead of B * S.
+__device__ __forceinline__ int64_t live_words(int64_t sz, int64_t dense, int per, int S) {
+  return (dense < 0 || sz <= dense) ? sz : dense + (sz - dense) / per * S;
+}
+__device__ __forceinline__ int64_t live_word(int64_t k, int64_t dense, int per, int S) {
+  if (dense < 0 || k < dense) return k;
+  const int64_t t = k - dense, f = t / S;
+  return dense + f * per + (t - f * S);
+}
+
 __global__ void hist_subtract_kernel(int64_t* __restrict__ hist, const int64_t* __restrict__ parent,
                                      const int64_t* __restrict__ parent_off, const int64_t* __restrict__ small_off,
-                                     const int64_t* __restrict__ out_off, const int64_t* __restrict__ size, int n) {
+                                     const int64_t* __restrict__ out_off, const int64_t* __restrict__ size, int n,
+                                     int64_t dense, int per, int S) {
   const int j = blockIdx.y;
   if (j >= n) return;
-  const int64_t sz = size[j];
+  const int64_t sz = live_words(size[j], dense, per, S);
   const int64_t* p = parent + parent_off[j];
   const int64_t* s = hist + small_off[j];
   int64_t* o = hist + out_off[j];
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += (int64_t)gridDim.x * blockDim.x)
-    o[k] = p[k] - s[k];
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t w = live_word(k, dense, per, S);
+    o[w] = p[w] - s[w];
+  }
 }
 
 // zero the histograms of nodes built from several row chunks (their items accumulate atomically);
 // single-chunk and derived nodes are fully overwritten, so the level buffer is never memset whole
 __global__ void zero_segments_kernel(int64_t* __restrict__ hist, const int64_t* __restrict__ off,
-                                     const int64_t* __restrict__ size, int n) {
+                                     const int64_t* __restrict__ size, int n, int64_t dense, int per, int S) {
   const int j = blockIdx.y;
   if (j >= n) return;
   int64_t* o = hist + off[j];
-  const int64_t sz = size[j];
+  const int64_t sz = live_words(size[j], dense, per, S);
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += (int64_t)gridDim.x * blockDim.x)
-    o[k] = 0;
+    o[live_word(k, dense, per, S)] = 0;
 }
 
 // ------------------------------------------------------------------------------- split finding
@@ -899,13 +915,14 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
 }
 
 int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
-                           const int64_t* out_off, const int64_t* size, int n, int64_t max_size, hipStream_t stream) {
+                           const int64_t* out_off, const int64_t* size, int n, int64_t max_size, int64_t dense,
+                           int per, int S, hipStream_t stream) {
   if (n == 0) return 0;
   int gx = (int)((max_size + 255) / 256);
   if (gx > 1024) gx = 1024;
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(hist_subtract_kernel, dim3(gx, n), dim3(256), 0, stream, hist, parent, parent_off, small_off,
-                     out_off, size, n);
+                     out_off, size, n, dense, per, S);
   return (int)hipGetLastError();
 }
 
@@ -938,10 +955,10 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
 }
 
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
-                           hipStream_t stream) {
+                           int64_t dense, int per, int S, hipStream_t stream) {
   if (n == 0) return 0;
   int gx = (int)min((max_size + 255) / 256, (int64_t)1024);
-  hipLaunchKernelGGL(zero_segments_kernel, dim3(gx, n), dim3(256), 0, stream, hist, off, size, n);
+  hipLaunchKernelGGL(zero_segments_kernel, dim3(gx, n), dim3(256), 0, stream, hist, off, size, n, dense, per, S);
   return (int)hipGetLastError();
 }
 

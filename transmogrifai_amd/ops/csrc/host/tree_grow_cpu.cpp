@@ -49,7 +49,7 @@ struct CpuBackend {
     return res.data();
   }
   const uint8_t* fetch(const uint8_t* p, size_t) { return p; }
-  void zero_segments(int64_t*, const int64_t*, const int64_t*, int, int64_t) {}   // CPU hist zeroes per node
+  void zero_segments(int64_t*, const int64_t*, const int64_t*, int, int64_t, int64_t, int, int) {}   // CPU hist zeroes per node
   void hist_build(const tmog::GrowArgs& g, const uint32_t* rows, const void*, int, const int32_t*,
                   const int32_t* flist, const int32_t*, const int64_t*, int64_t* hist, int nbuild,
                   const int64_t* bnb, const int64_t* bnc, const int32_t* bnfo, const int32_t* bnnf,
@@ -59,7 +59,7 @@ struct CpuBackend {
                           g.S, g.y, g.t1, g.t2, g.stride, g.qscale);
   }
   void hist_subtract(int64_t* hist, const int64_t* prev, const int64_t* poff, const int64_t* soff,
-                     const int64_t* ooff, const int64_t* size, int n, int64_t) {
+                     const int64_t* ooff, const int64_t* size, int n, int64_t, int64_t, int, int) {
     for (int j = 0; j < n; ++j) {
       const int64_t* p = prev + poff[j];
       const int64_t* s = hist + soff[j];
