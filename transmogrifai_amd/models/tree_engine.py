@@ -38,6 +38,7 @@ LEAF_ITEM = np.dtype([("begin", "<i8"), ("count", "<i8"), ("out", "<i8"), ("gid"
 assert HIST_ITEM.itemsize == 32 and PART_ITEM.itemsize == 40 and LEAF_ITEM.itemsize == 32
 
 ROW_MASK = 0xFFFFFF
+CSR_ITEM_ROWS = 1024          # rows per CSR histogram item (tree_grow.hpp kCsrRows)
 MAX_ROWS = 1 << 24
 
 
@@ -451,7 +452,9 @@ def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev):
     if mode == MODE_CLS or rows.numel() == 0:
         one = torch.ones(n_models, S, dtype=torch.float32, device=dev)
         return one, one.to(torch.float64)
-    qmax = float(min(1 << 22, (2 ** 31 - 1) // max(1, int(chunk_rows)) - 1))
+    # an LDS partial sums at most max(chunk_rows, CSR_ITEM_ROWS) rows (CSR items always span 1024 rows,
+    # tree_grow.hpp kCsrRows), so size the per-row bound from the larger of the two
+    qmax = float(min(1 << 22, (2 ** 31 - 1) // max(1, int(chunk_rows), CSR_ITEM_ROWS) - 1))
     wmax = ((rows >> 24) & 0xFF).max().to(torch.float32)
 
     def amax(t):

@@ -382,7 +382,8 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
           h.node = j;
           h.fg0 = fgp.f0;
           h.nf = fgp.nf;
-          h.excl = (nit == 1 ? 1 : 0) | (fgp.reg ? 2 : 0) | (fgp.csr ? 4 : 0);
+          h.excl = (nit == 1 ? 1 : 0) | (fgp.reg ? 2 : 0) | (fgp.csr ? 4 : 0) |
+                   ((fgp.reg || fgp.csr) && live_dense >= 0 ? 8 : 0);
           h.begin = nb[j] + c * step;
           h.count = std::min(step, cnt - c * step);
           hitems.push_back(h);

@@ -133,11 +133,10 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
   const int nf = it.nf;
   int* a0 = lds;            // bin-0 sum of q(w g) per column
   int* a1 = lds + nf;       // bin-0 sum of q(w h)
-  int* ctot = lds + 2 * nf; // chunk totals
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
-  for (int i = threadIdx.x; i < 2 * nf + 2; i += blockDim.x) lds[i] = 0;
+  for (int i = threadIdx.x; i < 2 * nf; i += blockDim.x) lds[i] = 0;
   __syncthreads();
   const int64_t model = node_model ? node_model[it.node] : 0;
   const float* qs = qscale + model * S;
@@ -150,15 +149,6 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
     const int64_t r = (uint32_t)mine.x & 0xFFFFFFu;
     const int64_t q0 = csr_ptr[r];
     const int64_t q1 = lane < nrows ? csr_ptr[r + 1] : q0;
-    int ta = lane < nrows ? mine.y : 0, tb = lane < nrows ? mine.z : 0;
-    for (int off = 32; off > 0; off >>= 1) {
-      ta += __shfl_xor(ta, off, 64);
-      tb += __shfl_xor(tb, off, 64);
-    }
-    if (lane == 0) {
-      atomicAdd(ctot, ta);
-      atomicAdd(ctot + 1, tb);
-    }
     for (int j = 0; j < nrows; j += kCsrU) {
       int col[kCsrU], gq[kCsrU], hq[kCsrU];
       bool ok[kCsrU];
@@ -190,19 +180,16 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
     }
   }
   __syncthreads();
-  // Only bin 0 and the missing bin of these columns are written: the split scan evaluates a
-  // one-present-bin column from its bin 0 alone (and the node totals come from a multi-bin column),
-  // so bins 1 .. B-2 are never read -- 2 instead of B words per column and statistic.
+  // Only bin 0 of these columns is written: the split scan and split reduce evaluate a one-present-bin
+  // column from its bin 0 and the node totals (read from a multi-bin column), and zero_segments /
+  // hist_subtract maintain only that word, so no other word of these columns is ever live.
   int64_t* out = hist + node_hist_off[it.node] + (int64_t)it.fg0 * B * S;
   const int per = B * S;
   const bool excl = (it.excl & 1) != 0;
-  for (int k = threadIdx.x; k < nf * 2 * S; k += blockDim.x) {
-    const int f = k / (2 * S);
-    const int rem = k - f * 2 * S;
-    const int which = rem / S, s = rem - which * S;
-    const int a = s ? a1[f] : a0[f];
-    const int v = which ? ctot[s] - a : a;
-    int64_t* w = out + (int64_t)f * per + (which ? skip_bin : 0) * S + s;
+  for (int k = threadIdx.x; k < nf * S; k += blockDim.x) {
+    const int f = k / S, s = k - f * S;
+    const int v = s ? a1[f] : a0[f];
+    int64_t* w = out + (int64_t)f * per + s;
     if (excl) *w = v;
     else if (v != 0) atomicAdd(reinterpret_cast<unsigned long long*>(w), (unsigned long long)(int64_t)v);
   }
@@ -335,8 +322,12 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
       row[skip_bin * S + s] = tot[s] - sum;
     }
     __syncthreads();
+    // excl bit 3: the group's columns have one present bin and only their bin 0 is live (the grower
+    // orders multi-bin columns first and zero / subtract maintain bin 0 alone, see hist_csr_item)
+    const int wlimit = (it.excl & 8) ? S : B * S;
     for (int k = threadIdx.x; k < words; k += blockDim.x) {
       const int f = k / (B * S);
+      if (k - f * (B * S) >= wlimit) continue;
       const int64_t acc = lds[f * rowstride + (k - f * (B * S))];
       if (excl) out[k] = acc;
       else if (acc != 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + k), (unsigned long long)acc);

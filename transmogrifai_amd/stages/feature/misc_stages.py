@@ -35,6 +35,8 @@ class _FnStage(UnaryTransformer):
 
     def __init__(self, fn: Optional[Callable] = None, uid=None, **kw):
         super().__init__(fn, uid=uid, **kw)
+        if fn is not None:
+            _fn_name(fn)                 # registers module-level functions for checkpoint reloads
 
     def ctor_args(self):
         return {"fn": _fn_name(self.fn)}

@@ -7,11 +7,14 @@ of the same name is used directly -- the fast path used by every large-data run.
 """
 from __future__ import annotations
 
-from typing import Any, Callable, Optional
+import logging
+from typing import Any, Callable, Dict, Optional
 
 from ..features import types as T
 from ..features.feature import FeatureLike
 from .base import OpPipelineStage, register_stage
+
+log = logging.getLogger(__name__)
 
 
 @register_stage
@@ -25,6 +28,8 @@ class FeatureGeneratorStage(OpPipelineStage):
         super().__init__(uid=uid, output_type=output_type)
         self.name = name
         self.extract_fn = extract_fn
+        if extract_fn is not None:
+            _fn_name(extract_fn)         # registers module-level functions for checkpoint reloads
         self.aggregator = aggregator
         self.aggregate_window = aggregate_window
         self.output_is_response = output_is_response
@@ -67,34 +72,65 @@ class FeatureGeneratorStage(OpPipelineStage):
                 "aggregateWindow": self.aggregate_window}
 
 
-def _fn_name(fn) -> str:
-    """Importable ``module.qualname`` of a module-level extract function (reloaded on model load, the
-    analogue of the reference's reflective ``extractFn`` class instances); ``ColumnExtract`` for
-    column extraction; ``PythonFunction`` for lambdas / closures, which cannot be restored."""
-    if fn is None:
-        return "ColumnExtract"
+# Functions a checkpoint may name (extract functions, predicate / map functions of _FnStage). A
+# checkpoint is data: loading one never imports a module or resolves an arbitrary attribute path; it can
+# only select a function that this process registered -- explicitly with ``register_function`` or
+# implicitly by handing it to a FeatureBuilder / stage (user code that the process already runs).
+_FUNCTIONS: Dict[str, Callable] = {}
+
+
+def register_function(fn: Callable = None, name: Optional[str] = None):
+    """Make ``fn`` loadable by name from checkpoints (decorator or call). Returns ``fn``."""
+    def reg(f):
+        key = name or _qual_name(f)
+        if key is None:
+            raise ValueError("only module-level functions (or an explicit name) can be registered")
+        _FUNCTIONS[key] = f
+        return f
+    return reg(fn) if fn is not None else reg
+
+
+def registered_functions() -> Dict[str, Callable]:
+    return dict(_FUNCTIONS)
+
+
+def _qual_name(fn) -> Optional[str]:
     mod, qn = getattr(fn, "__module__", None), getattr(fn, "__qualname__", "")
     if mod and qn and "<" not in qn:
         return f"{mod}.{qn}"
-    return "PythonFunction"
+    return None
+
+
+def _fn_name(fn) -> str:
+    """Registry name of a user function (``module.qualname``; registered as a side effect so the model
+    reloads in this process); ``ColumnExtract`` for column extraction; ``PythonFunction`` for lambdas /
+    closures, which cannot be restored."""
+    if fn is None:
+        return "ColumnExtract"
+    for k, v in _FUNCTIONS.items():
+        if v is fn:
+            return k
+    q = _qual_name(fn)
+    if q is None:
+        return "PythonFunction"
+    _FUNCTIONS.setdefault(q, fn)
+    return q
 
 
 def load_extract_fn(name: Optional[str]):
+    """Resolve a checkpoint function name through the registry only (no imports, no attribute walks).
+    Unknown names resolve to None: column-extract stages fall back to the column of the feature's name;
+    a stage that needs the function raises when it is applied (see ``require_function``)."""
     if not name or name in ("ColumnExtract", "PythonFunction"):
         return None
-    import importlib
-    mod, _, qn = name.rpartition(".")
-    while mod:
-        try:
-            obj = importlib.import_module(mod)
-            break
-        except ImportError:
-            mod, _, head = mod.rpartition(".")
-            qn = head + "." + qn
-    else:
-        return None
-    for part in qn.split("."):
-        obj = getattr(obj, part, None)
-        if obj is None:
-            return None
-    return obj if callable(obj) else None
+    fn = _FUNCTIONS.get(name)
+    if fn is None:
+        log.warning("checkpoint names function %r which is not registered in this process; register it with "
+                    "transmogrifai_amd.register_function before loading the model to restore it", name)
+    return fn
+
+
+def require_function(fn, name: Optional[str]):
+    if fn is None:
+        raise RuntimeError(f"function {name!r} is not registered; call register_function on it before loading")
+    return fn

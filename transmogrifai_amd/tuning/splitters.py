@@ -137,6 +137,7 @@ class DataBalancer(Splitter):
             self.already_balanced = True
             self.down_sample_fraction = min(mx / max(total, 1), 1.0)
             self.up_fraction = 1.0
+            reported_up = 0.0        # DataBalancer.scala:233-234 reports 0.0 when already balanced
         else:
             # getProportions (DataBalancer.scala:84-122)
             def fits(mult):
@@ -148,9 +149,10 @@ class DataBalancer(Splitter):
                 up = (mx * f) / small
                 down = (1 - f) * mx / big
             self.up_fraction, self.down_sample_fraction = up, min(down, 1.0)
+            reported_up = self.up_fraction
         self.summary = {"className": "com.salesforce.op.stages.impl.tuning.DataBalancerSummary",
                         "positiveLabels": int(pos), "negativeLabels": int(neg), "desiredFraction": f,
-                        "upSamplingFraction": self.up_fraction, "downSamplingFraction": self.down_sample_fraction}
+                        "upSamplingFraction": reported_up, "downSamplingFraction": self.down_sample_fraction}
         return self.summary
 
     def validation_prepare(self, row_ids, y, stream=7):
@@ -163,17 +165,24 @@ class DataBalancer(Splitter):
             return (u < self.down_sample_fraction).to(torch.int64)
         small_mask = (y > 0.5) if self.positive_is_small else (y <= 0.5)
         big_keep = (u < self.down_sample_fraction).to(torch.int64)
-        # Poisson(up) for the minority class via inverse CDF on the same uniform stream
         lam = self.up_fraction
         u2 = row_uniform(row_ids, self.seed, stream + 101)
-        k = torch.zeros_like(u2, dtype=torch.int64)
-        p = torch.exp(torch.tensor(-lam, dtype=torch.float64))
-        cdf = p.clone()
-        pk = p.clone()
-        for i in range(1, 64):
-            k += (u2 >= cdf).to(torch.int64)
-            pk = pk * lam / i
-            cdf = cdf + pk
+        # rebalance (DataBalancer.scala:287-291): up > 1 samples the minority with replacement
+        # (Poisson(up) multiplicities), up == 1 keeps it as is, up < 1 samples without replacement
+        if lam > 1.0:
+            k = torch.zeros_like(u2, dtype=torch.int64)
+            p = math.exp(-lam)
+            cdf, pk = p, p
+            for i in range(1, 64):
+                k += (u2 >= cdf).to(torch.int64)
+                pk = pk * lam / i
+                cdf = cdf + pk
+                if 1.0 - cdf < 1e-15:
+                    break
+        elif lam == 1.0:
+            k = torch.ones_like(u2, dtype=torch.int64)
+        else:
+            k = (u2 < lam).to(torch.int64)
         return torch.where(small_mask, k, big_keep)
 
     def params(self):

@@ -6,7 +6,9 @@ rawFeatureFilterResults; written gzip-compressed as ``op-model.json/part-00000.g
 (``features/.../stages/OpPipelineStageWriter.scala:67-88``: class, uid, paramMap, ctorArgs) and
 ``OpWorkflowModelReader`` (``OpWorkflowModelReader.scala:97-266``: falls back through ``part-00000.gz``,
 ``part-00000`` and the raw path; accepts the legacy ``blacklisted*`` field names). Learned tensors are
-stored inline as base64 arrays (:mod:`transmogrifai_amd.utils.serde`); nothing is unpickled on load.
+stored inline as base64 arrays (:mod:`transmogrifai_amd.utils.serde`); nothing is unpickled on load, and
+user functions named by a checkpoint (extract functions) resolve only through the in-process registry
+(``stages/generator.py`` ``register_function``): loading never imports a module.
 """
 from __future__ import annotations
 
