@@ -55,6 +55,15 @@ def parse():
     return ap.parse_args()
 
 
+def _expected_configs(args) -> int:
+    """Grid points the selector must evaluate (default binary grid: LR 8 + RF 18 + XGBoost 2)."""
+    from transmogrifai_amd.selector.factories import BinaryClassificationModelSelector
+    types = None if args.models == "default" else args.models.split(",")
+    sel = BinaryClassificationModelSelector.with_cross_validation(num_folds=args.folds, model_types_to_use=types,
+                                                                  seed=42)
+    return sum(len(grid) for _, grid in sel.models)
+
+
 def build_workflow(args, ds, label, preds):
     from transmogrifai_amd.dsl import transmogrify
     from transmogrifai_amd.readers.base import InMemoryReader
@@ -69,8 +78,31 @@ def build_workflow(args, ds, label, preds):
     return wf, pred
 
 
+def _spawned_rank(local_rank, n, port, argv):
+    """Entry of a rank process started by ``bench.py --gpus N`` without torchrun."""
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(n),
+                      LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.argv = argv
+    main()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one rank per GPU, spawned before anything in this process touches the GPU (never exec)
+        import torch.multiprocessing as mp
+        mp.start_processes(_spawned_rank, args=(args.gpus, _free_port(), list(sys.argv)), nprocs=args.gpus,
+                           join=True, start_method="spawn")
+        return
     import torch
     from transmogrifai_amd import config as CFG
     from transmogrifai_amd.parallel import dist as D
@@ -84,6 +116,9 @@ def main():
     else:
         dev = torch.device("cpu")
     D.init_from_env(device_id=local_rank if use_gpu else None)
+    world = D.world()
+    if world != max(1, args.gpus) and args.device != "cpu":
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} ranks")
     CFG.set_default_device(dev)
     if use_gpu:
         from transmogrifai_amd.ops import _native
@@ -113,8 +148,17 @@ def main():
         sel = model.get_origin_stage_of(pred)
         summ = sel.metadata.get("summary", {})
         ho = (summ.get("holdoutEvaluation") or {}).get("AuPR", float("nan"))
+        # a learner that dies must not make the headline faster: every configured grid point must have
+        # been evaluated and nothing may have failed
+        n_eval = len(summ.get("validationResults") or [])
+        if summ.get("failures") or n_eval != expected_configs:
+            raise SystemExit(f"model selector evaluated {n_eval}/{expected_configs} configs; failures: "
+                             f"{summ.get('failures')}")
         return dt, ho, summ, model
 
+    expected_configs = _expected_configs(args)
+    if use_gpu:
+        torch.cuda.reset_peak_memory_stats(dev)
     for _ in range(args.warmup):
         one_run()
     times, auprs, summ = [], [], None
@@ -125,6 +169,8 @@ def main():
     t = torch.tensor([sum(times)], dtype=torch.float64)
     t = D.all_reduce(t, "max")
     total = float(t.item())
+    peak = torch.tensor([float(torch.cuda.max_memory_allocated(dev)) if use_gpu else 0.0], dtype=torch.float64)
+    peak = float(D.all_reduce(peak, "max").item())
     per_step = total / max(args.steps, 1)
     if D.rank() == 0:
         out = {
@@ -142,6 +188,8 @@ def main():
             "data": "synthetic (device-generated, seeded), random-init models",
             "holdout_aupr": auprs[-1],
             "best_model": summ.get("bestModelType") if summ else None,
+            "configs_evaluated": len(summ.get("validationResults") or []) if summ else 0,
+            "peak_hbm_gb_per_gpu": round(peak / 1e9, 3),
             "config": {"model": "BinaryClassificationModelSelector(" +
                                 ("LR,RF,XGB default grid" if args.models == "default" else args.models) + ")",
                        "rows": args.rows, "raw_columns": args.real + args.ints + args.pick,

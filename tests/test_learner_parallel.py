@@ -1,0 +1,189 @@
+"""Intra-job parallelism of the learners over ranks (gloo, world_size 2 and 3).
+
+* Feature-parallel tree growth (parallel/learner_parallel.py, common/tree_grow.hpp): every rank
+  grows every tree over its feature slice and the ranks all-gather one split record per node and
+  level -- the forests must equal the single-process forests bit for bit (XGBoost's Rabit workers
+  produce the same trees as one worker, ``OpXGBoostClassifier.scala:111``).
+* Row-parallel linear models: the objective's sums are all-reduced per pass (Spark's
+  ``treeAggregate`` of the L-BFGS gradient) -- coefficients must match the
+  single-process fit to float tolerance and be identical on every rank.
+"""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn_name, out_dir):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(2)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = globals()[fn_name](rank, world)
+        with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
+            json.dump(res, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(fn_name, tmp_path, world=2):
+    port = _free_port()
+    mp.start_processes(_worker, args=(world, port, fn_name, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    return [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
+
+
+def _data(n=3000, d=24, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, d, generator=g)
+    X[:, 5] = (X[:, 5] > 0.3).float()            # 0/1 indicator columns (one present bin under missing=0)
+    X[:, 9] = (X[:, 9] > -0.2).float()
+    X[:, 11] = torch.where(torch.rand(n, generator=g) < 0.3, torch.zeros(n), X[:, 11])   # sparse numeric
+    logit = X[:, 0] - 0.7 * X[:, 3] + 0.9 * X[:, 5] + 0.4 * X[:, 11] * X[:, 2]
+    y = (torch.rand(n, generator=g) < torch.sigmoid(logit)).float()
+    return X, y
+
+
+def _forest_sig(state):
+    f = state["forest"]
+    return {k: np.asarray(f[k]).tolist() for k in ("tree_off", "nodes", "default_left", "value")}
+
+
+def _trees(par):
+    from transmogrifai_amd.models.base import FitJob, learner_class
+    X, y = _data()
+    rows = [torch.arange(0, 2000), torch.arange(1000, 3000)]
+    ctx = {"par": par} if par is not None else {}
+    out = {}
+    xgb = learner_class("OpXGBoostClassifier")()
+    jobs = [FitJob(dict(xgb.defaults, num_round=6, max_depth=5, min_child_weight=mcw, missing=0.0, eta=0.3,
+                        gamma=0.1, max_bins=32), r) for mcw in (1.0, 10.0) for r in rows]
+    out["xgb"] = [_forest_sig(s) for s in xgb.fit_batch(X, y, jobs, context=ctx)]
+    gbt = learner_class("OpGBTClassifier")()
+    out["gbt"] = [_forest_sig(s) for s in gbt.fit_batch(
+        X, y, [FitJob(dict(gbt.defaults, max_iter=3, max_depth=4), r) for r in rows], context=ctx)]
+    dt = learner_class("OpDecisionTreeClassifier")()
+    out["dt"] = [_forest_sig(s) for s in dt.fit_batch(
+        X, y, [FitJob(dict(dt.defaults, max_depth=6), r) for r in rows], context=ctx)]
+    return out
+
+
+def _trees_fp(rank, world):
+    from transmogrifai_amd.parallel.learner_parallel import LearnerParallel
+    return _trees(LearnerParallel())
+
+
+def test_feature_parallel_trees_bit_identical(tmp_path):
+    ref = _trees(None)
+    for world in (2, 3):
+        outs = _run("_trees_fp", tmp_path, world)
+        for r, o in enumerate(outs):
+            for k in ("xgb", "gbt", "dt"):
+                assert o[k] == ref[k], f"{k} forest differs on rank {r} of {world}"
+    # the trees are not trivial
+    assert any(len(f["nodes"]) > 10 for f in ref["xgb"])
+
+
+def _linear(par):
+    from transmogrifai_amd.models.base import FitJob, learner_class
+    X, y = _data(n=2000, d=12, seed=3)
+    rows = [torch.arange(0, 1500), torch.arange(500, 2000)]
+    ctx = {"par": par} if par is not None else {}
+    lr = learner_class("OpLogisticRegression")()
+    jobs = [FitJob(dict(lr.defaults, reg_param=rp, elastic_net_param=en, max_iter=50), r)
+            for rp, en in ((0.01, 0.0), (0.1, 0.5)) for r in rows]
+    res = {"lr": [s["coefficients"].tolist() + [s["intercept"]] for s in lr.fit_batch(X, y, jobs, context=ctx)]}
+    lin = learner_class("OpLinearRegression")()
+    yr = X[:, 0] * 2.0 - X[:, 4] + 0.1 * torch.randn(X.shape[0], generator=torch.Generator().manual_seed(1))
+    res["linreg"] = [s["coefficients"].tolist() + [s["intercept"]] for s in lin.fit_batch(
+        X, yr, [FitJob(dict(lin.defaults, reg_param=0.05, max_iter=50), r) for r in rows], context=ctx)]
+    return res
+
+
+def _linear_rp(rank, world):
+    from transmogrifai_amd.parallel.learner_parallel import LearnerParallel
+    return _linear(LearnerParallel())
+
+
+def test_row_parallel_linear_models(tmp_path):
+    ref = _linear(None)
+    outs = _run("_linear_rp", tmp_path, 2)
+    assert outs[0] == outs[1]                      # every rank holds the same coefficients
+    for k in ("lr", "linreg"):
+        # same optimum up to the optimizer tolerance (fp32 partial sums are added in another order)
+        np.testing.assert_allclose(np.asarray(outs[0][k]), np.asarray(ref[k]), rtol=0, atol=1.5e-3)
+
+
+def test_feature_slices_balance():
+    from transmogrifai_amd.parallel.learner_parallel import feature_slices
+    assert feature_slices(3, [1.0] * 10, 4) is None
+    sl = feature_slices(10, [5.0, 1.0, 1.0, 1.0, 1.0, 1.0], 2)
+    assert sl == [(0, 5, 0, 1), (5, 10, 1, 6)]
+    sl = feature_slices(8, [], 3)
+    assert [s[:2] for s in sl] == [(0, 2), (2, 5), (5, 8)] and all(s[2:] == (0, 0) for s in sl)
+
+
+@pytest.mark.gpu
+def test_feature_parallel_rccl_path_on_one_gpu():
+    """The GPU feature-parallel path (RCCL communicator per job group, on-stream ncclAllGather of the
+    split records, fp_merge_kernel) forced on a 1-rank world: XGBoost / GBT / DT trees equal the plain
+    single-GPU growth bit for bit. Multi-rank transport runs in the driver's multi-GPU bench."""
+    _fp_one_rank(torch.device("cuda"))
+
+
+def test_feature_parallel_exchange_path_one_rank_cpu():
+    _fp_one_rank(torch.device("cpu"))
+
+
+def _fp_one_rank(dev):
+    from transmogrifai_amd.models import tree_engine as TE
+    from transmogrifai_amd.models.binning import find_splits, quantize
+    from transmogrifai_amd.parallel.learner_parallel import LearnerParallel
+    X, y = _data(n=6000, d=40)
+    X, y = X.to(dev), y.to(dev)
+    par = LearnerParallel(rank=0, world=1)
+    spec = find_splits(X, 32, missing_value=0.0, reserve_missing=True)
+    Xb = quantize(X, spec)
+    N = X.shape[0]
+    g = torch.sigmoid(0.3 * X[:, 0]) - y
+    t1 = torch.stack([g, 0.5 * g]).float()
+    t2 = torch.full_like(t1, 0.25)
+    jobs = [TE.TreeJob(m, TE.TreeParams(max_depth=6, min_child_weight=1.0, reg_lambda=1.0, gamma=0.1, eta=0.3,
+                                        split_eps=1e-6), torch.arange(N, device=dev)) for m in range(2)]
+    kw = dict(mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=t1, t2=t2, B=32, missing_bin=spec.missing_bin,
+              collect_leaves=True)
+    gpu = dev.type == "cuda"
+    ref = TE.grow_forest(Xb, spec.n_bins, jobs, csr=TE.onebin_csr(Xb, spec.n_bins) if gpu else None, **kw)
+    fp = TE.fp_plan(Xb, spec.n_bins, par, sparse=True, force=True)
+    assert fp is not None
+    got = TE.grow_forest(Xb, spec.n_bins, jobs, csr=TE.onebin_csr(Xb, spec.n_bins, cols=fp.one_cols) if gpu else None,
+                         fp=fp, **kw)
+    for k in ("tree_off", "nodes", "default_left", "value"):
+        assert np.array_equal(getattr(ref, k), getattr(got, k)), k
+    # non-sparse (GBT variance / DT gini) slices
+    spec2 = find_splits(X, 32)
+    Xb2 = quantize(X, spec2)
+    jobs2 = [TE.TreeJob(0, TE.TreeParams(max_depth=6), torch.arange(N, device=dev))]
+    fp2 = TE.fp_plan(Xb2, spec2.n_bins, par, sparse=False, force=True)
+    for mode, kind, extra in ((TE.MODE_VAR, TE.KIND_VARIANCE, dict(t1=y.float()[None, :])),
+                              (TE.MODE_CLS, TE.KIND_GINI, dict(y=y, n_classes=2))):
+        a = TE.grow_forest(Xb2, spec2.n_bins, jobs2, mode=mode, kind=kind, B=32, **extra)
+        b = TE.grow_forest(Xb2, spec2.n_bins, jobs2, mode=mode, kind=kind, B=32, fp=fp2, **extra)
+        assert np.array_equal(a.nodes, b.nodes) and np.array_equal(a.value, b.value)

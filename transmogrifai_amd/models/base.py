@@ -88,6 +88,9 @@ class Learner:
     name = "Learner"
     problem = "binary"          # binary | multiclass | regression
     defaults: Dict[str, Any] = {}
+    # intra-job parallelism over ranks (parallel/learner_parallel.py): "rows" (linear models),
+    # "features" (boosted / single trees) or None (jobs sharded whole over the ranks)
+    parallel: Optional[str] = None
 
     def __init__(self, **params):
         p = dict(self.defaults)

@@ -29,11 +29,14 @@ from ..stages.base import register_stage
 class BatchedObjective:
     """Smooth objective of P linear problems sharing the design matrix ``X``."""
 
-    def __init__(self, X, y, W, inv_std, loss, l2, fit_intercept, y_scale=None):
+    def __init__(self, X, y, W, inv_std, loss, l2, fit_intercept, y_scale=None, par=None):
         self.X = X
         self.y = y
         self.W = W                      # [N, P] row weights (0 outside a problem's training rows)
-        self.wsum = W.sum(0).to(torch.float64).clamp_min(1e-300)
+        # row-parallel (parallel/learner_parallel.py): X / y / W hold this rank's rows; every per-problem
+        # sum is all-reduced (one fused collective per objective pass), the updates run identically
+        self.par = par
+        self.wsum = _psum(par, W.sum(0).to(torch.float64))[0].clamp_min(1e-300)
         self.inv_std = inv_std          # [d, P]
         self.loss = loss
         self.l2 = l2                    # [P]
@@ -79,16 +82,16 @@ class BatchedObjective:
 
     def value(self, U):
         if self.fused:
-            f = self._fused_pass(U, False)[0] / self.wsum
+            f = _psum(self.par, self._fused_pass(U, False)[0])[0] / self.wsum
             return f + 0.5 * self.l2 * (U[:self.d] ** 2).sum(0)
         M = self.margins(U)
         l, _ = self._elem(M, False)
-        f = (l * self.W).sum(0).to(torch.float64) / self.wsum
+        f = _psum(self.par, (l * self.W).sum(0).to(torch.float64))[0] / self.wsum
         return f + 0.5 * self.l2 * (U[:self.d] ** 2).sum(0)
 
     def value_grad(self, U):
         if self.fused:
-            f, r, G = self._fused_pass(U, True)
+            f, r, G = _psum(self.par, *self._fused_pass(U, True))
             g = torch.zeros_like(U)
             g[:self.d] = (G / self.wsum[None, :]) * self.inv_std + self.l2[None, :] * U[:self.d]
             g[self.d] = torch.where(self.fi, r / self.wsum, torch.zeros_like(self.wsum))
@@ -96,12 +99,14 @@ class BatchedObjective:
         M = self.margins(U)
         l, dm = self._elem(M, True)
         R = dm * self.W
-        f = (l * self.W).sum(0).to(torch.float64) / self.wsum
-        G = LK.gemm_t(self.X, R).to(torch.float64) / self.wsum[None, :]
+        fs, Gs, rs = _psum(self.par, (l * self.W).sum(0).to(torch.float64), LK.gemm_t(self.X, R).to(torch.float64),
+                           R.sum(0).to(torch.float64))
+        f = fs / self.wsum
+        G = Gs / self.wsum[None, :]
         self.passes += 1
         g = torch.zeros_like(U)
         g[:self.d] = G * self.inv_std + self.l2[None, :] * U[:self.d]
-        g[self.d] = torch.where(self.fi, R.sum(0).to(torch.float64) / self.wsum, torch.zeros_like(self.wsum))
+        g[self.d] = torch.where(self.fi, rs / self.wsum, torch.zeros_like(self.wsum))
         f = f + 0.5 * self.l2 * (U[:self.d] ** 2).sum(0)
         return f, g
 
@@ -111,10 +116,11 @@ class MultinomialObjective:
     ``[d+1, K]`` blocks (class-major coefficient columns), so the batched OWL-QN is reused unchanged.
     One GEMM ``X [N,d] @ V [d, P*K]`` produces every problem's class margins."""
 
-    def __init__(self, X, y, W, inv_std, l2, fit_intercept, K):
+    def __init__(self, X, y, W, inv_std, l2, fit_intercept, K, par=None):
         self.X, self.W, self.K = X, W, K
+        self.par = par
         self.Y = torch.nn.functional.one_hot(y.to(torch.int64), K).to(X.dtype)      # [N, K]
-        self.wsum = W.sum(0).to(torch.float64).clamp_min(1e-300)
+        self.wsum = _psum(par, W.sum(0).to(torch.float64))[0].clamp_min(1e-300)
         self.inv_std = inv_std      # [d, P]
         self.l2, self.fi = l2, fit_intercept
         self.d = X.shape[1]
@@ -143,7 +149,7 @@ class MultinomialObjective:
     def value(self, U):
         M = self.margins(U)
         l, _ = self._loss(M)
-        f = (l * self.W).sum(0).to(torch.float64) / self.wsum
+        f = _psum(self.par, (l * self.W).sum(0).to(torch.float64))[0] / self.wsum
         B = U.reshape(self.d + 1, self.K, -1)
         return f + 0.5 * self.l2 * (B[:self.d] ** 2).sum((0, 1))
 
@@ -153,14 +159,17 @@ class MultinomialObjective:
         Pr = torch.exp(M - lse[:, :, None])
         R = (Pr - self.Y[:, None, :]) * self.W[:, :, None]                        # [N, P, K]
         P = U.shape[1]
-        f = (l * self.W).sum(0).to(torch.float64) / self.wsum
-        G = LK.gemm_t(self.X, R.reshape(-1, P * self.K)).to(torch.float64).reshape(self.d, P, self.K)
+        fs, Gs, rs = _psum(self.par, (l * self.W).sum(0).to(torch.float64),
+                           LK.gemm_t(self.X, R.reshape(-1, P * self.K)).to(torch.float64),
+                           R.sum(0).to(torch.float64))
+        f = fs / self.wsum
+        G = Gs.reshape(self.d, P, self.K)
         G = G.permute(0, 2, 1) / self.wsum[None, None, :]                          # [d, K, P]
         self.passes += 1
         B = U.reshape(self.d + 1, self.K, P)
         g = torch.zeros_like(B)
         g[:self.d] = G * self.inv_std[:, None, :] + self.l2[None, None, :] * B[:self.d]
-        gb = R.sum(0).to(torch.float64).t() / self.wsum[None, :]                  # [K, P]
+        gb = rs.t() / self.wsum[None, :]                                           # [K, P]
         g[self.d] = torch.where(self.fi[None, :], gb, torch.zeros_like(gb))
         f = f + 0.5 * self.l2 * (B[:self.d] ** 2).sum((0, 1))
         return f, g.reshape(U.shape)
@@ -261,11 +270,22 @@ def _fold_weights(N, jobs: Sequence[FitJob], dev, dtype):
     return W
 
 
-def _feature_std(X, W):
+def _psum(par, *ts):
+    """Sum of per-rank partial sums (identity without a row-parallel context)."""
+    if par is None or par.world <= 1:
+        return list(ts)
+    return par.sum(*ts)
+
+
+def _row_par(context):
+    par = context.get("par") if isinstance(context, dict) else None
+    return par if (par is not None and par.world > 1) else None
+
+
+def _feature_std(X, W, par=None):
     """Unbiased weighted std per column and problem (``[d, P]``) via two GEMMs."""
-    n = W.sum(0).to(torch.float64)
-    s1 = LK.gemm_t(X, W).to(torch.float64)
-    s2 = LK.gemm_t(X * X, W).to(torch.float64)
+    n, s1, s2 = _psum(par, W.sum(0).to(torch.float64), LK.gemm_t(X, W).to(torch.float64),
+                      LK.gemm_t(X * X, W).to(torch.float64))
     mean = s1 / n.clamp_min(1)[None, :]
     var = (s2 - n[None, :] * mean * mean) / (n - 1).clamp_min(1)[None, :]
     return torch.sqrt(var.clamp_min(0)), mean
@@ -273,13 +293,21 @@ def _feature_std(X, W):
 
 class _LinearBase(Learner):
     loss = "logistic"
+    parallel = "rows"
 
-    def _setup(self, X, y, jobs):
+    def _setup(self, X, y, jobs, par=None):
+        """Fold weights, feature scales and per-problem hyper-parameters. With a row-parallel context
+        ``X`` / ``y`` / ``W`` are cut to this rank's contiguous row slice (``par.row_slice``) and the
+        column statistics are all-reduced. Returns ``(X, y, W, std, mean, inv_std, reg, en, fi,
+        max_iter, tol, stdz)``."""
         dev = X.device
         N, d = X.shape
         P = len(jobs)
         W = _fold_weights(N, jobs, dev, X.dtype)
-        std, mean = _feature_std(X, W)
+        if par is not None:
+            sl = par.row_slice(N)
+            X, y, W = X[sl], y[sl], W[sl].contiguous()
+        std, mean = _feature_std(X, W, par)
         stdz = [bool(j.params.get("standardization", True)) for j in jobs]
         inv_std = torch.where(std > 0, 1.0 / std.clamp_min(1e-300), torch.zeros_like(std))
         for p, s in enumerate(stdz):
@@ -290,7 +318,7 @@ class _LinearBase(Learner):
         fi = to_device([bool(j.params.get("fit_intercept", True)) for j in jobs], dev, np.bool_)
         max_iter = to_device([int(j.params.get("max_iter", 100)) for j in jobs], dev, np.int64)
         tol = to_device([float(j.params.get("tol", 1e-6)) for j in jobs], dev, np.float64)
-        return W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz
+        return X, y, W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz
 
 
 @register_learner
@@ -301,16 +329,17 @@ class LogisticRegressionLearner(_LinearBase):
                 "standardization": True, "tol": 1e-6, "threshold": 0.5}
     loss = "logistic"
 
-    def _fit_multinomial(self, X, y, jobs, K):
+    def _fit_multinomial(self, X, y, jobs, K, par=None):
         """Spark ``family=multinomial`` (chosen by ``auto`` when there are more than 2 classes)."""
         dev = X.device
         N, d = X.shape
         P = len(jobs)
-        W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs)
+        X, y, W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs, par)
         l2 = reg * (1 - en)
-        obj = MultinomialObjective(X, y, W, inv_std, l2, fi, K)
+        obj = MultinomialObjective(X, y, W, inv_std, l2, fi, K, par=par)
         U0 = torch.zeros(d + 1, K, P, dtype=torch.float64, device=dev)
-        cnt = torch.stack([(W * (y == k)[:, None].to(W.dtype)).sum(0) for k in range(K)]).to(torch.float64)
+        cnt = _psum(par, torch.stack([(W * (y == k)[:, None].to(W.dtype)).sum(0)
+                                      for k in range(K)]).to(torch.float64))[0]
         pri = (cnt / cnt.sum(0, keepdim=True).clamp_min(1e-300)).clamp_min(1e-12)
         lp = torch.log(pri)
         U0[d] = torch.where(fi[None, :], lp - lp.mean(0, keepdim=True), torch.zeros_like(lp))
@@ -333,16 +362,17 @@ class LogisticRegressionLearner(_LinearBase):
         if P == 0:
             return []
         K = int(y.max().item()) + 1 if y.numel() else 2
+        par = _row_par(context)
         if self.loss == "logistic" and K > 2:
-            return self._fit_multinomial(X, y, jobs, K)
-        W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs)
+            return self._fit_multinomial(X, y, jobs, K, par)
+        X, y, W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs, par)
         l2 = reg * (1 - en)
         l1v = reg * en
-        obj = BatchedObjective(X, y, W, inv_std, self.loss, l2, fi)
+        obj = BatchedObjective(X, y, W, inv_std, self.loss, l2, fi, par=par)
         U0 = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)
         if self.loss == "logistic":
-            pos = (W * y[:, None].to(W.dtype)).sum(0).to(torch.float64)
-            tot = W.sum(0).to(torch.float64)
+            pos, tot = _psum(par, (W * y[:, None].to(W.dtype)).sum(0).to(torch.float64),
+                             W.sum(0).to(torch.float64))
             p1 = (pos / tot.clamp_min(1e-300)).clamp(1e-12, 1 - 1e-12)
             U0[d] = torch.where(fi, torch.log(p1 / (1 - p1)), torch.zeros_like(p1))
         l1 = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)
@@ -425,14 +455,15 @@ class LinearRegressionLearner(_LinearBase):
         P = len(jobs)
         if P == 0:
             return []
-        W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs)
+        par = _row_par(context)
+        X, y, W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs, par)
         yv = y.to(torch.float64)
-        n = W.sum(0).to(torch.float64)
-        ym = (W.to(torch.float64) * yv[:, None]).sum(0) / n.clamp_min(1)
-        yvar = (W.to(torch.float64) * (yv[:, None] - ym[None, :]) ** 2).sum(0) / (n - 1).clamp_min(1)
+        n, sy = _psum(par, W.sum(0).to(torch.float64), (W.to(torch.float64) * yv[:, None]).sum(0))
+        ym = sy / n.clamp_min(1)
+        yvar = _psum(par, (W.to(torch.float64) * (yv[:, None] - ym[None, :]) ** 2).sum(0))[0] / (n - 1).clamp_min(1)
         ystd = torch.sqrt(yvar).clamp_min(1e-12)
         eff = reg / ystd
-        obj = BatchedObjective(X, y, W, inv_std, "squared", eff * (1 - en), fi, y_scale=ystd)
+        obj = BatchedObjective(X, y, W, inv_std, "squared", eff * (1 - en), fi, y_scale=ystd, par=par)
         U0 = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)
         U0[d] = torch.where(fi, ym / ystd, torch.zeros_like(ym))
         l1 = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)

@@ -245,18 +245,63 @@ class _GrowArgs(C.Structure):
                 ("leaf_rows", C.c_void_p), ("leaf_gid", C.c_void_p), ("n_groups", C.c_int32),
                 ("group_start", C.c_void_p), ("rng_seed", C.c_int64), ("stream", C.c_void_p),
                 ("n_bins_host", C.c_void_p), ("csr_ptr", C.c_void_p), ("csr_col", C.c_void_p),
-                ("csr_nf", C.c_int32)]
+                ("csr_nf", C.c_int32), ("fp_rank", C.c_int32), ("fp_world", C.c_int32), ("fp_mlo", C.c_int32),
+                ("fp_mhi", C.c_int32), ("fp_olo", C.c_int32), ("fp_ohi", C.c_int32), ("fp_comm", C.c_void_p),
+                ("fp_exchange", C.c_void_p), ("fp_ctx", C.c_void_p)]
 
 
-def onebin_csr(Xb: torch.Tensor, n_bins: np.ndarray, block_rows: int = 1 << 20):
+@dataclass
+class FpPlan:
+    """This rank's share of a feature-parallel ``grow_forest`` (see parallel/learner_parallel.py):
+    positions ``[mlo, mhi)`` of the multi-bin and ``[olo, ohi)`` of the one-present-bin growth-order
+    feature lists, and ``one_cols`` = the ``Xb`` columns of that one-present slice (the CSR to build)."""
+    par: object                      # parallel.learner_parallel.LearnerParallel
+    mlo: int
+    mhi: int
+    olo: int
+    ohi: int
+    one_cols: np.ndarray
+    sparse: bool = False
+
+
+def fp_plan(Xb: torch.Tensor, n_bins, par, sparse: bool, force: bool = False) -> Optional[FpPlan]:
+    """Split the features of ``Xb`` over ``par``'s ranks for feature-parallel growth (None when not
+    possible: one rank, or fewer multi-bin columns than ranks -- then every rank grows everything).
+    ``sparse``: MODE_GH with a missing bin, where one-present-bin columns form their own list."""
+    from ..parallel.learner_parallel import feature_slices
+    if par is None or (par.world <= 1 and not force):
+        return None
+    nb = np.asarray(n_bins)
+    if sparse:
+        multi, one = np.nonzero(nb != 1)[0], np.nonzero(nb == 1)[0]
+    else:
+        multi, one = np.arange(nb.size), np.zeros(0, np.int64)
+    if one.size:
+        idx = torch.as_tensor(one, dtype=torch.int64, device=Xb.device)
+        w = torch.zeros(one.size, dtype=torch.float64, device=Xb.device)
+        for r0 in range(0, int(Xb.shape[0]), 1 << 20):
+            w += (Xb[r0:r0 + (1 << 20)].index_select(1, idx) == 0).sum(0).to(torch.float64)
+        weights = w.cpu().numpy()
+    else:
+        weights = np.zeros(0)
+    sl = feature_slices(int(multi.size), weights, par.world, force=force)
+    if sl is None:
+        return None
+    mlo, mhi, olo, ohi = sl[par.rank]
+    return FpPlan(par, mlo, mhi, olo, ohi, one[olo:ohi].astype(np.int64), bool(sparse))
+
+
+def onebin_csr(Xb: torch.Tensor, n_bins: np.ndarray, block_rows: int = 1 << 20, cols: Optional[np.ndarray] = None):
     """Row-wise CSR of the one-present-bin columns of ``Xb`` (``n_bins == 1``: one-hot / null indicator
     columns under a sparse missing bin), for the histogram kernel's CSR path.
 
     Returns ``(ptr int64 [N + 1], col int16 [max(nnz, 1)] (read as uint16), n_cols)``: the entries of
     row ``r`` are ``col[ptr[r]:ptr[r + 1]]``, the ids (in ascending column order among the one-bin
-    columns) of its columns holding the present bin 0. None when there are none or ids do not fit."""
+    columns) of its columns holding the present bin 0. None when there are none or ids do not fit.
+    ``cols``: restrict to these one-present-bin columns (a feature-parallel rank's slice), ids local to
+    the subset."""
     nb = np.asarray(n_bins)
-    one = np.nonzero(nb == 1)[0]
+    one = np.nonzero(nb == 1)[0] if cols is None else np.asarray(cols, np.int64)
     if one.size == 0 or one.size >= (1 << 16) or Xb.dim() != 2:
         return None
     dev = Xb.device
@@ -295,7 +340,8 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 n_classes: int = 2, y: Optional[torch.Tensor] = None, t1: Optional[torch.Tensor] = None,
                 t2: Optional[torch.Tensor] = None, B: int = 32, missing_bin: int = -1,
                 subtract: bool = True, chunk_rows: int = 4096, rng_seed: int = 0,
-                collect_leaves: bool = False, groups: Optional[int] = None, csr=None, root=None) -> Forest:
+                collect_leaves: bool = False, groups: Optional[int] = None, csr=None, root=None,
+                fp: Optional[FpPlan] = None) -> Forest:
     """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``.
 
     The level loop runs natively (``ops/csrc/common/tree_grow.hpp``): on the GPU every job group gets
@@ -310,7 +356,12 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     columns' histograms are then built from the rows' CSR lists (identical results, fewer loads).
 
     ``collect_leaves``: also return, as ``forest.leaf_assign``, the final leaf of every training entry
-    (see ``LeafAssign``) so boosting can update margins without re-walking the new trees."""
+    (see ``LeafAssign``) so boosting can update margins without re-walking the new trees.
+
+    ``fp``: feature-parallel growth (``fp_plan``): every rank calls with the same jobs, rows and ``Xb``;
+    each builds histograms of its feature slice only (``csr`` must then be the slice's, from
+    ``onebin_csr(..., cols=fp.one_cols)``) and all ranks return the same forest -- the one a single
+    rank would grow. Jobs must not use per-node feature subsets."""
     dev = Xb.device
     on_gpu = dev.type == "cuda"
     Nrows, F = int(Xb.shape[0]), int(Xb.shape[1])
@@ -358,14 +409,30 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                and os.environ.get("TMOG_TREE_CSR") != "0")
     if use_csr and (int(csr[0].numel()) != Nrows + 1 or csr[0].device != dev or csr[1].dtype != torch.int16):
         raise ValueError("csr does not match Xb")
+    fpw = 0 if fp is None else int(fp.par.world)      # 0 = not feature-parallel
+    if fpw > 0:
+        if fp.sparse != (mode == MODE_GH and missing_bin >= 0):
+            raise ValueError("feature-parallel plan was made for another histogram mode")
+        if any(j.params.feature_subset is not None and 0 < int(j.params.feature_subset) < F for j in jobs):
+            raise ValueError("feature-parallel growth needs jobs without per-node feature subsets")
+        if use_csr and int(csr[2]) != fp.ohi - fp.olo:
+            raise ValueError("feature-parallel growth needs the CSR of this rank's one-present-bin slice")
+        fp_comm = fp.par.fp.comm_array(dev, ng) if on_gpu else None
+        fp_cb = None if on_gpu else fp.par.fp.exchange_fn()
+    else:
+        fp_comm = fp_cb = None
     a = _GrowArgs(N.ptr(Xb), Nrows, F, mode, kind, S, B, missing_bin, int(chunk_rows), int(bool(subtract)),
                   int(bool(collect_leaves)), N.ptr(yf), N.ptr(t1f), N.ptr(t2f), stride, N.ptr(qscale), N.ptr(qinv),
                   N.ptr(n_bins_t), T, hp["model"], hp["depth"], hp["inst"], hp["gain"], hp["mcw"], hp["lam"], hp["eps"],
                   hp["fsub"], hp["count"], N.ptr(rows), N.ptr(rows_alt), N.ptr(leaf_rows), N.ptr(leaf_gid), ng,
                   hp["cuts"], int(rng_seed), N.stream(dev) if on_gpu else None,
-                  None if os.environ.get("TMOG_TREE_PERM") == "0" else hp["nbins"],
+                  hp["nbins"] if (fpw > 0 or os.environ.get("TMOG_TREE_PERM") != "0") else None,
                   N.ptr(csr[0]) if use_csr else None, N.ptr(csr[1]) if use_csr else None,
-                  int(csr[2]) if use_csr else 0)
+                  int(csr[2]) if use_csr else 0,
+                  int(fp.par.rank) if fpw else 0, fpw, fp.mlo if fpw else 0, fp.mhi if fpw else 0,
+                  fp.olo if fpw else 0, fp.ohi if fpw else 0,
+                  C.cast(fp_comm, C.c_void_p) if fp_comm is not None else None,
+                  C.cast(fp_cb, C.c_void_p) if fp_cb is not None else None, None)
     lib = N.hip() if on_gpu else N.host()
     fn = (lambda name: getattr(lib, f"tmog_hip_{name}")) if on_gpu else (lambda name: getattr(lib, f"tmog_{name}_cpu"))
     h = fn("grow_forest")(C.byref(a))

@@ -49,6 +49,12 @@ class TreeContext:
         return self._cache[key]
 
 
+def _par(context):
+    """The validator's intra-job parallel context (parallel/learner_parallel.py), if any."""
+    par = context.get("par") if isinstance(context, dict) else None
+    return par if (par is not None and par.world > 1) else None
+
+
 def _ctx(X, context):
     if isinstance(context, TreeContext) and context.X is X:
         return context
@@ -157,6 +163,7 @@ class _ForestLearner(Learner):
     classification = True
     default_trees = 20
     is_forest = True
+    parallel = None             # forests: (grid x fold) jobs sharded over ranks
 
     def _num_classes(self, y):
         return max(2, int(y.max().item()) + 1) if y.numel() else 2
@@ -229,14 +236,21 @@ class _ForestLearner(Learner):
                     tjobs.append(TE.TreeJob(0, tp, rows, w, seed + t))
                     owner.append(i)
             root = (torch.cat(root_parts), root_counts) if forests_only and root_parts else None
+            # single trees (no per-node feature subsets) grow feature-parallel over the ranks
+            par = _par(context)
+            fp = None
+            if par is not None and all(t.params.feature_subset is None or t.params.feature_subset >= F
+                                       for t in tjobs):
+                fp = TE.fp_plan(Xb, spec.n_bins, par, sparse=False)
             if self.classification:
                 forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_CLS,
                                         kind=TE.KINDS[jobs[idxs[0]].params.get("impurity", "gini")], n_classes=K,
-                                        y=yg, B=mb, rng_seed=int(jobs[idxs[0]].params.get("seed", 0)), root=root)
+                                        y=yg, B=mb, rng_seed=int(jobs[idxs[0]].params.get("seed", 0)), root=root,
+                                        fp=fp)
             else:
                 forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_VAR, kind=TE.KIND_VARIANCE,
                                         t1=yg.to(torch.float32)[None, :], B=mb,
-                                        rng_seed=int(jobs[idxs[0]].params.get("seed", 0)), root=root)
+                                        rng_seed=int(jobs[idxs[0]].params.get("seed", 0)), root=root, fp=fp)
             owner = np.asarray(owner)
             for i in idxs:
                 ts = np.nonzero(owner == i)[0]
@@ -323,6 +337,7 @@ class DecisionTreeClassifierLearner(_ForestLearner):
     name = "OpDecisionTreeClassifier"
     problem = "multiclass"
     is_forest = False
+    parallel = "features"
     defaults = {"max_depth": 5, "max_bins": 32, "min_instances_per_node": 1, "min_info_gain": 0.0,
                 "impurity": "gini", "seed": 0}
 
@@ -343,6 +358,7 @@ class DecisionTreeRegressorLearner(_ForestLearner):
     problem = "regression"
     classification = False
     is_forest = False
+    parallel = "features"
     defaults = {"max_depth": 5, "max_bins": 32, "min_instances_per_node": 1, "min_info_gain": 0.0,
                 "impurity": "variance", "seed": 0}
 
@@ -351,6 +367,7 @@ class DecisionTreeRegressorLearner(_ForestLearner):
 class _BoostLearner(Learner):
     """Shared boosting loop: all jobs advance one round per engine call."""
     classification = True
+    parallel = "features"       # every rank grows every tree over its feature slice
 
     def _rounds(self, p):
         raise NotImplementedError
@@ -379,7 +396,7 @@ class _BoostLearner(Learner):
                     yd = yd.index_select(0, U)
                     NU = int(U.numel())
                     gjobs = [FitJob(j.params, r, j.weights) for j, r in zip(gjobs, parts)]
-            res = self._boost(Xb, spec, yd, gjobs, NU, F, dev, key[0])
+            res = self._boost(Xb, spec, yd, gjobs, NU, F, dev, key[0], par=_par(context))
             for k, i in enumerate(idxs):
                 out[i] = res[k]
         return out
@@ -432,10 +449,11 @@ class GBTClassifierLearner(_BoostLearner):
             return ys
         return 4 * ys / (1 + torch.exp(2 * ys * Fm))
 
-    def _boost(self, Xb, spec, y, jobs, N, F, dev, mb):
+    def _boost(self, Xb, spec, y, jobs, N, F, dev, mb, par=None):
         P = len(jobs)
         rows = [_rows(j, N, dev) for j in jobs]
         iters = [int(j.params.get("max_iter", 20)) for j in jobs]
+        fp = TE.fp_plan(Xb, spec.n_bins, par, sparse=False) if par is not None else None
         Fm = torch.zeros(P, N, dtype=torch.float64, device=dev)
         yy = y.to(torch.float64)
         forests, weights = [[] for _ in range(P)], [[] for _ in range(P)]
@@ -456,7 +474,7 @@ class GBTClassifierLearner(_BoostLearner):
                     w = (torch.rand(r.numel(), generator=g) < rate).to(torch.int64).to(dev)
                 tjobs.append(TE.TreeJob(p, tp, r, w))
             forest = TE.grow_forest(Xb, spec.n_bins, tjobs, mode=TE.MODE_VAR, kind=TE.KIND_VARIANCE, t1=t1, B=mb,
-                                    collect_leaves=True)
+                                    collect_leaves=True, fp=fp)
             wgts = [1.0 if it == 0 else float(jobs[p].params.get("step_size", 0.1)) for p in act]
             _add_tree_margins(Fm, forest, Xb, act, wgts, tjobs)
             for k, p in enumerate(act):
@@ -514,7 +532,7 @@ class XGBoostClassifierLearner(_BoostLearner):
         bs = min(max(bs, 1e-12), 1 - 1e-12)
         return math.log(bs / (1 - bs))
 
-    def _boost(self, Xb, spec, y, jobs, N, F, dev, mb):
+    def _boost(self, Xb, spec, y, jobs, N, F, dev, mb, par=None):
         from ..evaluators.metrics import binned_aupr_from_counts, binned_aupr_multi
         P = len(jobs)
         rows = [_rows(j, N, dev) for j in jobs]
@@ -547,8 +565,11 @@ class XGBoostClassifierLearner(_BoostLearner):
                 colperm = order.astype(np.int64)
                 Xg = Xb.index_select(1, torch.as_tensor(colperm, device=dev)).contiguous()
                 n_bins_g = nb_all[colperm]
+        # feature-parallel over the ranks: this rank's slice of the growth-order feature lists
+        fp = TE.fp_plan(Xg, n_bins_g, par, sparse=spec.missing_bin >= 0) if par is not None else None
         # one-hot / null-indicator columns: histogram from the rows' CSR lists (tree_kernels.hip)
-        csr = TE.onebin_csr(Xg, n_bins_g) if (dev.type == "cuda" and spec.missing_bin > 0) else None
+        csr = TE.onebin_csr(Xg, n_bins_g, cols=None if fp is None else fp.one_cols) \
+            if (dev.type == "cuda" and spec.missing_bin > 0) else None
         yf = yy.to(torch.float32).contiguous()
         for it in range(max(rounds)):
             act = [p for p in range(P) if it < rounds[p] and not stopped[p]]
@@ -585,7 +606,7 @@ class XGBoostClassifierLearner(_BoostLearner):
                 packed, cnts = root_cache[key]
                 root = (packed.clone(), cnts)
             forest = TE.grow_forest(Xg, n_bins_g, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
-                                    missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root)
+                                    missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root, fp=fp)
             if colperm is not None:
                 internal = forest.nodes[:, 2] >= 0
                 forest.nodes[internal, 0] = colperm[forest.nodes[internal, 0]]

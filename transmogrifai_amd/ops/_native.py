@@ -30,7 +30,8 @@ _HOST_SIGS = {
     "tmog_tree_finalize_cpu": [I64, I32, P, P, P, P, P, P, I32, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P,
                                P, P],
     "tmog_hist_build_cpu": [P, I64, I32, P, I32, P, P, P, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P],
-    "tmog_split_find_cpu": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, P, P],
+    "tmog_split_find_cpu": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, P, P, P, I64, I32, I32,
+                            I32],
     "tmog_partition_cpu": [P, I32, P, P, I32, P, P, P, P, P, I32, P, P],
     "tmog_forest_predict_cpu": [P, I32, I32, P, P, P, P, P, P, P, I32, P, I32, P],
     "tmog_find_splits_cpu": [P, I64, I32, I32, P, P],
@@ -57,7 +58,12 @@ _HOST_SIGS = {
 _HIP_SIGS = {
     "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P, P, P],
     "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
-    "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P, I32, P],
+    "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P, I32, P,
+                            I64, I32, I32, I32, P],
+    "tmog_hip_fp_merge": [P, I32, I32, I64, I32, P, P, P, P, P, P],
+    "tmog_hip_rccl_unique_id": [P, I32],
+    "tmog_hip_rccl_comm_init": [P, I32, I32],
+    "tmog_hip_rccl_comm_destroy": [P],
     "tmog_hip_partition_fused": [P, I32, P, P, P, I32, P, P, P, P, P, P, P, I32, P, P],
     "tmog_hip_leaf_collect": [P, P, I32, P, P, P],
     "tmog_hip_grow_forest": [P],
@@ -87,7 +93,7 @@ _HIP_SIGS = {
 _RESTYPES = {"tmog_tree_finalize_cpu": C.c_int64, "tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
              "tmog_shist_flush": None, "tmog_shist_merge": None, "tmog_shist_bins": None,
              "tmog_shist_size": C.c_int64, "tmog_shist_sum": C.c_double,
-             "tmog_hip_split_cand_bytes": C.c_size_t,
+             "tmog_hip_split_cand_bytes": C.c_size_t, "tmog_hip_rccl_comm_init": C.c_void_p,
              "tmog_grow_forest_cpu": C.c_void_p, "tmog_hip_grow_forest": C.c_void_p,
              "tmog_grow_nodes_cpu": C.c_int64, "tmog_hip_grow_nodes": C.c_int64,
              "tmog_grow_leaf_count_cpu": C.c_int64, "tmog_hip_grow_leaf_count": C.c_int64,

@@ -94,7 +94,7 @@ def build_hip(force: bool = False, arch: str = ARCH) -> Path:
                       "-munsafe-fp-atomics", f"-I{CSRC}", "-o", str(o), str(s)])
                 objs.append(str(o))
             tmp = HIP_SO.with_suffix(f".so.tmp{os.getpid()}")
-            _run([hipcc, f"--offload-arch={arch}", "-shared", "-fPIC", "-o", str(tmp)] + objs)
+            _run([hipcc, f"--offload-arch={arch}", "-shared", "-fPIC", "-o", str(tmp)] + objs + ["-lrccl"])
             os.replace(tmp, HIP_SO)
             for o in objs:
                 try:

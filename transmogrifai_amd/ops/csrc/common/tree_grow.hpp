@@ -62,7 +62,64 @@ struct GrowArgs {
   const int64_t* csr_ptr;     // [N + 1]
   const uint16_t* csr_col;
   int32_t csr_nf;             // number of one-present-bin columns the CSR indexes
+  // Feature-parallel growth (fp_world > 0; jobs without per-node feature subsets). Every rank runs the
+  // same jobs on the same replicated rows and binned matrix but builds histograms and scans splits for
+  // its own slice of the growth-order feature list only: positions [fp_mlo, fp_mhi) of the multi-bin
+  // list and [fp_olo, fp_ohi) of the one-present-bin list (all features count as multi-bin outside the
+  // sparse missing-bin mode). Per level the ranks all-gather one split record per node (fp_rec_bytes)
+  // and every rank merges them with the split scan's total order, so all ranks partition identically
+  // and the forests equal the single-rank ones bit for bit.
+  int32_t fp_rank, fp_world;
+  int32_t fp_mlo, fp_mhi, fp_olo, fp_ohi;
+  void* const* fp_comm;       // GPU: one RCCL communicator per job group
+  int (*fp_exchange)(void* ctx, int group, const void* send, void* recv, int64_t bytes);   // CPU all-gather
+  void* fp_ctx;
 };
+
+// Feature-parallel split record, one per node and rank:
+//   gain f64 @0 | fpos i32 @8 (position in the full growth-order feature list, the tie-break) |
+//   bin i32 @12 | dl i32 @16 | col i32 @20 (Xb column) | left f32[S] @24
+inline size_t fp_rec_bytes(int S) { return (24 + 4 * (size_t)S + 7) & ~size_t(7); }
+
+// Merge of the ranks' records of node j (host twin of tree_kernels.hip fp_merge_kernel).
+inline void fp_merge_host(const uint8_t* recv, int R, int m, size_t rb, int S, int32_t* feat, int32_t* bin,
+                          float* gain, uint8_t* dl, float* left) {
+  for (int j = 0; j < m; ++j) {
+    int w = -1;
+    double bg = -INFINITY;
+    int bf = 0x7fffffff, bd = 0, bb = 0;
+    for (int r = 0; r < R; ++r) {
+      const uint8_t* p = recv + ((size_t)r * m + j) * rb;
+      double g;
+      int32_t f, b, d;
+      std::memcpy(&g, p, 8);
+      std::memcpy(&f, p + 8, 4);
+      std::memcpy(&b, p + 12, 4);
+      std::memcpy(&d, p + 16, 4);
+      if (f == 0x7fffffff) continue;
+      const bool better = g != bg ? g > bg : (f != bf ? f < bf : (d != bd ? d < bd : b < bb));
+      if (w < 0 || better) {
+        w = r; bg = g; bf = f; bd = d; bb = b;
+      }
+    }
+    if (w < 0) {
+      feat[j] = -1;
+      bin[j] = -1;
+      gain[j] = -INFINITY;
+      dl[j] = 0;
+      for (int s = 0; s < S; ++s) left[(size_t)j * S + s] = 0.f;
+      continue;
+    }
+    const uint8_t* p = recv + ((size_t)w * m + j) * rb;
+    int32_t col;
+    std::memcpy(&col, p + 20, 4);
+    feat[j] = col;
+    bin[j] = bb;
+    gain[j] = (float)bg;
+    dl[j] = (uint8_t)bd;
+    std::memcpy(left + (size_t)j * S, p + 24, 4 * (size_t)S);
+  }
+}
 
 struct GroupResult {
   std::vector<int64_t> tree, feat, bin, left, right;
@@ -134,6 +191,13 @@ struct Staging {
   template <class T>
   size_t add(const std::vector<T>& v) { return add(v.data(), v.size() * sizeof(T)); }
   void clear() { buf.clear(); }
+};
+
+// Where split_find writes the feature-parallel split records (rec == nullptr: not feature-parallel).
+struct FpSlice {
+  uint8_t* rec;
+  int64_t rec_bytes;
+  int32_t mlo, nml, obase;   // local feature f -> position f < nml ? mlo + f : obase + (f - nml)
 };
 
 struct FeatGroup {
@@ -233,27 +297,47 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
   std::vector<int32_t> perm_feats;
   int split_n_multi = -1;   // GPU split scan: local features [n_multi, F) have one present bin
   int64_t live_dense = -1;  // GPU zero / subtract: words past this prefix are live only at bin 0
+  const bool fp = a.fp_world > 0;   // 1 rank is allowed (tests run the exchange path on one GPU)
+  if (fp && use_subset) throw std::runtime_error("feature-parallel growth needs jobs without feature subsets");
+  int fp_nml = 0, fp_obase = 0;   // split records: local feature -> position in the full feature list
   if (!use_subset && a.mode == 2 && a.missing_bin >= 0 && a.n_bins_host != nullptr) {
-    for (int f = 0; f < F; ++f)
-      if (a.n_bins_host[f] != 1) perm_feats.push_back(f);
-    const int n_multi = (int)perm_feats.size();
+    std::vector<int32_t> multi, one;
+    for (int f = 0; f < F; ++f) (a.n_bins_host[f] != 1 ? multi : one).push_back(f);
+    int m0 = 0, m1 = (int)multi.size(), o0 = 0, o1 = (int)one.size();
+    if (fp) {
+      m0 = a.fp_mlo; m1 = a.fp_mhi; o0 = a.fp_olo; o1 = a.fp_ohi;
+      if (m0 < 0 || m1 > (int)multi.size() || m1 <= m0 || o0 < 0 || o1 > (int)one.size() || o1 < o0)
+        throw std::runtime_error("bad feature-parallel slice");
+    }
+    perm_feats.assign(multi.begin() + m0, multi.begin() + m1);
+    const int n_multi = m1 - m0;
+    fp_nml = n_multi;
+    fp_obase = (int)multi.size() + o0;
     // node totals are read from local feature 0, which must be a multi-bin column: with no multi-bin
     // column at all every histogram word stays written and scanned (no CSR / reduced write-out)
     split_n_multi = n_multi > 0 ? n_multi : -1;
     if (BK::kGPU && n_multi > 0) live_dense = (int64_t)n_multi * a.B * a.S;
-    for (int f = 0; f < F; ++f)
-      if (a.n_bins_host[f] == 1) perm_feats.push_back(f);
+    perm_feats.insert(perm_feats.end(), one.begin() + o0, one.begin() + o1);
     for (const FeatGroup& g : equal_groups(n_multi)) full_groups.push_back(g);
-    const int n_one = F - n_multi;
+    const int n_one = o1 - o0;
     if (BK::kGPU && a.csr_ptr && a.csr_col && n_multi > 0 && n_one > 0 && a.csr_nf == n_one &&
         2 * n_one + 2 <= 64 * (B * S + 1))
       full_groups.push_back(FeatGroup{n_multi, n_one, false, true});   // one item walks the rows' CSR lists
     else
       for (const FeatGroup& g : equal_groups(n_one))
         full_groups.push_back(FeatGroup{n_multi + g.f0, g.nf, BK::kGPU, false});
+  } else if (fp) {
+    if (a.fp_mlo < 0 || a.fp_mhi > F || a.fp_mhi <= a.fp_mlo) throw std::runtime_error("bad feature-parallel slice");
+    for (int f = a.fp_mlo; f < a.fp_mhi; ++f) perm_feats.push_back(f);
+    fp_nml = (int)perm_feats.size();
+    fp_obase = F;
+    full_groups = equal_groups(fp_nml);
   } else {
     full_groups = equal_groups(F);
   }
+  const int F_use = perm_feats.empty() ? F : (int)perm_feats.size();
+  const int fp_mlo = fp ? a.fp_mlo : 0;
+  const size_t fp_rb = fp_rec_bytes(S);
   for (int depth = 0; depth <= max_depth; ++depth) {
     const int64_t n = (int64_t)lv_gid.size();
     if (n == 0) break;
@@ -289,7 +373,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     } else {
       for (int j = 0; j < m; ++j) {
         feat_off[j] = 0;
-        nfeat[j] = F;
+        nfeat[j] = F_use;
       }
       if (!perm_feats.empty()) feat_list = perm_feats;
     }
@@ -432,11 +516,16 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     const size_t r_cl = 0, r_feat = r_cl + 16 * (size_t)m, r_bin = r_feat + 4 * (size_t)m, r_gain = r_bin + 4 * (size_t)m;
     const size_t r_left = r_gain + 4 * (size_t)m, r_tot = r_left + 4 * (size_t)m * S, r_dl = r_tot + 4 * (size_t)m * S;
     const size_t r_bytes = r_dl + (size_t)m;
-    uint8_t* res = bk.result_buffer(r_bytes);
+    const size_t r_rec = (r_bytes + 7) & ~size_t(7);
+    uint8_t* res = bk.result_buffer(fp ? r_rec + fp_rb * (size_t)m : r_bytes);
+    const FpSlice fps{fp ? res + r_rec : nullptr, (int64_t)fp_rb, fp_mlo, fp_nml, fp_obase};
     bk.split_find(a, hist, m, TM_P(const int64_t, o_nho), TM_P(const int32_t, o_nnf), TM_P(const int32_t, o_nfo),
                   flist, TM_P(const float, o_par), TM_P(const int32_t, o_nmd), max_nf, (int32_t*)(res + r_feat),
                   (int32_t*)(res + r_bin), (float*)(res + r_gain), res + r_dl, (float*)(res + r_left),
-                  (float*)(res + r_tot), (int64_t*)(res + r_cl), use_subset ? -1 : split_n_multi);
+                  (float*)(res + r_tot), (int64_t*)(res + r_cl), use_subset ? -1 : split_n_multi, fps);
+    if (fp)   // all-gather the ranks' best splits, merge into this level's decisions (on-stream on the GPU)
+      bk.fp_exchange_merge(a, res + r_rec, m, fp_rb, (int32_t*)(res + r_feat), (int32_t*)(res + r_bin),
+                           (float*)(res + r_gain), res + r_dl, (float*)(res + r_left));
     if (BK::kGPU)   // partition in place of the node ranges, straight from the device decisions
       bk.partition_fused(a, rows, rows_alt, d1 + o_cit, (int)ncit, TM_P(const int64_t, o_nb),
                          TM_P(const int64_t, o_nc), (const int32_t*)(res + r_feat), (const int32_t*)(res + r_bin),

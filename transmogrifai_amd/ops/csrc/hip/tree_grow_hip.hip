@@ -3,7 +3,9 @@
 // device buffers kept across calls (stream-ordered hipMallocAsync when they grow), and the tmog_hip_* kernel launchers of
 // tree_kernels.hip. The only host<->device synchronisation is one result read per level and group.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -25,7 +27,9 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
                         const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
                         float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors, int n_multi,
-                        hipStream_t stream);
+                        void* rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase, hipStream_t stream);
+int tmog_hip_fp_merge(const void* recv, int R, int m, int64_t rec_bytes, int S, int32_t* out_feat, int32_t* out_bin,
+                      float* out_gain, uint8_t* out_dl, float* out_left, hipStream_t stream);
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
                            int64_t dense, int per, int S, hipStream_t stream);
 size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat);
@@ -62,6 +66,8 @@ struct GpuSlot {
   size_t cand_cap = 0;
   int32_t* feats = nullptr;
   int feats_n = 0;
+  uint8_t* fp_recv = nullptr;                 // feature-parallel: all-gathered split records
+  size_t fp_recv_cap = 0;
   uint8_t* hist[2] = {nullptr, nullptr};     // grow-only level histogram buffers (int64 words)
   size_t hist_cap[2] = {0, 0};
   int device = -1;
@@ -76,7 +82,8 @@ struct GpuBackend {
   static constexpr bool kGPU = true;
   GpuSlot& sl;
   const tmog::GrowArgs& a;
-  GpuBackend(GpuSlot& s, const tmog::GrowArgs& args) : sl(s), a(args) {}
+  int group;
+  GpuBackend(GpuSlot& s, const tmog::GrowArgs& args, int g) : sl(s), a(args), group(g) {}
 
   static void grow_dev(uint8_t*& p, size_t& cap, size_t need, hipStream_t s) {
     if (need <= cap) return;
@@ -156,11 +163,24 @@ struct GpuBackend {
   void split_find(const tmog::GrowArgs& g, const int64_t* hist, int m, const int64_t* nho, const int32_t* nnf,
                   const int32_t* nfo, const int32_t* flist, const float* params, const int32_t* nmd, int max_nf,
                   int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t* cursors,
-                  int n_multi) {
+                  int n_multi, const tmog::FpSlice& fps) {
     grow_dev(sl.cand, sl.cand_cap, tmog_hip_split_cand_bytes(m, max_nf), sl.stream);
     kchk(tmog_hip_split_find(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd,
-                             g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, cursors, n_multi, sl.stream),
+                             g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, cursors, n_multi, fps.rec,
+                             fps.rec_bytes, fps.mlo, fps.nml, fps.obase, sl.stream),
          "split_find");
+  }
+  // One RCCL all-gather of the level's split records over xGMI (this group's communicator, on the
+  // group's stream: no host round trip), then the merge kernel rewrites the decisions in place.
+  void fp_exchange_merge(const tmog::GrowArgs& g, const uint8_t* rec, int m, size_t rb, int32_t* feat, int32_t* bin,
+                         float* gain, uint8_t* dl, float* left) {
+    const size_t bytes = rb * (size_t)m;
+    grow_dev(sl.fp_recv, sl.fp_recv_cap, bytes * (size_t)g.fp_world, sl.stream);
+    ncclComm_t comm = (ncclComm_t)g.fp_comm[group];
+    const ncclResult_t r = ncclAllGather(rec, sl.fp_recv, bytes, ncclUint8, comm, sl.stream);
+    if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    kchk(tmog_hip_fp_merge(sl.fp_recv, g.fp_world, m, (int64_t)rb, g.S, feat, bin, gain, dl, left, sl.stream),
+         "fp_merge");
   }
   void partition_fused(const tmog::GrowArgs& g, const uint32_t* rows, uint32_t* rows_alt, const void* items, int n,
                        const int64_t* nb, const int64_t* nc, const int32_t* feat, const int32_t* bin, const uint8_t* dl,
@@ -190,6 +210,7 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
   res->groups.resize(ng);
   try {
     if (ng > (int)slots().size()) throw std::runtime_error("too many job groups");
+    if (a.fp_world > 0 && a.fp_comm == nullptr) throw std::runtime_error("feature-parallel growth needs communicators");
     int dev = 0;
     hchk(hipGetDevice(&dev), "hipGetDevice");
     hipStream_t base = (hipStream_t)a.stream;
@@ -210,7 +231,7 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
       th.emplace_back([&, g]() {
         try {
           hchk(hipSetDevice(dev), "hipSetDevice");
-          GpuBackend bk(slots()[g], a);
+          GpuBackend bk(slots()[g], a, g);
           tmog::grow_group(bk, a, g, res->groups[g]);
         } catch (const std::exception& e) {
           errs[g] = e.what();
@@ -250,5 +271,26 @@ void tmog_hip_grow_copy(void* h, int g, int64_t* tree, int64_t* feat, int64_t* b
   tmog::result_copy((tmog::GrowResult*)h, g, tree, feat, bin, dl, gain, tot, left, right);
 }
 void tmog_hip_grow_free(void* h) { delete (tmog::GrowResult*)h; }
+
+// RCCL communicators of the feature-parallel tree grower (one per job group; models/tree_engine.py
+// FeatureParallel creates them once per process: rank 0's unique id is broadcast through
+// torch.distributed, then every rank joins on its current device).
+int tmog_hip_rccl_unique_id(char* out, int cap) {
+  if (cap < (int)sizeof(ncclUniqueId)) return -2;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+  std::memcpy(out, &id, sizeof(id));
+  return (int)sizeof(id);
+}
+void* tmog_hip_rccl_comm_init(const char* id_bytes, int world, int rank) {
+  ncclUniqueId id;
+  std::memcpy(&id, id_bytes, sizeof(id));
+  ncclComm_t comm = nullptr;
+  if (ncclCommInitRank(&comm, world, id, rank) != ncclSuccess) return nullptr;
+  return (void*)comm;
+}
+int tmog_hip_rccl_comm_destroy(void* comm) {
+  return comm ? (int)ncclCommDestroy((ncclComm_t)comm) : 0;
+}
 
 }  // extern "C"

@@ -571,7 +571,8 @@ __global__ void __launch_bounds__(64) split_reduce_kernel(
     const int32_t* __restrict__ feat_list, int B, int S, int missing_bin, const int32_t* __restrict__ node_model,
     const double* __restrict__ qinv, int fbmax, const Best* __restrict__ cand, int32_t* __restrict__ out_feat,
     int32_t* __restrict__ out_bin, float* __restrict__ out_gain, uint8_t* __restrict__ out_dl,
-    float* __restrict__ out_left, float* __restrict__ out_total, unsigned long long* __restrict__ cursors) {
+    float* __restrict__ out_left, float* __restrict__ out_total, unsigned long long* __restrict__ cursors,
+    uint8_t* __restrict__ rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase) {
   const int j = blockIdx.x;
   const int lane = threadIdx.x;
   if (cursors && lane < 2) cursors[2 * j + lane] = 0;   // partition_fused_kernel's per-node slot cursors
@@ -609,8 +610,54 @@ __global__ void __launch_bounds__(64) split_reduce_kernel(
     if (lane == 0) {
       out_total[(int64_t)j * S + s] = (float)((double)t * qi[s]);
       out_left[(int64_t)j * S + s] = (float)((double)l * qi[s]);
+      if (rec) reinterpret_cast<float*>(rec + (int64_t)j * rec_bytes + 24)[s] = (float)((double)l * qi[s]);
     }
   }
+  if (rec && lane == 0) {   // feature-parallel split record (common/tree_grow.hpp fp_rec_bytes)
+    uint8_t* r = rec + (int64_t)j * rec_bytes;
+    *reinterpret_cast<double*>(r) = found ? b.gain : -INFINITY;
+    reinterpret_cast<int32_t*>(r)[2] = found ? (b.f < fp_nml ? fp_mlo + b.f : fp_obase + (b.f - fp_nml)) : 0x7fffffff;
+    reinterpret_cast<int32_t*>(r)[3] = found ? b.b : -1;
+    reinterpret_cast<int32_t*>(r)[4] = found ? b.dl : 0;
+    reinterpret_cast<int32_t*>(r)[5] = found ? feat_list[node_feat_off[j] + b.f] : -1;
+  }
+}
+
+// Feature-parallel merge: node j's decision is the best of the R ranks' records under the split scan's
+// order (gain, then lowest full-list position, dl, bin) -- the candidate a single rank scanning every
+// feature would pick. Host twin: common/tree_grow.hpp fp_merge_host.
+__global__ void fp_merge_kernel(const uint8_t* __restrict__ recv, int R, int m, int64_t rb, int S,
+                                int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin,
+                                float* __restrict__ out_gain, uint8_t* __restrict__ out_dl,
+                                float* __restrict__ out_left) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  int w = -1;
+  Best best{-INFINITY, 0x7fffffff, 0, 0};
+  for (int r = 0; r < R; ++r) {
+    const uint8_t* p = recv + ((int64_t)r * m + j) * rb;
+    const int32_t* pi = reinterpret_cast<const int32_t*>(p);
+    const Best c{*reinterpret_cast<const double*>(p), pi[2], pi[3], pi[4]};
+    if (c.f == 0x7fffffff) continue;
+    if (w < 0 || better(c, best)) {
+      w = r;
+      best = c;
+    }
+  }
+  if (w < 0) {
+    out_feat[j] = -1;
+    out_bin[j] = -1;
+    out_gain[j] = -INFINITY;
+    out_dl[j] = 0;
+    for (int s = 0; s < S; ++s) out_left[(int64_t)j * S + s] = 0.f;
+    return;
+  }
+  const uint8_t* p = recv + ((int64_t)w * m + j) * rb;
+  out_feat[j] = reinterpret_cast<const int32_t*>(p)[5];
+  out_bin[j] = best.b;
+  out_gain[j] = (float)best.gain;
+  out_dl[j] = (uint8_t)best.dl;
+  for (int s = 0; s < S; ++s) out_left[(int64_t)j * S + s] = reinterpret_cast<const float*>(p + 24)[s];
 }
 
 // ----------------------------------------------------------------------------------- partition
@@ -922,7 +969,8 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
                         const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
                         float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors,
-                        int n_multi, hipStream_t stream) {
+                        int n_multi, void* rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase,
+                        hipStream_t stream) {
   if (n_nodes == 0) return 0;
   if (S > TM_MAX_S || B > 64) return -2;
   if (n_multi > max_nfeat) n_multi = -1;
@@ -941,7 +989,16 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
 #undef TM_SPLIT
   hipLaunchKernelGGL(split_reduce_kernel, dim3(n_nodes), dim3(64), 0, stream, hist, node_hist_off, node_feat_off,
                      feat_list, B, S, missing_bin, node_model, qinv, fbmax, cand, out_feat, out_bin, out_gain, out_dl,
-                     out_left, out_total, (unsigned long long*)cursors);
+                     out_left, out_total, (unsigned long long*)cursors, (uint8_t*)rec, rec_bytes, fp_mlo, fp_nml,
+                     fp_obase);
+  return (int)hipGetLastError();
+}
+
+int tmog_hip_fp_merge(const void* recv, int R, int m, int64_t rec_bytes, int S, int32_t* out_feat, int32_t* out_bin,
+                      float* out_gain, uint8_t* out_dl, float* out_left, hipStream_t stream) {
+  if (m == 0) return 0;
+  hipLaunchKernelGGL(fp_merge_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, (const uint8_t*)recv, R, m,
+                     rec_bytes, S, out_feat, out_bin, out_gain, out_dl, out_left);
   return (int)hipGetLastError();
 }
 

@@ -108,7 +108,8 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
                         const double* qinv, int32_t* out_feat, int32_t* out_bin, float* out_gain,
-                        uint8_t* out_default_left, float* out_left, float* out_total) {
+                        uint8_t* out_default_left, float* out_left, float* out_total, uint8_t* rec,
+                        int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase) {
 #pragma omp parallel for schedule(dynamic, 4)
   for (int j = 0; j < n_nodes; ++j) {
     const int64_t* h = hist + node_hist_off[j];
@@ -131,7 +132,7 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
     const double pimp = impurity(tot, S, kind, &tcount);
     const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
     double best = -INFINITY;
-    int bf = -1, bb = -1, bdl = 0;
+    int bf = -1, bb = -1, bdl = 0, bfi = -1;
     int64_t bleft[16] = {0};
     for (int f = 0; f < nf; ++f) {
       const int gf = fl[f];
@@ -166,7 +167,7 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
             if (gain < min_gain) continue;
           }
           if (gain > best) {
-            best = gain; bf = gf; bb = b; bdl = dl;
+            best = gain; bf = gf; bb = b; bdl = dl; bfi = f;
             for (int s = 0; s < S; ++s) bleft[s] = lq[s];
           }
         }
@@ -177,6 +178,15 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
     out_gain[j] = bf >= 0 ? (float)best : -INFINITY;
     out_default_left[j] = (uint8_t)bdl;
     for (int s = 0; s < S; ++s) out_left[(int64_t)j * S + s] = (float)((double)bleft[s] * q[s]);
+    if (rec) {   // feature-parallel split record (common/tree_grow.hpp fp_rec_bytes)
+      uint8_t* r = rec + (int64_t)j * rec_bytes;
+      const double g = bf >= 0 ? best : -INFINITY;
+      const int32_t fpos = bf >= 0 ? (bfi < fp_nml ? fp_mlo + bfi : fp_obase + (bfi - fp_nml)) : 0x7fffffff;
+      const int32_t vals[4] = {fpos, bb, bdl, bf};
+      std::memcpy(r, &g, 8);
+      std::memcpy(r + 8, vals, 16);
+      std::memcpy(r + 24, out_left + (int64_t)j * S, 4 * (size_t)S);
+    }
   }
   return 0;
 }

@@ -19,7 +19,8 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
                         const double* qinv, int32_t* out_feat, int32_t* out_bin, float* out_gain,
-                        uint8_t* out_default_left, float* out_left, float* out_total);
+                        uint8_t* out_default_left, float* out_left, float* out_total, uint8_t* rec,
+                        int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase);
 int tmog_partition_cpu(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, int n_nodes,
                        const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                        const int32_t* split_bin, const uint8_t* default_left, int missing_bin,
@@ -30,6 +31,8 @@ namespace {
 
 struct CpuBackend {
   static constexpr bool kGPU = false;
+  int group = 0;
+  std::vector<uint8_t> fp_recv;
   std::vector<int32_t> feats;
   std::vector<uint8_t> res;
   std::vector<int64_t> hist[2];
@@ -69,9 +72,20 @@ struct CpuBackend {
   }
   void split_find(const tmog::GrowArgs& g, const int64_t* hist, int m, const int64_t* nho, const int32_t* nnf,
                   const int32_t* nfo, const int32_t* flist, const float* params, const int32_t* nmd, int,
-                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t*, int) {
+                  int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t*, int,
+                  const tmog::FpSlice& fps) {
     tmog_split_find_cpu(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd, g.qinv,
-                        feat, bin, gain, dl, left, tot);
+                        feat, bin, gain, dl, left, tot, fps.rec, fps.rec_bytes, fps.mlo, fps.nml, fps.obase);
+  }
+  // all-gather through the caller's exchange function (torch.distributed gloo in the CPU tests)
+  void fp_exchange_merge(const tmog::GrowArgs& g, const uint8_t* rec, int m, size_t rb, int32_t* feat, int32_t* bin,
+                         float* gain, uint8_t* dl, float* left) {
+    const size_t bytes = rb * (size_t)m;
+    fp_recv.assign(bytes * (size_t)g.fp_world, 0);
+    if (g.fp_exchange == nullptr) throw std::runtime_error("feature-parallel growth needs an exchange function");
+    if (g.fp_exchange(g.fp_ctx, group, rec, fp_recv.data(), (int64_t)bytes) != 0)
+      throw std::runtime_error("feature-parallel exchange failed");
+    tmog::fp_merge_host(fp_recv.data(), g.fp_world, m, rb, g.S, feat, bin, gain, dl, left);
   }
   void partition_fused(const tmog::GrowArgs&, const uint32_t*, uint32_t*, const void*, int, const int64_t*,
                        const int64_t*, const int32_t*, const int32_t*, const uint8_t*, const float*, const float*,
@@ -103,6 +117,7 @@ void* tmog_grow_forest_cpu(const tmog::GrowArgs* args) {
   try {
     for (int g = 0; g < args->n_groups; ++g) {
       CpuBackend bk;
+      bk.group = g;
       tmog::grow_group(bk, *args, g, res->groups[g]);
     }
   } catch (const std::exception& e) {

@@ -128,7 +128,15 @@ class ModelSelector(BinaryEstimator):
         else:
             rows = None
             job = FitJob(params)
-        state = learner.fit_batch(X, y, [job], context=ctx)[0]
+        # the winner's refit uses the same intra-job parallelism over the ranks as its CV fits
+        from ..parallel import dist as D
+        if D.world() > 1 and learner.parallel in ("rows", "features"):
+            from ..parallel.learner_parallel import LearnerParallel
+            ctx["par"] = LearnerParallel()
+        try:
+            state = learner.fit_batch(X, y, [job], context=ctx)[0]
+        finally:
+            ctx.pop("par", None)
         # training evaluation on the prepared data
         Xr = X if rows is None else X[rows]
         yr = y if rows is None else y[rows]

@@ -113,31 +113,54 @@ class OpValidator:
             for gi, p in enumerate(grid):
                 for k in range(len(splits)):
                     jobs.append((li, gi, k))
+        world, me = D.world(), D.rank()
+        # Learners with an intra-job parallel mode (linear: row-parallel; boosted / single trees:
+        # feature-parallel) run every one of their jobs on every rank with the parallel context
+        # (parallel/learner_parallel.py); the others' (grid x fold) jobs are sharded whole over the ranks
+        # by estimated cost (LPT).
+        par = None
+        if world > 1:
+            from ..parallel.learner_parallel import LearnerParallel
+            par = LearnerParallel()
+        spread = {li for li, (lname, _) in enumerate(models)
+                  if par is not None and learner_class(lname).parallel in ("rows", "features")}
         n_tr = max(1, int(train_rows[0][0].numel())) if train_rows else 1
-        costs = [_job_cost(models[li][0], models[li][1][gi], n_tr, X.shape[1]) for li, gi, k in jobs]
-        owner = D.lpt_assign(costs, D.world())
-        me = D.rank()
+        sharded = [j for j, (li, gi, k) in enumerate(jobs) if li not in spread]
+        costs = [_job_cost(models[jobs[j][0]][0], models[jobs[j][0]][1][jobs[j][1]], n_tr, X.shape[1])
+                 for j in sharded]
+        owner = [me] * len(jobs)
+        for j, w in zip(sharded, D.lpt_assign(costs, world)):
+            owner[j] = w
         ctx = context if context is not None else {}
         results: Dict[Tuple[int, int, int], float] = {}
         failures = []
         timings = {}
-        for li, (lname, grid) in enumerate(models):
+        # spread learners first (all ranks in lockstep through their collectives), then the shards
+        order = sorted(range(len(models)), key=lambda li: (li not in spread, li))
+        for li in order:
+            lname, grid = models[li]
             mine = [(j, (l, g, k)) for j, (l, g, k) in enumerate(jobs) if l == li and owner[j] == me]
             if not mine:
                 continue
+            # maxWait (OpValidator.scala:348, default 1 day): learners not started in time are dropped;
+            # spread learners take rank 0's decision so every rank skips the same collectives
+            late = time.time() - t0 > self.max_wait
+            if li in spread:
+                late = bool(D.broadcast_object(late, 0))
+            if late:
+                failures.append(f"{lname}: not started within maxWait={self.max_wait}s")
+                continue
             t1 = time.time()
-            learner = learner_class(lname)()
-            fjobs = [FitJob(dict(learner.defaults, **grid[g]), train_rows[k][0], train_rows[k][1])
-                     for _, (_, g, k) in mine]
+            # the context dict is shared (tree binning cache) -- the parallel context is set only
+            # around the spread learners
+            if li in spread:
+                ctx["par"] = par
             try:
-                states = learner.fit_batch(X, y, fjobs, context=ctx)
-                preds = learner.predict_batch(states, X, [val_rows[k] for _, (_, g, k) in mine], context=ctx)
-                for (j, (l, g, k)), (pred, raw, prob) in zip(mine, preds):
-                    yv = y[val_rows[k]]
-                    results[(l, g, k)] = float(self.evaluator.selection_metric(yv, pred, raw, prob))
-            except Exception as e:  # failed models are dropped, as in OpValidator.getSummary
-                log.warning("Model %s failed in model selector: %r", lname, e)
-                failures.append(f"{lname}: {e!r}")
+                res, fails = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, ctx)
+            finally:
+                ctx.pop("par", None)
+            results.update(res)
+            failures.extend(fails)
             timings[lname] = time.time() - t1
         # exchange metrics between ranks
         gathered = D.all_gather_object((results, failures, timings))
@@ -145,10 +168,47 @@ class OpValidator:
         allfail: List[str] = []
         for r, f, tm in gathered:
             allres.update(r)
-            allfail.extend(f)
+            for x in f:
+                if x not in allfail:
+                    allfail.append(x)
             for k, v in tm.items():
                 timings[k] = max(timings.get(k, 0.0), v)
         return self._select(models, allres, len(splits), allfail, timings, t0)
+
+    def _fit_eval(self, lname, grid, mine, X, y, train_rows, val_rows, ctx):
+        """Fit + score one learner's jobs as one batch. A failing batch is retried one grid point at a
+        time, so only the failing (estimator, ParamMap) fits are dropped, as the reference's per-fit
+        ``Future.recover`` does (OpValidator.scala:318-328)."""
+        results: Dict[Tuple[int, int, int], float] = {}
+        failures: List[str] = []
+
+        def run(batch):
+            learner = learner_class(lname)()
+            fjobs = [FitJob(dict(learner.defaults, **grid[g]), train_rows[k][0], train_rows[k][1])
+                     for _, (_, g, k) in batch]
+            states = learner.fit_batch(X, y, fjobs, context=ctx)
+            preds = learner.predict_batch(states, X, [val_rows[k] for _, (_, g, k) in batch], context=ctx)
+            out = {}
+            for (j, (l, g, k)), (pred, raw, prob) in zip(batch, preds):
+                yv = y[val_rows[k]]
+                out[(l, g, k)] = float(self.evaluator.selection_metric(yv, pred, raw, prob))
+            return out
+
+        try:
+            results.update(run(mine))
+            return results, failures
+        except Exception as e:
+            log.warning("Model %s failed in model selector as a batch (%r); retrying per grid point", lname, e)
+        by_grid: Dict[int, list] = {}
+        for item in mine:
+            by_grid.setdefault(item[1][1], []).append(item)
+        for g, batch in sorted(by_grid.items()):
+            try:
+                results.update(run(batch))
+            except Exception as e:  # failed models are dropped, as in OpValidator.getSummary
+                log.warning("Model %s with %s failed in model selector: %r", lname, grid[g], e)
+                failures.append(f"{lname} {grid[g]}: {e!r}")
+        return results, failures
 
     def _select(self, models, results, n_folds, failures, timings, t0) -> ValidationResult:
         larger = self.evaluator.is_larger_better
@@ -174,7 +234,8 @@ class OpValidator:
                 if better and not math.isnan(m):
                     best = (lname, dict(grid[gi]), m)
         if best is None:
-            raise RuntimeError("All models failed model selector! Models tried were: " +
+            raise RuntimeError("All models failed model selector or failed to finish within maxWait! "
+                               "Models tried were: " +
                                ", ".join(f"{m[0]} -> {len(m[1])} grid points" for m in models) +
                                (f"; failures: {failures}" if failures else ""))
         timings["total"] = time.time() - t0
