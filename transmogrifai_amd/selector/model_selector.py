@@ -74,6 +74,21 @@ class ModelSelector(BinaryEstimator):
         self.models = [(n, [dict(g) for g in grid]) for n, grid in models]
         self.evaluators = list(evaluators)
         self.best: Optional[Any] = None
+        self.best_estimator: Optional[Any] = None    # set by workflow-level CV (find_best_estimator)
+
+    def find_best_estimator(self, data, during) -> Any:
+        """Workflow-level CV (``ModelSelector.findBestEstimator``, ModelSelector.scala:116-128): validate
+        with the ``during`` DAG refit per fold; ``fit`` then refits the chosen learner without
+        re-validating."""
+        from ..parallel import dp
+        label, vec = self._inputs[0].name, self._inputs[1].name
+        if self.splitter is not None:
+            self._split_summary = self.splitter.pre_validation_prepare(dp.rows(data[label].values))
+        if not during:
+            self.best_estimator = None
+            return None
+        self.best_estimator = self.validator.validate_with_dag(self.models, data, label, vec, during, self.splitter)
+        return self.best_estimator
 
     # Row-sharded fits: the splitter's global statistics come from one label gather, then every rank
     # contributes the rows that any CV fold or the refit samples (masks are functions of the global
@@ -89,7 +104,10 @@ class ModelSelector(BinaryEstimator):
         t0 = time.time()
         split_summary = None
         if self.splitter is not None:
-            split_summary = self.splitter.pre_validation_prepare(dp.rows(y))
+            if self.best_estimator is not None and getattr(self, "_split_summary", None) is not None:
+                split_summary = self._split_summary
+            else:
+                split_summary = self.splitter.pre_validation_prepare(dp.rows(y))
         if dp.active():
             X, y, row_ids = self._gather_candidates(X, y, row_ids)
             with dp.local_only():
@@ -112,7 +130,10 @@ class ModelSelector(BinaryEstimator):
 
     def _fit(self, X, y, row_ids, split_summary, t0):
         ctx: Dict[str, Any] = {}
-        res = self.validator.validate(self.models, X, y, row_ids, self.splitter, context=ctx)
+        if self.best_estimator is not None:     # chosen by workflow-level CV
+            res = self.best_estimator
+        else:
+            res = self.validator.validate(self.models, X, y, row_ids, self.splitter, context=ctx)
         self.best = res
         # refit the winner on the prepared full training set
         learner = learner_class(res.best_learner)()

@@ -175,6 +175,59 @@ class OpValidator:
                 timings[k] = max(timings.get(k, 0.0), v)
         return self._select(models, allres, len(splits), allfail, timings, t0)
 
+    def validate_with_dag(self, models: Sequence[Tuple[str, Sequence[Dict]]], data, label_name: str,
+                          features_name: str, during, splitter: Optional[Splitter] = None) -> ValidationResult:
+        """Workflow-level CV (``OpCrossValidation.validate`` with a DAG, OpCrossValidation.scala:105-132, and
+        ``OpValidator.applyDAG``, OpValidator.scala:250-274): for every fold a fresh copy of the
+        label-dependent ``during`` stages (SanityChecker, label-aware bucketizers, ...) is fitted on the
+        fold's training rows only, both fold parts are transformed by it, and every (learner x grid point)
+        is scored on that fold's own feature matrix -- so nothing the during stages learn from a fold's
+        validation labels can leak into its metric. ``data`` holds the inputs of the during stages."""
+        from ..parallel import dp
+        from ..workflow.dag import copy_dag, fit_and_transform_dag
+        t0 = time.time()
+        row_ids = data.row_ids
+        y_all = data[label_name].values
+        splits = self.make_splits(row_ids, y_all)
+        results: Dict[Tuple[int, int, int], float] = {}
+        failures: List[str] = []
+        timings: Dict[str, float] = {}
+        for k, (tr, va) in enumerate(splits):
+            ti = torch.nonzero(tr).reshape(-1)
+            vi = torch.nonzero(va).reshape(-1)
+            t1 = time.time()
+            train_k, val_k, _ = fit_and_transform_dag(copy_dag(during), data.take(ti), data.take(vi))
+            timings[f"fold{k}:dag"] = time.time() - t1
+            Xt, yt = train_k[features_name].values, train_k[label_name].values
+            Xv, yv = val_k[features_name].values, val_k[label_name].values
+            rid_t = train_k.row_ids.to(Xt.device)
+            if dp.active():       # row-sharded: learners train on the fold rows of every rank
+                Xt, yt, rid_t, Xv, yv = dp.rows(Xt), dp.rows(yt), dp.rows(rid_t), dp.rows(Xv), dp.rows(yv)
+            X = torch.cat([Xt, Xv.to(Xt.dtype)])
+            y = torch.cat([yt, yv]).to(X.dtype)
+            nt = int(Xt.shape[0])
+            keep = torch.arange(nt, device=X.device)
+            weights = None
+            if splitter is not None:
+                if hasattr(splitter, "weights"):
+                    w = splitter.weights(rid_t, yt.to(X.dtype), stream=11 + k)
+                    keep = torch.nonzero(w > 0).reshape(-1)
+                    weights = w[keep]
+                else:
+                    keep = torch.nonzero(splitter.validation_prepare(rid_t, yt.to(X.dtype), stream=11 + k)).reshape(-1)
+            train_rows = {0: (keep, weights)}
+            val_rows = {0: torch.arange(nt, int(X.shape[0]), device=X.device)}
+            ctx: Dict[str, Any] = {}
+            with dp.local_only():
+                for li, (lname, grid) in enumerate(models):
+                    t2 = time.time()
+                    mine = [(gi, (li, gi, 0)) for gi in range(len(grid))]
+                    res, fails = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, ctx)
+                    results.update({(l, g, k): v for (l, g, _), v in res.items()})
+                    failures.extend(fails)
+                    timings[lname] = timings.get(lname, 0.0) + time.time() - t2
+        return self._select(models, results, len(splits), failures, timings, t0)
+
     def _fit_eval(self, lname, grid, mine, X, y, train_rows, val_rows, ctx):
         """Fit + score one learner's jobs as one batch. A failing batch is retried one grid point at a
         time, so only the failing (estimator, ParamMap) fits are dropped, as the reference's per-fit

@@ -131,3 +131,20 @@ def cut_dag(dag: Sequence[Layer]):
     flat = {id(st) for layer in during for st, _ in layer}
     before2 = [[(st, d) for st, d in layer if id(st) not in flat] for layer in non_ms]
     return ms, [l for l in before2 if l], during, after
+
+
+def copy_dag(dag: Sequence[Layer]) -> List[Layer]:
+    """Fresh stage copies of a DAG (``stage.copy(ParamMap.empty)`` per fold in OpCrossValidation.scala:
+    107-112): same uid, inputs and params, private params / metadata, so fitting a copy never
+    touches the workflow's own stages."""
+    import copy
+    out = []
+    for layer in dag:
+        nl = []
+        for st, d in layer:
+            c = copy.copy(st)
+            c.params = dict(getattr(st, "params", {}))
+            c.metadata = copy.deepcopy(getattr(st, "metadata", {}))
+            nl.append((c, d))
+        out.append(nl)
+    return out

@@ -249,8 +249,10 @@ class OpWorkflow(OpWorkflowCore):
                 tr2, te2, fb = fit_and_transform_dag(before, train, test, stage_t)
             fitted = list(fb)
             if ms is not None:
+                # OpWorkflow.scala:403-453: validate with the during-DAG refit inside every fold, then fit
+                # the during stages on the whole training split and refit the selected model on their output
                 with _Timer(timings, OpStep.CrossValidation):
-                    ms.during_dag = during
+                    ms.find_best_estimator(tr2, during)
                 rest = list(during) + [[(ms, 0)]] + list(after)
                 with _Timer(timings, OpStep.FeatureEngineering):
                     _, _, fr = fit_and_transform_dag(rest, tr2, te2, stage_t)
