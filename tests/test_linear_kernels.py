@@ -25,7 +25,8 @@ def _reference(X, y, W, V, b, loss, yscale):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,d,P", [(1000, 7, 1), (4099, 33, 24), (20011, 329, 24), (3001, 384, 40), (777, 256, 3), (50000, 130, 8)])
+@pytest.mark.parametrize("N,d,P", [(1000, 7, 1), (4099, 33, 24), (20011, 329, 24), (3001, 384, 40), (777, 256, 3),
+                                   (50000, 130, 8), (5003, 600, 24), (3001, 1500, 8), (2000, 2048, 33)])
 @pytest.mark.parametrize("loss", ["logistic", "hinge", "squared"])
 def test_fused_objective_matches_fp64(N, d, P, loss):
     g = torch.Generator().manual_seed(N + d + P)

@@ -367,13 +367,18 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     Nrows, F = int(Xb.shape[0]), int(Xb.shape[1])
     chunk_rows = int(os.environ.get("TMOG_TREE_CHUNK", chunk_rows))
     if Nrows >= MAX_ROWS:
-        raise ValueError(f"tree engine supports < {MAX_ROWS} rows per training set, got {Nrows}")
+        # packed row entries carry a 24-bit row id (row | weight << 24): the model selector's
+        # maxTrainingSample (1M by default, Splitter.scala:178) keeps training sets far below this
+        raise ValueError(f"tree engine supports < {MAX_ROWS} (2^24) rows per training set, got {Nrows}: lower "
+                         f"maxTrainingSample or subsample before fitting tree models")
     S = n_classes if mode == MODE_CLS else (3 if mode == MODE_VAR else 2)
     K = n_classes if mode == MODE_CLS else 1
     if missing_bin >= B:
         raise ValueError("missing_bin must be < B")
-    if S > 16:
-        raise ValueError("tree engine supports at most 16 statistics per bin (classes)")
+    if S > 256:
+        raise ValueError("tree engine supports at most 256 statistics per bin (classes)")
+    if on_gpu and (S > 16 or B > 64) and B * S > 16384:
+        raise ValueError(f"tree engine (GPU) supports bins x classes <= 16384, got {B} x {S}")
     n_bins_t = _const_tensor(np.asarray(n_bins, np.int32), dev)
     stride = int(t1.shape[1]) if (t1 is not None and t1.dim() == 2) else 0
     yf = y.to(device=dev, dtype=torch.float32).contiguous() if y is not None else None

@@ -56,7 +56,8 @@ _HOST_SIGS = {
 }
 
 _HIP_SIGS = {
-    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P, P, P],
+    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P, P, I32, P],
+    "tmog_hip_hist_stat_chunk": [I32, I32],
     "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
     "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P, I32, P,
                             I64, I32, I32, I32, P],
@@ -77,6 +78,7 @@ _HIP_SIGS = {
     "tmog_hip_poisson_pack": [P, I64, P, I32, P, I32, P, P, P, P],
     "tmog_hip_row_uniform": [P, I64, P, I32, P, P],
     "tmog_hip_lr_objective": [P, I64, I32, P, P, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P],
+    "tmog_hip_lr_epilogue_grad": [P, I64, I32, P, P, P, I32, I32, I32, P, I32, P, I32, P, P, P, I32, P],
     "tmog_hip_forest_predict": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P],
     "tmog_hip_col_stats": [P, P, I64, I32, I64, P, P],
     "tmog_hip_vectorize_numeric": [P, P, P, I64, I32, P, P, P, P, I64, I32, P],
@@ -93,7 +95,7 @@ _HIP_SIGS = {
 _RESTYPES = {"tmog_tree_finalize_cpu": C.c_int64, "tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
              "tmog_shist_flush": None, "tmog_shist_merge": None, "tmog_shist_bins": None,
              "tmog_shist_size": C.c_int64, "tmog_shist_sum": C.c_double,
-             "tmog_hip_split_cand_bytes": C.c_size_t, "tmog_hip_rccl_comm_init": C.c_void_p,
+             "tmog_hip_split_cand_bytes": C.c_size_t,  # (n_nodes, max_nfeat, B, S) "tmog_hip_rccl_comm_init": C.c_void_p,
              "tmog_grow_forest_cpu": C.c_void_p, "tmog_hip_grow_forest": C.c_void_p,
              "tmog_grow_nodes_cpu": C.c_int64, "tmog_hip_grow_nodes": C.c_int64,
              "tmog_grow_leaf_count_cpu": C.c_int64, "tmog_hip_grow_leaf_count": C.c_int64,

@@ -336,6 +336,11 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     full_groups = equal_groups(F);
   }
   const int F_use = perm_feats.empty() ? F : (int)perm_feats.size();
+  // GPU histogram items accumulate a chunk of the statistics when a B x S table exceeds the LDS (many
+  // classes / wide bins): one item per chunk, each writing disjoint words of the node histogram
+  const int stat_sc = bk.stat_chunk(B, S);
+  const int n_sc = (S + stat_sc - 1) / stat_sc;
+  if (n_sc > 256) throw std::runtime_error("too many statistic chunks (classes x bins too large)");
   const int fp_mlo = fp ? a.fp_mlo : 0;
   const size_t fp_rb = fp_rec_bytes(S);
   for (int depth = 0; depth <= max_depth; ++depth) {
@@ -461,17 +466,19 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
       for (const FeatGroup& fgp : grp) {
         const int64_t step = fgp.csr ? kCsrRows : a.chunk_rows;
         const int64_t nit = fgp.csr ? ncsr : nch;
-        for (int64_t c = 0; c < nit; ++c) {
-          HistItemH h;
-          h.node = j;
-          h.fg0 = fgp.f0;
-          h.nf = fgp.nf;
-          h.excl = (nit == 1 ? 1 : 0) | (fgp.reg ? 2 : 0) | (fgp.csr ? 4 : 0) |
-                   ((fgp.reg || fgp.csr) && live_dense >= 0 ? 8 : 0);
-          h.begin = nb[j] + c * step;
-          h.count = std::min(step, cnt - c * step);
-          hitems.push_back(h);
-        }
+        const int nchunk = (fgp.csr || fgp.reg) ? 1 : n_sc;
+        for (int sc = 0; sc < nchunk; ++sc)
+          for (int64_t c = 0; c < nit; ++c) {
+            HistItemH h;
+            h.node = j;
+            h.fg0 = fgp.f0;
+            h.nf = fgp.nf;
+            h.excl = (nit == 1 ? 1 : 0) | (fgp.reg ? 2 : 0) | (fgp.csr ? 4 : 0) |
+                     ((fgp.reg || fgp.csr) && live_dense >= 0 ? 8 : 0) | (sc << 8);
+            h.begin = nb[j] + c * step;
+            h.count = std::min(step, cnt - c * step);
+            hitems.push_back(h);
+          }
       }
     }
     std::vector<int64_t> d_soff, d_ooff, d_size;
@@ -506,7 +513,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
                   TM_P(const int32_t, o_nfo), flist, TM_P(const int32_t, o_nmd), TM_P(const int64_t, o_nho), hist,
                   (int)b_nb.size(), TM_P(const int64_t, o_bnb), TM_P(const int64_t, o_bnc),
                   TM_P(const int32_t, o_bnfo), TM_P(const int32_t, o_bnnf), TM_P(const int32_t, o_bnmd),
-                  TM_P(const int64_t, o_bnho));
+                  TM_P(const int64_t, o_bnho), stat_sc);
     if (!d_big.empty())
       bk.hist_subtract(hist, prev_hist, TM_P(const int64_t, o_dp), TM_P(const int64_t, o_ds),
                        TM_P(const int64_t, o_do), TM_P(const int64_t, o_dz), (int)d_big.size(), d_max, live_dense,

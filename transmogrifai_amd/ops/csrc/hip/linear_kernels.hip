@@ -216,9 +216,118 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
   }
 }
 
+// Wide-d variant (384 < d <= 2048; the LDS cannot hold a 64-row tile and V): the margins come from a
+// library GEMM (M = X V on hipBLASLt) and this kernel fuses everything after it -- loss, dl/dm, the
+// weighted sums and G += X_tile^T R on the matrix cores -- reading every X element exactly once, straight
+// from global memory (one coalesced 64-byte row segment per lane group and MFMA operand; the GB
+// output blocks of a wave keep that many loads in flight). Output partials as lr_objective_kernel.
+template <bool GRAD, int GB>
+__global__ void __launch_bounds__(NT) lr_epilogue_grad_kernel(
+    const float* __restrict__ X, int64_t N, int d, const float* __restrict__ M, const float* __restrict__ y,
+    const float* __restrict__ W, int ldw, int wcol0, int P, const float* __restrict__ bias, int loss,
+    const float* __restrict__ yscale, double* __restrict__ f_part, double* __restrict__ r_part,
+    float* __restrict__ G_part, int dpad) {
+  __shared__ float Rs[TM * PC];
+  __shared__ double sfr[2 * NT];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  const int nob = 2 * ((d + 15) >> 4);
+  f32x4 gacc[GB];
+#pragma unroll
+  for (int i = 0; i < GB; ++i) gacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  double f_acc = 0.0, r_acc = 0.0;
+  // epilogue mapping: thread -> problem column pe, rows re, re + 16, re + 32, re + 48
+  const int pe = threadIdx.x & (PC - 1), re = threadIdx.x >> 5;
+  const float be = bias[pe];
+  const float yse = yscale ? yscale[pe] : 1.f;
+  const int64_t ntiles = (N + TM - 1) / TM;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t r0 = tile * TM;
+    const int nrows = (int)min((int64_t)TM, N - r0);
+#pragma unroll
+    for (int k = 0; k < TM / 16; ++k) {
+      const int row = re + 16 * k;
+      float rv = 0.f;
+      if (row < nrows && pe < P) {
+        const int64_t gr = r0 + row;
+        const float w = W[gr * ldw + wcol0 + pe];
+        float l, g;
+        loss_and_grad(loss, M[gr * PC + pe] + be, y[gr], yse, &l, &g);
+        f_acc += (double)(l * w);
+        rv = g * w;
+        r_acc += (double)rv;
+      }
+      Rs[row * PC + pe] = rv;
+    }
+    if (GRAD) {
+      __syncthreads();
+#pragma unroll 2
+      for (int t = 0; t < TM / 4; ++t) {
+        const int row = 4 * t + q;
+        const float rv0 = Rs[row * PC + c], rv1 = Rs[row * PC + 16 + c];
+        const float* xr = X + (r0 + min(row, nrows - 1)) * (int64_t)d;   // rows past nrows have R = 0
+#pragma unroll
+        for (int i = 0; i < GB; ++i) {
+          const int ob = wave + 8 * i;
+          if (ob < nob) {
+            const int col = 16 * (ob >> 1) + c;
+            const float xv = col < d ? xr[col] : 0.f;
+            gacc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv, (ob & 1) ? rv1 : rv0, gacc[i], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();          // Rs is rewritten by the next tile
+  }
+  if (GRAD) {
+    float* gp = G_part + (int64_t)blockIdx.x * dpad * PC;
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int ob = wave + 8 * i;
+      if (ob < nob) {
+        const int db = ob >> 1, pbb = ob & 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gp[(int64_t)(16 * db + 4 * q + j) * PC + 16 * pbb + c] = gacc[i][j];
+      }
+    }
+  }
+  sfr[threadIdx.x] = f_acc;
+  sfr[NT + threadIdx.x] = r_acc;
+  __syncthreads();
+  if (threadIdx.x < PC) {
+    double fs = 0.0, rs = 0.0;
+    for (int k = 0; k < NT / PC; ++k) {        // threads sharing problem column pe (fixed order)
+      fs += sfr[k * PC + threadIdx.x];
+      rs += sfr[NT + k * PC + threadIdx.x];
+    }
+    f_part[(int64_t)blockIdx.x * PC + threadIdx.x] = fs;
+    r_part[(int64_t)blockIdx.x * PC + threadIdx.x] = rs;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// Wide-d objective tail: M [N][32] fp32 = X V (from a library GEMM, without bias); same outputs as
+// tmog_hip_lr_objective. d <= 2048.
+int tmog_hip_lr_epilogue_grad(const float* X, int64_t N, int d, const float* M, const float* y, const float* W,
+                              int ldw, int wcol0, int P, const float* bias, int loss, const float* yscale, int grad,
+                              double* f_part, double* r_part, float* G_part, int nblk, hipStream_t stream) {
+  if (d < 1 || d > 2048 || P > PC || P < 1 || nblk < 1) return -2;
+  const int dpad = ((d + 15) / 16) * 16;
+  const int nob = 2 * ((d + 15) / 16);
+#define TM_LRE(G, GB)                                                                                       \
+  hipLaunchKernelGGL((lr_epilogue_grad_kernel<G, GB>), dim3(nblk), dim3(NT), 0, stream, X, N, d, M, y, W, ldw, \
+                     wcol0, P, bias, loss, yscale, f_part, r_part, G_part, dpad)
+  if (!grad) TM_LRE(false, 1);
+  else if (nob <= 8 * 8) TM_LRE(true, 8);
+  else if (nob <= 8 * 16) TM_LRE(true, 16);
+  else TM_LRE(true, 32);
+#undef TM_LRE
+  return (int)hipGetLastError();
+}
+
 
 // Weighted loss sums f[p] = sum_i W[i,p] l(m_ip), r[p] = sum_i W[i,p] l'(m_ip) and (grad != 0)
 // G[:, p] = sum_i X[i,:] W[i,p] l'(m_ip), with m = X V + bias, for up to 32 problems (columns

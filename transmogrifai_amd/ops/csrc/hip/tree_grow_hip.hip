@@ -18,7 +18,7 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
-                        const int64_t* csr_ptr, const uint16_t* csr_col, hipStream_t stream);
+                        const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, hipStream_t stream);
 int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
                            const int64_t* out_off, const int64_t* size, int n, int64_t max_size, int64_t dense,
                            int per, int S, hipStream_t stream);
@@ -32,7 +32,8 @@ int tmog_hip_fp_merge(const void* recv, int R, int m, int64_t rec_bytes, int S, 
                       float* out_gain, uint8_t* out_dl, float* out_left, hipStream_t stream);
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
                            int64_t dense, int per, int S, hipStream_t stream);
-size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat);
+size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat, int B, int S);
+int tmog_hip_hist_stat_chunk(int B, int S);
 int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, const void* items,
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                              const int32_t* split_bin, const uint8_t* dl, const float* node_params,
@@ -149,13 +150,14 @@ struct GpuBackend {
   }
   void hist_build(const tmog::GrowArgs& g, const uint32_t* rows, const void* items, int n_items, const int32_t* nfo,
                   const int32_t* flist, const int32_t* nmd, const int64_t* nho, int64_t* hist, int, const int64_t*,
-                  const int64_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*) {
+                  const int64_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*, int Sc) {
     if (n_items)
       kchk(tmog_hip_hist_build(g.Xb, g.F, rows, items, n_items, nfo, flist, nmd, nho, hist, g.B, g.mode, g.S, g.y,
                                g.t1, g.t2, g.stride, g.qscale, g.mode == 2 ? g.missing_bin : -1, g.csr_ptr,
-                               g.csr_col, sl.stream),
+                               g.csr_col, Sc, sl.stream),
            "hist_build");
   }
+  int stat_chunk(int B, int S) const { return tmog_hip_hist_stat_chunk(B, S); }
   void hist_subtract(int64_t* hist, const int64_t* prev, const int64_t* poff, const int64_t* soff,
                      const int64_t* ooff, const int64_t* size, int n, int64_t mx, int64_t dense, int per, int S) {
     kchk(tmog_hip_hist_subtract(hist, prev, poff, soff, ooff, size, n, mx, dense, per, S, sl.stream), "hist_subtract");
@@ -164,7 +166,7 @@ struct GpuBackend {
                   const int32_t* nfo, const int32_t* flist, const float* params, const int32_t* nmd, int max_nf,
                   int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t* cursors,
                   int n_multi, const tmog::FpSlice& fps) {
-    grow_dev(sl.cand, sl.cand_cap, tmog_hip_split_cand_bytes(m, max_nf), sl.stream);
+    grow_dev(sl.cand, sl.cand_cap, tmog_hip_split_cand_bytes(m, max_nf, g.B, g.S), sl.stream);
     kchk(tmog_hip_split_find(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd,
                              g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, cursors, n_multi, fps.rec,
                              fps.rec_bytes, fps.mlo, fps.nml, fps.obase, sl.stream),

@@ -19,7 +19,9 @@
 #include <stdint.h>
 #include <math.h>
 
-#define TM_MAX_S 16
+#define TM_MAX_S 16          // narrow split scan / staged-record path: S <= 16 statistics
+#define TM_WIDE_MAX_S 256    // wide path (many classes): statistic-chunked histograms, LDS split scan
+#define TM_WIDE_MAX_BS 16384 // wide split scan keeps one feature's B x S int64 histogram in LDS
 
 namespace {
 
@@ -70,16 +72,24 @@ __device__ __forceinline__ int4 stage_row(uint32_t e, int64_t model, int64_t str
   return s;
 }
 
+// Statistic chunk [s0, s0 + Sc) of a histogram item (Sc < S when B * S does not fit the LDS table:
+// many classes or wide bins -- each chunk is its own item, writing disjoint words).
 template <int MODE>
-__device__ __forceinline__ void add_row(int* my, int bin, int S, const int4& st) {
+__device__ __forceinline__ void add_row(int* my, int bin, int S, int s0, int Sc, const int4& st) {
   if (MODE == 0) {
-    atomicAdd(my + bin * S + st.z, st.y);
+    const int c = st.z - s0;
+    if (c >= 0 && c < Sc) atomicAdd(my + bin * Sc + c, st.y);
   } else if (MODE == 1) {
-    int* hb = my + bin * 3;
-    atomicAdd(hb, st.y); atomicAdd(hb + 1, st.z); atomicAdd(hb + 2, st.w);
+    int* hb = my + bin * Sc;
+    const int v[3] = {st.y, st.z, st.w};
+    for (int k = 0; k < Sc; ++k) atomicAdd(hb + k, v[s0 + k]);
   } else {
-    int* hb = my + bin * 2;
-    atomicAdd(hb, st.y); atomicAdd(hb + 1, st.z);
+    int* hb = my + bin * Sc;
+    if (Sc == 2) {
+      atomicAdd(hb, st.y); atomicAdd(hb + 1, st.z);
+    } else {
+      atomicAdd(hb, s0 ? st.z : st.y);
+    }
   }
 }
 
@@ -204,9 +214,11 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
     int B, int S, const float* __restrict__ y, const float* __restrict__ t1, const float* __restrict__ t2,
     int64_t stride, const float* __restrict__ qscale, int skip_bin, const int64_t* __restrict__ csr_ptr,
-    const uint16_t* __restrict__ csr_col) {
+    const uint16_t* __restrict__ csr_col, int Sc) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
   const HistItem it = items[blockIdx.x];
+  const int s0 = ((it.excl >> 8) & 0xFF) * Sc;   // statistic chunk of this item (excl bits 8..15)
+  const int sc = min(Sc, S - s0);
   if (MODE == 2 && (it.excl & 4)) {
     hist_csr_item(it, rows, node_model, node_hist_off, hist, B, S, t1, t2, stride, qscale, skip_bin, csr_ptr,
                   csr_col, lds);
@@ -214,7 +226,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   }
   const int FG = it.nf;
   const int R = 64 / FG;
-  const int rowstride = B * S + 1;            // padded feature row
+  const int rowstride = B * sc + 1;           // padded feature row (this item's statistic chunk)
   const int ncopy_words = R * FG * rowstride;  // <= 64 * rowstride
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -287,7 +299,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
       for (int u = 0; u < HIST_U; ++u) bin[u] = (int)Xb[(int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F + feat];
 #pragma unroll
       for (int u = 0; u < HIST_U; ++u)
-        if (active && j0 + u * R + rsub < nrows && bin[u] != skip_bin) add_row<MODE>(my, bin[u], S, st[u]);
+        if (active && j0 + u * R + rsub < nrows && bin[u] != skip_bin) add_row<MODE>(my, bin[u], S, s0, sc, st[u]);
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -334,14 +346,17 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     }
     return;
   }
-  // fold the R private copies and write the node histogram of this feature group
-  for (int k = threadIdx.x; k < words; k += blockDim.x) {
-    const int f = k / (B * S);
-    const int rem = k - f * (B * S);
+  // fold the R private copies and write the node histogram of this feature group (chunk slots only)
+  const int cwords = FG * B * sc;
+  for (int k = threadIdx.x; k < cwords; k += blockDim.x) {
+    const int f = k / (B * sc);
+    const int rem = k - f * (B * sc);
     int64_t acc = 0;
     for (int r = 0; r < R; ++r) acc += lds[(r * FG + f) * rowstride + rem];
-    if (excl) out[k] = acc;
-    else if (acc != 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + k), (unsigned long long)acc);
+    const int bin = rem / sc, c = rem - bin * sc;
+    int64_t* w = out + ((int64_t)f * B + bin) * S + s0 + c;
+    if (excl) *w = acc;
+    else if (acc != 0) atomicAdd(reinterpret_cast<unsigned long long*>(w), (unsigned long long)acc);
   }
 }
 
@@ -566,6 +581,151 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
   }
 }
 
+// Wide split scan (S > 16 classes or B > 64 bins): one workgroup per (node, local feature). The
+// feature's B x S fixed-point histogram is copied into LDS and prefix-summed over bins per statistic
+// (one thread per statistic), node totals come from local feature 0 as in the narrow kernel, then the
+// threads stride over the (bin, missing direction) candidates and evaluate each with exactly the CPU
+// twin's operation order (impurity sums over s in order), so both paths pick the same split.
+__global__ void __launch_bounds__(256) split_scan_wide_kernel(
+    const int64_t* __restrict__ hist, const int64_t* __restrict__ node_hist_off, const int32_t* __restrict__ node_nfeat,
+    const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
+    const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
+    int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
+    Best* __restrict__ cand, int n_multi) {
+  extern __shared__ __attribute__((aligned(16))) int64_t wl[];
+  int64_t* H = wl;                       // [B][S] prefix sums
+  int64_t* totq = H + (int64_t)B * S;    // [S]
+  int64_t* miss = totq + S;              // [S]
+  double* q = reinterpret_cast<double*>(miss + S);   // [S]
+  __shared__ Best s_best[4];
+  const int j = blockIdx.x / fbmax;
+  const int f = blockIdx.x - j * fbmax;
+  const int nf = node_nfeat[j];
+  Best best{-INFINITY, 0x7fffffff, 0, 0};
+  const bool live = f < nf;
+  const int64_t* h = hist + node_hist_off[j];
+  const int32_t* fl = feat_list + node_feat_off[j];
+  const float* P = node_params + (int64_t)j * 8;
+  const double* qi = qinv + (int64_t)(node_model ? node_model[j] : 0) * S;
+  const double min_inst = P[0], min_gain = P[1], mcw = P[2], lambda = P[3];
+  const bool allow_missing = P[5] > 0.5f && missing_bin >= 0;
+  const int nb = live ? feat_nbins[fl[f]] : 0;
+  const bool one = live && n_multi >= 0 && f >= n_multi;     // one-present-bin column: bin 0 only
+  const int64_t* hf = h + (int64_t)f * B * S;
+  if (live) {
+    for (int i = threadIdx.x; i < B * S; i += blockDim.x) H[i] = (one && i >= S) ? 0 : hf[i];
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+      int64_t t = 0;
+      for (int bb = 0; bb < B; ++bb) t += h[(int64_t)bb * S + s];
+      totq[s] = t;
+      miss[s] = allow_missing ? hf[(int64_t)missing_bin * S + s] : 0;
+      q[s] = qi[s];
+    }
+  }
+  __syncthreads();
+  if (live)
+    for (int s = threadIdx.x; s < S; s += blockDim.x)
+      for (int bb = 1; bb < B; ++bb) H[(int64_t)bb * S + s] += H[(int64_t)(bb - 1) * S + s];
+  __syncthreads();
+  if (live) {
+    // parent impurity with the CPU twin's arithmetic
+    double tcount = 0, pimp = 0, parent_gain = 0;
+    if (kind == 0 || kind == 1) {
+      for (int s = 0; s < S; ++s) tcount += (double)totq[s] * q[s];
+      if (tcount > 0) {
+        pimp = kind == 0 ? 1.0 : 0.0;
+        for (int s = 0; s < S; ++s) {
+          const double p = ((double)totq[s] * q[s]) / tcount;
+          if (kind == 0) pimp -= p * p;
+          else if (p > 0) pimp -= p * log2(p);
+        }
+      }
+    } else {
+      double tot[4] = {0, 0, 0, 0};
+      for (int s = 0; s < S && s < 4; ++s) tot[s] = (double)totq[s] * q[s];
+      pimp = impurity_dev(tot, S, kind, &tcount);
+      parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
+    }
+    const int nd = allow_missing ? 2 : 1;
+    const int nbc = one ? 1 : nb - 1 + (allow_missing ? 1 : 0);   // candidate bins per direction
+    for (int c = threadIdx.x; c < nbc * nd; c += blockDim.x) {
+      const int dl = c / nbc, b = one ? 0 : c - dl * nbc;
+      if (one && (dl || !allow_missing)) continue;
+      if (!one && b == nb - 1 && dl) continue;
+      const int64_t* lp = H + (int64_t)b * S;
+      double gain;
+      bool ok = true;
+      if (kind == 0 || kind == 1) {
+        double lc = 0, rc = 0;
+        for (int s = 0; s < S; ++s) {
+          const int64_t lq = lp[s] + (dl ? miss[s] : 0);
+          lc += (double)lq * q[s];
+          rc += (double)(totq[s] - lq) * q[s];
+        }
+        double li = 0, ri = 0;
+        if (lc > 0) {
+          li = kind == 0 ? 1.0 : 0.0;
+          for (int s = 0; s < S; ++s) {
+            const double p = ((double)(lp[s] + (dl ? miss[s] : 0)) * q[s]) / lc;
+            if (kind == 0) li -= p * p;
+            else if (p > 0) li -= p * log2(p);
+          }
+        }
+        if (rc > 0) {
+          ri = kind == 0 ? 1.0 : 0.0;
+          for (int s = 0; s < S; ++s) {
+            const double p = ((double)(totq[s] - lp[s] - (dl ? miss[s] : 0)) * q[s]) / rc;
+            if (kind == 0) ri -= p * p;
+            else if (p > 0) ri -= p * log2(p);
+          }
+        }
+        if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) ok = false;
+        gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
+        if (gain < min_gain) ok = false;
+      } else {
+        double left[4] = {0, 0, 0, 0}, right[4] = {0, 0, 0, 0};
+        for (int s = 0; s < S && s < 4; ++s) {
+          const int64_t lq = lp[s] + (dl ? miss[s] : 0);
+          left[s] = (double)lq * q[s];
+          right[s] = (double)(totq[s] - lq) * q[s];
+        }
+        if (kind == 3) {
+          if (left[1] < mcw || right[1] < mcw) ok = false;
+          gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
+        } else {
+          double lc, rc;
+          const double li = impurity_dev(left, S, kind, &lc);
+          const double ri = impurity_dev(right, S, kind, &rc);
+          if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) ok = false;
+          gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
+          if (gain < min_gain) ok = false;
+        }
+      }
+      if (ok) {
+        const Best cb{gain, f, b, dl};
+        if (better(cb, best)) best = cb;
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int off = 32; off > 0; off >>= 1) {
+    Best o;
+    o.gain = __shfl_xor(best.gain, off, 64);
+    o.f = __shfl_xor(best.f, off, 64);
+    o.b = __shfl_xor(best.b, off, 64);
+    o.dl = __shfl_xor(best.dl, off, 64);
+    if (better(o, best)) best = o;
+  }
+  if (lane == 0) s_best[wave] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Best bb = s_best[0];
+    for (int w = 1; w < 4; ++w)
+      if (better(s_best[w], bb)) bb = s_best[w];
+    cand[blockIdx.x] = bb;
+  }
+}
+
 __global__ void __launch_bounds__(64) split_reduce_kernel(
     const int64_t* __restrict__ hist, const int64_t* __restrict__ node_hist_off, const int32_t* __restrict__ node_feat_off,
     const int32_t* __restrict__ feat_list, int B, int S, int missing_bin, const int32_t* __restrict__ node_model,
@@ -577,7 +737,10 @@ __global__ void __launch_bounds__(64) split_reduce_kernel(
   const int lane = threadIdx.x;
   if (cursors && lane < 2) cursors[2 * j + lane] = 0;   // partition_fused_kernel's per-node slot cursors
   Best b{-INFINITY, 0x7fffffff, 0, 0};
-  if (lane < fbmax) b = cand[(int64_t)j * fbmax + lane];
+  for (int i = lane; i < fbmax; i += 64) {      // any number of feature blocks
+    const Best c = cand[(int64_t)j * fbmax + i];
+    if (better(c, b)) b = c;
+  }
   for (int off = 32; off > 0; off >>= 1) {
     Best o;
     o.gain = __shfl_xor(b.gain, off, 64);
@@ -596,13 +759,13 @@ __global__ void __launch_bounds__(64) split_reduce_kernel(
     out_dl[j] = (uint8_t)(found ? b.dl : 0);
   }
   for (int s = 0; s < S; ++s) {
-    int64_t t = lane < B ? h[lane * S + s] : 0;
-    int64_t l = 0;
-    if (found) {
-      const int64_t* hf = h + (int64_t)b.f * B * S;
-      l = lane <= b.b ? hf[lane * S + s] : 0;
-      if (b.dl && lane == 0) l += hf[missing_bin * S + s];
+    int64_t t = 0, l = 0;
+    const int64_t* hf = h + (int64_t)(found ? b.f : 0) * B * S;
+    for (int bb = lane; bb < B; bb += 64) {       // any number of bins
+      t += h[(int64_t)bb * S + s];
+      if (found && bb <= b.b) l += hf[(int64_t)bb * S + s];
     }
+    if (found && b.dl && lane == 0) l += hf[(int64_t)missing_bin * S + s];
     for (int off = 32; off > 0; off >>= 1) {
       t += __shfl_xor(t, off, 64);
       l += __shfl_xor(l, off, 64);
@@ -930,25 +1093,27 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
-                        const int64_t* csr_ptr, const uint16_t* csr_col, hipStream_t stream) {
+                        const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, hipStream_t stream) {
   if (n_items == 0) return 0;
-  const size_t lds = (size_t)(((64 * (B * S + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
+  if (Sc <= 0 || Sc > S) Sc = S;
+  const size_t lds = (size_t)(((64 * (B * Sc + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
                      TM_MAX_S * sizeof(int);
   if (lds > 160 * 1024) return -2;
-  if (skip_bin >= B || (mode == 2 && skip_bin >= 0 && S != 2)) return -2;
+  if (skip_bin >= B || (mode == 2 && skip_bin >= 0 && (S != 2 || Sc != S))) return -2;
+  if (mode == 0 && S > TM_WIDE_MAX_S) return -2;
   if ((csr_ptr != nullptr) != (csr_col != nullptr) || (csr_ptr && (mode != 2 || skip_bin <= 0))) return -2;
   const HistItem* it = (const HistItem*)items;
   dim3 grid(n_items), block(256);
   if (mode == 0)
     hipLaunchKernelGGL(hist_build_kernel<0>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc);
   else if (mode == 1)
     hipLaunchKernelGGL(hist_build_kernel<1>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc);
   else
     hipLaunchKernelGGL(hist_build_kernel<2>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                       csr_col);
+                       csr_col, Sc);
   return (int)hipGetLastError();
 }
 
@@ -972,12 +1137,20 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         int n_multi, void* rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase,
                         hipStream_t stream) {
   if (n_nodes == 0) return 0;
-  if (S > TM_MAX_S || B > 64) return -2;
   if (n_multi > max_nfeat) n_multi = -1;
-  const int fbmax = n_multi >= 0 ? (n_multi + FPB - 1) / FPB + (max_nfeat - n_multi + 255) / 256
-                                 : (max_nfeat + FPB - 1) / FPB;
-  if (fbmax > 64) return -2;
-  Best* cand = (Best*)cand_ws;   // >= n_nodes * fbmax entries
+  Best* cand = (Best*)cand_ws;   // >= tmog_hip_split_cand_bytes(n_nodes, max_nfeat, B, S) bytes
+  const bool wide = S > TM_MAX_S || B > 64;
+  int fbmax;
+  if (wide) {
+    if (S > TM_WIDE_MAX_S || B * S > TM_WIDE_MAX_BS) return -2;
+    fbmax = max_nfeat;        // one workgroup per (node, feature)
+    const size_t lds = ((size_t)B * S + 3 * (size_t)S) * 8;
+    hipLaunchKernelGGL(split_scan_wide_kernel, dim3(n_nodes * fbmax), dim3(256), lds, stream, hist, node_hist_off,
+                       node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin,
+                       node_model, qinv, fbmax, cand, n_multi);
+  } else {
+  fbmax = n_multi >= 0 ? (n_multi + FPB - 1) / FPB + (max_nfeat - n_multi + 255) / 256
+                       : (max_nfeat + FPB - 1) / FPB;
 #define TM_SPLIT(SMV)                                                                                          \
   hipLaunchKernelGGL(split_scan_kernel<SMV>, dim3(n_nodes * fbmax), dim3(256), 0, stream, hist, node_hist_off,  \
                      node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin,    \
@@ -987,6 +1160,7 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
   else if (S <= 4) TM_SPLIT(4);
   else TM_SPLIT(TM_MAX_S);
 #undef TM_SPLIT
+  }
   hipLaunchKernelGGL(split_reduce_kernel, dim3(n_nodes), dim3(64), 0, stream, hist, node_hist_off, node_feat_off,
                      feat_list, B, S, missing_bin, node_model, qinv, fbmax, cand, out_feat, out_bin, out_gain, out_dl,
                      out_left, out_total, (unsigned long long*)cursors, (uint8_t*)rec, rec_bytes, fp_mlo, fp_nml,
@@ -1010,8 +1184,18 @@ int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* siz
   return (int)hipGetLastError();
 }
 
-size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat) {
-  return (size_t)n_nodes * ((max_nfeat + FPB - 1) / FPB) * sizeof(Best);
+size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat, int B, int S) {
+  const bool wide = S > TM_MAX_S || B > 64;
+  return (size_t)n_nodes * (wide ? max_nfeat : (max_nfeat + FPB - 1) / FPB) * sizeof(Best);
+}
+
+// Largest statistic chunk whose per-workgroup LDS table (64 copies of B x Sc words) fits the LDS.
+int tmog_hip_hist_stat_chunk(int B, int S) {
+  int sc = S;
+  while (sc > 1 && (size_t)(((64 * (B * sc + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
+                       TM_MAX_S * sizeof(int) > 160 * 1024)
+    --sc;
+  return sc;
 }
 
 int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, const void* items,

@@ -25,6 +25,8 @@
 #include <algorithm>
 #include <omp.h>
 
+constexpr int kMaxS = 256;   // statistics per bin (classes); the HIP wide path has the same bound
+
 extern "C" {
 
 static inline float stat_target(const float* t, int64_t model, int64_t stride, int64_t row) {
@@ -50,9 +52,8 @@ int tmog_hist_build_cpu(const uint8_t* Xb, int64_t N, int F, const uint32_t* row
       const uint32_t e = rows[b0 + i];
       const int64_t r = e & 0xFFFFFFu;
       const float w = (float)(e >> 24);
-      int64_t st[16];
+      int64_t st[kMaxS];
       if (mode == 0) {
-        for (int s = 0; s < S; ++s) st[s] = 0;
         st[(int)y[r]] = (int64_t)(e >> 24);
       } else if (mode == 1) {
         const float t = stat_target(t1, model, model_stride, r);
@@ -65,6 +66,11 @@ int tmog_hist_build_cpu(const uint8_t* Xb, int64_t N, int F, const uint32_t* row
         st[1] = (int64_t)(int)rintf((w * stat_target(t2, model, model_stride, r)) * qs[1]);
       }
       const uint8_t* xr = Xb + r * (int64_t)F;
+      if (mode == 0) {           // one class slot per row
+        const int cls = (int)y[r];
+        for (int f = 0; f < nf; ++f) h[((int64_t)f * B + xr[fl[f]]) * S + cls] += st[cls];
+        continue;
+      }
       for (int f = 0; f < nf; ++f) {
         const int bin = xr[fl[f]];
         int64_t* hb = h + ((int64_t)f * B + bin) * S;
@@ -119,8 +125,8 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
     const double* q = qinv + (int64_t)(node_model ? node_model[j] : 0) * S;
     const double min_inst = P[0], min_gain = P[1], mcw = P[2], lambda = P[3];
     const bool allow_missing = P[5] > 0.5f && missing_bin >= 0;
-    int64_t totq[16] = {0};
-    double tot[16];
+    int64_t totq[kMaxS] = {0};
+    double tot[kMaxS];
     // totals from feature 0 (every row is counted once per feature, including the missing bin)
     for (int b = 0; b < B; ++b)
       for (int s = 0; s < S; ++s) totq[s] += h[(int64_t)b * S + s];
@@ -133,22 +139,22 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
     const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
     double best = -INFINITY;
     int bf = -1, bb = -1, bdl = 0, bfi = -1;
-    int64_t bleft[16] = {0};
+    int64_t bleft[kMaxS] = {0};
     for (int f = 0; f < nf; ++f) {
       const int gf = fl[f];
       const int nb = feat_nbins[gf];
       const int64_t* hf = h + (int64_t)f * B * S;
-      int64_t miss[16] = {0};
+      int64_t miss[kMaxS] = {0};
       if (allow_missing)
         for (int s = 0; s < S; ++s) miss[s] = hf[(int64_t)missing_bin * S + s];
       for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
-        int64_t lq[16];
+        int64_t lq[kMaxS];
         for (int s = 0; s < S; ++s) lq[s] = dl ? miss[s] : 0;
         // with a missing bin, dl = 0 also tries b = nb - 1: every present value left, missing right
         // (XGBoost's present-vs-missing split; the only candidate of a one-bin indicator column)
         const int b_end = nb - 1 + ((allow_missing && dl == 0) ? 1 : 0);
         for (int b = 0; b < b_end; ++b) {
-          double left[16], right[16];
+          double left[kMaxS], right[kMaxS];
           for (int s = 0; s < S; ++s) {
             lq[s] += hf[(int64_t)b * S + s];
             left[s] = (double)lq[s] * q[s];

@@ -20,13 +20,15 @@ def gemm_t(X: torch.Tensor, R: torch.Tensor) -> torch.Tensor:
 
 
 LOSS_CODES = {"logistic": 0, "hinge": 1, "squared": 2}
-_LR_DMAX = 384
+_LR_DMAX = 384          # one-pass kernel: 64-row X tile + V resident in LDS
+_LR_WIDE_DMAX = 2048    # wide kernel: library GEMM margins + fused epilogue / MFMA gradient
 _LR_PC = 32
 
 
 def fused_objective_supported(X: torch.Tensor) -> bool:
-    """The fused HIP objective handles fp32 ``X`` on the GPU with ``d <= 384`` columns."""
-    return X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and 1 <= X.shape[1] <= _LR_DMAX \
+    """The fused HIP objective handles fp32 ``X`` on the GPU with ``d <= 2048`` columns (one pass over X
+    up to 384 columns, a library GEMM plus one fused pass above)."""
+    return X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and 1 <= X.shape[1] <= _LR_WIDE_DMAX \
         and X.is_contiguous()
 
 
@@ -46,7 +48,7 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
     N, d = X.shape
     P = W.shape[1]
     dev = X.device
-    if (N * d) % 4 or X.data_ptr() % 16:
+    if d <= _LR_DMAX and ((N * d) % 4 or X.data_ptr() % 16):
         # the kernel streams X in 16-byte chunks: run the <= 3 trailing rows through torch
         Nm = N - N % 4 if X.data_ptr() % 16 == 0 else 0
         parts = []
@@ -77,10 +79,17 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
         if yscale is not None:
             ys = torch.ones(_LR_PC, dtype=torch.float32, device=dev)
             ys[:pc] = yscale[c0:c0 + pc]
-        N_.check(N_.hip().tmog_hip_lr_objective(
-            N_.ptr(X), N, d, N_.ptr(yf), N_.ptr(Wf), P, c0, pc, N_.ptr(Vc), N_.ptr(bc), LOSS_CODES[loss],
-            N_.ptr(ys), int(grad), N_.ptr(fp), N_.ptr(rp), N_.ptr(gp) if grad else None, nblk, N_.stream(dev)),
-            "lr_objective")
+        if d <= _LR_DMAX:
+            N_.check(N_.hip().tmog_hip_lr_objective(
+                N_.ptr(X), N, d, N_.ptr(yf), N_.ptr(Wf), P, c0, pc, N_.ptr(Vc), N_.ptr(bc), LOSS_CODES[loss],
+                N_.ptr(ys), int(grad), N_.ptr(fp), N_.ptr(rp), N_.ptr(gp) if grad else None, nblk, N_.stream(dev)),
+                "lr_objective")
+        else:
+            M = (X @ Vc).contiguous()          # [N, 32] margins on hipBLASLt
+            N_.check(N_.hip().tmog_hip_lr_epilogue_grad(
+                N_.ptr(X), N, d, N_.ptr(M), N_.ptr(yf), N_.ptr(Wf), P, c0, pc, N_.ptr(bc), LOSS_CODES[loss],
+                N_.ptr(ys), int(grad), N_.ptr(fp), N_.ptr(rp), N_.ptr(gp) if grad else None, nblk, N_.stream(dev)),
+                "lr_epilogue_grad")
         f[c0:c0 + pc] = fp[:, :pc].sum(0)
         r[c0:c0 + pc] = rp[:, :pc].sum(0)
         if grad:
