@@ -50,3 +50,22 @@ def test_checkpoint_functions_resolve_only_through_registry():
     assert G.load_extract_fn(name) is None
     G.register_function(_secret_fn, name="my.extract")
     assert G.load_extract_fn("my.extract") is _secret_fn
+
+
+def test_pointer_returning_native_functions_declare_pointer_restype():
+    """A native function returning a pointer / handle must not default to ctypes' 32-bit int restype
+    (a truncated RCCL communicator handle segfaults inside the collective)."""
+    import ctypes as C
+    import re
+    from pathlib import Path
+    from transmogrifai_amd.ops import _native as N
+    src = Path(N.__file__).parent / "csrc"
+    ptr_fns = set()
+    for f in list(src.rglob("*.hip")) + list(src.rglob("*.cpp")):
+        for m in re.finditer(r"^(?:void|int64_t|size_t|uint64_t)\s*\*?\s*(tmog_\w+)\s*\(", f.read_text(), re.M):
+            line = m.group(0)
+            if "*" in line or line.startswith(("int64_t", "size_t", "uint64_t")):
+                ptr_fns.add(m.group(1))
+    declared = set(N._HOST_SIGS) | set(N._HIP_SIGS)
+    for fn in sorted(ptr_fns & declared):
+        assert N._RESTYPES.get(fn) in (C.c_void_p, C.c_int64, C.c_size_t), fn

@@ -95,7 +95,7 @@ _HIP_SIGS = {
 _RESTYPES = {"tmog_tree_finalize_cpu": C.c_int64, "tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
              "tmog_shist_flush": None, "tmog_shist_merge": None, "tmog_shist_bins": None,
              "tmog_shist_size": C.c_int64, "tmog_shist_sum": C.c_double,
-             "tmog_hip_split_cand_bytes": C.c_size_t,  # (n_nodes, max_nfeat, B, S) "tmog_hip_rccl_comm_init": C.c_void_p,
+             "tmog_hip_split_cand_bytes": C.c_size_t, "tmog_hip_rccl_comm_init": C.c_void_p,
              "tmog_grow_forest_cpu": C.c_void_p, "tmog_hip_grow_forest": C.c_void_p,
              "tmog_grow_nodes_cpu": C.c_int64, "tmog_hip_grow_nodes": C.c_int64,
              "tmog_grow_leaf_count_cpu": C.c_int64, "tmog_hip_grow_leaf_count": C.c_int64,

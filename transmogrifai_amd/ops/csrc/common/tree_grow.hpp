@@ -17,6 +17,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
@@ -336,6 +338,10 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     full_groups = equal_groups(F);
   }
   const int F_use = perm_feats.empty() ? F : (int)perm_feats.size();
+  const bool trace = std::getenv("TMOG_GROW_TRACE") != nullptr;   // progress to stderr (debugging)
+  if (trace)
+    std::fprintf(stderr, "[grow g%d] T=%d F=%d F_use=%d S=%d B=%d fp=%d slice m[%d,%d) o[%d,%d)\n", g, T, F, F_use, S,
+                 B, (int)fp, a.fp_mlo, a.fp_mhi, a.fp_olo, a.fp_ohi);
   // GPU histogram items accumulate a chunk of the statistics when a B x S table exceeds the LDS (many
   // classes / wide bins): one item per chunk, each writing disjoint words of the node histogram
   const int stat_sc = bk.stat_chunk(B, S);
@@ -523,16 +529,19 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     const size_t r_cl = 0, r_feat = r_cl + 16 * (size_t)m, r_bin = r_feat + 4 * (size_t)m, r_gain = r_bin + 4 * (size_t)m;
     const size_t r_left = r_gain + 4 * (size_t)m, r_tot = r_left + 4 * (size_t)m * S, r_dl = r_tot + 4 * (size_t)m * S;
     const size_t r_bytes = r_dl + (size_t)m;
-    const size_t r_rec = (r_bytes + 7) & ~size_t(7);
-    uint8_t* res = bk.result_buffer(fp ? r_rec + fp_rb * (size_t)m : r_bytes);
-    const FpSlice fps{fp ? res + r_rec : nullptr, (int64_t)fp_rb, fp_mlo, fp_nml, fp_obase};
+    uint8_t* res = bk.result_buffer(r_bytes);
+    uint8_t* fp_send = fp ? bk.fp_send_buffer(fp_rb * (size_t)m) : nullptr;
+    const FpSlice fps{fp_send, (int64_t)fp_rb, fp_mlo, fp_nml, fp_obase};
     bk.split_find(a, hist, m, TM_P(const int64_t, o_nho), TM_P(const int32_t, o_nnf), TM_P(const int32_t, o_nfo),
                   flist, TM_P(const float, o_par), TM_P(const int32_t, o_nmd), max_nf, (int32_t*)(res + r_feat),
                   (int32_t*)(res + r_bin), (float*)(res + r_gain), res + r_dl, (float*)(res + r_left),
                   (float*)(res + r_tot), (int64_t*)(res + r_cl), use_subset ? -1 : split_n_multi, fps);
-    if (fp)   // all-gather the ranks' best splits, merge into this level's decisions (on-stream on the GPU)
-      bk.fp_exchange_merge(a, res + r_rec, m, fp_rb, (int32_t*)(res + r_feat), (int32_t*)(res + r_bin),
+    if (trace) std::fprintf(stderr, "[grow g%d] depth %d: %d nodes split_find done\n", g, depth, m);
+    if (fp) {  // all-gather the ranks' best splits, merge into this level's decisions (on-stream on the GPU)
+      bk.fp_exchange_merge(a, fp_send, m, fp_rb, (int32_t*)(res + r_feat), (int32_t*)(res + r_bin),
                            (float*)(res + r_gain), res + r_dl, (float*)(res + r_left));
+      if (trace) std::fprintf(stderr, "[grow g%d] depth %d: exchange + merge issued\n", g, depth);
+    }
     if (BK::kGPU)   // partition in place of the node ranges, straight from the device decisions
       bk.partition_fused(a, rows, rows_alt, d1 + o_cit, (int)ncit, TM_P(const int64_t, o_nb),
                          TM_P(const int64_t, o_nc), (const int32_t*)(res + r_feat), (const int32_t*)(res + r_bin),

@@ -5,7 +5,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <csignal>
+#include <cstdlib>
 #include <cstring>
+#include <execinfo.h>
+#include <unistd.h>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -67,12 +72,19 @@ struct GpuSlot {
   size_t cand_cap = 0;
   int32_t* feats = nullptr;
   int feats_n = 0;
+  uint8_t* fp_send = nullptr;                 // feature-parallel: this rank's split records
+  size_t fp_send_cap = 0;
   uint8_t* fp_recv = nullptr;                 // feature-parallel: all-gathered split records
   size_t fp_recv_cap = 0;
   uint8_t* hist[2] = {nullptr, nullptr};     // grow-only level histogram buffers (int64 words)
   size_t hist_cap[2] = {0, 0};
   int device = -1;
 };
+
+std::mutex& rccl_mutex() {
+  static std::mutex m;
+  return m;
+}
 
 std::vector<GpuSlot>& slots() {
   static std::vector<GpuSlot> s(8);
@@ -172,14 +184,35 @@ struct GpuBackend {
                              fps.rec_bytes, fps.mlo, fps.nml, fps.obase, sl.stream),
          "split_find");
   }
+  // RCCL send / receive buffers come from plain hipMalloc (grow-only; never from the stream-ordered
+  // pool of grow_dev): the collective library inspects and may register the buffers it is given.
+  static void grow_plain(uint8_t*& p, size_t& cap, size_t need, hipStream_t s) {
+    if (need <= cap) return;
+    if (p) {
+      hchk(hipStreamSynchronize(s), "sync before rccl buffer realloc");
+      hchk(hipFree(p), "hipFree");
+    }
+    cap = need + need / 2 + 4096;
+    hchk(hipMalloc((void**)&p, cap), "hipMalloc");
+  }
+  uint8_t* fp_send_buffer(size_t bytes) {
+    grow_plain(sl.fp_send, sl.fp_send_cap, bytes, sl.stream);
+    return sl.fp_send;
+  }
   // One RCCL all-gather of the level's split records over xGMI (this group's communicator, on the
   // group's stream: no host round trip), then the merge kernel rewrites the decisions in place.
   void fp_exchange_merge(const tmog::GrowArgs& g, const uint8_t* rec, int m, size_t rb, int32_t* feat, int32_t* bin,
                          float* gain, uint8_t* dl, float* left) {
     const size_t bytes = rb * (size_t)m;
-    grow_dev(sl.fp_recv, sl.fp_recv_cap, bytes * (size_t)g.fp_world, sl.stream);
+    grow_plain(sl.fp_recv, sl.fp_recv_cap, bytes * (size_t)g.fp_world, sl.stream);
     ncclComm_t comm = (ncclComm_t)g.fp_comm[group];
-    const ncclResult_t r = ncclAllGather(rec, sl.fp_recv, bytes, ncclUint8, comm, sl.stream);
+    ncclResult_t r;
+    {
+      // enqueue under a process-wide lock: the job groups' host threads issue their (independent,
+      // per-communicator) collectives concurrently, and RCCL's enqueue path keeps process-global state
+      std::lock_guard<std::mutex> lk(rccl_mutex());
+      r = ncclAllGather(rec, sl.fp_recv, bytes, ncclUint8, comm, sl.stream);
+    }
     if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllGather: ") + ncclGetErrorString(r));
     kchk(tmog_hip_fp_merge(sl.fp_recv, g.fp_world, m, (int64_t)rb, g.S, feat, bin, gain, dl, left, sl.stream),
          "fp_merge");
@@ -205,7 +238,22 @@ struct GpuBackend {
 
 extern "C" {
 
+static void segv_backtrace(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "\n[tmog] native fault, backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
+  static bool handler = false;
+  if (!handler && std::getenv("TMOG_GROW_TRACE")) {   // debugging aid: name the faulting native frame
+    signal(SIGSEGV, segv_backtrace);
+    handler = true;
+  }
   tmog::GrowResult* res = new tmog::GrowResult();
   const tmog::GrowArgs& a = *args;
   const int ng = a.n_groups;
@@ -288,7 +336,22 @@ void* tmog_hip_rccl_comm_init(const char* id_bytes, int world, int rank) {
   ncclUniqueId id;
   std::memcpy(&id, id_bytes, sizeof(id));
   ncclComm_t comm = nullptr;
+  std::lock_guard<std::mutex> lk(rccl_mutex());
   if (ncclCommInitRank(&comm, world, id, rank) != ncclSuccess) return nullptr;
+  // one small all-gather right away, from this (single) thread: RCCL finishes its lazy per-communicator
+  // setup (connections, kernel resources) here instead of inside the grower's concurrent group threads
+  hipStream_t s = nullptr;
+  void* buf = nullptr;
+  bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+            hipMalloc(&buf, 64 * (size_t)world) == hipSuccess &&
+            ncclAllGather((char*)buf + 64 * (size_t)rank, buf, 64, ncclUint8, comm, s) == ncclSuccess &&
+            hipStreamSynchronize(s) == hipSuccess;
+  if (buf) (void)hipFree(buf);
+  if (s) (void)hipStreamDestroy(s);
+  if (!ok) {
+    ncclCommDestroy(comm);
+    return nullptr;
+  }
   return (void*)comm;
 }
 int tmog_hip_rccl_comm_destroy(void* comm) {

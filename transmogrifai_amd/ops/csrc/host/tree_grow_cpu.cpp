@@ -44,6 +44,11 @@ struct CpuBackend {
   }
   const uint8_t* ship(const tmog::Staging& st, int) { return st.buf.data(); }
   int stat_chunk(int, int S) const { return S; }
+  std::vector<uint8_t> fp_send;
+  uint8_t* fp_send_buffer(size_t bytes) {
+    fp_send.assign(bytes ? bytes : 8, 0);
+    return fp_send.data();
+  }
   int64_t* hist_buffer(int k, size_t words) {
     if (hist[k].size() < words) hist[k].resize(words + words / 4 + 16);
     return hist[k].data();

@@ -31,20 +31,40 @@ MODEL_DIR = "op-model.json"
 PART = "part-00000"
 
 
+# RawFeatureFilterResults of a workflow trained without a raw feature filter (the reference's defaults,
+# RawFeatureFilterResults.scala / OldModelVersion_0_7_1 fixture)
+_EMPTY_RFF = {"rawFeatureFilterConfig": {"minFill": 0.0, "maxFillDifference": float("inf"),
+                                         "maxFillRatioDiff": float("inf"), "maxJSDivergence": 1.0,
+                                         "maxCorrelation": 1.0, "correlationType": "Pearson",
+                                         "jsDivergenceProtectedFeatures": [], "protectedFeatures": []},
+              "rawFeatureDistributions": [], "rawFeatureFilterMetrics": [], "exclusionReasons": []}
+
+_VECTOR_KEYS = ("vector_columns", "vector_history", "vector_detected_sensitive")
+
+
 def _meta_to_json(meta: Dict) -> Dict:
+    """A stage's output metadata as the reference writes it: the OpVectorMetadata keys
+    (``vector_columns`` / ``vector_history`` / ``vector_detected_sensitive``, OpVectorMetadata.scala:187-189)
+    and Spark's ``ml_attr`` attribute group at the top level, other entries (summaries) beside them."""
     out = {}
     for k, v in meta.items():
         if isinstance(v, OpVectorMetadata):
-            out[k] = {"__vector_metadata__": v.name, **v.to_json()}
+            out.update(v.to_json())
+            out["ml_attr"] = {"num_attrs": len(v.columns)}
         else:
             out[k] = encode(v)
     return out
 
 
-def _meta_from_json(d: Dict) -> Dict:
+def _meta_from_json(d: Dict, name: Optional[str] = None) -> Dict:
     out = {}
-    for k, v in (d or {}).items():
-        if isinstance(v, dict) and "__vector_metadata__" in v:
+    d = d or {}
+    if "vector_columns" in d:
+        out["vector_metadata"] = OpVectorMetadata.from_json(name or "", {k: d[k] for k in _VECTOR_KEYS if k in d})
+    for k, v in d.items():
+        if k in _VECTOR_KEYS or k == "ml_attr":
+            continue
+        if isinstance(v, dict) and "__vector_metadata__" in v:       # round-1 checkpoints
             out[k] = OpVectorMetadata.from_json(v["__vector_metadata__"], v)
         else:
             out[k] = decode(v)
@@ -90,7 +110,7 @@ def model_to_json(model) -> Dict:
         "allFeatures": all_features,
         "parameters": model.parameters.to_string(),
         "trainParameters": model.train_parameters.to_string(),
-        "rawFeatureFilterResults": json.dumps(encode(rff.to_json() if hasattr(rff, "to_json") else (rff or {}))),
+        "rawFeatureFilterResults": json.dumps(encode(rff.to_json() if hasattr(rff, "to_json") else (rff or _EMPTY_RFF))),
         "trainTimings": encode(getattr(model, "train_timings", {})),
     }
 
@@ -152,7 +172,7 @@ def _build_stage(sj: Dict) -> OpPipelineStage:
         if k in ("inputFeatures", "outputFeatureName", "outputMetadata"):
             continue
         st.params[k] = decode(v)
-    st.metadata = _meta_from_json(pm.get("outputMetadata", {}))
+    st.metadata = _meta_from_json(pm.get("outputMetadata", {}), pm.get("outputFeatureName"))
     st._output_name = pm.get("outputFeatureName")
     st.load_ctor_args(args)
     return st
