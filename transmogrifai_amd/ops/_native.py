@@ -52,7 +52,10 @@ _HOST_SIGS = {
     "tmog_shist_size": [P],
     "tmog_shist_bins": [P, P, P],
     "tmog_shist_sum": [P, C.c_double],
-    "tmog_tokenize_batch": [P, P, I64, I32, I32, P, P, P, I64],
+    "tmog_tok_run": [P, P, I64, I32, I32, I32],
+    "tmog_tok_sizes": [P, P, P],
+    "tmog_tok_copy": [P, P, P, P, P],
+    "tmog_tok_free": [P],
 }
 
 _HIP_SIGS = {
@@ -87,12 +90,19 @@ _HIP_SIGS = {
     "tmog_hip_gram_f32": [P, I64, I32, I64, P, I32, P],
     "tmog_hip_logistic_grad": [P, P, P, I64, I32, P],
     "tmog_hip_label_colsum": [P, P, I64, I32, I64, I32, P, P],
+    "tmog_hip_hash_tokens": [P, P, I64, P, I32, I32, I32, I32, P, P],
+    "tmog_hip_hash_tf_rows": [P, I32, I64, I32, I32, P, I64, I64, P],
+    "tmog_hip_hash_feat_bytes": [],
+    "tmog_hip_code_count": [P, P, I32, I32, I64, P, P],
+    "tmog_hip_bucketize": [P, P, I64, P, I32, I32, I32, I32, P, I64, I64, I32, P, P],
+    "tmog_hip_date_unit_circle": [P, P, I64, I32, I32, I32, P, I64, I64, P],
     "tmog_hip_rff_summary": [P, P, P, I64, I32, P, I32, P, P],
     "tmog_hip_rff_hist": [P, P, P, I64, I32, P, P, I32, P, P],
 }
 
 
-_RESTYPES = {"tmog_tree_finalize_cpu": C.c_int64, "tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
+_RESTYPES = {"tmog_tok_run": C.c_void_p, "tmog_tok_sizes": None, "tmog_tok_copy": None, "tmog_tok_free": None,
+             "tmog_tree_finalize_cpu": C.c_int64, "tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
              "tmog_shist_flush": None, "tmog_shist_merge": None, "tmog_shist_bins": None,
              "tmog_shist_size": C.c_int64, "tmog_shist_sum": C.c_double,
              "tmog_hip_split_cand_bytes": C.c_size_t, "tmog_hip_rccl_comm_init": C.c_void_p,

@@ -31,7 +31,7 @@ def _sources(kind: str):
 
 
 def _headers():
-    return sorted(CSRC.rglob("*.h")) + sorted(CSRC.rglob("*.hpp"))
+    return sorted(CSRC.rglob("*.h")) + sorted(CSRC.rglob("*.hpp")) + sorted(CSRC.rglob("*.inc"))
 
 
 def _stale(so: Path, srcs) -> bool:

@@ -33,27 +33,56 @@ def column_means(cols: Sequence[NumericColumn]) -> List[float]:
     return [float(a / b) if b > 0 else float(a) for a, b in zip(s, n)]
 
 
+_MODE_RANGE = 1 << 20
+
+
 def column_modes(cols: Sequence[NumericColumn]) -> List[float]:
-    """Mode of non-null values per column, ties -> smallest value, 0 if empty (``ModeSeqNullInt``).
-    Row-sharded fits merge the per-rank (value, count) tables before the argmax."""
+    """Mode of non-null values per column, ties -> smallest value, 0 if empty (``ModeSeqNullInt``,
+    ``IntegralVectorizer.scala:79``).
+
+    Columns whose (global) value range spans at most 2^20 values are offset-coded and counted by the
+    HIP ``code_count_kernel`` (LDS-privatised histogram) in one launch, the counts all-reduced over
+    ranks in one collective; the first maximum of the dense count table is the smallest modal value.
+    Wider columns go through a sort-based ``unique`` whose (value, count) tables are merged over ranks."""
     from ..parallel import dp
-    tables = []
-    for c in cols:
-        v = c.values[c.valid]
-        u, cnt = torch.unique(v, return_counts=True)
-        tables.append((u.cpu().numpy(), cnt.cpu().numpy()))
-    parts = dp.objects(tables)
-    out = []
-    for j in range(len(cols)):
-        acc: dict = {}
-        for p in parts:
-            for val, k in zip(*p[j]):
-                acc[val.item()] = acc.get(val.item(), 0) + int(k)
-        if not acc:
-            out.append(0.0)
-            continue
-        best = max(acc.items(), key=lambda vc: (vc[1], -vc[0]))
-        out.append(float(best[0]))
+    from .text import code_counts
+    if not cols:
+        return []
+    dev = cols[0].values.device
+    big = torch.tensor(2 ** 62, dtype=torch.int64, device=dev)
+    vals = [c.values.to(torch.int64) for c in cols]
+    lo = torch.stack([torch.where(c.valid, v, big).min() if len(c) else big for c, v in zip(cols, vals)])
+    hi = torch.stack([torch.where(c.valid, v, -big).max() if len(c) else -big for c, v in zip(cols, vals)])
+    lo, hi = dp.min_(lo), dp.max_(hi)
+    lo_h, hi_h = lo.cpu().numpy(), hi.cpu().numpy()
+    out: List[float] = [0.0] * len(cols)
+    dense = [j for j in range(len(cols)) if lo_h[j] <= hi_h[j] and hi_h[j] - lo_h[j] < _MODE_RANGE]
+    wide = [j for j in range(len(cols)) if lo_h[j] <= hi_h[j] and hi_h[j] - lo_h[j] >= _MODE_RANGE]
+    if dense:
+        codes = [torch.where(cols[j].valid, vals[j] - int(lo_h[j]), torch.full_like(vals[j], -1)).to(torch.int32)
+                 for j in dense]
+        nv = [int(hi_h[j] - lo_h[j]) + 1 for j in dense]
+        counts = code_counts(codes, nv)
+        summed = np.concatenate([c[:-1] for c in counts])
+        if dp.active():
+            summed = dp.sum_([torch.as_tensor(summed, device=dev)])[0].cpu().numpy()
+        o = 0
+        for j, v in zip(dense, nv):
+            seg = summed[o:o + v]
+            o += v
+            out[j] = float(int(lo_h[j]) + int(np.argmax(seg)))
+    if wide:
+        tables = []
+        for j in wide:
+            u, cnt = torch.unique(vals[j][cols[j].valid], return_counts=True)
+            tables.append((u.cpu().numpy(), cnt.cpu().numpy()))
+        parts = dp.objects(tables)
+        for k, j in enumerate(wide):
+            u = np.concatenate([p[k][0] for p in parts])
+            c = np.concatenate([p[k][1] for p in parts])
+            uu, inv = np.unique(u, return_inverse=True)
+            tot = np.bincount(inv, weights=c)
+            out[j] = float(uu[int(np.argmax(tot))])
     return out
 
 

@@ -302,28 +302,13 @@ def check_splits(splits: Sequence[float]) -> bool:
 
 def bucketize_column(x: torch.Tensor, ok: torch.Tensor, splits: Sequence[float], track_nulls: bool,
                      track_invalid: bool, inclusion: str, dtype) -> torch.Tensor:
-    """One-hot bucket index via binary search (``NumericBucketizer.bucketize:219-265``)."""
+    """One-hot bucket index via binary search (``NumericBucketizer.bucketize:219-265``); HIP
+    ``bucketize_kernel`` on device (``ops/text.py``)."""
+    from ...ops.text import bucketize_into
     nb = len(splits) - 1
-    n = x.shape[0]
     width = nb + (1 if track_invalid else 0) + (1 if track_nulls else 0)
-    out = torch.zeros(n, width, dtype=dtype, device=x.device)
-    s = torch.as_tensor(list(splits), dtype=torch.float64, device=x.device)
-    if inclusion == "Left":
-        idx = torch.searchsorted(s, x, right=True) - 1          # splits[i] <= x < splits[i+1]
-    else:
-        idx = torch.searchsorted(s, x, right=False) - 1         # splits[i] < x <= splits[i+1]
-    invalid = (idx < 0) | (idx >= nb) | ~_finite(x)
-    if invalid[ok].any() and not track_invalid:
-        bad = x[ok & invalid][0].item()
-        raise ValueError(f"Numeric value {bad} falls outside the bounds of the specified buckets")
-    rows = torch.arange(n, device=x.device)
-    good = ok & ~invalid
-    out[rows[good], idx[good]] = 1.0
-    if track_invalid:
-        m = ok & invalid
-        out[rows[m], nb] = 1.0
-    if track_nulls:
-        out[rows[~ok], width - 1] = 1.0
+    out = torch.zeros(x.shape[0], width, dtype=dtype, device=x.device)
+    bucketize_into(out, x, ok, splits, track_nulls, track_invalid, inclusion == "Left")
     return out
 
 

@@ -25,7 +25,7 @@ from ...features import types as T
 from ...utils import text as TU
 from ..base import (OpEstimator, OpTransformer, SequenceTransformer, UnaryEstimator, UnaryTransformer,
                     register_stage)
-from .vectorizers import (HashingParams, VectorizerMixin, _terms_csr, hash_metadata, col_meta)
+from .vectorizers import (HashingParams, VectorizerMixin, hash_metadata, col_meta)
 from ...ops import vector as V
 
 # ------------------------------------------------------------------------------- named value maps
@@ -191,7 +191,9 @@ class TextTokenizer(UnaryTransformer):
     def transform_columns(self, *cols, ds=None):
         c = cols[0]
         if isinstance(c, TextColumn):
-            toks = [self.transform_fn(s) for s in c.vocab]
+            p = self.params
+            vocab = [TU.strip_html(s) for s in c.vocab] if p["strip_html"] else c.vocab
+            toks = TU.tokenize_batch(vocab, p["to_lowercase"], p["min_token_length"]).lists()
             codes = c.codes.cpu().numpy()
             out = np.empty(len(codes), dtype=object)
             for i, k in enumerate(codes):
@@ -212,7 +214,7 @@ class TextLenTransformer(VectorizerMixin, SequenceTransformer):
         parts = []
         for c in cols:
             if isinstance(c, TextColumn):
-                lens = torch.as_tensor([float(sum(len(t) for t in TU.tokenize(s))) for s in c.vocab] + [0.0],
+                lens = torch.as_tensor(np.append(TU.tokenize_batch(c.vocab).char_lengths().astype(np.float64), 0.0),
                                        device=dev)
                 idx = torch.where(c.codes >= 0, c.codes.long(), torch.full_like(c.codes.long(), len(c.vocab)))
                 parts.append(lens[idx])
@@ -246,12 +248,11 @@ class OpHashingTF(VectorizerMixin, OpTransformer):
         hp = HashingParams(self.params["num_features"], 1, 1 << 30, self.params["binary"], False, "separate")
         tfs = self.get_transient_features()
         self.metadata["vector_metadata"] = self.vector_metadata(hash_metadata(tfs, hp))
+        from ...ops.text import HashInput, hashed_tf
         lists = [[str(x) for x in (v or [])] for v in c.to_list()]
-        indptr, idx, vals = _terms_csr(lists, None, hp)
         dev = c.device
-        out = torch.zeros(len(lists), hp.num_features, dtype=vector_dtype(dev), device=dev)
-        V.csr_rows_scatter_add(out, torch.arange(len(lists), device=dev, dtype=torch.int32), indptr,
-                               idx.astype(np.int64), vals)
+        out = torch.empty(len(lists), hp.num_features, dtype=vector_dtype(dev), device=dev)
+        hashed_tf(out, [HashInput(None, TU.TokenBatch.from_lists(lists), None)], hp.num_features, True, hp.binary)
         return self._vec(out)
 
 

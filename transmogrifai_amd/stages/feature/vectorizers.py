@@ -17,7 +17,7 @@ sparse term vector and scatters it by code. On a GPU dataset these run as device
 from __future__ import annotations
 
 from collections import Counter
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -175,9 +175,8 @@ def _text_counts(col: TextColumn, clean: bool) -> Counter:
     """Counts of (cleaned) non-null values: device bincount over codes, string work per vocab entry."""
     if len(col.vocab) == 0:
         return Counter()
-    codes = col.codes
-    valid = codes >= 0
-    cnt = torch.bincount(codes[valid].long(), minlength=len(col.vocab)).cpu().numpy()
+    from ...ops.text import code_counts
+    cnt = code_counts([col.codes], [len(col.vocab)])[0][:-1]
     out: Counter = Counter()
     for s, c in zip(col.vocab, cnt):
         if c:
@@ -345,53 +344,34 @@ def hash_metadata(tfs, hp: HashingParams):
     return [col_meta(t) for t in tfs for _ in range(hp.num_features)]
 
 
-def _terms_csr(token_lists: Sequence[List[str]], prefix: Optional[int], hp: HashingParams):
-    """Sparse hashed TF for each token list -> (indptr, indices, values)."""
-    flat = []
-    lens = []
-    for toks in token_lists:
-        ts = [f"{prefix}_{t}" for t in toks] if prefix is not None else list(toks)
-        flat.extend(ts)
-        lens.append(len(ts))
-    idx = TU.hash_terms(flat, hp.num_features) if flat else np.zeros(0, np.int32)
-    indptr = np.zeros(len(lens) + 1, np.int64)
-    np.cumsum(lens, out=indptr[1:])
-    vals = np.ones(idx.size)
-    # collapse duplicates per list
-    ip2, ix2, vx2 = [0], [], []
-    for i in range(len(lens)):
-        seg = idx[indptr[i]:indptr[i + 1]]
-        if seg.size:
-            u, c = np.unique(seg, return_counts=True)
-            ix2.append(u)
-            vx2.append(np.ones_like(c, dtype=np.float64) if hp.binary else c.astype(np.float64))
-            ip2.append(ip2[-1] + u.size)
+def hash_inputs(cols, tfs, hp: HashingParams, tok_params: Optional[Tuple[bool, int]]):
+    """Per feature: dictionary codes + the tokens of each distinct value (native tokenizer) + the
+    feature-name prefix. ``tok_params`` = (to_lowercase, min_token_length), or ``None`` when the values
+    are already terms (lists / sets / maps)."""
+    from ...ops.text import HashInput
+    out = []
+    for c, t in zip(cols, tfs):
+        prefix = int(TU.hash_terms([t.name], hp.num_features)[0]) if hp.prepend_feature_name else None
+        if isinstance(c, TextColumn):
+            tb = TU.tokenize_batch(c.vocab, *tok_params) if tok_params is not None else \
+                TU.TokenBatch.from_lists([[s] for s in c.vocab])
+            out.append(HashInput(c.codes, tb, prefix))
         else:
-            ip2.append(ip2[-1])
-    return (np.asarray(ip2, np.int64), np.concatenate(ix2) if ix2 else np.zeros(0, np.int32),
-            np.concatenate(vx2) if vx2 else np.zeros(0))
+            lists = [[str(x) for x in v] if v else [] for v in c.to_list()]
+            out.append(HashInput(None, TU.TokenBatch.from_lists(lists), prefix))
+    return out
 
 
-def hash_text_columns(cols, tfs, hp: HashingParams, tokenize_fn, dtype) -> torch.Tensor:
-    """Hash each text column's tokens (per distinct value) into a shared or per-feature block."""
+def hash_text_columns(cols, tfs, hp: HashingParams, tok_params, dtype, inputs=None) -> torch.Tensor:
+    """Hashed TF block of the columns, shared or per-feature hash space (HIP ``hash_tf_rows`` on device)."""
+    from ...ops.text import hashed_tf
     dev = _device(cols)
     n = len(cols[0]) if cols else 0
     shared = hp.shared()
     width = hp.num_features if shared else hp.num_features * len(cols)
-    out = torch.zeros(n, width, dtype=dtype, device=dev)
-    for k, (c, t) in enumerate(zip(cols, tfs)):
-        prefix = int(TU.hash_terms([t.name], hp.num_features)[0]) if hp.prepend_feature_name else None
-        if isinstance(c, TextColumn):
-            toks = [tokenize_fn(s) for s in c.vocab]
-            indptr, idx, vals = _terms_csr(toks, prefix, hp)
-            base = 0 if shared else k * hp.num_features
-            V.csr_rows_scatter_add(out, c.codes, indptr, idx.astype(np.int64) + base, vals)
-        else:
-            lists = [list(v) if v else [] for v in c.to_list()]
-            indptr, idx, vals = _terms_csr([[str(x) for x in l] for l in lists], prefix, hp)
-            base = 0 if shared else k * hp.num_features
-            codes = torch.arange(n, dtype=torch.int32, device=dev)
-            V.csr_rows_scatter_add(out, codes, indptr, idx.astype(np.int64) + base, vals)
+    out = torch.empty(n, width, dtype=dtype, device=dev)
+    hashed_tf(out, inputs if inputs is not None else hash_inputs(cols, tfs, hp, tok_params), hp.num_features,
+              shared, hp.binary)
     return out
 
 
@@ -452,27 +432,31 @@ class SmartTextVectorizerModel(VectorizerMixin, SequenceTransformer):
         self.min_token_length = min_token_length
         self.to_lowercase = to_lowercase
 
-    def _tok(self, s):
-        return TU.tokenize(s, self.to_lowercase, self.min_token_length)
-
     def transform_columns(self, *cols, ds=None):
         dtype = vector_dtype(_device(cols))
         tfs = self.get_transient_features() if self._inputs else [None] * len(cols)
         piv = [i for i, m in enumerate(self.methods) if m == "pivot"]
         hsh = [i for i, m in enumerate(self.methods) if m == "hash"]
         ign = [i for i, m in enumerate(self.methods) if m == "ignore"]
+        rest = hsh + ign
+        # one native tokenizer pass per hashed / ignored column, over its distinct values
+        toks = {i: TU.tokenize_batch(cols[i].vocab, self.to_lowercase, self.min_token_length) for i in rest}
         blocks = []
         if piv:
             blocks.append(pivot_columns([cols[i] for i in piv], [self.top_values[i] for i in piv], self.clean_text,
                                         self.track_nulls, dtype))
         if hsh:
-            blocks.append(hash_text_columns([cols[i] for i in hsh], [tfs[i] for i in hsh], self.hashing, self._tok,
-                                            dtype))
-        rest = hsh + ign
+            from ...ops.text import HashInput
+            hp = self.hashing
+            ins = [HashInput(cols[i].codes, toks[i], int(TU.hash_terms([tfs[i].name], hp.num_features)[0])
+                             if hp.prepend_feature_name else None) for i in hsh]
+            blocks.append(hash_text_columns([cols[i] for i in hsh], None, hp, None, dtype, inputs=ins))
         if rest and self.track_text_len:
-            blocks.append(torch.stack([_token_len(cols[i], self._tok, dtype) for i in rest], 1))
+            blocks.append(torch.stack([_vocab_lut(cols[i], toks[i].char_lengths().astype(np.float64), 0.0, dtype)
+                                       for i in rest], 1))
         if rest and self.track_nulls:
-            blocks.append(torch.stack([_token_null(cols[i], self._tok, dtype) for i in rest], 1))
+            blocks.append(torch.stack([_vocab_lut(cols[i], (toks[i].counts() == 0).astype(np.float64), 1.0, dtype)
+                                       for i in rest], 1))
         dev = _device(cols)
         out = torch.cat(blocks, 1) if blocks else torch.zeros(len(cols[0]), 0, dtype=dtype, device=dev)
         return self._vec(out)
@@ -492,16 +476,9 @@ class SmartTextVectorizerModel(VectorizerMixin, SequenceTransformer):
         self.to_lowercase = a.get("toLowercase", True)
 
 
-def _token_null(c: TextColumn, tok, dtype):
-    empty = np.array([len(tok(s)) == 0 for s in c.vocab] + [True])
-    lut = torch.as_tensor(empty.astype(np.float64), dtype=dtype, device=c.codes.device)
-    idx = torch.where(c.codes >= 0, c.codes.long(), torch.full_like(c.codes.long(), len(c.vocab)))
-    return lut[idx]
-
-
-def _token_len(c: TextColumn, tok, dtype):
-    lens = np.array([sum(len(t) for t in tok(s)) for s in c.vocab] + [0], np.float64)
-    lut = torch.as_tensor(lens, dtype=dtype, device=c.codes.device)
+def _vocab_lut(c: TextColumn, per_value: np.ndarray, null_value: float, dtype) -> torch.Tensor:
+    """Row values from a per-distinct-value table (null rows take ``null_value``)."""
+    lut = torch.as_tensor(np.append(per_value, null_value), dtype=dtype, device=c.codes.device)
     idx = torch.where(c.codes >= 0, c.codes.long(), torch.full_like(c.codes.long(), len(c.vocab)))
     return lut[idx]
 
@@ -577,14 +554,13 @@ class DateToUnitCircleTransformer(VectorizerMixin, SequenceTransformer):
             {t.name: FeatureHistory(tuple(t.origin_features), tuple(t.stages)) for t in tfs})
         dev = _device(cols)
         dtype = vector_dtype(dev)
-        parts = []
-        for c in cols:
-            val, size = period_values(c.values.to(torch.int64), tp)
-            rad = 2 * np.pi * val.to(torch.float64) / size
-            x = torch.where(c.valid, torch.cos(rad), torch.zeros_like(rad))
-            y = torch.where(c.valid, torch.sin(rad), torch.zeros_like(rad))
-            parts += [x, y]
-        return self._vec(torch.stack(parts, 1).to(dtype) if parts else torch.zeros(0, 0))
+        from ...ops.text import date_unit_circle_into
+        if not cols:
+            return self._vec(torch.zeros(0, 0))
+        out = torch.empty(len(cols[0]), 2 * len(cols), dtype=dtype, device=dev)
+        for k, c in enumerate(cols):     # HIP date_unit_circle_kernel on device
+            date_unit_circle_into(out[:, 2 * k:2 * k + 2], c.values, c.valid, tp)
+        return self._vec(out)
 
 
 @register_stage

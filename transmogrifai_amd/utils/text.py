@@ -83,6 +83,92 @@ def tokenize(text: Optional[str], to_lowercase: bool = True, min_token_length: i
     return [t for t in analyze(s, stopwords) if len(t) >= min_token_length]
 
 
+class TokenBatch:
+    """Flat token list of a batch of strings: token ``t`` of string ``i`` is
+    ``data[tok_offs[row_ptr[i] + t] : tok_offs[row_ptr[i] + t + 1]]`` (UTF-8)."""
+
+    __slots__ = ("data", "tok_offs", "row_ptr")
+
+    def __init__(self, data: np.ndarray, tok_offs: np.ndarray, row_ptr: np.ndarray):
+        self.data, self.tok_offs, self.row_ptr = data, tok_offs, row_ptr
+
+    def __len__(self):
+        return self.row_ptr.size - 1
+
+    @property
+    def n_tokens(self) -> int:
+        return self.tok_offs.size - 1
+
+    def counts(self) -> np.ndarray:
+        return np.diff(self.row_ptr)
+
+    def char_lengths(self) -> np.ndarray:
+        """Per-string total token length in characters (UTF-8 continuation bytes excluded)."""
+        lead = (self.data & 0xC0) != 0x80
+        cum = np.zeros(self.data.size + 1, np.int64)
+        np.cumsum(lead, out=cum[1:])
+        tok_chars = cum[self.tok_offs[1:]] - cum[self.tok_offs[:-1]]
+        tc = np.zeros(tok_chars.size + 1, np.int64)
+        np.cumsum(tok_chars, out=tc[1:])
+        return tc[self.row_ptr[1:]] - tc[self.row_ptr[:-1]]
+
+    def lists(self) -> List[List[str]]:
+        b = self.data.tobytes()
+        o, r = self.tok_offs, self.row_ptr
+        return [[b[o[t]:o[t + 1]].decode("utf-8") for t in range(r[i], r[i + 1])] for i in range(len(self))]
+
+    @staticmethod
+    def from_lists(lists: Sequence[Sequence[str]]) -> "TokenBatch":
+        enc = [t.encode("utf-8") for l in lists for t in l]
+        lens = np.fromiter((len(e) for e in enc), dtype=np.int64, count=len(enc))
+        offs = np.zeros(len(enc) + 1, np.int64)
+        np.cumsum(lens, out=offs[1:])
+        rp = np.zeros(len(lists) + 1, np.int64)
+        np.cumsum([len(l) for l in lists], out=rp[1:])
+        return TokenBatch(np.frombuffer(b"".join(enc), dtype=np.uint8).copy(), offs, rp)
+
+
+def _encode_batch(strings: Sequence[Optional[str]]):
+    enc = [s.encode("utf-8") if s else b"" for s in strings]
+    offs = np.zeros(len(enc) + 1, np.int64)
+    np.cumsum(np.fromiter((len(e) for e in enc), dtype=np.int64, count=len(enc)), out=offs[1:])
+    return np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8), offs
+
+
+def tokenize_batch(strings: Sequence[Optional[str]], to_lowercase: bool = True, min_token_length: int = 1,
+                   stopwords=ENGLISH_STOPWORDS) -> TokenBatch:
+    """:func:`tokenize` of every string at once through the native multithreaded tokenizer
+    (``ops/csrc/host/tokenizer.cpp``). Strings the native tables flag (context-dependent lowercase,
+    non-BMP code points) and custom stop-word sets go through :func:`tokenize`, so the result always
+    equals ``[tokenize(s, ...) for s in strings]``."""
+    from ..ops import _native as N
+    n = len(strings)
+    if stopwords is not ENGLISH_STOPWORDS and len(stopwords) > 0:
+        return TokenBatch.from_lists([tokenize(s, to_lowercase, min_token_length, stopwords) for s in strings])
+    use_stop = 1 if stopwords is ENGLISH_STOPWORDS else 0
+    buf, offs = _encode_batch(strings)
+    lib = N.host()
+    h = lib.tmog_tok_run(buf.ctypes.data, offs.ctypes.data, n, int(to_lowercase), int(min_token_length), use_stop)
+    try:
+        nt, nb = np.zeros(1, np.int64), np.zeros(1, np.int64)
+        lib.tmog_tok_sizes(h, nt.ctypes.data, nb.ctypes.data)
+        data = np.empty(max(int(nb[0]), 1), np.uint8)
+        tok_offs = np.empty(int(nt[0]) + 1, np.int64)
+        row_ptr = np.empty(n + 1, np.int64)
+        fb = np.zeros(max(n, 1), np.uint8)
+        lib.tmog_tok_copy(h, data.ctypes.data, tok_offs.ctypes.data, row_ptr.ctypes.data, fb.ctypes.data)
+    finally:
+        lib.tmog_tok_free(h)
+    tb = TokenBatch(data[:int(nb[0])], tok_offs, row_ptr)
+    bad = np.flatnonzero(fb[:n])
+    if bad.size:
+        lists = tb.lists()
+        for i in bad:
+            lists[i] = tokenize(strings[i], to_lowercase, min_token_length, stopwords)
+        tb = TokenBatch.from_lists(lists)
+    return tb
+
+
 def strip_html(text: str) -> str:
     return re.sub(r"<[^>]*>", " ", text)
 
