@@ -34,13 +34,26 @@ sys.path.insert(0, ROOT)
 
 METRIC = "end-to-end AutoML wall-clock + hold-out AuPR, 10M-row binary-class tabular"
 
+# BASELINE.json configs: name -> (metric, default rows, selector kind, hold-out metric key)
+CONFIGS = {
+    "binary-10m": (METRIC, 10_000_000, "binary", "AuPR"),
+    "lr-rf-1m": ("end-to-end AutoML wall-clock + hold-out AuPR, 1M-row binary-class, LR + RandomForest selector",
+                 1_000_000, "binary", "AuPR"),
+    "multiclass-text": ("end-to-end AutoML wall-clock + hold-out error, multi-class tabular with text + categorical "
+                        "columns (SmartText hashing-TF + one-hot)", 1_000_000, "multi", "Error"),
+    "regression-100m": ("end-to-end AutoML wall-clock + hold-out RMSE, 100M-row regression, default regression "
+                        "selector grid", 100_000_000, "regression", "RootMeanSquaredError"),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--config", default="binary-10m", choices=sorted(CONFIGS),
+                    help="BASELINE.json config: the headline (binary-10m) or one of the secondary configs")
+    ap.add_argument("--rows", type=int, default=None, help="rows (default: the config's)")
     ap.add_argument("--real", type=int, default=170)
     ap.add_argument("--int", dest="ints", type=int, default=15)
     ap.add_argument("--pick", type=int, default=15)
@@ -52,27 +65,35 @@ def parse():
                     help="multi-GPU table layout: row shards with all-reduced fit statistics (data parallel), "
                          "or the whole table on every rank")
     ap.add_argument("--verbose", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.config == "lr-rf-1m" and a.models == "default":
+        a.models = "OpLogisticRegression,OpRandomForestClassifier"
+    if a.rows is None:
+        a.rows = CONFIGS[a.config][1]
+    return a
+
+
+def _selector_cls(args):
+    from transmogrifai_amd.selector import factories as F
+    return {"binary": F.BinaryClassificationModelSelector, "multi": F.MultiClassificationModelSelector,
+            "regression": F.RegressionModelSelector}[CONFIGS[args.config][2]]
 
 
 def _expected_configs(args) -> int:
     """Grid points the selector must evaluate (default binary grid: LR 8 + RF 18 + XGBoost 2)."""
-    from transmogrifai_amd.selector.factories import BinaryClassificationModelSelector
     types = None if args.models == "default" else args.models.split(",")
-    sel = BinaryClassificationModelSelector.with_cross_validation(num_folds=args.folds, model_types_to_use=types,
-                                                                  seed=42)
+    sel = _selector_cls(args).with_cross_validation(num_folds=args.folds, model_types_to_use=types, seed=42)
     return sum(len(grid) for _, grid in sel.models)
 
 
 def build_workflow(args, ds, label, preds):
     from transmogrifai_amd.dsl import transmogrify
     from transmogrifai_amd.readers.base import InMemoryReader
-    from transmogrifai_amd.selector.factories import BinaryClassificationModelSelector
     from transmogrifai_amd.workflow.workflow import OpWorkflow
     vec = transmogrify(preds)
     checked = label.sanity_check(vec, remove_bad_features=True)
     types = None if args.models == "default" else args.models.split(",")
-    pred = BinaryClassificationModelSelector.with_cross_validation(
+    pred = _selector_cls(args).with_cross_validation(
         num_folds=args.folds, model_types_to_use=types, seed=42).set_input(label, checked).get_output()
     wf = OpWorkflow().set_result_features(label, pred).set_reader(InMemoryReader(ds))
     return wf, pred
@@ -124,17 +145,27 @@ def main():
         from transmogrifai_amd.ops import _native
         _native.hip()   # fail loudly if the HIP kernels cannot be loaded
 
-    from transmogrifai_amd.testkit.synthetic import binary_table
+    from transmogrifai_amd.testkit import synthetic as SY
     from transmogrifai_amd import uid
+
+    def make_table():
+        if args.config == "multiclass-text":
+            return SY.multiclass_text_table(args.rows, seed=11, device=dev)
+        if args.config == "regression-100m":
+            return SY.regression_table(args.rows, seed=13, device=dev)
+        return SY.binary_table(args.rows, args.real, args.ints, args.pick, seed=7, device=dev)
 
     def sync():
         if use_gpu:
             torch.cuda.synchronize()
         D.barrier()
 
+    n_raw = [0]
+
     def one_run():
         uid.reset(0)
-        ds, label, preds = binary_table(args.rows, args.real, args.ints, args.pick, seed=7, device=dev)
+        ds, label, preds = make_table()
+        n_raw[0] = len(preds)
         if world > 1 and args.layout == "sharded":
             ds = ds.shard(D.rank(), world)      # N / world rows per GPU; global row ids kept
             if use_gpu:
@@ -147,7 +178,7 @@ def main():
         dt = time.perf_counter() - t0
         sel = model.get_origin_stage_of(pred)
         summ = sel.metadata.get("summary", {})
-        ho = (summ.get("holdoutEvaluation") or {}).get("AuPR", float("nan"))
+        ho = (summ.get("holdoutEvaluation") or {}).get(CONFIGS[args.config][3], float("nan"))
         # a learner that dies must not make the headline faster: every configured grid point must have
         # been evaluated and nothing may have failed
         n_eval = len(summ.get("validationResults") or [])
@@ -174,7 +205,7 @@ def main():
     per_step = total / max(args.steps, 1)
     if D.rank() == 0:
         out = {
-            "metric": METRIC,
+            "metric": CONFIGS[args.config][0],
             "value": per_step,
             "unit": "s per end-to-end AutoML train",
             "n_gpus": world if use_gpu else 0,
@@ -186,13 +217,15 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (device-generated, seeded), random-init models",
-            "holdout_aupr": auprs[-1],
+            ("holdout_aupr" if CONFIGS[args.config][3] == "AuPR" else
+             "holdout_" + CONFIGS[args.config][3].lower()): auprs[-1],
             "best_model": summ.get("bestModelType") if summ else None,
             "configs_evaluated": len(summ.get("validationResults") or []) if summ else 0,
             "peak_hbm_gb_per_gpu": round(peak / 1e9, 3),
-            "config": {"model": "BinaryClassificationModelSelector(" +
-                                ("LR,RF,XGB default grid" if args.models == "default" else args.models) + ")",
-                       "rows": args.rows, "raw_columns": args.real + args.ints + args.pick,
+            "config": {"name": args.config,
+                       "model": _selector_cls(args).__name__ + "(" +
+                                ("default grid" if args.models == "default" else args.models) + ")",
+                       "rows": args.rows, "raw_columns": n_raw[0],
                        "cv_folds": args.folds, "global_batch": args.rows, "seq_len": None,
                        "parallelism": (f"dp{world}" if args.layout == "sharded" else f"grid-shard{world}")
                        if world > 1 else "single"},

@@ -82,3 +82,119 @@ def binary_table(n_rows: int, n_real: int = 170, n_int: int = 15, n_pick: int = 
             continue
         preds.append(FeatureBuilder.of(c.ftype, name).as_predictor())
     return ds, label, preds
+
+
+def _topic_docs(n_docs: int, n_topics: int, n_words: int, seed: int) -> Tuple[List[str], "torch.Tensor"]:
+    """``n_docs`` distinct short documents, each written mostly from its topic's word slice."""
+    import numpy as np
+    r = np.random.default_rng(seed)
+    words = np.array([f"w{k:04d}" for k in range(n_words)] + ["the", "and", "of", "a", "to", "in"])
+    topic = r.integers(0, n_topics, n_docs)
+    lens = r.integers(3, 14, n_docs)
+    per = n_words // n_topics
+    docs = []
+    for d in range(n_docs):
+        on = r.random(lens[d]) < 0.55
+        w = np.where(on, topic[d] * per + r.integers(0, per, lens[d]), r.integers(0, len(words), lens[d]))
+        docs.append(" ".join(words[w]))
+    return docs, torch.as_tensor(topic)
+
+
+def multiclass_text_table(n_rows: int, n_classes: int = 6, n_real: int = 20, n_pick: int = 6, n_text: int = 2,
+                          n_docs: int = 200_000, n_cities: int = 300, seed: int = 11,
+                          device="cpu") -> Tuple[Dataset, object, List[object]]:
+    """BASELINE config 4 shape: multi-class label with numeric, categorical and text columns.
+
+    * ``n_real`` ``Real`` and ``n_pick`` ``PickList`` columns (device generated);
+    * one medium-cardinality ``Text`` column (``city``, ``n_cities`` values: SmartText pivots it);
+    * ``n_text`` free ``Text`` columns drawn from ``n_docs`` distinct topic documents (cardinality far above
+      SmartText's 1000: tokenized and murmur3-hashed); a row of class c picks a document of topic c with
+      probability 0.6, so the text carries label signal only through its words.
+    """
+    dev = torch.device(device)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    wg = torch.Generator(device="cpu")
+    wg.manual_seed(seed + 1)
+    cols: "OrderedDict[str, object]" = OrderedDict()
+    score = torch.zeros(n_rows, n_classes, device=dev)
+    wr = torch.randn(n_real, n_classes, generator=wg) * 0.5
+    for j in range(n_real):
+        x = torch.randn(n_rows, generator=g, device=dev)
+        if j < 8:
+            score += x[:, None] * wr[j].to(dev)[None, :]
+        valid = (torch.rand(n_rows, generator=g, device=dev) >= 0.1) if j % 5 == 0 else None
+        if valid is not None:
+            x = torch.where(valid, x, torch.zeros_like(x))
+        cols[f"real_{j:03d}"] = NumericColumn(T.Real, x.to(torch.float64) if dev.type == "cpu" else x, valid)
+    for j in range(n_pick):
+        nc = 12
+        codes = torch.randint(0, nc, (n_rows,), generator=g, device=dev, dtype=torch.int32)
+        if j < 2:
+            score += (torch.randn(nc, n_classes, generator=wg) * 0.6).to(dev)[codes.long()]
+        cols[f"cat_{j:03d}"] = TextColumn(T.PickList, codes, [f"k{j}_{k}" for k in range(nc)])
+    y = torch.argmax(score + torch.randn(n_rows, n_classes, generator=g, device=dev) * 1.5, dim=1)
+    p = torch.tensor([1.0 / (k + 1) ** 0.8 for k in range(n_cities)], device=dev)
+    city = torch.multinomial(p / p.sum(), n_rows, replacement=True, generator=g).to(torch.int32)
+    cols["city"] = TextColumn(T.Text, city, [f"City {k}" for k in range(n_cities)])
+    nd = min(n_docs, max(n_rows // 2, 1))
+    for t in range(n_text):
+        docs, topic = _topic_docs(nd, n_classes, 3000, seed + 10 + t)
+        topic = topic.to(dev)
+        order = torch.argsort(topic, stable=True)
+        counts = torch.bincount(topic, minlength=n_classes)
+        starts = torch.cumsum(counts, 0) - counts
+        pick_same = torch.rand(n_rows, generator=g, device=dev) < 0.6
+        r_same = starts[y] + (torch.rand(n_rows, generator=g, device=dev) * counts[y]).long().clamp(max=nd - 1)
+        r_any = torch.randint(0, nd, (n_rows,), generator=g, device=dev)
+        code = torch.where(pick_same, order[r_same.clamp(max=nd - 1)], r_any).to(torch.int32)
+        nul = torch.rand(n_rows, generator=g, device=dev) < 0.05
+        code = torch.where(nul, torch.full_like(code, -1), code)
+        cols[f"text_{t}"] = TextColumn(T.Text, code, docs)
+    cols["label"] = NumericColumn(T.RealNN, y.to(torch.float64 if dev.type == "cpu" else torch.float32), None)
+    ds = Dataset(cols, None, n_rows)
+    label = FeatureBuilder.RealNN("label").as_response()
+    preds = [FeatureBuilder.of(c.ftype, name).as_predictor() for name, c in cols.items() if name != "label"]
+    return ds, label, preds
+
+
+def regression_table(n_rows: int, n_real: int = 30, n_int: int = 5, n_pick: int = 5, seed: int = 13,
+                     device="cpu") -> Tuple[Dataset, object, List[object]]:
+    """BASELINE config 5 shape: a real-valued label with a linear + nonlinear signal over numeric and
+    categorical columns (device generated, chunk free)."""
+    dev = torch.device(device)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    wg = torch.Generator(device="cpu")
+    wg.manual_seed(seed + 1)
+    cols: "OrderedDict[str, object]" = OrderedDict()
+    w = torch.randn(n_real, generator=wg)
+    y = torch.zeros(n_rows, device=dev)
+    xs = []
+    for j in range(n_real):
+        x = torch.randn(n_rows, generator=g, device=dev)
+        if j < 12:
+            y += float(w[j]) * x
+        xs.append(x)
+        valid = (torch.rand(n_rows, generator=g, device=dev) >= 0.1) if j % 6 == 0 else None
+        if valid is not None:
+            x = torch.where(valid, x, torch.zeros_like(x))
+        cols[f"real_{j:03d}"] = NumericColumn(T.Real, x.to(torch.float64) if dev.type == "cpu" else x, valid)
+    if n_real >= 3:
+        y += 2.0 * torch.sin(xs[0] * xs[1]) + (xs[2] > 0.5).float() * 1.5
+    for j in range(n_int):
+        x = torch.poisson(torch.full((n_rows,), 2.0 + j, device=dev), generator=g).to(torch.int64)
+        if j == 0:
+            y += 0.3 * x.float()
+        cols[f"int_{j:03d}"] = NumericColumn(T.Integral, x, None)
+    for j in range(n_pick):
+        codes = torch.randint(0, 10, (n_rows,), generator=g, device=dev, dtype=torch.int32)
+        if j == 0:
+            y += (torch.randn(10, generator=wg) * 1.0).to(dev)[codes.long()]
+        cols[f"cat_{j:03d}"] = TextColumn(T.PickList, codes, [f"r{j}_{k}" for k in range(10)])
+    y += torch.randn(n_rows, generator=g, device=dev)
+    cols["label"] = NumericColumn(T.RealNN, y.to(torch.float64) if dev.type == "cpu" else y, None)
+    ds = Dataset(cols, None, n_rows)
+    label = FeatureBuilder.RealNN("label").as_response()
+    preds = [FeatureBuilder.of(c.ftype, name).as_predictor() for name, c in cols.items() if name != "label"]
+    return ds, label, preds
