@@ -13,7 +13,7 @@ Storage is chosen by the feature type's ``kind``:
 """
 from __future__ import annotations
 
-from typing import Any, List, Optional, Sequence
+from typing import Any, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -233,40 +233,132 @@ class TextColumn(Column):
 
 # ------------------------------------------------------------------------------------------- vector
 class VectorColumn(Column):
+    """Dense feature vectors ``[n, width]``.
+
+    A vector column is either one dense tensor or a *blocked view*: an ordered list of
+    ``(block [n, w_b], column index or None)`` parts whose concatenation is the logical matrix.
+    ``VectorsCombiner`` concatenates its inputs' blocks and the SanityChecker keep-mask selects columns
+    of them without copying the feature matrix; consumers that only need some rows
+    (the model selector's training sample, chunked scoring) call :meth:`take_rows`, which gathers
+    those rows of the selected columns straight from the blocks (HIP ``gather_rows_cols_kernel``).
+    ``values`` materialises the whole matrix on demand for every other consumer."""
     ftype = T.OPVector
 
-    def __init__(self, values: torch.Tensor, metadata: Optional[OpVectorMetadata] = None):
-        assert values.dim() == 2, values.shape
-        self.values = values
+    def __init__(self, values: Optional[torch.Tensor] = None, metadata: Optional[OpVectorMetadata] = None,
+                 blocks: Optional[Sequence[Tuple[torch.Tensor, Optional[torch.Tensor]]]] = None):
         self.metadata = metadata
+        if blocks is None:
+            assert values is not None and values.dim() == 2, None if values is None else values.shape
+            self._values = values
+            self._blocks = None
+            self._n, self._w = int(values.shape[0]), int(values.shape[1])
+            return
+        parts = []
+        for t, idx in blocks:
+            assert t.dim() == 2
+            w = int(t.shape[1]) if idx is None else int(idx.numel())
+            if w > 0:
+                parts.append((t, idx))
+        if not parts:
+            t0 = blocks[0][0] if blocks else torch.zeros(0, 0)
+            parts = [(t0[:, :0], None)]
+        if len({int(t.shape[0]) for t, _ in parts}) != 1:
+            raise ValueError("vector blocks differ in row count")
+        self._values = parts[0][0] if len(parts) == 1 and parts[0][1] is None else None
+        self._blocks = None if self._values is not None else parts
+        self._n = int(parts[0][0].shape[0])
+        self._w = sum(int(t.shape[1]) if i is None else int(i.numel()) for t, i in parts)
+
+    @property
+    def values(self) -> torch.Tensor:
+        if self._values is not None:
+            return self._values
+        return self.take_rows(None)
+
+    @values.setter
+    def values(self, v: torch.Tensor):
+        assert v.dim() == 2
+        self._values, self._blocks = v, None
+        self._n, self._w = int(v.shape[0]), int(v.shape[1])
+
+    @property
+    def is_blocked(self) -> bool:
+        return self._blocks is not None
+
+    @property
+    def blocks(self) -> List[Tuple[torch.Tensor, Optional[torch.Tensor]]]:
+        return list(self._blocks) if self._blocks is not None else [(self._values, None)]
+
+    @property
+    def dtype(self):
+        return self.blocks[0][0].dtype
 
     def __len__(self):
-        return int(self.values.shape[0])
+        return self._n
 
     @property
     def width(self) -> int:
-        return int(self.values.shape[1])
+        return self._w
 
     @property
     def device(self):
-        return self.values.device
+        return self.blocks[0][0].device
+
+    def take_rows(self, idx) -> torch.Tensor:
+        """Dense ``[len(idx), width]`` rows (all rows when ``idx`` is None) of the logical matrix."""
+        if self._values is not None:
+            return self._values if idx is None else self._values.index_select(
+                0, _as_index(idx, self._values.device))
+        from ..ops.vector import gather_rows_cols
+        return gather_rows_cols(self._blocks, None if idx is None else _as_index(idx, self.device), self._n)
+
+    def select_columns(self, idx, metadata: Optional[OpVectorMetadata] = None) -> "VectorColumn":
+        """Columns ``idx`` of the logical matrix as a blocked view (no copy)."""
+        dev = self.device
+        idx = torch.as_tensor(idx, dtype=torch.long).cpu()
+        parts, off = [], 0
+        bounds = []
+        for t, ci in self.blocks:
+            w = int(t.shape[1]) if ci is None else int(ci.numel())
+            bounds.append((off, off + w, t, ci))
+            off += w
+        if idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= off):
+            raise IndexError("column index out of range of the vector")
+        # consecutive output columns that fall in the same block become one part
+        k = 0
+        ids = idx.tolist()
+        while k < len(ids):
+            j = next(b for b in range(len(bounds)) if bounds[b][0] <= ids[k] < bounds[b][1])
+            lo, hi, t, ci = bounds[j]
+            m = k
+            while m < len(ids) and lo <= ids[m] < hi:
+                m += 1
+            local = torch.as_tensor(ids[k:m], dtype=torch.long) - lo
+            src = local if ci is None else ci.cpu()[local]
+            whole = ci is None and src.numel() == t.shape[1] and bool((src == torch.arange(t.shape[1])).all())
+            parts.append((t, None if whole else src.to(dev)))
+            k = m
+        if not parts:
+            parts = [(self.blocks[0][0][:, :0], None)]
+        return VectorColumn(metadata=metadata if metadata is not None else self.metadata, blocks=parts)
 
     def take(self, idx):
-        return VectorColumn(self.values[_as_index(idx, self.values.device)], self.metadata)
+        return VectorColumn(self.take_rows(idx), self.metadata)
 
     def to(self, device):
         return VectorColumn(self.values.to(device), self.metadata)
 
     def row(self, i):
-        return self.values[i].detach().cpu().numpy().astype(np.float64)
+        return self.take_rows(torch.tensor([i]))[0].detach().cpu().numpy().astype(np.float64)
 
     def to_list(self):
         a = self.values.detach().cpu().numpy().astype(np.float64)
         return [a[i] for i in range(a.shape[0])]
 
     def null_mask(self):
-        return torch.zeros(len(self), dtype=torch.bool, device=self.values.device) if self.width > 0 \
-            else torch.ones(len(self), dtype=torch.bool, device=self.values.device)
+        dev = self.device
+        return torch.zeros(len(self), dtype=torch.bool, device=dev) if self.width > 0 \
+            else torch.ones(len(self), dtype=torch.bool, device=dev)
 
     @staticmethod
     def from_values(values, device="cpu", metadata=None):

@@ -149,6 +149,25 @@ def probability_outputs(raw: torch.Tensor, binary_margin: bool = True, threshold
 
 
 # ------------------------------------------------------------------------------------------ stages
+PREDICT_CHUNK_ROWS = 2_000_000
+
+
+def predict_chunked(learner, state, vec, chunk: int = PREDICT_CHUNK_ROWS):
+    """``learner.predict`` over a (possibly blocked) vector column in row chunks, so scoring never
+    materialises the whole feature matrix (the blocked view is gathered ``chunk`` rows at a time)."""
+    n = len(vec)
+    if not getattr(vec, "is_blocked", False) and n <= chunk:
+        return learner.predict(state, vec.values)
+    outs = []
+    for a in range(0, max(n, 1), chunk):
+        b = min(n, a + chunk)
+        rows = torch.arange(a, b, device=vec.device)
+        outs.append(learner.predict(state, vec.take_rows(rows)))
+    if len(outs) == 1:
+        return outs[0]
+    return tuple(torch.cat([o[i] for o in outs], 0) for i in range(3))
+
+
 @register_stage
 class OpPredictorModel(BinaryTransformer):
     """A fitted learner as a pipeline stage (label, features) -> Prediction."""
@@ -167,8 +186,7 @@ class OpPredictorModel(BinaryTransformer):
         return learner_class(self.learner_name)(**self.learner_params)
 
     def transform_columns(self, *cols, ds=None):
-        X = cols[1].values
-        pred, raw, prob = self.learner.predict(self.state, X)
+        pred, raw, prob = predict_chunked(self.learner, self.state, cols[1])
         return PredictionColumn(pred.to(torch.float64), raw.to(torch.float64), prob.to(torch.float64))
 
     def transform_row(self, *values):

@@ -59,9 +59,42 @@ __global__ void __launch_bounds__(256) onehot_pivot_kernel(const int32_t* const*
   if (slot >= 0) out[r * W + off[c] + slot] = 1.f;
 }
 
+// Row x column gather from a blocked feature matrix (the SanityChecker keep-mask and
+// the VectorsCombiner concatenation applied lazily): out[r, j] = col_base[j][row(r) * col_ld[j]] with
+// row(r) = rows ? rows[r] : r. A workgroup covers 64 output columns x 32 rows; each lane keeps its
+// column's base / stride in registers and walks 8 rows, so one wave reads 64 adjacent source words of
+// a row (same block) and writes 256 B of the output row.
+constexpr int kGatherRows = 32;
+
+__global__ void __launch_bounds__(256) gather_rows_cols_kernel(const float* const* __restrict__ col_base,
+                                                               const int64_t* __restrict__ col_ld,
+                                                               const int64_t* __restrict__ rows, int64_t m, int k,
+                                                               float* __restrict__ out) {
+  const int j = blockIdx.y * 64 + (threadIdx.x & 63);
+  if (j >= k) return;
+  const float* base = col_base[j];
+  const int64_t ld = col_ld[j];
+  const int64_t r0 = (int64_t)blockIdx.x * kGatherRows + (threadIdx.x >> 6);
+  for (int rr = 0; rr < kGatherRows; rr += 4) {
+    const int64_t r = r0 + rr;
+    if (r >= m) break;
+    const int64_t src = rows ? rows[r] : r;
+    out[r * k + j] = base[src * ld];
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int tmog_hip_gather_rows_cols(const void* col_base, const int64_t* col_ld, const int64_t* rows, int64_t m, int k,
+                              float* out, hipStream_t stream) {
+  if (m == 0 || k == 0) return 0;
+  dim3 grid((unsigned)((m + kGatherRows - 1) / kGatherRows), (unsigned)((k + 63) / 64));
+  hipLaunchKernelGGL(gather_rows_cols_kernel, grid, dim3(256), 0, stream, (const float* const*)col_base, col_ld, rows,
+                     m, k, out);
+  return (int)hipGetLastError();
+}
 
 int tmog_hip_onehot_pivot(const void* codes, const void* luts, const int32_t* lut_n, const int64_t* off, int n_cols,
                           int64_t n, float* out, int64_t W, hipStream_t stream) {

@@ -86,6 +86,38 @@ def column_modes(cols: Sequence[NumericColumn]) -> List[float]:
     return out
 
 
+def gather_rows_cols(blocks, rows, n: int) -> torch.Tensor:
+    """Dense ``[len(rows), width]`` gather of the selected rows (all ``n`` when ``rows`` is None) from a
+    blocked vector (list of ``(block, column index or None)``). fp32 device blocks use the HIP
+    ``gather_rows_cols_kernel`` (one pass, no per-block temporaries); otherwise torch index ops."""
+    dev = blocks[0][0].device
+    dtype = blocks[0][0].dtype
+    widths = [int(t.shape[1]) if ci is None else int(ci.numel()) for t, ci in blocks]
+    k = sum(widths)
+    m = n if rows is None else int(rows.numel())
+    if dev.type == "cuda" and all(t.dtype == torch.float32 and t.stride(1) == 1 for t, _ in blocks):
+        out = torch.empty(m, k, dtype=torch.float32, device=dev)
+        if m == 0 or k == 0:
+            return out
+        base, ld = [], []
+        for (t, ci), w in zip(blocks, widths):
+            cols = np.arange(w, dtype=np.int64) if ci is None else ci.cpu().numpy().astype(np.int64)
+            base.append(t.data_ptr() + 4 * cols)
+            ld.append(np.full(w, t.stride(0), np.int64))
+        pk = Pack(dev)
+        i_b, i_l = pk.add(np.concatenate(base)), pk.add(np.concatenate(ld))
+        d = pk.ship()
+        r = None if rows is None else rows.to(device=dev, dtype=torch.int64).contiguous()
+        N.check(N.hip().tmog_hip_gather_rows_cols(N.ptr(d[i_b]), N.ptr(d[i_l]), N.ptr(r), m, k, N.ptr(out),
+                                                  N.stream(dev)), "gather_rows_cols")
+        return out
+    parts = []
+    for t, ci in blocks:
+        x = t if rows is None else t.index_select(0, rows.to(t.device))
+        parts.append(x if ci is None else x.index_select(1, ci.to(t.device)))
+    return torch.cat([p.to(dtype) for p in parts], 1) if parts else torch.zeros(m, 0, dtype=dtype, device=dev)
+
+
 def fill_and_track(cols: Sequence[NumericColumn], fills: Sequence[float], track_nulls: bool,
                    dtype: torch.dtype) -> torch.Tensor:
     """``[N, F]`` (or ``[N, 2F]`` interleaved with null flags) filled value block."""

@@ -46,9 +46,9 @@ class SelectedModel(OpPredictorModel):
         hold-out is scored locally and the (label, prediction) rows are all-gathered for the metrics
         (SURVEY.md §2.7 C12)."""
         from ..parallel import dp
+        from ..models.base import predict_chunked
         lab = ds[self._inputs[0].name].values.to(torch.float64)
-        vec = ds[self._inputs[1].name].values
-        pred, raw, prob = self.learner.predict(self.state, vec)
+        pred, raw, prob = predict_chunked(self.learner, self.state, ds[self._inputs[1].name])
         lab, pred, raw, prob = dp.rows_opt(lab, pred, raw, prob)
         res = {}
         for ev in self.evaluators:
@@ -98,9 +98,9 @@ class ModelSelector(BinaryEstimator):
 
     def fit_columns(self, label_col, vec_col, ds=None):
         from ..parallel import dp
-        X = vec_col.values
-        y = label_col.values.to(X.dtype)
-        row_ids = ds.row_ids.to(X.device) if ds is not None else torch.arange(X.shape[0], device=X.device)
+        dev = vec_col.device
+        y = label_col.values.to(vec_col.dtype)
+        row_ids = ds.row_ids.to(dev) if ds is not None else torch.arange(len(vec_col), device=dev)
         t0 = time.time()
         split_summary = None
         if self.splitter is not None:
@@ -108,24 +108,25 @@ class ModelSelector(BinaryEstimator):
                 split_summary = self._split_summary
             else:
                 split_summary = self.splitter.pre_validation_prepare(dp.rows(y))
+        # only the rows some CV fold or the refit may train on (the splitter's maxTrainingSample cap) are
+        # materialised from the (blocked) feature vector; folds are functions of the global row id
+        X, y, row_ids = self._gather_candidates(vec_col, y, row_ids)
         if dp.active():
-            X, y, row_ids = self._gather_candidates(X, y, row_ids)
             with dp.local_only():
                 return self._fit(X, y, row_ids, split_summary, t0)
         return self._fit(X, y, row_ids, split_summary, t0)
 
-    def _gather_candidates(self, X, y, row_ids):
+    def _gather_candidates(self, vec_col, y, row_ids):
         """Every rank's rows that some CV fold or the refit may train on, gathered to all ranks."""
         from ..parallel import dp
         if self.splitter is None:
-            keep = torch.ones(row_ids.shape[0], dtype=torch.bool, device=row_ids.device)
-        else:
-            n_folds = getattr(self.validator, "num_folds", 1)
-            keep = self.splitter.validation_prepare(row_ids, y, stream=5)
-            for k in range(n_folds):
-                keep |= self.splitter.validation_prepare(row_ids, y, stream=11 + k)
+            return dp.rows(vec_col.values), dp.rows(y), dp.rows(row_ids)
+        n_folds = getattr(self.validator, "num_folds", 1)
+        keep = self.splitter.validation_prepare(row_ids, y, stream=5)
+        for k in range(n_folds):
+            keep |= self.splitter.validation_prepare(row_ids, y, stream=11 + k)
         idx = torch.nonzero(keep).reshape(-1)
-        return dp.rows(X.index_select(0, idx).contiguous()), dp.rows(y.index_select(0, idx)), \
+        return dp.rows(vec_col.take_rows(idx).contiguous()), dp.rows(y.index_select(0, idx)), \
             dp.rows(row_ids.index_select(0, idx))
 
     def _fit(self, X, y, row_ids, split_summary, t0):

@@ -702,15 +702,17 @@ class VectorsCombinerModel(VectorizerMixin, SequenceTransformer):
     def transform_columns(self, *cols, ds=None):
         dev = _device(cols)
         dtype = vector_dtype(dev)
-        vals = [c.values.to(dtype) for c in cols]
-        out = torch.cat(vals, 1) if vals else torch.zeros(0, 0)
         meta = self.metadata.get("vector_metadata")
         if meta is None:
             metas = [c.metadata for c in cols]
             if all(m is not None for m in metas):
                 meta = OpVectorMetadata.flatten(self.get_output_feature_name(), metas)
                 self.metadata["vector_metadata"] = meta
-        return VectorColumn(out, meta)
+        if not cols:
+            return VectorColumn(torch.zeros(0, 0), meta)
+        # concatenation as a blocked view of the inputs' own storage: no copy of the feature matrix
+        blocks = [(t if t.dtype == dtype else t.to(dtype), ci) for c in cols for t, ci in c.blocks]
+        return VectorColumn(metadata=meta, blocks=blocks)
 
 
 @register_stage

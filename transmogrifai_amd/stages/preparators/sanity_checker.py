@@ -109,9 +109,9 @@ class SanityCheckerModel(BinaryTransformer):
         vec: VectorColumn = cols[1]
         meta = self.metadata.get("vector_metadata")
         if not self.remove_bad_features:
-            return VectorColumn(vec.values, meta or vec.metadata)
-        idx = torch.as_tensor(self.indices_to_keep, dtype=torch.long, device=vec.values.device)
-        return VectorColumn(vec.values.index_select(1, idx), meta)
+            return VectorColumn(metadata=meta or vec.metadata, blocks=vec.blocks)
+        # keep-mask as a column view of the input blocks (K18): rows are gathered only by consumers
+        return vec.select_columns(self.indices_to_keep, meta)
 
     def transform_row(self, *values):
         v = np.asarray(values[1], np.float64)
@@ -173,16 +173,18 @@ class SanityChecker(BinaryEstimator):
     def fit_columns(self, label_col, vec_col, ds=None):
         from ...parallel import dp
         p = self.params
-        X = vec_col.values
         y = label_col.values
-        n_all = dp.count(X.shape[0])
+        dev = vec_col.device
+        n_all = dp.count(len(vec_col))
         frac = self.fraction(n_all)
         if frac <= 0.0 or n_all == 0:
             raise ValueError("Sample size cannot be zero")
         if frac < 1.0:
-            rid = ds.row_ids.to(X.device) if ds is not None else torch.arange(n_all, device=X.device)
-            keep = row_uniform(rid, int(p["sample_seed"]), 9) < frac
-            X, y = X[keep], y[keep]
+            rid = ds.row_ids.to(dev) if ds is not None else torch.arange(n_all, device=dev)
+            keep = torch.nonzero(row_uniform(rid, int(p["sample_seed"]), 9) < frac).reshape(-1)
+            X, y = vec_col.take_rows(keep), y.index_select(0, keep.to(y.device))
+        else:
+            X = vec_col.values
         meta: OpVectorMetadata = vec_col.metadata
         d = X.shape[1]
         if d == 0:

@@ -65,16 +65,32 @@ def fit_and_transform_layer(layer: Layer, train: Dataset, test: Optional[Dataset
 
 
 def fit_and_transform_dag(dag: Sequence[Layer], train: Dataset, test: Optional[Dataset] = None,
-                          timings: Optional[dict] = None):
+                          timings: Optional[dict] = None, keep: Optional[set] = None):
+    """Fit and apply the DAG layer by layer.
+
+    With ``keep`` given (the column names some later DAG part still reads), a column is dropped from
+    ``train`` / ``test`` right after the transform of its last consumer inside this DAG, so raw columns
+    and intermediate vector blocks do not outlive their use (the feature matrix of a 10M-row table is
+    tens of GB; only the final selector's input has to stay resident)."""
+    last = _last_uses(dag) if keep is not None else {}
     fitted_all = []
-    for layer in dag:
+    for li, layer in enumerate(dag):
         # a hold-out must be transformed before a HasTestEval model of the next layer evaluates on it
-        train, test, fitted = _fit_layer_with_eval(layer, train, test, timings)
+        train, test, fitted = _fit_layer_with_eval(layer, train, test, timings, li, last, keep)
         fitted_all.extend(fitted)
     return train, test, fitted_all
 
 
-def _fit_layer_with_eval(layer, train, test, timings):
+def _last_uses(dag: Sequence[Layer]) -> Dict[str, Tuple[int, int]]:
+    last: Dict[str, Tuple[int, int]] = {}
+    for li, layer in enumerate(dag):
+        for si, (st, _) in enumerate(layer):
+            for f in st.get_input_features():
+                last[f.name] = max(last.get(f.name, (li, si)), (li, si))
+    return last
+
+
+def _fit_layer_with_eval(layer, train, test, timings, li=0, last=None, keep=None):
     fitted = []
     for st, _ in layer:
         t0 = time.time()
@@ -87,11 +103,17 @@ def _fit_layer_with_eval(layer, train, test, timings):
             fitted.append(st)
         if timings is not None:
             timings[f"fit:{st.stage_name()}"] = time.time() - t0
-    for m in fitted:
+    for si, m in enumerate(fitted):
         t0 = time.time()
         train = m.transform(train)
         if test is not None and len(test) > 0:
             test = m.transform(test)
+        if keep is not None and last:
+            dead = [n for n, pos in last.items() if pos == (li, si) and n not in keep]
+            if dead:
+                train = train.drop(dead)
+                if test is not None:
+                    test = test.drop(dead)
         if timings is not None:
             timings[f"transform:{m.stage_name()}"] = time.time() - t0
     return train, test, fitted

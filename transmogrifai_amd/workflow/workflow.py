@@ -200,7 +200,9 @@ class OpWorkflow(OpWorkflowCore):
                 self.raw_feature_filter_results = results
                 self.set_blocklist(to_drop, results.rawFeatureDistributions)
                 self.blocklist_map_keys = {k: sorted(v) for k, v in drop_keys.items()}
-        fitted = self.fit_stages(raw, timings)
+        box = [raw]
+        del raw     # handed over: released once split into train / hold-out
+        fitted = self.fit_stages(box, timings)
         model = OpWorkflowModel(self.uid, self.parameters)
         model.stages = fitted
         model.result_features = list(self.result_features)
@@ -227,26 +229,34 @@ class OpWorkflow(OpWorkflowCore):
         hi = torch.nonzero(te).reshape(-1)
         return data.take(ti), data.take(hi)
 
-    def fit_stages(self, data: Dataset, timings: Dict[str, float]) -> List[OpPipelineStage]:
+    def fit_stages(self, data, timings: Dict[str, float]) -> List[OpPipelineStage]:
+        """Fit every stage on ``data`` (a Dataset, or a one-element list handing the dataset over so the
+        raw table can be released once it is split into train / hold-out)."""
         from ..parallel import dp
+        box = data if isinstance(data, list) else [data]
         # a row-sharded input (Dataset.shard, one shard per rank) fits data-parallel: every estimator
         # reduces its statistics over the process group (parallel/dp.py)
-        with dp.scope(getattr(data, "sharded", False)):
-            return self._fit_stages(data, timings)
+        with dp.scope(getattr(box[0], "sharded", False)):
+            return self._fit_stages(box, timings)
 
-    def _fit_stages(self, data: Dataset, timings: Dict[str, float]) -> List[OpPipelineStage]:
+    def _fit_stages(self, box: list, timings: Dict[str, float]) -> List[OpPipelineStage]:
         with _Timer(timings, "HoldoutSplit"):
-            train, test = self._holdout_split(data)
+            train, test = self._holdout_split(box.pop())
         dag = [[(st, d) for st, d in layer if st in self.stages] for layer in compute_dag(self.result_features)]
         dag = [l for l in dag if l]
         stage_t: Dict[str, float] = {}
         if not self.workflow_cv:
             with _Timer(timings, OpStep.FeatureEngineering):
-                _, _, fitted = fit_and_transform_dag(dag, train, test, stage_t)
+                _, _, fitted = fit_and_transform_dag(dag, train, test, stage_t, keep=set())
         else:
             ms, before, during, after = cut_dag(dag)
+            later = {f.name for part in (during, after) for layer in part for st, _ in layer
+                     for f in st.get_input_features()}
+            if ms is not None:
+                later |= {f.name for f in ms.get_input_features()}
             with _Timer(timings, OpStep.FeatureEngineering):
-                tr2, te2, fb = fit_and_transform_dag(before, train, test, stage_t)
+                tr2, te2, fb = fit_and_transform_dag(before, train, test, stage_t, keep=later)
+            del train, test
             fitted = list(fb)
             if ms is not None:
                 # OpWorkflow.scala:403-453: validate with the during-DAG refit inside every fold, then fit
@@ -255,7 +265,7 @@ class OpWorkflow(OpWorkflowCore):
                     ms.find_best_estimator(tr2, during)
                 rest = list(during) + [[(ms, 0)]] + list(after)
                 with _Timer(timings, OpStep.FeatureEngineering):
-                    _, _, fr = fit_and_transform_dag(rest, tr2, te2, stage_t)
+                    _, _, fr = fit_and_transform_dag(rest, tr2, te2, stage_t, keep=set())
                 fitted += fr
         timings["stages"] = stage_t
         return fitted
