@@ -1,0 +1,100 @@
+"""SanityChecker statistics kernels (stats_kernels.hip) vs fp64 torch: stable column variance on large-offset
+columns, the MFMA centred Gramian with the label block (correlations, contingency sums, counts), the
+batched Spearman rank transform, and the SanityChecker fit on device vs host."""
+import numpy as np
+import pytest
+import torch
+
+from transmogrifai_amd.ops import stats as ST
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n=300_001, d=203, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, d, generator=g, dtype=torch.float64)
+    X[:, 0] = X[:, 0] * 1e-3 + 1e6            # large offset, tiny spread
+    X[:, 1] = 5.0                              # constant
+    X[:, 2] = (torch.rand(n, generator=g) < 0.3).double()   # indicator
+    X[:, 3] = X[:, 4] * 0.5 + 0.1 * X[:, 3]    # correlated pair
+    return X.to(torch.float32)                 # the data as stored on the device
+
+
+def test_col_stats_stable_variance():
+    X = _data()
+    ref = X.to(torch.float64)
+    cs = ST.col_stats(X.cuda())
+    var_ref = ref.var(0, unbiased=True)
+    rel = ((cs["variance"].cpu() - var_ref).abs() / var_ref.clamp_min(1e-300))
+    assert float(rel[0]) < 1e-9, float(rel[0])            # offset 1e6, std 1e-3 (cancellation case)
+    assert float(rel[2:].max()) < 1e-9
+    assert float(cs["variance"][1]) == 0.0
+    torch.testing.assert_close(cs["mean"].cpu(), ref.mean(0), rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(cs["min"].cpu(), ref.min(0).values)
+    torch.testing.assert_close(cs["max"].cpu(), ref.max(0).values)
+
+
+@pytest.mark.parametrize("n_labels", [2, 7])
+def test_gram_corr_and_label_sums(n_labels):
+    X = _data(d=300)
+    g = torch.Generator().manual_seed(1)
+    y = torch.randint(0, n_labels, (X.shape[0],), generator=g).to(torch.float32)
+    ref = X.to(torch.float64)
+    mean = ref.mean(0)
+    C, lab, sums, cnt = ST.corr_and_label_sums(X.cuda(), y.cuda(), mean.cuda())
+    Xc = ref - mean
+    G = Xc.t() @ Xc
+    sd = G.diag().sqrt()
+    Cr = G / (sd[:, None] * sd[None, :])
+    m = torch.isfinite(Cr)
+    Cg = C.cpu()
+    assert float((Cg[m] - Cr[m]).abs().max()) < 1e-6
+    assert torch.isnan(Cg[1, 5]) and torch.isnan(Cg[5, 1])
+    oh = torch.nn.functional.one_hot(y.long(), n_labels).double()
+    torch.testing.assert_close(cnt.cpu(), oh.sum(0), rtol=0, atol=1e-6)
+    sref = oh.t() @ ref
+    rel = (sums.cpu() - sref).abs() / sref.abs().clamp_min(1.0)
+    assert float(rel.max()) < 1e-9
+    np.testing.assert_array_equal(lab.cpu().numpy(), np.arange(n_labels, dtype=np.float64))
+
+
+def test_gram_asymmetric_blocks():
+    # exact small-integer data: any row/col swap in the C/D write shows up exactly
+    g = torch.Generator().manual_seed(3)
+    X = torch.randint(-3, 4, (4096, 261), generator=g).to(torch.float32)
+    mean = torch.zeros(261, dtype=torch.float64)
+    G = ST.gram_centered(X.cuda(), mean.cuda()).cpu()
+    torch.testing.assert_close(G, X.double().t() @ X.double(), rtol=0, atol=0)
+
+
+def test_spearman_batched_ranks():
+    g = torch.Generator().manual_seed(4)
+    X = torch.randint(0, 20, (5000, 300), generator=g).to(torch.float64)     # many ties
+    R = ST._rank_columns(X.cuda()).cpu()
+    for j in (0, 17, 299):
+        v = X[:, j].numpy()
+        from scipy.stats import rankdata
+        np.testing.assert_allclose(R[:, j].numpy(), rankdata(v, method="average"))
+
+
+def test_sanity_checker_device_matches_host():
+    from transmogrifai_amd.testkit.synthetic import binary_table
+    from transmogrifai_amd.dsl import transmogrify
+    from transmogrifai_amd.workflow.workflow import OpWorkflow
+    from transmogrifai_amd.readers.base import InMemoryReader
+    from transmogrifai_amd import uid
+    outs = []
+    for dev in ("cpu", "cuda"):
+        uid.reset(0)
+        ds, label, preds = binary_table(50_000, n_real=12, n_int=3, n_pick=4, seed=3, device=dev)
+        vec = transmogrify(preds)
+        checked = label.sanity_check(vec, remove_bad_features=True)
+        model = OpWorkflow().set_result_features(checked).set_reader(InMemoryReader(ds)).train()
+        outs.append(model.get_origin_stage_of(checked).metadata["summary"])
+    h, d = outs
+    assert h["dropped"] == d["dropped"]
+    ch = np.array([np.nan if v is None else v for v in h["correlationsWLabel"]["values"]], float)
+    cd = np.array([np.nan if v is None else v for v in d["correlationsWLabel"]["values"]], float)
+    np.testing.assert_allclose(cd, ch, rtol=1e-5, atol=1e-6)
+    for a, b in zip(h["categoricalStats"], d["categoricalStats"]):
+        np.testing.assert_allclose(b["cramersV"], a["cramersV"], rtol=1e-6, atol=1e-9)

@@ -87,9 +87,8 @@ _HIP_SIGS = {
     "tmog_hip_vectorize_numeric": [P, P, P, I64, I32, P, P, P, P, I64, I32, P],
     "tmog_hip_onehot_pivot": [P, P, P, P, I32, I64, P, I64, P],
     "tmog_hip_quantize": [P, I64, I32, I64, P, P, P, I32, P, I64, P],
-    "tmog_hip_gram_f32": [P, I64, I32, I64, P, I32, P],
+    "tmog_hip_gram_aug": [P, I64, I32, I64, P, P, I32, P, P],
     "tmog_hip_logistic_grad": [P, P, P, I64, I32, P],
-    "tmog_hip_label_colsum": [P, P, I64, I32, I64, I32, P, P],
     "tmog_hip_gather_rows_cols": [P, P, P, I64, I32, P, P],
     "tmog_hip_hash_tokens": [P, P, I64, P, I32, I32, I32, I32, P, P],
     "tmog_hip_hash_tf_rows": [P, I32, I64, I32, I32, P, I64, I64, P],

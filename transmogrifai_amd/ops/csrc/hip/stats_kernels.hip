@@ -1,8 +1,19 @@
-// Column moments in one HBM pass (Spark Statistics.colStats used by SanityChecker,
-// MinVarianceFilter, RecordInsightsCorr). Row-major fp32 [n][ld]; each workgroup covers 64 columns
-// x a row chunk: 4 waves stride the rows, every lane owns one column (256 B coalesced per row),
-// accumulating sum / sum of squares in fp64 plus min / max / non-zeros. Partials go to
-// part[chunk][5][d]; a tiny second kernel folds the chunks into out[6][d].
+// SanityChecker statistics (SanityChecker.scala:407-470, OpStatistics.scala:71-97).
+//
+// * col_partials_kernel / col_fold_kernel -- Spark Statistics.colStats in one HBM pass with a
+//   numerically stable variance: each workgroup covers 64 columns x a row chunk (4 waves stride the
+//   rows, one lane per column, 256 B coalesced per row) and accumulates fp64 sums of (x - K) and
+//   (x - K)^2 around a per-chunk shift K (the chunk's first value of the column), giving the chunk's
+//   (count, mean, M2) without the sum-of-squares cancellation; chunks are folded with Chan's pairwise
+//   update. Also min / max / non-zeros.
+// * gram_aug_kernel / gram_fold_kernel -- the centred Gramian of [X - mu | onehot(y)] on the matrix
+//   cores (v_mfma_f32_32x32x2_f32, exact fp32 products): 128x128 output tiles (upper triangle of tile
+//   pairs) x row chunks, 4 waves each owning a 64x64 quadrant (2x2 accumulators of 32x32), 32-row
+//   stages of both column tiles centred into LDS. The fp32 accumulators are flushed into fp64
+//   registers every 256 rows; chunks are summed in fp64 by the fold kernel, which also mirrors the
+//   tiles into the full symmetric matrix. The X-block gives Pearson correlations, the label block
+//   gives the label x column contingency sums (onehot(y)^T (X - mu), + n_l mu on the host) and the
+//   label counts -- all in one pass over the sampled rows.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <float.h>
@@ -17,11 +28,13 @@ __global__ void __launch_bounds__(256) col_partials_kernel(const float* __restri
   const int64_t r1 = min(n, r0 + rows_per_chunk);
   double s = 0, q = 0, nz = 0;
   float mn = FLT_MAX, mx = -FLT_MAX;
+  const double K = (c < d && r0 < r1) ? (double)X[r0 * ld + c] : 0.0;
   if (c < d) {
     for (int64_t r = r0 + ty; r < r1; r += 4) {
       const float v = X[r * ld + c];
-      s += v;
-      q += (double)v * v;
+      const double e = (double)v - K;
+      s += e;
+      q += e * e;
       mn = fminf(mn, v);
       mx = fmaxf(mx, v);
       nz += v != 0.f;
@@ -36,27 +49,145 @@ __global__ void __launch_bounds__(256) col_partials_kernel(const float* __restri
       s += sh[k][0][l]; q += sh[k][1][l]; nz += sh[k][4][l];
       mn = fminf(mn, (float)sh[k][2][l]); mx = fmaxf(mx, (float)sh[k][3][l]);
     }
-    double* p = part + (int64_t)blockIdx.y * 5 * d;
-    p[c] = s; p[d + c] = q; p[2 * d + c] = mn; p[3 * d + c] = mx; p[4 * d + c] = nz;
+    const double cnt = (double)(r1 > r0 ? r1 - r0 : 0);
+    const double mean = cnt > 0 ? K + s / cnt : 0.0;
+    const double m2 = cnt > 0 ? fmax(q - s * s / cnt, 0.0) : 0.0;
+    double* p = part + (int64_t)blockIdx.y * 6 * d;
+    p[c] = mean; p[d + c] = m2; p[2 * d + c] = mn; p[3 * d + c] = mx; p[4 * d + c] = nz; p[5 * d + c] = cnt;
   }
 }
 
+// out rows: 0 sum, 1 M2 (sum of squared deviations), 2 min, 3 max, 4 non-zeros, 5 mean
 __global__ void col_fold_kernel(const double* __restrict__ part, int chunks, int d, double* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= d) return;
-  double s = 0, q = 0, nz = 0, mn = DBL_MAX, mx = -DBL_MAX;
+  double na = 0, ma = 0, m2 = 0, nz = 0, mn = DBL_MAX, mx = -DBL_MAX;
   for (int k = 0; k < chunks; ++k) {
-    const double* p = part + (int64_t)k * 5 * d;
-    s += p[c]; q += p[d + c]; nz += p[4 * d + c];
-    mn = fmin(mn, p[2 * d + c]); mx = fmax(mx, p[3 * d + c]);
+    const double* p = part + (int64_t)k * 6 * d;
+    const double nb = p[5 * d + c];
+    if (nb <= 0) continue;
+    const double mb = p[c], n = na + nb, delta = mb - ma;
+    ma += delta * (nb / n);
+    m2 += p[d + c] + delta * delta * (na * nb / n);
+    na = n;
+    nz += p[4 * d + c];
+    mn = fmin(mn, p[2 * d + c]);
+    mx = fmax(mx, p[3 * d + c]);
   }
-  out[c] = s; out[d + c] = q; out[2 * d + c] = mn; out[3 * d + c] = mx; out[4 * d + c] = nz; out[5 * d + c] = 0;
+  out[c] = ma * na; out[d + c] = m2; out[2 * d + c] = mn; out[3 * d + c] = mx; out[4 * d + c] = nz;
+  out[5 * d + c] = ma;
+}
+
+// ------------------------------------------------------------------------------------ Gramian
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+constexpr int GT = 128;     // output tile edge (columns of the augmented matrix)
+constexpr int GK = 32;      // rows per LDS stage
+constexpr int kFlush = 8;   // stages between fp32 -> fp64 accumulator flushes (256 rows)
+
+struct TilePair {
+  int32_t i, j;
+};
+
+// p-th tile pair (i <= j) of the upper triangle of an nt x nt tile grid, row by row.
+__device__ __forceinline__ TilePair tile_pair(int p, int nt) {
+  int i = 0;
+  while (p >= nt - i) {
+    p -= nt - i;
+    ++i;
+  }
+  return TilePair{i, i + p};
+}
+
+// Augmented column c of row r: X[r][c] - mu[c] for c < d, (y[r] == c - d) for d <= c < d + L, else 0.
+__device__ __forceinline__ float aug(const float* __restrict__ X, int64_t ld, const float* __restrict__ mu,
+                                     const int32_t* __restrict__ y, int d, int L, int64_t r, int c) {
+  if (c < d) return X[r * ld + c] - mu[c];
+  if (c < d + L) return (y[r] == c - d) ? 1.f : 0.f;
+  return 0.f;
+}
+
+__global__ void __launch_bounds__(256) gram_aug_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ld,
+                                                       const float* __restrict__ mu, const int32_t* __restrict__ y,
+                                                       int L, int nt, int64_t rows_per_chunk,
+                                                       double* __restrict__ part) {
+  __shared__ float tA[GK][GT + 4];
+  __shared__ float tB[GK][GT + 4];
+  const TilePair tp = tile_pair(blockIdx.x, nt);
+  const int ca = tp.i * GT, cb = tp.j * GT;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = min(n, r0 + rows_per_chunk);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qa = (wave >> 1) * 64, qb = (wave & 1) * 64;   // this wave's 64x64 quadrant
+  const int li = lane & 31, lk = lane >> 5;
+  f32x16 acc[2][2];
+  double dacc[2][2][16];
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      acc[a][b] = f32x16{};
+      for (int e = 0; e < 16; ++e) dacc[a][b][e] = 0.0;
+    }
+  int stage = 0;
+  for (int64_t rs = r0; rs < r1; rs += GK, ++stage) {
+    for (int e = threadIdx.x; e < GK * GT; e += 256) {
+      const int rr = e / GT, cc = e % GT;
+      const int64_t r = rs + rr;
+      const bool in = r < r1;
+      tA[rr][cc] = in ? aug(X, ld, mu, y, d, L, r, ca + cc) : 0.f;
+      tB[rr][cc] = in ? aug(X, ld, mu, y, d, L, r, cb + cc) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < GK; k += 2) {
+      const float a0 = tA[k + lk][qa + li], a1 = tA[k + lk][qa + 32 + li];
+      const float b0 = tB[k + lk][qb + li], b1 = tB[k + lk][qb + 32 + li];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();
+    if ((stage + 1) % kFlush == 0) {
+      for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+          for (int e = 0; e < 16; ++e) dacc[a][b][e] += (double)acc[a][b][e];
+          acc[a][b] = f32x16{};
+        }
+    }
+  }
+  // C/D map of 32x32: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+  double* out = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * GT * GT;
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b)
+      for (int e = 0; e < 16; ++e) {
+        const int row = qa + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * lk;
+        const int col = qb + b * 32 + li;
+        out[row * GT + col] = dacc[a][b][e] + (double)acc[a][b][e];
+      }
+}
+
+// G[D][D] (D = d + L) = sum over chunks of the tile partials, mirrored into the lower triangle.
+__global__ void __launch_bounds__(256) gram_fold_kernel(const double* __restrict__ part, int chunks, int npairs,
+                                                        int nt, int D, double* __restrict__ G) {
+  const int p = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= GT * GT) return;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += part[((int64_t)c * npairs + p) * GT * GT + e];
+  const TilePair tp = tile_pair(p, nt);
+  const int i = tp.i * GT + e / GT, j = tp.j * GT + e % GT;
+  if (i < D && j < D) {
+    G[(int64_t)i * D + j] = s;
+    G[(int64_t)j * D + i] = s;
+  }
 }
 
 }  // namespace
 
-extern "C" int tmog_hip_col_stats(const float* X, const void* unused, int64_t n, int d, int64_t ld, double* out,
-                                  hipStream_t stream) {
+extern "C" {
+
+int tmog_hip_col_stats(const float* X, const void* unused, int64_t n, int d, int64_t ld, double* out,
+                       hipStream_t stream) {
   (void)unused;
   if (n == 0 || d == 0) return 0;
   const int cblocks = (d + 63) / 64;
@@ -65,10 +196,38 @@ extern "C" int tmog_hip_col_stats(const float* X, const void* unused, int64_t n,
   if (chunks < 1) chunks = 1;
   const int64_t rpc = (n + chunks - 1) / chunks;
   double* part = nullptr;
-  hipError_t e = hipMallocAsync((void**)&part, sizeof(double) * 5 * d * chunks, stream);
+  hipError_t e = hipMallocAsync((void**)&part, sizeof(double) * 6 * d * chunks, stream);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(col_partials_kernel, dim3(cblocks, (unsigned)chunks), dim3(256), 0, stream, X, n, d, ld, rpc, part);
   hipLaunchKernelGGL(col_fold_kernel, dim3((d + 255) / 256), dim3(256), 0, stream, part, (int)chunks, d, out);
   hipFreeAsync(part, stream);
   return (int)hipGetLastError();
 }
+
+// G (fp64, [(d+L)^2], fully written) = [X - mu | onehot(y)]^T [X - mu | onehot(y)] over n rows.
+int tmog_hip_gram_aug(const float* X, int64_t n, int d, int64_t ld, const float* mu, const int32_t* y, int L,
+                      double* G, hipStream_t stream) {
+  if (n <= 0 || d <= 0 || L < 0 || (L > 0 && y == nullptr)) return -1;
+  const int D = d + L;
+  const int nt = (D + GT - 1) / GT;
+  const int npairs = nt * (nt + 1) / 2;
+  int64_t chunks = (1024 + npairs - 1) / npairs;             // >= ~1024 workgroups
+  const int64_t max_chunks = 4096 / npairs > 1 ? 4096 / npairs : 1;  // partials <= 512 MB
+  if (chunks > max_chunks) chunks = max_chunks;
+  if (chunks > (n + 1023) / 1024) chunks = (n + 1023) / 1024;
+  if (chunks < 1) chunks = 1;
+  int64_t rpc = (n + chunks - 1) / chunks;
+  rpc = (rpc + GK - 1) / GK * GK;
+  chunks = (n + rpc - 1) / rpc;
+  double* part = nullptr;
+  hipError_t e = hipMallocAsync((void**)&part, sizeof(double) * GT * GT * npairs * chunks, stream);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(gram_aug_kernel, dim3((unsigned)npairs, (unsigned)chunks), dim3(256), 0, stream, X, n, d, ld, mu,
+                     y, L, nt, rpc, part);
+  hipLaunchKernelGGL(gram_fold_kernel, dim3(GT * GT / 256, (unsigned)npairs), dim3(256), 0, stream, part,
+                     (int)chunks, npairs, nt, D, G);
+  hipFreeAsync(part, stream);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

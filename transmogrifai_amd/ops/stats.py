@@ -8,7 +8,7 @@
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
 
@@ -16,53 +16,99 @@ from . import _native as N
 
 
 def _col_partials(X: torch.Tensor):
-    """(sum, sum of squares, min, max, non-zeros) per column, fp64, in one pass (HIP kernel on fp32 device data)."""
+    """(count, mean, M2, min, max, non-zeros) per column in fp64, one pass. fp32 device data runs the HIP
+    shifted-sum / Chan-merge kernel; host data the two-pass reference."""
     n, d = X.shape[0], X.shape[1]
-    if X.is_cuda and X.dtype == torch.float32 and n > 0 and X.is_contiguous():
+    if X.is_cuda and X.dtype == torch.float32 and n > 0 and X.stride(1) == 1:
         out = torch.empty(6, d, dtype=torch.float64, device=X.device)
-        N.check(N.hip().tmog_hip_col_stats(N.ptr(X), None, n, d, d, N.ptr(out), N.stream(X.device)), "col_stats")
-        return out[0], out[1], out[2], out[3], out[4]
+        N.check(N.hip().tmog_hip_col_stats(N.ptr(X), None, n, d, X.stride(0), N.ptr(out), N.stream(X.device)),
+                "col_stats")
+        return n, out[5], out[1], out[2], out[3], out[4]
     Xd = X.to(torch.float64)
     if n == 0:
         z = torch.zeros(d, dtype=torch.float64, device=X.device)
-        return z, z.clone(), torch.full_like(z, float("inf")), torch.full_like(z, float("-inf")), z.clone()
-    return Xd.sum(0), (Xd * Xd).sum(0), Xd.min(0).values, Xd.max(0).values, (Xd != 0).sum(0).to(torch.float64)
+        return 0, z, z.clone(), torch.full_like(z, float("inf")), torch.full_like(z, float("-inf")), z.clone()
+    mean = Xd.mean(0)
+    m2 = (Xd - mean).pow(2).sum(0)
+    return n, mean, m2, Xd.min(0).values, Xd.max(0).values, (Xd != 0).sum(0).to(torch.float64)
 
 
 def col_stats(X: torch.Tensor) -> Dict[str, torch.Tensor]:
-    """Spark ``Statistics.colStats``. In a row-sharded fit the per-rank partials are all-reduced (one packed
-    SUM of count / sums / non-zeros plus a MIN and a MAX, ``SanityChecker.scala:407``)."""
+    """Spark ``Statistics.colStats`` with a numerically stable variance (per-chunk shifted sums merged with
+    Chan's update on the device; ``SanityChecker.scala:407``). Row-sharded fits gather every rank's
+    (count, mean, M2) and merge them the same way, plus a MIN / MAX / SUM of the rest."""
     from ..parallel import dp
-    s1, s2, mn, mx, nnz = _col_partials(X)
-    n_t = torch.tensor([float(X.shape[0])], dtype=torch.float64, device=s1.device)
+    n, mean, m2, mn, mx, nnz = _col_partials(X)
     if dp.active():
-        n_t, s1, s2, nnz = dp.sum_([n_t, s1, s2, nnz])
+        d = mean.numel()
+        part = torch.cat([torch.tensor([float(n)], dtype=torch.float64, device=mean.device), mean, m2])[None, :]
+        allp = dp.rows(part)                      # [world, 1 + 2d]
+        ns, means, m2s = allp[:, 0], allp[:, 1:1 + d], allp[:, 1 + d:]
+        tot = float(ns.sum().item())
+        gmean = (ns[:, None] * means).sum(0) / max(tot, 1.0)
+        m2 = (m2s + ns[:, None] * (means - gmean[None, :]).pow(2)).sum(0)
+        mean, n = gmean, int(tot)
+        nnz, = dp.sum_([nnz])
         mn, mx = dp.min_(mn), dp.max_(mx)
-    n = int(n_t.item())
-    mean = s1 / max(n, 1)
-    if not dp.active() and not (X.is_cuda and X.dtype == torch.float32) and n > 1:
-        var = X.to(torch.float64).var(0, unbiased=True)      # host reference path: two-pass variance
-    else:
-        var = ((s2 - n * mean * mean) / max(n - 1, 1)).clamp_min(0)
+    var = (m2 / max(n - 1, 1)).clamp_min(0)
     if n == 0:
         mn, mx = mean, mean
     return {"count": n, "mean": mean, "variance": var, "min": mn, "max": mx, "numNonzeros": nnz}
 
 
-def _rank_columns(X: torch.Tensor) -> torch.Tensor:
-    """Average ranks per column (ties share the mean rank), as Spark's Spearman correlation."""
+def _rank_columns(X: torch.Tensor, chunk: int = 256) -> torch.Tensor:
+    """Average ranks per column (ties share the mean rank), as Spark's Spearman correlation: one batched
+    column sort per chunk of columns, tie groups from run starts / ends (cummax / reversed cummin)."""
     n, d = X.shape
     out = torch.empty(n, d, dtype=torch.float64, device=X.device)
-    for j in range(d):
-        v = X[:, j].to(torch.float64)
-        s, order = torch.sort(v, stable=True)
-        uniq, inv, cnt = torch.unique_consecutive(s, return_inverse=True, return_counts=True)
-        ends = torch.cumsum(cnt, 0).to(torch.float64)
-        avg = ends - (cnt.to(torch.float64) - 1) / 2.0
-        r = torch.empty(n, dtype=torch.float64, device=X.device)
-        r[order] = avg[inv]
-        out[:, j] = r
+    if n == 0:
+        return out
+    pos = torch.arange(n, device=X.device, dtype=torch.int64)[:, None]
+    for a in range(0, d, chunk):
+        v = X[:, a:a + chunk].to(torch.float64)
+        s, order = torch.sort(v, dim=0, stable=True)
+        first = torch.ones_like(s, dtype=torch.bool)
+        first[1:] = s[1:] != s[:-1]
+        last = torch.ones_like(s, dtype=torch.bool)
+        last[:-1] = first[1:]
+        start = torch.where(first, pos, torch.zeros_like(pos)).cummax(0).values
+        big = torch.full_like(pos, n - 1)
+        end = torch.where(last, pos, big).flip(0).cummin(0).values.flip(0)
+        avg = (start + end).to(torch.float64) / 2.0 + 1.0
+        out[:, a:a + chunk].scatter_(0, order, avg)
     return out
+
+
+def gram_centered(X: torch.Tensor, mean: torch.Tensor, y_codes: Optional[torch.Tensor] = None,
+                  n_labels: int = 0) -> torch.Tensor:
+    """``G = A^T A`` with ``A = [X - mean | onehot(y_codes)]`` (fp64 ``[d + L, d + L]``, this rank's rows).
+
+    fp32 device data runs the MFMA ``gram_aug_kernel`` (one pass: centred Gramian, label x column sums and
+    label counts); otherwise an fp64 torch reference."""
+    n, d = X.shape
+    L = int(n_labels)
+    if X.is_cuda and X.dtype == torch.float32 and X.stride(1) == 1 and n > 0:
+        G = torch.empty(d + L, d + L, dtype=torch.float64, device=X.device)
+        mu = mean.to(device=X.device, dtype=torch.float32).contiguous()
+        yc = None if L == 0 else y_codes.to(device=X.device, dtype=torch.int32).contiguous()
+        N.check(N.hip().tmog_hip_gram_aug(N.ptr(X), n, d, X.stride(0), N.ptr(mu), N.ptr(yc), L, N.ptr(G),
+                                          N.stream(X.device)), "gram_aug")
+        return G
+    A = X.to(torch.float64) - mean.to(device=X.device, dtype=torch.float64)[None, :]
+    if L:
+        oh = torch.zeros(n, L, dtype=torch.float64, device=X.device)
+        oh[torch.arange(n, device=X.device), y_codes.to(X.device).long()] = 1.0
+        A = torch.cat([A, oh], 1)
+    return A.t() @ A
+
+
+def _corr_from_gram(G: torch.Tensor, n: int) -> torch.Tensor:
+    G = G / max(n - 1, 1)
+    sd = torch.sqrt(torch.diag(G).clamp_min(0))
+    C = G / (sd[:, None] * sd[None, :])
+    C = torch.where((sd[:, None] == 0) | (sd[None, :] == 0), torch.full_like(C, float("nan")), C)
+    C.fill_diagonal_(1.0)
+    return C
 
 
 def corr_matrix(X: torch.Tensor, method: str = "pearson", mean=None) -> torch.Tensor:
@@ -83,14 +129,31 @@ def corr_matrix(X: torch.Tensor, method: str = "pearson", mean=None) -> torch.Te
     if mean is None:
         s, = dp.sum_([X.to(torch.float64).sum(0)])
         mean = s / max(n, 1)
-    Xc = (X - mean.to(X.dtype)[None, :])
-    G, = dp.sum_([(Xc.t() @ Xc).to(torch.float64)])
-    G = G / max(n - 1, 1)
-    sd = torch.sqrt(torch.diag(G))
-    C = G / (sd[:, None] * sd[None, :])
-    C = torch.where((sd[:, None] == 0) | (sd[None, :] == 0), torch.full_like(C, float("nan")), C)
-    C.fill_diagonal_(1.0)
-    return C
+    if X.dtype == torch.float64 and X.is_cuda:      # ranks: centred fp64 GEMM on the device
+        Xc = X - mean.to(X.dtype)[None, :]
+        G = Xc.t() @ Xc
+    else:
+        G = gram_centered(X, mean)
+    G, = dp.sum_([G])
+    return _corr_from_gram(G, n)
+
+
+def corr_and_label_sums(X: torch.Tensor, y: torch.Tensor, mean: torch.Tensor):
+    """Pearson correlation matrix of ``X`` plus the label contingency of its columns from ONE Gramian pass
+    (``SanityChecker.scala:464-470`` + ``categoricalTests:252-348``): returns ``(C [d, d], labels [L],
+    sums [L, d] = onehot(y)^T X, counts [L])``. Row-sharded: global labels, one SUM of the partial Gramian."""
+    from ..parallel import dp
+    labels = dp.unique_values(y.to(torch.float64))
+    codes = torch.searchsorted(labels, y.to(torch.float64))
+    L = labels.numel()
+    d = X.shape[1]
+    G = gram_centered(X, mean, codes, L)
+    G, = dp.sum_([G])
+    n = dp.count(X.shape[0])
+    C = _corr_from_gram(G[:d, :d], n)
+    counts = torch.diag(G[d:, d:]).clone()
+    sums = G[d:, :d] + counts[:, None] * mean.to(torch.float64)[None, :]
+    return C, labels, sums, counts
 
 
 def label_column_sums(X: torch.Tensor, y: torch.Tensor):

@@ -213,17 +213,27 @@ class SanityChecker(BinaryEstimator):
             cov = cov / max(count - 1, 1)
             sd = ss.div(max(count - 1, 1)).sqrt()
             corr_label = (cov / (sd * sd[-1])).cpu().numpy()
-        else:
-            C = ST.corr_matrix(Xy.index_select(1, ci), p["correlation_type"],
-                               mean=None if p["correlation_type"] == "spearman" else
-                               cs["mean"].index_select(0, ci.to(cs["mean"].device)).to(Xy.device)).cpu().numpy()
-            corr_label = C[:, -1]
-        # categorical tests
         labels_u = dp.unique_values(y)
         cat_label = p["categorical_label"]
+        want_cat = cat_label is not False and (cat_label is True or labels_u.numel() < min(100.0, count * 0.1))
+        pre_cat = None
+        if p["feature_feature_corr_level"] != "Off":
+            fused = (p["correlation_type"] == "pearson" and want_cat and len(corr_idx) == d + 1 and
+                     not any(c.has_parent_of_subtype(T.MultiPickList) for c in cols))
+            if fused:
+                # one MFMA Gramian pass: correlations + label x column contingency + label counts
+                Ct, lab, sums, cnts = ST.corr_and_label_sums(Xy, y, cs["mean"].to(Xy.device))
+                C = Ct.cpu().numpy()
+                pre_cat = (lab, sums[:, :d], cnts)
+            else:
+                C = ST.corr_matrix(Xy.index_select(1, ci), p["correlation_type"],
+                                   mean=None if p["correlation_type"] == "spearman" else
+                                   cs["mean"].index_select(0, ci.to(cs["mean"].device)).to(Xy.device)).cpu().numpy()
+            corr_label = C[:, -1]
+        # categorical tests
         cat_stats = []
-        if cat_label is not False and (cat_label is True or labels_u.numel() < min(100.0, count * 0.1)):
-            cat_stats = self._categorical_tests(X, y, cols)
+        if want_cat:
+            cat_stats = self._categorical_tests(X, y, cols, pre_cat)
         label_dist = None
         if labels_u.numel() <= 100:
             lu = labels_u
@@ -260,14 +270,17 @@ class SanityChecker(BinaryEstimator):
         return SanityCheckerModel(keep_idx, p["remove_bad_features"])
 
     # ----------------------------------------------------------------------------------------
-    def _categorical_tests(self, X, y, cols) -> List[Dict]:
-        mpl_idx = [c.index for c in cols if c.has_parent_of_subtype(T.MultiPickList)]
-        Xc = X
-        if mpl_idx:
-            Xc = X.clone()
-            mi = torch.as_tensor(mpl_idx, device=X.device)
-            Xc[:, mi] = torch.clamp(Xc[:, mi], max=1.0)
-        labels, sums, counts = ST.label_column_sums(Xc, y)
+    def _categorical_tests(self, X, y, cols, pre=None) -> List[Dict]:
+        if pre is not None:
+            labels, sums, counts = pre
+        else:
+            mpl_idx = [c.index for c in cols if c.has_parent_of_subtype(T.MultiPickList)]
+            Xc = X
+            if mpl_idx:
+                Xc = X.clone()
+                mi = torch.as_tensor(mpl_idx, device=X.device)
+                Xc[:, mi] = torch.clamp(Xc[:, mi], max=1.0)
+            labels, sums, counts = ST.label_column_sums(Xc, y)
         cont = torch.cat([sums, counts[:, None]], 1).cpu().numpy()   # [L, d+1] rows = labels
         groups: "OrderedDict[str, list]" = OrderedDict()
         for c in cols:
