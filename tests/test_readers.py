@@ -105,3 +105,60 @@ def test_avro_roundtrip(tmp_path):
             {"a": None, "b": "x", "c": [], "m": {}, "f": False}]
     write_avro(str(tmp_path / "r.avro"), schema, recs)
     assert read_avro(str(tmp_path / "r.avro")) == recs
+
+
+def _join_fixture():
+    import csv
+    from transmogrifai_amd.readers.base import InMemoryReader
+    ref = "/root/reference/test-data"
+    left = [dict(id=r[0], timestamp=int(r[1]), description=r[2]) for r in csv.reader(open(f"{ref}/SparkExampleJoin.csv"))]
+    right = [dict(sparkId=r[0], timestamp=int(r[1]), description=r[2], id=int(r[3]))
+             for r in csv.reader(open(f"{ref}/JoinTestData.csv"))]
+    lr = InMemoryReader(left, key=lambda r: r["id"])
+    rr = InMemoryReader(right, key=lambda r: str(r["id"]))
+    description = FeatureBuilder.Text("description").extract(lambda r: r["description"]).as_predictor()
+    time = FeatureBuilder.Date("time").extract(lambda r: r["timestamp"]).as_predictor()
+    description_j = FeatureBuilder.Text("descriptionJoin").extract(lambda r: r["description"]).as_predictor()
+    time_j = FeatureBuilder.Date("timeJoin").extract(lambda r: r["timestamp"]).as_predictor()
+    key_j = FeatureBuilder.Text("keyJoin").extract(lambda r: r["sparkId"]).as_predictor()
+    return lr, rr, (description, time, description_j, time_j, key_j)
+
+
+def test_joined_secondary_aggregation_dummy_aggregator():
+    """JoinedDataReaderDataGenerationTest.scala:196-252 on the reference's own CSV fixtures: a parent-child
+    outer join on keyJoin, then a TimeBasedFilter(condition = timeJoin, primary = time, 1000 days)."""
+    from transmogrifai_amd.readers.joined import (JoinKeys, JoinedReader, JoinTypes, TimeBasedFilter, TimeColumn)
+    lr, rr, feats = _join_fixture()
+    description, time, description_j, time_j, key_j = feats
+    keys = JoinKeys(left_key="key", right_key="keyJoin", result_key="key")
+    tf = TimeBasedFilter(TimeColumn("timeJoin"), TimeColumn("time"), 1000 * 86_400_000)
+    jr = JoinedReader(lr, rr, JoinTypes.Outer, right_features=["descriptionJoin", "timeJoin", "keyJoin"],
+                      join_keys=keys)
+    joined = jr.generate_dataset(list(feats))
+    agg = jr.with_secondary_aggregation(tf).generate_dataset(list(feats))
+    assert sorted(joined.key) == ["a", "b", "b", "c"]
+    rows = {k: i for i, k in enumerate(agg.key)}
+    assert sorted(rows) == ["a", "b", "c"]
+    # left (parent) fields unchanged by the aggregation
+    jl = {(d, t) for d, t in zip(joined["description"].to_list(), joined["time"].to_list())}
+    al = {(d, t) for d, t in zip(agg["description"].to_list(), agg["time"].to_list())}
+    assert jl == al
+    # 'c' had one child row that passes the filter: identical to the joined row
+    jc = list(joined.key).index("c")
+    for f in feats:
+        assert agg[f.name].to_list()[rows["c"]] == joined[f.name].to_list()[jc]
+    # 'a' does not pass the filter; 'b' aggregates both children (Text concat, Date max)
+    assert agg["descriptionJoin"].to_list()[rows["a"]] is None and agg["timeJoin"].to_list()[rows["a"]] is None
+    assert agg["descriptionJoin"].to_list()[rows["b"]] == "Important too But I hate to write them"
+    assert agg["timeJoin"].to_list()[rows["b"]] == 1499175176
+
+
+def test_join_keys_validation():
+    from transmogrifai_amd.readers.base import InMemoryReader
+    from transmogrifai_amd.readers.joined import JoinKeys, JoinedReader
+    r = InMemoryReader([], key=lambda x: x)
+    with pytest.raises(ValueError):
+        JoinedReader(r, r, join_keys=JoinKeys(left_key="a", right_key="b", result_key="key"))
+    assert JoinKeys(right_key="p", result_key="key").is_parent_child
+    assert JoinKeys(left_key="p", result_key="key").is_child_parent
+    assert JoinKeys().is_combined
