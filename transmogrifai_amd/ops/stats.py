@@ -138,21 +138,42 @@ def corr_matrix(X: torch.Tensor, method: str = "pearson", mean=None) -> torch.Te
     return _corr_from_gram(G, n)
 
 
-def corr_and_label_sums(X: torch.Tensor, y: torch.Tensor, mean: torch.Tensor):
+def _shift(mean: torch.Tensor, mn: Optional[torch.Tensor], mx: Optional[torch.Tensor]) -> torch.Tensor:
+    """Per-column centring shift: the nearest integer to the mean for integer-bounded columns (one-hot,
+    null indicators, counts: ``x - shift`` and every fp32 product / partial sum stay exact), else the
+    fp32-rounded mean."""
+    s = mean.to(torch.float32).to(torch.float64)
+    if mn is None or mx is None:
+        return s
+    mn, mx = mn.to(mean.device, torch.float64), mx.to(mean.device, torch.float64)
+    integral = (mn == torch.round(mn)) & (mx == torch.round(mx)) & ((mx - mn) < 2 ** 20)
+    return torch.where(integral, torch.round(mean), s)
+
+
+def corr_and_label_sums(X: torch.Tensor, y: torch.Tensor, mean: torch.Tensor, mn: Optional[torch.Tensor] = None,
+                        mx: Optional[torch.Tensor] = None):
     """Pearson correlation matrix of ``X`` plus the label contingency of its columns from ONE Gramian pass
     (``SanityChecker.scala:464-470`` + ``categoricalTests:252-348``): returns ``(C [d, d], labels [L],
-    sums [L, d] = onehot(y)^T X, counts [L])``. Row-sharded: global labels, one SUM of the partial Gramian."""
+    sums [L, d] = onehot(y)^T X, counts [L])``. Row-sharded: global labels, one SUM of the partial Gramian.
+
+    The kernel centres on a per-column shift ``s`` (``_shift``); the centred Gramian is recovered in fp64 as
+    ``G_s - n (mean - s)(mean - s)^T`` and the label sums as ``onehot^T (X - s) + n_l s`` -- exact for
+    indicator / count columns, whose contingency tables feed Cramér's V."""
     from ..parallel import dp
     labels = dp.unique_values(y.to(torch.float64))
     codes = torch.searchsorted(labels, y.to(torch.float64))
     L = labels.numel()
     d = X.shape[1]
-    G = gram_centered(X, mean, codes, L)
+    mean = mean.to(torch.float64)
+    sh = _shift(mean, mn, mx)
+    G = gram_centered(X, sh, codes, L)
     G, = dp.sum_([G])
     n = dp.count(X.shape[0])
-    C = _corr_from_gram(G[:d, :d], n)
+    delta = (mean - sh).to(G.device)
+    Gx = G[:d, :d] - n * delta[:, None] * delta[None, :]
+    C = _corr_from_gram(Gx, n)
     counts = torch.diag(G[d:, d:]).clone()
-    sums = G[d:, :d] + counts[:, None] * mean.to(torch.float64)[None, :]
+    sums = G[d:, :d] + counts[:, None] * sh.to(G.device)[None, :]
     return C, labels, sums, counts
 
 

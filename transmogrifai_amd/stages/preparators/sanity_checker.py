@@ -222,7 +222,7 @@ class SanityChecker(BinaryEstimator):
                      not any(c.has_parent_of_subtype(T.MultiPickList) for c in cols))
             if fused:
                 # one MFMA Gramian pass: correlations + label x column contingency + label counts
-                Ct, lab, sums, cnts = ST.corr_and_label_sums(Xy, y, cs["mean"].to(Xy.device))
+                Ct, lab, sums, cnts = ST.corr_and_label_sums(Xy, y, cs["mean"].to(Xy.device), cs["min"], cs["max"])
                 C = Ct.cpu().numpy()
                 pre_cat = (lab, sums[:, :d], cnts)
             else:
