@@ -431,3 +431,84 @@ def _min_var(self, min_variance: float = 1e-5, remove_bad_features: bool = True)
 @register(T.OPVector, "combine")
 def _combine(self, *others):
     return V.VectorsCombiner().set_input([self] + list(others)).get_output()
+
+
+# ----------------------------------------------------------------- NLP / type detection entry points
+@register(T.Text, "tokenize_regex")
+def _tokenize_regex(self, pattern: str, group: int = -1, min_token_length: int = 1, to_lowercase: bool = True):
+    """``RichTextFeature.tokenizeRegex`` (``RichTextFeature.scala:375-392``)."""
+    return TS.TextRegexTokenizer(pattern=pattern, group=group, min_token_length=min_token_length,
+                                 to_lowercase=to_lowercase).set_input(self).get_output()
+
+
+@register(T.Text, "detect_languages")
+def _detect_languages(self):
+    """``RichTextFeature.detectLanguages`` -> RealMap of language confidences."""
+    from ..stages.feature.nlp_stages import LangDetector
+    return LangDetector().set_input(self).get_output()
+
+
+@register(T.Text, "recognize_entities")
+def _recognize_entities(self):
+    """``RichTextFeature.recognizeEntities`` -> MultiPickListMap of entity type -> tokens."""
+    from ..stages.feature.nlp_stages import NameEntityRecognizer
+    return NameEntityRecognizer().set_input(self).get_output()
+
+
+@register(T.Text, "identify_if_human_name")
+def _identify_human_name(self, default_threshold: float = 0.5):
+    """``RichTextFeature.identifyIfHumanName`` -> NameStats."""
+    from ..stages.feature.nlp_stages import HumanNameDetector
+    return HumanNameDetector(default_threshold=default_threshold).set_input(self).get_output()
+
+
+@register(T.Phone, "parse_phone_default_country")
+def _parse_phone_default(self, default_region: str = "US"):
+    """``RichPhoneFeature.parsePhoneDefaultCountry`` -> normalised Phone."""
+    from ..stages.feature.nlp_stages import ParsePhoneNumber
+    return ParsePhoneNumber(default_region=default_region).set_input(self).get_output()
+
+
+@register(T.Phone, "parse_phone")
+def _parse_phone(self, default_region: str = "US"):
+    return _parse_phone_default(self, default_region)
+
+
+@register(T.URL, "is_valid_url")
+def _is_valid_url(self):
+    return TS.ValidUrlTransformer().set_input(self).get_output()
+
+
+@register(T.TextList, "remove_stop_words")
+def _remove_stop_words(self, stop_words=None, case_sensitive: bool = False):
+    """``RichListFeature.removeStopWords`` (``RichListFeature.scala:94-166``)."""
+    from ..stages.feature.nlp_stages import OpStopWordsRemover
+    return OpStopWordsRemover(stop_words=stop_words, case_sensitive=case_sensitive).set_input(self).get_output()
+
+
+@register(T.TextList, "ngram")
+def _ngram(self, n: int = 2):
+    from ..stages.feature.nlp_stages import OpNGram
+    return OpNGram(n=n).set_input(self).get_output()
+
+
+@register(T.TextList, "count_vec")
+def _count_vec(self, vocab_size: int = 1 << 18, min_df: float = 1.0, min_tf: float = 1.0, binary: bool = False):
+    from ..stages.feature.nlp_stages import OpCountVectorizer
+    return OpCountVectorizer(vocab_size=vocab_size, min_df=min_df, min_tf=min_tf,
+                             binary=binary).set_input(self).get_output()
+
+
+@register(T.TextList, "word2vec")
+def _word2vec(self, vector_size: int = 100, window_size: int = 5, min_count: int = 5, max_iter: int = 1,
+              step_size: float = 0.025, **kw):
+    from ..stages.feature.nlp_stages import OpWord2Vec
+    return OpWord2Vec(vector_size=vector_size, window_size=window_size, min_count=min_count, max_iter=max_iter,
+                      step_size=step_size, **kw).set_input(self).get_output()
+
+
+@register(T.OPVector, "lda")
+def _lda(self, k: int = 10, max_iter: int = 20, seed: int = 0, **kw):
+    """``RichVectorFeature.lda`` (``RichVectorFeature.scala:115``)."""
+    from ..stages.feature.nlp_stages import OpLDA
+    return OpLDA(k=k, max_iter=max_iter, seed=seed, **kw).set_input(self).get_output()

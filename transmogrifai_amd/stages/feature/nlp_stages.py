@@ -273,14 +273,18 @@ def lda_e_step(X, Elogbeta, alpha, iters: int = 100, tol: float = 1e-3):
     K = Elogbeta.shape[0]
     expEb = torch.exp(Elogbeta)                                     # [K, V]
     gamma = torch.ones(N, K, dtype=X.dtype, device=X.device) + X.sum(1, keepdim=True) / K
+    # per-document convergence (mean |change| over topics < tol, as Spark's online LDA): a document's
+    # result does not depend on the batch it is scored in, so row and batch scoring agree
+    active = torch.ones(N, dtype=torch.bool, device=X.device)
     for _ in range(iters):
         Elt = torch.digamma(gamma) - torch.digamma(gamma.sum(1, keepdim=True))
         expEt = torch.exp(Elt)                                      # [N, K]
         phinorm = expEt @ expEb + 1e-100                            # [N, V]
         new = alpha[None, :] + expEt * ((X / phinorm) @ expEb.t())
-        done = (new - gamma).abs().mean() < tol
-        gamma = new
-        if bool(done):
+        conv = (new - gamma).abs().mean(1) < tol
+        gamma = torch.where(active[:, None], new, gamma)
+        active = active & ~conv
+        if not bool(active.any()):
             break
     Elt = torch.digamma(gamma) - torch.digamma(gamma.sum(1, keepdim=True))
     expEt = torch.exp(Elt)

@@ -293,3 +293,35 @@ class IDF(VectorizerMixin, UnaryEstimator):
         if cols[0].metadata is not None:
             self.metadata["vector_metadata"] = cols[0].metadata.with_name(self.get_output_feature_name())
         return IDFModel(idf)
+
+
+@register_stage
+class TextRegexTokenizer(UnaryTransformer):
+    """``tokenizeRegex`` (``RichTextFeature.scala:375-392``, ``LuceneRegexTextAnalyzer``): with ``group < 0``
+    the text is split on ``pattern`` (empty tokens dropped); otherwise every match's ``group`` is a
+    token. Lowercasing and the minimum token length apply as in ``TextTokenizer``."""
+    operation_name = "textToken"
+    output_type = T.TextList
+    _defaults = {"pattern": r"\s+", "group": -1, "min_token_length": 1, "to_lowercase": True}
+
+    def transform_fn(self, v):
+        import re
+        if v is None:
+            return []
+        p = self.params
+        s = v.lower() if p["to_lowercase"] else v
+        rx = re.compile(p["pattern"])
+        g = int(p["group"])
+        toks = [t for t in rx.split(s) if t] if g < 0 else [m.group(g) for m in rx.finditer(s) if m.group(g)]
+        return [t for t in toks if len(t) >= int(p["min_token_length"])]
+
+
+@register_stage
+class ValidUrlTransformer(UnaryTransformer):
+    """``URL.isValidUrl`` (``RichTextFeature.scala:651``): Binary flag of a well-formed http/https/ftp URL,
+    empty for an empty input."""
+    operation_name = "isValidUrl"
+    output_type = T.Binary
+
+    def transform_fn(self, v):
+        return None if v is None else TU.is_valid_url(v)
