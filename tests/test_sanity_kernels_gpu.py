@@ -87,9 +87,11 @@ def test_sanity_checker_device_matches_host():
     from transmogrifai_amd.readers.base import InMemoryReader
     from transmogrifai_amd import uid
     outs = []
+    ds_host, _, _ = binary_table(50_000, n_real=12, n_int=3, n_pick=4, seed=3, device="cpu")
     for dev in ("cpu", "cuda"):
         uid.reset(0)
-        ds, label, preds = binary_table(50_000, n_real=12, n_int=3, n_pick=4, seed=3, device=dev)
+        _, label, preds = binary_table(10, n_real=12, n_int=3, n_pick=4, seed=3, device="cpu")
+        ds = ds_host.to(dev)        # the same table on both devices (device RNG streams differ)
         vec = transmogrify(preds)
         checked = label.sanity_check(vec, remove_bad_features=True)
         model = OpWorkflow().set_result_features(checked).set_reader(InMemoryReader(ds)).train()
