@@ -89,6 +89,32 @@ class MeanNumeric(MonoidAggregator):
         return None if r[1] == 0 else r[0] / r[1]
 
 
+class SumRealNN(SumNumeric):
+    """``SumRealNN`` (``aggregators/Numerics.scala:54``): zero 0.0, so a key without events gets 0.0."""
+    name = "SumRealNN"
+    zero = 0.0
+
+
+class MaxRealNN(MaxNumeric):
+    """``MaxRealNN`` (``Numerics.scala:70``): zero -inf."""
+    name = "MaxRealNN"
+    zero = float("-inf")
+
+
+class MinRealNN(MinNumeric):
+    """``MinRealNN`` (``Numerics.scala:77``): zero +inf."""
+    name = "MinRealNN"
+    zero = float("inf")
+
+
+class MeanRealNN(MeanNumeric):
+    """``MeanRealNN`` (``Numerics.scala:103``): 0.0 for a key without events."""
+    name = "MeanRealNN"
+
+    def present(self, r):
+        return 0.0 if r[1] == 0 else r[0] / r[1]
+
+
 class LogicalOr(MonoidAggregator):
     name = "LogicalOr"
     plus = staticmethod(_opt(lambda a, b: bool(a) or bool(b)))
@@ -240,6 +266,8 @@ def default_aggregator(t) -> MonoidAggregator:
         return MaxNumeric()
     if issubclass(t, T.Percent):
         return MeanNumeric()
+    if issubclass(t, T.RealNN):
+        return SumRealNN()
     if issubclass(t, T.OPNumeric):
         return SumNumeric()
     if issubclass(t, T.OPSet):
@@ -298,7 +326,8 @@ def aggregator_from_json(d) -> Optional[MonoidAggregator]:
     if not d:
         return None
     name = (d.get("value") or {}).get("name") or d.get("className")
-    simple = {c.name: c for c in (SumNumeric, MaxNumeric, MinNumeric, MeanNumeric, LogicalOr, ModePickList,
+    simple = {c.name: c for c in (SumNumeric, MaxNumeric, MinNumeric, MeanNumeric, SumRealNN, MaxRealNN, MinRealNN,
+                                  MeanRealNN, LogicalOr, ModePickList,
                                   ConcatList, UnionSet, GeolocationMidpoint, CombineVector)}
     if name in simple:
         return simple[name]()
