@@ -185,16 +185,19 @@ def main():
         if summ.get("failures") or n_eval != expected_configs:
             raise SystemExit(f"model selector evaluated {n_eval}/{expected_configs} configs; failures: "
                              f"{summ.get('failures')}")
-        return dt, ho, summ, model
+        if os.environ.get("TMOG_MEM_TRACE") == "1" and D.rank() == 0:
+            st = model.train_timings.get("stages", {})
+            print(json.dumps({k: v for k, v in st.items() if k.startswith("peak_gb")}), flush=True)
+        return dt, ho, summ
 
     expected_configs = _expected_configs(args)
-    if use_gpu:
-        torch.cuda.reset_peak_memory_stats(dev)
     for _ in range(args.warmup):
         one_run()
+    if use_gpu:
+        torch.cuda.reset_peak_memory_stats(dev)
     times, auprs, summ = [], [], None
     for _ in range(args.steps):
-        dt, ho, summ, model = one_run()
+        dt, ho, summ = one_run()
         times.append(dt)
         auprs.append(ho)
     t = torch.tensor([sum(times)], dtype=torch.float64)

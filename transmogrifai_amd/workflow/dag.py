@@ -10,6 +10,7 @@ row materialization.
 from __future__ import annotations
 
 import logging
+import os
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -19,6 +20,8 @@ from ..stages.base import OpEstimator, OpTransformer
 log = logging.getLogger(__name__)
 
 Layer = List[Tuple[object, int]]
+
+_MEM_TRACE = os.environ.get("TMOG_MEM_TRACE") == "1"
 
 
 def compute_dag(features) -> List[Layer]:
@@ -61,6 +64,7 @@ def fit_and_transform_layer(layer: Layer, train: Dataset, test: Optional[Dataset
             test = m.transform(test)
         if timings is not None:
             timings[f"transform:{m.stage_name()}"] = time.time() - t0
+        _mem_mark(timings, f"transform:{m.stage_name()}")
     return train, test, fitted
 
 
@@ -90,6 +94,16 @@ def _last_uses(dag: Sequence[Layer]) -> Dict[str, Tuple[int, int]]:
     return last
 
 
+def _mem_mark(timings, what):
+    """``TMOG_MEM_TRACE=1``: record the device memory high-water mark of each stage fit / transform."""
+    if timings is None or not _MEM_TRACE:
+        return
+    import torch
+    if torch.cuda.is_available():
+        timings[f"peak_gb:{what}"] = round(torch.cuda.max_memory_allocated() / 1e9, 3)
+        torch.cuda.reset_peak_memory_stats()
+
+
 def _fit_layer_with_eval(layer, train, test, timings, li=0, last=None, keep=None):
     fitted = []
     for st, _ in layer:
@@ -103,6 +117,7 @@ def _fit_layer_with_eval(layer, train, test, timings, li=0, last=None, keep=None
             fitted.append(st)
         if timings is not None:
             timings[f"fit:{st.stage_name()}"] = time.time() - t0
+        _mem_mark(timings, f"fit:{st.stage_name()}")
     for si, m in enumerate(fitted):
         t0 = time.time()
         train = m.transform(train)
@@ -116,6 +131,7 @@ def _fit_layer_with_eval(layer, train, test, timings, li=0, last=None, keep=None
                     test = test.drop(dead)
         if timings is not None:
             timings[f"transform:{m.stage_name()}"] = time.time() - t0
+        _mem_mark(timings, f"transform:{m.stage_name()}")
     return train, test, fitted
 
 
