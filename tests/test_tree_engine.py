@@ -215,3 +215,41 @@ def test_native_finalize_matches_numpy(mode, monkeypatch):
         np.testing.assert_array_equal(getattr(a, name), getattr(b, name), err_msg=name)
     if mode == te.MODE_GH:
         assert torch.equal(a.leaf_assign.value.cpu(), b.leaf_assign.value.cpu())
+
+
+def _grow_wide(dev, F=136, n_one=12, N=20_000, chunk_rows=4096):
+    """XGBoost-style Newton trees on a dword-aligned matrix (F % 4 == 0): on the GPU the multi-bin groups
+    run the wide-load histogram items (tree_kernels.hip hist_wide_item), groups sized in multiples of 4."""
+    g = torch.Generator().manual_seed(11)
+    B = 32
+    X = torch.randint(0, B - 1, (N, F), generator=g, dtype=torch.uint8)
+    X[torch.rand(N, F, generator=g) < 0.1] = B - 1                 # sparse missing bin
+    nbins = np.full(F, B - 1)
+    for c in range(F - n_one, F):
+        X[:, c] = torch.where(torch.rand(N, generator=g) < 0.3, 0, B - 1).to(torch.uint8)
+        nbins[c] = 1
+    t1 = torch.round(torch.randn(3, N, generator=g) * 64) / 64 + (X[:, 3].float() - 15) / 16
+    t2 = torch.rand(3, N, generator=g) * 0.25 + 0.01
+    jobs = [te.TreeJob(m, te.TreeParams(max_depth=7, min_child_weight=0.5, reg_lambda=1.0, gamma=0.1 * m,
+                                        split_eps=1e-6), torch.arange(N)[torch.arange(N) % (m + 2) != 1].to(dev))
+            for m in range(3)]
+    Xd = X.to(dev)
+    f = te.grow_forest(Xd, nbins, jobs, mode=te.MODE_GH, kind=te.KIND_NEWTON, t1=t1.to(dev), t2=t2.to(dev), B=B,
+                       missing_bin=B - 1, chunk_rows=chunk_rows,
+                       csr=te.onebin_csr(Xd, nbins) if n_one else None)
+    return f
+
+
+def test_cpu_engine_dword_aligned_matrix():
+    f = _grow_wide("cpu", N=3000)
+    assert f.n_trees == 3 and len(f.nodes) > 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F,n_one,chunk", [(136, 12, 4096), (68, 0, 1024), (200, 24, 512)])
+def test_hip_wide_hist_matches_host(F, n_one, chunk):
+    fc = _grow_wide("cpu", F, n_one, chunk_rows=chunk)
+    fg = _grow_wide("cuda", F, n_one, chunk_rows=chunk)
+    np.testing.assert_array_equal(fc.tree_off, fg.tree_off)
+    np.testing.assert_array_equal(fc.nodes, fg.nodes)
+    np.testing.assert_allclose(fc.value, fg.value, rtol=1e-6, atol=1e-6)

@@ -565,6 +565,18 @@ class XGBoostClassifierLearner(_BoostLearner):
                 colperm = order.astype(np.int64)
                 Xg = Xb.index_select(1, torch.as_tensor(colperm, device=dev)).contiguous()
                 n_bins_g = nb_all[colperm]
+        # wide-load histogram items (tree_kernels.hip hist_wide_item) read 4 bins per lane with dword loads:
+        # pad the growth matrix to a dword row stride with columns that hold only the missing bin (one
+        # "present" bin that no row has: they can never split, and are mapped to column 0 if ever read)
+        if dev.type == "cuda" and spec.missing_bin > 0 and os.environ.get("TMOG_HIST_WIDE") != "0" \
+                and Xg.shape[1] % 4 != 0:
+            F0 = Xg.shape[1]
+            F4 = (F0 + 3) // 4 * 4
+            pad = torch.full((Xg.shape[0], F4 - F0), spec.missing_bin, dtype=Xg.dtype, device=dev)
+            Xg = torch.cat([Xg, pad], 1).contiguous()
+            n_bins_g = np.concatenate([np.asarray(n_bins_g), np.ones(F4 - F0, dtype=np.asarray(n_bins_g).dtype)])
+            base_perm = colperm if colperm is not None else np.arange(F0, dtype=np.int64)
+            colperm = np.concatenate([base_perm, np.zeros(F4 - F0, np.int64)])
         # feature-parallel over the ranks: this rank's slice of the growth-order feature lists
         fp = TE.fp_plan(Xg, n_bins_g, par, sparse=spec.missing_bin >= 0) if par is not None else None
         # one-hot / null-indicator columns: histogram from the rows' CSR lists (tree_kernels.hip)

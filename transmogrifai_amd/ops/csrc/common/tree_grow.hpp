@@ -206,6 +206,7 @@ struct FeatGroup {
   int f0, nf;
   bool reg;
   bool csr = false;
+  bool wide = false;   // GPU: contiguous dword-aligned physical columns -> wide-load histogram items
 };
 
 constexpr int64_t kCsrRows = 1024;   // rows per CSR histogram item (GPU)
@@ -217,6 +218,17 @@ inline std::vector<FeatGroup> equal_groups(int n) {
   if (n <= 0) return out;
   const int ng = std::max(1, (n + 63) / 64);
   const int fg = (n + ng - 1) / ng;
+  for (int gi = 0; gi * fg < n; ++gi) out.push_back(FeatGroup{gi * fg, std::min(fg, n - gi * fg), false, false});
+  return out;
+}
+
+// Groups whose sizes are multiples of 4 (<= 64): with a dword-aligned first column every group of the
+// wide-load histogram path starts on a dword boundary of the row.
+inline std::vector<FeatGroup> equal_groups4(int n) {
+  std::vector<FeatGroup> out;
+  if (n <= 0) return out;
+  const int ng = std::max(1, (n + 63) / 64);
+  const int fg = std::min(64, ((n + ng - 1) / ng + 3) / 4 * 4);
   for (int gi = 0; gi * fg < n; ++gi) out.push_back(FeatGroup{gi * fg, std::min(fg, n - gi * fg), false, false});
   return out;
 }
@@ -320,7 +332,16 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     split_n_multi = n_multi > 0 ? n_multi : -1;
     if (BK::kGPU && n_multi > 0) live_dense = (int64_t)n_multi * a.B * a.S;
     perm_feats.insert(perm_feats.end(), one.begin() + o0, one.begin() + o1);
-    for (const FeatGroup& g : equal_groups(n_multi)) full_groups.push_back(g);
+    const char* wenv = std::getenv("TMOG_HIST_WIDE");
+    const bool wide_ok = BK::kGPU && a.mode == 2 && S == 2 && F % 4 == 0 && !(wenv && wenv[0] == '0');
+    for (FeatGroup g : (wide_ok ? equal_groups4(n_multi) : equal_groups(n_multi))) {
+      if (wide_ok) {
+        bool ok = perm_feats[g.f0] % 4 == 0;
+        for (int i = 1; ok && i < g.nf; ++i) ok = perm_feats[g.f0 + i] == perm_feats[g.f0] + i;
+        g.wide = ok;
+      }
+      full_groups.push_back(g);
+    }
     const int n_one = o1 - o0;
     if (BK::kGPU && a.csr_ptr && a.csr_col && n_multi > 0 && n_one > 0 && a.csr_nf == n_one &&
         2 * n_one + 2 <= 64 * (B * S + 1))
@@ -479,7 +500,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
             h.node = j;
             h.fg0 = fgp.f0;
             h.nf = fgp.nf;
-            h.excl = (nit == 1 ? 1 : 0) | (fgp.reg ? 2 : 0) | (fgp.csr ? 4 : 0) |
+            h.excl = (nit == 1 ? 1 : 0) | (fgp.reg ? 2 : 0) | (fgp.csr ? 4 : 0) | (fgp.wide ? 16 : 0) |
                      ((fgp.reg || fgp.csr) && live_dense >= 0 ? 8 : 0) | (sc << 8);
             h.begin = nb[j] + c * step;
             h.count = std::min(step, cnt - c * step);

@@ -205,6 +205,119 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
   }
 }
 
+
+// Wide-load path (MODE 2, excl bit 4): a dense group of FG <= 64 multi-bin columns that are physically
+// contiguous and dword aligned in Xb (col0 % 4 == 0, row stride % 4 == 0; the XGBoost learner pads its
+// growth-order matrix to that). Lane (rs, d) loads dword d of the group's row segment -- 4 bins of one
+// row in one 4-byte load -- so a wave-instruction covers 64 / ceil(FG/4) rows (4 for FG = 64) and
+// kWideU instructions keep 4x the bytes of the byte-gather path in flight for the same registers (the
+// kernel is gather-latency bound: MI355X_MICROARCH.md "72 KiB in flight per CU"). The statistics are
+// packed as one 64-bit word (q(g) << 32) + q(h) per (feature, bin) -- h >= 0 and its per-item sum stays
+// below 2^31 (qmax), so the low half never carries -- and added with ONE ds_add_u64 instead of two
+// ds_add_u32. Output is identical (integer sums) to the byte path and the CPU twin.
+constexpr int kWideU = 16;
+
+__device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t* __restrict__ Xb, int F, int col0,
+                                               const uint32_t* __restrict__ rows,
+                                               const int32_t* __restrict__ node_model,
+                                               const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
+                                               int B, const float* __restrict__ t1, const float* __restrict__ t2,
+                                               int64_t stride, const float* __restrict__ qscale, int skip_bin,
+                                               int* lds) {
+  const int FG = it.nf;
+  const int ND = (FG + 3) >> 2;
+  const int RPI = 64 / ND;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const int rs = lane / ND, d = lane - rs * ND;
+  const bool active = rs < RPI;
+  const int tstride = B + 1;                       // bin B: missing-bin value recovered at the end
+  unsigned long long* tab = reinterpret_cast<unsigned long long*>(lds);
+  const int twords = FG * tstride;
+  const int toff = (2 * twords + 3) & ~3;
+  int4* stage = reinterpret_cast<int4*>(lds + toff) + wave * 64;
+  int* tot = lds + toff + 4 * 64 * nwaves;
+  for (int i = threadIdx.x; i < twords; i += blockDim.x) tab[i] = 0ull;
+  if (threadIdx.x < 2) tot[threadIdx.x] = 0;
+  __syncthreads();
+  const bool sparse = skip_bin >= 0;
+  const int64_t model = node_model ? node_model[it.node] : 0;
+  const float* qs = qscale + model * 2;
+  const uint32_t* rp = rows + it.begin;
+  const int64_t cnt = it.count;
+  const uint8_t* xb0 = Xb + col0 + 4 * d;
+  for (int64_t base = (int64_t)wave * 64; base < cnt; base += (int64_t)nwaves * 64) {
+    const int64_t ri = min(base + lane, cnt - 1);
+    const int nrows = (int)min((int64_t)64, cnt - base);
+    const int4 mine = stage_row<2>(rp[ri], model, stride, nullptr, t1, t2, qs);
+    stage[lane] = mine;
+    if (sparse) {
+      int a = lane < nrows ? mine.y : 0, b = lane < nrows ? mine.z : 0;
+      for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off, 64);
+        b += __shfl_xor(b, off, 64);
+      }
+      if (lane == 0) {
+        atomicAdd(tot, a);
+        atomicAdd(tot + 1, b);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0): staged records visible to the wave
+    __builtin_amdgcn_wave_barrier();
+    for (int j0 = 0; j0 < nrows; j0 += RPI * kWideU) {
+      int4 st[kWideU];
+      uint32_t w[kWideU];
+#pragma unroll
+      for (int u = 0; u < kWideU; ++u) st[u] = stage[min(j0 + u * RPI + rs, 63)];
+#pragma unroll
+      for (int u = 0; u < kWideU; ++u)
+        w[u] = *reinterpret_cast<const uint32_t*>(xb0 + (int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F);
+#pragma unroll
+      for (int u = 0; u < kWideU; ++u) {
+        if (!active || j0 + u * RPI + rs >= nrows) continue;
+        const unsigned long long pk = ((unsigned long long)(uint32_t)st[u].y << 32) +
+                                      (unsigned long long)(uint32_t)st[u].z;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int f = 4 * d + k;
+          const int bin = (int)((w[u] >> (8 * k)) & 0xFFu);
+          if (f < FG && bin != skip_bin) atomicAdd(tab + f * tstride + bin, pk);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if (sparse) {       // missing bin = chunk totals - the other bins, packed into the pad slot
+    for (int f = threadIdx.x; f < FG; f += blockDim.x) {
+      long long g = 0, h = 0;
+      for (int b = 0; b < B; ++b) {
+        if (b == skip_bin) continue;
+        const unsigned long long v = tab[f * tstride + b];
+        g += (long long)v >> 32;
+        h += (long long)(v & 0xFFFFFFFFull);
+      }
+      const long long mg = (long long)tot[0] - g, mh = (long long)tot[1] - h;
+      tab[f * tstride + B] = ((unsigned long long)mg << 32) + (unsigned long long)(uint32_t)mh;
+    }
+    __syncthreads();
+  }
+  int64_t* out = hist + node_hist_off[it.node] + (int64_t)it.fg0 * B * 2;
+  const bool excl = (it.excl & 1) != 0;
+  for (int k = threadIdx.x; k < FG * B; k += blockDim.x) {
+    const int f = k / B, b = k - f * B;
+    const unsigned long long v = tab[f * tstride + ((sparse && b == skip_bin) ? B : b)];
+    const int64_t g = (long long)v >> 32, h = (long long)(v & 0xFFFFFFFFull);
+    int64_t* o = out + (int64_t)k * 2;
+    if (excl) {
+      o[0] = g;
+      o[1] = h;
+    } else {
+      if (g != 0) atomicAdd(reinterpret_cast<unsigned long long*>(o), (unsigned long long)g);
+      if (h != 0) atomicAdd(reinterpret_cast<unsigned long long*>(o + 1), (unsigned long long)h);
+    }
+  }
+}
+
 constexpr int HIST_U = 16;   // row bins gathered per lane before their LDS atomics (loads in flight)
 
 template <int MODE>
@@ -222,6 +335,11 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   if (MODE == 2 && (it.excl & 4)) {
     hist_csr_item(it, rows, node_model, node_hist_off, hist, B, S, t1, t2, stride, qscale, skip_bin, csr_ptr,
                   csr_col, lds);
+    return;
+  }
+  if (MODE == 2 && (it.excl & 16)) {
+    hist_wide_item(it, Xb, F, feat_list[node_feat_off[it.node] + it.fg0], rows, node_model, node_hist_off, hist, B,
+                   t1, t2, stride, qscale, skip_bin, lds);
     return;
   }
   const int FG = it.nf;
@@ -1096,8 +1214,12 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, hipStream_t stream) {
   if (n_items == 0) return 0;
   if (Sc <= 0 || Sc > S) Sc = S;
-  const size_t lds = (size_t)(((64 * (B * Sc + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
-                     TM_MAX_S * sizeof(int);
+  size_t lds = (size_t)(((64 * (B * Sc + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
+               TM_MAX_S * sizeof(int);
+  if (mode == 2 && S == 2) {   // wide-load items: 64 features x (B + 1) packed int64 words + stage + totals
+    const size_t wl = (size_t)((2 * 64 * (B + 1) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) + 4 * sizeof(int);
+    if (wl > lds) lds = wl;
+  }
   if (lds > 160 * 1024) return -2;
   if (skip_bin >= B || (mode == 2 && skip_bin >= 0 && (S != 2 || Sc != S))) return -2;
   if (mode == 0 && S > TM_WIDE_MAX_S) return -2;
