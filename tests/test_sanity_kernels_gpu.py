@@ -103,3 +103,22 @@ def test_sanity_checker_device_matches_host():
     np.testing.assert_allclose(cd, ch, rtol=1e-5, atol=1e-6)
     for a, b in zip(h["categoricalStats"], d["categoricalStats"]):
         np.testing.assert_allclose(b["cramersV"], a["cramersV"], rtol=1e-6, atol=1e-9)
+
+
+def test_class_column_sums_and_naive_bayes_on_device():
+    g = torch.Generator().manual_seed(8)
+    n, d = 70_001, 150
+    X = (torch.rand(n, d, generator=g) * 3).floor().to(torch.float32)
+    codes = torch.randint(-1, 4, (3, n), generator=g).to(torch.int32)
+    ref = ST.class_column_sums(X, codes, 4)
+    got = ST.class_column_sums(X.cuda(), codes.cuda(), 4).cpu()
+    torch.testing.assert_close(got, ref, rtol=0, atol=0)        # integer data: exact
+    from transmogrifai_amd.models.base import FitJob
+    from transmogrifai_amd.models.linear import NaiveBayesLearner
+    y = torch.randint(0, 3, (n,), generator=g).to(torch.float32)
+    jobs = [FitJob({"smoothing": 1.0}, torch.arange(0, n, 2)), FitJob({"smoothing": 0.5}, torch.arange(1, n, 3))]
+    sh = NaiveBayesLearner().fit_batch(X, y, jobs)
+    sd = NaiveBayesLearner().fit_batch(X.cuda(), y.cuda(), [FitJob(j.params, j.rows.cuda()) for j in jobs])
+    for a, b in zip(sh, sd):
+        np.testing.assert_allclose(b["theta"], a["theta"], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(b["pi"], a["pi"], rtol=1e-12, atol=1e-12)

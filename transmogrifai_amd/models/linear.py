@@ -492,18 +492,25 @@ class NaiveBayesLearner(Learner):
     defaults = {"smoothing": 1.0, "model_type": "multinomial"}
 
     def fit_batch(self, X, y, jobs, context=None):
+        from ..ops.stats import class_column_sums
         out = []
         K = int(y.max().item()) + 1 if y.numel() else 2
         K = max(K, 2)
-        for j in jobs:
-            Xr = X if j.rows is None else X[j.rows]
-            yr = (y if j.rows is None else y[j.rows]).long()
-            if (Xr < 0).any():
-                raise ValueError("Naive Bayes requires nonnegative feature values")
+        if bool((X < 0).any()):
+            raise ValueError("Naive Bayes requires nonnegative feature values")
+        # every job's class feature sums in one pass over X: codes[p, r] = class of row r in job p, -1 if
+        # the row is not in the job (HIP class_colsum_kernel)
+        n = X.shape[0]
+        codes = torch.full((len(jobs), n), -1, dtype=torch.int32, device=X.device)
+        yl = y.long()
+        for k, j in enumerate(jobs):
+            r = torch.arange(n, device=X.device) if j.rows is None else j.rows.to(X.device)
+            codes[k, r] = yl[r].to(torch.int32)
+        FS = class_column_sums(X, codes, K)                          # [P, K, d]
+        for k, j in enumerate(jobs):
             lam = float(j.params.get("smoothing", 1.0))
-            Y = torch.nn.functional.one_hot(yr, K).to(torch.float64)
-            cnt = Y.sum(0)
-            fs = LK.gemm_t(Xr.to(torch.float64), Y)                  # [d, K] class feature sums
+            cnt = torch.bincount(codes[k][codes[k] >= 0].long(), minlength=K).to(torch.float64)
+            fs = FS[k].t()                                           # [d, K] class feature sums
             pi = torch.log(cnt + lam) - math.log(float(cnt.sum()) + K * lam)
             if j.params.get("model_type", "multinomial") == "bernoulli":
                 theta = torch.log(fs + lam) - torch.log(cnt + 2 * lam)[None, :]

@@ -182,9 +182,77 @@ __global__ void __launch_bounds__(256) gram_fold_kernel(const double* __restrict
   }
 }
 
+// Per-problem, per-class column sums (the label x column contingency and the
+// NaiveBayes class feature sums): part[chunk][p * L + c][j] = sum of X[r][j] over rows r of the chunk with
+// codes[p][r] == c (-1 = row not in problem p). Lane = column (64 per workgroup), wave = row stride; every
+// wave keeps private fp64 accumulators in LDS, summed in a fixed order -- no atomics, deterministic.
+__global__ void __launch_bounds__(256) class_colsum_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ld,
+                                                           const int32_t* __restrict__ codes, int P, int L,
+                                                           int64_t rows_per_chunk, double* __restrict__ part) {
+  extern __shared__ double acc[];                 // [4 waves][P * L][64]
+  const int PL = P * L;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  double* my = acc + (size_t)wave * PL * 64;
+  for (int k = 0; k < PL; ++k) my[k * 64 + lane] = 0.0;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = min(n, r0 + rows_per_chunk);
+  if (j < d) {
+    for (int64_t r = r0 + wave; r < r1; r += 4) {
+      const double v = (double)X[r * ld + j];
+      for (int p = 0; p < P; ++p) {
+        const int c = codes[(int64_t)p * n + r];
+        if (c >= 0 && c < L) my[(p * L + c) * 64 + lane] += v;
+      }
+    }
+  }
+  __syncthreads();
+  if (wave == 0 && j < d) {
+    double* out = part + (int64_t)blockIdx.y * PL * d;
+    for (int k = 0; k < PL; ++k) {
+      double t = 0.0;
+      for (int w = 0; w < 4; ++w) t += acc[((size_t)w * PL + k) * 64 + lane];
+      out[(int64_t)k * d + j] = t;
+    }
+  }
+}
+
+__global__ void colsum_fold_kernel(const double* __restrict__ part, int chunks, int64_t words,
+                                   double* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= words) return;
+  double t = 0.0;
+  for (int c = 0; c < chunks; ++c) t += part[(int64_t)c * words + k];
+  out[k] = t;
+}
+
 }  // namespace
 
 extern "C" {
+
+// out[p][c][j] (fp64, P*L*d) = sum over rows with codes[p][row] == c of X[row][j]; P * L <= 64.
+int tmog_hip_class_colsum(const float* X, int64_t n, int d, int64_t ld, const int32_t* codes, int P, int L, double* out,
+                          hipStream_t stream) {
+  if (n <= 0 || d <= 0 || P <= 0 || L <= 0) return -1;
+  if (P * L > 64) return -2;
+  const int cblocks = (d + 63) / 64;
+  int64_t chunks = (1024 + cblocks - 1) / cblocks;
+  if (chunks > (n + 255) / 256) chunks = (n + 255) / 256;
+  if (chunks < 1) chunks = 1;
+  const int64_t rpc = (n + chunks - 1) / chunks;
+  chunks = (n + rpc - 1) / rpc;
+  const int64_t words = (int64_t)P * L * d;
+  double* part = nullptr;
+  hipError_t e = hipMallocAsync((void**)&part, sizeof(double) * words * chunks, stream);
+  if (e != hipSuccess) return (int)e;
+  const size_t lds = (size_t)4 * P * L * 64 * sizeof(double);
+  hipLaunchKernelGGL(class_colsum_kernel, dim3(cblocks, (unsigned)chunks), dim3(256), lds, stream, X, n, d, ld, codes, P,
+                     L, rpc, part);
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, stream, part, (int)chunks,
+                     words, out);
+  hipFreeAsync(part, stream);
+  return (int)hipGetLastError();
+}
 
 int tmog_hip_col_stats(const float* X, const void* unused, int64_t n, int d, int64_t ld, double* out,
                        hipStream_t stream) {

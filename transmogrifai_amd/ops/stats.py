@@ -177,6 +177,28 @@ def corr_and_label_sums(X: torch.Tensor, y: torch.Tensor, mean: torch.Tensor, mn
     return C, labels, sums, counts
 
 
+def class_column_sums(X: torch.Tensor, codes: torch.Tensor, n_classes: int) -> torch.Tensor:
+    """``[P, L, d]`` fp64 sums of the rows of ``X`` per problem ``p`` and class ``c`` (``codes[p, r] == c``;
+    -1 leaves row r out of problem p): the label x column contingency / NaiveBayes class feature sums.
+    fp32 device data with ``P * L <= 64`` runs the deterministic HIP ``class_colsum_kernel``."""
+    P, n = codes.shape
+    d = X.shape[1]
+    L = int(n_classes)
+    if X.is_cuda and X.dtype == torch.float32 and X.stride(1) == 1 and n > 0 and P * L <= 64:
+        out = torch.empty(P, L, d, dtype=torch.float64, device=X.device)
+        cd = codes.to(device=X.device, dtype=torch.int32).contiguous()
+        N.check(N.hip().tmog_hip_class_colsum(N.ptr(X), n, d, X.stride(0), N.ptr(cd), P, L, N.ptr(out),
+                                              N.stream(X.device)), "class_colsum")
+        return out
+    Xd = X.to(torch.float64)
+    out = torch.zeros(P, L, d, dtype=torch.float64, device=X.device)
+    for p in range(P):
+        c = codes[p].to(X.device).long()
+        m = c >= 0
+        out[p].index_add_(0, c[m], Xd[m])
+    return out
+
+
 def label_column_sums(X: torch.Tensor, y: torch.Tensor):
     """(sorted distinct labels, ``[L, d]`` per-label column sums, ``[L]`` counts): the skinny GEMM
     ``onehot(y)^T X``. Row-sharded fits use the global label set and all-reduce the sums
@@ -185,7 +207,7 @@ def label_column_sums(X: torch.Tensor, y: torch.Tensor):
     labels = dp.unique_values(y.to(torch.float64))
     inv = torch.searchsorted(labels, y.to(torch.float64))
     L = labels.numel()
-    oh = torch.zeros(X.shape[0], L, dtype=X.dtype, device=X.device)
-    oh[torch.arange(X.shape[0], device=X.device), inv] = 1
-    sums, cnt = dp.sum_([(oh.t() @ X).to(torch.float64), oh.sum(0).to(torch.float64)])
+    sums = class_column_sums(X, inv[None, :], L)[0]
+    cnt = torch.bincount(inv, minlength=L).to(torch.float64)
+    sums, cnt = dp.sum_([sums, cnt])
     return labels, sums, cnt
