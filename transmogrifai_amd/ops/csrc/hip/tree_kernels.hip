@@ -232,7 +232,11 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
   const bool active = rs < RPI;
   const int tstride = B + 1;                       // bin B: missing-bin value recovered at the end
   unsigned long long* tab = reinterpret_cast<unsigned long long*>(lds);
-  const int twords = FG * tstride;
+  // feature f's row starts at f * tstride + f / 4: the extra word per 4 features moves consecutive lanes
+  // (dword d = features 4d..4d+3) to distinct LDS banks for the 64-bit atomics (8 * tstride alone is
+  // 0 mod 8 dwords for any B, a 4-way conflict)
+  auto tix = [tstride](int f, int b) { return f * tstride + (f >> 2) + b; };
+  const int twords = FG * tstride + (FG >> 2) + 1;
   const int toff = (2 * twords + 3) & ~3;
   int4* stage = reinterpret_cast<int4*>(lds + toff) + wave * 64;
   int* tot = lds + toff + 4 * 64 * nwaves;
@@ -280,7 +284,7 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
         for (int k = 0; k < 4; ++k) {
           const int f = 4 * d + k;
           const int bin = (int)((w[u] >> (8 * k)) & 0xFFu);
-          if (f < FG && bin != skip_bin) atomicAdd(tab + f * tstride + bin, pk);
+          if (f < FG && bin != skip_bin) atomicAdd(tab + tix(f, bin), pk);
         }
       }
     }
@@ -292,12 +296,12 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
       long long g = 0, h = 0;
       for (int b = 0; b < B; ++b) {
         if (b == skip_bin) continue;
-        const unsigned long long v = tab[f * tstride + b];
+        const unsigned long long v = tab[tix(f, b)];
         g += (long long)v >> 32;
         h += (long long)(v & 0xFFFFFFFFull);
       }
       const long long mg = (long long)tot[0] - g, mh = (long long)tot[1] - h;
-      tab[f * tstride + B] = ((unsigned long long)mg << 32) + (unsigned long long)(uint32_t)mh;
+      tab[tix(f, B)] = ((unsigned long long)mg << 32) + (unsigned long long)(uint32_t)mh;
     }
     __syncthreads();
   }
@@ -305,7 +309,7 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
   const bool excl = (it.excl & 1) != 0;
   for (int k = threadIdx.x; k < FG * B; k += blockDim.x) {
     const int f = k / B, b = k - f * B;
-    const unsigned long long v = tab[f * tstride + ((sparse && b == skip_bin) ? B : b)];
+    const unsigned long long v = tab[tix(f, (sparse && b == skip_bin) ? B : b)];
     const int64_t g = (long long)v >> 32, h = (long long)(v & 0xFFFFFFFFull);
     int64_t* o = out + (int64_t)k * 2;
     if (excl) {
@@ -1217,7 +1221,8 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
   size_t lds = (size_t)(((64 * (B * Sc + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
                TM_MAX_S * sizeof(int);
   if (mode == 2 && S == 2) {   // wide-load items: 64 features x (B + 1) packed int64 words + stage + totals
-    const size_t wl = (size_t)((2 * 64 * (B + 1) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) + 4 * sizeof(int);
+    const size_t wl = (size_t)((2 * (64 * (B + 1) + 17) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
+                      4 * sizeof(int);
     if (wl > lds) lds = wl;
   }
   if (lds > 160 * 1024) return -2;
