@@ -104,3 +104,34 @@ def test_project_generator_runs(tmp_path):
     assert os.path.isdir(tmp_path / "gm" / "op-model.json")
     with pytest.raises(FileExistsError):
         generate(path, "y", "id", "Demo", str(tmp_path / "out"))
+
+
+def test_runner_collects_stage_metrics(tmp_path):
+    """AppMetrics carries per-stage metrics like OpSparkListener's StageMetrics / CumulativeStageMetrics."""
+    import json
+    from transmogrifai_amd.readers.base import InMemoryReader
+    from transmogrifai_amd.testkit.synthetic import binary_table
+    from transmogrifai_amd.dsl import transmogrify
+    from transmogrifai_amd.selector.factories import BinaryClassificationModelSelector
+    from transmogrifai_amd.workflow.params import OpParams
+    from transmogrifai_amd.workflow.runner import OpWorkflowRunner
+    from transmogrifai_amd.workflow.workflow import OpWorkflow
+    ds, label, preds = binary_table(2000, n_real=4, n_int=1, n_pick=1, seed=2)
+    vec = transmogrify(preds)
+    pred = BinaryClassificationModelSelector.with_cross_validation(
+        num_folds=2, seed=1, model_types_to_use=["OpLogisticRegression"]).set_input(label, vec).get_output()
+    wf = OpWorkflow().set_result_features(label, pred)
+    runner = OpWorkflowRunner(wf, training_reader=InMemoryReader(ds))
+    params = OpParams(model_location=str(tmp_path / "m"), metrics_location=str(tmp_path / "x"),
+                      collect_stage_metrics=True, log_stage_metrics=True)
+    res = runner.run("train", params)
+    sm = res.metrics.stageMetrics
+    names = {s["stageName"].split("_")[0] for s in sm}
+    assert {"vecReal", "combVec", "modelSelection"} <= names
+    assert all(s["durationSecs"] >= 0 and s["numRows"] > 0 for s in sm)
+    assert {s["phase"] for s in sm} == {"fit", "transform"}
+    assert any(s["jobGroup"] == "FeatureEngineering" for s in sm)
+    cum = res.metrics.cumulativeStageMetrics
+    assert cum["numStages"] == len(sm)
+    saved = json.load(open(tmp_path / "x" / "app_metrics.json"))
+    assert saved["versionInfo"]["version"] and len(saved["stageMetrics"]) == len(sm)

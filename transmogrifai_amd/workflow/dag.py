@@ -105,13 +105,15 @@ def _mem_mark(timings, what):
 
 
 def _fit_layer_with_eval(layer, train, test, timings, li=0, last=None, keep=None):
+    from ..utils import listener as L
     fitted = []
     for st, _ in layer:
         t0 = time.time()
         if isinstance(st, OpEstimator):
-            m = st.fit(train)
-            if test is not None and len(test) > 0 and hasattr(m, "evaluate_model"):
-                m.evaluate_model(test)
+            with L.stage(st.stage_name(), "fit", len(train)):
+                m = st.fit(train)
+                if test is not None and len(test) > 0 and hasattr(m, "evaluate_model"):
+                    m.evaluate_model(test)
             fitted.append(m)
         else:
             fitted.append(st)
@@ -120,9 +122,10 @@ def _fit_layer_with_eval(layer, train, test, timings, li=0, last=None, keep=None
         _mem_mark(timings, f"fit:{st.stage_name()}")
     for si, m in enumerate(fitted):
         t0 = time.time()
-        train = m.transform(train)
-        if test is not None and len(test) > 0:
-            test = m.transform(test)
+        with L.stage(m.stage_name(), "transform", len(train) + (len(test) if test is not None else 0)):
+            train = m.transform(train)
+            if test is not None and len(test) > 0:
+                test = m.transform(test)
         if keep is not None and last:
             dead = [n for n, pos in last.items() if pos == (li, si) and n not in keep]
             if dead:

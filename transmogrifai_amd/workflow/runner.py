@@ -45,6 +45,9 @@ class AppMetrics:
     appDurationSecs: float = 0.0
     stepTimings: Dict[str, Any] = field(default_factory=dict)
     deviceMaxMemoryBytes: Optional[int] = None
+    stageMetrics: List[Dict[str, Any]] = field(default_factory=list)
+    cumulativeStageMetrics: Dict[str, Any] = field(default_factory=dict)
+    versionInfo: Dict[str, Any] = field(default_factory=dict)
     customTagName: Optional[str] = None
     customTagValue: Optional[str] = None
 
@@ -282,7 +285,15 @@ class OpWorkflowRunner:
         fn = {OpWorkflowRunType.Train: self._train, OpWorkflowRunType.Score: self._score,
               OpWorkflowRunType.StreamingScore: self._streaming_score, OpWorkflowRunType.Features: self._features,
               OpWorkflowRunType.Evaluate: self._evaluate}[rt]
-        res = fn(params, m)
+        from ..utils import listener as LS
+        from ..utils.version import version_info
+        lst = LS.OpDeviceListener(self.app_name, rt, params.custom_tag_name, params.custom_tag_value,
+                                  bool(params.log_stage_metrics), params.collect_stage_metrics is not False)
+        with LS.listening(lst):
+            res = fn(params, m)
+        lj = lst.to_json()
+        m.stageMetrics, m.cumulativeStageMetrics = lj["stageMetrics"], lj["cumulativeStageMetrics"]
+        m.versionInfo = version_info().to_dict()
         m.appEndTime = time.time()
         m.appDurationSecs = m.appEndTime - m.appStartTime
         if torch.cuda.is_available():

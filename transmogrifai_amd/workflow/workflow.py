@@ -37,13 +37,20 @@ class OpStep:
 
 
 class _Timer:
+    """Wall time of a workflow step (``OpStep``) into ``sink``; the step is also the job group of the stage
+    metrics an active listener collects meanwhile (``utils/listener.py``)."""
+
     def __init__(self, sink: Dict[str, float], name: str):
         self.sink, self.name = sink, name
 
     def __enter__(self):
+        from ..utils import listener as L
         self.t = time.time()
+        self.jg = L.job_group(str(self.name))
+        self.jg.__enter__()
 
     def __exit__(self, *a):
+        self.jg.__exit__(*a)
         self.sink[self.name] = self.sink.get(self.name, 0.0) + time.time() - self.t
 
 
