@@ -90,6 +90,7 @@ _HIP_SIGS = {
     "tmog_hip_gram_aug": [P, I64, I32, I64, P, P, I32, P, P],
     "tmog_hip_class_colsum": [P, I64, I32, I64, P, I32, I32, P, P],
     "tmog_hip_logistic_grad": [P, P, P, I64, I32, P],
+    "tmog_hip_debug_flags": [I32],
     "tmog_hip_gather_rows_cols": [P, P, P, I64, I32, P, P],
     "tmog_hip_hash_tokens": [P, P, I64, P, I32, I32, I32, I32, P, P],
     "tmog_hip_hash_tf_rows": [P, I32, I64, I32, I32, P, I64, I64, P],
@@ -146,6 +147,9 @@ def hip():
                 torch.cuda.init()
                 lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
                 _declare(lib, _HIP_SIGS)
+                dbg = int(os.environ.get("TMOG_HIST_DEBUG", "0"))
+                if dbg:
+                    lib.tmog_hip_debug_flags(dbg)
                 _hip = lib
     return _hip
 

@@ -324,6 +324,10 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
 
 constexpr int HIST_U = 16;   // row bins gathered per lane before their LDS atomics (loads in flight)
 
+// Diagnostics only (tmog_hip_debug_flags, TMOG_HIST_DEBUG): bit 0 skips CSR items, bit 1 skips wide /
+// dense multi-bin items -- the trees are then wrong; used to time the item kinds separately.
+__device__ int g_hist_debug = 0;
+
 template <int MODE>
 __global__ void __launch_bounds__(256) hist_build_kernel(
     const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const HistItem* __restrict__ items,
@@ -336,6 +340,10 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   const HistItem it = items[blockIdx.x];
   const int s0 = ((it.excl >> 8) & 0xFF) * Sc;   // statistic chunk of this item (excl bits 8..15)
   const int sc = min(Sc, S - s0);
+  if (MODE == 2 && g_hist_debug) {
+    if ((g_hist_debug & 1) && (it.excl & 4)) return;
+    if ((g_hist_debug & 2) && !(it.excl & 4)) return;
+  }
   if (MODE == 2 && (it.excl & 4)) {
     hist_csr_item(it, rows, node_model, node_hist_off, hist, B, S, t1, t2, stride, qscale, skip_bin, csr_ptr,
                   csr_col, lds);
@@ -1210,6 +1218,10 @@ __global__ void __launch_bounds__(256) forest_predict_kernel(
 
 // ------------------------------------------------------------------------------------- C ABI
 extern "C" {
+
+int tmog_hip_debug_flags(int flags) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_hist_debug), &flags, sizeof(int));
+}
 
 int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
