@@ -391,33 +391,10 @@ class OpIndexToString(UnaryTransformer):
 
 
 # ---------------------------------------------------------------------------------- NLP detectors
-_LANG_WORDS = {
-    "en": "the of and to in is that it was for on are with as his they be at one have this from",
-    "fr": "le la les de des et un une est que qui dans pour pas sur au avec il elle nous vous",
-    "de": "der die das und ist nicht ein eine zu den mit von sie es ich auf auch dem des",
-    "es": "el la los las de y que en un una es por con para no se su al lo como",
-    "it": "il lo la gli le di e che un una non per con sono nel della sul anche come",
-    "pt": "o a os as de e que em um uma não para com por se na no mais como",
-    "nl": "de het een en van is dat niet te op zijn met voor er aan ook als",
-    "sv": "och att det som en på är av för med till den inte har de ett om",
-    "da": "og at det som en på er af for med til den ikke har de et om",
-    "pl": "i w nie na się z że do jest to jak o po ale co tak",
-}
-_LANG = {k: set(v.split()) for k, v in _LANG_WORDS.items()}
-
-
 def detect_languages(text: Optional[str]) -> Dict[str, float]:
-    """Stop-word profile language identification -> {language: confidence} (Optimaize replacement)."""
-    if not text:
-        return {}
-    toks = TU.tokenize(text, stopwords=frozenset())
-    if not toks:
-        return {}
-    hits = {lang: sum(1 for t in toks if t in words) for lang, words in _LANG.items()}
-    tot = sum(hits.values())
-    if tot == 0:
-        return {}
-    return {l: h / tot for l, h in sorted(hits.items(), key=lambda kv: -kv[1]) if h > 0}
+    """Language identification -> {language: confidence} (Optimaize replacement, ``utils/lang.py``)."""
+    from ...utils.lang import detect_languages as _dl
+    return _dl(text)
 
 
 @register_stage

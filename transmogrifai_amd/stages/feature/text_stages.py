@@ -180,20 +180,35 @@ class TextTokenizer(UnaryTransformer):
     operation_name = "textToken"
     output_type = T.TextList
     _defaults = {"to_lowercase": True, "min_token_length": 1, "auto_detect_language": False,
-                 "strip_html": False, "default_language": "Unknown"}
+                 "strip_html": False, "default_language": "Unknown", "auto_detect_threshold": 0.99}
+
+    def _language_aware(self) -> bool:
+        p = self.params
+        return bool(p["auto_detect_language"]) or p["default_language"] not in ("Unknown", None, "en")
 
     def transform_fn(self, v):
         if v is None:
             return []
-        s = TU.strip_html(v) if self.params["strip_html"] else v
-        return TU.tokenize(s, self.params["to_lowercase"], self.params["min_token_length"])
+        p = self.params
+        s = TU.strip_html(v) if p["strip_html"] else v
+        if self._language_aware():
+            # TextTokenizer.scala:160-188: detected language above the threshold, else the default; its
+            # analyzer (utils/lang.py: stop words + elisions of that language)
+            from ...utils import lang as LG
+            lang = LG.best_language(s, float(p["auto_detect_threshold"]), p["default_language"]) \
+                if p["auto_detect_language"] else p["default_language"]
+            return LG.analyze(s, lang, p["to_lowercase"], p["min_token_length"])
+        return TU.tokenize(s, p["to_lowercase"], p["min_token_length"])
 
     def transform_columns(self, *cols, ds=None):
         c = cols[0]
         if isinstance(c, TextColumn):
             p = self.params
-            vocab = [TU.strip_html(s) for s in c.vocab] if p["strip_html"] else c.vocab
-            toks = TU.tokenize_batch(vocab, p["to_lowercase"], p["min_token_length"]).lists()
+            if self._language_aware():
+                toks = [self.transform_fn(s) for s in c.vocab]
+            else:
+                vocab = [TU.strip_html(s) for s in c.vocab] if p["strip_html"] else c.vocab
+                toks = TU.tokenize_batch(vocab, p["to_lowercase"], p["min_token_length"]).lists()
             codes = c.codes.cpu().numpy()
             out = np.empty(len(codes), dtype=object)
             for i, k in enumerate(codes):

@@ -1,0 +1,155 @@
+"""Language identification and language-aware analysis (replaces Optimaize ``LanguageDetector`` and the
+per-language Lucene analyzers of ``LuceneTextAnalyzer.scala:87-236``; SURVEY.md L0 text interfaces).
+
+* :func:`detect_languages` -- ``{ISO 639-1 code: confidence}``. Text in a non-Latin script is identified
+  by its script (Cyrillic with Ukrainian letters -> uk, else ru; Greek, Arabic (Persian letters -> fa),
+  Hebrew, Devanagari, Thai, Hangul, kana -> ja, Han only -> zh); Latin-script text by the share of
+  each language's most frequent function words among its tokens (a stop-word profile in place of
+  Optimaize's n-gram profiles, which are not available offline).
+* :func:`analyze` -- the reference's per-language analysis minus stemming: the language's stop words,
+  elision stripping for French / Italian / Catalan (``l'amour`` -> ``amour``, Lucene ElisionFilter),
+  on top of the StandardAnalyzer word rules of :func:`utils.text.analyze`.
+"""
+from __future__ import annotations
+
+import unicodedata
+from typing import Dict, FrozenSet, List, Optional
+
+from . import text as TU
+
+UNKNOWN = "Unknown"
+
+_PROFILE = {
+    "en": "the of and to in is that it was for on are with as his they be at one have this from by not but "
+          "what all were we when your can said there use an each which she do how their if will",
+    "fr": "le la les de des et un une est que qui dans pour pas sur au avec il elle nous vous ce cette sont "
+          "du en aux ne se ses mais ou leur plus par je tu",
+    "de": "der die das und ist nicht ein eine zu den mit von sie es ich auf auch dem des sich im für wie "
+          "aber bei oder wir werden nach noch hat sind",
+    "es": "el la los las de y que en un una es por con para no se su al lo como del más pero sus le ya "
+          "o este fue ha muy sin sobre también",
+    "it": "il lo la gli le di e che un una non per con sono nel della sul anche come del dei ma si è ha "
+          "questo alla più era delle degli",
+    "pt": "o a os as de e que em um uma não para com por se na no mais como do da dos das ao foi são "
+          "ele ela mas tem seu sua",
+    "nl": "de het een en van is dat niet te op zijn met voor er aan ook als die maar om ik je bij naar "
+          "wordt heeft deze hij",
+    "sv": "och att det som en på är av för med till den inte har de ett om jag var sig men så kan vi "
+          "hade eller från",
+    "da": "og at det som en på er af for med til den ikke har de et om jeg var sig men så kan vi havde "
+          "eller fra",
+    "no": "og i det som en på er av for med til den ikke har de et om jeg var seg men så kan vi hadde "
+          "eller fra",
+    "pl": "i w nie na się z że do jest to jak o po ale co tak czy od już przez być jego",
+    "ca": "el la els les de i que en un una és per amb no es del al com més però dels",
+    "fi": "ja on ei se että oli hän olla mutta kun ovat tai jos niin myös kuin",
+    "tr": "ve bir bu da de için ile çok ama gibi daha olarak olan en ne var",
+    "ro": "și în de la cu nu o un care este pe din să se ca mai",
+}
+PROFILES: Dict[str, FrozenSet[str]] = {k: frozenset(v.split()) for k, v in _PROFILE.items()}
+
+# stop words of the per-language analyzers (English: Lucene's english_stop list of utils/text.py)
+STOPWORDS: Dict[str, FrozenSet[str]] = dict(PROFILES)
+STOPWORDS["en"] = TU.ENGLISH_STOPWORDS
+
+_ELISIONS = {"fr": ("l", "m", "t", "qu", "n", "s", "j", "d", "c", "jusqu", "quoiqu", "lorsqu", "puisqu"),
+             "it": ("c", "l", "all", "dall", "dell", "nell", "sull", "coll", "pell", "gl", "agl", "dagl",
+                    "degl", "negl", "sugl", "un", "m", "t", "s", "v", "d"),
+             "ca": ("d", "l", "m", "n", "s", "t")}
+
+
+def _script_counts(text: str) -> Dict[str, int]:
+    c: Dict[str, int] = {}
+    for ch in text:
+        o = ord(ch)
+        if o < 0x80:
+            if ch.isalpha():
+                c["Latin"] = c.get("Latin", 0) + 1
+            continue
+        if not ch.isalpha():
+            continue
+        if 0x3040 <= o <= 0x30FF:
+            s = "Kana"
+        elif 0xAC00 <= o <= 0xD7AF or 0x1100 <= o <= 0x11FF:
+            s = "Hangul"
+        elif 0x4E00 <= o <= 0x9FFF or 0x3400 <= o <= 0x4DBF:
+            s = "Han"
+        else:
+            try:
+                s = unicodedata.name(ch).split(" ")[0]
+            except ValueError:
+                continue
+        c[s] = c.get(s, 0) + 1
+    return c
+
+
+_ODDS = 4.0
+
+_SCRIPT_LANG = {"GREEK": "el", "HEBREW": "he", "DEVANAGARI": "hi", "THAI": "th", "Hangul": "ko", "BENGALI": "bn",
+                "ARMENIAN": "hy", "GEORGIAN": "ka", "TAMIL": "ta"}
+
+
+def detect_languages(text: Optional[str]) -> Dict[str, float]:
+    if not text:
+        return {}
+    sc = _script_counts(text)
+    letters = sum(sc.values())
+    if letters == 0:
+        return {}
+    latin = sc.get("LATIN", 0) + sc.get("Latin", 0)
+    out: Dict[str, float] = {}
+    if sc.get("Kana", 0):
+        out["ja"] = (sc["Kana"] + sc.get("Han", 0)) / letters
+    elif sc.get("Han", 0):
+        out["zh"] = sc["Han"] / letters
+    if sc.get("CYRILLIC", 0):
+        uk = any(ch in text for ch in "іїєґІЇЄҐ")
+        out["uk" if uk else "ru"] = sc["CYRILLIC"] / letters
+    if sc.get("ARABIC", 0):
+        fa = any(ch in text for ch in "پچژگ")
+        out["fa" if fa else "ar"] = sc["ARABIC"] / letters
+    for s, lang in _SCRIPT_LANG.items():
+        if sc.get(s, 0):
+            out[lang] = sc[s] / letters
+    if latin:
+        toks = TU.tokenize(text, stopwords=frozenset())
+        hits = {lang: sum(1 for t in toks if t in words) for lang, words in PROFILES.items()}
+        top = max(hits.values()) if hits else 0
+        if top:
+            # posterior of a naive token model: each profile hit multiplies a language's odds by _ODDS
+            share = latin / letters
+            w = {lang: _ODDS ** (h - top) for lang, h in hits.items() if h}
+            z = sum(w.values())
+            for lang, v in w.items():
+                out[lang] = out.get(lang, 0.0) + share * v / z
+    return dict(sorted(out.items(), key=lambda kv: -kv[1]))
+
+
+def best_language(text: Optional[str], threshold: float = 0.99, default: str = UNKNOWN) -> str:
+    """The top detected language when its confidence exceeds ``threshold``, else ``default``
+    (``TextTokenizer.tokenize`` with autoDetectLanguage, ``TextTokenizer.scala:168-176``)."""
+    langs = detect_languages(text)
+    if langs:
+        lang, conf = next(iter(langs.items()))
+        if conf > threshold:
+            return lang
+    return default
+
+
+def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_token_length: int = 1) -> List[str]:
+    """Per-language analysis: elision stripping (fr / it / ca), the language's stop words (English's for an
+    unknown language, as the reference's default StandardAnalyzer), StandardAnalyzer word rules."""
+    lang = language if language in STOPWORDS else "en"
+    toks = TU.tokenize(text, to_lowercase, 1, stopwords=frozenset())
+    el = _ELISIONS.get(lang)
+    if el:
+        out = []
+        for t in toks:
+            if "'" in t:
+                head, _, tail = t.partition("'")
+                if head in el and tail:
+                    t = tail
+            out.append(t)
+        toks = out
+    sw = STOPWORDS[lang]
+    return [t for t in toks if t not in sw and len(t) >= min_token_length]
