@@ -120,6 +120,61 @@ def _workflow_grid(rank, world):
 
 
 # ------------------------------------------------------------------------------------- tests
+def _events_records():
+    import random
+    r = random.Random(5)
+    return [{"k": f"u{r.randint(0, 40)}", "t": r.randint(0, 10_000), "amt": r.random() * 10,
+             "cat": r.choice(["a", "b", "c"])} for _ in range(600)]
+
+
+def _aggregate_shuffle(rank, world):
+    from transmogrifai_amd.features import aggregators as A
+    from transmogrifai_amd.features.builder import FeatureBuilder
+    from transmogrifai_amd.parallel import dist as D
+    from transmogrifai_amd.readers.aggregate import AggregateParams
+    from transmogrifai_amd.readers.files import DataReaders
+    # the all-to-all itself: rank r sends "r->k" to every k
+    got = D.all_to_all_bytes([f"{rank}->{k}".encode() for k in range(world)])
+    assert [g.decode() for g in got] == [f"{k}->{rank}" for k in range(world)]
+    amt = FeatureBuilder.Real("amt").extract(lambda e: e["amt"]).aggregate(A.SumNumeric()).as_predictor()
+    cat = FeatureBuilder.PickList("cat").extract(lambda e: e["cat"]).as_predictor()
+    rd = DataReaders.Aggregate.custom(_events_records(), key=lambda e: e["k"],
+                                      aggregate_params=AggregateParams(lambda e: e["t"],
+                                                                       A.CutOffTime.unix_epoch(6000)))
+    ds = rd.distribute().generate_dataset([amt, cat])
+    assert ds.sharded
+    return {"keys": [str(k) for k in ds.key], "amt": ds["amt"].to_list(), "cat": ds["cat"].to_list(),
+            "rid": ds.row_ids.tolist()}
+
+
+def test_keyed_shuffle_aggregate_reader_matches_single_process(tmp_path):
+    """C14: the aggregate reader shuffles events by key over the ranks (all-to-all) and each rank aggregates
+    the keys it owns; the union over ranks equals the single-process aggregation."""
+    from transmogrifai_amd.features import aggregators as A
+    from transmogrifai_amd.features.builder import FeatureBuilder
+    from transmogrifai_amd.readers.aggregate import AggregateParams
+    from transmogrifai_amd.readers.files import DataReaders
+    res = _run("_aggregate_shuffle", tmp_path)
+    amt = FeatureBuilder.Real("amt").extract(lambda e: e["amt"]).aggregate(A.SumNumeric()).as_predictor()
+    cat = FeatureBuilder.PickList("cat").extract(lambda e: e["cat"]).as_predictor()
+    ref = DataReaders.Aggregate.custom(_events_records(), key=lambda e: e["k"],
+                                       aggregate_params=AggregateParams(lambda e: e["t"],
+                                                                        A.CutOffTime.unix_epoch(6000))) \
+        .generate_dataset([amt, cat])
+    want = {str(k): (a, c) for k, a, c in zip(ref.key, ref["amt"].to_list(), ref["cat"].to_list())}
+    got = {}
+    for r in res:
+        for k, a, c in zip(r["keys"], r["amt"], r["cat"]):
+            assert k not in got               # every key aggregated on exactly one rank
+            got[k] = (a, c)
+    assert set(got) == set(want)
+    for k in want:
+        assert got[k][1] == want[k][1]
+        assert (got[k][0] is None and want[k][0] is None) or abs(got[k][0] - want[k][0]) < 1e-9
+    rids = sorted(i for r in res for i in r["rid"])
+    assert rids == list(range(len(want)))
+
+
 def test_collectives_gloo(tmp_path):
     r0, r1 = _run("_collectives", tmp_path)
     for r in (r0, r1):

@@ -117,6 +117,54 @@ def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
     return out.to(t.device)
 
 
+def all_to_all_bytes(per_dest: Sequence[bytes]) -> List[bytes]:
+    """Personalised exchange: rank r sends ``per_dest[k]`` to rank k and returns what every rank sent it
+    (two ``all_to_all_single`` calls: the sizes, then the payload with those splits)."""
+    if not is_dist():
+        return [per_dest[0]]
+    n = world()
+    if len(per_dest) != n:
+        raise ValueError("one payload per destination rank")
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    send_sizes = torch.tensor([len(b) for b in per_dest], dtype=torch.int64, device=dev)
+    recv_sizes = torch.empty_like(send_sizes)
+    dist.all_to_all_single(recv_sizes, send_sizes)
+    ss, rs = send_sizes.tolist(), recv_sizes.tolist()
+    payload = torch.frombuffer(bytearray(b"".join(per_dest)) or bytearray(1), dtype=torch.uint8)[:sum(ss)].to(dev)
+    out = torch.empty(sum(rs), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(out, payload, output_split_sizes=rs, input_split_sizes=ss)
+    data = out.cpu().numpy().tobytes()
+    res, o = [], 0
+    for k in rs:
+        res.append(data[o:o + k])
+        o += k
+    return res
+
+
+def key_owner(key, n: int) -> int:
+    """Rank owning a record key: a process-independent hash (crc32 of its string form)."""
+    import zlib
+    return zlib.crc32(str(key).encode("utf-8")) % n
+
+
+def shuffle_by_key(records: Sequence, key_fn) -> list:
+    """Keyed shuffle (Spark ``reduceByKey`` / ``groupByKey`` exchange): every record goes to
+    the rank that owns its key; returns the records this rank owns (from all ranks, rank order)."""
+    import pickle
+    if not is_dist():
+        return list(records)
+    n = world()
+    buckets: List[list] = [[] for _ in range(n)]
+    for r in records:
+        buckets[key_owner(key_fn(r), n)].append(r)
+    # payloads are this job's own in-memory records exchanged between its ranks
+    got = all_to_all_bytes([pickle.dumps(b, protocol=pickle.HIGHEST_PROTOCOL) for b in buckets])
+    out: list = []
+    for g in got:
+        out.extend(pickle.loads(g))
+    return out
+
+
 def lpt_assign(costs: Sequence[float], n_workers: int) -> List[int]:
     """Longest-processing-time-first assignment of tasks to workers; returns worker per task."""
     order = sorted(range(len(costs)), key=lambda i: -costs[i])

@@ -77,6 +77,15 @@ class _GroupedReader(DataReader):
     def __init__(self, source: DataReader, key: Callable[[Any], Any], device=None):
         super().__init__(key, device or source.device)
         self.source = source
+        self.distributed = False     # see distribute()
+
+    def distribute(self, on: bool = True) -> "_GroupedReader":
+        """Row-sharded reading under a process group: every rank takes every ``world``-th record of the
+        source, the records are shuffled by key to the rank that owns the key (``parallel.dist.
+        shuffle_by_key``, an all-to-all over RCCL / gloo) and each rank aggregates its own keys. The result
+        is this rank's row shard (``Dataset.sharded``), so the workflow then fits data-parallel."""
+        self.distributed = on
+        return self
 
     def _records(self, params) -> List[Any]:
         recs = self.source.read_records(params)
@@ -91,7 +100,11 @@ class _GroupedReader(DataReader):
         raise NotImplementedError
 
     def generate_dataset(self, raw_features: Sequence, params=None) -> Dataset:
+        from ..parallel import dist as D
         recs = self._records(params)
+        shard = self.distributed and D.world() > 1
+        if shard:
+            recs = D.shuffle_by_key(recs[D.rank()::D.world()], lambda r: str(self.key_fn(r)))
         dev = self.device or default_device()
         n = len(recs)
         keys = np.asarray([str(self.key_fn(r)) for r in recs], dtype=object)
@@ -118,7 +131,16 @@ class _GroupedReader(DataReader):
             out = self._aggregate(agg, vals, mask, seg, len(starts), f.is_response, ts)
             out = [out[g] for g in keep_groups]
             cols[f.name] = column_from_values(f.wtype, out, dev)
-        return Dataset(cols, np.asarray([group_keys[g] for g in keep_groups], dtype=object), len(keep_groups))
+        keys_out = np.asarray([group_keys[g] for g in keep_groups], dtype=object)
+        if not shard:
+            return Dataset(cols, keys_out, len(keep_groups))
+        # global row ids: this rank's keys follow the keys of the lower ranks
+        counts = D.all_gather_object(len(keep_groups))
+        base = sum(counts[:D.rank()])
+        ds = Dataset(cols, keys_out, len(keep_groups),
+                     torch.arange(base, base + len(keep_groups), device=dev))
+        ds.sharded = True
+        return ds
 
     @staticmethod
     def _aggregate(agg, vals, mask, seg, G, is_response, ts) -> list:
