@@ -610,26 +610,6 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     const double* qi = qinv + (int64_t)(node_model ? node_model[j] : 0) * S;
     const double min_inst = P[0], min_gain = P[1], mcw = P[2], lambda = P[3];
     const bool allow_missing = P[5] > 0.5f && missing_bin >= 0;
-    const int f_end = one_blk ? 0 : min(f_lim, (fb + 1) * FPB);
-    // This wave's (up to 4) features of the block: issue every histogram load first, then scan -- the
-    // per-feature chain (bins load -> 6-step prefix -> gains) no longer pays one memory latency each.
-    constexpr int WF = FPB / 4;
-    int nbv[WF];
-    int64_t vv[WF][SM], mm[WF][SM];
-#pragma unroll
-    for (int i = 0; i < WF; ++i) {
-      const int f = fb * FPB + wave + 4 * i;
-      nbv[i] = f < f_end ? feat_nbins[fl[f]] : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < WF; ++i) {
-      const int f = fb * FPB + wave + 4 * i;
-      const int64_t* hf = h + (int64_t)(f < f_end ? f : 0) * B * S;
-      for (int s = 0; s < S; ++s) {
-        vv[i][s] = (f < f_end && lane < nbv[i]) ? hf[lane * S + s] : 0;
-        mm[i][s] = (f < f_end && allow_missing) ? hf[missing_bin * S + s] : 0;
-      }
-    }
     // node totals from feature 0 (every row is counted once per feature, including the missing bin)
     int64_t totq[SM];
     double tot[SM], q[SM];
@@ -643,6 +623,7 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     double tcount;
     const double pimp = impurity_dev(tot, S, kind, &tcount);
     const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
+    const int f_end = one_blk ? 0 : min(f_lim, (fb + 1) * FPB);
     // one candidate (left statistics lq, bin b, missing direction dl) with the CPU twin's arithmetic
     auto consider = [&](const int64_t* lq, int f, int b, int dl) {
       double left[SM], right[SM];
@@ -677,25 +658,23 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
         consider(lq, f, 0, 0);
       }
     }
-#pragma unroll
-    for (int i = 0; i < WF; ++i) {
-      const int f = fb * FPB + wave + 4 * i;
-      if (f >= f_end) break;
-      const int nb = nbv[i];
+    for (int f = fb * FPB + wave; f < f_end; f += 4) {
+      const int nb = feat_nbins[fl[f]];
+      const int64_t* hf = h + (int64_t)f * B * S;
       if (nb == 1) {
         // one present bin (one-hot / null indicator): the only candidate is present-left,
         // missing-right -- no scan, one lane
         if (allow_missing && lane == 0) {
           int64_t lq[SM];
-          for (int s = 0; s < S; ++s) lq[s] = h[(int64_t)f * B * S + s];
+          for (int s = 0; s < S; ++s) lq[s] = hf[s];
           consider(lq, f, 0, 0);
         }
         continue;
       }
       int64_t v[SM], miss[SM];
       for (int s = 0; s < S; ++s) {
-        v[s] = vv[i][s];
-        miss[s] = mm[i][s];
+        v[s] = (lane < nb) ? hf[lane * S + s] : 0;
+        miss[s] = allow_missing ? hf[missing_bin * S + s] : 0;
       }
       for (int off = 1; off < 64; off <<= 1) {
         for (int s = 0; s < S; ++s) {
