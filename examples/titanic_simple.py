@@ -4,7 +4,7 @@ The reference example restricts the selector to ``OpLogisticRegression`` (``OpTi
 and that is the default here too; ``--all`` runs the full default binary grid (LR, RF, XGBoost), the
 setting of the README's model summary (RF selected, hold-out AuPR 0.8225, ``README.md:61-126``).
 
-Run: ``python examples/titanic_simple.py [path/to/PassengerDataAll.csv] [--all] [--quiet]``
+Run: ``python examples/titanic_simple.py [path/to/PassengerDataAll.csv] [--all] [--quiet] [--seed=N]``
 """
 from __future__ import annotations
 
@@ -28,7 +28,7 @@ SCHEMA = [("id", "int"), ("survived", "int"), ("pClass", "int"), ("name", "strin
 DEFAULT_CSV = "/root/reference/test-data/PassengerDataAll.csv"
 
 
-def build(lr_only: bool = True):
+def build(lr_only: bool = True, seed=None):
     survived = FeatureBuilder.RealNN("survived").extract(lambda r: float(r["survived"])).as_response()
     p_class = FeatureBuilder.PickList("pClass").extract(
         lambda r: None if r["pClass"] != r["pClass"] else str(int(r["pClass"]))).as_predictor()
@@ -53,7 +53,7 @@ def build(lr_only: bool = True):
     checked = survived.sanity_check(passenger_features, remove_bad_features=True)
     types = ["OpLogisticRegression"] if lr_only else None
     prediction = BinaryClassificationModelSelector.with_train_validation_split(
-        model_types_to_use=types).set_input(survived, checked).get_output()
+        model_types_to_use=types, seed=seed).set_input(survived, checked).get_output()
     return survived, prediction
 
 
@@ -64,7 +64,8 @@ def main(argv):
     global LAST_PREDICTION
     path = next((a for a in argv if not a.startswith("--")), DEFAULT_CSV)
     quiet = "--quiet" in argv
-    survived, prediction = build(lr_only="--all" not in argv)
+    seed = next((int(a.split("=", 1)[1]) for a in argv if a.startswith("--seed=")), None)
+    survived, prediction = build(lr_only="--all" not in argv, seed=seed)
     LAST_PREDICTION = prediction
     evaluator = Evaluators.BinaryClassification().set_label_col(survived).set_prediction_col(prediction)
     reader = CSVReader(path=path, schema=SCHEMA, key=lambda r: str(r["id"]))

@@ -165,7 +165,7 @@ def test_titanic_default_selector_holdout_in_readme_neighbourhood():
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples"))
     import titanic_simple
-    model, metrics = titanic_simple.main([titanic_simple.DEFAULT_CSV, "--all", "--quiet"])
+    model, metrics = titanic_simple.main([titanic_simple.DEFAULT_CSV, "--all", "--quiet", "--seed=42"])
     summ = model.get_origin_stage_of(titanic_simple.LAST_PREDICTION).metadata["summary"]
     ho = summ["holdoutEvaluation"]["AuPR"]
     # README.md:89: hold-out AuPR 0.8225 (RF selected, 73 hold-out rows); 3-fold CV AuPR of the models
