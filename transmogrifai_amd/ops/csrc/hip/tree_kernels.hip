@@ -682,9 +682,14 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
           if (lane >= off) v[s] += o;
         }
       }
-      // candidates b < nb - 1; with a missing bin dl = 0 also b = nb - 1 (present left, missing right)
+      // candidates b < nb - 1; with a missing bin dl = 0 also b = nb - 1 (present left, missing right).
+      // An empty missing bin makes every dl = 1 candidate equal to its dl = 0 twin, which wins the tie
+      // (better(): dl ascending; the CPU twin's first-wins scan order) -- skip them.
+      bool any_miss = false;
+      for (int s = 0; s < S; ++s) any_miss |= miss[s] != 0;
+      const int n_dl = allow_missing ? (any_miss ? 2 : 1) : 1;
       if (lane < nb - 1 + (allow_missing ? 1 : 0)) {
-        for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
+        for (int dl = 0; dl < n_dl; ++dl) {
           if (lane == nb - 1 && dl) continue;
           int64_t lq[SM];
           for (int s = 0; s < S; ++s) lq[s] = v[s] + (dl ? miss[s] : 0);

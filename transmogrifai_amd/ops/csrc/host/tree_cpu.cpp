@@ -147,7 +147,10 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
       int64_t miss[kMaxS] = {0};
       if (allow_missing)
         for (int s = 0; s < S; ++s) miss[s] = hf[(int64_t)missing_bin * S + s];
-      for (int dl = 0; dl < (allow_missing ? 2 : 1); ++dl) {
+      bool any_miss = false;
+      for (int s = 0; s < S; ++s) any_miss |= miss[s] != 0;
+      // an empty missing bin: the dl = 1 candidates repeat the dl = 0 ones and never win a tie
+      for (int dl = 0; dl < (allow_missing ? (any_miss ? 2 : 1) : 1); ++dl) {
         int64_t lq[kMaxS];
         for (int s = 0; s < S; ++s) lq[s] = dl ? miss[s] : 0;
         // with a missing bin, dl = 0 also tries b = nb - 1: every present value left, missing right
