@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
@@ -162,6 +163,9 @@ class OpValidator:
             results.update(res)
             failures.extend(fails)
             timings[lname] = time.time() - t1
+            if os.environ.get("TMOG_MEM_TRACE") == "1" and torch.cuda.is_available():
+                timings[f"peak_gb:{lname}"] = round(torch.cuda.max_memory_allocated() / 1e9, 3)
+                torch.cuda.reset_peak_memory_stats()
         # exchange metrics between ranks
         gathered = D.all_gather_object((results, failures, timings))
         allres: Dict[Tuple[int, int, int], float] = {}

@@ -68,7 +68,7 @@ def fit_and_transform_layer(layer: Layer, train: Dataset, test: Optional[Dataset
     return train, test, fitted
 
 
-def fit_and_transform_dag(dag: Sequence[Layer], train: Dataset, test: Optional[Dataset] = None,
+def fit_and_transform_dag(dag: Sequence[Layer], train, test: Optional[Dataset] = None,
                           timings: Optional[dict] = None, keep: Optional[set] = None):
     """Fit and apply the DAG layer by layer.
 
@@ -76,6 +76,10 @@ def fit_and_transform_dag(dag: Sequence[Layer], train: Dataset, test: Optional[D
     ``train`` / ``test`` right after the transform of its last consumer inside this DAG, so raw columns
     and intermediate vector blocks do not outlive their use (the feature matrix of a 10M-row table is
     tens of GB; only the final selector's input has to stay resident)."""
+    if isinstance(train, list):      # handed over as [train, test]: emptied here, so the caller keeps no
+        box = train                  # reference and columns dropped below are really released
+        train, test = box[0], box[1]
+        box.clear()
     last = _last_uses(dag) if keep is not None else {}
     fitted_all = []
     for li, layer in enumerate(dag):

@@ -248,13 +248,13 @@ class OpWorkflow(OpWorkflowCore):
 
     def _fit_stages(self, box: list, timings: Dict[str, float]) -> List[OpPipelineStage]:
         with _Timer(timings, "HoldoutSplit"):
-            train, test = self._holdout_split(box.pop())
+            split = list(self._holdout_split(box.pop()))     # handed to the DAG executor below
         dag = [[(st, d) for st, d in layer if st in self.stages] for layer in compute_dag(self.result_features)]
         dag = [l for l in dag if l]
         stage_t: Dict[str, float] = {}
         if not self.workflow_cv:
             with _Timer(timings, OpStep.FeatureEngineering):
-                _, _, fitted = fit_and_transform_dag(dag, train, test, stage_t, keep=set())
+                _, _, fitted = fit_and_transform_dag(dag, split, None, stage_t, keep=set())
         else:
             ms, before, during, after = cut_dag(dag)
             later = {f.name for part in (during, after) for layer in part for st, _ in layer
@@ -262,8 +262,7 @@ class OpWorkflow(OpWorkflowCore):
             if ms is not None:
                 later |= {f.name for f in ms.get_input_features()}
             with _Timer(timings, OpStep.FeatureEngineering):
-                tr2, te2, fb = fit_and_transform_dag(before, train, test, stage_t, keep=later)
-            del train, test
+                tr2, te2, fb = fit_and_transform_dag(before, split, None, stage_t, keep=later)
             fitted = list(fb)
             if ms is not None:
                 # OpWorkflow.scala:403-453: validate with the during-DAG refit inside every fold, then fit
