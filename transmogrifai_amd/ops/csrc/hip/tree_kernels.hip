@@ -125,6 +125,7 @@ __device__ __forceinline__ void add_row(int* my, int bin, int S, int s0, int Sc,
 // of one row are distinct, so an LDS atomic wave-instruction never conflicts), kCsrU rows in flight.
 // On the headline table that is ~50 entries per row instead of ~530 byte gathers.
 constexpr int kCsrU = 16;
+constexpr int kCsrG = 8;     // row slots per lane group in flight (register budget of the whole kernel)
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
@@ -158,32 +159,41 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
     const int4 mine = stage_row<2>(rp[ri], model, stride, nullptr, t1, t2, qs);
     const int64_t r = (uint32_t)mine.x & 0xFFFFFFu;
     const int64_t q0 = csr_ptr[r];
-    const int64_t q1 = lane < nrows ? csr_ptr[r + 1] : q0;
-    for (int j = 0; j < nrows; j += kCsrU) {
-      int col[kCsrU], gq[kCsrU], hq[kCsrU];
-      bool ok[kCsrU];
-      int64_t e1[kCsrU], k0[kCsrU];
+    const int len = lane < nrows ? (int)(csr_ptr[r + 1] - q0) : 0;
+    // Lane groups of W (a power of two >= this chunk's longest list, <= 64) take one row each, so a
+    // wave-instruction covers 64 / W rows at (nearly) full lane use instead of one row per instruction
+    // (the headline's rows carry ~17 entries). Row records reach the group by ds_bpermute.
+    int mx = len;
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+    const int W = mx <= 8 ? 8 : mx <= 16 ? 16 : mx <= 32 ? 32 : 64;
+    const int RPI = 64 / W;
+    const int rs = lane / W, k = lane - rs * W;
+    const int q0lo = (int)(uint32_t)(uint64_t)q0, q0hi = (int)((uint64_t)q0 >> 32);
+    for (int j0 = 0; j0 < nrows; j0 += RPI * kCsrG) {
+      int col[kCsrG], gq[kCsrG], hq[kCsrG], ln[kCsrG];
+      int64_t k0[kCsrG];
+      bool ok[kCsrG];
 #pragma unroll
-      for (int u = 0; u < kCsrU; ++u) {
-        const int jj = min(j + u, 63);            // rows past nrows have an empty list (q1 = q0)
-        k0[u] = readlane64(q0, jj);
-        e1[u] = readlane64(q1, jj);
-        gq[u] = __builtin_amdgcn_readlane(mine.y, jj);
-        hq[u] = __builtin_amdgcn_readlane(mine.z, jj);
-        const int64_t k = k0[u] + lane;
-        ok[u] = k < e1[u];
-        col[u] = csr_col[ok[u] ? k : k0[u] > 0 ? k0[u] - 1 : 0];   // unpredicated load of a valid id
+      for (int u = 0; u < kCsrG; ++u) {
+        const int src = j0 + u * RPI + rs;
+        const int sl = min(src, 63);
+        ln[u] = src < nrows ? __shfl(len, sl, 64) : 0;
+        k0[u] = (int64_t)(((uint64_t)(uint32_t)__shfl(q0hi, sl, 64) << 32) | (uint64_t)(uint32_t)__shfl(q0lo, sl, 64));
+        gq[u] = __shfl(mine.y, sl, 64);
+        hq[u] = __shfl(mine.z, sl, 64);
+        ok[u] = k < ln[u];
+        col[u] = csr_col[ok[u] ? k0[u] + k : k0[u] > 0 ? k0[u] - 1 : 0];   // unpredicated load of a valid id
       }
 #pragma unroll
-      for (int u = 0; u < kCsrU; ++u)
+      for (int u = 0; u < kCsrG; ++u)
         if (ok[u]) {
           atomicAdd(a0 + col[u], gq[u]);
           atomicAdd(a1 + col[u], hq[u]);
         }
 #pragma unroll
-      for (int u = 0; u < kCsrU; ++u)      // lists longer than one wave
-        for (int64_t k = k0[u] + 64 + lane; k < e1[u]; k += 64) {
-          const int c = csr_col[k];
+      for (int u = 0; u < kCsrG; ++u)      // lists longer than the lane group (only when W == 64)
+        for (int kk = k + W; kk < ln[u]; kk += W) {
+          const int c = csr_col[k0[u] + kk];
           atomicAdd(a0 + c, gq[u]);
           atomicAdd(a1 + c, hq[u]);
         }
