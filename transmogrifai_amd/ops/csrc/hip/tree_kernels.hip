@@ -177,7 +177,10 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
       for (int u = 0; u < kCsrG; ++u) {
         const int src = j0 + u * RPI + rs;
         const int sl = min(src, 63);
-        ln[u] = src < nrows ? __shfl(len, sl, 64) : 0;
+        // every shuffle runs with the full wave active: a bpermute under a divergent EXEC mask reads 0
+        // from source lanes that are off (in a tail chunk lane sl's own src can be >= nrows)
+        const int lsh = __shfl(len, sl, 64);
+        ln[u] = src < nrows ? lsh : 0;
         k0[u] = (int64_t)(((uint64_t)(uint32_t)__shfl(q0hi, sl, 64) << 32) | (uint64_t)(uint32_t)__shfl(q0lo, sl, 64));
         gq[u] = __shfl(mine.y, sl, 64);
         hq[u] = __shfl(mine.z, sl, 64);
