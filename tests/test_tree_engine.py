@@ -253,3 +253,98 @@ def test_hip_wide_hist_matches_host(F, n_one, chunk):
     np.testing.assert_array_equal(fc.tree_off, fg.tree_off)
     np.testing.assert_array_equal(fc.nodes, fg.nodes)
     np.testing.assert_allclose(fc.value, fg.value, rtol=1e-6, atol=1e-6)
+
+
+def _brute_newton_root(X, g, h, nb, miss, lam, mcw):
+    """Exhaustive XGBoost root split (sparsity-aware: missing rows go left or right) with the gain
+    G_L^2/(H_L+lam) + G_R^2/(H_R+lam) - G^2/(H+lam) (XGBoost's loss change, no 1/2, gamma compared to it)."""
+    G, H = g.sum(), h.sum()
+    parent = G * G / (H + lam)
+    best = (-np.inf, None, None, None)
+    for f in range(X.shape[1]):
+        m = X[:, f] == miss
+        for b in range(int(nb[f])):
+            for dl in (0, 1):
+                if b == nb[f] - 1 and dl == 1:
+                    continue
+                left = ((X[:, f] <= b) & ~m) | (m & bool(dl))
+                GL, HL = g[left].sum(), h[left].sum()
+                GR, HR = G - GL, H - HL
+                if HL < mcw or HR < mcw:
+                    continue
+                gain = GL * GL / (HL + lam) + GR * GR / (HR + lam) - parent
+                if gain > best[0] + 1e-12:
+                    best = (gain, f, b, dl)
+    return best
+
+
+def test_newton_root_split_and_leaf_values_match_hand_computation():
+    """Independent check of the XGBoost objective: the root split (feature, bin, default direction),
+    its loss change, the Newton leaf values -G/(H+lambda)*eta and gamma pruning, recomputed by brute force."""
+    g0 = torch.Generator().manual_seed(5)
+    N, F, B = 2000, 6, 16
+    miss = B - 1
+    X = torch.randint(0, B - 1, (N, F), generator=g0, dtype=torch.uint8)
+    X[torch.rand(N, F, generator=g0) < 0.15] = miss
+    nb = np.full(F, B - 1)
+    gq = torch.round((X[:, 2].double() - 7) / 4 + torch.randn(N, generator=g0, dtype=torch.float64) * 2) / 8
+    hq = torch.full((N,), 0.25, dtype=torch.float64)
+    lam, mcw, eta = 1.0, 1.0, 0.3
+    gain, bf, bb, bdl = _brute_newton_root(X.numpy(), gq.numpy(), hq.numpy(), nb, miss, lam, mcw)
+    jobs = [te.TreeJob(0, te.TreeParams(max_depth=1, min_child_weight=mcw, reg_lambda=lam, eta=eta), torch.arange(N))]
+    f = te.grow_forest(X, nb, jobs, mode=te.MODE_GH, kind=te.KIND_NEWTON, t1=gq[None].float(),
+                       t2=hq[None].float(), B=B, missing_bin=miss)
+    assert (int(f.nodes[0, 0]), int(f.nodes[0, 1])) == (bf, bb)
+    assert abs(float(f.gain[0]) - gain) <= 1e-6 * max(1.0, abs(gain))      # stored as float32
+    # leaves: Newton step of the rows routed there (missing rows follow the learned default direction)
+    m = X[:, bf] == miss
+    left = ((X[:, bf] <= bb) & ~m) | (m & bool(bdl))
+    for child, sel in ((int(f.nodes[0, 2]), left), (int(f.nodes[0, 3]), ~left)):
+        want = -gq[sel].sum() / (hq[sel].sum() + lam) * eta
+        assert abs(float(f.value[child].reshape(-1)[0]) - float(want)) < 1e-6
+    # gamma above the loss change prunes the split (XGBoost min_split_loss), below keeps it
+    for gam, n_nodes in ((gain * 1.01, 1), (gain * 0.99, 3)):
+        jobs = [te.TreeJob(0, te.TreeParams(max_depth=1, min_child_weight=mcw, reg_lambda=lam, eta=eta, gamma=gam),
+                           torch.arange(N))]
+        fp = te.grow_forest(X, nb, jobs, mode=te.MODE_GH, kind=te.KIND_NEWTON, t1=gq[None].float(),
+                            t2=hq[None].float(), B=B, missing_bin=miss)
+        assert len(fp.nodes) == n_nodes
+
+
+def _grow_csr_long(dev, n_multi=40, n_one=152, N=12_000, chunk_rows=4096):
+    """One-present-bin columns with row lists of very different lengths (0 .. ~150 entries): the GPU's
+    CSR histogram items take lane groups of 8 / 16 / 32 / 64 and, past 64 entries, the long-list loop."""
+    g = torch.Generator().manual_seed(21)
+    B = 32
+    F = n_multi + n_one
+    X = torch.randint(0, B - 1, (N, F), generator=g, dtype=torch.uint8)
+    X[torch.rand(N, F, generator=g) < 0.1] = B - 1
+    nbins = np.full(F, B - 1)
+    dens = torch.rand(N, 1, generator=g) ** 2                       # per-row presence rate
+    dens[torch.arange(N) % 7 == 0] = 0.0                            # rows with empty lists
+    dens[torch.arange(N) % 11 == 0] = 0.97                          # rows with ~150 entries
+    pres = torch.rand(N, n_one, generator=g) < dens
+    X[:, n_multi:] = torch.where(pres, 0, B - 1).to(torch.uint8)
+    nbins[n_multi:] = 1
+    t1 = torch.round(torch.randn(2, N, generator=g) * 64) / 64 + pres[:, :3].float().sum(1) / 4
+    t2 = torch.rand(2, N, generator=g) * 0.25 + 0.01
+    jobs = [te.TreeJob(m, te.TreeParams(max_depth=6, min_child_weight=0.5, reg_lambda=1.0, split_eps=1e-6),
+                       torch.arange(N)[torch.arange(N) % (m + 2) != 1].to(dev)) for m in range(2)]
+    Xd = X.to(dev)
+    return te.grow_forest(Xd, nbins, jobs, mode=te.MODE_GH, kind=te.KIND_NEWTON, t1=t1.to(dev), t2=t2.to(dev), B=B,
+                          missing_bin=B - 1, chunk_rows=chunk_rows, csr=te.onebin_csr(Xd, nbins))
+
+
+def test_cpu_engine_long_csr_lists():
+    f = _grow_csr_long("cpu", N=3000)
+    assert f.n_trees == 2 and len(f.nodes) > 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [4096, 512])
+def test_hip_long_csr_lists_match_host(chunk):
+    fc = _grow_csr_long("cpu", chunk_rows=chunk)
+    fg = _grow_csr_long("cuda", chunk_rows=chunk)
+    np.testing.assert_array_equal(fc.tree_off, fg.tree_off)
+    np.testing.assert_array_equal(fc.nodes, fg.nodes)
+    np.testing.assert_allclose(fc.value, fg.value, rtol=1e-6, atol=1e-6)
