@@ -112,6 +112,35 @@ def test_xgb_fused_round_epilogue_matches_torch_path(monkeypatch):
     assert _native_loaded()
 
 
+def test_xgb_pipelined_parts_identical_to_single_loop(monkeypatch):
+    """Boosting the jobs in concurrent halves (own host thread + stream each, disjoint native slots)
+    gives exactly the trees and early-stopping rounds of the single loop."""
+    from transmogrifai_amd.models.base import FitJob
+    from transmogrifai_amd.models.trees import XGBoostClassifierLearner
+    g = torch.Generator().manual_seed(4)
+    n, d = 30_000, 16
+    X = torch.randn(n, d, generator=g)
+    X[:, :4] = (X[:, :4] > 0.7).float()
+    y = ((X[:, 4] + X[:, 0] - 0.5 * X[:, 6] + 0.5 * torch.randn(n, generator=g)) > 0).float()
+    Xd, yd = X.cuda(), y.cuda()
+    params = dict(XGBoostClassifierLearner.defaults, num_round=25, max_depth=6, eta=0.3, missing=0.0,
+                  num_early_stopping_rounds=3)
+    jobs = [FitJob(dict(params, min_child_weight=m), torch.arange(k, n, 3, device="cuda"))
+            for m in (1.0, 10.0) for k in range(3)]
+    outs = []
+    for flag in ("1", "2", "3"):
+        monkeypatch.setenv("TMOG_XGB_PIPE", flag)
+        outs.append(XGBoostClassifierLearner().fit_batch(Xd, yd, jobs))
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert a["num_trees"] == b["num_trees"]
+            for k in a["forest"]:
+                va, vb = a["forest"][k], b["forest"][k]
+                if isinstance(va, np.ndarray):
+                    np.testing.assert_array_equal(va, vb, err_msg=k)
+    assert _native_loaded()
+
+
 def test_row_uniform_kernel_bit_identical():
     from transmogrifai_amd.tuning import splitters as SP
     rid = torch.randint(0, 1 << 40, (100_003,), dtype=torch.int64)

@@ -99,3 +99,16 @@ def test_regression_selector_and_validation_failure_dropped():
     summ = m.get_origin_stage_of(pred).metadata["summary"]
     assert summ["bestModelType"] == "OpLinearRegression"
     assert summ["failures"]
+
+
+def test_splitters_prepare_from_label_counts_equals_tensor():
+    """Data-parallel selectors pass merged label counts instead of gathered labels: same summaries."""
+    from transmogrifai_amd.tuning.splitters import DataBalancer, DataCutter, DataSplitter, label_counts
+    g = torch.Generator().manual_seed(2)
+    yb = (torch.rand(50_000, generator=g) < 0.07).double()
+    ym = torch.randint(0, 12, (30_000,), generator=g).double()
+    for mk, y in ((lambda: DataSplitter(max_training_sample=10_000), yb),
+                  (lambda: DataBalancer(sample_fraction=0.2, max_training_sample=20_000), yb),
+                  (lambda: DataCutter(max_label_categories=5, max_training_sample=8_000), ym)):
+        a, b = mk(), mk()
+        assert a.pre_validation_prepare(y) == b.pre_validation_prepare(label_counts(y))

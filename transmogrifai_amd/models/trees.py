@@ -510,6 +510,36 @@ class GBTRegressorLearner(GBTClassifierLearner):
         return m, e, e
 
 
+def _run_parts(dev, parts, fn):
+    """Run ``fn(jobs, slot_base, groups)`` for every part concurrently: one host thread and one stream
+    per part (both ordered after the caller's stream, which then waits for all of them). Native calls
+    release the GIL, so the parts' host work and GPU work interleave. The first error is re-raised."""
+    import threading
+    cur = torch.cuda.current_stream(dev)
+    streams = [torch.cuda.Stream(device=dev) for _ in parts]
+    for s in streams:
+        s.wait_stream(cur)
+    errs = []
+
+    def work(k):
+        try:
+            torch.cuda.set_device(dev)
+            with torch.cuda.stream(streams[k]):
+                fn(*parts[k])
+        except BaseException as e:          # noqa: BLE001  (re-raised on the caller's thread)
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(k,), daemon=True) for k in range(len(parts))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for s in streams:
+        cur.wait_stream(s)
+    if errs:
+        raise errs[0]
+
+
 @register_learner
 class XGBoostClassifierLearner(_BoostLearner):
     """Newton boosting with XGBoost semantics (binary:logistic)."""
@@ -551,8 +581,6 @@ class XGBoostClassifierLearner(_BoostLearner):
         fused = dev.type == "cuda" and all(float(j.params.get("subsample", 1.0)) >= 1.0 for j in jobs) and \
             os.environ.get("TMOG_XGB_FUSED", "1") != "0"
         AUC_BINS = 1 << 16
-        G = H = None
-        root_cache: Dict[tuple, tuple] = {}
         # Column order for growth: multi-bin columns first, then the one-present-bin ones (one-hot /
         # null indicators), physically -- the histogram kernel's multi-bin groups then gather contiguous
         # row bytes. It is the order the grower would use anyway (common/tree_grow.hpp), so trees are
@@ -583,67 +611,94 @@ class XGBoostClassifierLearner(_BoostLearner):
         csr = TE.onebin_csr(Xg, n_bins_g, cols=None if fp is None else fp.one_cols) \
             if (dev.type == "cuda" and spec.missing_bin > 0) else None
         yf = yy.to(torch.float32).contiguous()
-        for it in range(max(rounds)):
-            act = [p for p in range(P) if it < rounds[p] and not stopped[p]]
-            if not act:
-                break
-            if not fused or it == 0:
-                if G is None or not fused:
-                    G = torch.zeros(P, N, dtype=torch.float32, device=dev)
-                    H = torch.zeros(P, N, dtype=torch.float32, device=dev)
-                for p in act:
+        G = H = None
+        if fused:         # shared [P, N] statistics: each job's row is only touched by its own part
+            G = torch.zeros(P, N, dtype=torch.float32, device=dev)
+            H = torch.zeros(P, N, dtype=torch.float32, device=dev)
+            for p in range(P):
+                if rounds[p] > 0:
                     g, h = self._grad(yy, Fm[p])
                     G[p], H[p] = g.to(torch.float32), h.to(torch.float32)
-            tjobs = []
-            for p in act:
-                pr = jobs[p].params
-                tp = TE.TreeParams(max_depth=int(pr.get("max_depth", 6)),
-                                   min_child_weight=float(pr.get("min_child_weight", 1.0)),
-                                   reg_lambda=float(pr.get("reg_lambda", 1.0)), gamma=float(pr.get("gamma", 0.0)),
-                                   eta=float(pr.get("eta", 0.3)), split_eps=1e-6)
-                r = rows[p]
-                w = None
-                ss = float(pr.get("subsample", 1.0))
-                if ss < 1.0:
-                    gen = torch.Generator().manual_seed(int(pr.get("seed", 0)) + 17 * it + p)
-                    w = (torch.rand(r.numel(), generator=gen) < ss).to(torch.int64).to(dev)
-                tjobs.append(TE.TreeJob(p, tp, r, w))
-            root = None
-            if all(j.weights is None for j in tjobs):
-                # the packed root entries only change when a job stops: pack once per active set
-                key = tuple(act)
-                if key not in root_cache:
-                    root_cache.clear()
-                    root_cache[key] = TE._root_rows(tjobs, dev)
-                packed, cnts = root_cache[key]
-                root = (packed.clone(), cnts)
-            forest = TE.grow_forest(Xg, n_bins_g, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
-                                    missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root, fp=fp)
-            if colperm is not None:
-                internal = forest.nodes[:, 2] >= 0
-                forest.nodes[internal, 0] = colperm[forest.nodes[internal, 0]]
-            need = [p for p in act if esr[p] > 0]
-            auc_counts = None
-            if fused:
-                auc_counts = self._fused_epilogue(Fm, G, H, yf, forest, act, N,
-                                                  AUC_BINS if (need and self.classification) else 0)
-            else:
-                _add_tree_margins(Fm, forest, Xb, act, [1.0] * len(act), tjobs)
-            for k, p in enumerate(act):
-                forests[p].append(forest.tree(k))
-                weights[p].append(1.0)
-            # early stopping on the training metric (the reference sets no eval set)
-            if need and self.classification:
-                if auc_counts is not None:
-                    vals = binned_aupr_from_counts(auc_counts[need]).tolist()     # one sync per round
+
+        def run(ps, slot_base=0, groups=None):
+            """Boosting rounds of the jobs ``ps`` (their trees do not depend on which other jobs grow
+            alongside: no per-node randomness, per-model quantisation, weights all 1 on this path)."""
+            nonlocal G, H
+            root_cache: Dict[tuple, tuple] = {}
+            for it in range(max([rounds[p] for p in ps], default=0)):
+                act = [p for p in ps if it < rounds[p] and not stopped[p]]
+                if not act:
+                    break
+                if not fused:
+                    G = torch.zeros(P, N, dtype=torch.float32, device=dev)
+                    H = torch.zeros(P, N, dtype=torch.float32, device=dev)
+                    for p in act:
+                        g, h = self._grad(yy, Fm[p])
+                        G[p], H[p] = g.to(torch.float32), h.to(torch.float32)
+                tjobs = []
+                for p in act:
+                    pr = jobs[p].params
+                    tp = TE.TreeParams(max_depth=int(pr.get("max_depth", 6)),
+                                       min_child_weight=float(pr.get("min_child_weight", 1.0)),
+                                       reg_lambda=float(pr.get("reg_lambda", 1.0)), gamma=float(pr.get("gamma", 0.0)),
+                                       eta=float(pr.get("eta", 0.3)), split_eps=1e-6)
+                    r = rows[p]
+                    w = None
+                    ss = float(pr.get("subsample", 1.0))
+                    if ss < 1.0:
+                        gen = torch.Generator().manual_seed(int(pr.get("seed", 0)) + 17 * it + p)
+                        w = (torch.rand(r.numel(), generator=gen) < ss).to(torch.int64).to(dev)
+                    tjobs.append(TE.TreeJob(p, tp, r, w))
+                root = None
+                if all(j.weights is None for j in tjobs):
+                    # the packed root entries only change when a job stops: pack once per active set
+                    key = tuple(act)
+                    if key not in root_cache:
+                        root_cache.clear()
+                        root_cache[key] = TE._root_rows(tjobs, dev)
+                    packed, cnts = root_cache[key]
+                    root = (packed.clone(), cnts)
+                forest = TE.grow_forest(Xg, n_bins_g, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
+                                        missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root, fp=fp,
+                                        slot_base=slot_base, groups=groups)
+                if colperm is not None:
+                    internal = forest.nodes[:, 2] >= 0
+                    forest.nodes[internal, 0] = colperm[forest.nodes[internal, 0]]
+                need = [p for p in act if esr[p] > 0]
+                auc_counts = None
+                if fused:
+                    auc_counts = self._fused_epilogue(Fm, G, H, yf, forest, act, N,
+                                                      AUC_BINS if (need and self.classification) else 0)
                 else:
-                    vals = binned_aupr_multi([torch.sigmoid(Fm[p][rows[p]]) for p in need],
-                                             [ylab[p] for p in need]).tolist()
-                for p, v in zip(need, vals):
-                    if v > best[p] + 1e-12:
-                        best[p], best_round[p] = v, it
-                    elif it - best_round[p] >= esr[p]:
-                        stopped[p] = True
+                    _add_tree_margins(Fm, forest, Xb, act, [1.0] * len(act), tjobs)
+                for k, p in enumerate(act):
+                    forests[p].append(forest.tree(k))
+                    weights[p].append(1.0)
+                # early stopping on the training metric (the reference sets no eval set)
+                if need and self.classification:
+                    if auc_counts is not None:
+                        vals = binned_aupr_from_counts(auc_counts[need]).tolist()     # one sync per round
+                    else:
+                        vals = binned_aupr_multi([torch.sigmoid(Fm[p][rows[p]]) for p in need],
+                                                 [ylab[p] for p in need]).tolist()
+                    for p, v in zip(need, vals):
+                        if v > best[p] + 1e-12:
+                            best[p], best_round[p] = v, it
+                        elif it - best_round[p] >= esr[p]:
+                            stopped[p] = True
+
+        # Pipelined job parts (GPU, fused path): the jobs are split in two halves, each boosted by its
+        # own host thread on its own stream, so one half's per-round host work (tree finalisation,
+        # round set-up, the early-stopping read-back) overlaps the other half's kernels instead of
+        # idling the GPU. Trees are identical to the single-loop order (see run()).
+        parts = int(os.environ.get("TMOG_XGB_PIPE", "2"))
+        if fused and par is None and P >= 2 and parts >= 2:
+            parts = min(parts, P)
+            cuts = np.linspace(0, P, parts + 1).astype(int)
+            gpp = max(1, int(os.environ.get("TMOG_XGB_PIPE_GROUPS", "1")))
+            _run_parts(dev, [(list(range(int(cuts[k]), int(cuts[k + 1]))), k * gpp, gpp) for k in range(parts)], run)
+        else:
+            run(list(range(P)))
         res = []
         for p in range(P):
             keep = len(forests[p]) if not stopped[p] else best_round[p] + 1

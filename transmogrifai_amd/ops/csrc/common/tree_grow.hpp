@@ -76,6 +76,9 @@ struct GrowArgs {
   void* const* fp_comm;       // GPU: one RCCL communicator per job group
   int (*fp_exchange)(void* ctx, int group, const void* send, void* recv, int64_t bytes);   // CPU all-gather
   void* fp_ctx;
+  // GPU: first per-group resource slot (stream, staging, histogram buffers) of this call -- concurrent
+  // calls (e.g. the XGBoost learner's pipelined job halves, one host thread each) use disjoint slots
+  int32_t slot_base;
 };
 
 // Feature-parallel split record, one per node and rank:

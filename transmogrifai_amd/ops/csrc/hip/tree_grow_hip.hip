@@ -87,7 +87,7 @@ std::mutex& rccl_mutex() {
 }
 
 std::vector<GpuSlot>& slots() {
-  static std::vector<GpuSlot> s(8);
+  static std::vector<GpuSlot> s(16);
   return s;
 }
 
@@ -259,7 +259,8 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
   const int ng = a.n_groups;
   res->groups.resize(ng);
   try {
-    if (ng > (int)slots().size()) throw std::runtime_error("too many job groups");
+    const int sb = a.slot_base;
+    if (sb < 0 || sb + ng > (int)slots().size()) throw std::runtime_error("too many job groups");
     if (a.fp_world > 0 && a.fp_comm == nullptr) throw std::runtime_error("feature-parallel growth needs communicators");
     int dev = 0;
     hchk(hipGetDevice(&dev), "hipGetDevice");
@@ -268,7 +269,7 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
     hchk(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event");
     hchk(hipEventRecord(ready, base), "event record");
     for (int g = 0; g < ng; ++g) {
-      GpuSlot& s = slots()[g];
+      GpuSlot& s = slots()[sb + g];
       if (s.stream == nullptr || s.device != dev) {
         hchk(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "stream");
         s.device = dev;
@@ -281,7 +282,7 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
       th.emplace_back([&, g]() {
         try {
           hchk(hipSetDevice(dev), "hipSetDevice");
-          GpuBackend bk(slots()[g], a, g);
+          GpuBackend bk(slots()[sb + g], a, g);
           tmog::grow_group(bk, a, g, res->groups[g]);
         } catch (const std::exception& e) {
           errs[g] = e.what();
@@ -292,7 +293,7 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
     for (int g = 0; g < ng; ++g) {
       hipEvent_t done;
       hchk(hipEventCreateWithFlags(&done, hipEventDisableTiming), "event");
-      hchk(hipEventRecord(done, slots()[g].stream), "event record");
+      hchk(hipEventRecord(done, slots()[sb + g].stream), "event record");
       hchk(hipStreamWaitEvent(base, done, 0), "base wait");
       hchk(hipEventDestroy(done), "event destroy");
     }

@@ -153,13 +153,31 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
   const float* qs = qscale + model * S;
   const uint32_t* rp = rows + it.begin;
   const int64_t cnt = it.count;
-  for (int64_t base = (int64_t)wave * 64; base < cnt; base += (int64_t)nwaves * 64) {
-    const int64_t ri = min(base + lane, cnt - 1);
+  const float* t1m = t1 + model * stride;
+  const float* t2m = t2 + model * stride;
+  // One-chunk-ahead pipeline (as in hist_wide_item): the next chunk's entry is loaded before this
+  // chunk's list walk, its statistics and list bounds after the first batch of id loads.
+  const int64_t step = (int64_t)nwaves * 64;
+  uint32_t e_n = 0;
+  float g_n = 0.f, h_n = 0.f;
+  int64_t p0_n = 0, p1_n = 0;
+  if ((int64_t)wave * 64 < cnt) {
+    e_n = rp[min((int64_t)wave * 64 + lane, cnt - 1)];
+    const int64_t r = e_n & 0xFFFFFFu;
+    g_n = t1m[r]; h_n = t2m[r]; p0_n = csr_ptr[r]; p1_n = csr_ptr[r + 1];
+  }
+  for (int64_t base = (int64_t)wave * 64; base < cnt; base += step) {
     const int nrows = (int)min((int64_t)64, cnt - base);
-    const int4 mine = stage_row<2>(rp[ri], model, stride, nullptr, t1, t2, qs);
-    const int64_t r = (uint32_t)mine.x & 0xFFFFFFu;
-    const int64_t q0 = csr_ptr[r];
-    const int len = lane < nrows ? (int)(csr_ptr[r + 1] - q0) : 0;
+    const float wt = (float)(e_n >> 24);
+    int4 mine;
+    mine.x = (int)e_n;
+    mine.y = (int)rintf((wt * g_n) * qs[0]);
+    mine.z = (int)rintf((wt * h_n) * qs[1]);
+    mine.w = 0;
+    const int64_t q0 = p0_n;
+    const int len = lane < nrows ? (int)(p1_n - p0_n) : 0;
+    const bool more = base + step < cnt;             // wave-uniform
+    if (more) e_n = rp[min(base + step + lane, cnt - 1)];
     // Lane groups of W (a power of two >= this chunk's longest list, <= 64) take one row each, so a
     // wave-instruction covers 64 / W rows at (nearly) full lane use instead of one row per instruction
     // (the headline's rows carry ~17 entries). Row records reach the group by ds_bpermute.
@@ -187,6 +205,12 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
         ok[u] = k < ln[u];
         col[u] = csr_col[ok[u] ? k0[u] + k : k0[u] > 0 ? k0[u] - 1 : 0];   // unpredicated load of a valid id
       }
+      __builtin_amdgcn_sched_barrier(0);
+      if (j0 == 0 && more) {
+        const int64_t r = e_n & 0xFFFFFFu;
+        g_n = t1m[r]; h_n = t2m[r]; p0_n = csr_ptr[r]; p1_n = csr_ptr[r + 1];
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < kCsrG; ++u)
         if (ok[u]) {
@@ -262,10 +286,29 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
   const uint32_t* rp = rows + it.begin;
   const int64_t cnt = it.count;
   const uint8_t* xb0 = Xb + col0 + 4 * d;
-  for (int64_t base = (int64_t)wave * 64; base < cnt; base += (int64_t)nwaves * 64) {
-    const int64_t ri = min(base + lane, cnt - 1);
+  const float* t1m = t1 + model * stride;
+  const float* t2m = t2 + model * stride;
+  // Software pipeline over the wave's 64-row chunks: the next chunk's row entry is loaded before this
+  // chunk's bin gathers and its (g, h) right after them, so the dependent entry -> statistic -> bin
+  // latency chain of a chunk overlaps the previous chunk's gathers and atomics instead of adding up.
+  const int64_t step = (int64_t)nwaves * 64;
+  uint32_t e_n = 0;
+  float g_n = 0.f, h_n = 0.f;
+  if ((int64_t)wave * 64 < cnt) {
+    e_n = rp[min((int64_t)wave * 64 + lane, cnt - 1)];
+    g_n = t1m[e_n & 0xFFFFFFu];
+    h_n = t2m[e_n & 0xFFFFFFu];
+  }
+  for (int64_t base = (int64_t)wave * 64; base < cnt; base += step) {
     const int nrows = (int)min((int64_t)64, cnt - base);
-    const int4 mine = stage_row<2>(rp[ri], model, stride, nullptr, t1, t2, qs);
+    const float wt = (float)(e_n >> 24);
+    int4 mine;
+    mine.x = (int)e_n;
+    mine.y = (int)rintf((wt * g_n) * qs[0]);
+    mine.z = (int)rintf((wt * h_n) * qs[1]);
+    mine.w = 0;
+    const bool more = base + step < cnt;             // wave-uniform
+    if (more) e_n = rp[min(base + step + lane, cnt - 1)];
     stage[lane] = mine;
     if (sparse) {
       int a = lane < nrows ? mine.y : 0, b = lane < nrows ? mine.z : 0;
@@ -280,17 +323,23 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0): staged records visible to the wave
     __builtin_amdgcn_wave_barrier();
-    for (int j0 = 0; j0 < nrows; j0 += RPI * kWideU) {
+    {                                          // RPI * kWideU >= 64 (ND <= 16): one pass covers the chunk
       int4 st[kWideU];
       uint32_t w[kWideU];
 #pragma unroll
-      for (int u = 0; u < kWideU; ++u) st[u] = stage[min(j0 + u * RPI + rs, 63)];
+      for (int u = 0; u < kWideU; ++u) st[u] = stage[min(u * RPI + rs, 63)];
 #pragma unroll
       for (int u = 0; u < kWideU; ++u)
         w[u] = *reinterpret_cast<const uint32_t*>(xb0 + (int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F);
+      __builtin_amdgcn_sched_barrier(0);       // keep the next chunk's statistic loads behind the gathers
+      if (more) {
+        g_n = t1m[e_n & 0xFFFFFFu];
+        h_n = t2m[e_n & 0xFFFFFFu];
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < kWideU; ++u) {
-        if (!active || j0 + u * RPI + rs >= nrows) continue;
+        if (!active || u * RPI + rs >= nrows) continue;
         const unsigned long long pk = ((unsigned long long)(uint32_t)st[u].y << 32) +
                                       (unsigned long long)(uint32_t)st[u].z;
 #pragma unroll

@@ -34,6 +34,15 @@ def problem_type_of(metrics: Dict) -> str:
 
 
 @register_stage
+
+def _global_label_counts(y):
+    """Label value counts over every rank's rows (one small object all-gather instead of gathering all
+    labels to every rank); what the splitters' ``pre_validation_prepare`` needs."""
+    from collections import Counter
+    from ..parallel import dp
+    from ..tuning.splitters import label_counts
+    return dict(dp.merge_counters([Counter(label_counts(y))])[0])
+
 class SelectedModel(OpPredictorModel):
     operation_name = "modelSelection"
 
@@ -83,7 +92,7 @@ class ModelSelector(BinaryEstimator):
         from ..parallel import dp
         label, vec = self._inputs[0].name, self._inputs[1].name
         if self.splitter is not None:
-            self._split_summary = self.splitter.pre_validation_prepare(dp.rows(data[label].values))
+            self._split_summary = self.splitter.pre_validation_prepare(_global_label_counts(data[label].values))
         if not during:
             self.best_estimator = None
             return None
@@ -107,7 +116,7 @@ class ModelSelector(BinaryEstimator):
             if self.best_estimator is not None and getattr(self, "_split_summary", None) is not None:
                 split_summary = self._split_summary
             else:
-                split_summary = self.splitter.pre_validation_prepare(dp.rows(y))
+                split_summary = self.splitter.pre_validation_prepare(_global_label_counts(y))
         # only the rows some CV fold or the refit may train on (the splitter's maxTrainingSample cap) are
         # materialised from the (blocked) feature vector; folds are functions of the global row id
         X, y, row_ids = self._gather_candidates(vec_col, y, row_ids)

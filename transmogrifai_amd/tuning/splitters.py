@@ -85,7 +85,9 @@ class Splitter:
         test = u < self.reserve_test_fraction
         return ~test, test
 
-    def pre_validation_prepare(self, y: torch.Tensor, n_total: Optional[int] = None) -> Dict:
+    def pre_validation_prepare(self, y, n_total: Optional[int] = None) -> Dict:
+        """Prepare from the labels: a tensor, or their value counts ``{label: count}`` (what every
+        splitter needs -- data-parallel callers merge per-rank counts instead of gathering labels)."""
         raise NotImplementedError
 
     def validation_prepare(self, row_ids: torch.Tensor, y: torch.Tensor, stream: int = 7) -> torch.Tensor:
@@ -100,9 +102,20 @@ class Splitter:
         return {"className": type(self).__name__, "uid": self.uid, "params": self.params()}
 
 
+def label_counts(y) -> Dict[float, int]:
+    """``{label value: count}`` of a label tensor (a dict is returned as is)."""
+    if isinstance(y, dict):
+        return y
+    vals, cnt = torch.unique(y.to(torch.float64), return_counts=True)
+    return dict(zip(vals.tolist(), cnt.tolist()))
+
+
 class DataSplitter(Splitter):
     def pre_validation_prepare(self, y, n_total=None):
-        n = int(y.shape[0]) if n_total is None else int(n_total)
+        if n_total is not None:
+            n = int(n_total)
+        else:
+            n = int(sum(y.values())) if isinstance(y, dict) else int(y.shape[0])
         self.down_sample_fraction = min(self.max_training_sample / max(n, 1), 1.0)
         self.summary = {"className": "com.salesforce.op.stages.impl.tuning.DataSplitterSummary",
                         "preSplitterDataCount": n, "downSamplingFraction": self.down_sample_fraction}
@@ -126,8 +139,9 @@ class DataBalancer(Splitter):
         self.positive_is_small = True
 
     def pre_validation_prepare(self, y, n_total=None):
-        pos = float((y > 0.5).sum())
-        neg = float((y <= 0.5).sum())
+        cnt = label_counts(y)
+        pos = float(sum(c for v, c in cnt.items() if v > 0.5))
+        neg = float(sum(c for v, c in cnt.items() if not v > 0.5))
         small, big = (pos, neg) if pos < neg else (neg, pos)
         self.positive_is_small = pos < neg
         total = small + big
@@ -202,9 +216,9 @@ class DataCutter(Splitter):
         self.labels_kept = None
 
     def pre_validation_prepare(self, y, n_total=None):
-        vals, cnt = torch.unique(y.to(torch.float64), return_counts=True)
-        tot = float(cnt.sum())
-        order = sorted(zip(vals.tolist(), cnt.tolist()), key=lambda vc: (-vc[1], vc[0]))
+        cnt = label_counts(y)
+        tot = float(sum(cnt.values()))
+        order = sorted(cnt.items(), key=lambda vc: (-vc[1], vc[0]))
         kept = [v for v, c in order if c / tot >= self.min_label_fraction][:self.max_label_categories]
         dropped = [v for v, _ in order if v not in set(kept)]
         self.labels_kept = sorted(kept)
