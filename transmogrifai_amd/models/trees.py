@@ -530,10 +530,18 @@ def _run_parts(dev, parts, fn):
             errs.append(e)
 
     th = [threading.Thread(target=work, args=(k,), daemon=True) for k in range(len(parts))]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
+    # a thread returning from a native call must win the GIL back from the one running Python: the
+    # default 5 ms switch interval would stall it for up to a whole boosting round
+    import sys
+    swi = sys.getswitchinterval()
+    sys.setswitchinterval(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5")))
+    try:
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    finally:
+        sys.setswitchinterval(swi)
     for s in streams:
         cur.wait_stream(s)
     if errs:
