@@ -141,6 +141,28 @@ def test_xgb_pipelined_parts_identical_to_single_loop(monkeypatch):
     assert _native_loaded()
 
 
+def test_aupr_counts_kernel_matches_torch():
+    """Early-stopping AuPR from (label, score-bin) count tables: HIP kernel vs the torch path, including
+    leading empty bins, a set without positives and an empty set."""
+    from transmogrifai_amd.evaluators.metrics import _aupr_from_counts_torch, binned_aupr_from_counts
+    g = torch.Generator().manual_seed(7)
+    K, bins = 6, 1 << 16
+    h = torch.randint(0, 4, (K, 2, bins), generator=g, dtype=torch.int32)
+    h[:, :, : bins // 3] = 0                                   # leading empty bins
+    h[1, :, ::5] = 0
+    h[2, 1] = 0                                                # no positives
+    h[3] = 0                                                   # empty
+    h[4, :, bins - 7:] = 0                                     # trailing empty bins
+    h[5] = 0
+    h[5, 0, 100] = 3
+    h[5, 1, 101] = 2
+    want = _aupr_from_counts_torch(h.double()).numpy()
+    got = binned_aupr_from_counts(h.cuda()).cpu().numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-14)
+    assert got[2] == 0.0 and got[3] == 0.0
+    assert _native_loaded()
+
+
 def test_row_uniform_kernel_bit_identical():
     from transmogrifai_amd.tuning import splitters as SP
     rid = torch.randint(0, 1 << 40, (100_003,), dtype=torch.int64)

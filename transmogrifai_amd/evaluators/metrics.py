@@ -120,6 +120,20 @@ def binned_aupr_from_counts(h: torch.Tensor) -> torch.Tensor:
     score order (as filled by :func:`binned_aupr_multi` or the fused boosting-round kernel)."""
     K = h.shape[0]
     dev = h.device
+    if dev.type == "cuda" and K > 0 and h.dtype == torch.int32:
+        # one HIP launch (ops/csrc/hip/boost_kernels.hip aupr_counts_kernel), same per-bin arithmetic
+        from ..ops import _native as NV
+        hc = h.contiguous()
+        out = torch.empty(K, dtype=torch.float64, device=dev)
+        NV.check(NV.hip().tmog_hip_aupr_counts(NV.ptr(hc), int(K), int(hc.shape[2]), NV.ptr(out), NV.stream(dev)),
+                 "aupr_counts")
+        return out
+    return _aupr_from_counts_torch(h)
+
+
+def _aupr_from_counts_torch(h: torch.Tensor) -> torch.Tensor:
+    K = h.shape[0]
+    dev = h.device
     h = h.to(torch.float64)
     neg, pos = h[:, 0], h[:, 1]
     tp, fp = torch.cumsum(pos, 1), torch.cumsum(neg, 1)

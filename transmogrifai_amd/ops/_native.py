@@ -59,7 +59,7 @@ _HOST_SIGS = {
 }
 
 _HIP_SIGS = {
-    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P, P, I32, P],
+    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P, P, I32, I32, I32, P],
     "tmog_hip_hist_stat_chunk": [I32, I32],
     "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
     "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P, I32, P,
@@ -78,6 +78,7 @@ _HIP_SIGS = {
     "tmog_hip_grow_free": [P],
     "tmog_hip_zero_segments": [P, P, P, I32, I64, P],
     "tmog_hip_boost_epilogue": [P, P, I64, P, P, P, I64, P, P, P, P, I32, P, I32, I64, I64, I64, P],
+    "tmog_hip_aupr_counts": [P, I32, I32, P, P],
     "tmog_hip_poisson_pack": [P, I64, P, I32, P, I32, P, P, P, P],
     "tmog_hip_row_uniform": [P, I64, P, I32, P, P],
     "tmog_hip_lr_objective": [P, I64, I32, P, P, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P],

@@ -336,7 +336,9 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     if (BK::kGPU && n_multi > 0) live_dense = (int64_t)n_multi * a.B * a.S;
     perm_feats.insert(perm_feats.end(), one.begin() + o0, one.begin() + o1);
     const char* wenv = std::getenv("TMOG_HIST_WIDE");
-    const bool wide_ok = BK::kGPU && a.mode == 2 && S == 2 && F % 4 == 0 && !(wenv && wenv[0] == '0');
+    // (32-bit buffer offsets row * F + column: matrices below 2 GiB)
+    const bool wide_ok = BK::kGPU && a.mode == 2 && S == 2 && F % 4 == 0 && !(wenv && wenv[0] == '0') &&
+                         (int64_t)a.N * F < ((int64_t)1 << 31) - 64;
     for (FeatGroup g : (wide_ok ? equal_groups4(n_multi) : equal_groups(n_multi))) {
       if (wide_ok) {
         bool ok = perm_feats[g.f0] % 4 == 0;
@@ -347,7 +349,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     }
     const int n_one = o1 - o0;
     if (BK::kGPU && a.csr_ptr && a.csr_col && n_multi > 0 && n_one > 0 && a.csr_nf == n_one &&
-        2 * n_one + 2 <= 64 * (B * S + 1))
+        2 * n_one + 4 + 64 * 4 <= 64 * (B * S + 1))   // sums + list lengths of the CSR item (tree_kernels.hip)
       full_groups.push_back(FeatGroup{n_multi, n_one, false, true});   // one item walks the rows' CSR lists
     else
       for (const FeatGroup& g : equal_groups(n_one))
@@ -511,6 +513,12 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
           }
       }
     }
+    // wide-load items first: the GPU launches them as a kernel of their own (fewer registers)
+    const auto wide_end = std::stable_partition(hitems.begin(), hitems.end(),
+                                                [](const HistItemH& h) { return (h.excl & 16) != 0; });
+    const int n_wide = (int)(wide_end - hitems.begin());
+    int need_general = 0;          // any item on the byte-gather path (not CSR, not wide-load)?
+    for (const HistItemH& h : hitems) need_general |= (h.excl & (4 | 16)) == 0;
     std::vector<int64_t> d_soff, d_ooff, d_size;
     int64_t d_max = 0;
     for (size_t q = 0; q < d_big.size(); ++q) {
@@ -543,7 +551,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
                   TM_P(const int32_t, o_nfo), flist, TM_P(const int32_t, o_nmd), TM_P(const int64_t, o_nho), hist,
                   (int)b_nb.size(), TM_P(const int64_t, o_bnb), TM_P(const int64_t, o_bnc),
                   TM_P(const int32_t, o_bnfo), TM_P(const int32_t, o_bnnf), TM_P(const int32_t, o_bnmd),
-                  TM_P(const int64_t, o_bnho), stat_sc);
+                  TM_P(const int64_t, o_bnho), stat_sc, n_wide, need_general);
     if (!d_big.empty())
       bk.hist_subtract(hist, prev_hist, TM_P(const int64_t, o_dp), TM_P(const int64_t, o_ds),
                        TM_P(const int64_t, o_do), TM_P(const int64_t, o_dz), (int)d_big.size(), d_max, live_dense,

@@ -127,6 +127,79 @@ __global__ void __launch_bounds__(256) row_uniform_kernel(const int64_t* __restr
 
 }  // namespace
 
+
+// AuPR of K score sets from their (label, score-bin) count tables [K][2][bins] (bins in descending score
+// order; the boosting-round early-stopping metric, evaluators/metrics.py binned_aupr_from_counts): one
+// workgroup per set. Segment sums + a block scan give every thread its cumulative (tp, fp) entering its
+// 256-bin segment; the thread then walks the segment with the same per-bin arithmetic as the torch path
+// (precision tp / cnt, recall tp / P, trapezoid ((r - r') * (p + p')) * 0.5, leading empty bins taking the
+// first non-empty bin's precision) and the block sums the terms -- one launch instead of two 65536-long
+// fp64 scans plus ~20 small kernels per round.
+__global__ void __launch_bounds__(256) aupr_counts_kernel(const int32_t* __restrict__ counts, int bins,
+                                                          double* __restrict__ out) {
+  const int k = blockIdx.x, t = threadIdx.x;
+  const int32_t* neg = counts + (int64_t)k * 2 * bins;
+  const int32_t* pos = neg + bins;
+  const int seg = (bins + 255) / 256;
+  const int b0 = min(bins, t * seg), b1 = min(bins, b0 + seg);
+  long long sp = 0, sn = 0;
+  int first = 0x7fffffff;
+  for (int b = b0; b < b1; ++b) {
+    const int p = pos[b], n = neg[b];
+    sp += p;
+    sn += n;
+    if (p + n > 0 && first == 0x7fffffff) first = b;
+  }
+  __shared__ long long s_p[256], s_n[256];
+  __shared__ int s_first[256];
+  __shared__ double s_area[256];
+  s_p[t] = sp;
+  s_n[t] = sn;
+  s_first[t] = first;
+  __syncthreads();
+  if (t == 0) {                    // exclusive scan of 256 segment totals + global first non-empty bin
+    long long ap = 0, an = 0;
+    int f = 0x7fffffff;
+    for (int i = 0; i < 256; ++i) {
+      const long long vp = s_p[i], vn = s_n[i];
+      s_p[i] = ap;
+      s_n[i] = an;
+      ap += vp;
+      an += vn;
+      f = min(f, s_first[i]);
+    }
+    s_first[0] = f == 0x7fffffff ? 0 : f;
+    s_area[0] = (double)ap;        // total positives P
+  }
+  __syncthreads();
+  const double Pt = s_area[0];
+  const double Pm = Pt > 1.0 ? Pt : 1.0;
+  const int fb = s_first[0];
+  const double pf = (double)pos[fb] / fmax((double)pos[fb] + (double)neg[fb], 1.0);   // prec at the first bin
+  double tp = (double)s_p[t], fp = (double)s_n[t];
+  double prev_prec = (tp + fp > 0.0) ? tp / fmax(tp + fp, 1.0) : pf;
+  double prev_rec = tp / Pm;
+  double acc = 0.0;
+  for (int b = b0; b < b1; ++b) {
+    tp += (double)pos[b];
+    fp += (double)neg[b];
+    const double cnt = tp + fp;
+    const double pr = cnt > 0.0 ? tp / fmax(cnt, 1.0) : pf;
+    const double rc = tp / Pm;
+    acc += ((rc - prev_rec) * (pr + prev_prec)) * 0.5;
+    prev_prec = pr;
+    prev_rec = rc;
+  }
+  __syncthreads();
+  s_area[t] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) s_area[t] += s_area[t + w];
+    __syncthreads();
+  }
+  if (t == 0) out[k] = Pt > 0.0 ? s_area[0] : 0.0;
+}
+
 extern "C" {
 
 int tmog_hip_boost_epilogue(const uint32_t* entries, const int32_t* gid, int64_t n_entries, const float* gid_value,
@@ -157,6 +230,13 @@ int tmog_hip_row_uniform(const int64_t* row_ids, int64_t n, const int64_t* offse
   if (n == 0 || k_seeds == 0) return 0;
   hipLaunchKernelGGL(row_uniform_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, row_ids, n, offsets,
                      k_seeds, out);
+  return (int)hipGetLastError();
+}
+
+int tmog_hip_aupr_counts(const int32_t* counts, int K, int bins, double* out, hipStream_t stream) {
+  if (K <= 0) return 0;
+  if (bins <= 0) return -2;
+  hipLaunchKernelGGL(aupr_counts_kernel, dim3(K), dim3(256), 0, stream, counts, bins, out);
   return (int)hipGetLastError();
 }
 

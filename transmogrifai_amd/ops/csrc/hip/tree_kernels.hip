@@ -16,6 +16,7 @@
 // the workgroup share the table through integer LDS atomics; the R copies are folded on the way out
 // and a node covered by one row-chunk stores with plain stores, otherwise 64-bit integer atomics.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 #include <math.h>
 
@@ -147,6 +148,9 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int nwaves = blockDim.x >> 6;
+  const int soff = (2 * nf + 3) & ~3;        // per-wave row stage + list lengths after the sums
+  int4* stg = reinterpret_cast<int4*>(lds + soff) + wave * 64;
+  int* lens = lds + soff + 4 * 64 * nwaves + wave * 64;
   for (int i = threadIdx.x; i < 2 * nf; i += blockDim.x) lds[i] = 0;
   __syncthreads();
   const int64_t model = node_model ? node_model[it.node] : 0;
@@ -178,32 +182,33 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
     const int len = lane < nrows ? (int)(p1_n - p0_n) : 0;
     const bool more = base + step < cnt;             // wave-uniform
     if (more) e_n = rp[min(base + step + lane, cnt - 1)];
+    // Row records go through the wave's LDS stage (q(g), q(h), list start) + list length: the lane groups
+    // read them with plain LDS loads (no cross-lane shuffles, whose sources must all be active) and keep
+    // only the entry ids in registers across the id gathers.
+    stg[lane] = make_int4(mine.y, mine.z, (int)(uint32_t)(uint64_t)q0, (int)((uint64_t)q0 >> 32));
+    lens[lane] = len;
     // Lane groups of W (a power of two >= this chunk's longest list, <= 64) take one row each, so a
     // wave-instruction covers 64 / W rows at (nearly) full lane use instead of one row per instruction
-    // (the headline's rows carry ~17 entries). Row records reach the group by ds_bpermute.
+    // (the headline's rows carry ~17 entries).
     int mx = len;
     for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
     const int W = mx <= 8 ? 8 : mx <= 16 ? 16 : mx <= 32 ? 32 : 64;
     const int RPI = 64 / W;
     const int rs = lane / W, k = lane - rs * W;
-    const int q0lo = (int)(uint32_t)(uint64_t)q0, q0hi = (int)((uint64_t)q0 >> 32);
+    __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0): staged records visible to the wave
+    __builtin_amdgcn_wave_barrier();
     for (int j0 = 0; j0 < nrows; j0 += RPI * kCsrG) {
-      int col[kCsrG], gq[kCsrG], hq[kCsrG], ln[kCsrG];
-      int64_t k0[kCsrG];
+      int col[kCsrG];
       bool ok[kCsrG];
 #pragma unroll
       for (int u = 0; u < kCsrG; ++u) {
         const int src = j0 + u * RPI + rs;
         const int sl = min(src, 63);
-        // every shuffle runs with the full wave active: a bpermute under a divergent EXEC mask reads 0
-        // from source lanes that are off (in a tail chunk lane sl's own src can be >= nrows)
-        const int lsh = __shfl(len, sl, 64);
-        ln[u] = src < nrows ? lsh : 0;
-        k0[u] = (int64_t)(((uint64_t)(uint32_t)__shfl(q0hi, sl, 64) << 32) | (uint64_t)(uint32_t)__shfl(q0lo, sl, 64));
-        gq[u] = __shfl(mine.y, sl, 64);
-        hq[u] = __shfl(mine.z, sl, 64);
-        ok[u] = k < ln[u];
-        col[u] = csr_col[ok[u] ? k0[u] + k : k0[u] > 0 ? k0[u] - 1 : 0];   // unpredicated load of a valid id
+        const int ln = src < nrows ? lens[sl] : 0;
+        const int4 rr = stg[sl];
+        const int64_t k0 = (int64_t)(((uint64_t)(uint32_t)rr.w << 32) | (uint64_t)(uint32_t)rr.z);
+        ok[u] = k < ln;
+        col[u] = csr_col[ok[u] ? k0 + k : k0 > 0 ? k0 - 1 : 0];   // unpredicated load of a valid id
       }
       __builtin_amdgcn_sched_barrier(0);
       if (j0 == 0 && more) {
@@ -214,17 +219,28 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
 #pragma unroll
       for (int u = 0; u < kCsrG; ++u)
         if (ok[u]) {
-          atomicAdd(a0 + col[u], gq[u]);
-          atomicAdd(a1 + col[u], hq[u]);
+          const int2 gh = *reinterpret_cast<const int2*>(&stg[min(j0 + u * RPI + rs, 63)]);
+          atomicAdd(a0 + col[u], gh.x);
+          atomicAdd(a1 + col[u], gh.y);
         }
+      if (W == 64) {                       // lists longer than the lane group
 #pragma unroll
-      for (int u = 0; u < kCsrG; ++u)      // lists longer than the lane group (only when W == 64)
-        for (int kk = k + W; kk < ln[u]; kk += W) {
-          const int c = csr_col[k0[u] + kk];
-          atomicAdd(a0 + c, gq[u]);
-          atomicAdd(a1 + c, hq[u]);
+        for (int u = 0; u < kCsrG; ++u) {
+          const int src = j0 + u * RPI + rs;
+          const int sl = min(src, 63);
+          const int ln = src < nrows ? lens[sl] : 0;
+          if (ln <= 64) continue;
+          const int4 rr = stg[sl];
+          const int64_t k0 = (int64_t)(((uint64_t)(uint32_t)rr.w << 32) | (uint64_t)(uint32_t)rr.z);
+          for (int kk = k + 64; kk < ln; kk += 64) {
+            const int c = csr_col[k0 + kk];
+            atomicAdd(a0 + c, rr.x);
+            atomicAdd(a1 + c, rr.y);
+          }
         }
+      }
     }
+    __builtin_amdgcn_wave_barrier();           // the stage is rewritten by the next chunk
   }
   __syncthreads();
   // Only bin 0 of these columns is written: the split scan and split reduce evaluate a one-present-bin
@@ -273,7 +289,7 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
   // (dword d = features 4d..4d+3) to distinct LDS banks for the 64-bit atomics (8 * tstride alone is
   // 0 mod 8 dwords for any B, a 4-way conflict)
   auto tix = [tstride](int f, int b) { return f * tstride + (f >> 2) + b; };
-  const int twords = FG * tstride + (FG >> 2) + 1;
+  const int twords = 4 * ND * tstride + ND + 1;      // rows for the pad features of the last dword too
   const int toff = (2 * twords + 3) & ~3;
   int4* stage = reinterpret_cast<int4*>(lds + toff) + wave * 64;
   int* tot = lds + toff + 4 * 64 * nwaves;
@@ -285,7 +301,15 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
   const float* qs = qscale + model * 2;
   const uint32_t* rp = rows + it.begin;
   const int64_t cnt = it.count;
-  const uint8_t* xb0 = Xb + col0 + 4 * d;
+  // buffer loads: one descriptor for the group's first column (wave-uniform) and a 32-bit per-lane byte
+  // offset row * F + 4 d (the grower takes this path only for matrices below 2 GiB) -- one VGPR per
+  // gather address instead of two
+  const uint64_t xbase = (uint64_t)(uintptr_t)(Xb + col0);
+  const uint32_t xlo = __builtin_amdgcn_readfirstlane((uint32_t)xbase);
+  const uint32_t xhi = __builtin_amdgcn_readfirstlane((uint32_t)(xbase >> 32));
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(uintptr_t)(((uint64_t)xhi << 32) | xlo), (short)0, 0x7FFFFFFF, 0x00020000);
+  const uint32_t lane_off = 4u * (uint32_t)d;
   const float* t1m = t1 + model * stride;
   const float* t2m = t2 + model * stride;
   // Software pipeline over the wave's 64-row chunks: the next chunk's row entry is loaded before this
@@ -309,7 +333,7 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
     mine.w = 0;
     const bool more = base + step < cnt;             // wave-uniform
     if (more) e_n = rp[min(base + step + lane, cnt - 1)];
-    stage[lane] = mine;
+    stage[lane] = make_int4(mine.y, mine.z, mine.x, 0);   // (q(g), q(h), entry): (g, h) 8-byte aligned
     if (sparse) {
       int a = lane < nrows ? mine.y : 0, b = lane < nrows ? mine.z : 0;
       for (int off = 32; off > 0; off >>= 1) {
@@ -324,29 +348,35 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
     __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0): staged records visible to the wave
     __builtin_amdgcn_wave_barrier();
     {                                          // RPI * kWideU >= 64 (ND <= 16): one pass covers the chunk
-      int4 st[kWideU];
-      uint32_t w[kWideU];
-#pragma unroll
-      for (int u = 0; u < kWideU; ++u) st[u] = stage[min(u * RPI + rs, 63)];
+      // only the row ids stay in registers across the gathers; (g, h) are re-read from the LDS stage
+      // at the atomics (fewer VGPRs -> more waves, i.e. more gathers in flight per CU)
+      uint32_t off[kWideU], w[kWideU];
 #pragma unroll
       for (int u = 0; u < kWideU; ++u)
-        w[u] = *reinterpret_cast<const uint32_t*>(xb0 + (int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F);
+        off[u] = __umul24((uint32_t)stage[min(u * RPI + rs, 63)].z & 0xFFFFFFu, (uint32_t)F) + lane_off;
+#pragma unroll
+      for (int u = 0; u < kWideU; ++u) w[u] = __builtin_amdgcn_raw_buffer_load_b32(xrs, (int)off[u], 0, 0);
       __builtin_amdgcn_sched_barrier(0);       // keep the next chunk's statistic loads behind the gathers
       if (more) {
         g_n = t1m[e_n & 0xFFFFFFu];
         h_n = t2m[e_n & 0xFFFFFFu];
       }
       __builtin_amdgcn_sched_barrier(0);
+      // branch-free: masked-off work (lanes past the rows, pad features) adds 0 to the lane's own word
+      // instead of toggling EXEC around every atomic (a masked lane costs the same)
 #pragma unroll
       for (int u = 0; u < kWideU; ++u) {
-        if (!active || u * RPI + rs >= nrows) continue;
-        const unsigned long long pk = ((unsigned long long)(uint32_t)st[u].y << 32) +
-                                      (unsigned long long)(uint32_t)st[u].z;
+        const bool live = active && u * RPI + rs < nrows;
+        const int2 st = *reinterpret_cast<const int2*>(&stage[min(u * RPI + rs, 63)]);
+        const unsigned long long pk = live ? ((unsigned long long)(uint32_t)st.x << 32) + (unsigned long long)(uint32_t)st.y
+                                           : 0ull;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int f = 4 * d + k;
           const int bin = (int)((w[u] >> (8 * k)) & 0xFFu);
-          if (f < FG && bin != skip_bin) atomicAdd(tab + tix(f, bin), pk);
+          // the skipped missing bin's own word is never read (recovered into the pad word below), and the
+          // table has rows for the group's pad features 4 ND > FG, so every lane adds to its own word
+          atomicAdd(tab + tix(f, bin), f < FG ? pk : 0ull);
         }
       }
     }
@@ -390,7 +420,28 @@ constexpr int HIST_U = 16;   // row bins gathered per lane before their LDS atom
 // dense multi-bin items -- the trees are then wrong; used to time the item kinds separately.
 __device__ int g_hist_debug = 0;
 
-template <int MODE>
+// Wide-load items in a kernel of their own (TMOG_HIST_WIDE_SPLIT=1; the grower puts them first): the mixed
+// kernel's register budget is set by its general and CSR paths, this one's by the wide path alone, so
+// more waves -- more row gathers in flight -- fit on a CU (OCC = requested waves per SIMD: 7 is
+// the LDS limit of these 21 KB workgroups, at a couple of spilled registers; TMOG_HIST_WIDE_OCC picks).
+template <int OCC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) hist_wide_kernel(
+    const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const HistItem* __restrict__ items,
+    const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
+    const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
+    int B, const float* __restrict__ t1, const float* __restrict__ t2, int64_t stride,
+    const float* __restrict__ qscale, int skip_bin) {
+  extern __shared__ int lds_w[];
+  if (g_hist_debug & 2) return;
+  const HistItem it = items[blockIdx.x];
+  hist_wide_item(it, Xb, F, feat_list[node_feat_off[it.node] + it.fg0], rows, node_model, node_hist_off, hist, B,
+                 t1, t2, stride, qscale, skip_bin, lds_w);
+}
+
+
+// GEN = false (MODE 2 launches whose items are all CSR / wide-load, the XGBoost case): the byte-gather
+// path is not compiled in, so its registers do not cap the occupancy of the other two (106 -> ~74 VGPRs).
+template <int MODE, bool GEN = true>
 __global__ void __launch_bounds__(256) hist_build_kernel(
     const uint8_t* __restrict__ Xb, int F, const uint32_t* __restrict__ rows, const HistItem* __restrict__ items,
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
@@ -416,6 +467,9 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
                    t1, t2, stride, qscale, skip_bin, lds);
     return;
   }
+  if constexpr (!GEN) {
+    return;
+  } else {
   const int FG = it.nf;
   const int R = 64 / FG;
   const int rowstride = B * sc + 1;           // padded feature row (this item's statistic chunk)
@@ -550,6 +604,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     if (excl) *w = acc;
     else if (acc != 0) atomicAdd(reinterpret_cast<unsigned long long*>(w), (unsigned long long)acc);
   }
+  }   // GEN
 }
 
 // sibling = parent - small (histogram subtraction trick), size words each
@@ -1294,7 +1349,8 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
-                        const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, hipStream_t stream) {
+                        const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
+                        hipStream_t stream) {
   if (n_items == 0) return 0;
   if (Sc <= 0 || Sc > S) Sc = S;
   size_t lds = (size_t)(((64 * (B * Sc + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
@@ -1309,6 +1365,25 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
   if (mode == 0 && S > TM_WIDE_MAX_S) return -2;
   if ((csr_ptr != nullptr) != (csr_col != nullptr) || (csr_ptr && (mode != 2 || skip_bin <= 0))) return -2;
   const HistItem* it = (const HistItem*)items;
+  if (n_wide < 0 || n_wide > n_items || (n_wide > 0 && (mode != 2 || S != 2))) return -2;
+  // The grower lists the wide-load items first. By default they share the launch with the other items
+  // (the mixed kernel runs them concurrently with the CSR items); TMOG_HIST_WIDE_SPLIT=1 launches them
+  // as hist_wide_kernel -- measured slower on the headline (1086 vs 974 ms per step: the two launches
+  // serialise and each has its own tail), kept for experiments.
+  static const bool split_wide = [] { const char* e = std::getenv("TMOG_HIST_WIDE_SPLIT"); return e && e[0] == '1'; }();
+  if (!split_wide) n_wide = 0;
+  if (n_wide > 0) {
+    static const int occ = [] { const char* e = std::getenv("TMOG_HIST_WIDE_OCC"); return e ? std::atoi(e) : 6; }();
+    if (occ >= 7)
+      hipLaunchKernelGGL(hist_wide_kernel<7>, dim3(n_wide), dim3(256), lds, stream, Xb, F, rows, it, node_feat_off,
+                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin);
+    else
+      hipLaunchKernelGGL(hist_wide_kernel<6>, dim3(n_wide), dim3(256), lds, stream, Xb, F, rows, it, node_feat_off,
+                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin);
+    it += n_wide;
+    n_items -= n_wide;
+    if (n_items == 0) return (int)hipGetLastError();
+  }
   dim3 grid(n_items), block(256);
   if (mode == 0)
     hipLaunchKernelGGL(hist_build_kernel<0>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
@@ -1316,9 +1391,13 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
   else if (mode == 1)
     hipLaunchKernelGGL(hist_build_kernel<1>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc);
-  else
+  else if (need_general)
     hipLaunchKernelGGL(hist_build_kernel<2>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
+                       csr_col, Sc);
+  else
+    hipLaunchKernelGGL((hist_build_kernel<2, false>), grid, block, lds, stream, Xb, F, rows, it, node_feat_off,
+                       feat_list, node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
                        csr_col, Sc);
   return (int)hipGetLastError();
 }

@@ -62,7 +62,7 @@ struct CpuBackend {
   void hist_build(const tmog::GrowArgs& g, const uint32_t* rows, const void*, int, const int32_t*,
                   const int32_t* flist, const int32_t*, const int64_t*, int64_t* hist, int nbuild,
                   const int64_t* bnb, const int64_t* bnc, const int32_t* bnfo, const int32_t* bnnf,
-                  const int32_t* bnmd, const int64_t* bnho, int) {
+                  const int32_t* bnmd, const int64_t* bnho, int, int, int) {
     if (nbuild)
       tmog_hist_build_cpu(g.Xb, g.N, g.F, rows, nbuild, bnb, bnc, bnfo, bnnf, flist, bnmd, bnho, hist, g.B, g.mode,
                           g.S, g.y, g.t1, g.t2, g.stride, g.qscale);
