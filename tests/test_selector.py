@@ -112,3 +112,23 @@ def test_splitters_prepare_from_label_counts_equals_tensor():
                   (lambda: DataCutter(max_label_categories=5, max_training_sample=8_000), ym)):
         a, b = mk(), mk()
         assert a.pre_validation_prepare(y) == b.pre_validation_prepare(label_counts(y))
+
+
+def test_job_cost_model_recalibrates_from_measured_times(monkeypatch):
+    """LPT costs are seconds (work estimate x per-learner seconds-per-unit), re-calibrated from each
+    validation's measured per-learner times."""
+    from transmogrifai_amd.evaluators.evaluators import OpBinaryClassificationEvaluator
+    from transmogrifai_amd.tuning import validators as V
+    monkeypatch.setattr(V, "_COST_SCALE", dict(V._COST_SCALE))
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(600, 4, generator=g, dtype=torch.float64)
+    y = (X[:, 0] > 0).double()
+    cv = V.OpCrossValidation(num_folds=2, evaluator=OpBinaryClassificationEvaluator(), seed=1)
+    V._COST_SCALE.pop("OpNaiveBayes", None)
+    res = cv.validate([("OpNaiveBayes", [{"smoothing": 1.0}, {"smoothing": 0.5}])], X.abs(), y, torch.arange(600))
+    t = res.timings["OpNaiveBayes"]
+    sc = V._COST_SCALE["OpNaiveBayes"]
+    # 4 jobs (2 grid points x 2 folds) of n_tr x d = n_tr x 4 work units took t seconds
+    n_tr = t / (sc * 4 * 4)
+    assert 250 <= n_tr <= 350
+    assert V._scaled_cost("OpNaiveBayes", {}, n_tr, 4) == pytest.approx(t / 4)
