@@ -33,8 +33,6 @@ def problem_type_of(metrics: Dict) -> str:
     return "Regression"
 
 
-@register_stage
-
 def _global_label_counts(y):
     """Label value counts over every rank's rows (one small object all-gather instead of gathering all
     labels to every rank); what the splitters' ``pre_validation_prepare`` needs."""
@@ -43,6 +41,8 @@ def _global_label_counts(y):
     from ..tuning.splitters import label_counts
     return dict(dp.merge_counters([Counter(label_counts(y))])[0])
 
+
+@register_stage
 class SelectedModel(OpPredictorModel):
     operation_name = "modelSelection"
 
