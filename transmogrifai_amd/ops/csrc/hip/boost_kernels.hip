@@ -130,74 +130,98 @@ __global__ void __launch_bounds__(256) row_uniform_kernel(const int64_t* __restr
 
 // AuPR of K score sets from their (label, score-bin) count tables [K][2][bins] (bins in descending score
 // order; the boosting-round early-stopping metric, evaluators/metrics.py binned_aupr_from_counts): one
-// workgroup per set. Segment sums + a block scan give every thread its cumulative (tp, fp) entering its
-// 256-bin segment; the thread then walks the segment with the same per-bin arithmetic as the torch path
-// (precision tp / cnt, recall tp / P, trapezoid ((r - r') * (p + p')) * 0.5, leading empty bins taking the
-// first non-empty bin's precision) and the block sums the terms -- one launch instead of two 65536-long
-// fp64 scans plus ~20 small kernels per round.
-__global__ void __launch_bounds__(256) aupr_counts_kernel(const int32_t* __restrict__ counts, int bins,
-                                                          double* __restrict__ out) {
-  const int k = blockIdx.x, t = threadIdx.x;
+// 1024-thread workgroup per set. Pass 1 reduces the positive total P; pass 2 walks the bins in coalesced
+// 4096-bin chunks (4 consecutive bins per lane), a wave64 shuffle scan + 16 wave totals in LDS give every
+// bin its cumulative (tp, fp), and each bin's trapezoid term is evaluated independently with the torch
+// path's arithmetic (precision tp / cnt, recall tp / P, ((r - r') * (p + p')) * 0.5). The previous bin's
+// precision comes from the cumulative counts before the bin; with none before it (leading empty bins)
+// the torch path uses the first non-empty bin's precision, which is this bin's own whenever the term is
+// non-zero. Replaces a 256-thread version whose per-thread 256-bin segments were uncoalesced (181 us per
+// call at 6 x 65536 bins).
+constexpr int AUPR_NT = 1024;
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(AUPR_NT) aupr_counts_kernel(const int32_t* __restrict__ counts, int bins,
+                                                              double* __restrict__ out) {
+  const int k = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  constexpr int NW = AUPR_NT / 64;
   const int32_t* neg = counts + (int64_t)k * 2 * bins;
   const int32_t* pos = neg + bins;
-  const int seg = (bins + 255) / 256;
-  const int b0 = min(bins, t * seg), b1 = min(bins, b0 + seg);
-  long long sp = 0, sn = 0;
-  int first = 0x7fffffff;
-  for (int b = b0; b < b1; ++b) {
-    const int p = pos[b], n = neg[b];
-    sp += p;
-    sn += n;
-    if (p + n > 0 && first == 0x7fffffff) first = b;
-  }
-  __shared__ long long s_p[256], s_n[256];
-  __shared__ int s_first[256];
-  __shared__ double s_area[256];
-  s_p[t] = sp;
-  s_n[t] = sn;
-  s_first[t] = first;
+  __shared__ long long s_red[NW];
+  __shared__ int s_wp[NW], s_wn[NW];
+  __shared__ double s_acc[NW];
+  // pass 1: P
+  long long sp = 0;
+  for (int b = t; b < bins; b += AUPR_NT) sp += pos[b];
+  for (int o = 32; o > 0; o >>= 1) sp += __shfl_xor(sp, o, 64);
+  if (lane == 0) s_red[wv] = sp;
   __syncthreads();
-  if (t == 0) {                    // exclusive scan of 256 segment totals + global first non-empty bin
-    long long ap = 0, an = 0;
-    int f = 0x7fffffff;
-    for (int i = 0; i < 256; ++i) {
-      const long long vp = s_p[i], vn = s_n[i];
-      s_p[i] = ap;
-      s_n[i] = an;
-      ap += vp;
-      an += vn;
-      f = min(f, s_first[i]);
-    }
-    s_first[0] = f == 0x7fffffff ? 0 : f;
-    s_area[0] = (double)ap;        // total positives P
-  }
-  __syncthreads();
-  const double Pt = s_area[0];
+  long long Pi = 0;
+  for (int w = 0; w < NW; ++w) Pi += s_red[w];
+  const double Pt = (double)Pi;
   const double Pm = Pt > 1.0 ? Pt : 1.0;
-  const int fb = s_first[0];
-  const double pf = (double)pos[fb] / fmax((double)pos[fb] + (double)neg[fb], 1.0);   // prec at the first bin
-  double tp = (double)s_p[t], fp = (double)s_n[t];
-  double prev_prec = (tp + fp > 0.0) ? tp / fmax(tp + fp, 1.0) : pf;
-  double prev_rec = tp / Pm;
+  // pass 2: chunked scan + independent per-bin terms
+  int carry_p = 0, carry_n = 0;
   double acc = 0.0;
-  for (int b = b0; b < b1; ++b) {
-    tp += (double)pos[b];
-    fp += (double)neg[b];
-    const double cnt = tp + fp;
-    const double pr = cnt > 0.0 ? tp / fmax(cnt, 1.0) : pf;
-    const double rc = tp / Pm;
-    acc += ((rc - prev_rec) * (pr + prev_prec)) * 0.5;
-    prev_prec = pr;
-    prev_rec = rc;
-  }
-  __syncthreads();
-  s_area[t] = acc;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (t < w) s_area[t] += s_area[t + w];
+  for (int c0 = 0; c0 < bins; c0 += 4 * AUPR_NT) {
+    const int b0 = c0 + 4 * t;
+    int pv[4], nv[4];
+    int lp = 0, ln = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int b = b0 + i;
+      pv[i] = b < bins ? pos[b] : 0;
+      nv[i] = b < bins ? neg[b] : 0;
+      lp += pv[i];
+      ln += nv[i];
+    }
+    const int ip = wave_incl_scan(lp), in = wave_incl_scan(ln);
+    __syncthreads();                                   // previous chunk's readers of s_wp / s_wn are done
+    if (lane == 63) {
+      s_wp[wv] = ip;
+      s_wn[wv] = in;
+    }
     __syncthreads();
+    int ep = carry_p + ip - lp, en = carry_n + in - ln;
+    for (int w = 0; w < NW; ++w) {
+      const int a = s_wp[w], bn = s_wn[w];
+      if (w < wv) {
+        ep += a;
+        en += bn;
+      }
+      carry_p += a;
+      carry_n += bn;
+    }
+    double tp = (double)ep, fp = (double)en;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double tp1 = tp + (double)pv[i], fp1 = fp + (double)nv[i];
+      if (pv[i] > 0) {
+        const double pr = tp1 / fmax(tp1 + fp1, 1.0);
+        const double prev_prec = (tp + fp > 0.0) ? tp / fmax(tp + fp, 1.0) : pr;
+        acc += ((tp1 / Pm - tp / Pm) * (pr + prev_prec)) * 0.5;
+      }
+      tp = tp1;
+      fp = fp1;
+    }
   }
-  if (t == 0) out[k] = Pt > 0.0 ? s_area[0] : 0.0;
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) s_acc[wv] = acc;
+  __syncthreads();
+  if (t == 0) {
+    double a = 0.0;
+    for (int w = 0; w < NW; ++w) a += s_acc[w];
+    out[k] = Pt > 0.0 ? a : 0.0;
+  }
 }
 
 extern "C" {
@@ -236,7 +260,7 @@ int tmog_hip_row_uniform(const int64_t* row_ids, int64_t n, const int64_t* offse
 int tmog_hip_aupr_counts(const int32_t* counts, int K, int bins, double* out, hipStream_t stream) {
   if (K <= 0) return 0;
   if (bins <= 0) return -2;
-  hipLaunchKernelGGL(aupr_counts_kernel, dim3(K), dim3(256), 0, stream, counts, bins, out);
+  hipLaunchKernelGGL(aupr_counts_kernel, dim3(K), dim3(AUPR_NT), 0, stream, counts, bins, out);
   return (int)hipGetLastError();
 }
 

@@ -615,9 +615,10 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
 __device__ __forceinline__ int64_t live_words(int64_t sz, int64_t dense, int per, int S) {
   return (dense < 0 || sz <= dense) ? sz : dense + (sz - dense) / per * S;
 }
-__device__ __forceinline__ int64_t live_word(int64_t k, int64_t dense, int per, int S) {
+// 32-bit index math (a node's histogram is < 2^31 words; int64 division is a long software sequence)
+__device__ __forceinline__ int live_word(int k, int dense, int per, int S) {
   if (dense < 0 || k < dense) return k;
-  const int64_t t = k - dense, f = t / S;
+  const int t = k - dense, f = t / S;
   return dense + f * per + (t - f * S);
 }
 
@@ -627,12 +628,13 @@ __global__ void hist_subtract_kernel(int64_t* __restrict__ hist, const int64_t* 
                                      int64_t dense, int per, int S) {
   const int j = blockIdx.y;
   if (j >= n) return;
-  const int64_t sz = live_words(size[j], dense, per, S);
+  const int sz = (int)live_words(size[j], dense, per, S);
+  const int dn = (int)dense;
   const int64_t* p = parent + parent_off[j];
   const int64_t* s = hist + small_off[j];
   int64_t* o = hist + out_off[j];
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t w = live_word(k, dense, per, S);
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += gridDim.x * blockDim.x) {
+    const int w = live_word(k, dn, per, S);
     o[w] = p[w] - s[w];
   }
 }
@@ -644,9 +646,10 @@ __global__ void zero_segments_kernel(int64_t* __restrict__ hist, const int64_t* 
   const int j = blockIdx.y;
   if (j >= n) return;
   int64_t* o = hist + off[j];
-  const int64_t sz = live_words(size[j], dense, per, S);
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += (int64_t)gridDim.x * blockDim.x)
-    o[live_word(k, dense, per, S)] = 0;
+  const int sz = (int)live_words(size[j], dense, per, S);
+  const int dn = (int)dense;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += gridDim.x * blockDim.x)
+    o[live_word(k, dn, per, S)] = 0;
 }
 
 // ------------------------------------------------------------------------------- split finding
@@ -1402,12 +1405,18 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
   return (int)hipGetLastError();
 }
 
+// live words of the largest node: the grids of the subtract / zero kernels are sized to what they touch
+// (sized from the full B x S words they launched ~4x the workgroups the live region needs)
+static int64_t host_live_words(int64_t sz, int64_t dense, int per, int S) {
+  return (dense < 0 || sz <= dense) ? sz : dense + (sz - dense) / per * S;
+}
+
 int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
                            const int64_t* out_off, const int64_t* size, int n, int64_t max_size, int64_t dense,
                            int per, int S, hipStream_t stream) {
   if (n == 0) return 0;
-  int gx = (int)((max_size + 255) / 256);
-  if (gx > 1024) gx = 1024;
+  if (max_size >= (int64_t)1 << 31) return -2;
+  int gx = (int)min((host_live_words(max_size, dense, per, S) + 255) / 256, (int64_t)1024);
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(hist_subtract_kernel, dim3(gx, n), dim3(256), 0, stream, hist, parent, parent_off, small_off,
                      out_off, size, n, dense, per, S);
@@ -1464,7 +1473,9 @@ int tmog_hip_fp_merge(const void* recv, int R, int m, int64_t rec_bytes, int S, 
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
                            int64_t dense, int per, int S, hipStream_t stream) {
   if (n == 0) return 0;
-  int gx = (int)min((max_size + 255) / 256, (int64_t)1024);
+  if (max_size >= (int64_t)1 << 31) return -2;
+  int gx = (int)min((host_live_words(max_size, dense, per, S) + 255) / 256, (int64_t)1024);
+  if (gx < 1) gx = 1;
   hipLaunchKernelGGL(zero_segments_kernel, dim3(gx, n), dim3(256), 0, stream, hist, off, size, n, dense, per, S);
   return (int)hipGetLastError();
 }
