@@ -32,10 +32,15 @@ constexpr int DMAX = 384;      // LDS: 64*384*4 (X) + 384*33*4 (V) + 64*32*4 (R)
 
 __device__ __forceinline__ void loss_and_grad(int loss, float m, float y, float ysc, float* l, float* g) {
   if (loss == 0) {              // logistic
+    // log1p(e) for e in (0, 1] as log(u) * e / (u - 1) with u = 1 + e (exact-argument trick, a few ulp)
+    // and sigmoid through one reciprocal: ~15 VALU instead of the ~60 of log1pf + two IEEE divisions
     const float am = fabsf(m);
     const float e = __expf(-am);
-    *l = fmaxf(m, 0.f) + log1pf(e) - y * m;
-    const float sig = m >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
+    const float u = 1.f + e;
+    const float lp = (u == 1.f) ? e : __logf(u) * __fdividef(e, u - 1.f);
+    *l = fmaxf(m, 0.f) + lp - y * m;
+    const float inv = __builtin_amdgcn_rcpf(u);
+    const float sig = m >= 0.f ? inv : e * inv;
     *g = sig - y;
   } else if (loss == 1) {       // hinge
     const float ys = 2.f * y - 1.f;
@@ -66,7 +71,8 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
   float* Xs = lds;                          // [TM][d] + 64 words of overrun (finite, times V = 0)
   float* Vs = Xs + xs_words;                // [dk][VS], zero beyond d
   float* Rs = Vs + dk * VS;                 // [TM][PC]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: SGPR, scalar branches
   const int q = lane >> 4, c = lane & 15;
   const int rb = wave & 3, pb = wave >> 2;
   const int nob = 2 * ((d + 15) >> 4);
@@ -130,13 +136,21 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
     // ---- phase A: this wave's 16x16 margin block over all of d (two accumulators hide the
     // 40-cycle dependent-MFMA latency)
     // Full 64-column blocks use the bank-spread order; the ragged tail block steps 4 columns at a time.
+    // Per 64-column block the 16 k-steps read at compile-time offsets from two per-block bases (column
+    // 64 b + 16 q + s, s = 0..15): no per-step address arithmetic (it was ~7 VALU per MFMA, and the
+    // kernel was VALU-issue bound).
     f32x4 macc = {0.f, 0.f, 0.f, 0.f}, macc2 = {0.f, 0.f, 0.f, 0.f};
     const float* xa = Xs + (16 * rb + c) * d;
-#pragma unroll 4
-    for (int s = 0; s < ks_full; s += 2) {
-      const int k0 = kcol(s, q), k1 = kcol(s + 1, q);
-      macc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k0], va[k0 * VS], macc, 0, 0, 0);
-      macc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k1], va[k1 * VS], macc2, 0, 0, 0);
+    {
+      const float* xb = xa + 16 * q;
+      const float* vb = va + 16 * q * VS;
+      for (int b = 0; b < (ks_full >> 4); ++b, xb += 64, vb += 64 * VS) {
+#pragma unroll
+        for (int s = 0; s < 16; s += 2) {
+          macc = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s], vb[s * VS], macc, 0, 0, 0);
+          macc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s + 1], vb[(s + 1) * VS], macc2, 0, 0, 0);
+        }
+      }
     }
     for (int k = 4 * ks_full + q; k < 4 * ks_full + 4 * ks_tail; k += 8) {
       macc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k], va[k * VS], macc, 0, 0, 0);
@@ -146,6 +160,7 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
     macc += macc2;
 
     // ---- fused epilogue in registers: rows 16rb + 4q + j, problem p
+    float fl = 0.f, rl = 0.f;       // this lane's 4 rows in fp32, folded into the fp64 totals once per tile
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = 16 * rb + 4 * q + j;
@@ -154,25 +169,28 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
         const float w = cw[j];
         float l, g;
         loss_and_grad(loss, macc[j] + bp, cy[j], ysp, &l, &g);
-        f_acc += (double)(l * w);
+        fl += l * w;
         rv = g * w;
-        r_acc += (double)rv;
+        rl += rv;
       }
       if (GRAD) Rs[row * PC + p] = rv;
     }
+    f_acc += (double)fl;
+    r_acc += (double)rl;
     if (GRAD) {
       __syncthreads();
       // ---- phase B: G[16db.., 16pb'..] += X_tile^T R  (16 k-steps of 4 rows)
-#pragma unroll 2
+      // output blocks ob = wave + 8 i: column block (wave >> 1) + 4 i, problem half wave & 1 (8 i is even)
+      const float* xw = Xs + q * d + c + 16 * (wave >> 1);
+      const float* rw = Rs + q * PC + 16 * (wave & 1) + c;
+#pragma unroll 4
       for (int t = 0; t < TM / 4; ++t) {
-        const int row = 4 * t + q;
-        const float rv0 = Rs[row * PC + c], rv1 = Rs[row * PC + 16 + c];
-        const float* xr = Xs + row * d + c;
+        const float rv = rw[4 * t * PC];
+        const float* xr = xw + 4 * t * d;
 #pragma unroll
         for (int i = 0; i < GB; ++i) {
-          const int ob = wave + 8 * i;
-          if (ob < nob)
-            gacc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[16 * (ob >> 1)], (ob & 1) ? rv1 : rv0, gacc[i], 0, 0, 0);
+          if (wave + 8 * i < nob)
+            gacc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[64 * i], rv, gacc[i], 0, 0, 0);
         }
       }
     }
