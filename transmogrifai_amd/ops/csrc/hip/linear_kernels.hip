@@ -57,7 +57,7 @@ __device__ __forceinline__ void loss_and_grad(int loss, float m, float y, float 
 __device__ __forceinline__ int kcol(int s, int q) { return 64 * (s >> 4) + (s & 15) + 16 * q; }
 
 // GB = phase-B output blocks per wave, NPF = prefetch float4 slots per thread
-template <bool GRAD, int GB, int NPF>
+template <bool GRAD, int GB, int NPF, int DM>
 __global__ void __launch_bounds__(NT) lr_objective_kernel(
     const float* __restrict__ X, int64_t N, int d, const float* __restrict__ y,
     const float* __restrict__ W, int ldw, int wcol0, int P, const float* __restrict__ V,
@@ -87,6 +87,17 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
   for (int i = 0; i < GB; ++i) gacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int p = 16 * pb + c;                // this lane's problem column in phase A / epilogue
+  // phase-A B operands of the full 64-column blocks live in registers for the whole kernel: lane (q, c)
+  // of problem block pb only ever multiplies V[64 b + 16 q + s][16 pb + c] (s = 0..15), so per MFMA one
+  // LDS read (the X element) remains instead of two
+  constexpr int NB64 = DM / 64;
+  const int nb64 = d >> 6;
+  float vr[NB64 * 16];
+#pragma unroll
+  for (int b = 0; b < NB64; ++b)
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+      vr[16 * b + s2] = b < nb64 ? V[(int64_t)(64 * b + 16 * q + s2) * PC + p] : 0.f;
   const float bp = bias[p];
   const float ysp = yscale ? yscale[p] : 1.f;
   double f_acc = 0.0, r_acc = 0.0;
@@ -141,14 +152,14 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
     // kernel was VALU-issue bound).
     f32x4 macc = {0.f, 0.f, 0.f, 0.f}, macc2 = {0.f, 0.f, 0.f, 0.f};
     const float* xa = Xs + (16 * rb + c) * d;
-    {
-      const float* xb = xa + 16 * q;
-      const float* vb = va + 16 * q * VS;
-      for (int b = 0; b < (ks_full >> 4); ++b, xb += 64, vb += 64 * VS) {
 #pragma unroll
-        for (int s = 0; s < 16; s += 2) {
-          macc = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s], vb[s * VS], macc, 0, 0, 0);
-          macc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s + 1], vb[(s + 1) * VS], macc2, 0, 0, 0);
+    for (int b = 0; b < NB64; ++b) {
+      if (b < nb64) {
+        const float* xb = xa + 16 * q + 64 * b;
+#pragma unroll
+        for (int s2 = 0; s2 < 16; s2 += 2) {
+          macc = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s2], vr[16 * b + s2], macc, 0, 0, 0);
+          macc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s2 + 1], vr[16 * b + s2 + 1], macc2, 0, 0, 0);
         }
       }
     }
@@ -360,7 +371,7 @@ int tmog_hip_lr_objective(const float* X, int64_t N, int d, const float* y, cons
   const int dk = ((d + 63) / 64) * 64;
   const size_t lds = (size_t)(((TM * d + 64 + 3) & ~3) + dk * VS + TM * PC) * sizeof(float);
 #define TM_LR(G, GB, DM)                                                                                  \
-  hipLaunchKernelGGL((lr_objective_kernel<G, GB, (TM * DM / 4 + NT - 1) / NT>), dim3(nblk), dim3(NT), lds, \
+  hipLaunchKernelGGL((lr_objective_kernel<G, GB, (TM * DM / 4 + NT - 1) / NT, DM>), dim3(nblk), dim3(NT), lds, \
                      stream, X, N, d, y, W, ldw, wcol0, P, V, bias, loss, yscale, f_part, r_part, G_part, dpad)
 #define TM_LR_D(G)                                   \
   if (d <= 128) TM_LR(G, 2, 128);                    \
