@@ -1,0 +1,61 @@
+"""Forest sharing across the maxDepth x minInfoGain grid: a pruned deep forest equals the forest grown
+directly with the shallower depth / larger gain threshold (``tree_engine.prune_forest``), and the
+selector-level learner gives every grid point the forest it would have grown on its own."""
+import numpy as np
+import torch
+
+from transmogrifai_amd.models import tree_engine as te
+
+
+def _data(N=4000, F=12, B=32, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randint(0, B, (N, F), dtype=torch.uint8, generator=g)
+    y = ((X[:, 0].float() + 0.7 * X[:, 3].float() - 0.4 * X[:, 7].float() + 4 * torch.randn(N, generator=g))
+         > 14).float()
+    return X, y
+
+
+def _grow(X, y, depth, gain, n_trees=4):
+    rows = torch.arange(X.shape[0])
+    jobs = []
+    for t in range(n_trees):
+        # bootstrap-like integer weights, identical for every variant
+        w = torch.as_tensor(np.random.default_rng(100 + t).poisson(1.0, X.shape[0]), dtype=torch.int64)
+        jobs.append(te.TreeJob(0, te.TreeParams(max_depth=depth, min_instances=5, min_info_gain=gain), rows, w))
+    return te.grow_forest(X, np.full(X.shape[1], 32), jobs, mode=te.MODE_CLS, kind=te.KIND_GINI, y=y, B=32)
+
+
+def _same(a: te.Forest, b: te.Forest):
+    np.testing.assert_array_equal(a.tree_off, b.tree_off)
+    np.testing.assert_array_equal(a.nodes, b.nodes)
+    np.testing.assert_array_equal(a.default_left, b.default_left)
+    np.testing.assert_array_equal(a.value, b.value)
+    np.testing.assert_array_equal(a.gain, b.gain)
+    np.testing.assert_array_equal(a.cover, b.cover)
+
+
+def test_pruned_forest_equals_direct_growth():
+    X, y = _data()
+    deep = _grow(X, y, 8, 0.0005)
+    for depth, gain in [(8, 0.0005), (5, 0.0005), (3, 0.0005), (8, 0.002), (5, 0.01), (2, 0.05)]:
+        _same(te.prune_forest(deep, depth, gain), _grow(X, y, depth, gain))
+
+
+def test_selector_share_groups_match_unshared(monkeypatch):
+    """RF learner with the share on / off: every grid point's forest is identical when the per-node feature
+    subsets are off (all features), i.e. when the grid composition does not move the random stream."""
+    from transmogrifai_amd.models.base import FitJob
+    from transmogrifai_amd.models.trees import RandomForestClassifierLearner
+    X, y = _data(N=3000, F=8)
+    Xf = X.float()
+    rows = torch.arange(2400)
+    jobs = [FitJob(params={"max_depth": d, "min_info_gain": g, "min_instances_per_node": m, "num_trees": 3,
+                           "feature_subset_strategy": "all", "seed": 1}, rows=rows)
+            for d in (2, 4, 6) for g in (0.001, 0.01) for m in (5, 50)]
+    lr = RandomForestClassifierLearner()
+    monkeypatch.setenv("TMOG_RF_SHARE", "0")
+    ref = lr.fit_batch(Xf, y, jobs)
+    monkeypatch.setenv("TMOG_RF_SHARE", "1")
+    got = lr.fit_batch(Xf, y, jobs)
+    for a, b in zip(ref, got):
+        _same(te.Forest.from_state(a["forest"]), te.Forest.from_state(b["forest"]))

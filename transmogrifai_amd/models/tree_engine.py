@@ -141,6 +141,51 @@ class Forest:
         return imp / s if s > 0 else imp
 
 
+def prune_forest(f: Forest, max_depth: int, min_gain: float) -> Forest:
+    """The forest a grower run with a smaller ``max_depth`` and / or a larger ``min_info_gain`` would
+    have produced from the same nodes: a node stays split only while its depth is below ``max_depth``
+    and its recorded split gain is at least ``min_gain`` (the grower accepts a split exactly when its
+    best valid candidate's gain >= min_info_gain, and a larger threshold never changes which candidate
+    is best, only whether it is accepted); every other node becomes a leaf with its own statistics,
+    which the grower records for internal nodes too. Node order stays BFS per tree, as ``_finalize``
+    emits it. Lets the model selector grow one forest per (bootstrap, seed, minInstancesPerNode, ...)
+    for all of its maxDepth x minInfoGain grid points (``models/trees.py`` ``_ForestLearner``).
+    Thresholds are compared on the stored fp32 gain (a split whose fp64 gain lies within one fp32
+    ulp of the threshold may be kept)."""
+    n = len(f.nodes)
+    if n == 0:
+        return f
+    left = f.nodes[:, 2].astype(np.int64)
+    right = f.nodes[:, 3].astype(np.int64)
+    keep = np.zeros(n, bool)
+    split = np.zeros(n, bool)
+    frontier = f.tree_off[:-1].astype(np.int64)
+    frontier = frontier[frontier < f.tree_off[1:]]
+    keep[frontier] = True
+    mg = np.float32(min_gain)
+    d = 0
+    while frontier.size:
+        ok = (left[frontier] >= 0) & (d < max_depth) & (f.gain[frontier] >= mg)
+        sp = frontier[ok]
+        split[sp] = True
+        frontier = np.sort(np.concatenate([left[sp], right[sp]]))
+        keep[frontier] = True
+        d += 1
+    order = np.nonzero(keep)[0]
+    new_id = np.full(n, -1, np.int64)
+    new_id[order] = np.arange(order.size)
+    tree_off = np.searchsorted(order, f.tree_off).astype(np.int64)
+    isint = split[order]
+    nodes = np.zeros((order.size, 4), np.int32)
+    nodes[:, 0] = np.where(isint, f.nodes[order, 0], 0)
+    nodes[:, 1] = np.where(isint, f.nodes[order, 1], 0)
+    nodes[:, 2] = np.where(isint, new_id[np.maximum(left[order], 0)], -1)
+    nodes[:, 3] = np.where(isint, new_id[np.maximum(right[order], 0)], -1)
+    return Forest(tree_off, nodes, np.where(isint, f.default_left[order], 0).astype(np.uint8),
+                  f.value[order].copy(), np.where(isint, f.gain[order], 0).astype(np.float32),
+                  f.cover[order].copy(), f.tree_model.copy(), f.missing_bin)
+
+
 def pack_rows(rows: torch.Tensor, weights: Optional[torch.Tensor]) -> torch.Tensor:
     """Pack ``row | weight << 24`` into an int32 tensor (bit pattern read as uint32 by the kernels)."""
     r = rows.to(torch.int64)

@@ -200,8 +200,16 @@ class _ForestLearner(Learner):
             boot: Dict[tuple, tuple] = {}
             row_keys: Dict[tuple, int] = {}
             root_parts, root_counts = [], []
-            for i in idxs:
-                p = jobs[i].params
+            # Grid points that differ only in maxDepth / minInfoGain share their trees: one forest is grown
+            # at the deepest depth and smallest gain threshold of its share group and the others are
+            # pruned out of it (TE.prune_forest) -- for the default RF grid 2 grown forests per fold instead
+            # of 18, ~5x fewer tree levels. (Same bootstrap and seed as each grid point had before; the
+            # per-node feature-subset draws come from the group's stream, as for any grid composition.)
+            grow, members = _forest_share_groups(jobs, idxs, forests_only)
+            for i in grow:
+                p = dict(jobs[i].params)
+                md, mg = members[i][1], members[i][2]
+                p["max_depth"], p["min_info_gain"] = md, mg
                 nt = int(p.get("num_trees", self.default_trees)) if self.is_forest else 1
                 rows = jrows[i]
                 sub = _subset_size(p.get("feature_subset_strategy", "auto"), F, self.classification, nt)
@@ -252,11 +260,16 @@ class _ForestLearner(Learner):
                                         t1=yg.to(torch.float32)[None, :], B=mb,
                                         rng_seed=int(jobs[idxs[0]].params.get("seed", 0)), root=root, fp=fp)
             owner = np.asarray(owner)
-            for i in idxs:
-                ts = np.nonzero(owner == i)[0]
+            for g in grow:
+                ts = np.nonzero(owner == g)[0]
                 sub = Forest_subset(forest, ts)
-                out[i] = {"forest": sub.to_state(), "bins": spec.to_state(), "n_classes": K,
-                          "num_trees": len(ts), "max_bins": mb, "n_features": F}
+                md, mg = members[g][1], members[g][2]
+                for i in members[g][0]:
+                    pi = jobs[i].params
+                    di, gi = int(pi.get("max_depth", 5)), float(pi.get("min_info_gain", 0.0))
+                    fi = sub if (di, gi) == (md, mg) else TE.prune_forest(sub, di, gi)
+                    out[i] = {"forest": fi.to_state(), "bins": spec.to_state(), "n_classes": K,
+                              "num_trees": len(ts), "max_bins": mb, "n_features": F}
         return out
 
     # -- prediction
@@ -317,6 +330,30 @@ class _ForestLearner(Learner):
     def feature_contributions(self, state, d):
         forest, _ = self._forest(state)
         return forest.feature_importance(d)
+
+
+def _forest_share_groups(jobs, idxs, forests_only):
+    """``(grow, members)``: the job indices to grow, and per grown index ``(member job indices, max_depth,
+    min_info_gain)`` it is grown with. Jobs share when everything but maxDepth / minInfoGain matches
+    (training rows, seed, trees, sampling, minInstancesPerNode, impurity, subset strategy); off with
+    ``TMOG_RF_SHARE=0`` and for single trees (their weights / sampling are per job)."""
+    if not forests_only or os.environ.get("TMOG_RF_SHARE", "1") == "0":
+        return list(idxs), {i: ([i], int(jobs[i].params.get("max_depth", 5)),
+                                float(jobs[i].params.get("min_info_gain", 0.0))) for i in idxs}
+    by_key: Dict[tuple, List[int]] = {}
+    for i in idxs:
+        p = jobs[i].params
+        src = jobs[i].rows
+        rk = ("all",) if src is None else (src.data_ptr(), int(src.numel()), str(src.device))
+        rest = tuple(sorted((k, repr(v)) for k, v in p.items() if k not in ("max_depth", "min_info_gain")))
+        by_key.setdefault((rk, rest), []).append(i)
+    grow, members = [], {}
+    for ms in by_key.values():
+        g = ms[0]
+        grow.append(g)
+        members[g] = (ms, max(int(jobs[i].params.get("max_depth", 5)) for i in ms),
+                      min(float(jobs[i].params.get("min_info_gain", 0.0)) for i in ms))
+    return grow, members
 
 
 def Forest_subset(forest: TE.Forest, trees: np.ndarray) -> TE.Forest:
