@@ -59,3 +59,27 @@ def test_selector_share_groups_match_unshared(monkeypatch):
     got = lr.fit_batch(Xf, y, jobs)
     for a, b in zip(ref, got):
         _same(te.Forest.from_state(a["forest"]), te.Forest.from_state(b["forest"]))
+
+
+def test_hessian_gate_keeps_newton_trees_identical(monkeypatch):
+    """Newton trees skip nodes whose hessian sum is below 2 x min_child_weight (no valid split exists):
+    the tree structure, split gains and default directions equal the ungated growth bit for bit, with and
+    without the subtraction trick. A skipped leaf takes its (g, h) totals from its parent's split
+    statistics (fp32), as every max-depth leaf already does, instead of its own histogram: leaf values
+    agree to fp32 rounding."""
+    X, y = _data(N=6000, F=10)
+    p = torch.sigmoid(torch.randn(X.shape[0], generator=torch.Generator().manual_seed(3)))
+    g, h = (p - y).float(), (p * (1 - p)).float()
+    rows = torch.arange(X.shape[0])
+    for mcw in (1.0, 25.0, 120.0):
+        jobs = [te.TreeJob(0, te.TreeParams(max_depth=7, min_child_weight=mcw, reg_lambda=1.0, eta=0.3), rows)]
+        kw = dict(mode=te.MODE_GH, kind=te.KIND_NEWTON, t1=g[None, :], t2=h[None, :], B=32)
+        for sub in (True, False):
+            monkeypatch.setenv("TMOG_TREE_HESS_GATE", "0")
+            ref = te.grow_forest(X, np.full(X.shape[1], 32), jobs, subtract=sub, **kw)
+            monkeypatch.setenv("TMOG_TREE_HESS_GATE", "1")
+            got = te.grow_forest(X, np.full(X.shape[1], 32), jobs, subtract=sub, **kw)
+            for k in ("tree_off", "nodes", "default_left", "gain"):
+                np.testing.assert_array_equal(getattr(ref, k), getattr(got, k), err_msg=k)
+            np.testing.assert_allclose(got.value, ref.value, rtol=1e-5, atol=1e-7)
+            np.testing.assert_allclose(got.cover, ref.cover, rtol=1e-5, atol=1e-6)

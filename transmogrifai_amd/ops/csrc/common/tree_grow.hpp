@@ -375,6 +375,9 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
   if (n_sc > 256) throw std::runtime_error("too many statistic chunks (classes x bins too large)");
   const int fp_mlo = fp ? a.fp_mlo : 0;
   const size_t fp_rb = fp_rec_bytes(S);
+  const char* hg_env = std::getenv("TMOG_TREE_HESS_GATE");     // "0": off (A/B and the equality test)
+  const bool newton = a.mode == 2 && a.kind == 3 && S >= 2 &&   // (g, h) statistics, second-order gain
+                      !(hg_env && hg_env[0] == '0');
   for (int depth = 0; depth <= max_depth; ++depth) {
     const int64_t n = (int64_t)lv_gid.size();
     if (n == 0) break;
@@ -384,9 +387,23 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
       const int t = (int)lv_tree[i];
       can[i] = depth < a.job_depth[j0 + t] && lv_count[i] >= 2 &&
                (double)lv_count[i] >= 2 * a.job_min_inst[j0 + t] - 1e-9;
+      // Newton trees: both children of a split need a hessian sum >= min_child_weight, so a node whose
+      // hessian (from its parent's split statistics, fp32) is clearly below 2 mcw has no valid split --
+      // skip its histogram / scan (the 1e-6 margin keeps every node that could split)
+      if (can[i] && newton && depth > 0 && a.job_mcw[j0 + t] > 0 &&
+          R.tot[(size_t)lv_gid[i] * S + 1] < 2.0 * a.job_mcw[j0 + t] * (1.0 - 1e-6))
+        can[i] = 0;
       need[i] = can[i] || depth == 0;
-      if (need[i]) hist_nodes.push_back(i);
     }
+    // a splittable node whose sibling cannot split still gets its histogram by subtraction from the
+    // parent's: build the sibling's (scan skipped, params slot 7 = 0) rather than the node's own
+    if (a.subtract && !use_subset && prev_hist && depth > 0)
+      for (int64_t q = 0; 2 * q + 1 < n; ++q)
+        if (need[2 * q] != need[2 * q + 1] && lv_count[2 * q] >= 1 && lv_count[2 * q + 1] >= 1 &&
+            (can[2 * q] ? lv_count[2 * q + 1] <= lv_count[2 * q] : lv_count[2 * q] <= lv_count[2 * q + 1]))
+          need[2 * q] = need[2 * q + 1] = 1;
+    for (int64_t i = 0; i < n; ++i)
+      if (need[i]) hist_nodes.push_back(i);
     if (hist_nodes.empty()) {
       std::vector<int64_t> all(n);
       for (int64_t i = 0; i < n; ++i) all[i] = i;

@@ -723,7 +723,9 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
   const bool one_blk = fb >= fb_multi;
   __shared__ Best s_best[4];
   Best best{-INFINITY, 0x7fffffff, 0, 0};
-  if (one_blk ? (n_multi + (fb - fb_multi) * 256 < nf) : (fb * FPB < f_lim)) {
+  // params slot 7 = "may split" (tree_grow.hpp): nodes built only as a subtraction partner are not scanned
+  if (node_params[(int64_t)j * 8 + 7] > 0.5f &&
+      (one_blk ? (n_multi + (fb - fb_multi) * 256 < nf) : (fb * FPB < f_lim))) {
     const int64_t* h = hist + node_hist_off[j];
     const int32_t* fl = feat_list + node_feat_off[j];
     const float* P = node_params + (int64_t)j * 8;
@@ -857,7 +859,7 @@ __global__ void __launch_bounds__(256) split_scan_wide_kernel(
   const int f = blockIdx.x - j * fbmax;
   const int nf = node_nfeat[j];
   Best best{-INFINITY, 0x7fffffff, 0, 0};
-  const bool live = f < nf;
+  const bool live = f < nf && node_params[(int64_t)j * 8 + 7] > 0.5f;   // slot 7: node may split
   const int64_t* h = hist + node_hist_off[j];
   const int32_t* fl = feat_list + node_feat_off[j];
   const float* P = node_params + (int64_t)j * 8;
