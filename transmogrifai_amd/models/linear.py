@@ -15,6 +15,7 @@ vectorized over the ``P`` problems and run in lockstep; converged problems are f
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -175,6 +176,33 @@ class MultinomialObjective:
         return f, g.reshape(U.shape)
 
 
+def _owlqn_direction_torch(U, g, l1, has_l1, S, Y, RHO, hist_n, m):
+    """Pseudo-gradient, two-loop recursion, orthant projection (the spec of the HIP owlqn_direction_kernel)."""
+    pg = torch.where(U > 0, g + l1, torch.where(U < 0, g - l1,
+                     torch.where(g + l1 < 0, g + l1, torch.where(g - l1 > 0, g - l1, torch.zeros_like(g)))))
+    q = pg.clone()
+    k = min(hist_n, m)
+    alphas = []
+    for j in range(k):
+        idx = (hist_n - 1 - j) % m
+        a = RHO[idx] * (S[idx] * q).sum(0)
+        q = q - a[None, :] * Y[idx]
+        alphas.append((idx, a))
+    if k > 0:
+        last = (hist_n - 1) % m
+        yy = (Y[last] * Y[last]).sum(0)
+        gamma = torch.where(yy > 0, (S[last] * Y[last]).sum(0) / yy.clamp_min(1e-300), torch.ones_like(yy))
+        q = q * gamma[None, :]
+    for idx, a in reversed(alphas):
+        b = RHO[idx] * (Y[idx] * q).sum(0)
+        q = q + S[idx] * (a - b)[None, :]
+    D = -q
+    D = torch.where(has_l1 & (torch.sign(D) != torch.sign(-pg)), torch.zeros_like(D), D)
+    xi = torch.where(U != 0, torch.sign(U), torch.sign(-pg))
+    dnorm = torch.sqrt((pg * pg).sum(0)).clamp_min(1e-300)
+    return D, pg, xi, dnorm
+
+
 def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max_iter: torch.Tensor,
                   tol: torch.Tensor, m: int = 10, max_ls: int = 30):
     """Batched OWL-QN (L-BFGS when ``l1 == 0``) over the columns of ``U``.
@@ -193,34 +221,19 @@ def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max
     done = torch.zeros(P, dtype=torch.bool, device=dev)
     iters = torch.zeros(P, dtype=torch.int64, device=dev)
     has_l1 = l1 > 0
+    fused_dir = LK.owlqn_direction_supported(U, m) and os.environ.get("TMOG_OWLQN_FUSED", "1") != "0"
+    if fused_dir:
+        l1 = l1.to(U.dtype).contiguous()
     for it in range(int(max_iter.max().item()) if P else 0):
         done |= iters >= max_iter
         if bool(done.all()):
             break
-        # pseudo-gradient
-        pg = torch.where(U > 0, g + l1, torch.where(U < 0, g - l1,
-                         torch.where(g + l1 < 0, g + l1, torch.where(g - l1 > 0, g - l1, torch.zeros_like(g)))))
-        # two-loop recursion
-        q = pg.clone()
         k = min(hist_n, m)
-        alphas = []
-        for j in range(k):
-            idx = (hist_n - 1 - j) % m
-            a = RHO[idx] * (S[idx] * q).sum(0)
-            q = q - a[None, :] * Y[idx]
-            alphas.append((idx, a))
-        if k > 0:
-            last = (hist_n - 1) % m
-            yy = (Y[last] * Y[last]).sum(0)
-            gamma = torch.where(yy > 0, (S[last] * Y[last]).sum(0) / yy.clamp_min(1e-300), torch.ones_like(yy))
-            q = q * gamma[None, :]
-        for idx, a in reversed(alphas):
-            b = RHO[idx] * (Y[idx] * q).sum(0)
-            q = q + S[idx] * (a - b)[None, :]
-        D = -q
-        D = torch.where(has_l1 & (torch.sign(D) != torch.sign(-pg)), torch.zeros_like(D), D)
-        xi = torch.where(U != 0, torch.sign(U), torch.sign(-pg))
-        dnorm = torch.sqrt((pg * pg).sum(0)).clamp_min(1e-300)
+        if fused_dir:
+            # one HIP launch for everything up to the line search (ops/linear.py owlqn_direction)
+            D, pg, xi, dnorm = LK.owlqn_direction(U, g, l1, S, Y, RHO, hist_n, m)
+        else:
+            D, pg, xi, dnorm = _owlqn_direction_torch(U, g, l1, has_l1, S, Y, RHO, hist_n, m)
         alpha = torch.where(torch.full_like(dnorm, float(k == 0), dtype=torch.bool), 1.0 / dnorm,
                             torch.ones_like(dnorm))
         accepted = done.clone()

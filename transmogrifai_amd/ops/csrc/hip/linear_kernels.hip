@@ -334,6 +334,119 @@ __global__ void __launch_bounds__(NT) lr_epilogue_grad_kernel(
   }
 }
 
+// OWL-QN search direction for P problems in one launch (models/linear.py owlqn_batched): pseudo-gradient,
+// L-BFGS two-loop recursion over the m-slot history ring, initial Hessian scaling, orthant projection,
+// the orthant signs xi and |pg|. One 256-thread workgroup per problem column; the column's d1 entries
+// stay in registers (QMAX per thread) and every inner product is an fp64 block reduction. Replaces ~150
+// small torch launches per iteration (the optimiser was launch-bound: ~0.2 s of the LR learner's 0.3 s).
+constexpr int OW_NT = 256;
+constexpr int OW_QMAX = 16;      // d1 <= 4096
+constexpr int OW_MMAX = 32;      // history slots
+
+__device__ __forceinline__ double ow_block_sum(double v, double* sh) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  __syncthreads();                       // previous readers of sh are done
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+__device__ __forceinline__ double ow_sign(double x) { return (double)((x > 0.0) - (x < 0.0)); }
+
+__global__ void __launch_bounds__(OW_NT) owlqn_direction_kernel(
+    const double* __restrict__ U, const double* __restrict__ g, const double* __restrict__ l1,
+    const double* __restrict__ S, const double* __restrict__ Y, const double* __restrict__ RHO, int d1, int P,
+    int m, int hist_n, double* __restrict__ D_out, double* __restrict__ pg_out, double* __restrict__ xi_out,
+    double* __restrict__ dnorm_out) {
+  __shared__ double sh[4];
+  const int p = blockIdx.x, t = threadIdx.x;
+  double q[OW_QMAX], pgv[OW_QMAX];
+#pragma unroll
+  for (int r = 0; r < OW_QMAX; ++r) {
+    const int i = t + OW_NT * r;
+    double pv = 0.0;
+    if (i < d1) {
+      const int64_t e = (int64_t)i * P + p;
+      const double u = U[e], gg = g[e], l = l1[e];
+      pv = u > 0.0 ? gg + l : (u < 0.0 ? gg - l : (gg + l < 0.0 ? gg + l : (gg - l > 0.0 ? gg - l : 0.0)));
+    }
+    pgv[r] = pv;
+    q[r] = pv;
+  }
+  const int k = min(hist_n, m);
+  double a[OW_MMAX];
+  for (int j = 0; j < k; ++j) {
+    const int idx = ((hist_n - 1 - j) % m + m) % m;
+    const double* Sj = S + (int64_t)idx * d1 * P;
+    double acc = 0.0;
+#pragma unroll
+    for (int r = 0; r < OW_QMAX; ++r) {
+      const int i = t + OW_NT * r;
+      if (i < d1) acc += Sj[(int64_t)i * P + p] * q[r];
+    }
+    a[j] = RHO[(int64_t)idx * P + p] * ow_block_sum(acc, sh);
+    const double* Yj = Y + (int64_t)idx * d1 * P;
+#pragma unroll
+    for (int r = 0; r < OW_QMAX; ++r) {
+      const int i = t + OW_NT * r;
+      if (i < d1) q[r] -= a[j] * Yj[(int64_t)i * P + p];
+    }
+  }
+  if (k > 0) {
+    const int last = ((hist_n - 1) % m + m) % m;
+    const double* Sl = S + (int64_t)last * d1 * P;
+    const double* Yl = Y + (int64_t)last * d1 * P;
+    double yy = 0.0, sy = 0.0;
+#pragma unroll
+    for (int r = 0; r < OW_QMAX; ++r) {
+      const int i = t + OW_NT * r;
+      if (i < d1) {
+        const double yv = Yl[(int64_t)i * P + p];
+        yy += yv * yv;
+        sy += Sl[(int64_t)i * P + p] * yv;
+      }
+    }
+    yy = ow_block_sum(yy, sh);
+    sy = ow_block_sum(sy, sh);
+    const double gam = yy > 0.0 ? sy / fmax(yy, 1e-300) : 1.0;
+#pragma unroll
+    for (int r = 0; r < OW_QMAX; ++r) q[r] *= gam;
+  }
+  for (int j = k - 1; j >= 0; --j) {
+    const int idx = ((hist_n - 1 - j) % m + m) % m;
+    const double* Sj = S + (int64_t)idx * d1 * P;
+    const double* Yj = Y + (int64_t)idx * d1 * P;
+    double acc = 0.0;
+#pragma unroll
+    for (int r = 0; r < OW_QMAX; ++r) {
+      const int i = t + OW_NT * r;
+      if (i < d1) acc += Yj[(int64_t)i * P + p] * q[r];
+    }
+    const double b = RHO[(int64_t)idx * P + p] * ow_block_sum(acc, sh);
+#pragma unroll
+    for (int r = 0; r < OW_QMAX; ++r) {
+      const int i = t + OW_NT * r;
+      if (i < d1) q[r] += Sj[(int64_t)i * P + p] * (a[j] - b);
+    }
+  }
+  double pn = 0.0;
+#pragma unroll
+  for (int r = 0; r < OW_QMAX; ++r) {
+    const int i = t + OW_NT * r;
+    if (i < d1) {
+      const int64_t e = (int64_t)i * P + p;
+      const double u = U[e], l = l1[e], pv = pgv[r];
+      double dv = -q[r];
+      if (l > 0.0 && ow_sign(dv) != ow_sign(-pv)) dv = 0.0;
+      D_out[e] = dv;
+      pg_out[e] = pv;
+      xi_out[e] = u != 0.0 ? ow_sign(u) : ow_sign(-pv);
+      pn += pv * pv;
+    }
+  }
+  pn = ow_block_sum(pn, sh);
+  if (t == 0) dnorm_out[p] = fmax(sqrt(pn), 1e-300);
+}
+
 }  // namespace
 
 extern "C" {
@@ -380,6 +493,17 @@ int tmog_hip_lr_objective(const float* X, int64_t N, int d, const float* y, cons
   if (grad) { TM_LR_D(true) } else { TM_LR_D(false) }
 #undef TM_LR_D
 #undef TM_LR
+  return (int)hipGetLastError();
+}
+
+// OWL-QN direction (see owlqn_direction_kernel); all arrays fp64, [d1][P] / [m][d1][P] / [m][P] row-major.
+int tmog_hip_owlqn_direction(const double* U, const double* g, const double* l1, const double* S, const double* Y,
+                             const double* RHO, int d1, int P, int m, int hist_n, double* D, double* pg, double* xi,
+                             double* dnorm, hipStream_t stream) {
+  if (P < 1 || d1 < 1) return 0;
+  if (d1 > OW_NT * OW_QMAX || m < 1 || m > OW_MMAX || hist_n < 0) return -2;
+  hipLaunchKernelGGL(owlqn_direction_kernel, dim3(P), dim3(OW_NT), 0, stream, U, g, l1, S, Y, RHO, d1, P, m, hist_n,
+                     D, pg, xi, dnorm);
   return (int)hipGetLastError();
 }
 

@@ -116,3 +116,26 @@ def _torch_objective(X, y, W, V, bias, loss, yscale, grad):
     R = g * Wm
     G = (X.t() @ R).to(torch.float64) if grad else None
     return (l * Wm).sum(0).to(torch.float64), R.sum(0).to(torch.float64), G
+
+
+_OW_DMAX, _OW_MMAX = 256 * 16, 32
+
+
+def owlqn_direction_supported(U: torch.Tensor, m: int) -> bool:
+    return U.is_cuda and U.dtype == torch.float64 and U.dim() == 2 and U.shape[0] <= _OW_DMAX and m <= _OW_MMAX
+
+
+def owlqn_direction(U, g, l1, S, Y, RHO, hist_n: int, m: int):
+    """OWL-QN pseudo-gradient + two-loop L-BFGS direction + orthant projection for every column of ``U`` in
+    one HIP launch (``linear_kernels.hip`` owlqn_direction_kernel); same arithmetic as the torch loop of
+    ``models/linear.py`` owlqn_batched. Returns ``(D, pg, xi, dnorm)``."""
+    from . import _native as N_
+    U, g, l1 = U.contiguous(), g.contiguous(), l1.contiguous()
+    d1, P = U.shape
+    D, pg, xi = torch.empty_like(U), torch.empty_like(U), torch.empty_like(U)
+    dnorm = torch.empty(P, dtype=torch.float64, device=U.device)
+    N_.check(N_.hip().tmog_hip_owlqn_direction(
+        N_.ptr(U), N_.ptr(g), N_.ptr(l1), N_.ptr(S), N_.ptr(Y), N_.ptr(RHO), int(d1), int(P), int(m), int(hist_n),
+        N_.ptr(D), N_.ptr(pg), N_.ptr(xi), N_.ptr(dnorm), N_.stream(U.device)), "owlqn_direction")
+    return D, pg, xi, dnorm
+
