@@ -2,6 +2,7 @@
 directly with the shallower depth / larger gain threshold (``tree_engine.prune_forest``), and the
 selector-level learner gives every grid point the forest it would have grown on its own."""
 import numpy as np
+import pytest
 import torch
 
 from transmogrifai_amd.models import tree_engine as te
@@ -83,3 +84,23 @@ def test_hessian_gate_keeps_newton_trees_identical(monkeypatch):
                 np.testing.assert_array_equal(getattr(ref, k), getattr(got, k), err_msg=k)
             np.testing.assert_allclose(got.value, ref.value, rtol=1e-5, atol=1e-7)
             np.testing.assert_allclose(got.cover, ref.cover, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_forest_predict_multi_kernel_matches_pruned_forests():
+    """One walk per (row, tree) for all pruned variants (HIP forest_predict_multi_kernel) equals predicting
+    each pruned forest on its own, for two models with their own rows and variant lists."""
+    X, y = _data(N=5000, F=12)
+    deep = _grow(X, y, 9, 0.0002, n_trees=7)
+    Xc = X.cuda()
+    rows_a = torch.arange(0, 5000, 3, device="cuda")
+    rows_b = torch.arange(1, 4000, 2, device="cuda")
+    va = [(9, 0.0002), (2, 0.0002), (5, 0.004), (7, 0.02), (0, 0.0), (9, 0.5)]
+    vb = [(3, 0.001), (6, 0.001)]
+    trees_a, trees_b = [0, 1, 2, 3], [4, 5, 6]
+    got = te.forest_predict_multi(deep, Xc, [rows_a, rows_b], [trees_a, trees_b], [va, vb])
+    for rows, ts, vs, outs in ((rows_a, trees_a, va, got[0]), (rows_b, trees_b, vb, got[1])):
+        sub = te.Forest.concat([deep.tree(t) for t in ts])
+        for (d, g), o in zip(vs, outs):
+            want = te.forest_predict(te.prune_forest(sub, d, g), Xc, [rows], [list(range(sub.n_trees))])[0]
+            torch.testing.assert_close(o, want, rtol=1e-5, atol=1e-6)

@@ -19,7 +19,7 @@ import ctypes as C
 import math
 import os
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -721,6 +721,78 @@ def _finalize_py(jobs, G: "_Nodes", mode, kind, K, S, missing_bin, with_gid_valu
     if with_gid_values:
         f._gid_value, f._gid_tree = gid_value, tree.astype(np.int64)
     return f
+
+
+_PM_VK = 32      # tree_kernels.hip forest_predict_multi_kernel: variants x classes per model
+
+
+def forest_predict_multi(forest: Forest, Xb: torch.Tensor, model_rows: Sequence[Optional[torch.Tensor]],
+                         model_trees: Sequence[Sequence[int]],
+                         model_variants: Sequence[Sequence[Tuple[int, float]]]) -> List[List[torch.Tensor]]:
+    """Predictions of pruned variants of shared trees: model m's trees are grown trees and each of its
+    variants ``(max_depth, min_info_gain)`` is the forest ``prune_forest(trees, max_depth, min_info_gain)``
+    would give. On the GPU every (row, tree) is walked once for all of a model's variants
+    (``forest_predict_multi_kernel``); elsewhere (or for class counts the kernel does not take) each
+    variant is pruned and predicted on its own. Returns ``[model][variant] -> float32 [n_m, K]``."""
+    dev = Xb.device
+    K = forest.K
+    if dev.type != "cuda" or K not in (1, 2, 4, 8) or any(len(v) * K > _PM_VK or len(v) > 32
+                                                         for v in model_variants):
+        res = []
+        for rows, ts, vs in zip(model_rows, model_trees, model_variants):
+            sub = Forest.concat([forest.tree(int(t)) for t in ts])
+            res.append([forest_predict(prune_forest(sub, d, g), Xb, [rows], [list(range(sub.n_trees))])[0]
+                        for d, g in vs])
+        return res
+    Xb = Xb.contiguous()
+    Nrows, F = int(Xb.shape[0]), int(Xb.shape[1])
+    order = [t for ts in model_trees for t in ts]
+    mto = np.zeros(len(model_trees) + 1, np.int64)
+    mto[1:] = np.cumsum([len(ts) for ts in model_trees])
+    counts = [Nrows if r is None else int(r.numel()) for r in model_rows]
+    mro = np.zeros(len(model_rows) + 1, np.int64)
+    mro[1:] = np.cumsum(counts)
+    voff = np.zeros(len(model_variants) + 1, np.int32)
+    voff[1:] = np.cumsum([len(v) for v in model_variants])
+    vdep = np.asarray([d for vs in model_variants for d, _ in vs], np.int32)
+    vout = np.zeros(max(1, int(voff[-1])), np.int64)
+    pos = 0
+    for m, vs in enumerate(model_variants):
+        for k in range(len(vs)):
+            vout[int(voff[m]) + k] = pos
+            pos += counts[m] * K
+    # per-node variant stop bits of the depth-independent part of prune_forest's rule: a grown leaf stops
+    # every variant, an internal node those whose min gain exceeds its split gain (fp32 compare)
+    mask = np.zeros(len(forest.nodes), np.uint32)
+    leaf = forest.nodes[:, 2] < 0
+    for m, vs in enumerate(model_variants):
+        sel = np.zeros(len(forest.nodes), bool)
+        for t in model_trees[m]:
+            sel[int(forest.tree_off[t]):int(forest.tree_off[t + 1])] = True
+        bits = np.zeros(len(forest.nodes), np.uint32)
+        for k, (_, g) in enumerate(vs):
+            bits |= ((forest.gain < np.float32(g)) | leaf).astype(np.uint32) << np.uint32(k)
+        mask[sel] = bits[sel]
+    pk = _Pack(dev)
+    ids = [pk.add(forest.tree_off[:-1][order].astype(np.int64)), pk.add(np.ones(len(order), np.float32)),
+           pk.add(np.ascontiguousarray(forest.nodes)), pk.add(forest.default_left),
+           pk.add(np.ascontiguousarray(forest.value, np.float32)), pk.add(mask.view(np.int32))]
+    i_v = [pk.add(voff), pk.add(vdep), pk.add(vout), pk.add(mro), pk.add(mto)]
+    row_list = torch.cat([(torch.arange(Nrows, device=dev) if r is None else r.to(dev)).to(torch.int32)
+                          for r in model_rows])
+    dv = pk.ship()
+    t_off, t_w, nodes, dl, lv, gn = (dv[i] for i in ids)
+    voff_t, vdep_t, vout_t, mro_t, mto_t = (dv[i] for i in i_v)
+    out = torch.empty(max(pos, 1), dtype=torch.float32, device=dev)
+    N.check(N.hip().tmog_hip_forest_predict_multi(
+        N.ptr(Xb), F, len(model_rows), N.ptr(mro_t), N.ptr(row_list), max(counts) if counts else 0, N.ptr(mto_t),
+        N.ptr(t_off), N.ptr(t_w), N.ptr(nodes), N.ptr(dl), forest.missing_bin, N.ptr(lv), K, N.ptr(gn), N.ptr(voff_t),
+        N.ptr(vdep_t), N.ptr(vout_t), N.ptr(out), N.stream(dev)), "forest_predict_multi")
+    res = []
+    for m, vs in enumerate(model_variants):
+        res.append([out[int(vout[int(voff[m]) + k]):int(vout[int(voff[m]) + k]) + counts[m] * K].view(counts[m], K)
+                    for k in range(len(vs))])
+    return res
 
 
 def forest_predict(forest: Forest, Xb: torch.Tensor, model_rows: Sequence[Optional[torch.Tensor]],

@@ -175,6 +175,10 @@ class _ForestLearner(Learner):
         dev = X.device
         N, F = X.shape
         out: List[Optional[dict]] = [None] * len(jobs)
+        # shared-forest registry for predict_batch (id(state) -> (state, share key, depth, gain)): the grid
+        # points pruned from one grown forest are scored in one walk of it (TE.forest_predict_multi)
+        self._share_reg: Dict[int, tuple] = {}
+        self._share_forest: Dict[tuple, "TE.Forest"] = {}
         # group jobs by binning
         groups: Dict[int, List[int]] = {}
         for i, j in enumerate(jobs):
@@ -264,12 +268,17 @@ class _ForestLearner(Learner):
                 ts = np.nonzero(owner == g)[0]
                 sub = Forest_subset(forest, ts)
                 md, mg = members[g][1], members[g][2]
+                skey = (mb, g)
+                if len(members[g][0]) > 1:
+                    self._share_forest[skey] = sub
                 for i in members[g][0]:
                     pi = jobs[i].params
                     di, gi = int(pi.get("max_depth", 5)), float(pi.get("min_info_gain", 0.0))
                     fi = sub if (di, gi) == (md, mg) else TE.prune_forest(sub, di, gi)
                     out[i] = {"forest": fi.to_state(), "bins": spec.to_state(), "n_classes": K,
                               "num_trees": len(ts), "max_bins": mb, "n_features": F}
+                    if len(members[g][0]) > 1:
+                        self._share_reg[id(out[i])] = (out[i], skey, di, gi)
         return out
 
     # -- prediction
@@ -303,7 +312,31 @@ class _ForestLearner(Learner):
         for i, s in enumerate(states):
             groups.setdefault(int(s["max_bins"]), []).append(i)
         res = [None] * len(states)
+        reg = getattr(self, "_share_reg", {})
         for mb, idxs in groups.items():
+            # grid points pruned from one grown forest and scored on the same rows: one shared walk
+            shared: Dict[tuple, List[int]] = {}
+            for i in idxs:
+                e = reg.get(id(states[i]))
+                if e is not None and e[0] is states[i] and e[1] in self._share_forest:
+                    shared.setdefault((e[1], id(rows[i])), []).append(i)
+            shared = {k: v for k, v in shared.items() if len(v) > 1 and all(rows[j] is rows[v[0]] for j in v)}
+            if shared:
+                _, Xb = self._binned(states[idxs[0]], X, context)
+                keys = list(shared)
+                grown = [self._share_forest[k[0]] for k in keys]
+                big = TE.Forest.concat(grown)
+                off = np.cumsum([0] + [f.n_trees for f in grown])
+                raws = TE.forest_predict_multi(
+                    big, Xb, [rows[shared[k][0]] for k in keys],
+                    [list(range(off[n], off[n + 1])) for n in range(len(keys))],
+                    [[reg[id(states[i])][2:4] for i in shared[k]] for k in keys])
+                for n, k in enumerate(keys):
+                    for i, raw in zip(shared[k], raws[n]):
+                        res[i] = self._outputs(states[i], raw.to(torch.float64))
+                idxs = [i for i in idxs if res[i] is None]
+                if not idxs:
+                    continue
             forests = [self._forest(states[i])[0] for i in idxs]
             _, Xb = self._binned(states[idxs[0]], X, context)
             big = TE.Forest.concat(forests)

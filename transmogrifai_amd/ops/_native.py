@@ -85,7 +85,7 @@ _HIP_SIGS = {
     "tmog_hip_lr_objective": [P, I64, I32, P, P, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P],
     "tmog_hip_lr_epilogue_grad": [P, I64, I32, P, P, P, I32, I32, I32, P, I32, P, I32, P, P, P, I32, P],
     "tmog_hip_forest_predict": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P],
-    "tmog_hip_forest_predict_multi": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P, P, P, P, P, P],
+    "tmog_hip_forest_predict_multi": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P, P, P, P, P],
     "tmog_hip_col_stats": [P, P, I64, I32, I64, P, P],
     "tmog_hip_vectorize_numeric": [P, P, P, I64, I32, P, P, P, P, I64, I32, P],
     "tmog_hip_onehot_pivot": [P, P, P, P, I32, I64, P, I64, P],

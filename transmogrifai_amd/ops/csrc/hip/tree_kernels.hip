@@ -1280,6 +1280,113 @@ __global__ void __launch_bounds__(PRED_ROWS * PRED_TPR) forest_predict_lds_kerne
   }
 }
 
+// Shared-forest prediction for pruned variants (models/trees.py: RF grid points that differ only in
+// maxDepth / minInfoGain share one grown forest, tree_engine.prune_forest). Model m walks the grown
+// trees once per (row, tree) and serves all of its variants v in [var_off[m], var_off[m+1]) on the way
+// down: variant v stops at the first node that is a leaf of the grown tree, lies at depth >= var_depth[v]
+// or has a split gain < the variant's min gain (exactly prune_forest's rule; the leaf / gain part comes
+// precomputed as a per-node variant bitmask) and adds that node's value. One walk
+// instead of one per variant (~5x fewer node visits for the default RF grid). Rows staged in LDS as in
+// forest_predict_lds_kernel; 4 trees interleaved per thread; out[var_out_off[v] + (row - r0) * K + c].
+constexpr int PM_ROWS = 64;
+constexpr int PM_TPR = 4;
+constexpr int PM_TU = 4;
+constexpr int PM_VK = 32;      // variants x classes accumulated per thread
+
+template <int KT>     // classes (compile-time: the per-thread accumulators stay in registers)
+__global__ void __launch_bounds__(PM_ROWS * PM_TPR) forest_predict_multi_kernel(
+    const uint8_t* __restrict__ Xb, int F, const int64_t* __restrict__ model_row_off,
+    const int32_t* __restrict__ row_list, const int64_t* __restrict__ model_tree_off,
+    const int64_t* __restrict__ tree_off, const float* __restrict__ tree_weight, const int4* __restrict__ nodes,
+    const uint8_t* __restrict__ default_left, int missing_bin, const float* __restrict__ leaf_value, int K,
+    const uint32_t* __restrict__ node_mask, const int32_t* __restrict__ var_off, const int32_t* __restrict__ var_depth,
+    const int64_t* __restrict__ var_out_off, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t srows[];
+  const int m = blockIdx.y;
+  const int64_t r0 = model_row_off[m], r1 = model_row_off[m + 1];
+  const int64_t blk0 = r0 + (int64_t)blockIdx.x * PM_ROWS;
+  if (blk0 >= r1) return;
+  const int nrow = (int)min((int64_t)PM_ROWS, r1 - blk0);
+  const int v0 = var_off[m], V = var_off[m + 1] - v0;        // host guarantees V * K <= PM_VK
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  for (int r = wave; r < nrow; r += nwaves) {
+    const int64_t row = row_list ? row_list[blk0 + r] : (blk0 + r - r0);
+    const uint8_t* src = Xb + row * F;
+    for (int b = lane; b < F; b += 64) srows[r * F + b] = src[b];
+  }
+  __syncthreads();
+  // per-thread accumulators live in the LDS reduction area (dynamic variant index, no register arrays)
+  // depth stop masks: s_dmask[d] = variants whose max depth is <= d (the gain / grown-leaf part of the
+  // rule is precomputed per node by the host: node_mask[k] = variants that stop at node k regardless of depth)
+  __shared__ uint32_t s_dmask[33];
+  if (threadIdx.x < 33) {
+    uint32_t mk = 0u;
+    for (int v = 0; v < V; ++v) mk |= (var_depth[v0 + v] <= (int)threadIdx.x ? 1u : 0u) << v;
+    s_dmask[threadIdx.x] = mk;
+  }
+  const int rr = threadIdx.x % PM_ROWS, q = threadIdx.x / PM_ROWS;
+  float* red = reinterpret_cast<float*>(srows + ((PM_ROWS * F + 15) & ~15));
+  float* acc = red + (q * PM_ROWS + rr) * PM_VK;
+  for (int i = 0; i < PM_VK; ++i) acc[i] = 0.f;
+  __syncthreads();
+  if (rr < nrow) {
+    const uint8_t* xr = srows + rr * F;
+    const int64_t t_end = model_tree_off[m + 1];
+    const uint32_t all = (1u << V) - 1u;
+    for (int64_t t = model_tree_off[m] + (int64_t)q * PM_TU; t < t_end; t += (int64_t)PM_TU * PM_TPR) {
+      const int nu = (int)min((int64_t)PM_TU, t_end - t);
+      int64_t k[PM_TU];
+      int4 nd[PM_TU];
+      uint32_t live[PM_TU];
+      int dep[PM_TU];
+#pragma unroll
+      for (int u = 0; u < PM_TU; ++u) {
+        k[u] = u < nu ? tree_off[t + u] : tree_off[t];
+        nd[u] = nodes[k[u]];
+        live[u] = u < nu ? all : 0u;
+        dep[u] = 0;
+      }
+      bool active = true;
+      while (active) {
+        active = false;
+#pragma unroll
+        for (int u = 0; u < PM_TU; ++u) {
+          if (live[u] != 0u) {
+            const uint32_t stop = (node_mask[k[u]] | s_dmask[min(dep[u], 32)]) & live[u];
+            if (stop) {
+              const float w = tree_weight[t + u];
+              for (int c = 0; c < KT; ++c) {
+                const float val = w * leaf_value[k[u] * KT + c];
+                for (uint32_t sm = stop; sm; sm &= sm - 1u) acc[(__ffs(sm) - 1) * KT + c] += val;
+              }
+              live[u] &= ~stop;
+            }
+            if (live[u] != 0u) {
+              const uint8_t b = xr[nd[u].x];
+              const bool gl = (missing_bin >= 0 && b == missing_bin) ? (default_left[k[u]] != 0) : ((int)b <= nd[u].y);
+              k[u] = gl ? nd[u].z : nd[u].w;
+              nd[u] = nodes[k[u]];
+              dep[u] += 1;
+              active = true;
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (q == 0 && rr < nrow) {
+    for (int v = 0; v < V; ++v) {
+      float* o = out + var_out_off[v0 + v] + (blk0 + rr - r0) * KT;
+      for (int c = 0; c < KT; ++c) {
+        float x = red[rr * PM_VK + v * KT + c];
+        for (int qq = 1; qq < PM_TPR; ++qq) x += red[(qq * PM_ROWS + rr) * PM_VK + v * KT + c];
+        o[c] = x;
+      }
+    }
+  }
+}
+
 // grid.y = model; each thread walks every tree of its model for one of the model's rows.
 __global__ void __launch_bounds__(256) forest_predict_kernel(
     const uint8_t* __restrict__ Xb, int F, const int64_t* __restrict__ model_row_off,
@@ -1512,6 +1619,31 @@ int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, 
   if (n_items == 0) return 0;
   hipLaunchKernelGGL(leaf_collect_kernel, dim3(n_items), dim3(256), 0, stream, rows, (const LeafItem*)items,
                      out_rows, out_gid);
+  return (int)hipGetLastError();
+}
+
+// Shared-forest multi-variant prediction (forest_predict_multi_kernel). Every model's V x K <= 32, V <= 16.
+int tmog_hip_forest_predict_multi(const uint8_t* Xb, int F, int n_models, const int64_t* model_row_off,
+                                  const int32_t* row_list, int64_t max_rows, const int64_t* model_tree_off,
+                                  const int64_t* tree_off, const float* tree_weight, const int32_t* nodes,
+                                  const uint8_t* default_left, int missing_bin, const float* leaf_value, int K,
+                                  const uint32_t* node_mask, const int32_t* var_off, const int32_t* var_depth,
+                                  const int64_t* var_out_off, float* out, hipStream_t stream) {
+  if (n_models == 0 || max_rows == 0) return 0;
+  if (K != 1 && K != 2 && K != 4 && K != 8) return -2;
+  const size_t lds = (((size_t)PM_ROWS * F + 15) & ~(size_t)15) + sizeof(float) * PM_VK * PM_ROWS * PM_TPR;
+  if (lds > 160 * 1024) return -3;
+  dim3 g2((unsigned)((max_rows + PM_ROWS - 1) / PM_ROWS), n_models);
+#define TM_PM(KV)                                                                                               \
+  hipLaunchKernelGGL(forest_predict_multi_kernel<KV>, g2, dim3(PM_ROWS * PM_TPR), lds, stream, Xb, F,           \
+                     model_row_off, row_list, model_tree_off, tree_off, tree_weight, (const int4*)nodes,         \
+                     default_left, missing_bin, leaf_value, K, node_mask, var_off, var_depth, var_out_off,      \
+                     out)
+  if (K == 1) TM_PM(1);
+  else if (K == 2) TM_PM(2);
+  else if (K == 4) TM_PM(4);
+  else TM_PM(8);
+#undef TM_PM
   return (int)hipGetLastError();
 }
 
