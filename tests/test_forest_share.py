@@ -104,3 +104,20 @@ def test_forest_predict_multi_kernel_matches_pruned_forests():
         for (d, g), o in zip(vs, outs):
             want = te.forest_predict(te.prune_forest(sub, d, g), Xc, [rows], [list(range(sub.n_trees))])[0]
             torch.testing.assert_close(o, want, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_partition_from_feature_major_copy_identical():
+    """Newton growth on the GPU with the partition reading split columns from the feature-major copy
+    (GrowArgs.XbT) equals growth reading the row-major matrix."""
+    X, y = _data(N=20000, F=16)
+    p = torch.sigmoid(torch.randn(X.shape[0], generator=torch.Generator().manual_seed(4)))
+    g, h = (p - y).float().cuda(), (p * (1 - p)).float().cuda()
+    Xc = X.cuda()
+    rows = torch.arange(X.shape[0], device="cuda")
+    jobs = [te.TreeJob(0, te.TreeParams(max_depth=8, min_child_weight=5.0, reg_lambda=1.0, eta=0.3), rows),
+            te.TreeJob(0, te.TreeParams(max_depth=6, min_child_weight=1.0, reg_lambda=1.0, eta=0.3), rows[::2])]
+    kw = dict(mode=te.MODE_GH, kind=te.KIND_NEWTON, t1=g[None, :], t2=h[None, :], B=32)
+    a = te.grow_forest(Xc, np.full(X.shape[1], 32), jobs, **kw)
+    b = te.grow_forest(Xc, np.full(X.shape[1], 32), jobs, XbT=Xc.t().contiguous(), **kw)
+    _same(a, b)

@@ -292,7 +292,8 @@ class _GrowArgs(C.Structure):
                 ("n_bins_host", C.c_void_p), ("csr_ptr", C.c_void_p), ("csr_col", C.c_void_p),
                 ("csr_nf", C.c_int32), ("fp_rank", C.c_int32), ("fp_world", C.c_int32), ("fp_mlo", C.c_int32),
                 ("fp_mhi", C.c_int32), ("fp_olo", C.c_int32), ("fp_ohi", C.c_int32), ("fp_comm", C.c_void_p),
-                ("fp_exchange", C.c_void_p), ("fp_ctx", C.c_void_p), ("slot_base", C.c_int32)]
+                ("fp_exchange", C.c_void_p), ("fp_ctx", C.c_void_p), ("slot_base", C.c_int32),
+                ("XbT", C.c_void_p)]
 
 
 @dataclass
@@ -386,7 +387,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 t2: Optional[torch.Tensor] = None, B: int = 32, missing_bin: int = -1,
                 subtract: bool = True, chunk_rows: int = 4096, rng_seed: int = 0,
                 collect_leaves: bool = False, groups: Optional[int] = None, csr=None, root=None,
-                fp: Optional[FpPlan] = None, slot_base: int = 0) -> Forest:
+                fp: Optional[FpPlan] = None, slot_base: int = 0, XbT: Optional[torch.Tensor] = None) -> Forest:
     """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``.
 
     The level loop runs natively (``ops/csrc/common/tree_grow.hpp``): on the GPU every job group gets
@@ -485,7 +486,8 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                   int(fp.par.rank) if fpw else 0, fpw, fp.mlo if fpw else 0, fp.mhi if fpw else 0,
                   fp.olo if fpw else 0, fp.ohi if fpw else 0,
                   C.cast(fp_comm, C.c_void_p) if fp_comm is not None else None,
-                  C.cast(fp_cb, C.c_void_p) if fp_cb is not None else None, None, int(slot_base))
+                  C.cast(fp_cb, C.c_void_p) if fp_cb is not None else None, None, int(slot_base),
+                  N.ptr(XbT) if (on_gpu and XbT is not None) else None)
     lib = N.hip() if on_gpu else N.host()
     fn = (lambda name: getattr(lib, f"tmog_hip_{name}")) if on_gpu else (lambda name: getattr(lib, f"tmog_{name}_cpu"))
     h = fn("grow_forest")(C.byref(a))

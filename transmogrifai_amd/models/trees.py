@@ -688,6 +688,8 @@ class XGBoostClassifierLearner(_BoostLearner):
         # one-hot / null-indicator columns: histogram from the rows' CSR lists (tree_kernels.hip)
         csr = TE.onebin_csr(Xg, n_bins_g, cols=None if fp is None else fp.one_cols) \
             if (dev.type == "cuda" and spec.missing_bin > 0) else None
+        # feature-major copy for the partition kernel's split-column reads (tree_grow.hpp GrowArgs.XbT)
+        XgT = Xg.t().contiguous() if (dev.type == "cuda" and os.environ.get("TMOG_PART_T", "1") != "0") else None
         yf = yy.to(torch.float32).contiguous()
         G = H = None
         if fused:         # shared [P, N] statistics: each job's row is only touched by its own part
@@ -738,7 +740,7 @@ class XGBoostClassifierLearner(_BoostLearner):
                     root = (packed.clone(), cnts)
                 forest = TE.grow_forest(Xg, n_bins_g, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
                                         missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root, fp=fp,
-                                        slot_base=slot_base, groups=groups)
+                                        slot_base=slot_base, groups=groups, XbT=XgT)
                 if colperm is not None:
                     internal = forest.nodes[:, 2] >= 0
                     forest.nodes[internal, 0] = colperm[forest.nodes[internal, 0]]

@@ -68,7 +68,7 @@ _HIP_SIGS = {
     "tmog_hip_rccl_unique_id": [P, I32],
     "tmog_hip_rccl_comm_init": [P, I32, I32],
     "tmog_hip_rccl_comm_destroy": [P],
-    "tmog_hip_partition_fused": [P, I32, P, P, P, I32, P, P, P, P, P, P, P, I32, P, P],
+    "tmog_hip_partition_fused": [P, I32, P, P, P, I32, P, P, P, P, P, P, P, I32, P, P, I64, P],
     "tmog_hip_leaf_collect": [P, P, I32, P, P, P],
     "tmog_hip_grow_forest": [P],
     "tmog_hip_grow_status": [P, P, I32],

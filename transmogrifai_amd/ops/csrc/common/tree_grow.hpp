@@ -79,6 +79,10 @@ struct GrowArgs {
   // GPU: first per-group resource slot (stream, staging, histogram buffers) of this call -- concurrent
   // calls (e.g. the XGBoost learner's pipelined job halves, one host thread each) use disjoint slots
   int32_t slot_base;
+  // GPU, optional: feature-major copy of Xb ([F][N], row index = packed entry & 0xFFFFFF). The partition
+  // reads one split-column byte per row; from the feature-major copy the bytes of a node's rows share
+  // cache lines (from Xb every byte pulls its own line)
+  const uint8_t* XbT;
 };
 
 // Feature-parallel split record, one per node and rank:

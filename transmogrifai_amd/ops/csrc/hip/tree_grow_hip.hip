@@ -43,7 +43,8 @@ int tmog_hip_hist_stat_chunk(int B, int S);
 int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, const void* items,
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                              const int32_t* split_bin, const uint8_t* dl, const float* node_params,
-                             const float* split_gain, int missing_bin, int64_t* cursors, hipStream_t stream);
+                             const float* split_gain, int missing_bin, int64_t* cursors, const uint8_t* XbT, int64_t N,
+                             hipStream_t stream);
 int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
                           int32_t* out_gid, hipStream_t stream);
 }
@@ -223,7 +224,7 @@ struct GpuBackend {
                        const int64_t* nb, const int64_t* nc, const int32_t* feat, const int32_t* bin, const uint8_t* dl,
                        const float* params, const float* gain, int64_t* cursors) {
     kchk(tmog_hip_partition_fused(g.Xb, g.F, rows, rows_alt, items, n, nb, nc, feat, bin, dl, params, gain,
-                                  g.missing_bin, cursors, sl.stream),
+                                  g.missing_bin, cursors, g.XbT, g.N, sl.stream),
          "partition_fused");
   }
   void partition_nodes(const tmog::GrowArgs&, const uint32_t*, uint32_t*, int, const int64_t*, const int64_t*,

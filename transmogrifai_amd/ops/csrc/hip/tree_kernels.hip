@@ -1108,7 +1108,7 @@ __global__ void __launch_bounds__(256) partition_fused_kernel(
     const PartItem* __restrict__ items, const int64_t* __restrict__ node_begin, const int64_t* __restrict__ node_count,
     const int32_t* __restrict__ split_feat, const int32_t* __restrict__ split_bin, const uint8_t* __restrict__ dl,
     const float* __restrict__ node_params, const float* __restrict__ split_gain, int missing_bin,
-    unsigned long long* __restrict__ cursors) {
+    unsigned long long* __restrict__ cursors, const uint8_t* __restrict__ XbT, int64_t Nt) {
   const PartItem it = items[blockIdx.x];
   const int j = it.node;
   const int f = split_feat[j], sb = split_bin[j];
@@ -1134,7 +1134,8 @@ __global__ void __launch_bounds__(256) partition_fused_kernel(
     }
     uint8_t bn[PART_U];
 #pragma unroll
-    for (int u = 0; u < PART_U; ++u) bn[u] = Xb[(int64_t)(e[u] & 0xFFFFFFu) * F + f];
+    for (int u = 0; u < PART_U; ++u)
+      bn[u] = XbT ? XbT[(int64_t)f * Nt + (e[u] & 0xFFFFFFu)] : Xb[(int64_t)(e[u] & 0xFFFFFFu) * F + f];
     int wpre[PART_U];
 #pragma unroll
     for (int u = 0; u < PART_U; ++u) {
@@ -1606,11 +1607,12 @@ int tmog_hip_hist_stat_chunk(int B, int S) {
 int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, const void* items,
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                              const int32_t* split_bin, const uint8_t* dl, const float* node_params,
-                             const float* split_gain, int missing_bin, int64_t* cursors, hipStream_t stream) {
+                             const float* split_gain, int missing_bin, int64_t* cursors, const uint8_t* XbT,
+                             int64_t N, hipStream_t stream) {
   if (n_items == 0) return 0;
   hipLaunchKernelGGL(partition_fused_kernel, dim3(n_items), dim3(256), 0, stream, Xb, F, rows_in, rows_out,
                      (const PartItem*)items, node_begin, node_count, split_feat, split_bin, dl, node_params,
-                     split_gain, missing_bin, (unsigned long long*)cursors);
+                     split_gain, missing_bin, (unsigned long long*)cursors, XbT, N);
   return (int)hipGetLastError();
 }
 
