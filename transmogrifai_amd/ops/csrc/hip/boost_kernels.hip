@@ -34,30 +34,60 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
     int64_t N, double* __restrict__ F, float* __restrict__ G, float* __restrict__ H, const float* __restrict__ y,
     int objective, int32_t* __restrict__ auc_hist, int bins, int64_t n_gid, int64_t n_trees, int64_t P) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n_entries) return;
-  const int64_t r = entries[e] & 0xFFFFFFu;
-  const int32_t g_id = gid[e];
-  if (g_id < 0 || g_id >= n_gid || r >= N) return;                 // defensive: never index out of range
-  const int64_t t = gid_tree[g_id];
-  if (t < 0 || t >= n_trees) return;
-  const int64_t p = tree_job[t];
-  if (p < 0 || p >= P) return;
-  const int64_t k = p * N + r;
-  const double m = F[k] + (double)gid_value[g_id];
-  F[k] = m;
-  const float yr = y[r];
-  if (objective == 0) {
-    const double pr = 1.0 / (1.0 + exp(-m));
-    G[k] = (float)(pr - (double)yr);
-    H[k] = (float)fmax(pr * (1.0 - pr), 1e-16);
-    if (auc_hist) {
-      const float s = fminf(fmaxf((float)pr, 0.f), 1.f);
-      const int b = (int)(s * (float)(bins - 1));
-      atomicAdd(auc_hist + (p * 2 + (yr > 0.5f ? 1 : 0)) * bins + (bins - 1 - b), 1);
+  // no early returns: the AuPR-count aggregation below needs every lane of the wave
+  int64_t slot = -1;                           // this lane's (job, label, score-bin) counter, -1 = none
+  bool ok = e < n_entries;
+  int64_t r = 0, t = 0, p = 0;
+  int32_t g_id = 0;
+  if (ok) {
+    r = entries[e] & 0xFFFFFFu;
+    g_id = gid[e];
+    ok = g_id >= 0 && g_id < n_gid && r < N;   // defensive: never index out of range
+  }
+  if (ok) {
+    t = gid_tree[g_id];
+    ok = t >= 0 && t < n_trees;
+  }
+  if (ok) {
+    p = tree_job[t];
+    ok = p >= 0 && p < P;
+  }
+  if (ok) {
+    const int64_t k = p * N + r;
+    const double m = F[k] + (double)gid_value[g_id];
+    F[k] = m;
+    const float yr = y[r];
+    if (objective == 0) {
+      const double pr = 1.0 / (1.0 + exp(-m));
+      G[k] = (float)(pr - (double)yr);
+      H[k] = (float)fmax(pr * (1.0 - pr), 1e-16);
+      if (auc_hist) {
+        const float sc = fminf(fmaxf((float)pr, 0.f), 1.f);
+        const int b = (int)(sc * (float)(bins - 1));
+        slot = (p * 2 + (yr > 0.5f ? 1 : 0)) * bins + (bins - 1 - b);
+      }
+    } else {
+      G[k] = (float)(m - (double)yr);
+      H[k] = 1.f;
     }
-  } else {
-    G[k] = (float)(m - (double)yr);
-    H[k] = 1.f;
+  }
+  if (auc_hist) {
+    // Scores of a boosting round cluster in a few bins (eta-sized steps from a shared base margin), so
+    // per-lane atomics serialise on the same counters: the wave first peels off up to 8 distinct slots
+    // (ballot on the leader's slot, one atomic of the match count each), the rest go per lane.
+    const int lane = threadIdx.x & 63;
+    bool pend = slot >= 0;
+    for (int it = 0; it < 8; ++it) {
+      const unsigned long long act = __ballot(pend);
+      if (act == 0ull) break;
+      const int leader = __ffsll((long long)act) - 1;
+      const int64_t ls = __shfl(slot, leader, 64);
+      const bool mine = pend && slot == ls;
+      const unsigned long long mm = __ballot(mine);
+      if (lane == leader) atomicAdd(auc_hist + ls, (int)__popcll(mm));
+      pend = pend && !mine;
+    }
+    if (pend) atomicAdd(auc_hist + slot, 1);
   }
 }
 
