@@ -756,7 +756,8 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
       double gain;
       bool ok = true;
       if (kind == 3) {
-        if (left[1] < mcw || right[1] < mcw) ok = false;
+        // invalid by min_child_weight: skip the two fp64 divisions (whole waves skip at small nodes)
+        if (left[1] < mcw || right[1] < mcw) return;
         gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
       } else {
         double lc, rc;

@@ -42,6 +42,20 @@ def _global_label_counts(y):
     return dict(dp.merge_counters([Counter(label_counts(y))])[0])
 
 
+def _splitter_prepare(splitter, y):
+    """``splitter.pre_validation_prepare`` on the global label statistics it needs: the DataSplitter only
+    the global row count (one scalar all-reduce -- value counts of a continuous label are one entry per
+    row: 100M entries at the regression-100m config), the balancer / cutter the label value counts."""
+    from ..parallel import dp
+    from ..tuning.splitters import DataSplitter
+    if type(splitter) is DataSplitter and not isinstance(y, dict):
+        n = torch.tensor([float(y.shape[0])], dtype=torch.float64, device=y.device)
+        if dp.active():
+            n = dp.sum_([n])[0]
+        return splitter.pre_validation_prepare({}, n_total=int(n.item()))
+    return splitter.pre_validation_prepare(_global_label_counts(y))
+
+
 @register_stage
 class SelectedModel(OpPredictorModel):
     operation_name = "modelSelection"
@@ -92,7 +106,7 @@ class ModelSelector(BinaryEstimator):
         from ..parallel import dp
         label, vec = self._inputs[0].name, self._inputs[1].name
         if self.splitter is not None:
-            self._split_summary = self.splitter.pre_validation_prepare(_global_label_counts(data[label].values))
+            self._split_summary = _splitter_prepare(self.splitter, data[label].values)
         if not during:
             self.best_estimator = None
             return None
@@ -116,7 +130,7 @@ class ModelSelector(BinaryEstimator):
             if self.best_estimator is not None and getattr(self, "_split_summary", None) is not None:
                 split_summary = self._split_summary
             else:
-                split_summary = self.splitter.pre_validation_prepare(_global_label_counts(y))
+                split_summary = _splitter_prepare(self.splitter, y)
         # only the rows some CV fold or the refit may train on (the splitter's maxTrainingSample cap) are
         # materialised from the (blocked) feature vector; folds are functions of the global row id
         X, y, row_ids = self._gather_candidates(vec_col, y, row_ids)
