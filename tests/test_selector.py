@@ -132,3 +132,21 @@ def test_job_cost_model_recalibrates_from_measured_times(monkeypatch):
     n_tr = t / (sc * 4 * 4)
     assert 250 <= n_tr <= 350
     assert V._scaled_cost("OpNaiveBayes", {}, n_tr, 4) == pytest.approx(t / 4)
+
+
+def test_data_splitter_prepare_uses_row_count_only(monkeypatch):
+    """The DataSplitter needs the global row count only: a continuous label must not be turned into value
+    counts (one dict entry per row -- 45 s of the 100M-row regression config before)."""
+    import torch
+    from transmogrifai_amd.selector import model_selector as MS
+    from transmogrifai_amd.tuning import splitters as SP
+
+    def boom(y):
+        raise AssertionError("label value counts computed for a DataSplitter")
+    monkeypatch.setattr(SP, "label_counts", boom)
+    sp = SP.DataSplitter(seed=1)
+    summ = MS._splitter_prepare(sp, torch.rand(5000, dtype=torch.float64))
+    assert summ["preSplitterDataCount"] == 5000
+    monkeypatch.undo()
+    bal = SP.DataBalancer(seed=1)
+    assert "className" in MS._splitter_prepare(bal, (torch.rand(4000) < 0.1).double())
