@@ -161,6 +161,7 @@ def main():
         D.barrier()
 
     n_raw = [0]
+    stage_t = [{}]
 
     def one_run():
         uid.reset(0)
@@ -176,6 +177,7 @@ def main():
         model = wf.train()
         sync()
         dt = time.perf_counter() - t0
+        stage_t[0] = {k: round(v, 4) for k, v in model.train_timings.items() if isinstance(v, (int, float))}
         sel = model.get_origin_stage_of(pred)
         summ = sel.metadata.get("summary", {})
         ho = (summ.get("holdoutEvaluation") or {}).get(CONFIGS[args.config][3], float("nan"))
@@ -235,6 +237,7 @@ def main():
         }
         if args.verbose and summ:
             out["timings"] = summ.get("timings")
+            out["stage_timings"] = stage_t[0]
         print(json.dumps(out), flush=True)
     if D.is_dist():
         import torch.distributed as dist
