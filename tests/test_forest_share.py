@@ -121,3 +121,34 @@ def test_partition_from_feature_major_copy_identical():
     a = te.grow_forest(Xc, np.full(X.shape[1], 32), jobs, **kw)
     b = te.grow_forest(Xc, np.full(X.shape[1], 32), jobs, XbT=Xc.t().contiguous(), **kw)
     _same(a, b)
+
+
+def test_share_groups_regression_and_multiclass(monkeypatch):
+    """Shared growth + pruning gives the unshared forests for RF regression (variance) and 3-class RF."""
+    from transmogrifai_amd.models.base import FitJob
+    from transmogrifai_amd.models.trees import RandomForestClassifierLearner, RandomForestRegressorLearner
+    X, y = _data(N=2500, F=8)
+    Xf = X.float()
+    rows = torch.arange(2000)
+    y3 = (X[:, 0].long() % 3).double()
+    yr = X[:, 0].double() * 0.3 + X[:, 5].double() * 0.1
+    for L, yy in ((RandomForestClassifierLearner(), y3), (RandomForestRegressorLearner(), yr)):
+        jobs = [FitJob(params={"max_depth": d, "min_info_gain": g, "min_instances_per_node": 5, "num_trees": 3,
+                               "feature_subset_strategy": "all", "seed": 2}, rows=rows)
+                for d in (3, 7) for g in (0.0, 0.01)]
+        monkeypatch.setenv("TMOG_RF_SHARE", "0")
+        ref = L.fit_batch(Xf, yy, jobs)
+        monkeypatch.setenv("TMOG_RF_SHARE", "1")
+        got = L.fit_batch(Xf, yy, jobs)
+        for a, b in zip(ref, got):
+            fa, fb = te.Forest.from_state(a["forest"]), te.Forest.from_state(b["forest"])
+            for k in ("tree_off", "nodes", "default_left", "gain"):
+                np.testing.assert_array_equal(getattr(fa, k), getattr(fb, k), err_msg=k)
+            # a node pruned to a leaf keeps the statistics of its own histogram, where direct growth
+            # (leaf at max depth, no histogram) derives a right child's from parent - left in fp32:
+            # class counts are exact, regression sums agree to fp32 rounding
+            np.testing.assert_allclose(fb.value, fa.value, rtol=1e-6, atol=1e-6)
+        pr = L.predict_batch(got, Xf, [rows] * len(jobs))
+        for st, (p0, r0, q0) in zip(ref, pr):
+            p1, r1, q1 = L.predict_batch([st], Xf, [rows])[0]
+            torch.testing.assert_close(r0, r1, rtol=1e-5, atol=1e-5)

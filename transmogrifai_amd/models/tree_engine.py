@@ -151,7 +151,9 @@ def prune_forest(f: Forest, max_depth: int, min_gain: float) -> Forest:
     emits it. Lets the model selector grow one forest per (bootstrap, seed, minInstancesPerNode, ...)
     for all of its maxDepth x minInfoGain grid points (``models/trees.py`` ``_ForestLearner``).
     Thresholds are compared on the stored fp32 gain (a split whose fp64 gain lies within one fp32
-    ulp of the threshold may be kept)."""
+    ulp of the threshold may be kept). Leaf statistics: a pruned node keeps the totals of its own
+    histogram, where direct growth gives a max-depth right child parent - left (fp32): class counts are
+    identical, regression / Newton sums agree to fp32 rounding."""
     n = len(f.nodes)
     if n == 0:
         return f
