@@ -483,6 +483,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     std::vector<HistItemH> hitems;
     std::vector<PartItemH> citems;
     std::vector<int64_t> z_off, z_size;
+    std::vector<int64_t> zc_off, zc_size;   // nodes whose only multi-item group is the CSR one: zero its words
     std::vector<int64_t> b_nb, b_nc, b_nho;
     std::vector<int32_t> b_nfo, b_nnf, b_nmd;
     for (int j = 0; j < m; ++j) {
@@ -512,9 +513,19 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
       const int64_t ncsr = std::max<int64_t>(1, (cnt + kCsrRows - 1) / kCsrRows);
       bool has_csr = false;
       for (const FeatGroup& fgp : grp) has_csr |= fgp.csr;
-      if (nch > 1 || (has_csr && ncsr > 1)) {
+      if (nch > 1) {
         z_off.push_back(hoff[j]);
         z_size.push_back(hsz[j]);
+      } else if (has_csr && ncsr > 1) {
+        // single-chunk multi-bin groups write their words exclusively: only the one-present-bin region
+        // past the dense prefix (the CSR group's bin-0 words) accumulates atomically and needs zeroing
+        if (live_dense >= 0 && live_dense < hsz[j]) {
+          zc_off.push_back(hoff[j] + live_dense);
+          zc_size.push_back(hsz[j] - live_dense);
+        } else {
+          z_off.push_back(hoff[j]);
+          z_size.push_back(hsz[j]);
+        }
       }
       for (const FeatGroup& fgp : grp) {
         const int64_t step = fgp.csr ? kCsrRows : a.chunk_rows;
@@ -548,8 +559,9 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
       d_size.push_back(hsz[d_big[q]]);
       d_max = std::max(d_max, hsz[d_big[q]]);
     }
-    int64_t z_max = 0;
+    int64_t z_max = 0, zc_max = 0;
     for (int64_t z : z_size) z_max = std::max(z_max, z);
+    for (int64_t z : zc_size) zc_max = std::max(zc_max, z);
     // ---- ship everything in one copy
     st1.clear();
     const size_t o_nfo = st1.add(feat_off), o_nnf = st1.add(nfeat), o_nmd = st1.add(nmd), o_nho = st1.add(hoff);
@@ -558,6 +570,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     const size_t o_fl = own_list ? st1.add(feat_list) : 0;
     const size_t o_hit = st1.add(hitems), o_cit = st1.add(citems);
     const size_t o_zo = st1.add(z_off), o_zs = st1.add(z_size);
+    const size_t o_zco = st1.add(zc_off), o_zcs = st1.add(zc_size);
     const size_t o_dp = st1.add(d_poff), o_ds = st1.add(d_soff), o_do = st1.add(d_ooff), o_dz = st1.add(d_size);
     const size_t o_bnb = st1.add(b_nb), o_bnc = st1.add(b_nc), o_bnfo = st1.add(b_nfo), o_bnnf = st1.add(b_nnf);
     const size_t o_bnmd = st1.add(b_nmd), o_bnho = st1.add(b_nho);
@@ -568,6 +581,9 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
     // ---- histograms
     bk.zero_segments(hist, TM_P(const int64_t, o_zo), TM_P(const int64_t, o_zs), (int)z_off.size(), z_max, live_dense,
                      a.B * a.S, a.S);
+    if (!zc_off.empty())   // segments start at the one-present-bin region: dense prefix 0
+      bk.zero_segments(hist, TM_P(const int64_t, o_zco), TM_P(const int64_t, o_zcs), (int)zc_off.size(), zc_max, 0,
+                       a.B * a.S, a.S);
     bk.hist_build(a, rows, hitems.size() ? (const void*)(d1 + o_hit) : nullptr, (int)hitems.size(),
                   TM_P(const int32_t, o_nfo), flist, TM_P(const int32_t, o_nmd), TM_P(const int64_t, o_nho), hist,
                   (int)b_nb.size(), TM_P(const int64_t, o_bnb), TM_P(const int64_t, o_bnc),
