@@ -95,3 +95,25 @@ def test_owlqn_direction_kernel_matches_torch(d1, P, hist_n):
     got = LK.owlqn_direction(*c, hist_n, m)
     for w, r in zip(want, got):
         torch.testing.assert_close(r.cpu(), w, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_owlqn_candidate_kernel_matches_torch():
+    """Projected line-search candidate and its Armijo sums (HIP owlqn_candidate_kernel) vs torch in fp64."""
+    from transmogrifai_amd.ops import linear as LK
+    g0 = torch.Generator().manual_seed(11)
+    d1, P = 333, 24
+    U = torch.randn(d1, P, generator=g0, dtype=torch.float64)
+    U[torch.rand(d1, P, generator=g0) < 0.3] = 0.0
+    D = torch.randn(d1, P, generator=g0, dtype=torch.float64)
+    pg = torch.randn(d1, P, generator=g0, dtype=torch.float64)
+    xi = torch.where(U != 0, torch.sign(U), torch.sign(-pg))
+    l1 = torch.where(torch.rand(d1, P, generator=g0) < 0.5, torch.full((d1, P), 0.2, dtype=torch.float64),
+                     torch.zeros(d1, P, dtype=torch.float64))
+    alpha = torch.rand(P, generator=g0, dtype=torch.float64) + 0.1
+    cand = U + alpha[None, :] * D
+    cand = torch.where((l1 > 0) & (torch.sign(cand) != xi), torch.zeros_like(cand), cand)
+    want = (cand, (l1 * cand.abs()).sum(0), (pg * (cand - U)).sum(0))
+    got = LK.owlqn_candidate(*(t.cuda() for t in (U, D, xi, l1, pg, alpha)))
+    for w, r in zip(want, got):
+        torch.testing.assert_close(r.cpu(), w, rtol=1e-12, atol=1e-12)

@@ -240,10 +240,16 @@ def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max
         Un = U.clone()
         Fn = F.clone()
         for _ in range(max_ls):
-            cand = U + alpha[None, :] * D
-            cand = torch.where(has_l1 & (torch.sign(cand) != xi), torch.zeros_like(cand), cand)
-            fc = obj.value(cand) + (l1 * cand.abs()).sum(0)
-            ok = (fc <= F + 1e-4 * (pg * (cand - U)).sum(0)) & ~accepted
+            if fused_dir:
+                # projected candidate + its Armijo sums in one launch (ops/linear.py owlqn_candidate)
+                cand, l1t, dd = LK.owlqn_candidate(U, D, xi, l1, pg, alpha)
+                fc = obj.value(cand) + l1t
+                ok = (fc <= F + 1e-4 * dd) & ~accepted
+            else:
+                cand = U + alpha[None, :] * D
+                cand = torch.where(has_l1 & (torch.sign(cand) != xi), torch.zeros_like(cand), cand)
+                fc = obj.value(cand) + (l1 * cand.abs()).sum(0)
+                ok = (fc <= F + 1e-4 * (pg * (cand - U)).sum(0)) & ~accepted
             Un = torch.where(ok[None, :], cand, Un)
             Fn = torch.where(ok, fc, Fn)
             accepted |= ok

@@ -80,6 +80,7 @@ _HIP_SIGS = {
     "tmog_hip_boost_epilogue": [P, P, I64, P, P, P, I64, P, P, P, P, I32, P, I32, I64, I64, I64, P],
     "tmog_hip_aupr_counts": [P, I32, I32, P, P],
     "tmog_hip_owlqn_direction": [P, P, P, P, P, P, I32, I32, I32, I32, P, P, P, P, P],
+    "tmog_hip_owlqn_candidate": [P, P, P, P, P, P, I32, I32, P, P, P, P],
     "tmog_hip_poisson_pack": [P, I64, P, I32, P, I32, P, P, P, P],
     "tmog_hip_row_uniform": [P, I64, P, I32, P, P],
     "tmog_hip_lr_objective": [P, I64, I32, P, P, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P],

@@ -447,6 +447,34 @@ __global__ void __launch_bounds__(OW_NT) owlqn_direction_kernel(
   if (t == 0) dnorm_out[p] = fmax(sqrt(pn), 1e-300);
 }
 
+// OWL-QN line-search candidate for every problem column: cand = U + alpha D projected onto the orthant
+// xi (l1 > 0 coordinates whose sign left it are zeroed), with the two per-column sums the Armijo test
+// needs, sum l1 |cand| and sum pg (cand - U) -- one launch instead of ~12 torch ops per trial step.
+__global__ void __launch_bounds__(OW_NT) owlqn_candidate_kernel(
+    const double* __restrict__ U, const double* __restrict__ D, const double* __restrict__ xi,
+    const double* __restrict__ l1, const double* __restrict__ pg, const double* __restrict__ alpha, int d1, int P,
+    double* __restrict__ cand, double* __restrict__ l1t_out, double* __restrict__ dd_out) {
+  __shared__ double sh[4];
+  const int p = blockIdx.x;
+  const double a = alpha[p];
+  double l1t = 0.0, dd = 0.0;
+  for (int i = threadIdx.x; i < d1; i += OW_NT) {
+    const int64_t e = (int64_t)i * P + p;
+    const double u = U[e], l = l1[e];
+    double c = u + a * D[e];
+    if (l > 0.0 && ow_sign(c) != xi[e]) c = 0.0;
+    cand[e] = c;
+    l1t += l * fabs(c);
+    dd += pg[e] * (c - u);
+  }
+  l1t = ow_block_sum(l1t, sh);
+  dd = ow_block_sum(dd, sh);
+  if (threadIdx.x == 0) {
+    l1t_out[p] = l1t;
+    dd_out[p] = dd;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -504,6 +532,15 @@ int tmog_hip_owlqn_direction(const double* U, const double* g, const double* l1,
   if (d1 > OW_NT * OW_QMAX || m < 1 || m > OW_MMAX || hist_n < 0) return -2;
   hipLaunchKernelGGL(owlqn_direction_kernel, dim3(P), dim3(OW_NT), 0, stream, U, g, l1, S, Y, RHO, d1, P, m, hist_n,
                      D, pg, xi, dnorm);
+  return (int)hipGetLastError();
+}
+
+int tmog_hip_owlqn_candidate(const double* U, const double* D, const double* xi, const double* l1, const double* pg,
+                             const double* alpha, int d1, int P, double* cand, double* l1t, double* dd,
+                             hipStream_t stream) {
+  if (P < 1 || d1 < 1) return 0;
+  hipLaunchKernelGGL(owlqn_candidate_kernel, dim3(P), dim3(OW_NT), 0, stream, U, D, xi, l1, pg, alpha, d1, P, cand,
+                     l1t, dd);
   return (int)hipGetLastError();
 }
 

@@ -139,3 +139,18 @@ def owlqn_direction(U, g, l1, S, Y, RHO, hist_n: int, m: int):
         N_.ptr(D), N_.ptr(pg), N_.ptr(xi), N_.ptr(dnorm), N_.stream(U.device)), "owlqn_direction")
     return D, pg, xi, dnorm
 
+
+def owlqn_candidate(U, D, xi, l1, pg, alpha):
+    """OWL-QN line-search candidate ``cand = project_xi(U + alpha D)`` with ``sum l1 |cand|`` and
+    ``sum pg (cand - U)`` per column, one HIP launch (``owlqn_candidate_kernel``). All fp64, contiguous."""
+    from . import _native as N_
+    d1, P = U.shape
+    cand = torch.empty_like(U)
+    l1t = torch.empty(P, dtype=torch.float64, device=U.device)
+    dd = torch.empty_like(l1t)
+    a = alpha.to(torch.float64).contiguous()
+    N_.check(N_.hip().tmog_hip_owlqn_candidate(
+        N_.ptr(U), N_.ptr(D), N_.ptr(xi), N_.ptr(l1), N_.ptr(pg), N_.ptr(a), int(d1), int(P), N_.ptr(cand),
+        N_.ptr(l1t), N_.ptr(dd), N_.stream(U.device)), "owlqn_candidate")
+    return cand, l1t, dd
+
