@@ -69,12 +69,13 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
     fp = torch.empty(nblk, _LR_PC, dtype=torch.float64, device=dev)
     rp = torch.empty_like(fp)
     gp = torch.empty(nblk, dpad, _LR_PC, dtype=torch.float32, device=dev) if grad else fp
+    single = P <= _LR_PC
     for c0 in range(0, P, _LR_PC):
         pc = min(_LR_PC, P - c0)
-        Vc = torch.zeros(d, _LR_PC, dtype=torch.float32, device=dev)
-        Vc[:, :pc] = V[:, c0:c0 + pc]
-        bc = torch.zeros(_LR_PC, dtype=torch.float32, device=dev)
-        bc[:pc] = bias[c0:c0 + pc]
+        # zero-padded to the kernel's 32 problem columns in one launch each (the optimiser calls this ~300
+        # times per learner: allocation + slice-assign pairs were a visible share of its launch overhead)
+        Vc = torch.nn.functional.pad(V[:, c0:c0 + pc].to(torch.float32), (0, _LR_PC - pc)).contiguous()
+        bc = torch.nn.functional.pad(bias[c0:c0 + pc].to(torch.float32), (0, _LR_PC - pc)).contiguous()
         ys = None
         if yscale is not None:
             ys = torch.ones(_LR_PC, dtype=torch.float32, device=dev)
@@ -90,10 +91,15 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
                 N_.ptr(X), N, d, N_.ptr(M), N_.ptr(yf), N_.ptr(Wf), P, c0, pc, N_.ptr(bc), LOSS_CODES[loss],
                 N_.ptr(ys), int(grad), N_.ptr(fp), N_.ptr(rp), N_.ptr(gp) if grad else None, nblk, N_.stream(dev)),
                 "lr_epilogue_grad")
+        if single:
+            f, r = fp[:, :pc].sum(0), rp[:, :pc].sum(0)
+            if grad:
+                G = gp[:, :d, :pc].sum(0, dtype=torch.float64)
+            break
         f[c0:c0 + pc] = fp[:, :pc].sum(0)
         r[c0:c0 + pc] = rp[:, :pc].sum(0)
         if grad:
-            G[:, c0:c0 + pc] = gp[:, :d, :pc].to(torch.float64).sum(0)
+            G[:, c0:c0 + pc] = gp[:, :d, :pc].sum(0, dtype=torch.float64)
     return f, r, G
 
 
