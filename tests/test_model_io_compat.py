@@ -1,0 +1,210 @@
+"""Checkpoint read fidelity.
+
+* A model saved in one process loads and scores in a *fresh* Python process (the reference's serve
+  story: ``OpWorkflowModel.load`` in a new JVM, then ``scoreFunction``,
+  ``local/.../OpWorkflowModelLocal.scala:79-122``).
+* The reference's own old-version checkpoints (``core/src/test/resources/OldModelVersion*``, written by
+  the Scala writer with ``com.salesforce.op.*`` classes and ``AnyValue`` ctorArgs) load with and without
+  a workflow, as ``OpWorkflowModelReaderWriterTest.scala:323-341`` does, and score the reference's
+  ``test-data/PassengerData.avro`` rows (snappy-coded avro).
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from transmogrifai_amd import register_function, uid
+from transmogrifai_amd.features import types as T
+from transmogrifai_amd.features.builder import FeatureBuilder
+from transmogrifai_amd.readers.avro import read_avro
+from transmogrifai_amd.workflow.workflow import OpWorkflow, OpWorkflowModel
+
+REF = "/root/reference/core/src/test/resources"
+PASSENGERS = "/root/reference/test-data/PassengerData.avro"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DAY_MS = 86400000
+
+pytestmark = pytest.mark.skipif(not os.path.isdir(REF), reason="reference fixtures not mounted")
+
+# Python twins of PassengerFeaturesTest.scala:65-110 extract functions, registered under the Scala class
+# names the checkpoints hold
+_PT = "com.salesforce.op.test.PassengerFeaturesTest$"
+EXTRACTS = {
+    "AgeExtract": lambda p: p.get("age"),
+    "GenderAsMultiPickListExtract": lambda p: {p["gender"]} if p.get("gender") is not None else set(),
+    "HeightToRealNNExtract": lambda p: float(p["height"]) if p.get("height") is not None else 0.0,
+    "WeightToRealExtract": lambda p: p.get("weight"),
+    "DescriptionExtract": lambda p: p.get("description"),
+    "BoardedToDateListExtract": lambda p: [int(p["boarded"])],
+    "SurvivedExtract": lambda p: None if p.get("survived") is None else p["survived"] == 1,
+    "StringMapExtract": lambda p: p.get("stringMap") or {},
+    "NumericMapExtract": lambda p: p.get("numericMap") or {},
+    "BooleanMapExtract": lambda p: p.get("booleanMap") or {},
+}
+for _n, _f in EXTRACTS.items():
+    register_function(_f, name=_PT + _n)
+
+
+def cat_head(v):
+    """``OpWorkflowModelReaderWriterTest.CatHeadFn``: first element of the vector."""
+    return float(v[0]) if v is not None and len(v) else None
+
+
+register_function(cat_head, name="com.salesforce.op.OpWorkflowModelReaderWriterTest$CatHeadFn")
+
+
+def _passengers():
+    return read_avro(PASSENGERS)
+
+
+def test_snappy_avro_reads():
+    recs = _passengers()
+    assert len(recs) == 8
+    assert recs[0]["passengerId"] == 1 and recs[0]["gender"] == "Female" and recs[0]["boarded"] == 1471046200
+
+
+@pytest.mark.parametrize("version", ["OldModelVersion", "OldModelVersion_0_5_1"])
+def test_reference_checkpoint_loads_and_scores(version):
+    m = OpWorkflowModel.load(f"{REF}/{version}")
+    assert [type(s).__name__ for s in m.stages][-2:] == ["VectorsCombinerModel", "MapTransformer"]
+    assert m.blocklist == []
+    (res,) = m.result_features
+    assert res.wtype is T.Real
+    with open(f"{REF}/{version}/op-model.json/part-00000") as f:
+        j = json.load(f)
+    ref_date = next(s for s in j["stages"] if "DateListVectorizer" in s["class"])["paramMap"]["referenceDate"]
+    # pre-0.7 checkpoints hold no generator stages: raw features are read by name from the record
+    rows = [{"age": p["age"], "gender": EXTRACTS["GenderAsMultiPickListExtract"](p),
+             "height": EXTRACTS["HeightToRealNNExtract"](p), "description": p["description"],
+             "boarded": EXTRACTS["BoardedToDateListExtract"](p)} for p in _passengers()]
+    # nor the lambda's function class: without a workflow the result fails loudly ...
+    with pytest.raises(RuntimeError, match="not registered"):
+        m.score_function()(rows[0])
+    # ... while every fitted vectorizer scores: the combined vector starts with the DateList block, whole
+    # days from the latest boarded date to the checkpoint's reference date (DateListVectorizer.scala)
+    from transmogrifai_amd.readers.base import dataset_from_records
+    comb = res.parents[0]
+    scored = m.transform_dataset(dataset_from_records(rows, m.raw_features, "cpu"), [comb])
+    vec = scored[comb.name].values
+    assert vec[:, 0].tolist() == [float((ref_date - int(p["boarded"])) // DAY_MS) for p in _passengers()]
+    assert vec.shape[1] == len(j["stages"][-2]["paramMap"]["outputMetadata"]["vector_columns"])
+    # the row path gives the same vector
+    fstage = next(s for s in m.stages if type(s).__name__ == "VectorsCombinerModel")
+    row = {}
+    for st in m.stages[:-1]:
+        row[st.get_output_feature_name()] = st.transform_key_value(lambda k: row.get(k, rows[0].get(k)))
+    assert list(row[fstage.get_output_feature_name()]) == vec[0].tolist()
+
+
+def test_reference_checkpoint_0_7_1_blocklist_and_stages():
+    m = OpWorkflowModel.load(f"{REF}/OldModelVersion_0_7_1")
+    # OpWorkflowModelReaderWriterTest.scala:336-341
+    assert m.blocklist and m.blocklist_map_keys
+    assert [f.name for f in m.blocklist] == ["age"]
+    assert m.blocklist_map_keys == {"numericMap": ["gender"]}
+    assert m.result_features == []          # the checkpoint names a result it does not hold
+    # its fitted stages still transform the raw features
+    from transmogrifai_amd.readers.base import dataset_from_records
+    recs = _passengers()
+    ds = dataset_from_records(recs, m.raw_features, "cpu")
+    by_name = {type(s).__name__: s for s in m.stages}
+    surv = by_name["BinaryVectorizer"].transform(ds)[by_name["BinaryVectorizer"].get_output_feature_name()]
+    assert surv.values[:, 0].tolist() == [float(p["survived"] == 1) for p in recs]
+    h = by_name["RealNNVectorizer"].transform(ds)[by_name["RealNNVectorizer"].get_output_feature_name()]
+    assert h.values[:, 0].tolist() == [float(p["height"]) for p in recs]
+
+
+def _passenger_workflow():
+    """The reference test's raw features declared in ``PassengerFeaturesTest`` order (same uids), with the
+    lambda stage carrying the user function under the checkpoint's uid."""
+    from transmogrifai_amd.features.aggregators import MaxNumeric
+    from transmogrifai_amd.stages.feature.misc_stages import MapTransformer
+    from transmogrifai_amd.dsl import transmogrify
+    uid.reset(0)
+    fb = FeatureBuilder
+    age = fb.Real("age").extract(EXTRACTS["AgeExtract"]).aggregate(MaxNumeric()).as_predictor()
+    gender = fb.MultiPickList("gender").extract(EXTRACTS["GenderAsMultiPickListExtract"]).as_predictor()
+    fb.PickList("genderPL").extract(lambda p: p.get("gender")).as_predictor()
+    height = fb.RealNN("height").extract(EXTRACTS["HeightToRealNNExtract"]).window(300).as_predictor()
+    fb.Real("heightNoWindow").extract(lambda p: p.get("height")).as_predictor()
+    fb.Real("weight").extract(EXTRACTS["WeightToRealExtract"]).as_predictor()
+    description = fb.Text("description").extract(EXTRACTS["DescriptionExtract"]).as_predictor()
+    boarded = fb.DateList("boarded").extract(EXTRACTS["BoardedToDateListExtract"]).as_predictor()
+    assert (age.uid, gender.uid, height.uid, description.uid, boarded.uid) == (
+        "Real_000000000001", "MultiPickList_000000000002", "RealNN_000000000004", "Text_000000000007",
+        "DateList_000000000008")
+    vec = transmogrify([gender, boarded, height, age, description])
+    head = MapTransformer(cat_head, T.Real, uid="UnaryLambdaTransformer_000000000007").set_input(vec).get_output()
+    return OpWorkflow().set_result_features(head)
+
+
+def test_workflow_assisted_load_of_reference_checkpoint():
+    wf = _passenger_workflow()
+    recs = _passengers()
+    wf.set_input_dataset(recs)
+    m = wf.load_model(f"{REF}/OldModelVersion")
+    # raw features (and their extract functions) come from the workflow
+    wf_raw = {f.uid: f for f in wf.raw_features}
+    for f in m.raw_features:
+        if f.uid in wf_raw:
+            assert f.origin_stage is wf_raw[f.uid].origin_stage
+    (res,) = m.result_features
+    scored = m.score()
+    with open(f"{REF}/OldModelVersion/op-model.json/part-00000") as f:
+        j = json.load(f)
+    ref_date = next(s for s in j["stages"] if "DateListVectorizer" in s["class"])["paramMap"]["referenceDate"]
+    assert scored[res.name].to_list() == [float((ref_date - int(p["boarded"])) // DAY_MS) for p in recs]
+
+
+_FRESH = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+from transmogrifai_amd.workflow.workflow import OpWorkflowModel
+m = OpWorkflowModel.load({path!r})
+fn = m.score_function()
+rows = json.loads({rows!r})
+res = {res!r}
+assert res in [f.name for f in m.result_features]
+print(json.dumps([fn(r)[res] for r in rows]))
+"""
+
+
+def test_fresh_process_load_and_score(tmp_path):
+    """Train + save here, load + score in a new interpreter that imported nothing but the model class."""
+    import numpy as np
+    import pandas as pd
+    from transmogrifai_amd.dsl import transmogrify
+    from transmogrifai_amd.selector.factories import BinaryClassificationModelSelector
+    rng = np.random.default_rng(0)
+    n = 400
+    df = pd.DataFrame({"x1": rng.normal(size=n), "x2": rng.normal(size=n),
+                       "cat": rng.choice(["a", "b", "c"], size=n)})
+    df["y"] = ((df.x1 + (df.cat == "a") * 1.5 + rng.normal(scale=0.5, size=n)) > 0.5).astype(float)
+    df.loc[::7, "x2"] = None
+    uid.reset(0)
+    y = FeatureBuilder.RealNN("y").as_response()
+    x1, x2 = FeatureBuilder.Real("x1").as_predictor(), FeatureBuilder.Real("x2").as_predictor()
+    cat = FeatureBuilder.PickList("cat").as_predictor()
+    vec = transmogrify([x1, x2, cat])
+    pred = BinaryClassificationModelSelector.with_train_validation_split(
+        model_types_to_use=["OpLogisticRegression"], seed=3).set_input(y, vec).get_output()
+    model = OpWorkflow().set_result_features(y, pred).set_input_dataset(df).train()
+    path = str(tmp_path / "m")
+    model.save(path)
+    rows = [{"x1": float(r.x1), "x2": None if r.x2 != r.x2 else float(r.x2), "cat": r.cat}
+            for r in df.head(20).itertuples()]
+    expect = [model.score_function()(r)[pred.name] for r in rows]
+    code = _FRESH.format(root=ROOT, path=path, rows=json.dumps(rows), res=pred.name)
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    got = json.loads(out.stdout.strip().splitlines()[-1])
+    assert len(got) == len(expect)
+    for g, e in zip(got, expect):
+        assert g["prediction"] == e["prediction"]
+        for k in e:
+            assert abs(g[k] - e[k]) < 1e-6

@@ -107,7 +107,8 @@ class OpVectorColumnMetadata:
     @staticmethod
     def from_json(d) -> List["OpVectorColumnMetadata"]:
         base = OpVectorColumnMetadata(
-            tuple(d["parent_feature"]), tuple(d["parent_feature_type"]), d.get("grouping"),
+            tuple(d["parent_feature"]), tuple(d["parent_feature_type"]),
+            d.get("grouping", d.get("indicator_group")),     # pre-0.5 checkpoints: indicator_group
             d.get("indicator_value"), d.get("descriptor_value"), 0)
         return [base.with_index(int(i)) for i in d.get("indices", [0])]
 

@@ -116,6 +116,58 @@ def _decode(r: _Reader, schema, names) -> Any:
     raise ValueError(f"unsupported avro type {t}")
 
 
+def snappy_decompress(buf: bytes) -> bytes:
+    """Raw snappy format: a varint uncompressed length, then literal / back-reference elements whose tag
+    byte's low 2 bits select literal (0) or copy with a 1- (1), 2- (2) or 4-byte (3) offset."""
+    n, shift, i = 0, 0, 0
+    while True:
+        b = buf[i]
+        i += 1
+        n |= (b & 0x7F) << shift
+        shift += 7
+        if b < 0x80:
+            break
+    out = bytearray()
+    end = len(buf)
+    while i < end:
+        tag = buf[i]
+        i += 1
+        kind = tag & 3
+        if kind == 0:
+            ln = tag >> 2
+            if ln >= 60:
+                nb = ln - 59
+                ln = int.from_bytes(buf[i:i + nb], "little")
+                i += nb
+            ln += 1
+            out += buf[i:i + ln]
+            i += ln
+            continue
+        if kind == 1:
+            ln = ((tag >> 2) & 7) + 4
+            off = ((tag >> 5) << 8) | buf[i]
+            i += 1
+        elif kind == 2:
+            ln = (tag >> 2) + 1
+            off = int.from_bytes(buf[i:i + 2], "little")
+            i += 2
+        else:
+            ln = (tag >> 2) + 1
+            off = int.from_bytes(buf[i:i + 4], "little")
+            i += 4
+        if off == 0 or off > len(out):
+            raise ValueError("corrupt snappy stream (bad back-reference)")
+        start = len(out) - off
+        if off >= ln:
+            out += out[start:start + ln]
+        else:                       # overlapping copy: repeat the last `off` bytes
+            for k in range(ln):
+                out.append(out[start + k])
+    if len(out) != n:
+        raise ValueError(f"corrupt snappy stream ({len(out)} bytes, header says {n})")
+    return bytes(out)
+
+
 def read_avro_file(path: str) -> Iterator[Dict[str, Any]]:
     with open(path, "rb") as f:
         data = f.read()
@@ -134,6 +186,11 @@ def read_avro_file(path: str) -> Iterator[Dict[str, Any]]:
         block = r.read(size)
         if codec == "deflate":
             block = zlib.decompress(block, -15)
+        elif codec == "snappy":      # raw snappy block + big-endian CRC32 of the uncompressed bytes
+            body, crc = block[:-4], int.from_bytes(block[-4:], "big")
+            block = snappy_decompress(body)
+            if zlib.crc32(block) & 0xFFFFFFFF != crc:
+                raise ValueError(f"{path}: snappy block CRC mismatch")
         elif codec != "null":
             raise ValueError(f"unsupported avro codec {codec}")
         br = _Reader(block)

@@ -33,8 +33,44 @@ def register_stage(cls):
     return cls
 
 
+# every module of this package that defines checkpoint-loadable stages: a fresh process that loads a
+# model imports them on the first lookup miss (the registry is filled by the @register_stage decorators)
+_STAGE_MODULES = (
+    "transmogrifai_amd.stages.generator", "transmogrifai_amd.stages.feature.vectorizers",
+    "transmogrifai_amd.stages.feature.bucketizers", "transmogrifai_amd.stages.feature.indexers",
+    "transmogrifai_amd.stages.feature.maps", "transmogrifai_amd.stages.feature.math_stages",
+    "transmogrifai_amd.stages.feature.misc_stages", "transmogrifai_amd.stages.feature.nlp_stages",
+    "transmogrifai_amd.stages.feature.text_stages", "transmogrifai_amd.stages.feature.vector_stages",
+    "transmogrifai_amd.stages.insights.record_insights", "transmogrifai_amd.stages.preparators.min_variance",
+    "transmogrifai_amd.stages.preparators.sanity_checker", "transmogrifai_amd.models.base",
+    "transmogrifai_amd.models.linear", "transmogrifai_amd.models.glm", "transmogrifai_amd.models.mlp",
+    "transmogrifai_amd.models.trees", "transmogrifai_amd.selector.model_selector",
+    "transmogrifai_amd.selector.extras",
+)
+_ALL_IMPORTED = False
+
+
+def import_stage_modules() -> None:
+    """Import every stage-defining module of this package (a fixed list: checkpoint contents never
+    choose what is imported)."""
+    global _ALL_IMPORTED
+    if _ALL_IMPORTED:
+        return
+    import importlib
+    for m in _STAGE_MODULES:
+        importlib.import_module(m)
+    _ALL_IMPORTED = True
+
+
+def _lookup(name: str) -> Optional[type]:
+    return _STAGE_REGISTRY.get(name) or _STAGE_REGISTRY.get(name.rsplit(".", 1)[-1].rstrip("$"))
+
+
 def stage_class(name: str) -> type:
-    cls = _STAGE_REGISTRY.get(name) or _STAGE_REGISTRY.get(name.rsplit(".", 1)[-1])
+    cls = _lookup(name)
+    if cls is None:
+        import_stage_modules()
+        cls = _lookup(name)
     if cls is None:
         raise ValueError(f"Unknown stage class '{name}'")
     return cls

@@ -23,7 +23,7 @@ from ...data.columns import NumericColumn, ObjectColumn, TextColumn, column_from
 from ...features import types as T
 from ...utils.text import clean_string, email_domain, url_domain
 from ..base import BinaryTransformer, UnaryEstimator, UnaryTransformer, register_stage
-from ..generator import _fn_name, load_extract_fn
+from ..generator import _fn_name, load_extract_fn, require_function
 
 
 def _v(x):
@@ -438,4 +438,4 @@ class MapTransformer(_FnStage):
             self.operation_name = operation_name
 
     def transform_fn(self, v):
-        return self.fn(v)
+        return require_function(self.fn, f"transform function of {self.uid}")(v)

@@ -142,15 +142,26 @@ def _read_text(path: str) -> str:
 
 
 def _build_stage(sj: Dict) -> OpPipelineStage:
+    from . import reference_compat as RC
+    pm = sj.get("paramMap", {}) or {}
+    is_ref = RC.is_reference_class(sj["class"])
+    if is_ref and RC.simple_name(sj["class"]) != "FeatureGeneratorStage":
+        st = RC.build_reference_stage(sj)
+        st.uid = sj["uid"]
+        st.metadata = _meta_from_json(RC.any_value(pm.get("outputMetadata")) or {}, pm.get("outputFeatureName"))
+        st._output_name = pm.get("outputFeatureName")
+        return st
     cls = stage_class(sj["class"])
-    pm = sj.get("paramMap", {})
-    args = decode(sj.get("ctorArgs", {}))
+    args = decode(RC.decode_ctor_args(sj.get("ctorArgs")) if is_ref else sj.get("ctorArgs", {}))
     if cls is FeatureGeneratorStage:
         from ..features.aggregators import aggregator_from_json, default_aggregator
         from ..stages.generator import load_extract_fn
         ef = args.get("extractFn") or {}
         tto = T.feature_type_from_name(args.get("tto", sj.get("outputType", "Text")))
-        agg = aggregator_from_json(args.get("aggregator")) or default_aggregator(tto)
+        agg_j = args.get("aggregator")
+        if isinstance(agg_j, dict) and is_ref:     # com.salesforce.op.aggregators.SumReal$ -> SumReal
+            agg_j = {"className": RC.simple_name(agg_j.get("className", ""))}
+        agg = aggregator_from_json(agg_j) or default_aggregator(tto)
         st = FeatureGeneratorStage(args.get("outputName") or pm.get("outputFeatureName"), tto,
                                    load_extract_fn(ef.get("className")), agg, args.get("aggregateWindow"),
                                    bool(args.get("outputIsResponse")), args.get("extractSource"), uid=sj["uid"],
@@ -178,56 +189,122 @@ def _build_stage(sj: Dict) -> OpPipelineStage:
     return st
 
 
-def load_model(path: str, workflow=None):
-    from .workflow import OpWorkflowModel
-    j = json.loads(_read_text(path))
-    stages_j = j["stages"]
-    by_uid: Dict[str, OpPipelineStage] = {}
-    order: List[OpPipelineStage] = []
-    for sj in stages_j:
-        st = _build_stage(sj)
-        by_uid[st.uid] = st
-        order.append(st)
-    # features
-    fjs = {f["uid"]: f for f in j["allFeatures"]}
+def _resolve_features(fjs: List[Dict], by_uid: Dict[str, OpPipelineStage],
+                      known: Optional[Dict[str, FeatureLike]] = None) -> Dict[str, FeatureLike]:
+    """Features from their JSON (``FeatureJsonHelper.fromJson``), parents first; ``known`` features (of the
+    workflow) are reused by uid."""
+    fmap = {f["uid"]: f for f in fjs}
     built: Dict[str, FeatureLike] = {}
 
     def build(uid):
         if uid in built:
             return built[uid]
-        fj = fjs[uid]
+        if known and uid in known and known[uid].is_raw:
+            built[uid] = known[uid]
+            return built[uid]
+        fj = fmap[uid]
         parents = [build(p) for p in fj.get("parents", [])]
         st = by_uid.get(fj.get("originStage"))
-        f = FeatureLike(fj["name"], T.feature_type_from_name(fj["typeName"]), fj.get("isResponse", False), st,
-                        parents, uid=fj["uid"])
+        ftype = T.feature_type_from_name(fj["typeName"])
+        if st is None and not parents and fj.get("originStage"):
+            # pre-0.7 checkpoints hold no generator stages: the raw feature reads the column of its name
+            from ..features.aggregators import default_aggregator
+            st = FeatureGeneratorStage(fj["name"], ftype, None, default_aggregator(ftype), None,
+                                       bool(fj.get("isResponse")), uid=fj["originStage"])
+            by_uid[st.uid] = st
+        if st is not None and not isinstance(st, FeatureGeneratorStage):
+            st.output_type = ftype
+        f = FeatureLike(fj["name"], ftype, fj.get("isResponse", False), st, parents, uid=fj["uid"])
         built[uid] = f
         return f
 
-    for u in fjs:
+    for u in fmap:
         build(u)
-    # wire stage inputs / outputs
+    return built
+
+
+def _wire(stages_j: List[Dict], by_uid: Dict[str, OpPipelineStage], built: Dict[str, FeatureLike]) -> None:
+    """Set every stage's inputs (by the uids its JSON names) and output feature."""
     for sj in stages_j:
         st = by_uid[sj["uid"]]
-        ins = sj.get("paramMap", {}).get("inputFeatures", [])
+        ins = (sj.get("paramMap", {}) or {}).get("inputFeatures", [])
         if ins:
             st._inputs = [built[t["uid"]] for t in ins]
             st._transient = [TransientFeature.from_json(t) for t in ins]
         out = next((f for f in built.values() if f.origin_stage is st), None)
         if out is not None:
             st._output = out
-    gens = [s for s in order if isinstance(s, FeatureGeneratorStage)]
+
+
+def load_model(path: str, workflow=None):
+    """``OpWorkflowModelReader.loadJson`` (``OpWorkflowModelReader.scala:97-233``).
+
+    Without a workflow every stage is rebuilt from the checkpoint (including ``com.salesforce.op.*``
+    stages of reference-written checkpoints, :mod:`reference_compat`). With a workflow, its raw features
+    (and their extract functions) replace the checkpoint's generator stages, and stages of the workflow
+    with the same uid lend what a checkpoint cannot carry (user functions of lambda stages). Result
+    features the checkpoint names but does not hold are dropped, as the reference does; blocklisted
+    features resolve against the checkpoint's blocklisted stages and the workflow's features."""
+    from ..stages.base import import_stage_modules
+    from .workflow import OpWorkflowModel
+    import_stage_modules()
+    j = json.loads(_read_text(path))
+    stages_j = j["stages"]
+    wf_gens: Dict[str, OpPipelineStage] = {}
+    wf_stages: Dict[str, OpPipelineStage] = {}
+    wf_feats: Dict[str, FeatureLike] = {}
+    if workflow is not None:
+        for r in list(workflow.raw_features) + list(getattr(workflow, "blocklist", [])):
+            for x in (r.raw_features() if not r.is_raw else [r]):
+                wf_gens[x.origin_stage.uid] = x.origin_stage
+        wf_stages = {s.uid: s for s in workflow.stages}
+        for f in list(workflow.result_features) + list(getattr(workflow, "blocklist", [])):
+            for x in f.traverse():
+                wf_feats[x.uid] = x
+    by_uid: Dict[str, OpPipelineStage] = {}
+    order: List[OpPipelineStage] = []
+    for sj in stages_j:
+        st = wf_gens.get(sj["uid"]) or _build_stage(sj)
+        orig = wf_stages.get(sj["uid"])
+        if orig is not None and getattr(st, "fn", 0) is None and getattr(orig, "fn", None) is not None:
+            st.fn = orig.fn
+        by_uid[st.uid] = st
+        order.append(st)
+    built = _resolve_features(j["allFeatures"], by_uid, wf_feats)
+    _wire(stages_j, by_uid, built)
     fitted = [s for s in order if not isinstance(s, FeatureGeneratorStage)]
     model = OpWorkflowModel(j.get("uid"), OpParams.from_string(j.get("parameters", "{}")))
     model.train_parameters = OpParams.from_string(j.get("trainParameters", "{}"))
     model.stages = fitted
-    model.result_features = [built[u] for u in j["resultFeaturesUids"]]
-    model.raw_features = sorted([built[f.uid] for f in built.values() if f.is_raw and f.origin_stage in gens],
+    model.result_features = [built[u] for u in j["resultFeaturesUids"] if u in built]
+    model.raw_features = sorted([f for f in built.values() if f.is_raw and isinstance(f.origin_stage,
+                                                                                      FeatureGeneratorStage)],
                                 key=lambda f: f.name)
-    bl = j.get("blocklistedFeaturesUids", j.get("blacklistedFeaturesUids", []))
-    model.blocklist = [built[u] for u in bl if u in built]
-    model.blocklist_map_keys = j.get("blocklistedMapKeys", j.get("blacklistedMapKeys", {}))
+    # blocklist (OpWorkflowModelReader.resolveBlocklist): the longer of the new / legacy field lists
+    bl_feats: Dict[str, FeatureLike] = dict(wf_feats)
+    for key in ("blocklistedStages", "blacklistedStages"):
+        bst = j.get(key) or []
+        if bst:
+            extra = {}
+            for sj in bst:
+                st = wf_gens.get(sj["uid"]) or _build_stage(sj)
+                extra[st.uid] = st
+            for st in extra.values():
+                if isinstance(st, FeatureGeneratorStage):     # blocklisted raw features
+                    f = st.get_output()
+                    bl_feats.setdefault(f.uid, f)
+    bl_feats.update(built)
+    lists = [j.get("blocklistedFeaturesUids") or [], j.get("blacklistedFeaturesUids") or []]
+    bl = max(([bl_feats[u] for u in ids if u in bl_feats] for ids in lists), key=len)
+    model.blocklist = bl
+    keys = {}
+    for key in ("blocklistedMapKeys", "blacklistedMapKeys"):
+        for k, v in (j.get(key) or {}).items():
+            keys[k] = sorted(set(keys.get(k, [])) | set(v))
+    model.blocklist_map_keys = keys
     rff = j.get("rawFeatureFilterResults")
-    model.raw_feature_filter_results = decode(json.loads(rff)) if isinstance(rff, str) and rff else rff
+    model.raw_feature_filter_results = decode(json.loads(rff)) if isinstance(rff, str) and rff else (rff or
+                                                                                                     _EMPTY_RFF)
     model.train_timings = decode(j.get("trainTimings", {}))
     if workflow is not None:
         model.reader = workflow.reader
