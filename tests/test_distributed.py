@@ -138,13 +138,15 @@ def _aggregate_shuffle(rank, world):
     assert [g.decode() for g in got] == [f"{k}->{rank}" for k in range(world)]
     amt = FeatureBuilder.Real("amt").extract(lambda e: e["amt"]).aggregate(A.SumNumeric()).as_predictor()
     cat = FeatureBuilder.PickList("cat").extract(lambda e: e["cat"]).as_predictor()
+    txt = FeatureBuilder.Text("txt").extract(lambda e: e["cat"] + str(e["t"] % 7)).aggregate(A.ConcatText()) \
+        .as_predictor()
     rd = DataReaders.Aggregate.custom(_events_records(), key=lambda e: e["k"],
                                       aggregate_params=AggregateParams(lambda e: e["t"],
                                                                        A.CutOffTime.unix_epoch(6000)))
-    ds = rd.distribute().generate_dataset([amt, cat])
+    ds = rd.distribute().generate_dataset([amt, cat, txt])
     assert ds.sharded
     return {"keys": [str(k) for k in ds.key], "amt": ds["amt"].to_list(), "cat": ds["cat"].to_list(),
-            "rid": ds.row_ids.tolist()}
+            "txt": ds["txt"].to_list(), "rid": ds.row_ids.tolist()}
 
 
 def test_keyed_shuffle_aggregate_reader_matches_single_process(tmp_path):
@@ -157,19 +159,23 @@ def test_keyed_shuffle_aggregate_reader_matches_single_process(tmp_path):
     res = _run("_aggregate_shuffle", tmp_path)
     amt = FeatureBuilder.Real("amt").extract(lambda e: e["amt"]).aggregate(A.SumNumeric()).as_predictor()
     cat = FeatureBuilder.PickList("cat").extract(lambda e: e["cat"]).as_predictor()
+    txt = FeatureBuilder.Text("txt").extract(lambda e: e["cat"] + str(e["t"] % 7)).aggregate(A.ConcatText()) \
+        .as_predictor()
     ref = DataReaders.Aggregate.custom(_events_records(), key=lambda e: e["k"],
                                        aggregate_params=AggregateParams(lambda e: e["t"],
                                                                         A.CutOffTime.unix_epoch(6000))) \
-        .generate_dataset([amt, cat])
-    want = {str(k): (a, c) for k, a, c in zip(ref.key, ref["amt"].to_list(), ref["cat"].to_list())}
+        .generate_dataset([amt, cat, txt])
+    want = {str(k): (a, c, t) for k, a, c, t in zip(ref.key, ref["amt"].to_list(), ref["cat"].to_list(),
+                                                    ref["txt"].to_list())}
     got = {}
     for r in res:
-        for k, a, c in zip(r["keys"], r["amt"], r["cat"]):
+        for k, a, c, t in zip(r["keys"], r["amt"], r["cat"], r["txt"]):
             assert k not in got               # every key aggregated on exactly one rank
-            got[k] = (a, c)
+            got[k] = (a, c, t)
     assert set(got) == set(want)
     for k in want:
         assert got[k][1] == want[k][1]
+        assert got[k][2] == want[k][2]        # order-dependent concatenation in source order
         assert (got[k][0] is None and want[k][0] is None) or abs(got[k][0] - want[k][0]) < 1e-9
     rids = sorted(i for r in res for i in r["rid"])
     assert rids == list(range(len(want)))

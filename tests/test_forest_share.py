@@ -107,6 +107,42 @@ def test_forest_predict_multi_kernel_matches_pruned_forests():
 
 
 @pytest.mark.gpu
+def test_forest_predict_multi_regression_32_variants():
+    """K = 1 (regression) with 32 variants: the kernel's all-variants mask must not be the undefined
+    ``1u << 32`` (that silently zeroed every prediction)."""
+    X, y = _data(N=3000, F=10)
+    rows = torch.arange(X.shape[0])
+    jobs = [te.TreeJob(0, te.TreeParams(max_depth=8, min_instances=3, min_info_gain=0.0), rows) for _ in range(3)]
+    t1 = (y + 0.1 * X[:, 2].float())[None, :].contiguous()
+    deep = te.grow_forest(X, np.full(X.shape[1], 32), jobs, mode=te.MODE_VAR, kind=te.KIND_VARIANCE, t1=t1, B=32)
+    assert deep.K == 1
+    Xc = X.cuda()
+    rr = torch.arange(0, 3000, 2, device="cuda")
+    vs = [(d, g) for d in (1, 2, 3, 4, 5, 6, 7, 8) for g in (0.0, 1e-4, 1e-3, 1e-2)]
+    assert len(vs) == 32
+    got = te.forest_predict_multi(deep, Xc, [rr], [[0, 1, 2]], [vs])[0]
+    for (d, g), o in zip(vs, got):
+        want = te.forest_predict(te.prune_forest(deep, d, g), Xc, [rr], [[0, 1, 2]])[0]
+        torch.testing.assert_close(o, want, rtol=1e-5, atol=1e-6)
+    assert float(got[-1].abs().sum()) > 0
+
+
+@pytest.mark.gpu
+def test_forest_predict_multi_wide_matrix_falls_back():
+    """More than ~2000 columns do not fit 64 staged rows in LDS: the shared walk falls back to predicting
+    each pruned forest instead of failing the RF batch."""
+    X, y = _data(N=600, F=2600)
+    deep = _grow(X, y, 6, 0.0005, n_trees=2)
+    assert te._pm_lds_bytes(2600) > te._lds_limit(None)
+    Xc = X.cuda()
+    vs = [(6, 0.0005), (3, 0.0005)]
+    got = te.forest_predict_multi(deep, Xc, [None], [[0, 1]], [vs])[0]
+    for (d, g), o in zip(vs, got):
+        want = te.forest_predict(te.prune_forest(deep, d, g), Xc, [None], [[0, 1]])[0]
+        torch.testing.assert_close(o, want, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
 def test_partition_from_feature_major_copy_identical():
     """Newton growth on the GPU with the partition reading split columns from the feature-major copy
     (GrowArgs.XbT) equals growth reading the row-major matrix."""

@@ -150,3 +150,27 @@ def test_data_splitter_prepare_uses_row_count_only(monkeypatch):
     monkeypatch.undo()
     bal = SP.DataBalancer(seed=1)
     assert "className" in MS._splitter_prepare(bal, (torch.rand(4000) < 0.1).double())
+
+
+def test_cv_validates_on_whole_folds_with_downsampled_training(monkeypatch):
+    """OpCrossValidation.scala:122-129: ``validationPrepare`` (the maxTrainingSample down-sampling) applies to
+    each fold's training part only; every row of the held-out fold is scored."""
+    from transmogrifai_amd.evaluators import evaluators as E
+    from transmogrifai_amd.selector.factories import BinaryClassificationModelSelector as BMS
+    seen = []
+    orig = E.OpBinaryClassificationEvaluator.selection_metric
+
+    def spy(self, y, pred, raw, prob):
+        seen.append(int(y.shape[0]))
+        return orig(self, y, pred, raw, prob)
+    monkeypatch.setattr(E.OpBinaryClassificationEvaluator, "selection_metric", spy)
+    n = 3000
+    ds, (y, v) = _data(n=n, seed=4)
+    split = DataSplitter(seed=3, reserve_test_fraction=0.0, max_training_sample=300)
+    sel = BMS.with_cross_validation(splitter=split, num_folds=3, seed=7,
+                                    models_and_parameters=[("OpLogisticRegression", [{"reg_param": 0.01}])])
+    pred = sel.set_input(y, v).get_output()
+    m = OpWorkflow().set_result_features(pred).set_input_dataset(ds).train()
+    summ = m.get_origin_stage_of(pred).metadata["summary"]
+    assert len(seen) == 3 and sum(seen) == n, seen          # the three folds cover every row
+    assert summ["bestModelType"] == "OpLogisticRegression"

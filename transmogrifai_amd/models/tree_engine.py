@@ -730,6 +730,17 @@ def _finalize_py(jobs, G: "_Nodes", mode, kind, K, S, missing_bin, with_gid_valu
 _PM_VK = 32      # tree_kernels.hip forest_predict_multi_kernel: variants x classes per model
 
 
+def _pm_lds_bytes(F: int) -> int:
+    """LDS of one forest_predict_multi_kernel workgroup: 64 staged rows of F bins + 64 x 4 x 32 fp32
+    accumulators (tmog_hip_forest_predict_multi)."""
+    return ((64 * F + 15) & ~15) + 4 * _PM_VK * 64 * 4
+
+
+def _lds_limit(dev) -> int:
+    """LDS one workgroup may allocate (gfx950: 160 KB; the launcher refuses more with -3)."""
+    return 160 * 1024
+
+
 def forest_predict_multi(forest: Forest, Xb: torch.Tensor, model_rows: Sequence[Optional[torch.Tensor]],
                          model_trees: Sequence[Sequence[int]],
                          model_variants: Sequence[Sequence[Tuple[int, float]]]) -> List[List[torch.Tensor]]:
@@ -740,8 +751,10 @@ def forest_predict_multi(forest: Forest, Xb: torch.Tensor, model_rows: Sequence[
     variant is pruned and predicted on its own. Returns ``[model][variant] -> float32 [n_m, K]``."""
     dev = Xb.device
     K = forest.K
+    F = int(Xb.shape[1]) if Xb.dim() == 2 else 0
     if dev.type != "cuda" or K not in (1, 2, 4, 8) or any(len(v) * K > _PM_VK or len(v) > 32
-                                                         for v in model_variants):
+                                                         for v in model_variants) \
+            or _pm_lds_bytes(F) > _lds_limit(dev):
         res = []
         for rows, ts, vs in zip(model_rows, model_trees, model_variants):
             sub = Forest.concat([forest.tree(int(t)) for t in ts])

@@ -61,7 +61,7 @@ def _ctx(X, context):
     if isinstance(context, dict):
         c = context.get("tree")
         if c is None or c.X is not X:
-            c = TreeContext(X)
+            c = TreeContext(X, context.get("tree_rows"))
             context["tree"] = c
         return c
     return TreeContext(X)

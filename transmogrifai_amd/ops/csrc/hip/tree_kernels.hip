@@ -1334,7 +1334,7 @@ __global__ void __launch_bounds__(PM_ROWS * PM_TPR) forest_predict_multi_kernel(
   if (rr < nrow) {
     const uint8_t* xr = srows + rr * F;
     const int64_t t_end = model_tree_off[m + 1];
-    const uint32_t all = (1u << V) - 1u;
+    const uint32_t all = V >= 32 ? 0xFFFFFFFFu : (1u << V) - 1u;     // V == 32: a 32-bit shift by 32 is undefined
     for (int64_t t = model_tree_off[m] + (int64_t)q * PM_TU; t < t_end; t += (int64_t)PM_TU * PM_TPR) {
       const int nu = (int)min((int64_t)PM_TU, t_end - t);
       int64_t k[PM_TU];
@@ -1625,7 +1625,7 @@ int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, 
   return (int)hipGetLastError();
 }
 
-// Shared-forest multi-variant prediction (forest_predict_multi_kernel). Every model's V x K <= 32, V <= 16.
+// Shared-forest multi-variant prediction (forest_predict_multi_kernel). Every model's V x K <= 32 (V <= 32).
 int tmog_hip_forest_predict_multi(const uint8_t* Xb, int F, int n_models, const int64_t* model_row_off,
                                   const int32_t* row_list, int64_t max_rows, const int64_t* model_tree_off,
                                   const int64_t* tree_off, const float* tree_weight, const int32_t* nodes,

@@ -104,7 +104,13 @@ class _GroupedReader(DataReader):
         recs = self._records(params)
         shard = self.distributed and D.world() > 1
         if shard:
-            recs = D.shuffle_by_key(recs[D.rank()::D.world()], lambda r: str(self.key_fn(r)))
+            # records travel with their source index: after the key shuffle they are put back in source
+            # order, so the stable key sort below orders each key's records as one process would (the
+            # order-dependent aggregators -- ConcatText, ConcatList, UnionConcatTextMap -- then agree)
+            mine = [(i, recs[i]) for i in range(D.rank(), len(recs), D.world())]
+            pairs = D.shuffle_by_key(mine, lambda p: str(self.key_fn(p[1])))
+            pairs.sort(key=lambda p: p[0])
+            recs = [r for _, r in pairs]
         dev = self.device or default_device()
         n = len(recs)
         keys = np.asarray([str(self.key_fn(r)) for r in recs], dtype=object)

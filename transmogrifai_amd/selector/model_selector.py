@@ -131,29 +131,32 @@ class ModelSelector(BinaryEstimator):
                 split_summary = self._split_summary
             else:
                 split_summary = _splitter_prepare(self.splitter, y)
-        # only the rows some CV fold or the refit may train on (the splitter's maxTrainingSample cap) are
-        # materialised from the (blocked) feature vector; folds are functions of the global row id
-        X, y, row_ids = self._gather_candidates(vec_col, y, row_ids)
+        # every row is materialised: CV folds validate on their whole held-out fold and only their training
+        # part is down-sampled (OpCrossValidation.scala:122-129 applies validationPrepare to the training
+        # split only); the rows some fold or the refit may train on seed the tree binning sample
+        X, y, row_ids, cand = self._gather_rows(vec_col, y, row_ids)
         if dp.active():
             with dp.local_only():
-                return self._fit(X, y, row_ids, split_summary, t0)
-        return self._fit(X, y, row_ids, split_summary, t0)
+                return self._fit(X, y, row_ids, split_summary, t0, cand)
+        return self._fit(X, y, row_ids, split_summary, t0, cand)
 
-    def _gather_candidates(self, vec_col, y, row_ids):
-        """Every rank's rows that some CV fold or the refit may train on, gathered to all ranks."""
+    def _gather_rows(self, vec_col, y, row_ids):
+        """All rows of every rank (folds are functions of the global row id) and the positions of the rows
+        that some CV fold's or the refit's down-sampled training set may use (``None`` without a
+        splitter)."""
         from ..parallel import dp
+        X, y, row_ids = dp.rows(vec_col.values), dp.rows(y), dp.rows(row_ids)
         if self.splitter is None:
-            return dp.rows(vec_col.values), dp.rows(y), dp.rows(row_ids)
+            return X, y, row_ids, None
         n_folds = getattr(self.validator, "num_folds", 1)
         keep = self.splitter.validation_prepare(row_ids, y, stream=5)
         for k in range(n_folds):
             keep |= self.splitter.validation_prepare(row_ids, y, stream=11 + k)
-        idx = torch.nonzero(keep).reshape(-1)
-        return dp.rows(vec_col.take_rows(idx).contiguous()), dp.rows(y.index_select(0, idx)), \
-            dp.rows(row_ids.index_select(0, idx))
+        return X, y, row_ids, torch.nonzero(keep).reshape(-1)
 
-    def _fit(self, X, y, row_ids, split_summary, t0):
-        ctx: Dict[str, Any] = {}
+    def _fit(self, X, y, row_ids, split_summary, t0, cand=None):
+        # tree learners draw their quantile-binning sample from the training candidates only
+        ctx: Dict[str, Any] = {} if cand is None else {"tree_rows": cand}
         if self.best_estimator is not None:     # chosen by workflow-level CV
             res = self.best_estimator
         else:

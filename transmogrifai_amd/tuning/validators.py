@@ -233,8 +233,10 @@ class OpValidator:
             Xt, yt = train_k[features_name].values, train_k[label_name].values
             Xv, yv = val_k[features_name].values, val_k[label_name].values
             rid_t = train_k.row_ids.to(Xt.device)
+            rid_v = val_k.row_ids.to(Xt.device)
             if dp.active():       # row-sharded: learners train on the fold rows of every rank
-                Xt, yt, rid_t, Xv, yv = dp.rows(Xt), dp.rows(yt), dp.rows(rid_t), dp.rows(Xv), dp.rows(yv)
+                Xt, yt, rid_t, Xv, yv, rid_v = (dp.rows(Xt), dp.rows(yt), dp.rows(rid_t), dp.rows(Xv), dp.rows(yv),
+                                                dp.rows(rid_v))
             X = torch.cat([Xt, Xv.to(Xt.dtype)])
             y = torch.cat([yt, yv]).to(X.dtype)
             nt = int(Xt.shape[0])
@@ -248,7 +250,16 @@ class OpValidator:
                 else:
                     keep = torch.nonzero(splitter.validation_prepare(rid_t, yt.to(X.dtype), stream=11 + k)).reshape(-1)
             train_rows = {0: (keep, weights)}
-            val_rows = {0: torch.arange(nt, int(X.shape[0]), device=X.device)}
+            # applyDAG (OpValidator.scala:266-271) prepares the DAG-transformed validation part with the
+            # splitter too (an up-sampled row counts once per copy)
+            vsel = torch.arange(int(X.shape[0]) - nt, device=X.device)
+            if splitter is not None:
+                yvv = yv.to(X.dtype)
+                if hasattr(splitter, "weights"):
+                    vsel = torch.repeat_interleave(vsel, splitter.weights(rid_v, yvv, stream=41 + k).to(X.device))
+                else:
+                    vsel = torch.nonzero(splitter.validation_prepare(rid_v, yvv, stream=41 + k)).reshape(-1)
+            val_rows = {0: vsel + nt}
             ctx: Dict[str, Any] = {}
             with dp.local_only():
                 for li, (lname, grid) in enumerate(models):
