@@ -101,6 +101,25 @@ def test_feature_parallel_trees_bit_identical(tmp_path):
     assert any(len(f["nodes"]) > 10 for f in ref["xgb"])
 
 
+def _trees_fp_threads(rank, world):
+    """Two job groups grown on two host threads per rank (as the GPU backend does), rank 1's second group
+    delayed 25 ms before every exchange: the exchange turn order (tree_grow.hpp FpTurns) keeps the
+    collectives in one order on every rank."""
+    os.environ["TMOG_CPU_GROUP_THREADS"] = "1"
+    os.environ["TMOG_TREE_GROUPS"] = "2"
+    os.environ["TMOG_FP_DELAY"] = "1:1:25"
+    from transmogrifai_amd.parallel.learner_parallel import LearnerParallel
+    return _trees(LearnerParallel())
+
+
+def test_feature_parallel_concurrent_groups_deterministic_order(tmp_path):
+    ref = _trees(None)
+    outs = _run("_trees_fp_threads", tmp_path, 3)
+    for r, o in enumerate(outs):
+        for k in ("xgb", "gbt", "dt"):
+            assert o[k] == ref[k], f"{k} forest differs on rank {r} with concurrent groups"
+
+
 def _linear(par):
     from transmogrifai_amd.models.base import FitJob, learner_class
     X, y = _data(n=2000, d=12, seed=3)

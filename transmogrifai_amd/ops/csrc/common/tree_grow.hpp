@@ -16,16 +16,77 @@
 #pragma once
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace tmog {
+
+// Deterministic cross-group order of the feature-parallel split exchanges. Every job group grows on its
+// own host thread and issues one all-gather per level on its own communicator; left to the threads'
+// timing, rank A could enqueue (g0 level L, g1 level L) while rank B enqueues (g1, g0) -- collectives of
+// two communicators queued in different orders on different ranks is the classic RCCL/NCCL deadlock once
+// two streams share a hardware queue. The turn passes round-robin over the groups that are still
+// growing: g0 L0, g1 L0, g0 L1, g1 L1, ..., a finished group drops out. Each group's exchange count is
+// identical on every rank (all ranks merge the same decisions), so the global enqueue order is too.
+struct FpTurns {
+  std::mutex m;
+  std::condition_variable cv;
+  int turn = 0;
+  std::vector<char> done;
+  std::vector<int64_t> issued;          // exchanges issued per group (checked against the other ranks' in tests)
+  explicit FpTurns(int n) : done(std::max(1, n), 0), issued(std::max(1, n), 0) {}
+  void advance_locked() {
+    const int n = (int)done.size();
+    for (int k = 1; k <= n; ++k) {
+      const int c = (turn + k) % n;
+      if (!done[c]) {
+        turn = c;
+        return;
+      }
+    }
+  }
+  template <class Fn>
+  void run(int g, Fn&& fn) {
+    std::unique_lock<std::mutex> lk(m);
+    cv.wait(lk, [&] { return turn == g || done[g]; });
+    try {
+      fn();
+    } catch (...) {
+      ++issued[g];
+      advance_locked();
+      cv.notify_all();
+      throw;
+    }
+    ++issued[g];
+    advance_locked();
+    cv.notify_all();
+  }
+  void finish(int g) {
+    std::lock_guard<std::mutex> lk(m);
+    done[g] = 1;
+    if (turn == g) advance_locked();
+    cv.notify_all();
+  }
+};
+
+// Test hook: TMOG_FP_DELAY="rank:group:ms" sleeps before every exchange of that (rank, group), so a
+// multi-rank test can skew the groups' timing on one rank and check the order (and the trees) hold.
+inline int fp_delay_ms(int rank, int group) {
+  const char* e = std::getenv("TMOG_FP_DELAY");
+  int r = -1, gg = -1, ms = 0;
+  if (e == nullptr || std::sscanf(e, "%d:%d:%d", &r, &gg, &ms) != 3) return 0;
+  return (r == rank && gg == group) ? ms : 0;
+}
 
 struct GrowArgs {
   const uint8_t* Xb;
@@ -241,7 +302,7 @@ inline std::vector<FeatGroup> equal_groups4(int n) {
 }
 
 template <class BK>
-void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
+void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns = nullptr) {
   const int j0 = a.group_start[g], j1 = a.group_start[g + 1];
   const int T = j1 - j0;
   const int F = a.F, S = a.S, B = a.B;
@@ -607,8 +668,13 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R) {
                   (float*)(res + r_tot), (int64_t*)(res + r_cl), use_subset ? -1 : split_n_multi, fps);
     if (trace) std::fprintf(stderr, "[grow g%d] depth %d: %d nodes split_find done\n", g, depth, m);
     if (fp) {  // all-gather the ranks' best splits, merge into this level's decisions (on-stream on the GPU)
-      bk.fp_exchange_merge(a, fp_send, m, fp_rb, (int32_t*)(res + r_feat), (int32_t*)(res + r_bin),
-                           (float*)(res + r_gain), res + r_dl, (float*)(res + r_left));
+      if (const int ms = fp_delay_ms(a.fp_rank, g)) std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+      auto xchg = [&] {
+        bk.fp_exchange_merge(a, fp_send, m, fp_rb, (int32_t*)(res + r_feat), (int32_t*)(res + r_bin),
+                             (float*)(res + r_gain), res + r_dl, (float*)(res + r_left));
+      };
+      if (turns != nullptr) turns->run(g, xchg);
+      else xchg();
       if (trace) std::fprintf(stderr, "[grow g%d] depth %d: exchange + merge issued\n", g, depth);
     }
     if (BK::kGPU)   // partition in place of the node ranges, straight from the device decisions

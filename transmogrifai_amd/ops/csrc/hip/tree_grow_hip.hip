@@ -281,15 +281,19 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
     }
     std::vector<std::string> errs(ng);
     std::vector<std::thread> th;
+    // feature-parallel: the groups' per-level all-gathers are enqueued in one rank-independent order
+    tmog::FpTurns turns(ng);
+    tmog::FpTurns* tp = a.fp_world > 0 ? &turns : nullptr;
     for (int g = 0; g < ng; ++g) {
       th.emplace_back([&, g]() {
         try {
           hchk(hipSetDevice(dev), "hipSetDevice");
           GpuBackend bk(slots()[sb + g], a, g);
-          tmog::grow_group(bk, a, g, res->groups[g]);
+          tmog::grow_group(bk, a, g, res->groups[g], tp);
         } catch (const std::exception& e) {
           errs[g] = e.what();
         }
+        turns.finish(g);
       });
     }
     for (auto& t : th) t.join();

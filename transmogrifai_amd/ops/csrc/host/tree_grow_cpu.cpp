@@ -5,6 +5,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common/tree_grow.hpp"
@@ -121,10 +122,34 @@ void* tmog_grow_forest_cpu(const tmog::GrowArgs* args) {
   tmog::GrowResult* res = new tmog::GrowResult();
   res->groups.resize(args->n_groups);
   try {
-    for (int g = 0; g < args->n_groups; ++g) {
-      CpuBackend bk;
-      bk.group = g;
-      tmog::grow_group(bk, *args, g, res->groups[g]);
+    const int ng = args->n_groups;
+    if (args->fp_world > 0 && ng > 1 && std::getenv("TMOG_CPU_GROUP_THREADS") != nullptr) {
+      // one host thread per group, as the GPU backend runs them: exercises the exchange turn order
+      // (tmog::FpTurns) across ranks on the CPU (gloo) path
+      tmog::FpTurns turns(ng);
+      std::vector<std::string> errs(ng);
+      std::vector<std::thread> th;
+      for (int g = 0; g < ng; ++g) {
+        th.emplace_back([&, g]() {
+          try {
+            CpuBackend bk;
+            bk.group = g;
+            tmog::grow_group(bk, *args, g, res->groups[g], &turns);
+          } catch (const std::exception& e) {
+            errs[g] = e.what();
+          }
+          turns.finish(g);
+        });
+      }
+      for (auto& t : th) t.join();
+      for (int g = 0; g < ng; ++g)
+        if (!errs[g].empty()) throw std::runtime_error("group " + std::to_string(g) + ": " + errs[g]);
+    } else {
+      for (int g = 0; g < ng; ++g) {
+        CpuBackend bk;
+        bk.group = g;
+        tmog::grow_group(bk, *args, g, res->groups[g]);
+      }
     }
   } catch (const std::exception& e) {
     res->status = -1;
