@@ -73,6 +73,13 @@ def parse():
     return a
 
 
+def _rows_label(n: int) -> str:
+    for div, suf in ((1_000_000, "M"), (1_000, "K")):
+        if n % div == 0:
+            return f"{n // div}{suf}-row"
+    return f"{n}-row"
+
+
 def _selector_cls(args):
     from transmogrifai_amd.selector import factories as F
     return {"binary": F.BinaryClassificationModelSelector, "multi": F.MultiClassificationModelSelector,
@@ -207,10 +214,16 @@ def main():
     total = float(t.item())
     peak = torch.tensor([float(torch.cuda.max_memory_allocated(dev)) if use_gpu else 0.0], dtype=torch.float64)
     peak = float(D.all_reduce(peak, "max").item())
+    from transmogrifai_amd.parallel import dp as DP
+    _all_fallbacks = [x for part in (D.all_gather_object(list(DP.GATHER_FALLBACKS)) if D.is_dist()
+                                     else [DP.GATHER_FALLBACKS]) for x in part]
     per_step = total / max(args.steps, 1)
     if D.rank() == 0:
+        metric = CONFIGS[args.config][0]
+        if args.rows != CONFIGS[args.config][1]:       # the metric names the row count it was measured on
+            metric = metric.replace(_rows_label(CONFIGS[args.config][1]), _rows_label(args.rows))
         out = {
-            "metric": CONFIGS[args.config][0],
+            "metric": metric,
             "value": per_step,
             "unit": "s per end-to-end AutoML train",
             "n_gpus": world if use_gpu else 0,
@@ -227,6 +240,7 @@ def main():
             "best_model": summ.get("bestModelType") if summ else None,
             "configs_evaluated": len(summ.get("validationResults") or []) if summ else 0,
             "peak_hbm_gb_per_gpu": round(peak / 1e9, 3),
+            "dp_gather_fallbacks": sorted(set(_all_fallbacks)),
             "config": {"name": args.config,
                        "model": _selector_cls(args).__name__ + "(" +
                                 ("default grid" if args.models == "default" else args.models) + ")",

@@ -6,6 +6,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+TESTS = os.path.dirname(os.path.abspath(__file__))
+if TESTS not in sys.path:       # test-only helper modules (e.g. map_reference_impl)
+    sys.path.insert(0, TESTS)
 
 
 def pytest_configure(config):

@@ -1,0 +1,37 @@
+"""bench.py on 4 gloo ranks (row-sharded, data-parallel fits) reproduces the 1-rank selection for the BASELINE
+configs: same best model, configs evaluated and hold-out metric, and no estimator falls back to gathering its
+input columns (stages/base.py OpEstimator.fit)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(gpus, config, rows, models):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--device", "cpu", "--rows", str(rows),
+           "--steps", "1", "--warmup", "0", "--config", config, "--models", models]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith('{"metric"')][-1]
+    return json.loads(line)
+
+
+@pytest.mark.parametrize("config,rows,models", [
+    ("binary-10m", 6000, "OpLogisticRegression,OpRandomForestClassifier,OpXGBoostClassifier"),
+    ("multiclass-text", 3000, "default"),
+    ("regression-100m", 4000, "OpLinearRegression,OpRandomForestRegressor,OpGBTRegressor"),
+])
+def test_bench_four_ranks_matches_one_rank(config, rows, models):
+    one = _bench(1, config, rows, models)
+    four = _bench(4, config, rows, models)
+    assert four["config"]["parallelism"] == "dp4"
+    assert four["dp_gather_fallbacks"] == [] and one["dp_gather_fallbacks"] == []
+    assert four["best_model"] == one["best_model"]
+    assert four["configs_evaluated"] == one["configs_evaluated"]
+    key = [k for k in one if k.startswith("holdout_")][0]
+    assert abs(four[key] - one[key]) <= 1e-9, (key, one[key], four[key])

@@ -31,6 +31,9 @@ import torch
 from . import dist as D
 
 _STATE = threading.local()
+# class names of the estimators whose row-sharded fit fell back to gathering their input columns
+# (stages/base.py OpEstimator.fit); empty when every fit reduced its own statistics
+GATHER_FALLBACKS: List[str] = []
 
 
 def active() -> bool:

@@ -13,6 +13,8 @@ fitted model that shares their uid.
 """
 from __future__ import annotations
 
+import logging
+
 import copy as _copy
 import re
 from typing import Any, Callable, Dict, List, Optional, Sequence
@@ -22,6 +24,8 @@ from ..data.dataset import Dataset
 from ..features import types as T
 from ..features.feature import FeatureLike, TransientFeature, feature_uid
 from ..uid import make_uid
+
+log = logging.getLogger(__name__)
 
 _STAGE_REGISTRY: Dict[str, type] = {}
 
@@ -273,6 +277,11 @@ class OpEstimator(OpPipelineStage):
     def fit(self, ds: Dataset) -> OpTransformer:
         from ..parallel import dp
         if dp.active() and not self.dp_aware:
+            # generic fallback: correct, but every rank receives every row of the inputs -- logged and
+            # recorded (parallel/dp.py GATHER_FALLBACKS) so benchmarks and tests can assert it never fires
+            log.warning("%s (%s) has no data-parallel fit: gathering its %d input column(s) from every rank",
+                        type(self).__name__, self.uid, len(self._inputs))
+            dp.GATHER_FALLBACKS.append(type(self).__name__)
             ds = dp.gather_dataset(ds, dict.fromkeys(f.name for f in self._inputs))
             with dp.local_only():
                 model = self.fit_columns(*[ds[f.name] for f in self._inputs], ds=ds)

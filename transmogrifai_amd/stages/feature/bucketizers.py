@@ -8,6 +8,9 @@ engine as the model-selector forests.
 """
 from __future__ import annotations
 
+import math
+from typing import List
+
 import numpy as np
 import torch
 
@@ -23,7 +26,8 @@ from .math_stages import bucket_labels, bucket_metadata, bucketize_column, check
 
 def tree_splits(x: torch.Tensor, y: torch.Tensor, max_depth=5, max_bins=32, min_instances=1, min_info_gain=0.01,
                 impurity="gini") -> list:
-    """Sorted distinct thresholds of a single-feature classification tree."""
+    """Sorted distinct thresholds of a single-feature classification tree (grown by the batched tree
+    engine; the reference for :func:`tree_splits_dp`)."""
     if x.numel() == 0:
         return []
     X = x.to(torch.float64)[:, None]
@@ -39,6 +43,106 @@ def tree_splits(x: torch.Tensor, y: torch.Tensor, max_depth=5, max_bins=32, min_
     internal = f.nodes[:, 2] >= 0
     bins = sorted(set(int(b) for b in f.nodes[internal, 1]))
     return [float(spec.thresholds[0, b]) for b in bins]
+
+
+def _impurity(st: np.ndarray, kind: str):
+    """(impurity, count) with the tree engine's operation order (ops/csrc/host/tree_cpu.cpp impurity)."""
+    n = 0.0
+    for v in st:
+        n += float(v)
+    if n <= 0:
+        return 0.0, n
+    imp = 1.0 if kind == "gini" else 0.0
+    for v in st:
+        p = float(v) / n
+        if kind == "gini":
+            imp -= p * p
+        elif p > 0:
+            imp -= p * math.log2(p)
+    return imp, n
+
+
+def table_tree_splits(table: np.ndarray, max_depth=5, min_instances=1.0, min_info_gain=0.01,
+                      impurity="gini") -> List[int]:
+    """Split bins of a single-feature classification tree grown from its ``(bin, class)`` count table.
+
+    On one feature every node is a contiguous bin range and its statistics are sums of table rows, so the
+    whole tree follows from the ``B x K`` table: the same candidates, gains (engine operation order,
+    float64) and tie-breaking (first best bin) as the histogram engine growing it from the rows. A
+    row-sharded fit all-reduces the table (a few hundred bytes) instead of gathering the column."""
+    B = table.shape[0]
+    cum = np.vstack([np.zeros((1, table.shape[1]), np.int64), np.cumsum(table.astype(np.int64), 0)])
+    out = set()
+    level = [(0, B - 1)]
+    for depth in range(max_depth + 1):
+        nxt = []
+        for lo, hi in level:
+            tot = cum[hi + 1] - cum[lo]
+            tcount = float(tot.sum())
+            if not (depth < max_depth and tcount >= 2 and tcount >= 2 * min_instances - 1e-9):
+                continue
+            pimp, tc = _impurity(tot, impurity)
+            best, bb = -math.inf, -1
+            for b in range(lo, hi):
+                left = cum[b + 1] - cum[lo]
+                right = tot - left
+                li, lc = _impurity(left, impurity)
+                ri, rc = _impurity(right, impurity)
+                if lc < min_instances or rc < min_instances or lc <= 0 or rc <= 0:
+                    continue
+                gain = pimp - (lc / tc) * li - (rc / tc) * ri
+                if gain < min_info_gain:
+                    continue
+                if gain > best:
+                    best, bb = gain, b
+            if bb >= 0 and np.float32(best) > 0.0:
+                out.add(bb)
+                nxt += [(lo, bb), (bb + 1, hi)]
+        level = nxt
+        if not level:
+            break
+    return sorted(out)
+
+
+def _global_sample(x: torch.Tensor, max_bins: int) -> torch.Tensor:
+    """The rows of ``x`` (concatenated over the ranks in rank order) that ``find_splits`` samples: each rank
+    contributes its part of the global sample, so thresholds equal the single-process ones."""
+    from ...parallel import dp
+    from ...parallel import dist as D
+    from ...models.binning import sample_rows
+    n_loc = int(x.numel())
+    counts = dp.objects(n_loc)
+    me = D.rank() if dp.active() else 0
+    off, n = sum(counts[:me]), sum(counts)
+    idx = sample_rows(n, max_bins)
+    mine = idx[(idx >= off) & (idx < off + n_loc)] - off
+    part = x.detach().to("cpu", torch.float64)[mine].numpy()
+    parts = dp.objects(part)
+    return torch.as_tensor(np.concatenate(parts) if parts else part, dtype=torch.float64)
+
+
+def tree_splits_dp(x: torch.Tensor, y: torch.Tensor, max_depth=5, max_bins=32, min_instances=1,
+                   min_info_gain=0.01, impurity="gini") -> list:
+    """:func:`tree_splits` over every rank's rows with no column gather: the global binning sample, global
+    label classes, and one all-reduced ``(bin, class)`` count table."""
+    from ...parallel import dp
+    n = dp.count(int(x.numel()))
+    if n == 0:
+        return []
+    samp = _global_sample(x, max_bins)
+    spec = find_splits(samp[:, None], max_bins)
+    uniq = dp.unique_values(y.to(torch.float64))
+    K = max(2, int(uniq.numel()))
+    B = int(spec.n_bins[0])
+    if x.numel():
+        bins = quantize(x.to(torch.float64)[:, None], spec)[:, 0].to(torch.int64)
+        yi = torch.searchsorted(uniq.to(y.device), y.to(torch.float64).contiguous())
+        tab = torch.bincount(bins * K + yi, minlength=B * K).to(torch.float64)
+    else:
+        tab = torch.zeros(B * K, dtype=torch.float64, device=x.device)
+    tab = dp.sum_([tab])[0].reshape(B, K).cpu().numpy().round().astype(np.int64)
+    split_bins = table_tree_splits(tab, max_depth, float(min_instances), float(min_info_gain), impurity)
+    return [float(spec.thresholds[0, b]) for b in split_bins]
 
 
 @register_stage
@@ -82,14 +186,15 @@ class DecisionTreeNumericBucketizer(BinaryEstimator):
     allow_label_as_input = True
     _defaults = {"max_depth": 5, "max_bins": 32, "min_instances_per_node": 1, "min_info_gain": 0.01,
                  "impurity": "gini", "track_nulls": True, "track_invalid": False}
+    dp_aware = True     # global binning sample + one all-reduced (bin, class) table (tree_splits_dp)
 
     def fit_columns(self, label, a, ds=None):
         p = self.params
         ok = a.valid
         x = a.values.to(torch.float64)[ok]
         y = label.values[ok]
-        sp = tree_splits(x, y, p["max_depth"], p["max_bins"], p["min_instances_per_node"], p["min_info_gain"],
-                         p["impurity"])
+        sp = tree_splits_dp(x, y, p["max_depth"], p["max_bins"], p["min_instances_per_node"], p["min_info_gain"],
+                            p["impurity"])
         splits = [float("-inf")] + sp + [float("inf")]
         should = check_splits(splits)
         final = splits if should else []
@@ -116,18 +221,22 @@ class DecisionTreeNumericMapBucketizerModel(BinaryTransformer):
         self.track_nulls = track_nulls
 
     def transform_columns(self, label, m, ds=None):
-        vals = m.to_list()
-        dtype = vector_dtype(torch.device("cpu"))
+        from ...config import default_device
+        from .maps import map_coo
+        dev = default_device()
+        coo = map_coo(m, "real", False, dev)
+        dtype = vector_dtype(dev)
+        last = coo.last_entry(self.keys)
         blocks = []
-        for k, sp in zip(self.keys, self.splits):
-            x = torch.as_tensor([float(r[k]) if (r and r.get(k) is not None) else 0.0 for r in vals],
-                                dtype=torch.float64)
-            ok = torch.as_tensor([bool(r) and r.get(k) is not None for r in vals], dtype=torch.bool)
+        for j, sp in enumerate(self.splits):
+            e = last[:, j]
+            ok = e >= 0
+            x = coo.num[e.clamp_min(0)] if coo.nnz else torch.zeros(coo.n, dtype=torch.float64, device=dev)
             if sp:
                 blocks.append(bucketize_column(x, ok, sp, self.track_nulls, False, "Right", dtype))
             elif self.track_nulls:
                 blocks.append((~ok).to(dtype)[:, None])
-        out = torch.cat(blocks, 1) if blocks else torch.zeros(len(vals), 0, dtype=dtype)
+        out = torch.cat(blocks, 1) if blocks else torch.zeros(coo.n, 0, dtype=dtype, device=dev)
         return VectorColumn(out, self.metadata.get("vector_metadata"))
 
     def ctor_args(self):
@@ -144,20 +253,27 @@ class DecisionTreeNumericMapBucketizer(BinaryEstimator):
     output_type = T.OPVector
     allow_label_as_input = True
     _defaults = dict(DecisionTreeNumericBucketizer._defaults)
+    dp_aware = True     # key union + per-key tree_splits_dp
 
     def fit_columns(self, label, m, ds=None):
         from ...data.vector_metadata import OpVectorColumnMetadata, NULL_STRING
         p = self.params
-        vals = m.to_list()
-        y_all = label.values.to(torch.float64).cpu()
-        keys = sorted({k for r in vals for k, v in (r or {}).items() if v is not None})
+        from ...config import default_device
+        from .maps import _global_keys, map_coo
+        dev = default_device()
+        coo = map_coo(m, "real", False, dev)
+        y_all = label.values.to(device=dev, dtype=torch.float64)
+        used = torch.unique(coo.key).cpu().numpy() if coo.nnz else np.zeros(0, np.int64)
+        keys = _global_keys([[coo.keys[int(i)] for i in used]])[0]
+        last = coo.last_entry(keys)
         t = self.get_transient_features()[1]
         splits, cols = [], []
-        for k in keys:
-            rows = [i for i, r in enumerate(vals) if r and r.get(k) is not None]
-            x = torch.as_tensor([float(vals[i][k]) for i in rows], dtype=torch.float64)
-            sp = tree_splits(x, y_all[rows], p["max_depth"], p["max_bins"], p["min_instances_per_node"],
-                             p["min_info_gain"], p["impurity"])
+        for j, k in enumerate(keys):
+            e = last[:, j]
+            rows = torch.nonzero(e >= 0).reshape(-1)
+            x = coo.num[e[rows]] if coo.nnz else torch.zeros(0, dtype=torch.float64, device=dev)
+            sp = tree_splits_dp(x, y_all[rows], p["max_depth"], p["max_bins"], p["min_instances_per_node"],
+                                p["min_info_gain"], p["impurity"])
             full = [float("-inf")] + sp + [float("inf")]
             ok = check_splits(full)
             splits.append(full if ok else [])

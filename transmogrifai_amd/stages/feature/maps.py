@@ -3,25 +3,34 @@
 Reference: ``OPMapVectorizer`` family (``core/.../impl/feature/OPMapVectorizer.scala:60-468``: RealMap / IntegralMap /
 BinaryMap / DateMap / TextMapHashing; key discovery, per-key mean / mode / constant fill and null
 tracking), ``TextMapPivotVectorizer`` (``:53-145``), ``MultiPickListMapVectorizer`` (``:49-122``),
-``SmartTextMapVectorizer`` (``:57-418``), ``GeolocationMapVectorizer`` (``:42-129``) and
-``DateMapToUnitCircleVectorizer`` (``:63-134``). Maps are ragged host data (COO of row, key, value);
-every key becomes a dense device column block.
+``SmartTextMapVectorizer`` (``:57-418``), ``GeolocationMapVectorizer`` (``:42-129``),
+``DateMapToUnitCircleVectorizer`` (``:63-134``) and ``TextMapLenEstimator`` / ``TextMapNullEstimator``.
+
+MI355X design: a map column is flattened ONCE into a COO view (:class:`MapCOO`: entry e =
+``(row[e], key[e], value[e])`` as device tensors, keys and text values dictionary-coded; the only
+per-element host work is that flattening of the Python dicts). Every fit statistic is a segmented
+device reduction over the entries -- per-key sums / counts, ``(key, value)`` pair counts -- reduced over
+the ranks of a row-sharded fit with one collective (``dp_aware``; reference reductions
+``OPMapVectorizer.scala:134,238,280``), and every transform densifies the entries of the model's keys
+with one scatter (last value wins for keys that collide after cleaning, as a dict update does) and
+feeds the dense per-key columns to the same fill / one-hot pivot / hashing kernels as the scalar
+vectorizers (``ops/vector.py``, ``ops/text.py``).
 """
 from __future__ import annotations
 
 from collections import Counter
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
 
-from ...config import vector_dtype
-from ...data.columns import ObjectColumn
+from ...config import default_device, vector_dtype
+from ...data.columns import ObjectColumn, TextColumn
 from ...data.vector_metadata import NULL_STRING, OTHER_STRING, OpVectorColumnMetadata
 from ...features import types as T
 from ...utils import text as TU
 from ..base import SequenceEstimator, SequenceTransformer, register_stage
-from .vectorizers import VectorizerMixin, top_values
+from .vectorizers import VectorizerMixin, pivot_columns, top_values
 
 
 def _clean_key(k, clean):
@@ -46,6 +55,162 @@ def _kind_of(t) -> str:
     return "pivot"
 
 
+_VALUE_KIND = {"real": "num", "binary": "num", "integral": "int", "date": "int", "geo": "geo", "set": "set",
+               "pivot": "text", "smarttext": "text"}
+
+
+# ------------------------------------------------------------------------------------------- COO view
+class MapCOO:
+    """Entries of a map column with a non-null value.
+
+    ``row`` / ``key`` are int64 device tensors over the entries (``key`` indexes ``keys``, the cleaned key
+    strings); the value is one of ``num`` (float64), ``ival`` (int64: integral / date millis), ``vcode``
+    (int64 codes into ``vocab``: text), ``geo`` (float64 ``[nnz, 3]``) or, for sets, ``item_entry`` /
+    ``item_code`` (one row per set element: its entry and its code into ``vocab``)."""
+
+    def __init__(self, n, row, key, keys, device):
+        self.n, self.row, self.key, self.keys, self.device = n, row, key, keys, device
+        self.num = self.ival = self.vcode = self.geo = self.item_entry = self.item_code = None
+        self.vocab: List[str] = []
+
+    @property
+    def nnz(self) -> int:
+        return int(self.row.numel())
+
+    def slots(self, model_keys: Sequence[str]) -> torch.Tensor:
+        """``[len(keys)]`` int64: this column's key id -> position in ``model_keys`` (-1 = not a model key)."""
+        pos = {k: i for i, k in enumerate(model_keys)}
+        return torch.as_tensor(np.fromiter((pos.get(k, -1) for k in self.keys), np.int64, len(self.keys)),
+                               device=self.device)
+
+    def last_entry(self, model_keys: Sequence[str]) -> torch.Tensor:
+        """``[n, K]`` int64: the entry holding (row, model key k), -1 if the row has none (the last one when
+        several raw keys clean to the same key)."""
+        K = len(model_keys)
+        out = torch.full((self.n * max(K, 1),), -1, dtype=torch.int64, device=self.device)
+        if K and self.nnz:
+            s = self.slots(model_keys)[self.key]
+            sel = s >= 0
+            flat = self.row[sel] * K + s[sel]
+            out.scatter_reduce_(0, flat, torch.nonzero(sel).reshape(-1), reduce="amax")
+        return out.view(self.n, max(K, 1))[:, :K]
+
+
+def _flatten(vals) -> tuple:
+    n = len(vals)
+    lens = np.fromiter((len(m) if m else 0 for m in vals), np.int64, n)
+    ks = [k for m in vals if m for k in m]
+    vs = [v for m in vals if m for v in m.values()]
+    row = np.repeat(np.arange(n, dtype=np.int64), lens)
+    return n, row, ks, vs
+
+
+def map_coo(col, kind: str, clean_keys: bool, device=None) -> MapCOO:
+    """The :class:`MapCOO` of a map column (cached on the column object per ``(kind, clean_keys, device)``)."""
+    dev = torch.device(device) if device is not None else default_device()
+    vkind = _VALUE_KIND[kind]
+    cache = getattr(col, "_coo_cache", None)
+    if cache is None:
+        cache = {}
+        try:
+            col._coo_cache = cache
+        except AttributeError:
+            pass
+    ck = (vkind, bool(clean_keys), str(dev))
+    if ck in cache:
+        return cache[ck]
+    vals = col.values if isinstance(col, ObjectColumn) else col.to_list()
+    n, row, ks, vs = _flatten(vals)
+    if vkind == "geo":
+        keep = np.fromiter((bool(v) for v in vs), bool, len(vs))
+    else:
+        keep = np.fromiter((v is not None for v in vs), bool, len(vs))
+    row = row[keep]
+    ks = [k for k, o in zip(ks, keep) if o]
+    vs = [v for v, o in zip(vs, keep) if o]
+    raw: Dict[str, int] = {}
+    kc = np.fromiter((raw.setdefault(k, len(raw)) for k in ks), np.int64, len(ks))
+    clean: Dict[str, int] = {}
+    lut = np.fromiter((clean.setdefault(_clean_key(k, clean_keys), len(clean)) for k in raw), np.int64, len(raw))
+    key = lut[kc] if kc.size else kc
+    coo = MapCOO(n, torch.as_tensor(row, device=dev), torch.as_tensor(key, device=dev), list(clean), dev)
+    if vkind == "num":
+        coo.num = torch.as_tensor(np.fromiter((float(v) for v in vs), np.float64, len(vs)), device=dev)
+    elif vkind == "int":
+        coo.ival = torch.as_tensor(np.fromiter((int(v) for v in vs), np.int64, len(vs)), device=dev)
+    elif vkind == "geo":
+        g = np.asarray([list(v)[:3] for v in vs], np.float64).reshape(-1, 3)
+        coo.geo = torch.as_tensor(g, device=dev)
+    elif vkind == "text":
+        voc: Dict[str, int] = {}
+        coo.vcode = torch.as_tensor(np.fromiter((voc.setdefault(str(v), len(voc)) for v in vs), np.int64, len(vs)),
+                                    device=dev)
+        coo.vocab = list(voc)
+    else:   # set: one item row per element
+        items = [list(v) if isinstance(v, (set, frozenset, list, tuple)) else [v] for v in vs]
+        ilen = np.fromiter((len(i) for i in items), np.int64, len(items))
+        voc = {}
+        codes = np.fromiter((voc.setdefault(str(x), len(voc)) for i in items for x in i), np.int64, int(ilen.sum()))
+        coo.item_entry = torch.as_tensor(np.repeat(np.arange(len(items), dtype=np.int64), ilen), device=dev)
+        coo.item_code = torch.as_tensor(codes, device=dev)
+        coo.vocab = list(voc)
+    cache[ck] = coo
+    return coo
+
+
+def _global_keys(local_keys: Sequence[Sequence[str]]) -> List[List[str]]:
+    """Per column: sorted union of the keys of every rank (one object all-gather for all columns)."""
+    from ...parallel import dp
+    parts = dp.objects([sorted(k) for k in local_keys])
+    return [sorted(set().union(*[set(p[i]) for p in parts])) for i in range(len(local_keys))]
+
+
+def _filter_keys(keys, allow, block):
+    if allow:
+        keys = [k for k in keys if k in set(allow)]
+    if block:
+        keys = [k for k in keys if k not in set(block)]
+    return keys
+
+
+def _key_sums(coo: MapCOO, keys: Sequence[str], values: torch.Tensor) -> torch.Tensor:
+    """``[K, C]`` float64 sums over the entries of each model key of ``values [nnz, C]``."""
+    K = len(keys)
+    out = torch.zeros(K, values.shape[1], dtype=torch.float64, device=coo.device)
+    if coo.nnz and K:
+        s = coo.slots(keys)[coo.key]
+        sel = s >= 0
+        out.index_add_(0, s[sel], values[sel].to(torch.float64))
+    return out
+
+
+def _pair_counts(keys_of: torch.Tensor, codes: torch.Tensor, n_codes: int) -> tuple:
+    """Distinct ``(key id, code)`` pairs with counts (device unique, one host read)."""
+    if keys_of.numel() == 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)
+    pair = keys_of * max(n_codes, 1) + codes
+    u, c = torch.unique(pair, return_counts=True)
+    u, c = u.cpu().numpy(), c.cpu().numpy()
+    return u // max(n_codes, 1), u % max(n_codes, 1), c
+
+
+def _geo_fill(S: np.ndarray, A: float):
+    from ...features.aggregators import GeolocationMidpoint
+    return GeolocationMidpoint().present((S[0], S[1], S[2], int(S[3]), float(A)))
+
+
+def _per_key_text_columns(coo: MapCOO, keys: Sequence[str]) -> List[TextColumn]:
+    """One dictionary-coded column per model key: row -> value code of (row, key), -1 when absent."""
+    last = coo.last_entry(keys)
+    out = []
+    for j in range(len(keys)):
+        e = last[:, j]
+        codes = torch.where(e >= 0, coo.vcode[e.clamp_min(0)], torch.full_like(e, -1)) if coo.nnz else e
+        out.append(TextColumn(T.PickList, codes.to(torch.int32), coo.vocab))
+    return out
+
+
+# --------------------------------------------------------------------------------------------- model
 @register_stage
 class MapVectorizerModel(VectorizerMixin, SequenceTransformer):
     operation_name = "vecMap"
@@ -64,86 +229,110 @@ class MapVectorizerModel(VectorizerMixin, SequenceTransformer):
         self.methods = [list(m) for m in (methods or [])]
         self.num_features = num_features
 
+    def _numeric_block(self, coo: MapCOO, keys, fills, dtype) -> torch.Tensor:
+        K, n, dev = len(keys), coo.n, coo.device
+        last = coo.last_entry(keys)
+        present = last >= 0
+        e = last.clamp_min(0)
+        if self.kind == "date":
+            ms = coo.ival[e] if coo.nnz else torch.zeros(n, K, dtype=torch.int64, device=dev)
+            v = torch.div(int(self.reference_date) - ms, 86400000, rounding_mode="floor").to(torch.float64)
+        elif self.kind == "integral":
+            v = (coo.ival[e] if coo.nnz else torch.zeros(n, K, dtype=torch.int64, device=dev)).to(torch.float64)
+        else:
+            v = coo.num[e] if coo.nnz else torch.zeros(n, K, dtype=torch.float64, device=dev)
+            if self.kind == "binary":
+                v = (v != 0).to(torch.float64)
+        f = torch.as_tensor(np.asarray(fills, np.float64).reshape(-1), device=dev)
+        x = torch.where(present, v, f[None, :])
+        if not self.track_nulls:
+            return x.to(dtype)
+        return torch.stack([x, (~present).to(torch.float64)], 2).reshape(n, 2 * K).to(dtype)
+
+    def _geo_block(self, coo: MapCOO, keys, fills, dtype) -> torch.Tensor:
+        K, n, dev = len(keys), coo.n, coo.device
+        last = coo.last_entry(keys)
+        present = last >= 0
+        g = coo.geo[last.clamp_min(0)] if coo.nnz else torch.zeros(n, K, 3, dtype=torch.float64, device=dev)
+        f = torch.as_tensor(np.asarray([fl if fl else [0.0, 0.0, 0.0] for fl in fills], np.float64).reshape(K, 3),
+                            device=dev)
+        x = torch.where(present[:, :, None], g, f[None, :, :])
+        if self.track_nulls:
+            x = torch.cat([x, (~present).to(torch.float64)[:, :, None]], 2)
+        return x.reshape(n, K * (4 if self.track_nulls else 3)).to(dtype)
+
+    def _set_block(self, coo: MapCOO, keys, tops, dtype) -> torch.Tensor:
+        n, dev = coo.n, coo.device
+        widths = [len(t) + 1 + (1 if self.track_nulls else 0) for t in tops]
+        offs = np.concatenate([[0], np.cumsum(widths)]).astype(np.int64)
+        out = torch.zeros(n, int(offs[-1]), dtype=dtype, device=dev)
+        if not keys:
+            return out
+        has = torch.zeros(n, len(keys), dtype=torch.bool, device=dev)
+        if coo.item_code is not None and coo.item_code.numel():
+            s = coo.slots(keys)[coo.key]                         # per entry
+            es = s[coo.item_entry]                               # per item
+            sel = es >= 0
+            # (slot, code) -> column inside the slot's block, built once per distinct pair on the host
+            ks_, cs_, _ = _pair_counts(es[sel], coo.item_code[sel], len(coo.vocab))
+            idx = [{v: i for i, v in enumerate(t)} for t in tops]
+            col_of = np.empty(ks_.size, np.int64)
+            for i, (k, c) in enumerate(zip(ks_, cs_)):
+                v = coo.vocab[int(c)]
+                v = TU.clean_string(v) if self.clean_text else v
+                col_of[i] = offs[int(k)] + idx[int(k)].get(v, len(tops[int(k)]))
+            pair_ids = torch.as_tensor(ks_ * max(len(coo.vocab), 1) + cs_, device=dev)
+            mine = es[sel] * max(len(coo.vocab), 1) + coo.item_code[sel]
+            cols = torch.as_tensor(col_of, device=dev)[torch.searchsorted(pair_ids, mine)]
+            rows = coo.row[coo.item_entry[sel]]
+            out.view(-1).index_put_((rows * out.shape[1] + cols,), torch.ones_like(rows, dtype=dtype), accumulate=True)
+            has[rows, es[sel]] = True
+        if self.track_nulls:
+            for j in range(len(keys)):
+                out[:, int(offs[j + 1]) - 1] = (~has[:, j]).to(dtype)
+        return out
+
+    def _text_block(self, coo: MapCOO, keys, tops, methods, dtype) -> torch.Tensor:
+        from ...ops.text import HashInput, hashed_tf
+        n, dev = coo.n, coo.device
+        cols = _per_key_text_columns(coo, keys)
+        toks = None
+        parts = []
+        for j, c in enumerate(cols):
+            if methods and methods[j] == "hash":
+                if toks is None:
+                    toks = TU.tokenize_batch(coo.vocab)
+                blk = torch.zeros(n, self.num_features + (1 if self.track_nulls else 0), dtype=dtype, device=dev)
+                hashed_tf(blk[:, :self.num_features], [HashInput(c.codes, toks, None)], self.num_features, False,
+                          False)
+                if self.track_nulls:
+                    cnt = torch.as_tensor(np.append(toks.counts(), 0), dtype=torch.int64, device=dev)
+                    cc = c.codes.to(torch.int64)
+                    blk[:, -1] = (cnt[torch.where(cc >= 0, cc, torch.full_like(cc, cnt.numel() - 1))] == 0).to(dtype)
+                parts.append(blk)
+            else:
+                parts.append(pivot_columns([c], [tops[j]], self.clean_text, self.track_nulls, dtype))
+        return torch.cat(parts, 1) if parts else torch.zeros(n, 0, dtype=dtype, device=dev)
+
     def transform_columns(self, *cols, ds=None):
+        dev = default_device()
+        dtype = vector_dtype(dev)
         n = len(cols[0]) if cols else 0
         blocks = []
         for ci, c in enumerate(cols):
-            vals = c.values if isinstance(c, ObjectColumn) else np.array(c.to_list(), dtype=object)
+            coo = map_coo(c, self.kind, self.clean_keys, dev)
             keys = self.keys[ci]
-            kidx = {k: i for i, k in enumerate(keys)}
             if self.kind in ("real", "integral", "binary", "date"):
-                per = 2 if self.track_nulls else 1
-                b = np.zeros((n, len(keys) * per))
-                seen = np.zeros((n, len(keys)), bool)
-                for r, m in enumerate(vals):
-                    for k, v in (m or {}).items():
-                        j = kidx.get(_clean_key(k, self.clean_keys))
-                        if j is None or v is None:
-                            continue
-                        if self.kind == "date":
-                            v = float((int(self.reference_date) - int(v)) // 86400000)
-                        elif self.kind == "binary":
-                            v = 1.0 if v else 0.0
-                        b[r, j * per] = float(v)
-                        seen[r, j] = True
-                for j in range(len(keys)):
-                    miss = ~seen[:, j]
-                    b[miss, j * per] = self.fills[ci][j]
-                    if self.track_nulls:
-                        b[:, j * per + 1] = miss.astype(np.float64)
-                blocks.append(b)
+                blocks.append(self._numeric_block(coo, keys, self.fills[ci], dtype))
             elif self.kind == "geo":
-                per = 4 if self.track_nulls else 3
-                b = np.zeros((n, len(keys) * per))
-                for j in range(len(keys)):
-                    b[:, j * per:j * per + 3] = self.fills[ci][j] if self.fills[ci][j] else [0.0, 0.0, 0.0]
-                    if self.track_nulls:
-                        b[:, j * per + 3] = 1.0
-                for r, m in enumerate(vals):
-                    for k, v in (m or {}).items():
-                        j = kidx.get(_clean_key(k, self.clean_keys))
-                        if j is None or not v:
-                            continue
-                        b[r, j * per:j * per + 3] = v
-                        if self.track_nulls:
-                            b[r, j * per + 3] = 0.0
-                blocks.append(b)
-            else:  # pivot / set / smarttext (pivot or hash per key)
-                parts = []
-                for j, k in enumerate(keys):
-                    method = self.methods[ci][j] if self.methods else "pivot"
-                    top = self.tops[ci][j]
-                    if method == "hash":
-                        w = self.num_features + (1 if self.track_nulls else 0)
-                        bb = np.zeros((n, w))
-                        for r, m in enumerate(vals):
-                            v = _get(m, k, self.clean_keys)
-                            toks = TU.tokenize(v) if isinstance(v, str) else []
-                            if toks:
-                                idx = TU.hash_terms(toks, self.num_features)
-                                np.add.at(bb[r], idx, 1.0)
-                            elif self.track_nulls:
-                                bb[r, -1] = 1.0
-                        parts.append(bb)
-                        continue
-                    w = len(top) + 1 + (1 if self.track_nulls else 0)
-                    bb = np.zeros((n, w))
-                    ix = {v: i for i, v in enumerate(top)}
-                    for r, m in enumerate(vals):
-                        v = _get(m, k, self.clean_keys)
-                        items = ([] if v is None else (list(v) if isinstance(v, (set, frozenset, list)) else [v]))
-                        if not items:
-                            if self.track_nulls:
-                                bb[r, -1] = 1.0
-                            continue
-                        for it in items:
-                            s = TU.clean_string(str(it)) if self.clean_text else str(it)
-                            bb[r, ix.get(s, len(top))] += 1.0
-                    parts.append(bb)
-                blocks.append(np.concatenate(parts, 1) if parts else np.zeros((n, 0)))
-        dev = cols[0].device if cols else torch.device("cpu")
-        out = np.concatenate(blocks, 1) if blocks else np.zeros((n, 0))
-        return self._vec(torch.as_tensor(out, dtype=vector_dtype(dev), device=dev))
+                blocks.append(self._geo_block(coo, keys, self.fills[ci], dtype))
+            elif self.kind == "set":
+                blocks.append(self._set_block(coo, keys, self.tops[ci], dtype))
+            else:
+                blocks.append(self._text_block(coo, keys, self.tops[ci], self.methods[ci] if self.methods else None,
+                                               dtype))
+        out = torch.cat(blocks, 1) if blocks else torch.zeros(n, 0, dtype=dtype, device=dev)
+        return self._vec(out)
 
     def ctor_args(self):
         return {"kind": self.kind, "keys": self.keys, "fills": self.fills, "tops": self.tops,
@@ -167,6 +356,7 @@ def _get(m, k, clean):
     return None
 
 
+# ------------------------------------------------------------------------------------------ estimator
 @register_stage
 class MapVectorizer(VectorizerMixin, SequenceEstimator):
     operation_name = "vecMap"
@@ -174,59 +364,112 @@ class MapVectorizer(VectorizerMixin, SequenceEstimator):
                  "fill_with_mean": True, "fill_with_mode": True, "fill_value": 0.0, "top_k": 20, "min_support": 10,
                  "reference_date": None, "max_cardinality": 30, "num_features": 512, "allow_keys": None,
                  "block_keys": None}
+    # row-sharded fits reduce per-key statistics over the ranks: key union and (key, value) counts in one
+    # object all-gather, per-key sums in one all-reduce -- no map column is gathered
+    dp_aware = True
 
     def fit_columns(self, *cols, ds=None):
+        from ...parallel import dp
         from ...utils.dates import now_ms
         p = self.params
         kind = p["kind"]
         ref = p["reference_date"] or now_ms()
         self.params["reference_date"] = ref
-        all_keys, fills, tops, methods = [], [], [], []
-        colsm = []
-        for c, t in zip(cols, self.get_transient_features()):
-            vals = c.values if isinstance(c, ObjectColumn) else c.to_list()
-            per_key: Dict[str, list] = {}
-            for m in vals:
-                for k, v in (m or {}).items():
-                    if v is None:
-                        continue
-                    per_key.setdefault(_clean_key(k, p["clean_keys"]), []).append(v)
-            keys = sorted(per_key)
-            if p["allow_keys"]:
-                keys = [k for k in keys if k in set(p["allow_keys"])]
-            if p["block_keys"]:
-                keys = [k for k in keys if k not in set(p["block_keys"])]
-            all_keys.append(keys)
-            f_col, t_col, m_col = [], [], []
-            for k in keys:
-                vs = per_key[k]
-                if kind == "real":
-                    f_col.append(float(np.mean(vs)) if p["fill_with_mean"] else float(p["fill_value"]))
-                elif kind == "integral":
-                    if p["fill_with_mode"]:
-                        cnt = Counter(int(v) for v in vs)
-                        f_col.append(float(min(cnt.items(), key=lambda kv: (-kv[1], kv[0]))[0]))
-                    else:
-                        f_col.append(float(p["fill_value"]))
-                elif kind in ("binary", "date"):
-                    f_col.append(float(p["fill_value"]))
-                elif kind == "geo":
-                    from ...features.aggregators import Event, GeolocationMidpoint
-                    f_col.append(GeolocationMidpoint().aggregate(Event(0, v) for v in vs))
-                else:
+        dev = default_device()
+        coos = [map_coo(c, kind, p["clean_keys"], dev) for c in cols]
+        # keys with at least one value on some rank
+        present = []
+        for coo in coos:
+            used = torch.unique(coo.key).cpu().numpy() if coo.nnz else np.zeros(0, np.int64)
+            present.append([coo.keys[int(i)] for i in used])
+        all_keys = [_filter_keys(k, p["allow_keys"], p["block_keys"]) for k in _global_keys(present)]
+        fills: List[list] = [[] for _ in cols]
+        tops: List[list] = [[] for _ in cols]
+        methods: List[list] = [[] for _ in cols]
+        if kind == "real":
+            if p["fill_with_mean"]:
+                sums = [_key_sums(coo, keys, torch.stack([coo.num, torch.ones_like(coo.num)], 1))
+                        for coo, keys in zip(coos, all_keys)]
+                red = dp.sum_(sums) if sums else []
+                for i, r in enumerate(red):
+                    r = r.cpu().numpy()
+                    fills[i] = [float(a / b) if b > 0 else float(p["fill_value"]) for a, b in r]
+            else:
+                fills = [[float(p["fill_value"])] * len(k) for k in all_keys]
+        elif kind == "integral":
+            if p["fill_with_mode"]:
+                counters = []
+                for coo in coos:
                     cnt: Counter = Counter()
-                    for v in vs:
-                        items = list(v) if isinstance(v, (set, frozenset, list)) else [v]
-                        cnt.update(TU.clean_string(str(i)) if p["clean_text"] else str(i) for i in items)
+                    if coo.nnz:
+                        u, c = torch.unique(torch.stack([coo.key, coo.ival], 1), dim=0, return_counts=True)
+                        for (k, v), n_ in zip(u.cpu().numpy().tolist(), c.cpu().numpy().tolist()):
+                            cnt[(coo.keys[k], v)] += n_
+                    counters.append(cnt)
+                merged = dp.merge_counters(counters)
+                for i, keys in enumerate(all_keys):
+                    per: Dict[str, list] = {}
+                    for (k, v), n_ in merged[i].items():
+                        per.setdefault(k, []).append((v, n_))
+                    fills[i] = [float(min(per[k], key=lambda vc: (-vc[1], vc[0]))[0]) if k in per
+                                else float(p["fill_value"]) for k in keys]
+            else:
+                fills = [[float(p["fill_value"])] * len(k) for k in all_keys]
+        elif kind in ("binary", "date"):
+            fills = [[float(p["fill_value"])] * len(k) for k in all_keys]
+        elif kind == "geo":
+            sums, accs = [], []
+            for coo, keys in zip(coos, all_keys):
+                if coo.nnz:
+                    lat, lon = torch.deg2rad(coo.geo[:, 0]), torch.deg2rad(coo.geo[:, 1])
+                    xyz1 = torch.stack([torch.cos(lat) * torch.cos(lon), torch.cos(lat) * torch.sin(lon),
+                                        torch.sin(lat), torch.ones_like(lat)], 1)
+                    sums.append(_key_sums(coo, keys, xyz1))
+                    s = coo.slots(keys)[coo.key]
+                    sel = s >= 0
+                    a = torch.zeros(len(keys), dtype=torch.float64, device=dev)
+                    a.scatter_reduce_(0, s[sel], coo.geo[sel, 2], reduce="amax", include_self=True)
+                    accs.append(a)
+                else:
+                    sums.append(torch.zeros(len(keys), 4, dtype=torch.float64, device=dev))
+                    accs.append(torch.zeros(len(keys), dtype=torch.float64, device=dev))
+            sums = dp.sum_(sums) if sums else []
+            accs = [dp.max_(a) for a in accs]
+            for i, keys in enumerate(all_keys):
+                S, A = sums[i].cpu().numpy(), accs[i].cpu().numpy()
+                fills[i] = [_geo_fill(S[j], A[j]) for j in range(len(keys))]
+        else:
+            counters = []
+            for coo in coos:
+                cnt = Counter()
+                if kind == "set":
+                    if coo.item_code is not None and coo.item_code.numel():
+                        k_, c_, n_ = _pair_counts(coo.key[coo.item_entry], coo.item_code, len(coo.vocab))
+                    else:
+                        k_ = c_ = n_ = np.zeros(0, np.int64)
+                elif coo.nnz:
+                    k_, c_, n_ = _pair_counts(coo.key, coo.vcode, len(coo.vocab))
+                else:
+                    k_ = c_ = n_ = np.zeros(0, np.int64)
+                for k, c, m in zip(k_.tolist(), c_.tolist(), n_.tolist()):
+                    v = coo.vocab[c]
+                    cnt[(coo.keys[k], TU.clean_string(v) if p["clean_text"] else v)] += m
+                counters.append(cnt)
+            merged = dp.merge_counters(counters)
+            for i, keys in enumerate(all_keys):
+                per: Dict[str, Counter] = {}
+                for (k, v), m in merged[i].items():
+                    per.setdefault(k, Counter())[v] += m
+                for k in keys:
+                    cnt = per.get(k, Counter())
                     method = "pivot"
                     if kind == "smarttext" and len(cnt) > p["max_cardinality"]:
                         method = "hash"
-                    m_col.append(method)
-                    t_col.append(top_values(cnt, p["top_k"], p["min_support"]) if method == "pivot" else [])
-            fills.append(f_col)
-            tops.append(t_col)
-            methods.append(m_col)
-            for j, k in enumerate(keys):
+                    methods[i].append(method)
+                    tops[i].append(top_values(cnt, p["top_k"], p["min_support"]) if method == "pivot" else [])
+        colsm = []
+        for i, t in enumerate(self.get_transient_features()):
+            for j, k in enumerate(all_keys[i]):
                 base = dict(parent_feature_name=(t.name,), parent_feature_type=(t.type_name,), grouping=k)
                 if kind in ("real", "integral", "binary", "date"):
                     colsm.append(OpVectorColumnMetadata(**base))
@@ -236,12 +479,12 @@ class MapVectorizer(VectorizerMixin, SequenceEstimator):
                     colsm += [OpVectorColumnMetadata(descriptor_value=d, **base) for d in ("lat", "lon", "accuracy")]
                     if p["track_nulls"]:
                         colsm.append(OpVectorColumnMetadata(indicator_value=NULL_STRING, **base))
-                elif m_col[j] == "hash":
+                elif methods[i] and methods[i][j] == "hash":
                     colsm += [OpVectorColumnMetadata(**base) for _ in range(p["num_features"])]
                     if p["track_nulls"]:
                         colsm.append(OpVectorColumnMetadata(indicator_value=NULL_STRING, **base))
                 else:
-                    vals2 = t_col[j] + [OTHER_STRING] + ([NULL_STRING] if p["track_nulls"] else [])
+                    vals2 = tops[i][j] + [OTHER_STRING] + ([NULL_STRING] if p["track_nulls"] else [])
                     colsm += [OpVectorColumnMetadata(indicator_value=v, **base) for v in vals2]
         self.metadata["vector_metadata"] = self.vector_metadata(colsm)
         return MapVectorizerModel(kind, all_keys, fills, tops, p["clean_keys"], p["clean_text"], p["track_nulls"],
@@ -283,6 +526,16 @@ class TextMapHashingVectorizer(MapVectorizer):
     _defaults = dict(MapVectorizer._defaults, kind="smarttext", max_cardinality=-1)
 
 
+def _present_keys(cols, kind: str, clean: bool) -> List[List[str]]:
+    """Global (all ranks) sorted keys that hold a value, per column."""
+    local = []
+    for c in cols:
+        coo = map_coo(c, kind, clean)
+        used = torch.unique(coo.key).cpu().numpy() if coo.nnz else np.zeros(0, np.int64)
+        local.append([coo.keys[int(i)] for i in used])
+    return _global_keys(local)
+
+
 # ------------------------------------------------------------------------ date map unit circle
 @register_stage
 class DateMapToUnitCircleVectorizerModel(VectorizerMixin, SequenceTransformer):
@@ -295,25 +548,23 @@ class DateMapToUnitCircleVectorizerModel(VectorizerMixin, SequenceTransformer):
 
     def transform_columns(self, *cols, ds=None):
         from ...utils.dates import period_values
+        dev = default_device()
         n = len(cols[0]) if cols else 0
         blocks = []
         for ci, c in enumerate(cols):
-            vals = c.to_list()
+            coo = map_coo(c, "date", False, dev)
             keys = self.keys[ci]
-            b = np.zeros((n, 2 * len(keys)))
-            for j, k in enumerate(keys):
-                rows = [r for r, m in enumerate(vals) if m and m.get(k) is not None]
-                if not rows:
-                    continue
-                ms = torch.as_tensor([int(vals[r][k]) for r in rows], dtype=torch.int64)
+            last = coo.last_entry(keys)
+            present = last >= 0
+            b = torch.zeros(n, len(keys), 2, dtype=torch.float64, device=dev)
+            if coo.nnz and bool(present.any()):
+                ms = coo.ival[last[present]]
                 v, size = period_values(ms, self.time_period)
-                rad = 2 * np.pi * v.to(torch.float64).numpy() / size
-                b[rows, 2 * j] = np.cos(rad)
-                b[rows, 2 * j + 1] = np.sin(rad)
-            blocks.append(b)
-        dev = cols[0].device if cols else torch.device("cpu")
-        out = np.concatenate(blocks, 1) if blocks else np.zeros((n, 0))
-        return self._vec(torch.as_tensor(out, dtype=vector_dtype(dev), device=dev))
+                rad = 2 * np.pi * v.to(torch.float64) / size
+                b[present] = torch.stack([torch.cos(rad), torch.sin(rad)], 1)
+            blocks.append(b.reshape(n, 2 * len(keys)))
+        out = torch.cat(blocks, 1) if blocks else torch.zeros(n, 0, dtype=torch.float64, device=dev)
+        return self._vec(out.to(vector_dtype(dev)))
 
     def ctor_args(self):
         return {"keys": self.keys, "timePeriod": self.time_period}
@@ -327,13 +578,13 @@ class DateMapToUnitCircleVectorizer(VectorizerMixin, SequenceEstimator):
     """(cos, sin) of a time period per map key (``DateMapToUnitCircleVectorizer.scala:63-134``)."""
     operation_name = "dateMapToUnitCircle"
     _defaults = {"time_period": "HourOfDay", "clean_keys": False}
+    dp_aware = True     # key union only
 
     def fit_columns(self, *cols, ds=None):
-        all_keys, colsm = [], []
+        colsm = []
         tp = self.params["time_period"]
-        for c, t in zip(cols, self.get_transient_features()):
-            keys = sorted({k for m in c.to_list() for k, v in (m or {}).items() if v is not None})
-            all_keys.append(keys)
+        all_keys = _present_keys(cols, "date", False)
+        for keys, t in zip(all_keys, self.get_transient_features()):
             for k in keys:
                 for d in ("x", "y"):
                     colsm.append(OpVectorColumnMetadata((t.name,), (t.type_name,), k, None, f"{d}_{tp}"))
@@ -351,23 +602,27 @@ class TextMapLenModel(VectorizerMixin, SequenceTransformer):
         self.keys = [list(k) for k in (keys or [])]
         self.clean_keys = clean_keys
 
-    def _block(self, ci, vals, fn):
-        keys = self.keys[ci]
-        b = np.zeros((len(vals), len(keys)))
-        for r, m in enumerate(vals):
-            for j, k in enumerate(keys):
-                b[r, j] = fn(_get(m, k, self.clean_keys))
-        return b
+    def _per_value(self, vocab: List[str]) -> np.ndarray:
+        """Token-length sum of each distinct value (``TextMapLenEstimator``)."""
+        return TU.tokenize_batch(vocab).char_lengths().astype(np.float64) if vocab else np.zeros(0)
 
-    def _len(self, v):
-        return float(sum(len(t) for t in TU.tokenize(v))) if isinstance(v, str) else 0.0
+    absent_value = 0.0
 
     def transform_columns(self, *cols, ds=None):
+        dev = default_device()
         n = len(cols[0]) if cols else 0
-        blocks = [self._block(ci, c.to_list(), self._len) for ci, c in enumerate(cols)]
-        dev = cols[0].device if cols else torch.device("cpu")
-        out = np.concatenate(blocks, 1) if blocks else np.zeros((n, 0))
-        return self._vec(torch.as_tensor(out, dtype=vector_dtype(dev), device=dev))
+        blocks = []
+        for ci, c in enumerate(cols):
+            coo = map_coo(c, "pivot", self.clean_keys, dev)
+            keys = self.keys[ci]
+            lut = torch.as_tensor(np.append(self._per_value(coo.vocab), self.absent_value), device=dev)
+            b = torch.full((n, len(keys)), self.absent_value, dtype=torch.float64, device=dev)
+            for j, tc in enumerate(_per_key_text_columns(coo, keys)):
+                cc = tc.codes.to(torch.int64)
+                b[:, j] = lut[torch.where(cc >= 0, cc, torch.full_like(cc, lut.numel() - 1))]
+            blocks.append(b)
+        out = torch.cat(blocks, 1) if blocks else torch.zeros(n, 0, dtype=torch.float64, device=dev)
+        return self._vec(out.to(vector_dtype(dev)))
 
     def ctor_args(self):
         return {"keys": self.keys, "cleanKeys": self.clean_keys}
@@ -379,22 +634,22 @@ class TextMapLenModel(VectorizerMixin, SequenceTransformer):
 @register_stage
 class TextMapNullModel(TextMapLenModel):
     operation_name = "textMapNull"
+    absent_value = 1.0
 
-    def _len(self, v):
-        return 0.0 if isinstance(v, str) and v else 1.0
+    def _per_value(self, vocab):
+        return np.asarray([0.0 if v else 1.0 for v in vocab], np.float64)
 
 
 class _TextMapKeysEstimator(VectorizerMixin, SequenceEstimator):
     model_cls = TextMapLenModel
     descriptor = "TextLen"
     _defaults = {"clean_keys": False}
+    dp_aware = True     # key union only
 
     def fit_columns(self, *cols, ds=None):
-        all_keys, colsm = [], []
-        for c, t in zip(cols, self.get_transient_features()):
-            keys = sorted({_clean_key(k, self.params["clean_keys"]) for m in c.to_list()
-                           for k, v in (m or {}).items() if v is not None})
-            all_keys.append(keys)
+        colsm = []
+        all_keys = _present_keys(cols, "pivot", self.params["clean_keys"])
+        for keys, t in zip(all_keys, self.get_transient_features()):
             for k in keys:
                 if self.descriptor == "TextLen":
                     colsm.append(OpVectorColumnMetadata((t.name,), (t.type_name,), k, None, "TextLen"))

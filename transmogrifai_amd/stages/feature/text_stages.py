@@ -298,11 +298,15 @@ class IDF(VectorizerMixin, UnaryEstimator):
     """Spark IDF: ``log((m + 1) / (df + 1))``, zeroed for terms with df < minDocFreq."""
     operation_name = "idf"
     _defaults = {"min_doc_freq": 0}
+    dp_aware = True     # document frequencies and the row count are all-reduced (one packed collective)
 
     def fit_columns(self, *cols, ds=None):
+        from ...parallel import dp
         x = cols[0].values
-        m = x.shape[0]
-        df = (x != 0).sum(0).to(torch.float64).cpu().numpy()
+        m_t, df_t = dp.sum_([torch.tensor([float(x.shape[0])], dtype=torch.float64, device=x.device),
+                             (x != 0).sum(0).to(torch.float64)])
+        m = float(m_t.item())
+        df = df_t.cpu().numpy()
         idf = np.log((m + 1.0) / (df + 1.0))
         idf[df < self.params["min_doc_freq"]] = 0.0
         if cols[0].metadata is not None:

@@ -401,7 +401,31 @@ class OPCollectionHashingVectorizer(VectorizerMixin, SequenceTransformer):
 
 
 # --------------------------------------------------------------------------------------- smart text
+def _capped_plus(a: Counter, b: Counter, max_card: int) -> Counter:
+    """``TextStats.additionHelper`` (SmartTextVectorizer.scala:231-235): once a map holds more than
+    ``max_card`` keys it stops absorbing others."""
+    if len(a) > max_card:
+        return a
+    if len(b) > max_card:
+        return b
+    out = Counter(a)
+    out.update(b)
+    return out
+
+
+def _prefix_cutoff(first_seen: np.ndarray, max_card: int) -> Optional[int]:
+    """Row (inclusive) after which a left fold of one-key maps under :func:`_capped_plus` is frozen: the row
+    of the ``max_card + 1``-th distinct key; ``None`` while there are at most ``max_card`` keys."""
+    if first_seen.size <= max_card:
+        return None
+    return int(np.partition(first_seen, max_card)[max_card])
+
+
 class TextStats:
+    """Value counts and length counts of one text feature (``TextStats``, SmartTextVectorizer.scala:200-300),
+    with the reference's capped monoid: :meth:`of_column` folds a partition's rows in order, :meth:`plus`
+    merges partitions (ranks) in order."""
+
     def __init__(self, value_counts: Counter, length_counts: Counter):
         self.value_counts = value_counts
         self.length_counts = length_counts
@@ -415,14 +439,106 @@ class TextStats:
         var = sum(v * (k - mean) ** 2 for k, v in self.length_counts.items()) / n
         return var ** 0.5
 
+    def plus(self, other: "TextStats", max_card: int) -> "TextStats":
+        return TextStats(_capped_plus(self.value_counts, other.value_counts, max_card),
+                         _capped_plus(self.length_counts, other.length_counts, max_card))
+
+    @staticmethod
+    def of_column(col: TextColumn, clean: bool, token_lengths: bool, max_card: int) -> "TextStats":
+        """The left fold ``rows.map(computeTextStats).reduce(plus)`` of one partition, computed from
+        per-value counts and first occurrences (device histogram over the dictionary codes): values seen
+        after the ``max_card + 1``-th distinct value are not counted (the reference's frozen map)."""
+        V = len(col.vocab)
+        if V == 0:
+            return TextStats(Counter(), Counter())
+        from ...ops.text import code_counts
+        cleaned = [TU.clean_string(v) if clean else v for v in col.vocab]
+        ids: Dict[str, int] = {}
+        lut = np.fromiter((ids.setdefault(v, len(ids)) for v in cleaned), dtype=np.int64, count=V)
+        full = code_counts([col.codes], [V])[0][:-1]
+        codes = col.codes
+        n = int(codes.shape[0])
+        first = None
+        if len(ids) > max_card:
+            c = codes.to(torch.int64)
+            ok = c >= 0
+            rid = torch.arange(n, device=c.device)
+            fv = torch.full((V,), n, dtype=torch.int64, device=c.device).scatter_reduce_(
+                0, c[ok], rid[ok], reduce="amin")
+            first = fv.cpu().numpy()
+            first_id = np.full(len(ids), n, np.int64)
+            np.minimum.at(first_id, lut, first)
+            cut = _prefix_cutoff(first_id, max_card)
+            counts = code_counts([codes[:cut + 1]], [V])[0][:-1]
+        else:
+            counts = full
+        vc: Counter = Counter()
+        for j in np.flatnonzero(counts):
+            vc[cleaned[j]] += int(counts[j])
+        # length counts: every row of the partition (their own cap applies to distinct lengths)
+        lc: Counter = Counter()
+        if token_lengths:
+            # TextTokenizer.tokenizeString with the default analyzer; each row's map folds its token lengths
+            # under the same cap (textStatsFromString)
+            tb = TU.tokenize_batch(col.vocab)
+            tl = tb.token_char_lengths()
+            rp = tb.row_ptr
+            maps = []
+            for j in range(V):
+                m: Counter = Counter()
+                for L in tl[rp[j]:rp[j + 1]]:
+                    m = _capped_plus(m, Counter({int(L): 1}), max_card)
+                maps.append(m)
+            present = [j for j in np.flatnonzero(full)]
+            union = set().union(*[maps[j].keys() for j in present]) if present else set()
+            if len(union) <= max_card:
+                for j in present:
+                    for L, c in maps[j].items():
+                        lc[L] += c * int(full[j])
+            else:               # the cap triggers: fold the rows in order (rare: > max_card token lengths)
+                for code in codes.cpu().numpy():
+                    if code >= 0:
+                        lc = _capped_plus(lc, maps[int(code)], max_card)
+            return TextStats(vc, lc)
+        else:
+            for j in np.flatnonzero(full):
+                lc[len(cleaned[j])] += int(full[j])
+        if len(lc) > max_card:
+            # same prefix rule over the rows' lengths (first occurrence of each length value)
+            if first is None:
+                c = codes.to(torch.int64)
+                ok = c >= 0
+                rid = torch.arange(n, device=c.device)
+                first = torch.full((V,), n, dtype=torch.int64, device=c.device).scatter_reduce_(
+                    0, c[ok], rid[ok], reduce="amin").cpu().numpy()
+            lens = np.fromiter((len(v) for v in cleaned), dtype=np.int64, count=V)
+            uniq, inv = np.unique(lens, return_inverse=True)
+            first_len = np.full(uniq.size, n, np.int64)
+            np.minimum.at(first_len, inv, first)
+            cut = _prefix_cutoff(first_len, max_card)
+            pc = code_counts([codes[:cut + 1]], [V])[0][:-1]
+            lc = Counter()
+            for j in np.flatnonzero(pc):
+                lc[int(lens[j])] += int(pc[j])
+        return TextStats(vc, lc)
+
+
+def reduce_text_stats(parts: Sequence[List["TextStats"]], max_card: int) -> List["TextStats"]:
+    """Merge per-partition (per-rank) stats lists in partition order."""
+    acc = list(parts[0])
+    for p in parts[1:]:
+        acc = [a.plus(b, max_card) for a, b in zip(acc, p)]
+    return acc
+
 
 @register_stage
 class SmartTextVectorizerModel(VectorizerMixin, SequenceTransformer):
     operation_name = "smartTxtVec"
 
     def __init__(self, methods=None, top_values=None, clean_text=True, track_nulls=True, hashing=None,
-                 track_text_len=False, min_token_length=1, to_lowercase=True, uid=None, **kw):
+                 track_text_len=False, min_token_length=1, to_lowercase=True, strip_html=False, uid=None, **kw):
         super().__init__(uid=uid, **kw)
+        self.strip_html = strip_html
         self.methods = list(methods or [])
         self.top_values = [list(t) for t in (top_values or [])]
         self.clean_text = clean_text
@@ -440,7 +556,8 @@ class SmartTextVectorizerModel(VectorizerMixin, SequenceTransformer):
         ign = [i for i, m in enumerate(self.methods) if m == "ignore"]
         rest = hsh + ign
         # one native tokenizer pass per hashed / ignored column, over its distinct values
-        toks = {i: TU.tokenize_batch(cols[i].vocab, self.to_lowercase, self.min_token_length) for i in rest}
+        toks = {i: TU.tokenize_batch([TU.strip_html(v) for v in cols[i].vocab] if self.strip_html else cols[i].vocab,
+                                     self.to_lowercase, self.min_token_length) for i in rest}
         blocks = []
         if piv:
             blocks.append(pivot_columns([cols[i] for i in piv], [self.top_values[i] for i in piv], self.clean_text,
@@ -465,7 +582,8 @@ class SmartTextVectorizerModel(VectorizerMixin, SequenceTransformer):
         return {"vectorizationMethods": self.methods, "topValues": self.top_values,
                 "shouldCleanText": self.clean_text, "shouldTrackNulls": self.track_nulls,
                 "hashingParams": self.hashing.to_json(), "trackTextLen": self.track_text_len,
-                "minTokenLength": self.min_token_length, "toLowercase": self.to_lowercase}
+                "minTokenLength": self.min_token_length, "toLowercase": self.to_lowercase,
+                "stripHtml": self.strip_html}
 
     def load_ctor_args(self, a):
         self.methods, self.top_values = a["vectorizationMethods"], a["topValues"]
@@ -474,6 +592,7 @@ class SmartTextVectorizerModel(VectorizerMixin, SequenceTransformer):
         self.track_text_len = a.get("trackTextLen", False)
         self.min_token_length = a.get("minTokenLength", 1)
         self.to_lowercase = a.get("toLowercase", True)
+        self.strip_html = a.get("stripHtml", False)
 
 
 def _vocab_lut(c: TextColumn, per_value: np.ndarray, null_value: float, dtype) -> torch.Tensor:
@@ -491,17 +610,25 @@ class SmartTextVectorizer(VectorizerMixin, SequenceEstimator):
     _defaults = {"max_cardinality": 1000, "top_k": 20, "min_support": 10, "clean_text": True, "track_nulls": True,
                  "num_features": 512, "hash_space_strategy": "auto", "prepend_feature_name": True,
                  "binary_freq": False, "coverage_pct": 0.90, "min_length_std_dev": 0.0, "track_text_len": False,
-                 "min_token_length": 1, "to_lowercase": True, "unseen_name": OTHER_STRING}
+                 "min_token_length": 1, "to_lowercase": True, "unseen_name": OTHER_STRING,
+                 "text_length_type": "FullEntry", "strip_html": False}
+    # Row-sharded fits: every rank folds its own rows into capped TextStats (<= max_cardinality + 1 values
+    # per feature) and the ranks' stats are merged in rank order -- one small object all-gather, the
+    # reference's ``valueStats.reduce(_ + _)`` (SmartTextVectorizer.scala:87-91) with ranks as partitions
+    dp_aware = True
 
     def fit_columns(self, *cols, ds=None):
+        from ...parallel import dp
         p = self.params
+        tlt = str(p["text_length_type"]).lower()
+        if tlt not in ("fullentry", "tokens"):
+            raise ValueError(f"textLengthType must be FullEntry or Tokens, got {p['text_length_type']!r}")
+        max_card = int(p["max_cardinality"])
+        local = [TextStats.of_column(c, p["clean_text"], tlt == "tokens", max_card) for c in cols]
+        stats_all = reduce_text_stats(dp.objects(local), max_card)
         methods, tops = [], []
-        for c in cols:
-            vc = _text_counts(c, p["clean_text"])
-            lc = Counter()
-            for v, cnt in vc.items():
-                lc[len(v)] += cnt
-            stats = TextStats(vc, lc)
+        for stats in stats_all:
+            vc = stats.value_counts
             total = sum(vc.values())
             filt = {k: v for k, v in vc.items() if v >= p["min_support"]}
             sv = sorted(filt.values(), reverse=True)
@@ -509,9 +636,9 @@ class SmartTextVectorizer(VectorizerMixin, SequenceEstimator):
             k = min(p["top_k"], cum.size)
             coverage = (cum[k - 1] / total) if (k > 0 and total > 0) else 0.0
             card = len(vc)
-            if card > p["max_cardinality"] and card > p["top_k"] and coverage >= p["coverage_pct"]:
+            if card > max_card and card > p["top_k"] and coverage >= p["coverage_pct"]:
                 m = "pivot"
-            elif card <= p["max_cardinality"]:
+            elif card <= max_card:
                 m = "pivot"
             elif stats.length_std < p["min_length_std_dev"]:
                 m = "ignore"
@@ -535,7 +662,7 @@ class SmartTextVectorizer(VectorizerMixin, SequenceEstimator):
         self.metadata["vector_metadata"] = self.vector_metadata(colsm)
         self.metadata["text_methods"] = methods
         return SmartTextVectorizerModel(methods, tops, p["clean_text"], p["track_nulls"], hp, p["track_text_len"],
-                                        p["min_token_length"], p["to_lowercase"])
+                                        p["min_token_length"], p["to_lowercase"], p["strip_html"])
 
 
 # --------------------------------------------------------------------------------------------- dates
@@ -674,17 +801,30 @@ class GeolocationVectorizerModel(VectorizerMixin, SequenceTransformer):
 class GeolocationVectorizer(VectorizerMixin, SequenceEstimator):
     operation_name = "vecGeo"
     _defaults = {"fill_with_constant": False, "fill_value": [0.0, 0.0, 0.0], "track_nulls": True}
+    # the geographic midpoint is a monoid of (unit-sphere x, y, z sums, count, max accuracy): partial sums
+    # are all-reduced in one collective, the accuracy max in another (GeolocationVectorizer.scala:87)
+    dp_aware = True
 
     def fit_columns(self, *cols, ds=None):
-        from ...features.aggregators import Event, GeolocationMidpoint
+        from ...features.aggregators import GeolocationMidpoint
+        from ...parallel import dp
         fills = []
+        sums, accs = [], []
         for c in cols:
+            v = c.values[c.valid].to(torch.float64)
+            lat, lon = torch.deg2rad(v[:, 0]), torch.deg2rad(v[:, 1])
+            xyz = torch.stack([torch.cos(lat) * torch.cos(lon), torch.cos(lat) * torch.sin(lon), torch.sin(lat)], 1)
+            sums.append(torch.cat([xyz.sum(0), torch.tensor([float(v.shape[0])], dtype=torch.float64,
+                                                              device=v.device)]))
+            accs.append(v[:, 2].max() if v.shape[0] else torch.tensor(0.0, dtype=torch.float64, device=v.device))
+        if cols:
+            S = dp.sum_([torch.stack(sums)])[0].cpu().numpy()
+            A = dp.max_(torch.stack(accs).clamp_min(0.0)).cpu().numpy()
+        for i, c in enumerate(cols):
             if self.params["fill_with_constant"]:
                 fills.append(list(self.params["fill_value"]))
                 continue
-            agg = GeolocationMidpoint()
-            vals = c.values[c.valid].cpu().numpy()
-            fills.append(agg.aggregate(Event(0, list(v)) for v in vals))
+            fills.append(GeolocationMidpoint().present((S[i, 0], S[i, 1], S[i, 2], int(S[i, 3]), float(A[i]))))
         cm = []
         for t in self.get_transient_features():
             cm += [col_meta(t, descriptor=nm) for nm in GEO_NAMES]

@@ -102,12 +102,16 @@ class TokenBatch:
     def counts(self) -> np.ndarray:
         return np.diff(self.row_ptr)
 
-    def char_lengths(self) -> np.ndarray:
-        """Per-string total token length in characters (UTF-8 continuation bytes excluded)."""
+    def token_char_lengths(self) -> np.ndarray:
+        """Per-token length in characters (UTF-8 continuation bytes excluded), flat over the batch."""
         lead = (self.data & 0xC0) != 0x80
         cum = np.zeros(self.data.size + 1, np.int64)
         np.cumsum(lead, out=cum[1:])
-        tok_chars = cum[self.tok_offs[1:]] - cum[self.tok_offs[:-1]]
+        return cum[self.tok_offs[1:]] - cum[self.tok_offs[:-1]]
+
+    def char_lengths(self) -> np.ndarray:
+        """Per-string total token length in characters (UTF-8 continuation bytes excluded)."""
+        tok_chars = self.token_char_lengths()
         tc = np.zeros(tok_chars.size + 1, np.int64)
         np.cumsum(tok_chars, out=tc[1:])
         return tc[self.row_ptr[1:]] - tc[self.row_ptr[:-1]]
