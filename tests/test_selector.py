@@ -174,3 +174,33 @@ def test_cv_validates_on_whole_folds_with_downsampled_training(monkeypatch):
     summ = m.get_origin_stage_of(pred).metadata["summary"]
     assert len(seen) == 3 and sum(seen) == n, seen          # the three folds cover every row
     assert summ["bestModelType"] == "OpLogisticRegression"
+
+
+def test_max_wait_bounds_a_running_learner():
+    """maxWait (OpValidator.scala:348) bounds a learner that is still running: its grid points are reported
+    failed and the other learners' results are kept."""
+    import time
+    from transmogrifai_amd.evaluators.evaluators import OpBinaryClassificationEvaluator
+    from transmogrifai_amd.models.base import register_learner, learner_class
+    from transmogrifai_amd.tuning import validators as V
+
+    base = learner_class("OpNaiveBayes")
+
+    @register_learner
+    class _SlowNB(base):
+        name = "_TestSlowNaiveBayes"
+
+        def fit_batch(self, X, y, jobs, context=None):
+            time.sleep(3.0)
+            return super().fit_batch(X, y, jobs, context)
+
+    g = torch.Generator().manual_seed(0)
+    X = torch.rand(400, 3, generator=g, dtype=torch.float64)
+    y = (X[:, 0] > 0.5).double()
+    cv = V.OpCrossValidation(num_folds=2, evaluator=OpBinaryClassificationEvaluator(), seed=1, max_wait=1.0)
+    t0 = time.time()
+    res = cv.validate([("OpNaiveBayes", [{"smoothing": 1.0}]), ("_TestSlowNaiveBayes", [{"smoothing": 1.0}])],
+                      X, y, torch.arange(400))
+    assert time.time() - t0 < 2.9
+    assert res.best_learner == "OpNaiveBayes"
+    assert any("_TestSlowNaiveBayes" in f and "maxWait" in f for f in res.failures)

@@ -160,7 +160,9 @@ class ModelSelector(BinaryEstimator):
         if self.best_estimator is not None:     # chosen by workflow-level CV
             res = self.best_estimator
         else:
-            res = self.validator.validate(self.models, X, y, row_ids, self.splitter, context=ctx)
+            from ..workflow.workflow import OpStep, step
+            with step(OpStep.CrossValidation):
+                res = self.validator.validate(self.models, X, y, row_ids, self.splitter, context=ctx)
         self.best = res
         # refit the winner on the prepared full training set
         learner = learner_class(res.best_learner)()

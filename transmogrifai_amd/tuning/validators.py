@@ -62,6 +62,7 @@ class ValidationResult:
 _COST_SCALE: Dict[str, float] = {"OpLogisticRegression": 8.4e-12, "OpRandomForestClassifier": 1.3e-12,
                                  "OpXGBoostClassifier": 8.0e-13}
 _DEFAULT_SCALE = 1.3e-12
+_UNBOUNDED_WAIT = 86400.0       # the reference default maxWait (1 day): no worker thread needed
 
 
 def _scaled_cost(learner: str, params: Dict, n: int, d: int) -> float:
@@ -184,7 +185,11 @@ class OpValidator:
             if li in spread:
                 ctx["par"] = par
             try:
-                res, fails = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, ctx)
+                if li not in spread and self.max_wait < _UNBOUNDED_WAIT:
+                    res, fails = self._fit_eval_bounded(lname, grid, mine, X, y, train_rows, val_rows, ctx,
+                                                        self.max_wait - (time.time() - t0))
+                else:
+                    res, fails = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, ctx)
             finally:
                 ctx.pop("par", None)
             results.update(res)
@@ -270,6 +275,32 @@ class OpValidator:
                     failures.extend(fails)
                     timings[lname] = timings.get(lname, 0.0) + time.time() - t2
         return self._select(models, results, len(splits), failures, timings, t0)
+
+    def _fit_eval_bounded(self, lname, grid, mine, X, y, train_rows, val_rows, ctx, remaining: float):
+        """:meth:`_fit_eval` under the ``maxWait`` deadline (``awaitResult(..., maxWait)``, OpValidator.scala:348):
+        the learner runs on a worker thread; if it has not returned when the deadline passes, its grid
+        points are reported failed and validation goes on with the other learners (the abandoned fits are
+        never read, as Spark abandons its futures). Only for learners whose jobs are local to this rank --
+        a spread learner's collectives must not be left half-way on one rank."""
+        import threading
+        box: Dict[str, Any] = {}
+
+        def work():
+            try:
+                box["out"] = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, dict(ctx))
+            except BaseException as e:          # noqa: BLE001  (re-raised below)
+                box["err"] = e
+
+        th = threading.Thread(target=work, name=f"fit-{lname}", daemon=True)
+        th.start()
+        th.join(max(0.0, remaining))
+        if th.is_alive():
+            log.warning("Model %s did not finish within maxWait=%ss; its %d fits are dropped", lname,
+                        self.max_wait, len(mine))
+            return {}, [f"{lname}: did not finish within maxWait={self.max_wait}s"]
+        if "err" in box:
+            raise box["err"]
+        return box["out"]
 
     def _fit_eval(self, lname, grid, mine, X, y, train_rows, val_rows, ctx):
         """Fit + score one learner's jobs as one batch. A failing batch is retried one grid point at a

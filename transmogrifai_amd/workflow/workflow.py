@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import json
 import logging
+import threading
 import time
 from typing import Dict, List, Optional, Sequence
 
@@ -38,20 +39,48 @@ class OpStep:
 
 class _Timer:
     """Wall time of a workflow step (``OpStep``) into ``sink``; the step is also the job group of the stage
-    metrics an active listener collects meanwhile (``utils/listener.py``)."""
+    metrics an active listener collects meanwhile (``utils/listener.py``). Steps nest: a step opened inside
+    another (the model selector's ``CrossValidation`` inside ``FeatureEngineering``) is charged to itself
+    only, as Spark's job groups are (ModelSelector.scala:148,207)."""
+
+    _local = threading.local()
 
     def __init__(self, sink: Dict[str, float], name: str):
         self.sink, self.name = sink, name
 
+    @classmethod
+    def _stack(cls) -> list:
+        st = getattr(cls._local, "stack", None)
+        if st is None:
+            st = cls._local.stack = []
+        return st
+
     def __enter__(self):
         from ..utils import listener as L
         self.t = time.time()
+        self.child = 0.0
         self.jg = L.job_group(str(self.name))
         self.jg.__enter__()
+        self._stack().append(self)
 
     def __exit__(self, *a):
         self.jg.__exit__(*a)
-        self.sink[self.name] = self.sink.get(self.name, 0.0) + time.time() - self.t
+        st = self._stack()
+        st.pop()
+        dt = time.time() - self.t
+        self.sink[self.name] = self.sink.get(self.name, 0.0) + dt - self.child
+        if st:
+            st[-1].child += dt
+
+
+def step(name: str):
+    """A nested ``OpStep`` timer charged to the innermost open workflow step's timings (no-op outside a
+    workflow fit)."""
+    st = _Timer._stack()
+    if not st:
+        from contextlib import nullcontext
+        return nullcontext()
+    return _Timer(st[-1].sink, name)
 
 
 class OpWorkflowCore:
