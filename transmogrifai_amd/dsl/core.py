@@ -512,3 +512,90 @@ def _lda(self, k: int = 10, max_iter: int = 20, seed: int = 0, **kw):
     """``RichVectorFeature.lda`` (``RichVectorFeature.scala:115``)."""
     from ..stages.feature.nlp_stages import OpLDA
     return OpLDA(k=k, max_iter=max_iter, seed=seed, **kw).set_input(self).get_output()
+
+
+# ------------------------------------------------------------------------- round-3 DSL completions
+@register(T.OPVector, "idf")
+def _idf(self, min_doc_freq: int = 0):
+    """``RichVectorFeature.idf`` (RichVectorFeature.scala:57)."""
+    from ..stages.feature.text_stages import IDF
+    return IDF(min_doc_freq=min_doc_freq).set_input(self).get_output()
+
+
+@register(T.OPVector, "random_forest")
+def _random_forest(self, label, max_depth: int = 5, max_bins: int = 32, min_instance_per_node: int = 1,
+                   min_info_gain: float = 0.0, sub_sampling_rate: float = 1.0, num_trees: int = 20,
+                   impurity: str = "entropy", seed: Optional[int] = None, thresholds=()):
+    """``RichVectorFeature.randomForest`` (RichVectorFeature.scala:78-100): an OpRandomForestClassifier on
+    (label, this vector)."""
+    import random
+    from ..models.trees import OpRandomForestClassifier
+    params = dict(max_depth=max_depth, max_bins=max_bins, min_instances_per_node=min_instance_per_node,
+                  min_info_gain=min_info_gain, subsampling_rate=sub_sampling_rate, num_trees=num_trees,
+                  impurity=str(impurity).lower(), seed=random.getrandbits(31) if seed is None else int(seed))
+    if thresholds:
+        params["thresholds"] = list(thresholds)
+    return OpRandomForestClassifier(**params).set_input(label, self).get_output()
+
+
+@register((T.RealNN, T.Real, T.Integral), "deindexed")
+def _deindexed(self, labels=(), unseen_name: str = "UnseenIndex", handle_invalid: str = "NoFilter"):
+    """``RichNumericFeature.deindexed`` (RichNumericFeature.scala:418-432): index -> label, labels from the
+    argument or from the string indexer that produced this feature."""
+    from ..stages.feature.indexers import OpIndexToString, OpIndexToStringNoFilter
+    if str(handle_invalid).lower() == "error":
+        return OpIndexToString(labels=list(labels)).set_input(self).get_output()
+    return OpIndexToStringNoFilter(labels=list(labels), unseen_name=unseen_name).set_input(self).get_output()
+
+
+@register(T.Text, "to_multi_pick_list")
+def _to_mpl(self):
+    """``RichTextFeature.toMultiPickList`` (RichTextFeature.scala:53)."""
+    from ..stages.feature.misc_stages import TextToMultiPickList
+    return TextToMultiPickList().set_input(self).get_output()
+
+
+@register(T.DateTime, "to_date_time_list")
+def _to_dt_list(self):
+    """``RichDateTimeFeature.toDateTimeList``."""
+    from ..stages.feature.misc_stages import DateToListTransformer
+    st = DateToListTransformer()
+    st.output_type = T.DateTimeList
+    return st.set_input(self).get_output()
+
+
+@register(T.Date, "to_date_list")
+def _to_date_list(self):
+    """``RichDateFeature.toDateList`` (RichDateFeature.scala:55)."""
+    from ..stages.feature.misc_stages import DateToListTransformer
+    return DateToListTransformer().set_input(self).get_output()
+
+
+@register(T.Phone, "is_valid_phone")
+def _is_valid_phone(self, region_code, country_codes=None, is_strict: bool = False, default_region: str = "US"):
+    """``RichTextFeature.isValidPhone(regionCode, ...)`` (RichTextFeature.scala:519-536): validity against
+    the region given by a region-code / country-name feature."""
+    from ..utils import phone as PH
+    if country_codes is not None:
+        PH.check_codes(country_codes)
+    return TS.IsValidPhoneNumber(default_region=default_region, strict=is_strict,
+                                 codes_and_countries=dict(country_codes) if country_codes else None) \
+        .set_input(self, region_code).get_output()
+
+
+@register(T.Phone, "parse_phone_with_region")
+def _parse_phone_region(self, region_code, country_codes=None, is_strict: bool = False, default_region: str = "US"):
+    """``RichTextFeature.parsePhone(regionCode, ...)``: E.164 form against the region feature."""
+    return TS.ParsePhoneNumberWithRegion(default_region=default_region, strict=is_strict,
+                                         codes_and_countries=dict(country_codes) if country_codes else None) \
+        .set_input(self, region_code).get_output()
+
+
+@register(T.Text, "to_ngram_similarity")
+def _ngram_text_alias(self, other, n_gram_size: int = 3, to_lowercase: bool = True):
+    return _ngram_text(self, other, n_gram_size, to_lowercase)
+
+
+@register(T.MultiPickList, "to_ngram_similarity")
+def _ngram_set_alias(self, other, n_gram_size: int = 3, to_lowercase: bool = True):
+    return _ngram_set(self, other, n_gram_size, to_lowercase)

@@ -295,7 +295,24 @@ class _GrowArgs(C.Structure):
                 ("csr_nf", C.c_int32), ("fp_rank", C.c_int32), ("fp_world", C.c_int32), ("fp_mlo", C.c_int32),
                 ("fp_mhi", C.c_int32), ("fp_olo", C.c_int32), ("fp_ohi", C.c_int32), ("fp_comm", C.c_void_p),
                 ("fp_exchange", C.c_void_p), ("fp_ctx", C.c_void_p), ("slot_base", C.c_int32),
-                ("XbT", C.c_void_p)]
+                ("XbT", C.c_void_p), ("gh", C.c_void_p), ("gh_alt", C.c_void_p), ("n_entries", C.c_int64)]
+
+
+def _stage_gh(rows: torch.Tensor, counts, jobs, t1f, t2f, qscale, stride: int) -> torch.Tensor:
+    """``[total, 2]`` int32: each root entry's quantised (q(w g), q(w h)) under its job's model scales -- the
+    histogram kernels' ``rintf((w * t) * qscale)`` in the same fp32 operation order (tree_kernels.hip
+    stage_row), so the histograms are bit-identical to gathering t1 / t2 per row."""
+    dev = rows.device
+    e = rows.to(torch.int64) & 0xFFFFFFFF
+    r = e & 0xFFFFFF
+    w = (e >> 24).to(torch.float32)
+    model = torch.repeat_interleave(torch.as_tensor([j.model for j in jobs], dtype=torch.int64, device=dev),
+                                    torch.as_tensor(counts, dtype=torch.int64, device=dev))
+    idx = model * int(stride) + r
+    qs = qscale.reshape(-1, qscale.shape[-1])[model]
+    g = torch.round((w * t1f.reshape(-1)[idx]) * qs[:, 0]).to(torch.int32)
+    h = torch.round((w * t2f.reshape(-1)[idx]) * qs[:, 1]).to(torch.int32)
+    return torch.stack([g, h], 1).contiguous()
 
 
 @dataclass
@@ -449,6 +466,11 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     rows_alt = torch.empty_like(rows)
     qscale, qinv = _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev)
     total = int(rows.numel())
+    gh = gh_alt = None
+    if on_gpu and mode == MODE_GH and total and t1f is not None and t2f is not None \
+            and os.environ.get("TMOG_GH_STAGE", "1") != "0":
+        gh = _stage_gh(rows, counts, jobs, t1f, t2f, qscale, stride)
+        gh_alt = torch.empty_like(gh)
     leaf_rows = torch.empty(max(total, 1), dtype=torch.int32, device=dev) if collect_leaves else None
     leaf_gid = torch.empty(max(total, 1), dtype=torch.int32, device=dev) if collect_leaves else None
     host = dict(
@@ -489,7 +511,8 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                   fp.olo if fpw else 0, fp.ohi if fpw else 0,
                   C.cast(fp_comm, C.c_void_p) if fp_comm is not None else None,
                   C.cast(fp_cb, C.c_void_p) if fp_cb is not None else None, None, int(slot_base),
-                  N.ptr(XbT) if (on_gpu and XbT is not None) else None)
+                  N.ptr(XbT) if (on_gpu and XbT is not None) else None,
+                  N.ptr(gh) if gh is not None else None, N.ptr(gh_alt) if gh_alt is not None else None, total)
     lib = N.hip() if on_gpu else N.host()
     fn = (lambda name: getattr(lib, f"tmog_hip_{name}")) if on_gpu else (lambda name: getattr(lib, f"tmog_{name}_cpu"))
     h = fn("grow_forest")(C.byref(a))

@@ -144,6 +144,12 @@ struct GrowArgs {
   // reads one split-column byte per row; from the feature-major copy the bytes of a node's rows share
   // cache lines (from Xb every byte pulls its own line)
   const uint8_t* XbT;
+  // GPU, MODE 2, optional: the entries' quantised statistics (int32 pairs q(w g), q(w h)), one per entry of
+  // rows / rows_alt (same positions); the partition moves them with their entries so the histogram items
+  // read them coalesced instead of gathering t1 / t2 by row id. n_entries = size of rows (and of these).
+  int32_t* gh;
+  int32_t* gh_alt;
+  int64_t n_entries;
 };
 
 // Feature-parallel split record, one per node and rank:

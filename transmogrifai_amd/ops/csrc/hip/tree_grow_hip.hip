@@ -24,7 +24,7 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
-                        hipStream_t stream);
+                        hipStream_t stream, const int32_t* gh);
 int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
                            const int64_t* out_off, const int64_t* size, int n, int64_t max_size, int64_t dense,
                            int per, int S, hipStream_t stream);
@@ -44,7 +44,7 @@ int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, 
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                              const int32_t* split_bin, const uint8_t* dl, const float* node_params,
                              const float* split_gain, int missing_bin, int64_t* cursors, const uint8_t* XbT, int64_t N,
-                             hipStream_t stream);
+                             hipStream_t stream, const int32_t* gh_in, int32_t* gh_out);
 int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
                           int32_t* out_gid, hipStream_t stream);
 }
@@ -162,6 +162,13 @@ struct GpuBackend {
                      int S) {
     kchk(tmog_hip_zero_segments(hist, off, size, n, mx, dense, per, S, sl.stream), "zero_segments");
   }
+  // staged statistics of the entry buffer position ``p`` points into (rows or rows_alt), or null
+  int32_t* gh_of(const uint32_t* p) const {
+    if (a.gh == nullptr || a.gh_alt == nullptr || a.mode != 2) return nullptr;
+    if (p >= a.rows && p < a.rows + a.n_entries) return a.gh + 2 * (p - a.rows);
+    if (p >= a.rows_alt && p < a.rows_alt + a.n_entries) return a.gh_alt + 2 * (p - a.rows_alt);
+    return nullptr;
+  }
   void hist_build(const tmog::GrowArgs& g, const uint32_t* rows, const void* items, int n_items, const int32_t* nfo,
                   const int32_t* flist, const int32_t* nmd, const int64_t* nho, int64_t* hist, int, const int64_t*,
                   const int64_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*, int Sc,
@@ -169,7 +176,7 @@ struct GpuBackend {
     if (n_items)
       kchk(tmog_hip_hist_build(g.Xb, g.F, rows, items, n_items, nfo, flist, nmd, nho, hist, g.B, g.mode, g.S, g.y,
                                g.t1, g.t2, g.stride, g.qscale, g.mode == 2 ? g.missing_bin : -1, g.csr_ptr,
-                               g.csr_col, Sc, n_wide, need_general, sl.stream),
+                               g.csr_col, Sc, n_wide, need_general, sl.stream, gh_of(rows)),
            "hist_build");
   }
   int stat_chunk(int B, int S) const { return tmog_hip_hist_stat_chunk(B, S); }
@@ -223,8 +230,11 @@ struct GpuBackend {
   void partition_fused(const tmog::GrowArgs& g, const uint32_t* rows, uint32_t* rows_alt, const void* items, int n,
                        const int64_t* nb, const int64_t* nc, const int32_t* feat, const int32_t* bin, const uint8_t* dl,
                        const float* params, const float* gain, int64_t* cursors) {
+    int32_t* gi = gh_of(rows);
+    int32_t* go = gh_of(rows_alt);
+    if ((gi == nullptr) != (go == nullptr)) gi = go = nullptr;
     kchk(tmog_hip_partition_fused(g.Xb, g.F, rows, rows_alt, items, n, nb, nc, feat, bin, dl, params, gain,
-                                  g.missing_bin, cursors, g.XbT, g.N, sl.stream),
+                                  g.missing_bin, cursors, g.XbT, g.N, sl.stream, gi, go),
          "partition_fused");
   }
   void partition_nodes(const tmog::GrowArgs&, const uint32_t*, uint32_t*, int, const int64_t*, const int64_t*,

@@ -141,7 +141,8 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
                                               const float* __restrict__ t2, int64_t stride,
                                               const float* __restrict__ qscale, int skip_bin,
                                               const int64_t* __restrict__ csr_ptr,
-                                              const uint16_t* __restrict__ csr_col, int* lds) {
+                                              const uint16_t* __restrict__ csr_col, int* lds,
+                                              const int2* __restrict__ gh) {
   const int nf = it.nf;
   int* a0 = lds;            // bin-0 sum of q(w g) per column
   int* a1 = lds + nf;       // bin-0 sum of q(w h)
@@ -162,26 +163,34 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
   // One-chunk-ahead pipeline (as in hist_wide_item): the next chunk's entry is loaded before this
   // chunk's list walk, its statistics and list bounds after the first batch of id loads.
   const int64_t step = (int64_t)nwaves * 64;
+  // staged statistics (gh != null): the entry's quantised (g, h) ride with the entry in node order, one
+  // coalesced 8-byte load instead of two scattered 4-byte gathers per row
+  const int2* ghp = gh ? gh + it.begin : nullptr;
   uint32_t e_n = 0;
   float g_n = 0.f, h_n = 0.f;
+  int2 q_n = make_int2(0, 0);
   int64_t p0_n = 0, p1_n = 0;
   if ((int64_t)wave * 64 < cnt) {
-    e_n = rp[min((int64_t)wave * 64 + lane, cnt - 1)];
+    const int64_t i0 = min((int64_t)wave * 64 + lane, cnt - 1);
+    e_n = rp[i0];
     const int64_t r = e_n & 0xFFFFFFu;
-    g_n = t1m[r]; h_n = t2m[r]; p0_n = csr_ptr[r]; p1_n = csr_ptr[r + 1];
+    if (ghp) q_n = ghp[i0];
+    else { g_n = t1m[r]; h_n = t2m[r]; }
+    p0_n = csr_ptr[r]; p1_n = csr_ptr[r + 1];
   }
   for (int64_t base = (int64_t)wave * 64; base < cnt; base += step) {
     const int nrows = (int)min((int64_t)64, cnt - base);
     const float wt = (float)(e_n >> 24);
     int4 mine;
     mine.x = (int)e_n;
-    mine.y = (int)rintf((wt * g_n) * qs[0]);
-    mine.z = (int)rintf((wt * h_n) * qs[1]);
+    mine.y = ghp ? q_n.x : (int)rintf((wt * g_n) * qs[0]);
+    mine.z = ghp ? q_n.y : (int)rintf((wt * h_n) * qs[1]);
     mine.w = 0;
     const int64_t q0 = p0_n;
     const int len = lane < nrows ? (int)(p1_n - p0_n) : 0;
     const bool more = base + step < cnt;             // wave-uniform
-    if (more) e_n = rp[min(base + step + lane, cnt - 1)];
+    const int64_t i_n = min(base + step + lane, cnt - 1);
+    if (more) e_n = rp[i_n];
     // Row records go through the wave's LDS stage (q(g), q(h), list start) + list length: the lane groups
     // read them with plain LDS loads (no cross-lane shuffles, whose sources must all be active) and keep
     // only the entry ids in registers across the id gathers.
@@ -213,7 +222,9 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
       __builtin_amdgcn_sched_barrier(0);
       if (j0 == 0 && more) {
         const int64_t r = e_n & 0xFFFFFFu;
-        g_n = t1m[r]; h_n = t2m[r]; p0_n = csr_ptr[r]; p1_n = csr_ptr[r + 1];
+        if (ghp) q_n = ghp[i_n];
+        else { g_n = t1m[r]; h_n = t2m[r]; }
+        p0_n = csr_ptr[r]; p1_n = csr_ptr[r + 1];
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -276,7 +287,7 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
                                                const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
                                                int B, const float* __restrict__ t1, const float* __restrict__ t2,
                                                int64_t stride, const float* __restrict__ qscale, int skip_bin,
-                                               int* lds) {
+                                               int* lds, const int2* __restrict__ gh) {
   const int FG = it.nf;
   const int ND = (FG + 3) >> 2;
   const int RPI = 64 / ND;
@@ -316,23 +327,33 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
   // chunk's bin gathers and its (g, h) right after them, so the dependent entry -> statistic -> bin
   // latency chain of a chunk overlaps the previous chunk's gathers and atomics instead of adding up.
   const int64_t step = (int64_t)nwaves * 64;
+  const int2* ghp = gh ? gh + it.begin : nullptr;   // staged (g, h): coalesced with the entries
   uint32_t e_n = 0;
   float g_n = 0.f, h_n = 0.f;
+  int2 q_n = make_int2(0, 0);
   if ((int64_t)wave * 64 < cnt) {
-    e_n = rp[min((int64_t)wave * 64 + lane, cnt - 1)];
-    g_n = t1m[e_n & 0xFFFFFFu];
-    h_n = t2m[e_n & 0xFFFFFFu];
+    const int64_t i0 = min((int64_t)wave * 64 + lane, cnt - 1);
+    e_n = rp[i0];
+    if (ghp) q_n = ghp[i0];
+    else {
+      g_n = t1m[e_n & 0xFFFFFFu];
+      h_n = t2m[e_n & 0xFFFFFFu];
+    }
   }
   for (int64_t base = (int64_t)wave * 64; base < cnt; base += step) {
     const int nrows = (int)min((int64_t)64, cnt - base);
     const float wt = (float)(e_n >> 24);
     int4 mine;
     mine.x = (int)e_n;
-    mine.y = (int)rintf((wt * g_n) * qs[0]);
-    mine.z = (int)rintf((wt * h_n) * qs[1]);
+    mine.y = ghp ? q_n.x : (int)rintf((wt * g_n) * qs[0]);
+    mine.z = ghp ? q_n.y : (int)rintf((wt * h_n) * qs[1]);
     mine.w = 0;
     const bool more = base + step < cnt;             // wave-uniform
-    if (more) e_n = rp[min(base + step + lane, cnt - 1)];
+    const int64_t i_n = min(base + step + lane, cnt - 1);
+    if (more) {
+      e_n = rp[i_n];
+      if (ghp) q_n = ghp[i_n];                 // independent of the entry: issued with it
+    }
     stage[lane] = make_int4(mine.y, mine.z, mine.x, 0);   // (q(g), q(h), entry): (g, h) 8-byte aligned
     if (sparse) {
       int a = lane < nrows ? mine.y : 0, b = lane < nrows ? mine.z : 0;
@@ -357,7 +378,7 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
 #pragma unroll
       for (int u = 0; u < kWideU; ++u) w[u] = __builtin_amdgcn_raw_buffer_load_b32(xrs, (int)off[u], 0, 0);
       __builtin_amdgcn_sched_barrier(0);       // keep the next chunk's statistic loads behind the gathers
-      if (more) {
+      if (more && !ghp) {
         g_n = t1m[e_n & 0xFFFFFFu];
         h_n = t2m[e_n & 0xFFFFFFu];
       }
@@ -430,12 +451,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
     int B, const float* __restrict__ t1, const float* __restrict__ t2, int64_t stride,
-    const float* __restrict__ qscale, int skip_bin) {
+    const float* __restrict__ qscale, int skip_bin, const int2* __restrict__ gh) {
   extern __shared__ int lds_w[];
   if (g_hist_debug & 2) return;
   const HistItem it = items[blockIdx.x];
   hist_wide_item(it, Xb, F, feat_list[node_feat_off[it.node] + it.fg0], rows, node_model, node_hist_off, hist, B,
-                 t1, t2, stride, qscale, skip_bin, lds_w);
+                 t1, t2, stride, qscale, skip_bin, lds_w, gh);
 }
 
 
@@ -448,7 +469,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
     int B, int S, const float* __restrict__ y, const float* __restrict__ t1, const float* __restrict__ t2,
     int64_t stride, const float* __restrict__ qscale, int skip_bin, const int64_t* __restrict__ csr_ptr,
-    const uint16_t* __restrict__ csr_col, int Sc) {
+    const uint16_t* __restrict__ csr_col, int Sc, const int2* __restrict__ gh) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
   const HistItem it = items[blockIdx.x];
   const int s0 = ((it.excl >> 8) & 0xFF) * Sc;   // statistic chunk of this item (excl bits 8..15)
@@ -459,12 +480,12 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   }
   if (MODE == 2 && (it.excl & 4)) {
     hist_csr_item(it, rows, node_model, node_hist_off, hist, B, S, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                  csr_col, lds);
+                  csr_col, lds, gh);
     return;
   }
   if (MODE == 2 && (it.excl & 16)) {
     hist_wide_item(it, Xb, F, feat_list[node_feat_off[it.node] + it.fg0], rows, node_model, node_hist_off, hist, B,
-                   t1, t2, stride, qscale, skip_bin, lds);
+                   t1, t2, stride, qscale, skip_bin, lds, gh);
     return;
   }
   if constexpr (!GEN) {
@@ -502,7 +523,13 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   for (int64_t base = (int64_t)wave * 64; base < cnt; base += (int64_t)nwaves * 64) {
     const int64_t ri = min(base + lane, cnt - 1);
     const int nrows = (int)min((int64_t)64, cnt - base);
-    const int4 mine = stage_row<MODE>(rp[ri], model, stride, y, t1, t2, qs);
+    int4 mine;
+    if (MODE == 2 && gh) {
+      const int2 q = gh[it.begin + ri];
+      mine = make_int4((int)rp[ri], q.x, q.y, 0);
+    } else {
+      mine = stage_row<MODE>(rp[ri], model, stride, y, t1, t2, qs);
+    }
     stage[lane] = mine;
     if (sparse) {
       // chunk totals: one wave reduction of the 64 staged (g, h) records, one LDS add per wave
@@ -1109,7 +1136,8 @@ __global__ void __launch_bounds__(256) partition_fused_kernel(
     const PartItem* __restrict__ items, const int64_t* __restrict__ node_begin, const int64_t* __restrict__ node_count,
     const int32_t* __restrict__ split_feat, const int32_t* __restrict__ split_bin, const uint8_t* __restrict__ dl,
     const float* __restrict__ node_params, const float* __restrict__ split_gain, int missing_bin,
-    unsigned long long* __restrict__ cursors, const uint8_t* __restrict__ XbT, int64_t Nt) {
+    unsigned long long* __restrict__ cursors, const uint8_t* __restrict__ XbT, int64_t Nt,
+    const int2* __restrict__ gh_in, int2* __restrict__ gh_out) {
   const PartItem it = items[blockIdx.x];
   const int j = it.node;
   const int f = split_feat[j], sb = split_bin[j];
@@ -1126,12 +1154,14 @@ __global__ void __launch_bounds__(256) partition_fused_kernel(
   const unsigned long long below = (1ull << lane) - 1ull;
   for (int64_t base = 0; base < it.count; base += (int64_t)blockDim.x * PART_U) {
     uint32_t e[PART_U];
+    int2 q[PART_U];
     bool vd[PART_U], lf[PART_U];
 #pragma unroll
     for (int u = 0; u < PART_U; ++u) {
       const int64_t i = base + (int64_t)u * blockDim.x + threadIdx.x;
       vd[u] = i < it.count;
       e[u] = rows_in[it.begin + (vd[u] ? i : 0)];     // unpredicated: row 0 of the item is valid
+      if (gh_in) q[u] = gh_in[it.begin + (vd[u] ? i : 0)];   // the staged (g, h) move with their entry
     }
     uint8_t bn[PART_U];
 #pragma unroll
@@ -1170,7 +1200,10 @@ __global__ void __launch_bounds__(256) partition_fused_kernel(
       // guarded: a slot outside the node's range (impossible unless the cursors were not reset) is
       // dropped; the host checks every node's left + right count against its size
       const int64_t pos = lf[u] ? nb + (int64_t)s_base[0] + lpos : nend - 1 - (int64_t)s_base[1] - (idx - lpos);
-      if (pos >= nb && pos < nend) rows_out[pos] = e[u];
+      if (pos >= nb && pos < nend) {
+        rows_out[pos] = e[u];
+        if (gh_in) gh_out[pos] = q[u];
+      }
     }
     __syncthreads();
   }
@@ -1464,8 +1497,10 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
-                        hipStream_t stream) {
+                        hipStream_t stream, const int32_t* gh_words) {
   if (n_items == 0) return 0;
+  const int2* gh = reinterpret_cast<const int2*>(gh_words);
+  if (gh && mode != 2) return -2;
   if (Sc <= 0 || Sc > S) Sc = S;
   size_t lds = (size_t)(((64 * (B * Sc + 1)) + 3) & ~3) * sizeof(int) + 4 * 64 * sizeof(int4) +
                TM_MAX_S * sizeof(int);
@@ -1490,10 +1525,10 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
     static const int occ = [] { const char* e = std::getenv("TMOG_HIST_WIDE_OCC"); return e ? std::atoi(e) : 6; }();
     if (occ >= 7)
       hipLaunchKernelGGL(hist_wide_kernel<7>, dim3(n_wide), dim3(256), lds, stream, Xb, F, rows, it, node_feat_off,
-                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin);
+                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin, gh);
     else
       hipLaunchKernelGGL(hist_wide_kernel<6>, dim3(n_wide), dim3(256), lds, stream, Xb, F, rows, it, node_feat_off,
-                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin);
+                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin, gh);
     it += n_wide;
     n_items -= n_wide;
     if (n_items == 0) return (int)hipGetLastError();
@@ -1501,18 +1536,20 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
   dim3 grid(n_items), block(256);
   if (mode == 0)
     hipLaunchKernelGGL(hist_build_kernel<0>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc,
+                       nullptr);
   else if (mode == 1)
     hipLaunchKernelGGL(hist_build_kernel<1>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
-                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc);
+                       node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc,
+                       nullptr);
   else if (need_general)
     hipLaunchKernelGGL(hist_build_kernel<2>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                       csr_col, Sc);
+                       csr_col, Sc, gh);
   else
     hipLaunchKernelGGL((hist_build_kernel<2, false>), grid, block, lds, stream, Xb, F, rows, it, node_feat_off,
                        feat_list, node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                       csr_col, Sc);
+                       csr_col, Sc, gh);
   return (int)hipGetLastError();
 }
 
@@ -1609,11 +1646,13 @@ int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, 
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                              const int32_t* split_bin, const uint8_t* dl, const float* node_params,
                              const float* split_gain, int missing_bin, int64_t* cursors, const uint8_t* XbT,
-                             int64_t N, hipStream_t stream) {
+                             int64_t N, hipStream_t stream, const int32_t* gh_in, int32_t* gh_out) {
   if (n_items == 0) return 0;
+  if ((gh_in != nullptr) != (gh_out != nullptr)) return -2;
   hipLaunchKernelGGL(partition_fused_kernel, dim3(n_items), dim3(256), 0, stream, Xb, F, rows_in, rows_out,
                      (const PartItem*)items, node_begin, node_count, split_feat, split_bin, dl, node_params,
-                     split_gain, missing_bin, (unsigned long long*)cursors, XbT, N);
+                     split_gain, missing_bin, (unsigned long long*)cursors, XbT, N,
+                     reinterpret_cast<const int2*>(gh_in), reinterpret_cast<int2*>(gh_out));
   return (int)hipGetLastError();
 }
 

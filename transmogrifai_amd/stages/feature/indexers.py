@@ -46,8 +46,17 @@ class OpStringIndexerNoFilter(UnaryEstimator):
     output_type = T.RealNN
     _defaults = {"unseen_name": "UnseenLabel"}
 
+    dp_aware = True     # value counts merged over the ranks (one object all-gather)
+
     def fit_columns(self, c, ds=None):
-        cnt = Counter(v for v in c.to_list() if v is not None)
+        from ...parallel import dp
+        if isinstance(c, TextColumn):
+            from ...ops.text import code_counts
+            n = code_counts([c.codes], [len(c.vocab)])[0][:-1] if c.vocab else []
+            cnt = Counter({v: int(k) for v, k in zip(c.vocab, n) if k})
+        else:
+            cnt = Counter(v for v in c.to_list() if v is not None)
+        cnt = dp.merge_counters([cnt])[0]
         labels = [v for v, _ in sorted(cnt.items(), key=lambda kv: (-kv[1], kv[0]))]
         self.metadata["labels"] = labels + [self.params["unseen_name"]]
         return OpStringIndexerNoFilterModel(labels, self.params["unseen_name"])
@@ -59,9 +68,38 @@ class OpIndexToStringNoFilter(UnaryTransformer):
     output_type = T.Text
     _defaults = {"labels": [], "unseen_name": "UnseenIndex"}
 
+    def _labels(self):
+        """Given labels, else the fitted string indexer's labels from the input's origin stage metadata
+        (``OpIndexToStringNoFilter``: "if not provided or empty, metadata from input feature is used")."""
+        labels = list(self.params["labels"] or [])
+        if not labels and self._inputs:
+            st = self._inputs[0].origin_stage
+            md = getattr(st, "metadata", {}) or {}
+            labels = list(md.get("labels") or [])
+            if labels and isinstance(st, OpStringIndexerNoFilter):
+                labels = labels[:-1]              # the indexer's unseen label is not an index target
+            if not labels:
+                labels = list(getattr(st, "labels", []) or [])
+        return labels
+
     def transform_fn(self, v):
-        labels = self.params["labels"]
+        labels = self._labels()
         if v is None:
             return self.params["unseen_name"]
         i = int(v)
         return labels[i] if 0 <= i < len(labels) else self.params["unseen_name"]
+
+
+@register_stage
+class OpIndexToString(OpIndexToStringNoFilter):
+    """Spark ``IndexToString``: an index without a label is an error (handleInvalid = Error)."""
+    operation_name = "idx2strStrict"
+
+    def transform_fn(self, v):
+        labels = self._labels()
+        if v is None:
+            raise ValueError("OpIndexToString: null index")
+        i = int(v)
+        if not 0 <= i < len(labels):
+            raise ValueError(f"OpIndexToString: index {i} has no label (labels: {len(labels)})")
+        return labels[i]

@@ -439,3 +439,33 @@ class MapTransformer(_FnStage):
 
     def transform_fn(self, v):
         return require_function(self.fn, f"transform function of {self.uid}")(v)
+
+
+@register_stage
+class TextToMultiPickList(UnaryTransformer):
+    """Text -> MultiPickList holding the one value (``TextToMultiPickList``, RichTextFeature.scala:53)."""
+    operation_name = "textToMultiPickList"
+    output_type = T.MultiPickList
+
+    def transform_fn(self, v):
+        return set() if v is None else {v}
+
+
+@register_stage
+class DateToListTransformer(UnaryTransformer):
+    """Date -> DateList (DateTime -> DateTimeList) of the one date (``RichDateFeatureLambdas.ToDateList``,
+    RichDateFeature.scala:55)."""
+    operation_name = "dateToList"
+    output_type = T.DateList
+
+    def transform_fn(self, v):
+        return [] if v is None else [int(v)]
+
+    def transform_columns(self, *cols, ds=None):
+        c = cols[0]
+        if isinstance(c, NumericColumn):
+            vals = c.values.to(torch.int64).cpu().numpy()
+            ok = c.valid.cpu().numpy()
+            return column_from_values(self.output_type, [[int(v)] if o else [] for v, o in zip(vals, ok)],
+                                      "cpu")
+        return super().transform_columns(*cols, ds=ds)

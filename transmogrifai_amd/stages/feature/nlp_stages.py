@@ -530,24 +530,20 @@ class MimeTypeDetector(UnaryTransformer):
         return detect_mime(v)
 
 
-def parse_phone(s: Optional[str], region: str = "US") -> Optional[str]:
-    """Normalize to E.164 for valid numbers of the default region (libphonenumber replacement)."""
-    if s is None or not is_valid_phone(s, region):
-        return None
-    digits = re.sub(r"\D", "", s)
-    if len(digits) == 10:
-        digits = "1" + digits
-    return "+" + digits
+def parse_phone(s: Optional[str], region: str = "US", strict: bool = False) -> Optional[str]:
+    """E.164 form of a valid number of ``region`` (``PhoneNumberParser.parse``; utils/phone.py)."""
+    from ...utils import phone as PH
+    return PH.parse(s, region, strict)
 
 
 @register_stage
 class ParsePhoneNumber(UnaryTransformer):
     operation_name = "parsePhone"
     output_type = T.Phone
-    _defaults = {"default_region": "US"}
+    _defaults = {"default_region": "US", "strict": False}
 
     def transform_fn(self, v):
-        return parse_phone(v, self.params["default_region"])
+        return parse_phone(v, self.params["default_region"], self.params.get("strict", False))
 
 
 @register_stage

@@ -23,7 +23,7 @@ from ...data.columns import NumericColumn, ObjectColumn, TextColumn, VectorColum
 from ...data.vector_metadata import OpVectorColumnMetadata
 from ...features import types as T
 from ...utils import text as TU
-from ..base import (OpEstimator, OpTransformer, SequenceTransformer, UnaryEstimator, UnaryTransformer,
+from ..base import (BinaryTransformer, OpEstimator, OpTransformer, SequenceTransformer, UnaryEstimator, UnaryTransformer,
                     register_stage)
 from .vectorizers import (HashingParams, VectorizerMixin, hash_metadata, col_meta)
 from ...ops import vector as V
@@ -102,21 +102,11 @@ def detect_mime(s):
         return "application/octet-stream"
 
 
-_PHONE_DIGITS = re.compile(r"\d")
-
-
 def is_valid_phone(s: Optional[str], region: str = "US", strict: bool = False) -> Optional[bool]:
-    """NANP validity for the default region (libphonenumber replacement; parity unpinned)."""
-    if s is None:
-        return None
-    digits = "".join(_PHONE_DIGITS.findall(s))
-    if s.strip().startswith("+") and not digits.startswith("1"):
-        return 7 <= len(digits) <= 15
-    if len(digits) == 11 and digits[0] == "1":
-        digits = digits[1:]
-    if len(digits) != 10:
-        return False
-    return digits[0] in "23456789" and digits[3] in "23456789"
+    """``PhoneNumberParser.validate`` for one region (``utils/phone.py``: numbering-plan table in place of
+    libphonenumber metadata; parity unpinned beyond the reference's test vectors)."""
+    from ...utils import phone as PH
+    return PH.validate(s, region, strict)
 
 
 @register_stage
@@ -165,13 +155,42 @@ class PhoneValidator(UnaryTransformer):
 
     def transform_columns(self, *cols, ds=None):
         c = cols[0]
-        if isinstance(c, TextColumn):
-            lut = np.array([1.0 if is_valid_phone(s) else 0.0 for s in c.vocab] + [0.0])
-            ok = c.codes >= 0
-            idx = torch.where(ok, c.codes.long(), torch.full_like(c.codes.long(), len(c.vocab)))
+        if isinstance(c, TextColumn):       # once per distinct value, then a device gather
+            res = [is_valid_phone(s, self.params["default_region"], self.params["strict"]) for s in c.vocab]
+            lut = np.array([1.0 if r else 0.0 for r in res] + [0.0])
+            okv = np.array([r is not None for r in res] + [False])
+            idx = torch.where(c.codes >= 0, c.codes.long(), torch.full_like(c.codes.long(), len(c.vocab)))
             vals = torch.as_tensor(lut, device=c.codes.device)[idx] > 0.5
-            return NumericColumn(T.Binary, vals, ok)
+            return NumericColumn(T.Binary, vals, torch.as_tensor(okv, device=c.codes.device)[idx])
         return super().transform_columns(*cols, ds=ds)
+
+
+@register_stage
+class IsValidPhoneNumber(BinaryTransformer):
+    """(Phone, region Text) -> Binary (``IsValidPhoneNumber``, PhoneNumberParser.scala:198-214): the region comes
+    from the region feature -- a region code, or the closest country name -- and ``+`` numbers are parsed
+    internationally."""
+    operation_name = "validatePhone"
+    output_type = T.Binary
+    _defaults = {"default_region": "US", "strict": False, "codes_and_countries": None}
+
+    def transform_fn(self, phone, region):
+        from ...utils import phone as PH
+        return PH.validate_with_region(phone, region, self.params["default_region"], self.params["strict"],
+                                       self.params["codes_and_countries"])
+
+
+@register_stage
+class ParsePhoneNumberWithRegion(BinaryTransformer):
+    """(Phone, region Text) -> Phone in E.164 (``ParsePhoneNumber``, PhoneNumberParser.scala:160-196)."""
+    operation_name = "parsePhone"
+    output_type = T.Phone
+    _defaults = {"default_region": "US", "strict": False, "codes_and_countries": None}
+
+    def transform_fn(self, phone, region):
+        from ...utils import phone as PH
+        return PH.parse_with_region(phone, region, self.params["default_region"], self.params["strict"],
+                                    self.params["codes_and_countries"])
 
 
 @register_stage
