@@ -145,3 +145,36 @@ def test_xgb_column_permutation_leaves_trees_unchanged(monkeypatch):
         outs.append(st)
     np.testing.assert_array_equal(np.asarray(outs[0]["forest"]["nodes"]), np.asarray(outs[1]["forest"]["nodes"]))
     np.testing.assert_array_equal(np.asarray(outs[0]["forest"]["value"]), np.asarray(outs[1]["forest"]["value"]))
+
+
+def test_linear_regression_normal_equations_match_row_objective(monkeypatch):
+    """solver auto / normal (d <= 4096) solves from one weighted Gram per fold: Cholesky without L1 (equal to
+    the closed-form ridge solution), OWL-QN on the Gram quadratic with L1 -- the same optimum as OWL-QN over
+    the rows (Spark WeightedLeastSquares vs L-BFGS, OpLinearRegression.scala:48-209)."""
+    import numpy as np
+    import torch
+    from transmogrifai_amd.models.base import FitJob, learner_class
+    g = torch.Generator().manual_seed(7)
+    N, d = 3000, 6
+    X = torch.randn(N, d, generator=g, dtype=torch.float64) * torch.tensor([1.0, 2.0, 0.5, 3.0, 1.0, 1.0])
+    X[:, 5] = 1.0                                          # constant column
+    y = X[:, :5] @ torch.tensor([1.0, -2.0, 0.5, 0.3, 0.0], dtype=torch.float64) + 0.3 * torch.randn(N, generator=g,
+                                                                                                      dtype=torch.float64)
+    rows = [torch.arange(0, 2000), torch.arange(1000, 3000)]
+    L = learner_class("OpLinearRegression")()
+    grid = [dict(reg_param=0.0), dict(reg_param=0.1), dict(reg_param=0.1, elastic_net_param=0.5),
+            dict(reg_param=0.05, elastic_net_param=1.0, fit_intercept=False), dict(reg_param=0.2, standardization=False)]
+    jobs = [FitJob(dict(L.defaults, max_iter=500, tol=1e-12, **p), r) for p in grid for r in rows]
+    normal = L.fit_batch(X, y, jobs)
+    assert all(s["solver"] == "normal" for s in normal)
+    monkeypatch.setenv("TMOG_LINREG_NORMAL", "0")
+    rowwise = L.fit_batch(X, y, jobs)
+    for a, b in zip(normal, rowwise):
+        np.testing.assert_allclose(a["coefficients"], b["coefficients"], atol=2e-4)
+        assert abs(a["intercept"] - b["intercept"]) < 2e-4
+    # no regularisation: ordinary least squares
+    Xr, yr = X[rows[0], :5].numpy(), y[rows[0]].numpy()
+    A = np.hstack([Xr, np.ones((len(Xr), 1))])
+    beta = np.linalg.lstsq(A, yr, rcond=None)[0]
+    np.testing.assert_allclose(normal[0]["coefficients"][:5], beta[:5], rtol=1e-8, atol=1e-10)
+    assert abs(normal[0]["coefficients"][5]) < 1e-12 and abs(normal[0]["intercept"] - beta[5]) < 1e-8

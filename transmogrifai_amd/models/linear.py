@@ -176,6 +176,70 @@ class MultinomialObjective:
         return f, g.reshape(U.shape)
 
 
+class GramObjective:
+    """The squared-loss objective of :class:`BatchedObjective` evaluated from each problem's weighted Gram
+    instead of the rows (Spark ``WeightedLeastSquares``: normal-equation statistics aggregated once, then
+    Cholesky, or its QuasiNewton solver when there is an L1 term -- LinearRegression.scala solver
+    ``auto`` / ``normal``, OpLinearRegression.scala:48-209).
+
+    In the standardised coordinates ``U = [u; u0]`` (``z_j = x_j / sigma_j``, target ``t = y / sigma_y``) the
+    data objective ``1/(2n) sum_i w_i (z_i . u + u0 - t_i)^2 + l2/2 |u|^2`` is the quadratic
+    ``1/2 U^T H U - g^T U + c`` with ``H = 1/n sum w [z,1][z,1]^T + diag(l2, .., 0)``, ``g = 1/n sum w t [z,1]``
+    and ``c = 1/(2n) sum w t^2`` -- identical values, so OWL-QN takes the same path for a d x d cost per
+    evaluation instead of a pass over the rows."""
+
+    def __init__(self, H, g, c, l2, fit_intercept):
+        self.H, self.g, self.c = H, g, c          # [P, d+1, d+1], [P, d+1], [P]
+        self.l2, self.fi = l2, fit_intercept
+        self.d = H.shape[1] - 1
+        self.passes = 0
+
+    def _q(self, U):
+        Ut = U.t()                                 # [P, d+1]
+        HU = torch.bmm(self.H, Ut[:, :, None])[:, :, 0]
+        return Ut, HU
+
+    def value(self, U):
+        self.passes += 1
+        Ut, HU = self._q(U)
+        return 0.5 * (Ut * HU).sum(1) - (self.g * Ut).sum(1) + self.c + 0.5 * self.l2 * (U[:self.d] ** 2).sum(0)
+
+    def value_grad(self, U):
+        self.passes += 1
+        Ut, HU = self._q(U)
+        f = 0.5 * (Ut * HU).sum(1) - (self.g * Ut).sum(1) + self.c + 0.5 * self.l2 * (U[:self.d] ** 2).sum(0)
+        G = (HU - self.g).t().contiguous()         # [d+1, P]
+        G[:self.d] += self.l2[None, :] * U[:self.d]
+        G[self.d] = torch.where(self.fi, G[self.d], torch.zeros_like(G[self.d]))
+        return f, G
+
+
+def _weighted_grams(X, y, jobs, par=None, chunk: int = 1 << 18):
+    """Augmented weighted Grams ``A^T diag(w) A`` (``A = [X, 1, y]``, float64) per distinct fold-weight
+    column of ``jobs``: ``(G [k, d+2, d+2], group of each job)``. Jobs that share their training rows (the
+    grid points of one CV fold) share one Gram; row chunks bound the fp64 temporaries."""
+    dev = X.device
+    N, d = X.shape
+    keys, group = {}, []
+    for j in jobs:
+        k = ("all",) if j.rows is None else (j.rows.data_ptr(), int(j.rows.numel()),
+                                             None if j.weights is None else j.weights.data_ptr())
+        group.append(keys.setdefault(k, len(keys)))
+    reps = {}
+    for j, g in zip(jobs, group):
+        reps.setdefault(g, j)
+    W = _fold_weights(N, [reps[g] for g in range(len(keys))], dev, torch.float64)      # [N, k]
+    G = torch.zeros(len(keys), d + 2, d + 2, dtype=torch.float64, device=dev)
+    yd = y.to(device=dev, dtype=torch.float64)
+    for a in range(0, N, chunk):
+        Xc = X[a:a + chunk].to(torch.float64)
+        A = torch.cat([Xc, torch.ones(Xc.shape[0], 1, dtype=torch.float64, device=dev), yd[a:a + chunk, None]], 1)
+        for g in range(len(keys)):
+            G[g] += A.t() @ (A * W[a:a + chunk, g:g + 1])
+    G = _psum(par, G)[0]
+    return G, group
+
+
 def _owlqn_direction_torch(U, g, l1, has_l1, S, Y, RHO, hist_n, m):
     """Pseudo-gradient, two-loop recursion, orthant projection (the spec of the HIP owlqn_direction_kernel)."""
     pg = torch.where(U > 0, g + l1, torch.where(U < 0, g - l1,
@@ -301,10 +365,20 @@ def _row_par(context):
     return par if (par is not None and par.world > 1) else None
 
 
+_STD_CHUNK = 1 << 18
+
+
 def _feature_std(X, W, par=None):
-    """Unbiased weighted std per column and problem (``[d, P]``) via two GEMMs."""
-    n, s1, s2 = _psum(par, W.sum(0).to(torch.float64), LK.gemm_t(X, W).to(torch.float64),
-                      LK.gemm_t(X * X, W).to(torch.float64))
+    """Unbiased weighted std per column and problem (``[d, P]``): ``X^T W`` and ``(X*X)^T W`` GEMMs over
+    row chunks, so the squared matrix is never materialised whole (was a full copy of the fold matrix)."""
+    d, P = X.shape[1], W.shape[1]
+    s1 = torch.zeros(d, P, dtype=torch.float64, device=X.device)
+    s2 = torch.zeros_like(s1)
+    for a in range(0, X.shape[0], _STD_CHUNK):
+        Xc, Wc = X[a:a + _STD_CHUNK], W[a:a + _STD_CHUNK]
+        s1 += LK.gemm_t(Xc, Wc).to(torch.float64)
+        s2 += LK.gemm_t(Xc * Xc, Wc).to(torch.float64)
+    n, s1, s2 = _psum(par, W.sum(0).to(torch.float64), s1, s2)
     mean = s1 / n.clamp_min(1)[None, :]
     var = (s2 - n[None, :] * mean * mean) / (n - 1).clamp_min(1)[None, :]
     return torch.sqrt(var.clamp_min(0)), mean
@@ -467,6 +541,9 @@ class LinearRegressionLearner(_LinearBase):
                 "standardization": True, "tol": 1e-6, "solver": "auto"}
     loss = "squared"
 
+    # Spark WeightedLeastSquares.MAX_NUM_FEATURES: solver "auto" takes the normal equations up to this width
+    NORMAL_MAX_FEATURES = 4096
+
     def fit_batch(self, X, y, jobs, context=None):
         X, y, jobs = compact_rows(X, y, jobs)
         dev = X.device
@@ -475,6 +552,10 @@ class LinearRegressionLearner(_LinearBase):
         if P == 0:
             return []
         par = _row_par(context)
+        solvers = {str(j.params.get("solver", "auto")).lower() for j in jobs}
+        if solvers <= {"normal"} or (solvers <= {"auto", "normal"} and d <= self.NORMAL_MAX_FEATURES) \
+                and os.environ.get("TMOG_LINREG_NORMAL", "1") != "0":
+            return self._fit_normal(X, y, jobs, par)
         X, y, W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs, par)
         yv = y.to(torch.float64)
         n, sy = _psum(par, W.sum(0).to(torch.float64), (W.to(torch.float64) * yv[:, None]).sum(0))
@@ -492,6 +573,88 @@ class LinearRegressionLearner(_LinearBase):
         icpt = (torch.where(fi, U[d], torch.zeros_like(U[d])) * ystd).cpu().numpy()
         return [{"coefficients": coef[p].copy(), "intercept": float(icpt[p]), "n_iter": int(iters[p])}
                 for p in range(P)]
+
+    def _fit_normal(self, X, y, jobs, par=None):
+        """Normal-equation path: one weighted Gram per CV fold (a single pass over the rows), then per
+        problem a Cholesky solve of ``(Cov_z + l2 I) u = cov_zt`` when there is no L1 term, else OWL-QN on
+        the Gram quadratic (:class:`GramObjective`) -- Spark WLS's Cholesky / QuasiNewton solvers. A
+        singular system (collinear columns without L2) falls back to the quadratic OWL-QN, as WLS does."""
+        dev = X.device
+        d = X.shape[1]
+        P = len(jobs)
+        G, group = _weighted_grams(X, y, jobs, par)
+        gi = torch.as_tensor(group, dtype=torch.int64, device=dev)
+        Gp = G[gi]                                               # [P, d+2, d+2]
+        n = Gp[:, d, d]
+        Sx, Sy = Gp[:, :d, d], Gp[:, d, d + 1]
+        Sxx, Sxy, Syy = Gp[:, :d, :d], Gp[:, :d, d + 1], Gp[:, d + 1, d + 1]
+        nm1 = (n - 1).clamp_min(1)
+        var = (torch.diagonal(Sxx, dim1=1, dim2=2) - Sx * Sx / n.clamp_min(1)[:, None]) / nm1[:, None]
+        std = torch.sqrt(var.clamp_min(0))                        # [P, d], as _feature_std
+        stdz = torch.as_tensor([bool(j.params.get("standardization", True)) for j in jobs], device=dev)
+        inv = torch.where(std > 0, 1.0 / std.clamp_min(1e-300), torch.zeros_like(std))
+        inv = torch.where(stdz[:, None], inv, (std > 0).to(inv.dtype))
+        ym = Sy / n.clamp_min(1)
+        ystd = torch.sqrt(((Syy - Sy * Sy / n.clamp_min(1)) / nm1).clamp_min(0)).clamp_min(1e-12)
+        reg = to_device([float(j.params.get("reg_param", 0.0)) for j in jobs], dev, np.float64)
+        en = to_device([float(j.params.get("elastic_net_param", 0.0)) for j in jobs], dev, np.float64)
+        fi = to_device([bool(j.params.get("fit_intercept", True)) for j in jobs], dev, np.bool_)
+        max_iter = to_device([int(j.params.get("max_iter", 100)) for j in jobs], dev, np.int64)
+        tol = to_device([float(j.params.get("tol", 1e-6)) for j in jobs], dev, np.float64)
+        eff = reg / ystd
+        l2, l1v = eff * (1 - en), eff * en
+        # quadratic in U = [u; u0] over z = x * inv, t = y / ystd
+        nn = n.clamp_min(1e-300)
+        S1 = torch.cat([Sx, n[:, None]], 1)                      # sum w [x, 1]
+        M = torch.zeros(P, d + 1, d + 1, dtype=torch.float64, device=dev)
+        M[:, :d, :d] = Sxx
+        M[:, :d, d] = Sx
+        M[:, d, :d] = Sx
+        M[:, d, d] = n
+        sc = torch.cat([inv, torch.ones(P, 1, dtype=torch.float64, device=dev)], 1)     # z = x * inv, 1
+        H = M * sc[:, :, None] * sc[:, None, :] / nn[:, None, None]
+        gvec = torch.cat([Sxy, Sy[:, None]], 1) * sc / (nn * ystd)[:, None]
+        c = 0.5 * Syy / (nn * ystd * ystd)
+        # no intercept: the intercept coordinate is pinned to 0 (row / column cleared, unit diagonal)
+        nofi = ~fi
+        H[nofi, d, :] = 0.0
+        H[nofi, :, d] = 0.0
+        H[nofi, d, d] = 1.0
+        gvec[nofi, d] = 0.0
+        del S1
+        U = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)
+        iters = torch.zeros(P, dtype=torch.int64, device=dev)
+        exact = (l1v <= 0)
+        solved = torch.zeros(P, dtype=torch.bool, device=dev)
+        if bool(exact.any()):
+            A = H[exact].clone()
+            A[:, torch.arange(d), torch.arange(d)] += l2[exact][:, None]
+            # zero-variance columns (z = 0): keep their coefficient at 0
+            dead = torch.diagonal(A, dim1=1, dim2=2)[:, :d] <= 0
+            A[:, torch.arange(d), torch.arange(d)] += dead.to(A.dtype)
+            L, info = torch.linalg.cholesky_ex(A)
+            ok = info == 0
+            if bool(ok.any()):
+                sol = torch.cholesky_solve(gvec[exact][ok][:, :, None], L[ok])[:, :, 0]
+                idx = torch.nonzero(exact).reshape(-1)[ok]
+                U[:, idx] = sol.t()
+                solved[idx] = True
+        rest = ~solved
+        if bool(rest.any()):
+            r = torch.nonzero(rest).reshape(-1)
+            obj = GramObjective(H[r], gvec[r], c[r], l2[r], fi[r])
+            U0 = torch.zeros(d + 1, int(r.numel()), dtype=torch.float64, device=dev)
+            U0[d] = torch.where(fi[r], ym[r] / ystd[r], torch.zeros_like(ym[r]))
+            l1 = torch.zeros(d + 1, int(r.numel()), dtype=torch.float64, device=dev)
+            l1[:d] = l1v[r][None, :]
+            Ur, it, _ = owlqn_batched(obj, U0, l1, max_iter[r], tol[r])
+            U[:, r] = Ur
+            iters[r] = it
+        coef = (U[:d] * inv.t() * ystd[None, :]).t().cpu().numpy()
+        icpt = (torch.where(fi, U[d], torch.zeros_like(U[d])) * ystd).cpu().numpy()
+        it = iters.cpu().numpy()
+        return [{"coefficients": coef[p].copy(), "intercept": float(icpt[p]), "n_iter": int(it[p]),
+                 "solver": "normal"} for p in range(P)]
 
     def predict(self, state, X, context=None):
         c = torch.as_tensor(state["coefficients"], dtype=X.dtype, device=X.device)
