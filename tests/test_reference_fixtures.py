@@ -172,3 +172,29 @@ def test_titanic_default_selector_holdout_in_readme_neighbourhood():
     # README.md:62-64 range 0.675 .. 0.810 -- our random split differs, so pin the neighbourhood
     assert 0.75 <= ho <= 0.97, ho
     assert len(summ["validationResults"]) == 28
+
+
+def test_titanic_simple_lr_only_pinned():
+    """``OpTitanicSimple`` as the reference runs it: withTrainValidationSplit, LR only
+    (OpTitanicSimple.scala:135-136). Seeded hold-out AuPR pinned to +-0.03 and the top insights of
+    README.md:97-110 (sex and pClass lead; "sex = female" is absent because the current SanityChecker drops the
+    later of two features correlated above maxFeatureCorr = 0.99 -- DerivedFeatureFilterUtils.scala:224 -- so
+    only "sex = Male" remains, carrying the same |correlation|)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples"))
+    import titanic_simple
+    model, metrics = titanic_simple.main([titanic_simple.DEFAULT_CSV, "--quiet", "--seed=42"])
+    summ = model.get_origin_stage_of(titanic_simple.LAST_PREDICTION).metadata["summary"]
+    assert summ["bestModelType"] == "OpLogisticRegression"
+    assert summ["validationType"] == "TrainValidationSplit"
+    assert len(summ["validationResults"]) == 8
+    ho = summ["holdoutEvaluation"]["AuPR"]
+    assert abs(ho - 0.7967) <= 0.03, ho
+    txt = model.summary_pretty()
+    neg = txt[txt.index("Top Negative Correlations"):]
+    neg = neg[:neg.index("Top Contributions")]
+    assert "sex(sex = Male)" in neg and "pClass(pClass = 3)" in neg
+    pos = txt[txt.index("Top Positive Correlations"):txt.index("Top Negative Correlations")]
+    assert "pClass(pClass = 1)" in pos and "cabin(cabin = other)" in pos
+    sc = next(st for st in model.stages if "dropped" in (st.metadata.get("summary") or {}))
+    assert any("sex_Female" in d for d in sc.metadata["summary"]["dropped"])
