@@ -42,3 +42,22 @@ def test_language_aware_tokenizer():
     plain = TextTokenizer().set_input(t)
     check_transformer(plain, ds, expected=[["l'amour", "de", "la", "vie", "et", "le", "goût", "des", "choses"], [],
                                            ["cat", "dog"]])
+
+
+def test_porter_stemmer_reference_vectors():
+    """Porter (1980) examples, tartarus reference implementation (Lucene PorterStemFilter)."""
+    from transmogrifai_amd.utils.stemmer import porter_stem
+    pairs = {"caresses": "caress", "ponies": "poni", "ties": "ti", "cats": "cat", "agreed": "agre",
+             "plastered": "plaster", "motoring": "motor", "conflated": "conflat", "sized": "size",
+             "hopping": "hop", "falling": "fall", "filing": "file", "happy": "happi", "relational": "relat",
+             "conditional": "condit", "digitizer": "digit", "vietnamization": "vietnam", "hopefulness": "hope",
+             "sensibiliti": "sensibl", "electrical": "electr", "adjustable": "adjust", "adoption": "adopt",
+             "homologous": "homolog", "bowdlerize": "bowdler", "cease": "ceas", "controll": "control",
+             "generalizations": "gener", "oscillators": "oscil", "running": "run", "is": "is"}
+    assert {w: porter_stem(w) for w in pairs} == pairs
+
+
+def test_english_analyzer_stems_unknown_does_not():
+    from transmogrifai_amd.utils import lang as L
+    assert L.analyze("The runners were running to John's houses", "en") == ["runner", "run", "john", "hous"]
+    assert "running" in L.analyze("The runners were running", "Unknown")

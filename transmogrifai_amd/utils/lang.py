@@ -6,9 +6,10 @@ per-language Lucene analyzers of ``LuceneTextAnalyzer.scala:87-236``; SURVEY.md 
   Hebrew, Devanagari, Thai, Hangul, kana -> ja, Han only -> zh); Latin-script text by the share of
   each language's most frequent function words among its tokens (a stop-word profile in place of
   Optimaize's n-gram profiles, which are not available offline).
-* :func:`analyze` -- the reference's per-language analysis minus stemming: the language's stop words,
-  elision stripping for French / Italian / Catalan (``l'amour`` -> ``amour``, Lucene ElisionFilter),
-  on top of the StandardAnalyzer word rules of :func:`utils.text.analyze`.
+* :func:`analyze` -- the reference's per-language analysis: the language's stop words, elision stripping for
+  French / Italian / Catalan (``l'amour`` -> ``amour``, Lucene ElisionFilter), English possessive removal
+  and Porter stemming (``utils/stemmer.py``, Lucene EnglishAnalyzer), on top of the StandardAnalyzer word
+  rules of :func:`utils.text.analyze`. Other languages' Snowball / light stemmers are not reproduced.
 """
 from __future__ import annotations
 
@@ -152,4 +153,10 @@ def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_t
             out.append(t)
         toks = out
     sw = STOPWORDS[lang]
+    if language == "en":
+        # EnglishAnalyzer: possessive removal, stop words, Porter stemming (the default, unknown-language
+        # StandardAnalyzer does not stem)
+        from .stemmer import english_possessive, porter_stem
+        toks = [english_possessive(t) for t in toks]
+        return [porter_stem(t) for t in toks if t not in sw and len(t) >= min_token_length]
     return [t for t in toks if t not in sw and len(t) >= min_token_length]
