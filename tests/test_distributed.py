@@ -222,3 +222,23 @@ def test_grid_sharded_selector_matches_single_process(tmp_path):
     assert r0["n_validation_results"] == single["n_validation_results"]
     assert r0["best"] == single["best"]
     assert abs(r0["holdout_aupr"] - single["holdout_aupr"]) < 1e-9
+
+
+def _wcv(rank, world):
+    """Workflow-level CV on 2 ranks: the stacked fold jobs are LPT-sharded over the ranks."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_workflow_cv as W
+    _, _, summ = W._train(True, W._records())
+    return {"vr": [v["metricValues"]["AuPR"] for v in summ["validationResults"]], "best": summ["bestModelType"],
+            "params": summ["bestModelParameters"]}
+
+
+def test_workflow_cv_two_ranks_matches_one(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_workflow_cv as W
+    _, _, summ = W._train(True, W._records())
+    one = [v["metricValues"]["AuPR"] for v in summ["validationResults"]]
+    r0, r1 = _run("_wcv", tmp_path)
+    assert r0 == r1
+    np.testing.assert_allclose(r0["vr"], one, rtol=0, atol=1e-12)
+    assert r0["best"] == summ["bestModelType"]

@@ -206,3 +206,30 @@ def _fp_one_rank(dev):
         a = TE.grow_forest(Xb2, spec2.n_bins, jobs2, mode=mode, kind=kind, B=32, **extra)
         b = TE.grow_forest(Xb2, spec2.n_bins, jobs2, mode=mode, kind=kind, B=32, fp=fp2, **extra)
         assert np.array_equal(a.nodes, b.nodes) and np.array_equal(a.value, b.value)
+
+
+def _linreg_normal_rp(rank, world):
+    from transmogrifai_amd.parallel.learner_parallel import LearnerParallel
+    return _linreg_normal(LearnerParallel())
+
+
+def _linreg_normal(par):
+    from transmogrifai_amd.models.base import FitJob, learner_class
+    X, _ = _data(n=2000, d=12, seed=3)
+    X = X.double()
+    yr = X[:, 0] * 2.0 - X[:, 4] + 0.1 * torch.randn(X.shape[0], generator=torch.Generator().manual_seed(1),
+                                                     dtype=torch.float64)
+    rows = [torch.arange(0, 1500), torch.arange(500, 2000)]
+    ctx = {"par": par} if par is not None else {}
+    lin = learner_class("OpLinearRegression")()
+    st = lin.fit_batch(X, yr, [FitJob(dict(lin.defaults, reg_param=rp, elastic_net_param=en, max_iter=100), r)
+                               for rp, en in ((0.05, 0.0), (0.05, 0.5)) for r in rows], context=ctx)
+    return [s["coefficients"].tolist() + [s["intercept"]] for s in st]
+
+
+def test_row_parallel_normal_equations(tmp_path):
+    """The normal-equation path all-reduces each rank's slice of the fold Grams (not the whole Gram per rank)."""
+    ref = _linreg_normal(None)
+    outs = _run("_linreg_normal_rp", tmp_path, 2)
+    assert outs[0] == outs[1]
+    np.testing.assert_allclose(np.asarray(outs[0]), np.asarray(ref), rtol=0, atol=1e-6)

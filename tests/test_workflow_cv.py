@@ -91,3 +91,29 @@ def test_workflow_cv_without_label_stages_matches_plain_cv():
         m = (wf.with_workflow_cv() if cv else wf).train()
         res.append(m.get_origin_stage_of(pred).metadata["summary"]["validationResults"][0]["metricValues"]["AuPR"])
     assert res[0] == pytest.approx(res[1], rel=1e-9)
+
+
+def test_workflow_cv_batches_folds_in_one_fit(monkeypatch):
+    """The fold matrices are stacked (columns aligned by their metadata) and every learner fits all of its
+    (grid point x fold) jobs in one fit_batch: k times fewer learner launches, the same per-fold metrics as
+    validating fold by fold."""
+    from transmogrifai_amd.models.linear import LogisticRegressionLearner
+    recs = _records()
+    calls = []
+    orig = LogisticRegressionLearner.fit_batch
+
+    def counting(self, X, y, jobs, context=None):
+        calls.append(len(jobs))
+        return orig(self, X, y, jobs, context)
+    monkeypatch.setattr(LogisticRegressionLearner, "fit_batch", counting)
+    _, _, batched = _train(True, recs)
+    n_batched = list(calls)
+    calls.clear()
+    monkeypatch.setenv("TMOG_WCV_BATCHED", "0")
+    _, _, per_fold = _train(True, recs)
+    n_per_fold = list(calls)
+    # validation: one call of 3 grid x 2 folds jobs instead of one call per fold (+ the refit in both)
+    assert n_batched[0] == 6 and n_per_fold[:2] == [3, 3]
+    a = [v["metricValues"]["AuPR"] for v in batched["validationResults"]]
+    b = [v["metricValues"]["AuPR"] for v in per_fold["validationResults"]]
+    assert max(abs(x - y) for x, y in zip(a, b)) < 2e-3, (a, b)

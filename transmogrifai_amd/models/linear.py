@@ -229,8 +229,12 @@ def _weighted_grams(X, y, jobs, par=None, chunk: int = 1 << 18):
     for j, g in zip(jobs, group):
         reps.setdefault(g, j)
     W = _fold_weights(N, [reps[g] for g in range(len(keys))], dev, torch.float64)      # [N, k]
-    G = torch.zeros(len(keys), d + 2, d + 2, dtype=torch.float64, device=dev)
     yd = y.to(device=dev, dtype=torch.float64)
+    if par is not None:         # row-parallel: this rank's slice of the (replicated) rows, sums all-reduced
+        sl = par.row_slice(N)
+        X, W, yd = X[sl], W[sl], yd[sl]
+        N = int(X.shape[0])
+    G = torch.zeros(len(keys), d + 2, d + 2, dtype=torch.float64, device=dev)
     for a in range(0, N, chunk):
         Xc = X[a:a + chunk].to(torch.float64)
         A = torch.cat([Xc, torch.ones(Xc.shape[0], 1, dtype=torch.float64, device=dev), yd[a:a + chunk, None]], 1)

@@ -98,6 +98,18 @@ def _job_cost(learner: str, params: Dict, n: int, d: int) -> float:
     return float(n * d)
 
 
+def _fold_alignment(fitted, features_name: str, data):
+    """``(kept input columns, input width)`` when the fold's feature vector is the output of a
+    feature-dropping SanityChecker over a vector every fold shares, else ``None``."""
+    from ..stages.preparators.sanity_checker import SanityCheckerModel
+    st = next((s for s in fitted if s.get_output_feature_name() == features_name), None)
+    if isinstance(st, SanityCheckerModel) and st.remove_bad_features and st.indices_to_keep is not None:
+        in_name = st.get_input_features()[1].name
+        if in_name in data:
+            return list(st.indices_to_keep), int(data[in_name].width)
+    return None
+
+
 class OpValidator:
     validation_type = "CrossValidation"
 
@@ -136,6 +148,12 @@ class OpValidator:
             idx = torch.nonzero(keep).reshape(-1)
             train_rows.append((idx, None if weights is None else weights[idx]))
             val_rows.append(torch.nonzero(va).reshape(-1))
+        return self._run(models, X, y, train_rows, val_rows, len(splits), t0, context)
+
+    def _run(self, models, X, y, train_rows, val_rows, n_folds: int, t0: float, context=None) -> ValidationResult:
+        """Fit and score every (learner, grid point, fold) job on the fold row sets of ``X`` -- jobs of the
+        intra-job-parallel learners on every rank, the others LPT-sharded over the ranks -- and select."""
+        splits = range(n_folds)
         # all (learner, grid, fold) jobs
         jobs = []
         for li, (lname, grid) in enumerate(models):
@@ -210,7 +228,7 @@ class OpValidator:
             for k, v in tm.items():
                 timings[k] = max(timings.get(k, 0.0), v)
         _calibrate(models, jobs, owner, timings, n_tr, X.shape[1])
-        return self._select(models, allres, len(splits), allfail, timings, t0)
+        return self._select(models, allres, n_folds, allfail, timings, t0)
 
     def validate_with_dag(self, models: Sequence[Tuple[str, Sequence[Dict]]], data, label_name: str,
                           features_name: str, during, splitter: Optional[Splitter] = None) -> ValidationResult:
@@ -229,6 +247,27 @@ class OpValidator:
         results: Dict[Tuple[int, int, int], float] = {}
         failures: List[str] = []
         timings: Dict[str, float] = {}
+        # Batched path: the during DAG is fitted per fold, then the fold matrices -- aligned on the columns of
+        # the during SanityChecker's input, a column dropped in a fold being all-zero in that fold's rows --
+        # are stacked and every learner trains all of its (grid point x fold) jobs in ONE fit_batch, sharded
+        # over the ranks as in validate (k-fold fewer learner launches, no redundant work per rank).
+        if os.environ.get("TMOG_WCV_BATCHED", "1") != "0":
+            folds = []
+            for k, (tr, va) in enumerate(splits):
+                ti = torch.nonzero(tr).reshape(-1)
+                vi = torch.nonzero(va).reshape(-1)
+                t1 = time.time()
+                train_k, val_k, fitted = fit_and_transform_dag(copy_dag(during), data.take(ti), data.take(vi))
+                timings[f"fold{k}:dag"] = time.time() - t1
+                folds.append((train_k, val_k, _fold_alignment(fitted, features_name, data)))
+            stacked = self._stack_folds(folds, label_name, features_name, splitter)
+            if stacked is not None:
+                X, y, train_rows, val_rows = stacked
+                with dp.local_only():
+                    res = self._run(models, X, y, train_rows, val_rows, len(splits), t0)
+                res.timings.update(timings)
+                return res
+            log.warning("workflow CV: fold feature matrices cannot be aligned; validating fold by fold")
         for k, (tr, va) in enumerate(splits):
             ti = torch.nonzero(tr).reshape(-1)
             vi = torch.nonzero(va).reshape(-1)
@@ -275,6 +314,85 @@ class OpValidator:
                     failures.extend(fails)
                     timings[lname] = timings.get(lname, 0.0) + time.time() - t2
         return self._select(models, results, len(splits), failures, timings, t0)
+
+    def _fold_rows(self, k, rid_t, yt, rid_v, yv, nt, nv, dtype, dev, splitter):
+        """(training positions, weights) and validation positions of fold ``k`` inside its block."""
+        keep = torch.arange(nt, device=dev)
+        weights = None
+        if splitter is not None:
+            if hasattr(splitter, "weights"):
+                w = splitter.weights(rid_t, yt.to(dtype), stream=11 + k)
+                keep = torch.nonzero(w > 0).reshape(-1)
+                weights = w[keep]
+            else:
+                keep = torch.nonzero(splitter.validation_prepare(rid_t, yt.to(dtype), stream=11 + k)).reshape(-1)
+        # applyDAG (OpValidator.scala:266-271) prepares the DAG-transformed validation part with the
+        # splitter too (an up-sampled row counts once per copy)
+        vsel = torch.arange(nv, device=dev)
+        if splitter is not None:
+            yvv = yv.to(dtype)
+            if hasattr(splitter, "weights"):
+                vsel = torch.repeat_interleave(vsel, splitter.weights(rid_v, yvv, stream=41 + k).to(dev))
+            else:
+                vsel = torch.nonzero(splitter.validation_prepare(rid_v, yvv, stream=41 + k)).reshape(-1)
+        return (keep, weights), vsel + nt
+
+    def _stack_folds(self, folds, label_name, features_name, splitter):
+        """One matrix holding every fold's (train + validation) rows, the fold blocks one after another, and
+        the per-fold row sets in it; ``None`` when the fold matrices have different columns that cannot be
+        aligned."""
+        from ..parallel import dp
+        aligns = [a for _, _, a in folds]
+        widths = [int(tk[features_name].width) for tk, _, _ in folds]
+        metas = [tk[features_name].metadata for tk, _, _ in folds]
+        keys = None
+        if all(m is not None for m in metas):
+            keys = [[(c.parent_feature_name, c.parent_feature_type, c.grouping, c.indicator_value,
+                      c.descriptor_value) for c in m.columns] for m in metas]
+            if any(len(set(k)) != len(k) or len(k) != w for k, w in zip(keys, widths)):
+                keys = None         # repeated column descriptions (hashed text): not alignable by name
+        if all(a is not None for a in aligns) and len({a[1] for a in aligns}) == 1 and aligns[0][1] is not None:
+            # the during SanityChecker's kept columns of one shared input vector
+            union = sorted(set().union(*[set(a[0]) for a in aligns]))
+            pos = {c: i for i, c in enumerate(union)}
+            cols = [[pos[c] for c in a[0]] for a in aligns]
+            W = len(union)
+        elif keys is not None and len({tuple(k) for k in keys}) > 1:
+            # fold-fitted stages with fold-specific columns (label-aware bucketizers): union of the columns by
+            # their metadata description, in first-seen order
+            pos: Dict[tuple, int] = {}
+            for k in keys:
+                for c in k:
+                    pos.setdefault(c, len(pos))
+            cols = [[pos[c] for c in k] for k in keys]
+            W = len(pos)
+        elif len(set(widths)) == 1:
+            cols, W = [None] * len(folds), widths[0]
+        else:
+            return None
+        blocks, ys, train_rows, val_rows = [], [], {}, {}
+        off = 0
+        for k, (train_k, val_k, _) in enumerate(folds):
+            Xt, yt = train_k[features_name].values, train_k[label_name].values
+            Xv, yv = val_k[features_name].values, val_k[label_name].values
+            dev = Xt.device
+            rid_t, rid_v = train_k.row_ids.to(dev), val_k.row_ids.to(dev)
+            if dp.active():       # row-sharded: every rank holds every fold's rows
+                Xt, yt, rid_t, Xv, yv, rid_v = (dp.rows(Xt), dp.rows(yt), dp.rows(rid_t), dp.rows(Xv), dp.rows(yv),
+                                                dp.rows(rid_v))
+            Xk = torch.cat([Xt, Xv.to(Xt.dtype)])
+            if cols[k] is not None:
+                full = torch.zeros(Xk.shape[0], W, dtype=Xk.dtype, device=dev)
+                full[:, torch.as_tensor(cols[k], dtype=torch.int64, device=dev)] = Xk
+                Xk = full
+            nt, nv = int(Xt.shape[0]), int(Xv.shape[0])
+            (keep, weights), vsel = self._fold_rows(k, rid_t, yt, rid_v, yv, nt, nv, Xk.dtype, dev, splitter)
+            train_rows[k] = (keep + off, weights)
+            val_rows[k] = vsel + off
+            blocks.append(Xk)
+            ys.append(torch.cat([yt, yv]).to(Xk.dtype))
+            off += int(Xk.shape[0])
+        return torch.cat(blocks), torch.cat(ys), train_rows, val_rows
 
     def _fit_eval_bounded(self, lname, grid, mine, X, y, train_rows, val_rows, ctx, remaining: float):
         """:meth:`_fit_eval` under the ``maxWait`` deadline (``awaitResult(..., maxWait)``, OpValidator.scala:348):
