@@ -138,3 +138,23 @@ def test_log_loss_and_brier_match_sklearn():
     out = OpBinScoreEvaluator().evaluate_arrays(yb, (s > 0.5).double(), None, torch.stack([1 - s, s], 1))
     assert out["BrierScore"] == pytest.approx(skm.brier_score_loss(yb.numpy(), s.numpy()))
     assert sum(out["numberOfDataPoints"]) == len(yb)
+
+
+def test_binary_areas_batch_matches_per_curve():
+    """One segmented sort for J score sets gives each set's exact AuPR / AuROC (ties, constant scores, all
+    positives / negatives included)."""
+    import torch
+    from transmogrifai_amd.evaluators import metrics as M
+    g = torch.Generator().manual_seed(0)
+    n = 3000
+    y = (torch.rand(n, generator=g) < 0.3).double()
+    S = torch.stack([torch.rand(n, generator=g, dtype=torch.float64),
+                     torch.round(torch.rand(n, generator=g, dtype=torch.float64) * 10) / 10,   # heavy ties
+                     torch.full((n,), 0.5, dtype=torch.float64),                            # one run
+                     y + 0.01 * torch.rand(n, generator=g, dtype=torch.float64),           # perfect
+                     -y])                                                                  # inverted
+    aupr, auroc = M.binary_areas_batch(S, y, chunk_elems=2 * n)
+    for j in range(S.shape[0]):
+        c = M.binary_curves(S[j], y, 0)
+        assert abs(float(aupr[j]) - c["AuPR"]) < 1e-12, (j, float(aupr[j]), c["AuPR"])
+        assert abs(float(auroc[j]) - c["AuROC"]) < 1e-12, (j, float(auroc[j]), c["AuROC"])

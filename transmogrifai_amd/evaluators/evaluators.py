@@ -86,6 +86,17 @@ class OpBinaryClassificationEvaluator(OpEvaluatorBase):
     def evaluate_arrays(self, y, pred, raw, prob):
         return M.binary_classification_metrics(pred, _score(None, prob, pred), y, self.num_bins)
 
+    def selection_metric_batch(self, y, outputs):
+        """Selection metric of several models scored on the same validation rows (``outputs`` = their
+        ``(pred, raw, prob)``): AuPR / AuROC from one segmented sort of all score sets
+        (:func:`metrics.binary_areas_batch`); ``None`` for the other metrics."""
+        if self.metric not in ("AuPR", "AuROC") or not outputs:
+            return None
+        S = torch.stack([(raw[:, 1] if (raw is not None and raw.numel() and raw.shape[1] >= 2)
+                          else _score(raw, prob, pred)).to(torch.float64).reshape(-1) for pred, raw, prob in outputs])
+        aupr, auroc = M.binary_areas_batch(S, y)
+        return (aupr if self.metric == "AuPR" else auroc).tolist()
+
     def selection_metric(self, y, pred, raw, prob):
         # BinaryClassificationEvaluator on rawPrediction, exact curve (numBins = 0)
         if self.metric in ("AuPR", "AuROC"):

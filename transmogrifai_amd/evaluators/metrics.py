@@ -72,6 +72,58 @@ def binary_curves(scores, labels, num_bins: int = 0, weights=None) -> Dict[str, 
             "AuPR": _trapz(pr_x, pr_y), "AuROC": _trapz(roc_x, roc_y)}
 
 
+def binary_areas_batch(S: torch.Tensor, labels: torch.Tensor, chunk_elems: int = 1 << 27):
+    """Exact (``numBins = 0``) AuPR and AuROC of ``J`` score sets over the same labelled rows, ``S [J, n]``:
+    one segmented sort along the rows (``torch.sort(dim=1)``) and vectorised run-end / cumulative-count /
+    trapezoid passes for all curves at once, instead of one sort + curve build per model.
+    Same points as :func:`binary_curves` (distinct scores descending; PR prefixed with ``(0, precision_first)``,
+    ROC with ``(0, 0)``), so the areas agree to fp64 rounding. Returns two fp64 ``[J]`` tensors."""
+    J, n = S.shape
+    dev = S.device
+    if n == 0 or J == 0:
+        z = torch.zeros(J, dtype=torch.float64, device=dev)
+        return z, z
+    y = (labels.to(dev).reshape(-1) > 0.5)
+    rows = max(1, min(J, chunk_elems // max(n, 1)))
+    aupr, auroc = [], []
+    for a in range(0, J, rows):
+        s, order = torch.sort(S[a:a + rows].to(torch.float64), dim=1, descending=True)
+        pos = y[order].to(torch.float64)
+        tp = torch.cumsum(pos, 1)
+        fp = torch.cumsum(1.0 - pos, 1)
+        is_end = torch.ones_like(s, dtype=torch.bool)
+        if n > 1:
+            is_end[:, :-1] = s[:, 1:] != s[:, :-1]
+        Ptot, Ntot = tp[:, -1:], fp[:, -1:]
+        # previous run end of every position: the last is_end index strictly before it (-1 = none)
+        idx = torch.arange(n, device=dev).expand_as(s)
+        last_end = torch.cummax(torch.where(is_end, idx, torch.full_like(idx, -1)), 1).values
+        prev = torch.full_like(last_end, -1)
+        prev[:, 1:] = last_end[:, :-1]
+        has_prev = prev >= 0
+        pidx = prev.clamp_min(0)
+        tp_p = torch.where(has_prev, tp.gather(1, pidx), torch.zeros_like(tp))
+        fp_p = torch.where(has_prev, fp.gather(1, pidx), torch.zeros_like(fp))
+        prec = torch.where(tp + fp > 0, tp / (tp + fp).clamp_min(1e-300), torch.ones_like(tp))
+        rec = torch.where(Ptot > 0, tp / Ptot.clamp_min(1e-300), torch.zeros_like(tp))
+        # the PR curve starts at (0, precision of the first run end)
+        first = torch.argmax(is_end.to(torch.int8), 1, keepdim=True)
+        prec_first = prec.gather(1, first)
+        prec_p = torch.where(has_prev, torch.where(tp_p + fp_p > 0, tp_p / (tp_p + fp_p).clamp_min(1e-300),
+                                                   torch.ones_like(tp_p)), prec_first.expand_as(prec))
+        rec_p = torch.where(Ptot > 0, tp_p / Ptot.clamp_min(1e-300), torch.zeros_like(tp_p))
+        e = is_end.to(torch.float64)
+        aupr.append(((rec - rec_p) * (prec + prec_p) / 2.0 * e).sum(1))
+        fpr = torch.where(Ntot > 0, fp / Ntot.clamp_min(1e-300), torch.zeros_like(fp))
+        fpr_p = torch.where(Ntot > 0, fp_p / Ntot.clamp_min(1e-300), torch.zeros_like(fp_p))
+        roc = ((fpr - fpr_p) * (rec + rec_p) / 2.0 * e).sum(1)
+        # closing (1, 1) point after the last run end
+        last_fpr, last_rec = fpr[:, -1], rec[:, -1]
+        roc = roc + (1.0 - last_fpr) * (1.0 + last_rec) / 2.0
+        auroc.append(roc)
+    return torch.cat(aupr), torch.cat(auroc)
+
+
 def au_pr(scores, labels, num_bins: int = 0) -> float:
     return binary_curves(scores, labels, num_bins)["AuPR"]
 

@@ -120,7 +120,11 @@ class MultinomialObjective:
     def __init__(self, X, y, W, inv_std, l2, fit_intercept, K, par=None):
         self.X, self.W, self.K = X, W, K
         self.par = par
-        self.Y = torch.nn.functional.one_hot(y.to(torch.int64), K).to(X.dtype)      # [N, K]
+        # GPU: margins by GEMM / SpMM, then ONE fused softmax epilogue (log-sum-exp, weighted loss, R in place)
+        # and fixed-order column sums (ops/csrc/hip/sparse_kernels.hip) instead of ~15 torch passes over [N, P, K]
+        self.fused = X.device.type == "cuda" and os.environ.get("TMOG_MNL_FUSED", "1") != "0"
+        self.y = y
+        self.Y = None if self.fused else torch.nn.functional.one_hot(y.to(torch.int64), K).to(X.dtype)    # [N, K]
         self.wsum = _psum(par, W.sum(0).to(torch.float64))[0].clamp_min(1e-300)
         self.inv_std = inv_std      # [d, P]
         self.l2, self.fi = l2, fit_intercept
@@ -147,7 +151,19 @@ class MultinomialObjective:
         l = lse - (M * self.Y[:, None, :]).sum(2)
         return l, lse
 
+    def _fused_pass(self, U, grad):
+        B, V, b = self._split(U)
+        P = U.shape[1]
+        M = LK.gemm(self.X, V.permute(0, 2, 1).reshape(self.d, P * self.K).to(torch.float32)).contiguous()
+        self.passes += 1
+        f, rs = LK.softmax_objective(M, self.y, self.W, b.t().reshape(-1), P, self.K, grad)
+        return B, M, f, rs
+
     def value(self, U):
+        if self.fused:
+            B, _, f, _ = self._fused_pass(U, False)
+            f = _psum(self.par, f)[0] / self.wsum
+            return f + 0.5 * self.l2 * (B[:self.d] ** 2).sum((0, 1))
         M = self.margins(U)
         l, _ = self._loss(M)
         f = _psum(self.par, (l * self.W).sum(0).to(torch.float64))[0] / self.wsum
@@ -155,6 +171,18 @@ class MultinomialObjective:
         return f + 0.5 * self.l2 * (B[:self.d] ** 2).sum((0, 1))
 
     def value_grad(self, U):
+        if self.fused:
+            P = U.shape[1]
+            B, R, fs, rs = self._fused_pass(U, True)
+            fs, Gs, rs = _psum(self.par, fs, LK.gemm_t(self.X, R).to(torch.float64), rs)
+            f = fs / self.wsum
+            G = Gs.reshape(self.d, P, self.K).permute(0, 2, 1) / self.wsum[None, None, :]   # [d, K, P]
+            g = torch.zeros_like(B)
+            g[:self.d] = G * self.inv_std[:, None, :] + self.l2[None, None, :] * B[:self.d]
+            gb = rs.reshape(P, self.K).t() / self.wsum[None, :]                       # [K, P]
+            g[self.d] = torch.where(self.fi[None, :], gb, torch.zeros_like(gb))
+            f = f + 0.5 * self.l2 * (B[:self.d] ** 2).sum((0, 1))
+            return f, g.reshape(U.shape)
         M = self.margins(U)
         l, lse = self._loss(M)
         Pr = torch.exp(M - lse[:, :, None])
@@ -376,6 +404,11 @@ def _feature_std(X, W, par=None):
     """Unbiased weighted std per column and problem (``[d, P]``): ``X^T W`` and ``(X*X)^T W`` GEMMs over
     row chunks, so the squared matrix is never materialised whole (was a full copy of the fold matrix)."""
     d, P = X.shape[1], W.shape[1]
+    if isinstance(X, LK.SparseDesign):
+        n, s1, s2 = _psum(par, W.sum(0).to(torch.float64), X.tmm(W), X.tmm(W, square=True))
+        mean = s1 / n.clamp_min(1)[None, :]
+        var = (s2 - n[None, :] * mean * mean) / (n - 1).clamp_min(1)[None, :]
+        return torch.sqrt(var.clamp_min(0)), mean
     s1 = torch.zeros(d, P, dtype=torch.float64, device=X.device)
     s2 = torch.zeros_like(s1)
     for a in range(0, X.shape[0], _STD_CHUNK):
@@ -460,6 +493,9 @@ class LogisticRegressionLearner(_LinearBase):
             return []
         K = int(y.max().item()) + 1 if y.numel() else 2
         par = _row_par(context)
+        # mostly-zero wide matrices (hashed text, pivots): dense block + CSR / CSC (ops/linear.py SparseDesign)
+        if par is None and os.environ.get("TMOG_LR_SPARSE", "1") != "0" and LK.SparseDesign.worthwhile(X):
+            X = LK.SparseDesign(X)
         if self.loss == "logistic" and K > 2:
             return self._fit_multinomial(X, y, jobs, K, par)
         X, y, W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs, par)

@@ -59,7 +59,8 @@ _HOST_SIGS = {
 }
 
 _HIP_SIGS = {
-    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P, P, I32, I32, I32, P],
+    "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P, P, I32, I32, I32, P,
+                            P],
     "tmog_hip_hist_stat_chunk": [I32, I32],
     "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
     "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P, I32, P,
@@ -68,7 +69,7 @@ _HIP_SIGS = {
     "tmog_hip_rccl_unique_id": [P, I32],
     "tmog_hip_rccl_comm_init": [P, I32, I32],
     "tmog_hip_rccl_comm_destroy": [P],
-    "tmog_hip_partition_fused": [P, I32, P, P, P, I32, P, P, P, P, P, P, P, I32, P, P, I64, P],
+    "tmog_hip_partition_fused": [P, I32, P, P, P, I32, P, P, P, P, P, P, P, I32, P, P, I64, P, P, P],
     "tmog_hip_leaf_collect": [P, P, I32, P, P, P],
     "tmog_hip_grow_forest": [P],
     "tmog_hip_grow_status": [P, P, I32],
@@ -95,6 +96,10 @@ _HIP_SIGS = {
     "tmog_hip_class_colsum": [P, I64, I32, I64, P, I32, I32, P, P],
     "tmog_hip_logistic_grad": [P, P, P, I64, I32, P],
     "tmog_hip_debug_flags": [I32],
+    "tmog_hip_csr_spmm": [P, P, P, I64, P, I32, P, I32, I32, P],
+    "tmog_hip_csc_spmm_t": [P, P, P, I64, P, I64, P, I32, I32, P, P, P],
+    "tmog_hip_softmax_epilogue": [P, I64, I32, I32, P, P, P, I32, P, I32, P],
+    "tmog_hip_colsum": [P, I64, I32, I32, P, P],
     "tmog_hip_gather_rows_cols": [P, P, P, I64, I32, P, P],
     "tmog_hip_hash_tokens": [P, P, I64, P, I32, I32, I32, I32, P, P],
     "tmog_hip_hash_tf_rows": [P, I32, I64, I32, I32, P, I64, I64, P],

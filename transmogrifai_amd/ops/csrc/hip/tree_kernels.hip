@@ -730,7 +730,16 @@ __device__ __forceinline__ bool better(const Best& a, const Best& b) {
 // tie-break (gain, then lowest feature, dl, bin) and sums the winner's left statistics. Spreading a
 // node over feature blocks fills the chip at the shallow levels (6 root nodes = 6 workgroups before).
 // SM = compile-time bound on S (register arrays sized to it).
-constexpr int FPB = 16;
+constexpr int FPB = 16;      // default features per scan workgroup (TMOG_SPLIT_FPB: 4, 8 or 16; 4 waves)
+
+static int split_fpb() {
+  static const int v = [] {
+    const char* e = std::getenv("TMOG_SPLIT_FPB");
+    const int x = e ? std::atoi(e) : FPB;
+    return (x == 4 || x == 8 || x == 16) ? x : FPB;
+  }();
+  return v;
+}
 
 template <int SM>
 __global__ void __launch_bounds__(256) split_scan_kernel(
@@ -738,7 +747,7 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
     int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
-    Best* __restrict__ cand, int n_multi) {
+    Best* __restrict__ cand, int n_multi, int fpb) {
   const int j = blockIdx.x / fbmax;
   const int fb = blockIdx.x - j * fbmax;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -746,13 +755,13 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
   // n_multi >= 0: local features [n_multi, nf) have one present bin; their blocks (fb >= fb_multi)
   // take 256 features each, one thread per feature, instead of 16 per block through the scan
   const int f_lim = n_multi >= 0 ? min(n_multi, nf) : nf;
-  const int fb_multi = n_multi >= 0 ? (n_multi + FPB - 1) / FPB : fbmax;
+  const int fb_multi = n_multi >= 0 ? (n_multi + fpb - 1) / fpb : fbmax;
   const bool one_blk = fb >= fb_multi;
   __shared__ Best s_best[4];
   Best best{-INFINITY, 0x7fffffff, 0, 0};
   // params slot 7 = "may split" (tree_grow.hpp): nodes built only as a subtraction partner are not scanned
   if (node_params[(int64_t)j * 8 + 7] > 0.5f &&
-      (one_blk ? (n_multi + (fb - fb_multi) * 256 < nf) : (fb * FPB < f_lim))) {
+      (one_blk ? (n_multi + (fb - fb_multi) * 256 < nf) : (fb * fpb < f_lim))) {
     const int64_t* h = hist + node_hist_off[j];
     const int32_t* fl = feat_list + node_feat_off[j];
     const float* P = node_params + (int64_t)j * 8;
@@ -772,7 +781,7 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     double tcount;
     const double pimp = impurity_dev(tot, S, kind, &tcount);
     const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
-    const int f_end = one_blk ? 0 : min(f_lim, (fb + 1) * FPB);
+    const int f_end = one_blk ? 0 : min(f_lim, (fb + 1) * fpb);
     // one candidate (left statistics lq, bin b, missing direction dl) with the CPU twin's arithmetic
     auto consider = [&](const int64_t* lq, int f, int b, int dl) {
       double left[SM], right[SM];
@@ -808,7 +817,7 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
         consider(lq, f, 0, 0);
       }
     }
-    for (int f = fb * FPB + wave; f < f_end; f += 4) {
+    for (int f = fb * fpb + wave; f < f_end; f += 4) {
       const int nb = feat_nbins[fl[f]];
       const int64_t* hf = h + (int64_t)f * B * S;
       if (nb == 1) {
@@ -1591,12 +1600,13 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                        node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin,
                        node_model, qinv, fbmax, cand, n_multi);
   } else {
-  fbmax = n_multi >= 0 ? (n_multi + FPB - 1) / FPB + (max_nfeat - n_multi + 255) / 256
-                       : (max_nfeat + FPB - 1) / FPB;
+  const int fpb = split_fpb();
+  fbmax = n_multi >= 0 ? (n_multi + fpb - 1) / fpb + (max_nfeat - n_multi + 255) / 256
+                       : (max_nfeat + fpb - 1) / fpb;
 #define TM_SPLIT(SMV)                                                                                          \
   hipLaunchKernelGGL(split_scan_kernel<SMV>, dim3(n_nodes * fbmax), dim3(256), 0, stream, hist, node_hist_off,  \
                      node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin,    \
-                     node_model, qinv, fbmax, cand, n_multi)
+                     node_model, qinv, fbmax, cand, n_multi, fpb)
   if (S <= 2) TM_SPLIT(2);
   else if (S == 3) TM_SPLIT(3);
   else if (S <= 4) TM_SPLIT(4);
@@ -1630,7 +1640,8 @@ int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* siz
 
 size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat, int B, int S) {
   const bool wide = S > TM_MAX_S || B > 64;
-  return (size_t)n_nodes * (wide ? max_nfeat : (max_nfeat + FPB - 1) / FPB) * sizeof(Best);
+  const int fpb = split_fpb();       // (max_nfeat + fpb - 1) / fpb + 1 bounds fbmax for any n_multi split
+  return (size_t)n_nodes * (wide ? max_nfeat : (max_nfeat + fpb - 1) / fpb + 1) * sizeof(Best);
 }
 
 // Largest statistic chunk whose per-workgroup LDS table (64 copies of B x Sc words) fits the LDS.

@@ -434,9 +434,17 @@ class OpValidator:
             states = learner.fit_batch(X, y, fjobs, context=ctx)
             preds = learner.predict_batch(states, X, [val_rows[k] for _, (_, g, k) in batch], context=ctx)
             out = {}
-            for (j, (l, g, k)), (pred, raw, prob) in zip(batch, preds):
+            # the models of one fold share its validation rows: their curves come from one segmented sort
+            by_fold: Dict[int, list] = {}
+            for (j, (l, g, k)), pr in zip(batch, preds):
+                by_fold.setdefault(k, []).append(((l, g, k), pr))
+            batch_fn = getattr(self.evaluator, "selection_metric_batch", None)
+            for k, items in by_fold.items():
                 yv = y[val_rows[k]]
-                out[(l, g, k)] = float(self.evaluator.selection_metric(yv, pred, raw, prob))
+                vals = batch_fn(yv, [pr for _, pr in items]) if (batch_fn is not None and len(items) > 1) else None
+                if vals is None:
+                    vals = [float(self.evaluator.selection_metric(yv, *pr)) for _, pr in items]
+                out.update({key: float(v) for (key, _), v in zip(items, vals)})
             return out
 
         try:
