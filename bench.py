@@ -185,6 +185,10 @@ def main():
         sync()
         dt = time.perf_counter() - t0
         stage_t[0] = {k: round(v, 4) for k, v in model.train_timings.items() if isinstance(v, (int, float))}
+        per_stage = model.train_timings.get("stages", {})
+        stage_t[0]["top_stages"] = dict(sorted(((k, round(v, 4)) for k, v in per_stage.items()
+                                                if isinstance(v, (int, float)) and not k.startswith("peak_gb")),
+                                               key=lambda kv: -kv[1])[:12])
         sel = model.get_origin_stage_of(pred)
         summ = sel.metadata.get("summary", {})
         ho = (summ.get("holdoutEvaluation") or {}).get(CONFIGS[args.config][3], float("nan"))

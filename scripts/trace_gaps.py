@@ -1,0 +1,56 @@
+"""GPU occupancy of a rocprofv3 kernel trace: python scripts/trace_gaps.py <kernel_trace.csv> [name-substring ...]
+
+Prints the traced span, the time at least one kernel was running (union of the dispatch intervals over
+all queues), the idle gaps by size, and per-kernel totals. With name substrings, the window is cut to
+the first..last dispatch whose name contains any of them (e.g. the XGBoost phase: hist_build)."""
+import csv
+import sys
+from collections import defaultdict
+
+
+def main():
+    path, keys = sys.argv[1], sys.argv[2:]
+    rows = []
+    with open(path, newline="") as f:
+        rd = csv.DictReader(f)
+        for r in rd:
+            name = r.get("Kernel_Name") or r.get("KernelName") or ""
+            s = int(r.get("Start_Timestamp") or r.get("BeginNs"))
+            e = int(r.get("End_Timestamp") or r.get("EndNs"))
+            rows.append((s, e, name))
+    rows.sort()
+    if keys:
+        sel = [i for i, (_, _, n) in enumerate(rows) if any(k in n for k in keys)]
+        if not sel:
+            print("no dispatch matches", keys)
+            return
+        lo, hi = rows[sel[0]][0], rows[sel[-1]][1]
+        rows = [r for r in rows if r[0] >= lo and r[1] <= hi]
+    span = rows[-1][1] - rows[0][0]
+    busy = 0
+    cur_s, cur_e = rows[0][0], rows[0][1]
+    gaps = []
+    for s, e, _ in rows[1:]:
+        if s > cur_e:
+            busy += cur_e - cur_s
+            gaps.append(s - cur_e)
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    print(f"dispatches {len(rows)}  span {span / 1e6:.2f} ms  busy {busy / 1e6:.2f} ms ({100 * busy / span:.1f} %)")
+    edges = [0, 5_000, 20_000, 50_000, 100_000, 250_000, 1_000_000, 10_000_000, 1 << 62]
+    for a, b in zip(edges, edges[1:]):
+        g = [x for x in gaps if a <= x < b]
+        print(f"  gaps [{a / 1e3:>8.0f}, {b / 1e3:>8.0f}) us: n={len(g):6d}  total {sum(g) / 1e6:8.2f} ms")
+    tot = defaultdict(lambda: [0, 0])
+    for s, e, n in rows:
+        k = n.split("(")[0][:90]
+        tot[k][0] += 1
+        tot[k][1] += e - s
+    for k, (c, t) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:25]:
+        print(f"  {t / 1e6:9.2f} ms  {c:7d}  {k}")
+
+
+if __name__ == "__main__":
+    main()

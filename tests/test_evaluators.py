@@ -158,3 +158,23 @@ def test_binary_areas_batch_matches_per_curve():
         c = M.binary_curves(S[j], y, 0)
         assert abs(float(aupr[j]) - c["AuPR"]) < 1e-12, (j, float(aupr[j]), c["AuPR"])
         assert abs(float(auroc[j]) - c["AuROC"]) < 1e-12, (j, float(auroc[j]), c["AuROC"])
+
+
+def test_binary_areas_batch_fp32_packed_key():
+    """fp32 score sets take the packed (row, float-order) key sort: negative, zero, tied and extreme
+    scores give the same areas as the per-curve fp64 path."""
+    import torch
+    from transmogrifai_amd.evaluators import metrics as M
+    g = torch.Generator().manual_seed(1)
+    n = 2500
+    y = (torch.rand(n, generator=g) < 0.4).double()
+    S = torch.stack([torch.randn(n, generator=g) * 3,
+                     torch.round(torch.randn(n, generator=g) * 4) / 4,               # ties around 0, -0.0
+                     torch.where(y > 0, torch.tensor(3.0e38), torch.tensor(-3.0e38)),   # extremes
+                     -torch.rand(n, generator=g)]).to(torch.float32)
+    S[1, :7] = -0.0
+    aupr, auroc = M.binary_areas_batch(S, y)
+    for j in range(S.shape[0]):
+        c = M.binary_curves(S[j].double(), y, 0)
+        assert abs(float(aupr[j]) - c["AuPR"]) < 1e-12, (j, float(aupr[j]), c["AuPR"])
+        assert abs(float(auroc[j]) - c["AuROC"]) < 1e-12, (j, float(auroc[j]), c["AuROC"])

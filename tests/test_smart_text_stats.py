@@ -117,3 +117,23 @@ def test_text_length_type_tokens_ignores_constant_token_length_ids():
     assert model.methods == ["ignore", "hash"]
     with pytest.raises(ValueError):
         SmartTextVectorizer(text_length_type="Words").set_input(fi).fit(ds)
+
+
+def test_native_clean_batch_equals_clean_string():
+    """ops/csrc/host/text_clean.cpp: ASCII strings cleaned natively, the rest through clean_string; ids in
+    first-appearance order of equal cleaned values, lengths in characters."""
+    import numpy as np
+    from transmogrifai_amd.utils import text as TU
+    rng = np.random.default_rng(0)
+    alpha = list("abcXYZ ,.-_!?'\t09Éßİ")
+    vals = ["".join(rng.choice(alpha, size=rng.integers(0, 12))) for _ in range(5000)] + ["", "İstanbul", "ǅ x"]
+    cb = TU.clean_batch(vals, True)
+    py = [TU.clean_string(v) for v in vals]
+    ids = {}
+    exp = [ids.setdefault(v, len(ids)) for v in py]
+    assert [cb.value(j) for j in range(len(vals))] == py
+    assert cb.ids.tolist() == exp and cb.n_ids == len(ids)
+    assert cb.char_len.tolist() == [len(v) for v in py]
+    raw = TU.clean_batch(vals, False)
+    ids = {}
+    assert raw.ids.tolist() == [ids.setdefault(v, len(ids)) for v in vals]

@@ -92,8 +92,11 @@ class OpBinaryClassificationEvaluator(OpEvaluatorBase):
         (:func:`metrics.binary_areas_batch`); ``None`` for the other metrics."""
         if self.metric not in ("AuPR", "AuROC") or not outputs:
             return None
-        S = torch.stack([(raw[:, 1] if (raw is not None and raw.numel() and raw.shape[1] >= 2)
-                          else _score(raw, prob, pred)).to(torch.float64).reshape(-1) for pred, raw, prob in outputs])
+        sc = [(raw[:, 1] if (raw is not None and raw.numel() and raw.shape[1] >= 2)
+               else _score(raw, prob, pred)).reshape(-1) for pred, raw, prob in outputs]
+        # fp32 scores stay fp32 (one packed-key sort); anything else is compared in fp64
+        S = torch.stack(sc) if all(t.dtype == torch.float32 for t in sc) else \
+            torch.stack([t.to(torch.float64) for t in sc])
         aupr, auroc = M.binary_areas_batch(S, y)
         return (aupr if self.metric == "AuPR" else auroc).tolist()
 

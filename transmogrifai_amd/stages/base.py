@@ -88,8 +88,30 @@ def make_output_name(output_feature_uid: str, inputs: Sequence[TransientFeature]
     return f"{origins}_{n_stages}-stagesApplied_{output_feature_uid}"
 
 
+def _in_domain(value, dom) -> bool:
+    """``dom`` = (lo, hi, lo_inclusive, hi_inclusive); None bounds are open (Spark ``ParamValidators``)."""
+    lo, hi, lo_in, hi_in = dom
+    v = float(value)
+    if lo is not None and not (v >= lo if lo_in else v > lo):
+        return False
+    return hi is None or (v <= hi if hi_in else v < hi)
+
+
+def _fmt_domain(dom) -> str:
+    lo, hi, lo_in, hi_in = dom
+    return f"{'[' if lo_in else '('}{'-inf' if lo is None else lo}, {'inf' if hi is None else hi}{']' if hi_in else ')'}"
+
+
+# common domains of the reference's param validators
+GT0 = (0, None, False, False)
+GTEQ0 = (0, None, True, False)
+UNIT = (0.0, 1.0, True, True)
+
+
 class OpPipelineStage:
-    """Base of every stage. Subclasses set ``operation_name``, ``output_type`` and ``_defaults``."""
+    """Base of every stage. Subclasses set ``operation_name``, ``output_type`` and ``_defaults``; numeric
+    params with a domain (``_param_domains``: name -> (lo, hi, lo_inclusive, hi_inclusive)) are checked on
+    ``set`` the way Spark's ``ParamValidators`` reject an out-of-range ``setX``."""
 
     operation_name: str = "stage"
     output_type = T.FeatureType
@@ -121,6 +143,9 @@ class OpPipelineStage:
     def set(self, name: str, value) -> "OpPipelineStage":
         if name not in self.params and not self._accepts_param(name):
             raise ValueError(f"{type(self).__name__} has no param '{name}'")
+        dom = getattr(type(self), "_param_domains", {}).get(name)
+        if dom is not None and value is not None and not _in_domain(value, dom):
+            raise ValueError(f"{type(self).__name__} param {name} = {value!r} outside {_fmt_domain(dom)}")
         self.params[name] = value
         return self
 

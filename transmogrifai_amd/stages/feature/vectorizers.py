@@ -30,7 +30,8 @@ from ...features import types as T
 from ...ops import vector as V
 from ...utils import text as TU
 from ...utils.dates import TIME_PERIODS, period_values
-from ..base import OpEstimator, OpTransformer, SequenceEstimator, SequenceTransformer, register_stage
+from ..base import (GT0, GTEQ0, UNIT, OpEstimator, OpTransformer, SequenceEstimator, SequenceTransformer,
+                    register_stage)
 
 
 # ----------------------------------------------------------------------------------------- helpers
@@ -280,6 +281,9 @@ class OpTextPivotVectorizer(VectorizerMixin, SequenceEstimator):
     operation_name = "pivotText"
     _defaults = {"top_k": 20, "min_support": 10, "clean_text": True, "track_nulls": True,
                  "unseen_name": OTHER_STRING, "max_pct_cardinality": 1.0, "hll_bits": 12}
+    # Transmogrifier.scala:556-575 (topK > 0, minSupport >= 0), OpOneHotVectorizer.scala:250-266
+    _param_domains = {"top_k": GT0, "min_support": GTEQ0, "max_pct_cardinality": UNIT,
+                      "hll_bits": (4, 31, True, True)}
 
     def _counts(self, c):
         return _text_counts(c, self.params["clean_text"]) if isinstance(c, TextColumn) else \
@@ -452,29 +456,36 @@ class TextStats:
         if V == 0:
             return TextStats(Counter(), Counter())
         from ...ops.text import code_counts
-        cleaned = [TU.clean_string(v) if clean else v for v in col.vocab]
-        ids: Dict[str, int] = {}
-        lut = np.fromiter((ids.setdefault(v, len(ids)) for v in cleaned), dtype=np.int64, count=V)
+        # cleaned values of the whole vocabulary in one native pass (first-appearance ids of equal cleaned
+        # strings, character lengths); Python strings only for the values that end up counted
+        cb = TU.clean_batch(col.vocab, clean)
+        lut = cb.ids
         full = code_counts([col.codes], [V])[0][:-1]
         codes = col.codes
         n = int(codes.shape[0])
         first = None
-        if len(ids) > max_card:
+        if cb.n_ids > max_card:
             c = codes.to(torch.int64)
             ok = c >= 0
             rid = torch.arange(n, device=c.device)
             fv = torch.full((V,), n, dtype=torch.int64, device=c.device).scatter_reduce_(
                 0, c[ok], rid[ok], reduce="amin")
             first = fv.cpu().numpy()
-            first_id = np.full(len(ids), n, np.int64)
+            first_id = np.full(cb.n_ids, n, np.int64)
             np.minimum.at(first_id, lut, first)
             cut = _prefix_cutoff(first_id, max_card)
             counts = code_counts([codes[:cut + 1]], [V])[0][:-1]
         else:
             counts = full
         vc: Counter = Counter()
-        for j in np.flatnonzero(counts):
-            vc[cleaned[j]] += int(counts[j])
+        nzc = np.flatnonzero(counts)
+        if nzc.size:
+            per_id = np.bincount(lut[nzc], weights=counts[nzc], minlength=cb.n_ids)
+            first_j = np.full(cb.n_ids, V, np.int64)
+            np.minimum.at(first_j, lut[nzc], nzc)
+            live = np.flatnonzero(per_id)
+            for i in live[np.argsort(first_j[live], kind="stable")]:     # insertion order: first counted value
+                vc[cb.value(int(first_j[i]))] = int(per_id[i])
         # length counts: every row of the partition (their own cap applies to distinct lengths)
         lc: Counter = Counter()
         if token_lengths:
@@ -501,8 +512,11 @@ class TextStats:
                         lc = _capped_plus(lc, maps[int(code)], max_card)
             return TextStats(vc, lc)
         else:
-            for j in np.flatnonzero(full):
-                lc[len(cleaned[j])] += int(full[j])
+            nzf = np.flatnonzero(full)
+            if nzf.size:
+                bl = np.bincount(cb.char_len[nzf], weights=full[nzf])
+                for L in np.flatnonzero(bl):
+                    lc[int(L)] = int(bl[L])
         if len(lc) > max_card:
             # same prefix rule over the rows' lengths (first occurrence of each length value)
             if first is None:
@@ -511,7 +525,7 @@ class TextStats:
                 rid = torch.arange(n, device=c.device)
                 first = torch.full((V,), n, dtype=torch.int64, device=c.device).scatter_reduce_(
                     0, c[ok], rid[ok], reduce="amin").cpu().numpy()
-            lens = np.fromiter((len(v) for v in cleaned), dtype=np.int64, count=V)
+            lens = cb.char_len
             uniq, inv = np.unique(lens, return_inverse=True)
             first_len = np.full(uniq.size, n, np.int64)
             np.minimum.at(first_len, inv, first)
@@ -612,6 +626,9 @@ class SmartTextVectorizer(VectorizerMixin, SequenceEstimator):
                  "binary_freq": False, "coverage_pct": 0.90, "min_length_std_dev": 0.0, "track_text_len": False,
                  "min_token_length": 1, "to_lowercase": True, "unseen_name": OTHER_STRING,
                  "text_length_type": "FullEntry", "strip_html": False}
+    # SmartTextVectorizer.scala:378-405 + the shared topK / minSupport validators
+    _param_domains = {"top_k": GT0, "min_support": GTEQ0, "max_cardinality": (1, 1000, True, True),
+                      "coverage_pct": (0.0, 1.0, False, True), "min_length_std_dev": (0.0, 100.0, True, True)}
     # Row-sharded fits: every rank folds its own rows into capped TextStats (<= max_cardinality + 1 values
     # per feature) and the ranks' stats are merged in rank order -- one small object all-gather, the
     # reference's ``valueStats.reduce(_ + _)`` (SmartTextVectorizer.scala:87-91) with ranks as partitions
@@ -695,7 +712,8 @@ class DateListVectorizer(VectorizerMixin, SequenceTransformer):
     """Days since first/last date vs a reference date, or mode day/month/hour pivots
     (``DateListVectorizer.scala:60-309``). Accepts ``DateList`` or single ``Date`` columns."""
     operation_name = "vecDateList"
-    _defaults = {"pivot": "SinceLast", "reference_date": None, "track_nulls": True, "fill_value": 0.0}
+    _defaults = {"pivot": "SinceFirst", "reference_date": None, "track_nulls": True, "fill_value": 0.0}
+    _param_domains = {"reference_date": GTEQ0}          # DateListVectorizer.scala:150-155
 
     def _ref(self):
         r = self.params["reference_date"]

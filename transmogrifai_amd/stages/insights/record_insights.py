@@ -15,6 +15,7 @@ elementwise [rows, d] tensor op); top-K selection per record is ``torch.topk`` o
 from __future__ import annotations
 
 import json
+import math
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -51,6 +52,71 @@ def _short(t: str) -> str:
 
 def _history_json(h: dict) -> str:
     return json.dumps(h, separators=(",", ":"), sort_keys=False)
+
+
+def _jf(x: float) -> str:
+    """A float as ``json.dumps`` writes it (repr; NaN / Infinity for the non-finite)."""
+    return repr(x) if math.isfinite(x) else json.dumps(x)
+
+
+class InsightsColumn(ObjectColumn):
+    """``TextMap`` column of record insights kept as device tensors -- column index [n, K] (-1 = none),
+    score changes [n, K, C] and the vector's column-history keys -- and rendered to the reference's
+    ``{columnHistory JSON: "[[scoreIndex, diff], ...]"}`` maps only when rows are read on the host."""
+
+    def __init__(self, cols: torch.Tensor, diffs: torch.Tensor, keys: Sequence[str]):
+        self.ftype = T.TextMap
+        self.cols, self.diffs, self.keys = cols, diffs, list(keys)
+        self._values = None
+
+    @property
+    def values(self):
+        if self._values is None:
+            cols = self.cols.cpu().numpy()
+            diffs = self.diffs.cpu().numpy()
+            arr = np.empty(cols.shape[0], dtype=object)
+            for i in range(cols.shape[0]):
+                arr[i] = self._render(cols[i], diffs[i])
+            self._values = arr
+        return self._values
+
+    @values.setter
+    def values(self, v):
+        self._values = v
+
+    def _render(self, cols, diffs) -> Dict[str, str]:
+        return {self.keys[c]: "[" + ",".join(f"[{j},{_jf(x)}]" for j, x in enumerate(dv)) + "]"
+                for c, dv in zip(cols.tolist(), diffs.tolist()) if c >= 0}
+
+    def __len__(self):
+        return int(self.cols.shape[0])
+
+    @property
+    def device(self):
+        return self.cols.device
+
+    def take(self, idx):
+        i = idx.to(self.cols.device, torch.long) if isinstance(idx, torch.Tensor) else \
+            torch.as_tensor(np.asarray(idx, np.int64), device=self.cols.device)
+        return InsightsColumn(self.cols.index_select(0, i), self.diffs.index_select(0, i), self.keys)
+
+    def to(self, device):
+        return InsightsColumn(self.cols.to(device), self.diffs.to(device), self.keys)
+
+    def row(self, i):
+        if self._values is not None:
+            return self._values[i]
+        return self._render(self.cols[i].cpu().numpy(), self.diffs[i].cpu().numpy())
+
+    def null_mask(self):
+        return ~(self.cols >= 0).any(1).cpu()
+
+    @classmethod
+    def _concat(cls, cols):
+        if all(isinstance(c, InsightsColumn) and c.keys == cols[0].keys and c.diffs.shape[1:] == cols[0].diffs.shape[1:]
+               for c in cols):
+            return InsightsColumn(torch.cat([c.cols for c in cols]), torch.cat([c.diffs for c in cols]), cols[0].keys)
+        return ObjectColumn(T.TextMap, np.concatenate([c.values for c in cols]))
 
 
 # ---------------------------------------------------------------------------------------------- LOCO
@@ -100,85 +166,108 @@ class RecordInsightsLOCO(UnaryTransformer):
             groups.setdefault(name, []).append(j)
         return groups
 
-    def _loco_block(self, X: torch.Tensor, hist: List[dict]):
-        """Score changes for one block of records: returns per record a list of (col, value, diffs)."""
+    def _plan(self, hist: List[dict], d: int, device):
+        """Candidate layout of one vector width: plain columns first (in column order), then one
+        candidate per column group. Returns (cand_of_col [d], group size per candidate [m], plain
+        column per candidate (-1 for groups) [m], group column tensors)."""
+        groups = self._groups(hist)
+        in_group = torch.zeros(d, dtype=torch.bool)
+        for cols in groups.values():
+            in_group[cols] = True
+        plain = torch.nonzero(~in_group).flatten()
+        n_plain = int(plain.numel())
+        cand_of_col = torch.empty(d, dtype=torch.long)
+        cand_of_col[plain] = torch.arange(n_plain)
+        gsize = [1.0] * n_plain
+        gcols = []
+        for g, cols in enumerate(groups.values()):
+            cand_of_col[torch.as_tensor(cols)] = n_plain + g
+            gsize.append(float(len(cols)))
+            gcols.append(torch.as_tensor(cols, device=device))
+        plain_col = torch.cat([plain, torch.full((len(gcols),), -1, dtype=torch.long)])
+        return (cand_of_col.to(device), torch.as_tensor(gsize, dtype=torch.float64, device=device),
+                plain_col.to(device), gcols)
+
+    def _loco_block(self, X: torch.Tensor, hist: List[dict], plan=None):
+        """Top-K score changes of one block of records, all on the device: (column [n, K] (-1 = no
+        insight), diffs [n, K, C]). Every (record, non-zero column) perturbation is one row of a perturbed
+        batch; its score change is scattered into the record's candidate (the column itself, or its
+        text / date group: ``Avg`` divides the group sum by the group size, ``LeaveOutVector`` re-scores
+        the record with the whole group zeroed), then the top-K positive and negative candidates are
+        merged and ordered per record by one stable sort (``RecordInsightsLOCO.scala:246-273``)."""
         n, d = X.shape
+        dev = X.device
         base, pred_cls = self._scores(X)
         C = base.shape[1]
         if C == 0:
             raise RuntimeError("model does not produce scores for insights")
         if C == 1:
-            ex = torch.zeros(n, dtype=torch.long, device=X.device)
+            ex = torch.zeros(n, dtype=torch.long, device=dev)
         elif C == 2:
-            ex = torch.ones(n, dtype=torch.long, device=X.device)
+            ex = torch.ones(n, dtype=torch.long, device=dev)
         else:
             ex = pred_cls.to(torch.long)
-        groups = self._groups(hist)
-        in_group = torch.zeros(d, dtype=torch.bool)
-        for cols in groups.values():
-            in_group[cols] = True
+        cand_of_col, gsize, plain_col, gcols = plan if plan is not None else self._plan(hist, d, dev)
+        m = int(gsize.numel())
+        k = int(self.params["top_k"])
+        abs_mode = self.params["top_k_strategy"] == "abs"
+        kk = min(k, m)
+        K = min(k if abs_mode else 2 * k, 2 * kk)
+        if m == 0 or n == 0:
+            return (torch.full((n, K), -1, dtype=torch.long, device=dev),
+                    torch.zeros(n, K, C, dtype=torch.float64, device=dev))
         nz = X != 0
         rows, cols = torch.nonzero(nz, as_tuple=True)
-        diffs = torch.zeros(rows.numel(), C, dtype=torch.float64, device=X.device)
+        V = torch.zeros(n * m, C, dtype=torch.float64, device=dev)
+        cand = cand_of_col[cols]
         # one perturbed copy per (record, non-zero column), scored in bounded chunks
         step = max(1, self.chunk_elems // max(d, 1))
+        ar = torch.arange(min(step, rows.numel()), device=dev)
         for a in range(0, rows.numel(), step):
             r, c = rows[a:a + step], cols[a:a + step]
-            Xp = X.index_select(0, r).clone()
-            Xp[torch.arange(r.numel(), device=X.device), c] = 0
+            Xp = X.index_select(0, r)
+            Xp[ar[:r.numel()], c] = 0
             s, _ = self._scores(Xp)
-            diffs[a:a + step] = base.index_select(0, r) - s
-        D = torch.zeros(n, d, C, dtype=torch.float64, device=X.device)
-        D[rows, cols] = diffs
-        strategy = self.params["vector_aggregation_strategy"]
-        cand_vals = []       # [n] tensors of diffs (all classes) per candidate
-        cand_cols = []
-        plain = [j for j in range(d) if not bool(in_group[j])]
-        for j in plain:
-            cand_cols.append(torch.full((n,), j, dtype=torch.long, device=X.device))
-            cand_vals.append(D[:, j, :])
-        for name, gc in groups.items():
-            gct = torch.as_tensor(gc, device=X.device)
+            ca = cand[a:a + step]
+            V.index_add_(0, r * m + ca, (base.index_select(0, r) - s) / gsize[ca][:, None])
+        V = V.view(n, m, C)
+        Cc = plain_col[None, :].expand(n, m).clone()
+        n_plain = m - len(gcols)
+        leave_out = self.params["vector_aggregation_strategy"] != "Avg"
+        for g, gct in enumerate(gcols):
             active = nz[:, gct]
             has = active.any(1)
-            first = torch.where(has, gct[active.to(torch.int8).argmax(1)], torch.full((n,), -1, device=X.device))
-            if strategy == "Avg":
-                v = D[:, gct, :].sum(1) / len(gc)
-            else:   # LeaveOutVector: zero every active column of the group at once
+            Cc[:, n_plain + g] = torch.where(has, gct[active.to(torch.int8).argmax(1)], torch.full_like(has, -1,
+                                                                                                    dtype=torch.long))
+            if leave_out:       # LeaveOutVector: zero every active column of the group at once
                 Xp = X.clone()
                 Xp[:, gct] = 0
                 s, _ = self._scores(Xp)
-                v = torch.where(has[:, None], base - s, torch.zeros_like(base))
-            cand_cols.append(first)
-            cand_vals.append(v)
-        if not cand_vals:
-            return [[] for _ in range(n)]
-        V = torch.stack(cand_vals, 1)                      # [n, m, C]
-        Cc = torch.stack(cand_cols, 1)                     # [n, m]
-        val = V.gather(2, ex.view(n, 1, 1).expand(n, V.shape[1], 1)).squeeze(2)
+                V[:, n_plain + g] = torch.where(has[:, None], base - s, torch.zeros_like(base))
+        val = V.gather(2, ex.view(n, 1, 1).expand(n, m, 1)).squeeze(2)
         valid = (Cc >= 0) & (val != 0)
-        k = int(self.params["top_k"])
-        kk = min(k, val.shape[1])
-        pos = torch.where(valid & (val > 0), val, torch.full_like(val, -float("inf")))
-        neg = torch.where(valid & (val < 0), -val, torch.full_like(val, -float("inf")))
-        pv, pi = torch.topk(pos, kk, dim=1)
-        nv, ni = torch.topk(neg, kk, dim=1)
-        out = []
-        pv, pi, nv, ni = pv.cpu(), pi.cpu(), nv.cpu(), ni.cpu()
-        Vc, Cc_, valc = V.cpu(), Cc.cpu(), val.cpu()
-        for i in range(n):
-            items = [(int(Cc_[i, m]), float(valc[i, m]), Vc[i, m].tolist())
-                     for m, v in zip(pi[i].tolist(), pv[i].tolist()) if v != -float("inf")]
-            items += [(int(Cc_[i, m]), float(valc[i, m]), Vc[i, m].tolist())
-                      for m, v in zip(ni[i].tolist(), nv[i].tolist()) if v != -float("inf")]
-            if self.params["top_k_strategy"] == "abs":
-                items.sort(key=lambda t: -abs(t[1]))
-                items = items[:k]
-            else:
-                items.sort(key=lambda t: -t[1])
-                items = items[:2 * k]
-            out.append(items)
-        return out
+        ninf = torch.full_like(val, -float("inf"))
+        pv, pi = torch.topk(torch.where(valid & (val > 0), val, ninf), kk, dim=1)
+        nv, ni = torch.topk(torch.where(valid & (val < 0), -val, ninf), kk, dim=1)
+        idx = torch.cat([pi, ni], 1)                                   # positives first, then negatives
+        ok = torch.cat([pv, nv], 1) != -float("inf")
+        v = val.gather(1, idx)
+        key = torch.where(ok, v.abs() if abs_mode else v, torch.full_like(v, -float("inf")))
+        order = torch.sort(key, dim=1, descending=True, stable=True).indices[:, :K]
+        sel = idx.gather(1, order)
+        okK = ok.gather(1, order)
+        colsK = torch.where(okK, Cc.gather(1, sel), torch.full_like(sel, -1))
+        diffsK = V.gather(1, sel[:, :, None].expand(n, K, C))
+        return colsK, diffsK
+
+    def _run(self, X: torch.Tensor, hist: List[dict]):
+        n, d = X.shape
+        plan = self._plan(hist, d, X.device)
+        m, C = max(int(plan[1].numel()), 1), 2
+        block = max(64, (1 << 23) // (m * C))
+        parts = [self._loco_block(X[a:a + block], hist, plan) for a in range(0, n, block)] or \
+            [self._loco_block(X[:0], hist, plan)]
+        return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
 
     def transform_columns(self, *cols, ds=None):
         vec: VectorColumn = cols[0]
@@ -187,24 +276,15 @@ class RecordInsightsLOCO(UnaryTransformer):
         hist = self.histories
         if hist is None:
             raise ValueError("RecordInsightsLOCO needs the input vector metadata (column histories)")
-        X = vec.values
-        n = X.shape[0]
-        res = []
-        block = max(1, self.chunk_elems // max(X.shape[1] * max(X.shape[1], 1), 1))
-        block = max(block, 64)
-        for a in range(0, n, block):
-            res.extend(self._loco_block(X[a:a + block], hist))
-        texts = []
-        for items in res:
-            texts.append(dict(insight_to_text(_history_json(hist[c]), diffs) for c, _, diffs in items))
-        return ObjectColumn(T.TextMap, texts)
+        cidx, diffs = self._run(vec.values, hist)
+        return InsightsColumn(cidx, diffs, [_history_json(h) for h in hist])
 
     def transform_row(self, *values):
         x = torch.as_tensor(np.asarray(values[0], np.float64))[None, :]
         if self.histories is None:
             raise ValueError("RecordInsightsLOCO has not seen vector metadata yet")
-        items = self._loco_block(x, self.histories)[0]
-        return dict(insight_to_text(_history_json(self.histories[c]), diffs) for c, _, diffs in items)
+        cidx, diffs = self._loco_block(x, self.histories)
+        return InsightsColumn(cidx, diffs, [_history_json(h) for h in self.histories]).row(0)
 
     def ctor_args(self):
         from ...workflow.io import stage_to_json

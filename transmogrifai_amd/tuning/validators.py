@@ -438,7 +438,8 @@ class OpValidator:
             by_fold: Dict[int, list] = {}
             for (j, (l, g, k)), pr in zip(batch, preds):
                 by_fold.setdefault(k, []).append(((l, g, k), pr))
-            batch_fn = getattr(self.evaluator, "selection_metric_batch", None)
+            batch_fn = getattr(self.evaluator, "selection_metric_batch", None) \
+                if os.environ.get("TMOG_BATCH_METRIC", "1") != "0" else None
             for k, items in by_fold.items():
                 yv = y[val_rows[k]]
                 vals = batch_fn(yv, [pr for _, pr in items]) if (batch_fn is not None and len(items) > 1) else None

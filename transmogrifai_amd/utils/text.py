@@ -139,6 +139,51 @@ def _encode_batch(strings: Sequence[Optional[str]]):
     return np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8), offs
 
 
+class CleanedBatch:
+    """:func:`clean_string` (or the raw value) of every string of a vocabulary, kept as one UTF-8 buffer with
+    per-string byte ranges, plus the first-appearance id of each cleaned value (equal cleaned strings share
+    an id) and its length in characters. Strings are decoded only when :meth:`value` asks for them."""
+
+    def __init__(self, buf: np.ndarray, starts: np.ndarray, ends: np.ndarray, ids: np.ndarray, n_ids: int,
+                 char_len: np.ndarray):
+        self.buf, self.starts, self.ends = buf, starts, ends
+        self.ids, self.n_ids, self.char_len = ids, n_ids, char_len
+
+    def value(self, j: int) -> str:
+        return self.buf[self.starts[j]:self.ends[j]].tobytes().decode("utf-8")
+
+
+def clean_batch(strings: Sequence[Optional[str]], clean: bool = True) -> CleanedBatch:
+    """Native batch of :func:`clean_string` (``ops/csrc/host/text_clean.cpp``): ASCII strings are cleaned in
+    C++, the rest (Unicode case mapping) by :func:`clean_string`; ids by exact cleaned bytes."""
+    from ..ops import _native as N
+    lib = N.host()
+    n = len(strings)
+    buf, offs = _encode_batch(strings)
+    if clean:
+        out = np.empty(max(int(offs[-1]), 1), np.uint8)
+        oo = np.empty(n + 1, np.int64)
+        fb = np.zeros(max(n, 1), np.uint8)
+        lib.tmog_clean_ascii(buf.ctypes.data, offs.ctypes.data, n, out.ctypes.data, oo.ctypes.data, fb.ctypes.data)
+        starts, ends = oo[:-1].copy(), oo[1:].copy()
+        char_len = ends - starts
+        bad = np.flatnonzero(fb[:n])
+        if bad.size:
+            extra = [clean_string(strings[i] or "").encode("utf-8") for i in bad]
+            base = int(oo[-1])
+            lens = np.fromiter((len(e) for e in extra), dtype=np.int64, count=bad.size)
+            starts[bad] = base + np.concatenate([[0], np.cumsum(lens)[:-1]])
+            ends[bad] = starts[bad] + lens
+            out = np.concatenate([out[:base], np.frombuffer(b"".join(extra) or b"\0", np.uint8)])
+            char_len[bad] = [len(e.decode("utf-8")) for e in extra]
+    else:
+        out, starts, ends = buf, offs[:-1].copy(), offs[1:].copy()
+        char_len = np.fromiter((len(s) if s else 0 for s in strings), dtype=np.int64, count=n)
+    ids = np.empty(max(n, 1), np.int64)
+    n_ids = int(lib.tmog_first_ids(out.ctypes.data, starts.ctypes.data, ends.ctypes.data, n, ids.ctypes.data))
+    return CleanedBatch(out, starts, ends, ids[:n], n_ids, char_len)
+
+
 def tokenize_batch(strings: Sequence[Optional[str]], to_lowercase: bool = True, min_token_length: int = 1,
                    stopwords=ENGLISH_STOPWORDS) -> TokenBatch:
     """:func:`tokenize` of every string at once through the native multithreaded tokenizer

@@ -22,6 +22,17 @@ log = logging.getLogger(__name__)
 Layer = List[Tuple[object, int]]
 
 _MEM_TRACE = os.environ.get("TMOG_MEM_TRACE") == "1"
+_STAGE_SYNC = os.environ.get("TMOG_STAGE_SYNC") == "1"
+
+
+def _clock() -> float:
+    """Stage timer; ``TMOG_STAGE_SYNC=1`` drains the device first so asynchronous kernels are charged to the
+    stage that launched them (profiling only: it serialises the host with the GPU)."""
+    if _STAGE_SYNC:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    return time.time()
 
 
 def compute_dag(features) -> List[Layer]:
@@ -46,7 +57,7 @@ def compute_dag(features) -> List[Layer]:
 def fit_and_transform_layer(layer: Layer, train: Dataset, test: Optional[Dataset], timings: Optional[dict] = None):
     fitted = []
     for st, _ in layer:
-        t0 = time.time()
+        t0 = _clock()
         if isinstance(st, OpEstimator):
             m = st.fit(train)
             if test is not None and len(test) > 0 and hasattr(m, "evaluate_model"):
@@ -56,14 +67,14 @@ def fit_and_transform_layer(layer: Layer, train: Dataset, test: Optional[Dataset
         else:
             fitted.append(st)
         if timings is not None:
-            timings[f"fit:{st.stage_name()}"] = time.time() - t0
+            timings[f"fit:{st.stage_name()}"] = _clock() - t0
     for m in fitted:
-        t0 = time.time()
+        t0 = _clock()
         train = m.transform(train)
         if test is not None and len(test) > 0:
             test = m.transform(test)
         if timings is not None:
-            timings[f"transform:{m.stage_name()}"] = time.time() - t0
+            timings[f"transform:{m.stage_name()}"] = _clock() - t0
         _mem_mark(timings, f"transform:{m.stage_name()}")
     return train, test, fitted
 
@@ -112,7 +123,7 @@ def _fit_layer_with_eval(layer, train, test, timings, li=0, last=None, keep=None
     from ..utils import listener as L
     fitted = []
     for st, _ in layer:
-        t0 = time.time()
+        t0 = _clock()
         if isinstance(st, OpEstimator):
             with L.stage(st.stage_name(), "fit", len(train)):
                 m = st.fit(train)
@@ -122,10 +133,10 @@ def _fit_layer_with_eval(layer, train, test, timings, li=0, last=None, keep=None
         else:
             fitted.append(st)
         if timings is not None:
-            timings[f"fit:{st.stage_name()}"] = time.time() - t0
+            timings[f"fit:{st.stage_name()}"] = _clock() - t0
         _mem_mark(timings, f"fit:{st.stage_name()}")
     for si, m in enumerate(fitted):
-        t0 = time.time()
+        t0 = _clock()
         with L.stage(m.stage_name(), "transform", len(train) + (len(test) if test is not None else 0)):
             train = m.transform(train)
             if test is not None and len(test) > 0:
@@ -137,7 +148,7 @@ def _fit_layer_with_eval(layer, train, test, timings, li=0, last=None, keep=None
                 if test is not None:
                     test = test.drop(dead)
         if timings is not None:
-            timings[f"transform:{m.stage_name()}"] = time.time() - t0
+            timings[f"transform:{m.stage_name()}"] = _clock() - t0
         _mem_mark(timings, f"transform:{m.stage_name()}")
     return train, test, fitted
 

@@ -90,7 +90,7 @@ def _date_list(pm, a):
     elif pm.get("fillWithPivotModeHour"):
         pv = "ModeHour"
     else:
-        pv = "SinceFirst" if pm.get("first") else "SinceLast"
+        pv = "SinceFirst" if pm.get("first", True) else "SinceLast"
     st.params["pivot"] = pv
     if pm.get("referenceDate") is not None:
         st.params["reference_date"] = int(pm["referenceDate"])
