@@ -43,13 +43,30 @@ def main():
     for a, b in zip(edges, edges[1:]):
         g = [x for x in gaps if a <= x < b]
         print(f"  gaps [{a / 1e3:>8.0f}, {b / 1e3:>8.0f}) us: n={len(g):6d}  total {sum(g) / 1e6:8.2f} ms")
-    tot = defaultdict(lambda: [0, 0])
+    tot = defaultdict(list)
     for s, e, n in rows:
-        k = n.split("(")[0][:90]
-        tot[k][0] += 1
-        tot[k][1] += e - s
-    for k, (c, t) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:25]:
-        print(f"  {t / 1e6:9.2f} ms  {c:7d}  {k}")
+        tot[_short(n)].append(e - s)
+    print("  total ms   calls  p50 us  p90 us  max us | share of time in calls <20us, 20-100us, 100-500us, >500us")
+    for k, d in sorted(tot.items(), key=lambda kv: -sum(kv[1]))[:25]:
+        d = sorted(d)
+        t = sum(d)
+        q = lambda f: d[min(len(d) - 1, int(f * len(d)))] / 1e3
+        sh = [sum(x for x in d if a <= x < b) / max(t, 1) for a, b in
+              ((0, 20_000), (20_000, 100_000), (100_000, 500_000), (500_000, 1 << 62))]
+        print(f"  {t / 1e6:8.2f} {len(d):7d} {q(0.5):7.1f} {q(0.9):7.1f} {d[-1] / 1e3:7.0f} | "
+              + " ".join(f"{100 * x:5.1f}%" for x in sh) + f"  {k}")
+
+
+def _short(n: str) -> str:
+    n = n.replace("(anonymous namespace)::", "").replace("void ", "")
+    depth, out = 0, []
+    for ch in n:                      # drop the argument list, keep template arguments
+        if ch == "(" and depth == 0:
+            break
+        depth += ch == "<"
+        depth -= ch == ">"
+        out.append(ch)
+    return "".join(out)[:100]
 
 
 if __name__ == "__main__":
