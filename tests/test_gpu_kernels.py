@@ -141,6 +141,34 @@ def test_xgb_pipelined_parts_identical_to_single_loop(monkeypatch):
     assert _native_loaded()
 
 
+def test_xgb_epilogue_quantisation_maxima_identical_trees(monkeypatch):
+    """The per-job max |g| / max h that the round epilogue max-reduces (plus the once-computed max of the
+    rows a job never trains on) give exactly the scales, hence the trees, of scanning G / H each round."""
+    from transmogrifai_amd.models.base import FitJob
+    from transmogrifai_amd.models.trees import XGBoostClassifierLearner
+    g = torch.Generator().manual_seed(5)
+    n, d = 30_000, 14
+    X = torch.randn(n, d, generator=g)
+    X[:, :4] = (X[:, :4] > 0.7).float()
+    y = ((X[:, 4] + X[:, 0] - 0.5 * X[:, 6] + 0.5 * torch.randn(n, generator=g)) > 0).float()
+    Xd, yd = X.cuda(), y.cuda()
+    params = dict(XGBoostClassifierLearner.defaults, num_round=20, max_depth=6, eta=0.3, missing=0.0,
+                  num_early_stopping_rounds=4)
+    jobs = [FitJob(dict(params, min_child_weight=m), torch.arange(k, n, 3, device="cuda"))
+            for m in (1.0, 10.0) for k in range(3)]
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TMOG_XGB_AMAX", flag)
+        outs.append(XGBoostClassifierLearner().fit_batch(Xd, yd, jobs))
+    for a, b in zip(*outs):
+        assert a["num_trees"] == b["num_trees"]
+        for k in a["forest"]:
+            va, vb = a["forest"][k], b["forest"][k]
+            if isinstance(va, np.ndarray):
+                np.testing.assert_array_equal(va, vb, err_msg=k)
+    assert _native_loaded()
+
+
 def test_aupr_counts_kernel_matches_torch():
     """Early-stopping AuPR from (label, score-bin) count tables: HIP kernel vs the torch path, including
     leading empty bins, a set without positives and an empty set."""

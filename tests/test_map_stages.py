@@ -12,7 +12,7 @@ from transmogrifai_amd.stages.feature.bucketizers import DecisionTreeNumericMapB
 
 def test_real_map_vectorizer_mean_fill():
     ds, (m,) = TestFeatureBuilder.of(("m", T.RealMap, [{"a": 1.0, "b": 2.0}, {"a": 3.0}, {}]))
-    st = MP.RealMapVectorizer(track_nulls=True).set_input(m)
+    st = MP.RealMapVectorizer(track_nulls=True, fill_with_mean=True).set_input(m)
     model, out = check_estimator(st, ds, check_rows=False)
     assert out[0] == [1.0, 0.0, 2.0, 0.0] and out[1] == [3.0, 0.0, 2.0, 1.0] and out[2] == [2.0, 1.0, 2.0, 1.0]
 
@@ -189,3 +189,40 @@ def test_table_tree_splits_equal_engine_tree():
         for imp in ("gini", "entropy"):
             for md, mi, mg in ((5, 1, 0.01), (3, 20, 0.0)):
                 assert tree_splits(x, y, md, 32, mi, mg, imp) == tree_splits_dp(x, y, md, 32, mi, mg, imp)
+
+
+_TMP_TOP = [{"a": "d", "b": "d"}, {"a": "e"}, {"c": "D"}, {"c": "d", "a": "d"}]
+_TMP_BOT = [{"x": "W"}, {"z": "w", "y": "v"}, {"x": "w", "y": "V"}, {"z": "v"}]
+
+
+@pytest.mark.parametrize("kw,width,expected", [
+    (dict(top_k=10, min_support=0, track_nulls=False), 14, [[2, 5, 7], [3, 9, 12], [0, 7, 9], [0, 2, 11]]),
+    (dict(top_k=10, min_support=0, track_nulls=True), 20,
+     [[2, 3, 7, 10, 15, 19], [2, 4, 9, 12, 13, 17], [0, 6, 9, 10, 13, 19], [0, 3, 9, 12, 15, 16]]),
+    (dict(top_k=10, min_support=0, track_nulls=False, clean_text=False, clean_keys=False), 17,
+     [[3, 6, 8], [4, 12, 15], [0, 9, 11], [1, 3, 14]]),
+    (dict(top_k=1, min_support=0, track_nulls=False), 12, [[2, 4, 6], [3, 8, 11], [0, 6, 8], [0, 2, 10]]),
+    (dict(top_k=1, min_support=0, track_nulls=True), 18,
+     [[2, 3, 6, 9, 14, 17], [2, 4, 8, 11, 12, 16], [0, 5, 8, 9, 12, 17], [0, 3, 8, 11, 14, 15]]),
+    (dict(top_k=10, min_support=2, track_nulls=False), 10, [[2, 4, 5], [3, 7, 9], [0, 5, 7], [0, 2, 9]]),
+    (dict(top_k=10, min_support=2, track_nulls=True), 16,
+     [[2, 3, 6, 8, 13, 15], [2, 4, 7, 10, 11, 14], [0, 5, 7, 8, 11, 15], [0, 3, 7, 10, 13, 14]]),
+])
+def test_text_map_pivot_reference_expectations(kw, width, expected):
+    """TextMapPivotVectorizerTest.scala expected vectors. The reference lists the keys of a map in its Scala
+    Map iteration order (top: C, A, B; bot: X, Y, Z -- an artefact of Spark's reduce), ours in sorted key
+    order; the columns are compared after placing ours in the reference key order (values within a key
+    keep their count-then-value order on both sides)."""
+    ds, (t, b) = TestFeatureBuilder.of(("top", T.TextMap, _TMP_TOP), ("bot", T.TextMap, _TMP_BOT))
+    p = dict(clean_keys=True)
+    p.update(kw)
+    m = MP.TextMapPivotVectorizer(**p).set_input(t, b).fit(ds)
+    out = m.transform(ds)[m.get_output_feature_name()].values.numpy()
+    assert out.shape[1] == width
+    cols = m.metadata["vector_metadata"].columns
+    rank = {"top": "cab", "bot": "xyz"}
+    order = sorted(range(len(cols)), key=lambda i: (cols[i].parent_feature_name[0] != "top",
+                                                    rank[cols[i].parent_feature_name[0]].index(cols[i].grouping.lower()),
+                                                    i))
+    got = [[order.index(j) for j in np.flatnonzero(r)] for r in out]
+    assert [sorted(g) for g in got] == expected

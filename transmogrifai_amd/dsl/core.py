@@ -411,8 +411,11 @@ def _vec_geo(self, fill_with_mean: bool = True, track_nulls: bool = True, others
 
 @register(T.OPMap, "vectorize")
 def _vec_map(self, others=(), **kw):
+    """``RichMapFeature.vectorize`` (RichMapFeature.scala): Transmogrifier defaults, overridable by name
+    (``default_value``, ``fill_with_mean`` / ``fill_with_mode``, ``clean_keys``, ``top_k``, ``min_support``,
+    ``track_nulls``, ``white_list_keys`` / ``black_list_keys``, ...)."""
     from ..stages.feature.maps import map_vectorize
-    return map_vectorize(self.wtype, _others(self, others), None, D)[0]
+    return map_vectorize(self.wtype, _others(self, others), None, D, **kw)[0]
 
 
 @register(T.OPVector, "drop_indices_by")

@@ -19,7 +19,7 @@ import ctypes as C
 import math
 import os
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -298,6 +298,24 @@ class _GrowArgs(C.Structure):
                 ("XbT", C.c_void_p), ("gh", C.c_void_p), ("gh_alt", C.c_void_p), ("n_entries", C.c_int64)]
 
 
+_ENTRY_MODELS: Dict[tuple, torch.Tensor] = {}
+
+
+def _entry_models(models: tuple, counts: tuple, dev) -> torch.Tensor:
+    """Model id of every root entry (job j's ``counts[j]`` entries carry ``models[j]``), cached: the boosting
+    rounds of one active job set reuse it. One fill per job -- ``torch.repeat_interleave`` with a handful
+    of repeats runs one thread per repeat on ROCm (~350 us for 2M entries)."""
+    key = (models, counts, str(dev))
+    t = _ENTRY_MODELS.get(key)
+    if t is None:
+        if len(_ENTRY_MODELS) >= 8:
+            _ENTRY_MODELS.clear()
+        parts = [torch.full((c,), m, dtype=torch.int64, device=dev) for m, c in zip(models, counts) if c]
+        t = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev)
+        _ENTRY_MODELS[key] = t
+    return t
+
+
 def _stage_gh(rows: torch.Tensor, counts, jobs, t1f, t2f, qscale, stride: int) -> torch.Tensor:
     """``[total, 2]`` int32: each root entry's quantised (q(w g), q(w h)) under its job's model scales -- the
     histogram kernels' ``rintf((w * t) * qscale)`` in the same fp32 operation order (tree_kernels.hip
@@ -306,8 +324,7 @@ def _stage_gh(rows: torch.Tensor, counts, jobs, t1f, t2f, qscale, stride: int) -
     e = rows.to(torch.int64) & 0xFFFFFFFF
     r = e & 0xFFFFFF
     w = (e >> 24).to(torch.float32)
-    model = torch.repeat_interleave(torch.as_tensor([j.model for j in jobs], dtype=torch.int64, device=dev),
-                                    torch.as_tensor(counts, dtype=torch.int64, device=dev))
+    model = _entry_models(tuple(int(j.model) for j in jobs), tuple(int(c) for c in counts), dev)
     idx = model * int(stride) + r
     qs = qscale.reshape(-1, qscale.shape[-1])[model]
     g = torch.round((w * t1f.reshape(-1)[idx]) * qs[:, 0]).to(torch.int32)
@@ -406,7 +423,8 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 t2: Optional[torch.Tensor] = None, B: int = 32, missing_bin: int = -1,
                 subtract: bool = True, chunk_rows: int = 4096, rng_seed: int = 0,
                 collect_leaves: bool = False, groups: Optional[int] = None, csr=None, root=None,
-                fp: Optional[FpPlan] = None, slot_base: int = 0, XbT: Optional[torch.Tensor] = None) -> Forest:
+                fp: Optional[FpPlan] = None, slot_base: int = 0, XbT: Optional[torch.Tensor] = None,
+                quant_amax: Optional[torch.Tensor] = None, quant_wmax: Optional[float] = None) -> Forest:
     """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``.
 
     The level loop runs natively (``ops/csrc/common/tree_grow.hpp``): on the GPU every job group gets
@@ -425,6 +443,10 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
 
     ``slot_base``: first native per-group resource slot (stream, staging, histogram buffers) of this call;
     calls running concurrently from several host threads must use disjoint slot ranges.
+
+    ``quant_amax`` ``[n_models, 2]`` float32 / ``quant_wmax``: the per-model max |t1|, max |t2| over all N rows
+    and the max entry weight, when the caller already knows them (boosting: the round epilogue computes
+    them), instead of scanning ``t1`` / ``t2`` / the entries here -- same scales.
 
     ``fp``: feature-parallel growth (``fp_plan``): every rank calls with the same jobs, rows and ``Xb``;
     each builds histograms of its feature slice only (``csr`` must then be the slice's, from
@@ -464,7 +486,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     else:
         rows, counts = _root_rows(jobs, dev)
     rows_alt = torch.empty_like(rows)
-    qscale, qinv = _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev)
+    qscale, qinv = _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev, quant_amax, quant_wmax)
     total = int(rows.numel())
     gh = gh_alt = None
     if on_gpu and mode == MODE_GH and total and t1f is not None and t2f is not None \
@@ -590,7 +612,7 @@ def _const_tensor(a: np.ndarray, dev) -> torch.Tensor:
     return t
 
 
-def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev):
+def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev, amax_hint=None, wmax_hint=None):
     """Per-(model, stat) power-of-two fixed-point scales for the int64 histograms (see the
     "Fixed-point statistics" note in ops/csrc/hip/tree_kernels.hip). A row's contribution is
     ``rint(v * scale)`` with ``|v * scale| <= qmax``, so a ``chunk_rows``-row LDS partial fits int32.
@@ -602,9 +624,12 @@ def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev):
     # an LDS partial sums at most max(chunk_rows, CSR_ITEM_ROWS) rows (CSR items always span 1024 rows,
     # tree_grow.hpp kCsrRows), so size the per-row bound from the larger of the two
     qmax = float(min(1 << 22, (2 ** 31 - 1) // max(1, int(chunk_rows), CSR_ITEM_ROWS) - 1))
-    wmax = ((rows >> 24) & 0xFF).max().to(torch.float32)
+    wmax = torch.tensor(float(wmax_hint), dtype=torch.float32, device=dev) if wmax_hint is not None else \
+        ((rows >> 24) & 0xFF).max().to(torch.float32)
 
-    def amax(t):
+    def amax(t, k=0):
+        if amax_hint is not None:
+            return amax_hint[:n_models, k].to(torch.float32)
         if t is None:
             return torch.zeros(n_models, dtype=torch.float32, device=dev)
         v = t.reshape(t.shape[0], -1) if t.dim() == 2 else t.reshape(1, -1)
@@ -627,7 +652,7 @@ def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev):
         m1 = amax(t1f)
         sc = torch.stack([torch.ones_like(m1), pow2(m1), pow2(m1 * m1)], 1)
     else:
-        sc = torch.stack([pow2(amax(t1f)), pow2(amax(t2f))], 1)
+        sc = torch.stack([pow2(amax(t1f, 0)), pow2(amax(t2f, 1))], 1)
     sc = sc.to(torch.float32).contiguous()
     return sc, (1.0 / sc.to(torch.float64)).contiguous()
 

@@ -699,6 +699,19 @@ class XGBoostClassifierLearner(_BoostLearner):
                 if rounds[p] > 0:
                     g, h = self._grad(yy, Fm[p])
                     G[p], H[p] = g.to(torch.float32), h.to(torch.float32)
+        # Quantisation maxima of the next round's (g, h) per job (tree_engine._quant_scales: max over all N
+        # rows). Rows a job never trains on keep their round-0 statistics, so their max is taken once; the
+        # round epilogue max-reduces the rows it rewrites -- no [P, N] scan per round.
+        amax_cur = comp = tam = None
+        if fused and os.environ.get("TMOG_XGB_AMAX", "1") != "0":
+            amax_cur = torch.stack([G.abs().amax(1), H.abs().amax(1)], 1).contiguous()
+            comp = torch.zeros(P, 2, dtype=torch.float32, device=dev)
+            for p in range(P):
+                out = torch.ones(N, dtype=torch.bool, device=dev)
+                out[rows[p]] = False
+                comp[p, 0] = torch.where(out, G[p].abs(), torch.zeros_like(G[p])).amax()
+                comp[p, 1] = torch.where(out, H[p].abs(), torch.zeros_like(H[p])).amax()
+            tam = torch.zeros(P, 2, dtype=torch.int32, device=dev)
 
         def run(ps, slot_base=0, groups=None):
             """Boosting rounds of the jobs ``ps`` (their trees do not depend on which other jobs grow
@@ -740,15 +753,23 @@ class XGBoostClassifierLearner(_BoostLearner):
                     root = (packed.clone(), cnts)
                 forest = TE.grow_forest(Xg, n_bins_g, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
                                         missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root, fp=fp,
-                                        slot_base=slot_base, groups=groups, XbT=XgT)
+                                        slot_base=slot_base, groups=groups, XbT=XgT,
+                                        quant_amax=amax_cur, quant_wmax=1.0 if amax_cur is not None else None)
                 if colperm is not None:
                     internal = forest.nodes[:, 2] >= 0
                     forest.nodes[internal, 0] = colperm[forest.nodes[internal, 0]]
                 need = [p for p in act if esr[p] > 0]
                 auc_counts = None
                 if fused:
+                    ai = None
+                    if tam is not None:
+                        ai = TE._const_tensor(np.asarray(act, np.int64), dev)
+                        tam.index_fill_(0, ai, 0)
                     auc_counts = self._fused_epilogue(Fm, G, H, yf, forest, act, N,
-                                                      AUC_BINS if (need and self.classification) else 0)
+                                                      AUC_BINS if (need and self.classification) else 0, tam)
+                    if tam is not None:
+                        amax_cur.index_copy_(0, ai, torch.maximum(comp.index_select(0, ai),
+                                                                  tam.index_select(0, ai).view(torch.float32)))
                 else:
                     _add_tree_margins(Fm, forest, Xb, act, [1.0] * len(act), tjobs)
                 for k, p in enumerate(act):
@@ -789,7 +810,7 @@ class XGBoostClassifierLearner(_BoostLearner):
 
     objective_code = 0      # boost_epilogue_kernel: 0 = binary:logistic, 1 = squared error
 
-    def _fused_epilogue(self, Fm, G, H, yf, forest, act, N, bins):
+    def _fused_epilogue(self, Fm, G, H, yf, forest, act, N, bins, amax=None):
         """Margins += this round's leaf values, next round's (g, h), and (with ``bins``) the per-job
         (label, score-bin) counts of the new training scores, in one HIP launch."""
         from ..ops import _native as NV
@@ -802,7 +823,8 @@ class XGBoostClassifierLearner(_BoostLearner):
         NV.check(NV.hip().tmog_hip_boost_epilogue(
             NV.ptr(la.rows), NV.ptr(la.gid), int(la.rows.numel()), NV.ptr(val), NV.ptr(la.tree.contiguous()),
             NV.ptr(tree_job), int(N), NV.ptr(Fm), NV.ptr(G), NV.ptr(H), NV.ptr(yf), self.objective_code,
-            NV.ptr(counts), int(bins), int(val.shape[0]), len(act), int(P), NV.stream(dev)), "boost_epilogue")
+            NV.ptr(counts), int(bins), int(val.shape[0]), len(act), int(P), NV.stream(dev), NV.ptr(amax)),
+            "boost_epilogue")
         return counts
 
     def _outputs(self, state, m):

@@ -80,7 +80,7 @@ _HIP_SIGS = {
     "tmog_hip_grow_copy": [P, I32, P, P, P, P, P, P, P, P],
     "tmog_hip_grow_free": [P],
     "tmog_hip_zero_segments": [P, P, P, I32, I64, P],
-    "tmog_hip_boost_epilogue": [P, P, I64, P, P, P, I64, P, P, P, P, I32, P, I32, I64, I64, I64, P],
+    "tmog_hip_boost_epilogue": [P, P, I64, P, P, P, I64, P, P, P, P, I32, P, I32, I64, I64, I64, P, P],
     "tmog_hip_aupr_counts": [P, I32, I32, P, P],
     "tmog_hip_owlqn_direction": [P, P, P, P, P, P, I32, I32, I32, I32, P, P, P, P, P],
     "tmog_hip_owlqn_candidate": [P, P, P, P, P, P, I32, I32, P, P, P, P],

@@ -32,8 +32,10 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
     const uint32_t* __restrict__ entries, const int32_t* __restrict__ gid, int64_t n_entries,
     const float* __restrict__ gid_value, const int64_t* __restrict__ gid_tree, const int64_t* __restrict__ tree_job,
     int64_t N, double* __restrict__ F, float* __restrict__ G, float* __restrict__ H, const float* __restrict__ y,
-    int objective, int32_t* __restrict__ auc_hist, int bins, int64_t n_gid, int64_t n_trees, int64_t P) {
+    int objective, int32_t* __restrict__ auc_hist, int bins, int64_t n_gid, int64_t n_trees, int64_t P,
+    uint32_t* __restrict__ amax) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float ag = 0.f, ah = 0.f;                    // this lane's |g| and h (for the next round's quantisation)
   // no early returns: the AuPR-count aggregation below needs every lane of the wave
   int64_t slot = -1;                           // this lane's (job, label, score-bin) counter, -1 = none
   bool ok = e < n_entries;
@@ -59,16 +61,46 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
     const float yr = y[r];
     if (objective == 0) {
       const double pr = 1.0 / (1.0 + exp(-m));
-      G[k] = (float)(pr - (double)yr);
-      H[k] = (float)fmax(pr * (1.0 - pr), 1e-16);
+      const float gk = (float)(pr - (double)yr), hk = (float)fmax(pr * (1.0 - pr), 1e-16);
+      G[k] = gk;
+      H[k] = hk;
+      ag = fabsf(gk);
+      ah = hk;
       if (auc_hist) {
         const float sc = fminf(fmaxf((float)pr, 0.f), 1.f);
         const int b = (int)(sc * (float)(bins - 1));
         slot = (p * 2 + (yr > 0.5f ? 1 : 0)) * bins + (bins - 1 - b);
       }
     } else {
-      G[k] = (float)(m - (double)yr);
+      const float gk = (float)(m - (double)yr);
+      G[k] = gk;
       H[k] = 1.f;
+      ag = fabsf(gk);
+      ah = 1.f;
+    }
+  }
+  if (amax) {
+    // per-job max |g| and max h of the new statistics (tree_engine._quant_scales of the next round): the
+    // wave peels off its distinct jobs (usually one), max-reduces each over the matching lanes and issues
+    // one atomicMax per job on the float bits (non-negative floats order like their bit patterns)
+    const int lane = threadIdx.x & 63;
+    bool pend = ok;
+    for (int it = 0; it < 64; ++it) {
+      const unsigned long long act = __ballot(pend);
+      if (act == 0ull) break;
+      const int leader = __ffsll((long long)act) - 1;
+      const int64_t lp = __shfl(p, leader, 64);
+      const bool mine = pend && p == lp;
+      float mg = mine ? ag : 0.f, mh = mine ? ah : 0.f;
+      for (int off = 32; off > 0; off >>= 1) {
+        mg = fmaxf(mg, __shfl_xor(mg, off, 64));
+        mh = fmaxf(mh, __shfl_xor(mh, off, 64));
+      }
+      if (lane == leader) {
+        atomicMax(amax + 2 * lp, __float_as_uint(mg));
+        atomicMax(amax + 2 * lp + 1, __float_as_uint(mh));
+      }
+      pend = pend && !mine;
     }
   }
   if (auc_hist) {
@@ -259,12 +291,12 @@ extern "C" {
 int tmog_hip_boost_epilogue(const uint32_t* entries, const int32_t* gid, int64_t n_entries, const float* gid_value,
                             const int64_t* gid_tree, const int64_t* tree_job, int64_t N, double* F, float* G, float* H,
                             const float* y, int objective, int32_t* auc_hist, int bins, int64_t n_gid,
-                            int64_t n_trees, int64_t P, hipStream_t stream) {
+                            int64_t n_trees, int64_t P, hipStream_t stream, uint32_t* amax) {
   if (n_entries == 0) return 0;
   if (N >= (1 << 24)) return -2;
   hipLaunchKernelGGL(boost_epilogue_kernel, dim3((unsigned)((n_entries + 255) / 256)), dim3(256), 0, stream, entries,
                      gid, n_entries, gid_value, gid_tree, tree_job, N, F, G, H, y, objective, auc_hist, bins, n_gid,
-                     n_trees, P);
+                     n_trees, P, amax);
   return (int)hipGetLastError();
 }
 

@@ -361,7 +361,7 @@ def _get(m, k, clean):
 class MapVectorizer(VectorizerMixin, SequenceEstimator):
     operation_name = "vecMap"
     _defaults = {"kind": "real", "clean_keys": False, "clean_text": True, "track_nulls": True,
-                 "fill_with_mean": True, "fill_with_mode": True, "fill_value": 0.0, "top_k": 20, "min_support": 10,
+                 "fill_with_mean": False, "fill_with_mode": False, "fill_value": 0.0, "top_k": 20, "min_support": 10,
                  "reference_date": None, "max_cardinality": 30, "num_features": 512, "allow_keys": None,
                  "block_keys": None}
     # row-sharded fits reduce per-key statistics over the ranks: key union and (key, value) counts in one
@@ -491,14 +491,31 @@ class MapVectorizer(VectorizerMixin, SequenceEstimator):
                                   ref, methods, p["num_features"])
 
 
-def map_vectorize(t, feats, label, D) -> list:
+# RichMapFeature.vectorize argument names -> MapVectorizer params
+_MAP_ARGS = {"default_value": "fill_value", "fill_value": "fill_value", "fill_with_mean": "fill_with_mean",
+             "fill_with_mode": "fill_with_mode", "clean_keys": "clean_keys", "clean_text": "clean_text",
+             "track_nulls": "track_nulls", "top_k": "top_k", "min_support": "min_support",
+             "white_list_keys": "allow_keys", "allow_keys": "allow_keys", "black_list_keys": "block_keys",
+             "block_keys": "block_keys", "reference_date": "reference_date",
+             "max_categorical_cardinality": "max_cardinality", "num_hashes": "num_features"}
+
+
+def map_vectorize(t, feats, label, D, **overrides) -> list:
+    """The Transmogrifier's map vectorizer (Transmogrifier.scala:140-215: fill real maps with the mean and
+    integral maps with the mode, pivot the text-like maps); ``overrides`` take the RichMapFeature.vectorize
+    argument names."""
     kind = _kind_of(t)
     if t is T.PhoneMap or t is T.EmailMap or t is T.URLMap or t is T.Base64Map:
         kind = "pivot"
-    st = MapVectorizer(kind=kind, clean_keys=D.CleanKeys, clean_text=D.CleanText, track_nulls=D.TrackNulls,
-                       top_k=D.TopK, min_support=D.MinSupport, reference_date=D.ReferenceDate,
-                       max_cardinality=D.MaxCategoricalCardinality, num_features=D.DefaultNumOfFeatures,
-                       fill_value=float(D.FillValue))
+    params = dict(kind=kind, clean_keys=D.CleanKeys, clean_text=D.CleanText, track_nulls=D.TrackNulls,
+                  top_k=D.TopK, min_support=D.MinSupport, reference_date=D.ReferenceDate,
+                  max_cardinality=D.MaxCategoricalCardinality, num_features=D.DefaultNumOfFeatures,
+                  fill_value=float(D.FillValue), fill_with_mean=D.FillWithMean, fill_with_mode=D.FillWithMode)
+    for k, v in overrides.items():
+        if k not in _MAP_ARGS:
+            raise TypeError(f"map vectorize got an unexpected argument {k!r}")
+        params[_MAP_ARGS[k]] = v
+    st = MapVectorizer(**params)
     return [st.set_input(feats).get_output()]
 
 
