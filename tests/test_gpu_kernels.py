@@ -169,6 +169,41 @@ def test_xgb_epilogue_quantisation_maxima_identical_trees(monkeypatch):
     assert _native_loaded()
 
 
+@pytest.mark.parametrize("learner", ["xgb", "rf", "rf3"])
+def test_pair_scan_identical_to_subtract_then_scan(monkeypatch, learner):
+    """Sibling pairs' subtraction + split scan fused in one pass (pair_scan_kernel) grows exactly the trees
+    of hist_subtract followed by the node-wise split scan: Newton (XGBoost), Gini with 2 and 3 classes."""
+    from transmogrifai_amd.models.base import FitJob
+    from transmogrifai_amd.models.trees import RandomForestClassifierLearner, XGBoostClassifierLearner
+    g = torch.Generator().manual_seed(6)
+    n, d = 30_000, 18
+    X = torch.randn(n, d, generator=g)
+    X[:, :5] = (X[:, :5] > 0.6).float()
+    z = X[:, 5] + X[:, 0] - 0.5 * X[:, 7] + 0.5 * torch.randn(n, generator=g)
+    y = (z > 0).float() if learner != "rf3" else torch.bucketize(z, torch.tensor([-0.5, 0.5])).float()
+    Xd, yd = X.cuda(), y.cuda()
+    if learner == "xgb":
+        L = XGBoostClassifierLearner
+        params = dict(L.defaults, num_round=12, max_depth=7, eta=0.3, missing=0.0)
+        jobs = [FitJob(dict(params, min_child_weight=m), torch.arange(k, n, 3, device="cuda"))
+                for m in (1.0, 10.0) for k in range(3)]
+    else:
+        L = RandomForestClassifierLearner
+        params = dict(L.defaults, num_trees=6, max_depth=8, feature_subset_strategy="all")   # no subsets
+        jobs = [FitJob(dict(params, min_instances_per_node=mi), torch.arange(k, n, 2, device="cuda"))
+                for mi in (1, 10) for k in range(2)]
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TMOG_PAIR_SCAN", flag)
+        outs.append(L().fit_batch(Xd, yd, jobs))
+    for a, b in zip(*outs):
+        for k in a["forest"]:
+            va, vb = a["forest"][k], b["forest"][k]
+            if isinstance(va, np.ndarray):
+                np.testing.assert_array_equal(va, vb, err_msg=k)
+    assert _native_loaded()
+
+
 def test_aupr_counts_kernel_matches_torch():
     """Early-stopping AuPR from (label, score-bin) count tables: HIP kernel vs the torch path, including
     leading empty bins, a set without positives and an empty set."""

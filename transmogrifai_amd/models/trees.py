@@ -711,7 +711,7 @@ class XGBoostClassifierLearner(_BoostLearner):
                 out[rows[p]] = False
                 comp[p, 0] = torch.where(out, G[p].abs(), torch.zeros_like(G[p])).amax()
                 comp[p, 1] = torch.where(out, H[p].abs(), torch.zeros_like(H[p])).amax()
-            tam = torch.zeros(P, 2, dtype=torch.int32, device=dev)
+            tam = torch.zeros(64, P, 2, dtype=torch.int32, device=dev)     # boost_kernels.hip kAmaxCopies
 
         def run(ps, slot_base=0, groups=None):
             """Boosting rounds of the jobs ``ps`` (their trees do not depend on which other jobs grow
@@ -764,12 +764,12 @@ class XGBoostClassifierLearner(_BoostLearner):
                     ai = None
                     if tam is not None:
                         ai = TE._const_tensor(np.asarray(act, np.int64), dev)
-                        tam.index_fill_(0, ai, 0)
+                        tam.index_fill_(1, ai, 0)
                     auc_counts = self._fused_epilogue(Fm, G, H, yf, forest, act, N,
                                                       AUC_BINS if (need and self.classification) else 0, tam)
                     if tam is not None:
-                        amax_cur.index_copy_(0, ai, torch.maximum(comp.index_select(0, ai),
-                                                                  tam.index_select(0, ai).view(torch.float32)))
+                        amax_cur.index_copy_(0, ai, torch.maximum(
+                            comp.index_select(0, ai), tam.index_select(1, ai).view(torch.float32).amax(0)))
                 else:
                     _add_tree_margins(Fm, forest, Xb, act, [1.0] * len(act), tjobs)
                 for k, p in enumerate(act):

@@ -528,6 +528,17 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
     }
     std::vector<uint8_t> build(m, 1);
     for (int64_t b : d_big) build[b] = 0;
+    // GPU: a sibling pair's subtraction and both children's split scans run as one pass (pair_scan_kernel)
+    // -- the two nodes are flagged (params slot 4) so the node-wise scan skips them; same decisions
+    const char* ps_env = std::getenv("TMOG_PAIR_SCAN");
+    const bool pair_fuse = BK::kGPU && !use_subset && S <= 16 && B <= 64 && !d_big.empty() &&
+                           !(ps_env && ps_env[0] == '0');
+    std::vector<int32_t> d_sj, d_bj;
+    if (pair_fuse)
+      for (size_t q = 0; q < d_big.size(); ++q) {
+        d_sj.push_back((int32_t)d_small[q]);
+        d_bj.push_back((int32_t)d_big[q]);
+      }
     std::vector<int64_t> nb(m), nc(m);
     std::vector<int32_t> nmd(m);
     std::vector<float> params((size_t)m * 8, 0.f);
@@ -546,6 +557,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
       P[6] = (float)a.job_eps[j0 + t];
       P[7] = can[i] ? 1.f : 0.f;
     }
+    for (size_t q = 0; q < d_sj.size(); ++q) params[(size_t)d_sj[q] * 8 + 4] = params[(size_t)d_bj[q] * 8 + 4] = 1.f;
     // ---- work items (GPU) / built-node arrays (CPU)
     std::vector<HistItemH> hitems;
     std::vector<PartItemH> citems;
@@ -642,6 +654,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
     const size_t o_bnb = st1.add(b_nb), o_bnc = st1.add(b_nc), o_bnfo = st1.add(b_nfo), o_bnnf = st1.add(b_nnf);
     const size_t o_bnmd = st1.add(b_nmd), o_bnho = st1.add(b_nho);
     const size_t o_nb = st1.add(nb), o_nc = st1.add(nc);
+    const size_t o_sj = st1.add(d_sj), o_bj = st1.add(d_bj);
     const uint8_t* d1 = bk.ship(st1, 0);
 #define TM_P(T_, off) ((T_*)(d1 + (off)))
     const int32_t* flist = own_list ? TM_P(const int32_t, o_fl) : all_feats;
@@ -656,7 +669,17 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
                   (int)b_nb.size(), TM_P(const int64_t, o_bnb), TM_P(const int64_t, o_bnc),
                   TM_P(const int32_t, o_bnfo), TM_P(const int32_t, o_bnnf), TM_P(const int32_t, o_bnmd),
                   TM_P(const int64_t, o_bnho), stat_sc, n_wide, need_general);
-    if (!d_big.empty())
+    bool pairs_done = false;
+    if constexpr (BK::kGPU) {
+      if (pair_fuse) {
+        bk.pair_scan(a, hist, prev_hist, TM_P(const int64_t, o_dp), TM_P(const int32_t, o_sj),
+                     TM_P(const int32_t, o_bj), (int)d_sj.size(), TM_P(const int64_t, o_nho),
+                     TM_P(const int32_t, o_nnf), TM_P(const int32_t, o_nfo), flist, TM_P(const float, o_par),
+                     TM_P(const int32_t, o_nmd), max_nf, m, split_n_multi);
+        pairs_done = true;
+      }
+    }
+    if (!d_big.empty() && !pairs_done)
       bk.hist_subtract(hist, prev_hist, TM_P(const int64_t, o_dp), TM_P(const int64_t, o_ds),
                        TM_P(const int64_t, o_do), TM_P(const int64_t, o_dz), (int)d_big.size(), d_max, live_dense,
                        a.B * a.S, a.S);

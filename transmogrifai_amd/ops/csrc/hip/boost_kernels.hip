@@ -28,6 +28,8 @@
 
 namespace {
 
+constexpr int kAmaxCopies = 64;   // boost_epilogue_kernel's per-job maxima: [kAmaxCopies][P][2] (trees.py)
+
 __global__ void __launch_bounds__(256) boost_epilogue_kernel(
     const uint32_t* __restrict__ entries, const int32_t* __restrict__ gid, int64_t n_entries,
     const float* __restrict__ gid_value, const int64_t* __restrict__ gid_tree, const int64_t* __restrict__ tree_job,
@@ -82,7 +84,9 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
   if (amax) {
     // per-job max |g| and max h of the new statistics (tree_engine._quant_scales of the next round): the
     // wave peels off its distinct jobs (usually one), max-reduces each over the matching lanes and issues
-    // one atomicMax per job on the float bits (non-negative floats order like their bit patterns)
+    // one atomicMax per job on the float bits (non-negative floats order like their bit patterns) into one
+    // of kAmaxCopies copies (block-strided: same-address atomics from every wave would serialise); the
+    // host takes the max over the copies
     const int lane = threadIdx.x & 63;
     bool pend = ok;
     for (int it = 0; it < 64; ++it) {
@@ -97,8 +101,9 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
         mh = fmaxf(mh, __shfl_xor(mh, off, 64));
       }
       if (lane == leader) {
-        atomicMax(amax + 2 * lp, __float_as_uint(mg));
-        atomicMax(amax + 2 * lp + 1, __float_as_uint(mh));
+        uint32_t* dst = amax + ((int64_t)(blockIdx.x % kAmaxCopies) * P + lp) * 2;
+        atomicMax(dst, __float_as_uint(mg));
+        atomicMax(dst + 1, __float_as_uint(mh));
       }
       pend = pend && !mine;
     }

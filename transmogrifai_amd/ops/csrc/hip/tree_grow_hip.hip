@@ -36,6 +36,11 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         void* rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase, hipStream_t stream);
 int tmog_hip_fp_merge(const void* recv, int R, int m, int64_t rec_bytes, int S, int32_t* out_feat, int32_t* out_bin,
                       float* out_gain, uint8_t* out_dl, float* out_left, hipStream_t stream);
+int tmog_hip_pair_scan(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int32_t* small_j,
+                       const int32_t* big_j, int n_pairs, const int64_t* node_hist_off, const int32_t* node_nfeat,
+                       const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B, int S,
+                       int kind, const float* node_params, int missing_bin, const int32_t* node_model,
+                       const double* qinv, int max_nfeat, void* cand_ws, int n_multi, hipStream_t stream);
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
                            int64_t dense, int per, int S, hipStream_t stream);
 size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat, int B, int S);
@@ -183,6 +188,14 @@ struct GpuBackend {
   void hist_subtract(int64_t* hist, const int64_t* prev, const int64_t* poff, const int64_t* soff,
                      const int64_t* ooff, const int64_t* size, int n, int64_t mx, int64_t dense, int per, int S) {
     kchk(tmog_hip_hist_subtract(hist, prev, poff, soff, ooff, size, n, mx, dense, per, S, sl.stream), "hist_subtract");
+  }
+  void pair_scan(const tmog::GrowArgs& g, int64_t* hist, const int64_t* prev, const int64_t* poff, const int32_t* sj,
+                 const int32_t* bj, int n_pairs, const int64_t* nho, const int32_t* nnf, const int32_t* nfo,
+                 const int32_t* flist, const float* params, const int32_t* nmd, int max_nf, int m, int n_multi) {
+    grow_dev(sl.cand, sl.cand_cap, tmog_hip_split_cand_bytes(m, max_nf, g.B, g.S), sl.stream);
+    kchk(tmog_hip_pair_scan(hist, prev, poff, sj, bj, n_pairs, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params,
+                            g.missing_bin, nmd, g.qinv, max_nf, sl.cand, n_multi, sl.stream),
+         "pair_scan");
   }
   void split_find(const tmog::GrowArgs& g, const int64_t* hist, int m, const int64_t* nho, const int32_t* nnf,
                   const int32_t* nfo, const int32_t* flist, const float* params, const int32_t* nmd, int max_nf,

@@ -741,6 +741,113 @@ static int split_fpb() {
   return v;
 }
 
+// Per-node split evaluation state of the narrow scans (split_scan_kernel, pair_scan_kernel): node totals
+// (fixed point and scaled), the node's parameters, and this thread's best candidate so far.
+template <int SM>
+struct NodeScan {
+  int64_t totq[SM];
+  double tot[SM], q[SM];
+  double tcount, pimp, parent_gain, min_inst, min_gain, mcw, lambda;
+  int S, kind;
+  bool allow_missing;
+  Best best;
+
+  // totq_in: the node's fixed-point totals (every lane holds the same values)
+  __device__ __forceinline__ void init(const int64_t* totq_in, const double* qi, const float* P, int S_, int kind_,
+                                       int missing_bin) {
+    S = S_;
+    kind = kind_;
+    best = Best{-INFINITY, 0x7fffffff, 0, 0};
+    min_inst = P[0];
+    min_gain = P[1];
+    mcw = P[2];
+    lambda = P[3];
+    allow_missing = P[5] > 0.5f && missing_bin >= 0;
+    for (int s = 0; s < S; ++s) {
+      totq[s] = totq_in[s];
+      q[s] = qi[s];
+      tot[s] = (double)totq[s] * q[s];
+    }
+    pimp = impurity_dev(tot, S, kind, &tcount);
+    parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
+  }
+
+  // one candidate (left statistics lq, bin b, missing direction dl) with the CPU twin's arithmetic
+  __device__ __forceinline__ void consider(const int64_t* lq, int f, int b, int dl) {
+    double left[SM], right[SM];
+    for (int s = 0; s < S; ++s) {
+      left[s] = (double)lq[s] * q[s];
+      right[s] = (double)(totq[s] - lq[s]) * q[s];
+    }
+    double gain;
+    bool ok = true;
+    if (kind == 3) {
+      // invalid by min_child_weight: skip the two fp64 divisions (whole waves skip at small nodes)
+      if (left[1] < mcw || right[1] < mcw) return;
+      gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
+    } else {
+      double lc, rc;
+      const double li = impurity_dev(left, S, kind, &lc);
+      const double ri = impurity_dev(right, S, kind, &rc);
+      if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) ok = false;
+      gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
+      if (gain < min_gain) ok = false;
+    }
+    if (ok) {
+      Best c{gain, f, b, dl};
+      if (better(c, best)) best = c;
+    }
+  }
+
+  // multi-bin feature f: lane = bin, v = this lane's bin statistics (0 past nb), miss = the missing bin's
+  // (same on every lane). Exact int64 wave prefix sum, then the lane's (bin, dl) candidates.
+  __device__ __forceinline__ void scan_feature(int64_t* v, const int64_t* miss, int nb, int f, int lane) {
+    for (int off = 1; off < 64; off <<= 1) {
+      for (int s = 0; s < S; ++s) {
+        const int64_t o = __shfl_up(v[s], off, 64);
+        if (lane >= off) v[s] += o;
+      }
+    }
+    // candidates b < nb - 1; with a missing bin dl = 0 also b = nb - 1 (present left, missing right).
+    // An empty missing bin makes every dl = 1 candidate equal to its dl = 0 twin, which wins the tie
+    // (better(): dl ascending; the CPU twin's first-wins scan order) -- skip them.
+    bool any_miss = false;
+    for (int s = 0; s < S; ++s) any_miss |= miss[s] != 0;
+    const int n_dl = allow_missing ? (any_miss ? 2 : 1) : 1;
+    if (lane < nb - 1 + (allow_missing ? 1 : 0)) {
+      for (int dl = 0; dl < n_dl; ++dl) {
+        if (lane == nb - 1 && dl) continue;
+        int64_t lq[SM];
+        for (int s = 0; s < S; ++s) lq[s] = v[s] + (dl ? miss[s] : 0);
+        consider(lq, f, lane, dl);
+      }
+    }
+  }
+
+  // wave-level best (every lane ends with it)
+  __device__ __forceinline__ void wave_best() {
+    for (int off = 32; off > 0; off >>= 1) {
+      Best o;
+      o.gain = __shfl_xor(best.gain, off, 64);
+      o.f = __shfl_xor(best.f, off, 64);
+      o.b = __shfl_xor(best.b, off, 64);
+      o.dl = __shfl_xor(best.dl, off, 64);
+      if (better(o, best)) best = o;
+    }
+  }
+};
+
+// node totals from local feature 0 of a histogram (every row is counted once per feature, including the
+// missing bin), on every lane of the wave
+template <int SM>
+__device__ __forceinline__ void node_totals(const int64_t* h, int B, int S, int lane, int64_t* totq) {
+  for (int s = 0; s < S; ++s) {
+    int64_t v = lane < B ? h[lane * S + s] : 0;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    totq[s] = v;
+  }
+}
+
 template <int SM>
 __global__ void __launch_bounds__(256) split_scan_kernel(
     const int64_t* __restrict__ hist, const int64_t* __restrict__ node_hist_off, const int32_t* __restrict__ node_nfeat,
@@ -750,6 +857,8 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     Best* __restrict__ cand, int n_multi, int fpb) {
   const int j = blockIdx.x / fbmax;
   const int fb = blockIdx.x - j * fbmax;
+  // params slot 4: the node was scanned with its subtraction partner by pair_scan_kernel (same cand slots)
+  if (node_params[(int64_t)j * 8 + 4] > 0.5f) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nf = node_nfeat[j];
   // n_multi >= 0: local features [n_multi, nf) have one present bin; their blocks (fb >= fb_multi)
@@ -758,63 +867,25 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
   const int fb_multi = n_multi >= 0 ? (n_multi + fpb - 1) / fpb : fbmax;
   const bool one_blk = fb >= fb_multi;
   __shared__ Best s_best[4];
-  Best best{-INFINITY, 0x7fffffff, 0, 0};
+  NodeScan<SM> ns;
+  ns.best = Best{-INFINITY, 0x7fffffff, 0, 0};
   // params slot 7 = "may split" (tree_grow.hpp): nodes built only as a subtraction partner are not scanned
   if (node_params[(int64_t)j * 8 + 7] > 0.5f &&
       (one_blk ? (n_multi + (fb - fb_multi) * 256 < nf) : (fb * fpb < f_lim))) {
     const int64_t* h = hist + node_hist_off[j];
     const int32_t* fl = feat_list + node_feat_off[j];
-    const float* P = node_params + (int64_t)j * 8;
-    const double* qi = qinv + (int64_t)(node_model ? node_model[j] : 0) * S;
-    const double min_inst = P[0], min_gain = P[1], mcw = P[2], lambda = P[3];
-    const bool allow_missing = P[5] > 0.5f && missing_bin >= 0;
-    // node totals from feature 0 (every row is counted once per feature, including the missing bin)
     int64_t totq[SM];
-    double tot[SM], q[SM];
-    for (int s = 0; s < S; ++s) {
-      int64_t v = lane < B ? h[lane * S + s] : 0;
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      totq[s] = v;
-      q[s] = qi[s];
-      tot[s] = (double)v * q[s];
-    }
-    double tcount;
-    const double pimp = impurity_dev(tot, S, kind, &tcount);
-    const double parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
+    node_totals<SM>(h, B, S, lane, totq);
+    ns.init(totq, qinv + (int64_t)(node_model ? node_model[j] : 0) * S, node_params + (int64_t)j * 8, S, kind,
+            missing_bin);
     const int f_end = one_blk ? 0 : min(f_lim, (fb + 1) * fpb);
-    // one candidate (left statistics lq, bin b, missing direction dl) with the CPU twin's arithmetic
-    auto consider = [&](const int64_t* lq, int f, int b, int dl) {
-      double left[SM], right[SM];
-      for (int s = 0; s < S; ++s) {
-        left[s] = (double)lq[s] * q[s];
-        right[s] = (double)(totq[s] - lq[s]) * q[s];
-      }
-      double gain;
-      bool ok = true;
-      if (kind == 3) {
-        // invalid by min_child_weight: skip the two fp64 divisions (whole waves skip at small nodes)
-        if (left[1] < mcw || right[1] < mcw) return;
-        gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
-      } else {
-        double lc, rc;
-        const double li = impurity_dev(left, S, kind, &lc);
-        const double ri = impurity_dev(right, S, kind, &rc);
-        if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) ok = false;
-        gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
-        if (gain < min_gain) ok = false;
-      }
-      if (ok) {
-        Best c{gain, f, b, dl};
-        if (better(c, best)) best = c;
-      }
-    };
     if (one_blk) {
       const int f = n_multi + (fb - fb_multi) * 256 + (int)threadIdx.x;
-      if (f < nf && allow_missing && feat_nbins[fl[f]] == 1) {
+      if (f < nf && ns.allow_missing && feat_nbins[fl[f]] == 1) {
         const int64_t* hf = h + (int64_t)f * B * S;
         int64_t lq[SM];
         for (int s = 0; s < S; ++s) lq[s] = hf[s];
-        consider(lq, f, 0, 0);
+        ns.consider(lq, f, 0, 0);
       }
     }
     for (int f = fb * fpb + wave; f < f_end; f += 4) {
@@ -823,55 +894,140 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
       if (nb == 1) {
         // one present bin (one-hot / null indicator): the only candidate is present-left,
         // missing-right -- no scan, one lane
-        if (allow_missing && lane == 0) {
+        if (ns.allow_missing && lane == 0) {
           int64_t lq[SM];
           for (int s = 0; s < S; ++s) lq[s] = hf[s];
-          consider(lq, f, 0, 0);
+          ns.consider(lq, f, 0, 0);
         }
         continue;
       }
       int64_t v[SM], miss[SM];
       for (int s = 0; s < S; ++s) {
         v[s] = (lane < nb) ? hf[lane * S + s] : 0;
-        miss[s] = allow_missing ? hf[missing_bin * S + s] : 0;
+        miss[s] = ns.allow_missing ? hf[missing_bin * S + s] : 0;
       }
-      for (int off = 1; off < 64; off <<= 1) {
-        for (int s = 0; s < S; ++s) {
-          const int64_t o = __shfl_up(v[s], off, 64);
-          if (lane >= off) v[s] += o;
-        }
-      }
-      // candidates b < nb - 1; with a missing bin dl = 0 also b = nb - 1 (present left, missing right).
-      // An empty missing bin makes every dl = 1 candidate equal to its dl = 0 twin, which wins the tie
-      // (better(): dl ascending; the CPU twin's first-wins scan order) -- skip them.
-      bool any_miss = false;
-      for (int s = 0; s < S; ++s) any_miss |= miss[s] != 0;
-      const int n_dl = allow_missing ? (any_miss ? 2 : 1) : 1;
-      if (lane < nb - 1 + (allow_missing ? 1 : 0)) {
-        for (int dl = 0; dl < n_dl; ++dl) {
-          if (lane == nb - 1 && dl) continue;
-          int64_t lq[SM];
-          for (int s = 0; s < S; ++s) lq[s] = v[s] + (dl ? miss[s] : 0);
-          consider(lq, f, lane, dl);
-        }
-      }
+      ns.scan_feature(v, miss, nb, f, lane);
     }
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    Best o;
-    o.gain = __shfl_xor(best.gain, off, 64);
-    o.f = __shfl_xor(best.f, off, 64);
-    o.b = __shfl_xor(best.b, off, 64);
-    o.dl = __shfl_xor(best.dl, off, 64);
-    if (better(o, best)) best = o;
-  }
-  if (lane == 0) s_best[wave] = best;
+  ns.wave_best();
+  if (lane == 0) s_best[wave] = ns.best;
   __syncthreads();
   if (threadIdx.x == 0) {
     Best b = s_best[0];
     for (int w = 1; w < 4; ++w)
       if (better(s_best[w], b)) b = s_best[w];
     cand[blockIdx.x] = b;
+  }
+}
+
+// Subtraction + split scan of a sibling pair in one pass (replaces hist_subtract_kernel + the two nodes'
+// split_scan blocks). Block (q, fb) covers feature block fb of pair q exactly as split_scan_kernel does for
+// one node: it loads the parent's and the built (small) child's rows, stores big = parent - small, and
+// scans both children from registers -- the histograms the subtraction already streams are not read
+// again by a separate scan. Node totals: small from its feature 0, big = parent's - small's. Writes
+// cand[j_small][fb] and cand[j_big][fb]; the two nodes carry params slot 4 = 1 so split_scan_kernel skips
+// them. Words outside the live set (one-present-bin columns above bin 0) are left alone, as before.
+template <int SM>
+__global__ void __launch_bounds__(256) pair_scan_kernel(
+    int64_t* __restrict__ hist, const int64_t* __restrict__ parent, const int64_t* __restrict__ parent_off,
+    const int32_t* __restrict__ small_j, const int32_t* __restrict__ big_j, int n_pairs,
+    const int64_t* __restrict__ node_hist_off, const int32_t* __restrict__ node_nfeat,
+    const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
+    const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
+    int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
+    Best* __restrict__ cand, int n_multi, int fpb) {
+  const int q = blockIdx.x / fbmax;
+  const int fb = blockIdx.x - q * fbmax;
+  if (q >= n_pairs) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int js = small_j[q], jb = big_j[q];
+  const int nf = node_nfeat[js];           // no per-node feature subsets on this path: same list for both
+  const int f_lim = n_multi >= 0 ? min(n_multi, nf) : nf;
+  const int fb_multi = n_multi >= 0 ? (n_multi + fpb - 1) / fpb : fbmax;
+  const bool one_blk = fb >= fb_multi;
+  const int64_t* P = parent + parent_off[q];
+  const int64_t* Hs = hist + node_hist_off[js];
+  int64_t* Hb = hist + node_hist_off[jb];
+  const int32_t* fl = feat_list + node_feat_off[js];
+  const bool scan_s = node_params[(int64_t)js * 8 + 7] > 0.5f;
+  const bool scan_b = node_params[(int64_t)jb * 8 + 7] > 0.5f;
+  __shared__ Best s_best[2][4];
+  NodeScan<SM> ns, nb_;
+  {
+    int64_t ts[SM], tp[SM], tb[SM];
+    node_totals<SM>(Hs, B, S, lane, ts);
+    node_totals<SM>(P, B, S, lane, tp);
+    for (int s = 0; s < S; ++s) tb[s] = tp[s] - ts[s];
+    ns.init(ts, qinv + (int64_t)(node_model ? node_model[js] : 0) * S, node_params + (int64_t)js * 8, S, kind,
+            missing_bin);
+    nb_.init(tb, qinv + (int64_t)(node_model ? node_model[jb] : 0) * S, node_params + (int64_t)jb * 8, S, kind,
+             missing_bin);
+  }
+  if (one_blk) {
+    const int f = n_multi + (fb - fb_multi) * 256 + (int)threadIdx.x;
+    if (f < nf) {
+      const int64_t o = (int64_t)f * B * S;      // live words of a one-present-bin column: bin 0
+      int64_t ls[SM], lb[SM];
+      for (int s = 0; s < S; ++s) {
+        ls[s] = Hs[o + s];
+        lb[s] = P[o + s] - ls[s];
+        Hb[o + s] = lb[s];
+      }
+      if (feat_nbins[fl[f]] == 1) {
+        if (scan_s && ns.allow_missing) ns.consider(ls, f, 0, 0);
+        if (scan_b && nb_.allow_missing) nb_.consider(lb, f, 0, 0);
+      }
+    }
+  } else {
+    const int f_end = min(f_lim, (fb + 1) * fpb);
+    for (int f = fb * fpb + wave; f < f_end; f += 4) {
+      const int nbins = feat_nbins[fl[f]];
+      const int64_t o = (int64_t)f * B * S;
+      int64_t vs[SM], vb[SM], ms[SM], mb[SM];
+      for (int s = 0; s < S; ++s) {
+        int64_t a = 0, c = 0;
+        if (lane < B) {
+          a = Hs[o + lane * S + s];
+          c = P[o + lane * S + s] - a;
+          Hb[o + lane * S + s] = c;
+        }
+        // missing bin statistics from the lane holding it
+        ms[s] = missing_bin >= 0 ? __shfl(a, missing_bin, 64) : 0;
+        mb[s] = missing_bin >= 0 ? __shfl(c, missing_bin, 64) : 0;
+        vs[s] = lane < nbins ? a : 0;
+        vb[s] = lane < nbins ? c : 0;
+      }
+      if (nbins == 1) {
+        if (lane == 0) {
+          if (scan_s && ns.allow_missing) ns.consider(vs, f, 0, 0);
+          if (scan_b && nb_.allow_missing) nb_.consider(vb, f, 0, 0);
+        }
+        continue;
+      }
+      if (scan_s) {
+        if (!ns.allow_missing)
+          for (int s = 0; s < S; ++s) ms[s] = 0;
+        ns.scan_feature(vs, ms, nbins, f, lane);
+      }
+      if (scan_b) {
+        if (!nb_.allow_missing)
+          for (int s = 0; s < S; ++s) mb[s] = 0;
+        nb_.scan_feature(vb, mb, nbins, f, lane);
+      }
+    }
+  }
+  ns.wave_best();
+  nb_.wave_best();
+  if (lane == 0) {
+    s_best[0][wave] = ns.best;
+    s_best[1][wave] = nb_.best;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    Best b = s_best[threadIdx.x][0];
+    for (int w = 1; w < 4; ++w)
+      if (better(s_best[threadIdx.x][w], b)) b = s_best[threadIdx.x][w];
+    cand[(int64_t)(threadIdx.x ? jb : js) * fbmax + fb] = b;
   }
 }
 
@@ -1617,6 +1773,31 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                      feat_list, B, S, missing_bin, node_model, qinv, fbmax, cand, out_feat, out_bin, out_gain, out_dl,
                      out_left, out_total, (unsigned long long*)cursors, (uint8_t*)rec, rec_bytes, fp_mlo, fp_nml,
                      fp_obase);
+  return (int)hipGetLastError();
+}
+
+// Fused subtraction + split scan of sibling pairs (pair_scan_kernel); the same candidate layout as
+// tmog_hip_split_find, whose scan then skips the pairs' nodes (params slot 4). Narrow path only.
+int tmog_hip_pair_scan(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int32_t* small_j,
+                       const int32_t* big_j, int n_pairs, const int64_t* node_hist_off, const int32_t* node_nfeat,
+                       const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B, int S,
+                       int kind, const float* node_params, int missing_bin, const int32_t* node_model,
+                       const double* qinv, int max_nfeat, void* cand_ws, int n_multi, hipStream_t stream) {
+  if (n_pairs == 0) return 0;
+  if (S > TM_MAX_S || B > 64) return -2;
+  if (n_multi > max_nfeat) n_multi = -1;
+  const int fpb = split_fpb();
+  const int fbmax = n_multi >= 0 ? (n_multi + fpb - 1) / fpb + (max_nfeat - n_multi + 255) / 256
+                                 : (max_nfeat + fpb - 1) / fpb;
+#define TM_PAIR(SMV)                                                                                           \
+  hipLaunchKernelGGL(pair_scan_kernel<SMV>, dim3(n_pairs * fbmax), dim3(256), 0, stream, hist, parent, parent_off, \
+                     small_j, big_j, n_pairs, node_hist_off, node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, \
+                     kind, node_params, missing_bin, node_model, qinv, fbmax, (Best*)cand_ws, n_multi, fpb)
+  if (S <= 2) TM_PAIR(2);
+  else if (S == 3) TM_PAIR(3);
+  else if (S <= 4) TM_PAIR(4);
+  else TM_PAIR(TM_MAX_S);
+#undef TM_PAIR
   return (int)hipGetLastError();
 }
 
