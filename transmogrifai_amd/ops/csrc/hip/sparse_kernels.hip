@@ -24,6 +24,54 @@ namespace {
 
 constexpr int kMaxC = 256;     // output columns per launch (lanes x 4)
 
+// Both products walk a list of (index, value) pairs per wave and gather one row of a small dense operand per
+// pair (V[col] for X V, R[row] for X^T R). The gathers of kU pairs are issued before their FMAs, so kU
+// independent row loads are in flight per wave instead of one dependent load per pair (the loop was
+// load-latency bound: ~25x below the kernel's memory roofline). The FMAs keep the pairs' order, so
+// results are unchanged and deterministic. CU = ceil(C / 64) column chunks per lane.
+constexpr int kU = 8;
+
+template <int CU>
+__device__ __forceinline__ void gather_fma(const int64_t a, const int64_t b, const int32_t* __restrict__ idx,
+                                           const float* __restrict__ val, const float* __restrict__ D, int64_t ldd,
+                                           int C, int lane, float* acc) {
+  for (int64_t base = a; base < b; base += 64) {
+    const int n = (int)min((int64_t)64, b - base);
+    const int my_i = lane < n ? idx[base + lane] : 0;
+    const float my_v = lane < n ? val[base + lane] : 0.f;
+    int t = 0;
+    for (; t + kU <= n; t += kU) {
+      float xs[kU], vv[kU][CU];
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const int i = __shfl(my_i, t + k, 64);
+        xs[k] = __shfl(my_v, t + k, 64);
+        const float* dr = D + (int64_t)i * ldd;
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+          const int j = lane + 64 * u;
+          vv[k][u] = j < C ? dr[j] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kU; ++k)
+#pragma unroll
+        for (int u = 0; u < CU; ++u) acc[u] += xs[k] * vv[k][u];
+    }
+    for (; t < n; ++t) {
+      const int i = __shfl(my_i, t, 64);
+      const float x = __shfl(my_v, t, 64);
+      const float* dr = D + (int64_t)i * ldd;
+#pragma unroll
+      for (int u = 0; u < CU; ++u) {
+        const int j = lane + 64 * u;
+        if (j < C) acc[u] += x * dr[j];
+      }
+    }
+  }
+}
+
+template <int CU>
 __global__ void __launch_bounds__(256) csr_spmm_kernel(const int64_t* __restrict__ row_ptr,
                                                        const int32_t* __restrict__ col,
                                                        const float* __restrict__ val, int64_t N,
@@ -32,33 +80,19 @@ __global__ void __launch_bounds__(256) csr_spmm_kernel(const int64_t* __restrict
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
-  float acc[kMaxC / 64];
+  float acc[CU];
 #pragma unroll
-  for (int u = 0; u < kMaxC / 64; ++u) acc[u] = 0.f;
-  const int64_t a = row_ptr[row], b = row_ptr[row + 1];
-  for (int64_t base = a; base < b; base += 64) {
-    const int n = (int)min((int64_t)64, b - base);
-    const int my_c = lane < n ? col[base + lane] : 0;
-    const float my_v = lane < n ? val[base + lane] : 0.f;
-    for (int t = 0; t < n; ++t) {
-      const int c = __shfl(my_c, t, 64);
-      const float x = __shfl(my_v, t, 64);
-      const float* vr = V + (int64_t)c * C;
-#pragma unroll
-      for (int u = 0; u < kMaxC / 64; ++u) {
-        const int j = lane + 64 * u;
-        if (j < C) acc[u] += x * vr[j];
-      }
-    }
-  }
+  for (int u = 0; u < CU; ++u) acc[u] = 0.f;
+  gather_fma<CU>(row_ptr[row], row_ptr[row + 1], col, val, V, C, C, lane, acc);
   float* out = M + row * ldm;
 #pragma unroll
-  for (int u = 0; u < kMaxC / 64; ++u) {
+  for (int u = 0; u < CU; ++u) {
     const int j = lane + 64 * u;
     if (j < C) out[j] = accumulate ? out[j] + acc[u] : acc[u];
   }
 }
 
+template <int CU>
 __global__ void __launch_bounds__(256) csc_spmm_t_kernel(const int64_t* __restrict__ seg_begin,
                                                          const int32_t* __restrict__ row, const float* __restrict__ val,
                                                          int64_t n_seg, const float* __restrict__ R, int C, int ldr,
@@ -66,28 +100,13 @@ __global__ void __launch_bounds__(256) csc_spmm_t_kernel(const int64_t* __restri
   const int lane = threadIdx.x & 63;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= n_seg) return;
-  float acc[kMaxC / 64];
+  float acc[CU];
 #pragma unroll
-  for (int u = 0; u < kMaxC / 64; ++u) acc[u] = 0.f;
-  const int64_t a = seg_begin[s], b = seg_begin[s + 1];
-  for (int64_t base = a; base < b; base += 64) {
-    const int n = (int)min((int64_t)64, b - base);
-    const int my_r = lane < n ? row[base + lane] : 0;
-    const float my_v = lane < n ? val[base + lane] : 0.f;
-    for (int t = 0; t < n; ++t) {
-      const int r = __shfl(my_r, t, 64);
-      const float x = __shfl(my_v, t, 64);
-      const float* rr = R + (int64_t)r * ldr;
-#pragma unroll
-      for (int u = 0; u < kMaxC / 64; ++u) {
-        const int j = lane + 64 * u;
-        if (j < C) acc[u] += x * rr[j];
-      }
-    }
-  }
+  for (int u = 0; u < CU; ++u) acc[u] = 0.f;
+  gather_fma<CU>(seg_begin[s], seg_begin[s + 1], row, val, R, ldr, C, lane, acc);
   float* out = partial + s * C;
 #pragma unroll
-  for (int u = 0; u < kMaxC / 64; ++u) {
+  for (int u = 0; u < CU; ++u) {
     const int j = lane + 64 * u;
     if (j < C) out[j] = acc[u];
   }
@@ -160,8 +179,14 @@ int tmog_hip_csr_spmm(const int64_t* row_ptr, const int32_t* col, const float* v
                       float* M, int ldm, int accumulate, hipStream_t stream) {
   if (N == 0) return 0;
   if (C <= 0 || C > kMaxC) return -2;
-  hipLaunchKernelGGL(csr_spmm_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, stream, row_ptr, col, val, N, V,
-                     C, M, ldm, accumulate);
+#define TM_CSR(CUV)                                                                                            \
+  hipLaunchKernelGGL(csr_spmm_kernel<CUV>, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, stream, row_ptr, col, val, N, \
+                     V, C, M, ldm, accumulate)
+  if (C <= 64) TM_CSR(1);
+  else if (C <= 128) TM_CSR(2);
+  else if (C <= 192) TM_CSR(3);
+  else TM_CSR(4);
+#undef TM_CSR
   return (int)hipGetLastError();
 }
 
@@ -169,9 +194,16 @@ int tmog_hip_csc_spmm_t(const int64_t* seg_begin, const int32_t* row, const floa
                         const int64_t* col_seg, int64_t ds, const float* R, int C, int ldr, float* partial, double* G,
                         hipStream_t stream) {
   if (C <= 0 || C > kMaxC) return -2;
-  if (n_seg > 0)
-    hipLaunchKernelGGL(csc_spmm_t_kernel, dim3((unsigned)((n_seg + 3) / 4)), dim3(256), 0, stream, seg_begin, row,
-                       val, n_seg, R, C, ldr, partial);
+#define TM_CSC(CUV)                                                                                            \
+  hipLaunchKernelGGL(csc_spmm_t_kernel<CUV>, dim3((unsigned)((n_seg + 3) / 4)), dim3(256), 0, stream, seg_begin,    \
+                     row, val, n_seg, R, C, ldr, partial)
+  if (n_seg > 0) {
+    if (C <= 64) TM_CSC(1);
+    else if (C <= 128) TM_CSC(2);
+    else if (C <= 192) TM_CSC(3);
+    else TM_CSC(4);
+  }
+#undef TM_CSC
   if (ds > 0)
     hipLaunchKernelGGL(seg_reduce_kernel, dim3((unsigned)((ds * C + 255) / 256)), dim3(256), 0, stream, col_seg, ds,
                        partial, C, G);
