@@ -16,8 +16,10 @@ learners advance all their models one round per engine call.
 """
 from __future__ import annotations
 
+import json
 import math
 import os
+import time
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -618,6 +620,11 @@ def _run_parts(dev, parts, fn):
         raise errs[0]
 
 
+# TMOG_XGB_PROFILE=1: per pipelined part, host seconds spent before / inside / after the native grower and in
+# the early-stopping read-back, printed to stderr after each XGBoost fit (diagnostics)
+_XGB_PROF: Optional[Dict[int, Dict[str, float]]] = {} if os.environ.get("TMOG_XGB_PROFILE") == "1" else None
+
+
 @register_learner
 class XGBoostClassifierLearner(_BoostLearner):
     """Newton boosting with XGBoost semantics (binary:logistic)."""
@@ -718,10 +725,13 @@ class XGBoostClassifierLearner(_BoostLearner):
             alongside: no per-node randomness, per-model quantisation, weights all 1 on this path)."""
             nonlocal G, H
             root_cache: Dict[tuple, tuple] = {}
+            prof = _XGB_PROF.setdefault(slot_base, {}) if _XGB_PROF is not None else None
+            tick = time.perf_counter
             for it in range(max([rounds[p] for p in ps], default=0)):
                 act = [p for p in ps if it < rounds[p] and not stopped[p]]
                 if not act:
                     break
+                t_0 = tick()
                 if not fused:
                     G = torch.zeros(P, N, dtype=torch.float32, device=dev)
                     H = torch.zeros(P, N, dtype=torch.float32, device=dev)
@@ -751,10 +761,12 @@ class XGBoostClassifierLearner(_BoostLearner):
                         root_cache[key] = TE._root_rows(tjobs, dev)
                     packed, cnts = root_cache[key]
                     root = (packed.clone(), cnts)
+                t_1 = tick()
                 forest = TE.grow_forest(Xg, n_bins_g, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
                                         missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root, fp=fp,
                                         slot_base=slot_base, groups=groups, XbT=XgT,
                                         quant_amax=amax_cur, quant_wmax=1.0 if amax_cur is not None else None)
+                t_2 = tick()
                 if colperm is not None:
                     internal = forest.nodes[:, 2] >= 0
                     forest.nodes[internal, 0] = colperm[forest.nodes[internal, 0]]
@@ -775,6 +787,7 @@ class XGBoostClassifierLearner(_BoostLearner):
                 for k, p in enumerate(act):
                     forests[p].append(forest.tree(k))
                     weights[p].append(1.0)
+                t_3 = tick()
                 # early stopping on the training metric (the reference sets no eval set)
                 if need and self.classification:
                     if auc_counts is not None:
@@ -787,6 +800,11 @@ class XGBoostClassifierLearner(_BoostLearner):
                             best[p], best_round[p] = v, it
                         elif it - best_round[p] >= esr[p]:
                             stopped[p] = True
+                if prof is not None:
+                    t_4 = tick()
+                    for k_, v_ in (("pre", t_1 - t_0), ("grow", t_2 - t_1), ("post", t_3 - t_2), ("es", t_4 - t_3)):
+                        prof[k_] = prof.get(k_, 0.0) + v_
+                    prof["rounds"] = prof.get("rounds", 0) + 1
 
         # Pipelined job parts (GPU, fused path): the jobs are split in two halves, each boosted by its
         # own host thread on its own stream, so one half's per-round host work (tree finalisation,
@@ -800,6 +818,11 @@ class XGBoostClassifierLearner(_BoostLearner):
             _run_parts(dev, [(list(range(int(cuts[k]), int(cuts[k + 1]))), k * gpp, gpp) for k in range(parts)], run)
         else:
             run(list(range(P)))
+        if _XGB_PROF is not None:
+            import sys as _sys
+            _sys.stderr.write("[xgb-profile] " + json.dumps({k: {a: round(b, 4) for a, b in v.items()}
+                                                           for k, v in _XGB_PROF.items()}) + "\n")
+            _XGB_PROF.clear()
         res = []
         for p in range(P):
             keep = len(forests[p]) if not stopped[p] else best_round[p] + 1

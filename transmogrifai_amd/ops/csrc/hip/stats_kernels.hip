@@ -9,7 +9,7 @@
 // * gram_aug_kernel / gram_fold_kernel -- the centred Gramian of [X - mu | onehot(y)] on the matrix
 //   cores (v_mfma_f32_32x32x2_f32, exact fp32 products): 128x128 output tiles (upper triangle of tile
 //   pairs) x row chunks, 4 waves each owning a 64x64 quadrant (2x2 accumulators of 32x32), 32-row
-//   stages of both column tiles centred into LDS. The fp32 accumulators are flushed into fp64
+//   stages of both column tiles centred into double-buffered LDS. The fp32 accumulators are flushed into fp64
 //   registers every 256 rows; chunks are summed in fp64 by the fold kernel, which also mirrors the
 //   tiles into the full symmetric matrix. The X-block gives Pearson correlations, the label block
 //   gives the label x column contingency sums (onehot(y)^T (X - mu), + n_l mu on the host) and the
@@ -99,20 +99,45 @@ __device__ __forceinline__ TilePair tile_pair(int p, int nt) {
   return TilePair{i, i + p};
 }
 
-// Augmented column c of row r: X[r][c] - mu[c] for c < d, (y[r] == c - d) for d <= c < d + L, else 0.
-__device__ __forceinline__ float aug(const float* __restrict__ X, int64_t ld, const float* __restrict__ mu,
-                                     const int32_t* __restrict__ y, int d, int L, int64_t r, int c) {
-  if (c < d) return X[r * ld + c] - mu[c];
-  if (c < d + L) return (y[r] == c - d) ? 1.f : 0.f;
-  return 0.f;
+// Loads of one 32-row stage: thread t owns column t % 128 of both tiles and rows 2u + t / 128 (u < 16), so the
+// column's kind (data / label / padding) and centre are per-thread constants and its 16 row loads are
+// independent (all in flight at once).
+struct AugCol {
+  int kind;      // 0: X[r][c] - mu, 1: (y[r] == lbl), 2: zero
+  int c;
+  int lbl;
+  float mu;
+};
+
+__device__ __forceinline__ AugCol aug_col(int c, int d, int L, const float* __restrict__ mu) {
+  if (c < d) return AugCol{0, c, 0, mu[c]};
+  if (c < d + L) return AugCol{1, c, c - d, 0.f};
+  return AugCol{2, c, 0, 0.f};
 }
 
+__device__ __forceinline__ void aug_stage(const float* __restrict__ X, int64_t ld, const int32_t* __restrict__ y,
+                                          const AugCol& col, int64_t rs, int64_t r1, int rsub, float* v) {
+#pragma unroll
+  for (int u = 0; u < GK / 2; ++u) {
+    const int64_t r = rs + 2 * u + rsub;
+    float x = 0.f;
+    if (r < r1) {
+      if (col.kind == 0) x = X[r * ld + col.c] - col.mu;
+      else if (col.kind == 1) x = (y[r] == col.lbl) ? 1.f : 0.f;
+    }
+    v[u] = x;
+  }
+}
+
+// Double-buffered: the next stage's rows are loaded into registers while the matrix cores work on the
+// current LDS stage, then stored into the other LDS buffer -- one barrier per stage, global-load latency
+// hidden behind the MFMAs instead of serialised with them.
 __global__ void __launch_bounds__(256) gram_aug_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ld,
                                                        const float* __restrict__ mu, const int32_t* __restrict__ y,
                                                        int L, int nt, int64_t rows_per_chunk,
                                                        double* __restrict__ part) {
-  __shared__ float tA[GK][GT + 4];
-  __shared__ float tB[GK][GT + 4];
+  __shared__ float tA[2][GK][GT + 4];
+  __shared__ float tB[2][GK][GT + 4];
   const TilePair tp = tile_pair(blockIdx.x, nt);
   const int ca = tp.i * GT, cb = tp.j * GT;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
@@ -120,6 +145,8 @@ __global__ void __launch_bounds__(256) gram_aug_kernel(const float* __restrict__
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int qa = (wave >> 1) * 64, qb = (wave & 1) * 64;   // this wave's 64x64 quadrant
   const int li = lane & 31, lk = lane >> 5;
+  const int cc = threadIdx.x & (GT - 1), rsub = threadIdx.x >> 7;
+  const AugCol colA = aug_col(ca + cc, d, L, mu), colB = aug_col(cb + cc, d, L, mu);
   f32x16 acc[2][2];
   double dacc[2][2][16];
   for (int a = 0; a < 2; ++a)
@@ -127,26 +154,33 @@ __global__ void __launch_bounds__(256) gram_aug_kernel(const float* __restrict__
       acc[a][b] = f32x16{};
       for (int e = 0; e < 16; ++e) dacc[a][b][e] = 0.0;
     }
+  float va[GK / 2], vb[GK / 2];
+  if (r0 < r1) {
+    aug_stage(X, ld, y, colA, r0, r1, rsub, va);
+    aug_stage(X, ld, y, colB, r0, r1, rsub, vb);
+  }
   int stage = 0;
   for (int64_t rs = r0; rs < r1; rs += GK, ++stage) {
-    for (int e = threadIdx.x; e < GK * GT; e += 256) {
-      const int rr = e / GT, cc = e % GT;
-      const int64_t r = rs + rr;
-      const bool in = r < r1;
-      tA[rr][cc] = in ? aug(X, ld, mu, y, d, L, r, ca + cc) : 0.f;
-      tB[rr][cc] = in ? aug(X, ld, mu, y, d, L, r, cb + cc) : 0.f;
+    const int buf = stage & 1;
+#pragma unroll
+    for (int u = 0; u < GK / 2; ++u) {
+      tA[buf][2 * u + rsub][cc] = va[u];
+      tB[buf][2 * u + rsub][cc] = vb[u];
     }
     __syncthreads();
+    if (rs + GK < r1) {                          // next stage in flight during this stage's MFMAs
+      aug_stage(X, ld, y, colA, rs + GK, r1, rsub, va);
+      aug_stage(X, ld, y, colB, rs + GK, r1, rsub, vb);
+    }
 #pragma unroll 4
     for (int k = 0; k < GK; k += 2) {
-      const float a0 = tA[k + lk][qa + li], a1 = tA[k + lk][qa + 32 + li];
-      const float b0 = tB[k + lk][qb + li], b1 = tB[k + lk][qb + 32 + li];
+      const float a0 = tA[buf][k + lk][qa + li], a1 = tA[buf][k + lk][qa + 32 + li];
+      const float b0 = tB[buf][k + lk][qb + li], b1 = tB[buf][k + lk][qb + 32 + li];
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
     }
-    __syncthreads();
     if ((stage + 1) % kFlush == 0) {
       for (int a = 0; a < 2; ++a)
         for (int b = 0; b < 2; ++b) {
