@@ -727,6 +727,17 @@ class XGBoostClassifierLearner(_BoostLearner):
             root_cache: Dict[tuple, tuple] = {}
             prof = _XGB_PROF.setdefault(slot_base, {}) if _XGB_PROF is not None else None
             tick = time.perf_counter
+            pending: list = []
+
+            def resolve(it0, need0, vals_t):
+                for p, v in zip(need0, vals_t.tolist()):
+                    if stopped[p]:
+                        continue
+                    if v > best[p] + 1e-12:
+                        best[p], best_round[p] = v, it0
+                    elif it0 - best_round[p] >= esr[p]:
+                        stopped[p] = True
+
             for it in range(max([rounds[p] for p in ps], default=0)):
                 act = [p for p in ps if it < rounds[p] and not stopped[p]]
                 if not act:
@@ -788,23 +799,26 @@ class XGBoostClassifierLearner(_BoostLearner):
                     forests[p].append(forest.tree(k))
                     weights[p].append(1.0)
                 t_3 = tick()
-                # early stopping on the training metric (the reference sets no eval set)
+                # early stopping on the training metric (the reference sets no eval set). The AuPR of round it
+                # is read back after round it + 1 has been grown, so the host never waits for a round's
+                # epilogue: a job that should stop after round it grows one extra tree, which the final
+                # trim (best_round + 1 trees) drops -- the same models as checking every round in step.
                 if need and self.classification:
                     if auc_counts is not None:
-                        vals = binned_aupr_from_counts(auc_counts[need]).tolist()     # one sync per round
+                        vals_t = binned_aupr_from_counts(auc_counts[need])
                     else:
-                        vals = binned_aupr_multi([torch.sigmoid(Fm[p][rows[p]]) for p in need],
-                                                 [ylab[p] for p in need]).tolist()
-                    for p, v in zip(need, vals):
-                        if v > best[p] + 1e-12:
-                            best[p], best_round[p] = v, it
-                        elif it - best_round[p] >= esr[p]:
-                            stopped[p] = True
+                        vals_t = binned_aupr_multi([torch.sigmoid(Fm[p][rows[p]]) for p in need],
+                                                   [ylab[p] for p in need])
+                    if pending:
+                        resolve(*pending.pop())
+                    pending.append((it, need, vals_t))
                 if prof is not None:
                     t_4 = tick()
                     for k_, v_ in (("pre", t_1 - t_0), ("grow", t_2 - t_1), ("post", t_3 - t_2), ("es", t_4 - t_3)):
                         prof[k_] = prof.get(k_, 0.0) + v_
                     prof["rounds"] = prof.get("rounds", 0) + 1
+            if pending:
+                resolve(*pending.pop())
 
         # Pipelined job parts (GPU, fused path): the jobs are split in two halves, each boosted by its
         # own host thread on its own stream, so one half's per-round host work (tree finalisation,
