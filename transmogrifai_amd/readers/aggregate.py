@@ -22,9 +22,10 @@ import numpy as np
 import torch
 
 from ..config import default_device
-from ..data.columns import column_from_values
+from ..data.columns import NumericColumn, column_from_values
 from ..data.dataset import Dataset
 from ..features import aggregators as A
+from ..features import types as T
 from ..features.aggregators import CutOffTime, Event
 from .base import DataReader
 
@@ -134,9 +135,16 @@ class _GroupedReader(DataReader):
             win = st.aggregate_window if st.aggregate_window is not None else windows[1 if f.is_response else 0]
             mask = _event_mask(ts, cutoff_ev, f.is_response, win) if n else np.zeros(0, bool)
             vals = [st.extract(r) for r in recs_s]
-            out = self._aggregate(agg, vals, mask, seg, len(starts), f.is_response, ts)
-            out = [out[g] for g in keep_groups]
-            cols[f.name] = column_from_values(f.wtype, out, dev)
+            out = self._aggregate(agg, vals, mask, seg, len(starts), f.is_response, ts, dev, f.wtype)
+            if isinstance(out, NumericColumn):          # device-side numeric monoid
+                if len(keep_groups) != len(starts) or np.any(np.asarray(keep_groups) != np.arange(len(starts))):
+                    out = out.take(torch.as_tensor(np.asarray(keep_groups, np.int64), device=dev))
+                if not f.wtype.nullable and not bool(out.valid.all()):
+                    raise T.NonNullableEmptyException(f"{f.wtype.__name__} cannot contain empty values")
+                cols[f.name] = out
+            else:
+                out = [out[g] for g in keep_groups]
+                cols[f.name] = column_from_values(f.wtype, out, dev)
         keys_out = np.asarray([group_keys[g] for g in keep_groups], dtype=object)
         if not shard:
             return Dataset(cols, keys_out, len(keep_groups))
@@ -149,26 +157,37 @@ class _GroupedReader(DataReader):
         return ds
 
     @staticmethod
-    def _aggregate(agg, vals, mask, seg, G, is_response, ts) -> list:
+    def _aggregate(agg, vals, mask, seg, G, is_response, ts, dev=None, wtype=None):
+        """One feature's per-key monoid. Numeric monoids (sum / max / min / mean / logical or) are
+        segmented reductions over the key runs on the engine device and come back as a device
+        ``NumericColumn`` (the K32 path: no per-key host values); the other monoids fold each key's
+        events on the host and return a list of values."""
         red = _NUMERIC.get(agg.name)
         if red is not None and all(v is None or isinstance(v, (int, float, bool, np.number)) for v in vals):
+            dev = torch.device("cpu") if dev is None else torch.device(dev)
             ok = np.asarray([v is not None for v in vals], bool) & mask
-            x = torch.as_tensor(np.asarray([float(v) if v is not None else 0.0 for v in vals], np.float64))
-            idx = torch.as_tensor(seg, dtype=torch.int64)
-            okt = torch.as_tensor(ok)
-            cnt = torch.zeros(G, dtype=torch.float64).index_add_(0, idx, okt.to(torch.float64))
+            x = torch.as_tensor(np.asarray([float(v) if v is not None else 0.0 for v in vals], np.float64), device=dev)
+            idx = torch.as_tensor(seg, dtype=torch.int64, device=dev)
+            okt = torch.as_tensor(ok, device=dev)
+            cnt = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, idx, okt.to(torch.float64))
             if red in ("sum", "mean"):
-                s = torch.zeros(G, dtype=torch.float64).index_add_(0, idx, torch.where(okt, x, torch.zeros_like(x)))
+                s = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(
+                    0, idx, torch.where(okt, x, torch.zeros_like(x)))
                 r = s / cnt.clamp_min(1) if red == "mean" else s
             else:
                 fill = -np.inf if red == "amax" else np.inf
-                r = torch.full((G,), fill, dtype=torch.float64).scatter_reduce(
+                r = torch.full((G,), fill, dtype=torch.float64, device=dev).scatter_reduce(
                     0, idx, torch.where(okt, x, torch.full_like(x, fill)), reduce=red, include_self=True)
-            r = r.tolist()
-            c = cnt.tolist()
-            if agg.name == "LogicalOr":
-                return [None if c[g] == 0 else bool(r[g]) for g in range(G)]
-            return [None if c[g] == 0 else r[g] for g in range(G)]
+            valid = cnt > 0
+            if wtype is None:                       # list form (callers outside the reader)
+                rl, cl = r.tolist(), cnt.tolist()
+                if agg.name == "LogicalOr":
+                    return [None if cl[g] == 0 else bool(rl[g]) for g in range(G)]
+                return [None if cl[g] == 0 else rl[g] for g in range(G)]
+            kind = getattr(wtype, "dtype", "float64")
+            r = torch.where(valid, r, torch.zeros_like(r))
+            vt = r != 0 if kind == "bool" else (r.to(torch.int64) if kind == "int64" else r)
+            return NumericColumn(wtype, vt, valid)
         out = []
         bounds = np.searchsorted(seg, np.arange(G + 1)) if len(seg) else np.zeros(G + 1, np.int64)
         for g in range(G):
