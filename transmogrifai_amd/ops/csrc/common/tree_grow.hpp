@@ -648,8 +648,10 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
     const bool own_list = use_subset || !perm_feats.empty();
     const size_t o_fl = own_list ? st1.add(feat_list) : 0;
     const size_t o_hit = st1.add(hitems), o_cit = st1.add(citems);
-    const size_t o_zo = st1.add(z_off), o_zs = st1.add(z_size);
-    const size_t o_zco = st1.add(zc_off), o_zcs = st1.add(zc_size);
+    std::vector<int64_t> z_off_all(z_off), z_size_all(z_size);
+    z_off_all.insert(z_off_all.end(), zc_off.begin(), zc_off.end());
+    z_size_all.insert(z_size_all.end(), zc_size.begin(), zc_size.end());
+    const size_t o_zo = st1.add(z_off_all), o_zs = st1.add(z_size_all);
     const size_t o_dp = st1.add(d_poff), o_ds = st1.add(d_soff), o_do = st1.add(d_ooff), o_dz = st1.add(d_size);
     const size_t o_bnb = st1.add(b_nb), o_bnc = st1.add(b_nc), o_bnfo = st1.add(b_nfo), o_bnnf = st1.add(b_nnf);
     const size_t o_bnmd = st1.add(b_nmd), o_bnho = st1.add(b_nho);
@@ -659,11 +661,10 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
 #define TM_P(T_, off) ((T_*)(d1 + (off)))
     const int32_t* flist = own_list ? TM_P(const int32_t, o_fl) : all_feats;
     // ---- histograms
-    bk.zero_segments(hist, TM_P(const int64_t, o_zo), TM_P(const int64_t, o_zs), (int)z_off.size(), z_max, live_dense,
-                     a.B * a.S, a.S);
-    if (!zc_off.empty())   // segments start at the one-present-bin region: dense prefix 0
-      bk.zero_segments(hist, TM_P(const int64_t, o_zco), TM_P(const int64_t, o_zcs), (int)zc_off.size(), zc_max, 0,
-                       a.B * a.S, a.S);
+    // one launch: the first z_off.size() segments are whole node histograms (dense prefix live_dense), the
+    // rest start at a node's one-present-bin region (dense prefix 0)
+    bk.zero_segments(hist, TM_P(const int64_t, o_zo), TM_P(const int64_t, o_zs), (int)(z_off.size() + zc_off.size()),
+                     std::max(z_max, zc_max), live_dense, a.B * a.S, a.S, (int)z_off.size());
     bk.hist_build(a, rows, hitems.size() ? (const void*)(d1 + o_hit) : nullptr, (int)hitems.size(),
                   TM_P(const int32_t, o_nfo), flist, TM_P(const int32_t, o_nmd), TM_P(const int64_t, o_nho), hist,
                   (int)b_nb.size(), TM_P(const int64_t, o_bnb), TM_P(const int64_t, o_bnc),

@@ -42,7 +42,7 @@ int tmog_hip_pair_scan(int64_t* hist, const int64_t* parent, const int64_t* pare
                        int kind, const float* node_params, int missing_bin, const int32_t* node_model,
                        const double* qinv, int max_nfeat, void* cand_ws, int n_multi, hipStream_t stream);
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
-                           int64_t dense, int per, int S, hipStream_t stream);
+                           int64_t dense, int per, int S, hipStream_t stream, int n_dense);
 size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat, int B, int S);
 int tmog_hip_hist_stat_chunk(int B, int S);
 int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, const void* items,
@@ -164,8 +164,8 @@ struct GpuBackend {
     return sl.res_pin;
   }
   void zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t mx, int64_t dense, int per,
-                     int S) {
-    kchk(tmog_hip_zero_segments(hist, off, size, n, mx, dense, per, S, sl.stream), "zero_segments");
+                     int S, int n_dense) {
+    kchk(tmog_hip_zero_segments(hist, off, size, n, mx, dense, per, S, sl.stream, n_dense), "zero_segments");
   }
   // staged statistics of the entry buffer position ``p`` points into (rows or rows_alt), or null
   int32_t* gh_of(const uint32_t* p) const {

@@ -16,6 +16,7 @@
 // the workgroup share the table through integer LDS atomics; the R copies are folded on the way out
 // and a node covered by one row-chunk stores with plain stores, otherwise 64-bit integer atomics.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdlib>
 #include <stdint.h>
 #include <math.h>
@@ -669,12 +670,14 @@ __global__ void hist_subtract_kernel(int64_t* __restrict__ hist, const int64_t* 
 // zero the histograms of nodes built from several row chunks (their items accumulate atomically);
 // single-chunk and derived nodes are fully overwritten, so the level buffer is never memset whole
 __global__ void zero_segments_kernel(int64_t* __restrict__ hist, const int64_t* __restrict__ off,
-                                     const int64_t* __restrict__ size, int n, int64_t dense, int per, int S) {
+                                     const int64_t* __restrict__ size, int n, int64_t dense, int per, int S,
+                                     int n_dense) {
   const int j = blockIdx.y;
   if (j >= n) return;
   int64_t* o = hist + off[j];
-  const int sz = (int)live_words(size[j], dense, per, S);
-  const int dn = (int)dense;
+  const int64_t dj = j < n_dense ? dense : 0;      // segments past n_dense start at a one-present-bin region
+  const int sz = (int)live_words(size[j], dj, per, S);
+  const int dn = (int)dj;
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < sz; k += gridDim.x * blockDim.x)
     o[live_word(k, dn, per, S)] = 0;
 }
@@ -1810,12 +1813,14 @@ int tmog_hip_fp_merge(const void* recv, int R, int m, int64_t rec_bytes, int S, 
 }
 
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
-                           int64_t dense, int per, int S, hipStream_t stream) {
+                           int64_t dense, int per, int S, hipStream_t stream, int n_dense) {
   if (n == 0) return 0;
   if (max_size >= (int64_t)1 << 31) return -2;
-  int gx = (int)min((host_live_words(max_size, dense, per, S) + 255) / 256, (int64_t)1024);
+  const int64_t lw = std::max(host_live_words(max_size, dense, per, S), host_live_words(max_size, 0, per, S));
+  int gx = (int)min((lw + 255) / 256, (int64_t)1024);
   if (gx < 1) gx = 1;
-  hipLaunchKernelGGL(zero_segments_kernel, dim3(gx, n), dim3(256), 0, stream, hist, off, size, n, dense, per, S);
+  hipLaunchKernelGGL(zero_segments_kernel, dim3(gx, n), dim3(256), 0, stream, hist, off, size, n, dense, per, S,
+                     n_dense);
   return (int)hipGetLastError();
 }
 

@@ -59,7 +59,7 @@ struct CpuBackend {
     return res.data();
   }
   const uint8_t* fetch(const uint8_t* p, size_t) { return p; }
-  void zero_segments(int64_t*, const int64_t*, const int64_t*, int, int64_t, int64_t, int, int) {}   // CPU hist zeroes per node
+  void zero_segments(int64_t*, const int64_t*, const int64_t*, int, int64_t, int64_t, int, int, int) {}   // CPU hist zeroes per node
   void hist_build(const tmog::GrowArgs& g, const uint32_t* rows, const void*, int, const int32_t*,
                   const int32_t* flist, const int32_t*, const int64_t*, int64_t* hist, int nbuild,
                   const int64_t* bnb, const int64_t* bnc, const int32_t* bnfo, const int32_t* bnnf,
