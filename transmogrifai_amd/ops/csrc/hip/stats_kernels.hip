@@ -15,6 +15,7 @@
 //   gives the label x column contingency sums (onehot(y)^T (X - mu), + n_l mu on the host) and the
 //   label counts -- all in one pass over the sampled rows.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 #include <float.h>
 
@@ -135,7 +136,7 @@ __device__ __forceinline__ void aug_stage(const float* __restrict__ X, int64_t l
 __global__ void __launch_bounds__(256) gram_aug_kernel(const float* __restrict__ X, int64_t n, int d, int64_t ld,
                                                        const float* __restrict__ mu, const int32_t* __restrict__ y,
                                                        int L, int nt, int64_t rows_per_chunk,
-                                                       double* __restrict__ part) {
+                                                       double* __restrict__ part, int flush) {
   __shared__ float tA[2][GK][GT + 4];
   __shared__ float tB[2][GK][GT + 4];
   const TilePair tp = tile_pair(blockIdx.x, nt);
@@ -181,7 +182,7 @@ __global__ void __launch_bounds__(256) gram_aug_kernel(const float* __restrict__
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
     }
-    if ((stage + 1) % kFlush == 0) {
+    if ((stage + 1) % flush == 0) {
       for (int a = 0; a < 2; ++a)
         for (int b = 0; b < 2; ++b) {
           for (int e = 0; e < 16; ++e) dacc[a][b][e] += (double)acc[a][b][e];
@@ -324,8 +325,13 @@ int tmog_hip_gram_aug(const float* X, int64_t n, int d, int64_t ld, const float*
   double* part = nullptr;
   hipError_t e = hipMallocAsync((void**)&part, sizeof(double) * GT * GT * npairs * chunks, stream);
   if (e != hipSuccess) return (int)e;
+  static const int flush = [] {              // TMOG_GRAM_FLUSH: stages between fp64 flushes (diagnostics)
+    const char* e = std::getenv("TMOG_GRAM_FLUSH");
+    const int v = e ? std::atoi(e) : kFlush;
+    return v > 0 ? v : kFlush;
+  }();
   hipLaunchKernelGGL(gram_aug_kernel, dim3((unsigned)npairs, (unsigned)chunks), dim3(256), 0, stream, X, n, d, ld, mu,
-                     y, L, nt, rpc, part);
+                     y, L, nt, rpc, part, flush);
   hipLaunchKernelGGL(gram_fold_kernel, dim3(GT * GT / 256, (unsigned)npairs), dim3(256), 0, stream, part,
                      (int)chunks, npairs, nt, D, G);
   hipFreeAsync(part, stream);
