@@ -118,15 +118,23 @@ __device__ __forceinline__ AugCol aug_col(int c, int d, int L, const float* __re
 
 __device__ __forceinline__ void aug_stage(const float* __restrict__ X, int64_t ld, const int32_t* __restrict__ y,
                                           const AugCol& col, int64_t rs, int64_t r1, int rsub, float* v) {
+  // branch-free per row: all 16 loads (row clamped into the chunk) are issued before any is used -- a
+  // conditional load per row made the compiler wait for each one in turn (16 serial memory latencies)
+  if (col.kind == 0) {
+    float t[GK / 2];
 #pragma unroll
-  for (int u = 0; u < GK / 2; ++u) {
-    const int64_t r = rs + 2 * u + rsub;
-    float x = 0.f;
-    if (r < r1) {
-      if (col.kind == 0) x = X[r * ld + col.c] - col.mu;
-      else if (col.kind == 1) x = (y[r] == col.lbl) ? 1.f : 0.f;
-    }
-    v[u] = x;
+    for (int u = 0; u < GK / 2; ++u) t[u] = X[min(rs + 2 * u + rsub, r1 - 1) * ld + col.c];
+#pragma unroll
+    for (int u = 0; u < GK / 2; ++u) v[u] = rs + 2 * u + rsub < r1 ? t[u] - col.mu : 0.f;
+  } else if (col.kind == 1) {
+    int t[GK / 2];
+#pragma unroll
+    for (int u = 0; u < GK / 2; ++u) t[u] = y[min(rs + 2 * u + rsub, r1 - 1)];
+#pragma unroll
+    for (int u = 0; u < GK / 2; ++u) v[u] = (rs + 2 * u + rsub < r1 && t[u] == col.lbl) ? 1.f : 0.f;
+  } else {
+#pragma unroll
+    for (int u = 0; u < GK / 2; ++u) v[u] = 0.f;
   }
 }
 
