@@ -844,10 +844,12 @@ struct NodeScan {
 // missing bin), on every lane of the wave
 template <int SM>
 __device__ __forceinline__ void node_totals(const int64_t* h, int B, int S, int lane, int64_t* totq) {
+  int64_t v[SM];
+  for (int s = 0; s < S; ++s) v[s] = lane < B ? h[lane * S + s] : 0;     // all loads before the reductions
   for (int s = 0; s < S; ++s) {
-    int64_t v = lane < B ? h[lane * S + s] : 0;
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    totq[s] = v;
+    int64_t t = v[s];
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+    totq[s] = t;
   }
 }
 
@@ -905,9 +907,15 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
         continue;
       }
       int64_t v[SM], miss[SM];
+      const int bl = lane < nb ? lane : 0;
+      const int mbin = missing_bin >= 0 ? missing_bin : 0;
+      for (int s = 0; s < S; ++s) {          // unconditional loads, selected afterwards (issued together)
+        v[s] = hf[bl * S + s];
+        miss[s] = hf[mbin * S + s];
+      }
       for (int s = 0; s < S; ++s) {
-        v[s] = (lane < nb) ? hf[lane * S + s] : 0;
-        miss[s] = ns.allow_missing ? hf[missing_bin * S + s] : 0;
+        v[s] = lane < nb ? v[s] : 0;
+        miss[s] = ns.allow_missing ? miss[s] : 0;
       }
       ns.scan_feature(v, miss, nb, f, lane);
     }
@@ -986,14 +994,16 @@ __global__ void __launch_bounds__(256) pair_scan_kernel(
     for (int f = fb * fpb + wave; f < f_end; f += 4) {
       const int nbins = feat_nbins[fl[f]];
       const int64_t o = (int64_t)f * B * S;
-      int64_t vs[SM], vb[SM], ms[SM], mb[SM];
+      int64_t vs[SM], vb[SM], ms[SM], mb[SM], pa[SM], pp[SM];
+      const int bl = lane < B ? lane : 0;           // every load unconditional (issued together)
       for (int s = 0; s < S; ++s) {
-        int64_t a = 0, c = 0;
-        if (lane < B) {
-          a = Hs[o + lane * S + s];
-          c = P[o + lane * S + s] - a;
-          Hb[o + lane * S + s] = c;
-        }
+        pa[s] = Hs[o + bl * S + s];
+        pp[s] = P[o + bl * S + s];
+      }
+      for (int s = 0; s < S; ++s) {
+        const int64_t a = lane < B ? pa[s] : 0;
+        const int64_t c = lane < B ? pp[s] - pa[s] : 0;
+        if (lane < B) Hb[o + lane * S + s] = c;
         // missing bin statistics from the lane holding it
         ms[s] = missing_bin >= 0 ? __shfl(a, missing_bin, 64) : 0;
         mb[s] = missing_bin >= 0 ? __shfl(c, missing_bin, 64) : 0;

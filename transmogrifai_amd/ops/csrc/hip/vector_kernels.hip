@@ -75,11 +75,22 @@ __global__ void __launch_bounds__(256) gather_rows_cols_kernel(const float* cons
   const float* base = col_base[j];
   const int64_t ld = col_ld[j];
   const int64_t r0 = (int64_t)blockIdx.x * kGatherRows + (threadIdx.x >> 6);
-  for (int rr = 0; rr < kGatherRows; rr += 4) {
-    const int64_t r = r0 + rr;
-    if (r >= m) break;
-    const int64_t src = rows ? rows[r] : r;
-    out[r * k + j] = base[src * ld];
+  // all row ids, then all values, then the stores: independent loads in flight instead of a chain of
+  // (row id -> value) latencies per row
+  constexpr int NR = kGatherRows / 4;
+  int64_t src[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int64_t r = min(r0 + 4 * i, m - 1);
+    src[i] = rows ? rows[r] : r;
+  }
+  float v[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) v[i] = base[src[i] * ld];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int64_t r = r0 + 4 * i;
+    if (r < m) out[r * k + j] = v[i];
   }
 }
 
