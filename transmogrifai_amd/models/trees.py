@@ -834,8 +834,14 @@ class XGBoostClassifierLearner(_BoostLearner):
             run(list(range(P)))
         if _XGB_PROF is not None:
             import sys as _sys
-            _sys.stderr.write("[xgb-profile] " + json.dumps({k: {a: round(b, 4) for a, b in v.items()}
-                                                           for k, v in _XGB_PROF.items()}) + "\n")
+            rep = {k: {a: round(b, 4) for a, b in v.items()} for k, v in _XGB_PROF.items()}
+            if dev.type == "cuda" and os.environ.get("TMOG_GROW_TIMING"):
+                from ..ops import _native as NV
+                tm = np.zeros(4, np.int64)
+                NV.hip().tmog_hip_grow_timing(tm.ctypes.data, 1)
+                rep["native"] = {"plan_s": tm[0] / 1e9, "issue_s": tm[1] / 1e9, "wait_s": tm[2] / 1e9,
+                                 "levels": int(tm[3])}
+            _sys.stderr.write("[xgb-profile] " + json.dumps(rep) + "\n")
             _XGB_PROF.clear()
         res = []
         for p in range(P):

@@ -80,6 +80,7 @@ _HIP_SIGS = {
     "tmog_hip_grow_copy": [P, I32, P, P, P, P, P, P, P, P],
     "tmog_hip_grow_free": [P],
     "tmog_hip_zero_segments": [P, P, P, I32, I64, P],
+    "tmog_hip_grow_timing": [P, I32],
     "tmog_hip_boost_epilogue": [P, P, I64, P, P, P, I64, P, P, P, P, I32, P, I32, I64, I64, I64, P, P],
     "tmog_hip_aupr_counts": [P, I32, I32, P, P],
     "tmog_hip_owlqn_direction": [P, P, P, P, P, P, I32, I32, I32, I32, P, P, P, P, P],
@@ -114,7 +115,7 @@ _HIP_SIGS = {
 }
 
 
-_RESTYPES = {"tmog_tok_run": C.c_void_p, "tmog_tok_sizes": None, "tmog_tok_copy": None, "tmog_tok_free": None, "tmog_clean_ascii": None, "tmog_first_ids": I64,
+_RESTYPES = {"tmog_tok_run": C.c_void_p, "tmog_tok_sizes": None, "tmog_tok_copy": None, "tmog_tok_free": None, "tmog_hip_grow_timing": None, "tmog_clean_ascii": None, "tmog_first_ids": I64,
              "tmog_tree_finalize_cpu": C.c_int64, "tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
              "tmog_shist_flush": None, "tmog_shist_merge": None, "tmog_shist_bins": None,
              "tmog_shist_size": C.c_int64, "tmog_shist_sum": C.c_double,

@@ -16,6 +16,7 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -307,6 +308,17 @@ inline std::vector<FeatGroup> equal_groups4(int n) {
   return out;
 }
 
+// TMOG_GROW_TIMING=1: host nanoseconds per level spent planning (building the level's work lists and
+// reading the previous level's decisions), issuing (staging copy + kernel launches) and waiting for the
+// level's result read-back, summed over every group and call (diagnostics; read by the C ABI)
+struct GrowTiming {
+  std::atomic<int64_t> plan{0}, issue{0}, wait{0}, levels{0};
+};
+inline GrowTiming& grow_timing() {
+  static GrowTiming t;
+  return t;
+}
+
 template <class BK>
 void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns = nullptr) {
   const int j0 = a.group_start[g], j1 = a.group_start[g + 1];
@@ -449,9 +461,16 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
   const char* hg_env = std::getenv("TMOG_TREE_HESS_GATE");     // "0": off (A/B and the equality test)
   const bool newton = a.mode == 2 && a.kind == 3 && S >= 2 &&   // (g, h) statistics, second-order gain
                       !(hg_env && hg_env[0] == '0');
+  static const bool timing = std::getenv("TMOG_GROW_TIMING") != nullptr;
+  using tclock = std::chrono::steady_clock;
+  auto ns_since = [](tclock::time_point t) {
+    return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tclock::now() - t).count();
+  };
+  tclock::time_point t_lvl = tclock::now();
   for (int depth = 0; depth <= max_depth; ++depth) {
     const int64_t n = (int64_t)lv_gid.size();
     if (n == 0) break;
+    if (timing) t_lvl = tclock::now();
     std::vector<uint8_t> can(n), need(n);
     std::vector<int64_t> hist_nodes;
     for (int64_t i = 0; i < n; ++i) {
@@ -657,6 +676,8 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
     const size_t o_bnmd = st1.add(b_nmd), o_bnho = st1.add(b_nho);
     const size_t o_nb = st1.add(nb), o_nc = st1.add(nc);
     const size_t o_sj = st1.add(d_sj), o_bj = st1.add(d_bj);
+    tclock::time_point t_issue = tclock::now();
+    if (timing) grow_timing().plan += ns_since(t_lvl);
     const uint8_t* d1 = bk.ship(st1, 0);
 #define TM_P(T_, off) ((T_*)(d1 + (off)))
     const int32_t* flist = own_list ? TM_P(const int32_t, o_fl) : all_feats;
@@ -711,7 +732,14 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
       bk.partition_fused(a, rows, rows_alt, d1 + o_cit, (int)ncit, TM_P(const int64_t, o_nb),
                          TM_P(const int64_t, o_nc), (const int32_t*)(res + r_feat), (const int32_t*)(res + r_bin),
                          res + r_dl, TM_P(const float, o_par), (const float*)(res + r_gain), (int64_t*)(res + r_cl));
+    tclock::time_point t_wait = tclock::now();
+    if (timing) grow_timing().issue += ns_since(t_issue);
     const uint8_t* h = bk.fetch(res, r_bytes);
+    if (timing) {
+      grow_timing().wait += ns_since(t_wait);
+      grow_timing().levels += 1;
+      t_lvl = tclock::now();
+    }
     const int64_t* h_cur = (const int64_t*)(h + r_cl);   // GPU: [left, right] entries per node
     const int32_t* h_feat = (const int32_t*)(h + r_feat);
     const int32_t* h_bin = (const int32_t*)(h + r_bin);
@@ -794,6 +822,7 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
       pair_parent_off[q] = hoff[j];
     }
 #undef TM_P
+    if (timing) grow_timing().plan += ns_since(t_lvl);
     std::swap(hist, prev_hist);
     cur_slot ^= 1;
     std::swap(rows, rows_alt);

@@ -337,6 +337,17 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
   return res;
 }
 
+// TMOG_GROW_TIMING diagnostics: out = [plan, issue, wait] host nanoseconds and the level count, summed over
+// every grower call since the last reset
+void tmog_hip_grow_timing(int64_t* out, int reset) {
+  tmog::GrowTiming& t = tmog::grow_timing();
+  out[0] = t.plan.load();
+  out[1] = t.issue.load();
+  out[2] = t.wait.load();
+  out[3] = t.levels.load();
+  if (reset) t.plan = t.issue = t.wait = t.levels = 0;
+}
+
 int tmog_hip_grow_status(void* h, char* msg, int cap) {
   tmog::GrowResult* r = (tmog::GrowResult*)h;
   if (msg && cap > 0) {
