@@ -66,7 +66,7 @@ _HIP_SIGS = {
     "tmog_hip_hist_stat_chunk": [I32, I32],
     "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
     "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P, I32, P,
-                            I64, I32, I32, I32, P],
+                            I64, I32, I32, I32, P, P],
     "tmog_hip_fp_merge": [P, I32, I32, I64, I32, P, P, P, P, P, P],
     "tmog_hip_rccl_unique_id": [P, I32],
     "tmog_hip_rccl_comm_init": [P, I32, I32],

@@ -33,7 +33,8 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
                         const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
                         float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors, int n_multi,
-                        void* rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase, hipStream_t stream);
+                        void* rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase, hipStream_t stream,
+                        unsigned* done);
 int tmog_hip_fp_merge(const void* recv, int R, int m, int64_t rec_bytes, int S, int32_t* out_feat, int32_t* out_bin,
                       float* out_gain, uint8_t* out_dl, float* out_left, hipStream_t stream);
 int tmog_hip_pair_scan(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int32_t* small_j,
@@ -77,6 +78,8 @@ struct GpuSlot {
   size_t res_pin_cap = 0;
   uint8_t* cand = nullptr;
   size_t cand_cap = 0;
+  unsigned* done = nullptr;                  // per-node ticket counters of the fused split reduction (zeroed)
+  size_t done_cap = 0;
   int32_t* feats = nullptr;
   int feats_n = 0;
   uint8_t* fp_send = nullptr;                 // feature-parallel: this rank's split records
@@ -202,9 +205,19 @@ struct GpuBackend {
                   int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t* cursors,
                   int n_multi, const tmog::FpSlice& fps) {
     grow_dev(sl.cand, sl.cand_cap, tmog_hip_split_cand_bytes(m, max_nf, g.B, g.S), sl.stream);
+    static const bool fused_reduce = [] {
+      const char* e = std::getenv("TMOG_FUSED_REDUCE");
+      return !(e && e[0] == '0');
+    }();
+    if (fused_reduce && sl.done_cap < (size_t)m) {     // grow-only, zeroed; the kernels leave it zeroed
+      if (sl.done) hchk(hipFreeAsync(sl.done, sl.stream), "hipFreeAsync");
+      sl.done_cap = (size_t)m + m / 2 + 256;
+      hchk(hipMallocAsync((void**)&sl.done, sl.done_cap * sizeof(unsigned), sl.stream), "hipMallocAsync");
+      hchk(hipMemsetAsync(sl.done, 0, sl.done_cap * sizeof(unsigned), sl.stream), "memset done");
+    }
     kchk(tmog_hip_split_find(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd,
                              g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, cursors, n_multi, fps.rec,
-                             fps.rec_bytes, fps.mlo, fps.nml, fps.obase, sl.stream),
+                             fps.rec_bytes, fps.mlo, fps.nml, fps.obase, sl.stream, fused_reduce ? sl.done : nullptr),
          "split_find");
   }
   // RCCL send / receive buffers come from plain hipMalloc (grow-only; never from the stream-ordered

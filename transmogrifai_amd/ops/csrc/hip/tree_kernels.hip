@@ -744,6 +744,86 @@ static int split_fpb() {
   return v;
 }
 
+// Everything the per-node split reduction reads and writes (split_reduce_kernel, or the last scan block of a
+// node when the reduction is fused into the scan).
+struct ReduceArgs {
+  const int64_t* hist;
+  const int64_t* node_hist_off;
+  const int32_t* node_feat_off;
+  const int32_t* feat_list;
+  int B, S, missing_bin;
+  const int32_t* node_model;
+  const double* qinv;
+  int fbmax;
+  const Best* cand;
+  int32_t* out_feat;
+  int32_t* out_bin;
+  float* out_gain;
+  uint8_t* out_dl;
+  float* out_left;
+  float* out_total;
+  unsigned long long* cursors;
+  uint8_t* rec;
+  int64_t rec_bytes;
+  int fp_mlo, fp_nml, fp_obase;
+};
+
+// One wave: node j's best candidate under the CPU twin's tie-break (gain, then lowest feature, dl, bin), the
+// node totals and the winner's left statistics.
+__device__ __forceinline__ void reduce_node(const ReduceArgs& ra, int j, int lane) {
+  const int B = ra.B, S = ra.S, fbmax = ra.fbmax, missing_bin = ra.missing_bin;
+  if (ra.cursors && lane < 2) ra.cursors[2 * j + lane] = 0;   // partition_fused_kernel's per-node slot cursors
+  Best b{-INFINITY, 0x7fffffff, 0, 0};
+  for (int i = lane; i < fbmax; i += 64) {      // any number of feature blocks
+    const Best c = ra.cand[(int64_t)j * fbmax + i];
+    if (better(c, b)) b = c;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    Best o;
+    o.gain = __shfl_xor(b.gain, off, 64);
+    o.f = __shfl_xor(b.f, off, 64);
+    o.b = __shfl_xor(b.b, off, 64);
+    o.dl = __shfl_xor(b.dl, off, 64);
+    if (better(o, b)) b = o;
+  }
+  const bool found = b.f != 0x7fffffff && b.gain > -INFINITY;
+  const int64_t* h = ra.hist + ra.node_hist_off[j];
+  const double* qi = ra.qinv + (int64_t)(ra.node_model ? ra.node_model[j] : 0) * S;
+  if (lane == 0) {
+    ra.out_feat[j] = found ? ra.feat_list[ra.node_feat_off[j] + b.f] : -1;
+    ra.out_bin[j] = found ? b.b : -1;
+    ra.out_gain[j] = found ? (float)b.gain : -INFINITY;
+    ra.out_dl[j] = (uint8_t)(found ? b.dl : 0);
+  }
+  for (int s = 0; s < S; ++s) {
+    int64_t t = 0, l = 0;
+    const int64_t* hf = h + (int64_t)(found ? b.f : 0) * B * S;
+    for (int bb = lane; bb < B; bb += 64) {       // any number of bins
+      t += h[(int64_t)bb * S + s];
+      if (found && bb <= b.b) l += hf[(int64_t)bb * S + s];
+    }
+    if (found && b.dl && lane == 0) l += hf[(int64_t)missing_bin * S + s];
+    for (int off = 32; off > 0; off >>= 1) {
+      t += __shfl_xor(t, off, 64);
+      l += __shfl_xor(l, off, 64);
+    }
+    if (lane == 0) {
+      ra.out_total[(int64_t)j * S + s] = (float)((double)t * qi[s]);
+      ra.out_left[(int64_t)j * S + s] = (float)((double)l * qi[s]);
+      if (ra.rec) reinterpret_cast<float*>(ra.rec + (int64_t)j * ra.rec_bytes + 24)[s] = (float)((double)l * qi[s]);
+    }
+  }
+  if (ra.rec && lane == 0) {   // feature-parallel split record (common/tree_grow.hpp fp_rec_bytes)
+    uint8_t* r = ra.rec + (int64_t)j * ra.rec_bytes;
+    *reinterpret_cast<double*>(r) = found ? b.gain : -INFINITY;
+    reinterpret_cast<int32_t*>(r)[2] =
+        found ? (b.f < ra.fp_nml ? ra.fp_mlo + b.f : ra.fp_obase + (b.f - ra.fp_nml)) : 0x7fffffff;
+    reinterpret_cast<int32_t*>(r)[3] = found ? b.b : -1;
+    reinterpret_cast<int32_t*>(r)[4] = found ? b.dl : 0;
+    reinterpret_cast<int32_t*>(r)[5] = found ? ra.feat_list[ra.node_feat_off[j] + b.f] : -1;
+  }
+}
+
 // Per-node split evaluation state of the narrow scans (split_scan_kernel, pair_scan_kernel): node totals
 // (fixed point and scaled), the node's parameters, and this thread's best candidate so far.
 template <int SM>
@@ -859,12 +939,16 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
     int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
-    Best* __restrict__ cand, int n_multi, int fpb) {
+    Best* __restrict__ cand, int n_multi, int fpb, unsigned* __restrict__ done, ReduceArgs ra) {
   const int j = blockIdx.x / fbmax;
   const int fb = blockIdx.x - j * fbmax;
-  // params slot 4: the node was scanned with its subtraction partner by pair_scan_kernel (same cand slots)
-  if (node_params[(int64_t)j * 8 + 4] > 0.5f) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // params slot 4: the node was scanned with its subtraction partner by pair_scan_kernel (same cand slots, all
+  // written by that earlier launch): with the fused reduction its block 0 reduces it, the others have nothing to do
+  if (node_params[(int64_t)j * 8 + 4] > 0.5f) {
+    if (done && fb == 0 && wave == 0) reduce_node(ra, j, lane);
+    return;
+  }
   const int nf = node_nfeat[j];
   // n_multi >= 0: local features [n_multi, nf) have one present bin; their blocks (fb >= fb_multi)
   // take 256 features each, one thread per feature, instead of 16 per block through the scan
@@ -928,6 +1012,21 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     for (int w = 1; w < 4; ++w)
       if (better(s_best[w], b)) b = s_best[w];
     cand[blockIdx.x] = b;
+  }
+  if (done) {
+    // fused reduction: the last of the node's fbmax blocks to finish reduces it (release: candidate store,
+    // fence, ticket; acquire: ticket, fence, candidate loads) -- one launch per level fewer
+    __shared__ int s_last;
+    if (threadIdx.x == 0) {
+      __threadfence();
+      s_last = atomicAdd(done + j, 1u) == (unsigned)(fbmax - 1);
+    }
+    __syncthreads();
+    if (s_last) {
+      __threadfence();
+      if (wave == 0) reduce_node(ra, j, lane);
+      if (threadIdx.x == 0) done[j] = 0u;        // ready for the next level
+    }
   }
 }
 
@@ -1189,65 +1288,7 @@ __global__ void __launch_bounds__(256) split_scan_wide_kernel(
   }
 }
 
-__global__ void __launch_bounds__(64) split_reduce_kernel(
-    const int64_t* __restrict__ hist, const int64_t* __restrict__ node_hist_off, const int32_t* __restrict__ node_feat_off,
-    const int32_t* __restrict__ feat_list, int B, int S, int missing_bin, const int32_t* __restrict__ node_model,
-    const double* __restrict__ qinv, int fbmax, const Best* __restrict__ cand, int32_t* __restrict__ out_feat,
-    int32_t* __restrict__ out_bin, float* __restrict__ out_gain, uint8_t* __restrict__ out_dl,
-    float* __restrict__ out_left, float* __restrict__ out_total, unsigned long long* __restrict__ cursors,
-    uint8_t* __restrict__ rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase) {
-  const int j = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (cursors && lane < 2) cursors[2 * j + lane] = 0;   // partition_fused_kernel's per-node slot cursors
-  Best b{-INFINITY, 0x7fffffff, 0, 0};
-  for (int i = lane; i < fbmax; i += 64) {      // any number of feature blocks
-    const Best c = cand[(int64_t)j * fbmax + i];
-    if (better(c, b)) b = c;
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    Best o;
-    o.gain = __shfl_xor(b.gain, off, 64);
-    o.f = __shfl_xor(b.f, off, 64);
-    o.b = __shfl_xor(b.b, off, 64);
-    o.dl = __shfl_xor(b.dl, off, 64);
-    if (better(o, b)) b = o;
-  }
-  const bool found = b.f != 0x7fffffff && b.gain > -INFINITY;
-  const int64_t* h = hist + node_hist_off[j];
-  const double* qi = qinv + (int64_t)(node_model ? node_model[j] : 0) * S;
-  if (lane == 0) {
-    out_feat[j] = found ? feat_list[node_feat_off[j] + b.f] : -1;
-    out_bin[j] = found ? b.b : -1;
-    out_gain[j] = found ? (float)b.gain : -INFINITY;
-    out_dl[j] = (uint8_t)(found ? b.dl : 0);
-  }
-  for (int s = 0; s < S; ++s) {
-    int64_t t = 0, l = 0;
-    const int64_t* hf = h + (int64_t)(found ? b.f : 0) * B * S;
-    for (int bb = lane; bb < B; bb += 64) {       // any number of bins
-      t += h[(int64_t)bb * S + s];
-      if (found && bb <= b.b) l += hf[(int64_t)bb * S + s];
-    }
-    if (found && b.dl && lane == 0) l += hf[(int64_t)missing_bin * S + s];
-    for (int off = 32; off > 0; off >>= 1) {
-      t += __shfl_xor(t, off, 64);
-      l += __shfl_xor(l, off, 64);
-    }
-    if (lane == 0) {
-      out_total[(int64_t)j * S + s] = (float)((double)t * qi[s]);
-      out_left[(int64_t)j * S + s] = (float)((double)l * qi[s]);
-      if (rec) reinterpret_cast<float*>(rec + (int64_t)j * rec_bytes + 24)[s] = (float)((double)l * qi[s]);
-    }
-  }
-  if (rec && lane == 0) {   // feature-parallel split record (common/tree_grow.hpp fp_rec_bytes)
-    uint8_t* r = rec + (int64_t)j * rec_bytes;
-    *reinterpret_cast<double*>(r) = found ? b.gain : -INFINITY;
-    reinterpret_cast<int32_t*>(r)[2] = found ? (b.f < fp_nml ? fp_mlo + b.f : fp_obase + (b.f - fp_nml)) : 0x7fffffff;
-    reinterpret_cast<int32_t*>(r)[3] = found ? b.b : -1;
-    reinterpret_cast<int32_t*>(r)[4] = found ? b.dl : 0;
-    reinterpret_cast<int32_t*>(r)[5] = found ? feat_list[node_feat_off[j] + b.f] : -1;
-  }
-}
+__global__ void __launch_bounds__(64) split_reduce_kernel(ReduceArgs ra) { reduce_node(ra, blockIdx.x, threadIdx.x); }
 
 // Feature-parallel merge: node j's decision is the best of the R ranks' records under the split scan's
 // order (gain, then lowest full-list position, dl, bin) -- the candidate a single rank scanning every
@@ -1755,12 +1796,19 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
                         float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors,
                         int n_multi, void* rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase,
-                        hipStream_t stream) {
+                        hipStream_t stream, unsigned* done) {
   if (n_nodes == 0) return 0;
   if (n_multi > max_nfeat) n_multi = -1;
   Best* cand = (Best*)cand_ws;   // >= tmog_hip_split_cand_bytes(n_nodes, max_nfeat, B, S) bytes
   const bool wide = S > TM_MAX_S || B > 64;
   int fbmax;
+  // done (n_nodes zeroed counters, left zeroed): the node reduction runs inside the narrow scan's last block
+  auto make_ra = [&](int fbm) {
+    return ReduceArgs{hist, node_hist_off, node_feat_off, feat_list, B, S, missing_bin, node_model, qinv, fbm, cand,
+                      out_feat, out_bin, out_gain, out_dl, out_left, out_total, (unsigned long long*)cursors,
+                      (uint8_t*)rec, rec_bytes, fp_mlo, fp_nml, fp_obase};
+  };
+  ReduceArgs ra{};
   if (wide) {
     if (S > TM_WIDE_MAX_S || B * S > TM_WIDE_MAX_BS) return -2;
     fbmax = max_nfeat;        // one workgroup per (node, feature)
@@ -1772,20 +1820,20 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
   const int fpb = split_fpb();
   fbmax = n_multi >= 0 ? (n_multi + fpb - 1) / fpb + (max_nfeat - n_multi + 255) / 256
                        : (max_nfeat + fpb - 1) / fpb;
+  ra = make_ra(fbmax);
 #define TM_SPLIT(SMV)                                                                                          \
   hipLaunchKernelGGL(split_scan_kernel<SMV>, dim3(n_nodes * fbmax), dim3(256), 0, stream, hist, node_hist_off,  \
                      node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin,    \
-                     node_model, qinv, fbmax, cand, n_multi, fpb)
+                     node_model, qinv, fbmax, cand, n_multi, fpb, done, ra)
   if (S <= 2) TM_SPLIT(2);
   else if (S == 3) TM_SPLIT(3);
   else if (S <= 4) TM_SPLIT(4);
   else TM_SPLIT(TM_MAX_S);
 #undef TM_SPLIT
   }
-  hipLaunchKernelGGL(split_reduce_kernel, dim3(n_nodes), dim3(64), 0, stream, hist, node_hist_off, node_feat_off,
-                     feat_list, B, S, missing_bin, node_model, qinv, fbmax, cand, out_feat, out_bin, out_gain, out_dl,
-                     out_left, out_total, (unsigned long long*)cursors, (uint8_t*)rec, rec_bytes, fp_mlo, fp_nml,
-                     fp_obase);
+  if (wide) ra = make_ra(fbmax);
+  if (wide || done == nullptr)
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(n_nodes), dim3(64), 0, stream, ra);
   return (int)hipGetLastError();
 }
 
