@@ -169,10 +169,12 @@ def test_xgb_epilogue_quantisation_maxima_identical_trees(monkeypatch):
     assert _native_loaded()
 
 
+@pytest.mark.parametrize("switch", ["TMOG_PAIR_SCAN", "TMOG_FUSED_REDUCE"])
 @pytest.mark.parametrize("learner", ["xgb", "rf", "rf3"])
-def test_pair_scan_identical_to_subtract_then_scan(monkeypatch, learner):
-    """Sibling pairs' subtraction + split scan fused in one pass (pair_scan_kernel) grows exactly the trees
-    of hist_subtract followed by the node-wise split scan: Newton (XGBoost), Gini with 2 and 3 classes."""
+def test_pair_scan_identical_to_subtract_then_scan(monkeypatch, learner, switch):
+    """Sibling pairs' subtraction + split scan fused in one pass (pair_scan_kernel), and the node reduction
+    fused into the scan's last block, grow exactly the trees of the separate kernels (hist_subtract, node-wise
+    split scan, split_reduce): Newton (XGBoost), Gini with 2 and 3 classes."""
     from transmogrifai_amd.models.base import FitJob
     from transmogrifai_amd.models.trees import RandomForestClassifierLearner, XGBoostClassifierLearner
     g = torch.Generator().manual_seed(6)
@@ -194,7 +196,7 @@ def test_pair_scan_identical_to_subtract_then_scan(monkeypatch, learner):
                 for mi in (1, 10) for k in range(2)]
     outs = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("TMOG_PAIR_SCAN", flag)
+        monkeypatch.setenv(switch, flag)
         outs.append(L().fit_batch(Xd, yd, jobs))
     for a, b in zip(*outs):
         for k in a["forest"]:

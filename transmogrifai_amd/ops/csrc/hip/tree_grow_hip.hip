@@ -205,10 +205,8 @@ struct GpuBackend {
                   int32_t* feat, int32_t* bin, float* gain, uint8_t* dl, float* left, float* tot, int64_t* cursors,
                   int n_multi, const tmog::FpSlice& fps) {
     grow_dev(sl.cand, sl.cand_cap, tmog_hip_split_cand_bytes(m, max_nf, g.B, g.S), sl.stream);
-    static const bool fused_reduce = [] {
-      const char* e = std::getenv("TMOG_FUSED_REDUCE");
-      return !(e && e[0] == '0');
-    }();
+    const char* fr_env = std::getenv("TMOG_FUSED_REDUCE");      // read per call: A/B within one process
+    const bool fused_reduce = !(fr_env && fr_env[0] == '0');
     if (fused_reduce && sl.done_cap < (size_t)m) {     // grow-only, zeroed; the kernels leave it zeroed
       if (sl.done) hchk(hipFreeAsync(sl.done, sl.stream), "hipFreeAsync");
       sl.done_cap = (size_t)m + m / 2 + 256;
