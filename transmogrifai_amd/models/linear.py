@@ -619,10 +619,14 @@ class LinearRegressionLearner(_LinearBase):
         problem a Cholesky solve of ``(Cov_z + l2 I) u = cov_zt`` when there is no L1 term, else OWL-QN on
         the Gram quadratic (:class:`GramObjective`) -- Spark WLS's Cholesky / QuasiNewton solvers. A
         singular system (collinear columns without L2) falls back to the quadratic OWL-QN, as WLS does."""
-        dev = X.device
         d = X.shape[1]
         P = len(jobs)
         G, group = _weighted_grams(X, y, jobs, par)
+        # Everything after the Grams works on [P, d+2, d+2] systems: on the host (fp64 CPU torch), where the
+        # Cholesky solves and the quadratic OWL-QN's few hundred tiny steps are microseconds each -- on the
+        # GPU every one of them is a kernel launch (the regression config spent ~5 s there)
+        dev = torch.device("cpu")
+        G = G.to(dev)
         gi = torch.as_tensor(group, dtype=torch.int64, device=dev)
         Gp = G[gi]                                               # [P, d+2, d+2]
         n = Gp[:, d, d]

@@ -717,6 +717,24 @@ struct Best {
   int b;
   int dl;
 };
+static_assert(sizeof(Best) == 24, "candidate record: three 8-byte words (store_best_sc1 / load_best_sc1)");
+
+// A candidate as three 8-byte agent-scope (sc1) words -- stores that bypass the XCD-local caching and
+// loads served from L2, for the hand-off between workgroups of the fused split reduction
+__device__ __forceinline__ void store_best_sc1(Best* p, const Best& b) {
+  uint64_t* w = reinterpret_cast<uint64_t*>(p);
+  __hip_atomic_store(w, (uint64_t)__double_as_longlong(b.gain), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(w + 1, (uint64_t)(uint32_t)b.f | ((uint64_t)(uint32_t)b.b << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(w + 2, (uint64_t)(uint32_t)b.dl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ Best load_best_sc1(const Best* p) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(p);
+  const uint64_t g = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t fb = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t dl = __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return Best{__longlong_as_double((long long)g), (int)(uint32_t)fb, (int)(uint32_t)(fb >> 32), (int)(uint32_t)dl};
+}
 
 __device__ __forceinline__ bool better(const Best& a, const Best& b) {
   if (a.gain != b.gain) return a.gain > b.gain;
@@ -734,6 +752,11 @@ __device__ __forceinline__ bool better(const Best& a, const Best& b) {
 // node over feature blocks fills the chip at the shallow levels (6 root nodes = 6 workgroups before).
 // SM = compile-time bound on S (register arrays sized to it).
 constexpr int FPB = 16;      // default features per scan workgroup (TMOG_SPLIT_FPB: 4, 8 or 16; 4 waves)
+
+// Candidate slots per node: the node's feature blocks rounded up to 16 (16 x 24 B = 3 whole 128-B lines), so
+// no cache line holds two nodes' candidates -- a reducer's L2 never caches a line of a node it has not
+// finished (the fused split reduction's sc1 hand-off)
+static inline int cand_stride(int fbmax) { return (fbmax + 15) & ~15; }
 
 static int split_fpb() {
   static const int v = [] {
@@ -755,6 +778,7 @@ struct ReduceArgs {
   const int32_t* node_model;
   const double* qinv;
   int fbmax;
+  int cstride;      // candidate slots per node (fbmax rounded up to 16: 384 B, whole 128-B lines per node)
   const Best* cand;
   int32_t* out_feat;
   int32_t* out_bin;
@@ -770,12 +794,13 @@ struct ReduceArgs {
 
 // One wave: node j's best candidate under the CPU twin's tie-break (gain, then lowest feature, dl, bin), the
 // node totals and the winner's left statistics.
-__device__ __forceinline__ void reduce_node(const ReduceArgs& ra, int j, int lane) {
+__device__ __forceinline__ void reduce_node(const ReduceArgs& ra, int j, int lane, bool sc1 = false) {
   const int B = ra.B, S = ra.S, fbmax = ra.fbmax, missing_bin = ra.missing_bin;
   if (ra.cursors && lane < 2) ra.cursors[2 * j + lane] = 0;   // partition_fused_kernel's per-node slot cursors
   Best b{-INFINITY, 0x7fffffff, 0, 0};
   for (int i = lane; i < fbmax; i += 64) {      // any number of feature blocks
-    const Best c = ra.cand[(int64_t)j * fbmax + i];
+    const Best* cp = ra.cand + (int64_t)j * ra.cstride + i;
+    const Best c = sc1 ? load_best_sc1(cp) : *cp;
     if (better(c, b)) b = c;
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -940,6 +965,7 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
     int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
     Best* __restrict__ cand, int n_multi, int fpb, unsigned* __restrict__ done, ReduceArgs ra) {
+  const int cstride = ra.cstride;
   const int j = blockIdx.x / fbmax;
   const int fb = blockIdx.x - j * fbmax;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1007,25 +1033,35 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
   ns.wave_best();
   if (lane == 0) s_best[wave] = ns.best;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    Best b = s_best[0];
-    for (int w = 1; w < 4; ++w)
-      if (better(s_best[w], b)) b = s_best[w];
-    cand[blockIdx.x] = b;
-  }
-  if (done) {
-    // fused reduction: the last of the node's fbmax blocks to finish reduces it (release: candidate store,
-    // fence, ticket; acquire: ticket, fence, candidate loads) -- one launch per level fewer
-    __shared__ int s_last;
+  if (done == nullptr) {
     if (threadIdx.x == 0) {
-      __threadfence();
-      s_last = atomicAdd(done + j, 1u) == (unsigned)(fbmax - 1);
+      Best b = s_best[0];
+      for (int w = 1; w < 4; ++w)
+        if (better(s_best[w], b)) b = s_best[w];
+      cand[(int64_t)j * cstride + fb] = b;
     }
-    __syncthreads();
-    if (s_last) {
-      __threadfence();
-      if (wave == 0) reduce_node(ra, j, lane);
-      if (threadIdx.x == 0) done[j] = 0u;        // ready for the next level
+    return;
+  }
+  // Fused reduction: the last of the node's fbmax blocks to finish reduces it -- one launch per level fewer.
+  // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table): the candidate
+  // goes out as agent-scope (sc1) stores by wave 0, which waits for them (vmcnt(0)) before its agent-scope
+  // ticket add; the block whose add returns fbmax - 1 reads every candidate of the node with sc1 loads in
+  // that same wave. No L2 write-back / L1 invalidate fences.
+  if (wave == 0) {
+    unsigned last = 0;
+    if (lane == 0) {
+      Best b = s_best[0];
+      for (int w = 1; w < 4; ++w)
+        if (better(s_best[w], b)) b = s_best[w];
+      store_best_sc1(cand + (int64_t)j * cstride + fb, b);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the sc1 stores have left before the ticket
+      last = __hip_atomic_fetch_add(done + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (unsigned)(fbmax - 1);
+    }
+    last = __shfl(last, 0, 64);
+    if (last) {
+      reduce_node(ra, j, lane, true);
+      if (lane == 0) __hip_atomic_store(done + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1045,7 +1081,7 @@ __global__ void __launch_bounds__(256) pair_scan_kernel(
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
     int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
-    Best* __restrict__ cand, int n_multi, int fpb) {
+    Best* __restrict__ cand, int n_multi, int fpb, int cstride) {
   const int q = blockIdx.x / fbmax;
   const int fb = blockIdx.x - q * fbmax;
   if (q >= n_pairs) return;
@@ -1139,7 +1175,7 @@ __global__ void __launch_bounds__(256) pair_scan_kernel(
     Best b = s_best[threadIdx.x][0];
     for (int w = 1; w < 4; ++w)
       if (better(s_best[threadIdx.x][w], b)) b = s_best[threadIdx.x][w];
-    cand[(int64_t)(threadIdx.x ? jb : js) * fbmax + fb] = b;
+    cand[(int64_t)(threadIdx.x ? jb : js) * cstride + fb] = b;
   }
 }
 
@@ -1153,7 +1189,7 @@ __global__ void __launch_bounds__(256) split_scan_wide_kernel(
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
     int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
-    Best* __restrict__ cand, int n_multi) {
+    Best* __restrict__ cand, int n_multi, int cstride) {
   extern __shared__ __attribute__((aligned(16))) int64_t wl[];
   int64_t* H = wl;                       // [B][S] prefix sums
   int64_t* totq = H + (int64_t)B * S;    // [S]
@@ -1284,7 +1320,7 @@ __global__ void __launch_bounds__(256) split_scan_wide_kernel(
     Best bb = s_best[0];
     for (int w = 1; w < 4; ++w)
       if (better(s_best[w], bb)) bb = s_best[w];
-    cand[blockIdx.x] = bb;
+    cand[(int64_t)j * cstride + f] = bb;
   }
 }
 
@@ -1804,7 +1840,8 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
   int fbmax;
   // done (n_nodes zeroed counters, left zeroed): the node reduction runs inside the narrow scan's last block
   auto make_ra = [&](int fbm) {
-    return ReduceArgs{hist, node_hist_off, node_feat_off, feat_list, B, S, missing_bin, node_model, qinv, fbm, cand,
+    return ReduceArgs{hist, node_hist_off, node_feat_off, feat_list, B, S, missing_bin, node_model, qinv, fbm,
+                      cand_stride(fbm), cand,
                       out_feat, out_bin, out_gain, out_dl, out_left, out_total, (unsigned long long*)cursors,
                       (uint8_t*)rec, rec_bytes, fp_mlo, fp_nml, fp_obase};
   };
@@ -1815,7 +1852,7 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
     const size_t lds = ((size_t)B * S + 3 * (size_t)S) * 8;
     hipLaunchKernelGGL(split_scan_wide_kernel, dim3(n_nodes * fbmax), dim3(256), lds, stream, hist, node_hist_off,
                        node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin,
-                       node_model, qinv, fbmax, cand, n_multi);
+                       node_model, qinv, fbmax, cand, n_multi, cand_stride(fbmax));
   } else {
   const int fpb = split_fpb();
   fbmax = n_multi >= 0 ? (n_multi + fpb - 1) / fpb + (max_nfeat - n_multi + 255) / 256
@@ -1853,7 +1890,8 @@ int tmog_hip_pair_scan(int64_t* hist, const int64_t* parent, const int64_t* pare
 #define TM_PAIR(SMV)                                                                                           \
   hipLaunchKernelGGL(pair_scan_kernel<SMV>, dim3(n_pairs * fbmax), dim3(256), 0, stream, hist, parent, parent_off, \
                      small_j, big_j, n_pairs, node_hist_off, node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, \
-                     kind, node_params, missing_bin, node_model, qinv, fbmax, (Best*)cand_ws, n_multi, fpb)
+                     kind, node_params, missing_bin, node_model, qinv, fbmax, (Best*)cand_ws, n_multi, fpb,    \
+                     cand_stride(fbmax))
   if (S <= 2) TM_PAIR(2);
   else if (S == 3) TM_PAIR(3);
   else if (S <= 4) TM_PAIR(4);
@@ -1885,7 +1923,7 @@ int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* siz
 size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat, int B, int S) {
   const bool wide = S > TM_MAX_S || B > 64;
   const int fpb = split_fpb();       // (max_nfeat + fpb - 1) / fpb + 1 bounds fbmax for any n_multi split
-  return (size_t)n_nodes * (wide ? max_nfeat : (max_nfeat + fpb - 1) / fpb + 1) * sizeof(Best);
+  return (size_t)n_nodes * cand_stride(wide ? max_nfeat : (max_nfeat + fpb - 1) / fpb + 1) * sizeof(Best);
 }
 
 // Largest statistic chunk whose per-workgroup LDS table (64 copies of B x Sc words) fits the LDS.
