@@ -13,6 +13,7 @@ from typing import List
 import numpy as np
 import torch
 
+from .linear import tall_gram
 from .base import FitJob, Learner, OpPredictor, register_learner
 from ..stages.base import register_stage
 
@@ -108,8 +109,8 @@ class GeneralizedLinearRegressionLearner(Learner):
         var = FAMILIES[fam][0]
         Xa = torch.cat([Xd, torch.ones(N, 1, dtype=torch.float64, device=dev)], 1)     # [N, d+1]
         wsum = W0.sum(0).clamp_min(1e-300)
-        mean = (Xd.t() @ W0) / wsum[None, :]
-        var_x = ((Xd * Xd).t() @ W0) / wsum[None, :] - mean * mean
+        mean = tall_gram(Xd, W0) / wsum[None, :]
+        var_x = tall_gram(Xd * Xd, W0) / wsum[None, :] - mean * mean
         mu = _init_mu(fam, yd)[:, None].expand(N, P).clone()
         beta = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)
         it = 0
@@ -119,9 +120,9 @@ class GeneralizedLinearRegressionLearner(Learner):
             z = eta + (yd[:, None] - mu) * gp
             w = W0 / (gp * gp * var(mu, vp)).clamp_min(1e-300)
             w = torch.nan_to_num(w, nan=0.0, posinf=0.0)
-            # batched weighted normal equations
-            A = torch.einsum("np,ni,nj->pij", w, Xa, Xa)
-            b = torch.einsum("np,ni->pi", w * z, Xa)
+            # batched weighted normal equations (row-blocked batched GEMMs: tall_gram)
+            A = torch.stack([tall_gram(Xa, Xa * w[:, p:p + 1]) for p in range(P)])
+            b = torch.stack([tall_gram(Xa, (w[:, p] * z[:, p])[:, None])[:, 0] for p in range(P)])
             pen = torch.zeros(P, d + 1, dtype=torch.float64, device=dev)
             pen[:, :d] = (reg * wsum)[:, None] * var_x.t().clamp_min(0)
             A = A + torch.diag_embed(pen)
