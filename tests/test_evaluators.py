@@ -115,6 +115,21 @@ def test_regression_metrics_match_sklearn():
     assert sum(out["SignedPercentageErrorHistogram"]["counts"]) == 1000
 
 
+@pytest.mark.parametrize("metric", ["RootMeanSquaredError", "MeanSquaredError", "MeanAbsoluteError", "R2"])
+def test_regression_selection_metric_batch_equals_full_set(metric):
+    rng = np.random.default_rng(6)
+    y = torch.as_tensor(rng.normal(10, 3, 5000))
+    preds = [torch.as_tensor(y.numpy() + rng.normal(0, s, 5000)).float() for s in (0.5, 1.0, 2.0)]
+    ev = OpRegressionEvaluator(metric)
+    batch = ev.selection_metric_batch(y, [(p, None, None) for p in preds])
+    for p, b in zip(preds, batch):
+        full = M.regression_metrics(p, y)[metric]
+        assert b == pytest.approx(full, rel=1e-12)
+        assert ev.selection_metric(y, p, None, None) == pytest.approx(full, rel=1e-12)
+    const = torch.full((10,), 2.0, dtype=torch.float64)
+    assert OpRegressionEvaluator("R2").selection_metric(const, const + 1, None, None) == 0.0
+
+
 def test_forecast_smape_mase():
     y = np.array([1.0, 2.0, 4.0, 3.0, 5.0, 6.0])
     p = np.array([1.5, 2.0, 3.0, 3.5, 4.0, 6.5])

@@ -204,3 +204,7 @@ def test_max_wait_bounds_a_running_learner():
     assert time.time() - t0 < 2.9
     assert res.best_learner == "OpNaiveBayes"
     assert any("_TestSlowNaiveBayes" in f and "maxWait" in f for f in res.failures)
+    import threading
+    for th in threading.enumerate():        # let the abandoned fit end before the interpreter does
+        if th.name.startswith("fit-_TestSlowNaiveBayes"):
+            th.join(10.0)

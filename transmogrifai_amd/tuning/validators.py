@@ -441,8 +441,9 @@ class OpValidator:
             # TMOG_BATCH_METRIC=1: all models of a fold from one segmented sort. Measured on the headline
             # (3.3M-row folds) it is ~0.1 s per learner slower than one 1-D sort per model (the [J, n]
             # temporaries grow the allocator), so the per-model curves stay the default
-            batch_fn = getattr(self.evaluator, "selection_metric_batch", None) \
-                if os.environ.get("TMOG_BATCH_METRIC", "0") == "1" else None
+            flag = os.environ.get("TMOG_BATCH_METRIC")
+            use_batch = flag == "1" if flag in ("0", "1") else bool(getattr(self.evaluator, "batch_default", False))
+            batch_fn = getattr(self.evaluator, "selection_metric_batch", None) if use_batch else None
             for k, items in by_fold.items():
                 yv = y[val_rows[k]]
                 vals = batch_fn(yv, [pr for _, pr in items]) if (batch_fn is not None and len(items) > 1) else None
