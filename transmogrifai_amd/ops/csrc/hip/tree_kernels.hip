@@ -711,6 +711,38 @@ __device__ __forceinline__ double impurity_dev(const double* st, int S, int kind
   return 0.0;
 }
 
+// Loops over the statistics of a node inside the SM-templated scans: unrolled to the compile-time bound with a
+// runtime guard, so the per-statistic arrays (totals, scales, left / right sums) stay in registers -- a loop to
+// the runtime S indexes them dynamically and puts them in scratch memory
+#define TM_FOR_S(s) _Pragma("unroll") for (int s = 0; s < SM; ++s) if (s < S)
+
+// impurity_dev over a register array of at most SM statistics (same operation order)
+template <int SM>
+__device__ __forceinline__ double impurity_reg(const double* st, int S, int kind, double* cnt) {
+  if (kind == 0 || kind == 1) {
+    double n = 0;
+    TM_FOR_S(s) n += st[s];
+    *cnt = n;
+    if (n <= 0) return 0.0;
+    double imp = kind == 0 ? 1.0 : 0.0;
+    TM_FOR_S(s) {
+      const double p = st[s] / n;
+      if (kind == 0) imp -= p * p;
+      else if (p > 0) imp -= p * log2(p);
+    }
+    return imp;
+  }
+  if (kind == 2) {
+    const double n = st[0];
+    *cnt = n;
+    if (n <= 0) return 0.0;
+    const double m = st[1] / n;
+    return st[2] / n - m * m;
+  }
+  *cnt = st[1];
+  return 0.0;
+}
+
 struct Best {
   double gain;
   int f;    // local feature index (tie-break)
@@ -871,19 +903,19 @@ struct NodeScan {
     mcw = P[2];
     lambda = P[3];
     allow_missing = P[5] > 0.5f && missing_bin >= 0;
-    for (int s = 0; s < S; ++s) {
+    TM_FOR_S(s) {
       totq[s] = totq_in[s];
       q[s] = qi[s];
       tot[s] = (double)totq[s] * q[s];
     }
-    pimp = impurity_dev(tot, S, kind, &tcount);
+    pimp = impurity_reg<SM>(tot, S, kind, &tcount);
     parent_gain = kind == 3 ? tot[0] * tot[0] / (tot[1] + lambda) : 0.0;
   }
 
   // one candidate (left statistics lq, bin b, missing direction dl) with the CPU twin's arithmetic
   __device__ __forceinline__ void consider(const int64_t* lq, int f, int b, int dl) {
     double left[SM], right[SM];
-    for (int s = 0; s < S; ++s) {
+    TM_FOR_S(s) {
       left[s] = (double)lq[s] * q[s];
       right[s] = (double)(totq[s] - lq[s]) * q[s];
     }
@@ -895,8 +927,8 @@ struct NodeScan {
       gain = left[0] * left[0] / (left[1] + lambda) + right[0] * right[0] / (right[1] + lambda) - parent_gain;
     } else {
       double lc, rc;
-      const double li = impurity_dev(left, S, kind, &lc);
-      const double ri = impurity_dev(right, S, kind, &rc);
+      const double li = impurity_reg<SM>(left, S, kind, &lc);
+      const double ri = impurity_reg<SM>(right, S, kind, &rc);
       if (lc < min_inst || rc < min_inst || lc <= 0 || rc <= 0) ok = false;
       gain = pimp - (lc / tcount) * li - (rc / tcount) * ri;
       if (gain < min_gain) ok = false;
@@ -911,7 +943,7 @@ struct NodeScan {
   // (same on every lane). Exact int64 wave prefix sum, then the lane's (bin, dl) candidates.
   __device__ __forceinline__ void scan_feature(int64_t* v, const int64_t* miss, int nb, int f, int lane) {
     for (int off = 1; off < 64; off <<= 1) {
-      for (int s = 0; s < S; ++s) {
+      TM_FOR_S(s) {
         const int64_t o = __shfl_up(v[s], off, 64);
         if (lane >= off) v[s] += o;
       }
@@ -920,13 +952,13 @@ struct NodeScan {
     // An empty missing bin makes every dl = 1 candidate equal to its dl = 0 twin, which wins the tie
     // (better(): dl ascending; the CPU twin's first-wins scan order) -- skip them.
     bool any_miss = false;
-    for (int s = 0; s < S; ++s) any_miss |= miss[s] != 0;
+    TM_FOR_S(s) any_miss |= miss[s] != 0;
     const int n_dl = allow_missing ? (any_miss ? 2 : 1) : 1;
     if (lane < nb - 1 + (allow_missing ? 1 : 0)) {
       for (int dl = 0; dl < n_dl; ++dl) {
         if (lane == nb - 1 && dl) continue;
         int64_t lq[SM];
-        for (int s = 0; s < S; ++s) lq[s] = v[s] + (dl ? miss[s] : 0);
+        TM_FOR_S(s) lq[s] = v[s] + (dl ? miss[s] : 0);
         consider(lq, f, lane, dl);
       }
     }
@@ -950,8 +982,8 @@ struct NodeScan {
 template <int SM>
 __device__ __forceinline__ void node_totals(const int64_t* h, int B, int S, int lane, int64_t* totq) {
   int64_t v[SM];
-  for (int s = 0; s < S; ++s) v[s] = lane < B ? h[lane * S + s] : 0;     // all loads before the reductions
-  for (int s = 0; s < S; ++s) {
+  TM_FOR_S(s) v[s] = lane < B ? h[lane * S + s] : 0;     // all loads before the reductions
+  TM_FOR_S(s) {
     int64_t t = v[s];
     for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
     totq[s] = t;
@@ -999,7 +1031,7 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
       if (f < nf && ns.allow_missing && feat_nbins[fl[f]] == 1) {
         const int64_t* hf = h + (int64_t)f * B * S;
         int64_t lq[SM];
-        for (int s = 0; s < S; ++s) lq[s] = hf[s];
+        TM_FOR_S(s) lq[s] = hf[s];
         ns.consider(lq, f, 0, 0);
       }
     }
@@ -1011,7 +1043,7 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
         // missing-right -- no scan, one lane
         if (ns.allow_missing && lane == 0) {
           int64_t lq[SM];
-          for (int s = 0; s < S; ++s) lq[s] = hf[s];
+          TM_FOR_S(s) lq[s] = hf[s];
           ns.consider(lq, f, 0, 0);
         }
         continue;
@@ -1019,11 +1051,11 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
       int64_t v[SM], miss[SM];
       const int bl = lane < nb ? lane : 0;
       const int mbin = missing_bin >= 0 ? missing_bin : 0;
-      for (int s = 0; s < S; ++s) {          // unconditional loads, selected afterwards (issued together)
+      TM_FOR_S(s) {          // unconditional loads, selected afterwards (issued together)
         v[s] = hf[bl * S + s];
         miss[s] = hf[mbin * S + s];
       }
-      for (int s = 0; s < S; ++s) {
+      TM_FOR_S(s) {
         v[s] = lane < nb ? v[s] : 0;
         miss[s] = ns.allow_missing ? miss[s] : 0;
       }
@@ -1103,7 +1135,7 @@ __global__ void __launch_bounds__(256) pair_scan_kernel(
     int64_t ts[SM], tp[SM], tb[SM];
     node_totals<SM>(Hs, B, S, lane, ts);
     node_totals<SM>(P, B, S, lane, tp);
-    for (int s = 0; s < S; ++s) tb[s] = tp[s] - ts[s];
+    TM_FOR_S(s) tb[s] = tp[s] - ts[s];
     ns.init(ts, qinv + (int64_t)(node_model ? node_model[js] : 0) * S, node_params + (int64_t)js * 8, S, kind,
             missing_bin);
     nb_.init(tb, qinv + (int64_t)(node_model ? node_model[jb] : 0) * S, node_params + (int64_t)jb * 8, S, kind,
@@ -1114,7 +1146,7 @@ __global__ void __launch_bounds__(256) pair_scan_kernel(
     if (f < nf) {
       const int64_t o = (int64_t)f * B * S;      // live words of a one-present-bin column: bin 0
       int64_t ls[SM], lb[SM];
-      for (int s = 0; s < S; ++s) {
+      TM_FOR_S(s) {
         ls[s] = Hs[o + s];
         lb[s] = P[o + s] - ls[s];
         Hb[o + s] = lb[s];
@@ -1131,11 +1163,11 @@ __global__ void __launch_bounds__(256) pair_scan_kernel(
       const int64_t o = (int64_t)f * B * S;
       int64_t vs[SM], vb[SM], ms[SM], mb[SM], pa[SM], pp[SM];
       const int bl = lane < B ? lane : 0;           // every load unconditional (issued together)
-      for (int s = 0; s < S; ++s) {
+      TM_FOR_S(s) {
         pa[s] = Hs[o + bl * S + s];
         pp[s] = P[o + bl * S + s];
       }
-      for (int s = 0; s < S; ++s) {
+      TM_FOR_S(s) {
         const int64_t a = lane < B ? pa[s] : 0;
         const int64_t c = lane < B ? pp[s] - pa[s] : 0;
         if (lane < B) Hb[o + lane * S + s] = c;
@@ -1154,12 +1186,12 @@ __global__ void __launch_bounds__(256) pair_scan_kernel(
       }
       if (scan_s) {
         if (!ns.allow_missing)
-          for (int s = 0; s < S; ++s) ms[s] = 0;
+          TM_FOR_S(s) ms[s] = 0;
         ns.scan_feature(vs, ms, nbins, f, lane);
       }
       if (scan_b) {
         if (!nb_.allow_missing)
-          for (int s = 0; s < S; ++s) mb[s] = 0;
+          TM_FOR_S(s) mb[s] = 0;
         nb_.scan_feature(vb, mb, nbins, f, lane);
       }
     }
