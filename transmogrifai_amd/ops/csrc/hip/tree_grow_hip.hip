@@ -45,6 +45,7 @@ int tmog_hip_pair_scan(int64_t* hist, const int64_t* parent, const int64_t* pare
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
                            int64_t dense, int per, int S, hipStream_t stream, int n_dense);
 size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat, int B, int S);
+int tmog_hip_tree_prime();
 int tmog_hip_hist_stat_chunk(int B, int S);
 int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, const void* items,
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
@@ -301,6 +302,7 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
     if (a.fp_world > 0 && a.fp_comm == nullptr) throw std::runtime_error("feature-parallel growth needs communicators");
     int dev = 0;
     hchk(hipGetDevice(&dev), "hipGetDevice");
+    hchk((hipError_t)tmog_hip_tree_prime(), "tree kernels load");   // before the group threads' first launches
     hipStream_t base = (hipStream_t)a.stream;
     hipEvent_t ready;
     hchk(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event");

@@ -1952,6 +1952,15 @@ int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* siz
   return (int)hipGetLastError();
 }
 
+// Loads this file's code object on the current device from the calling thread. The HIP runtime loads a
+// translation unit's kernels at the first launch of any of them; the tree grower's first launches come from
+// its concurrent job-group threads, and that first load racing on two threads crashed inside the runtime
+// under the profiler (rocprofv3 --kernel-trace, XGBoost-only run). The grower calls this before it spawns them.
+int tmog_hip_tree_prime() {
+  hipFuncAttributes at;
+  return (int)hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&zero_segments_kernel));
+}
+
 size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat, int B, int S) {
   const bool wide = S > TM_MAX_S || B > 64;
   const int fpb = split_fpb();       // (max_nfeat + fpb - 1) / fpb + 1 bounds fbmax for any n_multi split
