@@ -214,17 +214,20 @@ class DecisionTreeNumericMapBucketizerModel(BinaryTransformer):
     output_type = T.OPVector
     allow_label_as_input = True
 
-    def __init__(self, keys=None, splits=None, track_nulls=True, uid=None, **kw):
+    def __init__(self, keys=None, splits=None, track_nulls=True, track_invalid=False, clean_keys=False, uid=None,
+                 **kw):
         super().__init__(None, uid=uid, **kw)
         self.keys = list(keys or [])
         self.splits = [list(s) for s in (splits or [])]
         self.track_nulls = track_nulls
+        self.track_invalid = track_invalid
+        self.clean_keys = clean_keys
 
     def transform_columns(self, label, m, ds=None):
         from ...config import default_device
         from .maps import map_coo
         dev = default_device()
-        coo = map_coo(m, "real", False, dev)
+        coo = map_coo(m, "real", self.clean_keys, dev)
         dtype = vector_dtype(dev)
         last = coo.last_entry(self.keys)
         blocks = []
@@ -233,17 +236,20 @@ class DecisionTreeNumericMapBucketizerModel(BinaryTransformer):
             ok = e >= 0
             x = coo.num[e.clamp_min(0)] if coo.nnz else torch.zeros(coo.n, dtype=torch.float64, device=dev)
             if sp:
-                blocks.append(bucketize_column(x, ok, sp, self.track_nulls, False, "Right", dtype))
+                blocks.append(bucketize_column(x, ok, sp, self.track_nulls, self.track_invalid, "Right", dtype))
             elif self.track_nulls:
                 blocks.append((~ok).to(dtype)[:, None])
         out = torch.cat(blocks, 1) if blocks else torch.zeros(coo.n, 0, dtype=dtype, device=dev)
         return VectorColumn(out, self.metadata.get("vector_metadata"))
 
     def ctor_args(self):
-        return {"keys": self.keys, "splits": self.splits, "trackNulls": self.track_nulls}
+        return {"keys": self.keys, "splits": self.splits, "trackNulls": self.track_nulls,
+                "trackInvalid": self.track_invalid, "shouldCleanKeys": self.clean_keys}
 
     def load_ctor_args(self, a):
         self.keys, self.splits, self.track_nulls = list(a["keys"]), [list(s) for s in a["splits"]], a["trackNulls"]
+        self.track_invalid = bool(a.get("trackInvalid", False))
+        self.clean_keys = bool(a.get("shouldCleanKeys", False))
 
 
 @register_stage
@@ -252,19 +258,21 @@ class DecisionTreeNumericMapBucketizer(BinaryEstimator):
     operation_name = "dtNumMapBuck"
     output_type = T.OPVector
     allow_label_as_input = True
-    _defaults = dict(DecisionTreeNumericBucketizer._defaults)
+    # cleanKeys / allow / block lists: MapPivotParams + Transmogrifier.scala filterKeys
+    _defaults = dict(DecisionTreeNumericBucketizer._defaults, clean_keys=False, allow_keys=None, block_keys=None)
     dp_aware = True     # key union + per-key tree_splits_dp
 
     def fit_columns(self, label, m, ds=None):
-        from ...data.vector_metadata import OpVectorColumnMetadata, NULL_STRING
+        from ...data.vector_metadata import OpVectorColumnMetadata, NULL_STRING, OTHER_STRING
         p = self.params
         from ...config import default_device
-        from .maps import _global_keys, map_coo
+        from .maps import _filter_keys, _global_keys, map_coo
         dev = default_device()
-        coo = map_coo(m, "real", False, dev)
+        coo = map_coo(m, "real", p["clean_keys"], dev)
         y_all = label.values.to(device=dev, dtype=torch.float64)
         used = torch.unique(coo.key).cpu().numpy() if coo.nnz else np.zeros(0, np.int64)
-        keys = _global_keys([[coo.keys[int(i)] for i in used]])[0]
+        keys = _filter_keys(_global_keys([[coo.keys[int(i)] for i in used]])[0], p["allow_keys"], p["block_keys"],
+                            p["clean_keys"])
         last = coo.last_entry(keys)
         t = self.get_transient_features()[1]
         splits, cols = [], []
@@ -280,9 +288,12 @@ class DecisionTreeNumericMapBucketizer(BinaryEstimator):
             if ok:
                 for lab in bucket_labels(full, "Right"):
                     cols.append(OpVectorColumnMetadata((t.name,), (t.type_name,), k, lab))
+                if p["track_invalid"]:
+                    cols.append(OpVectorColumnMetadata((t.name,), (t.type_name,), k, OTHER_STRING))
             if p["track_nulls"]:
                 cols.append(OpVectorColumnMetadata((t.name,), (t.type_name,), k, NULL_STRING))
         self.metadata["vector_metadata"] = OpVectorMetadata(
             self.get_output_feature_name(), cols,
             {t.name: FeatureHistory(tuple(t.origin_features), tuple(t.stages) + (self.stage_name(),))})
-        return DecisionTreeNumericMapBucketizerModel(keys, splits, p["track_nulls"])
+        return DecisionTreeNumericMapBucketizerModel(keys, splits, p["track_nulls"], p["track_invalid"],
+                                                     p["clean_keys"])

@@ -165,12 +165,11 @@ def _global_keys(local_keys: Sequence[Sequence[str]]) -> List[List[str]]:
     return [sorted(set().union(*[set(p[i]) for p in parts])) for i in range(len(local_keys))]
 
 
-def _filter_keys(keys, allow, block):
-    if allow:
-        keys = [k for k in keys if k in set(allow)]
-    if block:
-        keys = [k for k in keys if k not in set(block)]
-    return keys
+def _filter_keys(keys, allow, block, clean: bool = False):
+    """Allow / block lists (Transmogrifier.scala ``filterKeys``): the lists are cleaned like the map keys."""
+    allow = {_clean_key(k, clean) for k in allow} if allow else None
+    block = {_clean_key(k, clean) for k in block} if block else set()
+    return [k for k in keys if (allow is None or k in allow) and k not in block]
 
 
 def _key_sums(coo: MapCOO, keys: Sequence[str], values: torch.Tensor) -> torch.Tensor:
@@ -382,7 +381,7 @@ class MapVectorizer(VectorizerMixin, SequenceEstimator):
         for coo in coos:
             used = torch.unique(coo.key).cpu().numpy() if coo.nnz else np.zeros(0, np.int64)
             present.append([coo.keys[int(i)] for i in used])
-        all_keys = [_filter_keys(k, p["allow_keys"], p["block_keys"]) for k in _global_keys(present)]
+        all_keys = [_filter_keys(k, p["allow_keys"], p["block_keys"], p["clean_keys"]) for k in _global_keys(present)]
         fills: List[list] = [[] for _ in cols]
         tops: List[list] = [[] for _ in cols]
         methods: List[list] = [[] for _ in cols]
