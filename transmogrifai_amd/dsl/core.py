@@ -409,6 +409,19 @@ def _vec_geo(self, fill_with_mean: bool = True, track_nulls: bool = True, others
         _others(self, others)).get_output()
 
 
+@register((T.RealMap, T.IntegralMap), "auto_bucketize")
+def _auto_bucketize_map(self, label: FeatureLike, track_nulls: bool = True, track_invalid: bool = False,
+                        min_info_gain: float = 0.01, clean_keys: bool = False, allow_list_keys=(),
+                        block_list_keys=()):
+    """``RichRealMapFeature.autoBucketize`` / ``RichIntegralMapFeature.autoBucketize``: one label-aware tree per
+    map key (DecisionTreeNumericMapBucketizer)."""
+    from ..stages.feature.bucketizers import DecisionTreeNumericMapBucketizer
+    return DecisionTreeNumericMapBucketizer(
+        track_nulls=track_nulls, track_invalid=track_invalid, min_info_gain=min_info_gain, clean_keys=clean_keys,
+        allow_keys=list(allow_list_keys) or None, block_keys=list(block_list_keys) or None
+    ).set_input(label, self).get_output()
+
+
 @register(T.OPMap, "vectorize")
 def _vec_map(self, others=(), **kw):
     """``RichMapFeature.vectorize`` (RichMapFeature.scala): Transmogrifier defaults, overridable by name

@@ -330,11 +330,38 @@ class NumericBucketizer(OpTransformer):
     _defaults = {"splits": [float("-inf"), 0.0, float("inf")], "bucket_labels": None, "track_nulls": True,
                  "track_invalid": False, "split_inclusion": "Left"}
 
+    # NumericBucketizerParams (NumericBucketizer.scala): splits validated by checkSplits (>= 3 points, strictly
+    # increasing, no NaN), labels one fewer than the splits; labels derived from the splits follow a later
+    # change of the split inclusion, explicit ones stay
+    def set(self, name, value):
+        if name == "splits" and value is not None and not check_splits([float(v) for v in value]):
+            raise ValueError(f"invalid splits {list(value)}: need >= 3 strictly increasing points, no NaN")
+        if name == "split_inclusion" and value not in ("Left", "Right"):
+            raise ValueError(f"split_inclusion must be 'Left' or 'Right', got {value!r}")
+        return super().set(name, value)
+
+    def set_buckets(self, splits, bucket_labels=None) -> "NumericBucketizer":
+        splits = [float(v) for v in splits]
+        if not check_splits(splits):
+            raise ValueError(f"invalid splits {splits}: need >= 3 strictly increasing points, no NaN")
+        if bucket_labels is not None and len(bucket_labels) != len(splits) - 1:
+            raise ValueError("The number of labels should be one less than the number of split points")
+        self.set("splits", splits)
+        return self.set("bucket_labels", list(bucket_labels) if bucket_labels is not None else None)
+
+    def get_splits(self) -> List[float]:
+        return [float(v) for v in self.params["splits"]]
+
+    def get_bucket_labels(self) -> List[str]:
+        return list(self.params["bucket_labels"] or bucket_labels(self.get_splits(), self.params["split_inclusion"]))
+
     def transform_columns(self, a, ds=None):
         p = self.params
         splits = [float(v) for v in p["splits"]]
         x, ok = _f64(a)
         labels = p["bucket_labels"] or bucket_labels(splits, p["split_inclusion"])
+        if len(labels) != len(splits) - 1:
+            raise ValueError("The number of labels should be one less than the number of split points")
         if self._inputs:
             t = self.get_transient_features()[0]
             self.metadata["vector_metadata"] = OpVectorMetadata(
