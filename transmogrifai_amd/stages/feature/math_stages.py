@@ -375,31 +375,65 @@ class NumericBucketizer(OpTransformer):
 
 @register_stage
 class PercentileCalibratorModel(UnaryTransformer):
+    """Percentile bucket of a score (``PercentileCalibrator.scala`` ``PercentileCalibratorModel``): the insertion
+    index of the score in the quantile splits, rescaled to 0 .. expectedNumBuckets - 1 when fewer distinct
+    splits than expected buckets were found."""
     operation_name = "percentCalibrator"
     output_type = T.RealNN
 
-    def __init__(self, splits=None, uid=None, **kw):
+    def __init__(self, splits=None, actual_num_buckets=None, expected_num_buckets=100, uid=None, **kw):
         super().__init__(None, uid=uid, **kw)
-        self.splits = list(splits or [])
+        self.splits = [float(v) for v in (splits or [])]
+        self.actual_num_buckets = len(self.splits) if actual_num_buckets is None else int(actual_num_buckets)
+        self.expected_num_buckets = int(expected_num_buckets)
+
+    def calibrate(self, x: torch.Tensor) -> torch.Tensor:
+        s = torch.as_tensor(self.splits, dtype=torch.float64, device=x.device)
+        idx = torch.searchsorted(s, x.to(torch.float64), right=False).to(torch.float64)   # Found / InsertionPoint
+        act, exp = self.actual_num_buckets, self.expected_num_buckets
+        if act >= exp:
+            return idx - 1.0                                            # start at zero
+        old_max, new_max = max(act - 2, 0), max(exp - 1, 0)
+        if old_max == 0:
+            return torch.zeros_like(idx)
+        v = torch.floor(idx * float(new_max) / old_max + 0.5)            # Scala Double.round
+        return torch.clamp(v, max=float(new_max))
 
     def transform_columns(self, a, ds=None):
         x, ok = _f64(a)
-        s = torch.as_tensor(self.splits, dtype=torch.float64, device=x.device)
-        b = torch.searchsorted(s, x, right=False).clamp(max=max(len(self.splits) - 1, 0)).to(torch.float64)
-        scale = 99.0 / max(len(self.splits) - 1, 1)
-        v = b * scale
+        v = self.calibrate(x)
         return NumericColumn(T.RealNN, torch.where(ok, v, torch.zeros_like(v)), torch.ones_like(ok))
 
     def ctor_args(self):
-        return {"splits": self.splits}
+        return {"splits": self.splits, "actualNumBuckets": self.actual_num_buckets,
+                "expectedNumBuckets": self.expected_num_buckets}
 
     def load_ctor_args(self, a):
-        self.splits = list(a["splits"])
+        self.splits = [float(v) for v in a["splits"]]
+        self.actual_num_buckets = int(a.get("actualNumBuckets", len(self.splits)))
+        self.expected_num_buckets = int(a.get("expectedNumBuckets", 100))
+
+
+ORIG_SPLITS_KEY, SCALED_SPLITS_KEY = "origSplits", "scaledSplits"
+
+
+def exact_quantile_splits(v: torch.Tensor, num_buckets: int) -> List[float]:
+    """Spark ``QuantileDiscretizer`` with relativeError 0: the exact quantiles at 0, 1/k, .., 1 (the element of
+    rank ceil(p n)), ends replaced by -Inf / +Inf, duplicates dropped."""
+    vs = torch.sort(v.to(torch.float64)).values
+    n = vs.numel()
+    step = 1.0 / num_buckets
+    ps = [0.0 + step * i for i in range(num_buckets + 1)]
+    idx = [0 if p <= 0 else n - 1 if p >= 1 else min(max(math.ceil(p * n) - 1, 0), n - 1) for p in ps]
+    q = vs[torch.as_tensor(idx, device=vs.device)].tolist()
+    q[0], q[-1] = float("-inf"), float("inf")
+    return sorted(set(q))
 
 
 @register_stage
 class PercentileCalibrator(UnaryEstimator):
-    """Map a score to its percentile bucket (0..99) using quantile splits (``PercentileCalibrator.scala``)."""
+    """Map a score to its percentile bucket (``PercentileCalibrator.scala``): exact quantile splits of the
+    scores, the calibrated split values recorded in the summary metadata (origSplits / scaledSplits)."""
     operation_name = "percentCalibrator"
     output_type = T.RealNN
     _defaults = {"expected_num_buckets": 100}
@@ -407,11 +441,13 @@ class PercentileCalibrator(UnaryEstimator):
     def fit_columns(self, a, ds=None):
         x, ok = _f64(a)
         v = x[ok]
-        k = self.params["expected_num_buckets"]
-        if v.numel() == 0:
-            return PercentileCalibratorModel([0.0])
-        q = torch.quantile(v, torch.linspace(0, 1, k + 1, dtype=torch.float64, device=v.device)[1:])
-        return PercentileCalibratorModel(torch.unique(q).tolist())
+        k = int(self.params["expected_num_buckets"])
+        splits = exact_quantile_splits(v, k) if v.numel() else [float("-inf"), float("inf")]
+        model = PercentileCalibratorModel(splits, len(splits), k)
+        scaled = model.calibrate(torch.as_tensor(splits, dtype=torch.float64)).tolist()
+        self.metadata["summary"] = {ORIG_SPLITS_KEY: [java_double(s) for s in splits],
+                                    SCALED_SPLITS_KEY: [java_double(s) for s in scaled]}
+        return model
 
 
 @register_stage
@@ -465,14 +501,21 @@ def pava(x: np.ndarray, y: np.ndarray, w: Optional[np.ndarray] = None, increasin
         while len(vals) > 1 and vals[-2] > vals[-1]:
             v = (vals[-2] * wts[-2] + vals[-1] * wts[-1]) / (wts[-2] + wts[-1])
             wt = wts[-2] + wts[-1]
-            l2 = lo[-2]
+            h1 = hi[-1]
             vals.pop(); wts.pop(); lo.pop(); hi.pop()
-            vals[-1], wts[-1], lo[-1] = v, wt, l2
-    bnd, pred = [], []
+            vals[-1], wts[-1], hi[-1] = v, wt, h1        # the pooled block spans [lo of the first, hi of the last]
+    # Spark's compression: adjacent points with the same prediction keep only their two boundary points
+    runs = []
     for v, l, h in zip(vals, lo, hi):
+        if runs and runs[-1][0] == v:
+            runs[-1][2] = h
+        else:
+            runs.append([v, l, h])
+    bnd, pred = [], []
+    for v, l, h in runs:
         vv = v if increasing else -v
         bnd.append(l); pred.append(vv)
-        if h != l:
+        if h > l:
             bnd.append(h); pred.append(vv)
     return bnd, pred
 
