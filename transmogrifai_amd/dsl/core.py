@@ -172,9 +172,11 @@ def _scale(self, scaling_type: str = "Linear", slope: float = 1.0, intercept: fl
 
 def _scaling_of(scaled):
     st = scaled.origin_stage
-    if not isinstance(st, M.ScalerTransformer):
-        raise ValueError(f"feature '{scaled.name}' was not produced by a ScalerTransformer (scale())")
-    return {k: st.params[k] for k in ("scaling_type", "slope", "intercept")}
+    if isinstance(st, M.ScalerTransformer):
+        return {k: st.params[k] for k in ("scaling_type", "slope", "intercept")}
+    if isinstance(st, (M.OpScalarStandardScaler, M.OpScalarStandardScalerModel)):
+        return {}          # linear scaling known after the fit: read from the scaler metadata at transform
+    raise ValueError(f"feature '{scaled.name}' was not produced by a scaler (scale() / z_normalize())")
 
 
 @register(NUM, "descale")

@@ -207,7 +207,30 @@ class OpScalarStandardScaler(UnaryEstimator):
         v = x[ok]
         mean = float(v.mean()) if v.numel() else 0.0
         std = float(v.std(unbiased=True)) if v.numel() > 1 else 0.0
+        # the descaler's view of the fit (OpScalarStandardScaler.scala fitFn): linear, 1 / std, -mean / std
+        slope = 1.0 / std if std != 0 else float("inf")
+        self.metadata.update(scaler_metadata("Linear", slope, -mean * slope if std != 0 else float("-inf")))
         return OpScalarStandardScalerModel(mean, std, self.params["with_mean"], self.params["with_std"])
+
+
+SCALING_TYPE_KEY, SCALING_ARGS_KEY = "scalingType", "scalingArgs"
+
+
+def scaler_metadata(scaling_type: str, slope: float = 1.0, intercept: float = 0.0) -> dict:
+    """``ScalerMetadata.toMetadata`` (ScalerTransformer.scala): the scaling family and its JSON arguments."""
+    import json
+    args = {"slope": float(slope), "intercept": float(intercept)} if scaling_type == "Linear" else {}
+    return {SCALING_TYPE_KEY: scaling_type, SCALING_ARGS_KEY: json.dumps(args, separators=(",", ":"))}
+
+
+def parse_scaler_metadata(meta: dict) -> Optional[dict]:
+    """(scaling_type, slope, intercept) params from stage metadata written by ``scaler_metadata``, or None."""
+    import json
+    if not meta or SCALING_TYPE_KEY not in meta:
+        return None
+    args = json.loads(meta.get(SCALING_ARGS_KEY) or "{}")
+    return {"scaling_type": meta[SCALING_TYPE_KEY], "slope": float(args.get("slope", 1.0)),
+            "intercept": float(args.get("intercept", 0.0))}
 
 
 @register_stage
@@ -217,8 +240,22 @@ class ScalerTransformer(UnaryTransformer):
     output_type = T.Real
     _defaults = {"scaling_type": "Linear", "slope": 1.0, "intercept": 0.0}
 
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        self.metadata.update(scaler_metadata(self.params["scaling_type"], self.params["slope"],
+                                             self.params["intercept"]))
+
+    def set(self, name, value):
+        super().set(name, value)
+        if name in ("scaling_type", "slope", "intercept") and "metadata" in self.__dict__:
+            self.metadata.update(scaler_metadata(self.params["scaling_type"], self.params["slope"],
+                                                 self.params["intercept"]))
+        return self
+
     def transform_columns(self, a, ds=None):
         x, ok = _f64(a)
+        self.metadata.update(scaler_metadata(self.params["scaling_type"], self.params["slope"],
+                                             self.params["intercept"]))
         if self.params["scaling_type"] == "Logarithmic":
             v = torch.log(x)
         else:
@@ -232,13 +269,24 @@ class ScalerTransformer(UnaryTransformer):
 
 @register_stage
 class DescalerTransformer(BinaryTransformer):
-    """Inverse of the scaling recorded in the metadata of the second input's origin ``ScalerTransformer``."""
+    """Inverse of the scaling recorded in the metadata of the second input (``DescalerTransformer.scala``): the
+    ``ScalerMetadata`` of its origin stage -- a ``ScalerTransformer``, or a fitted ``OpScalarStandardScaler``
+    (linear, slope 1 / std, intercept -mean / std). The resolved scaling is kept in this stage's params, so a
+    saved model descales without its input's stage."""
     operation_name = "descaler"
     output_type = T.Real
     _defaults = {"scaling_type": "Linear", "slope": 1.0, "intercept": 0.0}
 
+    def _resolve_scaling(self):
+        if len(self._inputs) > 1:
+            st = self._inputs[1].origin_stage
+            sc = parse_scaler_metadata(getattr(st, "metadata", None) or {})
+            if sc is not None:
+                self.params.update(sc)
+
     def transform_columns(self, a, b=None, ds=None):
         x, ok = _f64(a)
+        self._resolve_scaling()
         if self.params["scaling_type"] == "Logarithmic":
             v = torch.exp(x)
         else:
