@@ -100,3 +100,49 @@ def test_prediction_descaler_inverts_scaler():
     pred_feat = FeatureBuilder.Real("p").as_predictor()
     d = descale_prediction(pred_feat, scaled)
     assert isinstance(d.origin_stage, PredictionDescaler)
+
+
+def _ms(y, mo, d, h=0, mi=0):
+    import datetime as _dt
+    return int(_dt.datetime(y, mo, d, h, mi, tzinfo=_dt.timezone.utc).timestamp() * 1000)
+
+
+_TP_DATES = [_ms(1879, 3, 14), _ms(1955, 11, 12, 10, 4), _ms(1999, 3, 8, 12), None, _ms(2019, 4, 30, 13)]
+_TP_EXPECTED = {   # TimePeriodTransformerTest.scala "correctly transform for all TimePeriod types" (UTC)
+    "DayOfMonth": [14, 12, 8, None, 30], "DayOfWeek": [5, 6, 1, None, 2], "DayOfYear": [73, 316, 67, None, 120],
+    "HourOfDay": [0, 10, 12, None, 13], "MonthOfYear": [3, 11, 3, None, 4], "WeekOfMonth": [3, 2, 2, None, 5],
+    "WeekOfYear": [11, 46, 11, None, 18],
+}
+
+
+@pytest.mark.parametrize("period", sorted(_TP_EXPECTED))
+def test_time_period_reference_table(period):
+    from transmogrifai_amd import dsl  # noqa: F401
+    ds, (d,) = TestFeatureBuilder.of(("d", T.Date, _TP_DATES))
+    check_transformer(M.TimePeriodTransformer(period=period).set_input(d), ds, expected=_TP_EXPECTED[period])
+    f = d.to_time_period(period)
+    col = f.origin_stage.transform(ds)[f.name]
+    assert [None if not ok else int(v) for v, ok in zip(col.values.tolist(), col.valid.tolist())] == \
+        _TP_EXPECTED[period]
+
+
+def test_time_period_list_and_map_reference():
+    """TimePeriodListTransformerTest / TimePeriodMapTransformerTest: day of month of the four dates; the
+    shortcuts on DateList / DateTimeList and DateMap / DateTimeMap."""
+    from transmogrifai_amd import dsl  # noqa: F401
+    dates = [v for v in _TP_DATES if v is not None]
+    ds, (l, m) = TestFeatureBuilder.of(("l", T.DateList, [dates]),
+                                       ("m", T.DateMap, [dict(zip(["n1", "n2", "n3", "n4"], dates))]))
+    out = check_transformer(M.TimePeriodListTransformer(period="DayOfMonth").set_input(l), ds, check_rows=False)
+    assert out[0] == [14.0, 12.0, 8.0, 30.0]
+    check_transformer(M.TimePeriodMapTransformer(period="DayOfMonth").set_input(m), ds,
+                      expected=[{"n1": 14, "n2": 12, "n3": 8, "n4": 30}])
+    ds2, (d1, d2, m1, m2) = TestFeatureBuilder.of(("d1", T.DateList, [[dates[0]]]), ("d2", T.DateTimeList, [[dates[0]]]),
+                                                  ("m1", T.DateMap, [{"n1": dates[0]}]),
+                                                  ("m2", T.DateTimeMap, [{"n1": dates[0]}]))
+    for f in (d1, d2):
+        g = f.to_time_period("DayOfMonth")
+        assert g.origin_stage.transform(ds2)[g.name].values.double().tolist() == [[14.0]]
+    for f in (m1, m2):
+        g = f.to_time_period("DayOfMonth")
+        assert g.origin_stage.transform(ds2)[g.name].values.tolist() == [{"n1": 14}]
