@@ -18,6 +18,7 @@ from __future__ import annotations
 import ctypes as C
 import math
 import os
+import threading
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -40,6 +41,24 @@ assert HIST_ITEM.itemsize == 32 and PART_ITEM.itemsize == 40 and LEAF_ITEM.items
 ROW_MASK = 0xFFFFFF
 CSR_ITEM_ROWS = 1024          # rows per CSR histogram item (tree_grow.hpp kCsrRows)
 MAX_ROWS = 1 << 24
+
+# Native per-group resource slots (stream, staging, histogram buffers; tree_grow_hip.hip slots()): grower calls
+# running concurrently from several host threads need disjoint slot ranges. A thread running a whole learner next
+# to others (tuning/validators.py concurrent learners) takes a lane of SLOT_LANE slots; every grow_forest call of
+# that thread -- and of the threads it starts through ``set_slot_lane`` -- offsets its slot_base by the lane.
+N_SLOTS, SLOT_LANE = 32, 8
+_lane = threading.local()
+
+
+def slot_lane() -> int:
+    """This thread's slot offset (0 unless a lane was set)."""
+    return getattr(_lane, "base", 0)
+
+
+def set_slot_lane(base: int) -> None:
+    if base < 0 or base + SLOT_LANE > N_SLOTS:
+        raise ValueError(f"slot lane {base} outside the {N_SLOTS} native slots")
+    _lane.base = int(base)
 
 
 @dataclass
@@ -454,6 +473,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     rank would grow. Jobs must not use per-node feature subsets."""
     dev = Xb.device
     on_gpu = dev.type == "cuda"
+    slot_base = int(slot_base) + slot_lane()
     Nrows, F = int(Xb.shape[0]), int(Xb.shape[1])
     chunk_rows = int(os.environ.get("TMOG_TREE_CHUNK", chunk_rows))
     if Nrows >= MAX_ROWS:

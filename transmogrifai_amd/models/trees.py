@@ -19,6 +19,7 @@ from __future__ import annotations
 import json
 import math
 import os
+import threading
 import time
 from typing import Dict, List, Optional, Sequence
 
@@ -41,14 +42,39 @@ class TreeContext:
         self.X = X
         self.rows = rows
         self._cache: Dict[tuple, tuple] = {}
+        self._ready: Dict[tuple, Optional[torch.cuda.Event]] = {}
+        self._lock = threading.Lock()
+
+    def _use(self, key):
+        """Entry ``key``, with the calling thread's stream ordered after the stream that quantized it (learners
+        on concurrent validator lanes share this cache)."""
+        ent, ev = self._cache[key], self._ready.get(key)
+        if ev is not None:
+            torch.cuda.current_stream(ent[1].device).wait_event(ev)
+        return ent
 
     def binned(self, max_bins: int, missing_value: Optional[float] = None, reserve_missing: bool = False):
         key = (max_bins, missing_value, reserve_missing)
-        if key not in self._cache:
-            spec = find_splits(self.X, max_bins, missing_value=missing_value, reserve_missing=reserve_missing,
-                               rows=self.rows)
-            self._cache[key] = (spec, quantize(self.X, spec))
-        return self._cache[key]
+        with self._lock:
+            if key not in self._cache:
+                spec = find_splits(self.X, max_bins, missing_value=missing_value, reserve_missing=reserve_missing,
+                                   rows=self.rows)
+                Xb = quantize(self.X, spec)
+                ev = None
+                if Xb.is_cuda:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(Xb.device))
+                self._cache[key], self._ready[key] = (spec, Xb), ev
+            return self._use(key)
+
+    def matching(self, spec, key=None):
+        """The cached quantized matrix binned exactly as ``spec`` (optionally only entry ``key``), or None."""
+        with self._lock:
+            for k, v in list(self._cache.items()):
+                if (key is None or k == key) and np.array_equal(v[0].thresholds, spec.thresholds) and \
+                        (key is not None or v[0].missing_bin == spec.missing_bin):
+                    return self._use(k)[1]
+        return None
 
 
 def _par(context):
@@ -57,14 +83,18 @@ def _par(context):
     return par if (par is not None and par.world > 1) else None
 
 
+_CTX_LOCK = threading.Lock()
+
+
 def _ctx(X, context):
     if isinstance(context, TreeContext) and context.X is X:
         return context
     if isinstance(context, dict):
-        c = context.get("tree")
-        if c is None or c.X is not X:
-            c = TreeContext(X, context.get("tree_rows"))
-            context["tree"] = c
+        with _CTX_LOCK:         # learners running concurrently (validator lanes) share one binning cache
+            c = context.get("tree")
+            if c is None or c.X is not X:
+                c = TreeContext(X, context.get("tree_rows"))
+                context["tree"] = c
         return c
     return TreeContext(X)
 
@@ -295,8 +325,9 @@ class _ForestLearner(Learner):
         if context is not None:
             ctx = _ctx(X, context)
             key = (int(state["max_bins"]), spec.missing_value, spec.missing_bin >= 0)
-            if key in ctx._cache and np.array_equal(ctx._cache[key][0].thresholds, spec.thresholds):
-                return forest, ctx._cache[key][1]
+            Xb = ctx.matching(spec, key)
+            if Xb is not None:
+                return forest, Xb
         return forest, quantize(X, spec)
 
     def raw_sum(self, state, X, rows=None, context=None):
@@ -486,10 +517,7 @@ class _BoostLearner(Learner):
         forest, spec = self._forest(state)
         Xb = None
         if context is not None:
-            ctx = _ctx(X, context)
-            for (k, v) in ctx._cache.items():
-                if np.array_equal(v[0].thresholds, spec.thresholds) and v[0].missing_bin == spec.missing_bin:
-                    Xb = v[1]
+            Xb = _ctx(X, context).matching(spec)
         if Xb is None:
             Xb = quantize(X, spec)
         m = TE.forest_predict(forest, Xb, [rows], [list(range(forest.n_trees))],
@@ -588,14 +616,16 @@ def _run_parts(dev, parts, fn):
     release the GIL, so the parts' host work and GPU work interleave. The first error is re-raised."""
     import threading
     cur = torch.cuda.current_stream(dev)
-    streams = [torch.cuda.Stream(device=dev) for _ in parts]
+    streams = [torch.cuda.Stream(device=dev, priority=cur.priority) for _ in parts]
     for s in streams:
         s.wait_stream(cur)
     errs = []
+    lane = TE.slot_lane()           # the caller's native slot lane (concurrent learners) carries over
 
     def work(k):
         try:
             torch.cuda.set_device(dev)
+            TE.set_slot_lane(lane)
             with torch.cuda.stream(streams[k]):
                 fn(*parts[k])
         except BaseException as e:          # noqa: BLE001  (re-raised on the caller's thread)

@@ -98,7 +98,7 @@ std::mutex& rccl_mutex() {
 }
 
 std::vector<GpuSlot>& slots() {
-  static std::vector<GpuSlot> s(16);
+  static std::vector<GpuSlot> s(32);   // models/tree_engine.py N_SLOTS (lanes of SLOT_LANE)
   return s;
 }
 
@@ -305,6 +305,12 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
     (void)tmog_hip_tree_prime();     // best effort, before the group threads' first launches (a failure here
                                      // leaves the lazy load to the first launch, as before)
     hipStream_t base = (hipStream_t)a.stream;
+    // One group: it runs on the caller's stream itself (no fork / join, one stream fewer sharing the process's
+    // few hardware queues -- boosting parts and concurrent learners each call with one group). The slot keeps
+    // its own stream for multi-group calls; every earlier use of the slot is ordered before `base` by the
+    // join of the call that made it, and a later multi-group call orders the slot's stream after `base` again.
+    const bool on_base = ng == 1 && base != nullptr;
+    hipStream_t own0 = nullptr;
     hipEvent_t ready;
     hchk(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event");
     hchk(hipEventRecord(ready, base), "event record");
@@ -313,6 +319,11 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
       if (s.stream == nullptr || s.device != dev) {
         hchk(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "stream");
         s.device = dev;
+      }
+      if (on_base) {
+        own0 = s.stream;
+        s.stream = base;
+        continue;
       }
       hchk(hipStreamWaitEvent(s.stream, ready, 0), "wait ready");
     }
@@ -334,7 +345,8 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
       });
     }
     for (auto& t : th) t.join();
-    for (int g = 0; g < ng; ++g) {
+    if (on_base) slots()[sb].stream = own0;
+    for (int g = 0; g < ng && !on_base; ++g) {
       hipEvent_t done;
       hchk(hipEventCreateWithFlags(&done, hipEventDisableTiming), "event");
       hchk(hipEventRecord(done, slots()[sb + g].stream), "event record");

@@ -8,6 +8,7 @@ buffers and ships them with one asynchronous copy; ``to_device`` is the one-arra
 """
 from __future__ import annotations
 
+import threading
 from typing import List
 
 import numpy as np
@@ -24,6 +25,7 @@ class Pack:
     (each ``torch.as_tensor(a, device=cuda)`` is its own blocking hipMemcpy: ~10 per tree level)."""
     _ring: dict = {}
     _RING = 16
+    _lock = threading.Lock()        # host threads of concurrent learners / boosting parts share the ring
 
     def __init__(self, dev):
         self.dev = dev
@@ -42,22 +44,23 @@ class Pack:
             tot += (a.nbytes + 15) & ~15
         tot = max(tot, 16)
         key = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
-        slots = Pack._ring.setdefault(key, {"i": 0, "bufs": [None] * self._RING, "ev": [None] * self._RING})
-        k = slots["i"] = (slots["i"] + 1) % self._RING
-        buf, ev = slots["bufs"][k], slots["ev"][k]
-        if ev is not None:
-            ev.synchronize()                 # the copy that last used this slot has finished
-        if buf is None or buf.numel() < tot:
-            buf = torch.empty(max(tot, 1 << 16), dtype=torch.uint8, pin_memory=True)
-            slots["bufs"][k] = buf
-        hb = buf.numpy()
-        for a, o in zip(self.arrs, offs):
-            hb[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
         d = torch.empty(tot, dtype=torch.uint8, device=self.dev)
-        d.copy_(buf[:tot], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.dev))
-        slots["ev"][k] = ev
+        with Pack._lock:
+            slots = Pack._ring.setdefault(key, {"i": 0, "bufs": [None] * self._RING, "ev": [None] * self._RING})
+            k = slots["i"] = (slots["i"] + 1) % self._RING
+            buf, ev = slots["bufs"][k], slots["ev"][k]
+            if ev is not None:
+                ev.synchronize()                 # the copy that last used this slot has finished
+            if buf is None or buf.numel() < tot:
+                buf = torch.empty(max(tot, 1 << 16), dtype=torch.uint8, pin_memory=True)
+                slots["bufs"][k] = buf
+            hb = buf.numpy()
+            for a, o in zip(self.arrs, offs):
+                hb[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
+            d.copy_(buf[:tot], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+            slots["ev"][k] = ev
         return [d[o:o + a.nbytes].view(_TORCH_OF_NP[a.dtype]).reshape(a.shape) if a.dtype in _TORCH_OF_NP
                 else d[o:o + a.nbytes] for a, o in zip(self.arrs, offs)]
 

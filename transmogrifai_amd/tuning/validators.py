@@ -14,6 +14,7 @@ exchanged (one ``all_gather_object``).
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import math
 import os
@@ -184,6 +185,11 @@ class OpValidator:
         timings = {}
         # spread learners first (all ranks in lockstep through their collectives), then the shards
         order = sorted(range(len(models)), key=lambda li: (li not in spread, li))
+        lanes = self._learner_lanes(X, world, len(order))
+        if lanes > 1:
+            results, failures, timings = self._fit_eval_concurrent(models, order, jobs, owner, me, X, y, train_rows,
+                                                                   val_rows, ctx, t0, lanes, n_tr)
+            order = []
         for li in order:
             lname, grid = models[li]
             mine = [(j, (l, g, k)) for j, (l, g, k) in enumerate(jobs) if l == li and owner[j] == me]
@@ -393,6 +399,114 @@ class OpValidator:
             ys.append(torch.cat([yt, yv]).to(Xk.dtype))
             off += int(Xk.shape[0])
         return torch.cat(blocks), torch.cat(ys), train_rows, val_rows
+
+    def _learner_lanes(self, X, world: int, n_learners: int) -> int:
+        """Learners fitted at once on one GPU (``parallelism``, OpValidator.scala:377: the reference runs up to 8
+        fits as concurrent futures). Only single-rank: spread learners move through collectives in lockstep.
+        Opt-in (``TMOG_LEARNER_LANES`` > 1): on the MI355X headline three lanes measured 2.19-2.37 s against
+        2.36-2.45 s sequential in good runs, but some runs stalled for 10-55 s (one past 180 s) -- with a dozen
+        streams (lanes, boosting parts, grower slots) over the process's 4 hardware queues, in-order queues
+        shared by streams that wait on each other serialise badly -- so one learner after the other stays the
+        default (profiles/README.md, round 3)."""
+        env = os.environ.get("TMOG_LEARNER_LANES")
+        # host-only runs stay sequential unless asked for (the CPU kernels already use every core)
+        if world > 1 or n_learners < 2 or not isinstance(X, torch.Tensor) or not (X.is_cuda or env):
+            return 1
+        from ..models.tree_engine import N_SLOTS, SLOT_LANE
+        cap = int(env) if env else 1
+        return max(1, min(cap, n_learners, N_SLOTS // SLOT_LANE))
+
+    def _fit_eval_concurrent(self, models, order, jobs, owner, me, X, y, train_rows, val_rows, ctx, t0, lanes, n_tr):
+        """Every learner's batch on one of ``lanes`` worker threads, each with its own HIP stream (ordered after
+        the caller's, which waits for all of them) and its own range of native tree-grower slots, longest
+        estimated learner first. One learner's host round trips (OWL-QN line searches, tree levels, early-stopping
+        reads) and small launches then overlap another's kernels instead of idling the GPU; every learner's
+        kernels and reductions are the ones the sequential path runs, so the metrics are identical. maxWait
+        bounds the whole search: learners not started in time are dropped, and learners still running at the
+        deadline are reported failed and abandoned (``awaitResult(maxWait)``, OpValidator.scala:348)."""
+        import sys
+        import threading
+        from ..models import tree_engine as TE
+        dev = X.device
+        todo = []
+        for li in order:
+            mine = [(j, (l, g, k)) for j, (l, g, k) in enumerate(jobs) if l == li and owner[j] == me]
+            if mine:
+                lname, grid = models[li]
+                cost = sum(_scaled_cost(lname, grid[g], n_tr, X.shape[1]) for _, (_, g, _) in mine)
+                todo.append((cost, li, mine))
+        todo.sort(key=lambda t: -t[0])
+        results: Dict[Tuple[int, int, int], float] = {}
+        failures: List[str] = []
+        timings: Dict[str, float] = {}
+        started, errs = set(), []
+        lock = threading.Lock()
+        gpu = dev.type == "cuda"
+        cur = torch.cuda.current_stream(dev) if gpu else None
+        # lane 0 takes the longest learner (the critical path): its stream -- and the boosting parts' streams it
+        # starts (models/trees.py _run_parts inherits the priority) -- get the high scheduling priority
+        hi = -1 if os.environ.get("TMOG_LANE_PRIO", "1") != "0" else 0
+        streams = [torch.cuda.Stream(device=dev, priority=hi if w == 0 else 0) for w in range(lanes)] if gpu \
+            else [None] * lanes
+        for st in streams:
+            if st is not None:
+                st.wait_stream(cur)
+
+        def worker(w):
+            try:
+                if gpu:
+                    torch.cuda.set_device(dev)
+                TE.set_slot_lane(w * TE.SLOT_LANE)
+                with (torch.cuda.stream(streams[w]) if gpu else contextlib.nullcontext()):
+                    while True:
+                        with lock:
+                            if not todo or errs:
+                                return
+                            _, li, mine = todo.pop(0)
+                            lname, grid = models[li]
+                            if time.time() - t0 > self.max_wait:
+                                failures.append(f"{lname}: not started within maxWait={self.max_wait}s")
+                                continue
+                            started.add(li)
+                        t1 = time.time()
+                        res, fails = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, ctx)
+                        with lock:
+                            results.update(res)
+                            failures.extend(fails)
+                            timings[lname] = time.time() - t1
+                            started.discard(li)
+            except BaseException as e:          # noqa: BLE001  (re-raised on the caller's thread)
+                with lock:
+                    errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(w,), name=f"fit-lane-{w}", daemon=True) for w in range(lanes)]
+        swi = sys.getswitchinterval()
+        # a lane returning from a native call must win the GIL back from one running Python promptly
+        sys.setswitchinterval(min(swi, float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))))
+        try:
+            for t in th:
+                t.start()
+            bounded = self.max_wait < _UNBOUNDED_WAIT
+            for t in th:
+                t.join(max(0.0, self.max_wait - (time.time() - t0)) if bounded else None)
+        finally:
+            sys.setswitchinterval(swi)
+        with lock:
+            if errs:
+                raise errs[0]
+            for li in sorted(started):      # still running at the maxWait deadline: abandoned
+                lname = models[li][0]
+                log.warning("Model %s did not finish within maxWait=%ss; its fits are dropped", lname, self.max_wait)
+                failures.append(f"{lname}: did not finish within maxWait={self.max_wait}s")
+            for key in [k for k in results if k[0] in started]:
+                del results[key]
+            done = not started
+        if done and gpu:
+            for st in streams:
+                cur.wait_stream(st)
+            # blocks freed on the lane streams are reused by later allocations only once their work has ended
+            torch.cuda.synchronize(dev)
+        return dict(results), list(failures), dict(timings)
 
     def _fit_eval_bounded(self, lname, grid, mine, X, y, train_rows, val_rows, ctx, remaining: float):
         """:meth:`_fit_eval` under the ``maxWait`` deadline (``awaitResult(..., maxWait)``, OpValidator.scala:348):
