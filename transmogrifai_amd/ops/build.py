@@ -87,12 +87,13 @@ def build_hip(force: bool = False, arch: str = ARCH) -> Path:
         raise RuntimeError("hipcc not found: cannot build the HIP kernels")
     with _Lock():
         if force or _stale(HIP_SO, srcs):
-            objs = []
-            for s in srcs:
-                o = LIB / (s.stem + ".o")
-                _run([hipcc, f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-c",
-                      "-munsafe-fp-atomics", f"-I{CSRC}", "-o", str(o), str(s)])
-                objs.append(str(o))
+            from concurrent.futures import ThreadPoolExecutor
+            objs = [str(LIB / (s.stem + ".o")) for s in srcs]
+            # one hipcc per translation unit, a few at a time (the tree kernels alone take ~1 min)
+            with ThreadPoolExecutor(max_workers=max(1, min(8, os.cpu_count() or 1))) as ex:
+                list(ex.map(lambda so: _run([hipcc, f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-c",
+                                             "-munsafe-fp-atomics", f"-I{CSRC}", "-o", so[1], str(so[0])]),
+                            zip(srcs, objs)))
             tmp = HIP_SO.with_suffix(f".so.tmp{os.getpid()}")
             _run([hipcc, f"--offload-arch={arch}", "-shared", "-fPIC", "-o", str(tmp)] + objs + ["-lrccl"])
             os.replace(tmp, HIP_SO)

@@ -309,7 +309,8 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
     // few hardware queues -- boosting parts and concurrent learners each call with one group). The slot keeps
     // its own stream for multi-group calls; every earlier use of the slot is ordered before `base` by the
     // join of the call that made it, and a later multi-group call orders the slot's stream after `base` again.
-    const bool on_base = ng == 1 && base != nullptr;
+    static const bool base_ok = [] { const char* e = std::getenv("TMOG_GROW_ON_BASE"); return !(e && e[0] == '0'); }();
+    const bool on_base = base_ok && ng == 1 && base != nullptr;
     hipStream_t own0 = nullptr;
     hipEvent_t ready;
     hchk(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event");

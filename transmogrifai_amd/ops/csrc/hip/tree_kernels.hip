@@ -282,6 +282,14 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
 // ds_add_u32. Output is identical (integer sums) to the byte path and the CPU twin.
 constexpr int kWideU = 16;
 
+// LDS table layout (bank-conflict free): the ds_add_u64 of a wave-instruction is serviced in 4 groups of 16
+// contiguous lanes, and a group conflicts when two of its lanes hit one bank (byte address / 4 mod 32). Lanes are
+// (rs, d) with the dword count padded to NP = 16 / 8 / 4 / 2 / 1 (a power of two), so a 16-lane group holds
+// 16 / NP rows of one group of NP dwords; lane position p = lane % 16 is unique in its group. Word
+// (k, b, p) = k * (B + 1) * 16 + b * 16 + p holds feature 4 d + k, bin b, for row slot p / NP: its bank pair
+// 2 p mod 32 depends on the lane position only, never on the (data-dependent) bin -- the feature-major layout
+// put lanes of random bins on random banks (~3.5-way per group). Row slots of one group are separate copies,
+// folded before the write-out; the table stays 64 x (B + 1) words.
 __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t* __restrict__ Xb, int F, int col0,
                                                const uint32_t* __restrict__ rows,
                                                const int32_t* __restrict__ node_model,
@@ -290,18 +298,15 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
                                                int64_t stride, const float* __restrict__ qscale, int skip_bin,
                                                int* lds, const int2* __restrict__ gh) {
   const int FG = it.nf;
-  const int ND = (FG + 3) >> 2;
-  const int RPI = 64 / ND;
+  const int ND = (FG + 3) >> 2;                    // dwords of the group's row segment (<= 16)
+  const int NP = ND <= 1 ? 1 : ND <= 2 ? 2 : ND <= 4 ? 4 : ND <= 8 ? 8 : 16;
+  const int RPI = 64 / NP;                         // rows per wave-instruction (>= 4)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-  const int rs = lane / ND, d = lane - rs * ND;
-  const bool active = rs < RPI;
-  const int tstride = B + 1;                       // bin B: missing-bin value recovered at the end
+  const int rs = lane / NP, d = lane - rs * NP;
+  const int pos = lane & 15;
+  const int sub = (B + 1) * 16;                    // words per k-plane
   unsigned long long* tab = reinterpret_cast<unsigned long long*>(lds);
-  // feature f's row starts at f * tstride + f / 4: the extra word per 4 features moves consecutive lanes
-  // (dword d = features 4d..4d+3) to distinct LDS banks for the 64-bit atomics (8 * tstride alone is
-  // 0 mod 8 dwords for any B, a 4-way conflict)
-  auto tix = [tstride](int f, int b) { return f * tstride + (f >> 2) + b; };
-  const int twords = 4 * ND * tstride + ND + 1;      // rows for the pad features of the last dword too
+  const int twords = 4 * sub;                      // == 64 * (B + 1): the launcher's LDS size
   const int toff = (2 * twords + 3) & ~3;
   int4* stage = reinterpret_cast<int4*>(lds + toff) + wave * 64;
   int* tot = lds + toff + 4 * 64 * nwaves;
@@ -315,13 +320,13 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
   const int64_t cnt = it.count;
   // buffer loads: one descriptor for the group's first column (wave-uniform) and a 32-bit per-lane byte
   // offset row * F + 4 d (the grower takes this path only for matrices below 2 GiB) -- one VGPR per
-  // gather address instead of two
+  // gather address instead of two. Pad lanes (d >= ND) re-read the last dword and add 0.
   const uint64_t xbase = (uint64_t)(uintptr_t)(Xb + col0);
   const uint32_t xlo = __builtin_amdgcn_readfirstlane((uint32_t)xbase);
   const uint32_t xhi = __builtin_amdgcn_readfirstlane((uint32_t)(xbase >> 32));
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(uintptr_t)(((uint64_t)xhi << 32) | xlo), (short)0, 0x7FFFFFFF, 0x00020000);
-  const uint32_t lane_off = 4u * (uint32_t)d;
+  const uint32_t lane_off = 4u * (uint32_t)min(d, ND - 1);
   const float* t1m = t1 + model * stride;
   const float* t2m = t2 + model * stride;
   // Software pipeline over the wave's 64-row chunks: the next chunk's row entry is loaded before this
@@ -369,7 +374,7 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0): staged records visible to the wave
     __builtin_amdgcn_wave_barrier();
-    {                                          // RPI * kWideU >= 64 (ND <= 16): one pass covers the chunk
+    {                                          // RPI * kWideU >= 64 (NP <= 16): one pass covers the chunk
       // only the row ids stay in registers across the gathers; (g, h) are re-read from the LDS stage
       // at the atomics (fewer VGPRs -> more waves, i.e. more gathers in flight per CU)
       uint32_t off[kWideU], w[kWideU];
@@ -384,28 +389,37 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
         h_n = t2m[e_n & 0xFFFFFFu];
       }
       __builtin_amdgcn_sched_barrier(0);
-      // branch-free: masked-off work (lanes past the rows, pad features) adds 0 to the lane's own word
+      // branch-free: masked-off work (rows past the chunk, pad features) adds 0 to the lane's own word
       // instead of toggling EXEC around every atomic (a masked lane costs the same)
 #pragma unroll
       for (int u = 0; u < kWideU; ++u) {
-        const bool live = active && u * RPI + rs < nrows;
+        const bool live = u * RPI + rs < nrows;
         const int2 st = *reinterpret_cast<const int2*>(&stage[min(u * RPI + rs, 63)]);
         const unsigned long long pk = live ? ((unsigned long long)(uint32_t)st.x << 32) + (unsigned long long)(uint32_t)st.y
                                            : 0ull;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const int f = 4 * d + k;
           const int bin = (int)((w[u] >> (8 * k)) & 0xFFu);
-          // the skipped missing bin's own word is never read (recovered into the pad word below), and the
-          // table has rows for the group's pad features 4 ND > FG, so every lane adds to its own word
-          atomicAdd(tab + tix(f, bin), f < FG ? pk : 0ull);
+          atomicAdd(tab + k * sub + bin * 16 + pos, 4 * d + k < FG ? pk : 0ull);
         }
       }
     }
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
-  if (sparse) {       // missing bin = chunk totals - the other bins, packed into the pad slot
+  // fold the 16 / NP row-slot copies of every (k, bin) row into its first NP words
+  if (NP < 16) {
+    for (int i = threadIdx.x; i < 4 * B * NP; i += blockDim.x) {
+      const int r = i / NP, dd = i - r * NP;                   // r = k * B + bin
+      unsigned long long* row = tab + (r / B) * sub + (r % B) * 16;
+      unsigned long long acc = row[dd];
+      for (int c = NP; c < 16; c += NP) acc += row[c + dd];
+      row[dd] = acc;
+    }
+    __syncthreads();
+  }
+  auto tix = [sub](int f, int b) { return (f & 3) * sub + b * 16 + (f >> 2); };
+  if (sparse) {       // missing bin = chunk totals - the other bins, packed into the spare bin-B word
     for (int f = threadIdx.x; f < FG; f += blockDim.x) {
       long long g = 0, h = 0;
       for (int b = 0; b < B; ++b) {
