@@ -11,4 +11,4 @@ timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --verbose > gpurun_ou
 grep '^{' gpurun_out/${T}_bench.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('bench', round(d['value'],4), d['holdout_aupr'], {k: round(v,3) for k,v in d['timings'].items()})"
 D=/tmp/prof_$T; rm -rf $D
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 bench.py --steps 1 --warmup 1 > gpurun_out/${T}_prof.log 2>&1 || exit $?
-cp $D/run_kernel_stats.csv gpurun_out/${T}_kernel_stats.csv && python3 scripts/kstats.py gpurun_out/${T}_kernel_stats.csv | head -12
+cp $D/run_kernel_stats.csv gpurun_out/${T}_kernel_stats.csv && python3 scripts/kstats.py gpurun_out/${T}_kernel_stats.csv > gpurun_out/${T}_kstats.txt; head -12 gpurun_out/${T}_kstats.txt
