@@ -103,6 +103,8 @@ _HIP_SIGS = {
     "tmog_hip_csc_spmm_t": [P, P, P, I64, P, I64, P, I32, I32, P, P, P],
     "tmog_hip_softmax_epilogue": [P, I64, I32, I32, P, P, P, I32, P, I32, P],
     "tmog_hip_colsum": [P, I64, I32, I32, P, P],
+    "tmog_hip_mlp_bias_sigmoid": [P, I32, I64, I32, P, P],
+    "tmog_hip_mlp_sigmoid_backprop": [P, P, I32, I64, I32, I32, P, P],
     "tmog_hip_gather_rows_cols": [P, P, P, I64, I32, P, P],
     "tmog_hip_hash_tokens": [P, P, I64, P, I32, I32, I32, I32, P, P],
     "tmog_hip_hash_tf_rows": [P, I32, I64, I32, I32, P, I64, I64, P],
