@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 T=${1:-hist}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_tree_engine.py tests/test_gpu_kernels.py tests/test_forest_share.py tests/test_tree_capacity.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${T}_test.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_tree_engine.py tests/test_gpu_kernels.py tests/test_forest_share.py tests/test_tree_capacity.py tests/test_mlp.py tests/test_sparse_linear_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${T}_test.log 2>&1
 rc=$?; tail -n 2 gpurun_out/${T}_test.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --verbose > gpurun_out/${T}_bench.log 2>&1 || exit $?
 grep '^{' gpurun_out/${T}_bench.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('bench', round(d['value'],4), d['holdout_aupr'], {k: round(v,3) for k,v in d['timings'].items()})"

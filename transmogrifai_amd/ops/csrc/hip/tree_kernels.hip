@@ -129,6 +129,26 @@ __device__ __forceinline__ void add_row(int* my, int bin, int S, int s0, int Sc,
 constexpr int kCsrU = 16;
 constexpr int kCsrG = 8;     // row slots per lane group in flight (register budget of the whole kernel)
 
+// Wave64 inclusive prefix sum of an int64 on the DPP lane network (GFX9 sequence: row_shr 1 / 2 / 4 / 8 inside
+// the 16-lane rows, then row_bcast:15 into rows 1 and 3 and row_bcast:31 into rows 2 and 3), two 32-bit halves
+// moved per step and added as one 64-bit value: 12 DPP moves + 6 adds instead of 6 x 2 ds_bpermute (LDS
+// crossbar) + selects. Lanes without a source keep `old` = 0. Integer sums: identical to any other order.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int64_t dpp_shift64(int64_t v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(uint64_t)v, CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)((uint64_t)v >> 32), CTRL, ROWS, 0xF, false);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
+__device__ __forceinline__ int64_t wave_scan64(int64_t v) {
+  v += dpp_shift64<0x111, 0xF>(v);    // row_shr:1
+  v += dpp_shift64<0x112, 0xF>(v);    // row_shr:2
+  v += dpp_shift64<0x114, 0xF>(v);    // row_shr:4
+  v += dpp_shift64<0x118, 0xF>(v);    // row_shr:8
+  v += dpp_shift64<0x142, 0xA>(v);    // row_bcast:15 -> rows 1, 3
+  v += dpp_shift64<0x143, 0xC>(v);    // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
   const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
@@ -956,12 +976,7 @@ struct NodeScan {
   // multi-bin feature f: lane = bin, v = this lane's bin statistics (0 past nb), miss = the missing bin's
   // (same on every lane). Exact int64 wave prefix sum, then the lane's (bin, dl) candidates.
   __device__ __forceinline__ void scan_feature(int64_t* v, const int64_t* miss, int nb, int f, int lane) {
-    for (int off = 1; off < 64; off <<= 1) {
-      TM_FOR_S(s) {
-        const int64_t o = __shfl_up(v[s], off, 64);
-        if (lane >= off) v[s] += o;
-      }
-    }
+    TM_FOR_S(s) v[s] = wave_scan64(v[s]);
     // candidates b < nb - 1; with a missing bin dl = 0 also b = nb - 1 (present left, missing right).
     // An empty missing bin makes every dl = 1 candidate equal to its dl = 0 twin, which wins the tie
     // (better(): dl ascending; the CPU twin's first-wins scan order) -- skip them.
@@ -997,11 +1012,7 @@ template <int SM>
 __device__ __forceinline__ void node_totals(const int64_t* h, int B, int S, int lane, int64_t* totq) {
   int64_t v[SM];
   TM_FOR_S(s) v[s] = lane < B ? h[lane * S + s] : 0;     // all loads before the reductions
-  TM_FOR_S(s) {
-    int64_t t = v[s];
-    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
-    totq[s] = t;
-  }
+  TM_FOR_S(s) totq[s] = readlane64(wave_scan64(v[s]), 63);
 }
 
 template <int SM>
@@ -1186,8 +1197,8 @@ __global__ void __launch_bounds__(256) pair_scan_kernel(
         const int64_t c = lane < B ? pp[s] - pa[s] : 0;
         if (lane < B) Hb[o + lane * S + s] = c;
         // missing bin statistics from the lane holding it
-        ms[s] = missing_bin >= 0 ? __shfl(a, missing_bin, 64) : 0;
-        mb[s] = missing_bin >= 0 ? __shfl(c, missing_bin, 64) : 0;
+        ms[s] = missing_bin >= 0 ? readlane64(a, missing_bin) : 0;   // kernel argument: wave-uniform lane
+        mb[s] = missing_bin >= 0 ? readlane64(c, missing_bin) : 0;
         vs[s] = lane < nbins ? a : 0;
         vb[s] = lane < nbins ? c : 0;
       }
