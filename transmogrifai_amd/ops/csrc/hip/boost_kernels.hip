@@ -30,6 +30,17 @@ namespace {
 
 constexpr int kAmaxCopies = 64;   // boost_epilogue_kernel's per-job maxima: [kAmaxCopies][P][2] (trees.py)
 
+// Wave64 max of non-negative floats (their bit patterns order like int32) on DPP -- row_shr 1/2/4/8 inside the
+// 16-lane rows, row_bcast 15/31 across them -- wave-uniform result, no ds_bpermute. Whole wave active.
+__device__ __forceinline__ float wave_max_nonneg(float f) {
+  int v = __float_as_int(f);
+#define TM_DPP_MAX(CTRL, ROWS) v = max(v, __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false));
+  TM_DPP_MAX(0x111, 0xF) TM_DPP_MAX(0x112, 0xF) TM_DPP_MAX(0x114, 0xF) TM_DPP_MAX(0x118, 0xF)
+  TM_DPP_MAX(0x142, 0xA) TM_DPP_MAX(0x143, 0xC)
+#undef TM_DPP_MAX
+  return __int_as_float(__builtin_amdgcn_readlane(v, 63));
+}
+
 __global__ void __launch_bounds__(256) boost_epilogue_kernel(
     const uint32_t* __restrict__ entries, const int32_t* __restrict__ gid, int64_t n_entries,
     const float* __restrict__ gid_value, const int64_t* __restrict__ gid_tree, const int64_t* __restrict__ tree_job,
@@ -93,13 +104,11 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
       const unsigned long long act = __ballot(pend);
       if (act == 0ull) break;
       const int leader = __ffsll((long long)act) - 1;
-      const int64_t lp = __shfl(p, leader, 64);
+      const int64_t lp = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)p >> 32), leader) << 32) |
+                                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)p, leader));
       const bool mine = pend && p == lp;
-      float mg = mine ? ag : 0.f, mh = mine ? ah : 0.f;
-      for (int off = 32; off > 0; off >>= 1) {
-        mg = fmaxf(mg, __shfl_xor(mg, off, 64));
-        mh = fmaxf(mh, __shfl_xor(mh, off, 64));
-      }
+      // NaN lanes contribute nothing (as fmaxf ignored them)
+      const float mg = wave_max_nonneg(mine && ag == ag ? ag : 0.f), mh = wave_max_nonneg(mine && ah == ah ? ah : 0.f);
       if (lane == leader) {
         uint32_t* dst = amax + ((int64_t)(blockIdx.x % kAmaxCopies) * P + lp) * 2;
         atomicMax(dst, __float_as_uint(mg));
@@ -118,7 +127,8 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
       const unsigned long long act = __ballot(pend);
       if (act == 0ull) break;
       const int leader = __ffsll((long long)act) - 1;
-      const int64_t ls = __shfl(slot, leader, 64);
+      const int64_t ls = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)slot >> 32), leader) << 32) |
+                                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)slot, leader));
       const bool mine = pend && slot == ls;
       const unsigned long long mm = __ballot(mine);
       if (lane == leader) atomicAdd(auc_hist + ls, (int)__popcll(mm));

@@ -149,6 +149,21 @@ __device__ __forceinline__ int64_t wave_scan64(int64_t v) {
   return v;
 }
 
+// Wave64 int32 sum / max of non-negatives on DPP, result wave-uniform (the inclusive scan ends in lane 63): 6 DPP
+// adds + one readlane instead of 6 ds_bpermute round trips through the LDS crossbar. Whole wave active.
+template <bool MAX>
+__device__ __forceinline__ int wave_reduce32(int v) {
+#define TM_DPP_STEP(CTRL, ROWS)                                                         \
+  {                                                                                     \
+    const int t = __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false);           \
+    v = MAX ? max(v, t) : v + t;                                                        \
+  }
+  TM_DPP_STEP(0x111, 0xF) TM_DPP_STEP(0x112, 0xF) TM_DPP_STEP(0x114, 0xF) TM_DPP_STEP(0x118, 0xF)
+  TM_DPP_STEP(0x142, 0xA) TM_DPP_STEP(0x143, 0xC)
+#undef TM_DPP_STEP
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
   const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
@@ -220,8 +235,7 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
     // Lane groups of W (a power of two >= this chunk's longest list, <= 64) take one row each, so a
     // wave-instruction covers 64 / W rows at (nearly) full lane use instead of one row per instruction
     // (the headline's rows carry ~17 entries).
-    int mx = len;
-    for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+    const int mx = wave_reduce32<true>(len);
     const int W = mx <= 8 ? 8 : mx <= 16 ? 16 : mx <= 32 ? 32 : 64;
     const int RPI = 64 / W;
     const int rs = lane / W, k = lane - rs * W;
@@ -382,11 +396,8 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
     }
     stage[lane] = make_int4(mine.y, mine.z, mine.x, 0);   // (q(g), q(h), entry): (g, h) 8-byte aligned
     if (sparse) {
-      int a = lane < nrows ? mine.y : 0, b = lane < nrows ? mine.z : 0;
-      for (int off = 32; off > 0; off >>= 1) {
-        a += __shfl_xor(a, off, 64);
-        b += __shfl_xor(b, off, 64);
-      }
+      const int a = wave_reduce32<false>(lane < nrows ? mine.y : 0);
+      const int b = wave_reduce32<false>(lane < nrows ? mine.z : 0);
       if (lane == 0) {
         atomicAdd(tot, a);
         atomicAdd(tot + 1, b);
@@ -568,11 +579,8 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     stage[lane] = mine;
     if (sparse) {
       // chunk totals: one wave reduction of the 64 staged (g, h) records, one LDS add per wave
-      int a = lane < nrows ? mine.y : 0, b = lane < nrows ? mine.z : 0;
-      for (int off = 32; off > 0; off >>= 1) {
-        a += __shfl_xor(a, off, 64);
-        b += __shfl_xor(b, off, 64);
-      }
+      const int a = wave_reduce32<false>(lane < nrows ? mine.y : 0);
+      const int b = wave_reduce32<false>(lane < nrows ? mine.z : 0);
       if (lane == 0) {
         atomicAdd(tot, a);
         atomicAdd(tot + 1, b);
