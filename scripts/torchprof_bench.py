@@ -1,8 +1,11 @@
 """Device-time attribution of torch ops in one headline step: python scripts/torchprof_bench.py OUT.txt <bench args>
 (torch.profiler with input shapes; the native HIP kernels show up under their own names)."""
+import os
 import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 out = sys.argv[1]
 sys.argv = ["bench.py"] + sys.argv[2:]

@@ -256,3 +256,26 @@ def test_poisson_pack_kernel_matches_host():
         a, b = pc[off[t]:off[t + 1]], pg[off[t]:off[t + 1]]
         assert torch.equal(a.sort().values, b.sort().values)
     assert _native_loaded()
+
+
+@pytest.mark.parametrize("max_bins,reserve,mv", [(32, False, None), (64, True, 0.0), (256, True, None), (2, False, None)])
+def test_hip_quantize_matches_torch_path(monkeypatch, max_bins, reserve, mv):
+    """quantize_kernels.hip against the torch searchsorted path: ties with the fp32 thresholds, NaN, +-inf, the
+    missing value, a feature count that is not a multiple of the 64-feature block."""
+    from transmogrifai_amd.models.binning import find_splits, quantize
+    g = torch.Generator().manual_seed(7)
+    n, d = 70_001, 131
+    X = torch.randn(n, d, generator=g)
+    X[:, :20] = (X[:, :20] > 0.5).float()                 # two-valued columns: exact ties with thresholds
+    X[:, 20:30] = torch.round(X[:, 20:30] * 3) / 3        # few distinct values
+    X[::97, 40] = float("nan")
+    X[::101, 41] = float("inf")
+    X[::103, 42] = -float("inf")
+    Xd = X.cuda()
+    spec = find_splits(Xd, max_bins, missing_value=mv, reserve_missing=reserve)
+    monkeypatch.setenv("TMOG_HIP_QUANTIZE", "0")
+    ref = quantize(Xd, spec)
+    monkeypatch.setenv("TMOG_HIP_QUANTIZE", "1")
+    got = quantize(Xd, spec)
+    assert torch.equal(got.cpu(), ref.cpu())
+    assert _native_loaded()

@@ -8,6 +8,8 @@ XGBoost-style missing handling reserves the last bin for missing values (``missi
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 from typing import Optional
 
@@ -78,9 +80,22 @@ def find_splits(X: torch.Tensor, max_bins: int = 32, seed: int = 0, missing_valu
 
 
 def quantize(X: torch.Tensor, spec: BinSpec, chunk_rows: int = 1 << 20) -> torch.Tensor:
-    """``uint8 [N, F]`` bins of ``X`` (float) under ``spec`` (row chunks bound the temporaries)."""
+    """``uint8 [N, F]`` bins of ``X`` (float) under ``spec`` (row chunks bound the temporaries). A contiguous fp32
+    device matrix takes one HIP pass (``ops/csrc/hip/quantize_kernels.hip``; same bins as the torch path:
+    ``searchsorted(side="left")`` on the fp32 thresholds, NaN after every threshold, the missing bin)."""
     dev = X.device
     n, F = int(X.shape[0]), int(X.shape[1])
+    ms = int(spec.thresholds.shape[1]) if spec.thresholds.ndim == 2 else 0
+    if (X.is_cuda and X.dtype == torch.float32 and X.is_contiguous() and 1 <= ms <= 255 and F > 0 and n > 0
+            and os.environ.get("TMOG_HIP_QUANTIZE", "1") != "0"):
+        from ..ops import _native as N_
+        thr32 = torch.as_tensor(np.ascontiguousarray(spec.thresholds, np.float32), device=dev)
+        out = torch.empty(n, F, dtype=torch.uint8, device=dev)
+        mv = spec.missing_value
+        N_.check(N_.hip().tmog_hip_quantize(N_.ptr(X), n, F, N_.ptr(thr32), ms, int(spec.missing_bin),
+                                            int(mv is not None), float(mv) if mv is not None else 0.0, N_.ptr(out),
+                                            N_.stream(dev)), "quantize")
+        return out
     thr = torch.as_tensor(spec.thresholds, device=dev)
     out = torch.empty(n, F, dtype=torch.uint8, device=dev)
     thr_t = thr.to(torch.float32 if X.dtype == torch.float32 else torch.float64).contiguous()

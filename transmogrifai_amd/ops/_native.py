@@ -94,7 +94,7 @@ _HIP_SIGS = {
     "tmog_hip_col_stats": [P, P, I64, I32, I64, P, P],
     "tmog_hip_vectorize_numeric": [P, P, P, I64, I32, P, P, P, P, I64, I32, P],
     "tmog_hip_onehot_pivot": [P, P, P, P, I32, I64, P, I64, P],
-    "tmog_hip_quantize": [P, I64, I32, I64, P, P, P, I32, P, I64, P],
+    "tmog_hip_quantize": [P, I64, I32, P, I32, I32, I32, F32, P, P],
     "tmog_hip_gram_aug": [P, I64, I32, I64, P, P, I32, P, P],
     "tmog_hip_class_colsum": [P, I64, I32, I64, P, I32, I32, P, P],
     "tmog_hip_logistic_grad": [P, P, P, I64, I32, P],
