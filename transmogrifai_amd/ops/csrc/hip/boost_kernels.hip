@@ -217,13 +217,14 @@ __global__ void __launch_bounds__(256) row_uniform_kernel(const int64_t* __restr
 // call at 6 x 65536 bins).
 constexpr int AUPR_NT = 1024;
 
+// wave64 inclusive prefix sum on DPP (row_shr 1 / 2 / 4 / 8, row_bcast 15 / 31; lanes without a source add 0)
 __device__ __forceinline__ int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(v, o, 64);
-    if (lane >= o) v += u;
-  }
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
   return v;
 }
 
