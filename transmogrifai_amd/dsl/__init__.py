@@ -44,6 +44,11 @@ def transmogrify(features, label=None, defaults=None):
     return transmogrify_combined(list(features), label, defaults or TransmogrifierDefaults)
 
 
+def auto_transform(features, label=None, defaults=None):
+    """``RichFeaturesCollection.autoTransform`` (RichFeaturesCollection.scala:79): alias of :func:`transmogrify`."""
+    return transmogrify(features, label, defaults)
+
+
 def combine(*vectors):
     from ..stages.feature.vectorizers import VectorsCombiner
     vs = []

@@ -338,8 +338,10 @@ def _phone_valid(self, default_region: str = "US", is_strict: bool = False):
 
 
 @register(T.Base64, "detect_mime_types")
-def _mime(self):
-    return TS.TextMapTransformer("MimeTypeDetector", T.Text).set_input(self).get_output()
+def _mime(self, type_hint: Optional[str] = None):
+    """``RichBase64Feature.detectMimeTypes`` (RichTextFeature.scala:712-731)."""
+    from ..stages.feature.nlp_stages import MimeTypeDetector
+    return MimeTypeDetector(type_hint=type_hint or "").set_input(self).get_output()
 
 
 @register(T.Text, "text_len")
@@ -431,6 +433,20 @@ def _vec_map(self, others=(), **kw):
     ``track_nulls``, ``white_list_keys`` / ``black_list_keys``, ...)."""
     from ..stages.feature.maps import map_vectorize
     return map_vectorize(self.wtype, _others(self, others), None, D, **kw)[0]
+
+
+@register(T.PhoneMap, "is_valid_phone_default_country_map")
+def _phone_map_valid(self, is_strict: bool = False, default_region: str = "US"):
+    """``RichPhoneMapFeature.isValidPhoneDefaultCountryMap`` (RichMapFeature.scala:979-993) -> BinaryMap."""
+    from ..stages.feature.nlp_stages import IsValidPhoneMapDefaultCountry
+    return IsValidPhoneMapDefaultCountry(default_region=default_region, strict=is_strict).set_input(self).get_output()
+
+
+@register(T.Base64Map, "detect_mime_types")
+def _mime_map(self, type_hint: Optional[str] = None):
+    """``RichBase64MapFeature.detectMimeTypes`` (RichMapFeature.scala:128-132) -> PickListMap."""
+    from ..stages.feature.nlp_stages import MimeTypeMapDetector
+    return MimeTypeMapDetector(type_hint=type_hint or "").set_input(self).get_output()
 
 
 @register(T.OPVector, "drop_indices_by")

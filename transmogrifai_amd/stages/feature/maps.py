@@ -362,7 +362,7 @@ class MapVectorizer(VectorizerMixin, SequenceEstimator):
     _defaults = {"kind": "real", "clean_keys": False, "clean_text": True, "track_nulls": True,
                  "fill_with_mean": False, "fill_with_mode": False, "fill_value": 0.0, "top_k": 20, "min_support": 10,
                  "reference_date": None, "max_cardinality": 30, "num_features": 512, "allow_keys": None,
-                 "block_keys": None}
+                 "block_keys": None, "max_pct_cardinality": 1.0}
     # row-sharded fits reduce per-key statistics over the ranks: key union and (key, value) counts in one
     # object all-gather, per-key sums in one all-reduce -- no map column is gathered
     dp_aware = True
@@ -455,10 +455,18 @@ class MapVectorizer(VectorizerMixin, SequenceEstimator):
                     cnt[(coo.keys[k], TU.clean_string(v) if p["clean_text"] else v)] += m
                 counters.append(cnt)
             merged = dp.merge_counters(counters)
+            pct = float(p.get("max_pct_cardinality", 1.0))
+            n_rows = dp.count(len(cols[0]) if cols else 0) if pct < 1.0 else 0
             for i, keys in enumerate(all_keys):
                 per: Dict[str, Counter] = {}
                 for (k, v), m in merged[i].items():
                     per.setdefault(k, Counter())[v] += m
+                if pct < 1.0 and n_rows > 0 and kind in ("pivot", "set"):
+                    # OpOneHotVectorizer.scala:291-313 filterByMaxCardinality: a key whose distinct-value count
+                    # reaches pct of the rows loses all its values before the fit, so it never becomes a key
+                    # (distinct counts are exact here, the reference estimates them with an HLL)
+                    keys = [k for k in keys if len(per.get(k, ())) / n_rows < pct]
+                    all_keys[i] = keys
                 for k in keys:
                     cnt = per.get(k, Counter())
                     method = "pivot"
@@ -496,25 +504,58 @@ _MAP_ARGS = {"default_value": "fill_value", "fill_value": "fill_value", "fill_wi
              "track_nulls": "track_nulls", "top_k": "top_k", "min_support": "min_support",
              "white_list_keys": "allow_keys", "allow_keys": "allow_keys", "black_list_keys": "block_keys",
              "block_keys": "block_keys", "reference_date": "reference_date",
-             "max_categorical_cardinality": "max_cardinality", "num_hashes": "num_features"}
+             "max_categorical_cardinality": "max_cardinality", "num_hashes": "num_features",
+             "allow_list_keys": "allow_keys", "block_list_keys": "block_keys",
+             "max_pct_cardinality": "max_pct_cardinality"}
 
 
 def map_vectorize(t, feats, label, D, **overrides) -> list:
     """The Transmogrifier's map vectorizer (Transmogrifier.scala:140-215: fill real maps with the mean and
-    integral maps with the mode, pivot the text-like maps); ``overrides`` take the RichMapFeature.vectorize
-    argument names."""
+    integral maps with the mode, pivot the categorical maps, smart-vectorize the free-text maps);
+    ``overrides`` take the RichMapFeature.vectorize argument names.
+
+    Four map types are converted before their vectorizer, as RichMapFeature does:
+      * ``EmailMap`` -> ``EmailToPickListMapTransformer`` (domains) -> pivot (RichMapFeature.scala:1039-1058)
+      * ``URLMap`` -> ``UrlMapToPickListMapTransformer`` (domains of valid URLs) -> pivot (:1067-1100)
+      * ``PhoneMap`` -> ``IsValidPhoneMapDefaultCountry`` -> ``BinaryMapVectorizer`` (:979-1013)
+      * ``Base64Map`` -> ``MimeTypeMapDetector`` -> ``TextMapPivotVectorizer`` (:121-179)
+    """
     kind = _kind_of(t)
-    if t is T.PhoneMap or t is T.EmailMap or t is T.URLMap or t is T.Base64Map:
+    ov = dict(overrides)
+    region = ov.pop("default_region", D.DefaultRegion)
+    strict = ov.pop("is_strict", False)
+    type_hint = ov.pop("type_hint", None)
+    feats = list(feats)
+    if issubclass(t, T.EmailMap):
+        from .misc_stages import EmailToPickListMapTransformer
+        feats = [EmailToPickListMapTransformer().set_input(f).get_output() for f in feats]
         kind = "pivot"
+    elif issubclass(t, T.URLMap):
+        from .misc_stages import UrlMapToPickListMapTransformer
+        feats = [UrlMapToPickListMapTransformer().set_input(f).get_output() for f in feats]
+        kind = "pivot"
+    elif issubclass(t, T.Base64Map):
+        from .nlp_stages import MimeTypeMapDetector
+        feats = [MimeTypeMapDetector(type_hint=type_hint or "").set_input(f).get_output() for f in feats]
+        kind = "pivot"
+    elif issubclass(t, T.PhoneMap):
+        from .nlp_stages import IsValidPhoneMapDefaultCountry
+        feats = [IsValidPhoneMapDefaultCountry(default_region=region, strict=strict).set_input(f).get_output()
+                 for f in feats]
+        kind = "binary"
     params = dict(kind=kind, clean_keys=D.CleanKeys, clean_text=D.CleanText, track_nulls=D.TrackNulls,
                   top_k=D.TopK, min_support=D.MinSupport, reference_date=D.ReferenceDate,
                   max_cardinality=D.MaxCategoricalCardinality, num_features=D.DefaultNumOfFeatures,
-                  fill_value=float(D.FillValue), fill_with_mean=D.FillWithMean, fill_with_mode=D.FillWithMode)
-    for k, v in overrides.items():
+                  fill_value=float(D.FillValue), fill_with_mean=D.FillWithMean, fill_with_mode=D.FillWithMode,
+                  max_pct_cardinality=float(getattr(D, "MaxPercentCardinality", 1.0)))
+    if kind == "binary":   # RichBinaryMapFeature.vectorize: constant fill only
+        params.update(fill_with_mean=False, fill_with_mode=False)
+    for k, v in ov.items():
         if k not in _MAP_ARGS:
             raise TypeError(f"map vectorize got an unexpected argument {k!r}")
         params[_MAP_ARGS[k]] = v
-    st = MapVectorizer(**params)
+    cls = {"pivot": TextMapPivotVectorizer, "binary": BinaryMapVectorizer}.get(kind, MapVectorizer)
+    st = cls(**params) if kind in ("pivot", "binary") and t is not T.OPMap else MapVectorizer(**params)
     return [st.set_input(feats).get_output()]
 
 

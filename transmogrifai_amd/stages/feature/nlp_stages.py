@@ -523,11 +523,33 @@ class HumanNameDetector(UnaryEstimator):
 
 @register_stage
 class MimeTypeDetector(UnaryTransformer):
+    """Base64 -> MIME type text (``MimeTypeDetector.scala:47-54``; magic-byte table in place of Tika,
+    ``text_stages.detect_mime``). ``type_hint`` / ``max_bytes_to_parse`` as ``MimeTypeDetectorParams``
+    (``:86-103``)."""
     operation_name = "mimeDetect"
-    output_type = T.PickList
+    output_type = T.Text
+    _defaults = {"type_hint": "", "max_bytes_to_parse": 1024}
 
     def transform_fn(self, v):
-        return detect_mime(v)
+        return detect_mime(v, self.params["max_bytes_to_parse"], self.params["type_hint"])
+
+
+@register_stage
+class MimeTypeMapDetector(UnaryTransformer):
+    """Base64Map -> PickListMap of each value's MIME type (``MimeTypeDetector.scala:61-77``): keys whose
+    value is empty or undecodable are dropped, as the reference's ``collect { case (k, Some(v)) }``."""
+    operation_name = "mimeMapDetect"
+    output_type = T.PickListMap
+    _defaults = {"type_hint": "", "max_bytes_to_parse": 1024}
+
+    def transform_fn(self, m):
+        mb, hint = self.params["max_bytes_to_parse"], self.params["type_hint"]
+        out = {}
+        for k, v in (m or {}).items():
+            d = detect_mime(v, mb, hint)
+            if d is not None:
+                out[k] = d
+        return out
 
 
 def parse_phone(s: Optional[str], region: str = "US", strict: bool = False) -> Optional[str]:
@@ -548,10 +570,18 @@ class ParsePhoneNumber(UnaryTransformer):
 
 @register_stage
 class IsValidPhoneMapDefaultCountry(UnaryTransformer):
-    operation_name = "validatePhoneMap"
+    """PhoneMap -> BinaryMap of validity against the default region (``PhoneNumberParser.scala:241-253``):
+    values that cannot be judged (empty / too short) are dropped from the map, as the reference's
+    ``collect { case (k, SomeValue(Some(b))) }``."""
+    operation_name = "validatePhoneMapNoCC"
     output_type = T.BinaryMap
-    _defaults = {"default_region": "US"}
+    _defaults = {"default_region": "US", "strict": False}
 
     def transform_fn(self, m):
-        return {k: bool(is_valid_phone(v, self.params["default_region"])) for k, v in (m or {}).items()
-                if v is not None}
+        region, strict = self.params["default_region"], self.params.get("strict", False)
+        out = {}
+        for k, v in (m or {}).items():
+            b = is_valid_phone(v, region, strict) if v is not None else None
+            if b is not None:
+                out[k] = bool(b)
+        return out

@@ -82,8 +82,11 @@ _MAGIC = [(b"%PDF", "application/pdf"), (b"\x89PNG", "image/png"), (b"\xff\xd8\x
 
 
 @value_fn("MimeTypeDetector")
-def detect_mime(s):
-    """Magic-byte MIME detection of base64 content (Tika replacement; parity unpinned)."""
+def detect_mime(s, max_bytes: int = 1024, type_hint: str = ""):
+    """Magic-byte MIME detection of base64 content (Tika replacement; parity unpinned). Only the first
+    ``max_bytes`` decoded bytes are examined (``BoundedInputStream``, MimeTypeDetector.scala:94); a
+    ``type_hint`` refines the generic answers (``application/octet-stream``, ``text/plain``) the way Tika's
+    detector lets the declared content type specialise its magic match."""
     if s is None:
         return None
     try:
@@ -92,14 +95,20 @@ def detect_mime(s):
         return None
     if not raw:
         return None
+    raw = raw[:max(0, int(max_bytes))] if max_bytes is not None else raw
+    if not raw:
+        return type_hint or "application/octet-stream"
     for sig, mime in _MAGIC:
         if raw[:len(sig)].lower() == sig.lower():
             return mime
     try:
         raw[:512].decode("utf-8")
-        return "text/plain"
+        found = "text/plain"
     except UnicodeDecodeError:
-        return "application/octet-stream"
+        found = "application/octet-stream"
+    if type_hint:   # the generic magic answers are refined by the declared type (Tika's type registry)
+        return type_hint
+    return found
 
 
 def is_valid_phone(s: Optional[str], region: str = "US", strict: bool = False) -> Optional[bool]:
