@@ -191,7 +191,10 @@ def test_max_wait_bounds_a_running_learner():
         name = "_TestSlowNaiveBayes"
 
         def fit_batch(self, X, y, jobs, context=None):
-            time.sleep(3.0)
+            from transmogrifai_amd.utils import cancel
+            for _ in range(30):            # a cooperative fit: checks for cancellation between iterations
+                time.sleep(0.1)
+                cancel.check()
             return super().fit_batch(X, y, jobs, context)
 
     g = torch.Generator().manual_seed(0)
@@ -205,6 +208,34 @@ def test_max_wait_bounds_a_running_learner():
     assert res.best_learner == "OpNaiveBayes"
     assert any("_TestSlowNaiveBayes" in f and "maxWait" in f for f in res.failures)
     import threading
-    for th in threading.enumerate():        # let the abandoned fit end before the interpreter does
-        if th.name.startswith("fit-_TestSlowNaiveBayes"):
-            th.join(10.0)
+    # the timed-out fit was cancelled and joined: nothing of it is left running
+    assert not [th for th in threading.enumerate() if th.name.startswith("fit-_TestSlowNaiveBayes")]
+
+
+def test_max_wait_cancels_boosting_then_other_learners_and_refit_run():
+    """A tree learner cut off by maxWait stops at its next boosting round and is joined; the learners after it
+    (RF on the same tree-grower slots and binning cache) and a refit run normally."""
+    import threading
+    import time
+    from transmogrifai_amd.evaluators.evaluators import OpBinaryClassificationEvaluator
+    from transmogrifai_amd.models.base import FitJob, learner_class
+    from transmogrifai_amd.tuning import validators as V
+    g = torch.Generator().manual_seed(4)
+    X = torch.rand(600, 5, generator=g, dtype=torch.float64)
+    y = ((X[:, 0] + 0.3 * X[:, 1]) > 0.6).double()
+    cv = V.OpCrossValidation(num_folds=2, evaluator=OpBinaryClassificationEvaluator(), seed=2, max_wait=2.0)
+    t0 = time.time()
+    # (maxWait is one deadline for the whole search: the learner after the timed-out one would not start)
+    res = cv.validate([("OpRandomForestClassifier", [{"num_trees": 5, "max_depth": 3}]),
+                       ("OpXGBoostClassifier", [{"num_round": 1_000_000, "max_depth": 3, "eta": 0.01}])],
+                      X, y, torch.arange(600))
+    assert time.time() - t0 < 30
+    assert any("OpXGBoostClassifier" in f and "maxWait" in f for f in res.failures)
+    assert res.best_learner == "OpRandomForestClassifier"
+    assert not [th for th in threading.enumerate() if th.name.startswith("fit-OpXGBoost")]
+    # refits on the same native slots afterwards: RF and a (short) XGBoost
+    for name, p in (("OpRandomForestClassifier", dict(num_trees=5, max_depth=3)),
+                    ("OpXGBoostClassifier", dict(num_round=5, max_depth=3))):
+        L = learner_class(name)()
+        st = L.fit_batch(X, y, [FitJob(dict(L.defaults, **p), None)])
+        assert st[0]["forest"]["nodes"].shape[0] > 1

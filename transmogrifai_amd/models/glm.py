@@ -114,7 +114,9 @@ class GeneralizedLinearRegressionLearner(Learner):
         mu = _init_mu(fam, yd)[:, None].expand(N, P).clone()
         beta = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)
         it = 0
+        from ..utils.cancel import check as _cancel_check
         for it in range(1, max_iter + 1):
+            _cancel_check()
             eta = g(mu)
             gp = gprime(mu)
             z = eta + (yd[:, None] - mu) * gp

@@ -336,7 +336,9 @@ def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max
     fused_dir = LK.owlqn_direction_supported(U, m) and os.environ.get("TMOG_OWLQN_FUSED", "1") != "0"
     if fused_dir:
         l1 = l1.to(U.dtype).contiguous()
+    from ..utils.cancel import check as _cancel_check
     for it in range(int(max_iter.max().item()) if P else 0):
+        _cancel_check()             # maxWait (tuning/validators.py _fit_eval_bounded)
         done |= iters >= max_iter
         if bool(done.all()):
             break

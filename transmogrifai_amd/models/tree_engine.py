@@ -317,6 +317,66 @@ class _GrowArgs(C.Structure):
                 ("XbT", C.c_void_p), ("gh", C.c_void_p), ("gh_alt", C.c_void_p), ("n_entries", C.c_int64)]
 
 
+class _ResidentIO(C.Structure):
+    """Mirror of ``ResidentIO`` (ops/csrc/hip/tree_resident.hip)."""
+    _fields_ = [("rec", C.c_void_p), ("gid_value", C.c_void_p), ("gid_tree", C.c_void_p), ("cap_nodes", C.c_int64),
+                ("job_eta", C.c_void_p), ("job_gamma", C.c_void_p)]
+
+
+REC_FIXED = 7     # record words before the S totals: tree feat bin dl gain left right (tree_resident.hip)
+
+
+@dataclass
+class ResidentTree:
+    """One device-planned ``grow_forest`` call (``resident=True``): the leaf assignment for the boosting
+    epilogue is ready on the device, the created-node records ``rec`` (``[1 + cap, 7 + S]`` int64, row 0 =
+    (nodes, leaf entries, error bits)) are read back later, in bulk, by :func:`resident_forests`."""
+    leaf_assign: "LeafAssign"
+    rec: torch.Tensor
+    jobs: list
+    mode: int
+    kind: int
+    S: int
+    missing_bin: int
+
+
+def resident_forests(trees: Sequence[ResidentTree]) -> List[Forest]:
+    """Host Forests of device-planned trees: ONE device->host copy of all their records, then the native
+    finalisation (``tmog_tree_finalize_cpu``, the host twin of the device's ``tree_finalize_kernel``)."""
+    if not trees:
+        return []
+    recs = [t.rec for t in trees]
+    host = torch.cat([r.reshape(-1) for r in recs]).cpu().numpy() if len(recs) > 1 else recs[0].reshape(-1).cpu().numpy()
+    out, off = [], 0
+    for t in trees:
+        W = REC_FIXED + t.S
+        sz = int(t.rec.numel())
+        blk = host[off:off + sz].reshape(-1, W)
+        off += sz
+        n, err = int(blk[0, 0]), int(blk[0, 2])
+        if err:
+            raise RuntimeError(f"device-planned tree growth failed (error bits {err}: 1 = partition cursor mismatch, "
+                               f"2 = work-list capacity)")
+        r = blk[1:1 + n]
+        G = _Nodes(n, t.S)
+        G.tree[:] = r[:, 0]
+        G.feat[:] = r[:, 1]
+        G.bin[:] = r[:, 2]
+        G.dl[:] = r[:, 3].astype(np.uint8)
+        G.gain[:] = r[:, 4].view(np.float64)
+        G.left[:] = r[:, 5]
+        G.right[:] = r[:, 6]
+        G.tot[:] = np.ascontiguousarray(r[:, REC_FIXED:REC_FIXED + t.S]).view(np.float64)
+        K = 1
+        out.append(_finalize(t.jobs, G, t.mode, t.kind, K, t.S, t.missing_bin))
+    return out
+
+
+def resident_enabled() -> bool:
+    """Device-planned level loop for boosting (``TMOG_TREE_RESIDENT``, default on)."""
+    return os.environ.get("TMOG_TREE_RESIDENT", "1") != "0"
+
+
 _ENTRY_MODELS: Dict[tuple, torch.Tensor] = {}
 
 
@@ -443,7 +503,8 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 subtract: bool = True, chunk_rows: int = 4096, rng_seed: int = 0,
                 collect_leaves: bool = False, groups: Optional[int] = None, csr=None, root=None,
                 fp: Optional[FpPlan] = None, slot_base: int = 0, XbT: Optional[torch.Tensor] = None,
-                quant_amax: Optional[torch.Tensor] = None, quant_wmax: Optional[float] = None) -> Forest:
+                quant_amax: Optional[torch.Tensor] = None, quant_wmax: Optional[float] = None,
+                resident: bool = False):
     """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``.
 
     The level loop runs natively (``ops/csrc/common/tree_grow.hpp``): on the GPU every job group gets
@@ -470,7 +531,12 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     ``fp``: feature-parallel growth (``fp_plan``): every rank calls with the same jobs, rows and ``Xb``;
     each builds histograms of its feature slice only (``csr`` must then be the slice's, from
     ``onebin_csr(..., cols=fp.one_cols)``) and all ranks return the same forest -- the one a single
-    rank would grow. Jobs must not use per-node feature subsets."""
+    rank would grow. Jobs must not use per-node feature subsets.
+
+    ``resident``: on the GPU, for one job group (``groups=1``), no per-node feature subsets and leaves
+    collected, grow with the device-planned level loop (``ops/csrc/hip/tree_resident.hip``): nothing is
+    read back, and a :class:`ResidentTree` is returned instead of a Forest (same trees; the host Forest is
+    built later by :func:`resident_forests`). Other configurations fall back to the host-planned loop."""
     dev = Xb.device
     on_gpu = dev.type == "cuda"
     slot_base = int(slot_base) + slot_lane()
@@ -556,6 +622,10 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                   N.ptr(XbT) if (on_gpu and XbT is not None) else None,
                   N.ptr(gh) if gh is not None else None, N.ptr(gh_alt) if gh_alt is not None else None, total)
     lib = N.hip() if on_gpu else N.host()
+    if resident and on_gpu and ng == 1 and collect_leaves:
+        rt = _grow_resident(lib, a, jobs, mode, kind, S, missing_bin, leaf_rows, leaf_gid, dev, total)
+        if rt is not None:
+            return rt
     fn = (lambda name: getattr(lib, f"tmog_hip_{name}")) if on_gpu else (lambda name: getattr(lib, f"tmog_{name}_cpu"))
     h = fn("grow_forest")(C.byref(a))
     try:
@@ -593,6 +663,27 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                                             torch.cat([x[1] + int(o) for x, o in zip(las, goff)]),
                                             torch.cat([x[2] for x in las]), torch.cat([x[3] for x in las]))
     return forest
+
+
+def _grow_resident(lib, a, jobs, mode, kind, S, missing_bin, leaf_rows, leaf_gid, dev, total) -> Optional[ResidentTree]:
+    cap = int(lib.tmog_hip_resident_cap_nodes(C.byref(a)))
+    if cap <= 0:
+        return None
+    rec = torch.empty(1 + cap, REC_FIXED + S, dtype=torch.int64, device=dev)
+    gid_value = torch.empty(cap, dtype=torch.float32, device=dev)
+    gid_tree = torch.empty(cap, dtype=torch.int64, device=dev)
+    eta = np.ascontiguousarray([j.params.eta for j in jobs], np.float64)
+    gam = np.ascontiguousarray([j.params.gamma for j in jobs], np.float64)
+    io = _ResidentIO(N.ptr(rec), N.ptr(gid_value), N.ptr(gid_tree), cap, eta.ctypes.data, gam.ctypes.data)
+    rc = int(lib.tmog_hip_grow_resident(C.byref(a), C.byref(io)))
+    if rc == 1:
+        return None
+    if rc != 0:
+        msg = C.create_string_buffer(512)
+        lib.tmog_hip_resident_error(msg, 512)
+        raise RuntimeError(f"device-planned tree growth failed: {msg.value.decode(errors='replace')}")
+    la = LeafAssign(leaf_rows[:total], leaf_gid[:total], gid_value, gid_tree)
+    return ResidentTree(la, rec, list(jobs), mode, kind, S, missing_bin)
 
 
 @dataclass

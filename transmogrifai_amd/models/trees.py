@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from . import tree_engine as TE
+from ..utils import cancel
 from .base import FitJob, Learner, OpPredictor, probability_outputs, register_learner, union_rows
 from .binning import BinSpec, find_splits, quantize
 from ..stages.base import register_stage
@@ -217,6 +218,7 @@ class _ForestLearner(Learner):
             groups.setdefault(int(j.params.get("max_bins", 32)), []).append(i)
         K = self._num_classes(y) if self.classification else 1
         for mb, idxs in groups.items():
+            cancel.check()
             spec, Xb = ctx.binned(mb)
             yg = y
             jrows = {i: _rows(jobs[i], N, dev) for i in idxs}
@@ -558,6 +560,7 @@ class GBTClassifierLearner(_BoostLearner):
         yy = y.to(torch.float64)
         forests, weights = [[] for _ in range(P)], [[] for _ in range(P)]
         for it in range(max(iters)):
+            cancel.check()
             act = [p for p in range(P) if it < iters[p]]
             t1 = torch.stack([self._target(yy, Fm[p], it == 0) for p in range(P)]).to(torch.float32)
             tjobs = []
@@ -621,12 +624,13 @@ def _run_parts(dev, parts, fn):
         s.wait_stream(cur)
     errs = []
     lane = TE.slot_lane()           # the caller's native slot lane (concurrent learners) carries over
+    token = cancel.current()        # and its maxWait cancellation token
 
     def work(k):
         try:
             torch.cuda.set_device(dev)
             TE.set_slot_lane(lane)
-            with torch.cuda.stream(streams[k]):
+            with cancel.scope(token), torch.cuda.stream(streams[k]):
                 fn(*parts[k])
         except BaseException as e:          # noqa: BLE001  (re-raised on the caller's thread)
             errs.append(e)
@@ -634,16 +638,12 @@ def _run_parts(dev, parts, fn):
     th = [threading.Thread(target=work, args=(k,), daemon=True) for k in range(len(parts))]
     # a thread returning from a native call must win the GIL back from the one running Python: the
     # default 5 ms switch interval would stall it for up to a whole boosting round
-    import sys
-    swi = sys.getswitchinterval()
-    sys.setswitchinterval(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5")))
-    try:
+    from ..utils.threads import fast_switch
+    with fast_switch(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))):
         for t in th:
             t.start()
         for t in th:
             t.join()
-    finally:
-        sys.setswitchinterval(swi)
     for s in streams:
         cur.wait_stream(s)
     if errs:
@@ -750,6 +750,13 @@ class XGBoostClassifierLearner(_BoostLearner):
                 comp[p, 1] = torch.where(out, H[p].abs(), torch.zeros_like(H[p])).amax()
             tam = torch.zeros(64, P, 2, dtype=torch.int32, device=dev)     # boost_kernels.hip kAmaxCopies
 
+        # Device-planned trees (models/tree_engine.py resident=True, ops/csrc/hip/tree_resident.hip): on the fused
+        # GPU path a round is enqueued without any host synchronisation -- the level plans, the tree finalisation
+        # and the epilogue all run on the device; the host Forests are built from the node records once, after
+        # the last round, and the early-stopping AuPR is read ES_LAG rounds late.
+        resident = fused and par is None and TE.resident_enabled()
+        es_lag = max(1, int(os.environ.get("TMOG_ES_LAG", "2"))) if resident else 1
+
         def run(ps, slot_base=0, groups=None):
             """Boosting rounds of the jobs ``ps`` (their trees do not depend on which other jobs grow
             alongside: no per-node randomness, per-model quantisation, weights all 1 on this path)."""
@@ -758,6 +765,7 @@ class XGBoostClassifierLearner(_BoostLearner):
             prof = _XGB_PROF.setdefault(slot_base, {}) if _XGB_PROF is not None else None
             tick = time.perf_counter
             pending: list = []
+            deferred: list = []        # (act, ResidentTree) per device-planned round, in round order
 
             def resolve(it0, need0, vals_t):
                 for p, v in zip(need0, vals_t.tolist()):
@@ -769,6 +777,7 @@ class XGBoostClassifierLearner(_BoostLearner):
                         stopped[p] = True
 
             for it in range(max([rounds[p] for p in ps], default=0)):
+                cancel.check()
                 act = [p for p in ps if it < rounds[p] and not stopped[p]]
                 if not act:
                     break
@@ -806,9 +815,11 @@ class XGBoostClassifierLearner(_BoostLearner):
                 forest = TE.grow_forest(Xg, n_bins_g, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
                                         missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root, fp=fp,
                                         slot_base=slot_base, groups=groups, XbT=XgT,
-                                        quant_amax=amax_cur, quant_wmax=1.0 if amax_cur is not None else None)
+                                        quant_amax=amax_cur, quant_wmax=1.0 if amax_cur is not None else None,
+                                        resident=resident and groups in (None, 1))
                 t_2 = tick()
-                if colperm is not None:
+                is_res = isinstance(forest, TE.ResidentTree)
+                if colperm is not None and not is_res:
                     internal = forest.nodes[:, 2] >= 0
                     forest.nodes[internal, 0] = colperm[forest.nodes[internal, 0]]
                 need = [p for p in act if esr[p] > 0]
@@ -825,9 +836,15 @@ class XGBoostClassifierLearner(_BoostLearner):
                             comp.index_select(0, ai), tam.index_select(1, ai).view(torch.float32).amax(0)))
                 else:
                     _add_tree_margins(Fm, forest, Xb, act, [1.0] * len(act), tjobs)
-                for k, p in enumerate(act):
-                    forests[p].append(forest.tree(k))
-                    weights[p].append(1.0)
+                if is_res:
+                    deferred.append((list(act), forest))
+                    for p in act:
+                        forests[p].append(None)          # filled from the device records after the last round
+                        weights[p].append(1.0)
+                else:
+                    for k, p in enumerate(act):
+                        forests[p].append(forest.tree(k))
+                        weights[p].append(1.0)
                 t_3 = tick()
                 # early stopping on the training metric (the reference sets no eval set). The AuPR of round it
                 # is read back after round it + 1 has been grown, so the host never waits for a round's
@@ -835,20 +852,33 @@ class XGBoostClassifierLearner(_BoostLearner):
                 # trim (best_round + 1 trees) drops -- the same models as checking every round in step.
                 if need and self.classification:
                     if auc_counts is not None:
-                        vals_t = binned_aupr_from_counts(auc_counts[need])
+                        sel = auc_counts if len(need) == P else \
+                            auc_counts.index_select(0, TE._const_tensor(np.asarray(need, np.int64), dev))
+                        vals_t = binned_aupr_from_counts(sel)
                     else:
                         vals_t = binned_aupr_multi([torch.sigmoid(Fm[p][rows[p]]) for p in need],
                                                    [ylab[p] for p in need])
-                    if pending:
-                        resolve(*pending.pop())
+                    while len(pending) >= es_lag:
+                        resolve(*pending.pop(0))
                     pending.append((it, need, vals_t))
                 if prof is not None:
                     t_4 = tick()
                     for k_, v_ in (("pre", t_1 - t_0), ("grow", t_2 - t_1), ("post", t_3 - t_2), ("es", t_4 - t_3)):
                         prof[k_] = prof.get(k_, 0.0) + v_
                     prof["rounds"] = prof.get("rounds", 0) + 1
-            if pending:
-                resolve(*pending.pop())
+            while pending:
+                resolve(*pending.pop(0))
+            if deferred:
+                fs = TE.resident_forests([rt for _, rt in deferred])
+                cursor = {p: 0 for p in ps}
+                for (act_r, _), f in zip(deferred, fs):
+                    if colperm is not None:
+                        internal = f.nodes[:, 2] >= 0
+                        f.nodes[internal, 0] = colperm[f.nodes[internal, 0]]
+                    for k, p in enumerate(act_r):
+                        while forests[p][cursor[p]] is not None:
+                            cursor[p] += 1
+                        forests[p][cursor[p]] = f.tree(k)
 
         # Pipelined job parts (GPU, fused path): the jobs are split in two halves, each boosted by its
         # own host thread on its own stream, so one half's per-round host work (tree finalisation,

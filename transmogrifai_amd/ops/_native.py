@@ -62,24 +62,27 @@ _HOST_SIGS = {
 
 _HIP_SIGS = {
     "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P, P, I32, I32, I32, P,
-                            P],
+                            P, P],
     "tmog_hip_hist_stat_chunk": [I32, I32],
     "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
     "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P, I32, P,
-                            I64, I32, I32, I32, P, P],
+                            I64, I32, I32, I32, P, P, P],
     "tmog_hip_fp_merge": [P, I32, I32, I64, I32, P, P, P, P, P, P],
     "tmog_hip_rccl_unique_id": [P, I32],
     "tmog_hip_rccl_comm_init": [P, I32, I32],
     "tmog_hip_rccl_comm_destroy": [P],
-    "tmog_hip_partition_fused": [P, I32, P, P, P, I32, P, P, P, P, P, P, P, I32, P, P, I64, P, P, P],
-    "tmog_hip_leaf_collect": [P, P, I32, P, P, P],
+    "tmog_hip_partition_fused": [P, I32, P, P, P, I32, P, P, P, P, P, P, P, I32, P, P, I64, P, P, P, P],
+    "tmog_hip_leaf_collect": [P, P, I32, P, P, P, P, P],
     "tmog_hip_grow_forest": [P],
+    "tmog_hip_grow_resident": [P, P],
+    "tmog_hip_resident_cap_nodes": [P],
+    "tmog_hip_resident_error": [P, I32],
     "tmog_hip_grow_status": [P, P, I32],
     "tmog_hip_grow_nodes": [P, I32],
     "tmog_hip_grow_leaf_count": [P, I32],
     "tmog_hip_grow_copy": [P, I32, P, P, P, P, P, P, P, P],
     "tmog_hip_grow_free": [P],
-    "tmog_hip_zero_segments": [P, P, P, I32, I64, P],
+    "tmog_hip_zero_segments": [P, P, P, I32, I64, I64, I32, I32, P, I32, P],
     "tmog_hip_grow_timing": [P, I32],
     "tmog_hip_boost_epilogue": [P, P, I64, P, P, P, I64, P, P, P, P, I32, P, I32, I64, I64, I64, P, P],
     "tmog_hip_aupr_counts": [P, I32, I32, P, P],
@@ -126,7 +129,7 @@ _RESTYPES = {"tmog_tok_run": C.c_void_p, "tmog_tok_sizes": None, "tmog_tok_copy"
              "tmog_grow_nodes_cpu": C.c_int64, "tmog_hip_grow_nodes": C.c_int64,
              "tmog_grow_leaf_count_cpu": C.c_int64, "tmog_hip_grow_leaf_count": C.c_int64,
              "tmog_grow_copy_cpu": None, "tmog_hip_grow_copy": None,
-             "tmog_grow_free_cpu": None, "tmog_hip_grow_free": None}
+             "tmog_grow_free_cpu": None, "tmog_hip_grow_free": None, "tmog_hip_resident_cap_nodes": C.c_int64}
 
 
 def _declare(lib, sigs):

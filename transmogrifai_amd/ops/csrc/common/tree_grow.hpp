@@ -319,6 +319,84 @@ inline GrowTiming& grow_timing() {
   return t;
 }
 
+// Histogram feature groups of a job group without per-node feature subsets (or the per-node default),
+// shared by the host-planned level loop (grow_group) and the device-planned one (hip/tree_resident.hip).
+struct GroupLayout {
+  std::vector<FeatGroup> full_groups;
+  std::vector<int32_t> perm_feats;
+  int split_n_multi = -1;   // GPU split scan: local features [n_multi, F) have one present bin
+  int64_t live_dense = -1;  // GPU zero / subtract: words past this prefix are live only at bin 0
+  int fp_nml = 0, fp_obase = 0;   // split records: local feature -> position in the full feature list
+  int F_use = 0;
+};
+
+template <bool GPU>
+GroupLayout group_layout(const GrowArgs& a, bool use_subset, bool fp) {
+  // Feature groups of the histogram kernel (<= 64 features each). Without per-node subsets the
+  // grouping is fixed: with a sparse missing bin (GPU, MODE 2) the one-present-bin columns (one-hot /
+  // null indicators) go last; given their row-wise CSR they form one group whose items walk only the
+  // present entries of each row (a few per row instead of one byte per column), otherwise groups of
+  // their own that the kernel accumulates in registers.
+  // The feature order is the same on both backends (stable: multi-bin columns first, then the
+  // one-present-bin columns), so split tie-breaks by local feature index stay identical GPU vs CPU.
+  GroupLayout L;
+  std::vector<FeatGroup>& full_groups = L.full_groups;
+  std::vector<int32_t>& perm_feats = L.perm_feats;
+  int& split_n_multi = L.split_n_multi;
+  int64_t& live_dense = L.live_dense;
+  int& fp_nml = L.fp_nml;
+  int& fp_obase = L.fp_obase;
+  const int F = a.F, B = a.B, S = a.S;
+  if (!use_subset && a.mode == 2 && a.missing_bin >= 0 && a.n_bins_host != nullptr) {
+    std::vector<int32_t> multi, one;
+    for (int f = 0; f < F; ++f) (a.n_bins_host[f] != 1 ? multi : one).push_back(f);
+    int m0 = 0, m1 = (int)multi.size(), o0 = 0, o1 = (int)one.size();
+    if (fp) {
+      m0 = a.fp_mlo; m1 = a.fp_mhi; o0 = a.fp_olo; o1 = a.fp_ohi;
+      if (m0 < 0 || m1 > (int)multi.size() || m1 <= m0 || o0 < 0 || o1 > (int)one.size() || o1 < o0)
+        throw std::runtime_error("bad feature-parallel slice");
+    }
+    perm_feats.assign(multi.begin() + m0, multi.begin() + m1);
+    const int n_multi = m1 - m0;
+    fp_nml = n_multi;
+    fp_obase = (int)multi.size() + o0;
+    // node totals are read from local feature 0, which must be a multi-bin column: with no multi-bin
+    // column at all every histogram word stays written and scanned (no CSR / reduced write-out)
+    split_n_multi = n_multi > 0 ? n_multi : -1;
+    if (GPU && n_multi > 0) live_dense = (int64_t)n_multi * a.B * a.S;
+    perm_feats.insert(perm_feats.end(), one.begin() + o0, one.begin() + o1);
+    const char* wenv = std::getenv("TMOG_HIST_WIDE");
+    // (32-bit buffer offsets row * F + column: matrices below 2 GiB)
+    const bool wide_ok = GPU && a.mode == 2 && S == 2 && F % 4 == 0 && !(wenv && wenv[0] == '0') &&
+                         (int64_t)a.N * F < ((int64_t)1 << 31) - 64;
+    for (FeatGroup g : (wide_ok ? equal_groups4(n_multi) : equal_groups(n_multi))) {
+      if (wide_ok) {
+        bool ok = perm_feats[g.f0] % 4 == 0;
+        for (int i = 1; ok && i < g.nf; ++i) ok = perm_feats[g.f0 + i] == perm_feats[g.f0] + i;
+        g.wide = ok;
+      }
+      full_groups.push_back(g);
+    }
+    const int n_one = o1 - o0;
+    if (GPU && a.csr_ptr && a.csr_col && n_multi > 0 && n_one > 0 && a.csr_nf == n_one &&
+        2 * n_one + 4 + 64 * 4 <= 64 * (B * S + 1))   // sums + list lengths of the CSR item (tree_kernels.hip)
+      full_groups.push_back(FeatGroup{n_multi, n_one, false, true});   // one item walks the rows' CSR lists
+    else
+      for (const FeatGroup& g : equal_groups(n_one))
+        full_groups.push_back(FeatGroup{n_multi + g.f0, g.nf, GPU, false});
+  } else if (fp) {
+    if (a.fp_mlo < 0 || a.fp_mhi > F || a.fp_mhi <= a.fp_mlo) throw std::runtime_error("bad feature-parallel slice");
+    for (int f = a.fp_mlo; f < a.fp_mhi; ++f) perm_feats.push_back(f);
+    fp_nml = (int)perm_feats.size();
+    fp_obase = F;
+    full_groups = equal_groups(fp_nml);
+  } else {
+    full_groups = equal_groups(F);
+  }
+  L.F_use = perm_feats.empty() ? F : (int)perm_feats.size();
+  return L;
+}
+
 template <class BK>
 void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns = nullptr) {
   const int j0 = a.group_start[g], j1 = a.group_start[g + 1];
@@ -386,66 +464,14 @@ void grow_group(BK& bk, const GrowArgs& a, int g, GroupResult& R, FpTurns* turns
     bk.leaf_collect(rows, d + o, (int)items.size(), leaf_rows, leaf_gid);
   };
 
-  // Feature groups of the histogram kernel (<= 64 features each). Without per-node subsets the
-  // grouping is fixed: with a sparse missing bin (GPU, MODE 2) the one-present-bin columns (one-hot /
-  // null indicators) go last; given their row-wise CSR they form one group whose items walk only the
-  // present entries of each row (a few per row instead of one byte per column), otherwise groups of
-  // their own that the kernel accumulates in registers.
-  // The feature order is the same on both backends (stable: multi-bin columns first, then the
-  // one-present-bin columns), so split tie-breaks by local feature index stay identical GPU vs CPU.
-  std::vector<FeatGroup> full_groups;
-  std::vector<int32_t> perm_feats;
-  int split_n_multi = -1;   // GPU split scan: local features [n_multi, F) have one present bin
-  int64_t live_dense = -1;  // GPU zero / subtract: words past this prefix are live only at bin 0
   const bool fp = a.fp_world > 0;   // 1 rank is allowed (tests run the exchange path on one GPU)
   if (fp && use_subset) throw std::runtime_error("feature-parallel growth needs jobs without feature subsets");
-  int fp_nml = 0, fp_obase = 0;   // split records: local feature -> position in the full feature list
-  if (!use_subset && a.mode == 2 && a.missing_bin >= 0 && a.n_bins_host != nullptr) {
-    std::vector<int32_t> multi, one;
-    for (int f = 0; f < F; ++f) (a.n_bins_host[f] != 1 ? multi : one).push_back(f);
-    int m0 = 0, m1 = (int)multi.size(), o0 = 0, o1 = (int)one.size();
-    if (fp) {
-      m0 = a.fp_mlo; m1 = a.fp_mhi; o0 = a.fp_olo; o1 = a.fp_ohi;
-      if (m0 < 0 || m1 > (int)multi.size() || m1 <= m0 || o0 < 0 || o1 > (int)one.size() || o1 < o0)
-        throw std::runtime_error("bad feature-parallel slice");
-    }
-    perm_feats.assign(multi.begin() + m0, multi.begin() + m1);
-    const int n_multi = m1 - m0;
-    fp_nml = n_multi;
-    fp_obase = (int)multi.size() + o0;
-    // node totals are read from local feature 0, which must be a multi-bin column: with no multi-bin
-    // column at all every histogram word stays written and scanned (no CSR / reduced write-out)
-    split_n_multi = n_multi > 0 ? n_multi : -1;
-    if (BK::kGPU && n_multi > 0) live_dense = (int64_t)n_multi * a.B * a.S;
-    perm_feats.insert(perm_feats.end(), one.begin() + o0, one.begin() + o1);
-    const char* wenv = std::getenv("TMOG_HIST_WIDE");
-    // (32-bit buffer offsets row * F + column: matrices below 2 GiB)
-    const bool wide_ok = BK::kGPU && a.mode == 2 && S == 2 && F % 4 == 0 && !(wenv && wenv[0] == '0') &&
-                         (int64_t)a.N * F < ((int64_t)1 << 31) - 64;
-    for (FeatGroup g : (wide_ok ? equal_groups4(n_multi) : equal_groups(n_multi))) {
-      if (wide_ok) {
-        bool ok = perm_feats[g.f0] % 4 == 0;
-        for (int i = 1; ok && i < g.nf; ++i) ok = perm_feats[g.f0 + i] == perm_feats[g.f0] + i;
-        g.wide = ok;
-      }
-      full_groups.push_back(g);
-    }
-    const int n_one = o1 - o0;
-    if (BK::kGPU && a.csr_ptr && a.csr_col && n_multi > 0 && n_one > 0 && a.csr_nf == n_one &&
-        2 * n_one + 4 + 64 * 4 <= 64 * (B * S + 1))   // sums + list lengths of the CSR item (tree_kernels.hip)
-      full_groups.push_back(FeatGroup{n_multi, n_one, false, true});   // one item walks the rows' CSR lists
-    else
-      for (const FeatGroup& g : equal_groups(n_one))
-        full_groups.push_back(FeatGroup{n_multi + g.f0, g.nf, BK::kGPU, false});
-  } else if (fp) {
-    if (a.fp_mlo < 0 || a.fp_mhi > F || a.fp_mhi <= a.fp_mlo) throw std::runtime_error("bad feature-parallel slice");
-    for (int f = a.fp_mlo; f < a.fp_mhi; ++f) perm_feats.push_back(f);
-    fp_nml = (int)perm_feats.size();
-    fp_obase = F;
-    full_groups = equal_groups(fp_nml);
-  } else {
-    full_groups = equal_groups(F);
-  }
+  GroupLayout L = group_layout<BK::kGPU>(a, use_subset, fp);
+  std::vector<FeatGroup>& full_groups = L.full_groups;
+  std::vector<int32_t>& perm_feats = L.perm_feats;
+  const int split_n_multi = L.split_n_multi;
+  const int64_t live_dense = L.live_dense;
+  const int fp_nml = L.fp_nml, fp_obase = L.fp_obase;
   const int F_use = perm_feats.empty() ? F : (int)perm_feats.size();
   const bool trace = std::getenv("TMOG_GROW_TRACE") != nullptr;   // progress to stderr (debugging)
   if (trace)

@@ -24,7 +24,7 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
-                        hipStream_t stream, const int32_t* gh);
+                        hipStream_t stream, const int32_t* gh, const int* dcount);
 int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
                            const int64_t* out_off, const int64_t* size, int n, int64_t max_size, int64_t dense,
                            int per, int S, hipStream_t stream);
@@ -34,16 +34,17 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
                         float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors, int n_multi,
                         void* rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase, hipStream_t stream,
-                        unsigned* done);
+                        unsigned* done, const int* dm);
 int tmog_hip_fp_merge(const void* recv, int R, int m, int64_t rec_bytes, int S, int32_t* out_feat, int32_t* out_bin,
                       float* out_gain, uint8_t* out_dl, float* out_left, hipStream_t stream);
 int tmog_hip_pair_scan(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int32_t* small_j,
                        const int32_t* big_j, int n_pairs, const int64_t* node_hist_off, const int32_t* node_nfeat,
                        const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B, int S,
                        int kind, const float* node_params, int missing_bin, const int32_t* node_model,
-                       const double* qinv, int max_nfeat, void* cand_ws, int n_multi, hipStream_t stream);
+                       const double* qinv, int max_nfeat, void* cand_ws, int n_multi, hipStream_t stream,
+                       const int* dnp);
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
-                           int64_t dense, int per, int S, hipStream_t stream, int n_dense);
+                           int64_t dense, int per, int S, hipStream_t stream, int n_dense, const int* dn);
 size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat, int B, int S);
 int tmog_hip_tree_prime();
 int tmog_hip_hist_stat_chunk(int B, int S);
@@ -51,9 +52,9 @@ int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, 
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                              const int32_t* split_bin, const uint8_t* dl, const float* node_params,
                              const float* split_gain, int missing_bin, int64_t* cursors, const uint8_t* XbT, int64_t N,
-                             hipStream_t stream, const int32_t* gh_in, int32_t* gh_out);
+                             hipStream_t stream, const int32_t* gh_in, int32_t* gh_out, const int* dcount);
 int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
-                          int32_t* out_gid, hipStream_t stream);
+                          int32_t* out_gid, hipStream_t stream, const uint32_t* rows_alt, const int* dcount);
 }
 
 namespace {
@@ -169,7 +170,7 @@ struct GpuBackend {
   }
   void zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t mx, int64_t dense, int per,
                      int S, int n_dense) {
-    kchk(tmog_hip_zero_segments(hist, off, size, n, mx, dense, per, S, sl.stream, n_dense), "zero_segments");
+    kchk(tmog_hip_zero_segments(hist, off, size, n, mx, dense, per, S, sl.stream, n_dense, nullptr), "zero_segments");
   }
   // staged statistics of the entry buffer position ``p`` points into (rows or rows_alt), or null
   int32_t* gh_of(const uint32_t* p) const {
@@ -185,7 +186,7 @@ struct GpuBackend {
     if (n_items)
       kchk(tmog_hip_hist_build(g.Xb, g.F, rows, items, n_items, nfo, flist, nmd, nho, hist, g.B, g.mode, g.S, g.y,
                                g.t1, g.t2, g.stride, g.qscale, g.mode == 2 ? g.missing_bin : -1, g.csr_ptr,
-                               g.csr_col, Sc, n_wide, need_general, sl.stream, gh_of(rows)),
+                               g.csr_col, Sc, n_wide, need_general, sl.stream, gh_of(rows), nullptr),
            "hist_build");
   }
   int stat_chunk(int B, int S) const { return tmog_hip_hist_stat_chunk(B, S); }
@@ -198,7 +199,7 @@ struct GpuBackend {
                  const int32_t* flist, const float* params, const int32_t* nmd, int max_nf, int m, int n_multi) {
     grow_dev(sl.cand, sl.cand_cap, tmog_hip_split_cand_bytes(m, max_nf, g.B, g.S), sl.stream);
     kchk(tmog_hip_pair_scan(hist, prev, poff, sj, bj, n_pairs, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params,
-                            g.missing_bin, nmd, g.qinv, max_nf, sl.cand, n_multi, sl.stream),
+                            g.missing_bin, nmd, g.qinv, max_nf, sl.cand, n_multi, sl.stream, nullptr),
          "pair_scan");
   }
   void split_find(const tmog::GrowArgs& g, const int64_t* hist, int m, const int64_t* nho, const int32_t* nnf,
@@ -216,7 +217,8 @@ struct GpuBackend {
     }
     kchk(tmog_hip_split_find(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd,
                              g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, cursors, n_multi, fps.rec,
-                             fps.rec_bytes, fps.mlo, fps.nml, fps.obase, sl.stream, fused_reduce ? sl.done : nullptr),
+                             fps.rec_bytes, fps.mlo, fps.nml, fps.obase, sl.stream, fused_reduce ? sl.done : nullptr,
+                             nullptr),
          "split_find");
   }
   // RCCL send / receive buffers come from plain hipMalloc (grow-only; never from the stream-ordered
@@ -259,7 +261,7 @@ struct GpuBackend {
     int32_t* go = gh_of(rows_alt);
     if ((gi == nullptr) != (go == nullptr)) gi = go = nullptr;
     kchk(tmog_hip_partition_fused(g.Xb, g.F, rows, rows_alt, items, n, nb, nc, feat, bin, dl, params, gain,
-                                  g.missing_bin, cursors, g.XbT, g.N, sl.stream, gi, go),
+                                  g.missing_bin, cursors, g.XbT, g.N, sl.stream, gi, go, nullptr),
          "partition_fused");
   }
   void partition_nodes(const tmog::GrowArgs&, const uint32_t*, uint32_t*, int, const int64_t*, const int64_t*,
@@ -267,7 +269,7 @@ struct GpuBackend {
     throw std::logic_error("partition_nodes is the CPU backend's path");
   }
   void leaf_collect(const uint32_t* rows, const void* items, int n, uint32_t* out_rows, int32_t* out_gid) {
-    kchk(tmog_hip_leaf_collect(rows, items, n, out_rows, out_gid, sl.stream), "leaf_collect");
+    kchk(tmog_hip_leaf_collect(rows, items, n, out_rows, out_gid, sl.stream, nullptr, nullptr), "leaf_collect");
   }
   void finish() {}
 };

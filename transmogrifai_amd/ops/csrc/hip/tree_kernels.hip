@@ -515,8 +515,10 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
     int B, int S, const float* __restrict__ y, const float* __restrict__ t1, const float* __restrict__ t2,
     int64_t stride, const float* __restrict__ qscale, int skip_bin, const int64_t* __restrict__ csr_ptr,
-    const uint16_t* __restrict__ csr_col, int Sc, const int2* __restrict__ gh) {
+    const uint16_t* __restrict__ csr_col, int Sc, const int2* __restrict__ gh, const int* __restrict__ dcount) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
+  // dcount (device-planned levels, tree_resident.hip): the grid is an upper bound, the item count is on the device
+  if (dcount != nullptr && (int)blockIdx.x >= *dcount) return;
   const HistItem it = items[blockIdx.x];
   const int s0 = ((it.excl >> 8) & 0xFF) * Sc;   // statistic chunk of this item (excl bits 8..15)
   const int sc = min(Sc, S - s0);
@@ -713,8 +715,12 @@ __global__ void hist_subtract_kernel(int64_t* __restrict__ hist, const int64_t* 
 // single-chunk and derived nodes are fully overwritten, so the level buffer is never memset whole
 __global__ void zero_segments_kernel(int64_t* __restrict__ hist, const int64_t* __restrict__ off,
                                      const int64_t* __restrict__ size, int n, int64_t dense, int per, int S,
-                                     int n_dense) {
+                                     int n_dense, const int* __restrict__ dcnt) {
   const int j = blockIdx.y;
+  if (dcnt != nullptr) {       // device-planned level: [segments, whole-node segments] on the device
+    n = dcnt[0];
+    n_dense = dcnt[1];
+  }
   if (j >= n) return;
   int64_t* o = hist + off[j];
   const int64_t dj = j < n_dense ? dense : 0;      // segments past n_dense start at a one-present-bin region
@@ -1029,10 +1035,12 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
     int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
-    Best* __restrict__ cand, int n_multi, int fpb, unsigned* __restrict__ done, ReduceArgs ra) {
+    Best* __restrict__ cand, int n_multi, int fpb, unsigned* __restrict__ done, ReduceArgs ra,
+    const int* __restrict__ dm) {
   const int cstride = ra.cstride;
   const int j = blockIdx.x / fbmax;
   const int fb = blockIdx.x - j * fbmax;
+  if (dm != nullptr && j >= *dm) return;      // device-planned level: node count on the device
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // params slot 4: the node was scanned with its subtraction partner by pair_scan_kernel (same cand slots, all
   // written by that earlier launch): with the fused reduction its block 0 reduces it, the others have nothing to do
@@ -1146,9 +1154,10 @@ __global__ void __launch_bounds__(256) pair_scan_kernel(
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ feat_nbins, int B, int S, int kind, const float* __restrict__ node_params,
     int missing_bin, const int32_t* __restrict__ node_model, const double* __restrict__ qinv, int fbmax,
-    Best* __restrict__ cand, int n_multi, int fpb, int cstride) {
+    Best* __restrict__ cand, int n_multi, int fpb, int cstride, const int* __restrict__ dnp) {
   const int q = blockIdx.x / fbmax;
   const int fb = blockIdx.x - q * fbmax;
+  if (dnp != nullptr) n_pairs = *dnp;          // device-planned level: pair count on the device
   if (q >= n_pairs) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int js = small_j[q], jb = big_j[q];
@@ -1457,7 +1466,8 @@ __global__ void __launch_bounds__(256) partition_fused_kernel(
     const int32_t* __restrict__ split_feat, const int32_t* __restrict__ split_bin, const uint8_t* __restrict__ dl,
     const float* __restrict__ node_params, const float* __restrict__ split_gain, int missing_bin,
     unsigned long long* __restrict__ cursors, const uint8_t* __restrict__ XbT, int64_t Nt,
-    const int2* __restrict__ gh_in, int2* __restrict__ gh_out) {
+    const int2* __restrict__ gh_in, int2* __restrict__ gh_out, const int* __restrict__ dcount) {
+  if (dcount != nullptr && (int)blockIdx.x >= *dcount) return;
   const PartItem it = items[blockIdx.x];
   const int j = it.node;
   const int f = split_feat[j], sb = split_bin[j];
@@ -1538,16 +1548,20 @@ struct LeafItem {
   int64_t count;
   int64_t out;      // output position
   int32_t gid;      // node id
-  int32_t pad;
+  int32_t buf;      // row buffer: 0 = rows, 1 = rows_alt (device-planned levels collect from both)
 };
 
 __global__ void __launch_bounds__(256) leaf_collect_kernel(const uint32_t* __restrict__ rows,
+                                                           const uint32_t* __restrict__ rows_alt,
                                                            const LeafItem* __restrict__ items,
                                                            uint32_t* __restrict__ out_rows,
-                                                           int32_t* __restrict__ out_gid) {
+                                                           int32_t* __restrict__ out_gid,
+                                                           const int* __restrict__ dcount) {
+  if (dcount != nullptr && (int)blockIdx.x >= *dcount) return;
   const LeafItem it = items[blockIdx.x];
+  const uint32_t* src = (it.buf && rows_alt) ? rows_alt : rows;
   for (int64_t i = threadIdx.x; i < it.count; i += blockDim.x) {
-    out_rows[it.out + i] = rows[it.begin + i];
+    out_rows[it.out + i] = src[it.begin + i];
     out_gid[it.out + i] = it.gid;
   }
 }
@@ -1817,8 +1831,9 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
-                        hipStream_t stream, const int32_t* gh_words) {
+                        hipStream_t stream, const int32_t* gh_words, const int* dcount) {
   if (n_items == 0) return 0;
+  if (dcount != nullptr && n_wide != 0) return -2;   // device-counted launches: one mixed launch
   const int2* gh = reinterpret_cast<const int2*>(gh_words);
   if (gh && mode != 2) return -2;
   if (Sc <= 0 || Sc > S) Sc = S;
@@ -1857,19 +1872,19 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
   if (mode == 0)
     hipLaunchKernelGGL(hist_build_kernel<0>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc,
-                       nullptr);
+                       nullptr, dcount);
   else if (mode == 1)
     hipLaunchKernelGGL(hist_build_kernel<1>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc,
-                       nullptr);
+                       nullptr, dcount);
   else if (need_general)
     hipLaunchKernelGGL(hist_build_kernel<2>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                       csr_col, Sc, gh);
+                       csr_col, Sc, gh, dcount);
   else
     hipLaunchKernelGGL((hist_build_kernel<2, false>), grid, block, lds, stream, Xb, F, rows, it, node_feat_off,
                        feat_list, node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                       csr_col, Sc, gh);
+                       csr_col, Sc, gh, dcount);
   return (int)hipGetLastError();
 }
 
@@ -1897,8 +1912,10 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
                         const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
                         float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors,
                         int n_multi, void* rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase,
-                        hipStream_t stream, unsigned* done) {
+                        hipStream_t stream, unsigned* done, const int* dm) {
   if (n_nodes == 0) return 0;
+  // device-counted launches take the narrow scan with the fused reduction (no separate per-node launch)
+  if (dm != nullptr && (done == nullptr || S > TM_MAX_S || B > 64)) return -2;
   if (n_multi > max_nfeat) n_multi = -1;
   Best* cand = (Best*)cand_ws;   // >= tmog_hip_split_cand_bytes(n_nodes, max_nfeat, B, S) bytes
   const bool wide = S > TM_MAX_S || B > 64;
@@ -1926,7 +1943,7 @@ int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hi
 #define TM_SPLIT(SMV)                                                                                          \
   hipLaunchKernelGGL(split_scan_kernel<SMV>, dim3(n_nodes * fbmax), dim3(256), 0, stream, hist, node_hist_off,  \
                      node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, kind, node_params, missing_bin,    \
-                     node_model, qinv, fbmax, cand, n_multi, fpb, done, ra)
+                     node_model, qinv, fbmax, cand, n_multi, fpb, done, ra, dm)
   if (S <= 2) TM_SPLIT(2);
   else if (S == 3) TM_SPLIT(3);
   else if (S <= 4) TM_SPLIT(4);
@@ -1945,7 +1962,8 @@ int tmog_hip_pair_scan(int64_t* hist, const int64_t* parent, const int64_t* pare
                        const int32_t* big_j, int n_pairs, const int64_t* node_hist_off, const int32_t* node_nfeat,
                        const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B, int S,
                        int kind, const float* node_params, int missing_bin, const int32_t* node_model,
-                       const double* qinv, int max_nfeat, void* cand_ws, int n_multi, hipStream_t stream) {
+                       const double* qinv, int max_nfeat, void* cand_ws, int n_multi, hipStream_t stream,
+                       const int* dnp) {
   if (n_pairs == 0) return 0;
   if (S > TM_MAX_S || B > 64) return -2;
   if (n_multi > max_nfeat) n_multi = -1;
@@ -1956,7 +1974,7 @@ int tmog_hip_pair_scan(int64_t* hist, const int64_t* parent, const int64_t* pare
   hipLaunchKernelGGL(pair_scan_kernel<SMV>, dim3(n_pairs * fbmax), dim3(256), 0, stream, hist, parent, parent_off, \
                      small_j, big_j, n_pairs, node_hist_off, node_nfeat, node_feat_off, feat_list, feat_nbins, B, S, \
                      kind, node_params, missing_bin, node_model, qinv, fbmax, (Best*)cand_ws, n_multi, fpb,    \
-                     cand_stride(fbmax))
+                     cand_stride(fbmax), dnp)
   if (S <= 2) TM_PAIR(2);
   else if (S == 3) TM_PAIR(3);
   else if (S <= 4) TM_PAIR(4);
@@ -1974,14 +1992,14 @@ int tmog_hip_fp_merge(const void* recv, int R, int m, int64_t rec_bytes, int S, 
 }
 
 int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
-                           int64_t dense, int per, int S, hipStream_t stream, int n_dense) {
+                           int64_t dense, int per, int S, hipStream_t stream, int n_dense, const int* dn) {
   if (n == 0) return 0;
   if (max_size >= (int64_t)1 << 31) return -2;
   const int64_t lw = std::max(host_live_words(max_size, dense, per, S), host_live_words(max_size, 0, per, S));
   int gx = (int)min((lw + 255) / 256, (int64_t)1024);
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(zero_segments_kernel, dim3(gx, n), dim3(256), 0, stream, hist, off, size, n, dense, per, S,
-                     n_dense);
+                     n_dense, dn);
   return (int)hipGetLastError();
 }
 
@@ -2013,21 +2031,21 @@ int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, 
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                              const int32_t* split_bin, const uint8_t* dl, const float* node_params,
                              const float* split_gain, int missing_bin, int64_t* cursors, const uint8_t* XbT,
-                             int64_t N, hipStream_t stream, const int32_t* gh_in, int32_t* gh_out) {
+                             int64_t N, hipStream_t stream, const int32_t* gh_in, int32_t* gh_out, const int* dcount) {
   if (n_items == 0) return 0;
   if ((gh_in != nullptr) != (gh_out != nullptr)) return -2;
   hipLaunchKernelGGL(partition_fused_kernel, dim3(n_items), dim3(256), 0, stream, Xb, F, rows_in, rows_out,
                      (const PartItem*)items, node_begin, node_count, split_feat, split_bin, dl, node_params,
                      split_gain, missing_bin, (unsigned long long*)cursors, XbT, N,
-                     reinterpret_cast<const int2*>(gh_in), reinterpret_cast<int2*>(gh_out));
+                     reinterpret_cast<const int2*>(gh_in), reinterpret_cast<int2*>(gh_out), dcount);
   return (int)hipGetLastError();
 }
 
 int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
-                          int32_t* out_gid, hipStream_t stream) {
+                          int32_t* out_gid, hipStream_t stream, const uint32_t* rows_alt, const int* dcount) {
   if (n_items == 0) return 0;
-  hipLaunchKernelGGL(leaf_collect_kernel, dim3(n_items), dim3(256), 0, stream, rows, (const LeafItem*)items,
-                     out_rows, out_gid);
+  hipLaunchKernelGGL(leaf_collect_kernel, dim3(n_items), dim3(256), 0, stream, rows, rows_alt, (const LeafItem*)items,
+                     out_rows, out_gid, dcount);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,1046 @@
+// Device-planned tree growth ("resident" level loop) for one job group on the caller's stream.
+//
+// The host-planned grower (common/tree_grow.hpp grow_group) reads every level's split decisions back to the
+// host, plans the next level there (node bookkeeping, histogram / partition / leaf work items, sibling
+// pairs, zero segments) and ships the plan in one staged copy: one blocking round trip per level and
+// group, 66-170 us of stream idle per level on the XGBoost headline (profiles/r4_levels_base.txt). Here the
+// same plan is computed ON THE DEVICE by one 1024-thread workgroup (level_plan_kernel) between the level
+// kernels, and every level kernel is launched with a host upper bound of its grid and reads the real item
+// count from device memory (tree_kernels.hip `dcount` arguments): the host enqueues a whole tree -- every
+// level, the leaf collection and the tree finalisation (leaf values, gamma pruning; tree_finalize_kernel) --
+// without a single synchronisation, and boosting (models/trees.py) enqueues round after round. The host
+// reads the created-node records once per fit.
+//
+// The device plan reproduces grow_group's decisions exactly (same can / need rules, Newton hessian gate,
+// subtraction pairing, feature groups from group_layout, item chunking), so the trees are bit-identical
+// to the host-planned grower (tests/test_tree_resident_gpu.py); work-item ORDER may differ where it does not
+// matter (integer histogram atomics and exclusive stores are order-independent, partition order inside a
+// child is not stable on either path).
+//
+// Reference behaviour: XGBoost4J's hist updater as wrapped by OpXGBoostClassifier.scala:47-403.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "common/tree_grow.hpp"
+
+extern "C" {
+int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
+                        const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* node_model,
+                        const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
+                        const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
+                        const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
+                        hipStream_t stream, const int32_t* gh, const int* dcount);
+int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
+                        const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
+                        int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
+                        const double* qinv, int max_nfeat, void* cand_ws, int32_t* out_feat, int32_t* out_bin,
+                        float* out_gain, uint8_t* out_dl, float* out_left, float* out_total, int64_t* cursors, int n_multi,
+                        void* rec, int64_t rec_bytes, int fp_mlo, int fp_nml, int fp_obase, hipStream_t stream,
+                        unsigned* done, const int* dm);
+int tmog_hip_pair_scan(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int32_t* small_j,
+                       const int32_t* big_j, int n_pairs, const int64_t* node_hist_off, const int32_t* node_nfeat,
+                       const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B, int S,
+                       int kind, const float* node_params, int missing_bin, const int32_t* node_model,
+                       const double* qinv, int max_nfeat, void* cand_ws, int n_multi, hipStream_t stream,
+                       const int* dnp);
+int tmog_hip_zero_segments(int64_t* hist, const int64_t* off, const int64_t* size, int n, int64_t max_size,
+                           int64_t dense, int per, int S, hipStream_t stream, int n_dense, const int* dn);
+size_t tmog_hip_split_cand_bytes(int n_nodes, int max_nfeat, int B, int S);
+int tmog_hip_tree_prime();
+int tmog_hip_hist_stat_chunk(int B, int S);
+int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, const void* items,
+                             int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
+                             const int32_t* split_bin, const uint8_t* dl, const float* node_params,
+                             const float* split_gain, int missing_bin, int64_t* cursors, const uint8_t* XbT, int64_t N,
+                             hipStream_t stream, const int32_t* gh_in, int32_t* gh_out, const int* dcount);
+int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
+                          int32_t* out_gid, hipStream_t stream, const uint32_t* rows_alt, const int* dcount);
+}
+
+// plan / finalisation arithmetic with the host twins' IEEE operation sequence (no FMA contraction)
+#pragma clang fp contract(off)
+
+namespace {
+
+using tmog::HistItemH;
+using tmog::LeafItemH;
+using tmog::PartItemH;
+
+// device counters of the current level (int32 each)
+enum : int {
+  C_N = 0,     // nodes of the current level
+  C_M,         // histogram (scanned) nodes
+  C_NP,        // sibling pairs
+  C_NH,        // histogram items
+  C_NC,        // partition items
+  C_NZ,        // zero segments (C_NZ, C_NZD adjacent: zero_segments_kernel reads both)
+  C_NZD,       // ... of which whole-node segments (listed first)
+  C_NL,        // leaf items
+  C_NCREATED,  // created nodes of the tree
+  C_ERR,       // bit 0: partition cursor mismatch, bit 1: capacity overflow
+  C_COUNT = 16
+};
+
+constexpr int kRecFixed = 7;   // record words before the S totals: tree feat bin dl gain left right
+
+struct PlanArgs {
+  int d, T, S, chunk_rows, n_groups, n_sc, newton, subtract, pair_fuse, F_use, has_missing;
+  int64_t hsz, live_dense;
+  const int4* groups;          // (f0, nf, flags): bit 0 register path, bit 1 CSR, bit 2 wide-load
+  const int32_t* j_depth;
+  const int32_t* j_model;
+  const int64_t* j_count;
+  const double* j_inst;
+  const double* j_gain;
+  const double* j_mcw;
+  const double* j_lam;
+  const double* j_eps;
+  int32_t* lv_tree[2];
+  int32_t* lv_gid[2];
+  int64_t* lv_begin[2];
+  int64_t* lv_count[2];
+  int32_t* hn[2];              // histogram node j -> level node i
+  int32_t* nmd[2];
+  int64_t* nho[2];
+  float* par[2];
+  int64_t* nb[2];
+  int64_t* nc[2];
+  int32_t* nfo;
+  int32_t* nnf;
+  int32_t* sj;
+  int32_t* bj;
+  int64_t* poff;
+  int64_t* zoff;
+  int64_t* zsize;
+  int64_t* ppo;                // parent histogram offset of the previous level's q-th split
+  HistItemH* hitems;
+  PartItemH* citems;
+  LeafItemH* litems;
+  const int32_t* r_feat;
+  const int32_t* r_bin;
+  const float* r_gain;
+  const float* r_left;
+  const float* r_tot;
+  const uint8_t* r_dl;
+  const int64_t* r_cur;
+  int64_t* rec;
+  int W;
+  int32_t* level_off;
+  int* cnt;
+  int64_t* leaf_pos;
+  int64_t* sa;
+  int64_t* sb;
+  int64_t* sc;
+  int64_t* sd;
+  int64_t* se;
+  int32_t* flag;
+  int32_t* loc;
+  int64_t cap_nl, cap_m, cap_nodes, cap_h, cap_c, cap_l;
+};
+
+__device__ __forceinline__ int64_t dbits(double v) { return __double_as_longlong(v); }
+__device__ __forceinline__ double bitsd(int64_t v) { return __longlong_as_double(v); }
+
+// Exclusive prefix sums of v[0, n) in place; every thread of the block calls it and gets the total.
+__device__ int64_t block_scan(int64_t* v, int64_t n, int64_t* sh) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  const int64_t per = (n + nt - 1) / nt;
+  const int64_t lo = min(n, (int64_t)t * per), hi = min(n, lo + per);
+  int64_t s = 0;
+  for (int64_t i = lo; i < hi; ++i) s += v[i];
+  sh[t] = s;
+  __syncthreads();
+  for (int off = 1; off < nt; off <<= 1) {
+    const int64_t x = t >= off ? sh[t - off] : 0;
+    __syncthreads();
+    sh[t] += x;
+    __syncthreads();
+  }
+  int64_t run = sh[t] - s;
+  const int64_t total = sh[nt - 1];
+  for (int64_t i = lo; i < hi; ++i) {
+    const int64_t x = v[i];
+    v[i] = run;
+    run += x;
+  }
+  __syncthreads();
+  return total;
+}
+
+// last i in [0, n) with pre[i] <= k (pre: exclusive prefix sums, k < total): the owner of item k
+__device__ __forceinline__ int64_t owner(const int64_t* pre, int64_t n, int64_t k) {
+  int64_t lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (pre[mid] <= k) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void init_node(int64_t* r, int64_t tree, int S) {
+  r[0] = tree;
+  r[1] = -1;
+  r[2] = -1;
+  r[3] = 0;
+  r[4] = dbits(0.0);
+  r[5] = -1;
+  r[6] = -1;
+  for (int s = 0; s < S; ++s) r[kRecFixed + s] = dbits(0.0);
+}
+
+__device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Leaf items of the nodes i in [0, n) whose sa-flag is 0 (sa == nullptr: all nodes), reading buffer `buf`.
+// Appends to litems at C_NL and advances the leaf cursor (host twin: the collect lambda of grow_group).
+__device__ void emit_leaves(const PlanArgs& A, int lvl, int n, const int32_t* split, int buf, int64_t* sh) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  const int64_t* cnt_ = A.lv_count[lvl];
+  for (int i = t; i < n; i += nt) {
+    const bool leaf = split == nullptr || split[i] == 0;
+    const int64_t c = cnt_[i];
+    A.sd[i] = leaf && c > 0 ? c : 0;
+    A.se[i] = leaf && c > 0 ? cdiv(c, A.chunk_rows) : 0;
+  }
+  __syncthreads();
+  const int64_t lbase = *A.leaf_pos;
+  const int64_t nl0 = A.cnt[C_NL];
+  __syncthreads();
+  const int64_t tot_rows = block_scan(A.sd, n, sh);
+  const int64_t tot_items = block_scan(A.se, n, sh);
+  const int64_t n_emit = min(tot_items, A.cap_l - nl0);
+  for (int64_t k = t; k < n_emit; k += nt) {
+    const int64_t i = owner(A.se, n, k);
+    const int64_t o = (k - A.se[i]) * A.chunk_rows;
+    LeafItemH it;
+    it.begin = A.lv_begin[lvl][i] + o;
+    it.count = min((int64_t)A.chunk_rows, cnt_[i] - o);
+    it.out = lbase + A.sd[i] + o;
+    it.gid = A.lv_gid[lvl][i];
+    it.pad = buf;
+    A.litems[nl0 + k] = it;
+  }
+  __syncthreads();
+  if (t == 0) {
+    *A.leaf_pos = lbase + tot_rows;
+    A.cnt[C_NL] = (int)(nl0 + n_emit);
+    if (n_emit < tot_items) A.cnt[C_ERR] |= 2;
+  }
+  __syncthreads();
+}
+
+// One level of planning. d > 0 first turns level d - 1's device decisions (split_find + partition) into
+// the tree records, the leaf items of its non-splitting nodes and the children (level d); then level d's
+// work lists are built. Host twin: common/tree_grow.hpp grow_group (GPU backend, no feature subsets).
+__global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
+  __shared__ int64_t sh[1024];
+  __shared__ int s_n_prev, s_m_prev, s_created;
+  const int t = threadIdx.x, nt = blockDim.x;
+  const int d = A.d, S = A.S, T = A.T;
+  auto R = [&](int64_t g) { return A.rec + (g + 1) * (int64_t)A.W; };
+  if (t == 0) {
+    s_n_prev = d > 0 ? A.cnt[C_N] : 0;
+    s_m_prev = d > 0 ? A.cnt[C_M] : 0;
+    s_created = d > 0 ? A.cnt[C_NCREATED] : 0;
+  }
+  __syncthreads();
+  if (t == 0) {
+    A.cnt[C_NL] = 0;
+    if (d == 0) {
+      A.cnt[C_ERR] = 0;
+      *A.leaf_pos = 0;
+    }
+  }
+  __syncthreads();
+  int n = 0;
+  const int C = d & 1;
+  if (d == 0) {
+    if (t == 0) {
+      int64_t b = 0;
+      for (int j = 0; j < T; ++j) {
+        A.lv_tree[0][j] = j;
+        A.lv_gid[0][j] = j;
+        A.lv_begin[0][j] = b;
+        A.lv_count[0][j] = A.j_count[j];
+        b += A.j_count[j];
+      }
+      A.cnt[C_NCREATED] = T;
+      A.level_off[0] = 0;
+    }
+    for (int j = t; j < T; j += nt) init_node(R(j), j, S);
+    n = T;
+    __syncthreads();
+  } else {
+    const int P = (d - 1) & 1;
+    const int n_prev = s_n_prev, m_prev = s_m_prev;
+    if (t == 0) A.level_off[d] = s_created;
+    if (n_prev == 0) {
+      if (t == 0) {
+        for (int k = C_N; k <= C_NZD; ++k) A.cnt[k] = 0;
+      }
+      return;
+    }
+    // (a) node totals of the scanned nodes, split flags (flag[i], sa[j])
+    for (int i = t; i < n_prev; i += nt) A.flag[i] = 0;
+    __syncthreads();
+    for (int j = t; j < m_prev; j += nt) {
+      const int i = A.hn[P][j];
+      const int gid = A.lv_gid[P][i];
+      int64_t* r = R(gid);
+      for (int s = 0; s < S; ++s) r[kRecFixed + s] = dbits((double)A.r_tot[(int64_t)j * S + s]);
+      const float* Pp = A.par[P] + (int64_t)j * 8;
+      const bool ok = Pp[7] > 0.5f && A.r_feat[j] >= 0 && A.r_gain[j] > Pp[6];
+      A.flag[i] = ok ? 1 : 0;
+      A.sa[j] = ok ? 1 : 0;
+    }
+    __syncthreads();
+    // (b) leaves of level d - 1: every node that does not split, from the buffer level d - 1 read
+    emit_leaves(A, P, n_prev, A.flag, P, sh);
+    // (c) splits -> records + children (level d)
+    const int64_t ns = block_scan(A.sa, m_prev, sh);
+    const int base = s_created;
+    if (2 * ns > A.cap_nl || base + 2 * ns > A.cap_nodes) {   // (cannot happen: caps bound every level)
+      if (t == 0) {
+        A.cnt[C_ERR] |= 2;
+        A.cnt[C_N] = 0;
+        for (int k = C_M; k <= C_NZD; ++k) A.cnt[k] = 0;
+      }
+      return;
+    }
+    for (int j = t; j < m_prev; j += nt) {
+      const int i = A.hn[P][j];
+      if (!A.flag[i]) continue;
+      const int64_t q = A.sa[j];
+      const int gid = A.lv_gid[P][i];
+      int64_t* r = R(gid);
+      r[1] = A.r_feat[j];
+      r[2] = A.r_bin[j];
+      r[3] = A.r_dl[j];
+      r[4] = dbits((double)A.r_gain[j]);
+      const int64_t ncnt = A.nc[P][j];
+      const int64_t nl = A.r_cur[2 * j];
+      if (nl < 0 || nl + A.r_cur[2 * j + 1] != ncnt) A.cnt[C_ERR] |= 1;
+      const int64_t gl = base + 2 * q, gr = gl + 1;
+      r[5] = gl;
+      r[6] = gr;
+      const int tree = A.lv_tree[P][i];
+      int64_t* rl = R(gl);
+      int64_t* rr = R(gr);
+      init_node(rl, tree, S);
+      init_node(rr, tree, S);
+      for (int s = 0; s < S; ++s) {
+        const double lt = (double)A.r_left[(int64_t)j * S + s];
+        const double tt = (double)A.r_tot[(int64_t)j * S + s];
+        rl[kRecFixed + s] = dbits(lt);
+        rr[kRecFixed + s] = dbits(tt - lt);
+      }
+      const int64_t b0 = A.nb[P][j];
+      A.lv_tree[C][2 * q] = tree;
+      A.lv_gid[C][2 * q] = (int32_t)gl;
+      A.lv_begin[C][2 * q] = b0;
+      A.lv_count[C][2 * q] = nl;
+      A.lv_tree[C][2 * q + 1] = tree;
+      A.lv_gid[C][2 * q + 1] = (int32_t)gr;
+      A.lv_begin[C][2 * q + 1] = b0 + nl;
+      A.lv_count[C][2 * q + 1] = ncnt - nl;
+      A.ppo[q] = A.nho[P][j];
+    }
+    n = (int)(2 * ns);
+    if (t == 0) A.cnt[C_NCREATED] = base + n;
+    __syncthreads();
+  }
+  if (n == 0) {
+    if (t == 0) {
+      A.cnt[C_N] = 0;
+      for (int k = C_M; k <= C_NZD; ++k) A.cnt[k] = 0;
+    }
+    return;
+  }
+  // ---- plan level d: can / need (flag = can, sa = need)
+  const int32_t* ltree = A.lv_tree[C];
+  const int64_t* lcnt = A.lv_count[C];
+  for (int i = t; i < n; i += nt) {
+    const int jt = ltree[i];
+    const int64_t c = lcnt[i];
+    bool can = d < A.j_depth[jt] && c >= 2 && (double)c >= 2 * A.j_inst[jt] - 1e-9;
+    if (can && A.newton && d > 0 && A.j_mcw[jt] > 0 &&
+        bitsd(R(A.lv_gid[C][i])[kRecFixed + 1]) < 2.0 * A.j_mcw[jt] * (1.0 - 1e-6))
+      can = false;
+    A.flag[i] = can ? 1 : 0;
+    A.sa[i] = (can || d == 0) ? 1 : 0;
+  }
+  __syncthreads();
+  if (A.subtract && d > 0) {
+    for (int q = t; 2 * q + 1 < n; q += nt) {
+      const int li = 2 * q, ri = li + 1;
+      if (A.sa[li] != A.sa[ri] && lcnt[li] >= 1 && lcnt[ri] >= 1 &&
+          (A.flag[li] ? lcnt[ri] <= lcnt[li] : lcnt[li] <= lcnt[ri]))
+        A.sa[li] = A.sa[ri] = 1;
+    }
+    __syncthreads();
+  }
+  for (int i = t; i < n; i += nt) A.sb[i] = A.sa[i];     // need flags (sa becomes positions)
+  __syncthreads();
+  const int m = (int)block_scan(A.sa, n, sh);
+  if (m > A.cap_m) {                       // (cannot happen: caps bound every level)
+    if (t == 0) {
+      A.cnt[C_ERR] |= 2;
+      A.cnt[C_N] = 0;
+      for (int k = C_M; k <= C_NZD; ++k) A.cnt[k] = 0;
+    }
+    return;
+  }
+  if (m == 0) {                            // nothing to scan: every node of level d is a leaf
+    emit_leaves(A, C, n, nullptr, C, sh);
+    if (t == 0) {
+      A.cnt[C_N] = 0;
+      for (int k = C_M; k <= C_NZD; ++k) A.cnt[k] = 0;
+    }
+    return;
+  }
+  for (int i = t; i < n; i += nt)
+    if (A.sb[i]) {
+      const int j = (int)A.sa[i];
+      A.hn[C][j] = i;
+      A.loc[i] = j;
+    }
+  __syncthreads();
+  for (int j = t; j < m; j += nt) {
+    const int i = A.hn[C][j];
+    const int jt = ltree[i];
+    A.nmd[C][j] = A.j_model[jt];
+    A.nho[C][j] = (int64_t)j * A.hsz;
+    A.nb[C][j] = A.lv_begin[C][i];
+    A.nc[C][j] = lcnt[i];
+    A.nfo[j] = 0;
+    A.nnf[j] = A.F_use;
+    float* Pp = A.par[C] + (int64_t)j * 8;
+    Pp[0] = (float)A.j_inst[jt];
+    Pp[1] = (float)A.j_gain[jt];
+    Pp[2] = (float)A.j_mcw[jt];
+    Pp[3] = (float)A.j_lam[jt];
+    Pp[4] = 0.f;
+    Pp[5] = A.has_missing ? 1.f : 0.f;
+    Pp[6] = (float)A.j_eps[jt];
+    Pp[7] = A.flag[i] ? 1.f : 0.f;
+  }
+  __syncthreads();
+  // ---- sibling pairs: (small, big) histogram node ids, parent offsets; big nodes are derived (flag = is_big)
+  for (int j = t; j < m; j += nt) A.flag[j] = 0;
+  __syncthreads();
+  int n_pairs = 0;
+  if (A.subtract && d > 0) {
+    const int nq = n / 2;
+    for (int q = t; q < nq; q += nt) A.sc[q] = (A.sb[2 * q] && A.sb[2 * q + 1]) ? 1 : 0;
+    __syncthreads();
+    n_pairs = (int)block_scan(A.sc, nq, sh);
+    for (int q = t; q < nq; q += nt) {
+      if (!(A.sb[2 * q] && A.sb[2 * q + 1])) continue;
+      const int li = 2 * q, ri = li + 1;
+      const bool left_big = lcnt[li] >= lcnt[ri];
+      const int big = A.loc[left_big ? li : ri], small = A.loc[left_big ? ri : li];
+      const int64_t k = A.sc[q];
+      A.sj[k] = small;
+      A.bj[k] = big;
+      A.poff[k] = A.ppo[q];
+      A.flag[big] = 1;
+      if (A.pair_fuse) {
+        A.par[C][(int64_t)small * 8 + 4] = 1.f;
+        A.par[C][(int64_t)big * 8 + 4] = 1.f;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- per-node work counts: wide / other histogram items, partition items, zero segments
+  const bool dense_split = A.live_dense >= 0 && A.live_dense < A.hsz;
+  for (int j = t; j < m; j += nt) {
+    const int64_t c = A.nc[C][j];
+    const int64_t nch = max((int64_t)1, cdiv(c, A.chunk_rows));
+    const int64_t ncsr = max((int64_t)1, cdiv(c, tmog::kCsrRows));
+    const int64_t npi = max((int64_t)1, cdiv(c, tmog::kPartRows));
+    const bool build = A.flag[j] == 0;
+    int64_t wide = 0, other = 0;
+    bool has_csr = false;
+    if (build)
+      for (int g = 0; g < A.n_groups; ++g) {
+        const int fl = A.groups[g].z;
+        const bool reg = fl & 1, csr = fl & 2, wd = fl & 4;
+        const int64_t k = (csr ? ncsr : nch) * ((csr || reg) ? 1 : A.n_sc);
+        if (wd) wide += k;
+        else other += k;
+        has_csr |= csr;
+      }
+    A.sa[j] = wide;
+    A.sb[j] = other;
+    A.sc[j] = npi;
+    A.sd[j] = build && (nch > 1 || (has_csr && ncsr > 1 && !dense_split)) ? 1 : 0;
+    A.se[j] = build && nch == 1 && has_csr && ncsr > 1 && dense_split ? 1 : 0;
+  }
+  __syncthreads();
+  const int64_t n_wide = block_scan(A.sa, m, sh);
+  const int64_t n_other = block_scan(A.sb, m, sh);
+  const int64_t n_part = block_scan(A.sc, m, sh);
+  const int64_t n_zw = block_scan(A.sd, m, sh);
+  const int64_t n_zc = block_scan(A.se, m, sh);
+  const int64_t n_hist = n_wide + n_other;
+  const int64_t h_emit = min(n_hist, A.cap_h), c_emit = min(n_part, A.cap_c);
+  // histogram items, wide-load items first (the host's stable partition), then the others
+  for (int64_t k = t; k < h_emit; k += nt) {
+    const bool wsec = k < n_wide;
+    const int64_t* pre = wsec ? A.sa : A.sb;
+    const int64_t kk = wsec ? k : k - n_wide;
+    const int64_t j = owner(pre, m, kk);
+    int64_t local = kk - pre[j];
+    const int64_t c = A.nc[C][j];
+    const int64_t nch = max((int64_t)1, cdiv(c, A.chunk_rows));
+    const int64_t ncsr = max((int64_t)1, cdiv(c, tmog::kCsrRows));
+    for (int g = 0; g < A.n_groups; ++g) {
+      const int4 gr = A.groups[g];
+      const bool reg = gr.z & 1, csr = gr.z & 2, wd = gr.z & 4;
+      if (wd != wsec) continue;
+      const int64_t nit = csr ? ncsr : nch;
+      const int64_t nchunk = (csr || reg) ? 1 : A.n_sc;
+      if (local >= nit * nchunk) {
+        local -= nit * nchunk;
+        continue;
+      }
+      const int64_t sc_ = local / nit, ci = local - sc_ * nit;
+      const int64_t step = csr ? tmog::kCsrRows : A.chunk_rows;
+      HistItemH h;
+      h.node = (int32_t)j;
+      h.fg0 = gr.x;
+      h.nf = gr.y;
+      h.excl = (nit == 1 ? 1 : 0) | (reg ? 2 : 0) | (csr ? 4 : 0) | (wd ? 16 : 0) |
+               ((reg || csr) && A.live_dense >= 0 ? 8 : 0) | (int32_t)(sc_ << 8);
+      h.begin = A.nb[C][j] + ci * step;
+      h.count = min(step, c - ci * step);
+      A.hitems[k] = h;
+      break;
+    }
+  }
+  // partition items of every scanned node (kPartRows-row slices)
+  for (int64_t k = t; k < c_emit; k += nt) {
+    const int64_t j = owner(A.sc, m, k);
+    const int64_t ci = k - A.sc[j];
+    const int64_t c = A.nc[C][j];
+    PartItemH p;
+    p.node = (int32_t)j;
+    p.pad = 0;
+    p.begin = A.nb[C][j] + ci * tmog::kPartRows;
+    p.count = min((int64_t)tmog::kPartRows, c - ci * tmog::kPartRows);
+    p.out_left = p.out_right = 0;
+    A.citems[k] = p;
+  }
+  // zero segments: whole nodes first (dense prefix), then CSR-only regions past the dense prefix
+  for (int j = t; j < m; j += nt) {
+    const bool zw = (j + 1 < m ? A.sd[j + 1] : n_zw) != A.sd[j];
+    const bool zc = (j + 1 < m ? A.se[j + 1] : n_zc) != A.se[j];
+    if (zw) {
+      A.zoff[A.sd[j]] = A.nho[C][j];
+      A.zsize[A.sd[j]] = A.hsz;
+    }
+    if (zc) {
+      A.zoff[n_zw + A.se[j]] = A.nho[C][j] + A.live_dense;
+      A.zsize[n_zw + A.se[j]] = A.hsz - A.live_dense;
+    }
+  }
+  if (t == 0) {
+    A.cnt[C_N] = n;
+    A.cnt[C_M] = m;
+    A.cnt[C_NP] = n_pairs;
+    A.cnt[C_NH] = (int)h_emit;
+    A.cnt[C_NC] = (int)c_emit;
+    A.cnt[C_NZ] = (int)(n_zw + n_zc);
+    A.cnt[C_NZD] = (int)n_zw;
+    if (h_emit < n_hist || c_emit < n_part) A.cnt[C_ERR] |= 2;
+  }
+}
+
+struct FinArgs {
+  int T, S, mode, kind, n_levels;
+  int64_t* rec;
+  int W;
+  const int32_t* level_off;
+  const int* cnt;
+  const int64_t* leaf_pos;
+  const double* j_lam;
+  const double* j_eta;
+  const double* j_gamma;
+  float* gid_value;
+  int64_t* gid_tree;
+  int64_t* left_w;
+  int64_t* right_w;
+  int64_t* parent;
+  int32_t* reach;
+  double* value;
+};
+
+// Device twin of tmog_tree_finalize_cpu's values / gamma pruning / gid values (ops/csrc/host/tree_cpu.cpp):
+// the leaf output of every created node id for the boosting epilogue, a pruned node's descendants taking
+// their kept ancestor's value. The host rebuilds the Forest from the same records with tree_cpu.cpp.
+// Pruning bottom-up level by level is the sequential reverse-id loop (children have higher ids than parents).
+__global__ void __launch_bounds__(1024) tree_finalize_kernel(FinArgs A) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  const int64_t n = A.cnt[C_NCREATED];
+  auto R = [&](int64_t g) { return A.rec + (g + 1) * (int64_t)A.W; };
+  for (int64_t i = t; i < n; i += nt) {
+    const int64_t* r = R(i);
+    const int64_t jt = r[0];
+    const double t0 = bitsd(r[kRecFixed]);
+    const double t1 = A.S > 1 ? bitsd(r[kRecFixed + 1]) : 0.0;
+    double v;
+    if (A.mode == 1) v = t0 > 0 ? t1 / fmax(t0, 1e-300) : 0.0;
+    else v = -t0 / (t1 + A.j_lam[jt]) * A.j_eta[jt];
+    A.value[i] = v;
+    A.left_w[i] = r[5];
+    A.right_w[i] = r[6];
+    A.parent[i] = -1;
+    A.reach[i] = i < A.T ? 1 : 0;
+  }
+  __syncthreads();
+  for (int64_t i = t; i < n; i += nt) {
+    const int64_t* r = R(i);
+    if (r[5] >= 0) {
+      A.parent[r[5]] = i;
+      A.parent[r[6]] = i;
+    }
+  }
+  __syncthreads();
+  auto lvl_lo = [&](int L) { return (int64_t)A.level_off[L]; };
+  auto lvl_hi = [&](int L) { return L + 1 < A.n_levels ? (int64_t)A.level_off[L + 1] : n; };
+  if (A.kind == 3) {
+    for (int L = A.n_levels - 1; L >= 0; --L) {
+      for (int64_t i = lvl_lo(L) + t; i < lvl_hi(L); i += nt) {
+        const int64_t l = A.left_w[i];
+        if (l < 0) continue;
+        const int64_t r = A.right_w[i];
+        const int64_t* rr = R(i);
+        if (A.left_w[l] < 0 && A.left_w[r] < 0 && bitsd(rr[4]) < A.j_gamma[rr[0]]) {
+          A.left_w[i] = -1;
+          A.right_w[i] = -1;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int L = 0; L < A.n_levels; ++L) {
+    for (int64_t i = lvl_lo(L) + t; i < lvl_hi(L); i += nt)
+      if (A.reach[i] && A.left_w[i] >= 0) {
+        A.reach[A.left_w[i]] = 1;
+        A.reach[A.right_w[i]] = 1;
+      }
+    __syncthreads();
+  }
+  for (int L = 0; L < A.n_levels; ++L) {
+    for (int64_t i = lvl_lo(L) + t; i < lvl_hi(L); i += nt) {
+      const int64_t p = A.parent[i];
+      A.gid_value[i] = (A.reach[i] || p < 0) ? (float)A.value[i] : A.gid_value[p];
+      A.gid_tree[i] = R(i)[0];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    A.rec[0] = n;
+    A.rec[1] = *A.leaf_pos;
+    A.rec[2] = A.cnt[C_ERR];
+  }
+}
+
+inline void hchk(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+inline void kchk(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string("kernel ") + what + " failed with code " + std::to_string(rc));
+}
+
+// Per-slot device resources of the resident grower (grow-only; stream-ordered allocations on the caller's
+// stream, which every use of the slot is ordered on).
+struct Buf {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  void need(size_t bytes, hipStream_t s) {
+    if (bytes <= cap) return;
+    if (p) hchk(hipFreeAsync(p, s), "hipFreeAsync");
+    cap = bytes + bytes / 4 + 4096;
+    hchk(hipMallocAsync((void**)&p, cap, s), "hipMallocAsync");
+  }
+};
+
+struct ResSlot {
+  Buf arena, hist0, hist1, cand, done, res, consts;
+  uint8_t* pin = nullptr;      // pinned staging of the per-call constants
+  size_t pin_cap = 0;
+  hipEvent_t copied = nullptr;
+  std::vector<uint8_t> last;   // constants last shipped (skipped when unchanged)
+  size_t done_zeroed = 0;
+  int device = -1;
+};
+
+std::vector<ResSlot>& res_slots() {
+  static std::vector<ResSlot> s(32);
+  return s;
+}
+
+thread_local std::string g_err;
+
+struct Carve {
+  uint8_t* base;
+  size_t off = 0;
+  template <class T>
+  T* take(int64_t n) {
+    off = (off + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(base + off);
+    off += sizeof(T) * (size_t)std::max<int64_t>(n, 1);
+    return p;
+  }
+};
+
+struct Caps {
+  int D = 0;
+  std::vector<int64_t> nmax;   // nodes per level bound, d = 0..D + 1 (level D + 1 is empty)
+  int64_t cap_nl = 0, cap_m = 0, cap_nodes = 0, cap_h = 0, cap_c = 0, cap_l = 0;
+};
+
+Caps caps_of(const tmog::GrowArgs& a, const tmog::GroupLayout& L, int n_sc) {
+  Caps c;
+  const int T = a.T;
+  int64_t total = 0;
+  for (int j = 0; j < T; ++j) {
+    total += a.job_count[j];
+    c.D = std::max(c.D, (int)a.job_depth[j]);
+  }
+  c.nmax.assign(c.D + 2, 0);
+  for (int d = 0; d <= c.D; ++d) {
+    int64_t s = 0;
+    for (int j = 0; j < T; ++j)
+      if (d <= a.job_depth[j]) s += std::min(d >= 40 ? a.job_count[j] : ((int64_t)1 << d), std::max<int64_t>(a.job_count[j], 1));
+    c.nmax[d] = std::max<int64_t>(1, std::min<int64_t>(s, std::max<int64_t>(total, T)));
+    c.cap_nl = std::max(c.cap_nl, c.nmax[d]);
+    if (d < c.D || d == 0) c.cap_m = std::max(c.cap_m, c.nmax[d]);   // levels that build histograms
+    c.cap_nodes += c.nmax[d];
+  }
+  c.cap_m = std::max<int64_t>(c.cap_m, 1);
+  for (const tmog::FeatGroup& g : L.full_groups) {
+    const int64_t step = g.csr ? tmog::kCsrRows : a.chunk_rows;
+    c.cap_h += ((g.csr || g.reg) ? 1 : n_sc) * (total / step + c.cap_m + 1);
+  }
+  c.cap_c = total / tmog::kPartRows + c.cap_m + 1;
+  c.cap_l = 2 * (total / std::max<int64_t>(a.chunk_rows, 1) + c.cap_nl + 1);
+  return c;
+}
+
+// per-level grid bounds
+int64_t hist_bound(const tmog::GrowArgs& a, const tmog::GroupLayout& L, int n_sc, int64_t total, int64_t m) {
+  int64_t h = 0;
+  for (const tmog::FeatGroup& g : L.full_groups) {
+    const int64_t step = g.csr ? tmog::kCsrRows : a.chunk_rows;
+    h += ((g.csr || g.reg) ? 1 : n_sc) * (total / step + m + 1);
+  }
+  return h;
+}
+
+// Configurations the device plan covers (everything else stays on the host-planned grower): one job group,
+// no per-node feature subsets, not feature-parallel, subtraction + fused pair scan, narrow split scan with
+// the fused reduction, statistics in one histogram chunk, leaves collected, Newton (MODE 2) or variance
+// (MODE 1) values. Returns an empty string when supported.
+std::string unsupported(const tmog::GrowArgs& a) {
+  if (a.n_groups != 1) return "more than one job group";
+  if (a.fp_world > 0) return "feature-parallel";
+  if (!a.collect_leaves) return "leaves not collected";
+  if (!a.subtract) return "no subtraction";
+  if (a.mode == 0) return "class-count histograms";
+  if (a.S > 16 || a.B > 64) return "wide statistics";
+  for (int j = 0; j < a.T; ++j) {
+    const int k = a.job_fsub[j];
+    if (k > 0 && k < a.F) return "per-node feature subsets";
+  }
+  const char* ps = std::getenv("TMOG_PAIR_SCAN");
+  if (ps && ps[0] == '0') return "pair scan disabled";
+  const char* fr = std::getenv("TMOG_FUSED_REDUCE");
+  if (fr && fr[0] == '0') return "fused reduction disabled";
+  const char* ws = std::getenv("TMOG_HIST_WIDE_SPLIT");
+  if (ws && ws[0] == '1') return "split wide-load launches";
+  if (tmog_hip_hist_stat_chunk(a.B, a.S) < a.S) return "chunked statistics";
+  return "";
+}
+
+}  // namespace
+
+extern "C" {
+
+// Outputs of one device-planned tree (models/tree_engine.py _ResidentIO).
+struct ResidentIO {
+  int64_t* rec;          // [1 + cap_nodes][7 + S] int64: header (nodes, leaf entries, error bits), then node records
+  float* gid_value;      // [cap_nodes] leaf output per created node id (pruning applied)
+  int64_t* gid_tree;     // [cap_nodes] job of each created node
+  int64_t cap_nodes;
+  const double* job_eta;    // [T]
+  const double* job_gamma;  // [T]
+};
+
+int64_t tmog_hip_resident_cap_nodes(const tmog::GrowArgs* args) {
+  const tmog::GrowArgs& a = *args;
+  if (!unsupported(a).empty()) return -1;
+  const tmog::GroupLayout L = tmog::group_layout<true>(a, false, false);
+  return caps_of(a, L, 1).cap_nodes;
+}
+
+int tmog_hip_resident_error(char* msg, int cap) {
+  if (msg && cap > 0) {
+    std::strncpy(msg, g_err.c_str(), cap - 1);
+    msg[cap - 1] = 0;
+  }
+  return (int)g_err.size();
+}
+
+// Enqueue the growth of one tree per job of the (single) group on a.stream. Returns 0 when enqueued,
+// 1 when the configuration is not covered (nothing enqueued; use tmog_hip_grow_forest), -1 on error
+// (tmog_hip_resident_error). No host synchronisation with the device.
+int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
+  g_err.clear();
+  try {
+    const tmog::GrowArgs& a = *args;
+    const std::string why = unsupported(a);
+    if (!why.empty()) {
+      g_err = why;
+      return 1;
+    }
+    const int T = a.T, S = a.S, B = a.B;
+    if (a.slot_base < 0 || a.slot_base >= (int)res_slots().size()) throw std::runtime_error("bad slot");
+    hipStream_t st = (hipStream_t)a.stream;
+    int dev = 0;
+    hchk(hipGetDevice(&dev), "hipGetDevice");
+    (void)tmog_hip_tree_prime();
+    ResSlot& sl = res_slots()[a.slot_base];
+    if (sl.device != dev) {
+      sl = ResSlot();
+      sl.device = dev;
+    }
+    const tmog::GroupLayout L = tmog::group_layout<true>(a, false, false);
+    const int n_sc = 1;
+    const Caps cp = caps_of(a, L, n_sc);
+    if (io->cap_nodes < cp.cap_nodes) throw std::runtime_error("record buffer too small");
+    int64_t total = 0;
+    for (int j = 0; j < T; ++j) total += a.job_count[j];
+    const int F_use = L.F_use;
+    const int64_t hsz = (int64_t)F_use * B * S;
+    const int W = kRecFixed + S;
+    // ---- per-call constants: groups, feature list, job table (shipped only when they change)
+    std::vector<int4> groups;
+    bool need_general = false;
+    for (const tmog::FeatGroup& g : L.full_groups) {
+      groups.push_back(make_int4(g.f0, g.nf, (g.reg ? 1 : 0) | (g.csr ? 2 : 0) | (g.wide ? 4 : 0), 0));
+      need_general |= !g.csr && !g.wide;
+    }
+    std::vector<int32_t> flist(F_use);
+    for (int f = 0; f < F_use; ++f) flist[f] = L.perm_feats.empty() ? f : L.perm_feats[f];
+    tmog::Staging cs;
+    const size_t o_groups = cs.add(groups), o_flist = cs.add(flist);
+    const size_t o_depth = cs.add(a.job_depth, 4 * (size_t)T), o_model = cs.add(a.job_model, 4 * (size_t)T);
+    const size_t o_count = cs.add(a.job_count, 8 * (size_t)T), o_inst = cs.add(a.job_min_inst, 8 * (size_t)T);
+    const size_t o_gain = cs.add(a.job_min_gain, 8 * (size_t)T), o_mcw = cs.add(a.job_mcw, 8 * (size_t)T);
+    const size_t o_lam = cs.add(a.job_lambda, 8 * (size_t)T), o_eps = cs.add(a.job_eps, 8 * (size_t)T);
+    const size_t o_eta = cs.add(io->job_eta, 8 * (size_t)T), o_gam = cs.add(io->job_gamma, 8 * (size_t)T);
+    sl.consts.need(cs.buf.size(), st);
+    if (cs.buf != sl.last) {
+      if (sl.copied) hchk(hipEventSynchronize(sl.copied), "constants copy wait");
+      else hchk(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming), "event");
+      if (sl.pin_cap < cs.buf.size()) {
+        if (sl.pin) hchk(hipHostFree(sl.pin), "hipHostFree");
+        sl.pin_cap = cs.buf.size() + 4096;
+        hchk(hipHostMalloc((void**)&sl.pin, sl.pin_cap, hipHostMallocDefault), "hipHostMalloc");
+      }
+      std::memcpy(sl.pin, cs.buf.data(), cs.buf.size());
+      hchk(hipMemcpyAsync(sl.consts.p, sl.pin, cs.buf.size(), hipMemcpyHostToDevice, st), "constants copy");
+      hchk(hipEventRecord(sl.copied, st), "event record");
+      sl.last = cs.buf;
+    }
+    const uint8_t* K = sl.consts.p;
+    // ---- arena
+    auto carve_all = [&](Carve& cv, PlanArgs& P, FinArgs& Fa, int** cnt, int64_t** leaf_pos, int32_t** level_off,
+                         int32_t** r_feat, int32_t** r_bin, float** r_gain, float** r_left, float** r_tot,
+                         uint8_t** r_dl, int64_t** r_cur) {
+      for (int k = 0; k < 2; ++k) {
+        P.lv_tree[k] = cv.take<int32_t>(cp.cap_nl);
+        P.lv_gid[k] = cv.take<int32_t>(cp.cap_nl);
+        P.lv_begin[k] = cv.take<int64_t>(cp.cap_nl);
+        P.lv_count[k] = cv.take<int64_t>(cp.cap_nl);
+        P.hn[k] = cv.take<int32_t>(cp.cap_m);
+        P.nmd[k] = cv.take<int32_t>(cp.cap_m);
+        P.nho[k] = cv.take<int64_t>(cp.cap_m);
+        P.par[k] = cv.take<float>(8 * cp.cap_m);
+        P.nb[k] = cv.take<int64_t>(cp.cap_m);
+        P.nc[k] = cv.take<int64_t>(cp.cap_m);
+      }
+      P.nfo = cv.take<int32_t>(cp.cap_m);
+      P.nnf = cv.take<int32_t>(cp.cap_m);
+      P.sj = cv.take<int32_t>(cp.cap_m);
+      P.bj = cv.take<int32_t>(cp.cap_m);
+      P.poff = cv.take<int64_t>(cp.cap_m);
+      P.zoff = cv.take<int64_t>(cp.cap_m);
+      P.zsize = cv.take<int64_t>(cp.cap_m);
+      P.ppo = cv.take<int64_t>(cp.cap_nl);
+      P.hitems = cv.take<HistItemH>(cp.cap_h);
+      P.citems = cv.take<PartItemH>(cp.cap_c);
+      P.litems = cv.take<LeafItemH>(cp.cap_l);
+      P.sa = cv.take<int64_t>(cp.cap_nl);
+      P.sb = cv.take<int64_t>(cp.cap_nl);
+      P.sc = cv.take<int64_t>(cp.cap_nl);
+      P.sd = cv.take<int64_t>(cp.cap_nl);
+      P.se = cv.take<int64_t>(cp.cap_nl);
+      P.flag = cv.take<int32_t>(cp.cap_nl);
+      P.loc = cv.take<int32_t>(cp.cap_nl);
+      *cnt = cv.take<int>(C_COUNT);
+      *leaf_pos = cv.take<int64_t>(1);
+      *level_off = cv.take<int32_t>(cp.D + 2);
+      *r_feat = cv.take<int32_t>(cp.cap_m);
+      *r_bin = cv.take<int32_t>(cp.cap_m);
+      *r_gain = cv.take<float>(cp.cap_m);
+      *r_left = cv.take<float>((int64_t)S * cp.cap_m);
+      *r_tot = cv.take<float>((int64_t)S * cp.cap_m);
+      *r_dl = cv.take<uint8_t>(cp.cap_m);
+      *r_cur = cv.take<int64_t>(2 * cp.cap_m);
+      Fa.left_w = cv.take<int64_t>(cp.cap_nodes);
+      Fa.right_w = cv.take<int64_t>(cp.cap_nodes);
+      Fa.parent = cv.take<int64_t>(cp.cap_nodes);
+      Fa.reach = cv.take<int32_t>(cp.cap_nodes);
+      Fa.value = cv.take<double>(cp.cap_nodes);
+    };
+    PlanArgs P{};
+    FinArgs Fa{};
+    int* cnt;
+    int64_t* leaf_pos;
+    int32_t* level_off;
+    int32_t *r_feat, *r_bin;
+    float *r_gain, *r_left, *r_tot;
+    uint8_t* r_dl;
+    int64_t* r_cur;
+    {
+      Carve probe{nullptr};
+      carve_all(probe, P, Fa, &cnt, &leaf_pos, &level_off, &r_feat, &r_bin, &r_gain, &r_left, &r_tot, &r_dl, &r_cur);
+      sl.arena.need(probe.off + 256, st);
+      Carve cv{sl.arena.p};
+      carve_all(cv, P, Fa, &cnt, &leaf_pos, &level_off, &r_feat, &r_bin, &r_gain, &r_left, &r_tot, &r_dl, &r_cur);
+    }
+    sl.hist0.need(sizeof(int64_t) * (size_t)hsz * cp.cap_m, st);
+    sl.hist1.need(sizeof(int64_t) * (size_t)hsz * cp.cap_m, st);
+    sl.cand.need(tmog_hip_split_cand_bytes((int)cp.cap_m, F_use, B, S), st);
+    sl.done.need(sizeof(unsigned) * (size_t)cp.cap_m, st);
+    if (sl.done_zeroed < sl.done.cap) {      // ticket counters start (and are left) at zero
+      hchk(hipMemsetAsync(sl.done.p, 0, sl.done.cap, st), "memset done");
+      sl.done_zeroed = sl.done.cap;
+    }
+    int64_t* hist[2] = {(int64_t*)sl.hist0.p, (int64_t*)sl.hist1.p};
+    uint32_t* rows[2] = {a.rows, a.rows_alt};
+    int32_t* gh[2] = {a.gh, a.gh_alt};
+    const bool use_gh = a.gh != nullptr && a.gh_alt != nullptr && a.mode == 2;
+    P.T = T;
+    P.S = S;
+    P.chunk_rows = (int)a.chunk_rows;
+    P.n_groups = (int)groups.size();
+    P.n_sc = n_sc;
+    P.newton = (a.mode == 2 && a.kind == 3 && S >= 2 && !(std::getenv("TMOG_TREE_HESS_GATE") &&
+                                                            std::getenv("TMOG_TREE_HESS_GATE")[0] == '0')) ? 1 : 0;
+    P.subtract = 1;
+    P.pair_fuse = 1;
+    P.F_use = F_use;
+    P.hsz = hsz;
+    P.live_dense = L.live_dense;
+    P.groups = (const int4*)(K + o_groups);
+    P.j_depth = (const int32_t*)(K + o_depth);
+    P.j_model = (const int32_t*)(K + o_model);
+    P.j_count = (const int64_t*)(K + o_count);
+    P.j_inst = (const double*)(K + o_inst);
+    P.j_gain = (const double*)(K + o_gain);
+    P.j_mcw = (const double*)(K + o_mcw);
+    P.j_lam = (const double*)(K + o_lam);
+    P.j_eps = (const double*)(K + o_eps);
+    P.r_feat = r_feat;
+    P.r_bin = r_bin;
+    P.r_gain = r_gain;
+    P.r_left = r_left;
+    P.r_tot = r_tot;
+    P.r_dl = r_dl;
+    P.r_cur = r_cur;
+    P.rec = io->rec;
+    P.W = W;
+    P.level_off = level_off;
+    P.cnt = cnt;
+    P.leaf_pos = leaf_pos;
+    P.cap_nl = cp.cap_nl;
+    P.cap_m = cp.cap_m;
+    P.cap_nodes = cp.cap_nodes;
+    P.cap_h = cp.cap_h;
+    P.cap_c = cp.cap_c;
+    P.cap_l = cp.cap_l;
+    P.has_missing = a.missing_bin >= 0 ? 1 : 0;
+    const int32_t* flist_d = (const int32_t*)(K + o_flist);
+    // levels 0..D build histograms (level D only when D == 0: deeper, no node of level D may split), and
+    // plan D + 1 turns the last decisions into leaves
+    for (int d = 0; d <= cp.D + 1; ++d) {
+      P.d = d;
+      hipLaunchKernelGGL(level_plan_kernel, dim3(1), dim3(1024), 0, st, P);
+      kchk((int)hipGetLastError(), "level_plan");
+      const int64_t nprev = d > 0 ? cp.nmax[d - 1] : 0;
+      const int64_t lbound = (total / std::max<int64_t>(a.chunk_rows, 1) + nprev + 1) +
+                             (total / std::max<int64_t>(a.chunk_rows, 1) + cp.nmax[d] + 1);
+      kchk(tmog_hip_leaf_collect(rows[0], P.litems, (int)std::min(lbound, cp.cap_l), a.leaf_rows, a.leaf_gid, st,
+                                 rows[1], cnt + C_NL),
+           "leaf_collect");
+      if (d > cp.D || (d == cp.D && d > 0)) continue;
+      const int c = d & 1;
+      const int64_t mb = cp.nmax[d];
+      kchk(tmog_hip_zero_segments(hist[c], P.zoff, P.zsize, (int)mb, hsz, L.live_dense, B * S, S, st, 0, cnt + C_NZ),
+           "zero_segments");
+      kchk(tmog_hip_hist_build(a.Xb, a.F, rows[c], P.hitems, (int)std::min(hist_bound(a, L, n_sc, total, mb), cp.cap_h),
+                               P.nfo, flist_d, P.nmd[c], P.nho[c], hist[c], B, a.mode, S, a.y, a.t1, a.t2, a.stride,
+                               a.qscale, a.mode == 2 ? a.missing_bin : -1, a.csr_ptr, a.csr_col, S, 0,
+                               need_general ? 1 : 0, st, use_gh ? gh[c] : nullptr, cnt + C_NH),
+           "hist_build");
+      if (d > 0)
+        kchk(tmog_hip_pair_scan(hist[c], hist[c ^ 1], P.poff, P.sj, P.bj, (int)std::max<int64_t>(1, mb / 2), P.nho[c],
+                                P.nnf, P.nfo, flist_d, a.n_bins, B, S, a.kind, P.par[c], a.missing_bin, P.nmd[c],
+                                a.qinv, F_use, sl.cand.p, L.split_n_multi, st, cnt + C_NP),
+             "pair_scan");
+      kchk(tmog_hip_split_find(hist[c], (int)mb, P.nho[c], P.nnf, P.nfo, flist_d, a.n_bins, B, S, a.kind, P.par[c],
+                               a.missing_bin, P.nmd[c], a.qinv, F_use, sl.cand.p, r_feat, r_bin, r_gain, r_dl, r_left,
+                               r_tot, r_cur, L.split_n_multi, nullptr, 0, 0, 0, 0, st, (unsigned*)sl.done.p,
+                               cnt + C_M),
+           "split_find");
+      kchk(tmog_hip_partition_fused(a.Xb, a.F, rows[c], rows[c ^ 1], P.citems,
+                                    (int)std::min<int64_t>(total / tmog::kPartRows + mb + 1, cp.cap_c), P.nb[c],
+                                    P.nc[c], r_feat, r_bin, r_dl, P.par[c], r_gain, a.missing_bin, r_cur, a.XbT, a.N,
+                                    st, use_gh ? gh[c] : nullptr, use_gh ? gh[c ^ 1] : nullptr, cnt + C_NC),
+           "partition_fused");
+    }
+    Fa.T = T;
+    Fa.S = S;
+    Fa.mode = a.mode;
+    Fa.kind = a.kind;
+    Fa.n_levels = cp.D + 1;
+    Fa.rec = io->rec;
+    Fa.W = W;
+    Fa.level_off = level_off;
+    Fa.cnt = cnt;
+    Fa.leaf_pos = leaf_pos;
+    Fa.j_lam = P.j_lam;
+    Fa.j_eta = (const double*)(K + o_eta);
+    Fa.j_gamma = (const double*)(K + o_gam);
+    Fa.gid_value = io->gid_value;
+    Fa.gid_tree = io->gid_tree;
+    hipLaunchKernelGGL(tree_finalize_kernel, dim3(1), dim3(1024), 0, st, Fa);
+    kchk((int)hipGetLastError(), "tree_finalize");
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+}  // extern "C"

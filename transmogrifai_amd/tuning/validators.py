@@ -439,8 +439,10 @@ class OpValidator:
         results: Dict[Tuple[int, int, int], float] = {}
         failures: List[str] = []
         timings: Dict[str, float] = {}
+        from ..utils import cancel
         started, errs = set(), []
         lock = threading.Lock()
+        token = threading.Event()       # set at the maxWait deadline: running fits stop at their next check
         gpu = dev.type == "cuda"
         cur = torch.cuda.current_stream(dev) if gpu else None
         # lane 0 takes the longest learner (the critical path): its stream -- and the boosting parts' streams it
@@ -457,7 +459,7 @@ class OpValidator:
                 if gpu:
                     torch.cuda.set_device(dev)
                 TE.set_slot_lane(w * TE.SLOT_LANE)
-                with (torch.cuda.stream(streams[w]) if gpu else contextlib.nullcontext()):
+                with cancel.scope(token), (torch.cuda.stream(streams[w]) if gpu else contextlib.nullcontext()):
                     while True:
                         with lock:
                             if not todo or errs:
@@ -475,33 +477,35 @@ class OpValidator:
                             failures.extend(fails)
                             timings[lname] = time.time() - t1
                             started.discard(li)
+            except cancel.FitCancelled:
+                return                          # its learner stays in `started`: reported as timed out
             except BaseException as e:          # noqa: BLE001  (re-raised on the caller's thread)
                 with lock:
                     errs.append(e)
 
         th = [threading.Thread(target=worker, args=(w,), name=f"fit-lane-{w}", daemon=True) for w in range(lanes)]
-        swi = sys.getswitchinterval()
+        from ..utils.threads import fast_switch
         # a lane returning from a native call must win the GIL back from one running Python promptly
-        sys.setswitchinterval(min(swi, float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))))
-        try:
+        with fast_switch(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))):
             for t in th:
                 t.start()
             bounded = self.max_wait < _UNBOUNDED_WAIT
             for t in th:
                 t.join(max(0.0, self.max_wait - (time.time() - t0)) if bounded else None)
-        finally:
-            sys.setswitchinterval(swi)
+            if any(t.is_alive() for t in th):
+                token.set()                     # cooperative cancel, then join: nothing is left running
+                for t in th:
+                    t.join()
         with lock:
             if errs:
                 raise errs[0]
-            for li in sorted(started):      # still running at the maxWait deadline: abandoned
+            for li in sorted(started):      # still running at the maxWait deadline: cancelled
                 lname = models[li][0]
                 log.warning("Model %s did not finish within maxWait=%ss; its fits are dropped", lname, self.max_wait)
                 failures.append(f"{lname}: did not finish within maxWait={self.max_wait}s")
             for key in [k for k in results if k[0] in started]:
                 del results[key]
-            done = not started
-        if done and gpu:
+        if gpu:
             for st in streams:
                 cur.wait_stream(st)
             # blocks freed on the lane streams are reused by later allocations only once their work has ended
@@ -510,16 +514,28 @@ class OpValidator:
 
     def _fit_eval_bounded(self, lname, grid, mine, X, y, train_rows, val_rows, ctx, remaining: float):
         """:meth:`_fit_eval` under the ``maxWait`` deadline (``awaitResult(..., maxWait)``, OpValidator.scala:348):
-        the learner runs on a worker thread; if it has not returned when the deadline passes, its grid
-        points are reported failed and validation goes on with the other learners (the abandoned fits are
-        never read, as Spark abandons its futures). Only for learners whose jobs are local to this rank --
-        a spread learner's collectives must not be left half-way on one rank."""
+        the learner runs on a worker thread with the caller's device and stream; if it has not returned when
+        the deadline passes, its grid points are reported failed. The reference abandons the future; here the
+        fit is cancelled cooperatively (utils/cancel.py: the learners check between rounds / iterations) and
+        the worker is JOINED before validation goes on, so a timed-out fit never shares the GPU stream, the
+        native tree-grower slots or the binning cache with the learners that follow. Only for learners whose
+        jobs are local to this rank -- a spread learner's collectives must not be left half-way on one rank."""
         import threading
+        from ..utils import cancel
         box: Dict[str, Any] = {}
+        token = threading.Event()
+        gpu = isinstance(X, torch.Tensor) and X.is_cuda
+        dev = X.device if gpu else None
+        stream = torch.cuda.current_stream(dev) if gpu else None
 
         def work():
             try:
-                box["out"] = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, dict(ctx))
+                if gpu:
+                    torch.cuda.set_device(dev)
+                with cancel.scope(token), (torch.cuda.stream(stream) if gpu else contextlib.nullcontext()):
+                    box["out"] = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, dict(ctx))
+            except cancel.FitCancelled:
+                box["cancelled"] = True
             except BaseException as e:          # noqa: BLE001  (re-raised below)
                 box["err"] = e
 
@@ -527,11 +543,15 @@ class OpValidator:
         th.start()
         th.join(max(0.0, remaining))
         if th.is_alive():
+            token.set()
+            th.join()           # returns at the fit's next cancellation check
             log.warning("Model %s did not finish within maxWait=%ss; its %d fits are dropped", lname,
                         self.max_wait, len(mine))
             return {}, [f"{lname}: did not finish within maxWait={self.max_wait}s"]
         if "err" in box:
             raise box["err"]
+        if box.get("cancelled"):
+            return {}, [f"{lname}: did not finish within maxWait={self.max_wait}s"]
         return box["out"]
 
     def _fit_eval(self, lname, grid, mine, X, y, train_rows, val_rows, ctx):
