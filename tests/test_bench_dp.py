@@ -1,4 +1,5 @@
-"""bench.py on 4 gloo ranks (row-sharded, data-parallel fits) reproduces the 1-rank selection for the BASELINE
+"""bench.py on 4 and 8 gloo ranks (row-sharded, data-parallel fits; learners sharded or spread by the cost
+model of parallel/scheduler.py) reproduces the 1-rank selection for the BASELINE
 configs: same best model, configs evaluated and hold-out metric, and no estimator falls back to gathering its
 input columns (stages/base.py OpEstimator.fit)."""
 import json
@@ -26,10 +27,11 @@ def _bench(gpus, config, rows, models):
     ("multiclass-text", 3000, "default"),
     ("regression-100m", 4000, "OpLinearRegression,OpRandomForestRegressor,OpGBTRegressor"),
 ])
-def test_bench_four_ranks_matches_one_rank(config, rows, models):
+@pytest.mark.parametrize("ranks", [4, 8])
+def test_bench_many_ranks_matches_one_rank(config, rows, models, ranks):
     one = _bench(1, config, rows, models)
-    four = _bench(4, config, rows, models)
-    assert four["config"]["parallelism"] == "dp4"
+    four = _bench(ranks, config, rows, models)
+    assert four["config"]["parallelism"] == f"dp{ranks}"
     assert four["dp_gather_fallbacks"] == [] and one["dp_gather_fallbacks"] == []
     assert four["best_model"] == one["best_model"]
     assert four["configs_evaluated"] == one["configs_evaluated"]

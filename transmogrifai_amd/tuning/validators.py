@@ -170,9 +170,18 @@ class OpValidator:
         if world > 1:
             from ..parallel.learner_parallel import LearnerParallel
             par = LearnerParallel()
-        spread = {li for li, (lname, _) in enumerate(models)
-                  if par is not None and learner_class(lname).parallel in ("rows", "features")}
         n_tr = max(1, int(train_rows[0][0].numel())) if train_rows else 1
+        # shard whole jobs or spread every job over the ranks: per learner, by the calibrated cost model
+        # (parallel/scheduler.py); rank 0's choice is broadcast so every rank runs the same collectives
+        spread = set()
+        if par is not None:
+            from ..parallel import scheduler as SCH
+            choices = SCH.choose(models, n_folds, n_tr, X.shape[1], world,
+                                 lambda name: learner_class(name).parallel,
+                                 lambda name, p: _scaled_cost(name, p, n_tr, X.shape[1]))
+            spread = {li for li, c in choices.items() if c.mode == "spread"}
+            spread = set(D.broadcast_object(sorted(spread), 0))
+            self.last_schedule = {models[li][0]: (c.mode, c.shard_s, c.spread_s) for li, c in choices.items()}
         sharded = [j for j, (li, gi, k) in enumerate(jobs) if li not in spread]
         costs = [_scaled_cost(models[jobs[j][0]][0], models[jobs[j][0]][1][jobs[j][1]], n_tr, X.shape[1])
                  for j in sharded]
