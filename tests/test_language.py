@@ -1,5 +1,5 @@
 """Language identification and language-aware tokenization (LangDetectorTest, TextTokenizerTest with
-autoDetectLanguage; LuceneTextAnalyzer per-language analyzers minus stemming)."""
+autoDetectLanguage; LuceneTextAnalyzer per-language analyzers with their light / Snowball stemmers)."""
 import transmogrifai_amd.dsl  # noqa: F401
 from transmogrifai_amd.features import types as T
 from transmogrifai_amd.stages.feature.text_stages import TextTokenizer
@@ -37,7 +37,8 @@ def test_language_aware_tokenizer():
     ds, (t,) = TestFeatureBuilder.of(("t", T.Text, ["L'amour de la vie et le goût des choses", None,
                                                     "The cat and the dog"]))
     st = TextTokenizer(auto_detect_language=True, auto_detect_threshold=0.5).set_input(t)
-    check_transformer(st, ds, expected=[["amour", "vie", "goût", "choses"], [], ["cat", "dog"]])
+    # FrenchAnalyzer stems (FrenchLightStemFilter): amour -> amou, choses -> chos
+    check_transformer(st, ds, expected=[["amou", "vie", "goût", "chos"], [], ["cat", "dog"]])
     # the default (no detection) keeps the StandardAnalyzer English behaviour
     plain = TextTokenizer().set_input(t)
     check_transformer(plain, ds, expected=[["l'amour", "de", "la", "vie", "et", "le", "goût", "des", "choses"], [],
@@ -61,3 +62,47 @@ def test_english_analyzer_stems_unknown_does_not():
     from transmogrifai_amd.utils import lang as L
     assert L.analyze("The runners were running to John's houses", "en") == ["runner", "run", "john", "hous"]
     assert "running" in L.analyze("The runners were running", "Unknown")
+
+
+# ------------------------------------------------------------- per-language stemming (round 4)
+FRENCH = ["Première détection d’une atmosphère autour d’une exoplanète de la taille de la Terre",
+          "Les deux commissions, créées respectivement en juin 2016 et janvier 2017",
+          "Il publie sa théorie de la relativité restreinte en 1905",
+          'Il <h2 class="a">publie sa théorie de la relativité restreinte en 1905', ""]
+# TextTokenizerTest.scala trait French (FrenchAnalyzer: elision, stop words, FrenchLightStemFilter)
+FRENCH_EXPECTED = [["premier", "detection", "atmosph", "autou", "exoplanet", "tail", "tere"],
+                   ["deu", "comision", "cre", "respectif", "juin", "2016", "janvi", "2017"],
+                   ["publ", "theo", "relativit", "restreint", "1905"],
+                   ["h2", "clas", "a", "publ", "theo", "relativit", "restreint", "1905"], []]
+
+
+def test_french_analyzer_matches_reference_fixture():
+    ds, (f,) = TestFeatureBuilder.of(("t", T.Text, FRENCH))
+    st = TextTokenizer(default_language="fr").set_input(f)
+    out = check_transformer(st, ds)
+    assert [list(x or []) for x in out] == FRENCH_EXPECTED
+    html = TextTokenizer(default_language="fr", strip_html=True).set_input(f)
+    out = check_transformer(html, ds)
+    assert list(out[3]) == FRENCH_EXPECTED[2]          # expectedHtml: the tag and its attribute are gone
+
+
+def test_light_stemmers_published_examples():
+    from transmogrifai_amd.utils import stemmers as S
+    # Savoy's light stemmers (Lucene *LightStemFilter) on their documented behaviour
+    assert S.german_analyze_stem("häuser") == "haus" and S.german_analyze_stem("straße") == "strass"
+    assert S.german_normalize("schoen") == "schon" and S.german_normalize("quelle") == "quelle"
+    assert S.spanish_light_stem("chicas") == "chic" and S.spanish_light_stem("luces") == "luz"
+    assert S.italian_light_stem("ragazzi") == "ragazz" and S.italian_light_stem("amiche") == "amic"
+    assert S.portuguese_light_stem("bons") == "bom" and S.portuguese_light_stem("animais") == "animal"
+    assert S.norwegian_light_stem("bilene") == "bil" and S.norwegian_light_stem("kaker") == "kak"
+    # Snowball Swedish / Danish (snowballstem.org sample vocabulary)
+    assert S.swedish_stem("klokheten") == "klok" and S.swedish_stem("jaktkarlarne") == "jaktkarl"
+    assert S.danish_stem("indtagelse") == "indtag" and S.danish_stem("undervisningen") == "undervisning"
+
+
+def test_stemming_language_tokenizer():
+    ds, (f,) = TestFeatureBuilder.of(("t", T.Text, ["Die Häuser der Straßen", "Las chicas y las luces"]))
+    de = check_transformer(TextTokenizer(default_language="de").set_input(f), ds)
+    assert list(de[0]) == ["haus", "strass"]
+    es = check_transformer(TextTokenizer(default_language="es").set_input(f), ds)
+    assert list(es[1]) == ["chic", "luz"]

@@ -52,6 +52,15 @@ PROFILES: Dict[str, FrozenSet[str]] = {k: frozenset(v.split()) for k, v in _PROF
 # stop words of the per-language analyzers (English: Lucene's english_stop list of utils/text.py)
 STOPWORDS: Dict[str, FrozenSet[str]] = dict(PROFILES)
 STOPWORDS["en"] = TU.ENGLISH_STOPWORDS
+# FrenchAnalyzer's stop set (the Snowball French list)
+STOPWORDS["fr"] = PROFILES["fr"] | frozenset("""
+au aux avec ce ces dans de des du elle en et eux il je la le leur lui ma mais me même mes moi mon ne nos notre nous
+on ou par pas pour qu que qui sa se ses son sur ta te tes toi ton tu un une vos votre vous c d j l à m n s t y été
+étée étées étés étant étante étants étantes suis es est sommes êtes sont serai seras sera serons serez seront serais
+serait serions seriez seraient étais était étions étiez étaient fus fut fûmes fûtes furent sois soit soyons soyez
+soient fusse fusses fût fussions fussiez fussent ayant ayante ayantes ayants eu eue eues eus ai as avons avez ont
+aurai auras aura aurons aurez auront aurais aurait aurions auriez auraient avais avait avions aviez avaient eut eûmes
+eûtes eurent aie aies ait ayons ayez aient eusse eusses eût eussions eussiez eussent""".split())
 
 _ELISIONS = {"fr": ("l", "m", "t", "qu", "n", "s", "j", "d", "c", "jusqu", "quoiqu", "lorsqu", "puisqu"),
              "it": ("c", "l", "all", "dall", "dell", "nell", "sull", "coll", "pell", "gl", "agl", "dagl",
@@ -146,9 +155,10 @@ def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_t
     if el:
         out = []
         for t in toks:
-            if "'" in t:
-                head, _, tail = t.partition("'")
-                if head in el and tail:
+            q = t.replace("\u2019", "'")        # ElisionFilter takes both apostrophes
+            if "'" in q:
+                head, _, tail = q.partition("'")
+                if head.lower() in el and tail:
                     t = tail
             out.append(t)
         toks = out
@@ -159,4 +169,9 @@ def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_t
         from .stemmer import english_possessive, porter_stem
         toks = [english_possessive(t) for t in toks]
         return [porter_stem(t) for t in toks if t not in sw and len(t) >= min_token_length]
-    return [t for t in toks if t not in sw and len(t) >= min_token_length]
+    from .stemmers import STEMMERS
+    stem = STEMMERS.get(language)
+    kept = [t for t in toks if t not in sw]
+    if stem is not None:          # the language's Lucene analyzer stems after its stop filter
+        kept = [stem(t) for t in kept]
+    return [t for t in kept if len(t) >= min_token_length]

@@ -1,0 +1,438 @@
+"""Stemmers of the per-language Lucene analyzers the reference tokenizes with (``LuceneTextAnalyzer.scala:87-126``,
+Lucene 7.3 ``*Analyzer`` chains):
+
+* French ``FrenchLightStemFilter``, German ``GermanNormalizationFilter`` + ``GermanLightStemFilter``, Spanish /
+  Italian / Portuguese ``*LightStemFilter`` and Norwegian (bokmål) ``NorwegianLightStemFilter`` -- J. Savoy's light
+  stemmers, which those analyzers use;
+* Swedish and Danish: the Snowball stemmers of ``SwedishAnalyzer`` / ``DanishAnalyzer``.
+
+Implemented from the published algorithms (Savoy, "Light stemming approaches for the French, Portuguese, German
+and Hungarian languages", SAC 2006; snowballstem.org), not from Lucene's sources; the French one is pinned by the
+reference's own expectations (``TextTokenizerTest.scala`` French fixture, ``tests/test_language.py``). English
+(Porter) is in :mod:`.stemmer`.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List
+
+_ACC_A = {"à": "a", "á": "a", "â": "a", "ä": "a"}
+_ACC_O = {"ò": "o", "ó": "o", "ô": "o", "ö": "o"}
+_ACC_E = {"è": "e", "é": "e", "ê": "e", "ë": "e"}
+_ACC_U = {"ù": "u", "ú": "u", "û": "u", "ü": "u"}
+_ACC_I = {"ì": "i", "í": "i", "î": "i", "ï": "i"}
+_ROMANCE = {**_ACC_A, **_ACC_O, **_ACC_E, **_ACC_U, **_ACC_I}
+
+
+# ------------------------------------------------------------------------------------------------ French
+_FR_NORM = {"à": "a", "á": "a", "â": "a", "ô": "o", "è": "e", "é": "e", "ê": "e", "ù": "u", "û": "u", "î": "i",
+            "ç": "c"}
+
+
+def _fr_norm(s: List[str]) -> List[str]:
+    if len(s) > 4:
+        s = [_FR_NORM.get(c, c) for c in s]
+        out = [s[0]]
+        for c in s[1:]:                       # collapse doubled letters (commission -> comision)
+            if c == out[-1] and c.isalpha():
+                continue
+            out.append(c)
+        s = out
+    if len(s) > 4 and s[-2:] == ["i", "e"]:
+        s = s[:-2]
+    if len(s) > 4:
+        if s[-1] == "r":
+            s = s[:-1]
+        if s[-1] == "e":
+            s = s[:-1]
+        if s[-1] == "e":
+            s = s[:-1]
+        if s[-1] == s[-2] and s[-1].isalpha():
+            s = s[:-1]
+    return s
+
+
+def french_light_stem(word: str) -> str:
+    s = list(word)
+    n = len
+
+    def ends(x):
+        return "".join(s[-len(x):]) == x if len(s) >= len(x) else False
+
+    if n(s) > 5 and s[-1] == "x":
+        if s[-3] == "a" and s[-2] == "u" and s[-4] != "e":
+            s[-2] = "l"
+        s = s[:-1]
+    if n(s) > 3 and s[-1] == "x":
+        s = s[:-1]
+    if n(s) > 3 and s[-1] == "s":
+        s = s[:-1]
+    if n(s) > 9 and ends("issement"):
+        s = s[:-6]
+        s[-1] = "r"
+        return "".join(_fr_norm(s))
+    if n(s) > 8 and ends("issant"):
+        s = s[:-4]
+        s[-1] = "r"
+        return "".join(_fr_norm(s))
+    if n(s) > 6 and ends("ement"):
+        s = s[:-4]
+        if n(s) > 3 and ends("ive"):
+            s = s[:-1]
+            s[-1] = "f"
+        return "".join(_fr_norm(s))
+    if n(s) > 11 and ends("ficatrice"):
+        s = s[:-5]
+        s[-2:] = ["e", "r"]
+        return "".join(_fr_norm(s))
+    if n(s) > 10 and ends("ficateur"):
+        s = s[:-4]
+        s[-2:] = ["e", "r"]
+        return "".join(_fr_norm(s))
+    if n(s) > 9 and ends("catrice"):
+        s = s[:-3]
+        s[-4:-1] = ["q", "u", "e"]
+        return "".join(_fr_norm(s))
+    if n(s) > 8 and ends("cateur"):
+        s = s[:-2]
+        s[-4:] = ["q", "u", "e", "r"]
+        return "".join(_fr_norm(s))
+    if n(s) > 8 and ends("atrice"):
+        s = s[:-4]
+        s[-2:] = ["e", "r"]
+        return "".join(_fr_norm(s))
+    if n(s) > 7 and ends("ateur"):
+        s = s[:-3]
+        s[-2:] = ["e", "r"]
+        return "".join(_fr_norm(s))
+    if n(s) > 6 and ends("trice"):
+        s = s[:-1]
+        s[-3:] = ["e", "u", "r"]
+    if n(s) > 5 and ends("ième"):
+        return "".join(_fr_norm(s[:-4]))
+    if n(s) > 7 and ends("teuse"):
+        s = s[:-2]
+        s[-1] = "r"
+        return "".join(_fr_norm(s))
+    if n(s) > 6 and ends("teur"):
+        s = s[:-1]
+        s[-1] = "r"
+        return "".join(_fr_norm(s))
+    if n(s) > 5 and ends("euse"):
+        return "".join(_fr_norm(s[:-2]))
+    if n(s) > 8 and ends("ère"):
+        s = s[:-1]
+        s[-2] = "e"
+        return "".join(_fr_norm(s))
+    if n(s) > 7 and ends("ive"):
+        s = s[:-1]
+        s[-1] = "f"
+        return "".join(_fr_norm(s))
+    if n(s) > 4 and (ends("folle") or ends("molle")):
+        s = s[:-2]
+        s[-1] = "u"
+        return "".join(_fr_norm(s))
+    if n(s) > 9 and ends("nnelle"):
+        return "".join(_fr_norm(s[:-5]))
+    if n(s) > 9 and ends("nnel"):
+        return "".join(_fr_norm(s[:-3]))
+    if n(s) > 4 and ends("ète"):
+        s = s[:-1]
+        s[-2] = "e"
+    if n(s) > 8 and ends("ique"):
+        s = s[:-4]
+    if n(s) > 8 and ends("esse"):
+        return "".join(_fr_norm(s[:-3]))
+    if n(s) > 7 and ends("inage"):
+        return "".join(_fr_norm(s[:-3]))
+    if n(s) > 9 and ends("isation"):
+        s = s[:-7]
+        if n(s) > 5 and ends("ual"):
+            s[-2] = "e"
+        return "".join(_fr_norm(s))
+    if n(s) > 9 and ends("isateur"):
+        return "".join(_fr_norm(s[:-7]))
+    if n(s) > 8 and ends("ation"):
+        return "".join(_fr_norm(s[:-5]))
+    if n(s) > 8 and ends("ition"):
+        return "".join(_fr_norm(s[:-5]))
+    return "".join(_fr_norm(s))
+
+
+# ------------------------------------------------------------------------------------------------ German
+def german_normalize(word: str) -> str:
+    """GermanNormalizationFilter: umlauts folded, ß -> ss, and 'ae' / 'oe' / 'ue' (not after q) -> a / o / u."""
+    out: List[str] = []
+    state = 0          # 0: other, 1: after a vowel that blocks, 2: after a / o / u (an 'e' next is dropped)
+    for c in word:
+        if c in "ao":
+            state = 2
+            out.append(c)
+        elif c == "u":
+            state = 2 if state == 0 else 1
+            out.append(c)
+        elif c == "e":
+            if state != 2:
+                out.append(c)
+            state = 1
+        elif c in "iqy":
+            state = 1
+            out.append(c)
+        elif c == "ä":
+            out.append("a")
+            state = 1
+        elif c == "ö":
+            out.append("o")
+            state = 1
+        elif c == "ü":
+            out.append("u")
+            state = 1
+        elif c == "ß":
+            out.append("ss")
+            state = 0
+        else:
+            state = 0
+            out.append(c)
+    return "".join(out)
+
+
+_DE_FOLD = {**_ACC_A, **_ACC_O, **_ACC_I, **_ACC_U}
+_ST_ENDING = set("bdfghklmnt")
+
+
+def german_light_stem(word: str) -> str:
+    s = [_DE_FOLD.get(c, c) for c in word]
+    n = len(s)
+    # step 1
+    if n > 5 and s[-3:] == ["e", "r", "n"]:
+        s = s[:-3]
+    elif n > 4 and s[-2] == "e" and s[-1] in "mnrs":
+        s = s[:-2]
+    elif n > 3 and s[-1] == "e":
+        s = s[:-1]
+    elif n > 3 and s[-1] == "s" and s[-2] in _ST_ENDING:
+        s = s[:-1]
+    n = len(s)
+    # step 2
+    if n > 5 and s[-3:] == ["e", "s", "t"]:
+        s = s[:-3]
+    elif n > 4 and s[-2] == "e" and s[-1] in "rn":
+        s = s[:-2]
+    elif n > 4 and s[-2:] == ["s", "t"] and s[-3] in _ST_ENDING:
+        s = s[:-2]
+    return "".join(s)
+
+
+def german_analyze_stem(word: str) -> str:
+    return german_light_stem(german_normalize(word))
+
+
+# ----------------------------------------------------------------------------------- Spanish / Italian
+def spanish_light_stem(word: str) -> str:
+    if len(word) < 5:
+        return word
+    s = [_ROMANCE.get(c, c) for c in word]
+    c = s[-1]
+    if c in "oae":
+        return "".join(s[:-1])
+    if c == "s":
+        if s[-2] == "e" and s[-3] == "s" and s[-4] == "e":
+            return "".join(s[:-2])
+        if s[-2] == "e" and s[-3] == "c":
+            s[-3] = "z"
+            return "".join(s[:-2])
+        if s[-2] in "oae":
+            return "".join(s[:-2])
+    return "".join(s)
+
+
+def italian_light_stem(word: str) -> str:
+    if len(word) < 6:
+        return word
+    s = [_ROMANCE.get(c, c) for c in word]
+    c, p = s[-1], s[-2]
+    if c == "e":
+        return "".join(s[:-2] if p in "ih" else s[:-1])
+    if c == "i":
+        return "".join(s[:-2] if p in "hi" else s[:-1])
+    if c in "ao":
+        return "".join(s[:-2] if p == "i" else s[:-1])
+    return "".join(s)
+
+
+# ---------------------------------------------------------------------------------------------- Portuguese
+_PT_FOLD = {**_ROMANCE, "ã": "a", "õ": "o", "ç": "c"}
+
+
+def _endsl(s: List[str], x: str) -> bool:
+    return len(s) >= len(x) and "".join(s[-len(x):]) == x
+
+
+def _pt_remove_suffix(s: List[str]) -> List[str]:
+    n = len(s)
+    if n > 4 and _endsl(s, "es") and s[-3] in "rslz":
+        return s[:-2]
+    if n > 3 and _endsl(s, "ns"):
+        s[-2] = "m"
+        return s[:-1]
+    if n > 4 and (_endsl(s, "eis") or _endsl(s, "éis")):
+        s[-3], s[-2] = "e", "l"
+        return s[:-1]
+    if n > 4 and _endsl(s, "ais"):
+        s[-2] = "l"
+        return s[:-1]
+    if n > 4 and _endsl(s, "óis"):
+        s[-3], s[-2] = "o", "l"
+        return s[:-1]
+    if n > 4 and _endsl(s, "is"):
+        s[-1] = "l"
+        return s
+    if n > 3 and (_endsl(s, "ões") or _endsl(s, "ães")):
+        s = s[:-1]
+        s[-2], s[-1] = "ã", "o"
+        return s
+    if n > 6 and _endsl(s, "mente"):
+        return s[:-5]
+    if n > 3 and s[-1] == "s":
+        return s[:-1]
+    return s
+
+
+def _pt_norm_feminine(s: List[str]) -> List[str]:
+    n = len(s)
+    if n > 7 and (_endsl(s, "inha") or _endsl(s, "iaca") or _endsl(s, "eira")):
+        s[-1] = "o"
+        return s
+    if n > 6:
+        if any(_endsl(s, x) for x in ("osa", "ica", "ida", "ada", "iva", "ama")):
+            s[-1] = "o"
+            return s
+        if _endsl(s, "ona"):
+            s[-3], s[-2] = "ã", "o"
+            return s[:-1]
+        if _endsl(s, "ora"):
+            return s[:-1]
+        if _endsl(s, "esa"):
+            s[-3] = "ê"
+            return s[:-1]
+        if _endsl(s, "na"):
+            s[-1] = "o"
+            return s
+    return s
+
+
+def portuguese_light_stem(word: str) -> str:
+    if len(word) < 4:
+        return word
+    s = _pt_remove_suffix(list(word))
+    if len(s) > 3 and s[-1] == "a":
+        s = _pt_norm_feminine(s)
+    if len(s) > 4 and s[-1] in "eao":
+        s = s[:-1]
+    return "".join(_PT_FOLD.get(c, c) for c in s)
+
+
+# ------------------------------------------------------------------------------------------ Norwegian
+def norwegian_light_stem(word: str) -> str:
+    """NorwegianLightStemmer, bokmål (the NorwegianAnalyzer default)."""
+    s = word
+    if len(s) > 4 and s.endswith("s"):
+        s = s[:-1]
+    n = len(s)
+    if n > 7 and (s.endswith("heter") or s.endswith("heten")):
+        return s[:-5]
+    if n > 5 and (s.endswith("dom") or s.endswith("het")):
+        return s[:-3]
+    if n > 7 and (s.endswith("elser") or s.endswith("elsen")):
+        return s[:-5]
+    if n > 6 and any(s.endswith(x) for x in ("ende", "else", "este", "eren")):
+        return s[:-4]
+    if n > 5 and any(s.endswith(x) for x in ("ere", "est", "ene")):
+        return s[:-3]
+    if n > 4 and any(s.endswith(x) for x in ("er", "en", "et", "st", "te")):
+        return s[:-2]
+    if n > 3 and s[-1] in "aen":
+        return s[:-1]
+    return s
+
+
+# ---------------------------------------------------------------------------- Snowball: Swedish / Danish
+def _r1(word: str, vowels: str) -> int:
+    """Start of Snowball's R1 (after the first non-vowel following a vowel), at least 3."""
+    for i in range(1, len(word)):
+        if word[i] not in vowels and word[i - 1] in vowels:
+            return max(3, i + 1)
+    return len(word)
+
+
+_SV_V = "aeiouyäåö"
+_SV_S1 = sorted("a arna erna heterna orna ad e ade ande arne are aste en anden aren heten ern ar er heter or as "
+                "arnas ernas ornas es ades andes ens arens hetens erns at andet het ast".split(), key=len, reverse=True)
+_SV_SEND = set("bcdfghjklmnoprtvy")
+
+
+def swedish_stem(word: str) -> str:
+    r1 = _r1(word, _SV_V)
+    w = word
+    # step 1
+    for suf in _SV_S1:
+        if w.endswith(suf) and len(w) - len(suf) >= r1:
+            w = w[:-len(suf)]
+            break
+    else:
+        if w.endswith("s") and len(w) - 1 >= r1 and len(w) >= 2 and w[-2] in _SV_SEND:
+            w = w[:-1]
+    # step 2
+    for suf in ("dd", "gd", "nn", "dt", "gt", "kt", "tt"):
+        if w.endswith(suf) and len(w) - 2 >= r1:
+            w = w[:-1]
+            break
+    # step 3
+    for suf, rep in (("fullt", "full"), ("löst", "lös"), ("lig", ""), ("els", ""), ("ig", "")):
+        if w.endswith(suf) and len(w) - len(suf) >= r1:
+            w = w[:-len(suf)] + rep
+            break
+    return w
+
+
+_DA_V = "aeiouyæåø"
+_DA_S1 = sorted("hed ethed ered e erede ende erende ene erne ere en heden eren er heder erer heds es endes erendes "
+                "enes ernes eres ens hedens erens ers ets erets et eret".split(), key=len, reverse=True)
+_DA_SEND = set("abcdfghjklmnoprtvyzå")
+
+
+def _da_step2(w: str, r1: int) -> str:
+    for suf in ("gd", "dt", "gt", "kt"):
+        if w.endswith(suf) and len(w) - 2 >= r1:
+            return w[:-1]
+    return w
+
+
+def danish_stem(word: str) -> str:
+    r1 = _r1(word, _DA_V)
+    w = word
+    for suf in _DA_S1:
+        if w.endswith(suf) and len(w) - len(suf) >= r1:
+            w = w[:-len(suf)]
+            break
+    else:
+        if w.endswith("s") and len(w) - 1 >= r1 and len(w) >= 2 and w[-2] in _DA_SEND:
+            w = w[:-1]
+    w = _da_step2(w, r1)
+    if w.endswith("igst"):
+        w = w[:-2]
+    for suf in ("elig", "lig", "els", "ig", "løst"):
+        if w.endswith(suf) and len(w) - len(suf) >= r1:
+            if suf == "løst":
+                w = w[:-1]
+            else:
+                w = _da_step2(w[:-len(suf)], r1)
+            break
+    if len(w) >= 2 and len(w) - 1 >= r1 and w[-1] == w[-2] and w[-1] not in _DA_V and w[-1].isalpha():
+        w = w[:-1]
+    return w
+
+
+STEMMERS: Dict[str, Callable[[str], str]] = {
+    "fr": french_light_stem, "de": german_analyze_stem, "es": spanish_light_stem, "it": italian_light_stem,
+    "pt": portuguese_light_stem, "no": norwegian_light_stem, "sv": swedish_stem, "da": danish_stem,
+}
