@@ -170,7 +170,7 @@ def test_xgb_epilogue_quantisation_maxima_identical_trees(monkeypatch):
 
 
 @pytest.mark.parametrize("switch", ["TMOG_PAIR_SCAN", "TMOG_FUSED_REDUCE"])
-@pytest.mark.parametrize("learner", ["xgb", "rf", "rf3"])
+@pytest.mark.parametrize("learner", ["xgb", "xgbdeep", "rf", "rf3"])
 def test_pair_scan_identical_to_subtract_then_scan(monkeypatch, learner, switch):
     """Sibling pairs' subtraction + split scan fused in one pass (pair_scan_kernel), and the node reduction
     fused into the scan's last block, grow exactly the trees of the separate kernels (hist_subtract, node-wise
@@ -184,11 +184,14 @@ def test_pair_scan_identical_to_subtract_then_scan(monkeypatch, learner, switch)
     z = X[:, 5] + X[:, 0] - 0.5 * X[:, 7] + 0.5 * torch.randn(n, generator=g)
     y = (z > 0).float() if learner != "rf3" else torch.bucketize(z, torch.tensor([-0.5, 0.5])).float()
     Xd, yd = X.cuda(), y.cuda()
-    if learner == "xgb":
+    if learner in ("xgb", "xgbdeep"):
         L = XGBoostClassifierLearner
-        params = dict(L.defaults, num_round=12, max_depth=7, eta=0.3, missing=0.0)
+        # xgbdeep: depth-10 trees with a small min_child_weight -- hundreds of nodes per level, the many-node /
+        # many-level case of the fused reduction's cross-workgroup hand-off
+        params = dict(L.defaults, num_round=12, max_depth=7, eta=0.3, missing=0.0) if learner == "xgb" else \
+            dict(L.defaults, num_round=6, max_depth=10, eta=0.3, missing=0.0, gamma=0.0)
         jobs = [FitJob(dict(params, min_child_weight=m), torch.arange(k, n, 3, device="cuda"))
-                for m in (1.0, 10.0) for k in range(3)]
+                for m in ((1.0, 10.0) if learner == "xgb" else (0.05, 0.5)) for k in range(3)]
     else:
         L = RandomForestClassifierLearner
         params = dict(L.defaults, num_trees=6, max_depth=8, feature_subset_strategy="all")   # no subsets

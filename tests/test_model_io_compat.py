@@ -208,3 +208,24 @@ def test_fresh_process_load_and_score(tmp_path):
         assert g["prediction"] == e["prediction"]
         for k in e:
             assert abs(g[k] - e[k]) < 1e-6
+
+
+def test_reader_map_key_merge_and_result_order(tmp_path):
+    """OpWorkflowModelReader: blocklisted map keys of the new and the legacy field merge with toMap
+    (the legacy list wins a shared key, no union), and result features come back in allFeatures order."""
+    import shutil
+    src = f"{REF}/OldModelVersion_0_7_1"
+    dst = tmp_path / "m"
+    shutil.copytree(src, dst)
+    part = dst / "op-model.json" / "part-00000"
+    with open(part) as f:
+        j = json.load(f)
+    j["blocklistedMapKeys"] = {"numericMap": ["gender", "x"], "other": ["a"]}
+    j["blacklistedMapKeys"] = {"numericMap": ["y"]}
+    feats = [f["uid"] for f in j["allFeatures"]]
+    j["resultFeaturesUids"] = [feats[2], feats[0]]          # reversed relative to allFeatures
+    with open(part, "w") as f:
+        json.dump(j, f)
+    m = OpWorkflowModel.load(str(dst))
+    assert m.blocklist_map_keys == {"numericMap": ["y"], "other": ["a"]}
+    assert [f.uid for f in m.result_features] == [feats[0], feats[2]]

@@ -1120,6 +1120,13 @@ __global__ void __launch_bounds__(256) split_scan_kernel(
   // goes out as agent-scope (sc1) stores by wave 0, which waits for them (vmcnt(0)) before its agent-scope
   // ticket add; the block whose add returns fbmax - 1 reads every candidate of the node with sc1 loads in
   // that same wave. No L2 write-back / L1 invalidate fences.
+  // HARDWARE ASSUMPTION (not a HIP memory-model guarantee -- every access here is relaxed): on gfx950 an
+  // sc1 store is written through to the coherence point before vmcnt reaches 0, an sc1 load is served from
+  // it, and the reader's loads cannot be hoisted above the ticket add (they are issued after the wave-uniform
+  // branch on its result, and the atomics are volatile to the compiler). The portable form -- release on
+  // the ticket add, an agent-scope acquire fence in the winning block -- costs an L2 write-back per node on
+  // this part (agent scope spans the 8 XCDs' L2s). TMOG_FUSED_REDUCE=0 selects the separate reduce launch;
+  // tests/test_gpu_kernels.py checks the two paths give identical trees over many nodes and levels.
   if (wave == 0) {
     unsigned last = 0;
     if (lane == 0) {

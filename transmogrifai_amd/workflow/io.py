@@ -276,7 +276,10 @@ def load_model(path: str, workflow=None):
     model = OpWorkflowModel(j.get("uid"), OpParams.from_string(j.get("parameters", "{}")))
     model.train_parameters = OpParams.from_string(j.get("trainParameters", "{}"))
     model.stages = fitted
-    model.result_features = [built[u] for u in j["resultFeaturesUids"] if u in built]
+    # OpWorkflowModelReader.resolveResultFeatures filters the loaded features by the result uids, so they come
+    # back in allFeatures order (not resultFeaturesUids order)
+    res_ids = set(j["resultFeaturesUids"])
+    model.result_features = [built[f["uid"]] for f in j["allFeatures"] if f.get("uid") in res_ids and f["uid"] in built]
     model.raw_features = sorted([f for f in built.values() if f.is_raw and isinstance(f.origin_stage,
                                                                                       FeatureGeneratorStage)],
                                 key=lambda f: f.name)
@@ -297,10 +300,12 @@ def load_model(path: str, workflow=None):
     lists = [j.get("blocklistedFeaturesUids") or [], j.get("blacklistedFeaturesUids") or []]
     bl = max(([bl_feats[u] for u in ids if u in bl_feats] for ids in lists), key=len)
     model.blocklist = bl
+    # resolveBlocklistMapKeys: the new and the legacy field are merged with toMap -- a key present in both takes
+    # the legacy field's list (the later entry wins), they are not unioned
     keys = {}
     for key in ("blocklistedMapKeys", "blacklistedMapKeys"):
         for k, v in (j.get(key) or {}).items():
-            keys[k] = sorted(set(keys.get(k, [])) | set(v))
+            keys[k] = sorted(set(v))
     model.blocklist_map_keys = keys
     rff = j.get("rawFeatureFilterResults")
     model.raw_feature_filter_results = decode(json.loads(rff)) if isinstance(rff, str) and rff else (rff or
