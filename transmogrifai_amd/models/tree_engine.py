@@ -40,7 +40,15 @@ assert HIST_ITEM.itemsize == 32 and PART_ITEM.itemsize == 40 and LEAF_ITEM.items
 
 ROW_MASK = 0xFFFFFF
 CSR_ITEM_ROWS = 1024          # rows per CSR histogram item (tree_grow.hpp kCsrRows)
-MAX_ROWS = 1 << 24
+MAX_ROWS = 1 << 24            # packed entries (row | weight << 24) below this many training rows
+MAX_WIDE_ROWS = 1 << 31       # wide entries (32-bit row id, weight 1)
+
+
+def wide_rows(n_rows: int) -> bool:
+    """Entry format of a training set of ``n_rows`` rows: below 2^24 rows the row id and an 8-bit weight share
+    one 32-bit entry; from 2^24 rows on (or with ``TMOG_TREE_WIDE_ROWS=1``, for tests) an entry is the row id
+    alone and weights become repeated entries (``tree_kernels.hip`` ``ent_row`` / ``ent_w``)."""
+    return n_rows >= MAX_ROWS or os.environ.get("TMOG_TREE_WIDE_ROWS") == "1"
 
 # Native per-group resource slots (stream, staging, histogram buffers; tree_grow_hip.hip slots()): grower calls
 # running concurrently from several host threads need disjoint slot ranges. A thread running a whole learner next
@@ -207,8 +215,14 @@ def prune_forest(f: Forest, max_depth: int, min_gain: float) -> Forest:
                   f.cover[order].copy(), f.tree_model.copy(), f.missing_bin)
 
 
-def pack_rows(rows: torch.Tensor, weights: Optional[torch.Tensor]) -> torch.Tensor:
-    """Pack ``row | weight << 24`` into an int32 tensor (bit pattern read as uint32 by the kernels)."""
+def pack_rows(rows: torch.Tensor, weights: Optional[torch.Tensor], wide: bool = False) -> torch.Tensor:
+    """Pack ``row | weight << 24`` into an int32 tensor (bit pattern read as uint32 by the kernels). ``wide``:
+    entries are the row ids themselves, a weight w > 1 repeating the row w times (zero-weight rows dropped)."""
+    if wide:
+        r = rows.to(torch.int64)
+        if weights is not None:
+            r = torch.repeat_interleave(r, weights.to(torch.int64).clamp(0, 255).to(r.device))
+        return r.to(torch.int32)
     r = rows.to(torch.int64)
     w = torch.ones_like(r) if weights is None else weights.to(torch.int64).clamp(0, 255)
     e = r | (w << 24)
@@ -230,7 +244,7 @@ def poisson_cdf_table(rate: float) -> List[float]:
     return out
 
 
-def bootstrap_pack(rows: torch.Tensor, seeds: Sequence[int], rate: float):
+def bootstrap_pack(rows: torch.Tensor, seeds: Sequence[int], rate: float, wide: bool = False):
     """Poisson(``rate``) bootstrap of ``rows`` for one tree per seed, packed as tree-engine root
     entries (``row | w << 24``, zero draws dropped): ``(int32 entries, int64 counts per tree)``.
 
@@ -241,7 +255,7 @@ def bootstrap_pack(rows: torch.Tensor, seeds: Sequence[int], rate: float):
     cdf = poisson_cdf_table(rate)
     rid = rows.to(torch.int64).contiguous()
     k, n = len(seeds), int(rid.numel())
-    if dev.type == "cuda" and n and k:
+    if dev.type == "cuda" and n and k and not wide:
         offs = np.asarray([_s64(int(sd) * 0x632BE59BD9B4E019 + 23 * 0x2545F4914F6CDD1D) for sd in seeds], np.int64)
         pk = _Pack(dev)
         i_o, i_c = pk.add(offs), pk.add(np.asarray(cdf, np.float64))
@@ -264,17 +278,23 @@ def bootstrap_pack(rows: torch.Tensor, seeds: Sequence[int], rate: float):
     parts, counts = [], []
     for t in range(k):
         keep = w[t] > 0
-        parts.append(pack_rows(rid[keep], w[t][keep]))
-        counts.append(int(keep.sum()))
+        parts.append(pack_rows(rid[keep], w[t][keep], wide))
+        counts.append(int(parts[-1].numel()))
     out = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int32, device=dev)
     return out, np.asarray(counts, np.int64)
 
 
-def _root_rows(jobs, dev):
+def _root_rows(jobs, dev, wide: bool = False):
     """Packed root entries of every job, zero-weight (out-of-bag) rows dropped for all weighted jobs
-    with one compaction (two host syncs per call instead of one per tree)."""
+    with one compaction (two host syncs per call instead of one per tree). ``wide``: see :func:`pack_rows`."""
     packs: List[Optional[torch.Tensor]] = [None] * len(jobs)
     counts = [0] * len(jobs)
+    if wide:
+        for k, j in enumerate(jobs):
+            packs[k] = pack_rows(j.rows.to(dev), None if j.weights is None else j.weights.to(dev), True)
+            counts[k] = int(packs[k].numel())
+        rows = torch.cat(packs) if packs else torch.zeros(0, dtype=torch.int32, device=dev)
+        return rows, counts
     wj = [k for k, j in enumerate(jobs) if j.weights is not None]
     for k, j in enumerate(jobs):
         if j.weights is None:
@@ -314,7 +334,8 @@ class _GrowArgs(C.Structure):
                 ("csr_nf", C.c_int32), ("fp_rank", C.c_int32), ("fp_world", C.c_int32), ("fp_mlo", C.c_int32),
                 ("fp_mhi", C.c_int32), ("fp_olo", C.c_int32), ("fp_ohi", C.c_int32), ("fp_comm", C.c_void_p),
                 ("fp_exchange", C.c_void_p), ("fp_ctx", C.c_void_p), ("slot_base", C.c_int32),
-                ("XbT", C.c_void_p), ("gh", C.c_void_p), ("gh_alt", C.c_void_p), ("n_entries", C.c_int64)]
+                ("XbT", C.c_void_p), ("gh", C.c_void_p), ("gh_alt", C.c_void_p), ("n_entries", C.c_int64),
+                ("wide_rows", C.c_int32)]
 
 
 class _ResidentIO(C.Structure):
@@ -395,14 +416,14 @@ def _entry_models(models: tuple, counts: tuple, dev) -> torch.Tensor:
     return t
 
 
-def _stage_gh(rows: torch.Tensor, counts, jobs, t1f, t2f, qscale, stride: int) -> torch.Tensor:
+def _stage_gh(rows: torch.Tensor, counts, jobs, t1f, t2f, qscale, stride: int, wide: bool = False) -> torch.Tensor:
     """``[total, 2]`` int32: each root entry's quantised (q(w g), q(w h)) under its job's model scales -- the
     histogram kernels' ``rintf((w * t) * qscale)`` in the same fp32 operation order (tree_kernels.hip
     stage_row), so the histograms are bit-identical to gathering t1 / t2 per row."""
     dev = rows.device
     e = rows.to(torch.int64) & 0xFFFFFFFF
-    r = e & 0xFFFFFF
-    w = (e >> 24).to(torch.float32)
+    r = e if wide else e & 0xFFFFFF
+    w = torch.ones_like(e, dtype=torch.float32) if wide else (e >> 24).to(torch.float32)
     model = _entry_models(tuple(int(j.model) for j in jobs), tuple(int(c) for c in counts), dev)
     idx = model * int(stride) + r
     qs = qscale.reshape(-1, qscale.shape[-1])[model]
@@ -542,11 +563,9 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     slot_base = int(slot_base) + slot_lane()
     Nrows, F = int(Xb.shape[0]), int(Xb.shape[1])
     chunk_rows = int(os.environ.get("TMOG_TREE_CHUNK", chunk_rows))
-    if Nrows >= MAX_ROWS:
-        # packed row entries carry a 24-bit row id (row | weight << 24): the model selector's
-        # maxTrainingSample (1M by default, Splitter.scala:178) keeps training sets far below this
-        raise ValueError(f"tree engine supports < {MAX_ROWS} (2^24) rows per training set, got {Nrows}: lower "
-                         f"maxTrainingSample or subsample before fitting tree models")
+    wide = wide_rows(Nrows)
+    if Nrows >= MAX_WIDE_ROWS:
+        raise ValueError(f"tree engine supports < 2^31 rows per training set, got {Nrows}")
     S = n_classes if mode == MODE_CLS else (3 if mode == MODE_VAR else 2)
     K = n_classes if mode == MODE_CLS else 1
     if missing_bin >= B:
@@ -570,14 +589,15 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         if len(counts) != len(jobs) or sum(counts) != int(rows.numel()):
             raise ValueError("root entries do not match the jobs")
     else:
-        rows, counts = _root_rows(jobs, dev)
+        rows, counts = _root_rows(jobs, dev, wide)
     rows_alt = torch.empty_like(rows)
-    qscale, qinv = _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev, quant_amax, quant_wmax)
+    qscale, qinv = _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev, quant_amax,
+                                 1.0 if wide else quant_wmax)
     total = int(rows.numel())
     gh = gh_alt = None
     if on_gpu and mode == MODE_GH and total and t1f is not None and t2f is not None \
             and os.environ.get("TMOG_GH_STAGE", "1") != "0":
-        gh = _stage_gh(rows, counts, jobs, t1f, t2f, qscale, stride)
+        gh = _stage_gh(rows, counts, jobs, t1f, t2f, qscale, stride, wide)
         gh_alt = torch.empty_like(gh)
     leaf_rows = torch.empty(max(total, 1), dtype=torch.int32, device=dev) if collect_leaves else None
     leaf_gid = torch.empty(max(total, 1), dtype=torch.int32, device=dev) if collect_leaves else None
@@ -620,10 +640,11 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                   C.cast(fp_comm, C.c_void_p) if fp_comm is not None else None,
                   C.cast(fp_cb, C.c_void_p) if fp_cb is not None else None, None, int(slot_base),
                   N.ptr(XbT) if (on_gpu and XbT is not None) else None,
-                  N.ptr(gh) if gh is not None else None, N.ptr(gh_alt) if gh_alt is not None else None, total)
+                  N.ptr(gh) if gh is not None else None, N.ptr(gh_alt) if gh_alt is not None else None, total,
+                  int(wide))
     lib = N.hip() if on_gpu else N.host()
     if resident and on_gpu and ng == 1 and collect_leaves:
-        rt = _grow_resident(lib, a, jobs, mode, kind, S, missing_bin, leaf_rows, leaf_gid, dev, total)
+        rt = _grow_resident(lib, a, jobs, mode, kind, S, missing_bin, leaf_rows, leaf_gid, dev, total, wide)
         if rt is not None:
             return rt
     fn = (lambda name: getattr(lib, f"tmog_hip_{name}")) if on_gpu else (lambda name: getattr(lib, f"tmog_{name}_cpu"))
@@ -656,16 +677,17 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     if collect_leaves:
         if ng == 1:
             r_, g_, v_, t_ = las[0]
-            forest.leaf_assign = LeafAssign(r_, g_, v_, t_)
+            forest.leaf_assign = LeafAssign(r_, g_, v_, t_, wide)
         else:
             goff = np.concatenate([[0], np.cumsum([int(x[2].shape[0]) for x in las])[:-1]])
             forest.leaf_assign = LeafAssign(torch.cat([x[0] for x in las]),
                                             torch.cat([x[1] + int(o) for x, o in zip(las, goff)]),
-                                            torch.cat([x[2] for x in las]), torch.cat([x[3] for x in las]))
+                                            torch.cat([x[2] for x in las]), torch.cat([x[3] for x in las]), wide)
     return forest
 
 
-def _grow_resident(lib, a, jobs, mode, kind, S, missing_bin, leaf_rows, leaf_gid, dev, total) -> Optional[ResidentTree]:
+def _grow_resident(lib, a, jobs, mode, kind, S, missing_bin, leaf_rows, leaf_gid, dev, total,
+                   wide: bool = False) -> Optional[ResidentTree]:
     cap = int(lib.tmog_hip_resident_cap_nodes(C.byref(a)))
     if cap <= 0:
         return None
@@ -682,7 +704,7 @@ def _grow_resident(lib, a, jobs, mode, kind, S, missing_bin, leaf_rows, leaf_gid
         msg = C.create_string_buffer(512)
         lib.tmog_hip_resident_error(msg, 512)
         raise RuntimeError(f"device-planned tree growth failed: {msg.value.decode(errors='replace')}")
-    la = LeafAssign(leaf_rows[:total], leaf_gid[:total], gid_value, gid_tree)
+    la = LeafAssign(leaf_rows[:total], leaf_gid[:total], gid_value, gid_tree, wide)
     return ResidentTree(la, rec, list(jobs), mode, kind, S, missing_bin)
 
 
@@ -695,8 +717,11 @@ class LeafAssign:
     gid: torch.Tensor
     value: torch.Tensor
     tree: torch.Tensor
+    wide: bool = False          # entries are plain row ids (training sets of >= 2^24 rows)
 
     def row_ids(self) -> torch.Tensor:
+        if self.wide:
+            return self.rows.to(torch.int64) & 0xFFFFFFFF
         return (self.rows & 0xFFFFFF).to(torch.int64)
 
     def entry_tree(self) -> torch.Tensor:

@@ -261,7 +261,8 @@ class _ForestLearner(Learner):
                     seed = int(p.get("seed", 0)) + 7919 * row_keys.setdefault(rk, len(row_keys))
                     key = (rk, seed, nt, rate)
                     if key not in boot:
-                        packed, cnts = TE.bootstrap_pack(rows, [seed * 1009 + t for t in range(nt)], rate)
+                        packed, cnts = TE.bootstrap_pack(rows, [seed * 1009 + t for t in range(nt)], rate,
+                                                         TE.wide_rows(int(Xb.shape[0])))
                         boot[key] = (packed, cnts, np.concatenate([[0], np.cumsum(cnts)]))
                     packed, cnts, offs = boot[key]
                     for t in range(nt):
@@ -808,7 +809,7 @@ class XGBoostClassifierLearner(_BoostLearner):
                     key = tuple(act)
                     if key not in root_cache:
                         root_cache.clear()
-                        root_cache[key] = TE._root_rows(tjobs, dev)
+                        root_cache[key] = TE._root_rows(tjobs, dev, TE.wide_rows(int(Xg.shape[0])))
                     packed, cnts = root_cache[key]
                     root = (packed.clone(), cnts)
                 t_1 = tick()
@@ -926,7 +927,8 @@ class XGBoostClassifierLearner(_BoostLearner):
         NV.check(NV.hip().tmog_hip_boost_epilogue(
             NV.ptr(la.rows), NV.ptr(la.gid), int(la.rows.numel()), NV.ptr(val), NV.ptr(la.tree.contiguous()),
             NV.ptr(tree_job), int(N), NV.ptr(Fm), NV.ptr(G), NV.ptr(H), NV.ptr(yf), self.objective_code,
-            NV.ptr(counts), int(bins), int(val.shape[0]), len(act), int(P), NV.stream(dev), NV.ptr(amax)),
+            NV.ptr(counts), int(bins), int(val.shape[0]), len(act), int(P), NV.stream(dev), NV.ptr(amax),
+            int(getattr(la, "wide", False))),
             "boost_epilogue")
         return counts
 

@@ -29,10 +29,10 @@ F32 = C.c_float
 _HOST_SIGS = {
     "tmog_tree_finalize_cpu": [I64, I32, P, P, P, P, P, P, I32, P, P, I32, I32, I32, P, P, P, I32, P, P, P, P, P,
                                P, P],
-    "tmog_hist_build_cpu": [P, I64, I32, P, I32, P, P, P, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P],
+    "tmog_hist_build_cpu": [P, I64, I32, P, I32, P, P, P, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32],
     "tmog_split_find_cpu": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, P, P, P, I64, I32, I32,
                             I32],
-    "tmog_partition_cpu": [P, I32, P, P, I32, P, P, P, P, P, I32, P, P],
+    "tmog_partition_cpu": [P, I32, P, P, I32, P, P, P, P, P, I32, P, P, I32],
     "tmog_forest_predict_cpu": [P, I32, I32, P, P, P, P, P, P, P, I32, P, I32, P],
     "tmog_find_splits_cpu": [P, I64, I32, I32, P, P],
     "tmog_murmur3_batch": [P, P, I64, I32, P],
@@ -62,7 +62,7 @@ _HOST_SIGS = {
 
 _HIP_SIGS = {
     "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P, P, I32, I32, I32, P,
-                            P, P],
+                            P, P, I32],
     "tmog_hip_hist_stat_chunk": [I32, I32],
     "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
     "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P, I32, P,
@@ -71,7 +71,7 @@ _HIP_SIGS = {
     "tmog_hip_rccl_unique_id": [P, I32],
     "tmog_hip_rccl_comm_init": [P, I32, I32],
     "tmog_hip_rccl_comm_destroy": [P],
-    "tmog_hip_partition_fused": [P, I32, P, P, P, I32, P, P, P, P, P, P, P, I32, P, P, I64, P, P, P, P],
+    "tmog_hip_partition_fused": [P, I32, P, P, P, I32, P, P, P, P, P, P, P, I32, P, P, I64, P, P, P, P, I32],
     "tmog_hip_leaf_collect": [P, P, I32, P, P, P, P, P],
     "tmog_hip_grow_forest": [P],
     "tmog_hip_grow_resident": [P, P],
@@ -84,7 +84,7 @@ _HIP_SIGS = {
     "tmog_hip_grow_free": [P],
     "tmog_hip_zero_segments": [P, P, P, I32, I64, I64, I32, I32, P, I32, P],
     "tmog_hip_grow_timing": [P, I32],
-    "tmog_hip_boost_epilogue": [P, P, I64, P, P, P, I64, P, P, P, P, I32, P, I32, I64, I64, I64, P, P],
+    "tmog_hip_boost_epilogue": [P, P, I64, P, P, P, I64, P, P, P, P, I32, P, I32, I64, I64, I64, P, P, I32],
     "tmog_hip_aupr_counts": [P, I32, I32, P, P],
     "tmog_hip_owlqn_direction": [P, P, P, P, P, P, I32, I32, I32, I32, P, P, P, P, P],
     "tmog_hip_owlqn_candidate": [P, P, P, P, P, P, I32, I32, P, P, P, P],

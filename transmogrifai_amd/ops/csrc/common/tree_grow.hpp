@@ -151,6 +151,9 @@ struct GrowArgs {
   int32_t* gh;
   int32_t* gh_alt;
   int64_t n_entries;
+  // training sets of >= 2^24 rows: entries are plain 32-bit row ids of weight 1 instead of row | weight << 24
+  // (weighted roots are expanded into repeated entries by the caller, models/tree_engine.py)
+  int32_t wide_rows;
 };
 
 // Feature-parallel split record, one per node and rank:

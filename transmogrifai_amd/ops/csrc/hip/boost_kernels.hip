@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
     const float* __restrict__ gid_value, const int64_t* __restrict__ gid_tree, const int64_t* __restrict__ tree_job,
     int64_t N, double* __restrict__ F, float* __restrict__ G, float* __restrict__ H, const float* __restrict__ y,
     int objective, int32_t* __restrict__ auc_hist, int bins, int64_t n_gid, int64_t n_trees, int64_t P,
-    uint32_t* __restrict__ amax) {
+    uint32_t* __restrict__ amax, int wide) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float ag = 0.f, ah = 0.f;                    // this lane's |g| and h (for the next round's quantisation)
   // no early returns: the AuPR-count aggregation below needs every lane of the wave
@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
   int64_t r = 0, t = 0, p = 0;
   int32_t g_id = 0;
   if (ok) {
-    r = entries[e] & 0xFFFFFFu;
+    r = wide ? (int64_t)entries[e] : (int64_t)(entries[e] & 0xFFFFFFu);   // tree_kernels.hip ent_row
     g_id = gid[e];
     ok = g_id >= 0 && g_id < n_gid && r < N;   // defensive: never index out of range
   }
@@ -307,12 +307,12 @@ extern "C" {
 int tmog_hip_boost_epilogue(const uint32_t* entries, const int32_t* gid, int64_t n_entries, const float* gid_value,
                             const int64_t* gid_tree, const int64_t* tree_job, int64_t N, double* F, float* G, float* H,
                             const float* y, int objective, int32_t* auc_hist, int bins, int64_t n_gid,
-                            int64_t n_trees, int64_t P, hipStream_t stream, uint32_t* amax) {
+                            int64_t n_trees, int64_t P, hipStream_t stream, uint32_t* amax, int wide_rows) {
   if (n_entries == 0) return 0;
-  if (N >= (1 << 24)) return -2;
+  if (N >= (1 << 24) && !wide_rows) return -2;
   hipLaunchKernelGGL(boost_epilogue_kernel, dim3((unsigned)((n_entries + 255) / 256)), dim3(256), 0, stream, entries,
                      gid, n_entries, gid_value, gid_tree, tree_job, N, F, G, H, y, objective, auc_hist, bins, n_gid,
-                     n_trees, P, amax);
+                     n_trees, P, amax, wide_rows);
   return (int)hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
-                        hipStream_t stream, const int32_t* gh, const int* dcount);
+                        hipStream_t stream, const int32_t* gh, const int* dcount, int wide_rows);
 int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
                            const int64_t* out_off, const int64_t* size, int n, int64_t max_size, int64_t dense,
                            int per, int S, hipStream_t stream);
@@ -52,7 +52,8 @@ int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, 
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                              const int32_t* split_bin, const uint8_t* dl, const float* node_params,
                              const float* split_gain, int missing_bin, int64_t* cursors, const uint8_t* XbT, int64_t N,
-                             hipStream_t stream, const int32_t* gh_in, int32_t* gh_out, const int* dcount);
+                             hipStream_t stream, const int32_t* gh_in, int32_t* gh_out, const int* dcount,
+                             int wide_rows);
 int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
                           int32_t* out_gid, hipStream_t stream, const uint32_t* rows_alt, const int* dcount);
 }
@@ -186,7 +187,7 @@ struct GpuBackend {
     if (n_items)
       kchk(tmog_hip_hist_build(g.Xb, g.F, rows, items, n_items, nfo, flist, nmd, nho, hist, g.B, g.mode, g.S, g.y,
                                g.t1, g.t2, g.stride, g.qscale, g.mode == 2 ? g.missing_bin : -1, g.csr_ptr,
-                               g.csr_col, Sc, n_wide, need_general, sl.stream, gh_of(rows), nullptr),
+                               g.csr_col, Sc, n_wide, need_general, sl.stream, gh_of(rows), nullptr, g.wide_rows),
            "hist_build");
   }
   int stat_chunk(int B, int S) const { return tmog_hip_hist_stat_chunk(B, S); }
@@ -261,7 +262,7 @@ struct GpuBackend {
     int32_t* go = gh_of(rows_alt);
     if ((gi == nullptr) != (go == nullptr)) gi = go = nullptr;
     kchk(tmog_hip_partition_fused(g.Xb, g.F, rows, rows_alt, items, n, nb, nc, feat, bin, dl, params, gain,
-                                  g.missing_bin, cursors, g.XbT, g.N, sl.stream, gi, go, nullptr),
+                                  g.missing_bin, cursors, g.XbT, g.N, sl.stream, gi, go, nullptr, g.wide_rows),
          "partition_fused");
   }
   void partition_nodes(const tmog::GrowArgs&, const uint32_t*, uint32_t*, int, const int64_t*, const int64_t*,

@@ -50,20 +50,27 @@ struct HistItem {
 //   MODE 0 (class counts):   q0 = w, q1 = class
 //   MODE 1 (variance stats): q0 = w, q1 = q(w*t), q2 = q(w*t*t)
 //   MODE 2 (grad / hess):    q0 = q(w*g), q1 = q(w*h)
+// Entry decoding. Packed (default): row | weight << 24 (rows < 2^24). Wide rows (training sets of >= 2^24
+// rows, GrowArgs.wide_rows): the entry is the 32-bit row id and every entry weighs 1 -- weighted roots are
+// expanded into repeated entries by the host (models/tree_engine.py), which adds the same integer
+// statistics to every histogram.
+__device__ __forceinline__ uint32_t ent_row(uint32_t e, int wide) { return wide ? e : (e & 0xFFFFFFu); }
+__device__ __forceinline__ uint32_t ent_w(uint32_t e, int wide) { return wide ? 1u : (e >> 24); }
+
 template <int MODE>
 __device__ __forceinline__ int4 stage_row(uint32_t e, int64_t model, int64_t stride, const float* __restrict__ y,
                                           const float* __restrict__ t1, const float* __restrict__ t2,
-                                          const float* __restrict__ qs) {
-  const int64_t r = e & 0xFFFFFFu;
-  const float w = (float)(e >> 24);
+                                          const float* __restrict__ qs, int wide) {
+  const int64_t r = ent_row(e, wide);
+  const float w = (float)ent_w(e, wide);
   int4 s;
   s.x = (int)e;
   if (MODE == 0) {
-    s.y = (int)(e >> 24); s.z = (int)y[r]; s.w = 0;
+    s.y = (int)ent_w(e, wide); s.z = (int)y[r]; s.w = 0;
   } else if (MODE == 1) {
     const float t = t1[model * stride + r];
     const float wt = w * t;
-    s.y = (int)(e >> 24);
+    s.y = (int)ent_w(e, wide);
     s.z = (int)rintf(wt * qs[1]);
     s.w = (int)rintf((wt * t) * qs[2]);
   } else {
@@ -178,7 +185,7 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
                                               const float* __restrict__ qscale, int skip_bin,
                                               const int64_t* __restrict__ csr_ptr,
                                               const uint16_t* __restrict__ csr_col, int* lds,
-                                              const int2* __restrict__ gh) {
+                                              const int2* __restrict__ gh, int wide) {
   const int nf = it.nf;
   int* a0 = lds;            // bin-0 sum of q(w g) per column
   int* a1 = lds + nf;       // bin-0 sum of q(w h)
@@ -209,14 +216,14 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
   if ((int64_t)wave * 64 < cnt) {
     const int64_t i0 = min((int64_t)wave * 64 + lane, cnt - 1);
     e_n = rp[i0];
-    const int64_t r = e_n & 0xFFFFFFu;
+    const int64_t r = ent_row(e_n, wide);
     if (ghp) q_n = ghp[i0];
     else { g_n = t1m[r]; h_n = t2m[r]; }
     p0_n = csr_ptr[r]; p1_n = csr_ptr[r + 1];
   }
   for (int64_t base = (int64_t)wave * 64; base < cnt; base += step) {
     const int nrows = (int)min((int64_t)64, cnt - base);
-    const float wt = (float)(e_n >> 24);
+    const float wt = (float)ent_w(e_n, wide);
     int4 mine;
     mine.x = (int)e_n;
     mine.y = ghp ? q_n.x : (int)rintf((wt * g_n) * qs[0]);
@@ -256,7 +263,7 @@ __device__ __forceinline__ void hist_csr_item(const HistItem& it, const uint32_t
       }
       __builtin_amdgcn_sched_barrier(0);
       if (j0 == 0 && more) {
-        const int64_t r = e_n & 0xFFFFFFu;
+        const int64_t r = ent_row(e_n, wide);
         if (ghp) q_n = ghp[i_n];
         else { g_n = t1m[r]; h_n = t2m[r]; }
         p0_n = csr_ptr[r]; p1_n = csr_ptr[r + 1];
@@ -330,7 +337,7 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
                                                const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
                                                int B, const float* __restrict__ t1, const float* __restrict__ t2,
                                                int64_t stride, const float* __restrict__ qscale, int skip_bin,
-                                               int* lds, const int2* __restrict__ gh) {
+                                               int* lds, const int2* __restrict__ gh, int wide) {
   const int FG = it.nf;
   const int ND = (FG + 3) >> 2;                    // dwords of the group's row segment (<= 16)
   const int NP = ND <= 1 ? 1 : ND <= 2 ? 2 : ND <= 4 ? 4 : ND <= 8 ? 8 : 16;
@@ -376,13 +383,13 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
     e_n = rp[i0];
     if (ghp) q_n = ghp[i0];
     else {
-      g_n = t1m[e_n & 0xFFFFFFu];
-      h_n = t2m[e_n & 0xFFFFFFu];
+      g_n = t1m[ent_row(e_n, wide)];
+      h_n = t2m[ent_row(e_n, wide)];
     }
   }
   for (int64_t base = (int64_t)wave * 64; base < cnt; base += step) {
     const int nrows = (int)min((int64_t)64, cnt - base);
-    const float wt = (float)(e_n >> 24);
+    const float wt = (float)ent_w(e_n, wide);
     int4 mine;
     mine.x = (int)e_n;
     mine.y = ghp ? q_n.x : (int)rintf((wt * g_n) * qs[0]);
@@ -411,13 +418,14 @@ __device__ __forceinline__ void hist_wide_item(const HistItem& it, const uint8_t
       uint32_t off[kWideU], w[kWideU];
 #pragma unroll
       for (int u = 0; u < kWideU; ++u)
-        off[u] = __umul24((uint32_t)stage[min(u * RPI + rs, 63)].z & 0xFFFFFFu, (uint32_t)F) + lane_off;
+        off[u] = (wide ? (uint32_t)stage[min(u * RPI + rs, 63)].z * (uint32_t)F     // < 2^31 (grower guard)
+                       : __umul24((uint32_t)stage[min(u * RPI + rs, 63)].z & 0xFFFFFFu, (uint32_t)F)) + lane_off;
 #pragma unroll
       for (int u = 0; u < kWideU; ++u) w[u] = __builtin_amdgcn_raw_buffer_load_b32(xrs, (int)off[u], 0, 0);
       __builtin_amdgcn_sched_barrier(0);       // keep the next chunk's statistic loads behind the gathers
       if (more && !ghp) {
-        g_n = t1m[e_n & 0xFFFFFFu];
-        h_n = t2m[e_n & 0xFFFFFFu];
+        g_n = t1m[ent_row(e_n, wide)];
+        h_n = t2m[ent_row(e_n, wide)];
       }
       __builtin_amdgcn_sched_barrier(0);
       // branch-free: masked-off work (rows past the chunk, pad features) adds 0 to the lane's own word
@@ -497,12 +505,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
     int B, const float* __restrict__ t1, const float* __restrict__ t2, int64_t stride,
-    const float* __restrict__ qscale, int skip_bin, const int2* __restrict__ gh) {
+    const float* __restrict__ qscale, int skip_bin, const int2* __restrict__ gh, int wide) {
   extern __shared__ int lds_w[];
   if (g_hist_debug & 2) return;
   const HistItem it = items[blockIdx.x];
   hist_wide_item(it, Xb, F, feat_list[node_feat_off[it.node] + it.fg0], rows, node_model, node_hist_off, hist, B,
-                 t1, t2, stride, qscale, skip_bin, lds_w, gh);
+                 t1, t2, stride, qscale, skip_bin, lds_w, gh, wide);
 }
 
 
@@ -515,7 +523,8 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
     int B, int S, const float* __restrict__ y, const float* __restrict__ t1, const float* __restrict__ t2,
     int64_t stride, const float* __restrict__ qscale, int skip_bin, const int64_t* __restrict__ csr_ptr,
-    const uint16_t* __restrict__ csr_col, int Sc, const int2* __restrict__ gh, const int* __restrict__ dcount) {
+    const uint16_t* __restrict__ csr_col, int Sc, const int2* __restrict__ gh, const int* __restrict__ dcount,
+    int wide) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
   // dcount (device-planned levels, tree_resident.hip): the grid is an upper bound, the item count is on the device
   if (dcount != nullptr && (int)blockIdx.x >= *dcount) return;
@@ -528,12 +537,12 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
   }
   if (MODE == 2 && (it.excl & 4)) {
     hist_csr_item(it, rows, node_model, node_hist_off, hist, B, S, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                  csr_col, lds, gh);
+                  csr_col, lds, gh, wide);
     return;
   }
   if (MODE == 2 && (it.excl & 16)) {
     hist_wide_item(it, Xb, F, feat_list[node_feat_off[it.node] + it.fg0], rows, node_model, node_hist_off, hist, B,
-                   t1, t2, stride, qscale, skip_bin, lds, gh);
+                   t1, t2, stride, qscale, skip_bin, lds, gh, wide);
     return;
   }
   if constexpr (!GEN) {
@@ -576,7 +585,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
       const int2 q = gh[it.begin + ri];
       mine = make_int4((int)rp[ri], q.x, q.y, 0);
     } else {
-      mine = stage_row<MODE>(rp[ri], model, stride, y, t1, t2, qs);
+      mine = stage_row<MODE>(rp[ri], model, stride, y, t1, t2, qs, wide);
     }
     stage[lane] = mine;
     if (sparse) {
@@ -597,7 +606,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
 #pragma unroll
         for (int u = 0; u < 8; ++u) st[u] = stage[min(j0 + u * R + rsub, 63)];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) bin[u] = (int)Xb[(int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F + feat];
+        for (int u = 0; u < 8; ++u) bin[u] = (int)Xb[(int64_t)ent_row((uint32_t)st[u].x, wide) * F + feat];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const bool hit = j0 + u * R + rsub < nrows && bin[u] == 0;
@@ -614,7 +623,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
 #pragma unroll
       for (int u = 0; u < HIST_U; ++u) st[u] = stage[min(j0 + u * R + rsub, 63)];
 #pragma unroll
-      for (int u = 0; u < HIST_U; ++u) bin[u] = (int)Xb[(int64_t)((uint32_t)st[u].x & 0xFFFFFFu) * F + feat];
+      for (int u = 0; u < HIST_U; ++u) bin[u] = (int)Xb[(int64_t)ent_row((uint32_t)st[u].x, wide) * F + feat];
 #pragma unroll
       for (int u = 0; u < HIST_U; ++u)
         if (active && j0 + u * R + rsub < nrows && bin[u] != skip_bin) add_row<MODE>(my, bin[u], S, s0, sc, st[u]);
@@ -1473,7 +1482,7 @@ __global__ void __launch_bounds__(256) partition_fused_kernel(
     const int32_t* __restrict__ split_feat, const int32_t* __restrict__ split_bin, const uint8_t* __restrict__ dl,
     const float* __restrict__ node_params, const float* __restrict__ split_gain, int missing_bin,
     unsigned long long* __restrict__ cursors, const uint8_t* __restrict__ XbT, int64_t Nt,
-    const int2* __restrict__ gh_in, int2* __restrict__ gh_out, const int* __restrict__ dcount) {
+    const int2* __restrict__ gh_in, int2* __restrict__ gh_out, const int* __restrict__ dcount, int wide) {
   if (dcount != nullptr && (int)blockIdx.x >= *dcount) return;
   const PartItem it = items[blockIdx.x];
   const int j = it.node;
@@ -1503,7 +1512,7 @@ __global__ void __launch_bounds__(256) partition_fused_kernel(
     uint8_t bn[PART_U];
 #pragma unroll
     for (int u = 0; u < PART_U; ++u)
-      bn[u] = XbT ? XbT[(int64_t)f * Nt + (e[u] & 0xFFFFFFu)] : Xb[(int64_t)(e[u] & 0xFFFFFFu) * F + f];
+      bn[u] = XbT ? XbT[(int64_t)f * Nt + ent_row(e[u], wide)] : Xb[(int64_t)ent_row(e[u], wide) * F + f];
     int wpre[PART_U];
 #pragma unroll
     for (int u = 0; u < PART_U; ++u) {
@@ -1838,7 +1847,7 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
-                        hipStream_t stream, const int32_t* gh_words, const int* dcount) {
+                        hipStream_t stream, const int32_t* gh_words, const int* dcount, int wide_rows) {
   if (n_items == 0) return 0;
   if (dcount != nullptr && n_wide != 0) return -2;   // device-counted launches: one mixed launch
   const int2* gh = reinterpret_cast<const int2*>(gh_words);
@@ -1867,10 +1876,10 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
     static const int occ = [] { const char* e = std::getenv("TMOG_HIST_WIDE_OCC"); return e ? std::atoi(e) : 6; }();
     if (occ >= 7)
       hipLaunchKernelGGL(hist_wide_kernel<7>, dim3(n_wide), dim3(256), lds, stream, Xb, F, rows, it, node_feat_off,
-                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin, gh);
+                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin, gh, wide_rows);
     else
       hipLaunchKernelGGL(hist_wide_kernel<6>, dim3(n_wide), dim3(256), lds, stream, Xb, F, rows, it, node_feat_off,
-                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin, gh);
+                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin, gh, wide_rows);
     it += n_wide;
     n_items -= n_wide;
     if (n_items == 0) return (int)hipGetLastError();
@@ -1879,19 +1888,19 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
   if (mode == 0)
     hipLaunchKernelGGL(hist_build_kernel<0>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc,
-                       nullptr, dcount);
+                       nullptr, dcount, wide_rows);
   else if (mode == 1)
     hipLaunchKernelGGL(hist_build_kernel<1>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc,
-                       nullptr, dcount);
+                       nullptr, dcount, wide_rows);
   else if (need_general)
     hipLaunchKernelGGL(hist_build_kernel<2>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                       csr_col, Sc, gh, dcount);
+                       csr_col, Sc, gh, dcount, wide_rows);
   else
     hipLaunchKernelGGL((hist_build_kernel<2, false>), grid, block, lds, stream, Xb, F, rows, it, node_feat_off,
                        feat_list, node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                       csr_col, Sc, gh, dcount);
+                       csr_col, Sc, gh, dcount, wide_rows);
   return (int)hipGetLastError();
 }
 
@@ -2038,13 +2047,14 @@ int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, 
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                              const int32_t* split_bin, const uint8_t* dl, const float* node_params,
                              const float* split_gain, int missing_bin, int64_t* cursors, const uint8_t* XbT,
-                             int64_t N, hipStream_t stream, const int32_t* gh_in, int32_t* gh_out, const int* dcount) {
+                             int64_t N, hipStream_t stream, const int32_t* gh_in, int32_t* gh_out, const int* dcount,
+                             int wide_rows) {
   if (n_items == 0) return 0;
   if ((gh_in != nullptr) != (gh_out != nullptr)) return -2;
   hipLaunchKernelGGL(partition_fused_kernel, dim3(n_items), dim3(256), 0, stream, Xb, F, rows_in, rows_out,
                      (const PartItem*)items, node_begin, node_count, split_feat, split_bin, dl, node_params,
                      split_gain, missing_bin, (unsigned long long*)cursors, XbT, N,
-                     reinterpret_cast<const int2*>(gh_in), reinterpret_cast<int2*>(gh_out), dcount);
+                     reinterpret_cast<const int2*>(gh_in), reinterpret_cast<int2*>(gh_out), dcount, wide_rows);
   return (int)hipGetLastError();
 }
 

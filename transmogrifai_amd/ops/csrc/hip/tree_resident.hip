@@ -35,7 +35,7 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
-                        hipStream_t stream, const int32_t* gh, const int* dcount);
+                        hipStream_t stream, const int32_t* gh, const int* dcount, int wide_rows);
 int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
@@ -58,7 +58,8 @@ int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, 
                              int n_items, const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                              const int32_t* split_bin, const uint8_t* dl, const float* node_params,
                              const float* split_gain, int missing_bin, int64_t* cursors, const uint8_t* XbT, int64_t N,
-                             hipStream_t stream, const int32_t* gh_in, int32_t* gh_out, const int* dcount);
+                             hipStream_t stream, const int32_t* gh_in, int32_t* gh_out, const int* dcount,
+                             int wide_rows);
 int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
                           int32_t* out_gid, hipStream_t stream, const uint32_t* rows_alt, const int* dcount);
 }
@@ -1001,7 +1002,7 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
       kchk(tmog_hip_hist_build(a.Xb, a.F, rows[c], P.hitems, (int)std::min(hist_bound(a, L, n_sc, total, mb), cp.cap_h),
                                P.nfo, flist_d, P.nmd[c], P.nho[c], hist[c], B, a.mode, S, a.y, a.t1, a.t2, a.stride,
                                a.qscale, a.mode == 2 ? a.missing_bin : -1, a.csr_ptr, a.csr_col, S, 0,
-                               need_general ? 1 : 0, st, use_gh ? gh[c] : nullptr, cnt + C_NH),
+                               need_general ? 1 : 0, st, use_gh ? gh[c] : nullptr, cnt + C_NH, a.wide_rows),
            "hist_build");
       if (d > 0)
         kchk(tmog_hip_pair_scan(hist[c], hist[c ^ 1], P.poff, P.sj, P.bj, (int)std::max<int64_t>(1, mb / 2), P.nho[c],
@@ -1016,7 +1017,8 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
       kchk(tmog_hip_partition_fused(a.Xb, a.F, rows[c], rows[c ^ 1], P.citems,
                                     (int)std::min<int64_t>(total / tmog::kPartRows + mb + 1, cp.cap_c), P.nb[c],
                                     P.nc[c], r_feat, r_bin, r_dl, P.par[c], r_gain, a.missing_bin, r_cur, a.XbT, a.N,
-                                    st, use_gh ? gh[c] : nullptr, use_gh ? gh[c ^ 1] : nullptr, cnt + C_NC),
+                                    st, use_gh ? gh[c] : nullptr, use_gh ? gh[c ^ 1] : nullptr, cnt + C_NC,
+                                    a.wide_rows),
            "partition_fused");
     }
     Fa.T = T;

@@ -4,7 +4,8 @@
 // data layout exactly (see transmogrifai_amd/models/tree_engine.py for the orchestration):
 //
 //   Xb        uint8 [N][F] row-major binned feature matrix
-//   rows      uint32 packed row entries: (row & 0xFFFFFF) | (weight << 24)
+//   rows      uint32 packed row entries: (row & 0xFFFFFF) | (weight << 24); with wide = 1 (training sets of
+//             >= 2^24 rows) the 32-bit row id, weight 1
 //   nodes     j = 0..n_nodes-1 : [node_begin[j], node_begin[j]+node_count[j]) slice of `rows`
 //   features  node j histograms features feat_list[node_feat_off[j] + 0 .. node_nfeat[j]-1]
 //   hist      int64 fixed point [node_hist_off[j] + (fl * B + bin) * S + s]; value = hist * qinv[model][s]
@@ -37,7 +38,7 @@ int tmog_hist_build_cpu(const uint8_t* Xb, int64_t N, int F, const uint32_t* row
                         const int64_t* node_begin, const int64_t* node_count, const int32_t* node_feat_off,
                         const int32_t* node_nfeat, const int32_t* feat_list, const int32_t* node_model,
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
-                        const float* t1, const float* t2, int64_t model_stride, const float* qscale) {
+                        const float* t1, const float* t2, int64_t model_stride, const float* qscale, int wide) {
   (void)N;
 #pragma omp parallel for schedule(dynamic, 1)
   for (int j = 0; j < n_nodes; ++j) {
@@ -50,15 +51,17 @@ int tmog_hist_build_cpu(const uint8_t* Xb, int64_t N, int F, const uint32_t* row
     const float* qs = qscale + model * S;
     for (int64_t i = 0; i < cnt; ++i) {
       const uint32_t e = rows[b0 + i];
-      const int64_t r = e & 0xFFFFFFu;
-      const float w = (float)(e >> 24);
+      // packed row | weight << 24, or (wide: >= 2^24-row training sets) the row itself with weight 1
+      const int64_t r = wide ? (int64_t)e : (int64_t)(e & 0xFFFFFFu);
+      const int64_t wi = wide ? 1 : (int64_t)(e >> 24);
+      const float w = (float)wi;
       int64_t st[kMaxS];
       if (mode == 0) {
-        st[(int)y[r]] = (int64_t)(e >> 24);
+        st[(int)y[r]] = wi;
       } else if (mode == 1) {
         const float t = stat_target(t1, model, model_stride, r);
         const float wt = w * t;
-        st[0] = (int64_t)(e >> 24);
+        st[0] = wi;
         st[1] = (int64_t)(int)rintf(wt * qs[1]);
         st[2] = (int64_t)(int)rintf((wt * t) * qs[2]);
       } else {
@@ -206,7 +209,7 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
 int tmog_partition_cpu(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, int n_nodes,
                        const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                        const int32_t* split_bin, const uint8_t* default_left, int missing_bin,
-                       const int64_t* out_begin, int64_t* out_left_count) {
+                       const int64_t* out_begin, int64_t* out_left_count, int wide) {
 #pragma omp parallel for schedule(dynamic, 1)
   for (int j = 0; j < n_nodes; ++j) {
     if (split_feat[j] < 0) { out_left_count[j] = 0; continue; }
@@ -216,14 +219,14 @@ int tmog_partition_cpu(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32
     const int64_t cnt = node_count[j];
     int64_t nl = 0;
     for (int64_t i = 0; i < cnt; ++i) {
-      const int bin = Xb[(int64_t)(in[i] & 0xFFFFFFu) * F + f];
+      const int bin = Xb[(int64_t)(wide ? in[i] : (in[i] & 0xFFFFFFu)) * F + f];
       const bool left = (missing_bin >= 0 && bin == missing_bin) ? dl : (bin <= sb);
       nl += left;
     }
     uint32_t* out = rows_out + out_begin[j];
     int64_t li = 0, ri = nl;
     for (int64_t i = 0; i < cnt; ++i) {
-      const int bin = Xb[(int64_t)(in[i] & 0xFFFFFFu) * F + f];
+      const int bin = Xb[(int64_t)(wide ? in[i] : (in[i] & 0xFFFFFFu)) * F + f];
       const bool left = (missing_bin >= 0 && bin == missing_bin) ? dl : (bin <= sb);
       if (left) out[li++] = in[i]; else out[ri++] = in[i];
     }

@@ -15,7 +15,7 @@ int tmog_hist_build_cpu(const uint8_t* Xb, int64_t N, int F, const uint32_t* row
                         const int64_t* node_begin, const int64_t* node_count, const int32_t* node_feat_off,
                         const int32_t* node_nfeat, const int32_t* feat_list, const int32_t* node_model,
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
-                        const float* t1, const float* t2, int64_t model_stride, const float* qscale);
+                        const float* t1, const float* t2, int64_t model_stride, const float* qscale, int wide);
 int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
@@ -25,7 +25,7 @@ int tmog_split_find_cpu(const int64_t* hist, int n_nodes, const int64_t* node_hi
 int tmog_partition_cpu(const uint8_t* Xb, int F, const uint32_t* rows_in, uint32_t* rows_out, int n_nodes,
                        const int64_t* node_begin, const int64_t* node_count, const int32_t* split_feat,
                        const int32_t* split_bin, const uint8_t* default_left, int missing_bin,
-                       const int64_t* out_begin, int64_t* out_left_count);
+                       const int64_t* out_begin, int64_t* out_left_count, int wide);
 }
 
 namespace {
@@ -66,7 +66,7 @@ struct CpuBackend {
                   const int32_t* bnmd, const int64_t* bnho, int, int, int) {
     if (nbuild)
       tmog_hist_build_cpu(g.Xb, g.N, g.F, rows, nbuild, bnb, bnc, bnfo, bnnf, flist, bnmd, bnho, hist, g.B, g.mode,
-                          g.S, g.y, g.t1, g.t2, g.stride, g.qscale);
+                          g.S, g.y, g.t1, g.t2, g.stride, g.qscale, g.wide_rows);
   }
   void hist_subtract(int64_t* hist, const int64_t* prev, const int64_t* poff, const int64_t* soff,
                      const int64_t* ooff, const int64_t* size, int n, int64_t, int64_t, int, int) {
@@ -102,7 +102,7 @@ struct CpuBackend {
   void partition_nodes(const tmog::GrowArgs& g, const uint32_t* rows, uint32_t* rows_alt, int ns, const int64_t* nb,
                        const int64_t* nc, const int32_t* f, const int32_t* b, const uint8_t* d, const int64_t* ob,
                        int64_t* nl) {
-    tmog_partition_cpu(g.Xb, g.F, rows, rows_alt, ns, nb, nc, f, b, d, g.missing_bin, ob, nl);
+    tmog_partition_cpu(g.Xb, g.F, rows, rows_alt, ns, nb, nc, f, b, d, g.missing_bin, ob, nl, g.wide_rows);
   }
   void leaf_collect(const uint32_t* rows, const void* items, int n, uint32_t* out_rows, int32_t* out_gid) {
     const tmog::LeafItemH* it = (const tmog::LeafItemH*)items;
