@@ -143,9 +143,14 @@ def main():
         dev = torch.device("cuda", local_rank)
     else:
         dev = torch.device("cpu")
-    D.init_from_env(device_id=local_rank if use_gpu else None)
+    sim = os.environ.get("TMOG_SIM_WORLD")
+    if sim:      # projection (scripts/project_schedule.py): this process times rank TMOG_SIM_RANK's share
+        D.simulate(int(os.environ.get("TMOG_SIM_RANK", "0")), int(sim))
+        os.environ.setdefault("TMOG_PARALLEL_MODE", "shard")    # spread learners would need real peers
+    else:
+        D.init_from_env(device_id=local_rank if use_gpu else None)
     world = D.world()
-    if world != max(1, args.gpus) and args.device != "cpu":
+    if world != max(1, args.gpus) and args.device != "cpu" and not sim:
         raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} ranks")
     CFG.set_default_device(dev)
     if use_gpu:
@@ -195,7 +200,7 @@ def main():
         # a learner that dies must not make the headline faster: every configured grid point must have
         # been evaluated and nothing may have failed
         n_eval = len(summ.get("validationResults") or [])
-        if summ.get("failures") or n_eval != expected_configs:
+        if summ.get("failures") or (n_eval != expected_configs and not sim):   # (a simulated rank sees its share)
             raise SystemExit(f"model selector evaluated {n_eval}/{expected_configs} configs; failures: "
                              f"{summ.get('failures')}")
         if os.environ.get("TMOG_MEM_TRACE") == "1" and D.rank() == 0:
@@ -222,7 +227,7 @@ def main():
     _all_fallbacks = [x for part in (D.all_gather_object(list(DP.GATHER_FALLBACKS)) if D.is_dist()
                                      else [DP.GATHER_FALLBACKS]) for x in part]
     per_step = total / max(args.steps, 1)
-    if D.rank() == 0:
+    if D.rank() == 0 or sim:
         metric = CONFIGS[args.config][0]
         if args.rows != CONFIGS[args.config][1]:       # the metric names the row count it was measured on
             metric = metric.replace(_rows_label(CONFIGS[args.config][1]), _rows_label(args.rows))
@@ -256,8 +261,11 @@ def main():
         if args.verbose and summ:
             out["timings"] = summ.get("timings")
             out["stage_timings"] = stage_t[0]
+        if sim:
+            out["simulated"] = {"rank": D.rank(), "world": D.world(),
+                                "note": "one rank's share timed on one GPU; collectives not executed"}
         print(json.dumps(out), flush=True)
-    if D.is_dist():
+    if D.is_dist() and not sim:
         import torch.distributed as dist
         dist.destroy_process_group()
 

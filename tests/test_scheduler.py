@@ -59,3 +59,23 @@ def test_forced_mode(monkeypatch):
     monkeypatch.setenv("TMOG_PARALLEL_MODE", "spread")
     ch = S.choose([("OpXGBoostClassifier", F._xgb_bin_grid())], 3, 1000, 10, 4, _par, lambda n, p: 0.2)
     assert ch[0].mode == "spread"
+
+
+def test_projection_mode_collectives():
+    """parallel/dist.py projection mode: one process plays rank r of W ranks holding identical shards."""
+    import torch
+    from transmogrifai_amd.parallel import dist as D
+    try:
+        D.simulate(3, 8)
+        assert D.is_dist() and D.rank() == 3 and D.world() == 8
+        assert D.all_reduce(torch.tensor([2.0]), "sum").item() == 16.0
+        assert D.all_reduce(torch.tensor([2.0]), "max").item() == 2.0
+        assert D.all_gather_rows(torch.arange(3)).tolist() == list(range(3)) * 8
+        assert D.all_gather_object({"a": 1}) == [{"a": 1}] * 8
+        assert D.broadcast_object(5) == 5
+        assert D.all_to_all_bytes([bytes([k]) for k in range(8)]) == [bytes([3])] * 8
+        owners = D.lpt_assign([1.0] * 20, D.world())
+        assert sorted(set(owners)) == list(range(8))
+    finally:
+        D.simulate(0, 1)
+    assert not D.simulated() and not D.is_dist()

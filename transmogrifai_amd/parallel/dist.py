@@ -15,19 +15,41 @@ import torch
 import torch.distributed as dist
 
 
+# Projection mode (scripts/project_schedule.py): one process plays rank `rank` of `world` ranks that all hold
+# shards identical to its own -- every collective returns what it would return then (sums scale by the world,
+# gathers tile), without any communication. The per-rank share of a multi-GPU run can so be timed on one GPU;
+# it is a timing device only (the data of the other ranks is not the real data).
+_SIM = None
+
+
+def simulate(rank_: int, world_: int) -> None:
+    global _SIM
+    _SIM = (int(rank_), int(world_)) if world_ > 1 else None
+
+
+def simulated() -> bool:
+    return _SIM is not None
+
+
 def is_dist() -> bool:
-    return dist.is_available() and dist.is_initialized()
+    return _SIM is not None or (dist.is_available() and dist.is_initialized())
 
 
 def rank() -> int:
+    if _SIM is not None:
+        return _SIM[0]
     return dist.get_rank() if is_dist() else 0
 
 
 def world() -> int:
+    if _SIM is not None:
+        return _SIM[1]
     return dist.get_world_size() if is_dist() else 1
 
 
 def barrier():
+    if _SIM is not None:
+        return
     if is_dist():
         dist.barrier()
 
@@ -48,12 +70,14 @@ def init_from_env(backend: str = None, device_id: int = None):
 
 
 def _comm_device(t: torch.Tensor):
-    if is_dist() and dist.get_backend() == "nccl" and t.device.type != "cuda":
+    if _SIM is None and is_dist() and dist.get_backend() == "nccl" and t.device.type != "cuda":
         return torch.device("cuda", torch.cuda.current_device())
     return t.device
 
 
 def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    if _SIM is not None:
+        return t * _SIM[1] if op == "sum" else t.clone()
     if not is_dist():
         return t
     dev = _comm_device(t)
@@ -79,6 +103,9 @@ def bucketed_all_reduce(tensors: Sequence[torch.Tensor], op: str = "sum") -> Lis
 
 
 def all_gather_object(obj) -> list:
+    if _SIM is not None:
+        import copy
+        return [obj] + [copy.deepcopy(obj) for _ in range(_SIM[1] - 1)]
     if not is_dist():
         return [obj]
     out = [None] * world()
@@ -87,7 +114,7 @@ def all_gather_object(obj) -> list:
 
 
 def broadcast_object(obj, src: int = 0):
-    if not is_dist():
+    if _SIM is not None or not is_dist():
         return obj
     box = [obj]
     dist.broadcast_object_list(box, src=src)
@@ -96,6 +123,8 @@ def broadcast_object(obj, src: int = 0):
 
 def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
     """Concatenate a row-sharded tensor from every rank (variable row counts)."""
+    if _SIM is not None:
+        return torch.cat([t] * _SIM[1])
     if not is_dist():
         return t
     dev = _comm_device(t)
@@ -120,6 +149,8 @@ def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
 def all_to_all_bytes(per_dest: Sequence[bytes]) -> List[bytes]:
     """Personalised exchange: rank r sends ``per_dest[k]`` to rank k and returns what every rank sent it
     (two ``all_to_all_single`` calls: the sizes, then the payload with those splits)."""
+    if _SIM is not None:
+        return [per_dest[_SIM[0]]] * _SIM[1]
     if not is_dist():
         return [per_dest[0]]
     n = world()
