@@ -75,3 +75,32 @@ def test_detectors():
     assert out[0]["gender"] == "Female" and out[1]["firstName"] == "John"
     ds2, (p,) = TestFeatureBuilder.of(("p", T.Phone, ["(650) 555-1234", "123", None]))
     check_transformer(N.ParsePhoneNumber().set_input(p), ds2, expected=["+16505551234", None, None])
+
+
+def test_mime_detector_reference_fixtures():
+    """MimeTypeDetectorTest.scala: the reference's own test files, with and without the JSON type hint."""
+    import base64
+    import os
+    import pytest
+    from transmogrifai_amd.stages.feature.nlp_stages import MimeTypeDetector
+    ref = "/root/reference"
+    names = ["core/src/test/resources/811harmo24to36.mp3", "core/src/test/resources/820orig36to48.wav",
+             "core/src/test/resources/face.png", "features/src/test/resources/log4j.properties",
+             "core/src/test/resources/note.xml", "core/src/test/resources/RunnerParams.json",
+             "core/src/test/resources/dummy.csv", "core/src/test/resources/Canon_40D.jpg",
+             "core/src/test/resources/sample.pdf"]
+    if not all(os.path.exists(os.path.join(ref, n)) for n in names):
+        pytest.skip("reference test resources not mounted")
+    data = [base64.b64encode(open(os.path.join(ref, n), "rb").read()).decode() for n in names]
+    expected = ["audio/mpeg", "audio/vnd.wave", "image/png", "text/plain", "application/xml", "text/plain",
+                "text/plain", "image/jpeg", "application/pdf"]
+    expected_json = ["audio/mpeg", "audio/vnd.wave", "image/png", "application/json", "application/xml",
+                     "application/json", "application/json", "image/jpeg", "application/pdf"]
+    assert [MimeTypeDetector().transform_fn(d) for d in data] == expected
+    assert [MimeTypeDetector(type_hint="application/json").transform_fn(d) for d in data] == expected_json
+    # Base64.empty -> empty, Base64("") and random bytes -> application/octet-stream
+    rng = __import__("numpy").random.default_rng(42)
+    rand = [base64.b64encode(rng.integers(0, 256, int(n), dtype="uint8").tobytes()).decode()
+            for n in rng.integers(16, 10000, 10)]
+    assert [MimeTypeDetector().transform_fn(v) for v in [None, ""] + rand] == \
+        [None] + ["application/octet-stream"] * 11

@@ -76,37 +76,61 @@ def _clean(s):
 
 _MAGIC = [(b"%PDF", "application/pdf"), (b"\x89PNG", "image/png"), (b"\xff\xd8\xff", "image/jpeg"),
           (b"GIF8", "image/gif"), (b"PK\x03\x04", "application/zip"), (b"ID3", "audio/mpeg"),
-          (b"RIFF", "audio/x-wav"), (b"<?xml", "application/xml"), (b"\x1f\x8b", "application/gzip"),
+          (b"<?xml", "application/xml"), (b"\x1f\x8b", "application/gzip"),
           (b"BM", "image/bmp"), (b"OggS", "audio/ogg"), (b"fLaC", "audio/x-flac"), (b"<html", "text/html"),
-          (b"<!DOCTYPE html", "text/html")]
+          (b"<!DOCTYPE html", "text/html"), (b"\x7fELF", "application/x-executable"),
+          (b"\xd0\xcf\x11\xe0\xa1\xb1\x1a\xe1", "application/x-tika-msoffice")]
+# MPEG audio frame sync (Tika's audio/mpeg magic: 0xFFFA / FB / F2 / F3 / E3)
+_MPEG_SYNC = (b"\xff\xfb", b"\xff\xfa", b"\xff\xf3", b"\xff\xf2", b"\xff\xe3")
+# RIFF containers: the form type at offset 8 (Tika 1.x names)
+_RIFF = {b"WAVE": "audio/vnd.wave", b"AVI ": "video/x-msvideo", b"WEBP": "image/webp"}
+_CONTROL = set(range(0x00, 0x09)) | set(range(0x0E, 0x1B)) | set(range(0x1C, 0x20))
+
+
+def _looks_like_text(raw: bytes) -> bool:
+    """Tika's TextDetector: no control bytes, and mostly printable ASCII or valid UTF-8 (an empty stream is not
+    text -- Tika answers application/octet-stream)."""
+    if not raw:
+        return False
+    if any(b in _CONTROL for b in raw):
+        return False
+    ascii_ = sum(1 for b in raw if 0x20 <= b < 0x7F or b in (0x09, 0x0A, 0x0B, 0x0C, 0x0D, 0x1B))
+    if ascii_ * 10 >= len(raw) * 9:
+        return True
+    try:
+        raw.decode("utf-8")
+        return True
+    except UnicodeDecodeError:
+        try:        # a multi-byte character cut by the byte limit
+            raw[:-3].decode("utf-8")
+            return len(raw) > 3
+        except UnicodeDecodeError:
+            return False
 
 
 @value_fn("MimeTypeDetector")
 def detect_mime(s, max_bytes: int = 1024, type_hint: str = ""):
-    """Magic-byte MIME detection of base64 content (Tika replacement; parity unpinned). Only the first
-    ``max_bytes`` decoded bytes are examined (``BoundedInputStream``, MimeTypeDetector.scala:94); a
-    ``type_hint`` refines the generic answers (``application/octet-stream``, ``text/plain``) the way Tika's
-    detector lets the declared content type specialise its magic match."""
+    """Magic-byte MIME detection of base64 content (Tika ``DefaultDetector`` replacement; expectations of
+    ``MimeTypeDetectorTest.scala`` pinned in ``tests/test_nlp_stages.py``). Only the first ``max_bytes`` decoded
+    bytes are examined (``BoundedInputStream``, MimeTypeDetector.scala:94); a ``type_hint`` refines the generic
+    answers (``application/octet-stream``, ``text/plain``) the way Tika lets the declared content type
+    specialise its magic match. ``None`` stays ``None``; an empty value is ``application/octet-stream``."""
     if s is None:
         return None
     try:
         raw = base64.b64decode(s, validate=False)
     except Exception:
         return None
-    if not raw:
-        return None
     raw = raw[:max(0, int(max_bytes))] if max_bytes is not None else raw
-    if not raw:
-        return type_hint or "application/octet-stream"
     for sig, mime in _MAGIC:
-        if raw[:len(sig)].lower() == sig.lower():
+        if raw[:len(sig)] == sig or (sig[:1].isalpha() and raw[:len(sig)].lower() == sig.lower()):
             return mime
-    try:
-        raw[:512].decode("utf-8")
-        found = "text/plain"
-    except UnicodeDecodeError:
-        found = "application/octet-stream"
-    if type_hint:   # the generic magic answers are refined by the declared type (Tika's type registry)
+    if raw[:2] in _MPEG_SYNC:
+        return "audio/mpeg"
+    if raw[:4] == b"RIFF" and raw[8:12] in _RIFF:
+        return _RIFF[raw[8:12]]
+    found = "text/plain" if _looks_like_text(raw) else "application/octet-stream"
+    if type_hint:   # the generic answers are refined by the declared type (Tika's type registry)
         return type_hint
     return found
 
