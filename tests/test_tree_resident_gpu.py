@@ -90,18 +90,22 @@ def test_xgboost_learner_resident_on_off_identical(monkeypatch):
     folds = [torch.arange(N)[torch.arange(N) % 3 != k].cuda() for k in range(2)]
     jobs = [FitJob(p, r) for p in params for r in folds]
     out = {}
-    for flag in ("0", "1"):
+    # host-planned; device-planned with the torch round set-up; device-planned with the fused prologue
+    for flag, pro in (("0", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("TMOG_TREE_RESIDENT", flag)
+        monkeypatch.setenv("TMOG_XGB_PROLOGUE", pro)
         L = learner_class("OpXGBoostClassifier")()
         states = L.fit_batch(Xd, yd, jobs)
-        out[flag] = (states, L.predict_batch(states, Xd, [None] * len(states)))
-    for a, b in zip(out["0"][0], out["1"][0]):
-        assert a["num_trees"] == b["num_trees"]
-        for k in ("tree_off", "nodes", "value"):
-            np.testing.assert_array_equal(np.asarray(a["forest"][k]), np.asarray(b["forest"][k]), err_msg=k)
-    for pa, pb_ in zip(out["0"][1], out["1"][1]):
-        for ta, tb in zip(pa, pb_):
-            torch.testing.assert_close(ta, tb, rtol=0, atol=0)
+        out[flag + pro] = (states, L.predict_batch(states, Xd, [None] * len(states)))
+    for key in ("10", "11"):
+        for a, b in zip(out["00"][0], out[key][0]):
+            assert a["num_trees"] == b["num_trees"]
+            for k in ("tree_off", "nodes", "value"):
+                np.testing.assert_array_equal(np.asarray(a["forest"][k]), np.asarray(b["forest"][k]),
+                                              err_msg=f"{key} {k}")
+        for pa, pb_ in zip(out["00"][1], out[key][1]):
+            for ta, tb in zip(pa, pb_):
+                torch.testing.assert_close(ta, tb, rtol=0, atol=0)
 
 
 def test_resident_request_on_cpu_falls_back():

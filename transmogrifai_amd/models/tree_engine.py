@@ -525,7 +525,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 collect_leaves: bool = False, groups: Optional[int] = None, csr=None, root=None,
                 fp: Optional[FpPlan] = None, slot_base: int = 0, XbT: Optional[torch.Tensor] = None,
                 quant_amax: Optional[torch.Tensor] = None, quant_wmax: Optional[float] = None,
-                resident: bool = False):
+                resident: bool = False, prestaged=None):
     """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``.
 
     The level loop runs natively (``ops/csrc/common/tree_grow.hpp``): on the GPU every job group gets
@@ -557,7 +557,10 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     ``resident``: on the GPU, for one job group (``groups=1``), no per-node feature subsets and leaves
     collected, grow with the device-planned level loop (``ops/csrc/hip/tree_resident.hip``): nothing is
     read back, and a :class:`ResidentTree` is returned instead of a Forest (same trees; the host Forest is
-    built later by :func:`resident_forests`). Other configurations fall back to the host-planned loop."""
+    built later by :func:`resident_forests`). Other configurations fall back to the host-planned loop.
+
+    ``prestaged``: ``(rows, counts, gh, qscale, qinv)`` already prepared on this stream by the fused round
+    prologue (``boost_prologue``): the root entries (consumed), their quantised statistics and the scales."""
     dev = Xb.device
     on_gpu = dev.type == "cuda"
     slot_base = int(slot_base) + slot_lane()
@@ -584,18 +587,26 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     ng = groups if groups is not None else min(T, max(1, min(8, int(os.environ.get("TMOG_TREE_GROUPS", "2")))))
     ng = max(1, min(ng, T)) if T else 1
     cuts = np.linspace(0, T, ng + 1).astype(np.int32)
-    if root is not None:
+    if prestaged is not None:
+        rows, counts = prestaged[0], [int(c) for c in prestaged[1]]
+        if len(counts) != len(jobs) or sum(counts) != int(rows.numel()):
+            raise ValueError("root entries do not match the jobs")
+    elif root is not None:
         rows, counts = root[0].to(device=dev, dtype=torch.int32).contiguous(), [int(c) for c in root[1]]
         if len(counts) != len(jobs) or sum(counts) != int(rows.numel()):
             raise ValueError("root entries do not match the jobs")
     else:
         rows, counts = _root_rows(jobs, dev, wide)
     rows_alt = torch.empty_like(rows)
-    qscale, qinv = _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev, quant_amax,
-                                 1.0 if wide else quant_wmax)
     total = int(rows.numel())
     gh = gh_alt = None
-    if on_gpu and mode == MODE_GH and total and t1f is not None and t2f is not None \
+    if prestaged is not None:
+        gh, qscale, qinv = prestaged[2], prestaged[3], prestaged[4]
+        gh_alt = torch.empty_like(gh)
+    else:
+        qscale, qinv = _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev, quant_amax,
+                                     1.0 if wide else quant_wmax)
+    if gh is None and on_gpu and mode == MODE_GH and total and t1f is not None and t2f is not None \
             and os.environ.get("TMOG_GH_STAGE", "1") != "0":
         gh = _stage_gh(rows, counts, jobs, t1f, t2f, qscale, stride, wide)
         gh_alt = torch.empty_like(gh)
@@ -748,6 +759,43 @@ def _const_tensor(a: np.ndarray, dev) -> torch.Tensor:
     return t
 
 
+def quant_qmax(chunk_rows: int = 4096) -> float:
+    """Per-row bound of a quantised statistic: an LDS partial sums at most max(chunk_rows, CSR_ITEM_ROWS) rows
+    (CSR items always span 1024 rows, tree_grow.hpp kCsrRows), and must fit int32."""
+    chunk_rows = int(os.environ.get("TMOG_TREE_CHUNK", chunk_rows))
+    return float(min(1 << 22, (2 ** 31 - 1) // max(1, int(chunk_rows), CSR_ITEM_ROWS) - 1))
+
+
+def boost_prologue(root: torch.Tensor, counts, act, G: torch.Tensor, H: torch.Tensor, amax: torch.Tensor,
+                   comp: torch.Tensor, tam_prev: Optional[torch.Tensor], tam_next: torch.Tensor, out: dict,
+                   wide: bool = False):
+    """Set-up of one device-resident boosting round in a single launch (ops/csrc/hip/boost_kernels.hip
+    boost_prologue_kernel): the quantisation maxima of the active jobs ``act`` (model index = job) from
+    ``comp`` and the previous epilogue's ``tam_prev`` (None: first round, ``amax`` as it is), their
+    power-of-two scales, a copy of the packed ``root`` entries and their quantised (g, h); zeroes the jobs'
+    entries of ``tam_next``. ``out`` holds the reusable buffers; returns grow_forest's ``prestaged``."""
+    dev = root.device
+    total = int(root.numel())
+    P = int(G.shape[0])
+    if out.get("rows") is None or out["rows"].numel() < total:
+        out["rows"] = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+        out["gh"] = torch.empty(max(total, 1), 2, dtype=torch.int32, device=dev)
+    if out.get("qscale") is None:
+        out["qscale"] = torch.ones(P, 2, dtype=torch.float32, device=dev)
+        out["qinv"] = torch.ones(P, 2, dtype=torch.float64, device=dev)
+    rows, gh = out["rows"][:total], out["gh"][:total]
+    act_t = _const_tensor(np.asarray(act, np.int32), dev)
+    off = _const_tensor(np.concatenate([[0], np.cumsum(np.asarray(counts, np.int64))]).astype(np.int64), dev)
+    rc = N.hip().tmog_hip_boost_prologue(N.ptr(tam_prev) if tam_prev is not None else None, N.ptr(tam_next),
+                                         N.ptr(comp), N.ptr(amax), P, N.ptr(act_t), len(act), N.ptr(off),
+                                         N.ptr(root), N.ptr(rows), total, N.ptr(G), N.ptr(H), int(G.shape[1]),
+                                         N.ptr(gh), N.ptr(out["qscale"]), N.ptr(out["qinv"]), quant_qmax(),
+                                         int(bool(wide)), N.stream(dev))
+    if rc != 0:
+        raise RuntimeError(f"boost prologue launch failed ({rc})")
+    return rows, list(counts), gh, out["qscale"], out["qinv"]
+
+
 def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev, amax_hint=None, wmax_hint=None):
     """Per-(model, stat) power-of-two fixed-point scales for the int64 histograms (see the
     "Fixed-point statistics" note in ops/csrc/hip/tree_kernels.hip). A row's contribution is
@@ -757,9 +805,7 @@ def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev, amax_hint=None
     if mode == MODE_CLS or rows.numel() == 0:
         one = torch.ones(n_models, S, dtype=torch.float32, device=dev)
         return one, one.to(torch.float64)
-    # an LDS partial sums at most max(chunk_rows, CSR_ITEM_ROWS) rows (CSR items always span 1024 rows,
-    # tree_grow.hpp kCsrRows), so size the per-row bound from the larger of the two
-    qmax = float(min(1 << 22, (2 ** 31 - 1) // max(1, int(chunk_rows), CSR_ITEM_ROWS) - 1))
+    qmax = quant_qmax(chunk_rows)
     wmax = torch.tensor(float(wmax_hint), dtype=torch.float32, device=dev) if wmax_hint is not None else \
         ((rows >> 24) & 0xFF).max().to(torch.float32)
 
@@ -781,8 +827,11 @@ def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev, amax_hint=None
         return m.expand(n_models) if m.numel() == 1 else m[:n_models]
 
     def pow2(bound):
+        # 2^floor(log2 x), exponent read exactly with frexp (x = m 2^e, m in [0.5, 1)) -- the fused round
+        # prologue (boost_kernels.hip pow2_scale) computes the same bits
         x = qmax / (bound * wmax).clamp_min(1e-30)
-        return torch.exp2(torch.floor(torch.log2(x))).clamp(2.0 ** -60, 2.0 ** 60)
+        _, e = torch.frexp(x)
+        return torch.ldexp(torch.ones_like(x), (e - 1).clamp(-60, 60))
 
     if mode == MODE_VAR:
         m1 = amax(t1f)

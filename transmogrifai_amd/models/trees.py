@@ -757,6 +757,12 @@ class XGBoostClassifierLearner(_BoostLearner):
         # the last round, and the early-stopping AuPR is read ES_LAG rounds late.
         resident = fused and par is None and TE.resident_enabled()
         es_lag = max(1, int(os.environ.get("TMOG_ES_LAG", "2"))) if resident else 1
+        # Fused round prologue (tree_engine.boost_prologue): the scales, the root copy and the staged (g, h) in
+        # one launch; the epilogue's maxima buffer is double-buffered (round it writes tam2[it & 1], which round
+        # it's prologue zeroed; round it + 1's prologue reads it).
+        prologue = resident and tam is not None and P <= 64 and os.environ.get("TMOG_XGB_PROLOGUE", "1") != "0" \
+            and all(float(j.params.get("subsample", 1.0)) >= 1.0 for j in jobs)
+        tam2 = torch.zeros(2, 64, P, 2, dtype=torch.int32, device=dev) if prologue else None
 
         def run(ps, slot_base=0, groups=None):
             """Boosting rounds of the jobs ``ps`` (their trees do not depend on which other jobs grow
@@ -767,6 +773,7 @@ class XGBoostClassifierLearner(_BoostLearner):
             tick = time.perf_counter
             pending: list = []
             deferred: list = []        # (act, ResidentTree) per device-planned round, in round order
+            pro_buf: dict = {}         # boost_prologue's reusable per-part buffers
 
             def resolve(it0, need0, vals_t):
                 for p, v in zip(need0, vals_t.tolist()):
@@ -811,13 +818,18 @@ class XGBoostClassifierLearner(_BoostLearner):
                         root_cache.clear()
                         root_cache[key] = TE._root_rows(tjobs, dev, TE.wide_rows(int(Xg.shape[0])))
                     packed, cnts = root_cache[key]
-                    root = (packed.clone(), cnts)
+                    root = None if prologue else (packed.clone(), cnts)
+                pre = None
+                if prologue:
+                    pre = TE.boost_prologue(packed, cnts, act, G, H, amax_cur, comp,
+                                            tam2[(it - 1) & 1] if it > 0 else None, tam2[it & 1], pro_buf,
+                                            TE.wide_rows(int(Xg.shape[0])))
                 t_1 = tick()
                 forest = TE.grow_forest(Xg, n_bins_g, tjobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=G, t2=H, B=mb,
                                         missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root, fp=fp,
                                         slot_base=slot_base, groups=groups, XbT=XgT,
                                         quant_amax=amax_cur, quant_wmax=1.0 if amax_cur is not None else None,
-                                        resident=resident and groups in (None, 1))
+                                        resident=resident and groups in (None, 1), prestaged=pre)
                 t_2 = tick()
                 is_res = isinstance(forest, TE.ResidentTree)
                 if colperm is not None and not is_res:
@@ -827,12 +839,13 @@ class XGBoostClassifierLearner(_BoostLearner):
                 auc_counts = None
                 if fused:
                     ai = None
-                    if tam is not None:
+                    if tam is not None and not prologue:
                         ai = TE._const_tensor(np.asarray(act, np.int64), dev)
                         tam.index_fill_(1, ai, 0)
                     auc_counts = self._fused_epilogue(Fm, G, H, yf, forest, act, N,
-                                                      AUC_BINS if (need and self.classification) else 0, tam)
-                    if tam is not None:
+                                                      AUC_BINS if (need and self.classification) else 0,
+                                                      tam2[it & 1] if prologue else tam)
+                    if tam is not None and not prologue:
                         amax_cur.index_copy_(0, ai, torch.maximum(
                             comp.index_select(0, ai), tam.index_select(1, ai).view(torch.float32).amax(0)))
                 else:

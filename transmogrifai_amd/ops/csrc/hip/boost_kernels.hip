@@ -23,6 +23,7 @@
 // tuning/splitters.row_uniform (hold-out split, CV folds, down-sampling, bootstrap, sanity-check
 // sample) as one fused pass instead of ~12 int64 elementwise torch kernels; bit-identical results.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 #include <math.h>
 
@@ -135,6 +136,85 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
       pend = pend && !mine;
     }
     if (pend) atomicAdd(auc_hist + slot, 1);
+  }
+}
+
+// boost_prologue_kernel -- the set-up of a device-resident boosting round (models/trees.py, resident grower) in
+// one launch instead of ~35 small torch ops: per active job p (= its model index)
+//   * the quantisation maxima of the new (g, h): max(rows outside the job's training set, the last
+//     epilogue's per-copy maxima tam_prev) -> amax[p] (tree_engine._quant_scales' amax_hint),
+//   * the power-of-two fixed-point scales q = 2^floor(log2(qmax / max(amax, 1e-30))) clamped to 2^[-60, 60]
+//     (exponent taken with frexp: exact, as tree_engine._quant_scales computes it) -> qscale[p], qinv[p],
+//   * every root entry copied into the grower's row buffer and its quantised (q(w g), q(w h)) staged
+//     (tree_engine._stage_gh: rintf((w * t) * q), the same fp32 operation order),
+//   * the job's copies of the NEXT epilogue's maxima buffer zeroed (double buffered by the caller).
+// Every block recomputes the T scales from the (tiny) maxima tables; block 0 writes them out.
+__device__ __forceinline__ float pow2_scale(float qmax, float a) {
+  const float x = qmax / fmaxf(a, 1e-30f);
+  int e;
+  (void)frexpf(x, &e);                       // x = m 2^e, m in [0.5, 1): floor(log2 x) = e - 1
+  const int k = min(60, max(-60, e - 1));
+  return ldexpf(1.f, k);
+}
+
+constexpr int kMaxProJobs = 64;
+
+__global__ void __launch_bounds__(256) boost_prologue_kernel(
+    const uint32_t* __restrict__ tam_prev, uint32_t* __restrict__ tam_next, const float* __restrict__ comp,
+    float* __restrict__ amax, int P, const int32_t* __restrict__ act, int T, const int64_t* __restrict__ job_off,
+    const uint32_t* __restrict__ root, uint32_t* __restrict__ rows, const float* __restrict__ G,
+    const float* __restrict__ H, int64_t stride, int2* __restrict__ gh, float* __restrict__ qscale,
+    double* __restrict__ qinv, float qmax, int wide) {
+  __shared__ float s_sc[kMaxProJobs][2];
+  __shared__ int64_t s_off[kMaxProJobs + 1];
+  __shared__ int s_p[kMaxProJobs];
+  for (int t = threadIdx.x; t < T; t += blockDim.x) {
+    const int p = act[t];
+    float a0, a1;
+    if (tam_prev) {
+      a0 = comp[2 * p];
+      a1 = comp[2 * p + 1];
+      for (int c = 0; c < kAmaxCopies; ++c) {
+        a0 = fmaxf(a0, __uint_as_float(tam_prev[((int64_t)c * P + p) * 2]));
+        a1 = fmaxf(a1, __uint_as_float(tam_prev[((int64_t)c * P + p) * 2 + 1]));
+      }
+    } else {
+      a0 = amax[2 * p];
+      a1 = amax[2 * p + 1];
+    }
+    const float q0 = pow2_scale(qmax, a0), q1 = pow2_scale(qmax, a1);
+    s_sc[t][0] = q0;
+    s_sc[t][1] = q1;
+    s_p[t] = p;
+    if (blockIdx.x == 0) {
+      amax[2 * p] = a0;
+      amax[2 * p + 1] = a1;
+      qscale[2 * p] = q0;
+      qscale[2 * p + 1] = q1;
+      qinv[2 * p] = 1.0 / (double)q0;
+      qinv[2 * p + 1] = 1.0 / (double)q1;
+    }
+  }
+  for (int t = threadIdx.x; t <= T; t += blockDim.x) s_off[t] = job_off[t];
+  if (blockIdx.x == 0 && tam_next)
+    for (int i = threadIdx.x; i < kAmaxCopies * T; i += blockDim.x) {
+      const int c = i / T, t = i - c * T;
+      tam_next[((int64_t)c * P + act[t]) * 2] = 0u;
+      tam_next[((int64_t)c * P + act[t]) * 2 + 1] = 0u;
+    }
+  __syncthreads();
+  const int64_t total = s_off[T];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int t = 0;
+    while (t + 1 < T && s_off[t + 1] <= e) ++t;
+    const uint32_t en = root[e];
+    rows[e] = en;
+    const int64_t r = wide ? (int64_t)en : (int64_t)(en & 0xFFFFFFu);
+    const float w = (float)(wide ? 1u : (en >> 24));
+    const int64_t k = (int64_t)s_p[t] * stride + r;
+    const float g = w * G[k];
+    const float h = w * H[k];
+    gh[e] = make_int2((int)rintf(g * s_sc[t][0]), (int)rintf(h * s_sc[t][1]));
   }
 }
 
@@ -313,6 +393,21 @@ int tmog_hip_boost_epilogue(const uint32_t* entries, const int32_t* gid, int64_t
   hipLaunchKernelGGL(boost_epilogue_kernel, dim3((unsigned)((n_entries + 255) / 256)), dim3(256), 0, stream, entries,
                      gid, n_entries, gid_value, gid_tree, tree_job, N, F, G, H, y, objective, auc_hist, bins, n_gid,
                      n_trees, P, amax, wide_rows);
+  return (int)hipGetLastError();
+}
+
+// Round prologue of device-resident boosting (boost_prologue_kernel). tam_prev == null: first round, the
+// maxima in amax are used as they are. T <= 64 active jobs.
+int tmog_hip_boost_prologue(const uint32_t* tam_prev, uint32_t* tam_next, const float* comp, float* amax, int P,
+                            const int32_t* act, int T, const int64_t* job_off, const uint32_t* root, uint32_t* rows,
+                            int64_t total, const float* G, const float* H, int64_t stride, int32_t* gh,
+                            float* qscale, double* qinv, float qmax, int wide, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (T > kMaxProJobs) return -2;
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, (total + 255) / 256), 2048);
+  hipLaunchKernelGGL(boost_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, tam_prev, tam_next, comp,
+                     amax, P, act, T, job_off, root, rows, G, H, stride, reinterpret_cast<int2*>(gh), qscale, qinv,
+                     qmax, wide);
   return (int)hipGetLastError();
 }
 
