@@ -258,6 +258,10 @@ def main():
                        "parallelism": (f"dp{world}" if args.layout == "sharded" else f"grid-shard{world}")
                        if world > 1 else "single"},
         }
+        out["step_s"] = [round(x, 4) for x in times]
+        from transmogrifai_amd.utils import watchdog as WD
+        if WD.STALLS:                                   # fit-progress stalls seen by the lanes watchdog
+            out["stalls"] = list(WD.STALLS)
         if args.verbose and summ:
             out["timings"] = summ.get("timings")
             out["stage_timings"] = stage_t[0]

@@ -659,7 +659,24 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
         if rt is not None:
             return rt
     fn = (lambda name: getattr(lib, f"tmog_hip_{name}")) if on_gpu else (lambda name: getattr(lib, f"tmog_{name}_cpu"))
-    h = fn("grow_forest")(C.byref(a))
+    side = []
+    if on_gpu and ng > 1 and fpw == 0:
+        # groups beyond the first run on side streams of the process-wide set (ops/streams.py), shared when
+        # fewer are free; the grouping itself (and so every tree) does not depend on how many were free
+        from ..ops import streams as SP
+        null_base = int(N.stream(dev) or 0) == 0
+        side = SP.lease(dev, ng if null_base else ng - 1)
+        for g in range(ng):
+            k = g if null_base else g - 1
+            if k >= 0:
+                lib.tmog_hip_slot_stream(slot_base + g, side[k % len(side)].cuda_stream if side else None,
+                                         1 if side else 0)
+    try:
+        h = fn("grow_forest")(C.byref(a))
+    finally:
+        if side:
+            from ..ops import streams as SP
+            SP.release(dev, side)
     try:
         msg = C.create_string_buffer(512)
         if fn("grow_status")(h, msg, 512) != 0:

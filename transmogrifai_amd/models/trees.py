@@ -615,40 +615,58 @@ class GBTRegressorLearner(GBTClassifierLearner):
 
 
 def _run_parts(dev, parts, fn):
-    """Run ``fn(jobs, slot_base, groups)`` for every part concurrently: one host thread and one stream
-    per part (both ordered after the caller's stream, which then waits for all of them). Native calls
-    release the GIL, so the parts' host work and GPU work interleave. The first error is re-raised."""
+    """Run ``fn(jobs, slot_base, groups)`` for every part concurrently: the first part on the caller's thread
+    and stream, every other part on a host thread of its own and a side stream leased from ops/streams.py
+    (ordered after the caller's stream, which then waits for all of them). With fewer side streams free than
+    parts, parts are merged (jobs of part k go to part k mod the streams available): the trees of a job do
+    not depend on the jobs grown beside it. Native calls release the GIL, so the parts' host work and GPU work
+    interleave. The first error is re-raised."""
     import threading
+    from ..ops import streams as SP
     cur = torch.cuda.current_stream(dev)
-    streams = [torch.cuda.Stream(device=dev, priority=cur.priority) for _ in parts]
-    for s in streams:
-        s.wait_stream(cur)
-    errs = []
-    lane = TE.slot_lane()           # the caller's native slot lane (concurrent learners) carries over
-    token = cancel.current()        # and its maxWait cancellation token
+    side = SP.lease(dev, len(parts) - 1)
+    try:
+        k_used = 1 + len(side)
+        if k_used < len(parts):
+            merged = [list(p) for p in parts[:k_used]]
+            for k, p in enumerate(parts[k_used:], start=k_used):
+                merged[k % k_used][0] = list(merged[k % k_used][0]) + list(p[0])
+            parts = [tuple(p) for p in merged]
+        for s in side:
+            s.wait_stream(cur)
+        errs = []
+        lane = TE.slot_lane()           # the caller's native slot lane (concurrent learners) carries over
+        token = cancel.current()        # and its maxWait cancellation token
 
-    def work(k):
-        try:
-            torch.cuda.set_device(dev)
-            TE.set_slot_lane(lane)
-            with cancel.scope(token), torch.cuda.stream(streams[k]):
-                fn(*parts[k])
-        except BaseException as e:          # noqa: BLE001  (re-raised on the caller's thread)
-            errs.append(e)
+        def work(k):
+            try:
+                torch.cuda.set_device(dev)
+                TE.set_slot_lane(lane)
+                with cancel.scope(token), torch.cuda.stream(side[k - 1]):
+                    fn(*parts[k])
+            except BaseException as e:          # noqa: BLE001  (re-raised on the caller's thread)
+                errs.append(e)
 
-    th = [threading.Thread(target=work, args=(k,), daemon=True) for k in range(len(parts))]
-    # a thread returning from a native call must win the GIL back from the one running Python: the
-    # default 5 ms switch interval would stall it for up to a whole boosting round
-    from ..utils.threads import fast_switch
-    with fast_switch(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))):
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-    for s in streams:
-        cur.wait_stream(s)
-    if errs:
-        raise errs[0]
+        th = [threading.Thread(target=work, args=(k,), daemon=True, name=f"boost-part-{k}")
+              for k in range(1, len(parts))]
+        # a thread returning from a native call must win the GIL back from the one running Python: the
+        # default 5 ms switch interval would stall it for up to a whole boosting round
+        from ..utils.threads import fast_switch
+        with fast_switch(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))):
+            for t in th:
+                t.start()
+            try:
+                fn(*parts[0])
+            except BaseException as e:          # noqa: BLE001
+                errs.append(e)
+            for t in th:
+                t.join()
+        for s in side:
+            cur.wait_stream(s)
+        if errs:
+            raise errs[0]
+    finally:
+        SP.release(dev, side)
 
 
 # TMOG_XGB_PROFILE=1: per pipelined part, host seconds spent before / inside / after the native grower and in

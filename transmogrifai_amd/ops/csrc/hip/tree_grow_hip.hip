@@ -70,6 +70,8 @@ inline void kchk(int rc, const char* what) {
 // per-(group slot) persistent resources: stream, pinned staging slots, device staging, result mirror
 struct GpuSlot {
   hipStream_t stream = nullptr;
+  hipStream_t ext = nullptr;                 // caller-provided stream for this slot (tmog_hip_slot_stream)
+  bool ext_set = false;
   uint8_t* pin[3] = {nullptr, nullptr, nullptr};
   size_t pin_cap[3] = {0, 0, 0};
   uint8_t* dev[3] = {nullptr, nullptr, nullptr};
@@ -299,8 +301,10 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
   const tmog::GrowArgs& a = *args;
   const int ng = a.n_groups;
   res->groups.resize(ng);
+  std::vector<hipStream_t> own(ng, nullptr);   // each slot's own stream, restored after the call
+  int swapped = 0;
+  const int sb = a.slot_base;
   try {
-    const int sb = a.slot_base;
     if (sb < 0 || sb + ng > (int)slots().size()) throw std::runtime_error("too many job groups");
     if (a.fp_world > 0 && a.fp_comm == nullptr) throw std::runtime_error("feature-parallel growth needs communicators");
     int dev = 0;
@@ -308,28 +312,38 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
     (void)tmog_hip_tree_prime();     // best effort, before the group threads' first launches (a failure here
                                      // leaves the lazy load to the first launch, as before)
     hipStream_t base = (hipStream_t)a.stream;
-    // One group: it runs on the caller's stream itself (no fork / join, one stream fewer sharing the process's
-    // few hardware queues -- boosting parts and concurrent learners each call with one group). The slot keeps
-    // its own stream for multi-group calls; every earlier use of the slot is ordered before `base` by the
-    // join of the call that made it, and a later multi-group call orders the slot's stream after `base` again.
     static const bool base_ok = [] { const char* e = std::getenv("TMOG_GROW_ON_BASE"); return !(e && e[0] == '0'); }();
-    const bool on_base = base_ok && ng == 1 && base != nullptr;
-    hipStream_t own0 = nullptr;
+    // Group 0 runs on the caller's stream itself (no fork / join for single-group calls: boosting parts and
+    // concurrent learners each call with one group). Other groups run on the stream the caller assigned to their
+    // slot (tmog_hip_slot_stream: a side stream of the process-wide set, ops/streams.py -- groups may share
+    // one), else on the slot's own stream. Every earlier use of a slot is ordered before `base` by the join of
+    // the call that made it; this call orders each group stream after `base` again.
+    const bool on_base = base_ok && base != nullptr;
+    std::vector<char> joined(ng, 0);
     hipEvent_t ready;
     hchk(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event");
     hchk(hipEventRecord(ready, base), "event record");
     for (int g = 0; g < ng; ++g) {
       GpuSlot& s = slots()[sb + g];
-      if (s.stream == nullptr || s.device != dev) {
-        hchk(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "stream");
-        s.device = dev;
+      hipStream_t use;
+      if (on_base && g == 0) {
+        use = base;
+      } else if (s.ext_set && a.fp_world == 0) {
+        use = s.ext;           // feature-parallel groups keep streams of their own (one collective order each)
+      } else {
+        if (s.stream == nullptr || s.device != dev) {
+          hchk(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "stream");
+          s.device = dev;
+        }
+        use = s.stream;
       }
-      if (on_base) {
-        own0 = s.stream;
-        s.stream = base;
-        continue;
+      own[g] = s.stream;
+      swapped = g + 1;
+      s.stream = use;
+      if (use != base) {
+        hchk(hipStreamWaitEvent(use, ready, 0), "wait ready");
+        joined[g] = 1;
       }
-      hchk(hipStreamWaitEvent(s.stream, ready, 0), "wait ready");
     }
     std::vector<std::string> errs(ng);
     std::vector<std::thread> th;
@@ -349,8 +363,8 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
       });
     }
     for (auto& t : th) t.join();
-    if (on_base) slots()[sb].stream = own0;
-    for (int g = 0; g < ng && !on_base; ++g) {
+    for (int g = 0; g < ng; ++g) {
+      if (!joined[g]) continue;
       hipEvent_t done;
       hchk(hipEventCreateWithFlags(&done, hipEventDisableTiming), "event");
       hchk(hipEventRecord(done, slots()[sb + g].stream), "event record");
@@ -358,11 +372,14 @@ void* tmog_hip_grow_forest(const tmog::GrowArgs* args) {
       hchk(hipEventDestroy(done), "event destroy");
     }
     hchk(hipEventDestroy(ready), "event destroy");
+    for (int g = 0; g < ng; ++g) slots()[sb + g].stream = own[g];
+    swapped = 0;
     for (int g = 0; g < ng; ++g)
       if (!errs[g].empty()) throw std::runtime_error("group " + std::to_string(g) + ": " + errs[g]);
   } catch (const std::exception& e) {
     res->status = -1;
     res->error = e.what();
+    for (int g = 0; g < swapped; ++g) slots()[sb + g].stream = own[g];
   }
   return res;
 }
@@ -376,6 +393,15 @@ void tmog_hip_grow_timing(int64_t* out, int reset) {
   out[2] = t.wait.load();
   out[3] = t.levels.load();
   if (reset) t.plan = t.issue = t.wait = t.levels = 0;
+}
+
+// The stream the job group using native slot `slot` runs on in later multi-group calls (null clears: the slot's
+// own stream). Set by models/tree_engine.py from the process-wide side streams before each such call.
+int tmog_hip_slot_stream(int slot, void* stream, int set) {
+  if (slot < 0 || slot >= (int)slots().size()) return -1;
+  slots()[slot].ext = (hipStream_t)stream;
+  slots()[slot].ext_set = set != 0;
+  return 0;
 }
 
 int tmog_hip_grow_status(void* h, char* msg, int cap) {

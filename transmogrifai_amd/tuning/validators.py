@@ -454,14 +454,15 @@ class OpValidator:
         token = threading.Event()       # set at the maxWait deadline: running fits stop at their next check
         gpu = dev.type == "cuda"
         cur = torch.cuda.current_stream(dev) if gpu else None
-        # lane 0 takes the longest learner (the critical path): its stream -- and the boosting parts' streams it
-        # starts (models/trees.py _run_parts inherits the priority) -- get the high scheduling priority
-        hi = -1 if os.environ.get("TMOG_LANE_PRIO", "1") != "0" else 0
-        streams = [torch.cuda.Stream(device=dev, priority=hi if w == 0 else 0) for w in range(lanes)] if gpu \
-            else [None] * lanes
-        for st in streams:
-            if st is not None:
+        # lane 0 runs on the caller's stream, the others on side streams of the fixed process-wide set
+        # (ops/streams.py: one stream per hardware queue); fewer free side streams -> fewer lanes
+        from ..ops import streams as SP
+        side = SP.lease(dev, lanes - 1) if gpu else []
+        if gpu:
+            lanes = 1 + len(side)
+            for st in side:
                 st.wait_stream(cur)
+        streams = ([cur] + side) if gpu else [None] * lanes
 
         def worker(w):
             try:
@@ -494,8 +495,10 @@ class OpValidator:
 
         th = [threading.Thread(target=worker, args=(w,), name=f"fit-lane-{w}", daemon=True) for w in range(lanes)]
         from ..utils.threads import fast_switch
-        # a lane returning from a native call must win the GIL back from one running Python promptly
-        with fast_switch(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))):
+        from ..utils.watchdog import Watchdog
+        # a lane returning from a native call must win the GIL back from one running Python promptly; the
+        # watchdog dumps every thread's stack if no fit makes progress for TMOG_WATCHDOG_S seconds
+        with fast_switch(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))), Watchdog("learner lanes"):
             for t in th:
                 t.start()
             bounded = self.max_wait < _UNBOUNDED_WAIT
@@ -505,6 +508,12 @@ class OpValidator:
                 token.set()                     # cooperative cancel, then join: nothing is left running
                 for t in th:
                     t.join()
+        if gpu:
+            for st in side:
+                cur.wait_stream(st)
+            # blocks freed on the lane streams are reused by later allocations only once their work has ended
+            torch.cuda.synchronize(dev)
+            SP.release(dev, side)
         with lock:
             if errs:
                 raise errs[0]
@@ -514,11 +523,6 @@ class OpValidator:
                 failures.append(f"{lname}: did not finish within maxWait={self.max_wait}s")
             for key in [k for k in results if k[0] in started]:
                 del results[key]
-        if gpu:
-            for st in streams:
-                cur.wait_stream(st)
-            # blocks freed on the lane streams are reused by later allocations only once their work has ended
-            torch.cuda.synchronize(dev)
         return dict(results), list(failures), dict(timings)
 
     def _fit_eval_bounded(self, lname, grid, mine, X, y, train_rows, val_rows, ctx, remaining: float):

@@ -13,6 +13,8 @@ import contextlib
 import threading
 from typing import Optional
 
+from . import watchdog as _watchdog
+
 _local = threading.local()
 
 
@@ -36,6 +38,9 @@ def scope(token: Optional[threading.Event]):
 
 
 def check() -> None:
+    """Raise :class:`FitCancelled` when this thread's token is set; also the fits' progress heartbeat
+    (utils/watchdog.py)."""
+    _watchdog.beat()
     tok = current()
     if tok is not None and tok.is_set():
         raise FitCancelled("fit cancelled: maxWait deadline passed")
