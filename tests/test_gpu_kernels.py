@@ -27,6 +27,24 @@ def test_col_stats_matches_fp64():
     assert _native_loaded()
 
 
+def test_masked_colsum_matches_fp64():
+    """RealVectorizer fill-with-mean: one masked multi-column sum launch vs the fp64 torch path."""
+    from transmogrifai_amd.ops import vector as V
+    g = torch.Generator().manual_seed(4)
+    cols = []
+    for j, n_ok in enumerate([1.0, 0.9, 0.0, 0.5, 1.0]):
+        x = torch.randn(300_001, generator=g) * (10 ** j)
+        valid = torch.rand(300_001, generator=g) < n_ok
+        x = x.to(torch.float64) if j == 3 else x.to(torch.float32)
+        cols.append(NumericColumn(T.Real, x, None if j == 4 else valid))
+    host = V.column_means(cols)
+    dev = V.column_means([c.to("cuda") if c.valid is not None else
+                          NumericColumn(T.Real, c.values.cuda(), None) for c in cols])
+    for a, b in zip(host, dev):
+        assert abs(a - b) <= 1e-9 * max(1.0, abs(a)), (a, b)
+    assert host[2] == 0.0 and dev[2] == 0.0
+
+
 def test_vectorize_numeric_matches_host():
     from transmogrifai_amd.ops import vector as V
     g = torch.Generator().manual_seed(1)

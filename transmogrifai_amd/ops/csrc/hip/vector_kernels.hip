@@ -94,9 +94,75 @@ __global__ void __launch_bounds__(256) gather_rows_cols_kernel(const float* cons
   }
 }
 
+// Masked column sums of many columns in one launch (RealVectorizer fill-with-mean, RealVectorizer.scala:82-86:
+// the mean of every column's non-null values). grid = (row chunks, columns); column c is fp32 (dtype 0) or fp64
+// (1), its validity bytes optional (null = all valid). Each thread keeps 4 independent row loads in flight per
+// step (rows r, r + 256, ...: every wave reads 256 B / 512 B runs), sums in fp64; the block's (sum, count)
+// goes to part[c][chunk] and the chunks are folded by the caller in a fixed order.
+constexpr int kSumUnroll = 4;
+
+__global__ void __launch_bounds__(256) masked_colsum_kernel(const void* const* __restrict__ vals,
+                                                            const uint8_t* const* __restrict__ valid,
+                                                            const int32_t* __restrict__ dtype, int64_t n,
+                                                            int64_t rows_per_chunk, double* __restrict__ part) {
+  const int c = blockIdx.y;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
+  const int64_t r1 = min(n, r0 + rows_per_chunk);
+  const uint8_t* ok = valid[c];
+  const bool f64 = dtype[c] == 1;
+  const float* vf = (const float*)vals[c];
+  const double* vd = (const double*)vals[c];
+  double s = 0.0, k = 0.0;
+  for (int64_t base = r0 + threadIdx.x; base < r1; base += 256 * kSumUnroll) {
+    double v[kSumUnroll];
+    bool m[kSumUnroll];
+#pragma unroll
+    for (int u = 0; u < kSumUnroll; ++u) {
+      const int64_t r = base + 256 * u;
+      const int64_t rc = min(r, r1 - 1);          // clamped, loads issued together; masked below
+      v[u] = f64 ? vd[rc] : (double)vf[rc];
+      m[u] = r < r1 && (ok == nullptr || ok[rc] != 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kSumUnroll; ++u)
+      if (m[u]) {
+        s += v[u];
+        k += 1.0;
+      }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    k += __shfl_xor(k, o, 64);
+  }
+  __shared__ double sh[2][4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][w] = s;
+    sh[1][w] = k;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double* o = part + ((int64_t)c * gridDim.x + blockIdx.x) * 2;
+    o[0] = (sh[0][0] + sh[0][1]) + (sh[0][2] + sh[0][3]);
+    o[1] = (sh[1][0] + sh[1][1]) + (sh[1][2] + sh[1][3]);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// part [n_cols][chunks][2] fp64 (sum, count) partials; chunks = ceil(n / rows_per_chunk).
+int tmog_hip_masked_colsum(const void* vals, const void* valid, const int32_t* dtype, int n_cols, int64_t n,
+                           int64_t rows_per_chunk, double* part, hipStream_t stream) {
+  if (n <= 0 || n_cols <= 0) return 0;
+  if (rows_per_chunk <= 0) return -1;
+  const int64_t chunks = (n + rows_per_chunk - 1) / rows_per_chunk;
+  if (chunks > (1 << 20) || n_cols > 65535) return -2;
+  hipLaunchKernelGGL(masked_colsum_kernel, dim3((unsigned)chunks, (unsigned)n_cols), dim3(256), 0, stream,
+                     (const void* const*)vals, (const uint8_t* const*)valid, dtype, n, rows_per_chunk, part);
+  return (int)hipGetLastError();
+}
 
 int tmog_hip_gather_rows_cols(const void* col_base, const int64_t* col_ld, const int64_t* rows, int64_t m, int k,
                               float* out, hipStream_t stream) {

@@ -24,13 +24,38 @@ def column_means(cols: Sequence[NumericColumn]) -> List[float]:
     from ..parallel import dp
     if not cols:
         return []
-    sums = torch.stack([torch.where(c.valid, c.values.to(torch.float64), torch.zeros((), dtype=torch.float64,
-                                                                                        device=c.values.device)).sum()
-                        for c in cols])
-    cnts = torch.stack([c.valid.sum().to(torch.float64) for c in cols])
+    dev = cols[0].values.device
+    if dev.type == "cuda" and all(c.values.dtype in (torch.float32, torch.float64) and c.values.dim() == 1
+                                  and len(c) == len(cols[0]) for c in cols) and len(cols[0]) > 0:
+        sums, cnts = _masked_colsums_hip(cols, dev)
+    else:
+        sums = torch.stack([torch.where(c.valid, c.values.to(torch.float64),
+                                        torch.zeros((), dtype=torch.float64, device=c.values.device)).sum()
+                            for c in cols])
+        cnts = torch.stack([c.valid.sum().to(torch.float64) for c in cols])
     sums, cnts = dp.sum_([sums, cnts])
     s, n = sums.cpu().numpy(), cnts.cpu().numpy()
     return [float(a / b) if b > 0 else float(a) for a, b in zip(s, n)]
+
+
+def _masked_colsums_hip(cols: Sequence[NumericColumn], dev):
+    """(sums, counts) fp64 of the valid values of every column: one ``masked_colsum_kernel`` launch over all
+    of them (vector_kernels.hip) instead of ~5 torch launches per column."""
+    n = len(cols[0])
+    vals = [c.values.contiguous() for c in cols]
+    oks = [c.valid.contiguous() if c.valid is not None else None for c in cols]
+    rpc = max(1 << 16, -(-n // max(1, 2048 // len(cols))))       # >= ~2048 workgroups in all
+    chunks = -(-n // rpc)
+    part = torch.empty(len(cols), chunks, 2, dtype=torch.float64, device=dev)
+    pk = Pack(dev)
+    i_v = pk.add(np.array([t.data_ptr() for t in vals], np.int64))
+    i_o = pk.add(np.array([t.data_ptr() if t is not None else 0 for t in oks], np.int64))
+    i_d = pk.add(np.array([1 if t.dtype == torch.float64 else 0 for t in vals], np.int32))
+    d = pk.ship()
+    N.check(N.hip().tmog_hip_masked_colsum(N.ptr(d[i_v]), N.ptr(d[i_o]), N.ptr(d[i_d]), len(cols), n, rpc,
+                                           N.ptr(part), N.stream(dev)), "masked_colsum")
+    tot = part.sum(1)
+    return tot[:, 0].contiguous(), tot[:, 1].contiguous()
 
 
 _MODE_RANGE = 1 << 20
