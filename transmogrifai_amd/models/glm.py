@@ -13,7 +13,6 @@ from typing import List
 import numpy as np
 import torch
 
-from .linear import tall_gram
 from .base import FitJob, Learner, OpPredictor, register_learner
 from ..stages.base import register_stage
 
@@ -108,9 +107,13 @@ class GeneralizedLinearRegressionLearner(Learner):
         g, ginv, gprime = _link(link, link_power)
         var = FAMILIES[fam][0]
         Xa = torch.cat([Xd, torch.ones(N, 1, dtype=torch.float64, device=dev)], 1)     # [N, d+1]
+        from ..ops.stats import weighted_gram
+        Xg = X if (X.is_cuda and X.dtype == torch.float32) else Xd      # the Gram kernel widens fp32 itself
+        # weighted column sums and sums of squares of every problem: row d and the diagonal of [X | 1]'s Gram
+        G0 = weighted_gram(Xg, W0)
         wsum = W0.sum(0).clamp_min(1e-300)
-        mean = tall_gram(Xd, W0) / wsum[None, :]
-        var_x = tall_gram(Xd * Xd, W0) / wsum[None, :] - mean * mean
+        mean = G0[:, :d, d].t() / wsum[None, :]
+        var_x = torch.diagonal(G0[:, :d, :d], dim1=1, dim2=2).t() / wsum[None, :] - mean * mean
         mu = _init_mu(fam, yd)[:, None].expand(N, P).clone()
         beta = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)
         it = 0
@@ -122,9 +125,11 @@ class GeneralizedLinearRegressionLearner(Learner):
             z = eta + (yd[:, None] - mu) * gp
             w = W0 / (gp * gp * var(mu, vp)).clamp_min(1e-300)
             w = torch.nan_to_num(w, nan=0.0, posinf=0.0)
-            # batched weighted normal equations (row-blocked batched GEMMs: tall_gram)
-            A = torch.stack([tall_gram(Xa, Xa * w[:, p:p + 1]) for p in range(P)])
-            b = torch.stack([tall_gram(Xa, (w[:, p] * z[:, p])[:, None])[:, 0] for p in range(P)])
+            # batched weighted normal equations: the Gram of [X | 1 | z_p] under w_p holds both
+            # A_p = Xa^T W_p Xa and b_p = Xa^T W_p z_p (fp64 matrix cores, one pass for all problems)
+            Gz = weighted_gram(Xg, w, z)
+            A = Gz[:, :d + 1, :d + 1].contiguous()
+            b = Gz[:, :d + 1, d + 1].contiguous()
             pen = torch.zeros(P, d + 1, dtype=torch.float64, device=dev)
             pen[:, :d] = (reg * wsum)[:, None] * var_x.t().clamp_min(0)
             A = A + torch.diag_embed(pen)

@@ -262,30 +262,11 @@ def _weighted_grams(X, y, jobs, par=None, chunk: int = 1 << 18):
         sl = par.row_slice(N)
         X, W, yd = X[sl], W[sl], yd[sl]
         N = int(X.shape[0])
-    G = torch.zeros(len(keys), d + 2, d + 2, dtype=torch.float64, device=dev)
-    for a in range(0, N, chunk):
-        Xc = X[a:a + chunk].to(torch.float64)
-        A = torch.cat([Xc, torch.ones(Xc.shape[0], 1, dtype=torch.float64, device=dev), yd[a:a + chunk, None]], 1)
-        for g in range(len(keys)):
-            G[g] += tall_gram(A, A * W[a:a + chunk, g:g + 1])
+    from ..ops.stats import weighted_gram
+    # fp64 matrix-core Grams of [X | 1 | y] for every fold-weight column in one pass (stats_kernels.hip wgram)
+    G = weighted_gram(X, W, yd, chunk=chunk)
     G = _psum(par, G)[0]
     return G, group
-
-
-def tall_gram(A: torch.Tensor, B: torch.Tensor, blocks: int = 256) -> torch.Tensor:
-    """``A^T B`` for tall, narrow fp64 operands (``[n, p]``, ``n >> p``). A single GEMM gives the library one
-    or two output tiles and a sequential reduction over all n rows (the regression config spent ~5 s in
-    three of them); here the rows are cut into ``blocks`` row blocks multiplied as one batched GEMM (every
-    CU busy) and the block products summed."""
-    n = A.shape[0]
-    if A.device.type != "cuda" or n < 8 * blocks:
-        return A.t() @ B
-    rb = -(-n // blocks)
-    pad = rb * blocks - n
-    if pad:
-        A = torch.cat([A, A.new_zeros(pad, A.shape[1])])
-        B = torch.cat([B, B.new_zeros(pad, B.shape[1])])
-    return torch.bmm(A.view(blocks, rb, -1).transpose(1, 2), B.view(blocks, rb, -1)).sum(0)
 
 
 def _owlqn_direction_torch(U, g, l1, has_l1, S, Y, RHO, hist_n, m):

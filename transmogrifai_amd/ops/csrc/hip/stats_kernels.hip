@@ -15,6 +15,7 @@
 //   gives the label x column contingency sums (onehot(y)^T (X - mu), + n_l mu on the host) and the
 //   label counts -- all in one pass over the sampled rows.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdlib>
 #include <stdint.h>
 #include <float.h>
@@ -225,6 +226,153 @@ __global__ void __launch_bounds__(256) gram_fold_kernel(const double* __restrict
   }
 }
 
+// ------------------------------------------------------------------------------- weighted fp64 Grams
+// wgram_kernel / wgram_fold_kernel -- the normal-equation statistics of the linear learners (SURVEY.md K22:
+// Spark WeightedLeastSquares / IRLS, OpLinearRegression.scala:48-209, OpGeneralizedLinearRegression.scala:
+// 49-203): G_k = A_k^T diag(w_k) A_k with A_k = [X | 1 | y_k] for K weight columns at once, on the fp64
+// matrix cores (v_mfma_f64_16x16x4_f64: exact fp64 products and sums, the numerics of the fp64 library GEMM
+// it replaces). X is read as fp32 and widened in LDS; the weights and the optional per-weight (or shared)
+// response are fp64. Workgroup = one 64x64 output tile pair (upper triangle) x one row chunk x KW weights;
+// 4 waves each own a 32x32 quadrant (2x2 accumulators of 16x16 per weight), the weight scales the A
+// operand in registers and the response column is substituted per weight, so one LDS stage of X serves all
+// KW weights. Chunk partials are summed in a fixed order by the fold kernel (deterministic), which mirrors
+// the tiles into the full symmetric matrices.
+using f64x4 = __attribute__((ext_vector_type(4))) double;
+
+constexpr int WT = 64;      // output tile edge
+constexpr int WK = 16;      // rows per LDS stage
+constexpr int KW = 4;       // weight columns per workgroup
+
+struct WGramArgs {
+  const float* X;
+  int64_t n;
+  int d;
+  int64_t ldx;
+  const double* W;          // [n][ldw], columns 0..K-1
+  int64_t ldw;
+  const double* Y;          // [n][ldy] or null; column k (per_weight) or 0
+  int64_t ldy;
+  int per_weight;
+  int D;                    // d + 1 (+ 1 with Y)
+  int K;
+  int nt;
+  int npairs;
+  int64_t rpc;
+  double* part;             // [chunks][npairs][K][WT][WT]
+};
+
+__device__ __forceinline__ TilePair wtile_pair(int p, int nt) { return tile_pair(p, nt); }
+
+__global__ void __launch_bounds__(256) wgram_kernel(WGramArgs a) {
+  __shared__ double tA[WK][WT + 1];
+  __shared__ double tB[WK][WT + 1];
+  __shared__ double tw[WK][KW];
+  __shared__ double ty[WK][KW];
+  const TilePair tp = wtile_pair(blockIdx.x, a.nt);
+  const int ca = tp.i * WT, cb = tp.j * WT;
+  const int w0 = blockIdx.z * KW;
+  const int64_t r0 = (int64_t)blockIdx.y * a.rpc;
+  const int64_t r1 = min(a.n, r0 + a.rpc);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qa = (wave >> 1) * 32, qb = (wave & 1) * 32;
+  const int li = lane & 15, lk = lane >> 4;
+  const int ycol = a.Y ? a.d + 1 : -1;
+  const int cc = threadIdx.x & (WT - 1), rsub = threadIdx.x >> 6;   // loader: column cc, rows rsub + 4u
+  f64x4 acc[KW][2][2];
+#pragma unroll
+  for (int k = 0; k < KW; ++k)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) acc[k][x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+  // this lane's operand columns (fixed for the whole kernel)
+  int colA[2], colB[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    colA[x] = ca + qa + 16 * x + li;
+    colB[x] = cb + qb + 16 * x + li;
+  }
+  for (int64_t rs = r0; rs < r1; rs += WK) {
+#pragma unroll
+    for (int u = 0; u < WK / 4; ++u) {
+      const int rr = rsub + 4 * u;
+      const int64_t r = rs + rr;
+      const int64_t rc = min(r, r1 - 1);
+      const int c1 = ca + cc, c2 = cb + cc;
+      const float x1 = a.X[rc * a.ldx + min(c1, a.d - 1)];
+      const float x2 = a.X[rc * a.ldx + min(c2, a.d - 1)];
+      const bool in = r < r1;
+      tA[rr][cc] = !in ? 0.0 : (c1 < a.d ? (double)x1 : (c1 == a.d ? 1.0 : 0.0));
+      tB[rr][cc] = !in ? 0.0 : (c2 < a.d ? (double)x2 : (c2 == a.d ? 1.0 : 0.0));
+    }
+    if (threadIdx.x < WK * KW) {
+      const int rr = threadIdx.x / KW, k = threadIdx.x % KW;
+      const int64_t r = rs + rr;
+      const bool ok = r < r1 && w0 + k < a.K;
+      tw[rr][k] = ok ? a.W[r * a.ldw + w0 + k] : 0.0;
+      ty[rr][k] = (ok && a.Y) ? a.Y[r * a.ldy + (a.per_weight ? w0 + k : 0)] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < WK / 4; ++s) {
+      const int kk = 4 * s + lk;
+      double av[2], bv[2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        av[x] = tA[kk][qa + 16 * x + li];
+        bv[x] = tB[kk][qb + 16 * x + li];
+      }
+#pragma unroll
+      for (int k = 0; k < KW; ++k) {
+        const double w = tw[kk][k], yk = ty[kk][k];
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          const double aw = (colA[x] == ycol ? yk : av[x]) * w;
+#pragma unroll
+          for (int y = 0; y < 2; ++y) {
+            const double b = colB[y] == ycol ? yk : bv[y];
+            acc[k][x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(aw, b, acc[k][x][y], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // f64 16x16x4 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+  for (int k = 0; k < KW; ++k) {
+    if (w0 + k >= a.K) break;
+    double* out = a.part + (((int64_t)blockIdx.y * a.npairs + blockIdx.x) * a.K + w0 + k) * WT * WT;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = qa + 16 * x + lk + 4 * e;
+          const int col = qb + 16 * y + li;
+          out[row * WT + col] = acc[k][x][y][e];
+        }
+  }
+}
+
+// G[k][D][D] = sum over chunks of the tile partials, mirrored into the lower triangle. grid (WT*WT/256, npairs, K)
+__global__ void __launch_bounds__(256) wgram_fold_kernel(const double* __restrict__ part, int chunks, int npairs,
+                                                         int K, int nt, int D, double* __restrict__ G) {
+  const int p = blockIdx.y, k = blockIdx.z;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= WT * WT) return;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += part[(((int64_t)c * npairs + p) * K + k) * WT * WT + e];
+  const TilePair tp = tile_pair(p, nt);
+  const int i = tp.i * WT + e / WT, j = tp.j * WT + e % WT;
+  if (i < D && j < D) {
+    double* g = G + (int64_t)k * D * D;
+    g[(int64_t)i * D + j] = s;
+    g[(int64_t)j * D + i] = s;
+  }
+}
+
 // Per-problem, per-class column sums (the label x column contingency and the
 // NaiveBayes class feature sums): part[chunk][p * L + c][j] = sum of X[r][j] over rows r of the chunk with
 // codes[p][r] == c (-1 = row not in problem p). Lane = column (64 per workgroup), wave = row stride; every
@@ -311,6 +459,36 @@ int tmog_hip_col_stats(const float* X, const void* unused, int64_t n, int d, int
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(col_partials_kernel, dim3(cblocks, (unsigned)chunks), dim3(256), 0, stream, X, n, d, ld, rpc, part);
   hipLaunchKernelGGL(col_fold_kernel, dim3((d + 255) / 256), dim3(256), 0, stream, part, (int)chunks, d, out);
+  hipFreeAsync(part, stream);
+  return (int)hipGetLastError();
+}
+
+// G (fp64, [K][D][D], fully written; D = d + 1 + (Y != null)) = A_k^T diag(W[:, k]) A_k, A_k = [X | 1 | Y[:, k]]
+// (Y column 0 for every k unless per_weight). X fp32 [n][ldx]; W, Y fp64.
+int tmog_hip_wgram(const float* X, int64_t n, int d, int64_t ldx, const double* W, int64_t ldw, int K,
+                   const double* Y, int64_t ldy, int per_weight, double* G, hipStream_t stream) {
+  if (n <= 0 || d <= 0 || K <= 0) return -1;
+  const int D = d + 1 + (Y ? 1 : 0);
+  const int nt = (D + WT - 1) / WT;
+  const int npairs = nt * (nt + 1) / 2;
+  const int kg = (K + KW - 1) / KW;
+  // partials bounded to ~128 MB; >= ~512 workgroups when the rows allow
+  const int64_t per_chunk = (int64_t)npairs * K * WT * WT * (int64_t)sizeof(double);
+  int64_t chunks = (512 + (int64_t)npairs * kg - 1) / ((int64_t)npairs * kg);
+  const int64_t max_chunks = std::max<int64_t>(1, ((int64_t)128 << 20) / per_chunk);
+  chunks = std::min(chunks, max_chunks);
+  chunks = std::min(chunks, (n + 255) / 256);
+  chunks = std::max<int64_t>(chunks, 1);
+  int64_t rpc = (n + chunks - 1) / chunks;
+  rpc = (rpc + WK - 1) / WK * WK;
+  chunks = (n + rpc - 1) / rpc;
+  double* part = nullptr;
+  hipError_t e = hipMallocAsync((void**)&part, per_chunk * chunks, stream);
+  if (e != hipSuccess) return (int)e;
+  WGramArgs a{X, n, d, ldx, W, ldw, Y, ldy, per_weight, D, K, nt, npairs, rpc, part};
+  hipLaunchKernelGGL(wgram_kernel, dim3((unsigned)npairs, (unsigned)chunks, (unsigned)kg), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(wgram_fold_kernel, dim3(WT * WT / 256, (unsigned)npairs, (unsigned)K), dim3(256), 0, stream, part,
+                     (int)chunks, npairs, K, nt, D, G);
   hipFreeAsync(part, stream);
   return (int)hipGetLastError();
 }

@@ -211,3 +211,42 @@ def label_column_sums(X: torch.Tensor, y: torch.Tensor):
     cnt = torch.bincount(inv, minlength=L).to(torch.float64)
     sums, cnt = dp.sum_([sums, cnt])
     return labels, sums, cnt
+
+
+def weighted_gram(X: torch.Tensor, W: torch.Tensor, Y: Optional[torch.Tensor] = None,
+                  chunk: int = 1 << 18) -> torch.Tensor:
+    """``[K, D, D]`` fp64 weighted Grams ``A_k^T diag(W[:, k]) A_k`` with ``A_k = [X | 1 | Y_k]`` (``D = d + 1``,
+    ``+ 1`` with ``Y``): the normal-equation statistics of the linear learners (Spark WeightedLeastSquares /
+    IRLS). ``Y`` is ``[n]`` (one response shared by every weight column) or ``[n, K]`` (one per column, the
+    IRLS working responses). fp32 device ``X`` runs the HIP fp64-MFMA kernel (``stats_kernels.hip``
+    ``wgram_kernel``: X read once per tile pair for 4 weight columns, exact fp64 products); otherwise the
+    row-chunked fp64 torch reference."""
+    n, d = int(X.shape[0]), int(X.shape[1])
+    K = int(W.shape[1])
+    dev = X.device
+    D = d + 1 + (0 if Y is None else 1)
+    per_weight = Y is not None and Y.dim() == 2
+    if Y is not None and Y.dim() == 2 and int(Y.shape[1]) != K:
+        raise ValueError("Y must be [n] or [n, K]")
+    if dev.type == "cuda" and X.dtype == torch.float32 and X.stride(1) == 1 and n > 0 and d > 0 and K > 0:
+        Wd = W.to(torch.float64).contiguous()
+        Yd = None if Y is None else Y.to(torch.float64).contiguous()
+        G = torch.empty(K, D, D, dtype=torch.float64, device=dev)
+        N.check(N.hip().tmog_hip_wgram(N.ptr(X), n, d, X.stride(0), N.ptr(Wd), K, K, N.ptr(Yd),
+                                       (K if per_weight else 1) if Yd is not None else 0, int(per_weight),
+                                       N.ptr(G), N.stream(dev)), "wgram")
+        return G
+    G = torch.zeros(K, D, D, dtype=torch.float64, device=dev)
+    for a in range(0, n, chunk):
+        Xc = X[a:a + chunk].to(torch.float64)
+        m = Xc.shape[0]
+        base = torch.cat([Xc, torch.ones(m, 1, dtype=torch.float64, device=dev)], 1)
+        Wc = W[a:a + chunk].to(torch.float64)
+        for k in range(K):
+            if Y is None:
+                A = base
+            else:
+                yk = (Y[a:a + chunk, k] if per_weight else Y[a:a + chunk]).to(torch.float64)
+                A = torch.cat([base, yk[:, None]], 1)
+            G[k] += A.t() @ (A * Wc[:, k:k + 1])
+    return G
