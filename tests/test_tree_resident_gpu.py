@@ -52,7 +52,7 @@ def test_resident_trees_match_host_planned(F, n_one, chunk, depth):
     res = _grow(pb, True, chunk)
     assert isinstance(res, te.ResidentTree), "device-planned path not taken"
     (dev_forest,) = te.resident_forests([res])
-    for name in ("tree_off", "nodes", "dl", "value", "gain", "cover"):
+    for name in ("tree_off", "nodes", "default_left", "value", "gain", "cover", "tree_model"):
         np.testing.assert_array_equal(getattr(host, name), getattr(dev_forest, name), err_msg=name)
     n_rows = int(pb["Xb"].shape[0])
     kh, gh, vh = _per_row(host.leaf_assign, n_rows)

@@ -844,11 +844,13 @@ def _quant_scales(mode, S, jobs, t1f, t2f, rows, chunk_rows, dev, amax_hint=None
         return m.expand(n_models) if m.numel() == 1 else m[:n_models]
 
     def pow2(bound):
-        # 2^floor(log2 x), exponent read exactly with frexp (x = m 2^e, m in [0.5, 1)) -- the fused round
-        # prologue (boost_kernels.hip pow2_scale) computes the same bits
-        x = qmax / (bound * wmax).clamp_min(1e-30)
-        _, e = torch.frexp(x)
-        return torch.ldexp(torch.ones_like(x), (e - 1).clamp(-60, 60))
+        # 2^floor(log2 x) built from the exponent bits of x = qmax / bound (an IEEE division, not torch's
+        # reciprocal-times-scalar): exact and identical on every device, and the same bits as the fused round
+        # prologue (boost_kernels.hip pow2_scale)
+        b = (bound * wmax).to(torch.float32).clamp_min(1e-30)
+        x = torch.full_like(b, qmax) / b
+        e = ((x.view(torch.int32) >> 23) & 0xFF) - 127
+        return ((e.clamp(-60, 60) + 127) << 23).to(torch.int32).view(torch.float32)
 
     if mode == MODE_VAR:
         m1 = amax(t1f)

@@ -144,17 +144,16 @@ __global__ void __launch_bounds__(256) boost_epilogue_kernel(
 //   * the quantisation maxima of the new (g, h): max(rows outside the job's training set, the last
 //     epilogue's per-copy maxima tam_prev) -> amax[p] (tree_engine._quant_scales' amax_hint),
 //   * the power-of-two fixed-point scales q = 2^floor(log2(qmax / max(amax, 1e-30))) clamped to 2^[-60, 60]
-//     (exponent taken with frexp: exact, as tree_engine._quant_scales computes it) -> qscale[p], qinv[p],
+//     (built from the exponent bits: exact, as tree_engine._quant_scales computes it) -> qscale[p], qinv[p],
 //   * every root entry copied into the grower's row buffer and its quantised (q(w g), q(w h)) staged
 //     (tree_engine._stage_gh: rintf((w * t) * q), the same fp32 operation order),
 //   * the job's copies of the NEXT epilogue's maxima buffer zeroed (double buffered by the caller).
 // Every block recomputes the T scales from the (tiny) maxima tables; block 0 writes them out.
 __device__ __forceinline__ float pow2_scale(float qmax, float a) {
   const float x = qmax / fmaxf(a, 1e-30f);
-  int e;
-  (void)frexpf(x, &e);                       // x = m 2^e, m in [0.5, 1): floor(log2 x) = e - 1
-  const int k = min(60, max(-60, e - 1));
-  return ldexpf(1.f, k);
+  const int e = (int)((__float_as_uint(x) >> 23) & 0xFFu) - 127;   // floor(log2 x) for normal x
+  const int k = min(60, max(-60, e));
+  return __uint_as_float((uint32_t)(k + 127) << 23);
 }
 
 constexpr int kMaxProJobs = 64;

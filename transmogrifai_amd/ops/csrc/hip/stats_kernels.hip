@@ -365,6 +365,9 @@ __global__ void __launch_bounds__(256) wgram_fold_kernel(const double* __restric
   double s = 0.0;
   for (int c = 0; c < chunks; ++c) s += part[(((int64_t)c * npairs + p) * K + k) * WT * WT + e];
   const TilePair tp = tile_pair(p, nt);
+  // a diagonal tile holds both (i, j) and (j, i), computed with different roundings (the weight scales the
+  // A operand): its upper triangle alone is mirrored, so the result is symmetric and race-free
+  if (tp.i == tp.j && e / WT > e % WT) return;
   const int i = tp.i * WT + e / WT, j = tp.j * WT + e % WT;
   if (i < D && j < D) {
     double* g = G + (int64_t)k * D * D;
