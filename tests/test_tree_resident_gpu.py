@@ -44,10 +44,12 @@ def _per_row(la, n_rows):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F,n_one,chunk,depth", [(136, 12, 4096, 7), (68, 0, 1024, 5), (200, 24, 512, 9),
-                                                 (66, 10, 4096, 6)])
-def test_resident_trees_match_host_planned(F, n_one, chunk, depth):
-    pb = _problem("cuda", F=F, n_one=n_one, depth=depth)
+@pytest.mark.parametrize("F,n_one,chunk,depth,gamma", [(136, 12, 4096, 7, 0.1), (68, 0, 1024, 5, 0.1),
+                                                       (200, 24, 512, 9, 0.1), (66, 10, 4096, 6, 0.1),
+                                                       (136, 12, 4096, 8, 0.0)])
+def test_resident_trees_match_host_planned(F, n_one, chunk, depth, gamma):
+    """gamma 0: the finalisation's no-pruning fast path; gamma > 0: level-wise pruning."""
+    pb = _problem("cuda", F=F, n_one=n_one, depth=depth, gamma=gamma)
     host = _grow(pb, False, chunk)
     res = _grow(pb, True, chunk)
     assert isinstance(res, te.ResidentTree), "device-planned path not taken"

@@ -933,6 +933,15 @@ class XGBoostClassifierLearner(_BoostLearner):
                 NV.hip().tmog_hip_grow_timing(tm.ctypes.data, 1)
                 rep["native"] = {"plan_s": tm[0] / 1e9, "issue_s": tm[1] / 1e9, "wait_s": tm[2] / 1e9,
                                  "levels": int(tm[3])}
+            if dev.type == "cuda" and os.environ.get("TMOG_PLAN_PROFILE") == "1":
+                from ..ops import _native as NV
+                torch.cuda.synchronize(dev)
+                pp = np.zeros(32, np.uint64)
+                NV.hip().tmog_hip_plan_profile(pp.ctypes.data, 1)
+                calls = max(1, int(pp[31]))
+                # mean microseconds per level_plan_kernel call in each phase (100 MHz wall clock)
+                rep["plan_phase_us"] = {"calls": int(pp[31]),
+                                        **{str(k): round(float(pp[k]) / 100.0 / calls, 2) for k in range(12)}}
             _sys.stderr.write("[xgb-profile] " + json.dumps(rep) + "\n")
             _XGB_PROF.clear()
         res = []

@@ -143,35 +143,67 @@ struct PlanArgs {
   int32_t* flag;
   int32_t* loc;
   int64_t cap_nl, cap_m, cap_nodes, cap_h, cap_c, cap_l;
+  int profile;                 // TMOG_PLAN_PROFILE: per-phase wall-clock ticks into g_plan_prof
 };
+
+// TMOG_PLAN_PROFILE diagnostics: wall-clock ticks (100 MHz) spent in each phase of level_plan_kernel, summed
+// over calls (entry 31: calls); read with tmog_hip_plan_profile.
+__device__ unsigned long long g_plan_prof[32];
 
 __device__ __forceinline__ int64_t dbits(double v) { return __double_as_longlong(v); }
 __device__ __forceinline__ double bitsd(int64_t v) { return __longlong_as_double(v); }
 
-// Exclusive prefix sums of v[0, n) in place; every thread of the block calls it and gets the total.
-__device__ int64_t block_scan(int64_t* v, int64_t n, int64_t* sh) {
-  const int t = threadIdx.x, nt = blockDim.x;
+// Exclusive prefix sums of K arrays v[k][0, n) in place at once; every thread of the block calls it and gets the
+// totals. Each thread sums a contiguous run of ceil(n / 1024) entries, the runs are scanned inside each wave on
+// the lane network (6 shuffle steps, no barrier), the 16 wave totals go through LDS: two barriers per call
+// whatever K, instead of 2 log2(1024) per array.
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t x, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+template <int K>
+__device__ void block_scan_multi(int64_t* const (&v)[K], int64_t n, int64_t (&total)[K], int64_t* sh) {
+  const int t = threadIdx.x, nt = blockDim.x, lane = t & 63, wave = t >> 6, nw = nt >> 6;
   const int64_t per = (n + nt - 1) / nt;
   const int64_t lo = min(n, (int64_t)t * per), hi = min(n, lo + per);
-  int64_t s = 0;
-  for (int64_t i = lo; i < hi; ++i) s += v[i];
-  sh[t] = s;
-  __syncthreads();
-  for (int off = 1; off < nt; off <<= 1) {
-    const int64_t x = t >= off ? sh[t - off] : 0;
-    __syncthreads();
-    sh[t] += x;
-    __syncthreads();
-  }
-  int64_t run = sh[t] - s;
-  const int64_t total = sh[nt - 1];
-  for (int64_t i = lo; i < hi; ++i) {
-    const int64_t x = v[i];
-    v[i] = run;
-    run += x;
+  int64_t s[K], incl[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    s[k] = 0;
+    for (int64_t i = lo; i < hi; ++i) s[k] += v[k][i];
+    incl[k] = wave_incl_scan(s[k], lane);
+    if (lane == 63) sh[k * 16 + wave] = incl[k];
   }
   __syncthreads();
-  return total;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    int64_t before = 0, all = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int64_t x = sh[k * 16 + w];
+      before += w < wave ? x : 0;
+      all += x;
+    }
+    total[k] = all;
+    int64_t run = before + incl[k] - s[k];
+    for (int64_t i = lo; i < hi; ++i) {
+      const int64_t x = v[k][i];
+      v[k][i] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ int64_t block_scan(int64_t* v, int64_t n, int64_t* sh) {
+  int64_t* const a[1] = {v};
+  int64_t tot[1];
+  block_scan_multi<1>(a, n, tot, sh);
+  return tot[0];
 }
 
 // last i in [0, n) with pre[i] <= k (pre: exclusive prefix sums, k < total): the owner of item k
@@ -213,8 +245,10 @@ __device__ void emit_leaves(const PlanArgs& A, int lvl, int n, const int32_t* sp
   const int64_t lbase = *A.leaf_pos;
   const int64_t nl0 = A.cnt[C_NL];
   __syncthreads();
-  const int64_t tot_rows = block_scan(A.sd, n, sh);
-  const int64_t tot_items = block_scan(A.se, n, sh);
+  int64_t* const arr[2] = {A.sd, A.se};
+  int64_t tots[2];
+  block_scan_multi<2>(arr, n, tots, sh);
+  const int64_t tot_rows = tots[0], tot_items = tots[1];
   const int64_t n_emit = min(tot_items, A.cap_l - nl0);
   for (int64_t k = t; k < n_emit; k += nt) {
     const int64_t i = owner(A.se, n, k);
@@ -245,6 +279,18 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
   const int t = threadIdx.x, nt = blockDim.x;
   const int d = A.d, S = A.S, T = A.T;
   auto R = [&](int64_t g) { return A.rec + (g + 1) * (int64_t)A.W; };
+  uint64_t t_prev = 0;
+  if (A.profile && t == 0) {
+    t_prev = wall_clock64();
+    atomicAdd(&g_plan_prof[31], 1ull);
+  }
+  auto mark = [&](int k) {
+    if (A.profile && t == 0) {
+      const uint64_t now = wall_clock64();
+      atomicAdd(&g_plan_prof[k], (unsigned long long)(now - t_prev));
+      t_prev = now;
+    }
+  };
   if (t == 0) {
     s_n_prev = d > 0 ? A.cnt[C_N] : 0;
     s_m_prev = d > 0 ? A.cnt[C_M] : 0;
@@ -277,6 +323,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     for (int j = t; j < T; j += nt) init_node(R(j), j, S);
     n = T;
     __syncthreads();
+  mark(0);
   } else {
     const int P = (d - 1) & 1;
     const int n_prev = s_n_prev, m_prev = s_m_prev;
@@ -301,8 +348,10 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
       A.sa[j] = ok ? 1 : 0;
     }
     __syncthreads();
+    mark(1);
     // (b) leaves of level d - 1: every node that does not split, from the buffer level d - 1 read
     emit_leaves(A, P, n_prev, A.flag, P, sh);
+    mark(2);
     // (c) splits -> records + children (level d)
     const int64_t ns = block_scan(A.sa, m_prev, sh);
     const int base = s_created;
@@ -355,6 +404,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     n = (int)(2 * ns);
     if (t == 0) A.cnt[C_NCREATED] = base + n;
     __syncthreads();
+    mark(3);
   }
   if (n == 0) {
     if (t == 0) {
@@ -377,6 +427,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     A.sa[i] = (can || d == 0) ? 1 : 0;
   }
   __syncthreads();
+  mark(4);
   if (A.subtract && d > 0) {
     for (int q = t; 2 * q + 1 < n; q += nt) {
       const int li = 2 * q, ri = li + 1;
@@ -389,6 +440,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
   for (int i = t; i < n; i += nt) A.sb[i] = A.sa[i];     // need flags (sa becomes positions)
   __syncthreads();
   const int m = (int)block_scan(A.sa, n, sh);
+  mark(5);
   if (m > A.cap_m) {                       // (cannot happen: caps bound every level)
     if (t == 0) {
       A.cnt[C_ERR] |= 2;
@@ -432,6 +484,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     Pp[7] = A.flag[i] ? 1.f : 0.f;
   }
   __syncthreads();
+  mark(6);
   // ---- sibling pairs: (small, big) histogram node ids, parent offsets; big nodes are derived (flag = is_big)
   for (int j = t; j < m; j += nt) A.flag[j] = 0;
   __syncthreads();
@@ -458,6 +511,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     }
     __syncthreads();
   }
+  mark(7);
   // ---- per-node work counts: wide / other histogram items, partition items, zero segments
   const bool dense_split = A.live_dense >= 0 && A.live_dense < A.hsz;
   for (int j = t; j < m; j += nt) {
@@ -484,11 +538,12 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     A.se[j] = build && nch == 1 && has_csr && ncsr > 1 && dense_split ? 1 : 0;
   }
   __syncthreads();
-  const int64_t n_wide = block_scan(A.sa, m, sh);
-  const int64_t n_other = block_scan(A.sb, m, sh);
-  const int64_t n_part = block_scan(A.sc, m, sh);
-  const int64_t n_zw = block_scan(A.sd, m, sh);
-  const int64_t n_zc = block_scan(A.se, m, sh);
+  mark(8);
+  int64_t* const arr5[5] = {A.sa, A.sb, A.sc, A.sd, A.se};
+  int64_t tot5[5];
+  block_scan_multi<5>(arr5, m, tot5, sh);
+  const int64_t n_wide = tot5[0], n_other = tot5[1], n_part = tot5[2], n_zw = tot5[3], n_zc = tot5[4];
+  mark(9);
   const int64_t n_hist = n_wide + n_other;
   const int64_t h_emit = min(n_hist, A.cap_h), c_emit = min(n_part, A.cap_c);
   // histogram items, wide-load items first (the host's stable partition), then the others
@@ -525,6 +580,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
       break;
     }
   }
+  mark(10);
   // partition items of every scanned node (kPartRows-row slices)
   for (int64_t k = t; k < c_emit; k += nt) {
     const int64_t j = owner(A.sc, m, k);
@@ -561,10 +617,12 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     A.cnt[C_NZD] = (int)n_zw;
     if (h_emit < n_hist || c_emit < n_part) A.cnt[C_ERR] |= 2;
   }
+  mark(11);
 }
 
 struct FinArgs {
   int T, S, mode, kind, n_levels;
+  int prune;                   // some job has gamma > 0 (Newton): pruning can happen
   int64_t* rec;
   int W;
   const int32_t* level_off;
@@ -590,6 +648,27 @@ __global__ void __launch_bounds__(1024) tree_finalize_kernel(FinArgs A) {
   const int t = threadIdx.x, nt = blockDim.x;
   const int64_t n = A.cnt[C_NCREATED];
   auto R = [&](int64_t g) { return A.rec + (g + 1) * (int64_t)A.W; };
+  if (!(A.kind == 3 && A.prune)) {
+    // nothing can be pruned (no gamma > 0: a recorded split's gain exceeds split_eps > 0), so every created
+    // node is reachable and keeps its own value: one pass, no level loops
+    for (int64_t i = t; i < n; i += nt) {
+      const int64_t* r = R(i);
+      const int64_t jt = r[0];
+      const double t0 = bitsd(r[kRecFixed]);
+      const double t1 = A.S > 1 ? bitsd(r[kRecFixed + 1]) : 0.0;
+      double v;
+      if (A.mode == 1) v = t0 > 0 ? t1 / fmax(t0, 1e-300) : 0.0;
+      else v = -t0 / (t1 + A.j_lam[jt]) * A.j_eta[jt];
+      A.gid_value[i] = (float)v;
+      A.gid_tree[i] = jt;
+    }
+    if (t == 0) {
+      A.rec[0] = n;
+      A.rec[1] = *A.leaf_pos;
+      A.rec[2] = A.cnt[C_ERR];
+    }
+    return;
+  }
   for (int64_t i = t; i < n; i += nt) {
     const int64_t* r = R(i);
     const int64_t jt = r[0];
@@ -792,6 +871,18 @@ int64_t tmog_hip_resident_cap_nodes(const tmog::GrowArgs* args) {
   return caps_of(a, L, 1).cap_nodes;
 }
 
+// TMOG_PLAN_PROFILE: copy the planner's per-phase tick sums (32 entries, 100 MHz wall clock; [31] = calls).
+int tmog_hip_plan_profile(uint64_t* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_plan_prof), sizeof(unsigned long long) * 32, 0,
+                                     hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return (int)e;
+  if (reset) {
+    static const unsigned long long zero[32] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_plan_prof), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+  }
+  return (int)e;
+}
+
 int tmog_hip_resident_error(char* msg, int cap) {
   if (msg && cap > 0) {
     std::strncpy(msg, g_err.c_str(), cap - 1);
@@ -914,6 +1005,8 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
       Fa.value = cv.take<double>(cp.cap_nodes);
     };
     PlanArgs P{};
+    static const bool plan_prof = [] { const char* e = std::getenv("TMOG_PLAN_PROFILE"); return e && e[0] == '1'; }();
+    P.profile = plan_prof ? 1 : 0;
     FinArgs Fa{};
     int* cnt;
     int64_t* leaf_pos;
@@ -1036,6 +1129,8 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
     Fa.j_gamma = (const double*)(K + o_gam);
     Fa.gid_value = io->gid_value;
     Fa.gid_tree = io->gid_tree;
+    Fa.prune = 0;
+    for (int j = 0; j < T; ++j) Fa.prune |= io->job_gamma[j] > 0.0 ? 1 : 0;
     hipLaunchKernelGGL(tree_finalize_kernel, dim3(1), dim3(1024), 0, st, Fa);
     kchk((int)hipGetLastError(), "tree_finalize");
     return 0;
