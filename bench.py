@@ -65,6 +65,8 @@ def parse():
                     help="multi-GPU table layout: row shards with all-reduced fit statistics (data parallel), "
                          "or the whole table on every rank")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--max-training-sample", dest="max_training_sample", type=int, default=None,
+                    help="the selector splitter's maxTrainingSample (default: the reference's 1M)")
     a = ap.parse_args()
     if a.config == "lr-rf-1m" and a.models == "default":
         a.models = "OpLogisticRegression,OpRandomForestClassifier"
@@ -100,8 +102,12 @@ def build_workflow(args, ds, label, preds):
     vec = transmogrify(preds)
     checked = label.sanity_check(vec, remove_bad_features=True)
     types = None if args.models == "default" else args.models.split(",")
+    splitter = "default"
+    if args.max_training_sample:
+        splitter = _selector_cls(args)._default_splitter(42)
+        splitter.max_training_sample = int(args.max_training_sample)
     pred = _selector_cls(args).with_cross_validation(
-        num_folds=args.folds, model_types_to_use=types, seed=42).set_input(label, checked).get_output()
+        splitter=splitter, num_folds=args.folds, model_types_to_use=types, seed=42).set_input(label, checked).get_output()
     wf = OpWorkflow().set_result_features(label, pred).set_reader(InMemoryReader(ds))
     return wf, pred
 
@@ -255,6 +261,7 @@ def main():
                                 ("default grid" if args.models == "default" else args.models) + ")",
                        "rows": args.rows, "raw_columns": n_raw[0],
                        "cv_folds": args.folds, "global_batch": args.rows, "seq_len": None,
+                       "max_training_sample": args.max_training_sample or 1_000_000,
                        "parallelism": (f"dp{world}" if args.layout == "sharded" else f"grid-shard{world}")
                        if world > 1 else "single"},
         }
