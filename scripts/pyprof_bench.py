@@ -2,7 +2,10 @@
 (cProfile of bench.main; blocking device syncs show up as the time of the call that waited)."""
 import cProfile
 import pstats
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 out = sys.argv[1]
 sys.argv = ["bench.py"] + sys.argv[2:]

@@ -421,6 +421,10 @@ def _feature_std(X, W, par=None):
 
 
 class _LinearBase(Learner):
+    # the model selector may add the winner's full-training-set refit of every grid point to the CV batch
+    # (tuning/validators.py): independent problems of one batched optimiser, so the refit rides along in
+    # the same passes over X instead of a separate fit after the selection
+    batched_refit = True
     loss = "logistic"
     parallel = "rows"
 

@@ -916,7 +916,7 @@ class XGBoostClassifierLearner(_BoostLearner):
         # own host thread on its own stream, so one half's per-round host work (tree finalisation,
         # round set-up, the early-stopping read-back) overlaps the other half's kernels instead of
         # idling the GPU. Trees are identical to the single-loop order (see run()).
-        parts = int(os.environ.get("TMOG_XGB_PIPE", "2"))
+        parts = int(os.environ.get("TMOG_XGB_PIPE", "4"))
         if fused and par is None and P >= 2 and parts >= 2:
             parts = min(parts, P)
             cuts = np.linspace(0, P, parts + 1).astype(int)

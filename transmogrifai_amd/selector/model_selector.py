@@ -8,6 +8,7 @@ hold-out evaluation of ``HasTestEval`` (``ModelSelectorNames.scala:73-123``).
 from __future__ import annotations
 
 import logging
+import os
 import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -157,6 +158,21 @@ class ModelSelector(BinaryEstimator):
     def _fit(self, X, y, row_ids, split_summary, t0, cand=None):
         # tree learners draw their quantile-binning sample from the training candidates only
         ctx: Dict[str, Any] = {} if cand is None else {"tree_rows": cand}
+        # the prepared full training set of the winner's refit (fixed before the selection: batched learners
+        # fit it for every grid point inside their CV batch, tuning/validators.py)
+        if self.splitter is not None:
+            if hasattr(self.splitter, "weights"):
+                w = self.splitter.weights(row_ids, y, stream=5)
+                rows = torch.nonzero(w > 0).reshape(-1)
+                refit_rows = (rows, w[rows])
+            else:
+                rows = torch.nonzero(self.splitter.validation_prepare(row_ids, y, stream=5)).reshape(-1)
+                refit_rows = (rows, None)
+        else:
+            rows = None
+            refit_rows = (None, None)
+        if self.best_estimator is None and os.environ.get("TMOG_BATCHED_REFIT", "1") != "0":
+            ctx["refit_job"] = refit_rows
         if self.best_estimator is not None:     # chosen by workflow-level CV
             res = self.best_estimator
         else:
@@ -167,24 +183,17 @@ class ModelSelector(BinaryEstimator):
         # refit the winner on the prepared full training set
         learner = learner_class(res.best_learner)()
         params = dict(learner.defaults, **res.best_params)
-        if self.splitter is not None:
-            if hasattr(self.splitter, "weights"):
-                w = self.splitter.weights(row_ids, y, stream=5)
-                rows = torch.nonzero(w > 0).reshape(-1)
-                job = FitJob(params, rows, w[rows])
-            else:
-                rows = torch.nonzero(self.splitter.validation_prepare(row_ids, y, stream=5)).reshape(-1)
-                job = FitJob(params, rows)
-        else:
-            rows = None
-            job = FitJob(params)
+        job = FitJob(params, refit_rows[0], refit_rows[1])
+        from ..tuning.validators import refit_key
+        ready = (ctx.pop("refit_states", None) or {}).get(refit_key(res.best_learner, params))
+        ctx.pop("refit_job", None)
         # the winner's refit uses the same intra-job parallelism over the ranks as its CV fits
         from ..parallel import dist as D
         if D.world() > 1 and learner.parallel in ("rows", "features"):
             from ..parallel.learner_parallel import LearnerParallel
             ctx["par"] = LearnerParallel()
         try:
-            state = learner.fit_batch(X, y, [job], context=ctx)[0]
+            state = ready if ready is not None else learner.fit_batch(X, y, [job], context=ctx)[0]
         finally:
             ctx.pop("par", None)
         # training evaluation on the prepared data

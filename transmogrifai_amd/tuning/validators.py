@@ -111,6 +111,12 @@ def _fold_alignment(fitted, features_name: str, data):
     return None
 
 
+def refit_key(lname: str, params: Dict[str, Any]) -> str:
+    """Key of a speculative refit state: learner name + its full parameter map."""
+    import json
+    return lname + ":" + json.dumps(params, sort_keys=True, default=str)
+
+
 class OpValidator:
     validation_type = "CrossValidation"
 
@@ -578,7 +584,17 @@ class OpValidator:
             learner = learner_class(lname)()
             fjobs = [FitJob(dict(learner.defaults, **grid[g]), train_rows[k][0], train_rows[k][1])
                      for _, (_, g, k) in batch]
+            # speculative refits (model_selector.py): each grid point's fit on the selector's full training
+            # rows joins the CV batch of a batched learner on one rank; the selector uses the winner's
+            refit = ctx.get("refit_job") if (getattr(learner, "batched_refit", False) and D.world() == 1) else None
+            extra = sorted({g for _, (_, g, _) in batch}) if refit is not None else []
+            fjobs += [FitJob(dict(learner.defaults, **grid[g]), refit[0], refit[1]) for g in extra]
             states = learner.fit_batch(X, y, fjobs, context=ctx)
+            if extra:
+                store = ctx.setdefault("refit_states", {})
+                for g, st in zip(extra, states[len(batch):]):
+                    store[refit_key(lname, dict(learner.defaults, **grid[g]))] = st
+                states = states[:len(batch)]
             preds = learner.predict_batch(states, X, [val_rows[k] for _, (_, g, k) in batch], context=ctx)
             out = {}
             # the models of one fold share its validation rows: their curves come from one segmented sort
