@@ -55,6 +55,24 @@ def test_fused_objective_matches_fp64(N, d, P, loss):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,d", [(4099, 33), (20011, 329), (3001, 384)])
+def test_fused_objective_columns_independent(N, d):
+    """Each problem column is computed on its own: one column alone equals the same column inside a 24-wide
+    batch bit for bit (ragged N d included) -- what lets the selector fold refits into the CV batch."""
+    g = torch.Generator().manual_seed(N * 3 + d)
+    X = torch.randn(N, d, generator=g).cuda()
+    y = (torch.rand(N, generator=g) < 0.4).float().cuda()
+    W = (torch.rand(N, 24, generator=g) < 0.7).float().cuda()
+    V = (torch.randn(d, 24, generator=g) / d ** 0.5).cuda()
+    b = (torch.randn(24, generator=g) * 0.1).cuda()
+    f, r, G = LK.fused_objective(X, y, W, V, b, "logistic", None, grad=True)
+    for k in (0, 17):
+        f1, r1, G1 = LK.fused_objective(X, y, W[:, k:k + 1].contiguous(), V[:, k:k + 1].contiguous(), b[k:k + 1],
+                                        "logistic", None, grad=True)
+        assert torch.equal(f1[0], f[k]) and torch.equal(r1[0], r[k]) and torch.equal(G1[:, 0], G[:, k])
+
+
+@pytest.mark.gpu
 def test_logistic_regression_gpu_matches_cpu():
     from transmogrifai_amd.models.base import FitJob
     from transmogrifai_amd.models.linear import LogisticRegressionLearner

@@ -109,13 +109,19 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
   // The epilogue's W / y values of the next tile ride along (rows clamped to N - 1, masked later).
   f32x4 pf[NPF];
   float pw[4], py[4];
-  int nval4 = 0;
+  f32x4 pt = {0.f, 0.f, 0.f, 0.f};          // the last tile's 1-3 trailing floats past 4 * nval4 ((N d) % 4 != 0)
+  int nval4 = 0, ntail = 0;
   auto prefetch = [&](int64_t tile) {
     const int64_t r0 = tile * TM;
-    nval4 = (int)((min((int64_t)TM, N - r0) * d) >> 2);
+    const int nval = (int)(min((int64_t)TM, N - r0) * d);
+    nval4 = nval >> 2;
+    ntail = nval & 3;
     const f32x4* src = reinterpret_cast<const f32x4*>(X + r0 * (int64_t)d);
 #pragma unroll
-    for (int i = 0; i < NPF; ++i) pf[i] = src[min((int)threadIdx.x + NT * i, nval4 - 1)];
+    for (int i = 0; i < NPF; ++i) pf[i] = src[min((int)threadIdx.x + NT * i, max(nval4 - 1, 0))];
+    const float* xt = X + r0 * (int64_t)d;   // every lane reads the same <= 3 words (clamped into the tile)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pt[k] = k < ntail ? xt[min(4 * nval4 + k, nval - 1)] : 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t gr = min(r0 + 16 * rb + 4 * q + j, N - 1);
@@ -136,7 +142,7 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
     for (int i = 0; i < NPF; ++i) {
       const int e4 = threadIdx.x + NT * i;
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      if (e4 < tile_f4) xs4[e4] = e4 < nval4 ? pf[i] : z;
+      if (e4 < tile_f4) xs4[e4] = e4 < nval4 ? pf[i] : (e4 == nval4 && ntail ? pt : z);
     }
     float cw[4], cy[4];
 #pragma unroll
@@ -507,7 +513,7 @@ int tmog_hip_lr_objective(const float* X, int64_t N, int d, const float* y, cons
                           int P, const float* V, const float* bias, int loss, const float* yscale, int grad,
                           double* f_part, double* r_part, float* G_part, int nblk, hipStream_t stream) {
   if (d > DMAX || d < 1 || P > PC || P < 1 || nblk < 1) return -2;
-  if ((reinterpret_cast<uintptr_t>(X) & 15) != 0 || (N * d) % 4 != 0) return -3;
+  if ((reinterpret_cast<uintptr_t>(X) & 15) != 0) return -3;
   const int dpad = ((d + 15) / 16) * 16;
   const int dk = ((d + 63) / 64) * 64;
   const size_t lds = (size_t)(((TM * d + 64 + 3) & ~3) + dk * VS + TM * PC) * sizeof(float);

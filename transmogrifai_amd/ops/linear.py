@@ -195,9 +195,10 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
     N, d = X.shape
     P = W.shape[1]
     dev = X.device
-    if d <= _LR_DMAX and ((N * d) % 4 or X.data_ptr() % 16):
-        # the kernel streams X in 16-byte chunks: run the <= 3 trailing rows through torch
-        Nm = N - N % 4 if X.data_ptr() % 16 == 0 else 0
+    if d <= _LR_DMAX and (X.data_ptr() % 16 or N * d < 16):
+        # the kernel streams X in 16-byte chunks from a 16-byte aligned base (it loads a ragged end of the
+        # last tile itself, so every problem column is computed the same whatever the other columns are)
+        Nm = 0
         parts = []
         if Nm:
             parts.append(fused_objective(X[:Nm], y[:Nm], W[:Nm], V, bias, loss, yscale, grad))
