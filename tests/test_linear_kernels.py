@@ -135,3 +135,23 @@ def test_owlqn_candidate_kernel_matches_torch():
     got = LK.owlqn_candidate(*(t.cuda() for t in (U, D, xi, l1, pg, alpha)))
     for w, r in zip(want, got):
         torch.testing.assert_close(r.cpu(), w, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,d,P", [(10_001, 33, 3), (70_000, 329, 24), (5000, 7, 40)])
+def test_feature_std_kernel_matches_fp64(N, d, P):
+    """Weighted per-problem column mean / std on the device (stats_kernels.hip weighted_colsums) vs fp64 torch,
+    and a problem's statistics independent of the batch it is in."""
+    from transmogrifai_amd.models.linear import _feature_std
+    g = torch.Generator().manual_seed(N + d)
+    X = torch.randn(N, d, generator=g) * torch.linspace(0.5, 20, d) + 3
+    W = (torch.rand(N, P, generator=g) < 0.6).float()
+    Xd, Wd = X.double(), W.double()
+    n = Wd.sum(0)
+    mean = (Xd.t() @ Wd) / n
+    var = ((Xd * Xd).t() @ Wd - n * mean * mean) / (n - 1)
+    std, mu = _feature_std(X.cuda(), W.cuda())
+    torch.testing.assert_close(mu.cpu(), mean, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(std.cpu(), var.sqrt(), rtol=1e-9, atol=1e-12)
+    s1, m1 = _feature_std(X.cuda(), W[:, 1:2].contiguous().cuda())
+    assert torch.equal(s1[:, 0], std[:, 1]) and torch.equal(m1[:, 0], mu[:, 1])

@@ -408,6 +408,18 @@ def _feature_std(X, W, par=None):
         mean = s1 / n.clamp_min(1)[None, :]
         var = (s2 - n[None, :] * mean * mean) / (n - 1).clamp_min(1)[None, :]
         return torch.sqrt(var.clamp_min(0)), mean
+    if X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and X.stride(1) == 1 and X.shape[0] > 0:
+        # fp64 sums on the device (stats_kernels.hip weighted_colsums): a problem's statistics do not depend
+        # on the other problems of the batch (a library GEMM picks its blocking by the batch width)
+        from ..ops import _native as N_
+        Wf = W.to(torch.float32).contiguous()
+        out = torch.empty(P, 2, d, dtype=torch.float64, device=X.device)
+        N_.check(N_.hip().tmog_hip_weighted_colsums(N_.ptr(X), X.shape[0], d, X.stride(0), N_.ptr(Wf), P, P,
+                                                    N_.ptr(out), N_.stream(X.device)), "weighted_colsums")
+        n, s1, s2 = _psum(par, W.to(torch.float64).sum(0), out[:, 0].t().contiguous(), out[:, 1].t().contiguous())
+        mean = s1 / n.clamp_min(1)[None, :]
+        var = (s2 - n[None, :] * mean * mean) / (n - 1).clamp_min(1)[None, :]
+        return torch.sqrt(var.clamp_min(0)), mean
     s1 = torch.zeros(d, P, dtype=torch.float64, device=X.device)
     s2 = torch.zeros_like(s1)
     for a in range(0, X.shape[0], _STD_CHUNK):

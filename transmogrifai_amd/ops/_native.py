@@ -90,6 +90,7 @@ _HIP_SIGS = {
     "tmog_hip_plan_profile": [P, I32],
     "tmog_hip_masked_colsum": [P, P, P, I32, I64, I64, P, P],
     "tmog_hip_wgram": [P, I64, I32, I64, P, I64, I32, P, I64, I32, P, P],
+    "tmog_hip_weighted_colsums": [P, I64, I32, I64, P, I64, I32, P, P],
     "tmog_hip_boost_prologue": [P, P, P, P, I32, P, I32, P, P, P, I64, P, P, I64, P, P, P, C.c_float, I32, P],
     "tmog_hip_owlqn_direction": [P, P, P, P, P, P, I32, I32, I32, I32, P, P, P, P, P],
     "tmog_hip_owlqn_candidate": [P, P, P, P, P, P, I32, I32, P, P, P, P],

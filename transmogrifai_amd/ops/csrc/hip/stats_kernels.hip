@@ -376,6 +376,64 @@ __global__ void __launch_bounds__(256) wgram_fold_kernel(const double* __restric
   }
 }
 
+// weighted_colsums_kernel / weighted_colsums_fold_kernel -- per problem p and column j the fp64 sums
+// s1 = sum_r W[r, p] X[r, j] and s2 = sum_r W[r, p] X[r, j]^2 (the linear learners' feature standardisation,
+// Spark's weighted summarizer; models/linear.py _feature_std). Lane = column, 4 waves stride the rows of a
+// fixed 4096-row chunk, 16 problems per workgroup; the chunk partials are folded in chunk order. Neither the
+// chunking nor the arithmetic of a problem depends on the other problems of the launch, so a problem's
+// statistics are the same bits whatever batch it is fitted in (the selector's speculative refits).
+constexpr int kWcsRows = 4096;
+constexpr int kWcsP = 16;
+
+__global__ void __launch_bounds__(256) weighted_colsums_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                               int64_t ldx, const float* __restrict__ W,
+                                                               int64_t ldw, int P, double* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  const int64_t chunk = blockIdx.y;
+  const int p0 = blockIdx.z * kWcsP;
+  const int np = min(kWcsP, P - p0);
+  const int64_t r0 = chunk * kWcsRows, r1 = min(n, r0 + kWcsRows);
+  double s1[kWcsP], s2[kWcsP];
+#pragma unroll
+  for (int q = 0; q < kWcsP; ++q) s1[q] = s2[q] = 0.0;
+  const int jc = min(j, d - 1);
+  for (int64_t r = r0 + wave; r < r1; r += 4) {
+    const double x = (double)X[r * ldx + jc];
+    const double xx = x * x;
+#pragma unroll
+    for (int q = 0; q < kWcsP; ++q) {
+      const double w = q < np ? (double)W[r * ldw + p0 + q] : 0.0;
+      s1[q] += w * x;
+      s2[q] += w * xx;
+    }
+  }
+  __shared__ double sh[4][2][kWcsP][64];
+#pragma unroll
+  for (int q = 0; q < kWcsP; ++q) {
+    sh[wave][0][q][lane] = s1[q];
+    sh[wave][1][q][lane] = s2[q];
+  }
+  __syncthreads();
+  if (wave == 0 && j < d) {
+    for (int q = 0; q < np; ++q)
+      for (int k = 0; k < 2; ++k) {
+        const double v = ((sh[0][k][q][lane] + sh[1][k][q][lane]) + sh[2][k][q][lane]) + sh[3][k][q][lane];
+        part[((chunk * P + p0 + q) * 2 + k) * (int64_t)d + j] = v;
+      }
+  }
+}
+
+// out[p][k][j] = sum over chunks in chunk order of part[chunk][p][k][j]
+__global__ void weighted_colsums_fold_kernel(const double* __restrict__ part, int64_t chunks, int64_t words,
+                                             double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= words) return;
+  double s = 0.0;
+  for (int64_t c = 0; c < chunks; ++c) s += part[c * words + e];
+  out[e] = s;
+}
+
 // Per-problem, per-class column sums (the label x column contingency and the
 // NaiveBayes class feature sums): part[chunk][p * L + c][j] = sum of X[r][j] over rows r of the chunk with
 // codes[p][r] == c (-1 = row not in problem p). Lane = column (64 per workgroup), wave = row stride; every
@@ -462,6 +520,25 @@ int tmog_hip_col_stats(const float* X, const void* unused, int64_t n, int d, int
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(col_partials_kernel, dim3(cblocks, (unsigned)chunks), dim3(256), 0, stream, X, n, d, ld, rpc, part);
   hipLaunchKernelGGL(col_fold_kernel, dim3((d + 255) / 256), dim3(256), 0, stream, part, (int)chunks, d, out);
+  hipFreeAsync(part, stream);
+  return (int)hipGetLastError();
+}
+
+// out [P][2][d] fp64: sum_r W[r, p] X[r, j] and sum_r W[r, p] X[r, j]^2 (fixed 4096-row chunks, chunk-ordered fold).
+int tmog_hip_weighted_colsums(const float* X, int64_t n, int d, int64_t ldx, const float* W, int64_t ldw, int P,
+                              double* out, hipStream_t stream) {
+  if (n <= 0 || d <= 0 || P <= 0) return -1;
+  const int64_t chunks = (n + kWcsRows - 1) / kWcsRows;
+  if (chunks > 65535) return -2;
+  const int64_t words = (int64_t)P * 2 * d;
+  double* part = nullptr;
+  hipError_t e = hipMallocAsync((void**)&part, sizeof(double) * words * chunks, stream);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(weighted_colsums_kernel, dim3((unsigned)((d + 63) / 64), (unsigned)chunks,
+                                                   (unsigned)((P + kWcsP - 1) / kWcsP)),
+                     dim3(256), 0, stream, X, n, d, ldx, W, ldw, P, part);
+  hipLaunchKernelGGL(weighted_colsums_fold_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, stream, part,
+                     chunks, words, out);
   hipFreeAsync(part, stream);
   return (int)hipGetLastError();
 }
