@@ -59,13 +59,15 @@ def test_batched_refit_equals_separate_refit(monkeypatch, regression, models):
 
 
 @pytest.mark.gpu
-def test_batched_refit_bit_identical_on_gpu(monkeypatch):
-    """The fused objective computes every problem column independently: the refit inside the CV batch is the
-    separate refit, bit for bit."""
+def test_batched_refit_matches_separate_refit_on_gpu(monkeypatch):
+    """The fused objective and the standardisation statistics compute every problem column independently
+    (tests/test_linear_kernels.py); the optimiser's small torch column reductions still sum in a batch-width
+    dependent order, so the refit inside the CV batch equals the separate refit to ~1 ulp."""
     s0, st0 = _train(monkeypatch, "0", device="cuda", models=["OpLogisticRegression"])
     s1, st1 = _train(monkeypatch, "1", device="cuda", models=["OpLogisticRegression"])
-    np.testing.assert_array_equal(_coef(st0), _coef(st1))
-    assert s0["holdoutEvaluation"] == s1["holdoutEvaluation"]
+    np.testing.assert_allclose(_coef(st0), _coef(st1), rtol=1e-12, atol=1e-14)
+    for k, v in s0["holdoutEvaluation"].items():
+        assert abs(v - s1["holdoutEvaluation"][k]) <= 1e-9, k
 
 
 def test_refit_rides_in_the_cv_batch(monkeypatch):
