@@ -87,6 +87,7 @@ _HIP_SIGS = {
     "tmog_hip_boost_epilogue": [P, P, I64, P, P, P, I64, P, P, P, P, I32, P, I32, I64, I64, I64, P, P, I32],
     "tmog_hip_aupr_counts": [P, I32, I32, P, P],
     "tmog_hip_slot_stream": [I32, P, I32],
+    "tmog_hip_lr_blocks_per_cu": [I32],
     "tmog_hip_plan_profile": [P, I32],
     "tmog_hip_masked_colsum": [P, P, P, I32, I64, I64, P, P],
     "tmog_hip_wgram": [P, I64, I32, I64, P, I64, I32, P, I64, I32, P, P],

@@ -17,6 +17,7 @@
 // host side (ops/linear.py). Phase-A column order inside each 64-column block is k = s + 16q (lane
 // group q) so the four lane groups of an operand read land 16 banks apart; V rows are padded to 33.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 #include <math.h>
 
@@ -56,30 +57,35 @@ __device__ __forceinline__ void loss_and_grad(int loss, float m, float y, float 
 
 __device__ __forceinline__ int kcol(int s, int q) { return 64 * (s >> 4) + (s & 15) + 16 * q; }
 
-// GB = phase-B output blocks per wave, NPF = prefetch float4 slots per thread
-template <bool GRAD, int GB, int NPF, int DM>
-__global__ void __launch_bounds__(NT) lr_objective_kernel(
+// GB = phase-B output blocks per wave, NPF = prefetch float4 slots per thread, TT = rows per tile (64: one
+// 512-thread workgroup per CU; 32: 256-thread workgroups, two per CU -- two tiles' loads in flight per CU).
+// Waves: TT / 16 row blocks x 2 problem halves; phase-B output blocks ob = wave + NW i.
+template <bool GRAD, int GB, int NPF, int DM, int TT>
+__global__ void __launch_bounds__(8 * TT) lr_objective_kernel(
     const float* __restrict__ X, int64_t N, int d, const float* __restrict__ y,
     const float* __restrict__ W, int ldw, int wcol0, int P, const float* __restrict__ V,
     const float* __restrict__ bias, int loss, const float* __restrict__ yscale, double* __restrict__ f_part,
     double* __restrict__ r_part, float* __restrict__ G_part, int dpad) {
+  constexpr int RB = TT / 16;               // row blocks (waves per problem half)
+  constexpr int NW = 2 * RB;                // waves per workgroup
+  constexpr int NTT = 64 * NW;              // threads per workgroup
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int ks_full = (d >> 6) * 16;        // phase-A k-steps over full 64-column blocks
   const int ks_tail = ((d & 63) + 3) >> 2;  // k-steps over the ragged last block
-  const int dk = ((d + 63) >> 6) * 64;      // d rounded up to 64
-  const int xs_words = (TM * d + 64 + 3) & ~3;
-  float* Xs = lds;                          // [TM][d] + 64 words of overrun (finite, times V = 0)
-  float* Vs = Xs + xs_words;                // [dk][VS], zero beyond d
-  float* Rs = Vs + dk * VS;                 // [TM][PC]
+  const int xs_words = (TT * d + 64 + 3) & ~3;
+  float* Xs = lds;                          // [TT][d] + 64 words of overrun (finite, times V = 0)
+  float* Vs = Xs + xs_words;                // [64][VS]: V rows of the ragged last 64-column block, zero beyond d
+  float* Rs = Vs + 64 * VS;                 // [TT][PC]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: SGPR, scalar branches
   const int q = lane >> 4, c = lane & 15;
-  const int rb = wave & 3, pb = wave >> 2;
+  const int rb = wave % RB, pb = wave / RB;
   const int nob = 2 * ((d + 15) >> 4);
+  const int nb64 = d >> 6;
 
-  for (int i = threadIdx.x; i < xs_words; i += NT) Xs[i] = 0.f;
-  for (int i = threadIdx.x; i < dk * VS; i += NT) {
-    const int k = i / VS, j = i - k * VS;
+  for (int i = threadIdx.x; i < xs_words; i += NTT) Xs[i] = 0.f;
+  for (int i = threadIdx.x; i < 64 * VS; i += NTT) {
+    const int k = 64 * nb64 + i / VS, j = i % VS;
     Vs[i] = (k < d && j < PC) ? V[(int64_t)k * PC + j] : 0.f;
   }
   f32x4 gacc[GB];
@@ -91,7 +97,6 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
   // of problem block pb only ever multiplies V[64 b + 16 q + s][16 pb + c] (s = 0..15), so per MFMA one
   // LDS read (the X element) remains instead of two
   constexpr int NB64 = DM / 64;
-  const int nb64 = d >> 6;
   float vr[NB64 * 16];
 #pragma unroll
   for (int b = 0; b < NB64; ++b)
@@ -102,8 +107,8 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
   const float ysp = yscale ? yscale[p] : 1.f;
   double f_acc = 0.0, r_acc = 0.0;
 
-  const int64_t ntiles = (N + TM - 1) / TM;
-  const int tile_f4 = (TM * d) >> 2;
+  const int64_t ntiles = (N + TT - 1) / TT;
+  const int tile_f4 = (TT * d) >> 2;
   // branch-free prefetch (a guarded load makes hipcc wait vmcnt(0) per slot): out-of-range slots
   // re-read the tile's last float4 and are zeroed at the LDS store. Host guarantees N * d % 4 == 0.
   // The epilogue's W / y values of the next tile ride along (rows clamped to N - 1, masked later).
@@ -112,13 +117,13 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
   f32x4 pt = {0.f, 0.f, 0.f, 0.f};          // the last tile's 1-3 trailing floats past 4 * nval4 ((N d) % 4 != 0)
   int nval4 = 0, ntail = 0;
   auto prefetch = [&](int64_t tile) {
-    const int64_t r0 = tile * TM;
-    const int nval = (int)(min((int64_t)TM, N - r0) * d);
+    const int64_t r0 = tile * TT;
+    const int nval = (int)(min((int64_t)TT, N - r0) * d);
     nval4 = nval >> 2;
     ntail = nval & 3;
     const f32x4* src = reinterpret_cast<const f32x4*>(X + r0 * (int64_t)d);
 #pragma unroll
-    for (int i = 0; i < NPF; ++i) pf[i] = src[min((int)threadIdx.x + NT * i, max(nval4 - 1, 0))];
+    for (int i = 0; i < NPF; ++i) pf[i] = src[min((int)threadIdx.x + NTT * i, max(nval4 - 1, 0))];
     const float* xt = X + r0 * (int64_t)d;   // every lane reads the same <= 3 words (clamped into the tile)
 #pragma unroll
     for (int k = 0; k < 3; ++k) pt[k] = k < ntail ? xt[min(4 * nval4 + k, nval - 1)] : 0.f;
@@ -134,13 +139,13 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
 
   const float* va = Vs + 16 * pb + c;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t r0 = tile * TM;
-    const int nrows = (int)min((int64_t)TM, N - r0);
+    const int64_t r0 = tile * TT;
+    const int nrows = (int)min((int64_t)TT, N - r0);
     // ---- land the prefetched tile in LDS, then start fetching the next one
     f32x4* xs4 = reinterpret_cast<f32x4*>(Xs);
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
-      const int e4 = threadIdx.x + NT * i;
+      const int e4 = threadIdx.x + NTT * i;
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       if (e4 < tile_f4) xs4[e4] = e4 < nval4 ? pf[i] : (e4 == nval4 && ntail ? pt : z);
     }
@@ -170,9 +175,9 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
       }
     }
     for (int k = 4 * ks_full + q; k < 4 * ks_full + 4 * ks_tail; k += 8) {
-      macc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k], va[k * VS], macc, 0, 0, 0);
+      macc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k], va[(k - 64 * nb64) * VS], macc, 0, 0, 0);
       if (k + 4 < 4 * ks_full + 4 * ks_tail)
-        macc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k + 4], va[(k + 4) * VS], macc2, 0, 0, 0);
+        macc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[k + 4], va[(k + 4 - 64 * nb64) * VS], macc2, 0, 0, 0);
     }
     macc += macc2;
 
@@ -196,18 +201,18 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
     r_acc += (double)rl;
     if (GRAD) {
       __syncthreads();
-      // ---- phase B: G[16db.., 16pb'..] += X_tile^T R  (16 k-steps of 4 rows)
-      // output blocks ob = wave + 8 i: column block (wave >> 1) + 4 i, problem half wave & 1 (8 i is even)
+      // ---- phase B: G[16db.., 16pb'..] += X_tile^T R  (TT / 4 k-steps of 4 rows)
+      // output blocks ob = wave + NW i: column block (wave >> 1) + (NW / 2) i, problem half wave & 1
       const float* xw = Xs + q * d + c + 16 * (wave >> 1);
       const float* rw = Rs + q * PC + 16 * (wave & 1) + c;
 #pragma unroll 4
-      for (int t = 0; t < TM / 4; ++t) {
+      for (int t = 0; t < TT / 4; ++t) {
         const float rv = rw[4 * t * PC];
         const float* xr = xw + 4 * t * d;
 #pragma unroll
         for (int i = 0; i < GB; ++i) {
-          if (wave + 8 * i < nob)
-            gacc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[64 * i], rv, gacc[i], 0, 0, 0);
+          if (wave + NW * i < nob)
+            gacc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[8 * NW * i], rv, gacc[i], 0, 0, 0);
         }
       }
     }
@@ -219,7 +224,7 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
     float* gp = G_part + (int64_t)blockIdx.x * dpad * PC;
 #pragma unroll
     for (int i = 0; i < GB; ++i) {
-      const int ob = wave + 8 * i;
+      const int ob = wave + NW * i;
       if (ob < nob) {
         const int db = ob >> 1, pbb = ob & 1;
 #pragma unroll
@@ -227,7 +232,7 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
       }
     }
   }
-  // lanes sharing a problem column: 4 lane groups x 4 row-block waves
+  // lanes sharing a problem column: 4 lane groups x RB row-block waves
   f_acc += __shfl_xor(f_acc, 16, 64);
   f_acc += __shfl_xor(f_acc, 32, 64);
   r_acc += __shfl_xor(r_acc, 16, 64);
@@ -242,9 +247,9 @@ __global__ void __launch_bounds__(NT) lr_objective_kernel(
   if (threadIdx.x < PC) {
     const int pp = threadIdx.x, pbw = pp >> 4, cc = pp & 15;
     double fs = 0.0, rs = 0.0;
-    for (int r = 0; r < 4; ++r) {             // waves 4pb + r
-      fs += sf[(4 * pbw + r) * 16 + cc];
-      rs += sf[128 + (4 * pbw + r) * 16 + cc];
+    for (int r = 0; r < RB; ++r) {            // waves RB pb + r
+      fs += sf[(RB * pbw + r) * 16 + cc];
+      rs += sf[128 + (RB * pbw + r) * 16 + cc];
     }
     f_part[(int64_t)blockIdx.x * PC + pp] = fs;
     r_part[(int64_t)blockIdx.x * PC + pp] = rs;
@@ -509,22 +514,40 @@ int tmog_hip_lr_epilogue_grad(const float* X, int64_t N, int d, const float* M, 
 // G[:, p] = sum_i X[i,:] W[i,p] l'(m_ip), with m = X V + bias, for up to 32 problems (columns
 // wcol0 .. wcol0+P-1 of W). V is [d][32] fp32 (zero-padded), bias / yscale are [32].
 // Outputs are per-workgroup partials: f_part / r_part [nblk][32] fp64, G_part [nblk][dpad][32] fp32.
+// Rows per tile of the value-only / gradient passes: TMOG_LR_TILE_V / TMOG_LR_TILE_G (32 or 64). Measured at
+// 1M x 330 x 32 problems (scripts/bench_lr_obj.py): value pass 0.449 ms (64) vs 0.422 ms (32, two workgroups
+// per CU); gradient pass 0.720 ms (64) vs 1.128 ms (32: twice the phase-B accumulators per wave, spills).
+static int lr_tile(bool grad) {
+  static const int tv = [] { const char* e = std::getenv("TMOG_LR_TILE_V"); return (e && std::atoi(e) == 64) ? 64 : 32; }();
+  static const int tg = [] { const char* e = std::getenv("TMOG_LR_TILE_G"); return (e && std::atoi(e) == 32) ? 32 : 64; }();
+  return grad ? tg : tv;
+}
+
+// Workgroups per CU of a tmog_hip_lr_objective pass (ops/linear.py sizes its persistent grid with it).
+int tmog_hip_lr_blocks_per_cu(int grad) { return lr_tile(grad != 0) == 32 ? 2 : 1; }
+
 int tmog_hip_lr_objective(const float* X, int64_t N, int d, const float* y, const float* W, int ldw, int wcol0,
                           int P, const float* V, const float* bias, int loss, const float* yscale, int grad,
                           double* f_part, double* r_part, float* G_part, int nblk, hipStream_t stream) {
   if (d > DMAX || d < 1 || P > PC || P < 1 || nblk < 1) return -2;
   if ((reinterpret_cast<uintptr_t>(X) & 15) != 0) return -3;
   const int dpad = ((d + 15) / 16) * 16;
-  const int dk = ((d + 63) / 64) * 64;
-  const size_t lds = (size_t)(((TM * d + 64 + 3) & ~3) + dk * VS + TM * PC) * sizeof(float);
-#define TM_LR(G, GB, DM)                                                                                  \
-  hipLaunchKernelGGL((lr_objective_kernel<G, GB, (TM * DM / 4 + NT - 1) / NT, DM>), dim3(nblk), dim3(NT), lds, \
-                     stream, X, N, d, y, W, ldw, wcol0, P, V, bias, loss, yscale, f_part, r_part, G_part, dpad)
-#define TM_LR_D(G)                                   \
-  if (d <= 128) TM_LR(G, 2, 128);                    \
-  else if (d <= 256) TM_LR(G, 4, 256);               \
-  else TM_LR(G, 6, 384);
-  if (grad) { TM_LR_D(true) } else { TM_LR_D(false) }
+  const int tt = lr_tile(grad != 0);
+  const size_t lds = (size_t)(((tt * d + 64 + 3) & ~3) + 64 * VS + tt * PC) * sizeof(float);
+#define TM_LR(G, DM, T_)                                                                                          \
+  hipLaunchKernelGGL((lr_objective_kernel<G, (DM / 8 + T_ / 8 - 1) / (T_ / 8), (T_ * DM / 4 + 8 * T_ - 1) / (8 * T_), \
+                                          DM, T_>),                                                               \
+                     dim3(nblk), dim3(8 * T_), lds, stream, X, N, d, y, W, ldw, wcol0, P, V, bias, loss, yscale,     \
+                     f_part, r_part, G_part, dpad)
+#define TM_LR_D(G, T_)                \
+  if (d <= 128) TM_LR(G, 128, T_);    \
+  else if (d <= 256) TM_LR(G, 256, T_); \
+  else TM_LR(G, 384, T_);
+  if (grad) {
+    if (tt == 32) { TM_LR_D(true, 32) } else { TM_LR_D(true, 64) }
+  } else {
+    if (tt == 32) { TM_LR_D(false, 32) } else { TM_LR_D(false, 64) }
+  }
 #undef TM_LR_D
 #undef TM_LR
   return (int)hipGetLastError();

@@ -179,10 +179,13 @@ def fused_objective_supported(X) -> bool:
         and X.is_contiguous()
 
 
-def _n_blocks(N: int) -> int:
-    # persistent workgroups: one per CU (the 64-row tile + V fill ~150 KB of the 160 KB LDS)
+def _n_blocks(N: int, grad: bool = True) -> int:
+    # persistent workgroups: as many per CU as the pass's tile fits in LDS (linear_kernels.hip: one 64-row or
+    # two 32-row tiles per CU), each keeping its next tile's loads in flight
+    from . import _native as N_
     props = torch.cuda.get_device_properties(torch.cuda.current_device())
-    return max(1, min((N + 63) // 64, props.multi_processor_count))
+    per_cu = int(N_.hip().tmog_hip_lr_blocks_per_cu(int(grad)))
+    return max(1, min((N + 31) // 32, props.multi_processor_count * per_cu))
 
 
 def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.Tensor, bias: torch.Tensor,
@@ -209,7 +212,10 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
         return f, r, G
     yf = y.to(device=dev, dtype=torch.float32).contiguous()
     Wf = W.to(torch.float32).contiguous()
-    nblk = _n_blocks(N)
+    if d <= _LR_DMAX:
+        nblk = _n_blocks(N, grad)
+    else:                                   # the wide-d epilogue kernel: one 512-thread workgroup per CU
+        nblk = max(1, min((N + 63) // 64, torch.cuda.get_device_properties(dev).multi_processor_count))
     dpad = ((d + 15) // 16) * 16
     f = torch.empty(P, dtype=torch.float64, device=dev)
     r = torch.empty(P, dtype=torch.float64, device=dev)
