@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 ARGS="--rows ${ROWS:-2000000} --steps 1 --warmup 0 --models ${MODELS:-OpXGBoostClassifier,OpLogisticRegression}"
-RX='hist_build|split_scan|partition_fused|lr_objective|hist_subtract|forest_predict'
+RX=${RX:-'hist_build|split_scan|pair_scan|partition_fused|lr_objective|level_plan|boost_epilogue|forest_predict'}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc/stats -o s -- python3 bench.py $ARGS > gpurun_out/pmc/stats.log 2>&1 || exit 1
 i=0
 for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS" \
