@@ -418,17 +418,18 @@ class OpValidator:
     def _learner_lanes(self, X, world: int, n_learners: int) -> int:
         """Learners fitted at once on one GPU (``parallelism``, OpValidator.scala:377: the reference runs up to 8
         fits as concurrent futures). Only single-rank: spread learners move through collectives in lockstep.
-        Opt-in (``TMOG_LEARNER_LANES`` > 1): on the MI355X headline three lanes measured 2.19-2.37 s against
-        2.36-2.45 s sequential in good runs, but some runs stalled for 10-55 s (one past 180 s) -- with a dozen
-        streams (lanes, boosting parts, grower slots) over the process's 4 hardware queues, in-order queues
-        shared by streams that wait on each other serialise badly -- so one learner after the other stays the
-        default (profiles/README.md, round 3)."""
+        Default on the GPU: 2 lanes (``TMOG_LEARNER_LANES`` overrides). The longest learner (XGBoost on the
+        headline) keeps lane 0 and the caller's stream plus the free side streams for its boosting parts, the
+        other lane runs the remaining learners one after the other on a side stream: with the stream set bounded
+        to one per hardware queue (ops/streams.py) the round-3 stalls are gone and the headline step drops from
+        1.94 to 1.75-1.77 s on one box (3 lanes: 1.77-1.97 s -- the boosting parts lose a stream; more streams
+        than hardware queues: 1.95 s; profiles/r4_lanes_*.log, docs/ROUND4.md)."""
         env = os.environ.get("TMOG_LEARNER_LANES")
         # host-only runs stay sequential unless asked for (the CPU kernels already use every core)
         if world > 1 or n_learners < 2 or not isinstance(X, torch.Tensor) or not (X.is_cuda or env):
             return 1
         from ..models.tree_engine import N_SLOTS, SLOT_LANE
-        cap = int(env) if env else 1
+        cap = int(env) if env else 2
         return max(1, min(cap, n_learners, N_SLOTS // SLOT_LANE))
 
     def _fit_eval_concurrent(self, models, order, jobs, owner, me, X, y, train_rows, val_rows, ctx, t0, lanes, n_tr):
