@@ -140,6 +140,8 @@ struct PlanArgs {
   int64_t* sc;
   int64_t* sd;
   int64_t* se;
+  int64_t* sf;
+  int64_t* sg;
   int32_t* flag;
   int32_t* loc;
   int64_t cap_nl, cap_m, cap_nodes, cap_h, cap_c, cap_l;
@@ -323,10 +325,10 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     for (int j = t; j < T; j += nt) init_node(R(j), j, S);
     n = T;
     __syncthreads();
-  mark(0);
+    mark(0);
   } else {
     const int P = (d - 1) & 1;
-    const int n_prev = s_n_prev, m_prev = s_m_prev;
+    const int n_prev = s_n_prev;
     if (t == 0) A.level_off[d] = s_created;
     if (n_prev == 0) {
       if (t == 0) {
@@ -334,26 +336,33 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
       }
       return;
     }
-    // (a) node totals of the scanned nodes, split flags (flag[i], sa[j])
-    for (int i = t; i < n_prev; i += nt) A.flag[i] = 0;
-    __syncthreads();
-    for (int j = t; j < m_prev; j += nt) {
-      const int i = A.hn[P][j];
-      const int gid = A.lv_gid[P][i];
-      int64_t* r = R(gid);
-      for (int s = 0; s < S; ++s) r[kRecFixed + s] = dbits((double)A.r_tot[(int64_t)j * S + s]);
-      const float* Pp = A.par[P] + (int64_t)j * 8;
-      const bool ok = Pp[7] > 0.5f && A.r_feat[j] >= 0 && A.r_gain[j] > Pp[6];
-      A.flag[i] = ok ? 1 : 0;
-      A.sa[j] = ok ? 1 : 0;
+    // (a) per node of level d - 1 (loc[i] = its histogram node j, or -1): node totals, split flag, leaf work
+    const int64_t* pcnt = A.lv_count[P];
+    for (int i = t; i < n_prev; i += nt) {
+      const int j = A.loc[i];
+      bool split = false;
+      if (j >= 0) {
+        int64_t* r = R(A.lv_gid[P][i]);
+        for (int s = 0; s < S; ++s) r[kRecFixed + s] = dbits((double)A.r_tot[(int64_t)j * S + s]);
+        const float* Pp = A.par[P] + (int64_t)j * 8;
+        split = Pp[7] > 0.5f && A.r_feat[j] >= 0 && A.r_gain[j] > Pp[6];
+      }
+      const int64_t c = pcnt[i];
+      const bool leaf = !split && c > 0;
+      A.sd[i] = leaf ? c : 0;
+      A.se[i] = leaf ? cdiv(c, A.chunk_rows) : 0;
+      A.sf[i] = split ? 1 : 0;
+      A.flag[i] = split ? 1 : 0;
     }
     __syncthreads();
     mark(1);
-    // (b) leaves of level d - 1: every node that does not split, from the buffer level d - 1 read
-    emit_leaves(A, P, n_prev, A.flag, P, sh);
+    const int64_t lbase = *A.leaf_pos;
+    const int64_t nl0 = A.cnt[C_NL];
+    int64_t* const arr3[3] = {A.sd, A.se, A.sf};
+    int64_t tot3[3];
+    block_scan_multi<3>(arr3, n_prev, tot3, sh);
+    const int64_t tot_rows = tot3[0], tot_items = tot3[1], ns = tot3[2];
     mark(2);
-    // (c) splits -> records + children (level d)
-    const int64_t ns = block_scan(A.sa, m_prev, sh);
     const int base = s_created;
     if (2 * ns > A.cap_nl || base + 2 * ns > A.cap_nodes) {   // (cannot happen: caps bound every level)
       if (t == 0) {
@@ -363,17 +372,30 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
       }
       return;
     }
-    for (int j = t; j < m_prev; j += nt) {
-      const int i = A.hn[P][j];
+    // (b) leaf items of the nodes that do not split (read from the buffer level d - 1 read)
+    const int64_t n_emit = min(tot_items, A.cap_l - nl0);
+    for (int64_t k = t; k < n_emit; k += nt) {
+      const int64_t i = owner(A.se, n_prev, k);
+      const int64_t o = (k - A.se[i]) * A.chunk_rows;
+      LeafItemH it;
+      it.begin = A.lv_begin[P][i] + o;
+      it.count = min((int64_t)A.chunk_rows, pcnt[i] - o);
+      it.out = lbase + A.sd[i] + o;
+      it.gid = A.lv_gid[P][i];
+      it.pad = P;
+      A.litems[nl0 + k] = it;
+    }
+    // (c) splits -> records + children (level d), in split order
+    for (int i = t; i < n_prev; i += nt) {
       if (!A.flag[i]) continue;
-      const int64_t q = A.sa[j];
-      const int gid = A.lv_gid[P][i];
-      int64_t* r = R(gid);
+      const int j = A.loc[i];
+      const int64_t q = A.sf[i];
+      int64_t* r = R(A.lv_gid[P][i]);
       r[1] = A.r_feat[j];
       r[2] = A.r_bin[j];
       r[3] = A.r_dl[j];
       r[4] = dbits((double)A.r_gain[j]);
-      const int64_t ncnt = A.nc[P][j];
+      const int64_t ncnt = pcnt[i];
       const int64_t nl = A.r_cur[2 * j];
       if (nl < 0 || nl + A.r_cur[2 * j + 1] != ncnt) A.cnt[C_ERR] |= 1;
       const int64_t gl = base + 2 * q, gr = gl + 1;
@@ -390,7 +412,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
         rl[kRecFixed + s] = dbits(lt);
         rr[kRecFixed + s] = dbits(tt - lt);
       }
-      const int64_t b0 = A.nb[P][j];
+      const int64_t b0 = A.lv_begin[P][i];
       A.lv_tree[C][2 * q] = tree;
       A.lv_gid[C][2 * q] = (int32_t)gl;
       A.lv_begin[C][2 * q] = b0;
@@ -402,7 +424,12 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
       A.ppo[q] = A.nho[P][j];
     }
     n = (int)(2 * ns);
-    if (t == 0) A.cnt[C_NCREATED] = base + n;
+    if (t == 0) {
+      *A.leaf_pos = lbase + tot_rows;
+      A.cnt[C_NL] = (int)(nl0 + n_emit);
+      if (n_emit < tot_items) A.cnt[C_ERR] |= 2;
+      A.cnt[C_NCREATED] = base + n;
+    }
     __syncthreads();
     mark(3);
   }
@@ -413,33 +440,73 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     }
     return;
   }
-  // ---- plan level d: can / need (flag = can, sa = need)
+  // ---- plan level d, one pass over sibling pairs (level 0: over the roots). Per node i: flag bits
+  // 1 = can split, 2 = needs a histogram, 4 = left node of a histogram pair, 8 = the pair's derived (big) node;
+  // counts for one multi-scan: sa need, sb wide-load hist items, sc other hist items, sd partition items,
+  // se whole-node zero segments, sf CSR-region zero segments, sg pairs (at the left node)
   const int32_t* ltree = A.lv_tree[C];
   const int64_t* lcnt = A.lv_count[C];
-  for (int i = t; i < n; i += nt) {
+  const bool dense_split = A.live_dense >= 0 && A.live_dense < A.hsz;
+  auto can_split = [&](int i) {
     const int jt = ltree[i];
     const int64_t c = lcnt[i];
     bool can = d < A.j_depth[jt] && c >= 2 && (double)c >= 2 * A.j_inst[jt] - 1e-9;
     if (can && A.newton && d > 0 && A.j_mcw[jt] > 0 &&
         bitsd(R(A.lv_gid[C][i])[kRecFixed + 1]) < 2.0 * A.j_mcw[jt] * (1.0 - 1e-6))
       can = false;
-    A.flag[i] = can ? 1 : 0;
-    A.sa[i] = (can || d == 0) ? 1 : 0;
+    return can;
+  };
+  auto counts = [&](int i, int fl) {
+    const bool need = fl & 2;
+    const int64_t c = lcnt[i];
+    const int64_t nch = max((int64_t)1, cdiv(c, A.chunk_rows));
+    const int64_t ncsr = max((int64_t)1, cdiv(c, tmog::kCsrRows));
+    const bool build = need && !(fl & 8);
+    int64_t wide = 0, other = 0;
+    bool has_csr = false;
+    if (build)
+      for (int g = 0; g < A.n_groups; ++g) {
+        const int gfl = A.groups[g].z;
+        const bool reg = gfl & 1, csr = gfl & 2, wd = gfl & 4;
+        const int64_t k = (csr ? ncsr : nch) * ((csr || reg) ? 1 : A.n_sc);
+        if (wd) wide += k;
+        else other += k;
+        has_csr |= csr;
+      }
+    A.flag[i] = fl;
+    A.sa[i] = need ? 1 : 0;
+    A.sb[i] = wide;
+    A.sc[i] = other;
+    A.sd[i] = need ? max((int64_t)1, cdiv(c, tmog::kPartRows)) : 0;
+    A.se[i] = build && (nch > 1 || (has_csr && ncsr > 1 && !dense_split)) ? 1 : 0;
+    A.sf[i] = build && nch == 1 && has_csr && ncsr > 1 && dense_split ? 1 : 0;
+    A.sg[i] = (fl & 4) ? 1 : 0;
+  };
+  if (d == 0) {
+    for (int i = t; i < n; i += nt) counts(i, (can_split(i) ? 1 : 0) | 2);
+  } else {
+    for (int q = t; 2 * q + 1 < n; q += nt) {
+      const int li = 2 * q, ri = li + 1;
+      const bool cl = can_split(li), cr = can_split(ri);
+      bool nl = cl, nr = cr;
+      // subtraction pairing: when one sibling needs a histogram, the other gets one too if it is the smaller
+      // (built) one -- then the bigger one is derived from the parent
+      if (nl != nr && lcnt[li] >= 1 && lcnt[ri] >= 1 && (cl ? lcnt[ri] <= lcnt[li] : lcnt[li] <= lcnt[ri]))
+        nl = nr = true;
+      const bool pair = nl && nr;
+      const bool left_big = lcnt[li] >= lcnt[ri];
+      counts(li, (cl ? 1 : 0) | (nl ? 2 : 0) | (pair ? 4 : 0) | (pair && left_big ? 8 : 0));
+      counts(ri, (cr ? 1 : 0) | (nr ? 2 : 0) | (pair && !left_big ? 8 : 0));
+    }
   }
   __syncthreads();
   mark(4);
-  if (A.subtract && d > 0) {
-    for (int q = t; 2 * q + 1 < n; q += nt) {
-      const int li = 2 * q, ri = li + 1;
-      if (A.sa[li] != A.sa[ri] && lcnt[li] >= 1 && lcnt[ri] >= 1 &&
-          (A.flag[li] ? lcnt[ri] <= lcnt[li] : lcnt[li] <= lcnt[ri]))
-        A.sa[li] = A.sa[ri] = 1;
-    }
-    __syncthreads();
-  }
-  for (int i = t; i < n; i += nt) A.sb[i] = A.sa[i];     // need flags (sa becomes positions)
-  __syncthreads();
-  const int m = (int)block_scan(A.sa, n, sh);
+  int64_t* const arr7[7] = {A.sa, A.sb, A.sc, A.sd, A.se, A.sf, A.sg};
+  int64_t tot7[7];
+  block_scan_multi<7>(arr7, n, tot7, sh);
+  const int m = (int)tot7[0];
+  const int64_t n_wide = tot7[1], n_other = tot7[2], n_part = tot7[3], n_zw = tot7[4], n_zc = tot7[5];
+  const int n_pairs = (int)tot7[6];
   mark(5);
   if (m > A.cap_m) {                       // (cannot happen: caps bound every level)
     if (t == 0) {
@@ -450,6 +517,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     return;
   }
   if (m == 0) {                            // nothing to scan: every node of level d is a leaf
+    for (int i = t; i < n; i += nt) A.loc[i] = -1;
     emit_leaves(A, C, n, nullptr, C, sh);
     if (t == 0) {
       A.cnt[C_N] = 0;
@@ -457,105 +525,67 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     }
     return;
   }
-  for (int i = t; i < n; i += nt)
-    if (A.sb[i]) {
-      const int j = (int)A.sa[i];
-      A.hn[C][j] = i;
-      A.loc[i] = j;
+  // ---- emission: per-node tables (histogram node j = need prefix, in node order), pairs, zero segments
+  for (int i = t; i < n; i += nt) {
+    const int fl = A.flag[i];
+    if (!(fl & 2)) {
+      A.loc[i] = -1;
+      continue;
     }
-  __syncthreads();
-  for (int j = t; j < m; j += nt) {
-    const int i = A.hn[C][j];
+    const int j = (int)A.sa[i];
     const int jt = ltree[i];
+    A.hn[C][j] = i;
+    A.loc[i] = j;
     A.nmd[C][j] = A.j_model[jt];
     A.nho[C][j] = (int64_t)j * A.hsz;
     A.nb[C][j] = A.lv_begin[C][i];
     A.nc[C][j] = lcnt[i];
     A.nfo[j] = 0;
     A.nnf[j] = A.F_use;
+    const bool paired = d > 0 && (((i & 1) == 0 && (fl & 4)) || ((i & 1) == 1 && (A.flag[i - 1] & 4)));
     float* Pp = A.par[C] + (int64_t)j * 8;
     Pp[0] = (float)A.j_inst[jt];
     Pp[1] = (float)A.j_gain[jt];
     Pp[2] = (float)A.j_mcw[jt];
     Pp[3] = (float)A.j_lam[jt];
-    Pp[4] = 0.f;
+    Pp[4] = paired ? 1.f : 0.f;             // pair_fuse: the pair scan derives / scans both siblings
     Pp[5] = A.has_missing ? 1.f : 0.f;
     Pp[6] = (float)A.j_eps[jt];
-    Pp[7] = A.flag[i] ? 1.f : 0.f;
-  }
-  __syncthreads();
-  mark(6);
-  // ---- sibling pairs: (small, big) histogram node ids, parent offsets; big nodes are derived (flag = is_big)
-  for (int j = t; j < m; j += nt) A.flag[j] = 0;
-  __syncthreads();
-  int n_pairs = 0;
-  if (A.subtract && d > 0) {
-    const int nq = n / 2;
-    for (int q = t; q < nq; q += nt) A.sc[q] = (A.sb[2 * q] && A.sb[2 * q + 1]) ? 1 : 0;
-    __syncthreads();
-    n_pairs = (int)block_scan(A.sc, nq, sh);
-    for (int q = t; q < nq; q += nt) {
-      if (!(A.sb[2 * q] && A.sb[2 * q + 1])) continue;
-      const int li = 2 * q, ri = li + 1;
-      const bool left_big = lcnt[li] >= lcnt[ri];
-      const int big = A.loc[left_big ? li : ri], small = A.loc[left_big ? ri : li];
-      const int64_t k = A.sc[q];
-      A.sj[k] = small;
-      A.bj[k] = big;
-      A.poff[k] = A.ppo[q];
-      A.flag[big] = 1;
-      if (A.pair_fuse) {
-        A.par[C][(int64_t)small * 8 + 4] = 1.f;
-        A.par[C][(int64_t)big * 8 + 4] = 1.f;
-      }
+    Pp[7] = (fl & 1) ? 1.f : 0.f;
+    if (fl & 4) {                          // left node of a pair: (small, big) histogram nodes, parent offset
+      const int jr = (int)A.sa[i + 1];
+      const bool left_big = fl & 8;
+      const int64_t k = A.sg[i];
+      A.sj[k] = left_big ? jr : j;
+      A.bj[k] = left_big ? j : jr;
+      A.poff[k] = A.ppo[i >> 1];
     }
-    __syncthreads();
+    const bool zw = (i + 1 < n ? A.se[i + 1] : n_zw) != A.se[i];
+    const bool zc = (i + 1 < n ? A.sf[i + 1] : n_zc) != A.sf[i];
+    if (zw) {
+      A.zoff[A.se[i]] = (int64_t)j * A.hsz;
+      A.zsize[A.se[i]] = A.hsz;
+    }
+    if (zc) {
+      A.zoff[n_zw + A.sf[i]] = (int64_t)j * A.hsz + A.live_dense;
+      A.zsize[n_zw + A.sf[i]] = A.hsz - A.live_dense;
+    }
   }
-  mark(7);
-  // ---- per-node work counts: wide / other histogram items, partition items, zero segments
-  const bool dense_split = A.live_dense >= 0 && A.live_dense < A.hsz;
-  for (int j = t; j < m; j += nt) {
-    const int64_t c = A.nc[C][j];
-    const int64_t nch = max((int64_t)1, cdiv(c, A.chunk_rows));
-    const int64_t ncsr = max((int64_t)1, cdiv(c, tmog::kCsrRows));
-    const int64_t npi = max((int64_t)1, cdiv(c, tmog::kPartRows));
-    const bool build = A.flag[j] == 0;
-    int64_t wide = 0, other = 0;
-    bool has_csr = false;
-    if (build)
-      for (int g = 0; g < A.n_groups; ++g) {
-        const int fl = A.groups[g].z;
-        const bool reg = fl & 1, csr = fl & 2, wd = fl & 4;
-        const int64_t k = (csr ? ncsr : nch) * ((csr || reg) ? 1 : A.n_sc);
-        if (wd) wide += k;
-        else other += k;
-        has_csr |= csr;
-      }
-    A.sa[j] = wide;
-    A.sb[j] = other;
-    A.sc[j] = npi;
-    A.sd[j] = build && (nch > 1 || (has_csr && ncsr > 1 && !dense_split)) ? 1 : 0;
-    A.se[j] = build && nch == 1 && has_csr && ncsr > 1 && dense_split ? 1 : 0;
-  }
-  __syncthreads();
-  mark(8);
-  int64_t* const arr5[5] = {A.sa, A.sb, A.sc, A.sd, A.se};
-  int64_t tot5[5];
-  block_scan_multi<5>(arr5, m, tot5, sh);
-  const int64_t n_wide = tot5[0], n_other = tot5[1], n_part = tot5[2], n_zw = tot5[3], n_zc = tot5[4];
-  mark(9);
+  mark(6);
   const int64_t n_hist = n_wide + n_other;
   const int64_t h_emit = min(n_hist, A.cap_h), c_emit = min(n_part, A.cap_c);
   // histogram items, wide-load items first (the host's stable partition), then the others
   for (int64_t k = t; k < h_emit; k += nt) {
     const bool wsec = k < n_wide;
-    const int64_t* pre = wsec ? A.sa : A.sb;
+    const int64_t* pre = wsec ? A.sb : A.sc;
     const int64_t kk = wsec ? k : k - n_wide;
-    const int64_t j = owner(pre, m, kk);
-    int64_t local = kk - pre[j];
-    const int64_t c = A.nc[C][j];
+    const int64_t i = owner(pre, n, kk);
+    int64_t local = kk - pre[i];
+    const int64_t c = lcnt[i];
     const int64_t nch = max((int64_t)1, cdiv(c, A.chunk_rows));
     const int64_t ncsr = max((int64_t)1, cdiv(c, tmog::kCsrRows));
+    const int64_t b0 = A.lv_begin[C][i];
+    const int32_t j = (int32_t)A.sa[i];
     for (int g = 0; g < A.n_groups; ++g) {
       const int4 gr = A.groups[g];
       const bool reg = gr.z & 1, csr = gr.z & 2, wd = gr.z & 4;
@@ -569,43 +599,29 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
       const int64_t sc_ = local / nit, ci = local - sc_ * nit;
       const int64_t step = csr ? tmog::kCsrRows : A.chunk_rows;
       HistItemH h;
-      h.node = (int32_t)j;
+      h.node = j;
       h.fg0 = gr.x;
       h.nf = gr.y;
       h.excl = (nit == 1 ? 1 : 0) | (reg ? 2 : 0) | (csr ? 4 : 0) | (wd ? 16 : 0) |
                ((reg || csr) && A.live_dense >= 0 ? 8 : 0) | (int32_t)(sc_ << 8);
-      h.begin = A.nb[C][j] + ci * step;
+      h.begin = b0 + ci * step;
       h.count = min(step, c - ci * step);
       A.hitems[k] = h;
       break;
     }
   }
-  mark(10);
   // partition items of every scanned node (kPartRows-row slices)
   for (int64_t k = t; k < c_emit; k += nt) {
-    const int64_t j = owner(A.sc, m, k);
-    const int64_t ci = k - A.sc[j];
-    const int64_t c = A.nc[C][j];
-    PartItemH p;
-    p.node = (int32_t)j;
-    p.pad = 0;
-    p.begin = A.nb[C][j] + ci * tmog::kPartRows;
-    p.count = min((int64_t)tmog::kPartRows, c - ci * tmog::kPartRows);
-    p.out_left = p.out_right = 0;
-    A.citems[k] = p;
-  }
-  // zero segments: whole nodes first (dense prefix), then CSR-only regions past the dense prefix
-  for (int j = t; j < m; j += nt) {
-    const bool zw = (j + 1 < m ? A.sd[j + 1] : n_zw) != A.sd[j];
-    const bool zc = (j + 1 < m ? A.se[j + 1] : n_zc) != A.se[j];
-    if (zw) {
-      A.zoff[A.sd[j]] = A.nho[C][j];
-      A.zsize[A.sd[j]] = A.hsz;
-    }
-    if (zc) {
-      A.zoff[n_zw + A.se[j]] = A.nho[C][j] + A.live_dense;
-      A.zsize[n_zw + A.se[j]] = A.hsz - A.live_dense;
-    }
+    const int64_t i = owner(A.sd, n, k);
+    const int64_t ci = k - A.sd[i];
+    const int64_t c = lcnt[i];
+    PartItemH pi;
+    pi.node = (int32_t)A.sa[i];
+    pi.pad = 0;
+    pi.begin = A.lv_begin[C][i] + ci * tmog::kPartRows;
+    pi.count = min((int64_t)tmog::kPartRows, c - ci * tmog::kPartRows);
+    pi.out_left = pi.out_right = 0;
+    A.citems[k] = pi;
   }
   if (t == 0) {
     A.cnt[C_N] = n;
@@ -617,7 +633,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
     A.cnt[C_NZD] = (int)n_zw;
     if (h_emit < n_hist || c_emit < n_part) A.cnt[C_ERR] |= 2;
   }
-  mark(11);
+  mark(7);
 }
 
 struct FinArgs {
@@ -986,6 +1002,8 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
       P.sc = cv.take<int64_t>(cp.cap_nl);
       P.sd = cv.take<int64_t>(cp.cap_nl);
       P.se = cv.take<int64_t>(cp.cap_nl);
+      P.sf = cv.take<int64_t>(cp.cap_nl);
+      P.sg = cv.take<int64_t>(cp.cap_nl);
       P.flag = cv.take<int32_t>(cp.cap_nl);
       P.loc = cv.take<int32_t>(cp.cap_nl);
       *cnt = cv.take<int>(C_COUNT);
