@@ -180,6 +180,19 @@ def main():
 
     n_raw = [0]
     stage_t = [{}]
+    # time the interpreter spends in garbage collection inside each timed train (per-step diagnostics)
+    import gc
+    gc_t = [0.0, None]
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_t[1] = time.perf_counter()
+        elif gc_t[1] is not None:
+            gc_t[0] += time.perf_counter() - gc_t[1]
+            gc_t[1] = None
+
+    gc.callbacks.append(_gc_cb)
+    gc_steps = []
 
     def one_run():
         uid.reset(0)
@@ -191,10 +204,12 @@ def main():
                 torch.cuda.empty_cache()
         wf, pred = build_workflow(args, ds, label, preds)
         sync()
+        gc_t[0] = 0.0
         t0 = time.perf_counter()
         model = wf.train()
         sync()
         dt = time.perf_counter() - t0
+        gc_steps.append(round(gc_t[0], 4))
         stage_t[0] = {k: round(v, 4) for k, v in model.train_timings.items() if isinstance(v, (int, float))}
         per_stage = model.train_timings.get("stages", {})
         stage_t[0]["top_stages"] = dict(sorted(((k, round(v, 4)) for k, v in per_stage.items()
@@ -266,6 +281,7 @@ def main():
                        if world > 1 else "single"},
         }
         out["step_s"] = [round(x, 4) for x in times]
+        out["gc_s"] = gc_steps[-len(times):] if times else []
         from transmogrifai_amd.utils import watchdog as WD
         if WD.STALLS:                                   # fit-progress stalls seen by the lanes watchdog
             out["stalls"] = list(WD.STALLS)

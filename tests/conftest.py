@@ -12,6 +12,14 @@ if TESTS not in sys.path:       # test-only helper modules (e.g. map_reference_i
 
 
 def pytest_configure(config):
+    # host torch ops of the (small) test problems: intra-op threads beyond a few cost more than they give on
+    # shared vCPUs (softplus of a 4500 x 32 block: 1.9 ms on 1 thread, 13.5 ms on 8 here), and xdist workers
+    # each spin their own pool; TMOG_TEST_THREADS overrides
+    try:
+        import torch
+        torch.set_num_threads(int(os.environ.get("TMOG_TEST_THREADS", "1")))
+    except Exception:
+        pass
     config.addinivalue_line("markers", "gpu: test needs an MI355X (HIP) device")
     config.addinivalue_line("markers", "slow: long-running test")
 
