@@ -146,6 +146,7 @@ struct PlanArgs {
   int32_t* loc;
   int64_t cap_nl, cap_m, cap_nodes, cap_h, cap_c, cap_l;
   int profile;                 // TMOG_PLAN_PROFILE: per-phase wall-clock ticks into g_plan_prof
+  int64_t lds_cap;             // > 0: scratch arrays in dynamic LDS with this many entries each
 };
 
 // TMOG_PLAN_PROFILE diagnostics: wall-clock ticks (100 MHz) spent in each phase of level_plan_kernel, summed
@@ -275,8 +276,25 @@ __device__ void emit_leaves(const PlanArgs& A, int lvl, int n, const int32_t* sp
 // One level of planning. d > 0 first turns level d - 1's device decisions (split_find + partition) into
 // the tree records, the leaf items of its non-splitting nodes and the children (level d); then level d's
 // work lists are built. Host twin: common/tree_grow.hpp grow_group (GPU backend, no feature subsets).
-__global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
+constexpr int kPlanScratch = 7;     // int64 per-node scratch arrays of the planner (sa .. sg) + one int32 (flag)
+
+__global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
   __shared__ int64_t sh[1024];
+  // the per-node scratch arrays live in LDS when the level capacity fits (A0.lds_cap > 0): every scan, owner
+  // search and flag read of the plan is then an LDS access instead of an L2 round trip
+  extern __shared__ int64_t dyn_scratch[];
+  PlanArgs A = A0;
+  if (A0.lds_cap > 0) {
+    int64_t* base = dyn_scratch;
+    A.sa = base;
+    A.sb = base + A0.lds_cap;
+    A.sc = base + 2 * A0.lds_cap;
+    A.sd = base + 3 * A0.lds_cap;
+    A.se = base + 4 * A0.lds_cap;
+    A.sf = base + 5 * A0.lds_cap;
+    A.sg = base + 6 * A0.lds_cap;
+    A.flag = reinterpret_cast<int32_t*>(base + 7 * A0.lds_cap);
+  }
   __shared__ int s_n_prev, s_m_prev, s_created;
   const int t = threadIdx.x, nt = blockDim.x;
   const int d = A.d, S = A.S, T = A.T;
@@ -1094,10 +1112,20 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
     P.has_missing = a.missing_bin >= 0 ? 1 : 0;
     const int32_t* flist_d = (const int32_t*)(K + o_flist);
     // levels 0..D build histograms (level D only when D == 0: deeper, no node of level D may split), and
+    // planner scratch in LDS when the per-level node capacity fits (TMOG_PLAN_LDS=0: global memory)
+    static const bool plan_lds_ok = [] { const char* e = std::getenv("TMOG_PLAN_LDS"); return !(e && e[0] == '0'); }();
+    const size_t per_node = (size_t)kPlanScratch * sizeof(int64_t) + sizeof(int32_t);
+    static const bool lds_attr = hipFuncSetAttribute((const void*)level_plan_kernel,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 148 * 1024) ==
+                                 hipSuccess;   // once per process (thread-safe static initialisation)
+    const bool lds_fit = plan_lds_ok && lds_attr && cp.cap_nl > 0 &&
+                         per_node * (size_t)cp.cap_nl + 64 <= (size_t)148 * 1024;
+    P.lds_cap = lds_fit ? cp.cap_nl : 0;
+    const size_t plan_lds = lds_fit ? per_node * (size_t)cp.cap_nl + 64 : 0;
     // plan D + 1 turns the last decisions into leaves
     for (int d = 0; d <= cp.D + 1; ++d) {
       P.d = d;
-      hipLaunchKernelGGL(level_plan_kernel, dim3(1), dim3(1024), 0, st, P);
+      hipLaunchKernelGGL(level_plan_kernel, dim3(1), dim3(1024), plan_lds, st, P);
       kchk((int)hipGetLastError(), "level_plan");
       const int64_t nprev = d > 0 ? cp.nmax[d - 1] : 0;
       const int64_t lbound = (total / std::max<int64_t>(a.chunk_rows, 1) + nprev + 1) +
