@@ -235,31 +235,38 @@ __device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 
 
 // Leaf items of the nodes i in [0, n) whose sa-flag is 0 (sa == nullptr: all nodes), reading buffer `buf`.
 // Appends to litems at C_NL and advances the leaf cursor (host twin: the collect lambda of grow_group).
-__device__ void emit_leaves(const PlanArgs& A, int lvl, int n, const int32_t* split, int buf, int64_t* sh) {
+// The planner's per-node scratch arrays (global memory, or dynamic LDS when the level capacity fits).
+struct PlanScratch {
+  int64_t *sa, *sb, *sc, *sd, *se, *sf, *sg;
+  int32_t* flag;
+};
+
+__device__ void emit_leaves(const PlanArgs& A, const PlanScratch& Z, int lvl, int n, const int32_t* split, int buf,
+                            int64_t* sh) {
   const int t = threadIdx.x, nt = blockDim.x;
   const int64_t* cnt_ = A.lv_count[lvl];
   for (int i = t; i < n; i += nt) {
     const bool leaf = split == nullptr || split[i] == 0;
     const int64_t c = cnt_[i];
-    A.sd[i] = leaf && c > 0 ? c : 0;
-    A.se[i] = leaf && c > 0 ? cdiv(c, A.chunk_rows) : 0;
+    Z.sd[i] = leaf && c > 0 ? c : 0;
+    Z.se[i] = leaf && c > 0 ? cdiv(c, A.chunk_rows) : 0;
   }
   __syncthreads();
   const int64_t lbase = *A.leaf_pos;
   const int64_t nl0 = A.cnt[C_NL];
   __syncthreads();
-  int64_t* const arr[2] = {A.sd, A.se};
+  int64_t* const arr[2] = {Z.sd, Z.se};
   int64_t tots[2];
   block_scan_multi<2>(arr, n, tots, sh);
   const int64_t tot_rows = tots[0], tot_items = tots[1];
   const int64_t n_emit = min(tot_items, A.cap_l - nl0);
   for (int64_t k = t; k < n_emit; k += nt) {
-    const int64_t i = owner(A.se, n, k);
-    const int64_t o = (k - A.se[i]) * A.chunk_rows;
+    const int64_t i = owner(Z.se, n, k);
+    const int64_t o = (k - Z.se[i]) * A.chunk_rows;
     LeafItemH it;
     it.begin = A.lv_begin[lvl][i] + o;
     it.count = min((int64_t)A.chunk_rows, cnt_[i] - o);
-    it.out = lbase + A.sd[i] + o;
+    it.out = lbase + Z.sd[i] + o;
     it.gid = A.lv_gid[lvl][i];
     it.pad = buf;
     A.litems[nl0 + k] = it;
@@ -278,22 +285,16 @@ __device__ void emit_leaves(const PlanArgs& A, int lvl, int n, const int32_t* sp
 // work lists are built. Host twin: common/tree_grow.hpp grow_group (GPU backend, no feature subsets).
 constexpr int kPlanScratch = 7;     // int64 per-node scratch arrays of the planner (sa .. sg) + one int32 (flag)
 
-__global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
+__global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
   __shared__ int64_t sh[1024];
-  // the per-node scratch arrays live in LDS when the level capacity fits (A0.lds_cap > 0): every scan, owner
+  // the per-node scratch arrays live in LDS when the level capacity fits (A.lds_cap > 0): every scan, owner
   // search and flag read of the plan is then an LDS access instead of an L2 round trip
   extern __shared__ int64_t dyn_scratch[];
-  PlanArgs A = A0;
-  if (A0.lds_cap > 0) {
+  PlanScratch Z{A.sa, A.sb, A.sc, A.sd, A.se, A.sf, A.sg, A.flag};
+  if (A.lds_cap > 0) {
     int64_t* base = dyn_scratch;
-    A.sa = base;
-    A.sb = base + A0.lds_cap;
-    A.sc = base + 2 * A0.lds_cap;
-    A.sd = base + 3 * A0.lds_cap;
-    A.se = base + 4 * A0.lds_cap;
-    A.sf = base + 5 * A0.lds_cap;
-    A.sg = base + 6 * A0.lds_cap;
-    A.flag = reinterpret_cast<int32_t*>(base + 7 * A0.lds_cap);
+    Z = PlanScratch{base, base + A.lds_cap, base + 2 * A.lds_cap, base + 3 * A.lds_cap, base + 4 * A.lds_cap,
+                    base + 5 * A.lds_cap, base + 6 * A.lds_cap, reinterpret_cast<int32_t*>(base + 7 * A.lds_cap)};
   }
   __shared__ int s_n_prev, s_m_prev, s_created;
   const int t = threadIdx.x, nt = blockDim.x;
@@ -367,16 +368,16 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
       }
       const int64_t c = pcnt[i];
       const bool leaf = !split && c > 0;
-      A.sd[i] = leaf ? c : 0;
-      A.se[i] = leaf ? cdiv(c, A.chunk_rows) : 0;
-      A.sf[i] = split ? 1 : 0;
-      A.flag[i] = split ? 1 : 0;
+      Z.sd[i] = leaf ? c : 0;
+      Z.se[i] = leaf ? cdiv(c, A.chunk_rows) : 0;
+      Z.sf[i] = split ? 1 : 0;
+      Z.flag[i] = split ? 1 : 0;
     }
     __syncthreads();
     mark(1);
     const int64_t lbase = *A.leaf_pos;
     const int64_t nl0 = A.cnt[C_NL];
-    int64_t* const arr3[3] = {A.sd, A.se, A.sf};
+    int64_t* const arr3[3] = {Z.sd, Z.se, Z.sf};
     int64_t tot3[3];
     block_scan_multi<3>(arr3, n_prev, tot3, sh);
     const int64_t tot_rows = tot3[0], tot_items = tot3[1], ns = tot3[2];
@@ -393,21 +394,21 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
     // (b) leaf items of the nodes that do not split (read from the buffer level d - 1 read)
     const int64_t n_emit = min(tot_items, A.cap_l - nl0);
     for (int64_t k = t; k < n_emit; k += nt) {
-      const int64_t i = owner(A.se, n_prev, k);
-      const int64_t o = (k - A.se[i]) * A.chunk_rows;
+      const int64_t i = owner(Z.se, n_prev, k);
+      const int64_t o = (k - Z.se[i]) * A.chunk_rows;
       LeafItemH it;
       it.begin = A.lv_begin[P][i] + o;
       it.count = min((int64_t)A.chunk_rows, pcnt[i] - o);
-      it.out = lbase + A.sd[i] + o;
+      it.out = lbase + Z.sd[i] + o;
       it.gid = A.lv_gid[P][i];
       it.pad = P;
       A.litems[nl0 + k] = it;
     }
     // (c) splits -> records + children (level d), in split order
     for (int i = t; i < n_prev; i += nt) {
-      if (!A.flag[i]) continue;
+      if (!Z.flag[i]) continue;
       const int j = A.loc[i];
-      const int64_t q = A.sf[i];
+      const int64_t q = Z.sf[i];
       int64_t* r = R(A.lv_gid[P][i]);
       r[1] = A.r_feat[j];
       r[2] = A.r_bin[j];
@@ -491,14 +492,14 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
         else other += k;
         has_csr |= csr;
       }
-    A.flag[i] = fl;
-    A.sa[i] = need ? 1 : 0;
-    A.sb[i] = wide;
-    A.sc[i] = other;
-    A.sd[i] = need ? max((int64_t)1, cdiv(c, tmog::kPartRows)) : 0;
-    A.se[i] = build && (nch > 1 || (has_csr && ncsr > 1 && !dense_split)) ? 1 : 0;
-    A.sf[i] = build && nch == 1 && has_csr && ncsr > 1 && dense_split ? 1 : 0;
-    A.sg[i] = (fl & 4) ? 1 : 0;
+    Z.flag[i] = fl;
+    Z.sa[i] = need ? 1 : 0;
+    Z.sb[i] = wide;
+    Z.sc[i] = other;
+    Z.sd[i] = need ? max((int64_t)1, cdiv(c, tmog::kPartRows)) : 0;
+    Z.se[i] = build && (nch > 1 || (has_csr && ncsr > 1 && !dense_split)) ? 1 : 0;
+    Z.sf[i] = build && nch == 1 && has_csr && ncsr > 1 && dense_split ? 1 : 0;
+    Z.sg[i] = (fl & 4) ? 1 : 0;
   };
   if (d == 0) {
     for (int i = t; i < n; i += nt) counts(i, (can_split(i) ? 1 : 0) | 2);
@@ -519,7 +520,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
   }
   __syncthreads();
   mark(4);
-  int64_t* const arr7[7] = {A.sa, A.sb, A.sc, A.sd, A.se, A.sf, A.sg};
+  int64_t* const arr7[7] = {Z.sa, Z.sb, Z.sc, Z.sd, Z.se, Z.sf, Z.sg};
   int64_t tot7[7];
   block_scan_multi<7>(arr7, n, tot7, sh);
   const int m = (int)tot7[0];
@@ -536,7 +537,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
   }
   if (m == 0) {                            // nothing to scan: every node of level d is a leaf
     for (int i = t; i < n; i += nt) A.loc[i] = -1;
-    emit_leaves(A, C, n, nullptr, C, sh);
+    emit_leaves(A, Z, C, n, nullptr, C, sh);
     if (t == 0) {
       A.cnt[C_N] = 0;
       for (int k = C_M; k <= C_NZD; ++k) A.cnt[k] = 0;
@@ -545,12 +546,12 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
   }
   // ---- emission: per-node tables (histogram node j = need prefix, in node order), pairs, zero segments
   for (int i = t; i < n; i += nt) {
-    const int fl = A.flag[i];
+    const int fl = Z.flag[i];
     if (!(fl & 2)) {
       A.loc[i] = -1;
       continue;
     }
-    const int j = (int)A.sa[i];
+    const int j = (int)Z.sa[i];
     const int jt = ltree[i];
     A.hn[C][j] = i;
     A.loc[i] = j;
@@ -560,7 +561,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
     A.nc[C][j] = lcnt[i];
     A.nfo[j] = 0;
     A.nnf[j] = A.F_use;
-    const bool paired = d > 0 && (((i & 1) == 0 && (fl & 4)) || ((i & 1) == 1 && (A.flag[i - 1] & 4)));
+    const bool paired = d > 0 && (((i & 1) == 0 && (fl & 4)) || ((i & 1) == 1 && (Z.flag[i - 1] & 4)));
     float* Pp = A.par[C] + (int64_t)j * 8;
     Pp[0] = (float)A.j_inst[jt];
     Pp[1] = (float)A.j_gain[jt];
@@ -571,22 +572,22 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
     Pp[6] = (float)A.j_eps[jt];
     Pp[7] = (fl & 1) ? 1.f : 0.f;
     if (fl & 4) {                          // left node of a pair: (small, big) histogram nodes, parent offset
-      const int jr = (int)A.sa[i + 1];
+      const int jr = (int)Z.sa[i + 1];
       const bool left_big = fl & 8;
-      const int64_t k = A.sg[i];
+      const int64_t k = Z.sg[i];
       A.sj[k] = left_big ? jr : j;
       A.bj[k] = left_big ? j : jr;
       A.poff[k] = A.ppo[i >> 1];
     }
-    const bool zw = (i + 1 < n ? A.se[i + 1] : n_zw) != A.se[i];
-    const bool zc = (i + 1 < n ? A.sf[i + 1] : n_zc) != A.sf[i];
+    const bool zw = (i + 1 < n ? Z.se[i + 1] : n_zw) != Z.se[i];
+    const bool zc = (i + 1 < n ? Z.sf[i + 1] : n_zc) != Z.sf[i];
     if (zw) {
-      A.zoff[A.se[i]] = (int64_t)j * A.hsz;
-      A.zsize[A.se[i]] = A.hsz;
+      A.zoff[Z.se[i]] = (int64_t)j * A.hsz;
+      A.zsize[Z.se[i]] = A.hsz;
     }
     if (zc) {
-      A.zoff[n_zw + A.sf[i]] = (int64_t)j * A.hsz + A.live_dense;
-      A.zsize[n_zw + A.sf[i]] = A.hsz - A.live_dense;
+      A.zoff[n_zw + Z.sf[i]] = (int64_t)j * A.hsz + A.live_dense;
+      A.zsize[n_zw + Z.sf[i]] = A.hsz - A.live_dense;
     }
   }
   mark(6);
@@ -595,7 +596,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
   // histogram items, wide-load items first (the host's stable partition), then the others
   for (int64_t k = t; k < h_emit; k += nt) {
     const bool wsec = k < n_wide;
-    const int64_t* pre = wsec ? A.sb : A.sc;
+    const int64_t* pre = wsec ? Z.sb : Z.sc;
     const int64_t kk = wsec ? k : k - n_wide;
     const int64_t i = owner(pre, n, kk);
     int64_t local = kk - pre[i];
@@ -603,7 +604,7 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
     const int64_t nch = max((int64_t)1, cdiv(c, A.chunk_rows));
     const int64_t ncsr = max((int64_t)1, cdiv(c, tmog::kCsrRows));
     const int64_t b0 = A.lv_begin[C][i];
-    const int32_t j = (int32_t)A.sa[i];
+    const int32_t j = (int32_t)Z.sa[i];
     for (int g = 0; g < A.n_groups; ++g) {
       const int4 gr = A.groups[g];
       const bool reg = gr.z & 1, csr = gr.z & 2, wd = gr.z & 4;
@@ -630,11 +631,11 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A0) {
   }
   // partition items of every scanned node (kPartRows-row slices)
   for (int64_t k = t; k < c_emit; k += nt) {
-    const int64_t i = owner(A.sd, n, k);
-    const int64_t ci = k - A.sd[i];
+    const int64_t i = owner(Z.sd, n, k);
+    const int64_t ci = k - Z.sd[i];
     const int64_t c = lcnt[i];
     PartItemH pi;
-    pi.node = (int32_t)A.sa[i];
+    pi.node = (int32_t)Z.sa[i];
     pi.pad = 0;
     pi.begin = A.lv_begin[C][i] + ci * tmog::kPartRows;
     pi.count = min((int64_t)tmog::kPartRows, c - ci * tmog::kPartRows);
