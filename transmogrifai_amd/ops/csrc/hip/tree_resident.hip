@@ -290,6 +290,9 @@ __global__ void __launch_bounds__(1024) level_plan_kernel(PlanArgs A) {
   // the per-node scratch arrays live in LDS when the level capacity fits (A.lds_cap > 0): every scan, owner
   // search and flag read of the plan is then an LDS access instead of an L2 round trip
   extern __shared__ int64_t dyn_scratch[];
+  // the plan is the serial link between two levels of this tree while its CU usually also runs other boosting
+  // parts' histogram waves: issue priority over them
+  __builtin_amdgcn_s_setprio(3);
   PlanScratch Z{A.sa, A.sb, A.sc, A.sd, A.se, A.sf, A.sg, A.flag};
   if (A.lds_cap > 0) {
     int64_t* base = dyn_scratch;
@@ -680,6 +683,7 @@ struct FinArgs {
 // their kept ancestor's value. The host rebuilds the Forest from the same records with tree_cpu.cpp.
 // Pruning bottom-up level by level is the sequential reverse-id loop (children have higher ids than parents).
 __global__ void __launch_bounds__(1024) tree_finalize_kernel(FinArgs A) {
+  __builtin_amdgcn_s_setprio(3);            // serial link between two boosting rounds (see level_plan_kernel)
   const int t = threadIdx.x, nt = blockDim.x;
   const int64_t n = A.cnt[C_NCREATED];
   auto R = [&](int64_t g) { return A.rec + (g + 1) * (int64_t)A.W; };
