@@ -405,10 +405,10 @@ def _entry_models(models: tuple, counts: tuple, dev) -> torch.Tensor:
     """Model id of every root entry (job j's ``counts[j]`` entries carry ``models[j]``), cached: the boosting
     rounds of one active job set reuse it. One fill per job -- ``torch.repeat_interleave`` with a handful
     of repeats runs one thread per repeat on ROCm (~350 us for 2M entries)."""
-    key = (models, counts, str(dev))
+    key = (models, counts, str(dev), _stream_key(dev))
     t = _ENTRY_MODELS.get(key)
     if t is None:
-        if len(_ENTRY_MODELS) >= 8:
+        if len(_ENTRY_MODELS) >= 32:
             _ENTRY_MODELS.clear()
         parts = [torch.full((c,), m, dtype=torch.int64, device=dev) for m, c in zip(models, counts) if c]
         t = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev)
@@ -765,9 +765,19 @@ from ..ops.staging import Pack as _Pack  # noqa: E402  (re-exported for the lear
 _CONST: dict = {}
 
 
+def _stream_key(dev) -> int:
+    """The calling thread's current stream on ``dev`` (0 on the host). The device-tensor caches below are kept
+    per stream: a cached tensor is then only ever read by kernels of the stream it was allocated on, so when an
+    eviction frees it the caching allocator can hand its block only to later work of that same stream. Shared
+    across streams (the boosting parts, the learner lanes), an evicted tensor's block could be reused on its
+    allocation stream while another stream's queued kernels still read it -- stale index tensors, and faults."""
+    dev = torch.device(dev)
+    return int(torch.cuda.current_stream(dev).cuda_stream) if dev.type == "cuda" else 0
+
+
 def _const_tensor(a: np.ndarray, dev) -> torch.Tensor:
-    """Device copy of a small constant host array, cached by content (no per-call blocking copy)."""
-    key = (str(dev), a.dtype.str, a.shape, a.tobytes())
+    """Device copy of a small constant host array, cached by content and stream (no per-call blocking copy)."""
+    key = (str(dev), _stream_key(dev), a.dtype.str, a.shape, a.tobytes())
     t = _CONST.get(key)
     if t is None:
         if len(_CONST) > 256:
