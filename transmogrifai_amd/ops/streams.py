@@ -10,7 +10,12 @@ the concurrency they were meant to buy turns into head-of-line blocking (docs/RO
 Here every such user leases from ``TMOG_SIDE_STREAMS`` (default 3) persistent streams created once per device:
 with the caller's stream that is one stream per hardware queue. A lease never blocks -- a user that gets fewer
 streams than it asked for shares: lanes and boosting parts merge their work, grower groups share a stream --
-and none of those choices changes a result (trees and metrics do not depend on the stream layout)."""
+and none of those choices changes a result (trees and metrics do not depend on the stream layout).
+
+A second set of high-priority streams serves the critical path of a lanes run (``TMOG_LANE_PRIO``): the longest
+learner's lane and every stream it leases (its boosting parts, grower groups) run at high queue priority, so
+when the lanes' kernels compete for compute units the hardware dispatcher feeds the critical learner first and
+the shorter lanes fill the gaps. A lease made from a high-priority stream draws from the high set."""
 from __future__ import annotations
 
 import contextlib
@@ -21,8 +26,8 @@ from typing import Dict, List
 import torch
 
 _LOCK = threading.Lock()
-_POOL: Dict[int, List[torch.cuda.Stream]] = {}
-_BUSY: Dict[int, set] = {}
+_POOL: Dict[tuple, List[torch.cuda.Stream]] = {}
+_BUSY: Dict[tuple, set] = {}
 
 
 def n_side() -> int:
@@ -34,17 +39,26 @@ def _index(dev) -> int:
     return dev.index if dev.index is not None else torch.cuda.current_device()
 
 
-def lease(dev, n: int) -> List[torch.cuda.Stream]:
-    """Up to ``n`` currently unleased side streams of ``dev`` (possibly none)."""
+def is_high(stream) -> bool:
+    return stream is not None and getattr(stream, "priority", 0) < 0
+
+
+def lease(dev, n: int, high=None) -> List[torch.cuda.Stream]:
+    """Up to ``n`` currently unleased side streams of ``dev`` (possibly none). ``high`` selects the
+    high-priority set; by default a caller running on a high-priority stream leases from it."""
     if n <= 0 or torch.device(dev).type != "cuda":
         return []
     i = _index(dev)
+    if high is None:
+        high = is_high(torch.cuda.current_stream(torch.device("cuda", i)))
+    key = (i, bool(high))
     with _LOCK:
-        pool = _POOL.get(i)
+        pool = _POOL.get(key)
         if pool is None:
-            pool = _POOL[i] = [torch.cuda.Stream(device=torch.device("cuda", i)) for _ in range(n_side())]
-            _BUSY[i] = set()
-        busy = _BUSY[i]
+            pool = _POOL[key] = [torch.cuda.Stream(device=torch.device("cuda", i), priority=-1 if high else 0)
+                                 for _ in range(n_side())]
+            _BUSY[key] = set()
+        busy = _BUSY[key]
         got = [k for k in range(len(pool)) if k not in busy][:n]
         busy.update(got)
         return [pool[k] for k in got]
@@ -55,16 +69,19 @@ def release(dev, streams: List[torch.cuda.Stream]) -> None:
         return
     i = _index(dev)
     with _LOCK:
-        pool, busy = _POOL[i], _BUSY[i]
-        for s in streams:
-            for k, p in enumerate(pool):
-                if p == s:
-                    busy.discard(k)
+        for key in ((i, False), (i, True)):
+            if key not in _POOL:
+                continue
+            pool, busy = _POOL[key], _BUSY[key]
+            for s in streams:
+                for k, p in enumerate(pool):
+                    if p == s:
+                        busy.discard(k)
 
 
 @contextlib.contextmanager
-def leased(dev, n: int):
-    got = lease(dev, n)
+def leased(dev, n: int, high=None):
+    got = lease(dev, n, high)
     try:
         yield got
     finally:
@@ -75,4 +92,4 @@ def in_use(dev) -> int:
     """Streams of ``dev`` currently leased (tests / diagnostics)."""
     i = _index(dev)
     with _LOCK:
-        return len(_BUSY.get(i, ()))
+        return len(_BUSY.get((i, False), ())) + len(_BUSY.get((i, True), ()))

@@ -464,12 +464,18 @@ class OpValidator:
         # lane 0 runs on the caller's stream, the others on side streams of the fixed process-wide set
         # (ops/streams.py: one stream per hardware queue); fewer free side streams -> fewer lanes
         from ..ops import streams as SP
-        side = SP.lease(dev, lanes - 1) if gpu else []
+        # TMOG_LANE_PRIO=1: the critical (first, longest) learner's lane runs on a high-priority stream (its boosting
+        # parts and grower groups then lease high-priority streams too) and the caller's stream goes to the next lane
+        crit = SP.lease(dev, 1, high=True) if gpu and lanes > 1 and os.environ.get("TMOG_LANE_PRIO", "0") == "1" \
+            else []
+        side = crit + (SP.lease(dev, lanes - 1 - len(crit)) if gpu else [])
         if gpu:
-            lanes = 1 + len(side)
+            streams = crit + [cur] + side[len(crit):]
+            lanes = len(streams)
             for st in side:
                 st.wait_stream(cur)
-        streams = ([cur] + side) if gpu else [None] * lanes
+        else:
+            streams = [None] * lanes
 
         def worker(w):
             try:
