@@ -65,6 +65,11 @@ def parse():
                     help="multi-GPU table layout: row shards with all-reduced fit statistics (data parallel), "
                          "or the whole table on every rank")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--ingest", default="memory", choices=["memory", "parquet"],
+                    help="memory: the device-resident synthetic table is the reader's input (the headline); parquet: "
+                         "the table is written to a Parquet file before timing and every timed train reads it "
+                         "(readers/columnar.py) inside the timed region")
+    ap.add_argument("--ingest-dir", default=None, help="directory of the --ingest parquet file (default /tmp)")
     ap.add_argument("--max-training-sample", dest="max_training_sample", type=int, default=None,
                     help="the selector splitter's maxTrainingSample (default: the reference's 1M)")
     a = ap.parse_args()
@@ -95,7 +100,7 @@ def _expected_configs(args) -> int:
     return sum(len(grid) for _, grid in sel.models)
 
 
-def build_workflow(args, ds, label, preds):
+def build_workflow(args, ds, label, preds, reader=None):
     from transmogrifai_amd.dsl import transmogrify
     from transmogrifai_amd.readers.base import InMemoryReader
     from transmogrifai_amd.workflow.workflow import OpWorkflow
@@ -108,7 +113,7 @@ def build_workflow(args, ds, label, preds):
         splitter.max_training_sample = int(args.max_training_sample)
     pred = _selector_cls(args).with_cross_validation(
         splitter=splitter, num_folds=args.folds, model_types_to_use=types, seed=42).set_input(label, checked).get_output()
-    wf = OpWorkflow().set_result_features(label, pred).set_reader(InMemoryReader(ds))
+    wf = OpWorkflow().set_result_features(label, pred).set_reader(reader or InMemoryReader(ds))
     return wf, pred
 
 
@@ -194,6 +199,8 @@ def main():
     gc.callbacks.append(_gc_cb)
     gc_steps = []
 
+    pq_path = [None]
+
     def one_run():
         uid.reset(0)
         ds, label, preds = make_table()
@@ -202,7 +209,23 @@ def main():
             ds = ds.shard(D.rank(), world)      # N / world rows per GPU; global row ids kept
             if use_gpu:
                 torch.cuda.empty_cache()
-        wf, pred = build_workflow(args, ds, label, preds)
+        reader = None
+        if args.ingest == "parquet":
+            from transmogrifai_amd.readers.columnar import dataset_to_parquet
+            from transmogrifai_amd.readers.files import ParquetReader
+            if pq_path[0] is None:              # written once, untimed; the same seeded table every run
+                d = args.ingest_dir or "/tmp"
+                pq_path[0] = os.path.join(d, f"tmog_bench_{args.config}_{args.rows}_{os.getpid()}.parquet")
+                t_w = time.perf_counter()
+                dataset_to_parquet(ds, pq_path[0], names=[f.name for f in [label] + list(preds)])
+                print(f"[ingest] wrote {pq_path[0]} ({os.path.getsize(pq_path[0]) / 1e9:.2f} GB) in "
+                      f"{time.perf_counter() - t_w:.1f} s", file=sys.stderr, flush=True)
+            reader = ParquetReader(pq_path[0], device=dev)
+            del ds
+            ds = None
+            if use_gpu:
+                torch.cuda.empty_cache()
+        wf, pred = build_workflow(args, ds, label, preds, reader)
         sync()
         gc_t[0] = 0.0
         t0 = time.perf_counter()
@@ -230,6 +253,19 @@ def main():
         return dt, ho, summ
 
     expected_configs = _expected_configs(args)
+    if args.ingest == "parquet" and world > 1:
+        raise SystemExit("--ingest parquet is a single-GPU measurement")
+    try:
+        _timed(args, one_run, expected_configs, use_gpu, dev, torch, D, sim, n_raw, stage_t, gc_steps, world)
+    finally:
+        if pq_path[0] and os.path.exists(pq_path[0]):
+            os.remove(pq_path[0])
+    if D.is_dist() and not sim:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def _timed(args, one_run, expected_configs, use_gpu, dev, torch, D, sim, n_raw, stage_t, gc_steps, world):
     for _ in range(args.warmup):
         one_run()
     if use_gpu:
@@ -291,10 +327,11 @@ def main():
         if sim:
             out["simulated"] = {"rank": D.rank(), "world": D.world(),
                                 "note": "one rank's share timed on one GPU; collectives not executed"}
+        if args.ingest == "parquet":
+            out["config"]["ingest"] = "parquet"
+            out["data"] = ("synthetic (device-generated, seeded), written to a Parquet file before timing and read "
+                           "by every timed train (readers/columnar.py), random-init models")
         print(json.dumps(out), flush=True)
-    if D.is_dist() and not sim:
-        import torch.distributed as dist
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,94 @@
+"""Columnar Parquet ingest (readers/columnar.py) against the generic pandas path (readers/base.py): identical
+datasets -- values, null masks, text dictionaries and codes, key -- over several row groups, nulls at row-group
+boundaries, float32 / float64 / int columns."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from transmogrifai_amd.features.builder import FeatureBuilder
+from transmogrifai_amd.readers.files import DataReaders
+
+
+def _frame(n, seed=0):
+    rng = np.random.default_rng(seed)
+    r32 = rng.standard_normal(n).astype(np.float32)
+    r64 = rng.standard_normal(n)
+    r64[rng.random(n) < 0.2] = np.nan
+    r64[36:38] = np.nan                                   # across the 37-row row-group boundary
+    ints = pd.array(rng.integers(-5, 50, n), dtype="Int64")
+    ints[rng.random(n) < 0.1] = pd.NA
+    cats = np.array(["a", "bb", "", "c d"], dtype=object)[rng.integers(0, 4, n)]
+    cats[rng.random(n) < 0.15] = None
+    txt = np.array([f"w{k} z" for k in rng.integers(0, 30, n)], dtype=object)
+    return pd.DataFrame({"key": [f"k{i}" for i in range(n)], "r32": r32, "r64": r64, "i": ints,
+                         "cat": cats, "txt": txt, "y": (rng.random(n) < 0.4).astype(np.float64)})
+
+
+def _features():
+    return [FeatureBuilder.Real("r32").as_predictor(), FeatureBuilder.Real("r64").as_predictor(),
+            FeatureBuilder.Integral("i").as_predictor(), FeatureBuilder.PickList("cat").as_predictor(),
+            FeatureBuilder.Text("txt").as_predictor(), FeatureBuilder.RealNN("y").as_response()]
+
+
+def _read(path, dev, columnar, monkeypatch):
+    monkeypatch.setenv("TMOG_COLUMNAR", "1" if columnar else "0")
+    return DataReaders.Simple.parquet(path, device=dev).generate_dataset(_features())
+
+
+def _compare(a, b, same_dtype=True):
+    assert a.n_rows == b.n_rows and list(a.columns) == list(b.columns)
+    assert (a.key is None and b.key is None) or list(a.key) == list(b.key)
+    for name in a.columns:
+        ca, cb = a[name], b[name]
+        if hasattr(ca, "codes"):
+            assert ca.vocab == cb.vocab
+            assert torch.equal(ca.codes.cpu(), cb.codes.cpu())
+        else:
+            assert torch.equal(ca.valid.cpu(), cb.valid.cpu()), name
+            if same_dtype:
+                assert ca.values.dtype == cb.values.dtype
+            assert torch.equal(ca.values.cpu().to(torch.float64), cb.values.cpu().to(torch.float64)), name
+
+
+@pytest.mark.parametrize("rg", [37, 1000])
+def test_columnar_parquet_equals_pandas_path_cpu(tmp_path, monkeypatch, rg):
+    path = str(tmp_path / "t.parquet")
+    _frame(300).to_parquet(path, row_group_size=rg)
+    fast = _read(path, "cpu", True, monkeypatch)
+    slow = _read(path, "cpu", False, monkeypatch)
+    _compare(fast, slow)
+
+
+def test_columnar_falls_back_for_uncovered_types(tmp_path, monkeypatch):
+    from transmogrifai_amd.readers.columnar import parquet_dataset
+    path = str(tmp_path / "t.parquet")
+    df = _frame(50)
+    df["b"] = df["y"] > 0.5
+    df.to_parquet(path)
+    assert parquet_dataset(path, [FeatureBuilder.Binary("b").as_predictor()], "cpu") is None
+    ds = DataReaders.Simple.parquet(path).generate_dataset([FeatureBuilder.Binary("b").as_predictor()])
+    assert ds["b"].to_list() == list(df["b"])
+
+
+@pytest.mark.gpu
+def test_columnar_parquet_equals_pandas_path_gpu(tmp_path, monkeypatch):
+    path = str(tmp_path / "t.parquet")
+    _frame(5000, seed=3).to_parquet(path, row_group_size=777)
+    fast = _read(path, "cuda", True, monkeypatch)
+    slow = _read(path, "cuda", False, monkeypatch)
+    assert fast["r32"].values.dtype == torch.float32 and fast["r32"].values.is_cuda
+    _compare(fast, slow, same_dtype=False)
+
+
+def test_dataset_to_parquet_round_trip(tmp_path, monkeypatch):
+    from transmogrifai_amd.readers.columnar import dataset_to_parquet
+    path = str(tmp_path / "t.parquet")
+    _frame(300, seed=5).to_parquet(path, row_group_size=64)
+    ds = _read(path, "cpu", True, monkeypatch)
+    out = str(tmp_path / "o.parquet")
+    dataset_to_parquet(ds, out, row_group_rows=100)
+    monkeypatch.setenv("TMOG_COLUMNAR", "1")
+    back = DataReaders.Simple.parquet(out).generate_dataset(_features())
+    ds.key = None
+    _compare(back, ds)

@@ -29,7 +29,7 @@ def column_from_series(ftype, series, device) -> Column:
             valid = vals.notna().to_numpy()
             arr = vals.fillna(False).astype(bool).to_numpy()
             return NumericColumn(ftype, torch.as_tensor(arr, device=device), torch.as_tensor(valid, device=device))
-        if np.issubdtype(series.dtype, np.datetime64):
+        if pd.api.types.is_datetime64_any_dtype(series.dtype):
             valid = series.notna().to_numpy()
             arr = series.astype("int64").to_numpy() // 1_000_000
             return NumericColumn(ftype, torch.as_tensor(arr, device=device), torch.as_tensor(valid, device=device))

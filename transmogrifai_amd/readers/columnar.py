@@ -1,0 +1,278 @@
+"""Columnar Parquet -> device ingest (the fast path of :class:`~.files.ParquetReader`).
+
+Reference: ``ParquetProductReader.scala:47-90`` / ``DataReader.generateDataFrame`` (``DataReader.scala:57-198``)
+read Parquet into a Spark DataFrame of one column per raw feature. The generic path here (:mod:`.base`) goes
+through a pandas DataFrame and converts each column on the host (``to_numeric``, ``fillna``, float64), then
+copies it to the device -- at 10M x 200 that is tens of seconds of single-threaded host work.
+
+This path keeps the data in Arrow's columnar buffers end to end:
+
+* row groups are decoded by pyarrow's multi-threaded C++ reader, the next one on a prefetch thread while the
+  current one is copied;
+* each numeric column chunk is copied as its raw value buffer (float32 stays float32 on the GPU -- the
+  precision the GPU vectorizers run at) and, when it has nulls, its packed validity bitmap (1 bit per row);
+  the chunks of a row group are packed into one pinned host buffer (memcpys on a thread pool) and sent with one
+  asynchronous host-to-device copy on a copy stream, double-buffered against the next row group's packing;
+* on the device the bitmaps are unpacked, null slots zeroed (the pandas path's ``fillna(0)``) and the values
+  scattered into the preallocated columns;
+* text columns are dictionary-encoded by Arrow (first-appearance order and -1 for null, exactly
+  ``pandas.factorize``), integral columns keep int64.
+
+Columns the fast path does not cover (custom extract functions, Binary / date types, text stored as
+non-strings, integral stored as floats) make :func:`parquet_dataset` return ``None`` and the reader falls back
+to the pandas path. ``tests/test_columnar_ingest.py`` checks both paths give identical datasets."""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+from collections import OrderedDict
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..data.columns import NumericColumn, TextColumn
+from ..data.dataset import Dataset
+from ..features import types as T
+
+
+def _plan(schema, raw_features):
+    """``[(feature, column, kind)]`` with kind in {"real", "int", "text"}, or None if any feature needs the
+    generic path."""
+    import pyarrow as pa
+    out = []
+    for f in raw_features:
+        st = f.origin_stage
+        if st.extract_fn is not None or st.column is None or st.column not in schema.names:
+            return None
+        at = schema.field(st.column).type
+        ft = f.wtype
+        if ft.kind == "numeric":
+            if issubclass(ft, T.Binary) or not (pa.types.is_floating(at) or pa.types.is_integer(at)):
+                return None
+            if issubclass(ft, T.Integral):
+                if not pa.types.is_integer(at):
+                    return None
+                out.append((f, st.column, "int"))
+            else:
+                out.append((f, st.column, "real"))
+        elif ft.kind == "text":
+            vt = at.value_type if pa.types.is_dictionary(at) else at
+            if not (pa.types.is_string(vt) or pa.types.is_large_string(vt)):
+                return None
+            out.append((f, st.column, "text"))
+        else:
+            return None
+    return out
+
+
+def _real_dtype(at, dev):
+    import pyarrow as pa
+    if dev.type == "cuda" and pa.types.is_float32(at):
+        return torch.float32
+    return torch.float64
+
+
+def _bitmap_bytes(n):
+    return (n + 7) // 8
+
+
+class _Slot:
+    """One pinned staging buffer, the device buffer it is copied into, and the event that marks the copy done."""
+
+    def __init__(self, nbytes, dev):
+        self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        self.event = None
+
+
+def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads: Optional[int] = None
+                    ) -> Optional[Dataset]:
+    """Dataset of ``raw_features`` from the Parquet file ``path`` on ``dev``, or None (use the generic path)."""
+    try:
+        import pyarrow as pa
+        import pyarrow.compute as pc
+        import pyarrow.parquet as pq
+    except ImportError:
+        return None
+    if key_fn is not None:
+        return None
+    dev = torch.device(dev)
+    pf = pq.ParquetFile(path)
+    schema = pf.schema_arrow
+    plan = _plan(schema, raw_features)
+    if plan is None:
+        return None
+    n = pf.metadata.num_rows
+    num = [(f, c, k) for f, c, k in plan if k in ("real", "int")]
+    txt = [(f, c, k) for f, c, k in plan if k == "text"]
+    ncols = list(dict.fromkeys(c for _, c, _ in num))
+    types = {c: schema.field(c).type for c in ncols}
+    dtype = {c: (torch.int64 if any(k == "int" and cc == c for _, cc, k in num) else _real_dtype(types[c], dev))
+             for c in ncols}
+    vals = {c: torch.empty(n, dtype=dtype[c], device=dev) for c in ncols}
+    valid = {c: None for c in ncols}
+    gpu = dev.type == "cuda"
+    threads = threads or min(16, os.cpu_count() or 4)
+    pool = cf.ThreadPoolExecutor(threads)
+    prefetch = cf.ThreadPoolExecutor(1)
+    n_rg = pf.metadata.num_row_groups
+
+    def read(i):
+        return pf.read_row_group(i, columns=ncols, use_threads=True) if ncols else None
+
+    def host_chunk(arr, c):
+        """(values ndarray in the column's device dtype, validity bitmap bytes or None, bit offset)."""
+        want = dtype[c]
+        npd = {torch.float32: np.float32, torch.float64: np.float64, torch.int64: np.int64}[want]
+        bufs = arr.buffers()
+        v = np.frombuffer(bufs[1], dtype=arr.type.to_pandas_dtype(), count=len(arr) + arr.offset)[arr.offset:]
+        if v.dtype != npd:
+            v = v.astype(npd)
+        bm = None
+        if arr.null_count > 0:
+            bm = np.frombuffer(bufs[0], dtype=np.uint8, count=_bitmap_bytes(len(arr) + arr.offset))
+        return v, bm, arr.offset
+
+    slots: List[Optional[_Slot]] = [None, None]
+    copy_stream = torch.cuda.Stream(device=dev) if gpu else None
+    fut = prefetch.submit(read, 0) if n_rg else None
+    row0 = 0
+    try:
+        for g in range(n_rg):
+            tab = fut.result()
+            fut = prefetch.submit(read, g + 1) if g + 1 < n_rg else None
+            rows = tab.num_rows
+            pieces = []                  # (column, row offset, values ndarray, bitmap, bit offset)
+            for c in ncols:
+                r = row0
+                for ch in tab.column(c).chunks:
+                    pieces.append((c, r) + host_chunk(ch, c))
+                    r += len(ch)
+            if not gpu:
+                for c, r, v, bm, bo in pieces:
+                    dst = vals[c][r:r + len(v)]
+                    dst.copy_(torch.from_numpy(v))
+                    if bm is not None:
+                        ok = torch.from_numpy(np.unpackbits(bm, bitorder="little")[bo:bo + len(v)].astype(bool))
+                        if valid[c] is None:
+                            valid[c] = torch.ones(n, dtype=torch.bool)
+                        valid[c][r:r + len(v)] = ok
+                        dst.masked_fill_(~ok, 0)
+                row0 += rows
+                continue
+            # pack the row group into one pinned buffer (8-byte aligned pieces), one async H2D copy
+            layout, off = [], 0
+            for c, r, v, bm, bo in pieces:
+                vo = off
+                off += (v.nbytes + 7) // 8 * 8
+                bmo = None
+                if bm is not None:
+                    bmo = off
+                    off += (bm.nbytes + 7) // 8 * 8
+                layout.append((c, r, v, bm, bo, vo, bmo))
+            k = g & 1
+            s = slots[k]
+            if s is None or s.host.numel() < off:
+                if s is not None and s.event is not None:
+                    s.event.synchronize()
+                s = slots[k] = _Slot(max(off, 1), dev)
+            elif s.event is not None:
+                s.event.synchronize()          # the copy of row group g - 2 has left this buffer
+            hb = s.host.numpy()
+
+            def pack(item):
+                c, r, v, bm, bo, vo, bmo = item
+                hb[vo:vo + v.nbytes] = v.view(np.uint8)
+                if bm is not None:
+                    hb[bmo:bmo + bm.nbytes] = bm
+
+            list(pool.map(pack, layout))
+            with torch.cuda.stream(copy_stream):
+                s.dev[:off].copy_(s.host[:off], non_blocking=True)
+                for c, r, v, bm, bo, vo, bmo in layout:
+                    m = len(v)
+                    src = s.dev[vo:vo + v.nbytes].view(vals[c].dtype)
+                    dst = vals[c][r:r + m]
+                    if bm is None:
+                        dst.copy_(src)
+                    else:
+                        bits = s.dev[bmo:bmo + bm.nbytes]
+                        ok = ((bits[:, None] >> torch.arange(8, device=dev, dtype=torch.uint8)) & 1).reshape(-1)
+                        ok = ok[bo:bo + m].bool()
+                        if valid[c] is None:
+                            valid[c] = torch.ones(n, dtype=torch.bool, device=dev)
+                        valid[c][r:r + m] = ok
+                        dst.copy_(torch.where(ok, src, torch.zeros_like(src)))
+                s.event = torch.cuda.Event()
+                s.event.record(copy_stream)
+            row0 += rows
+        if gpu:
+            torch.cuda.current_stream(dev).wait_stream(copy_stream)
+            for c in ncols:            # allocated on the caller's stream, written on the copy stream
+                vals[c].record_stream(copy_stream)
+                if valid[c] is not None:
+                    valid[c].record_stream(copy_stream)
+            for s in slots:
+                if s is not None and s.event is not None:
+                    s.event.synchronize()
+    finally:
+        pool.shutdown(wait=False)
+        prefetch.shutdown(wait=False)
+    cols = OrderedDict()
+    for f, c, k in plan:
+        if k == "text":
+            continue
+        ok = valid[c]
+        if not f.wtype.nullable and ok is not None and not bool(ok.all()):
+            raise T.NonNullableEmptyException(f"{f.wtype.__name__} column '{c}' contains empty values")
+        cols[f.name] = NumericColumn(f.wtype, vals[c], ok)
+    if txt:
+        tt = pf.read(columns=list(dict.fromkeys(c for _, c, _ in txt)), use_threads=True)
+        enc = {}
+        for f, c, _ in txt:
+            if c not in enc:
+                arr = tt.column(c).combine_chunks()
+                if pa.types.is_dictionary(arr.type):       # written dictionary-encoded: decode, re-encode in order
+                    arr = arr.cast(arr.type.value_type)
+                d = pc.dictionary_encode(arr)
+                codes = pc.fill_null(d.indices, -1).to_numpy(zero_copy_only=False).astype(np.int32)
+                enc[c] = (torch.as_tensor(codes, device=dev), [str(u) for u in d.dictionary.to_pylist()])
+            cols[f.name] = TextColumn(f.wtype, *enc[c])
+    order = OrderedDict((f.name, cols[f.name]) for f in raw_features)
+    key = None
+    if "key" in schema.names:
+        key = pf.read(columns=["key"]).column("key").to_pandas().astype(str).to_numpy(dtype=object)
+    return Dataset(order, key, n)
+
+
+def dataset_to_parquet(ds: Dataset, path: str, row_group_rows: int = 1 << 20, names: Optional[Sequence[str]] = None,
+                       compression: str = "snappy") -> None:
+    """Write the numeric and text columns of ``ds`` (nulls kept) to a Parquet file, one row group per
+    ``row_group_rows`` rows, streaming from the device one row group at a time. Text columns are written
+    dictionary-encoded. Used by ``bench.py --ingest parquet`` to put the benchmark table on disk."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    names = list(names) if names is not None else list(ds.columns)
+    writer = None
+    try:
+        for r0 in range(0, ds.n_rows, row_group_rows):
+            r1 = min(ds.n_rows, r0 + row_group_rows)
+            arrays = []
+            for nm in names:
+                c = ds[nm]
+                if isinstance(c, TextColumn):
+                    codes = c.codes[r0:r1].cpu().numpy().astype(np.int32)
+                    arrays.append(pa.DictionaryArray.from_arrays(pa.array(codes, mask=codes < 0),
+                                                                 pa.array(c.vocab, type=pa.string())))
+                else:
+                    v = c.values[r0:r1].cpu().numpy()
+                    ok = c.valid[r0:r1].cpu().numpy()
+                    arrays.append(pa.array(v, mask=None if ok.all() else ~ok))
+            tab = pa.Table.from_arrays(arrays, names=names)
+            if writer is None:
+                writer = pq.ParquetWriter(path, tab.schema, compression=compression)
+            writer.write_table(tab, row_group_size=r1 - r0)
+    finally:
+        if writer is not None:
+            writer.close()

@@ -57,10 +57,25 @@ class ParquetReader(DataReader):
         super().__init__(key, device)
         self.path = path
 
+    def _path(self, params):
+        return params.path if (params is not None and getattr(params, "path", None)) else self.path
+
     def read_frame(self, params=None):
         import pandas as pd
-        path = params.path if (params is not None and getattr(params, "path", None)) else self.path
-        return pd.read_parquet(path)
+        return pd.read_parquet(self._path(params))
+
+    def generate_dataset(self, raw_features, params=None):
+        """Columnar fast path (readers/columnar.py: Arrow buffers -> pinned row-group copies -> device) when
+        every raw feature is a plain numeric / string column; the pandas path otherwise (TMOG_COLUMNAR=0)."""
+        import os
+        from ..config import default_device
+        path = self._path(params)
+        if os.environ.get("TMOG_COLUMNAR", "1") != "0" and isinstance(path, str) and os.path.isfile(path):
+            from .columnar import parquet_dataset
+            ds = parquet_dataset(path, raw_features, self.device or default_device(), self.key_fn)
+            if ds is not None:
+                return ds
+        return super().generate_dataset(raw_features, params)
 
 
 class AvroReader(DataReader):
