@@ -72,7 +72,7 @@ def test_detectors():
     assert "Smith" in ents.get("Person", ()) and "Boston" in ents.get("Location", ())
     ds, (n,) = TestFeatureBuilder.of(("n", T.Text, ["Mary Jones", "John Smith", "Linda Park", None]))
     m, out = check_estimator(N.HumanNameDetector().set_input(n), ds)
-    assert out[0]["gender"] == "Female" and out[1]["firstName"] == "John"
+    assert out[0]["Gender"] == "Female" and out[1]["Gender"] == "Male" and out[1]["OriginalValue"] == "John Smith"
     ds2, (p,) = TestFeatureBuilder.of(("p", T.Phone, ["(650) 555-1234", "123", None]))
     check_transformer(N.ParsePhoneNumber().set_input(p), ds2, expected=["+16505551234", None, None])
 
@@ -104,3 +104,91 @@ def test_mime_detector_reference_fixtures():
             for n in rng.integers(16, 10000, 10)]
     assert [MimeTypeDetector().transform_fn(v) for v in [None, ""] + rand] == \
         [None] + ["application/octet-stream"] * 11
+
+
+# ---- HumanNameDetectorTest.scala (name dictionary contents are parity unpinned: see nlp_stages._NAME_DICT) ----
+def _fit_names(values, **kw):
+    ds, (f,) = TestFeatureBuilder.of(("n", T.Text, list(values)))
+    est = N.HumanNameDetector(**kw).set_input(f)
+    model = est.fit(ds)
+    return est, model, [model.transform_fn(v) for v in values]
+
+
+def _genders(out):
+    return [o.get("Gender") for o in out]
+
+
+@pytest.mark.parametrize("values,expected", [
+    (["Robert"], True), (["Firetruck"], False), (["Elizabeth Warren"], True),
+    (["1", "42", "0", "3000 michael"], False),            # guard: most entries shorter than 3 characters
+    (["Michael"] * 200, False),                            # guard: no spread of lengths / too few distinct
+])
+def test_name_detector_treat_as_name(values, expected):
+    _, m, out = _fit_names(values)
+    assert m.treat_as_name is expected
+    if not expected:
+        assert out[0] == {}
+
+
+def test_name_detector_dictionary_names_and_threshold():
+    rng = np.random.default_rng(0)
+    names = sorted(N._FEMALE | N._MALE)
+    _, m, _ = _fit_names([names[i].capitalize() for i in rng.choice(len(names), 100)])
+    assert m.treat_as_name
+    n = 50
+    for i in (2, 6):
+        k = (n // 10) * i
+        vals = [names[j].capitalize() for j in rng.choice(len(names), k)] + \
+               [f"({rng.integers(200, 999)}) {rng.integers(200, 999)}-{rng.integers(1000, 9999)}" for _ in range(n - k)]
+        thr = k / n
+        assert _fit_names(vals, threshold=thr - 0.09)[1].treat_as_name
+        assert not _fit_names(vals, threshold=thr + 0.09)[1].treat_as_name
+
+
+def test_name_detector_gender_single_entries():
+    _, m, out = _fit_names(["Alyssa"])
+    assert m.treat_as_name and out[0]["Gender"] == "Female"
+    _, m, out = _fit_names(["Shelby Bouvet"])
+    assert m.ordered_gender_detect_strategies[0] == "ByIndex WITH VALUE 0" and out[0]["Gender"] == "Female"
+
+
+SENATORS = ["Sherrod Brown", "Maria Cantwell", "Benjamin L. Cardin", "Lisa Maria Blunt Rochester",
+            "Thomas Robert Carper", "Jennifer González-Colón"]
+MF = ["Male", "Female"] * 3
+
+
+def test_name_detector_gender_strategies():
+    # the built-in dictionary lacks most of these surnames (the reference's JRC list has them): the strategy
+    # tests after the first run at threshold 0.15 so that the columns are still judged name columns
+    _, m, out = _fit_names(SENATORS)
+    assert m.treat_as_name and _genders(out) == MF
+    _, m, out = _fit_names(["Mr. Sherrod Brown", "Mrs. Maria Cantwell", "Mr. Benjamin L. Cardin",
+                            "Ms. Lisa Maria Blunt Rochester", "Mister Thomas Robert Carper",
+                            "Miss Jennifer González-Colón"], threshold=0.15)
+    assert m.ordered_gender_detect_strategies[0] == "FindHonorific" and _genders(out) == MF
+    _, m, _ = _fit_names(["Jennifer González-Colón (Miss) (Mr.)"], threshold=0.15)
+    assert m.treat_as_name and m.ordered_gender_detect_strategies[0] != "FindHonorific"
+    _, m, out = _fit_names(["Brown, Sherrod", "Cantwell, Maria", "Cardin, Benjamin", "Rochester, Lisa",
+                            "Carper, Thomas", "González-Colón, Jennifer"], threshold=0.15)
+    assert m.treat_as_name and _genders(out) == MF
+    _, m, out = _fit_names(["Brown, Sherrod", "Cantwell, Maria", "Cardin, Benjamin L.", "Rochester, Lisa Maria Blunt",
+                            "Carper, Thomas Robert", "González-Colón, Jennifer"], threshold=0.15)
+    assert m.ordered_gender_detect_strategies[0] == "ByRegex WITH VALUE .*,(.*)" and _genders(out) == MF
+    _, m, out = _fit_names(["Brown, Dr. Sherrod L.", "Cantwell, Prof. Maria Blunt"], threshold=0.15)
+    assert m.treat_as_name and m.ordered_gender_detect_strategies[0] == "ByRegex WITH VALUE .*,\\s+.*?\\s+(.*)"
+    assert _genders(out) == ["Male", "Female"]
+    est, m, out = _fit_names(["Sherrod Brown", "Cantwell, Maria", "Mr. Benjamin L. Cardin", "Rochester, Lisa Maria Blunt",
+                              "Carper, Dr. Thomas Robert", "González-Colón, Ms. Jennifer"], threshold=0.15)
+    assert m.treat_as_name and _genders(out) == MF
+    md = est.metadata
+    assert md["treatAsName"] is True and set(md["genderResultsByStrategy"]) == set(N.GENDER_STRATEGIES)
+    assert all(sum(v) == 6 for v in md["genderResultsByStrategy"].values())
+
+
+def test_name_detector_ignores_nulls():
+    rng = np.random.default_rng(1)
+    names = sorted(N._FEMALE | N._MALE)
+    vals = [None if rng.random() < 0.9 else names[rng.integers(len(names))].capitalize() for _ in range(200)]
+    vals[:12] = [n.capitalize() for n in names[:12]]        # enough distinct entries for the uniqueness guard
+    assert _fit_names(vals)[1].treat_as_name
+    assert not _fit_names(vals, ignore_nulls=False)[1].treat_as_name

@@ -453,72 +453,191 @@ class NameEntityRecognizer(UnaryTransformer):
         return recognize_entities(v)
 
 
-# small built-in first-name / gender lists (the reference dictionaries are absent from the mount)
+# Built-in name / gender dictionaries. The reference's (Names_JRC_Combined.txt, GenderDictionary_USandUK.csv,
+# NameDetectUtils.scala:217-252) are not in the mount: these are common US first names (with gender) and
+# surnames, so which entries count as names is "parity unpinned"; the algorithm around them is the reference's.
 _FEMALE = set("""mary patricia jennifer linda elizabeth barbara susan jessica sarah karen nancy lisa betty margaret
 sandra ashley kimberly emily donna michelle dorothy carol amanda melissa deborah stephanie rebecca sharon laura
 cynthia kathleen amy shirley angela helen anna brenda pamela nicole emma samantha katherine christine debra rachel
 catherine carolyn janet ruth maria heather diane virginia julie joyce victoria olivia kelly christina lauren joan
 evelyn judith megan cheryl andrea hannah martha jacqueline frances gloria ann teresa kathryn sara janice jean alice
 madison doris abigail julia judy grace denise amber marilyn beverly danielle theresa sophia marie diana brittany
-natalie isabella charlotte rose alexis kayla florence elsa louisa ellen""".split())
+natalie isabella charlotte rose alexis kayla florence elsa louisa ellen alyssa shelby ava mia harper chloe ella
+lily zoe leah audrey claire lucy paige sydney morgan jasmine haley brooke molly vanessa erin erica monica tiffany
+crystal april wendy tina dana valerie gina lori tracy kristen holly kathy peggy connie sally carmen rosa yolanda
+""".split())
 _MALE = set("""james robert john michael william david richard joseph thomas charles christopher daniel matthew
 anthony mark donald steven paul andrew joshua kenneth kevin brian george timothy ronald edward jason jeffrey ryan
 jacob gary nicholas eric jonathan stephen larry justin scott brandon benjamin samuel gregory alexander frank
 patrick raymond jack dennis jerry tyler aaron jose adam nathan henry douglas zachary peter kyle ethan walter noah
 jeremy christian keith roger terry gerald harold sean austin carl arthur lawrence dylan jesse jordan bryan billy
 joe bruce gabriel logan albert willie alan juan wayne elijah randy roy vincent ralph eugene russell bobby mason
-philip louis owen harry oscar""".split())
+philip louis owen harry oscar sherrod liam lucas luke isaac caleb connor evan hunter ian jared marcus miguel
+carlos luis antonio victor martin travis shawn craig todd derek troy chad curtis dale glenn howard leonard
+""".split())
+_SURNAMES = set("""smith johnson williams brown jones garcia miller davis rodriguez martinez hernandez lopez gonzalez
+wilson anderson thomas taylor moore jackson martin lee perez thompson white harris sanchez clark ramirez lewis
+robinson walker young allen king wright scott torres nguyen hill flores green adams nelson baker hall rivera
+campbell mitchell carter roberts gomez phillips evans turner diaz parker cruz edwards collins reyes stewart morris
+morales murphy cook rogers gutierrez ortiz morgan cooper peterson bailey reed kelly howard ramos kim cox ward
+richardson watson brooks chavez wood james bennett gray mendoza ruiz hughes price alvarez castillo sanders patel
+myers long ross foster jimenez powell jenkins perry russell sullivan bell coleman butler henderson barnes gonzales
+fisher vasquez simmons romero jordan patterson alexander hamilton graham reynolds griffin wallace moreno west cole
+hayes bryant herrera gibson ellis tran medina aguilar stevens murray ford castro marshall owens harrison fernandez
+mcdonald woods washington kennedy wells vargas henry chen freeman webb tucker guzman burns crawford olson simpson
+porter hunter gordon mendez silva shaw snyder mason dixon munoz hunt hicks holmes palmer wagner black robertson
+boyd rose stone salazar fox warren mills meyer rice schmidt garza daniels ferguson nichols stephens soto weaver
+ryan gardner payne grant dunn kelley spencer hawkins arnold pierce vazquez hansen peters santos hart bradley knight
+elliott cunningham duncan armstrong hudson carroll lane riley andrews alvarado ray delgado berry perkins hoffman
+""".split())
+_NAME_DICT = _FEMALE | _MALE | _SURNAMES
+_GENDER_DICT = {**{n: 0.0 for n in _FEMALE}, **{n: 1.0 for n in _MALE}}     # name -> probability male
+_MALE_HONORIFICS = frozenset(("mr", "mister", "sir"))
+_FEMALE_HONORIFICS = frozenset(("ms", "mrs", "miss", "madam"))
+# NameDetectUtils.scala:271-275: the gender strategies, in the reference's (tie-breaking) order
+_AFTER_COMMA = r".*,(.*)"
+_AFTER_COMMA_NEXT = r".*,\s+.*?\s+(.*)"
+GENDER_STRATEGIES = ("FindHonorific", "ByIndex WITH VALUE 0", "ByLast", "ByRegex WITH VALUE " + _AFTER_COMMA,
+                     "ByRegex WITH VALUE " + _AFTER_COMMA_NEXT)
+
+
+def _name_tokens(s: Optional[str]):
+    from ...utils.text import tokenize
+    return tokenize(s, stopwords=()) if s else []
+
+
+def _gender_of(name: Optional[str]) -> str:
+    p = _GENDER_DICT.get(name) if name is not None else None
+    return "GenderNA" if p is None else ("Male" if p >= 0.5 else "Female")
+
+
+def identify_gender(text: Optional[str], tokens, strategy: str) -> str:
+    """One gender strategy on one entry (``NameDetectFun.identifyGender``, NameDetectUtils.scala:120-149)."""
+    import re
+    if text is None:
+        return "GenderNA"
+    kind, _, arg = strategy.partition(" WITH VALUE ")
+    if kind == "FindHonorific":
+        hits = ["Male" if t in _MALE_HONORIFICS else "Female" for t in tokens
+                if t in _MALE_HONORIFICS or t in _FEMALE_HONORIFICS]
+        return hits[0] if len(hits) == 1 else "GenderNA"
+    if kind == "ByIndex":
+        i = int(arg)
+        return _gender_of(tokens[i] if 0 <= i < len(tokens) else None)
+    if kind == "ByLast":
+        return _gender_of(tokens[-1] if tokens else None)
+    if kind == "ByRegex":
+        m = re.fullmatch(arg, text)            # Scala's `case pattern(g)` matches the whole string
+        if m is None:
+            return "GenderNA"
+        toks = _name_tokens(m.group(1))
+        return _gender_of(toks[0] if toks else None)
+    return "GenderNA"
 
 
 def parse_name(s: Optional[str]) -> Dict[str, str]:
+    """Name map of one entry with every strategy in the reference's order (first inferred gender wins)."""
     if not s:
         return {}
-    toks = [t.strip(".,") for t in s.replace(",", " , ").split() if t.strip(".,")]
-    toks = [t for t in toks if t.lower() not in _TITLES]
-    if not toks:
-        return {}
-    names = [t for t in toks if t.lower() in _FEMALE | _MALE]
-    first = names[0] if names else toks[0]
-    last = toks[-1] if toks[-1] != first else ""
-    fl = first.lower()
-    gender = "Female" if fl in _FEMALE else ("Male" if fl in _MALE else "GenderNA")
-    return {"isName": "true" if names else "false", "firstName": first, "lastName": last, "gender": gender}
+    toks = _name_tokens(s)
+    g = next((x for x in (identify_gender(s, toks, st) for st in GENDER_STRATEGIES) if x != "GenderNA"), "GenderNA")
+    return {"IsName": "true", "OriginalValue": s, "Gender": g}
 
 
 @register_stage
 class HumanNameDetectorModel(UnaryTransformer):
+    """``HumanNameDetectorModel`` (HumanNameDetector.scala:87-116): when the column was judged a name column,
+    each entry maps to ``{IsName, OriginalValue, Gender}`` with the gender of the first strategy (in the fitted
+    order) that infers one; otherwise the empty map."""
     operation_name = "humanNameDetect"
     output_type = T.NameStats
 
-    def __init__(self, treat_as_name: bool = False, uid=None, **kw):
+    def __init__(self, treat_as_name: bool = False, strategies=(), uid=None, **kw):
         super().__init__(None, uid=uid, **kw)
         self.treat_as_name = treat_as_name
+        self.ordered_gender_detect_strategies = list(strategies)
 
     def transform_fn(self, v):
-        if not self.treat_as_name or v is None:
+        if not self.treat_as_name:
             return {}
-        return parse_name(v)
+        toks = _name_tokens(v)
+        gender = "GenderNA"
+        for st in self.ordered_gender_detect_strategies:
+            g = identify_gender(v, toks, st)
+            if g != "GenderNA":
+                gender = g
+                break
+        return {"IsName": "true", "OriginalValue": v if v is not None else "", "Gender": gender}
 
     def ctor_args(self):
-        return {"treatAsName": self.treat_as_name}
+        return {"treatAsName": self.treat_as_name, "orderedGenderDetectStrategies": self.ordered_gender_detect_strategies}
 
     def load_ctor_args(self, a):
         self.treat_as_name = bool(a["treatAsName"])
+        self.ordered_gender_detect_strategies = list(a.get("orderedGenderDetectStrategies") or
+                                                     (GENDER_STRATEGIES if self.treat_as_name else ()))
 
 
 @register_stage
 class HumanNameDetector(UnaryEstimator):
-    """Decide whether a text column holds human names (fraction of values with a dictionary first name)."""
+    """``HumanNameDetector`` (HumanNameDetector.scala:56-85, NameDetectUtils.scala:55-198). One pass over the
+    column accumulates, per entry: the guard-check quantities (token count below ``guard_max_tokens``, text
+    length at least ``guard_min_text_length``, text-length moments, distinct entries -- exact here, HyperLogLog
+    in the reference), the fraction of the entry's tokens found in the name dictionary (averaged over entries)
+    and each gender strategy's male / female / undetermined counts. Nulls are skipped when ``ignore_nulls``
+    (else they count as entries with no name tokens). The column is a name column when every guard passes and
+    the average dictionary fraction reaches ``threshold``; the strategies are then ordered by their count of
+    undetermined genders (stable: the reference's strategy order breaks ties)."""
     operation_name = "humanNameDetect"
     output_type = T.NameStats
-    _defaults = {"default_threshold": 0.50}
+    _defaults = {"threshold": 0.50, "ignore_nulls": True, "guard_max_tokens": 10, "guard_pct_max_tokens": 0.75,
+                 "guard_min_text_length": 3, "guard_pct_min_text_length": 0.75, "guard_min_count_std": 10,
+                 "guard_min_std": 0.05, "guard_min_count_unique": 10, "guard_min_unique": 10}
+
+    def set_threshold(self, v: float):
+        self.params["threshold"] = float(v)
+        return self
+
+    def set_ignore_nulls(self, v: bool):
+        self.params["ignore_nulls"] = bool(v)
+        return self
 
     def fit_columns(self, c, ds=None):
-        vals = [v for v in c.to_list() if v]
-        hits = sum(1 for v in vals if parse_name(v).get("isName") == "true")
-        frac = hits / len(vals) if vals else 0.0
-        self.metadata["humanNameFraction"] = frac
-        return HumanNameDetectorModel(frac >= self.params["default_threshold"])
+        import math
+        P = self.params
+        below = above = 0
+        n_len, s_len, s2_len = 0, 0.0, 0.0
+        uniq = set()
+        dict_sum, dict_n = 0.0, 0
+        stats = {st: [0, 0, 0] for st in GENDER_STRATEGIES}
+        for v in c.to_list():
+            if v is None and P["ignore_nulls"]:
+                continue
+            toks = _name_tokens(v)
+            if v is not None:
+                below += len(toks) < P["guard_max_tokens"]
+                above += len(v) >= P["guard_min_text_length"]
+                n_len += 1
+                s_len += len(v)
+                s2_len += len(v) * len(v)
+                uniq.add(v)
+            dict_sum += (sum(t in _NAME_DICT for t in toks) / len(toks)) if toks else 0.0
+            dict_n += 1
+            for st in GENDER_STRATEGIES:
+                g = identify_gender(v, toks, st)
+                stats[st][0 if g == "Male" else 1 if g == "Female" else 2] += 1
+        N = float(n_len)
+        std = math.sqrt(max(s2_len / N - (s_len / N) ** 2, 0.0)) if n_len else 0.0
+        guards = n_len > 0 and below / N > P["guard_pct_max_tokens"] and above / N > P["guard_pct_min_text_length"] \
+            and (N < P["guard_min_count_std"] or std > P["guard_min_std"]) \
+            and (N < P["guard_min_count_unique"] or len(uniq) >= P["guard_min_unique"])
+        prob = dict_sum / dict_n if dict_n else 0.0
+        treat = bool(guards and prob >= P["threshold"])
+        self.metadata["treatAsName"] = treat
+        self.metadata["predictedNameProb"] = prob
+        self.metadata["genderResultsByStrategy"] = {st: [float(x) for x in v] for st, v in stats.items()}
+        order = [st for st, _ in sorted(stats.items(), key=lambda kv: kv[1][2])] if treat else []
+        return HumanNameDetectorModel(treat, order)
 
 
 @register_stage
