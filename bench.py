@@ -335,4 +335,5 @@ def _timed(args, one_run, expected_configs, use_gpu, dev, torch, D, sim, n_raw, 
 
 
 if __name__ == "__main__":
-    main()
+    from transmogrifai_amd.utils.device_errors import run_main
+    run_main(main, "bench.py")

@@ -92,3 +92,51 @@ def test_dataset_to_parquet_round_trip(tmp_path, monkeypatch):
     back = DataReaders.Simple.parquet(out).generate_dataset(_features())
     ds.key = None
     _compare(back, ds)
+
+
+def _write_nan_table(path, n=500, seed=7):
+    """A file whose float columns hold non-null NaNs (written with from_pandas=False: Spark / Arrow writers keep
+    NaN apart from null), plus real nulls in another column."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    rng = np.random.default_rng(seed)
+    r64 = rng.standard_normal(n)
+    r64[rng.random(n) < 0.1] = np.nan
+    r32 = rng.standard_normal(n).astype(np.float32)
+    r32[5] = np.nan
+    nulls = rng.random(n) < 0.2
+    rnull = pa.array(np.where(nulls, 0.0, rng.standard_normal(n)), mask=nulls)
+    tab = pa.table({"r64": pa.array(r64, from_pandas=False), "r32": pa.array(r32, from_pandas=False),
+                    "rnull": rnull, "y": pa.array((rng.random(n) < 0.5).astype(np.float64))})
+    assert tab.column("r64").null_count == 0 and tab.column("rnull").null_count > 0
+    pq.write_table(tab, path, row_group_size=128)
+    return r64, r32
+
+
+def _nan_features():
+    return [FeatureBuilder.Real("r64").as_predictor(), FeatureBuilder.Real("r32").as_predictor(),
+            FeatureBuilder.Real("rnull").as_predictor(), FeatureBuilder.RealNN("y").as_response()]
+
+
+def _check_nan_read(path, dev, monkeypatch, r64, r32):
+    monkeypatch.setenv("TMOG_COLUMNAR", "1")
+    fast = DataReaders.Simple.parquet(path, device=dev).generate_dataset(_nan_features())
+    monkeypatch.setenv("TMOG_COLUMNAR", "0")
+    slow = DataReaders.Simple.parquet(path, device=dev).generate_dataset(_nan_features())
+    _compare(fast, slow, same_dtype=False)
+    assert torch.equal(fast["r64"].valid.cpu(), torch.from_numpy(~np.isnan(r64)))
+    assert not bool(torch.isnan(fast["r64"].values).any()) and not bool(torch.isnan(fast["r32"].values).any())
+    assert not bool(fast["r32"].valid[5])
+
+
+def test_columnar_parquet_non_null_nan_is_missing_cpu(tmp_path, monkeypatch):
+    path = str(tmp_path / "nan.parquet")
+    r64, r32 = _write_nan_table(path)
+    _check_nan_read(path, "cpu", monkeypatch, r64, r32)
+
+
+@pytest.mark.gpu
+def test_columnar_parquet_non_null_nan_is_missing_gpu(tmp_path, monkeypatch):
+    path = str(tmp_path / "nan.parquet")
+    r64, r32 = _write_nan_table(path)
+    _check_nan_read(path, "cuda", monkeypatch, r64, r32)

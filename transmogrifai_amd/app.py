@@ -49,7 +49,8 @@ class OpApp:
         cfg = parse_args(sys.argv[1:] if argv is None else argv, self.app_name)
         params = cfg.to_op_params()
         cfg.validate(params)
-        return self.run(cfg.run_type, params)
+        from .utils.device_errors import run_main
+        return run_main(lambda: self.run(cfg.run_type, params), self.app_name)
 
 
 class OpAppWithRunner(OpApp):

@@ -490,10 +490,10 @@ def _recognize_entities(self):
 
 
 @register(T.Text, "identify_if_human_name")
-def _identify_human_name(self, default_threshold: float = 0.5):
-    """``RichTextFeature.identifyIfHumanName`` -> NameStats."""
+def _identify_human_name(self, threshold: float = 0.5):
+    """``RichTextFeature.identifyIfHumanName(threshold)`` -> NameStats (``RichTextFeature.scala:456-457``)."""
     from ..stages.feature.nlp_stages import HumanNameDetector
-    return HumanNameDetector(default_threshold=default_threshold).set_input(self).get_output()
+    return HumanNameDetector(threshold=threshold).set_input(self).get_output()
 
 
 @register(T.Phone, "parse_phone_default_country")

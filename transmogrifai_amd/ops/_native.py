@@ -160,6 +160,18 @@ def host():
     return _host
 
 
+def _release_torch_cache():
+    """Native out-of-memory handler (called from a grower thread, GIL taken by ctypes)."""
+    try:
+        torch.cuda.empty_cache()
+    except Exception:  # noqa: BLE001 - a handler must not unwind into native code
+        pass
+
+
+_OOM_HANDLER_T = C.CFUNCTYPE(None)
+_OOM_HANDLER = _OOM_HANDLER_T(_release_torch_cache)      # module-level: must outlive the library's use of it
+
+
 def hip():
     global _hip
     if _hip is None:
@@ -174,6 +186,13 @@ def hip():
                 dbg = int(os.environ.get("TMOG_HIST_DEBUG", "0"))
                 if dbg:
                     lib.tmog_hip_debug_flags(dbg)
+                # one device-memory budget: a native buffer growth that runs out of memory first returns
+                # torch's cached-but-unused blocks to the device, then retries (ops/csrc/hip/dev_alloc.hpp)
+                lib.tmog_hip_set_oom_handler.argtypes = [_OOM_HANDLER_T]
+                lib.tmog_hip_set_oom_handler.restype = None
+                lib.tmog_hip_set_oom_handler(_OOM_HANDLER)
+                lib.tmog_hip_fail_alloc.argtypes = [C.c_long]
+                lib.tmog_hip_fail_alloc.restype = None
                 _hip = lib
     return _hip
 

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "common/tree_grow.hpp"
+#include "hip/dev_alloc.hpp"
 
 extern "C" {
 int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
@@ -113,29 +114,35 @@ struct GpuBackend {
   int group;
   GpuBackend(GpuSlot& s, const tmog::GrowArgs& args, int g) : sl(s), a(args), group(g) {}
 
+  // grow-only device buffers: dev_alloc.hpp (a failed growth leaves the buffer empty, never a stale capacity)
   static void grow_dev(uint8_t*& p, size_t& cap, size_t need, hipStream_t s) {
-    if (need <= cap) return;
-    if (p) hchk(hipFreeAsync(p, s), "hipFreeAsync");
-    cap = need + need / 2 + 4096;
-    hchk(hipMallocAsync((void**)&p, cap, s), "hipMallocAsync");
+    tmog::grow_device(p, cap, need, need + need / 2 + 4096, s);
   }
   static void grow_pin(uint8_t*& p, size_t& cap, size_t need, hipStream_t s) {
-    if (need <= cap) return;
+    if (need <= cap && p != nullptr) return;
     if (p) {
       hchk(hipStreamSynchronize(s), "sync before pinned realloc");
-      hchk(hipHostFree(p), "hipHostFree");
+      hipError_t e = hipHostFree(p);
+      p = nullptr;
+      cap = 0;
+      hchk(e, "hipHostFree");
     }
-    cap = need + need / 2 + 4096;
-    hchk(hipHostMalloc((void**)&p, cap, hipHostMallocDefault), "hipHostMalloc");
+    const size_t nc = need + need / 2 + 4096;
+    hchk(hipHostMalloc((void**)&p, nc, hipHostMallocDefault), "hipHostMalloc");
+    cap = nc;
   }
   const int32_t* all_features(int F) {
     if (sl.feats_n < F) {
-      if (sl.feats) hchk(hipFreeAsync(sl.feats, sl.stream), "hipFreeAsync");
+      uint8_t* p = reinterpret_cast<uint8_t*>(sl.feats);
+      size_t cap = sl.feats ? sizeof(int32_t) * (size_t)sl.feats_n : 0;
+      sl.feats = nullptr;
+      sl.feats_n = 0;
+      tmog::grow_device(p, cap, sizeof(int32_t) * (size_t)F, sizeof(int32_t) * (size_t)F, sl.stream);
       std::vector<int32_t> h(F);
       for (int i = 0; i < F; ++i) h[i] = i;
-      hchk(hipMallocAsync((void**)&sl.feats, sizeof(int32_t) * F, sl.stream), "hipMallocAsync");
-      hchk(hipMemcpyAsync(sl.feats, h.data(), sizeof(int32_t) * F, hipMemcpyHostToDevice, sl.stream), "copy feats");
+      hchk(hipMemcpyAsync(p, h.data(), sizeof(int32_t) * F, hipMemcpyHostToDevice, sl.stream), "copy feats");
       hchk(hipStreamSynchronize(sl.stream), "sync feats");
+      sl.feats = reinterpret_cast<int32_t*>(p);
       sl.feats_n = F;
     }
     return sl.feats;
@@ -213,10 +220,15 @@ struct GpuBackend {
     const char* fr_env = std::getenv("TMOG_FUSED_REDUCE");      // read per call: A/B within one process
     const bool fused_reduce = !(fr_env && fr_env[0] == '0');
     if (fused_reduce && sl.done_cap < (size_t)m) {     // grow-only, zeroed; the kernels leave it zeroed
-      if (sl.done) hchk(hipFreeAsync(sl.done, sl.stream), "hipFreeAsync");
-      sl.done_cap = (size_t)m + m / 2 + 256;
-      hchk(hipMallocAsync((void**)&sl.done, sl.done_cap * sizeof(unsigned), sl.stream), "hipMallocAsync");
-      hchk(hipMemsetAsync(sl.done, 0, sl.done_cap * sizeof(unsigned), sl.stream), "memset done");
+      uint8_t* p = reinterpret_cast<uint8_t*>(sl.done);
+      size_t cap = sl.done_cap * sizeof(unsigned);
+      sl.done = nullptr;
+      sl.done_cap = 0;
+      const size_t n = (size_t)m + m / 2 + 256;
+      tmog::grow_device(p, cap, (size_t)m * sizeof(unsigned), n * sizeof(unsigned), sl.stream);
+      hchk(hipMemsetAsync(p, 0, n * sizeof(unsigned), sl.stream), "memset done");
+      sl.done = reinterpret_cast<unsigned*>(p);
+      sl.done_cap = n;
     }
     kchk(tmog_hip_split_find(hist, m, nho, nnf, nfo, flist, g.n_bins, g.B, g.S, g.kind, params, g.missing_bin, nmd,
                              g.qinv, max_nf, sl.cand, feat, bin, gain, dl, left, tot, cursors, n_multi, fps.rec,
@@ -227,13 +239,17 @@ struct GpuBackend {
   // RCCL send / receive buffers come from plain hipMalloc (grow-only; never from the stream-ordered
   // pool of grow_dev): the collective library inspects and may register the buffers it is given.
   static void grow_plain(uint8_t*& p, size_t& cap, size_t need, hipStream_t s) {
-    if (need <= cap) return;
+    if (need <= cap && p != nullptr) return;
     if (p) {
       hchk(hipStreamSynchronize(s), "sync before rccl buffer realloc");
-      hchk(hipFree(p), "hipFree");
+      hipError_t e = hipFree(p);
+      p = nullptr;
+      cap = 0;
+      hchk(e, "hipFree");
     }
-    cap = need + need / 2 + 4096;
-    hchk(hipMalloc((void**)&p, cap), "hipMalloc");
+    const size_t nc = need + need / 2 + 4096;
+    hchk(hipMalloc((void**)&p, nc), "hipMalloc");
+    cap = nc;
   }
   uint8_t* fp_send_buffer(size_t bytes) {
     grow_plain(sl.fp_send, sl.fp_send_cap, bytes, sl.stream);
@@ -403,6 +419,11 @@ int tmog_hip_slot_stream(int slot, void* stream, int set) {
   slots()[slot].ext_set = set != 0;
   return 0;
 }
+
+// dev_alloc.hpp: the out-of-memory handler (torch.cuda.empty_cache from ops/_native.py) and the test hook
+// that fails the n-th native allocation from now (0 = off).
+void tmog_hip_set_oom_handler(void (*fn)()) { tmog::g_oom_handler.store(fn); }
+void tmog_hip_fail_alloc(long n) { tmog::g_fail_at.store(n > 0 ? n : 0); }
 
 int tmog_hip_grow_status(void* h, char* msg, int cap) {
   tmog::GrowResult* r = (tmog::GrowResult*)h;

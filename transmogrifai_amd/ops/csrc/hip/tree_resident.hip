@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "common/tree_grow.hpp"
+#include "hip/dev_alloc.hpp"
 
 extern "C" {
 int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const void* items, int n_items,
@@ -783,11 +784,8 @@ inline void kchk(int rc, const char* what) {
 struct Buf {
   uint8_t* p = nullptr;
   size_t cap = 0;
-  void need(size_t bytes, hipStream_t s) {
-    if (bytes <= cap) return;
-    if (p) hchk(hipFreeAsync(p, s), "hipFreeAsync");
-    cap = bytes + bytes / 4 + 4096;
-    hchk(hipMallocAsync((void**)&p, cap, s), "hipMallocAsync");
+  void need(size_t bytes, hipStream_t s) {     // dev_alloc.hpp: a failed growth leaves the buffer empty
+    tmog::grow_device(p, cap, bytes, bytes + bytes / 4 + 4096, s);
   }
 };
 
@@ -797,7 +795,7 @@ struct ResSlot {
   size_t pin_cap = 0;
   hipEvent_t copied = nullptr;
   std::vector<uint8_t> last;   // constants last shipped (skipped when unchanged)
-  size_t done_zeroed = 0;
+  const uint8_t* done_zeroed = nullptr;   // the ticket-counter block last zeroed (a new block is zeroed again)
   int device = -1;
 };
 
@@ -978,14 +976,21 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
     const size_t o_gain = cs.add(a.job_min_gain, 8 * (size_t)T), o_mcw = cs.add(a.job_mcw, 8 * (size_t)T);
     const size_t o_lam = cs.add(a.job_lambda, 8 * (size_t)T), o_eps = cs.add(a.job_eps, 8 * (size_t)T);
     const size_t o_eta = cs.add(io->job_eta, 8 * (size_t)T), o_gam = cs.add(io->job_gamma, 8 * (size_t)T);
+    const uint8_t* consts_before = sl.consts.p;
     sl.consts.need(cs.buf.size(), st);
+    if (sl.consts.p != consts_before) sl.last.clear();     // a new block holds nothing yet
     if (cs.buf != sl.last) {
       if (sl.copied) hchk(hipEventSynchronize(sl.copied), "constants copy wait");
       else hchk(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming), "event");
-      if (sl.pin_cap < cs.buf.size()) {
-        if (sl.pin) hchk(hipHostFree(sl.pin), "hipHostFree");
+      if (sl.pin_cap < cs.buf.size() || sl.pin == nullptr) {
+        if (sl.pin) {
+          hipError_t e = hipHostFree(sl.pin);
+          sl.pin = nullptr;
+          sl.pin_cap = 0;
+          hchk(e, "hipHostFree");
+        }
+        hchk(hipHostMalloc((void**)&sl.pin, cs.buf.size() + 4096, hipHostMallocDefault), "hipHostMalloc");
         sl.pin_cap = cs.buf.size() + 4096;
-        hchk(hipHostMalloc((void**)&sl.pin, sl.pin_cap, hipHostMallocDefault), "hipHostMalloc");
       }
       std::memcpy(sl.pin, cs.buf.data(), cs.buf.size());
       hchk(hipMemcpyAsync(sl.consts.p, sl.pin, cs.buf.size(), hipMemcpyHostToDevice, st), "constants copy");
@@ -1067,9 +1072,9 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
     sl.hist1.need(sizeof(int64_t) * (size_t)hsz * cp.cap_m, st);
     sl.cand.need(tmog_hip_split_cand_bytes((int)cp.cap_m, F_use, B, S), st);
     sl.done.need(sizeof(unsigned) * (size_t)cp.cap_m, st);
-    if (sl.done_zeroed < sl.done.cap) {      // ticket counters start (and are left) at zero
+    if (sl.done_zeroed != sl.done.p) {       // ticket counters start (and are left) at zero
       hchk(hipMemsetAsync(sl.done.p, 0, sl.done.cap, st), "memset done");
-      sl.done_zeroed = sl.done.cap;
+      sl.done_zeroed = sl.done.p;
     }
     int64_t* hist[2] = {(int64_t*)sl.hist0.p, (int64_t*)sl.hist1.p};
     uint32_t* rows[2] = {a.rows, a.rows_alt};

@@ -136,6 +136,14 @@ def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads
 
     slots: List[Optional[_Slot]] = [None, None]
     copy_stream = torch.cuda.Stream(device=dev) if gpu else None
+    if gpu:
+        # float columns: validity also drops non-null NaNs, decided on the device; columns that turn out
+        # all-valid lose their mask after the copies (one host read for all of them)
+        for c in ncols:
+            if dtype[c].is_floating_point:
+                valid[c] = torch.ones(n, dtype=torch.bool, device=dev)
+        # the copy stream writes buffers allocated on the caller's stream: order after its queued work
+        copy_stream.wait_stream(torch.cuda.current_stream(dev))
     fut = prefetch.submit(read, 0) if n_rg else None
     row0 = 0
     try:
@@ -153,8 +161,14 @@ def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads
                 for c, r, v, bm, bo in pieces:
                     dst = vals[c][r:r + len(v)]
                     dst.copy_(torch.from_numpy(v))
+                    ok = None
                     if bm is not None:
                         ok = torch.from_numpy(np.unpackbits(bm, bitorder="little")[bo:bo + len(v)].astype(bool))
+                    if dst.is_floating_point():         # a non-null NaN is missing too (pandas path: notna)
+                        fin = ~torch.isnan(dst)
+                        if not bool(fin.all()):
+                            ok = fin if ok is None else ok & fin
+                    if ok is not None:
                         if valid[c] is None:
                             valid[c] = torch.ones(n, dtype=torch.bool)
                         valid[c][r:r + len(v)] = ok
@@ -188,20 +202,26 @@ def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads
                     hb[bmo:bmo + bm.nbytes] = bm
 
             list(pool.map(pack, layout))
+            for c, r, v, bm, bo, vo, bmo in layout:
+                if bm is not None and valid[c] is None:     # on the caller's stream, like vals
+                    valid[c] = torch.ones(n, dtype=torch.bool, device=dev)
             with torch.cuda.stream(copy_stream):
                 s.dev[:off].copy_(s.host[:off], non_blocking=True)
                 for c, r, v, bm, bo, vo, bmo in layout:
                     m = len(v)
                     src = s.dev[vo:vo + v.nbytes].view(vals[c].dtype)
                     dst = vals[c][r:r + m]
-                    if bm is None:
-                        dst.copy_(src)
-                    else:
+                    ok = None
+                    if bm is not None:
                         bits = s.dev[bmo:bmo + bm.nbytes]
                         ok = ((bits[:, None] >> torch.arange(8, device=dev, dtype=torch.uint8)) & 1).reshape(-1)
                         ok = ok[bo:bo + m].bool()
-                        if valid[c] is None:
-                            valid[c] = torch.ones(n, dtype=torch.bool, device=dev)
+                    if src.is_floating_point():         # a non-null NaN is missing too (pandas path: notna)
+                        fin = ~torch.isnan(src)
+                        ok = fin if ok is None else ok & fin
+                    if ok is None:
+                        dst.copy_(src)
+                    else:
                         valid[c][r:r + m] = ok
                         dst.copy_(torch.where(ok, src, torch.zeros_like(src)))
                 s.event = torch.cuda.Event()
@@ -216,6 +236,12 @@ def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads
             for s in slots:
                 if s is not None and s.event is not None:
                     s.event.synchronize()
+            masked = [c for c in ncols if valid[c] is not None]
+            if masked:
+                full = torch.stack([valid[c].all() for c in masked]).tolist()
+                for c, f in zip(masked, full):
+                    if f:
+                        valid[c] = None
     finally:
         pool.shutdown(wait=False)
         prefetch.shutdown(wait=False)

@@ -31,7 +31,12 @@ _STAGE_REGISTRY: Dict[str, type] = {}
 
 
 def register_stage(cls):
-    """Class decorator: make a stage class loadable from checkpoints by name."""
+    """Class decorator: make a stage class loadable from checkpoints by name. Reference checkpoints name
+    stages by their JVM class (``com.salesforce.op...OpIndexToString``) and resolve by the short name, so
+    two different classes may not share one: that would make loading depend on import order."""
+    prev = _STAGE_REGISTRY.get(cls.__name__)
+    if prev is not None and (prev.__module__, prev.__qualname__) != (cls.__module__, cls.__qualname__):
+        raise TypeError(f"stage class name {cls.__name__!r} registered twice: {prev.__module__} and {cls.__module__}")
     _STAGE_REGISTRY[cls.__name__] = cls
     _STAGE_REGISTRY[f"{cls.__module__}.{cls.__qualname__}"] = cls
     return cls

@@ -374,20 +374,9 @@ class OpStringIndexer(UnaryEstimator):
         return OpStringIndexerModel(labels, self.params["handle_invalid"])
 
 
-@register_stage
-class OpIndexToString(UnaryTransformer):
-    operation_name = "idxToStr"
-    output_type = T.Text
-    _defaults = {"labels": []}
-
-    def transform_fn(self, v):
-        labels = self.params["labels"]
-        if v is None:
-            return None
-        i = int(v)
-        if not 0 <= i < len(labels):
-            raise ValueError(f"Unseen index: {i}")
-        return labels[i]
+# ``OpIndexToString`` lives in ``indexers.py`` (one class per reference name: the checkpoint registry resolves
+# ``com.salesforce.op.stages.impl.feature.OpIndexToString`` by its short name)
+from .indexers import OpIndexToString  # noqa: E402,F401
 
 
 # ---------------------------------------------------------------------------------- NLP detectors

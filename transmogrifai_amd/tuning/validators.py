@@ -27,6 +27,7 @@ import torch
 
 from ..models.base import FitJob, learner_class
 from ..parallel import dist as D
+from ..utils.device_errors import DeviceFault, is_device_fault
 from .splitters import Splitter, row_uniform
 
 log = logging.getLogger(__name__)
@@ -64,6 +65,11 @@ _COST_SCALE: Dict[str, float] = {"OpLogisticRegression": 8.4e-12, "OpRandomFores
                                  "OpXGBoostClassifier": 8.0e-13}
 _DEFAULT_SCALE = 1.3e-12
 _UNBOUNDED_WAIT = 86400.0       # the reference default maxWait (1 day): no worker thread needed
+
+
+def _cancel_grace_s() -> float:
+    """Seconds a cancelled fit gets to reach its next cancellation check before it is abandoned."""
+    return float(os.environ.get("TMOG_CANCEL_GRACE_S", "30"))
 
 
 def _scaled_cost(learner: str, params: Dict, n: int, d: int) -> float:
@@ -517,16 +523,30 @@ class OpValidator:
             bounded = self.max_wait < _UNBOUNDED_WAIT
             for t in th:
                 t.join(max(0.0, self.max_wait - (time.time() - t0)) if bounded else None)
+            abandoned = []
             if any(t.is_alive() for t in th):
-                token.set()                     # cooperative cancel, then join: nothing is left running
+                token.set()                     # cooperative cancel: running fits stop at their next check
+                grace_end = time.time() + _cancel_grace_s()
                 for t in th:
-                    t.join()
+                    t.join(max(0.0, grace_end - time.time()))
+                # a fit inside a long native call never reaches a check: give it up (the reference abandons
+                # its future) rather than block the selector past maxWait + grace
+                abandoned = [w for w, t in enumerate(th) if t.is_alive()]
+                if abandoned:
+                    log.warning("maxWait: %d learner lane(s) did not stop within %.0fs of cancellation; abandoned",
+                                len(abandoned), _cancel_grace_s())
         if gpu:
-            for st in side:
+            live = [st for w, st in enumerate(streams) if w not in abandoned and st is not cur]
+            for st in live:
                 cur.wait_stream(st)
             # blocks freed on the lane streams are reused by later allocations only once their work has ended
-            torch.cuda.synchronize(dev)
-            SP.release(dev, side)
+            if abandoned:
+                for st in live + [cur]:
+                    st.synchronize()
+                SP.release(dev, live)           # an abandoned lane keeps its stream leased
+            else:
+                torch.cuda.synchronize(dev)
+                SP.release(dev, side)
         with lock:
             if errs:
                 raise errs[0]
@@ -553,13 +573,15 @@ class OpValidator:
         gpu = isinstance(X, torch.Tensor) and X.is_cuda
         dev = X.device if gpu else None
         stream = torch.cuda.current_stream(dev) if gpu else None
+        ctx.setdefault("refit_states", {})     # shared by the worker's copy: the selector reads the refits
+        wctx = dict(ctx)
 
         def work():
             try:
                 if gpu:
                     torch.cuda.set_device(dev)
                 with cancel.scope(token), (torch.cuda.stream(stream) if gpu else contextlib.nullcontext()):
-                    box["out"] = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, dict(ctx))
+                    box["out"] = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, wctx)
             except cancel.FitCancelled:
                 box["cancelled"] = True
             except BaseException as e:          # noqa: BLE001  (re-raised below)
@@ -570,7 +592,10 @@ class OpValidator:
         th.join(max(0.0, remaining))
         if th.is_alive():
             token.set()
-            th.join()           # returns at the fit's next cancellation check
+            th.join(_cancel_grace_s())      # returns at the fit's next cancellation check
+            if th.is_alive():           # inside a long native call: abandoned, as the reference's future is
+                log.warning("Model %s did not stop within %.0fs of its maxWait cancellation; abandoned", lname,
+                            _cancel_grace_s())
             log.warning("Model %s did not finish within maxWait=%ss; its %d fits are dropped", lname,
                         self.max_wait, len(mine))
             return {}, [f"{lname}: did not finish within maxWait={self.max_wait}s"]
@@ -622,10 +647,13 @@ class OpValidator:
                 out.update({key: float(v) for (key, _), v in zip(items, vals)})
             return out
 
+        dev = X.device if isinstance(X, torch.Tensor) else None
         try:
             results.update(run(mine))
             return results, failures
         except Exception as e:
+            if is_device_fault(e, dev):     # sticky: every later fit on this context would fail too
+                raise DeviceFault(f"{lname}: {e!r}") from e
             log.warning("Model %s failed in model selector as a batch (%r); retrying per grid point", lname, e)
         by_grid: Dict[int, list] = {}
         for item in mine:
@@ -634,6 +662,8 @@ class OpValidator:
             try:
                 results.update(run(batch))
             except Exception as e:  # failed models are dropped, as in OpValidator.getSummary
+                if is_device_fault(e, dev):
+                    raise DeviceFault(f"{lname} {grid[g]}: {e!r}") from e
                 log.warning("Model %s with %s failed in model selector: %r", lname, grid[g], e)
                 failures.append(f"{lname} {grid[g]}: {e!r}")
         return results, failures

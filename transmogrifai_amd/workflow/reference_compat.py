@@ -162,7 +162,23 @@ def _lambda(pm, a):
     return st
 
 
+def _index_to_string(no_filter: bool):
+    """``OpIndexToString`` (a Spark ``IndexToString`` wrapper, ``OpIndexToString.scala:50-74``) and
+    ``OpIndexToStringNoFilter(labels, unseenName)``: the labels come from the wrapped stage's params (or the
+    ctor args); empty labels fall back to the input indexer's metadata at transform time."""
+    def build(pm, a):
+        from ..stages.feature.indexers import OpIndexToString, OpIndexToStringNoFilter
+        spark = pm.get("sparkMlStage") if isinstance(pm.get("sparkMlStage"), dict) else {}
+        labels = list(a.get("labels") or pm.get("labels") or spark.get("labels") or [])
+        if no_filter:
+            return OpIndexToStringNoFilter(labels=labels, unseen_name=str(a.get("unseenName", "UnseenIndex")))
+        return OpIndexToString(labels=labels)
+    return build
+
+
 ADAPTERS: Dict[str, Callable] = {
+    "OpIndexToString": _index_to_string(False),
+    "OpIndexToStringNoFilter": _index_to_string(True),
     "RealNNVectorizer": _real_nn,
     "BinaryVectorizer": _binary,
     "DateListVectorizer": _date_list,
