@@ -323,6 +323,9 @@ def _timed(args, one_run, expected_configs, use_gpu, dev, torch, D, sim, n_raw, 
             out["stalls"] = list(WD.STALLS)
         if args.verbose and summ:
             out["timings"] = summ.get("timings")
+            from transmogrifai_amd.tuning.validators import PHASE_TIMES
+            if PHASE_TIMES:         # TMOG_FIT_PHASES=1, summed over the warm-up and timed steps
+                out["fit_phases"] = {k: round(v, 4) for k, v in PHASE_TIMES.items()}
             out["stage_timings"] = stage_t[0]
         if sim:
             out["simulated"] = {"rank": D.rank(), "world": D.world(),

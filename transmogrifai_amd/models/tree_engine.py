@@ -335,7 +335,7 @@ class _GrowArgs(C.Structure):
                 ("fp_mhi", C.c_int32), ("fp_olo", C.c_int32), ("fp_ohi", C.c_int32), ("fp_comm", C.c_void_p),
                 ("fp_exchange", C.c_void_p), ("fp_ctx", C.c_void_p), ("slot_base", C.c_int32),
                 ("XbT", C.c_void_p), ("gh", C.c_void_p), ("gh_alt", C.c_void_p), ("n_entries", C.c_int64),
-                ("wide_rows", C.c_int32)]
+                ("wide_rows", C.c_int32), ("Xh", C.c_void_p), ("Fh", C.c_int32)]
 
 
 class _ResidentIO(C.Structure):
@@ -525,7 +525,7 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                 collect_leaves: bool = False, groups: Optional[int] = None, csr=None, root=None,
                 fp: Optional[FpPlan] = None, slot_base: int = 0, XbT: Optional[torch.Tensor] = None,
                 quant_amax: Optional[torch.Tensor] = None, quant_wmax: Optional[float] = None,
-                resident: bool = False, prestaged=None):
+                resident: bool = False, prestaged=None, Xh: Optional[torch.Tensor] = None):
     """Grow one tree per job, all jobs level-synchronously. ``Xb`` is ``uint8 [N, F]``.
 
     The level loop runs natively (``ops/csrc/common/tree_grow.hpp``): on the GPU every job group gets
@@ -553,6 +553,10 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
     each builds histograms of its feature slice only (``csr`` must then be the slice's, from
     ``onebin_csr(..., cols=fp.one_cols)``) and all ranks return the same forest -- the one a single
     rank would grow. Jobs must not use per-node feature subsets.
+
+    ``Xh``: GPU, optional ``uint8 [N, Fh]`` row-major copy of ``Xb[:, :Fh]`` (``Fh`` a multiple of 64) holding the
+    multi-bin columns; the wide-load histogram items read it instead of ``Xb`` (aligned row segments, a smaller
+    footprint for the Infinity Cache). Same trees.
 
     ``resident``: on the GPU, for one job group (``groups=1``), no per-node feature subsets and leaves
     collected, grow with the device-planned level loop (``ops/csrc/hip/tree_resident.hip``): nothing is
@@ -652,7 +656,8 @@ def grow_forest(Xb: torch.Tensor, n_bins: np.ndarray, jobs: Sequence[TreeJob], *
                   C.cast(fp_cb, C.c_void_p) if fp_cb is not None else None, None, int(slot_base),
                   N.ptr(XbT) if (on_gpu and XbT is not None) else None,
                   N.ptr(gh) if gh is not None else None, N.ptr(gh_alt) if gh_alt is not None else None, total,
-                  int(wide))
+                  int(wide), N.ptr(Xh) if (on_gpu and Xh is not None) else None,
+                  int(Xh.shape[1]) if (on_gpu and Xh is not None) else 0)
     lib = N.hip() if on_gpu else N.host()
     if resident and on_gpu and ng == 1 and collect_leaves:
         rt = _grow_resident(lib, a, jobs, mode, kind, S, missing_bin, leaf_rows, leaf_gid, dev, total, wide)

@@ -698,6 +698,7 @@ class XGBoostClassifierLearner(_BoostLearner):
 
     def _boost(self, Xb, spec, y, jobs, N, F, dev, mb, par=None):
         from ..evaluators.metrics import binned_aupr_from_counts, binned_aupr_multi
+        t_setup0 = time.perf_counter()
         P = len(jobs)
         rows = [_rows(j, N, dev) for j in jobs]
         rounds = [int(j.params.get("num_round", 100)) for j in jobs]
@@ -739,6 +740,16 @@ class XGBoostClassifierLearner(_BoostLearner):
             n_bins_g = np.concatenate([np.asarray(n_bins_g), np.ones(F4 - F0, dtype=np.asarray(n_bins_g).dtype)])
             base_perm = colperm if colperm is not None else np.arange(F0, dtype=np.int64)
             colperm = np.concatenate([base_perm, np.zeros(F4 - F0, np.int64)])
+        # compact histogram matrix: the leading multi-bin columns of Xg at a 64-byte row stride (aligned row
+        # segments, and a footprint that fits the Infinity Cache better than the full padded rows); only the
+        # wide-load histogram items read it (tree_grow.hpp GrowArgs.Xh)
+        Xh = None
+        if dev.type == "cuda" and spec.missing_bin > 0 and os.environ.get("TMOG_HIST_COMPACT", "1") != "0":
+            nbg = np.asarray(n_bins_g)
+            n_multi = int(np.argmax(nbg == 1)) if (nbg == 1).any() else nbg.size
+            Fh = (n_multi + 63) // 64 * 64
+            if 0 < n_multi and Fh < Xg.shape[1] and (nbg[:n_multi] != 1).all():
+                Xh = Xg[:, :Fh].contiguous()
         # feature-parallel over the ranks: this rank's slice of the growth-order feature lists
         fp = TE.fp_plan(Xg, n_bins_g, par, sparse=spec.missing_bin >= 0) if par is not None else None
         # one-hot / null-indicator columns: histogram from the rows' CSR lists (tree_kernels.hip)
@@ -847,7 +858,7 @@ class XGBoostClassifierLearner(_BoostLearner):
                                         missing_bin=spec.missing_bin, collect_leaves=True, csr=csr, root=root, fp=fp,
                                         slot_base=slot_base, groups=groups, XbT=XgT,
                                         quant_amax=amax_cur, quant_wmax=1.0 if amax_cur is not None else None,
-                                        resident=resident and groups in (None, 1), prestaged=pre)
+                                        resident=resident and groups in (None, 1), prestaged=pre, Xh=Xh)
                 t_2 = tick()
                 is_res = isinstance(forest, TE.ResidentTree)
                 if colperm is not None and not is_res:
@@ -917,6 +928,11 @@ class XGBoostClassifierLearner(_BoostLearner):
         # round set-up, the early-stopping read-back) overlaps the other half's kernels instead of
         # idling the GPU. Trees are identical to the single-loop order (see run()).
         parts = int(os.environ.get("TMOG_XGB_PIPE", "4"))
+        if _XGB_PROF is not None:
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            _XGB_PROF.setdefault("phases", {})["setup"] = time.perf_counter() - t_setup0
+            t_loop0 = time.perf_counter()
         if fused and par is None and P >= 2 and parts >= 2:
             parts = min(parts, P)
             cuts = np.linspace(0, P, parts + 1).astype(int)
@@ -926,6 +942,9 @@ class XGBoostClassifierLearner(_BoostLearner):
             run(list(range(P)))
         if _XGB_PROF is not None:
             import sys as _sys
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            _XGB_PROF.setdefault("phases", {})["loop"] = time.perf_counter() - t_loop0
             rep = {k: {a: round(b, 4) for a, b in v.items()} for k, v in _XGB_PROF.items()}
             if dev.type == "cuda" and os.environ.get("TMOG_GROW_TIMING"):
                 from ..ops import _native as NV

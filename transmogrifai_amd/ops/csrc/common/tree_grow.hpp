@@ -154,6 +154,12 @@ struct GrowArgs {
   // training sets of >= 2^24 rows: entries are plain 32-bit row ids of weight 1 instead of row | weight << 24
   // (weighted roots are expanded into repeated entries by the caller, models/tree_engine.py)
   int32_t wide_rows;
+  // GPU, optional: row-major matrix the wide-load histogram items read instead of Xb -- the multi-bin columns
+  // only (their Xb column positions), row stride Fh bytes (a multiple of 64: every row segment starts a cache
+  // line and the matrix is smaller than Xb, so more of it stays in the Infinity Cache). Groups whose columns
+  // reach past Fh stay on Xb.
+  const uint8_t* Xh;
+  int32_t Fh;
 };
 
 // Feature-parallel split record, one per node and rank:
@@ -376,6 +382,8 @@ GroupLayout group_layout(const GrowArgs& a, bool use_subset, bool fp) {
       if (wide_ok) {
         bool ok = perm_feats[g.f0] % 4 == 0;
         for (int i = 1; ok && i < g.nf; ++i) ok = perm_feats[g.f0 + i] == perm_feats[g.f0] + i;
+        // with a compact histogram matrix every wide group must lie inside it (the kernel reads Xh only)
+        if (ok && a.Xh != nullptr) ok = a.Fh % 4 == 0 && perm_feats[g.f0] + g.nf <= a.Fh;
         g.wide = ok;
       }
       full_groups.push_back(g);

@@ -25,7 +25,8 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
-                        hipStream_t stream, const int32_t* gh, const int* dcount, int wide_rows);
+                        hipStream_t stream, const int32_t* gh, const int* dcount, int wide_rows,
+                        const uint8_t* Xh, int Fh);
 int tmog_hip_hist_subtract(int64_t* hist, const int64_t* parent, const int64_t* parent_off, const int64_t* small_off,
                            const int64_t* out_off, const int64_t* size, int n, int64_t max_size, int64_t dense,
                            int per, int S, hipStream_t stream);
@@ -196,7 +197,8 @@ struct GpuBackend {
     if (n_items)
       kchk(tmog_hip_hist_build(g.Xb, g.F, rows, items, n_items, nfo, flist, nmd, nho, hist, g.B, g.mode, g.S, g.y,
                                g.t1, g.t2, g.stride, g.qscale, g.mode == 2 ? g.missing_bin : -1, g.csr_ptr,
-                               g.csr_col, Sc, n_wide, need_general, sl.stream, gh_of(rows), nullptr, g.wide_rows),
+                               g.csr_col, Sc, n_wide, need_general, sl.stream, gh_of(rows), nullptr, g.wide_rows, g.Xh,
+                               g.Fh),
            "hist_build");
   }
   int stat_chunk(int B, int S) const { return tmog_hip_hist_stat_chunk(B, S); }

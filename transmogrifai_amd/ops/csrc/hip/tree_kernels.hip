@@ -505,11 +505,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
     const int32_t* __restrict__ node_feat_off, const int32_t* __restrict__ feat_list,
     const int32_t* __restrict__ node_model, const int64_t* __restrict__ node_hist_off, int64_t* __restrict__ hist,
     int B, const float* __restrict__ t1, const float* __restrict__ t2, int64_t stride,
-    const float* __restrict__ qscale, int skip_bin, const int2* __restrict__ gh, int wide) {
+    const float* __restrict__ qscale, int skip_bin, const int2* __restrict__ gh, int wide,
+    const uint8_t* __restrict__ Xh, int Fh) {
   extern __shared__ int lds_w[];
   if (g_hist_debug & 2) return;
   const HistItem it = items[blockIdx.x];
-  hist_wide_item(it, Xb, F, feat_list[node_feat_off[it.node] + it.fg0], rows, node_model, node_hist_off, hist, B,
+  hist_wide_item(it, Xh, Fh, feat_list[node_feat_off[it.node] + it.fg0], rows, node_model, node_hist_off, hist, B,
                  t1, t2, stride, qscale, skip_bin, lds_w, gh, wide);
 }
 
@@ -524,7 +525,7 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
     int B, int S, const float* __restrict__ y, const float* __restrict__ t1, const float* __restrict__ t2,
     int64_t stride, const float* __restrict__ qscale, int skip_bin, const int64_t* __restrict__ csr_ptr,
     const uint16_t* __restrict__ csr_col, int Sc, const int2* __restrict__ gh, const int* __restrict__ dcount,
-    int wide) {
+    int wide, const uint8_t* __restrict__ Xh, int Fh) {
   extern __shared__ __attribute__((aligned(16))) int lds[];
   // dcount (device-planned levels, tree_resident.hip): the grid is an upper bound, the item count is on the device
   if (dcount != nullptr && (int)blockIdx.x >= *dcount) return;
@@ -540,8 +541,8 @@ __global__ void __launch_bounds__(256) hist_build_kernel(
                   csr_col, lds, gh, wide);
     return;
   }
-  if (MODE == 2 && (it.excl & 16)) {
-    hist_wide_item(it, Xb, F, feat_list[node_feat_off[it.node] + it.fg0], rows, node_model, node_hist_off, hist, B,
+  if (MODE == 2 && (it.excl & 16)) {        // wide-load items read the compact matrix (GrowArgs.Xh, or Xb)
+    hist_wide_item(it, Xh, Fh, feat_list[node_feat_off[it.node] + it.fg0], rows, node_model, node_hist_off, hist, B,
                    t1, t2, stride, qscale, skip_bin, lds, gh, wide);
     return;
   }
@@ -1847,8 +1848,13 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
-                        hipStream_t stream, const int32_t* gh_words, const int* dcount, int wide_rows) {
+                        hipStream_t stream, const int32_t* gh_words, const int* dcount, int wide_rows,
+                        const uint8_t* Xh, int Fh) {
   if (n_items == 0) return 0;
+  if (Xh == nullptr) {
+    Xh = Xb;
+    Fh = F;
+  }
   if (dcount != nullptr && n_wide != 0) return -2;   // device-counted launches: one mixed launch
   const int2* gh = reinterpret_cast<const int2*>(gh_words);
   if (gh && mode != 2) return -2;
@@ -1876,10 +1882,10 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
     static const int occ = [] { const char* e = std::getenv("TMOG_HIST_WIDE_OCC"); return e ? std::atoi(e) : 6; }();
     if (occ >= 7)
       hipLaunchKernelGGL(hist_wide_kernel<7>, dim3(n_wide), dim3(256), lds, stream, Xb, F, rows, it, node_feat_off,
-                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin, gh, wide_rows);
+                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin, gh, wide_rows, Xh, Fh);
     else
       hipLaunchKernelGGL(hist_wide_kernel<6>, dim3(n_wide), dim3(256), lds, stream, Xb, F, rows, it, node_feat_off,
-                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin, gh, wide_rows);
+                         feat_list, node_model, node_hist_off, hist, B, t1, t2, stride, qscale, skip_bin, gh, wide_rows, Xh, Fh);
     it += n_wide;
     n_items -= n_wide;
     if (n_items == 0) return (int)hipGetLastError();
@@ -1888,19 +1894,19 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
   if (mode == 0)
     hipLaunchKernelGGL(hist_build_kernel<0>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc,
-                       nullptr, dcount, wide_rows);
+                       nullptr, dcount, wide_rows, Xh, Fh);
   else if (mode == 1)
     hipLaunchKernelGGL(hist_build_kernel<1>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, -1, nullptr, nullptr, Sc,
-                       nullptr, dcount, wide_rows);
+                       nullptr, dcount, wide_rows, Xh, Fh);
   else if (need_general)
     hipLaunchKernelGGL(hist_build_kernel<2>, grid, block, lds, stream, Xb, F, rows, it, node_feat_off, feat_list,
                        node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                       csr_col, Sc, gh, dcount, wide_rows);
+                       csr_col, Sc, gh, dcount, wide_rows, Xh, Fh);
   else
     hipLaunchKernelGGL((hist_build_kernel<2, false>), grid, block, lds, stream, Xb, F, rows, it, node_feat_off,
                        feat_list, node_model, node_hist_off, hist, B, S, y, t1, t2, stride, qscale, skip_bin, csr_ptr,
-                       csr_col, Sc, gh, dcount, wide_rows);
+                       csr_col, Sc, gh, dcount, wide_rows, Xh, Fh);
   return (int)hipGetLastError();
 }
 

@@ -36,7 +36,8 @@ int tmog_hip_hist_build(const uint8_t* Xb, int F, const uint32_t* rows, const vo
                         const int64_t* node_hist_off, int64_t* hist, int B, int mode, int S, const float* y,
                         const float* t1, const float* t2, int64_t stride, const float* qscale, int skip_bin,
                         const int64_t* csr_ptr, const uint16_t* csr_col, int Sc, int n_wide, int need_general,
-                        hipStream_t stream, const int32_t* gh, const int* dcount, int wide_rows);
+                        hipStream_t stream, const int32_t* gh, const int* dcount, int wide_rows,
+                        const uint8_t* Xh, int Fh);
 int tmog_hip_split_find(const int64_t* hist, int n_nodes, const int64_t* node_hist_off, const int32_t* node_nfeat,
                         const int32_t* node_feat_off, const int32_t* feat_list, const int32_t* feat_nbins, int B,
                         int S, int kind, const float* node_params, int missing_bin, const int32_t* node_model,
@@ -1151,7 +1152,8 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
       kchk(tmog_hip_hist_build(a.Xb, a.F, rows[c], P.hitems, (int)std::min(hist_bound(a, L, n_sc, total, mb), cp.cap_h),
                                P.nfo, flist_d, P.nmd[c], P.nho[c], hist[c], B, a.mode, S, a.y, a.t1, a.t2, a.stride,
                                a.qscale, a.mode == 2 ? a.missing_bin : -1, a.csr_ptr, a.csr_col, S, 0,
-                               need_general ? 1 : 0, st, use_gh ? gh[c] : nullptr, cnt + C_NH, a.wide_rows),
+                               need_general ? 1 : 0, st, use_gh ? gh[c] : nullptr, cnt + C_NH, a.wide_rows, a.Xh,
+                               a.Fh),
            "hist_build");
       if (d > 0)
         kchk(tmog_hip_pair_scan(hist[c], hist[c ^ 1], P.poff, P.sj, P.bj, (int)std::max<int64_t>(1, mb / 2), P.nho[c],

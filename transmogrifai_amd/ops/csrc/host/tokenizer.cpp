@@ -2,7 +2,8 @@
 // LuceneTextAnalyzer / StandardAnalyzer path used by TextTokenizer.tokenizeString
 // (core/.../TextTokenizer.scala:160-188, core/.../utils/text/LuceneTextAnalyzer.scala:160-166):
 // letter-led words (letters may be joined by ' or .), digit-led numbers (digits joined by . or ,),
-// underscore-led words, per-character split of CJK tokens, lowercase, 255-char cap, English stop
+// underscore-led words, StandardTokenizer split of CJK tokens (ideographs and hiragana one token each, katakana
+// and hangul runs words), lowercase, 255-char cap, English stop
 // words, minimum token length.
 //
 // The executable spec is transmogrifai_amd/utils/text.py:analyze; the character classes and the
@@ -17,6 +18,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <unordered_set>
 #include <vector>
@@ -115,60 +117,89 @@ int64_t tokenize_one(const uint8_t* p, int64_t n, bool lowercase, int min_len, b
   if (lowercase)
     for (auto& c : cps) c = T.lower[c];
   const int64_t L = (int64_t)cps.size();
-  auto is_w = [&](int64_t i) { return i < L && (T.cls[cps[i]] & kWord); };
-  auto is_d = [&](int64_t i) { return i < L && (T.cls[cps[i]] & kDigit); };
-  auto is_letter = [&](int64_t i) { return is_w(i) && !is_d(i) && cps[i] != '_'; };
   int64_t emitted = 0;
-  int64_t i = 0;
-  while (i < L) {
-    int64_t j;
-    if (is_letter(i)) {
-      j = i + 1;
-      for (;;) {
-        if (is_w(j)) ++j;
-        else if (j < L && (cps[j] == '\'' || cps[j] == '.') && is_letter(j + 1)) ++j;
-        else break;
-      }
-    } else if (is_d(i)) {
-      j = i + 1;
-      for (;;) {
-        if (is_w(j)) ++j;
-        else if (j < L && (cps[j] == '.' || cps[j] == ',') && is_d(j + 1)) ++j;
-        else break;
-      }
-    } else if (cps[i] == '_') {
-      j = i + 1;
-      while (is_w(j)) ++j;
+  // CJK script of a code point (utils/text.py cjk_class: the kCjk ranges): 1 Han, 2 hiragana, 3 katakana, 4 hangul
+  auto cjk_cls = [](uint32_t o) -> int {
+    if ((o >= 0x4E00 && o <= 0x9FFF) || (o >= 0x3400 && o <= 0x4DBF)) return 1;
+    if (o >= 0x3040 && o <= 0x309F) return 2;
+    if (o >= 0x30A0 && o <= 0x30FF) return 3;
+    if (o >= 0xAC00 && o <= 0xD7AF) return 4;
+    return 0;
+  };
+  auto emit_word = [&](int64_t i, int64_t j) {
+    if (j - i > 255 || j - i < min_len) return;
+    const size_t start = sink.bytes.size();
+    for (int64_t k = i; k < j; ++k) put_utf8(sink.bytes, T.lower[cps[k]]);
+    bool stop = false;
+    if (use_stop) {
+      scratch.assign((const char*)sink.bytes.data() + start, sink.bytes.size() - start);
+      stop = stopwords().count(scratch) != 0;
+    }
+    if (stop) {
+      sink.bytes.resize(start);
     } else {
-      ++i;
-      continue;
+      sink.ends.push_back((int64_t)sink.bytes.size());
+      ++emitted;
     }
-    bool cjk = false;
-    for (int64_t k = i; k < j; ++k) cjk |= (T.cls[cps[k]] & kCjk) != 0;
-    if (cjk) {  // every char of the token becomes a token (not lowercased beyond the string-level pass)
-      for (int64_t k = i; k < j; ++k) {
-        if (1 < min_len) continue;
-        put_utf8(sink.bytes, cps[k]);
-        sink.ends.push_back((int64_t)sink.bytes.size());
-        ++emitted;
-      }
-    } else if (j - i <= 255 && j - i >= min_len) {
-      const size_t start = sink.bytes.size();
-      for (int64_t k = i; k < j; ++k) put_utf8(sink.bytes, T.lower[cps[k]]);
-      bool stop = false;
-      if (use_stop) {
-        scratch.assign((const char*)sink.bytes.data() + start, sink.bytes.size() - start);
-        stop = stopwords().count(scratch) != 0;
-      }
-      if (stop) {
-        sink.bytes.resize(start);
+  };
+  // word rules over cps[lo, hi); a word holding CJK characters is split as StandardTokenizer does (every
+  // ideograph and hiragana a token, katakana / hangul runs words, the other characters scanned again)
+  std::function<void(int64_t, int64_t)> scan = [&](int64_t lo, int64_t hi) {
+    auto is_w = [&](int64_t i) { return i < hi && (T.cls[cps[i]] & kWord); };
+    auto is_d = [&](int64_t i) { return i < hi && (T.cls[cps[i]] & kDigit); };
+    auto is_letter = [&](int64_t i) { return is_w(i) && !is_d(i) && cps[i] != '_'; };
+    int64_t i = lo;
+    while (i < hi) {
+      int64_t j;
+      if (is_letter(i)) {
+        j = i + 1;
+        for (;;) {
+          if (is_w(j)) ++j;
+          else if (j < hi && (cps[j] == '\'' || cps[j] == '.') && is_letter(j + 1)) ++j;
+          else break;
+        }
+      } else if (is_d(i)) {
+        j = i + 1;
+        for (;;) {
+          if (is_w(j)) ++j;
+          else if (j < hi && (cps[j] == '.' || cps[j] == ',') && is_d(j + 1)) ++j;
+          else break;
+        }
+      } else if (cps[i] == '_') {
+        j = i + 1;
+        while (is_w(j)) ++j;
       } else {
-        sink.ends.push_back((int64_t)sink.bytes.size());
-        ++emitted;
+        ++i;
+        continue;
       }
+      bool cjk = false;
+      for (int64_t k = i; k < j; ++k) cjk |= (T.cls[cps[k]] & kCjk) != 0;
+      if (cjk) {
+        int64_t k = i;
+        while (k < j) {
+          const int c = cjk_cls(cps[k]);
+          int64_t e = k + 1;
+          if (c == 3 || c == 4) {
+            while (e < j && cjk_cls(cps[e]) == c) ++e;
+          } else if (c == 0) {
+            while (e < j && cjk_cls(cps[e]) == 0) ++e;
+          }
+          if (c == 0) {
+            scan(k, e);
+          } else if (e - k >= min_len && e - k <= 255) {   // not lowercased beyond the string-level pass
+            for (int64_t q = k; q < e; ++q) put_utf8(sink.bytes, cps[q]);
+            sink.ends.push_back((int64_t)sink.bytes.size());
+            ++emitted;
+          }
+          k = e;
+        }
+      } else {
+        emit_word(i, j);
+      }
+      i = j;
     }
-    i = j;
-  }
+  };
+  scan(0, L);
   return emitted;
 }
 

@@ -67,6 +67,21 @@ _DEFAULT_SCALE = 1.3e-12
 _UNBOUNDED_WAIT = 86400.0       # the reference default maxWait (1 day): no worker thread needed
 
 
+# TMOG_FIT_PHASES=1: wall-clock of each learner's fit / validation predict / metric phases (the device is
+# synchronised at each boundary, so the phases add up to the learner's time; diagnostics)
+PHASE_TIMES: Dict[str, float] = {}
+import threading as _threading  # noqa: E402
+_PHASE_LOCK = _threading.Lock()
+
+
+def _phase_clock(X) -> Optional[float]:
+    if os.environ.get("TMOG_FIT_PHASES") != "1":
+        return None
+    if isinstance(X, torch.Tensor) and X.is_cuda:
+        torch.cuda.current_stream(X.device).synchronize()
+    return time.perf_counter()
+
+
 def _cancel_grace_s() -> float:
     """Seconds a cancelled fit gets to reach its next cancellation check before it is abandoned."""
     return float(os.environ.get("TMOG_CANCEL_GRACE_S", "30"))
@@ -621,13 +636,16 @@ class OpValidator:
             refit = ctx.get("refit_job") if (getattr(learner, "batched_refit", False) and D.world() == 1) else None
             extra = sorted({g for _, (_, g, _) in batch}) if refit is not None else []
             fjobs += [FitJob(dict(learner.defaults, **grid[g]), refit[0], refit[1]) for g in extra]
+            tp0 = _phase_clock(X)
             states = learner.fit_batch(X, y, fjobs, context=ctx)
+            tp1 = _phase_clock(X)
             if extra:
                 store = ctx.setdefault("refit_states", {})
                 for g, st in zip(extra, states[len(batch):]):
                     store[refit_key(lname, dict(learner.defaults, **grid[g]))] = st
                 states = states[:len(batch)]
             preds = learner.predict_batch(states, X, [val_rows[k] for _, (_, g, k) in batch], context=ctx)
+            tp2 = _phase_clock(X)
             out = {}
             # the models of one fold share its validation rows: their curves come from one segmented sort
             by_fold: Dict[int, list] = {}
@@ -645,6 +663,11 @@ class OpValidator:
                 if vals is None:
                     vals = [float(self.evaluator.selection_metric(yv, *pr)) for _, pr in items]
                 out.update({key: float(v) for (key, _), v in zip(items, vals)})
+            if tp0 is not None:
+                tp3 = _phase_clock(X)
+                with _PHASE_LOCK:
+                    for ph, dt in (("fit", tp1 - tp0), ("predict", tp2 - tp1), ("metric", tp3 - tp2)):
+                        PHASE_TIMES[f"{lname}:{ph}"] = PHASE_TIMES.get(f"{lname}:{ph}", 0.0) + dt
             return out
 
         dev = X.device if isinstance(X, torch.Tensor) else None

@@ -125,6 +125,12 @@ def detect_languages(text: Optional[str]) -> Dict[str, float]:
         toks = TU.tokenize(text, stopwords=frozenset())
         hits = {lang: sum(1 for t in toks if t in words) for lang, words in PROFILES.items()}
         top = max(hits.values()) if hits else 0
+        distinct = max((len(set(toks) & words) for words in PROFILES.values()), default=0)
+        if distinct < 2 and len(out) and latin < letters:
+            # Latin tokens with fewer than two distinct function words next to another script -- markup, names,
+            # URLs: they identify nothing, so the other scripts' shares are taken among the rest of the letters
+            rest = letters - latin
+            return dict(sorted(((k, min(1.0, v * letters / rest)) for k, v in out.items()), key=lambda kv: -kv[1]))
         if top:
             # posterior of a naive token model: each profile hit multiplies a language's odds by _ODDS
             share = latin / letters
@@ -146,9 +152,25 @@ def best_language(text: Optional[str], threshold: float = 0.99, default: str = U
     return default
 
 
+# the reference's Language enum names (utils/.../text/Language.scala) -> the codes used here
+LANGUAGE_NAMES = {"English": "en", "French": "fr", "German": "de", "Spanish": "es", "Italian": "it", "Portuguese": "pt",
+                  "Brazilian": "pt", "Dutch": "nl", "Swedish": "sv", "Danish": "da", "Norwegian": "no", "Polish": "pl",
+                  "Catalan": "ca", "Finnish": "fi", "Turkish": "tr", "Romanian": "ro", "Russian": "ru",
+                  "Hungarian": "hu", "Japanese": "ja", "Korean": "ko", "SimplifiedChinese": "zh-cn",
+                  "TraditionalChinese": "zh-tw", "Chinese": "zh"}
+# Lucene CJKAnalyzer languages (LuceneTextAnalyzer.scala: Korean, SimplifiedChinese, TraditionalChinese)
+CJK_BIGRAM = frozenset({"zh", "zh-cn", "zh-tw", "ko"})
+
+
 def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_token_length: int = 1) -> List[str]:
     """Per-language analysis: elision stripping (fr / it / ca), the language's stop words (English's for an
-    unknown language, as the reference's default StandardAnalyzer), StandardAnalyzer word rules."""
+    unknown language, as the reference's default StandardAnalyzer), StandardAnalyzer word rules; Chinese and
+    Korean through the CJKAnalyzer bigrams (:func:`utils.text.analyze_cjk_bigrams`). Japanese (Kuromoji
+    morphology in the reference) keeps the StandardAnalyzer segmentation: parity unpinned."""
+    language = LANGUAGE_NAMES.get(language, language)
+    if language in CJK_BIGRAM:
+        s = text.lower() if to_lowercase else text
+        return [t for t in TU.analyze_cjk_bigrams(s, TU.ENGLISH_STOPWORDS) if len(t) >= min_token_length]
     lang = language if language in STOPWORDS else "en"
     toks = TU.tokenize(text, to_lowercase, 1, stopwords=frozenset())
     el = _ELISIONS.get(lang)

@@ -57,6 +57,46 @@ _WORD = re.compile(
     re.UNICODE)
 _CJK = re.compile(r"[぀-ヿ㐀-䶿一-鿿가-힯]")
 
+# CJK script classes (the code-point ranges of _CJK; ops/csrc/host/tokenizer.cpp uses the same)
+HAN, HIRAGANA, KATAKANA, HANGUL = 1, 2, 3, 4
+
+
+def cjk_class(ch: str) -> int:
+    o = ord(ch)
+    if 0x4E00 <= o <= 0x9FFF or 0x3400 <= o <= 0x4DBF:
+        return HAN
+    if 0x3040 <= o <= 0x309F:
+        return HIRAGANA
+    if 0x30A0 <= o <= 0x30FF:
+        return KATAKANA
+    if 0xAC00 <= o <= 0xD7AF:
+        return HANGUL
+    return 0
+
+
+def _segments(tok: str):
+    """StandardTokenizer (UAX#29) split of a word holding CJK characters: every ideograph and every hiragana
+    is a token of its own, katakana and hangul runs are words, the other characters form ordinary words.
+    Yields (text, is_cjk)."""
+    i, n = 0, len(tok)
+    while i < n:
+        c = cjk_class(tok[i])
+        j = i + 1
+        if c in (KATAKANA, HANGUL):
+            while j < n and cjk_class(tok[j]) == c:
+                j += 1
+        elif c == 0:
+            while j < n and cjk_class(tok[j]) == 0:
+                j += 1
+        yield tok[i:j], c != 0
+        i = j
+
+
+def _plain(tok: str, stopwords, max_len: int, out: List[str]) -> None:
+    tok = tok.lower()
+    if len(tok) <= max_len and tok not in stopwords:
+        out.append(tok)
+
 
 def analyze(text: str, stopwords=ENGLISH_STOPWORDS, max_len: int = 255) -> List[str]:
     """StandardAnalyzer-style analysis (lowercase + stop filter) of an already lowercased or raw string."""
@@ -64,15 +104,56 @@ def analyze(text: str, stopwords=ENGLISH_STOPWORDS, max_len: int = 255) -> List[
     for m in _WORD.finditer(text):
         tok = m.group(0)
         if _CJK.search(tok):
-            out.extend(c for c in tok)
+            for seg, cjk in _segments(tok):
+                if cjk:
+                    if len(seg) <= max_len:
+                        out.append(seg)
+                elif _WORD.fullmatch(seg):
+                    _plain(seg, stopwords, max_len, out)
+                else:
+                    for m2 in _WORD.finditer(seg):
+                        _plain(m2.group(0), stopwords, max_len, out)
             continue
-        tok = tok.lower()
-        if len(tok) > max_len:
-            continue
-        if tok in stopwords:
-            continue
-        out.append(tok)
+        _plain(tok, stopwords, max_len, out)
     return out
+
+
+# CJKWidthFilter: full-width ASCII variants -> ASCII
+_FULLWIDTH = {c: c - 0xFEE0 for c in range(0xFF01, 0xFF5F)}
+_FULLWIDTH[0x3000] = 0x20
+
+
+def analyze_cjk_bigrams(text: str, stopwords=ENGLISH_STOPWORDS, max_len: int = 255) -> List[str]:
+    """Lucene ``CJKAnalyzer`` (``LuceneTextAnalyzer.scala``: Korean, Simplified and Traditional Chinese; English
+    stop words): StandardTokenizer, CJKWidthFilter, lowercase, CJKBigramFilter over all four CJK scripts,
+    stop filter. Adjacent CJK characters -- with no character between them in the text -- form one run; a run
+    emits its overlapping bigrams, a run of one character the character itself. Other tokens pass through
+    (``TextTokenizerTest.scala:145-181``: sliding 2-grams that do not cross spaces or punctuation)."""
+    text = text.translate(_FULLWIDTH)
+    out: List[str] = []
+    for m in _WORD.finditer(text):
+        tok = m.group(0)
+        if not _CJK.search(tok):
+            _plain(tok, stopwords, max_len, out)
+            continue
+        run = ""
+        for seg, cjk in _segments(tok):
+            if cjk:
+                run += seg
+                continue
+            _flush_bigrams(run, out)
+            run = ""
+            for m2 in _WORD.finditer(seg):
+                _plain(m2.group(0), stopwords, max_len, out)
+        _flush_bigrams(run, out)
+    return out
+
+
+def _flush_bigrams(run: str, out: List[str]) -> None:
+    if len(run) == 1:
+        out.append(run)
+    else:
+        out.extend(run[k:k + 2] for k in range(len(run) - 1))
 
 
 def tokenize(text: Optional[str], to_lowercase: bool = True, min_token_length: int = 1,
