@@ -106,3 +106,25 @@ def test_stemming_language_tokenizer():
     assert list(de[0]) == ["haus", "strass"]
     es = check_transformer(TextTokenizer(default_language="es").set_input(f), ds)
     assert list(es[1]) == ["chic", "luz"]
+
+
+def test_russian_snowball_stemmer():
+    """Snowball Russian (RussianAnalyzer's SnowballFilter), expectations derived by hand from the published
+    algorithm (perfective gerund / adjectival with participle / verb / noun endings in RV, superlative, нн)."""
+    from transmogrifai_amd.utils.snowball import russian_stem
+    pairs = {"вазы": "ваз", "вавилонского": "вавилонск", "важная": "важн", "важнейшие": "важн", "вагоне": "вагон",
+             "читаешь": "чита", "столами": "стол", "длинный": "длин", "сделавший": "сдела", "бегущий": "бегущ",
+             "радости": "радост", "книги": "книг"}
+    assert {w: russian_stem(w) for w in pairs} == pairs
+    assert LG.analyze("Все счастливые семьи похожи друг на друга", "ru") == ["счастлив", "сем", "похож", "друг",
+                                                                           "друг"]
+
+
+def test_dutch_snowball_stemmer():
+    """Snowball Dutch with DutchAnalyzer's stem overrides (fiets, ei -> eier, kind -> kinder)."""
+    from transmogrifai_amd.utils.snowball import dutch_stem
+    pairs = {"lichamelijke": "licham", "opgaven": "opgav", "kinderen": "kinder", "fietsen": "fiets", "ei": "eier",
+             "boeken": "boek", "maanden": "maand", "gevaarlijk": "gevar", "vrijheden": "vrijheid",
+             "koninklijke": "konink"}
+    assert {w: dutch_stem(w) for w in pairs} == pairs
+    assert LG.analyze("De kinderen lopen met de fietsen naar huis", "nl") == ["kinder", "lop", "fiets", "huis"]

@@ -62,6 +62,20 @@ soient fusse fusses fût fussions fussiez fussent ayant ayante ayantes ayants eu
 aurai auras aura aurons aurez auront aurais aurait aurions auriez auraient avais avait avions aviez avaient eut eûmes
 eûtes eurent aie aies ait ayons ayez aient eusse eusses eût eussions eussiez eussent""".split())
 
+# Snowball stop lists of the Russian and Dutch analyzers
+STOPWORDS["ru"] = frozenset("""
+и в во не что он на я с со как а то все она так его но да ты к у же вы за бы по только ее мне было вот от меня еще нет
+о из ему теперь когда даже ну вдруг ли если уже или ни быть был него до вас нибудь опять уж вам ведь там потом себя
+ничего ей может они тут где есть надо ней для мы тебя их чем была сам чтоб без будто чего раз тоже себе под будет ж
+тогда кто этот того потому этого какой совсем ним здесь этом один почти мой тем чтобы нее сейчас были куда зачем всех
+никогда можно при наконец два об другой хоть после над больше тот через эти нас про всего них какая много разве три
+эту моя впрочем хорошо свою этой перед иногда лучше чуть том нельзя такой им более всегда конечно всю между""".split())
+STOPWORDS["nl"] = PROFILES["nl"] | frozenset("""
+de en van ik te dat die in een hij het niet zijn is was op aan met als voor had er maar om hem dan zou of wat mijn men
+dit zo door over ze zich bij ook tot je mij uit der daar haar naar heb hoe heeft hebben deze u want nog zal me zij nu
+ge geen omdat iets worden toch al waren veel meer doen toen moet ben zonder kan hun dus alles onder ja eens hier wie
+werd altijd doch wordt wezen kunnen ons zelf tegen na reeds wil kon niets uw iemand geweest andere""".split())
+
 _ELISIONS = {"fr": ("l", "m", "t", "qu", "n", "s", "j", "d", "c", "jusqu", "quoiqu", "lorsqu", "puisqu"),
              "it": ("c", "l", "all", "dall", "dell", "nell", "sull", "coll", "pell", "gl", "agl", "dagl",
                     "degl", "negl", "sugl", "un", "m", "t", "s", "v", "d"),
