@@ -307,6 +307,8 @@ def _timed(args, one_run, expected_configs, use_gpu, dev, torch, D, sim, n_raw, 
             "configs_evaluated": len(summ.get("validationResults") or []) if summ else 0,
             "peak_hbm_gb_per_gpu": round(peak / 1e9, 3),
             "dp_gather_fallbacks": sorted(set(_all_fallbacks)),
+            "schedule": {k: v[0] if v[0] != "hybrid" else f"hybrid:{v[3]}" for k, v in
+                         (summ.get("schedule") or {}).items()} if summ else {},
             "config": {"name": args.config,
                        "model": _selector_cls(args).__name__ + "(" +
                                 ("default grid" if args.models == "default" else args.models) + ")",

@@ -12,10 +12,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(gpus, config, rows, models):
+def _bench(gpus, config, rows, models, **env_extra):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--device", "cpu", "--rows", str(rows),
            "--steps", "1", "--warmup", "0", "--config", config, "--models", models]
-    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env = dict(os.environ, OMP_NUM_THREADS="2", **env_extra)
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith('{"metric"')][-1]
@@ -37,3 +37,18 @@ def test_bench_many_ranks_matches_one_rank(config, rows, models, ranks):
     assert four["configs_evaluated"] == one["configs_evaluated"]
     key = [k for k in one if k.startswith("holdout_")][0]
     assert abs(four[key] - one[key]) <= 1e-9, (key, one[key], four[key])
+
+
+@pytest.mark.parametrize("mode,lanes", [("hybrid:2", "1"), ("shard", "2")])
+def test_bench_hybrid_groups_and_lanes_match_one_rank(mode, lanes):
+    """4 gloo ranks with every intra-job-parallel learner forced onto 2 groups of 2 ranks (parallel/scheduler.py
+    hybrid: LR row-parallel and XGBoost feature-parallel inside each group, jobs dealt to the groups), and with
+    all-shard schedules run in 2 learner lanes per rank: the 1-rank selection is reproduced."""
+    models = "OpLogisticRegression,OpRandomForestClassifier,OpXGBoostClassifier"
+    one = _bench(1, "binary-10m", 6000, models)
+    many = _bench(4, "binary-10m", 6000, models, TMOG_PARALLEL_MODE=mode, TMOG_LEARNER_LANES=lanes)
+    assert many["best_model"] == one["best_model"]
+    assert many["configs_evaluated"] == one["configs_evaluated"]
+    assert abs(many["holdout_aupr"] - one["holdout_aupr"]) <= 1e-9
+    want = {"OpLogisticRegression": mode, "OpXGBoostClassifier": mode, "OpRandomForestClassifier": "shard"}
+    assert many["schedule"] == want, many["schedule"]

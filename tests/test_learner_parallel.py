@@ -233,3 +233,32 @@ def test_row_parallel_normal_equations(tmp_path):
     outs = _run("_linreg_normal_rp", tmp_path, 2)
     assert outs[0] == outs[1]
     np.testing.assert_allclose(np.asarray(outs[0]), np.asarray(ref), rtol=0, atol=1e-6)
+
+
+def _trees_groups(rank, world):
+    """Hybrid schedule building block: the 4 ranks form 2 groups of 2 (parallel/dist.py partition, created
+    collectively); each group grows the trees feature-parallel over its own 2 ranks and its own gloo
+    subgroup, group 1 with a delay so the groups' exchanges interleave."""
+    from transmogrifai_amd.parallel import dist as D
+    from transmogrifai_amd.parallel.learner_parallel import LearnerParallel
+    grp = D.partition(2)
+    assert grp.world == 2 and grp.ranks == ((0, 1) if rank < 2 else (2, 3)) and grp.rank == rank % 2
+    assert D.partition(2) is grp                      # cached: no second collective creation
+    if rank >= 2:
+        import time
+        time.sleep(0.2)
+    out = _trees(LearnerParallel(group=grp))
+    out["lr"] = _linear(LearnerParallel(group=grp))["lr"]
+    return out
+
+
+def test_rank_groups_feature_and_row_parallel(tmp_path):
+    ref = _trees(None)
+    ref_lr = _linear(None)["lr"]
+    outs = _run("_trees_groups", tmp_path, 4)
+    for r, o in enumerate(outs):
+        for k in ("xgb", "gbt", "dt"):
+            assert o[k] == ref[k], f"{k} forest differs on rank {r} (groups of 2)"
+        # same optimum up to the optimizer tolerance (fp32 partial sums in another order), as for the world
+        np.testing.assert_allclose(np.asarray(o["lr"]), np.asarray(ref_lr), rtol=0, atol=1.5e-3)
+    assert outs[0]["lr"] == outs[1]["lr"] and outs[2]["lr"] == outs[3]["lr"]   # identical inside a group

@@ -79,3 +79,31 @@ def test_projection_mode_collectives():
     finally:
         D.simulate(0, 1)
     assert not D.simulated() and not D.is_dist()
+
+
+def test_hybrid_group_beats_both_pure_modes():
+    """2 long XGBoost jobs on 8 ranks: sharding leaves 6 ranks idle, spreading both over all 8 replicates the
+    serial part twice on every rank; 2 groups of 4 ranks, one job each, beat both."""
+    models = [("OpXGBoostClassifier", [dict(num_round=200, max_depth=10)])]
+    ch = S.choose(models, 2, 1_000_000, 330, 8, _par, lambda n, p: 10.0)[0]
+    assert ch.mode == "hybrid" and ch.group_size == 4, ch
+    assert ch.hybrid_s < ch.shard_s and ch.hybrid_s < ch.spread_s
+    assert set(ch.options) == {1, 2, 4, 8}
+    rows = S.project(models, {0: ch}, 2, 8, lambda n, p: 10.0)
+    assert rows[0]["mode"] == "hybrid" and rows[0]["group_size"] == 4
+    per = rows[-1]["per_rank_s"]
+    assert max(per) == min(per) and abs(max(per) - ch.hybrid_s) < 0.5      # both groups carry one job
+
+
+def test_forced_hybrid_size(monkeypatch):
+    monkeypatch.setenv("TMOG_PARALLEL_MODE", "hybrid:2")
+    ch = S.choose([("OpXGBoostClassifier", F._xgb_bin_grid())], 3, 1000, 10, 4, _par, lambda n, p: 0.2)[0]
+    assert ch.mode == "hybrid" and ch.group_size == 2
+    monkeypatch.setenv("TMOG_PARALLEL_MODE", "hybrid:3")      # not a divisor: the best hybrid size
+    ch = S.choose([("OpXGBoostClassifier", F._xgb_bin_grid())], 3, 1000, 10, 4, _par, lambda n, p: 0.2)[0]
+    assert ch.mode == "hybrid" and ch.group_size == 2
+
+
+def test_assign_groups_is_lpt_and_deterministic():
+    assert S.assign_groups([5, 1, 4, 2], 2) == [0, 0, 1, 1]
+    assert S.assign_groups([1.0] * 6, 3) == [0, 1, 2, 0, 1, 2]

@@ -75,25 +75,81 @@ def _comm_device(t: torch.Tensor):
     return t.device
 
 
-def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+class RankGroup:
+    """A subset of the ranks that runs collectives of its own: ``ranks`` (global ranks, ascending), this
+    process's ``rank`` inside it and the ``torch.distributed`` group (None in projection mode)."""
+
+    def __init__(self, ranks: Sequence[int], pg=None, cpu_pg=None):
+        self.ranks = tuple(int(r) for r in ranks)
+        self.pg = pg
+        self.cpu_pg = cpu_pg        # gloo twin for host-memory collectives when the main backend is nccl
+        me = rank()
+        self.rank = self.ranks.index(me) if me in self.ranks else -1
+        self.world = len(self.ranks)
+
+    @property
+    def leader(self) -> int:
+        return self.ranks[0]
+
+
+_PARTITIONS: dict = {}
+
+
+def partition(group_size: int) -> RankGroup:
+    """The group of ``group_size`` consecutive ranks this rank belongs to, out of ``world / group_size``
+    groups. Creating process groups is collective over ALL ranks (every rank creates every group, in the
+    same order), so every rank must call this at the same point; results are cached per size."""
+    n = world()
+    if group_size <= 0 or n % group_size != 0:
+        raise ValueError(f"group size {group_size} does not divide the world {n}")
+    if group_size in _PARTITIONS:
+        return _PARTITIONS[group_size]
+    me = rank()
+    mine = None
+    for g in range(n // group_size):
+        ranks_g = list(range(g * group_size, (g + 1) * group_size))
+        pg = cpu = None
+        if _SIM is None and is_dist() and group_size < n:
+            pg = dist.new_group(ranks=ranks_g)
+            if dist.get_backend() != "gloo":
+                cpu = dist.new_group(ranks=ranks_g, backend="gloo")
+        elif _SIM is None and is_dist():
+            pg = dist.group.WORLD
+        if me in ranks_g:
+            mine = RankGroup(ranks_g, pg, cpu)
+    _PARTITIONS[group_size] = mine
+    return mine
+
+
+def _pg(group):
+    return group.pg if isinstance(group, RankGroup) else group
+
+
+def _gsize(group) -> int:
+    if isinstance(group, RankGroup):
+        return group.world
+    return world()
+
+
+def all_reduce(t: torch.Tensor, op: str = "sum", group=None) -> torch.Tensor:
     if _SIM is not None:
-        return t * _SIM[1] if op == "sum" else t.clone()
-    if not is_dist():
+        return t * _gsize(group) if op == "sum" else t.clone()
+    if not is_dist() or _gsize(group) <= 1:
         return t
     dev = _comm_device(t)
     x = t.to(dev)
     o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
-    dist.all_reduce(x, op=o)
+    dist.all_reduce(x, op=o, group=_pg(group))
     return x.to(t.device)
 
 
-def bucketed_all_reduce(tensors: Sequence[torch.Tensor], op: str = "sum") -> List[torch.Tensor]:
+def bucketed_all_reduce(tensors: Sequence[torch.Tensor], op: str = "sum", group=None) -> List[torch.Tensor]:
     """Flatten, reduce once, unflatten (same dtype required per bucket; mixed dtypes go via float64)."""
     if not is_dist() or not tensors:
         return list(tensors)
     dt = torch.float64
     flat = torch.cat([t.reshape(-1).to(dt) for t in tensors])
-    flat = all_reduce(flat, op)
+    flat = all_reduce(flat, op, group)
     out, off = [], 0
     for t in tensors:
         n = t.numel()
@@ -113,11 +169,13 @@ def all_gather_object(obj) -> list:
     return out
 
 
-def broadcast_object(obj, src: int = 0):
-    if _SIM is not None or not is_dist():
+def broadcast_object(obj, src: int = 0, group=None):
+    """``src`` is a global rank (the group's leader for a :class:`RankGroup`)."""
+    if _SIM is not None or not is_dist() or _gsize(group) <= 1:
         return obj
     box = [obj]
-    dist.broadcast_object_list(box, src=src)
+    pg = group.cpu_pg or group.pg if isinstance(group, RankGroup) else group
+    dist.broadcast_object_list(box, src=src, group=pg)
     return box[0]
 
 

@@ -43,11 +43,15 @@ class FeatureParallel:
     process: rank 0's unique id is broadcast through ``torch.distributed``, every rank joins on its
     current device. CPU: an all-gather callback over a gloo group (the tests' multi-process path)."""
 
-    _comms: Dict[Tuple[int, int, int, int], int] = {}
+    _comms: Dict[tuple, int] = {}
 
-    def __init__(self, rank: Optional[int] = None, world: Optional[int] = None):
-        self.rank = D.rank() if rank is None else rank
-        self.world = D.world() if world is None else world
+    def __init__(self, rank: Optional[int] = None, world: Optional[int] = None, group: Optional[D.RankGroup] = None):
+        self.group = group
+        if group is not None:
+            self.rank, self.world = group.rank, group.world
+        else:
+            self.rank = D.rank() if rank is None else rank
+            self.world = D.world() if world is None else world
         self._cpu_group = None
         self._cb = None
 
@@ -57,8 +61,9 @@ class FeatureParallel:
         lib = N.hip()
         dev = device.index if device.index is not None else torch.cuda.current_device()
         handles = []
+        members = self.group.ranks if self.group is not None else tuple(range(self.world))
         for g in range(n_groups):
-            key = (dev, self.world, self.rank, g)
+            key = (dev, members, self.rank, g)
             h = FeatureParallel._comms.get(key)
             if h is None:
                 uid = None
@@ -68,7 +73,9 @@ class FeatureParallel:
                     if n <= 0:
                         raise RuntimeError("ncclGetUniqueId failed")
                     uid = buf.raw[:n]
-                uid = D.broadcast_object(uid, 0)
+                # the group's leader (rank 0 of the group) generated it; broadcast inside the group
+                uid = D.broadcast_object(uid, members[0], self.group) if self.group is not None \
+                    else D.broadcast_object(uid, 0)
                 with torch.cuda.device(dev):
                     h = lib.tmog_hip_rccl_comm_init(C.c_char_p(uid), self.world, self.rank)
                 if not h:
@@ -84,7 +91,10 @@ class FeatureParallel:
         import torch.distributed as dist
         if self._cb is not None:
             return self._cb
-        if D.is_dist() and dist.get_backend() != "gloo":
+        if self.group is not None:
+            # a rank subgroup: its gloo twin was created collectively with it (dist.partition)
+            self._cpu_group = self.group.cpu_pg or self.group.pg
+        elif D.is_dist() and dist.get_backend() != "gloo":
             self._cpu_group = dist.new_group(backend="gloo")
         world, grp = self.world, self._cpu_group
 
@@ -109,12 +119,18 @@ class FeatureParallel:
 
 
 class LearnerParallel:
-    """What a learner needs to split one batch of jobs over all ranks."""
+    """What a learner needs to split one batch of jobs over all ranks, or over the ranks of one
+    :class:`parallel.dist.RankGroup` (hybrid schedules: each group of ranks runs its own jobs, every job
+    spread over the group, parallel/scheduler.py)."""
 
-    def __init__(self, rank: Optional[int] = None, world: Optional[int] = None):
-        self.rank = D.rank() if rank is None else rank
-        self.world = D.world() if world is None else world
-        self.fp = FeatureParallel(self.rank, self.world)
+    def __init__(self, rank: Optional[int] = None, world: Optional[int] = None, group: Optional[D.RankGroup] = None):
+        self.group = group
+        if group is not None:
+            self.rank, self.world = group.rank, group.world
+        else:
+            self.rank = D.rank() if rank is None else rank
+            self.world = D.world() if world is None else world
+        self.fp = FeatureParallel(self.rank, self.world, group)
 
     # -- rows ------------------------------------------------------------------------------------
     def row_slice(self, n: int) -> slice:
@@ -127,7 +143,7 @@ class LearnerParallel:
         """Element-wise sum over ranks of several tensors in one collective (float64 on the wire)."""
         if self.world <= 1:
             return list(tensors)
-        return D.bucketed_all_reduce(list(tensors), "sum")
+        return D.bucketed_all_reduce(list(tensors), "sum", self.group)
 
 
 def feature_slices(n_multi: int, one_weights: Sequence[float], world: int,

@@ -8,6 +8,7 @@ hold-out evaluation of ``HasTestEval`` (``ModelSelectorNames.scala:73-123``).
 from __future__ import annotations
 
 import logging
+import math
 import os
 import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple
@@ -220,6 +221,10 @@ class ModelSelector(BinaryEstimator):
             "failures": res.failures,
             "timings": dict(res.timings, selector_total=time.time() - t0),
         }
+        sched = getattr(self.validator, "last_schedule", None)
+        if sched:        # multi-rank: per learner (mode, shard s, spread s, ranks per group, hybrid s)
+            summary["schedule"] = {k: [x if not (isinstance(x, float) and not math.isfinite(x)) else None
+                                       for x in v] for k, v in sched.items()}
         self.metadata[SUMMARY_KEY] = summary
         m = SelectedModel(res.best_learner, state, params)
         m.evaluators = list(self.evaluators)

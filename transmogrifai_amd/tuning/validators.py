@@ -91,16 +91,31 @@ def _scaled_cost(learner: str, params: Dict, n: int, d: int) -> float:
     return _job_cost(learner, params, n, d) * _COST_SCALE.get(learner, _DEFAULT_SCALE)
 
 
-def _calibrate(models, jobs, owner, timings, n: int, d: int):
-    """Update the per-learner seconds-per-unit from this validation's measured (max over ranks) times."""
+def SCH_SERIAL(mode) -> float:
+    from ..parallel.scheduler import SERIAL_FRACTION
+    return SERIAL_FRACTION.get(mode, 0.0)
+
+
+def _calibrate(models, jobs, owner, timings, n: int, d: int, spread=None):
+    """Update the per-learner seconds-per-unit from this validation's measured (max over ranks) times.
+    ``spread``: learner -> (ranks per job, replicated fraction) of the spread / hybrid learners, whose measured
+    time is divided back to single-rank seconds with the scheduler's speed-up model; sharded learners divide
+    by the ranks their jobs ran on."""
+    spread = spread or {}
     for li, (lname, grid) in enumerate(models):
         t = timings.get(lname)
         mine = [j for j, (l, g, k) in enumerate(jobs) if l == li]
         if not t or not mine:
             continue
         units = sum(_job_cost(lname, grid[jobs[j][1]], n, d) for j in mine)
-        ranks = max(1, len({owner[j] for j in mine}))
-        if units > 0:
+        if units <= 0:
+            continue
+        if li in spread:
+            gsz, s = spread[li]
+            groups = max(1, D.world() // max(1, gsz))
+            _COST_SCALE[lname] = float(t) * groups / (units * (s + (1.0 - s) / max(1, gsz)))
+        else:
+            ranks = max(1, len({owner[j] for j in mine}))
             _COST_SCALE[lname] = float(t) * ranks / units
 
 
@@ -201,51 +216,71 @@ class OpValidator:
         # shard whole jobs or spread every job over the ranks: per learner, by the calibrated cost model
         # (parallel/scheduler.py); rank 0's choice is broadcast so every rank runs the same collectives
         spread = set()
+        hybrid: Dict[int, int] = {}          # learner -> ranks per group
+        pars: Dict[int, Any] = {}            # learner -> its intra-job parallel context
         if par is not None:
             from ..parallel import scheduler as SCH
             choices = SCH.choose(models, n_folds, n_tr, X.shape[1], world,
                                  lambda name: learner_class(name).parallel,
                                  lambda name, p: _scaled_cost(name, p, n_tr, X.shape[1]))
-            spread = {li for li, c in choices.items() if c.mode == "spread"}
-            spread = set(D.broadcast_object(sorted(spread), 0))
-            self.last_schedule = {models[li][0]: (c.mode, c.shard_s, c.spread_s) for li, c in choices.items()}
-        sharded = [j for j, (li, gi, k) in enumerate(jobs) if li not in spread]
+            dec = D.broadcast_object(sorted((li, c.mode, c.group_size) for li, c in choices.items()), 0)
+            spread = {li for li, m, _ in dec if m == "spread"}
+            hybrid = {li: int(g) for li, m, g in dec if m == "hybrid"}
+            self.last_schedule = {models[li][0]: (c.mode, c.shard_s, c.spread_s, c.group_size, c.hybrid_s)
+                                  for li, c in choices.items()}
+            pars = {li: par for li in spread}
+        sharded = [j for j, (li, gi, k) in enumerate(jobs) if li not in spread and li not in hybrid]
         costs = [_scaled_cost(models[jobs[j][0]][0], models[jobs[j][0]][1][jobs[j][1]], n_tr, X.shape[1])
                  for j in sharded]
         owner = [me] * len(jobs)
         for j, w in zip(sharded, D.lpt_assign(costs, world)):
             owner[j] = w
+        # hybrid learners: every rank creates every subgroup (collective), then the learner's jobs are dealt to the
+        # groups by LPT; this rank runs its group's jobs, each spread over the group
+        for li in sorted(hybrid):
+            from ..parallel import scheduler as SCH
+            from ..parallel.learner_parallel import LearnerParallel
+            g = hybrid[li]
+            grp = D.partition(g)
+            pars[li] = LearnerParallel(group=grp)
+            lj = [j for j, (l, _, _) in enumerate(jobs) if l == li]
+            lc = [_scaled_cost(models[li][0], models[li][1][jobs[j][1]], n_tr, X.shape[1]) for j in lj]
+            for j, k in zip(lj, SCH.assign_groups(lc, world // g)):
+                owner[j] = me if k == me // g else -1
         ctx = context if context is not None else {}
         results: Dict[Tuple[int, int, int], float] = {}
         failures = []
         timings = {}
         # spread learners first (all ranks in lockstep through their collectives), then the shards
-        order = sorted(range(len(models)), key=lambda li: (li not in spread, li))
-        lanes = self._learner_lanes(X, world, len(order))
+        order = sorted(range(len(models)), key=lambda li: (li not in spread, li not in hybrid, li))
+        lanes = self._learner_lanes(X, world, len(order), n_collective=len(pars))
         if lanes > 1:
             results, failures, timings = self._fit_eval_concurrent(models, order, jobs, owner, me, X, y, train_rows,
-                                                                   val_rows, ctx, t0, lanes, n_tr)
+                                                                   val_rows, ctx, t0, lanes, n_tr, pars)
             order = []
         for li in order:
             lname, grid = models[li]
             mine = [(j, (l, g, k)) for j, (l, g, k) in enumerate(jobs) if l == li and owner[j] == me]
-            if not mine:
+            collective = li in pars
+            if not mine and not collective:
                 continue
             # maxWait (OpValidator.scala:348, default 1 day): learners not started in time are dropped;
-            # spread learners take rank 0's decision so every rank skips the same collectives
+            # spread / hybrid learners take rank 0's decision so every rank skips the same collectives
             late = time.time() - t0 > self.max_wait
-            if li in spread:
+            if collective:
                 late = bool(D.broadcast_object(late, 0))
             if late:
                 failures.append(f"{lname}: not started within maxWait={self.max_wait}s")
                 continue
+            if not mine:            # a hybrid group without jobs of this learner
+                continue
             t1 = time.time()
             # the context dict is shared (tree binning cache) -- the parallel context is set only
-            # around the spread learners
-            if li in spread:
-                ctx["par"] = par
+            # around the spread / hybrid learners
+            if collective:
+                ctx["par"] = pars[li]
             try:
-                if li not in spread and self.max_wait < _UNBOUNDED_WAIT:
+                if not collective and self.max_wait < _UNBOUNDED_WAIT:
                     res, fails = self._fit_eval_bounded(lname, grid, mine, X, y, train_rows, val_rows, ctx,
                                                         self.max_wait - (time.time() - t0))
                 else:
@@ -269,7 +304,8 @@ class OpValidator:
                     allfail.append(x)
             for k, v in tm.items():
                 timings[k] = max(timings.get(k, 0.0), v)
-        _calibrate(models, jobs, owner, timings, n_tr, X.shape[1])
+        _calibrate(models, jobs, owner, timings, n_tr, X.shape[1],
+                   {li: (p.world, SCH_SERIAL(learner_class(models[li][0]).parallel)) for li, p in pars.items()})
         return self._select(models, allres, n_folds, allfail, timings, t0)
 
     def validate_with_dag(self, models: Sequence[Tuple[str, Sequence[Dict]]], data, label_name: str,
@@ -436,7 +472,7 @@ class OpValidator:
             off += int(Xk.shape[0])
         return torch.cat(blocks), torch.cat(ys), train_rows, val_rows
 
-    def _learner_lanes(self, X, world: int, n_learners: int) -> int:
+    def _learner_lanes(self, X, world: int, n_learners: int, n_collective: int = 0) -> int:
         """Learners fitted at once on one GPU (``parallelism``, OpValidator.scala:377: the reference runs up to 8
         fits as concurrent futures). Only single-rank: spread learners move through collectives in lockstep.
         Default on the GPU: 2 lanes (``TMOG_LEARNER_LANES`` overrides). The longest learner (XGBoost on the
@@ -447,13 +483,18 @@ class OpValidator:
         than hardware queues: 1.95 s; profiles/r4_lanes_*.log, docs/ROUND4.md)."""
         env = os.environ.get("TMOG_LEARNER_LANES")
         # host-only runs stay sequential unless asked for (the CPU kernels already use every core)
-        if world > 1 or n_learners < 2 or not isinstance(X, torch.Tensor) or not (X.is_cuda or env):
+        if n_learners < 2 or not isinstance(X, torch.Tensor) or not (X.is_cuda or env):
+            return 1
+        # several ranks: lanes only when at most one learner runs collectives (the others' jobs are local to the
+        # rank) and maxWait is unbounded (a deadline could cancel a collective fit on one rank and not another)
+        if world > 1 and (n_collective > 1 or (n_collective and self.max_wait < _UNBOUNDED_WAIT)):
             return 1
         from ..models.tree_engine import N_SLOTS, SLOT_LANE
         cap = int(env) if env else 2
         return max(1, min(cap, n_learners, N_SLOTS // SLOT_LANE))
 
-    def _fit_eval_concurrent(self, models, order, jobs, owner, me, X, y, train_rows, val_rows, ctx, t0, lanes, n_tr):
+    def _fit_eval_concurrent(self, models, order, jobs, owner, me, X, y, train_rows, val_rows, ctx, t0, lanes, n_tr,
+                             pars=None):
         """Every learner's batch on one of ``lanes`` worker threads, each with its own HIP stream (ordered after
         the caller's, which waits for all of them) and its own range of native tree-grower slots, longest
         estimated learner first. One learner's host round trips (OWL-QN line searches, tree levels, early-stopping
@@ -473,6 +514,12 @@ class OpValidator:
                 cost = sum(_scaled_cost(lname, grid[g], n_tr, X.shape[1]) for _, (_, g, _) in mine)
                 todo.append((cost, li, mine))
         todo.sort(key=lambda t: -t[0])
+        pars = pars or {}
+        if pars:     # copies of the context must share its caches: create them before the lanes copy it
+            ctx.setdefault("refit_states", {})
+            if any(getattr(learner_class(models[li][0]), "parallel", None) == "features" for li in pars):
+                from ..models.trees import _ctx as _tree_ctx
+                _tree_ctx(X, ctx)
         results: Dict[Tuple[int, int, int], float] = {}
         failures: List[str] = []
         timings: Dict[str, float] = {}
@@ -515,7 +562,9 @@ class OpValidator:
                                 continue
                             started.add(li)
                         t1 = time.time()
-                        res, fails = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, ctx)
+                        # the collective learner's view of the shared context carries its parallel context
+                        lctx = dict(ctx, par=pars[li]) if li in pars else ctx
+                        res, fails = self._fit_eval(lname, grid, mine, X, y, train_rows, val_rows, lctx)
                         with lock:
                             results.update(res)
                             failures.extend(fails)
