@@ -8,6 +8,8 @@ and returns a metrics dict; ``evaluate`` returns the single selection metric.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Callable, Dict, Optional
 
 import torch
@@ -97,13 +99,26 @@ class OpBinaryClassificationEvaluator(OpEvaluatorBase):
         # fp32 scores stay fp32 (one packed-key sort); anything else is compared in fp64
         S = torch.stack(sc) if all(t.dtype == torch.float32 for t in sc) else \
             torch.stack([t.to(torch.float64) for t in sc])
-        aupr, auroc = M.binary_areas_batch(S, y)
+        if S.is_cuda:       # one HIP launch for all curves (metric_kernels.hip)
+            aupr, auroc = M.binary_areas_device(S, y)
+        elif os.environ.get("TMOG_BATCH_METRIC") == "1":
+            aupr, auroc = M.binary_areas_batch(S, y)
+        else:               # host: one curve per model (binary_curves)
+            return [M.binary_curves(t, y, 0)[self.metric] for t in sc]
         return (aupr if self.metric == "AuPR" else auroc).tolist()
+
+    @property
+    def batch_default(self) -> bool:
+        """The validator scores all models of a fold in one batch by default on the GPU (the HIP curve kernel
+        has no [J, n] torch temporaries); TMOG_BATCH_METRIC=0 / 1 overrides."""
+        return self.metric in ("AuPR", "AuROC")
 
     def selection_metric(self, y, pred, raw, prob):
         # BinaryClassificationEvaluator on rawPrediction, exact curve (numBins = 0)
         if self.metric in ("AuPR", "AuROC"):
             s = raw[:, 1] if (raw is not None and raw.numel() and raw.shape[1] >= 2) else _score(raw, prob, pred)
+            if s.is_cuda:
+                return self.selection_metric_batch(y, [(pred, raw, prob)])[0]
             c = M.binary_curves(s, y, 0)
             return c[self.metric]
         if self.metric == "Error":

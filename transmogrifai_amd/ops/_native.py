@@ -124,6 +124,7 @@ _HIP_SIGS = {
     "tmog_hip_date_unit_circle": [P, P, I64, I32, I32, I32, P, I64, I64, P],
     "tmog_hip_rff_summary": [P, P, P, I64, I32, P, I32, P, P],
     "tmog_hip_rff_hist": [P, P, P, I64, I32, P, P, I32, P, P],
+    "tmog_hip_binary_areas": [P, I32, P, I64, I32, P, P, P, P],
 }
 
 

@@ -190,7 +190,8 @@ class ModelSelector(BinaryEstimator):
         ctx.pop("refit_job", None)
         # the winner's refit uses the same intra-job parallelism over the ranks as its CV fits
         from ..parallel import dist as D
-        if D.world() > 1 and learner.parallel in ("rows", "features"):
+        # (projection mode answers collectives locally but cannot emulate the tree grower's RCCL exchange: local refit)
+        if D.world() > 1 and not D.simulated() and learner.parallel in ("rows", "features"):
             from ..parallel.learner_parallel import LearnerParallel
             ctx["par"] = LearnerParallel()
         try:
