@@ -1,8 +1,12 @@
 """Selection-metric microbenchmark: exact AuPR of J score sets over n validation rows (the RF grid's 18 x 3 folds
 on the headline: J = 18 per fold, n = 333K), per-model torch curves vs the batched HIP curve kernel."""
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from transmogrifai_amd.evaluators import metrics as M
 

@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -554,13 +554,21 @@ class LogisticRegressionLearner(_LinearBase):
             return []
         if any("coefficient_matrix" in s for s in states):
             return Learner.predict_batch(self, states, X, rows, context)
-        C = torch.as_tensor(np.stack([s["coefficients"] for s in states], 1), dtype=X.dtype, device=X.device)
-        b = torch.as_tensor([s["intercept"] for s in states], dtype=torch.float64, device=X.device)
-        M = LK.gemm(X, C).to(torch.float64) + b[None, :]
-        out = []
-        for p, (s, r) in enumerate(zip(states, rows)):
-            m = M[:, p] if r is None else M[r, p]
-            out.append(probability_outputs(m, threshold=s.get("threshold", 0.5)))
+        # margins only of the rows each model is scored on: the models of one validation fold share its rows
+        # (one GEMM per fold over those rows, not one over every fold's rows for every model)
+        groups: Dict[tuple, List[int]] = {}
+        for p, r in enumerate(rows):
+            key = ("all",) if r is None else (r.data_ptr(), int(r.numel()), str(r.device))
+            groups.setdefault(key, []).append(p)
+        out: List = [None] * len(states)
+        for key, ps in groups.items():
+            r = rows[ps[0]]
+            Xr = X if r is None else X.index_select(0, r.to(X.device))     # a gather: no host synchronisation
+            C = torch.as_tensor(np.stack([states[p]["coefficients"] for p in ps], 1), dtype=X.dtype, device=X.device)
+            b = torch.as_tensor([states[p]["intercept"] for p in ps], dtype=torch.float64, device=X.device)
+            M = LK.gemm(Xr, C).to(torch.float64) + b[None, :]
+            for c, p in enumerate(ps):
+                out[p] = probability_outputs(M[:, c], threshold=states[p].get("threshold", 0.5))
         return out
 
     def feature_contributions(self, state, d):
