@@ -65,7 +65,7 @@ def parse():
                     help="multi-GPU table layout: row shards with all-reduced fit statistics (data parallel), "
                          "or the whole table on every rank")
     ap.add_argument("--verbose", action="store_true")
-    ap.add_argument("--ingest", default="memory", choices=["memory", "parquet"],
+    ap.add_argument("--ingest", default="memory", choices=["memory", "parquet", "csv"],
                     help="memory: the device-resident synthetic table is the reader's input (the headline); parquet: "
                          "the table is written to a Parquet file before timing and every timed train reads it "
                          "(readers/columnar.py) inside the timed region")
@@ -210,17 +210,19 @@ def main():
             if use_gpu:
                 torch.cuda.empty_cache()
         reader = None
-        if args.ingest == "parquet":
-            from transmogrifai_amd.readers.columnar import dataset_to_parquet
-            from transmogrifai_amd.readers.files import ParquetReader
+        if args.ingest in ("parquet", "csv"):
+            from transmogrifai_amd.readers.columnar import dataset_to_csv, dataset_to_parquet
+            from transmogrifai_amd.readers.files import CSVReader, ParquetReader
             if pq_path[0] is None:              # written once, untimed; the same seeded table every run
                 d = args.ingest_dir or "/tmp"
-                pq_path[0] = os.path.join(d, f"tmog_bench_{args.config}_{args.rows}_{os.getpid()}.parquet")
+                pq_path[0] = os.path.join(d, f"tmog_bench_{args.config}_{args.rows}_{os.getpid()}.{args.ingest}")
                 t_w = time.perf_counter()
-                dataset_to_parquet(ds, pq_path[0], names=[f.name for f in [label] + list(preds)])
+                (dataset_to_parquet if args.ingest == "parquet" else dataset_to_csv)(
+                    ds, pq_path[0], names=[f.name for f in [label] + list(preds)])
                 print(f"[ingest] wrote {pq_path[0]} ({os.path.getsize(pq_path[0]) / 1e9:.2f} GB) in "
                       f"{time.perf_counter() - t_w:.1f} s", file=sys.stderr, flush=True)
-            reader = ParquetReader(pq_path[0], device=dev)
+            reader = ParquetReader(pq_path[0], device=dev) if args.ingest == "parquet" else \
+                CSVReader(pq_path[0], has_header=True, device=dev)
             del ds
             ds = None
             if use_gpu:
@@ -253,8 +255,8 @@ def main():
         return dt, ho, summ
 
     expected_configs = _expected_configs(args)
-    if args.ingest == "parquet" and world > 1:
-        raise SystemExit("--ingest parquet is a single-GPU measurement")
+    if args.ingest != "memory" and world > 1:
+        raise SystemExit("--ingest parquet / csv is a single-GPU measurement")
     try:
         _timed(args, one_run, expected_configs, use_gpu, dev, torch, D, sim, n_raw, stage_t, gc_steps, world)
     finally:
@@ -332,10 +334,10 @@ def _timed(args, one_run, expected_configs, use_gpu, dev, torch, D, sim, n_raw, 
         if sim:
             out["simulated"] = {"rank": D.rank(), "world": D.world(),
                                 "note": "one rank's share timed on one GPU; collectives not executed"}
-        if args.ingest == "parquet":
-            out["config"]["ingest"] = "parquet"
-            out["data"] = ("synthetic (device-generated, seeded), written to a Parquet file before timing and read "
-                           "by every timed train (readers/columnar.py), random-init models")
+        if args.ingest != "memory":
+            out["config"]["ingest"] = args.ingest
+            out["data"] = (f"synthetic (device-generated, seeded), written to a {args.ingest} file before timing and "
+                           "read by every timed train (readers/columnar.py), random-init models")
         print(json.dumps(out), flush=True)
 
 

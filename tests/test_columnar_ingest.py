@@ -140,3 +140,56 @@ def test_columnar_parquet_non_null_nan_is_missing_gpu(tmp_path, monkeypatch):
     path = str(tmp_path / "nan.parquet")
     r64, r32 = _write_nan_table(path)
     _check_nan_read(path, "cuda", monkeypatch, r64, r32)
+
+
+def _csv_read(path, dev, columnar, monkeypatch, **kw):
+    monkeypatch.setenv("TMOG_COLUMNAR", "1" if columnar else "0")
+    from transmogrifai_amd.readers.files import CSVReader
+    return CSVReader(path, device=dev, **kw).generate_dataset(_features())
+
+
+def test_columnar_csv_equals_pandas_path_cpu(tmp_path, monkeypatch):
+    """CSV through pyarrow's parser into the columnar pipeline (readers/columnar.py csv_dataset) gives the
+    pandas path's dataset: values, null masks (pandas' NA strings), text dictionaries and codes, key."""
+    df = _frame(3000, seed=4)
+    path = str(tmp_path / "t.csv")
+    df.to_csv(path, index=False, na_rep="")
+    from transmogrifai_amd.readers import columnar
+    calls = []
+    orig = columnar._arrow_dataset
+    monkeypatch.setattr(columnar, "_arrow_dataset", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    fast = _csv_read(path, "cpu", True, monkeypatch, has_header=True)
+    assert calls, "columnar CSV path not taken"
+    slow = _csv_read(path, "cpu", False, monkeypatch, has_header=True)
+    _compare(fast, slow)
+
+
+def test_columnar_csv_schema_no_header_and_fallbacks(tmp_path, monkeypatch):
+    df = _frame(500, seed=6)
+    path = str(tmp_path / "n.csv")
+    df.to_csv(path, index=False, header=False, na_rep="NA")
+    schema = [("key", "string"), ("r32", "real"), ("r64", "real"), ("i", "integral"), ("cat", "string"),
+              ("txt", "string"), ("y", "real")]
+    fast = _csv_read(path, "cpu", True, monkeypatch, schema=schema)
+    slow = _csv_read(path, "cpu", False, monkeypatch, schema=schema)
+    _compare(fast, slow)
+    # a junk cell in a numeric column: Arrow cannot parse it, pandas coerces it to missing -> pandas path
+    bad = str(tmp_path / "b.csv")
+    df2 = df.copy()
+    df2["r64"] = df2["r64"].astype(object)
+    df2.loc[3, "r64"] = "oops"
+    df2.to_csv(bad, index=False)
+    from transmogrifai_amd.readers.columnar import csv_dataset
+    assert csv_dataset(bad, _features(), "cpu") is None
+    ds = _csv_read(bad, "cpu", True, monkeypatch, has_header=True)
+    assert not bool(ds["r64"].valid[3])
+
+
+@pytest.mark.gpu
+def test_columnar_csv_equals_pandas_path_gpu(tmp_path, monkeypatch):
+    path = str(tmp_path / "g.csv")
+    _frame(7000, seed=8).to_csv(path, index=False, na_rep="")
+    fast = _csv_read(path, "cuda", True, monkeypatch, has_header=True)
+    slow = _csv_read(path, "cuda", False, monkeypatch, has_header=True)
+    assert fast["r64"].values.is_cuda
+    _compare(fast, slow, same_dtype=False)

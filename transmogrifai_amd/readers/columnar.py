@@ -1,4 +1,5 @@
-"""Columnar Parquet -> device ingest (the fast path of :class:`~.files.ParquetReader`).
+"""Columnar Parquet / CSV -> device ingest (the fast paths of :class:`~.files.ParquetReader` and
+:class:`~.files.CSVReader`).
 
 Reference: ``ParquetProductReader.scala:47-90`` / ``DataReader.generateDataFrame`` (``DataReader.scala:57-198``)
 read Parquet into a Spark DataFrame of one column per raw feature. The generic path here (:mod:`.base`) goes
@@ -86,24 +87,116 @@ class _Slot:
         self.event = None
 
 
+class _ParquetSource:
+    """Row groups of a Parquet file (decoded on demand by pyarrow's multi-threaded reader)."""
+
+    def __init__(self, path):
+        import pyarrow.parquet as pq
+        self.pf = pq.ParquetFile(path)
+        self.schema = self.pf.schema_arrow
+        self.n = self.pf.metadata.num_rows
+        self.n_chunks = self.pf.metadata.num_row_groups
+
+    def read(self, i, cols):
+        return self.pf.read_row_group(i, columns=cols, use_threads=True)
+
+    def read_all(self, cols):
+        return self.pf.read(columns=cols, use_threads=True)
+
+
+class _TableSource:
+    """An in-memory Arrow table (e.g. a parsed CSV file) fed to the device pipeline in slices of ``rows``."""
+
+    def __init__(self, table, rows: int = 1 << 20):
+        self.table = table
+        self.schema = table.schema
+        self.n = table.num_rows
+        self.rows = max(1, rows)
+        self.n_chunks = (self.n + self.rows - 1) // self.rows
+
+    def read(self, i, cols):
+        return self.table.select(cols).slice(i * self.rows, self.rows)
+
+    def read_all(self, cols):
+        return self.table.select(cols)
+
+
 def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads: Optional[int] = None
                     ) -> Optional[Dataset]:
     """Dataset of ``raw_features`` from the Parquet file ``path`` on ``dev``, or None (use the generic path)."""
     try:
+        import pyarrow  # noqa: F401
+    except ImportError:
+        return None
+    if key_fn is not None:
+        return None
+    return _arrow_dataset(_ParquetSource(path), raw_features, torch.device(dev), threads)
+
+
+# pandas.read_csv's default NA strings (keep_default_na=True): the CSV fast path marks the same cells missing
+_PANDAS_NA = ["", "#N/A", "#N/A N/A", "#NA", "-1.#IND", "-1.#QNAN", "-NaN", "-nan", "1.#IND", "1.#QNAN", "<NA>",
+              "N/A", "NA", "NULL", "NaN", "None", "n/a", "nan", "null"]
+
+
+def csv_dataset(path: str, raw_features: Sequence, dev, names: Optional[Sequence[str]] = None,
+                has_header: bool = True, separator: str = ",", text_columns: Sequence[str] = (),
+                key_fn=None, threads: Optional[int] = None) -> Optional[Dataset]:
+    """Dataset of ``raw_features`` from the CSV file ``path`` (``CSVReaders.scala:54-122`` / ``CSVAutoReaders``)
+    on ``dev``, or None (use the pandas path): pyarrow's multi-threaded CSV parser builds the Arrow columns,
+    which then take the same pinned, double-buffered copy pipeline as Parquet row groups. Numeric features
+    parse as float64 / int64 (the pandas path's dtypes), pandas' NA strings are nulls, and a text feature is
+    taken only when Arrow types its column as strings (a numeric-looking column keeps the pandas path's
+    number-to-text rendering)."""
+    try:
         import pyarrow as pa
-        import pyarrow.compute as pc
-        import pyarrow.parquet as pq
+        import pyarrow.csv as pacsv
     except ImportError:
         return None
     if key_fn is not None:
         return None
     dev = torch.device(dev)
-    pf = pq.ParquetFile(path)
-    schema = pf.schema_arrow
+    want = {}
+    for f in raw_features:
+        st = f.origin_stage
+        if st.extract_fn is not None or st.column is None:
+            return None
+        if f.wtype.kind == "numeric" and not issubclass(f.wtype, T.Binary):
+            want[st.column] = pa.int64() if issubclass(f.wtype, T.Integral) else pa.float64()
+        elif f.wtype.kind == "text":
+            if st.column in text_columns:
+                want[st.column] = pa.string()
+        else:
+            return None
+    ro = pacsv.ReadOptions(column_names=list(names) if (names is not None and not has_header) else None,
+                           autogenerate_column_names=False, use_threads=True, block_size=1 << 24)
+    if names is not None and has_header:
+        ro = pacsv.ReadOptions(column_names=list(names), skip_rows=1, use_threads=True, block_size=1 << 24)
+    if names is None:               # header names (the first line), to know whether a key column exists
+        import csv
+        with open(path, newline="") as fh:
+            names = next(csv.reader(fh, delimiter=separator), [])
+    cols = list(dict.fromkeys(f.origin_stage.column for f in raw_features))
+    if any(c not in names for c in cols):
+        return None
+    co = pacsv.ConvertOptions(column_types=want, null_values=_PANDAS_NA, strings_can_be_null=True,
+                              include_columns=cols + (["key"] if "key" in names and "key" not in cols else []))
+    try:
+        table = pacsv.read_csv(path, read_options=ro, parse_options=pacsv.ParseOptions(delimiter=separator),
+                               convert_options=co)
+    except (pa.ArrowInvalid, pa.ArrowTypeError, KeyError, ValueError):
+        return None            # unparsable numbers, missing columns, ...: the pandas path decides
+    return _arrow_dataset(_TableSource(table), raw_features, dev, threads)
+
+
+def _arrow_dataset(src, raw_features: Sequence, dev: torch.device, threads: Optional[int] = None
+                   ) -> Optional[Dataset]:
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    schema = src.schema
     plan = _plan(schema, raw_features)
     if plan is None:
         return None
-    n = pf.metadata.num_rows
+    n = src.n
     num = [(f, c, k) for f, c, k in plan if k in ("real", "int")]
     txt = [(f, c, k) for f, c, k in plan if k == "text"]
     ncols = list(dict.fromkeys(c for _, c, _ in num))
@@ -116,10 +209,10 @@ def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads
     threads = threads or min(16, os.cpu_count() or 4)
     pool = cf.ThreadPoolExecutor(threads)
     prefetch = cf.ThreadPoolExecutor(1)
-    n_rg = pf.metadata.num_row_groups
+    n_rg = src.n_chunks
 
     def read(i):
-        return pf.read_row_group(i, columns=ncols, use_threads=True) if ncols else None
+        return src.read(i, ncols) if ncols else None
 
     def host_chunk(arr, c):
         """(values ndarray in the column's device dtype, validity bitmap bytes or None, bit offset)."""
@@ -150,6 +243,8 @@ def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads
         for g in range(n_rg):
             tab = fut.result()
             fut = prefetch.submit(read, g + 1) if g + 1 < n_rg else None
+            if tab is None:
+                continue
             rows = tab.num_rows
             pieces = []                  # (column, row offset, values ndarray, bitmap, bit offset)
             for c in ncols:
@@ -254,7 +349,7 @@ def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads
             raise T.NonNullableEmptyException(f"{f.wtype.__name__} column '{c}' contains empty values")
         cols[f.name] = NumericColumn(f.wtype, vals[c], ok)
     if txt:
-        tt = pf.read(columns=list(dict.fromkeys(c for _, c, _ in txt)), use_threads=True)
+        tt = src.read_all(list(dict.fromkeys(c for _, c, _ in txt)))
         enc = {}
         for f, c, _ in txt:
             if c not in enc:
@@ -268,7 +363,7 @@ def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads
     order = OrderedDict((f.name, cols[f.name]) for f in raw_features)
     key = None
     if "key" in schema.names:
-        key = pf.read(columns=["key"]).column("key").to_pandas().astype(str).to_numpy(dtype=object)
+        key = src.read_all(["key"]).column("key").to_pandas().astype(str).to_numpy(dtype=object)
     return Dataset(order, key, n)
 
 
@@ -299,6 +394,36 @@ def dataset_to_parquet(ds: Dataset, path: str, row_group_rows: int = 1 << 20, na
             if writer is None:
                 writer = pq.ParquetWriter(path, tab.schema, compression=compression)
             writer.write_table(tab, row_group_size=r1 - r0)
+    finally:
+        if writer is not None:
+            writer.close()
+
+
+def dataset_to_csv(ds: Dataset, path: str, row_group_rows: int = 1 << 20, names: Optional[Sequence[str]] = None) -> None:
+    """Write the numeric and text columns of ``ds`` to a CSV file with a header (empty cells for nulls), streaming
+    one slice of rows at a time through pyarrow's CSV writer. Used by ``bench.py --ingest csv``."""
+    import pyarrow as pa
+    import pyarrow.csv as pacsv
+    names = list(names) if names is not None else list(ds.columns)
+    writer = None
+    try:
+        for r0 in range(0, ds.n_rows, row_group_rows):
+            r1 = min(ds.n_rows, r0 + row_group_rows)
+            arrays = []
+            for nm in names:
+                c = ds[nm]
+                if isinstance(c, TextColumn):
+                    codes = c.codes[r0:r1].cpu().numpy().astype(np.int64)
+                    vocab = np.asarray(list(c.vocab) + [None], dtype=object)
+                    arrays.append(pa.array(vocab[np.where(codes < 0, len(c.vocab), codes)], type=pa.string()))
+                else:
+                    v = c.values[r0:r1].cpu().numpy()
+                    ok = c.valid[r0:r1].cpu().numpy()
+                    arrays.append(pa.array(v, mask=None if ok.all() else ~ok))
+            tab = pa.Table.from_arrays(arrays, names=names)
+            if writer is None:
+                writer = pacsv.CSVWriter(path, tab.schema)
+            writer.write_table(tab)
     finally:
         if writer is not None:
             writer.close()

@@ -40,9 +40,31 @@ class CSVReader(DataReader):
         if self.schema is not None and all(isinstance(s, (tuple, list)) for s in self.schema):
             m = {"string": str, "text": str}
             dtype = {n: m[k] for n, k in self.schema if k in m}
+        # round-trip float parsing: correctly rounded like Java's Double.parseDouble under Spark's CSV reader
+        # (pandas' default fast parser can be one ulp off) and like the Arrow parser of the columnar path
         df = pd.read_csv(path, header=0 if self.has_header else None, names=names, sep=self.separator,
-                         dtype=dtype, keep_default_na=True, skipinitialspace=False)
+                         dtype=dtype, keep_default_na=True, skipinitialspace=False, float_precision="round_trip")
         return df
+
+    def _path(self, params):
+        return params.path if (params is not None and getattr(params, "path", None)) else self.path
+
+    def generate_dataset(self, raw_features, params=None):
+        """Columnar fast path (readers/columnar.py csv_dataset: pyarrow's multi-threaded parser -> Arrow columns ->
+        pinned row-slice copies -> device) when every raw feature is a plain numeric / string column; the pandas
+        path otherwise (TMOG_COLUMNAR=0)."""
+        import os
+        from ..config import default_device
+        path = self._path(params)
+        if os.environ.get("TMOG_COLUMNAR", "1") != "0" and isinstance(path, str) and os.path.isfile(path):
+            from .columnar import csv_dataset
+            text = [n for n, k in self.schema if k in ("string", "text")] \
+                if (self.schema is not None and all(isinstance(s, (tuple, list)) for s in self.schema)) else []
+            ds = csv_dataset(path, raw_features, self.device or default_device(), self._names(), self.has_header,
+                             self.separator, text, self.key_fn)
+            if ds is not None:
+                return ds
+        return super().generate_dataset(raw_features, params)
 
 
 class CSVAutoReader(CSVReader):
