@@ -188,15 +188,15 @@ def csv_dataset(path: str, raw_features: Sequence, dev, names: Optional[Sequence
     return _arrow_dataset(_TableSource(table), raw_features, dev, threads)
 
 
-def _arrow_dataset(src, raw_features: Sequence, dev: torch.device, threads: Optional[int] = None
+def _arrow_dataset(source, raw_features: Sequence, dev: torch.device, threads: Optional[int] = None
                    ) -> Optional[Dataset]:
     import pyarrow as pa
     import pyarrow.compute as pc
-    schema = src.schema
+    schema = source.schema
     plan = _plan(schema, raw_features)
     if plan is None:
         return None
-    n = src.n
+    n = source.n
     num = [(f, c, k) for f, c, k in plan if k in ("real", "int")]
     txt = [(f, c, k) for f, c, k in plan if k == "text"]
     ncols = list(dict.fromkeys(c for _, c, _ in num))
@@ -209,10 +209,10 @@ def _arrow_dataset(src, raw_features: Sequence, dev: torch.device, threads: Opti
     threads = threads or min(16, os.cpu_count() or 4)
     pool = cf.ThreadPoolExecutor(threads)
     prefetch = cf.ThreadPoolExecutor(1)
-    n_rg = src.n_chunks
+    n_rg = source.n_chunks
 
     def read(i):
-        return src.read(i, ncols) if ncols else None
+        return source.read(i, ncols) if ncols else None
 
     def host_chunk(arr, c):
         """(values ndarray in the column's device dtype, validity bitmap bytes or None, bit offset)."""
@@ -349,7 +349,7 @@ def _arrow_dataset(src, raw_features: Sequence, dev: torch.device, threads: Opti
             raise T.NonNullableEmptyException(f"{f.wtype.__name__} column '{c}' contains empty values")
         cols[f.name] = NumericColumn(f.wtype, vals[c], ok)
     if txt:
-        tt = src.read_all(list(dict.fromkeys(c for _, c, _ in txt)))
+        tt = source.read_all(list(dict.fromkeys(c for _, c, _ in txt)))
         enc = {}
         for f, c, _ in txt:
             if c not in enc:
@@ -363,7 +363,7 @@ def _arrow_dataset(src, raw_features: Sequence, dev: torch.device, threads: Opti
     order = OrderedDict((f.name, cols[f.name]) for f in raw_features)
     key = None
     if "key" in schema.names:
-        key = src.read_all(["key"]).column("key").to_pandas().astype(str).to_numpy(dtype=object)
+        key = source.read_all(["key"]).column("key").to_pandas().astype(str).to_numpy(dtype=object)
     return Dataset(order, key, n)
 
 
