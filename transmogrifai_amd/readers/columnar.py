@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import os
+import time
 from collections import OrderedDict
 from typing import List, Optional, Sequence
 
@@ -92,16 +93,29 @@ class _ParquetSource:
 
     def __init__(self, path):
         import pyarrow.parquet as pq
+        import threading
+        self.path = path
+        self._tl = threading.local()
         self.pf = pq.ParquetFile(path)
         self.schema = self.pf.schema_arrow
         self.n = self.pf.metadata.num_rows
         self.n_chunks = self.pf.metadata.num_row_groups
 
     def read(self, i, cols):
-        return self.pf.read_row_group(i, columns=cols, use_threads=True)
+        # a ParquetFile is not safe for concurrent reads: every prefetch thread decodes through its own
+        import pyarrow.parquet as pq
+        pf = getattr(self._tl, "pf", None)
+        if pf is None:
+            pf = self._tl.pf = pq.ParquetFile(self.path)
+        return pf.read_row_group(i, columns=cols, use_threads=True)
 
     def read_all(self, cols):
         return self.pf.read(columns=cols, use_threads=True)
+
+    def read_text(self, cols):
+        """String columns with their Parquet dictionaries kept (no per-row string materialisation)."""
+        import pyarrow.parquet as pq
+        return pq.ParquetFile(self.path, read_dictionary=cols).read(columns=cols, use_threads=True)
 
 
 class _TableSource:
@@ -119,6 +133,8 @@ class _TableSource:
 
     def read_all(self, cols):
         return self.table.select(cols)
+
+    read_text = read_all
 
 
 def parquet_dataset(path: str, raw_features: Sequence, dev, key_fn=None, threads: Optional[int] = None
@@ -164,7 +180,7 @@ def csv_dataset(path: str, raw_features: Sequence, dev, names: Optional[Sequence
             want[st.column] = pa.int64() if issubclass(f.wtype, T.Integral) else pa.float64()
         elif f.wtype.kind == "text":
             if st.column in text_columns:
-                want[st.column] = pa.string()
+                want[st.column] = pa.dictionary(pa.int32(), pa.string())
         else:
             return None
     ro = pacsv.ReadOptions(column_names=list(names) if (names is not None and not has_header) else None,
@@ -208,8 +224,10 @@ def _arrow_dataset(source, raw_features: Sequence, dev: torch.device, threads: O
     gpu = dev.type == "cuda"
     threads = threads or min(16, os.cpu_count() or 4)
     pool = cf.ThreadPoolExecutor(threads)
-    prefetch = cf.ThreadPoolExecutor(1)
+    prefetch = cf.ThreadPoolExecutor(max(1, int(os.environ.get("TMOG_INGEST_PREFETCH", "3"))))
     n_rg = source.n_chunks
+    t_start = time.perf_counter()
+    prof = {"wait_decode": 0.0, "pack": 0.0, "copy_wait": 0.0}
 
     def read(i):
         return source.read(i, ncols) if ncols else None
@@ -237,12 +255,16 @@ def _arrow_dataset(source, raw_features: Sequence, dev: torch.device, threads: O
                 valid[c] = torch.ones(n, dtype=torch.bool, device=dev)
         # the copy stream writes buffers allocated on the caller's stream: order after its queued work
         copy_stream.wait_stream(torch.cuda.current_stream(dev))
-    fut = prefetch.submit(read, 0) if n_rg else None
+    depth = max(1, int(os.environ.get("TMOG_INGEST_PREFETCH", "3")))     # row groups decoded ahead
+    futs = [prefetch.submit(read, g) for g in range(min(depth, n_rg))]
     row0 = 0
     try:
         for g in range(n_rg):
-            tab = fut.result()
-            fut = prefetch.submit(read, g + 1) if g + 1 < n_rg else None
+            t_w = time.perf_counter()
+            tab = futs.pop(0).result()
+            prof["wait_decode"] += time.perf_counter() - t_w
+            if g + depth < n_rg:
+                futs.append(prefetch.submit(read, g + depth))
             if tab is None:
                 continue
             rows = tab.num_rows
@@ -296,7 +318,9 @@ def _arrow_dataset(source, raw_features: Sequence, dev: torch.device, threads: O
                 if bm is not None:
                     hb[bmo:bmo + bm.nbytes] = bm
 
+            t_p = time.perf_counter()
             list(pool.map(pack, layout))
+            prof["pack"] += time.perf_counter() - t_p
             for c, r, v, bm, bo, vo, bmo in layout:
                 if bm is not None and valid[c] is None:     # on the caller's stream, like vals
                     valid[c] = torch.ones(n, dtype=torch.bool, device=dev)
@@ -328,9 +352,11 @@ def _arrow_dataset(source, raw_features: Sequence, dev: torch.device, threads: O
                 vals[c].record_stream(copy_stream)
                 if valid[c] is not None:
                     valid[c].record_stream(copy_stream)
+            t_c = time.perf_counter()
             for s in slots:
                 if s is not None and s.event is not None:
                     s.event.synchronize()
+            prof["copy_wait"] += time.perf_counter() - t_c
             masked = [c for c in ncols if valid[c] is not None]
             if masked:
                 full = torch.stack([valid[c].all() for c in masked]).tolist()
@@ -349,22 +375,56 @@ def _arrow_dataset(source, raw_features: Sequence, dev: torch.device, threads: O
             raise T.NonNullableEmptyException(f"{f.wtype.__name__} column '{c}' contains empty values")
         cols[f.name] = NumericColumn(f.wtype, vals[c], ok)
     if txt:
-        tt = source.read_all(list(dict.fromkeys(c for _, c, _ in txt)))
+        t_t = time.perf_counter()
+        tt = source.read_text(list(dict.fromkeys(c for _, c, _ in txt)))
         enc = {}
         for f, c, _ in txt:
             if c not in enc:
-                arr = tt.column(c).combine_chunks()
-                if pa.types.is_dictionary(arr.type):       # written dictionary-encoded: decode, re-encode in order
-                    arr = arr.cast(arr.type.value_type)
-                d = pc.dictionary_encode(arr)
-                codes = pc.fill_null(d.indices, -1).to_numpy(zero_copy_only=False).astype(np.int32)
-                enc[c] = (torch.as_tensor(codes, device=dev), [str(u) for u in d.dictionary.to_pylist()])
+                enc[c] = _encode_text(tt.column(c), dev)
             cols[f.name] = TextColumn(f.wtype, *enc[c])
+        prof["text"] = time.perf_counter() - t_t
     order = OrderedDict((f.name, cols[f.name]) for f in raw_features)
     key = None
     if "key" in schema.names:
         key = source.read_all(["key"]).column("key").to_pandas().astype(str).to_numpy(dtype=object)
+    if os.environ.get("TMOG_INGEST_PROFILE") == "1":
+        import sys
+        prof["total"] = time.perf_counter() - t_start
+        sys.stderr.write("[ingest-profile] " + " ".join(f"{k}={v:.3f}" for k, v in prof.items()) + "\n")
     return Dataset(order, key, n)
+
+
+def _encode_text(chunked, dev):
+    """``(codes, vocab)`` of a string column in ``pandas.factorize`` semantics -- codes in order of first appearance
+    over the rows, -1 for null, unused dictionary entries dropped. Dictionary-encoded input (Parquet string columns
+    read with their dictionaries, CSV columns parsed as dictionaries) is unified across chunks and its indices are
+    reordered by first appearance on the device (a scatter-min of row positions per code), so no per-string
+    hashing runs on the host; plain strings are dictionary-encoded by Arrow first."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    if not pa.types.is_dictionary(chunked.type):
+        chunked = pc.dictionary_encode(chunked)
+    chunked = chunked.unify_dictionaries()
+    dictionary = chunked.chunk(0).dictionary if chunked.num_chunks else pa.array([], pa.string())
+    idx = np.concatenate([pc.fill_null(ch.indices.cast(pa.int32()), -1).to_numpy(zero_copy_only=False)
+                          for ch in chunked.chunks]) if chunked.num_chunks else np.zeros(0, np.int32)
+    K = len(dictionary)
+    codes = torch.as_tensor(idx.astype(np.int32, copy=False), device=dev)
+    n = int(codes.numel())
+    if K == 0 or n == 0:
+        return codes, []
+    ok = codes >= 0
+    pos = torch.arange(n, device=dev, dtype=torch.int64)
+    first = torch.full((K,), n, dtype=torch.int64, device=dev)
+    first.scatter_reduce_(0, codes[ok].to(torch.int64), pos[ok], reduce="amin")
+    order = torch.argsort(first)
+    used = int((first < n).sum())
+    order = order[:used]
+    remap = torch.full((K,), -1, dtype=torch.int32, device=dev)
+    remap[order] = torch.arange(used, dtype=torch.int32, device=dev)
+    out = torch.where(ok, remap[codes.clamp_min(0).to(torch.int64)], codes)
+    vocab = dictionary.take(pa.array(order.cpu().numpy())).to_pylist()
+    return out, [str(u) for u in vocab]
 
 
 def dataset_to_parquet(ds: Dataset, path: str, row_group_rows: int = 1 << 20, names: Optional[Sequence[str]] = None,
