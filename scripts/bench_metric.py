@@ -12,7 +12,7 @@ from transmogrifai_amd.evaluators import metrics as M
 
 
 def main():
-    for J, n, ties in ((18, 333_333, 0), (18, 333_333, 51), (8, 333_333, 0)):
+    for J, n, ties in ((18, 333_333, 0), (18, 333_333, 51), (8, 333_333, 0), (18, 3_300_000, 0), (8, 3_300_000, 0)):
         g = torch.Generator().manual_seed(1)
         S = torch.rand(J, n, generator=g, dtype=torch.float64)
         if ties:

@@ -19,7 +19,8 @@ def _case(J, n, seed, ties, dtype, pos_rate=0.3):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("J,n,ties", [(1, 1, 0), (3, 7, 0), (5, 1024, 0), (4, 1025, 13), (6, 5000, 0),
-                                      (7, 33333, 50), (2, 200_000, 1000), (3, 4097, 1)])
+                                      (7, 33333, 50), (2, 200_000, 1000), (3, 4097, 1),
+                                      (2, 3 * 65536 + 5, 3), (1, 65536, 0), (2, 65537, 2)])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_binary_areas_device_matches_host_curves(J, n, ties, dtype):
     S, y = _case(J, n, J * 1000 + n, ties, dtype)
