@@ -28,7 +28,7 @@ import concurrent.futures as cf
 import os
 import time
 from collections import OrderedDict
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -95,6 +95,7 @@ class _ParquetSource:
         import pyarrow.parquet as pq
         import threading
         self.path = path
+        self.text_cols: List[str] = []
         self._tl = threading.local()
         self.pf = pq.ParquetFile(path)
         self.schema = self.pf.schema_arrow
@@ -105,8 +106,8 @@ class _ParquetSource:
         # a ParquetFile is not safe for concurrent reads: every prefetch thread decodes through its own
         import pyarrow.parquet as pq
         pf = getattr(self._tl, "pf", None)
-        if pf is None:
-            pf = self._tl.pf = pq.ParquetFile(self.path)
+        if pf is None:      # string columns keep their dictionaries (no per-row string materialisation)
+            pf = self._tl.pf = pq.ParquetFile(self.path, read_dictionary=self.text_cols or None)
         return pf.read_row_group(i, columns=cols, use_threads=True)
 
     def read_all(self, cols):
@@ -216,6 +217,9 @@ def _arrow_dataset(source, raw_features: Sequence, dev: torch.device, threads: O
     num = [(f, c, k) for f, c, k in plan if k in ("real", "int")]
     txt = [(f, c, k) for f, c, k in plan if k == "text"]
     ncols = list(dict.fromkeys(c for _, c, _ in num))
+    tcols = [c for c in dict.fromkeys(c for _, c, _ in txt) if c not in ncols]
+    source.text_cols = tcols
+    text_chunks: Dict[str, list] = {c: [] for c in tcols}
     types = {c: schema.field(c).type for c in ncols}
     dtype = {c: (torch.int64 if any(k == "int" and cc == c for _, cc, k in num) else _real_dtype(types[c], dev))
              for c in ncols}
@@ -229,8 +233,8 @@ def _arrow_dataset(source, raw_features: Sequence, dev: torch.device, threads: O
     t_start = time.perf_counter()
     prof = {"wait_decode": 0.0, "pack": 0.0, "copy_wait": 0.0}
 
-    def read(i):
-        return source.read(i, ncols) if ncols else None
+    def read(i):     # numeric and text columns of one row group (text decoded on the prefetch threads too)
+        return source.read(i, ncols + tcols) if (ncols or tcols) else None
 
     def host_chunk(arr, c):
         """(values ndarray in the column's device dtype, validity bitmap bytes or None, bit offset)."""
@@ -267,6 +271,8 @@ def _arrow_dataset(source, raw_features: Sequence, dev: torch.device, threads: O
                 futs.append(prefetch.submit(read, g + depth))
             if tab is None:
                 continue
+            for c in tcols:
+                text_chunks[c].extend(tab.column(c).chunks)
             rows = tab.num_rows
             pieces = []                  # (column, row offset, values ndarray, bitmap, bit offset)
             for c in ncols:
@@ -376,11 +382,14 @@ def _arrow_dataset(source, raw_features: Sequence, dev: torch.device, threads: O
         cols[f.name] = NumericColumn(f.wtype, vals[c], ok)
     if txt:
         t_t = time.perf_counter()
-        tt = source.read_text(list(dict.fromkeys(c for _, c, _ in txt)))
         enc = {}
         for f, c, _ in txt:
             if c not in enc:
-                enc[c] = _encode_text(tt.column(c), dev)
+                if c in text_chunks:
+                    ch = pa.chunked_array(text_chunks[c]) if text_chunks[c] else pa.chunked_array([], pa.string())
+                else:       # a column also read as numbers: its strings separately
+                    ch = source.read_all([c]).column(c)
+                enc[c] = _encode_text(ch, dev)
             cols[f.name] = TextColumn(f.wtype, *enc[c])
         prof["text"] = time.perf_counter() - t_t
     order = OrderedDict((f.name, cols[f.name]) for f in raw_features)
