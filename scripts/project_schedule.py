@@ -35,9 +35,13 @@ def main():
         cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--rows", str(a.rows), "--steps", str(a.steps),
                "--warmup", str(a.warmup), "--verbose"]
         t0 = time.time()
-        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout, cwd=ROOT)
-        with open(os.path.join(a.out, f"rank{r}.log"), "w") as f:
-            f.write(p.stdout + "\n--- stderr ---\n" + p.stderr[-20000:])
+        # the rank's output goes straight to its log file (progress visible while it runs)
+        logp = os.path.join(a.out, f"rank{r}.log")
+        with open(logp, "w") as f:
+            p = subprocess.run(cmd, env=env, stdout=f, stderr=subprocess.STDOUT, text=True, timeout=a.timeout,
+                               cwd=ROOT)
+        with open(logp) as f:
+            p.stdout = f.read()
         if p.returncode != 0:
             print(f"rank {r}: exit {p.returncode}; see {a.out}/rank{r}.log", flush=True)
             sys.exit(p.returncode)

@@ -423,12 +423,16 @@ def _encode_text(chunked, dev):
     if K == 0 or n == 0:
         return codes, []
     ok = codes >= 0
-    pos = torch.arange(n, device=dev, dtype=torch.int64)
-    first = torch.full((K,), n, dtype=torch.int64, device=dev)
-    first.scatter_reduce_(0, codes[ok].to(torch.int64), pos[ok], reduce="amin")
-    order = torch.argsort(first)
-    used = int((first < n).sum())
-    order = order[:used]
+    # first appearance of every used code: a stable radix sort of the valid rows' codes (a scatter-min onto the K
+    # codes would pile millions of atomics onto a few addresses); each run's first element is its first row
+    rows = torch.nonzero(ok).squeeze(1)
+    sc, perm = torch.sort(codes[rows], stable=True)
+    starts = torch.ones_like(sc, dtype=torch.bool)
+    if sc.numel() > 1:
+        starts[1:] = sc[1:] != sc[:-1]
+    first_row = rows[perm[starts]]
+    order = sc[starts][torch.argsort(first_row)].to(torch.int64)      # used codes, by first appearance
+    used = int(order.numel())
     remap = torch.full((K,), -1, dtype=torch.int32, device=dev)
     remap[order] = torch.arange(used, dtype=torch.int32, device=dev)
     out = torch.where(ok, remap[codes.clamp_min(0).to(torch.int64)], codes)
