@@ -192,3 +192,16 @@ def test_name_detector_ignores_nulls():
     vals[:12] = [n.capitalize() for n in names[:12]]        # enough distinct entries for the uniqueness guard
     assert _fit_names(vals)[1].treat_as_name
     assert not _fit_names(vals, ignore_nulls=False)[1].treat_as_name
+
+
+def test_mime_hint_only_specialises_the_detected_type():
+    import base64
+    from transmogrifai_amd.stages.feature.text_stages import detect_mime
+    text = base64.b64encode(b"just some plain words").decode()
+    rnd = base64.b64encode(bytes([0x00, 0xFF, 0x13, 0x80, 0x7F, 0x01] * 8)).decode()
+    png = base64.b64encode(b"\x89PNG\r\n\x1a\n" + b"\x00" * 16).decode()
+    assert detect_mime(text, type_hint="application/json") == "application/json"     # the reference fixture
+    assert detect_mime(text, type_hint="text/csv") == "text/csv"
+    assert detect_mime(text, type_hint="image/png") == "text/plain"
+    assert detect_mime(rnd, type_hint="image/png") == "image/png"                    # refines octet-stream
+    assert detect_mime(png, type_hint="text/plain") == "image/png"

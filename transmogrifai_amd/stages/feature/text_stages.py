@@ -130,9 +130,27 @@ def detect_mime(s, max_bytes: int = 1024, type_hint: str = ""):
     if raw[:4] == b"RIFF" and raw[8:12] in _RIFF:
         return _RIFF[raw[8:12]]
     found = "text/plain" if _looks_like_text(raw) else "application/octet-stream"
-    if type_hint:   # the generic answers are refined by the declared type (Tika's type registry)
+    if type_hint and _specialises(type_hint.strip().lower(), found):
         return type_hint
     return found
+
+
+# text/plain subtypes in Tika's type registry that a declared type may pick for plain-text content
+_TEXT_FAMILY = ("application/json", "application/xml", "application/javascript", "application/x-javascript",
+                "application/ecmascript", "application/x-sh", "application/sql", "application/rtf")
+
+
+def _specialises(hint: str, detected: str) -> bool:
+    """Tika takes a declared content type only when it specialises the magic-detected one (MimeTypes registry
+    supertypes): anything refines application/octet-stream; text/plain is refined by text/* and the
+    JSON / XML / script family. Other combinations keep the detected type: plain text declared image/png stays
+    text/plain, a PNG declared text/plain stays image/png. Beyond the reference's MimeTypeDetectorTest fixtures
+    (application/json over text): parity unpinned."""
+    if detected == "application/octet-stream":
+        return True
+    if detected == "text/plain":
+        return hint.startswith("text/") or hint in _TEXT_FAMILY or hint.endswith("+xml") or hint.endswith("+json")
+    return False
 
 
 def is_valid_phone(s: Optional[str], region: str = "US", strict: bool = False) -> Optional[bool]:
