@@ -7,6 +7,8 @@ and drives column offsets of the device-resident feature matrix.
 """
 from __future__ import annotations
 
+from functools import lru_cache
+
 from dataclasses import dataclass, field, replace
 from typing import Dict, List, Optional, Sequence
 
@@ -34,6 +36,14 @@ class FeatureHistory:
     @staticmethod
     def from_json(d):
         return FeatureHistory(tuple(d.get("originFeatures", [])), tuple(d.get("stages", [])))
+
+
+@lru_cache(maxsize=4096)
+def _has_subtype(type_names: tuple, t) -> bool:
+    """Any of the parent type names a subclass of ``t`` (memoised: the SanityChecker asks for every column of
+    wide text vectors, whose columns share a few parent-type tuples)."""
+    from ..features.types import feature_type_from_name
+    return any(issubclass(feature_type_from_name(n), t) for n in type_names)
 
 
 @dataclass(frozen=True)
@@ -72,8 +82,7 @@ class OpVectorColumnMetadata:
         return f"{s}_{self.index}"
 
     def has_parent_of_subtype(self, t) -> bool:
-        from ..features.types import feature_type_from_name
-        return any(issubclass(feature_type_from_name(n), t) for n in self.parent_feature_type)
+        return _has_subtype(self.parent_feature_type, t)
 
     def parent_names_with_map_keys(self) -> List[str]:
         from ..features.types import OPMap

@@ -265,7 +265,7 @@ class SanityChecker(BinaryEstimator):
             "labelDistribution": label_dist,
             "names": [c.make_col_name() for c in cols] + [self._inputs[0].name],
             "categoricalStats": [dict(s, contingencyMatrix=s.get("contingency")) for s in cat_stats],
-            "columnStatistics": [{k: v for k, v in s.items() if k != "column"} for s in stats],
+            "columnStatistics": [{k: v for k, v in s.items() if k not in ("column", "_ffhit")} for s in stats],
         }
         return SanityCheckerModel(keep_idx, p["remove_bad_features"])
 
@@ -346,6 +346,20 @@ class SanityChecker(BinaryEstimator):
             vals = [v for v in vals if v is not None]
             return max(vals) if vals else None
 
+        # the feature-feature correlation rule per column, vectorised: the first earlier feature (position below
+        # the column's index) whose |correlation| exceeds maxFeatureCorr (NaN never does)
+        ff_hit: Dict[int, float] = {}
+        if C is not None:
+            thr = self.params["max_feature_correlation"]
+            with np.errstate(invalid="ignore"):
+                big = np.abs(C[:-1, :]) > thr
+            for c in cols:
+                k = pos.get(c.index)
+                if k is None:
+                    continue
+                col = big[:min(c.index, big.shape[0]), k]
+                if col.any():
+                    ff_hit[c.index] = float(C[int(col.argmax()), k])
         mean, var = cs["mean"].cpu().numpy(), cs["variance"].cpu().numpy()
         mn, mx = cs["min"].cpu().numpy(), cs["max"].cpu().numpy()
         stats = [{"name": self._inputs[0].name, "column": None, "isLabel": True, "count": cs["count"],
@@ -362,6 +376,7 @@ class SanityChecker(BinaryEstimator):
                 "corrLabel": None if k is None else float(corr_label[k]),
                 "cramersV": cv_map.get(name),
                 "featureCorrs": [] if (k is None or C is None) else C[:-1, k].tolist(),
+                "_ffhit": ff_hit.get(i),
                 "parentCorr": parent_val(c, corr_parent, corr_parent_nk),
                 "parentCramersV": parent_val(c, cv_parent, cv_parent_nk),
                 "maxRuleConfidences": conf_map.get(name, []), "supports": sup_map.get(name, [])})
@@ -404,8 +419,10 @@ class SanityChecker(BinaryEstimator):
                 R.append(f"correlation {cl} higher than max correlation {p['max_correlation']}")
         c = s["column"]
         if c is not None and s["featureCorrs"]:
-            prev = s["featureCorrs"][:c.index]
-            hit = next((x for x in prev if not math.isnan(x) and abs(x) > p["max_feature_correlation"]), None)
+            hit = s.get("_ffhit")
+            if "_ffhit" not in s:       # statistics built elsewhere: the same rule, element by element
+                prev = s["featureCorrs"][:c.index]
+                hit = next((x for x in prev if not math.isnan(x) and abs(x) > p["max_feature_correlation"]), None)
             if hit is not None:
                 R.append(f"this feature has correlations {hit} with another feature higher than max feature-feature"
                          f" correlation {p['max_feature_correlation']}")
