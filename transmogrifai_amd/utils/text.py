@@ -213,7 +213,37 @@ class TokenBatch:
         return TokenBatch(np.frombuffer(b"".join(enc), dtype=np.uint8).copy(), offs, rp)
 
 
+# Results of the batch text functions for the vocabularies they last ran on: SmartText's fit and transform (and the
+# hashing of the same columns) clean / tokenise the same vocabulary list objects. Keyed by the list object itself
+# (held, so its id cannot be reused) and the parameters; lists are never mutated after a column is built.
+_BATCH_CACHE: "OrderedDict[tuple, tuple]" = None
+_BATCH_CACHE_SIZE = 24
+
+
+def _cached(strings, kind, params, fn):
+    global _BATCH_CACHE
+    from collections import OrderedDict
+    if _BATCH_CACHE is None:
+        _BATCH_CACHE = OrderedDict()
+    if not isinstance(strings, list) or len(strings) < 1024:
+        return fn()
+    key = (id(strings), len(strings), kind, params)
+    hit = _BATCH_CACHE.get(key)
+    if hit is not None and hit[0] is strings:
+        _BATCH_CACHE.move_to_end(key)
+        return hit[1]
+    out = fn()
+    _BATCH_CACHE[key] = (strings, out)
+    while len(_BATCH_CACHE) > _BATCH_CACHE_SIZE:
+        _BATCH_CACHE.popitem(last=False)
+    return out
+
+
 def _encode_batch(strings: Sequence[Optional[str]]):
+    return _cached(strings, "utf8", (), lambda: _encode_batch_impl(strings))
+
+
+def _encode_batch_impl(strings: Sequence[Optional[str]]):
     enc = [s.encode("utf-8") if s else b"" for s in strings]
     offs = np.zeros(len(enc) + 1, np.int64)
     np.cumsum(np.fromiter((len(e) for e in enc), dtype=np.int64, count=len(enc)), out=offs[1:])
@@ -237,6 +267,10 @@ class CleanedBatch:
 def clean_batch(strings: Sequence[Optional[str]], clean: bool = True) -> CleanedBatch:
     """Native batch of :func:`clean_string` (``ops/csrc/host/text_clean.cpp``): ASCII strings are cleaned in
     C++, the rest (Unicode case mapping) by :func:`clean_string`; ids by exact cleaned bytes."""
+    return _cached(strings, "clean", (bool(clean),), lambda: _clean_batch_impl(strings, clean))
+
+
+def _clean_batch_impl(strings: Sequence[Optional[str]], clean: bool = True) -> CleanedBatch:
     from ..ops import _native as N
     lib = N.host()
     n = len(strings)
@@ -271,6 +305,13 @@ def tokenize_batch(strings: Sequence[Optional[str]], to_lowercase: bool = True, 
     (``ops/csrc/host/tokenizer.cpp``). Strings the native tables flag (context-dependent lowercase,
     non-BMP code points) and custom stop-word sets go through :func:`tokenize`, so the result always
     equals ``[tokenize(s, ...) for s in strings]``."""
+    if stopwords is ENGLISH_STOPWORDS or len(stopwords) == 0:
+        return _cached(strings, "tok", (bool(to_lowercase), int(min_token_length), stopwords is ENGLISH_STOPWORDS),
+                       lambda: _tokenize_batch_impl(strings, to_lowercase, min_token_length, stopwords))
+    return _tokenize_batch_impl(strings, to_lowercase, min_token_length, stopwords)
+
+
+def _tokenize_batch_impl(strings, to_lowercase, min_token_length, stopwords) -> TokenBatch:
     from ..ops import _native as N
     n = len(strings)
     if stopwords is not ENGLISH_STOPWORDS and len(stopwords) > 0:
