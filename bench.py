@@ -72,9 +72,14 @@ def parse():
     ap.add_argument("--ingest-dir", default=None, help="directory of the --ingest parquet file (default /tmp)")
     ap.add_argument("--max-training-sample", dest="max_training_sample", type=int, default=None,
                     help="the selector splitter's maxTrainingSample (default: the reference's 1M)")
+    ap.add_argument("--dtype", default=None, choices=["fp32", "bf16"],
+                    help="linear learners' design-matrix precision (config.linear_dtype): fp32, or bf16 on the bf16 "
+                         "matrix cores; default bf16 for lr-rf-1m (BASELINE config '1 MI355X bf16'), fp32 otherwise")
     a = ap.parse_args()
     if a.config == "lr-rf-1m" and a.models == "default":
         a.models = "OpLogisticRegression,OpRandomForestClassifier"
+    if a.dtype is None:
+        a.dtype = "bf16" if a.config == "lr-rf-1m" else "fp32"
     if a.rows is None:
         a.rows = CONFIGS[a.config][1]
     return a
@@ -164,6 +169,7 @@ def main():
     if world != max(1, args.gpus) and args.device != "cpu" and not sim:
         raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} ranks")
     CFG.set_default_device(dev)
+    CFG.set_linear_dtype(args.dtype)
     if use_gpu:
         from transmogrifai_amd.ops import _native
         _native.hip()   # fail loudly if the HIP kernels cannot be loaded
@@ -301,7 +307,7 @@ def _timed(args, one_run, expected_configs, use_gpu, dev, torch, D, sim, n_raw, 
             "higher_is_better": False,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": args.dtype,
             "data": "synthetic (device-generated, seeded), random-init models",
             ("holdout_aupr" if CONFIGS[args.config][3] == "AuPR" else
              "holdout_" + CONFIGS[args.config][3].lower()): auprs[-1],

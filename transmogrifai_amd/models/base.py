@@ -65,11 +65,20 @@ def compact_rows(X: torch.Tensor, y: torch.Tensor, jobs: Sequence[FitJob]):
     remapped, or the inputs unchanged when a job uses every row or the union is all of ``X``."""
     if not jobs or any(j.rows is None for j in jobs):
         return X, y, list(jobs)
-    U, parts = union_rows([j.rows for j in jobs], X.shape[0], X.device)
+    # jobs that share a row set (the grid points of one fold) keep sharing one remapped tensor, so the learners
+    # can still group them by it (one weight column / statistic per fold, models/linear.py)
+    keys, uniq, which = {}, [], []
+    for j in jobs:
+        k = (j.rows.data_ptr(), int(j.rows.numel()), tuple(j.rows.stride()), j.rows.device)
+        if k not in keys:
+            keys[k] = len(uniq)
+            uniq.append(j.rows)
+        which.append(keys[k])
+    U, parts = union_rows(uniq, X.shape[0], X.device)
     if U.numel() >= X.shape[0]:
         return X, y, list(jobs)
     return X.index_select(0, U), y.to(X.device).index_select(0, U), \
-        [FitJob(j.params, r, j.weights) for j, r in zip(jobs, parts)]
+        [FitJob(j.params, parts[i], j.weights) for j, i in zip(jobs, which)]
 
 
 def union_rows(rows: Sequence[torch.Tensor], N: int, device):

@@ -30,7 +30,7 @@ from ..stages.base import register_stage
 class BatchedObjective:
     """Smooth objective of P linear problems sharing the design matrix ``X``."""
 
-    def __init__(self, X, y, W, inv_std, loss, l2, fit_intercept, y_scale=None, par=None):
+    def __init__(self, X, y, W, inv_std, loss, l2, fit_intercept, y_scale=None, par=None, wcols=None):
         self.X = X
         self.y = y
         self.W = W                      # [N, P] row weights (0 outside a problem's training rows)
@@ -51,11 +51,26 @@ class BatchedObjective:
             self.yf = y.to(device=X.device, dtype=torch.float32).contiguous()
             self.Wf = W.to(torch.float32).contiguous()
             self.ysf = None if y_scale is None else y_scale.to(device=X.device, dtype=torch.float32)
+        # bf16 design copy on the bf16 matrix cores (ops/csrc/hip/linear_bf16_kernels.hip) when configured
+        from .. import config as _cfg
+        self.bf16 = LK.Bf16Design.of(X) if (self.fused and _cfg.linear_dtype() == "bf16"
+                                            and LK.Bf16Design.supported(X)) else None
+        if self.bf16 is not None:
+            # one weight column per distinct training-row set (wcols: _weight_columns of the jobs), mapped per problem
+            P = W.shape[1]
+            wc = list(range(P)) if wcols is None else list(wcols)
+            uniq = sorted(set(wc))
+            pos = {c: i for i, c in enumerate(uniq)}
+            self.Wb = self.Wf if len(uniq) == P else self.Wf[:, uniq].contiguous()
+            self.wmap = LK.weight_map([pos[c] for c in wc], P, X.device)
 
     def _fused_pass(self, U, grad):
         V = (U[:self.d] * self.inv_std).to(torch.float32)
         b = torch.where(self.fi, U[self.d], torch.zeros_like(U[self.d])).to(torch.float32)
         self.passes += 1
+        if self.bf16 is not None:
+            return LK.fused_objective_bf16(self.bf16, self.yf, self.Wb, V, b, self.loss, self.ysf, grad=grad,
+                                           wmap=self.wmap)
         return LK.fused_objective(self.X, self.yf, self.Wf, V, b, self.loss, self.ysf, grad=grad)
 
     def margins(self, U):
@@ -373,6 +388,19 @@ def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max
     return U, iters, F
 
 
+def _weight_columns(jobs: Sequence[FitJob]) -> List[int]:
+    """For each job the index of the first job with the same training rows and weights (the grid points of one
+    CV fold share their row tensor, ``compact_rows``): such jobs have identical fold-weight columns."""
+    first: Dict[tuple, int] = {}
+    out = []
+    for p, j in enumerate(jobs):
+        k = ("all",) if j.rows is None else (j.rows.data_ptr(), int(j.rows.numel()), tuple(j.rows.stride()))
+        k = k + (None if j.weights is None else (j.weights.data_ptr(), int(j.weights.numel()),
+                                                 tuple(j.weights.stride())),)
+        out.append(first.setdefault(k, p))
+    return out
+
+
 def _fold_weights(N, jobs: Sequence[FitJob], dev, dtype):
     W = torch.zeros(N, len(jobs), dtype=dtype, device=dev)
     for p, j in enumerate(jobs):
@@ -452,7 +480,16 @@ class _LinearBase(Learner):
         if par is not None:
             sl = par.row_slice(N)
             X, y, W = X[sl], y[sl], W[sl].contiguous()
-        std, mean = _feature_std(X, W, par)
+        # column statistics once per distinct fold-weight column (each problem's are computed alone either way)
+        wc = _weight_columns(jobs)
+        uniq = sorted(set(wc))
+        if len(uniq) < P:
+            pos = {c: i for i, c in enumerate(uniq)}
+            std_u, mean_u = _feature_std(X, W[:, uniq].contiguous(), par)
+            sel = torch.tensor([pos[c] for c in wc], dtype=torch.int64, device=std_u.device)
+            std, mean = std_u.index_select(1, sel), mean_u.index_select(1, sel)
+        else:
+            std, mean = _feature_std(X, W, par)
         stdz = [bool(j.params.get("standardization", True)) for j in jobs]
         inv_std = torch.where(std > 0, 1.0 / std.clamp_min(1e-300), torch.zeros_like(std))
         for p, s in enumerate(stdz):
@@ -516,7 +553,7 @@ class LogisticRegressionLearner(_LinearBase):
         X, y, W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs, par)
         l2 = reg * (1 - en)
         l1v = reg * en
-        obj = BatchedObjective(X, y, W, inv_std, self.loss, l2, fi, par=par)
+        obj = BatchedObjective(X, y, W, inv_std, self.loss, l2, fi, par=par, wcols=_weight_columns(jobs))
         U0 = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)
         if self.loss == "logistic":
             pos, tot = _psum(par, (W * y[:, None].to(W.dtype)).sum(0).to(torch.float64),
@@ -626,7 +663,8 @@ class LinearRegressionLearner(_LinearBase):
         yvar = _psum(par, (W.to(torch.float64) * (yv[:, None] - ym[None, :]) ** 2).sum(0))[0] / (n - 1).clamp_min(1)
         ystd = torch.sqrt(yvar).clamp_min(1e-12)
         eff = reg / ystd
-        obj = BatchedObjective(X, y, W, inv_std, "squared", eff * (1 - en), fi, y_scale=ystd, par=par)
+        obj = BatchedObjective(X, y, W, inv_std, "squared", eff * (1 - en), fi, y_scale=ystd, par=par,
+                               wcols=_weight_columns(jobs))
         U0 = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)
         U0[d] = torch.where(fi, ym / ystd, torch.zeros_like(ym))
         l1 = torch.zeros(d + 1, P, dtype=torch.float64, device=dev)

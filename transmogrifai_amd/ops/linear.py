@@ -6,6 +6,8 @@ library-shaped GEMMs, fp32 in / fp32 accumulate), on the host through BLAS.
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 
 
@@ -245,6 +247,104 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
                 N_.ptr(X), N, d, N_.ptr(M), N_.ptr(yf), N_.ptr(Wf), P, c0, pc, N_.ptr(bc), LOSS_CODES[loss],
                 N_.ptr(ys), int(grad), N_.ptr(fp), N_.ptr(rp), N_.ptr(gp) if grad else None, nblk, N_.stream(dev)),
                 "lr_epilogue_grad")
+        if single:
+            f, r = fp[:, :pc].sum(0), rp[:, :pc].sum(0)
+            if grad:
+                G = gp[:, :d, :pc].sum(0, dtype=torch.float64)
+            break
+        f[c0:c0 + pc] = fp[:, :pc].sum(0)
+        r[c0:c0 + pc] = rp[:, :pc].sum(0)
+        if grad:
+            G[:, c0:c0 + pc] = gp[:, :d, :pc].sum(0, dtype=torch.float64)
+    return f, r, G
+
+
+_BF16_DMAX = 384        # linear_bf16_kernels.hip: 12 feature blocks of 32 resident in the accumulators
+
+
+class Bf16Design:
+    """A dense fp32 device design matrix rounded once to bf16 for ``fused_objective_bf16``: ``Xb [Npad, dpad]``
+    row-major, rows padded to a multiple of 32 and columns to a multiple of 32 with zeros (the kernel's 32-row
+    tiles and 32-feature blocks read no ragged edges). One copy serves the value and the gradient products."""
+
+    def __init__(self, X: torch.Tensor):
+        N, d = X.shape
+        self.N, self.d = int(N), int(d)
+        self.dpad = ((d + 31) // 32) * 32
+        npad = ((N + 31) // 32) * 32
+        self.Xb = torch.zeros(npad, self.dpad, dtype=torch.bfloat16, device=X.device)
+        self.Xb[:N, :d] = X
+        self.device = X.device
+        self.shape = X.shape
+
+    @staticmethod
+    def supported(X) -> bool:
+        return (isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.float32 and X.dim() == 2
+                and 1 <= X.shape[1] <= _BF16_DMAX and X.shape[0] >= 1)
+
+    @staticmethod
+    def of(X: torch.Tensor) -> "Bf16Design":
+        """The bf16 copy of ``X``, made once per tensor (every grid point and fold of a learner shares the design
+        matrix, and the learners of one selector share it too); dropped with ``X``."""
+        D = getattr(X, "_tmog_bf16", None)
+        if D is None or D[0] != X._version:
+            D = (X._version, Bf16Design(X))
+            X._tmog_bf16 = D
+        return D[1]
+
+
+def _bf16_blocks(dpad: int, grad: bool, N: int) -> int:
+    from . import _native as N_
+    props = torch.cuda.get_device_properties(torch.cuda.current_device())
+    per_cu = int(N_.hip().tmog_hip_lr_bf16_blocks_per_cu(dpad, int(grad)))
+    return max(1, min((N + 127) // 128, props.multi_processor_count * per_cu))
+
+
+def weight_map(wcols, P: int, device) -> torch.Tensor:
+    """Device ``int32 [ceil(P / 32) * 32]`` map problem -> weight column for ``fused_objective_bf16`` (padding
+    entries repeat a valid column; their problems weigh nothing)."""
+    wc = list(range(P)) if wcols is None else [int(c) for c in wcols]
+    n = ((P + _LR_PC - 1) // _LR_PC) * _LR_PC
+    wc = wc + [wc[-1]] * (n - P)
+    return torch.tensor(wc, dtype=torch.int32).to(device)
+
+
+def fused_objective_bf16(D: Bf16Design, y: torch.Tensor, W: torch.Tensor, V: torch.Tensor, bias: torch.Tensor,
+                         loss: str, yscale=None, grad: bool = True, wmap: Optional[torch.Tensor] = None):
+    """``fused_objective`` on the bf16 design copy (``ops/csrc/hip/linear_bf16_kernels.hip``): the same outputs
+    ``(f [P], r [P], G [d, P] or None)`` in fp64, of the objective whose design matrix is ``X`` rounded to bf16;
+    V and the residual weights enter the bf16 matrix cores as high + low bf16 parts. ``P`` is ``V``'s width;
+    problem p's row weights are column ``wmap[p]`` of ``W`` (``weight_map``; default column p), so problems that
+    share their training rows (the grid points of one fold) share one weight column."""
+    from . import _native as N_
+    N, d, dpad = D.N, D.d, D.dpad
+    P = V.shape[1]
+    dev = D.device
+    yf = y.to(device=dev, dtype=torch.float32).contiguous()
+    Wf = W.to(torch.float32).contiguous()
+    if wmap is None:
+        wmap = weight_map(None, P, dev)
+    nblk = _bf16_blocks(dpad, grad, N)
+    f = torch.empty(P, dtype=torch.float64, device=dev)
+    r = torch.empty(P, dtype=torch.float64, device=dev)
+    G = torch.empty(d, P, dtype=torch.float64, device=dev) if grad else None
+    fp = torch.empty(nblk * 4, _LR_PC, dtype=torch.float64, device=dev)
+    rp = torch.empty_like(fp)
+    gp = torch.empty(nblk, dpad, _LR_PC, dtype=torch.float32, device=dev) if grad else None
+    single = P <= _LR_PC
+    for c0 in range(0, P, _LR_PC):
+        pc = min(_LR_PC, P - c0)
+        Vc = torch.nn.functional.pad(V[:, c0:c0 + pc].to(torch.float32), (0, _LR_PC - pc, 0, dpad - d)).contiguous()
+        bc = torch.nn.functional.pad(bias[c0:c0 + pc].to(torch.float32), (0, _LR_PC - pc)).contiguous()
+        ys = None
+        if yscale is not None:
+            ys = torch.ones(_LR_PC, dtype=torch.float32, device=dev)
+            ys[:pc] = yscale[c0:c0 + pc]
+        N_.check(N_.hip().tmog_hip_lr_bf16(
+            N_.ptr(D.Xb), dpad, N, dpad, N_.ptr(yf), N_.ptr(Wf), Wf.shape[1], N_.ptr(wmap[c0:c0 + _LR_PC]), pc,
+            N_.ptr(Vc), N_.ptr(bc), LOSS_CODES[loss],
+            N_.ptr(ys), int(grad), N_.ptr(fp), N_.ptr(rp), N_.ptr(gp) if grad else None, nblk, N_.stream(dev)),
+            "lr_bf16")
         if single:
             f, r = fp[:, :pc].sum(0), rp[:, :pc].sum(0)
             if grad:
