@@ -128,3 +128,34 @@ def test_dutch_snowball_stemmer():
              "koninklijke": "konink"}
     assert {w: dutch_stem(w) for w in pairs} == pairs
     assert LG.analyze("De kinderen lopen met de fietsen naar huis", "nl") == ["kinder", "lop", "fiets", "huis"]
+
+
+def test_romanian_snowball_stemmer():
+    """Snowball Romanian (RomanianAnalyzer): step 0 plurals in R1, combining suffixes, standard suffixes in R2,
+    verb suffixes in RV only when nothing was removed, final vowel in RV; comma-below letters folded."""
+    from transmogrifai_amd.utils.snowball import romanian_stem
+    pairs = {"copiilor": "cop", "frumoasă": "frumoas", "abilitatea": "abil", "naţionale": "naţional",
+             "naționale": "naţional", "românească": "român", "continuare": "continu", "lucrătorilor": "lucrat"}
+    assert {w: romanian_stem(w) for w in pairs} == pairs
+    # copiii: the middle i lies between vowels and is marked as a consonant first (prelude), so only one i goes
+    assert LG.analyze("Copiii citesc cărţile frumoase", "ro") == ["copii", "citesc", "cărţ", "frumoas"]
+
+
+def test_hungarian_snowball_stemmer():
+    """Snowball Hungarian (HungarianAnalyzer): instrumental after a double consonant, cases, owner and plural
+    suffixes, a final á / é restored to a / e; R1 after the first consonant (digraph) or vowel."""
+    from transmogrifai_amd.utils.snowball import hungarian_stem
+    pairs = {"házban": "ház", "embereknek": "ember", "kutyák": "kutya", "könyvemet": "könyv", "városokban": "város",
+             "hajóval": "hajó", "asztalok": "asztal", "barátaimmal": "barát"}
+    assert {w: hungarian_stem(w) for w in pairs} == pairs
+    assert LG.analyze("A kutyák a házban vannak", "Hungarian") == ["kutya", "ház"]
+
+
+def test_finnish_snowball_stemmer():
+    """Snowball Finnish (FinnishAnalyzer): particles, possessives, cases with their vowel conditions, other
+    endings, i / t plurals and the tidying steps (long vowel, final vowel after a consonant, undoubling)."""
+    from transmogrifai_amd.utils.snowball import finnish_stem
+    pairs = {"taloissa": "talo", "kirjoissa": "kirj", "autossa": "auto", "taloon": "talo", "koirat": "koira",
+             "ihmisille": "ihmis", "eläkkeellä": "eläk", "aatonaattona": "aatonaato", "kirjastossa": "kirjasto"}
+    assert {w: finnish_stem(w) for w in pairs} == pairs
+    assert LG.analyze("Koirat juoksevat taloissa", "fi") == ["koira", "juoksev", "talo"]

@@ -9,7 +9,8 @@ per-language Lucene analyzers of ``LuceneTextAnalyzer.scala:87-236``; SURVEY.md 
 * :func:`analyze` -- the reference's per-language analysis: the language's stop words, elision stripping for
   French / Italian / Catalan (``l'amour`` -> ``amour``, Lucene ElisionFilter), English possessive removal
   and Porter stemming (``utils/stemmer.py``, Lucene EnglishAnalyzer), on top of the StandardAnalyzer word
-  rules of :func:`utils.text.analyze`. Other languages' Snowball / light stemmers are not reproduced.
+  rules of :func:`utils.text.analyze`; the languages of ``utils/stemmers.py`` STEMMERS stem after their stop
+  filter. Turkish (TurkishAnalyzer's Snowball stemmer) is not reproduced: its tokens are stop-filtered only.
 """
 from __future__ import annotations
 
@@ -75,6 +76,49 @@ de en van ik te dat die in een hij het niet zijn is was op aan met als voor had 
 dit zo door over ze zich bij ook tot je mij uit der daar haar naar heb hoe heeft hebben deze u want nog zal me zij nu
 ge geen omdat iets worden toch al waren veel meer doen toen moet ben zonder kan hun dus alles onder ja eens hier wie
 werd altijd doch wordt wezen kunnen ons zelf tegen na reeds wil kon niets uw iemand geweest andere""".split())
+
+# Snowball stop lists of the Finnish, Hungarian and Romanian analyzers (Lucene's RomanianAnalyzer list for ro)
+STOPWORDS["fi"] = PROFILES["fi"] | frozenset("""
+olla olen olet on olemme olette ovat ole oli olisi olisit olisin olisimme olisitte olisivat olit olin olimme olitte
+olivat ollut olleet en et ei emme ette eivät minä minun minut minua minussa minusta minuun minulla minulta minulle sinä
+sinun sinut sinua sinussa sinusta sinuun sinulla sinulta sinulle hän hänen hänet häntä hänessä hänestä häneen hänellä
+häneltä hänelle me meidän meidät meitä meissä meistä meihin meillä meiltä meille te teidän teidät teitä teissä teistä
+teihin teillä teiltä teille he heidän heidät heitä heissä heistä heihin heillä heiltä heille tämä tämän tätä tässä
+tästä tähän tällä tältä tälle tänä täksi tuo tuon tuota tuossa tuosta tuohon tuolla tuolta tuolle tuona tuoksi se sen
+sitä siinä siitä siihen sillä siltä sille sinä siksi nämä näiden näitä näissä näistä näihin näillä näiltä näille näinä
+näiksi nuo noiden noita noissa noista noihin noilla noilta noille noina noiksi ne niiden niitä niissä niistä niihin
+niillä niiltä niille niinä niiksi kuka kenen kenet ketä kenessä kenestä keneen kenellä keneltä kenelle kenenä keneksi
+ketkä keiden keitä keissä keistä keihin keillä keiltä keille keinä keiksi mikä minkä mitä missä mistä mihin millä
+miltä mille miksi mitkä joka jonka jota jossa josta johon jolla jolta jolle jona joksi jotka joiden joita joissa
+joista joihin joilla joilta joille joina joiksi että ja jos koska kuin mutta niin sekä tai vaan vai vaikka kanssa
+mukaan noin poikki yli kun nyt itse""".split())
+STOPWORDS["hu"] = frozenset("""
+a ahogy ahol aki akik akkor alatt által általában amely amelyek amelyekben amelyeket amelyet amelynek ami amit amolyan
+amíg amikor át abban ahhoz annak arra arról az azok azon azt azzal azért aztán azután azonban bár be belül benne cikk
+cikkek cikkeket csak de e eddig egész egy egyes egyetlen egyéb egyik egyre ekkor el elég ellen elő először előtt első
+én éppen ebben ehhez emilyen ennek erre ez ezt ezek ezen ezzel ezért és fel felé hanem hiszen hogy hogyan igen így
+illetve ill ilyen ilyenkor ismét itt jó jól jobban kell kellett keresztül keressünk ki kívül között közül legalább
+lehet lehetett legyen lenne lenni lesz lett maga magát majd már más másik meg még mellett mert mely melyek mi mit míg
+miért milyen mikor minden mindent mindenki mindig mint mintha mivel most nagy nagyobb nagyon ne néha nekem neki nem
+néhány nélkül nincs olyan ott össze ő ők őket pedig persze rá s saját sem semmi sok sokat sokkal számára szemben
+szerint szinte talán tehát teljes tovább továbbá több úgy ugyanis új újabb újra után utána utolsó vagy vagyis valaki
+valami valamint való vagyok van vannak volt voltam voltak voltunk vissza vele viszont volna""".split())
+STOPWORDS["ro"] = PROFILES["ro"] | frozenset("""
+a abia acea aceasta această aceea acei aceia acel acela acele acelea acest acesta aceste acestea acestei acestia
+acestui aceşti aceştia acolo acum ai aia aibă aici al ale alea alt alta altceva altcineva alte altfel alti altii altul
+am anume apoi ar are as asa asta astazi astfel asupra atare atat atata atatea atatia ati atit atita atitea atitia
+atunci au avea avem avut azi aş aşadar aţi ba bine bucur bună ca cand care careia carora caruia cat catre ce cea ceea
+cei ceilalti cel cele celor ceva chiar ci cind cine cineva cit cita cite citeva citi citiva cu cui cum cumva da daca
+dar dat dată de deasupra deci decit deja desi despre din dintr dintre doar doi doilea două drept dupa după ea ei el ele
+era este eu exact eşti face fara fata fel fi fie fiecare fii fim fiu fiţi foarte fost fără geaba ia iar ii il imi in
+inainte inapoi inca incit insa intr intre isi iti la le li lor lui ma mai mea mei mele mereu meu mi mie mine mod mult
+multa multe multi mâine mîine ne ni nici nimeni nimic niste nişte noastre noastră noi nostri nostru nou noua nouă
+noştri nu numai or ori oricare orice oricine oricum oricând oricît oriunde pai parca patra patru pe pentru peste pic
+pina poate pot prea prima primul prin printr putini puţin puţina puţină până pînă sa sai sale sau se si sint sintem
+spate spre sub sunt suntem sunteţi sus să săi său ta tale te ti tine toata toate toată tocmai tot toti totul totusi
+totuşi toţi trei treia treilea tu tuturor tăi tău ul ului un una unde undeva unei uneia unele uneori unii unor unora
+unu unui unuia unul va vi voastre voastră voi vom vor vostru vouă voştri vreo vreun vă zi zice îi îl îmi în îţi ăla
+ălea ăsta ăstea ăştia şi ţi ţie""".split())
 
 _ELISIONS = {"fr": ("l", "m", "t", "qu", "n", "s", "j", "d", "c", "jusqu", "quoiqu", "lorsqu", "puisqu"),
              "it": ("c", "l", "all", "dall", "dell", "nell", "sull", "coll", "pell", "gl", "agl", "dagl",

@@ -9,6 +9,10 @@ Implemented from the published Snowball algorithm descriptions (snowballstem.org
   endings, undoubling, and the vowel undoubling of step 4; DutchAnalyzer's stem overrides (fiets, bromfiets,
   ei, kind) are applied first, as its StemmerOverrideFilter does.
 
+* :func:`romanian_stem`, :func:`hungarian_stem`, :func:`finnish_stem` -- the RomanianAnalyzer, HungarianAnalyzer
+  and FinnishAnalyzer stemmers (steps named in each function). Their outputs are pinned by the algorithms' own
+  rules in ``tests/test_language.py``; no reference fixture covers these languages (parity unpinned).
+
 ``among`` semantics: of the listed suffixes the longest one present is taken, and its condition decides;
 a failing condition does not fall back to a shorter suffix.
 """
@@ -208,3 +212,304 @@ def dutch_stem(word: str) -> str:
             and w[-4] not in _NL_V:
         w = w[:-2] + w[-1]
     return w.replace("Y", "y").replace("I", "i")
+
+
+# ---------------------------------------------------------------------------------------------- Romanian
+# RomanianAnalyzer: lower case, stop words, SnowballFilter(Romanian). The Snowball Romanian algorithm is written
+# with the cedilla letters ş ţ; the comma-below forms (ș ț) are folded onto them first.
+_RO_V = set("aăâeiîou")
+_RO_COMMA = str.maketrans("șțŞŢȘȚ", "şţşţşţ")
+
+
+def _ro_mark(w: str) -> str:
+    """u and i between vowels -> U, I (consonants for the regions and the suffix conditions)."""
+    c = list(w)
+    for i in range(1, len(c) - 1):
+        if c[i] in "ui" and c[i - 1] in _RO_V and c[i + 1] in _RO_V:
+            c[i] = c[i].upper()
+    return "".join(c)
+
+
+def _rv_standard(w: str, vowels) -> int:
+    """RV of the Romance Snowball stemmers: after the next vowel when the 2nd letter is a consonant, after the
+    next consonant when the first two are vowels, else after the 3rd letter; the end if none applies."""
+    n = len(w)
+    if n < 2:
+        return n
+    if w[1] not in vowels:
+        for i in range(2, n):
+            if w[i] in vowels:
+                return i + 1
+        return n
+    if w[0] in vowels:
+        for i in range(2, n):
+            if w[i] not in vowels:
+                return i + 1
+        return n
+    return 3 if n >= 3 else n
+
+
+def _r1r2(w: str, vowels) -> Tuple[int, int]:
+    def r_after(start: int) -> int:
+        for i in range(start + 1, len(w)):
+            if w[i] not in vowels and w[i - 1] in vowels:
+                return i + 1
+        return len(w)
+    r1 = r_after(0)
+    return r1, (r_after(r1) if r1 < len(w) else len(w))
+
+
+_RO_STEP0 = {"ul": "", "ului": "", "aua": "a", "ea": "e", "ele": "e", "elor": "e", "ii": "i", "iua": "i", "iei": "i",
+             "iile": "i", "iilor": "i", "ilor": "i", "ile": "i", "atei": "at", "aţie": "aţi", "aţia": "aţi"}
+_RO_COMBO = {}
+for _rep, _sufs in (("abil", "abilitate abilitati abilităi abilităţi"), ("ibil", "ibilitate"),
+                    ("iv", "ivitate ivitati ivităi ivităţi"),
+                    ("ic", "icitate icitati icităi icităţi icator icatori iciv iciva icive icivi icivă ical icala icale "
+                           "icali icală"),
+                    ("at", "ativ ativa ative ativi ativă aţiune atoare ator atori ătoare ător ători"),
+                    ("it", "itiv itiva itive itivi itivă iţiune itoare itor itori")):
+    for _s in _sufs.split():
+        _RO_COMBO[_s] = _rep
+_RO_STD_DEL = tuple("at ata ată ati ate ut uta ută uti ute it ita ită iti ite ic ica ice ici ică abil abila abile abili "
+                    "abilă ibil ibila ibile ibili ibilă oasa oasă oase os osi oşi ant anta ante anti antă ator atori "
+                    "itate itati ităi ităţi iv iva ive ivi ivă".split())
+_RO_STD_IST = tuple("ism isme ist ista iste isti istă işti".split())
+_RO_VERB1 = tuple("are ere ire âre ind ând indu ându eze ească ez ezi ează esc eşti eşte ăsc ăşti ăşte am ai au eam eai "
+                  "ea eaţi eau iam iai ia iaţi iau ui aşi arăm arăţi ară uşi urăm urăţi ură işi irăm irăţi iră âi âşi "
+                  "ârăm ârăţi âră asem aseşi ase aserăm aserăţi aseră isem iseşi ise iserăm iserăţi iseră âsem âseşi "
+                  "âse âserăm âserăţi âseră usem useşi use userăm userăţi useră".split())
+_RO_VERB2 = tuple("ăm aţi em eţi im iţi âm âţi seşi serăm serăţi seră sei se sesem seseşi sese seserăm seserăţi "
+                  "seseră".split())
+
+
+def romanian_stem(word: str) -> str:
+    w = _ro_mark(word.translate(_RO_COMMA))
+    rv = _rv_standard(w, _RO_V)
+    r1, r2 = _r1r2(w, _RO_V)
+    # step 0: plurals and other simplifications, in R1
+    s = _longest(w, 0, _RO_STEP0)
+    if s is not None and len(w) - len(s) >= r1:
+        if not (s == "ile" and w[:-3].endswith("ab")):
+            w = w[:-len(s)] + _RO_STEP0[s]
+    # step 1: combining suffixes in R1, repeated while one is replaced
+    removed = False
+    while True:
+        s = _longest(w, 0, _RO_COMBO)
+        if s is None or len(w) - len(s) < r1:
+            break
+        w = w[:-len(s)] + _RO_COMBO[s]
+        removed = True
+    # step 2: standard suffixes in R2
+    s = _longest(w, 0, _RO_STD_DEL + _RO_STD_IST + ("iune", "iuni"))
+    if s is not None and len(w) - len(s) >= r2:
+        if s in ("iune", "iuni"):
+            if w[:-len(s)].endswith("ţ"):
+                w = w[:-len(s) - 1] + "t"
+                removed = True
+        elif s in _RO_STD_IST:
+            w = w[:-len(s)] + "ist"
+            removed = True
+        else:
+            w = w[:-len(s)]
+            removed = True
+    # step 3: verb suffixes in RV, when steps 1 and 2 removed nothing
+    if not removed:
+        s = _longest(w, rv, _RO_VERB1 + _RO_VERB2)
+        if s is not None:
+            k = len(w) - len(s)
+            if s in _RO_VERB2:
+                w = w[:k]
+            elif k - 1 >= rv and (w[k - 1] not in _RO_V or w[k - 1] == "u"):
+                w = w[:k]
+    # step 4: final vowel in RV
+    s = _longest(w, rv, ("a", "e", "i", "ie", "ă"))
+    if s is not None:
+        w = w[:-len(s)]
+    return w.replace("I", "i").replace("U", "u")
+
+
+# --------------------------------------------------------------------------------------------- Hungarian
+# HungarianAnalyzer: lower case, stop words, SnowballFilter(Hungarian).
+_HU_V = set("aáeéiíoóöőuúüű")
+_HU_DIGRAPHS = ("dzs", "cs", "dz", "gy", "ly", "ny", "sz", "ty", "zs")
+_HU_DOUBLES = ("bb", "cc", "ccs", "dd", "ff", "gg", "ggy", "jj", "kk", "ll", "lly", "mm", "nn", "nny", "pp", "rr", "ss",
+               "ssz", "tt", "tty", "vv", "zz", "zzs")
+
+
+def _hu_r1(w: str) -> int:
+    """After the first consonant (a digraph counts as one) when the word starts with a vowel; after the first
+    vowel when it starts with a consonant; the end when the word lacks either."""
+    if not w:
+        return 0
+    if w[0] in _HU_V:
+        for i in range(1, len(w)):
+            if w[i] not in _HU_V:
+                for dg in _HU_DIGRAPHS:
+                    if w.startswith(dg, i):
+                        return i + len(dg)
+                return i + 1
+        return len(w)
+    for i in range(1, len(w)):
+        if w[i] in _HU_V:
+            return i + 1
+    return len(w)
+
+
+def _hu_undouble_after(w: str, suffix_len: int, r1: int) -> str:
+    """Delete a suffix that lies in R1 and follows a double consonant, then one letter of that double."""
+    k = len(w) - suffix_len
+    if k < r1 or not w[:k].endswith(_HU_DOUBLES):
+        return w
+    w = w[:k]
+    return w[:-2] + w[-1]
+
+
+def _hu_table(w: str, r1: int, table) -> str:
+    s = _longest(w, 0, table)
+    if s is not None and len(w) - len(s) >= r1:
+        return w[:-len(s)] + table[s]
+    return w
+
+
+_HU_CASE = tuple("ban ben ba be ra re nak nek val vel tól től ról ről ból ből hoz hez höz nál nél ig at et ot öt ért képp "
+                 "képpen kor ul ül vá vé onként enként anként ként en on an ön n t".split())
+_HU_SPECIAL = {"én": "e", "án": "a", "ánként": "a"}
+_HU_OTHER = {"astul": "", "estül": "", "stul": "", "stül": "", "ástul": "a", "éstül": "e"}
+_HU_OWNED = {"oké": "", "öké": "", "aké": "", "eké": "", "ké": "", "éi": "", "é": "", "áké": "a", "áéi": "a", "éké": "e",
+             "ééi": "e", "éé": "e"}
+_HU_SING = {s: "" for s in "ünk unk nk juk jük uk ük em om am m od ed ad öd d ja je a e o".split()}
+_HU_SING.update({s: "a" for s in "ánk ájuk ám ád á".split()})
+_HU_SING.update({s: "e" for s in "énk éjük ém éd é".split()})
+_HU_PLUR = {s: "" for s in ("jaim jeim aim eim im jaid jeid aid eid id jai jei ai ei i jaink jeink eink aink ink jaitok "
+                            "jeitek aitok eitek itek jeik jaik aik eik ik").split()}
+_HU_PLUR.update({s: "a" for s in "áim áid ái áink áitok áik".split()})
+_HU_PLUR.update({s: "e" for s in "éim éid éi éink éitek éik".split()})
+_HU_PLURAL = {"ák": "a", "ék": "e", "ök": "", "ok": "", "ek": "", "ak": "", "k": ""}
+
+
+def hungarian_stem(word: str) -> str:
+    w = word
+    r1 = _hu_r1(w)
+    # instrumental: -al / -el after a double consonant
+    if w.endswith(("al", "el")):
+        w = _hu_undouble_after(w, 2, r1)
+    # frequent cases, then a final á / é (in R1) back to a / e
+    s = _longest(w, 0, _HU_CASE)
+    if s is not None and len(w) - len(s) >= r1:
+        w = w[:-len(s)]
+        if len(w) - 1 >= r1 and w.endswith(("á", "é")):
+            w = w[:-1] + ("a" if w[-1] == "á" else "e")
+    w = _hu_table(w, r1, _HU_SPECIAL)
+    w = _hu_table(w, r1, _HU_OTHER)
+    # factive: -á / -é after a double consonant
+    if w.endswith(("á", "é")):
+        w = _hu_undouble_after(w, 1, r1)
+    w = _hu_table(w, r1, _HU_OWNED)
+    w = _hu_table(w, r1, _HU_SING)
+    w = _hu_table(w, r1, _HU_PLUR)
+    w = _hu_table(w, r1, _HU_PLURAL)
+    return w
+
+
+# ----------------------------------------------------------------------------------------------- Finnish
+# FinnishAnalyzer: lower case, stop words, SnowballFilter(Finnish).
+_FI_V1 = set("aeiouyäö")
+_FI_V2 = set("aeiouäö")
+_FI_C = set("bcdfghjklmnpqrstvwxz")
+_FI_LV = ("aa", "ee", "ii", "oo", "uu", "ää", "öö")
+
+
+def _fi_vi(w: str, k: int) -> bool:
+    """the text before position k ends with a V2 vowel followed by i"""
+    return k >= 2 and w[k - 1] == "i" and w[k - 2] in _FI_V2
+
+
+def finnish_stem(word: str) -> str:
+    w = word
+    r1, r2 = _r1r2(w, _FI_V1)
+    # step 1: particles (after n, t or a vowel) and -sti (in R2), the suffix in R1
+    s = _longest(w, r1, ("kin", "kaan", "kään", "ko", "kö", "han", "hän", "pa", "pä", "sti"))
+    if s is not None:
+        k = len(w) - len(s)
+        if s == "sti":
+            if k >= r2:
+                w = w[:k]
+        elif k >= 1 and (w[k - 1] in _FI_V1 or w[k - 1] in "nt"):
+            w = w[:k]
+    # step 2: possessives, the suffix in R1
+    s = _longest(w, r1, ("si", "ni", "nsa", "nsä", "mme", "nne", "an", "än", "en"))
+    if s is not None:
+        k = len(w) - len(s)
+        head = w[:k]
+        if s == "si":
+            if not head.endswith("k"):
+                w = head
+        elif s == "ni":
+            w = head[:-3] + "ksi" if head.endswith("kse") else head
+        elif s in ("nsa", "nsä", "mme", "nne"):
+            w = head
+        elif s == "an":
+            if head.endswith(("ta", "ssa", "sta", "lla", "lta", "na")):
+                w = head
+        elif s == "än":
+            if head.endswith(("tä", "ssä", "stä", "llä", "ltä", "nä")):
+                w = head
+        elif s == "en":
+            if head.endswith(("lle", "ine")):
+                w = head
+    # step 3: cases, the suffix in R1
+    ending_removed = False
+    s = _longest(w, r1, ("han", "hen", "hin", "hon", "hun", "hyn", "hän", "hön", "siin", "den", "tten", "seen", "a",
+                         "ä", "tta", "ttä", "ta", "tä", "ssa", "ssä", "sta", "stä", "lla", "llä", "lta", "ltä", "lle",
+                         "na", "nä", "ksi", "ine", "n"))
+    if s is not None:
+        k = len(w) - len(s)
+        ok = False
+        if len(s) == 3 and s[0] == "h" and s[2] == "n":
+            ok = k >= 1 and w[k - 1] == s[1]
+        elif s in ("siin", "den", "tten"):
+            ok = _fi_vi(w, k)
+        elif s == "seen":
+            ok = w[:k].endswith(_FI_LV)
+        elif s in ("a", "ä"):
+            ok = k >= 2 and w[k - 1] in _FI_V1 and w[k - 2] in _FI_C
+        elif s in ("tta", "ttä"):
+            ok = k >= 1 and w[k - 1] == "e"
+        else:
+            ok = True
+        if ok:
+            w = w[:k]
+            if s == "n" and w.endswith(_FI_LV + ("ie",)):
+                w = w[:-1]
+            ending_removed = True
+    # step 4: other endings, the suffix in R2
+    s = _longest(w, r2, ("mpi", "mpa", "mpä", "mmi", "mma", "mmä", "impi", "impa", "impä", "immi", "imma", "immä",
+                         "eja", "ejä"))
+    if s is not None:
+        if not (len(s) == 3 and s[0] == "m" and w[:-3].endswith("po")):
+            w = w[:-len(s)]
+    # step 5: plurals
+    if ending_removed:
+        if w.endswith(("i", "j")) and len(w) - 1 >= r1:
+            w = w[:-1]
+    elif w.endswith("t") and len(w) - 1 >= r1 and len(w) >= 2 and w[-2] in _FI_V1:
+        w = w[:-1]
+        s = _longest(w, r2, ("mma", "imma"))
+        if s is not None and not (s == "mma" and w[:-3].endswith("po")):
+            w = w[:-len(s)]
+    # step 6: tidying, the letters concerned in R1
+    if w.endswith(_FI_LV) and len(w) - 2 >= r1:
+        w = w[:-1]
+    if len(w) >= 2 and w[-1] in "aäei" and w[-2] in _FI_C and len(w) - 2 >= r1:
+        w = w[:-1]
+    if w.endswith(("oj", "uj")) and len(w) - 2 >= r1:
+        w = w[:-1]
+    if w.endswith("jo") and len(w) - 2 >= r1:
+        w = w[:-1]
+    # a double consonant followed by zero or more vowels: drop one of the pair (regardless of R1)
+    i = len(w)
+    while i > 0 and w[i - 1] in _FI_V1:
+        i -= 1
+    if i >= 2 and w[i - 1] == w[i - 2] and w[i - 1] in _FI_C:
+        w = w[:i - 1] + w[i:]
+    return w
