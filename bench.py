@@ -73,13 +73,14 @@ def parse():
     ap.add_argument("--max-training-sample", dest="max_training_sample", type=int, default=None,
                     help="the selector splitter's maxTrainingSample (default: the reference's 1M)")
     ap.add_argument("--dtype", default=None, choices=["fp32", "bf16"],
-                    help="linear learners' design-matrix precision (config.linear_dtype): fp32, or bf16 on the bf16 "
-                         "matrix cores; default bf16 for lr-rf-1m (BASELINE config '1 MI355X bf16'), fp32 otherwise")
+                    help="linear learners' design-matrix precision (config.linear_dtype): fp32, or bf16 on the "
+                         "bf16 matrix cores (default; BASELINE config '1 MI355X bf16'); tree learners bin their "
+                         "inputs either way")
     a = ap.parse_args()
     if a.config == "lr-rf-1m" and a.models == "default":
         a.models = "OpLogisticRegression,OpRandomForestClassifier"
     if a.dtype is None:
-        a.dtype = "bf16" if a.config == "lr-rf-1m" else "fp32"
+        a.dtype = "bf16"
     if a.rows is None:
         a.rows = CONFIGS[a.config][1]
     return a

@@ -71,7 +71,8 @@ def test_real_design_matches_fp64_of_rounded_x(loss):
     W = (torch.rand(N, P, device="cuda") < 0.67).float()
     ys = 0.5 + torch.rand(P, device="cuda")
     D = LK.Bf16Design(X)
-    Xb = D.Xb[:N, :d].float()
+    assert D.shifted and D.n_exact == 0
+    Xb = D.Xb[:N, :d].double() * D.scale + D.mu         # the design the stored (centred, scaled) copy encodes
     f, r, G = LK.fused_objective_bf16(D, y, W, V, bias, loss, ys if loss == "squared" else None, grad=True)
     fr, rr, Gr = _ref(Xb, y, W, V, bias, loss, ys)
     scale_f = fr.abs().max().clamp_min(1.0)
@@ -132,3 +133,44 @@ def test_weight_map_equals_expanded_weights():
     b = LK.fused_objective_bf16(D, y, Wu, V, bias, "logistic", grad=True, wmap=LK.weight_map(cols, P, X.device))
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+def _mnl_ref(Xb, V, y, W, bias, P, K):
+    X = Xb.to(torch.float64)
+    M = (X @ V.to(torch.float64) + bias.to(torch.float64)[None, :]).reshape(-1, P, K)
+    lse = torch.logsumexp(M, 2)
+    yi = y.long()
+    my = M.gather(2, yi[:, None, None].expand(-1, P, 1))[:, :, 0]
+    Wd = W.to(torch.float64)
+    f = ((lse - my) * Wd).sum(0)
+    R = (torch.softmax(M, 2) - torch.nn.functional.one_hot(yi, K).to(torch.float64)[:, None, :]) * Wd[:, :, None]
+    R = R.reshape(-1, P * K)
+    return f, R.sum(0), X.t() @ R
+
+
+@pytest.mark.parametrize("N,d,P,K", [(5000, 130, 24, 6), (1203, 33, 5, 3), (700, 64, 40, 16)])
+def test_multinomial_bf16_matches_fp64(N, d, P, K):
+    _need_gpu()
+    from transmogrifai_amd.ops import linear as LK
+    torch.manual_seed(N)
+    X = torch.randn(N, d, device="cuda")
+    X[:, :5] = (X[:, :5] > 0).float()                     # exact columns, stored as they are
+    X[:, 5] += 1000.0                                     # large offset: centred before rounding
+    D = LK.Bf16Design.of(X, pad=False)
+    assert D.shifted and D.n_exact == 5
+    Xb = D.Xb.double() * D.scale + D.mu
+    V = 0.05 * torch.randn(d, P * K, device="cuda")
+    bias = 0.1 * torch.randn(P * K, device="cuda")
+    y = torch.randint(0, K, (N,), device="cuda").float()
+    Wu = (torch.rand(N, 3, device="cuda") < 0.67).float()
+    cols = [p % 3 for p in range(P)]
+    wmap = torch.tensor(cols, dtype=torch.int32, device="cuda")
+    f, rs, G = LK.mnl_objective_bf16(D, V, y, Wu, bias, P, K, grad=True, wmap=wmap)
+    fr, rr, Gr = _mnl_ref(Xb, V, y, Wu[:, cols], bias, P, K)
+    assert ((f - fr).abs() / fr.abs().clamp_min(1.0)).max() < 2e-5
+    n = Wu[:, cols].sum(0).to(torch.float64)
+    assert ((rs - rr).abs().reshape(P, K) / n[:, None]).max() < 1e-5
+    mag = (Xb.abs().t() @ Wu[:, cols].to(torch.float64)).repeat_interleave(K, 1)
+    assert ((G - Gr).abs() / mag.clamp_min(1.0)).max() < 1e-4
+    fv, rv, Gv = LK.mnl_objective_bf16(D, V, y, Wu, bias, P, K, grad=False, wmap=wmap)
+    assert Gv is None and torch.equal(fv, f) and torch.equal(rv, rs)

@@ -132,12 +132,25 @@ class MultinomialObjective:
     ``[d+1, K]`` blocks (class-major coefficient columns), so the batched OWL-QN is reused unchanged.
     One GEMM ``X [N,d] @ V [d, P*K]`` produces every problem's class margins."""
 
-    def __init__(self, X, y, W, inv_std, l2, fit_intercept, K, par=None):
+    def __init__(self, X, y, W, inv_std, l2, fit_intercept, K, par=None, wcols=None):
         self.X, self.W, self.K = X, W, K
         self.par = par
         # GPU: margins by GEMM / SpMM, then ONE fused softmax epilogue (log-sum-exp, weighted loss, R in place)
         # and fixed-order column sums (ops/csrc/hip/sparse_kernels.hip) instead of ~15 torch passes over [N, P, K]
         self.fused = X.device.type == "cuda" and os.environ.get("TMOG_MNL_FUSED", "1") != "0"
+        # bf16 design copy (config.linear_dtype): bf16 library GEMMs with [hi | lo] coefficient / residual parts
+        # around one fused epilogue launch (ops/linear.py mnl_objective_bf16)
+        from .. import config as _cfg
+        P = W.shape[1]
+        self.Xb = None
+        if (self.fused and _cfg.linear_dtype() == "bf16" and isinstance(X, torch.Tensor) and
+                X.dtype == torch.float32 and X.dim() == 2 and K <= 16 and P <= 256):
+            self.Xb = LK.Bf16Design.of(X, pad=False)
+            wc = list(range(P)) if wcols is None else list(wcols)
+            uniq = sorted(set(wc))
+            pos = {c: i for i, c in enumerate(uniq)}
+            self.Wb = W.to(torch.float32)[:, uniq].contiguous()
+            self.wmap = torch.tensor([pos[c] for c in wc], dtype=torch.int32).to(X.device)
         self.y = y
         self.Y = None if self.fused else torch.nn.functional.one_hot(y.to(torch.int64), K).to(X.dtype)    # [N, K]
         self.wsum = _psum(par, W.sum(0).to(torch.float64))[0].clamp_min(1e-300)
@@ -166,6 +179,14 @@ class MultinomialObjective:
         l = lse - (M * self.Y[:, None, :]).sum(2)
         return l, lse
 
+    def _bf16_pass(self, U, grad):
+        B, V, b = self._split(U)
+        P = U.shape[1]
+        self.passes += 1
+        f, rs, G = LK.mnl_objective_bf16(self.Xb, V.permute(0, 2, 1).reshape(self.d, P * self.K), self.y, self.Wb,
+                                         b.t().reshape(-1), P, self.K, grad, wmap=self.wmap)
+        return B, f, rs, G
+
     def _fused_pass(self, U, grad):
         B, V, b = self._split(U)
         P = U.shape[1]
@@ -175,6 +196,10 @@ class MultinomialObjective:
         return B, M, f, rs
 
     def value(self, U):
+        if self.Xb is not None:
+            B, f, _, _ = self._bf16_pass(U, False)
+            f = _psum(self.par, f)[0] / self.wsum
+            return f + 0.5 * self.l2 * (B[:self.d] ** 2).sum((0, 1))
         if self.fused:
             B, _, f, _ = self._fused_pass(U, False)
             f = _psum(self.par, f)[0] / self.wsum
@@ -188,8 +213,12 @@ class MultinomialObjective:
     def value_grad(self, U):
         if self.fused:
             P = U.shape[1]
-            B, R, fs, rs = self._fused_pass(U, True)
-            fs, Gs, rs = _psum(self.par, fs, LK.gemm_t(self.X, R).to(torch.float64), rs)
+            if self.Xb is not None:
+                B, fs, rs, Gs = self._bf16_pass(U, True)
+                fs, Gs, rs = _psum(self.par, fs, Gs, rs)
+            else:
+                B, R, fs, rs = self._fused_pass(U, True)
+                fs, Gs, rs = _psum(self.par, fs, LK.gemm_t(self.X, R).to(torch.float64), rs)
             f = fs / self.wsum
             G = Gs.reshape(self.d, P, self.K).permute(0, 2, 1) / self.wsum[None, None, :]   # [d, K, P]
             g = torch.zeros_like(B)
@@ -311,6 +340,9 @@ def _owlqn_direction_torch(U, g, l1, has_l1, S, Y, RHO, hist_n, m):
     return D, pg, xi, dnorm
 
 
+_TRACE = os.environ.get("TMOG_OWLQN_TRACE", "0") == "1"
+
+
 def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max_iter: torch.Tensor,
                   tol: torch.Tensor, m: int = 10, max_ls: int = 30):
     """Batched OWL-QN (L-BFGS when ``l1 == 0``) over the columns of ``U``.
@@ -333,6 +365,10 @@ def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max
     if fused_dir:
         l1 = l1.to(U.dtype).contiguous()
     from ..utils.cancel import check as _cancel_check
+    # the first line-search trial is evaluated with its gradient while the previous iteration's first trial was
+    # accepted by every problem (adaptive: a value-only trial is cheaper when backtracking is likely)
+    spec_on = os.environ.get("TMOG_OWLQN_SPEC", "1") != "0"
+    spec_grad = spec_on
     for it in range(int(max_iter.max().item()) if P else 0):
         _cancel_check()             # maxWait (tuning/validators.py _fit_eval_bounded)
         done |= iters >= max_iter
@@ -349,26 +385,43 @@ def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max
         accepted = done.clone()
         Un = U.clone()
         Fn = F.clone()
-        for _ in range(max_ls):
+        first = None            # (f, g) of the first trial point when it is evaluated with its gradient
+        late = False            # some problem accepted after the first trial
+        for trial in range(max_ls):
             if fused_dir:
                 # projected candidate + its Armijo sums in one launch (ops/linear.py owlqn_candidate)
                 cand, l1t, dd = LK.owlqn_candidate(U, D, xi, l1, pg, alpha)
-                fc = obj.value(cand) + l1t
-                ok = (fc <= F + 1e-4 * dd) & ~accepted
+                rhs = F + 1e-4 * dd
             else:
                 cand = U + alpha[None, :] * D
                 cand = torch.where(has_l1 & (torch.sign(cand) != xi), torch.zeros_like(cand), cand)
-                fc = obj.value(cand) + (l1 * cand.abs()).sum(0)
-                ok = (fc <= F + 1e-4 * (pg * (cand - U)).sum(0)) & ~accepted
+                l1t = (l1 * cand.abs()).sum(0)
+                rhs = F + 1e-4 * (pg * (cand - U)).sum(0)
+            if trial == 0 and spec_grad:
+                # the first trial is accepted by most problems once the curvature pairs are in: its gradient
+                # comes from the same pass (a value pass + a gradient pass become one gradient pass)
+                first = obj.value_grad(cand)
+                fc = first[0] + l1t
+            else:
+                fc = obj.value(cand) + l1t
+                late = True
+            ok = (fc <= rhs) & ~accepted
             Un = torch.where(ok[None, :], cand, Un)
             Fn = torch.where(ok, fc, Fn)
             accepted |= ok
+            if _TRACE:
+                print(f"[owlqn] it {it} trial {trial} ok {int(ok.sum())} accepted {int(accepted.sum())}/{P} "
+                      f"alpha {alpha.tolist()}", flush=True)
             if bool(accepted.all()):
                 break
             alpha = torch.where(accepted, alpha, alpha * 0.5)
         failed = ~accepted
         moved = accepted & ~done
-        fn, gn = obj.value_grad(Un)
+        if first is not None and not late:
+            fn, gn = first          # every moved problem sits at the first trial point
+        else:
+            fn, gn = obj.value_grad(Un)
+        spec_grad = spec_on and not late
         s = Un - U
         yv = gn - g
         sy = (s * yv).sum(0)
@@ -518,7 +571,7 @@ class LogisticRegressionLearner(_LinearBase):
         P = len(jobs)
         X, y, W, std, mean, inv_std, reg, en, fi, max_iter, tol, stdz = self._setup(X, y, jobs, par)
         l2 = reg * (1 - en)
-        obj = MultinomialObjective(X, y, W, inv_std, l2, fi, K, par=par)
+        obj = MultinomialObjective(X, y, W, inv_std, l2, fi, K, par=par, wcols=_weight_columns(jobs))
         U0 = torch.zeros(d + 1, K, P, dtype=torch.float64, device=dev)
         cnt = _psum(par, torch.stack([(W * (y == k)[:, None].to(W.dtype)).sum(0)
                                       for k in range(K)]).to(torch.float64))[0]
@@ -546,7 +599,11 @@ class LogisticRegressionLearner(_LinearBase):
         K = int(y.max().item()) + 1 if y.numel() else 2
         par = _row_par(context)
         # mostly-zero wide matrices (hashed text, pivots): dense block + CSR / CSC (ops/linear.py SparseDesign)
-        if par is None and os.environ.get("TMOG_LR_SPARSE", "1") != "0" and LK.SparseDesign.worthwhile(X):
+        from .. import config as _cfg
+        # the multinomial bf16 path streams the whole (compacted) design in bf16 through library GEMMs instead
+        bf16_mnl = self.loss == "logistic" and K > 2 and _cfg.linear_dtype() == "bf16" and X.is_cuda and K <= 16
+        if par is None and not bf16_mnl and os.environ.get("TMOG_LR_SPARSE", "1") != "0" and \
+                LK.SparseDesign.worthwhile(X):
             X = LK.SparseDesign(X)
         if self.loss == "logistic" and K > 2:
             return self._fit_multinomial(X, y, jobs, K, par)

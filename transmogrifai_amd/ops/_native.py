@@ -126,6 +126,7 @@ _HIP_SIGS = {
     "tmog_hip_rff_hist": [P, P, P, I64, I32, P, P, I32, P, P],
     "tmog_hip_binary_areas": [P, I32, P, I64, I32, P, P, P, P],
     "tmog_hip_lr_bf16_blocks_per_cu": [I32, I32],
+    "tmog_hip_mnl_epilogue": [P, I64, I32, I32, P, P, P, I32, P, I32, P, P, P, I32, P],
     "tmog_hip_lr_bf16": [P, I64, I64, I32, P, P, I32, P, I32, P, P, I32, P, I32, P, P, P, I32, P],
 }
 

@@ -263,18 +263,45 @@ _BF16_DMAX = 384        # linear_bf16_kernels.hip: 12 feature blocks of 32 resid
 
 
 class Bf16Design:
-    """A dense fp32 device design matrix rounded once to bf16 for ``fused_objective_bf16``: ``Xb [Npad, dpad]``
+    """A dense fp32 device design matrix stored once in bf16 for ``fused_objective_bf16``: ``Xb [Npad, dpad]``
     row-major, rows padded to a multiple of 32 and columns to a multiple of 32 with zeros (the kernel's 32-row
-    tiles and 32-feature blocks read no ragged edges). One copy serves the value and the gradient products."""
+    tiles and 32-feature blocks read no ragged edges). One copy serves the value and the gradient products.
 
-    def __init__(self, X: torch.Tensor):
+    Columns whose values are all exact in bf16 (one-hot, null indicators, small counts: most of a transmogrified
+    matrix) are stored as they are. Every other column j is stored centred and scaled, ``(x - mu_j) / s_j`` with
+    ``s_j`` the power of two nearest its standard deviation, so its rounding error is relative to its spread, not to
+    its magnitude (a column of values near 19000 with a spread of 10 keeps its information; plain bf16 would round
+    it in steps of 128). The objective folds the shift and scale back exactly: ``X v = Xs (s v) + mu . v`` and
+    ``X^T r = s (Xs^T r) + mu sum(r)``."""
+
+    def __init__(self, X: torch.Tensor, chunk: int = 1 << 18, pad: bool = True):
         N, d = X.shape
         self.N, self.d = int(N), int(d)
-        self.dpad = ((d + 31) // 32) * 32
-        npad = ((N + 31) // 32) * 32
-        self.Xb = torch.zeros(npad, self.dpad, dtype=torch.bfloat16, device=X.device)
-        self.Xb[:N, :d] = X
-        self.device = X.device
+        self.dpad = ((d + 31) // 32) * 32 if pad else int(d)
+        npad = ((N + 31) // 32) * 32 if pad else int(N)
+        dev = X.device
+        exact = torch.ones(d, dtype=torch.bool, device=dev)
+        s1 = torch.zeros(d, dtype=torch.float64, device=dev)
+        s2 = torch.zeros(d, dtype=torch.float64, device=dev)
+        for a in range(0, N, chunk):
+            Xc = X[a:a + chunk]
+            exact &= (Xc.to(torch.bfloat16).to(torch.float32) == Xc).all(0)
+            Xd = Xc.to(torch.float64)
+            s1 += Xd.sum(0)
+            s2 += (Xd * Xd).sum(0)
+        mean = s1 / max(N, 1)
+        std = torch.sqrt((s2 / max(N, 1) - mean * mean).clamp_min(0))
+        e = torch.round(torch.log2(torch.where(std > 0, std, torch.ones_like(std))))
+        self.mu = torch.where(exact, torch.zeros_like(mean), mean.to(torch.float32).to(torch.float64))
+        self.scale = torch.where(exact, torch.ones_like(std), torch.pow(2.0, e))                 # fp64, exact
+        self.shifted = not bool(exact.all())
+        self.n_exact = int(exact.sum())
+        mu32, sc32 = self.mu.to(torch.float32), self.scale.to(torch.float32)
+        self.Xb = torch.zeros(npad, self.dpad, dtype=torch.bfloat16, device=dev)
+        for a in range(0, N, chunk):
+            Xc = X[a:a + chunk]
+            self.Xb[a:a + Xc.shape[0], :d] = (Xc - mu32) / sc32 if self.shifted else Xc
+        self.device = dev
         self.shape = X.shape
 
     @staticmethod
@@ -283,14 +310,29 @@ class Bf16Design:
                 and 1 <= X.shape[1] <= _BF16_DMAX and X.shape[0] >= 1)
 
     @staticmethod
-    def of(X: torch.Tensor) -> "Bf16Design":
+    def of(X: torch.Tensor, pad: bool = True) -> "Bf16Design":
         """The bf16 copy of ``X``, made once per tensor (every grid point and fold of a learner shares the design
-        matrix, and the learners of one selector share it too); dropped with ``X``."""
-        D = getattr(X, "_tmog_bf16", None)
+        matrix, and the learners of one selector share it too); dropped with ``X``. ``pad=False``: the unpadded
+        ``[N, d]`` copy of the library-GEMM paths (``mnl_objective_bf16``)."""
+        attr = "_tmog_bf16" if pad else "_tmog_bf16_plain"
+        D = getattr(X, attr, None)
         if D is None or D[0] != X._version:
-            D = (X._version, Bf16Design(X))
-            X._tmog_bf16 = D
+            D = (X._version, Bf16Design(X, pad=pad))
+            setattr(X, attr, D)
         return D[1]
+
+    def fold_in(self, V: torch.Tensor, bias: torch.Tensor):
+        """Coefficients and bias on the stored (centred / scaled) columns: ``(s v, b + mu . v)`` (fp64)."""
+        if not self.shifted:
+            return V, bias
+        V64 = V.to(torch.float64)
+        return V64 * self.scale[:, None], bias.to(torch.float64) + self.mu @ V64
+
+    def fold_out(self, G: torch.Tensor, rsum: torch.Tensor) -> torch.Tensor:
+        """``X^T r`` from the stored columns' ``Xs^T r`` and ``sum(r)`` per output column."""
+        if not self.shifted:
+            return G
+        return G * self.scale[:, None] + self.mu[:, None] * rsum[None, :]
 
 
 def _bf16_blocks(dpad: int, grad: bool, N: int) -> int:
@@ -324,6 +366,7 @@ def fused_objective_bf16(D: Bf16Design, y: torch.Tensor, W: torch.Tensor, V: tor
     Wf = W.to(torch.float32).contiguous()
     if wmap is None:
         wmap = weight_map(None, P, dev)
+    V, bias = D.fold_in(V, bias)        # centred / scaled columns: s v for the stored columns, mu . v in the bias
     nblk = _bf16_blocks(dpad, grad, N)
     f = torch.empty(P, dtype=torch.float64, device=dev)
     r = torch.empty(P, dtype=torch.float64, device=dev)
@@ -354,7 +397,50 @@ def fused_objective_bf16(D: Bf16Design, y: torch.Tensor, W: torch.Tensor, V: tor
         r[c0:c0 + pc] = rp[:, :pc].sum(0)
         if grad:
             G[:, c0:c0 + pc] = gp[:, :d, :pc].sum(0, dtype=torch.float64)
+    if grad:
+        G = D.fold_out(G, r)
     return f, r, G
+
+
+def split_bf16(A: torch.Tensor) -> torch.Tensor:
+    """``[A_hi | A_lo]`` side by side in bf16: ``A_hi = bf16(A)``, ``A_lo = bf16(A - A_hi)`` (~16 mantissa bits)."""
+    A = A.to(torch.float32)
+    hi = A.to(torch.bfloat16)
+    lo = (A - hi.to(torch.float32)).to(torch.bfloat16)
+    return torch.cat([hi, lo], 1).contiguous()
+
+
+def mnl_objective_bf16(D: Bf16Design, V: torch.Tensor, y: torch.Tensor, W: torch.Tensor, bias: torch.Tensor,
+                       P: int, K: int, grad: bool, wmap: Optional[torch.Tensor] = None):
+    """Multinomial objective of P problems x K classes on the unpadded bf16 design copy ``D`` (``Bf16Design.of(X,
+    pad=False)``): margins by one library GEMM ``Xs [V_hi | V_lo]`` (fp32 out), then ``ops/csrc/hip/mnl_kernels.hip``
+    (softmax, weighted loss, per-block fp64 sums, ``[R_hi | R_lo]``), then the gradient GEMM ``Xs^T [R_hi | R_lo]``.
+    ``V [d, C]`` and ``bias [C]`` problem-major (column ``p * K + k``). Returns ``(f [P], rsum [C], G [d, C] or
+    None)`` in fp64."""
+    from . import _native as N_
+    Xb = D.Xb
+    N, d = Xb.shape
+    C = P * K
+    dev = Xb.device
+    V, bias = D.fold_in(V, bias)
+    M2 = torch.mm(Xb, split_bf16(V), out_dtype=torch.float32)                  # [N, 2C]
+    nblk = max(1, min(4096, (N + 255) // 256))
+    fp = torch.empty(nblk, P, dtype=torch.float64, device=dev)
+    rp = torch.empty(nblk, C, dtype=torch.float64, device=dev)
+    R2 = torch.empty(N, 2 * C, dtype=torch.bfloat16, device=dev) if grad else None
+    yf = y.to(device=dev, dtype=torch.float32).contiguous()
+    Wf = W.to(torch.float32).contiguous()
+    bf = bias.to(torch.float32).contiguous()
+    N_.check(N_.hip().tmog_hip_mnl_epilogue(N_.ptr(M2), N, P, K, N_.ptr(bf), N_.ptr(yf), N_.ptr(Wf), Wf.shape[1],
+                                            N_.ptr(wmap), int(grad), N_.ptr(R2), N_.ptr(fp), N_.ptr(rp),
+                                            nblk, N_.stream(dev)), "mnl_epilogue")
+    del M2
+    f, rs = fp.sum(0), rp.sum(0)
+    G = None
+    if grad:
+        G2 = torch.mm(Xb.t(), R2, out_dtype=torch.float32)                     # [d, 2C]
+        G = D.fold_out(G2[:, :C].to(torch.float64) + G2[:, C:].to(torch.float64), rs)
+    return f, rs, G
 
 
 def _torch_objective(X, y, W, V, bias, loss, yscale, grad):
