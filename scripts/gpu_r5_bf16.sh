@@ -5,7 +5,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_linear_bf16_gpu.py > gpurun_out/r5_bf16_tests.log 2>&1 || { tail -40 gpurun_out/r5_bf16_tests.log; exit 1; }
+timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_linear_bf16_gpu.py tests/test_sanity_kernels_gpu.py > gpurun_out/r5_bf16_tests.log 2>&1 || { tail -40 gpurun_out/r5_bf16_tests.log; exit 1; }
 tail -1 gpurun_out/r5_bf16_tests.log
 for cfg in ${CFGS:-binary-10m lr-rf-1m}; do
 for dt in fp32 bf16; do

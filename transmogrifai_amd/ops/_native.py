@@ -106,6 +106,7 @@ _HIP_SIGS = {
     "tmog_hip_onehot_pivot": [P, P, P, P, I32, I64, P, I64, P],
     "tmog_hip_quantize": [P, I64, I32, P, I32, I32, I32, F32, P, P],
     "tmog_hip_gram_aug": [P, I64, I32, I64, P, P, I32, P, P],
+    "tmog_hip_gram_bf16": [P, I64, I64, I32, P, P],
     "tmog_hip_class_colsum": [P, I64, I32, I64, P, I32, I32, P, P],
     "tmog_hip_logistic_grad": [P, P, P, I64, I32, P],
     "tmog_hip_debug_flags": [I32],

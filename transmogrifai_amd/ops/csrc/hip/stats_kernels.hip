@@ -210,6 +210,105 @@ __global__ void __launch_bounds__(256) gram_aug_kernel(const float* __restrict__
       }
 }
 
+// ------------------------------------------------------------------------------ bf16 Gramian
+// gram_bf16_kernel -- A^T A of a bf16 matrix A [n][lda] on the bf16 matrix cores (v_mfma_f32_32x32x16_bf16:
+// products of bf16 values are exact in fp32). ops/stats.py builds A from the SanityChecker input: the columns
+// whose values are exact in bf16 (one-hot, indicators, counts) as they are, a ones column, and every other column
+// centred and split into three bf16 parts (hi + mid + lo = the fp32 value exactly), so the Gramian of the
+// original columns is assembled exactly from A's blocks in fp64 (8x the K per instruction of the fp32 MFMA of
+// gram_aug_kernel, half the bytes). Same tiling and fp64 flush / chunk fold as gram_aug_kernel: 128 x 128 output
+// tile pairs (upper triangle) x row chunks, 4 waves owning 64 x 64 quadrants; each 32-row stage is stored
+// row-major into double-buffered LDS with 16-byte writes and read back transposed (row on the k axis) with
+// ds_read_b64_tr_b16 (cdna_hip_programming.md T10), rows padded to 320 B so the four rows of a read fall on
+// distinct banks.
+typedef __bf16 gbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 gbf16x4 __attribute__((ext_vector_type(4)));
+typedef short gs16x4 __attribute__((ext_vector_type(4)));
+constexpr int GS = GT + 32;           // LDS row stride (bf16 elements)
+
+__device__ __forceinline__ gbf16x4 gtr_read(const __bf16* p) {
+  const gs16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) gs16x4*)(p));
+  return __builtin_bit_cast(gbf16x4, v);
+}
+
+// operand fragment of k-step s for the 32 columns c0 .. c0 + 31 of a [32 rows][GS] stage: lane l holds column
+// c0 + (l & 31), rows 16 s + 8 (l >> 5) + j (j = 0..7)
+__device__ __forceinline__ gbf16x8 gram_frag(const __bf16* T, int c0, int s, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const __bf16* a = T + (16 * s + 8 * (g >> 1) + q) * GS + c0 + 16 * (g & 1) + 4 * p;
+  const gbf16x4 lo = gtr_read(a), hi = gtr_read(a + 4 * GS);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+__global__ void __launch_bounds__(256) gram_bf16_kernel(const __bf16* __restrict__ A, int64_t n, int64_t lda, int nt,
+                                                        int64_t rows_per_chunk, double* __restrict__ part, int flush) {
+  __shared__ __attribute__((aligned(16))) __bf16 tA[2][GK * GS];
+  __shared__ __attribute__((aligned(16))) __bf16 tB[2][GK * GS];
+  const TilePair tp = tile_pair(blockIdx.x, nt);
+  const int ca = tp.i * GT, cb = tp.j * GT;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = min(n, r0 + rows_per_chunk);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qa = (wave >> 1) * 64, qb = (wave & 1) * 64;
+  const int li = lane & 31, lk = lane >> 5;
+  const int lr = threadIdx.x >> 4, c8 = (threadIdx.x & 15) * 8;      // stage loads: rows lr, lr + 16
+  f32x16 acc[2][2];
+  double dacc[2][2][16];
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      acc[a][b] = f32x16{};
+      for (int e = 0; e < 16; ++e) dacc[a][b][e] = 0.0;
+    }
+  gbf16x8 va[2], vb[2];
+  auto load = [&](int64_t rs) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t r = rs + lr + 16 * u;
+      const int64_t rc = r < r1 ? r : r1 - 1;                 // clamped, then zeroed: loads issued together
+      const gbf16x8 xa = *reinterpret_cast<const gbf16x8*>(A + rc * lda + ca + c8);
+      const gbf16x8 xb = *reinterpret_cast<const gbf16x8*>(A + rc * lda + cb + c8);
+      va[u] = r < r1 ? xa : gbf16x8{};
+      vb[u] = r < r1 ? xb : gbf16x8{};
+    }
+  };
+  if (r0 < r1) load(r0);
+  int stage = 0;
+  for (int64_t rs = r0; rs < r1; rs += GK, ++stage) {
+    const int buf = stage & 1;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      *reinterpret_cast<gbf16x8*>(&tA[buf][(lr + 16 * u) * GS + c8]) = va[u];
+      *reinterpret_cast<gbf16x8*>(&tB[buf][(lr + 16 * u) * GS + c8]) = vb[u];
+    }
+    __syncthreads();
+    if (rs + GK < r1) load(rs + GK);                          // next stage in flight during this stage's MFMAs
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const gbf16x8 a0 = gram_frag(tA[buf], qa, s, lane), a1 = gram_frag(tA[buf], qa + 32, s, lane);
+      const gbf16x8 b0 = gram_frag(tB[buf], qb, s, lane), b1 = gram_frag(tB[buf], qb + 32, s, lane);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if ((stage + 1) % flush == 0) {
+      for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+          for (int e = 0; e < 16; ++e) dacc[a][b][e] += (double)acc[a][b][e];
+          acc[a][b] = f32x16{};
+        }
+    }
+  }
+  double* out = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * GT * GT;
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b)
+      for (int e = 0; e < 16; ++e) {
+        const int row = qa + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * lk;
+        const int col = qb + b * 32 + li;
+        out[row * GT + col] = dacc[a][b][e] + (double)acc[a][b][e];
+      }
+}
+
 // G[D][D] (D = d + L) = sum over chunks of the tile partials, mirrored into the lower triangle.
 __global__ void __launch_bounds__(256) gram_fold_kernel(const double* __restrict__ part, int chunks, int npairs,
                                                         int nt, int D, double* __restrict__ G) {
@@ -598,6 +697,32 @@ int tmog_hip_gram_aug(const float* X, int64_t n, int d, int64_t ld, const float*
   }();
   hipLaunchKernelGGL(gram_aug_kernel, dim3((unsigned)npairs, (unsigned)chunks), dim3(256), 0, stream, X, n, d, ld, mu,
                      y, L, nt, rpc, part, flush);
+  hipLaunchKernelGGL(gram_fold_kernel, dim3(GT * GT / 256, (unsigned)npairs), dim3(256), 0, stream, part,
+                     (int)chunks, npairs, nt, D, G);
+  hipFreeAsync(part, stream);
+  return (int)hipGetLastError();
+}
+
+// G (fp64, [D][D], fully written) = A^T A for a bf16 A [n][lda] whose columns D .. nt * 128 - 1 are zero (lda >=
+// nt * 128, a multiple of 8; A 16-byte aligned).
+int tmog_hip_gram_bf16(const void* A, int64_t n, int64_t lda, int D, double* G, hipStream_t stream) {
+  if (n <= 0 || D <= 0) return -1;
+  const int nt = (D + GT - 1) / GT;
+  if (lda < (int64_t)nt * GT || lda % 8 || (uintptr_t)A % 16) return -2;
+  const int npairs = nt * (nt + 1) / 2;
+  int64_t chunks = (1024 + npairs - 1) / npairs;
+  const int64_t max_chunks = 4096 / npairs > 1 ? 4096 / npairs : 1;
+  if (chunks > max_chunks) chunks = max_chunks;
+  if (chunks > (n + 1023) / 1024) chunks = (n + 1023) / 1024;
+  if (chunks < 1) chunks = 1;
+  int64_t rpc = (n + chunks - 1) / chunks;
+  rpc = (rpc + GK - 1) / GK * GK;
+  chunks = (n + rpc - 1) / rpc;
+  double* part = nullptr;
+  hipError_t e = hipMallocAsync((void**)&part, sizeof(double) * GT * GT * npairs * chunks, stream);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(gram_bf16_kernel, dim3((unsigned)npairs, (unsigned)chunks), dim3(256), 0, stream,
+                     (const __bf16*)A, n, lda, nt, rpc, part, kFlush);
   hipLaunchKernelGGL(gram_fold_kernel, dim3(GT * GT / 256, (unsigned)npairs), dim3(256), 0, stream, part,
                      (int)chunks, npairs, nt, D, G);
   hipFreeAsync(part, stream);

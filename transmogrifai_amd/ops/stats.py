@@ -8,6 +8,8 @@
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, Optional
 
 import torch
@@ -87,6 +89,9 @@ def gram_centered(X: torch.Tensor, mean: torch.Tensor, y_codes: Optional[torch.T
     label counts); otherwise an fp64 torch reference."""
     n, d = X.shape
     L = int(n_labels)
+    if X.is_cuda and X.dtype == torch.float32 and X.stride(1) == 1 and n > 0 and \
+            os.environ.get("TMOG_GRAM_BF16", "1") != "0":
+        return _gram_centered_bf16(X, mean, y_codes, L)
     if X.is_cuda and X.dtype == torch.float32 and X.stride(1) == 1 and n > 0:
         G = torch.empty(d + L, d + L, dtype=torch.float64, device=X.device)
         mu = mean.to(device=X.device, dtype=torch.float32).contiguous()
@@ -100,6 +105,78 @@ def gram_centered(X: torch.Tensor, mean: torch.Tensor, y_codes: Optional[torch.T
         oh[torch.arange(n, device=X.device), y_codes.to(X.device).long()] = 1.0
         A = torch.cat([A, oh], 1)
     return A.t() @ A
+
+
+def _gram_centered_bf16(X: torch.Tensor, mean: torch.Tensor, y_codes, L: int, chunk: int = 1 << 18) -> torch.Tensor:
+    """``gram_centered`` on the bf16 matrix cores (``stats_kernels.hip`` gram_bf16_kernel), exactly: the Gramian of
+    ``B = [X_E | 1 | C_hi | C_mid | C_lo | onehot(y)]`` where ``E`` are the columns whose values are exact in bf16
+    (kept raw) and ``C = X_R - mean_R`` the other columns centred in fp32 as the fp32 kernel does and split into
+    three bf16 parts that sum to it exactly. Every product is exact, sums are fp32 over 256 rows then fp64; the
+    centred blocks of the original columns are assembled from ``B^T B`` in fp64 (the ones column gives the raw
+    column sums and the row count)."""
+    n, d = X.shape
+    dev = X.device
+    exact = torch.ones(d, dtype=torch.bool, device=dev)
+    for a in range(0, n, chunk):
+        Xc = X[a:a + chunk]
+        exact &= (Xc.to(torch.bfloat16).to(torch.float32) == Xc).all(0)
+    E = torch.nonzero(exact).reshape(-1)
+    R = torch.nonzero(~exact).reshape(-1)
+    nE, nR = int(E.numel()), int(R.numel())
+    mu64 = mean.to(device=dev, dtype=torch.float64)
+    mu32 = mu64.to(torch.float32)
+    D = nE + 1 + 3 * nR + L
+    lda = ((D + 127) // 128) * 128
+    B = torch.zeros(n, lda, dtype=torch.bfloat16, device=dev)
+    B[:, :nE] = X.index_select(1, E)
+    B[:, nE] = 1.0
+    iH = nE + 1
+    for a in range(0, n, chunk):
+        C = X[a:a + chunk].index_select(1, R) - mu32[R]
+        h = C.to(torch.bfloat16)
+        r1 = C - h.to(torch.float32)
+        m = r1.to(torch.bfloat16)
+        lo = (r1 - m.to(torch.float32)).to(torch.bfloat16)
+        B[a:a + C.shape[0], iH:iH + nR] = h
+        B[a:a + C.shape[0], iH + nR:iH + 2 * nR] = m
+        B[a:a + C.shape[0], iH + 2 * nR:iH + 3 * nR] = lo
+    iY = iH + 3 * nR
+    if L:
+        B[torch.arange(n, device=dev), iY + y_codes.to(dev).long()] = 1.0
+    GA = torch.empty(D, D, dtype=torch.float64, device=dev)
+    N.check(N.hip().tmog_hip_gram_bf16(N.ptr(B), n, lda, D, N.ptr(GA), N.stream(dev)), "gram_bf16")
+    del B
+    ie = torch.arange(nE, device=dev)
+    io = nE
+    parts = [torch.arange(iH + k * nR, iH + (k + 1) * nR, device=dev) for k in range(3)]
+    iy = torch.arange(iY, iY + L, device=dev)
+
+    def blk(a, b):
+        return GA.index_select(0, a).index_select(1, b)
+
+    muE = mu64.index_select(0, E)
+    sE = GA[io].index_select(0, ie)                     # raw column sums of the exact columns
+    cnt = GA[io, io]
+    SR = sum(GA[io].index_select(0, p) for p in parts)  # sums of the centred other columns
+    G = torch.empty(d + L, d + L, dtype=torch.float64, device=dev)
+    G_EE = blk(ie, ie) - muE[:, None] * sE[None, :] - sE[:, None] * muE[None, :] + cnt * muE[:, None] * muE[None, :]
+    G_ER = sum(blk(ie, p) for p in parts) - muE[:, None] * SR[None, :]
+    G_RR = sum(blk(p, q) for p in parts for q in parts)
+    G[E[:, None], E[None, :]] = G_EE
+    G[E[:, None], R[None, :]] = G_ER
+    G[R[:, None], E[None, :]] = G_ER.t()
+    G[R[:, None], R[None, :]] = G_RR
+    if L:
+        ly = torch.arange(d, d + L, device=dev)
+        nl = GA[iy, io]
+        G_YE = blk(iy, ie) - nl[:, None] * muE[None, :]
+        G_YR = sum(blk(iy, p) for p in parts)
+        G[ly[:, None], E[None, :]] = G_YE
+        G[E[:, None], ly[None, :]] = G_YE.t()
+        G[ly[:, None], R[None, :]] = G_YR
+        G[R[:, None], ly[None, :]] = G_YR.t()
+        G[ly[:, None], ly[None, :]] = blk(iy, iy)
+    return G
 
 
 def _corr_from_gram(G: torch.Tensor, n: int) -> torch.Tensor:
