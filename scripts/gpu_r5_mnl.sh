@@ -1,0 +1,12 @@
+#!/bin/bash
+# fused multinomial bf16 kernel: GPU tests, multiclass-text kernel statistics and bench
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_linear_bf16_gpu.py > gpurun_out/r5_mnl_tests.log 2>&1 || { tail -40 gpurun_out/r5_mnl_tests.log; exit 1; }
+tail -1 gpurun_out/r5_mnl_tests.log
+CFGS=multiclass-text bash scripts/gpu_r5_prof2.sh || exit 1
+o=gpurun_out/r5_mnl_bench_mct.log
+TMOG_FIT_PHASES=1 timeout -k 10 400 python3 -u bench.py --config multiclass-text --steps 3 --warmup 1 --verbose > $o 2>&1 || { tail -20 $o; exit 1; }
+grep -a '^{' $o | grep -o '"value": [0-9.]*\|"holdout_error": [0-9.]*\|"step_s": [^]]*\|"timings": {[^}]*}'

@@ -148,7 +148,7 @@ def _mnl_ref(Xb, V, y, W, bias, P, K):
     return f, R.sum(0), X.t() @ R
 
 
-@pytest.mark.parametrize("N,d,P,K", [(5000, 130, 24, 6), (1203, 33, 5, 3), (700, 64, 40, 16)])
+@pytest.mark.parametrize("N,d,P,K", [(5000, 130, 24, 6), (1203, 33, 5, 3), (700, 64, 40, 16), (2000, 150, 40, 4)])
 def test_multinomial_bf16_matches_fp64(N, d, P, K):
     _need_gpu()
     from transmogrifai_amd.ops import linear as LK
@@ -158,7 +158,7 @@ def test_multinomial_bf16_matches_fp64(N, d, P, K):
     X[:, 5] += 1000.0                                     # large offset: centred before rounding
     D = LK.Bf16Design.of(X, pad=False)
     assert D.shifted and D.n_exact == 5
-    Xb = D.Xb.double() * D.scale + D.mu
+    Xb = D.Xb[:N, :d].double() * D.scale + D.mu
     V = 0.05 * torch.randn(d, P * K, device="cuda")
     bias = 0.1 * torch.randn(P * K, device="cuda")
     y = torch.randint(0, K, (N,), device="cuda").float()
@@ -174,3 +174,23 @@ def test_multinomial_bf16_matches_fp64(N, d, P, K):
     assert ((G - Gr).abs() / mag.clamp_min(1.0)).max() < 1e-4
     fv, rv, Gv = LK.mnl_objective_bf16(D, V, y, Wu, bias, P, K, grad=False, wmap=wmap)
     assert Gv is None and torch.equal(fv, f) and torch.equal(rv, rs)
+
+
+def test_multinomial_fused_equals_library_path(monkeypatch):
+    """The fused kernel (K <= 6) and the library-GEMM path compute the same objective (to the fp32 sums)."""
+    _need_gpu()
+    from transmogrifai_amd.ops import linear as LK
+    torch.manual_seed(9)
+    N, d, P, K = 3001, 200, 32, 5
+    X = torch.randn(N, d, device="cuda")
+    D = LK.Bf16Design.of(X, pad=False)
+    V = 0.05 * torch.randn(d, P * K, device="cuda")
+    bias = 0.1 * torch.randn(P * K, device="cuda")
+    y = torch.randint(0, K, (N,), device="cuda").float()
+    W = (torch.rand(N, 2, device="cuda") < 0.7).float()
+    wmap = torch.tensor([p % 2 for p in range(P)], dtype=torch.int32, device="cuda")
+    a = LK.mnl_objective_bf16(D, V, y, W, bias, P, K, grad=True, wmap=wmap)
+    monkeypatch.setenv("TMOG_MNL_FUSED_BF16", "0")
+    b = LK.mnl_objective_bf16(D, V, y, W, bias, P, K, grad=True, wmap=wmap)
+    for u, v in zip(a, b):
+        assert torch.allclose(u, v, rtol=1e-5, atol=1e-4), (u - v).abs().max()

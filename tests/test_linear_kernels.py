@@ -91,7 +91,7 @@ def test_logistic_regression_gpu_matches_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d1,P,hist_n", [(41, 4, 0), (330, 24, 3), (330, 24, 17), (1201, 7, 10)])
+@pytest.mark.parametrize("d1,P,hist_n", [(41, 4, 0), (330, 24, 3), (330, 24, 17), (1201, 7, 10), (8454, 5, 12)])
 def test_owlqn_direction_kernel_matches_torch(d1, P, hist_n):
     """Fused OWL-QN direction (pseudo-gradient, two-loop recursion over the history ring incl. wrap-around,
     orthant projection) vs the torch spec in fp64."""

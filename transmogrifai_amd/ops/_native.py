@@ -107,6 +107,8 @@ _HIP_SIGS = {
     "tmog_hip_quantize": [P, I64, I32, P, I32, I32, I32, F32, P, P],
     "tmog_hip_gram_aug": [P, I64, I32, I64, P, P, I32, P, P],
     "tmog_hip_gram_bf16": [P, I64, I64, I32, P, P],
+    "tmog_hip_col_bf16_exact": [P, I64, I32, I64, P, P],
+    "tmog_hip_bf16_pack": [P, I64, I64, P, P, P, P, P, P, I64, P],
     "tmog_hip_class_colsum": [P, I64, I32, I64, P, I32, I32, P, P],
     "tmog_hip_logistic_grad": [P, P, P, I64, I32, P],
     "tmog_hip_debug_flags": [I32],
@@ -128,6 +130,7 @@ _HIP_SIGS = {
     "tmog_hip_binary_areas": [P, I32, P, I64, I32, P, P, P, P],
     "tmog_hip_lr_bf16_blocks_per_cu": [I32, I32],
     "tmog_hip_mnl_epilogue": [P, I64, I32, I32, P, P, P, I32, P, I32, P, P, P, I32, P],
+    "tmog_hip_mnl_bf16": [P, I64, I64, I32, P, P, I32, P, I32, I32, P, P, I32, P, P, P, I32, P],
     "tmog_hip_lr_bf16": [P, I64, I64, I32, P, P, I32, P, I32, P, P, I32, P, I32, P, P, P, I32, P],
 }
 

@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(NT) lr_epilogue_grad_kernel(
 // stay in registers (QMAX per thread) and every inner product is an fp64 block reduction. Replaces ~150
 // small torch launches per iteration (the optimiser was launch-bound: ~0.2 s of the LR learner's 0.3 s).
 constexpr int OW_NT = 256;
-constexpr int OW_QMAX = 16;      // d1 <= 4096
+constexpr int OW_QMAX = 48;      // d1 <= 12288 (16 per thread up to 4096)
 constexpr int OW_MMAX = 32;      // history slots
 
 __device__ __forceinline__ double ow_block_sum(double v, double* sh) {
@@ -363,6 +363,7 @@ __device__ __forceinline__ double ow_block_sum(double v, double* sh) {
 }
 __device__ __forceinline__ double ow_sign(double x) { return (double)((x > 0.0) - (x < 0.0)); }
 
+template <int QMAX>
 __global__ void __launch_bounds__(OW_NT) owlqn_direction_kernel(
     const double* __restrict__ U, const double* __restrict__ g, const double* __restrict__ l1,
     const double* __restrict__ S, const double* __restrict__ Y, const double* __restrict__ RHO, int d1, int P,
@@ -370,17 +371,21 @@ __global__ void __launch_bounds__(OW_NT) owlqn_direction_kernel(
     double* __restrict__ dnorm_out) {
   __shared__ double sh[4];
   const int p = blockIdx.x, t = threadIdx.x;
-  double q[OW_QMAX], pgv[OW_QMAX];
+  // q in registers; the pseudo-gradient goes straight to pg_out and is read back by the same thread at the end
+  // (the multinomial columns, (d + 1) K entries, need the registers for q)
+  double q[QMAX];
+  double pn = 0.0;
 #pragma unroll
-  for (int r = 0; r < OW_QMAX; ++r) {
+  for (int r = 0; r < QMAX; ++r) {
     const int i = t + OW_NT * r;
     double pv = 0.0;
     if (i < d1) {
       const int64_t e = (int64_t)i * P + p;
       const double u = U[e], gg = g[e], l = l1[e];
       pv = u > 0.0 ? gg + l : (u < 0.0 ? gg - l : (gg + l < 0.0 ? gg + l : (gg - l > 0.0 ? gg - l : 0.0)));
+      pg_out[e] = pv;
+      pn += pv * pv;
     }
-    pgv[r] = pv;
     q[r] = pv;
   }
   const int k = min(hist_n, m);
@@ -390,14 +395,14 @@ __global__ void __launch_bounds__(OW_NT) owlqn_direction_kernel(
     const double* Sj = S + (int64_t)idx * d1 * P;
     double acc = 0.0;
 #pragma unroll
-    for (int r = 0; r < OW_QMAX; ++r) {
+    for (int r = 0; r < QMAX; ++r) {
       const int i = t + OW_NT * r;
       if (i < d1) acc += Sj[(int64_t)i * P + p] * q[r];
     }
     a[j] = RHO[(int64_t)idx * P + p] * ow_block_sum(acc, sh);
     const double* Yj = Y + (int64_t)idx * d1 * P;
 #pragma unroll
-    for (int r = 0; r < OW_QMAX; ++r) {
+    for (int r = 0; r < QMAX; ++r) {
       const int i = t + OW_NT * r;
       if (i < d1) q[r] -= a[j] * Yj[(int64_t)i * P + p];
     }
@@ -408,7 +413,7 @@ __global__ void __launch_bounds__(OW_NT) owlqn_direction_kernel(
     const double* Yl = Y + (int64_t)last * d1 * P;
     double yy = 0.0, sy = 0.0;
 #pragma unroll
-    for (int r = 0; r < OW_QMAX; ++r) {
+    for (int r = 0; r < QMAX; ++r) {
       const int i = t + OW_NT * r;
       if (i < d1) {
         const double yv = Yl[(int64_t)i * P + p];
@@ -420,7 +425,7 @@ __global__ void __launch_bounds__(OW_NT) owlqn_direction_kernel(
     sy = ow_block_sum(sy, sh);
     const double gam = yy > 0.0 ? sy / fmax(yy, 1e-300) : 1.0;
 #pragma unroll
-    for (int r = 0; r < OW_QMAX; ++r) q[r] *= gam;
+    for (int r = 0; r < QMAX; ++r) q[r] *= gam;
   }
   for (int j = k - 1; j >= 0; --j) {
     const int idx = ((hist_n - 1 - j) % m + m) % m;
@@ -428,30 +433,27 @@ __global__ void __launch_bounds__(OW_NT) owlqn_direction_kernel(
     const double* Yj = Y + (int64_t)idx * d1 * P;
     double acc = 0.0;
 #pragma unroll
-    for (int r = 0; r < OW_QMAX; ++r) {
+    for (int r = 0; r < QMAX; ++r) {
       const int i = t + OW_NT * r;
       if (i < d1) acc += Yj[(int64_t)i * P + p] * q[r];
     }
     const double b = RHO[(int64_t)idx * P + p] * ow_block_sum(acc, sh);
 #pragma unroll
-    for (int r = 0; r < OW_QMAX; ++r) {
+    for (int r = 0; r < QMAX; ++r) {
       const int i = t + OW_NT * r;
       if (i < d1) q[r] += Sj[(int64_t)i * P + p] * (a[j] - b);
     }
   }
-  double pn = 0.0;
 #pragma unroll
-  for (int r = 0; r < OW_QMAX; ++r) {
+  for (int r = 0; r < QMAX; ++r) {
     const int i = t + OW_NT * r;
     if (i < d1) {
       const int64_t e = (int64_t)i * P + p;
-      const double u = U[e], l = l1[e], pv = pgv[r];
+      const double u = U[e], l = l1[e], pv = pg_out[e];
       double dv = -q[r];
       if (l > 0.0 && ow_sign(dv) != ow_sign(-pv)) dv = 0.0;
       D_out[e] = dv;
-      pg_out[e] = pv;
       xi_out[e] = u != 0.0 ? ow_sign(u) : ow_sign(-pv);
-      pn += pv * pv;
     }
   }
   pn = ow_block_sum(pn, sh);
@@ -559,7 +561,11 @@ int tmog_hip_owlqn_direction(const double* U, const double* g, const double* l1,
                              double* dnorm, hipStream_t stream) {
   if (P < 1 || d1 < 1) return 0;
   if (d1 > OW_NT * OW_QMAX || m < 1 || m > OW_MMAX || hist_n < 0) return -2;
-  hipLaunchKernelGGL(owlqn_direction_kernel, dim3(P), dim3(OW_NT), 0, stream, U, g, l1, S, Y, RHO, d1, P, m, hist_n,
+  if (d1 <= 16 * OW_NT)
+    hipLaunchKernelGGL(owlqn_direction_kernel<16>, dim3(P), dim3(OW_NT), 0, stream, U, g, l1, S, Y, RHO, d1, P, m, hist_n,
+                     D, pg, xi, dnorm);
+  else
+    hipLaunchKernelGGL(owlqn_direction_kernel<OW_QMAX>, dim3(P), dim3(OW_NT), 0, stream, U, g, l1, S, Y, RHO, d1, P, m, hist_n,
                      D, pg, xi, dnorm);
   return (int)hipGetLastError();
 }

@@ -309,6 +309,59 @@ __global__ void __launch_bounds__(256) gram_bf16_kernel(const __bf16* __restrict
       }
 }
 
+// col_bf16_exact_kernel -- per column, whether every value of the column is exact in bf16 (the low 16 bits of its
+// fp32 pattern are zero): lane = column, waves stride a row chunk, one atomic OR per thread (order-free).
+__global__ void __launch_bounds__(256) col_bf16_exact_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                             int64_t ld, int64_t rows_per_chunk,
+                                                             unsigned* __restrict__ low_bits) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (c >= d) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = min(n, r0 + rows_per_chunk);
+  unsigned acc = 0;
+  for (int64_t r = r0 + (threadIdx.x >> 6); r < r1; r += 4) acc |= __float_as_uint(X[r * ld + c]) & 0xFFFFu;
+  if (acc) atomicOr(low_bits + c, acc);
+}
+
+// bf16_pack_kernel -- B[r][j] (bf16, row stride ldb) from the fp32 rows of X per output column j:
+//   mode 0 zero, 1 one, 2 X[r][src] as is, 3 / 4 / 5 the high / middle / low bf16 part of (X[r][src] - mu) * sc
+//   (the three parts sum to the fp32 value exactly), 6 (y[r] == src) -- the operand images of gram_bf16_kernel
+// and of the linear learners' bf16 design copy (ops/stats.py, ops/linear.py). Thread = (row, 8 output columns):
+// one 16-byte store.
+__global__ void __launch_bounds__(256) bf16_pack_kernel(const float* __restrict__ X, int64_t n, int64_t ld,
+                                                        const int32_t* __restrict__ y, const int32_t* __restrict__ src,
+                                                        const int32_t* __restrict__ mode, const float* __restrict__ mu,
+                                                        const float* __restrict__ sc, __bf16* __restrict__ B,
+                                                        int64_t ldb) {
+  const int64_t groups = ldb / 8;
+  const int64_t total = n * groups;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / groups;
+    const int j0 = (int)(e - r * groups) * 8;
+    gbf16x8 out;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u;
+      const int m = mode[j];
+      float v = 0.f;
+      if (m == 1) {
+        v = 1.f;
+      } else if (m == 2) {
+        v = X[r * ld + src[j]];
+      } else if (m >= 3 && m <= 5) {
+        const float c = (X[r * ld + src[j]] - mu[j]) * sc[j];
+        const float h = (float)(__bf16)c;
+        const float mid = (float)(__bf16)(c - h);
+        v = m == 3 ? h : (m == 4 ? mid : c - h - mid);
+      } else if (m == 6) {
+        v = y[r] == src[j] ? 1.f : 0.f;
+      }
+      out[u] = (__bf16)v;
+    }
+    *reinterpret_cast<gbf16x8*>(B + r * ldb + j0) = out;
+  }
+}
+
 // G[D][D] (D = d + L) = sum over chunks of the tile partials, mirrored into the lower triangle.
 __global__ void __launch_bounds__(256) gram_fold_kernel(const double* __restrict__ part, int chunks, int npairs,
                                                         int nt, int D, double* __restrict__ G) {
@@ -700,6 +753,36 @@ int tmog_hip_gram_aug(const float* X, int64_t n, int d, int64_t ld, const float*
   hipLaunchKernelGGL(gram_fold_kernel, dim3(GT * GT / 256, (unsigned)npairs), dim3(256), 0, stream, part,
                      (int)chunks, npairs, nt, D, G);
   hipFreeAsync(part, stream);
+  return (int)hipGetLastError();
+}
+
+// low_bits[c] (zeroed here) = OR over the rows of the low 16 bits of column c: zero <=> the column is exact in bf16.
+int tmog_hip_col_bf16_exact(const float* X, int64_t n, int d, int64_t ld, unsigned* low_bits, hipStream_t stream) {
+  if (d <= 0) return 0;
+  hipError_t e = hipMemsetAsync(low_bits, 0, sizeof(unsigned) * d, stream);
+  if (e != hipSuccess) return (int)e;
+  if (n <= 0) return 0;
+  const int cblocks = (d + 63) / 64;
+  int64_t chunks = (2048 + cblocks - 1) / cblocks;
+  if (chunks > (n + 1023) / 1024) chunks = (n + 1023) / 1024;
+  if (chunks < 1) chunks = 1;
+  const int64_t rpc = (n + chunks - 1) / chunks;
+  chunks = (n + rpc - 1) / rpc;
+  hipLaunchKernelGGL(col_bf16_exact_kernel, dim3(cblocks, (unsigned)chunks), dim3(256), 0, stream, X, n, d, ld, rpc,
+                     low_bits);
+  return (int)hipGetLastError();
+}
+
+// B [n][ldb] bf16 (ldb a multiple of 8, B 16-byte aligned) from X per output column: src / mode / mu / sc have ldb
+// entries (bf16_pack_kernel).
+int tmog_hip_bf16_pack(const float* X, int64_t n, int64_t ld, const int32_t* y, const int32_t* src, const int32_t* mode,
+                       const float* mu, const float* sc, void* B, int64_t ldb, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (ldb <= 0 || ldb % 8 || (uintptr_t)B % 16) return -2;
+  const int64_t total = n * (ldb / 8);
+  const unsigned nblk = (unsigned)min((total + 255) / 256, (int64_t)16384);
+  hipLaunchKernelGGL(bf16_pack_kernel, dim3(nblk), dim3(256), 0, stream, X, n, ld, y, src, mode, mu, sc, (__bf16*)B,
+                     ldb);
   return (int)hipGetLastError();
 }
 

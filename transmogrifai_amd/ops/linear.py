@@ -6,6 +6,7 @@ library-shaped GEMMs, fp32 in / fp32 accumulate), on the host through BLAS.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -260,6 +261,7 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
 
 
 _BF16_DMAX = 384        # linear_bf16_kernels.hip: 12 feature blocks of 32 resident in the accumulators
+_SPLIT_K = 16           # row chunks of the X^T R library GEMM (a [d, 2C] output alone is a few dozen tiles)
 
 
 class Bf16Design:
@@ -274,33 +276,30 @@ class Bf16Design:
     it in steps of 128). The objective folds the shift and scale back exactly: ``X v = Xs (s v) + mu . v`` and
     ``X^T r = s (Xs^T r) + mu sum(r)``."""
 
-    def __init__(self, X: torch.Tensor, chunk: int = 1 << 18, pad: bool = True):
+    def __init__(self, X: torch.Tensor, pad: bool = True):
+        from . import stats as ST
         N, d = X.shape
         self.N, self.d = int(N), int(d)
-        self.dpad = ((d + 31) // 32) * 32 if pad else int(d)
-        npad = ((N + 31) // 32) * 32 if pad else int(N)
+        # pad=True: the binary kernel's 32-row tiles and 32-feature blocks; pad=False (multinomial): the fused
+        # kernel's 64-feature chunks and a row count that also splits into _SPLIT_K equal GEMM chunks
+        self.dpad = ((d + 31) // 32) * 32 if pad else ((d + 63) // 64) * 64
+        npad = ((N + 31) // 32) * 32 if pad else ((N + 32 * _SPLIT_K - 1) // (32 * _SPLIT_K)) * 32 * _SPLIT_K
         dev = X.device
-        exact = torch.ones(d, dtype=torch.bool, device=dev)
-        s1 = torch.zeros(d, dtype=torch.float64, device=dev)
-        s2 = torch.zeros(d, dtype=torch.float64, device=dev)
-        for a in range(0, N, chunk):
-            Xc = X[a:a + chunk]
-            exact &= (Xc.to(torch.bfloat16).to(torch.float32) == Xc).all(0)
-            Xd = Xc.to(torch.float64)
-            s1 += Xd.sum(0)
-            s2 += (Xd * Xd).sum(0)
-        mean = s1 / max(N, 1)
-        std = torch.sqrt((s2 / max(N, 1) - mean * mean).clamp_min(0))
+        # one pass for the exactness flags, one (the fp64 stable column moments) for the centres and scales, one
+        # packing pass (stats_kernels.hip bf16_pack_kernel)
+        exact = ST.bf16_exact_columns(X)
+        n_, mean, m2 = ST._col_partials(X)[:3]          # this process's rows (no collective inside a learner)
+        mean = mean.to(torch.float64)
+        std = torch.sqrt((m2.to(torch.float64) / max(int(n_), 1)).clamp_min(0))
         e = torch.round(torch.log2(torch.where(std > 0, std, torch.ones_like(std))))
         self.mu = torch.where(exact, torch.zeros_like(mean), mean.to(torch.float32).to(torch.float64))
         self.scale = torch.where(exact, torch.ones_like(std), torch.pow(2.0, e))                 # fp64, exact
         self.shifted = not bool(exact.all())
         self.n_exact = int(exact.sum())
-        mu32, sc32 = self.mu.to(torch.float32), self.scale.to(torch.float32)
-        self.Xb = torch.zeros(npad, self.dpad, dtype=torch.bfloat16, device=dev)
-        for a in range(0, N, chunk):
-            Xc = X[a:a + chunk]
-            self.Xb[a:a + Xc.shape[0], :d] = (Xc - mu32) / sc32 if self.shifted else Xc
+        src = torch.arange(d, device=dev)
+        mode = torch.where(exact, torch.full_like(src, ST.PACK_RAW), torch.full_like(src, ST.PACK_HI))
+        self.Xb = ST.bf16_pack(X, src, mode, self.mu.to(torch.float32), (1.0 / self.scale).to(torch.float32),
+                               self.dpad, rows=npad)
         self.device = dev
         self.shape = X.shape
 
@@ -419,15 +418,24 @@ def mnl_objective_bf16(D: Bf16Design, V: torch.Tensor, y: torch.Tensor, W: torch
     None)`` in fp64."""
     from . import _native as N_
     Xb = D.Xb
-    N, d = Xb.shape
+    N, d = D.N, D.d
+    npad, dpad = Xb.shape
     C = P * K
     dev = Xb.device
     V, bias = D.fold_in(V, bias)
-    M2 = torch.mm(Xb, split_bf16(V), out_dtype=torch.float32)                  # [N, 2C]
+    if 2 <= K <= _MNL_KMAX and dpad % 64 == 0 and npad % 32 == 0 and os.environ.get("TMOG_MNL_FUSED_BF16", "1") != "0":
+        return _mnl_fused_bf16(D, V, y, W, bias, P, K, grad, wmap)
+    if dpad > d:
+        V = torch.nn.functional.pad(V, (0, 0, 0, dpad - d))
+    M2 = torch.mm(Xb, split_bf16(V), out_dtype=torch.float32)                  # [npad, 2C]
     nblk = max(1, min(4096, (N + 255) // 256))
     fp = torch.empty(nblk, P, dtype=torch.float64, device=dev)
     rp = torch.empty(nblk, C, dtype=torch.float64, device=dev)
-    R2 = torch.empty(N, 2 * C, dtype=torch.bfloat16, device=dev) if grad else None
+    R2 = None
+    if grad:
+        R2 = torch.empty(npad, 2 * C, dtype=torch.bfloat16, device=dev)
+        if npad > N:
+            R2[N:].zero_()
     yf = y.to(device=dev, dtype=torch.float32).contiguous()
     Wf = W.to(torch.float32).contiguous()
     bf = bias.to(torch.float32).contiguous()
@@ -438,8 +446,72 @@ def mnl_objective_bf16(D: Bf16Design, V: torch.Tensor, y: torch.Tensor, W: torch
     f, rs = fp.sum(0), rp.sum(0)
     G = None
     if grad:
-        G2 = torch.mm(Xb.t(), R2, out_dtype=torch.float32)                     # [d, 2C]
-        G = D.fold_out(G2[:, :C].to(torch.float64) + G2[:, C:].to(torch.float64), rs)
+        # split-K by hand: _SPLIT_K row chunks as one batched GEMM, chunk results summed in fp64
+        S = _SPLIT_K if npad % _SPLIT_K == 0 else 1
+        Xs = Xb.view(S, npad // S, dpad).transpose(1, 2)
+        G2 = torch.bmm(Xs, R2.view(S, npad // S, 2 * C), out_dtype=torch.float32).sum(0, dtype=torch.float64)
+        G = D.fold_out(G2[:d, :C] + G2[:d, C:], rs)
+    return f, rs, G
+
+
+_MNL_KMAX = 6           # mnl_kernels.hip mnl_bf16_kernel: K accumulators of 32 x 32 in two waves' VGPRs per SIMD
+
+
+def _mnl_fused_bf16(D: "Bf16Design", V: torch.Tensor, y: torch.Tensor, W: torch.Tensor, bias: torch.Tensor, P: int,
+                    K: int, grad: bool, wmap: Optional[torch.Tensor]):
+    """``mnl_objective_bf16`` through the fused kernel (``mnl_kernels.hip`` mnl_bf16_kernel, 32 problems a launch,
+    class-major columns): margins, softmax, loss and R without a margin matrix in memory; with ``grad`` the
+    launch writes ``[R_hi | R_lo]`` and ``X^T R`` is one split-K library GEMM. ``V``, ``bias`` already folded."""
+    from . import _native as N_
+    Xb = D.Xb
+    N, d = D.N, D.d
+    npad, dpad = Xb.shape
+    dev = Xb.device
+    props = torch.cuda.get_device_properties(dev)
+    nblk = max(1, min((npad // 32 + 7) // 8, props.multi_processor_count))
+    V3 = V.to(torch.float32).reshape(d, P, K)
+    b2 = bias.to(torch.float32).reshape(P, K)
+    wm = torch.arange(P, dtype=torch.int32, device=dev) if wmap is None else wmap.to(dev, torch.int32)
+    Wf = W.to(torch.float32).contiguous()
+    yf = y.to(device=dev, dtype=torch.float32).contiguous()
+    f = torch.empty(P, dtype=torch.float64, device=dev)
+    rs = torch.empty(P * K, dtype=torch.float64, device=dev)
+    G = torch.empty(d, P * K, dtype=torch.float64, device=dev) if grad else None
+    NC = K * 32
+    fp = torch.empty(nblk * 8, 32, dtype=torch.float64, device=dev)
+    rp = torch.empty(nblk * 8, NC, dtype=torch.float64, device=dev)
+    R2 = None
+    if grad:
+        R2 = torch.empty(npad, 2 * NC, dtype=torch.bfloat16, device=dev)
+        if npad > N:
+            R2[N:].zero_()
+    for p0 in range(0, P, 32):
+        pc = min(32, P - p0)
+        # class-major V^T [K * 32, dpad] (column k * 32 + p), zero for padding problems / features
+        Vt = torch.zeros(K, 32, dpad, dtype=torch.float32, device=dev)
+        Vt[:, :pc, :d] = V3[:, p0:p0 + pc, :].permute(2, 1, 0)
+        Vt = Vt.reshape(NC, dpad)
+        hi = Vt.to(torch.bfloat16)
+        Vhl = torch.cat([hi, (Vt - hi.to(torch.float32)).to(torch.bfloat16)], 0).contiguous()
+        bt = torch.zeros(K, 32, dtype=torch.float32, device=dev)
+        bt[:, :pc] = b2[p0:p0 + pc].t()
+        wc = torch.zeros(32, dtype=torch.int32, device=dev)
+        wc[:pc] = wm[p0:p0 + pc]
+        wc[pc:] = wm[p0]
+        N_.check(N_.hip().tmog_hip_mnl_bf16(N_.ptr(Xb), dpad, N, dpad, N_.ptr(yf), N_.ptr(Wf), Wf.shape[1], N_.ptr(wc),
+                                            pc, K, N_.ptr(Vhl), N_.ptr(bt.reshape(-1)), int(grad), N_.ptr(R2),
+                                            N_.ptr(fp), N_.ptr(rp), nblk, N_.stream(dev)), "mnl_bf16")
+        f[p0:p0 + pc] = fp.sum(0)[:pc]
+        rk = rp.sum(0).reshape(K, 32)[:, :pc]                              # [K, pc] -> problem-major
+        rs[p0 * K:(p0 + pc) * K] = rk.t().reshape(-1)
+        if grad:
+            S = _SPLIT_K if npad % _SPLIT_K == 0 else 1
+            Xs = Xb.view(S, npad // S, dpad).transpose(1, 2)
+            G2 = torch.bmm(Xs, R2.view(S, npad // S, 2 * NC), out_dtype=torch.float32).sum(0, dtype=torch.float64)
+            Gk = (G2[:d, :NC] + G2[:d, NC:]).reshape(d, K, 32)[:, :, :pc]      # [d, K, pc]
+            G[:, p0 * K:(p0 + pc) * K] = Gk.permute(0, 2, 1).reshape(d, pc * K)
+    if grad:
+        G = D.fold_out(G, rs)
     return f, rs, G
 
 
@@ -464,7 +536,7 @@ def _torch_objective(X, y, W, V, bias, loss, yscale, grad):
     return (l * Wm).sum(0).to(torch.float64), R.sum(0).to(torch.float64), G
 
 
-_OW_DMAX, _OW_MMAX = 256 * 16, 32
+_OW_DMAX, _OW_MMAX = 256 * 48, 32
 
 
 def owlqn_direction_supported(U: torch.Tensor, m: int) -> bool:

@@ -107,19 +107,54 @@ def gram_centered(X: torch.Tensor, mean: torch.Tensor, y_codes: Optional[torch.T
     return A.t() @ A
 
 
-def _gram_centered_bf16(X: torch.Tensor, mean: torch.Tensor, y_codes, L: int, chunk: int = 1 << 18) -> torch.Tensor:
+def bf16_exact_columns(X: torch.Tensor) -> torch.Tensor:
+    """``[d]`` bool: every value of the column is exact in bf16 (``stats_kernels.hip`` col_bf16_exact_kernel)."""
+    n, d = X.shape
+    bits = torch.empty(d, dtype=torch.int32, device=X.device)
+    N.check(N.hip().tmog_hip_col_bf16_exact(N.ptr(X), n, d, X.stride(0), N.ptr(bits), N.stream(X.device)),
+            "col_bf16_exact")
+    return bits == 0
+
+
+# bf16_pack_kernel column modes
+PACK_ZERO, PACK_ONE, PACK_RAW, PACK_HI, PACK_MID, PACK_LO, PACK_LABEL = range(7)
+
+
+def bf16_pack(X: torch.Tensor, src, mode, mu, sc, ldb: int, rows: Optional[int] = None, y=None) -> torch.Tensor:
+    """``B [rows, ldb]`` bf16 built from the fp32 rows of ``X`` per output column (``stats_kernels.hip``
+    bf16_pack_kernel: zero / one / raw / hi, mid, lo parts of ``(x - mu) * sc`` / label indicator); output columns
+    past ``len(src)`` and rows past ``X``'s are zero."""
+    n = X.shape[0]
+    dev = X.device
+    rows = n if rows is None else rows
+    k = len(src)
+
+    def col(v, dtype):
+        t = torch.zeros(ldb, dtype=dtype, device=dev)
+        if k:
+            t[:k] = torch.as_tensor(v, dtype=dtype).to(dev) if not isinstance(v, torch.Tensor) else v.to(dev, dtype)
+        return t
+    src_t, mode_t = col(src, torch.int32), col(mode, torch.int32)
+    mu_t, sc_t = col(mu, torch.float32), col(sc, torch.float32)
+    B = torch.empty(rows, ldb, dtype=torch.bfloat16, device=dev)
+    if rows > n:
+        B[n:].zero_()
+    yc = None if y is None else y.to(device=dev, dtype=torch.int32).contiguous()
+    N.check(N.hip().tmog_hip_bf16_pack(N.ptr(X), n, X.stride(0), N.ptr(yc), N.ptr(src_t), N.ptr(mode_t), N.ptr(mu_t),
+                                       N.ptr(sc_t), N.ptr(B), ldb, N.stream(dev)), "bf16_pack")
+    return B
+
+
+def _gram_centered_bf16(X: torch.Tensor, mean: torch.Tensor, y_codes, L: int) -> torch.Tensor:
     """``gram_centered`` on the bf16 matrix cores (``stats_kernels.hip`` gram_bf16_kernel), exactly: the Gramian of
     ``B = [X_E | 1 | C_hi | C_mid | C_lo | onehot(y)]`` where ``E`` are the columns whose values are exact in bf16
     (kept raw) and ``C = X_R - mean_R`` the other columns centred in fp32 as the fp32 kernel does and split into
-    three bf16 parts that sum to it exactly. Every product is exact, sums are fp32 over 256 rows then fp64; the
-    centred blocks of the original columns are assembled from ``B^T B`` in fp64 (the ones column gives the raw
-    column sums and the row count)."""
+    three bf16 parts that sum to it exactly (one packing pass, ``bf16_pack``). Every product is exact, sums are
+    fp32 over 256 rows then fp64; the centred blocks of the original columns are assembled from ``B^T B`` in fp64
+    (the ones column gives the raw column sums and the row count)."""
     n, d = X.shape
     dev = X.device
-    exact = torch.ones(d, dtype=torch.bool, device=dev)
-    for a in range(0, n, chunk):
-        Xc = X[a:a + chunk]
-        exact &= (Xc.to(torch.bfloat16).to(torch.float32) == Xc).all(0)
+    exact = bf16_exact_columns(X)
     E = torch.nonzero(exact).reshape(-1)
     R = torch.nonzero(~exact).reshape(-1)
     nE, nR = int(E.numel()), int(R.numel())
@@ -127,27 +162,23 @@ def _gram_centered_bf16(X: torch.Tensor, mean: torch.Tensor, y_codes, L: int, ch
     mu32 = mu64.to(torch.float32)
     D = nE + 1 + 3 * nR + L
     lda = ((D + 127) // 128) * 128
-    B = torch.zeros(n, lda, dtype=torch.bfloat16, device=dev)
-    B[:, :nE] = X.index_select(1, E)
-    B[:, nE] = 1.0
-    iH = nE + 1
-    for a in range(0, n, chunk):
-        C = X[a:a + chunk].index_select(1, R) - mu32[R]
-        h = C.to(torch.bfloat16)
-        r1 = C - h.to(torch.float32)
-        m = r1.to(torch.bfloat16)
-        lo = (r1 - m.to(torch.float32)).to(torch.bfloat16)
-        B[a:a + C.shape[0], iH:iH + nR] = h
-        B[a:a + C.shape[0], iH + nR:iH + 2 * nR] = m
-        B[a:a + C.shape[0], iH + 2 * nR:iH + 3 * nR] = lo
-    iY = iH + 3 * nR
-    if L:
-        B[torch.arange(n, device=dev), iY + y_codes.to(dev).long()] = 1.0
+    zi = torch.zeros(1, dtype=torch.int64, device=dev)
+    src = torch.cat([E, zi, R, R, R, torch.arange(L, device=dev)])
+    mode = torch.cat([torch.full((nE,), PACK_RAW, device=dev), torch.full((1,), PACK_ONE, device=dev),
+                      torch.full((nR,), PACK_HI, device=dev), torch.full((nR,), PACK_MID, device=dev),
+                      torch.full((nR,), PACK_LO, device=dev), torch.full((L,), PACK_LABEL, device=dev)])
+    zf = torch.zeros(nE + 1, dtype=torch.float32, device=dev)
+    muR = mu32.index_select(0, R)
+    mu_cols = torch.cat([zf, muR, muR, muR, torch.zeros(L, dtype=torch.float32, device=dev)])
+    sc_cols = torch.ones(D, dtype=torch.float32, device=dev)
+    B = bf16_pack(X, src, mode, mu_cols, sc_cols, lda, y=y_codes if L else None)
     GA = torch.empty(D, D, dtype=torch.float64, device=dev)
     N.check(N.hip().tmog_hip_gram_bf16(N.ptr(B), n, lda, D, N.ptr(GA), N.stream(dev)), "gram_bf16")
     del B
     ie = torch.arange(nE, device=dev)
     io = nE
+    iH = nE + 1
+    iY = iH + 3 * nR
     parts = [torch.arange(iH + k * nR, iH + (k + 1) * nR, device=dev) for k in range(3)]
     iy = torch.arange(iY, iY + L, device=dev)
 
