@@ -168,6 +168,26 @@ def host():
     return _host
 
 
+_pyhost = None
+
+
+def pyhost():
+    """The host library's CPython-API entry points (``csrc/host/utf8_pack.cpp``), through ``ctypes.PyDLL``: the
+    GIL stays held during the call."""
+    global _pyhost
+    if _pyhost is None:
+        host()                      # built and loaded first (host() takes _lock itself)
+        with _lock:
+            if _pyhost is None:
+                lib = C.PyDLL(str(build.HOST_SO))
+                lib.tmog_utf8_offsets.argtypes = [C.py_object, P]
+                lib.tmog_utf8_offsets.restype = C.c_int64
+                lib.tmog_utf8_copy.argtypes = [C.py_object, P, P]
+                lib.tmog_utf8_copy.restype = C.c_int
+                _pyhost = lib
+    return _pyhost
+
+
 def _release_torch_cache():
     """Native out-of-memory handler (called from a grower thread, GIL taken by ctypes)."""
     try:

@@ -74,8 +74,10 @@ def build_host(force: bool = False) -> Path:
         if force or _stale(HOST_SO, srcs):
             tmp = HOST_SO.with_suffix(f".so.tmp{os.getpid()}")
             cxx = shutil.which("g++") or "c++"
+            import sysconfig
+            # utf8_pack.cpp reads str objects through the CPython API (symbols from the running interpreter)
             _run([cxx, "-O3", "-march=x86-64-v2", "-ffp-contract=off", "-std=c++17", "-fopenmp", "-fPIC", "-shared",
-                  f"-I{CSRC}", "-o", str(tmp)] + [str(s) for s in srcs])
+                  f"-I{CSRC}", f"-I{sysconfig.get_paths()['include']}", "-o", str(tmp)] + [str(s) for s in srcs])
             os.replace(tmp, HOST_SO)
     return HOST_SO
 

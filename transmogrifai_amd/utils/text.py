@@ -244,6 +244,19 @@ def _encode_batch(strings: Sequence[Optional[str]]):
 
 
 def _encode_batch_impl(strings: Sequence[Optional[str]]):
+    if isinstance(strings, list) and strings:
+        # straight from the str objects (ops/csrc/host/utf8_pack.cpp); -1 (a non-str item, a lone surrogate)
+        # falls through to the encode-and-join path
+        from ..ops import _native as N
+        lib = N.pyhost()
+        offs = np.empty(len(strings) + 1, np.int64)
+        tot = int(lib.tmog_utf8_offsets(strings, offs.ctypes.data))
+        if tot >= 0:
+            buf = np.empty(max(tot, 1), np.uint8)
+            if tot == 0:
+                buf[0] = 0
+            if lib.tmog_utf8_copy(strings, offs.ctypes.data, buf.ctypes.data) == 0:
+                return buf, offs
     enc = [s.encode("utf-8") if s else b"" for s in strings]
     offs = np.zeros(len(enc) + 1, np.int64)
     np.cumsum(np.fromiter((len(e) for e in enc), dtype=np.int64, count=len(enc)), out=offs[1:])
