@@ -151,7 +151,9 @@ class TextColumn(Column):
     def __init__(self, ftype, codes: torch.Tensor, vocab: Sequence[str]):
         self.ftype = ftype
         self.codes = codes
-        self.vocab = list(vocab)
+        # row subsets and device moves share their parent's vocabulary list (never mutated): the batch text
+        # results cached per vocabulary object (utils/text.py) then serve the training rows and the hold-out alike
+        self.vocab = vocab if isinstance(vocab, list) else list(vocab)
 
     def __len__(self):
         return int(self.codes.shape[0])

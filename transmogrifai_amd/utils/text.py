@@ -220,6 +220,12 @@ _BATCH_CACHE: "OrderedDict[tuple, tuple]" = None
 _BATCH_CACHE_SIZE = 24
 
 
+def clear_batch_cache() -> None:
+    """Forget every cached batch result (``OpWorkflow.train`` starts each train with an empty cache)."""
+    global _BATCH_CACHE
+    _BATCH_CACHE = None
+
+
 def _cached(strings, kind, params, fn):
     global _BATCH_CACHE
     from collections import OrderedDict

@@ -249,6 +249,10 @@ class OpWorkflow(OpWorkflowCore):
 
     def _train(self, params: Optional[OpParams] = None) -> "OpWorkflowModel":
         timings: Dict[str, float] = {}
+        # every train does its own text work: the batch text results (utils/text.py) are shared between the
+        # fits and transforms of one train, never carried over from an earlier train of the same data
+        from ..utils import text as _text
+        _text.clear_batch_cache()
         t0 = time.time()
         with _Timer(timings, OpStep.DataReadingAndFiltering):
             raw = self.generate_raw_data(params or self.parameters)
