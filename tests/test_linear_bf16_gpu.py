@@ -194,3 +194,39 @@ def test_multinomial_fused_equals_library_path(monkeypatch):
     b = LK.mnl_objective_bf16(D, V, y, W, bias, P, K, grad=True, wmap=wmap)
     for u, v in zip(a, b):
         assert torch.allclose(u, v, rtol=1e-5, atol=1e-4), (u - v).abs().max()
+
+
+def test_objective_graph_replay_equals_eager(monkeypatch):
+    """The captured objective pass (hipGraph) gives the bits of the eager pass, value and gradient, across
+    several replays with different coefficients."""
+    _need_gpu()
+    from transmogrifai_amd import config as CFG
+    from transmogrifai_amd.models import linear as L
+    torch.manual_seed(13)
+    N, d, P = 20000, 90, 36
+    X = torch.randn(N, d, device="cuda")
+    X[:, :10] = (X[:, :10] > 0).float()
+    y = (torch.rand(N, device="cuda") < 0.4).float()
+    W = (torch.rand(N, P, device="cuda") < 0.7).float()
+    inv_std = torch.ones(d, P, device="cuda", dtype=torch.float64)
+    l2 = torch.full((P,), 0.01, device="cuda", dtype=torch.float64)
+    fi = torch.ones(P, dtype=torch.bool, device="cuda")
+    old = CFG.linear_dtype()
+    CFG.set_linear_dtype("bf16")
+    try:
+        monkeypatch.setattr(L, "_LR_GRAPHS", True)
+        og = L.BatchedObjective(X, y, W, inv_std, "logistic", l2, fi)
+        monkeypatch.setattr(L, "_LR_GRAPHS", False)
+        oe = L.BatchedObjective(X, y, W, inv_std, "logistic", l2, fi)
+        for k in range(3):
+            U = 0.1 * torch.randn(d + 1, P, device="cuda", dtype=torch.float64)
+            monkeypatch.setattr(L, "_LR_GRAPHS", True)
+            fg, gg = og.value_grad(U)
+            vg = og.value(U)
+            monkeypatch.setattr(L, "_LR_GRAPHS", False)
+            fe, ge = oe.value_grad(U)
+            ve = oe.value(U)
+            assert torch.equal(fg, fe) and torch.equal(gg, ge) and torch.equal(vg, ve)
+        assert getattr(og, "_graphs", None) and len(og._graphs) == 2
+    finally:
+        CFG.set_linear_dtype(old)

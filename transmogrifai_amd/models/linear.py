@@ -27,6 +27,12 @@ from ..ops.staging import to_device
 from ..stages.base import register_stage
 
 
+# hipGraph replay of the bf16 objective passes (BatchedObjective._capture), TMOG_LR_GRAPH=1. Off by default: on
+# lr-rf-1m the LR lane measured 0.205-0.210 s with it against 0.176-0.177 s eager (profiles/r5_graph_ab_*.log) --
+# the two captures per fit cost more than the launches they save; the passes wait on the line search's syncs
+_LR_GRAPHS = os.environ.get("TMOG_LR_GRAPH", "0") == "1"
+
+
 class BatchedObjective:
     """Smooth objective of P linear problems sharing the design matrix ``X``."""
 
@@ -64,14 +70,54 @@ class BatchedObjective:
             self.Wb = self.Wf if len(uniq) == P else self.Wf[:, uniq].contiguous()
             self.wmap = LK.weight_map([pos[c] for c in wc], P, X.device)
 
-    def _fused_pass(self, U, grad):
+    def _pass_body(self, U, grad):
         V = (U[:self.d] * self.inv_std).to(torch.float32)
         b = torch.where(self.fi, U[self.d], torch.zeros_like(U[self.d])).to(torch.float32)
-        self.passes += 1
         if self.bf16 is not None:
             return LK.fused_objective_bf16(self.bf16, self.yf, self.Wb, V, b, self.loss, self.ysf, grad=grad,
                                            wmap=self.wmap)
         return LK.fused_objective(self.X, self.yf, self.Wf, V, b, self.loss, self.ysf, grad=grad)
+
+    def _fused_pass(self, U, grad):
+        self.passes += 1
+        if self.bf16 is not None and _LR_GRAPHS:
+            g = self._graphs.get(grad) if hasattr(self, "_graphs") else None
+            if g is None and getattr(self, "_graph_ok", True):
+                g = self._capture(U, grad)
+            if g is not None:
+                gU, out, graph = g
+                gU.copy_(U)
+                graph.replay()
+                return tuple(None if t is None else t.clone() for t in out)
+        return self._pass_body(U, grad)
+
+    def _capture(self, U, grad):
+        """The pass (coefficient scaling, the per-chunk pads, the kernel launches, the partial sums and the fold
+        of the centred columns: ~20 launches and their Python) as one hipGraph, replayed for every later pass of
+        this fit: the optimiser's ~230 passes per fit were launch-bound at 1M rows. Capture is thread-local (the
+        other learner lanes keep launching); any failure falls back to the eager pass for this objective."""
+        try:
+            dev = U.device
+            gU = U.detach().clone()
+            cur = torch.cuda.current_stream(dev)
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._pass_body(gU, grad)               # warm-up: lazy initialisation, allocator blocks
+            cur.wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
+                out = self._pass_body(gU, grad)
+            cur.wait_stream(side)
+            if not hasattr(self, "_graphs"):
+                self._graphs = {}
+            self._graphs[grad] = (gU, out, graph)
+            return self._graphs[grad]
+        except Exception as e:  # noqa: BLE001 - eager fallback
+            import logging
+            logging.getLogger(__name__).debug("objective graph capture failed (%r): eager passes", e)
+            self._graph_ok = False
+            return None
 
     def margins(self, U):
         V = (U[:self.d] * self.inv_std).to(self.X.dtype)
