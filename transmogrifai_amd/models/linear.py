@@ -413,8 +413,11 @@ def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max
     from ..utils.cancel import check as _cancel_check
     # the first line-search trial is evaluated with its gradient while the previous iteration's first trial was
     # accepted by every problem (adaptive: a value-only trial is cheaper when backtracking is likely)
-    spec_on = os.environ.get("TMOG_OWLQN_SPEC", "1") != "0"
+    spec_on = os.environ.get("TMOG_OWLQN_SPEC", "0") == "1"     # measured no faster on the headline: opt-in
     spec_grad = spec_on
+    # TMOG_LS_BATCH=k: look at the acceptance every k trials. Measured neutral-to-slower at k = 2, 3 on lr-rf-1m and
+    # multiclass-text (profiles/r5_ls_ab_*.log): the passes, not the synchronisations, are the time
+    ls_batch = max(1, int(os.environ.get("TMOG_LS_BATCH", "1")))
     for it in range(int(max_iter.max().item()) if P else 0):
         _cancel_check()             # maxWait (tuning/validators.py _fit_eval_bounded)
         done |= iters >= max_iter
@@ -458,7 +461,9 @@ def owlqn_batched(obj: BatchedObjective, U0: torch.Tensor, l1: torch.Tensor, max
             if _TRACE:
                 print(f"[owlqn] it {it} trial {trial} ok {int(ok.sum())} accepted {int(accepted.sum())}/{P} "
                       f"alpha {alpha.tolist()}", flush=True)
-            if bool(accepted.all()):
+            # the host looks at the acceptance every ls_batch trials: the next trial is enqueued while the
+            # previous one runs (a trial after everything was accepted changes nothing -- ok is all False)
+            if ((trial + 1) % ls_batch == 0 or trial == max_ls - 1) and bool(accepted.all()):
                 break
             alpha = torch.where(accepted, alpha, alpha * 0.5)
         failed = ~accepted
