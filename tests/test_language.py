@@ -159,3 +159,16 @@ def test_finnish_snowball_stemmer():
              "ihmisille": "ihmis", "eläkkeellä": "eläk", "aatonaattona": "aatonaato", "kirjastossa": "kirjasto"}
     assert {w: finnish_stem(w) for w in pairs} == pairs
     assert LG.analyze("Koirat juoksevat taloissa", "fi") == ["koira", "juoksev", "talo"]
+
+
+def test_arabic_normalization_and_light_stemmer():
+    """ArabicAnalyzer: stop words, Unicode digits -> ASCII, ArabicNormalizer (alef forms, teh marbuta, dotless
+    yeh, tatweel / harakat) and ArabicStemmer (one prefix with its length rule, then the suffix list); the
+    expectations follow the Lucene algorithms -- no reference fixture covers Arabic (parity unpinned)."""
+    from transmogrifai_amd.utils.stemmers import arabic_analyze_stem, arabic_normalize
+    assert arabic_normalize("أإآ") == "ااا" and arabic_normalize("مدرسة") == "مدرسه"
+    assert arabic_normalize("كَتَبَ") == "كتب" and arabic_normalize("كـتـاب") == "كتاب"
+    pairs = {"الكتاب": "كتاب", "والكتاب": "كتاب", "بالمدرسة": "مدرس", "المعلمون": "معلم", "كتابها": "كتاب",
+             "سيارات": "سيار", "وقال": "قال", "وقت": "وقت", "كتب": "كتب"}
+    assert {w: arabic_analyze_stem(w) for w in pairs} == pairs
+    assert LG.analyze("ذهب الطلاب إلى المدرسة في الصباح ٢٠٢٤", "Arabic") == ["ذهب", "طلاب", "مدرس", "صباح", "2024"]

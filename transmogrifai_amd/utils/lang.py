@@ -120,6 +120,14 @@ totuşi toţi trei treia treilea tu tuturor tăi tău ul ului un una unde undeva
 unu unui unuia unul va vi voastre voastră voi vom vor vostru vouă voştri vreo vreun vă zi zice îi îl îmi în îţi ăla
 ălea ăsta ăstea ăştia şi ţi ţie""".split())
 
+# ArabicAnalyzer's stop set (matched before normalisation, as its StopFilter runs first)
+STOPWORDS["ar"] = frozenset("""
+من ومن منها منه في وفي فيها فيه و ف ثم او أو ب بها به ا أ اى اي أي أى لا ولا الا ألا إلا لكن ما وما كما فما عن مع
+اذا إذا ان أن إن انها أنها إنها انه أنه إنه بان بأن فان فأن وان وأن وإن التى التي الذى الذي الذين الى الي إلى إلي
+على عليها عليه اما أما إما ايضا أيضا كل وكل لم ولم لن ولن هى هي هو وهى وهي وهو فهى فهي فهو انت أنت لك لها له هذه
+هذا تلك ذلك هناك كانت كان يكون تكون وكانت وكان غير بعض قد نحو بين بينما منذ ضمن حيث الان الآن خلال بعد قبل حتى
+عند عندما لدى جميع""".split())
+
 _ELISIONS = {"fr": ("l", "m", "t", "qu", "n", "s", "j", "d", "c", "jusqu", "quoiqu", "lorsqu", "puisqu"),
              "it": ("c", "l", "all", "dall", "dell", "nell", "sull", "coll", "pell", "gl", "agl", "dagl",
                     "degl", "negl", "sugl", "un", "m", "t", "s", "v", "d"),
@@ -215,7 +223,7 @@ LANGUAGE_NAMES = {"English": "en", "French": "fr", "German": "de", "Spanish": "e
                   "Brazilian": "pt", "Dutch": "nl", "Swedish": "sv", "Danish": "da", "Norwegian": "no", "Polish": "pl",
                   "Catalan": "ca", "Finnish": "fi", "Turkish": "tr", "Romanian": "ro", "Russian": "ru",
                   "Hungarian": "hu", "Japanese": "ja", "Korean": "ko", "SimplifiedChinese": "zh-cn",
-                  "TraditionalChinese": "zh-tw", "Chinese": "zh"}
+                  "TraditionalChinese": "zh-tw", "Chinese": "zh", "Arabic": "ar"}
 # Lucene CJKAnalyzer languages (LuceneTextAnalyzer.scala: Korean, SimplifiedChinese, TraditionalChinese)
 CJK_BIGRAM = frozenset({"zh", "zh-cn", "zh-tw", "ko"})
 
@@ -251,6 +259,9 @@ def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_t
         return [porter_stem(t) for t in toks if t not in sw and len(t) >= min_token_length]
     from .stemmers import STEMMERS
     stem = STEMMERS.get(language)
+    if language == "ar":          # DecimalDigitFilter: any Unicode decimal digit -> its ASCII digit
+        toks = ["".join(str(unicodedata.digit(c)) if c.isdecimal() and not c.isascii() else c for c in t)
+                for t in toks]
     kept = [t for t in toks if t not in sw]
     if stem is not None:          # the language's Lucene analyzer stems after its stop filter
         kept = [stem(t) for t in kept]

@@ -432,10 +432,50 @@ def danish_stem(word: str) -> str:
     return w
 
 
+# ------------------------------------------------------------------------------------------------- Arabic
+# ArabicAnalyzer: StandardTokenizer, lower case, decimal digits to ASCII, the Arabic stop set, then
+# ArabicNormalizationFilter and ArabicStemFilter (Larkey et al.'s light stemming as Lucene implements it).
+_AR_NORM = {"\u0622": "\u0627", "\u0623": "\u0627", "\u0625": "\u0627",     # alef with madda / hamza -> alef
+            "\u0649": "\u064a",                                            # dotless yeh -> yeh
+            "\u0629": "\u0647"}                                            # teh marbuta -> heh
+_AR_DROP = set("\u0640\u064b\u064c\u064d\u064e\u064f\u0650\u0651\u0652")    # tatweel, harakat
+_AR_PREFIXES = ("\u0627\u0644", "\u0648\u0627\u0644", "\u0628\u0627\u0644", "\u0643\u0627\u0644",
+                "\u0641\u0627\u0644", "\u0644\u0644", "\u0648")
+_AR_SUFFIXES = ("\u0647\u0627", "\u0627\u0646", "\u0627\u062a", "\u0648\u0646", "\u064a\u0646",
+                "\u064a\u0647", "\u064a\u0629", "\u0647", "\u0629", "\u064a")
+
+
+def arabic_normalize(word: str) -> str:
+    """ArabicNormalizer: alef forms -> bare alef, dotless yeh -> yeh, teh marbuta -> heh, tatweel and the
+    harakat removed."""
+    return "".join(_AR_NORM.get(c, c) for c in word if c not in _AR_DROP)
+
+
+def arabic_light_stem(word: str) -> str:
+    """ArabicStemmer: at most one prefix (wa- needs 3 letters left, the others 2), then every listed suffix in
+    turn that leaves at least 2 letters."""
+    w = word
+    for p in _AR_PREFIXES:
+        if (len(p) == 1 and len(w) < 4) or len(w) < len(p) + 2:
+            continue
+        if w.startswith(p):
+            w = w[len(p):]
+            break
+    for sfx in _AR_SUFFIXES:
+        if len(w) >= len(sfx) + 2 and w.endswith(sfx):
+            w = w[:-len(sfx)]
+    return w
+
+
+def arabic_analyze_stem(word: str) -> str:
+    return arabic_light_stem(arabic_normalize(word))
+
+
 from .snowball import dutch_stem, finnish_stem, hungarian_stem, romanian_stem, russian_stem  # noqa: E402
 
 STEMMERS: Dict[str, Callable[[str], str]] = {
     "fr": french_light_stem, "de": german_analyze_stem, "es": spanish_light_stem, "it": italian_light_stem,
     "pt": portuguese_light_stem, "no": norwegian_light_stem, "sv": swedish_stem, "da": danish_stem,
     "ru": russian_stem, "nl": dutch_stem, "ro": romanian_stem, "hu": hungarian_stem, "fi": finnish_stem,
+    "ar": arabic_analyze_stem,
 }
