@@ -96,3 +96,18 @@ def test_native_tokenizer_matches_python_spec_on_mixed_scripts():
     for min_len in (1, 2):
         nat = TU.tokenize_batch(samples, True, min_len).lists()
         assert nat == [TU.tokenize(s, min_token_length=min_len) for s in samples]
+
+
+def test_native_tokenizer_keeps_combining_marks_in_words():
+    """UAX#29 Extend: combining marks (Devanagari vowel signs, Arabic harakat, a decomposed accent) and ZWJ /
+    ZWNJ continue the word they follow, on the Python spec and the native tokenizer alike."""
+    import random
+    assert TU.tokenize("पढ़ रही हैं") == ["पढ़", "रही", "हैं"]
+    assert TU.tokenize("كَتَبَ الدرسَ") == ["كَتَبَ", "الدرسَ"]
+    assert TU.tokenize("café x‍y") == ["café", "x‍y"]
+    rnd = random.Random(5)
+    alpha = "ab किां् َّب 1_.́‌,"
+    samples = ["".join(rnd.choice(alpha) for _ in range(rnd.randint(0, 24))) for _ in range(3000)]
+    for min_len in (1, 2):
+        nat = TU.tokenize_batch(samples, True, min_len).lists()
+        assert nat == [TU.tokenize(s, min_token_length=min_len) for s in samples]

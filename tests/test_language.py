@@ -172,3 +172,15 @@ def test_arabic_normalization_and_light_stemmer():
              "سيارات": "سيار", "وقال": "قال", "وقت": "وقت", "كتب": "كتب"}
     assert {w: arabic_analyze_stem(w) for w in pairs} == pairs
     assert LG.analyze("ذهب الطلاب إلى المدرسة في الصباح ٢٠٢٤", "Arabic") == ["ذهب", "طلاب", "مدرس", "صباح", "2024"]
+
+
+def test_hindi_normalization_and_light_stemmer():
+    """HindiAnalyzer: stop words, digits, HindiNormalizer (nukta, candrabindu, dead n, long -> short vowels) and
+    HindiStemmer (longest suffix class whose word is long enough); Lucene's algorithms, no reference fixture
+    (parity unpinned)."""
+    from transmogrifai_amd.utils.stemmers import hindi_analyze_stem, hindi_normalize
+    assert hindi_normalize("लड़की") == "लडकि"              # nukta dropped, long i -> short i
+    assert hindi_normalize("हँसना") == "हंसना"              # candrabindu -> anusvara
+    pairs = {"लड़कियाँ": "लडक", "किताबें": "किताब", "जाएंगे": "जा", "घरों": "घर", "करता": "कर", "खाना": "खा"}
+    assert {w: hindi_analyze_stem(w) for w in pairs} == pairs
+    assert LG.analyze("लड़कियाँ किताबें पढ़ रही हैं ३", "Hindi") == ["लडक", "किताब", "पढ", "रह", "3"]

@@ -45,7 +45,7 @@ const Tables& tables() {
   return t;
 }
 
-constexpr uint8_t kWord = 1, kDigit = 2, kFallback = 4, kCjk = 8;
+constexpr uint8_t kWord = 1, kDigit = 2, kFallback = 4, kCjk = 8, kMark = 16;
 
 const char* kStop[] = {
     "i", "me", "my", "myself", "we", "our", "ours", "ourselves", "you", "your", "yours", "yourself", "yourselves",
@@ -146,6 +146,8 @@ int64_t tokenize_one(const uint8_t* p, int64_t n, bool lowercase, int min_len, b
   // ideograph and hiragana a token, katakana / hangul runs words, the other characters scanned again)
   std::function<void(int64_t, int64_t)> scan = [&](int64_t lo, int64_t hi) {
     auto is_w = [&](int64_t i) { return i < hi && (T.cls[cps[i]] & kWord); };
+    // continues a word: a word character or a combining mark / ZWJ / ZWNJ (UAX#29 Extend)
+    auto is_wc = [&](int64_t i) { return i < hi && (T.cls[cps[i]] & (kWord | kMark)); };
     auto is_d = [&](int64_t i) { return i < hi && (T.cls[cps[i]] & kDigit); };
     auto is_letter = [&](int64_t i) { return is_w(i) && !is_d(i) && cps[i] != '_'; };
     int64_t i = lo;
@@ -154,20 +156,20 @@ int64_t tokenize_one(const uint8_t* p, int64_t n, bool lowercase, int min_len, b
       if (is_letter(i)) {
         j = i + 1;
         for (;;) {
-          if (is_w(j)) ++j;
+          if (is_wc(j)) ++j;
           else if (j < hi && (cps[j] == '\'' || cps[j] == '.') && is_letter(j + 1)) ++j;
           else break;
         }
       } else if (is_d(i)) {
         j = i + 1;
         for (;;) {
-          if (is_w(j)) ++j;
+          if (is_wc(j)) ++j;
           else if (j < hi && (cps[j] == '.' || cps[j] == ',') && is_d(j + 1)) ++j;
           else break;
         }
       } else if (cps[i] == '_') {
         j = i + 1;
-        while (is_w(j)) ++j;
+        while (is_wc(j)) ++j;
       } else {
         ++i;
         continue;

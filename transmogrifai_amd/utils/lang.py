@@ -128,6 +128,18 @@ STOPWORDS["ar"] = frozenset("""
 هذا تلك ذلك هناك كانت كان يكون تكون وكانت وكان غير بعض قد نحو بين بينما منذ ضمن حيث الان الآن خلال بعد قبل حتى
 عند عندما لدى جميع""".split())
 
+# HindiAnalyzer's stop set (common function words of the Lucene list; matched before normalisation)
+STOPWORDS["hi"] = frozenset("""
+अंदर अत अदि अप अपना अपनि अपनी अपने अभि अभी आदि आप इंहिं इंहें इंहों इतयादि इत्यादि इन इनका इन्हीं इन्हें इन्हों इस इसका इसकि
+इसकी इसके इसमें इसि इसी इसे उंहिं उंहें उंहों उन उनका उनकि उनकी उनके उनको उन्हीं उन्हें उन्हों उस उसके उसि उसी उसे एक एवं एस
+एसे ऐसे ओर और कइ कई कर करता करते करना करने करें कहते कहा का काफि काफ़ी कि किंहें किंहों कितना किन्हें किन्हों किया किर किस
+किसि किसी किसे की कुछ कुल के को कोइ कोई कोन कोनसा कौन कौनसा गया घर जब जहाँ जहां जा जिंहें जिंहों जितना जिधर जिन जिन्हें
+जिन्हों जिस जिसे जीधर जेसा जेसे जैसा जैसे जो तक तब तरह तिंहें तिंहों तिन तिन्हें तिन्हों तिस तिसे तो था थि थी थे दबारा दवारा
+दिया दुसरा दुसरे दूसरे दो द्वारा न नहिं नहीं ना निचे निहायत नीचे ने पर पहले पुरा पूरा पे फिर बनि बनी बहि बही बहुत बाद बाला
+बिलकुल भि भितर भी भीतर मगर मानो मे में यदि यह यहाँ यहां यहि यही या यिह ये रखें रवासा रहा रहे ऱ्वासा लिए लिये लेकिन व वगेरह वरग
+वर्ग वह वहाँ वहां वहिं वहीं वाले वुह वे वग़ैरह संग सकता सकते सबसे सभि सभी साथ साबुत साभ सारा से सो हि ही हुअ हुआ हुइ हुई
+हुए हे हें है हैं हो होता होति होती होते होना होने""".split())
+
 _ELISIONS = {"fr": ("l", "m", "t", "qu", "n", "s", "j", "d", "c", "jusqu", "quoiqu", "lorsqu", "puisqu"),
              "it": ("c", "l", "all", "dall", "dell", "nell", "sull", "coll", "pell", "gl", "agl", "dagl",
                     "degl", "negl", "sugl", "un", "m", "t", "s", "v", "d"),
@@ -223,7 +235,8 @@ LANGUAGE_NAMES = {"English": "en", "French": "fr", "German": "de", "Spanish": "e
                   "Brazilian": "pt", "Dutch": "nl", "Swedish": "sv", "Danish": "da", "Norwegian": "no", "Polish": "pl",
                   "Catalan": "ca", "Finnish": "fi", "Turkish": "tr", "Romanian": "ro", "Russian": "ru",
                   "Hungarian": "hu", "Japanese": "ja", "Korean": "ko", "SimplifiedChinese": "zh-cn",
-                  "TraditionalChinese": "zh-tw", "Chinese": "zh", "Arabic": "ar"}
+                  "TraditionalChinese": "zh-tw", "Chinese": "zh", "Arabic": "ar",
+                  "Hindi": "hi"}
 # Lucene CJKAnalyzer languages (LuceneTextAnalyzer.scala: Korean, SimplifiedChinese, TraditionalChinese)
 CJK_BIGRAM = frozenset({"zh", "zh-cn", "zh-tw", "ko"})
 
@@ -259,7 +272,7 @@ def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_t
         return [porter_stem(t) for t in toks if t not in sw and len(t) >= min_token_length]
     from .stemmers import STEMMERS
     stem = STEMMERS.get(language)
-    if language == "ar":          # DecimalDigitFilter: any Unicode decimal digit -> its ASCII digit
+    if language in ("ar", "hi"):  # DecimalDigitFilter: any Unicode decimal digit -> its ASCII digit
         toks = ["".join(str(unicodedata.digit(c)) if c.isdecimal() and not c.isascii() else c for c in t)
                 for t in toks]
     kept = [t for t in toks if t not in sw]

@@ -471,11 +471,70 @@ def arabic_analyze_stem(word: str) -> str:
     return arabic_light_stem(arabic_normalize(word))
 
 
+# -------------------------------------------------------------------------------------------------- Hindi
+# HindiAnalyzer: StandardTokenizer, lower case, decimal digits, the Hindi stop set, HindiNormalizer (orthographic
+# variants folded), HindiStemmer (the longest suffix of a length class whose word is long enough; Ramanathan &
+# Rao's light stemmer as Lucene implements it).
+_HI_MAP = {"\u0901": "\u0902",                                                   # candrabindu -> bindu
+           "\u0929": "\u0928", "\u0931": "\u0930", "\u0934": "\u0933",       # nukta letters -> base
+           "\u0958": "\u0915", "\u0959": "\u0916", "\u095a": "\u0917", "\u095b": "\u091c",
+           "\u095c": "\u0921", "\u095d": "\u0922", "\u095e": "\u092b", "\u095f": "\u092f",
+           "\u0945": "\u0947", "\u0946": "\u0947", "\u0949": "\u094b", "\u094a": "\u094b",
+           "\u090d": "\u090f", "\u090e": "\u090f", "\u0911": "\u0913", "\u0912": "\u0913",
+           "\u0972": "\u0905", "\u0906": "\u0905", "\u0908": "\u0907", "\u090a": "\u0909",
+           "\u0960": "\u090b", "\u0961": "\u090c", "\u0910": "\u090f", "\u0914": "\u0913",
+           "\u0940": "\u093f", "\u0942": "\u0941", "\u0944": "\u0943", "\u0963": "\u0962",
+           "\u0948": "\u0947", "\u094c": "\u094b"}
+_HI_DROP = set("\u093c\u200d\u200c\u094d")                                   # nukta, ZWJ, ZWNJ, virama
+
+
+def hindi_normalize(word: str) -> str:
+    """HindiNormalizer: dead n (na + virama) -> anusvara, candrabindu -> anusvara, nukta forms -> their base
+    letters, ZWJ / ZWNJ / virama removed, chandra and short e / o signs folded, long vowels -> short."""
+    out = []
+    i, n = 0, len(word)
+    while i < n:
+        c = word[i]
+        if c == "\u0928" and i + 1 < n and word[i + 1] == "\u094d":
+            out.append("\u0902")
+            i += 2
+            continue
+        if c not in _HI_DROP:
+            out.append(_HI_MAP.get(c, c))
+        i += 1
+    return "".join(out)
+
+
+_HI_SUFFIXES = (
+    (5, 6, ("ाएंगी", "ाएंगे", "ाऊंगी", "ाऊंगा", "ाइयाँ", "ाइयों", "ाइयां")),
+    (4, 5, ("ाएगी", "ाएगा", "ाओगी", "ाओगे", "एंगी", "ेंगी", "एंगे", "ेंगे", "ूंगी", "ूंगा", "ातीं", "नाओं", "नाएं",
+            "ताओं", "ताएं", "ियाँ", "ियों", "ियां")),
+    (3, 4, ("ाकर", "ाइए", "ाईं", "ाया", "ेगी", "ेगा", "ोगी", "ोगे", "ाने", "ाना", "ाते", "ाती", "ाता", "तीं", "ाओं",
+            "ाएं", "ुओं", "ुएं", "ुआं")),
+    (2, 3, ("कर", "ाओ", "िए", "ाई", "ाए", "ने", "नी", "ना", "ते", "ीं", "ती", "ता", "ाँ", "ां", "ों", "ें")),
+    (1, 2, ("ो", "े", "ू", "ु", "ी", "ि", "ा")),
+)
+
+
+def hindi_light_stem(word: str) -> str:
+    """HindiStemmer: the first length class (5, 4, 3, 2, 1 characters) with a matching suffix whose word is longer
+    than class length + 1 loses that suffix."""
+    n = len(word)
+    for k, min_len, sufs in _HI_SUFFIXES:
+        if n > min_len and word.endswith(sufs):
+            return word[:-k]
+    return word
+
+
+def hindi_analyze_stem(word: str) -> str:
+    return hindi_light_stem(hindi_normalize(word))
+
+
 from .snowball import dutch_stem, finnish_stem, hungarian_stem, romanian_stem, russian_stem  # noqa: E402
 
 STEMMERS: Dict[str, Callable[[str], str]] = {
     "fr": french_light_stem, "de": german_analyze_stem, "es": spanish_light_stem, "it": italian_light_stem,
     "pt": portuguese_light_stem, "no": norwegian_light_stem, "sv": swedish_stem, "da": danish_stem,
     "ru": russian_stem, "nl": dutch_stem, "ro": romanian_stem, "hu": hungarian_stem, "fi": finnish_stem,
-    "ar": arabic_analyze_stem,
+    "ar": arabic_analyze_stem, "hi": hindi_analyze_stem,
 }

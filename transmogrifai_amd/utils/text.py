@@ -49,11 +49,31 @@ here there when where why how all any both each few more most other some such no
 than too very
 """.split())
 
-# word = runs of letters/digits/underscore, letters may be joined by ' or . , digits by . or ,
+
+
+def _mark_class() -> str:
+    """Regex class of the BMP combining marks (Mn, Mc, Me) and ZWJ / ZWNJ: UAX#29 Extend characters continue
+    the word they follow (Devanagari vowel signs, Arabic harakat ...); scripts/gen/gen_unicode_tables.py gives
+    the native tokenizer the same set."""
+    import unicodedata
+    runs, start = [], None
+    for cp in range(0x10000):
+        m = unicodedata.category(chr(cp)) in ("Mn", "Mc", "Me") or cp in (0x200C, 0x200D)
+        if m and start is None:
+            start = cp
+        elif not m and start is not None:
+            runs.append((start, cp - 1))
+            start = None
+    return "[" + "".join(f"\\u{a:04x}" if a == b else f"\\u{a:04x}-\\u{b:04x}" for a, b in runs) + "]"
+
+
+_MARKS = _mark_class()
+# word = runs of letters/digits/underscore (and the combining marks that follow them), letters may be joined by
+# ' or . , digits by . or ,
 _WORD = re.compile(
-    r"[^\W\d_](?:[\w]|['.](?=[^\W\d_]))*"          # letter-led word (may contain digits)
-    r"|\d(?:[\w]|[.,](?=\d))*"                      # number-led token
-    r"|_+\w*",
+    r"[^\W\d_](?:[\w]|" + _MARKS + r"|['.](?=[^\W\d_]))*"          # letter-led word (may contain digits)
+    r"|\d(?:[\w]|" + _MARKS + r"|[.,](?=\d))*"                      # number-led token
+    r"|_+(?:\w|" + _MARKS + r")*",
     re.UNICODE)
 _CJK = re.compile(r"[぀-ヿ㐀-䶿一-鿿가-힯]")
 
