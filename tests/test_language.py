@@ -184,3 +184,14 @@ def test_hindi_normalization_and_light_stemmer():
     pairs = {"लड़कियाँ": "लडक", "किताबें": "किताब", "जाएंगे": "जा", "घरों": "घर", "करता": "कर", "खाना": "खा"}
     assert {w: hindi_analyze_stem(w) for w in pairs} == pairs
     assert LG.analyze("लड़कियाँ किताबें पढ़ रही हैं ३", "Hindi") == ["लडक", "किताब", "पढ", "रह", "3"]
+
+
+def test_bulgarian_light_stemmer():
+    """BulgarianAnalyzer: stop words and BulgarianStemmer (article, plural with its consonant alternations, final
+    vowels, -ен, ъN); Lucene's algorithm, no reference fixture (parity unpinned)."""
+    from transmogrifai_amd.utils.stemmers import bulgarian_stem
+    pairs = {"книгата": "книг", "градовете": "град", "учителят": "учител", "студентите": "студент",
+             "човекът": "човек", "приятели": "приятял", "езици": "езиц", "стаи": "стаи"}
+    assert {w: bulgarian_stem(w) for w in pairs} == pairs
+    assert LG.analyze("Студентите четат книгите в градовете", "Bulgarian") == ["студент", "четат", "книг", "град"]
+    assert LG.best_language("Това е първата книга, която четем във вторник.", 0.5) == "bg"

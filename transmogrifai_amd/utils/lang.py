@@ -140,6 +140,17 @@ STOPWORDS["hi"] = frozenset("""
 वर्ग वह वहाँ वहां वहिं वहीं वाले वुह वे वग़ैरह संग सकता सकते सबसे सभि सभी साथ साबुत साभ सारा से सो हि ही हुअ हुआ हुइ हुई
 हुए हे हें है हैं हो होता होति होती होते होना होने""".split())
 
+# BulgarianAnalyzer's stop set (Savoy's Bulgarian list, as shipped with Lucene)
+STOPWORDS["bg"] = frozenset("""
+а аз ако ала бе без беше би бил била били било близо бъдат бъде бяха в вас ваш ваша вероятно вече взема ви вие винаги
+все всеки всички всичко всяка във въпреки върху г ги главно го д да дали до докато докога дори досега доста е едва
+един ето за зад заедно заради засега затова защо защото и из или им има имат иска й каза как каква какво както какъв
+като кога когато което които кой който колко която къде където към ли м ме между мен ми мнозина мога могат може моля
+момента му н на над назад най направи напред например нас не него нея ни ние никой нито но някои някой няма обаче
+около освен особено от отгоре отново още пак по повече повечето под поне поради после почти прави пред преди през
+при пък първо с са само се сега си скоро след сме според сред срещу сте съм със също т тази така такива такъв там
+твой те тези ти то това тогава този той толкова точно трябва тук тъй тя тях у харесва ч че често чрез ще щом я""".split())
+
 _ELISIONS = {"fr": ("l", "m", "t", "qu", "n", "s", "j", "d", "c", "jusqu", "quoiqu", "lorsqu", "puisqu"),
              "it": ("c", "l", "all", "dall", "dell", "nell", "sull", "coll", "pell", "gl", "agl", "dagl",
                     "degl", "negl", "sugl", "un", "m", "t", "s", "v", "d"),
@@ -192,7 +203,9 @@ def detect_languages(text: Optional[str]) -> Dict[str, float]:
         out["zh"] = sc["Han"] / letters
     if sc.get("CYRILLIC", 0):
         uk = any(ch in text for ch in "іїєґІЇЄҐ")
-        out["uk" if uk else "ru"] = sc["CYRILLIC"] / letters
+        # Bulgarian writes ъ as a vowel and has no ы / э: ъ without either marks it
+        bg = not uk and any(ch in text for ch in "ъЪ") and not any(ch in text for ch in "ыЫэЭ")
+        out["uk" if uk else ("bg" if bg else "ru")] = sc["CYRILLIC"] / letters
     if sc.get("ARABIC", 0):
         fa = any(ch in text for ch in "پچژگ")
         out["fa" if fa else "ar"] = sc["ARABIC"] / letters
@@ -236,7 +249,7 @@ LANGUAGE_NAMES = {"English": "en", "French": "fr", "German": "de", "Spanish": "e
                   "Catalan": "ca", "Finnish": "fi", "Turkish": "tr", "Romanian": "ro", "Russian": "ru",
                   "Hungarian": "hu", "Japanese": "ja", "Korean": "ko", "SimplifiedChinese": "zh-cn",
                   "TraditionalChinese": "zh-tw", "Chinese": "zh", "Arabic": "ar",
-                  "Hindi": "hi"}
+                  "Hindi": "hi", "Bulgarian": "bg"}
 # Lucene CJKAnalyzer languages (LuceneTextAnalyzer.scala: Korean, SimplifiedChinese, TraditionalChinese)
 CJK_BIGRAM = frozenset({"zh", "zh-cn", "zh-tw", "ko"})
 

@@ -530,11 +530,72 @@ def hindi_analyze_stem(word: str) -> str:
     return hindi_light_stem(hindi_normalize(word))
 
 
+# ---------------------------------------------------------------------------------------------- Bulgarian
+# BulgarianAnalyzer: StandardTokenizer, lower case, the Bulgarian stop set, BulgarianStemmer (Nakov's light
+# stemmer as Lucene implements it: definite article, plural, final vowels, -ен, ъN).
+def _bg_remove_article(w: str) -> str:
+    n = len(w)
+    if n > 6 and w.endswith("ият"):
+        return w[:-3]
+    if n > 5 and w.endswith(("ът", "то", "те", "та", "ия")):
+        return w[:-2]
+    if n > 4 and w.endswith("ят"):
+        return w[:-2]
+    return w
+
+
+def _bg_remove_plural(w: str) -> str:
+    n = len(w)
+    if n > 6:
+        if w.endswith("овци"):
+            return w[:-3]                      # -овци -> -о
+        if w.endswith("ове"):
+            return w[:-3]
+        if w.endswith("еве"):
+            return w[:-3] + "й"                # -еве -> -й
+    if n > 5:
+        if w.endswith("ища"):
+            return w[:-3]
+        if w.endswith("та"):
+            return w[:-2]
+        if w.endswith("ци"):
+            return w[:-2] + "к"
+        if w.endswith("зи"):
+            return w[:-2] + "г"
+        if w[-3] == "е" and w[-1] == "и":
+            return w[:-3] + "я" + w[-2]        # -еXи -> -яX
+    if n > 4:
+        if w.endswith("си"):
+            return w[:-2] + "х"
+        if w.endswith("и"):
+            return w[:-1]
+    return w
+
+
+def bulgarian_stem(word: str) -> str:
+    w = word
+    if len(w) < 4:
+        return w
+    if len(w) > 5 and w.endswith("ища"):
+        return w[:-3]
+    w = _bg_remove_plural(_bg_remove_article(w))
+    if len(w) > 3:
+        if w.endswith("я"):
+            w = w[:-1]
+        if w.endswith(("а", "о", "е")):
+            w = w[:-1]
+    if len(w) > 4 and w.endswith("ен"):
+        w = w[:-2] + "н"
+    if len(w) > 5 and w[-2] == "ъ":
+        w = w[:-2] + w[-1]
+    return w
+
+
 from .snowball import dutch_stem, finnish_stem, hungarian_stem, romanian_stem, russian_stem  # noqa: E402
 
 STEMMERS: Dict[str, Callable[[str], str]] = {
     "fr": french_light_stem, "de": german_analyze_stem, "es": spanish_light_stem, "it": italian_light_stem,
     "pt": portuguese_light_stem, "no": norwegian_light_stem, "sv": swedish_stem, "da": danish_stem,
     "ru": russian_stem, "nl": dutch_stem, "ro": romanian_stem, "hu": hungarian_stem, "fi": finnish_stem,
-    "ar": arabic_analyze_stem, "hi": hindi_analyze_stem,
+    "ar": arabic_analyze_stem, "hi": hindi_analyze_stem, "bg": bulgarian_stem,
 }
