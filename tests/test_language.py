@@ -195,3 +195,14 @@ def test_bulgarian_light_stemmer():
     assert {w: bulgarian_stem(w) for w in pairs} == pairs
     assert LG.analyze("Студентите четат книгите в градовете", "Bulgarian") == ["студент", "четат", "книг", "град"]
     assert LG.best_language("Това е първата книга, която четем във вторник.", 0.5) == "bg"
+
+
+def test_czech_light_stemmer():
+    """CzechAnalyzer: stop words and CzechStemmer (case endings by length class, possessives, final-consonant
+    normalisation); Lucene's algorithm, no reference fixture (parity unpinned)."""
+    from transmogrifai_amd.utils.stemmers import czech_stem
+    pairs = {"hradech": "hrad", "městem": "měst", "ženami": "žn", "studentů": "student", "učitelovi": "učitl",
+             "matčin": "matk", "knihou": "knih", "ptáci": "pták", "muži": "muh"}
+    assert {w: czech_stem(w) for w in pairs} == pairs
+    assert LG.analyze("Studenti čtou knihy v knihovnách a ve městech", "Czech") == ["student", "čto", "knih",
+                                                                                 "knihovn", "měst"]

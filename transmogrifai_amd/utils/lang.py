@@ -47,6 +47,7 @@ _PROFILE = {
     "fi": "ja on ei se että oli hän olla mutta kun ovat tai jos niin myös kuin",
     "tr": "ve bir bu da de için ile çok ama gibi daha olarak olan en ne var",
     "ro": "și în de la cu nu o un care este pe din să se ca mai",
+    "cs": "a se na je že to v z do o s k ve jsou ale jak pro po by jako jsem už jeho které který není také",
 }
 PROFILES: Dict[str, FrozenSet[str]] = {k: frozenset(v.split()) for k, v in _PROFILE.items()}
 
@@ -151,6 +152,16 @@ STOPWORDS["bg"] = frozenset("""
 при пък първо с са само се сега си скоро след сме според сред срещу сте съм със също т тази така такива такъв там
 твой те тези ти то това тогава този той толкова точно трябва тук тъй тя тях у харесва ч че често чрез ще щом я""".split())
 
+# CzechAnalyzer's stop set
+STOPWORDS["cs"] = PROFILES["cs"] | frozenset("""
+a s k o i u v z dnes cz tímto budeš budem byli jseš můj svým ta tomto tohle tuto tyto jej zda proč máte tato kam
+tohoto kdo kteří mi nám tom tomuto mít nic proto kterou byla toho protože asi ho naši napište re což tím takže svých
+její svými jste aj tu tedy teto bylo kde ke pravé ji nad nejsou či pod téma mezi přes ty pak vám ani když však neg
+jsem tento článku články aby jsme před pta jejich byl ještě až bez také pouze první vaše která nás nový tipy pokud
+může strana jeho své jiné zprávy nové není vás jen podle zde už být více bude již než který by které co nebo ten
+tak má při od po jsou jak další ale si se ve to jako za zpět ze do pro je na atd atp jakmile přičemž já on ona ono
+oni ony my vy jí mě mne jemu tomu těm těmu němu němuž jehož jíž jelikož jež jakož načež""".split())
+
 _ELISIONS = {"fr": ("l", "m", "t", "qu", "n", "s", "j", "d", "c", "jusqu", "quoiqu", "lorsqu", "puisqu"),
              "it": ("c", "l", "all", "dall", "dell", "nell", "sull", "coll", "pell", "gl", "agl", "dagl",
                     "degl", "negl", "sugl", "un", "m", "t", "s", "v", "d"),
@@ -249,7 +260,7 @@ LANGUAGE_NAMES = {"English": "en", "French": "fr", "German": "de", "Spanish": "e
                   "Catalan": "ca", "Finnish": "fi", "Turkish": "tr", "Romanian": "ro", "Russian": "ru",
                   "Hungarian": "hu", "Japanese": "ja", "Korean": "ko", "SimplifiedChinese": "zh-cn",
                   "TraditionalChinese": "zh-tw", "Chinese": "zh", "Arabic": "ar",
-                  "Hindi": "hi", "Bulgarian": "bg"}
+                  "Hindi": "hi", "Bulgarian": "bg", "Czech": "cs"}
 # Lucene CJKAnalyzer languages (LuceneTextAnalyzer.scala: Korean, SimplifiedChinese, TraditionalChinese)
 CJK_BIGRAM = frozenset({"zh", "zh-cn", "zh-tw", "ko"})
 

@@ -591,11 +591,51 @@ def bulgarian_stem(word: str) -> str:
     return w
 
 
+# -------------------------------------------------------------------------------------------------- Czech
+# CzechAnalyzer: StandardTokenizer, lower case, the Czech stop set, CzechStemmer (Dolamic & Savoy's light
+# stemmer as Lucene implements it: case endings, possessives, then a normalisation of the final consonants).
+_CS_CASE = (
+    (7, ("atech",)),
+    (6, ("ětem", "etem", "atům")),
+    (5, ("ech", "ich", "ích", "ého", "ěmi", "emi", "ému", "ěte", "ete", "ěti", "eti", "ího", "iho", "ími", "ímu",
+         "imu", "ách", "ata", "aty", "ých", "ama", "ami", "ové", "ovi", "ými")),
+    (4, ("em", "es", "ém", "ím", "ům", "at", "ám", "os", "us", "ým", "mi", "ou")),
+)
+
+
+def czech_stem(word: str) -> str:
+    w = word
+    for min_len, sufs in _CS_CASE:                       # remove case: the longest class whose word is long enough
+        if len(w) > min_len and w.endswith(sufs):
+            w = w[:-len(next(x for x in sufs if w.endswith(x)))]
+            break
+    else:
+        if len(w) > 3 and w[-1] in "aeiouůyáéíýě":
+            w = w[:-1]
+    if len(w) > 5 and w.endswith(("ov", "in", "ův")):  # possessives
+        w = w[:-2]
+    if not w:
+        return w
+    if w.endswith("čt"):                               # normalise
+        return w[:-2] + "ck"
+    if w.endswith("št"):
+        return w[:-2] + "sk"
+    if w[-1] in "cč":
+        return w[:-1] + "k"
+    if w[-1] in "zž":
+        return w[:-1] + "h"
+    if len(w) > 1 and w[-2] == "e":
+        return w[:-2] + w[-1]
+    if len(w) > 2 and w[-2] == "ů":
+        return w[:-2] + "o" + w[-1]
+    return w
+
+
 from .snowball import dutch_stem, finnish_stem, hungarian_stem, romanian_stem, russian_stem  # noqa: E402
 
 STEMMERS: Dict[str, Callable[[str], str]] = {
     "fr": french_light_stem, "de": german_analyze_stem, "es": spanish_light_stem, "it": italian_light_stem,
     "pt": portuguese_light_stem, "no": norwegian_light_stem, "sv": swedish_stem, "da": danish_stem,
     "ru": russian_stem, "nl": dutch_stem, "ro": romanian_stem, "hu": hungarian_stem, "fi": finnish_stem,
-    "ar": arabic_analyze_stem, "hi": hindi_analyze_stem, "bg": bulgarian_stem,
+    "ar": arabic_analyze_stem, "hi": hindi_analyze_stem, "bg": bulgarian_stem, "cs": czech_stem,
 }
