@@ -178,11 +178,11 @@ def test_hindi_normalization_and_light_stemmer():
     """HindiAnalyzer: stop words, digits, HindiNormalizer (nukta, candrabindu, dead n, long -> short vowels) and
     HindiStemmer (longest suffix class whose word is long enough); Lucene's algorithms, no reference fixture
     (parity unpinned)."""
-    from transmogrifai_amd.utils.stemmers import hindi_analyze_stem, hindi_normalize
+    from transmogrifai_amd.utils.stemmers import hindi_light_stem, hindi_normalize
     assert hindi_normalize("लड़की") == "लडकि"              # nukta dropped, long i -> short i
     assert hindi_normalize("हँसना") == "हंसना"              # candrabindu -> anusvara
     pairs = {"लड़कियाँ": "लडक", "किताबें": "किताब", "जाएंगे": "जा", "घरों": "घर", "करता": "कर", "खाना": "खा"}
-    assert {w: hindi_analyze_stem(w) for w in pairs} == pairs
+    assert {w: hindi_light_stem(hindi_normalize(w)) for w in pairs} == pairs
     assert LG.analyze("लड़कियाँ किताबें पढ़ रही हैं ३", "Hindi") == ["लडक", "किताब", "पढ", "रह", "3"]
 
 
@@ -206,3 +206,12 @@ def test_czech_light_stemmer():
     assert {w: czech_stem(w) for w in pairs} == pairs
     assert LG.analyze("Studenti čtou knihy v knihovnách a ve městech", "Czech") == ["student", "čto", "knih",
                                                                                  "knihovn", "měst"]
+
+
+def test_persian_normalization_and_stop_words():
+    """PersianAnalyzer (Lucene 7, no stemmer): ZWNJ splits words, Arabic + Persian normalisation (farsi yeh,
+    keheh, heh variants), digits, then the stop set; detected from its Persian letters (parity unpinned)."""
+    from transmogrifai_amd.utils.stemmers import persian_normalize
+    assert persian_normalize("کتابی") == "كتابي"
+    assert LG.analyze("کتاب‌های خوب را می‌خوانم و این کتاب ۳ است", "Persian") == ["كتاب", "خوب", "خوانم", "كتاب", "3"]
+    assert LG.best_language("کتاب‌های خوب را می‌خوانم", 0.5) == "fa"

@@ -162,6 +162,23 @@ mÅ¯Å¾e strana jeho svÃ© jinÃ© zprÃ¡vy novÃ© nenÃ­ vÃ¡s jen podle zde uÅ¾ bÃ½t vÃ
 tak mÃ¡ pÅ™i od po jsou jak dalÅ¡Ã­ ale si se ve to jako za zpÄ›t ze do pro je na atd atp jakmile pÅ™iÄemÅ¾ jÃ¡ on ona ono
 oni ony my vy jÃ­ mÄ› mne jemu tomu tÄ›m tÄ›mu nÄ›mu nÄ›muÅ¾ jehoÅ¾ jÃ­Å¾ jelikoÅ¾ jeÅ¾ jakoÅ¾ naÄeÅ¾""".split())
 
+# PersianAnalyzer's stop set (normalised forms: its StopFilter runs after the normalisation filters)
+STOPWORDS["fa"] = frozenset("""
+Ø§Ù†Ø§Ù† Ù†Ø¯Ø§Ø´ØªÙ‡ Ø³Ø±Ø§Ø³Ø± Ø®ÙŠØ§Ù‡ Ø§ÙŠØ´Ø§Ù† ÙˆÙŠ ØªØ§ÙƒÙ†ÙˆÙ† Ø¨ÙŠØ´ØªØ±ÙŠ Ø¯ÙˆÙ… Ù¾Ø³ Ù†Ø§Ø´ÙŠ ÙˆÚ¯Ùˆ ÙŠØ§ Ø¯Ø§Ø´ØªÙ†Ø¯ Ø³Ù¾Ø³ Ù‡Ù†Ú¯Ø§Ù… Ù‡Ø±Ú¯Ø² Ù¾Ù†Ø¬ Ù†Ø´Ø§Ù† Ø§Ù…Ø³Ø§Ù„ Ø¯ÙŠÚ¯Ø± Ú¯Ø±ÙˆÙ‡ÙŠ
+Ø´Ø¯Ù†Ø¯ Ú†Ø·ÙˆØ± Ø¯Ù‡ Ùˆ Ø¯Ùˆ Ù†Ø®Ø³ØªÙŠÙ† ÙˆÙ„ÙŠ Ú†Ø±Ø§ Ú†Ù‡ ÙˆØ³Ø· Ù‡ ÙƒØ¯Ø§Ù… Ù‚Ø§Ø¨Ù„ ÙŠÙƒ Ø±ÙØª Ù‡ÙØª Ù‡Ù…Ú†Ù†ÙŠÙ† Ø¯Ø± Ù‡Ø²Ø§Ø± Ø¨Ù„Ù‡ Ø¨Ù„ÙŠ Ø´Ø§ÙŠØ¯ Ø§Ù…Ø§ Ø´Ù†Ø§Ø³ÙŠ Ú¯Ø±ÙØªÙ‡ Ø¯Ù‡Ø¯
+Ø¯Ø§Ø´ØªÙ‡ Ø¯Ø§Ù†Ø³Øª Ø¯Ø§Ø´ØªÙ† Ø®ÙˆØ§Ù‡ÙŠÙ… Ù…ÙŠÙ„ÙŠØ§Ø±Ø¯ ÙˆÙ‚ØªÙŠ Ø§Ù…Ø¯ Ø®ÙˆØ§Ù‡Ø¯ Ø¬Ø² Ø§ÙˆØ±Ø¯Ù‡ Ø´Ø¯Ù‡ Ø¨Ù„ÙƒÙ‡ Ø®Ø¯Ù…Ø§Øª Ø´Ø¯Ù† Ø¨Ø±Ø®ÙŠ Ù†Ø¨ÙˆØ¯ Ø¨Ø³ÙŠØ§Ø±ÙŠ Ø¬Ù„ÙˆÚ¯ÙŠØ±ÙŠ Ø­Ù‚ ÙƒØ±Ø¯Ù†Ø¯
+Ù†ÙˆØ¹ÙŠ Ø¨Ø¹Ø±ÙŠ Ù†ÙƒØ±Ø¯Ù‡ Ù†Ø¸ÙŠØ± Ù†Ø¨Ø§ÙŠØ¯ Ø¨ÙˆØ¯Ù‡ Ø¨ÙˆØ¯Ù† Ø¯Ø§Ø¯ Ø§ÙˆØ±Ø¯ Ù‡Ø³Øª Ø¬Ø§ÙŠÙŠ Ø´ÙˆØ¯ Ø¯Ù†Ø¨Ø§Ù„ Ø¯Ø§Ø¯Ù‡ Ø¨Ø§ÙŠØ¯ Ø³Ø§Ø¨Ù‚ Ù‡ÙŠÚ† Ù‡Ù…Ø§Ù† Ø§Ù†Ø¬Ø§ ÙƒÙ…ØªØ± ÙƒØ¬Ø§Ø³Øª Ú¯Ø±Ø¯Ø¯ ÙƒØ³ÙŠ
+ØªØ± Ù…Ø±Ø¯Ù… ØªØ§Ù† Ø¯Ø§Ø¯Ù† Ø¨ÙˆØ¯Ù†Ø¯ Ø³Ø±ÙŠ Ø¬Ø¯Ø§ Ù†Ø¯Ø§Ø±Ù†Ø¯ Ù…Ú¯Ø± ÙŠÙƒØ¯ÙŠÚ¯Ø± Ø¯Ø§Ø±Ø¯ Ø¯Ù‡Ù†Ø¯ Ø¨Ù†Ø§Ø¨Ø±Ø§ÙŠÙ† Ù‡Ù†Ú¯Ø§Ù…ÙŠ Ø³Ù…Øª Ø¬Ø§ Ø§Ù†Ú†Ù‡ Ø®ÙˆØ¯ Ø¯Ø§Ø¯Ù†Ø¯ Ø²ÙŠØ§Ø¯ Ø¯Ø§Ø±Ù†Ø¯ Ø§Ø«Ø±
+Ø¨Ø¯ÙˆÙ† Ø¨Ù‡ØªØ±ÙŠÙ† Ø¨ÙŠØ´ØªØ± Ø§Ù„Ø¨ØªÙ‡ Ø¨Ù‡ Ø¨Ø±Ø§Ø³Ø§Ø³ Ø¨ÙŠØ±ÙˆÙ† ÙƒØ±Ø¯ Ø¨Ø¹Ø¶ÙŠ Ú¯Ø±ÙØª ØªÙˆÙŠ Ø§ÙŠ Ù…ÙŠÙ„ÙŠÙˆÙ† Ø§Ùˆ Ø¬Ø±ÙŠØ§Ù† ØªÙˆÙ„ Ø¨Ø± Ù…Ø§Ù†Ù†Ø¯ Ø¨Ø±Ø§Ø¨Ø± Ø¨Ø§Ø´ÙŠÙ… Ù…Ø¯ØªÙŠ Ú¯ÙˆÙŠÙ†Ø¯
+Ø§ÙƒÙ†ÙˆÙ† ØªØ§ ØªÙ†Ù‡Ø§ Ø¬Ø¯ÙŠØ¯ Ú†Ù†Ø¯ Ø¨ÙŠ Ù†Ø´Ø¯Ù‡ ÙƒØ±Ø¯Ù† ÙƒØ±Ø¯Ù… Ú¯ÙˆÙŠØ¯ ÙƒØ±Ø¯Ù‡ ÙƒÙ†ÙŠÙ… Ù†Ù…ÙŠ Ù†Ø²Ø¯ Ø±ÙˆÙŠ Ù‚ØµØ¯ ÙÙ‚Ø· Ø¨Ø§Ù„Ø§ÙŠ Ø¯ÙŠÚ¯Ø±Ø§Ù† Ø§ÙŠÙ† Ø¯ÙŠØ±ÙˆØ² ØªÙˆØ³Ø· Ø³ÙˆÙ… Ø§ÙŠÙ…
+Ø¯Ø§Ù†Ù†Ø¯ Ø³ÙˆÙŠ Ø§Ø³ØªÙØ§Ø¯Ù‡ Ø´Ù…Ø§ ÙƒÙ†Ø§Ø± Ø¯Ø§Ø±ÙŠÙ… Ø³Ø§Ø®ØªÙ‡ Ø·ÙˆØ± Ø§Ù…Ø¯Ù‡ Ø±ÙØªÙ‡ Ù†Ø®Ø³Øª Ø¨ÙŠØ³Øª Ù†Ø²Ø¯ÙŠÙƒ Ø·ÙŠ ÙƒÙ†ÙŠØ¯ Ø§Ø² Ø§Ù†Ù‡Ø§ ØªÙ…Ø§Ù…ÙŠ Ø¯Ø§Ø´Øª ÙŠÙƒÙŠ Ø·Ø±ÙŠÙ‚ Ø§Ø´ Ú†ÙŠØ³Øª
+Ø±ÙˆØ¨ Ù†Ù…Ø§ÙŠØ¯ Ú¯ÙØª Ú†Ù†Ø¯ÙŠÙ† Ú†ÙŠØ²ÙŠ ØªÙˆØ§Ù†Ø¯ Ø§Ù… Ø§ÙŠØ§ Ø¨Ø§ Ø§Ù† Ø§ÙŠØ¯ ØªØ±ÙŠÙ† Ø§ÙŠÙ†ÙƒÙ‡ Ø¯ÙŠÚ¯Ø±ÙŠ Ø±Ø§Ù‡ Ù‡Ø§ÙŠÙŠ Ø¨Ø±ÙˆØ² Ù‡Ù…Ú†Ù†Ø§Ù† Ù¾Ø§Ø¹ÙŠÙ† ÙƒØ³ Ø­Ø¯ÙˆØ¯ Ù…Ø®ØªÙ„Ù Ù…Ù‚Ø§Ø¨Ù„
+Ú†ÙŠØ² Ú¯ÙŠØ±Ø¯ Ù†Ø¯Ø§Ø±Ø¯ Ø¶Ø¯ Ù‡Ù…Ú†ÙˆÙ† Ø³Ø§Ø²ÙŠ Ø´Ø§Ù† Ù…ÙˆØ±Ø¯ Ø¨Ø§Ø±Ù‡ Ù…Ø±Ø³ÙŠ Ø®ÙˆÙŠØ´ Ø¨Ø±Ø®ÙˆØ±Ø¯Ø§Ø± Ú†ÙˆÙ† Ø®Ø§Ø±Ø¬ Ø´Ø´ Ù‡Ù†ÙˆØ² ØªØ­Øª Ø¶Ù…Ù† Ù‡Ø³ØªÙŠÙ… Ú¯ÙØªÙ‡ ÙÙƒØ± Ø¨Ø³ÙŠØ§Ø± Ù¾ÙŠØ´
+Ø¨Ø±Ø§ÙŠ Ø±ÙˆØ²Ù‡Ø§ÙŠ Ø§Ù†ÙƒÙ‡ Ù†Ø®ÙˆØ§Ù‡Ø¯ Ø¨Ø§Ù„Ø§ ÙƒÙ„ ÙƒÙŠ Ú†Ù†ÙŠÙ† ÙƒÙ‡ Ú¯ÙŠØ±ÙŠ Ù†ÙŠØ³Øª Ø§Ø³Øª ÙƒØ¬Ø§ ÙƒÙ†Ø¯ Ù†ÙŠØ² ÙŠØ§Ø¨Ø¯ Ø¨Ù†Ø¯ÙŠ Ø­ØªÙŠ ØªÙˆØ§Ù†Ù†Ø¯ Ø¹Ù‚Ø¨ Ø®ÙˆØ§Ø³Øª ÙƒÙ†Ù†Ø¯ Ø¨ÙŠÙ†
+ØªÙ…Ø§Ù… Ù‡Ù…Ù‡ Ù…Ø§ Ø¨Ø§Ø´Ù†Ø¯ Ù…Ø«Ù„ Ø´Ø¯ Ø§Ø±ÙŠ Ø¨Ø§Ø´Ø¯ Ø§Ø±Ù‡ Ø·Ø¨Ù‚ Ø¨Ø¹Ø¯ Ø§Ú¯Ø± ØµÙˆØ±Øª ØºÙŠØ± Ø¬Ø§ÙŠ Ø¨ÙŠØ´ Ø±ÙŠØ²ÙŠ Ø§Ù†Ø¯ Ø²ÙŠØ±Ø§ Ú†Ú¯ÙˆÙ†Ù‡ Ø¨Ø§Ø± Ù„Ø·ÙØ§ Ù…ÙŠ Ø¯Ø±Ø¨Ø§Ø±Ù‡ Ù…Ù†
+Ø¯ÙŠØ¯Ù‡ Ù‡Ù…ÙŠÙ† Ú¯Ø°Ø§Ø±ÙŠ Ø¨Ø±Ø¯Ø§Ø±ÙŠ Ø¹Ù„Øª Ú¯Ø°Ø§Ø´ØªÙ‡ Ù‡Ù… ÙÙˆÙ‚ Ù†Ù‡ Ù‡Ø§ Ø´ÙˆÙ†Ø¯ Ø§Ø¨Ø§Ø¯ Ù‡Ù…ÙˆØ§Ø±Ù‡ Ù‡Ø± Ø§ÙˆÙ„ Ø®ÙˆØ§Ù‡Ù†Ø¯ Ú†Ù‡Ø§Ø± Ù†Ø§Ù… Ø§Ù…Ø±ÙˆØ² Ù…Ø§Ù† Ù‡Ø§ÙŠ Ù‚Ø¨Ù„ ÙƒÙ†Ù… Ø³Ø¹ÙŠ
+ØªØ§Ø²Ù‡ Ø±Ø§ Ù‡Ø³ØªÙ†Ø¯ Ø²ÙŠØ± Ø¬Ù„ÙˆÙŠ Ø¹Ù†ÙˆØ§Ù† Ø¨ÙˆØ¯""".split())
+
 _ELISIONS = {"fr": ("l", "m", "t", "qu", "n", "s", "j", "d", "c", "jusqu", "quoiqu", "lorsqu", "puisqu"),
              "it": ("c", "l", "all", "dall", "dell", "nell", "sull", "coll", "pell", "gl", "agl", "dagl",
                     "degl", "negl", "sugl", "un", "m", "t", "s", "v", "d"),
@@ -218,7 +235,7 @@ def detect_languages(text: Optional[str]) -> Dict[str, float]:
         bg = not uk and any(ch in text for ch in "ÑŠÐª") and not any(ch in text for ch in "Ñ‹Ð«ÑÐ­")
         out["uk" if uk else ("bg" if bg else "ru")] = sc["CYRILLIC"] / letters
     if sc.get("ARABIC", 0):
-        fa = any(ch in text for ch in "Ù¾Ú†Ú˜Ú¯")
+        fa = any(ch in text for ch in "Ù¾Ú†Ú˜Ú¯\u06a9\u06cc")      # + keheh, farsi yeh
         out["fa" if fa else "ar"] = sc["ARABIC"] / letters
     for s, lang in _SCRIPT_LANG.items():
         if sc.get(s, 0):
@@ -260,9 +277,18 @@ LANGUAGE_NAMES = {"English": "en", "French": "fr", "German": "de", "Spanish": "e
                   "Catalan": "ca", "Finnish": "fi", "Turkish": "tr", "Romanian": "ro", "Russian": "ru",
                   "Hungarian": "hu", "Japanese": "ja", "Korean": "ko", "SimplifiedChinese": "zh-cn",
                   "TraditionalChinese": "zh-tw", "Chinese": "zh", "Arabic": "ar",
-                  "Hindi": "hi", "Bulgarian": "bg", "Czech": "cs"}
+                  "Hindi": "hi", "Bulgarian": "bg", "Czech": "cs",
+                  "Persian": "fa"}
 # Lucene CJKAnalyzer languages (LuceneTextAnalyzer.scala: Korean, SimplifiedChinese, TraditionalChinese)
 CJK_BIGRAM = frozenset({"zh", "zh-cn", "zh-tw", "ko"})
+
+
+def _pre_stop_normalizers():
+    from .stemmers import hindi_normalize, persian_normalize
+    return {"hi": hindi_normalize, "fa": persian_normalize}
+
+
+_PRE_STOP_NORMALIZERS = _pre_stop_normalizers()
 
 
 def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_token_length: int = 1) -> List[str]:
@@ -275,6 +301,8 @@ def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_t
         s = text.lower() if to_lowercase else text
         return [t for t in TU.analyze_cjk_bigrams(s, TU.ENGLISH_STOPWORDS) if len(t) >= min_token_length]
     lang = language if language in STOPWORDS else "en"
+    if lang == "fa":              # PersianCharFilter: ZWNJ separates words
+        text = text.replace("\u200c", " ")
     toks = TU.tokenize(text, to_lowercase, 1, stopwords=frozenset())
     el = _ELISIONS.get(lang)
     if el:
@@ -296,9 +324,13 @@ def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_t
         return [porter_stem(t) for t in toks if t not in sw and len(t) >= min_token_length]
     from .stemmers import STEMMERS
     stem = STEMMERS.get(language)
-    if language in ("ar", "hi"):  # DecimalDigitFilter: any Unicode decimal digit -> its ASCII digit
+    if language in ("ar", "hi", "fa"):  # DecimalDigitFilter: any Unicode decimal digit -> its ASCII digit
         toks = ["".join(str(unicodedata.digit(c)) if c.isdecimal() and not c.isascii() else c for c in t)
                 for t in toks]
+    # analyzers whose normalisation filters run before their stop filter (HindiAnalyzer, PersianAnalyzer)
+    pre = _PRE_STOP_NORMALIZERS.get(language)
+    if pre is not None:
+        toks = [pre(t) for t in toks]
     kept = [t for t in toks if t not in sw]
     if stem is not None:          # the language's Lucene analyzer stems after its stop filter
         kept = [stem(t) for t in kept]

@@ -471,6 +471,17 @@ def arabic_analyze_stem(word: str) -> str:
     return arabic_light_stem(arabic_normalize(word))
 
 
+# PersianAnalyzer (no stemmer): ZWNJ splits words, then ArabicNormalizer and PersianNormalizer before the stop set
+_FA_NORM = {"\u06cc": "\u064a", "\u06d2": "\u064a",           # farsi yeh, yeh barree -> yeh
+            "\u06a9": "\u0643",                               # keheh -> kaf
+            "\u06c0": "\u0647", "\u06c1": "\u0647"}          # heh with yeh, heh goal -> heh
+
+
+def persian_normalize(word: str) -> str:
+    """ArabicNormalizer then PersianNormalizer (yeh / kaf / heh variants folded, hamza above removed)."""
+    return "".join(_FA_NORM.get(c, c) for c in arabic_normalize(word) if c != "\u0654")
+
+
 # -------------------------------------------------------------------------------------------------- Hindi
 # HindiAnalyzer: StandardTokenizer, lower case, decimal digits, the Hindi stop set, HindiNormalizer (orthographic
 # variants folded), HindiStemmer (the longest suffix of a length class whose word is long enough; Ramanathan &
@@ -527,7 +538,8 @@ def hindi_light_stem(word: str) -> str:
 
 
 def hindi_analyze_stem(word: str) -> str:
-    return hindi_light_stem(hindi_normalize(word))
+    """HindiStemmer on a token already normalised before the stop filter (lang.analyze)."""
+    return hindi_light_stem(word)
 
 
 # ---------------------------------------------------------------------------------------------- Bulgarian
