@@ -215,3 +215,18 @@ def test_persian_normalization_and_stop_words():
     assert persian_normalize("کتابی") == "كتابي"
     assert LG.analyze("کتاب‌های خوب را می‌خوانم و این کتاب ۳ است", "Persian") == ["كتاب", "خوب", "خوانم", "كتاب", "3"]
     assert LG.best_language("کتاب‌های خوب را می‌خوانم", 0.5) == "fa"
+
+
+def test_turkish_snowball_stemmer_and_analyzer():
+    """TurkishAnalyzer: apostrophe filter, Turkish lower case (I -> ı, İ -> i), stop words, Snowball Turkish
+    (nominal verb suffixes, the noun suffix chains through -ki, U restoration and final-consonant devoicing);
+    the published algorithm, no reference fixture (parity unpinned)."""
+    from transmogrifai_amd.utils.snowball import turkish_lower, turkish_stem
+    pairs = {"kitabı": "kitap", "kitaplarımızdan": "kitap", "evlerinde": "ev", "okullarda": "okul", "ağacı": "ağaç",
+             "çocukların": "çocuk", "masadaki": "masa", "öğrencilerin": "öğrenci", "yapmışlar": "yap",
+             "kalemler": "kalem", "ad": "ad", "ev": "ev"}
+    assert {w: turkish_stem(w) for w in pairs} == pairs
+    assert turkish_lower("IĞDIR İzmir") == "ığdır izmir"
+    assert LG.analyze("Türkiye'nin en büyük şehri İSTANBUL’da kitapları ve okullarında okuyoruz", "Turkish") == [
+        "türki", "büyük", "şehri", "istanbul", "kitap", "okul", "okuyor"]
+    assert LG.best_language("bu kitap çok güzel ve ben onu okudum ama daha bitirmedim", 0.5) == "tr"

@@ -163,6 +163,19 @@ tak má při od po jsou jak další ale si se ve to jako za zpět ze do pro je n
 oni ony my vy jí mě mne jemu tomu těm těmu němu němuž jehož jíž jelikož jež jakož načež""".split())
 
 # PersianAnalyzer's stop set (normalised forms: its StopFilter runs after the normalisation filters)
+STOPWORDS["tr"] = PROFILES["tr"] | frozenset("""
+acaba altmış altı ama ancak arada aslında ayrıca bana bazı belki ben benden beni benim beri beş bile bin bir birçok
+biri birkaç birkez birşey birşeyi biz bize bizden bizi bizim böyle böylece bu buna bunda bundan bunlar bunları
+bunların bunu bunun burada çok çünkü da daha dahi de defa değil diğer diye doksan dokuz dolayı dolayısıyla dört
+edecek eden ederek edilecek ediliyor edilmesi ediyor eğer elli en etmesi etti ettiği ettiğini gibi göre halen hangi
+hatta hem henüz hep hepsi her herhangi herkesin hiç hiçbir için iki ile ilgili ise işte itibaren itibariyle kadar
+karşın katrilyon kendi kendilerine kendini kendisi kendisine kendisini kez ki kim kimden kime kimi kimse kırk milyar
+milyon mu mü mı nasıl ne neden nedenle nerde nerede nereye niye niçin o olan olarak oldu olduğu olduğunu olduklarını
+olmadı olmadığı olmak olması olmayan olmaz olsa olsun olup olur olursa oluyor on ona ondan onlar onlardan onları
+onların onu onun otuz oysa öyle pek rağmen sadece sanki sekiz seksen sen senden seni senin siz sizden sizi sizin şey
+şeyden şeyi şeyler şöyle şu şuna şunda şundan şunları şunu tarafından trilyon tüm üç üzere var vardı ve veya ya
+yani yapacak yapılan yapılması yapıyor yapmak yaptı yaptığı yaptığını yaptıkları yedi yerine yetmiş yine yirmi
+yoksa yüz zaten""".split())
 STOPWORDS["fa"] = frozenset("""
 انان نداشته سراسر خياه ايشان وي تاكنون بيشتري دوم پس ناشي وگو يا داشتند سپس هنگام هرگز پنج نشان امسال ديگر گروهي
 شدند چطور ده و دو نخستين ولي چرا چه وسط ه كدام قابل يك رفت هفت همچنين در هزار بله بلي شايد اما شناسي گرفته دهد
@@ -303,7 +316,16 @@ def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_t
     lang = language if language in STOPWORDS else "en"
     if lang == "fa":              # PersianCharFilter: ZWNJ separates words
         text = text.replace("\u200c", " ")
+    if lang == "tr":
+        # StandardTokenizer keeps a word joined by ' or \u2019 whole, ApostropheFilter then drops the apostrophe
+        # and what follows it (Türkiye'nin -> türkiye); TurkishLowerCaseFilter maps I -> ı and İ -> i
+        text = text.replace("\u2019", "'")
+        if to_lowercase:
+            from .snowball import turkish_lower
+            text = turkish_lower(text)
     toks = TU.tokenize(text, to_lowercase, 1, stopwords=frozenset())
+    if lang == "tr":
+        toks = [t.partition("'")[0] for t in toks]
     el = _ELISIONS.get(lang)
     if el:
         out = []

@@ -12,6 +12,9 @@ Implemented from the published Snowball algorithm descriptions (snowballstem.org
 * :func:`romanian_stem`, :func:`hungarian_stem`, :func:`finnish_stem` -- the RomanianAnalyzer, HungarianAnalyzer
   and FinnishAnalyzer stemmers (steps named in each function). Their outputs are pinned by the algorithms' own
   rules in ``tests/test_language.py``; no reference fixture covers these languages (parity unpinned).
+* :func:`turkish_stem` -- TurkishAnalyzer's Snowball Turkish: a backtracking suffix grammar (nominal verb
+  suffixes, noun suffix chains through -ki) on a small backward-mode matcher with Snowball's cursor and slice
+  semantics, then U restoration and final-consonant devoicing; :func:`turkish_lower` is TurkishLowerCaseFilter.
 
 ``among`` semantics: of the listed suffixes the longest one present is taken, and its condition decides;
 a failing condition does not fall back to a shorter suffix.
@@ -513,3 +516,333 @@ def finnish_stem(word: str) -> str:
     if i >= 2 and w[i - 1] == w[i - 2] and w[i - 1] in _FI_C:
         w = w[:i - 1] + w[i:]
     return w
+
+
+# ----------------------------------------------------------------------------------------------- Turkish
+# TurkishAnalyzer: apostrophe filter, Turkish lower case, stop words, SnowballFilter(Turkish). The Turkish
+# algorithm is a backtracking suffix grammar (nominal verb suffixes, then the noun suffix chains through -ki),
+# so it runs on a small backward-mode matcher with Snowball's cursor / slice semantics: saved cursors are
+# offsets from the end of the word (deletions to their left keep them valid), ``alt`` restores the cursor
+# between alternatives, ``opt`` (try) restores it on failure, and deletions are never undone.
+_TR_V = frozenset("aeıioöuü")
+_TR_U = frozenset("ıiuü")
+_TR_HARMONY = (("a", frozenset("aıou")), ("e", frozenset("eiöü")), ("ı", frozenset("aı")), ("i", frozenset("ei")),
+               ("o", frozenset("ou")), ("ö", frozenset("öü")), ("u", frozenset("ou")), ("ü", frozenset("öü")))
+
+
+class _TrMatcher:
+    __slots__ = ("w", "c", "bra", "ket", "cont")
+
+    def __init__(self, w: str):
+        self.w, self.c, self.bra, self.ket, self.cont = w, len(w), len(w), len(w), True
+
+    def save(self) -> int:
+        return len(self.w) - self.c
+
+    def restore(self, v: int) -> None:
+        self.c = len(self.w) - v
+
+    def eq(self, s: str) -> bool:
+        if self.w.endswith(s, 0, self.c):
+            self.c -= len(s)
+            return True
+        return False
+
+    def among(self, sufs) -> bool:              # longest listed suffix ending at the cursor
+        for s in sufs:
+            if self.eq(s):
+                return True
+        return False
+
+    def isin(self, g) -> bool:
+        if self.c > 0 and self.w[self.c - 1] in g:
+            self.c -= 1
+            return True
+        return False
+
+    def notin(self, g) -> bool:
+        if self.c > 0 and self.w[self.c - 1] not in g:
+            self.c -= 1
+            return True
+        return False
+
+    def goto(self, g) -> bool:                  # stop before the nearest char in g (not consumed)
+        while True:
+            if self.c > 0 and self.w[self.c - 1] in g:
+                return True
+            if self.c <= 0:
+                return False
+            self.c -= 1
+
+    def nxt(self) -> bool:
+        if self.c <= 0:
+            return False
+        self.c -= 1
+        return True
+
+    def test(self, f) -> bool:
+        v = self.save()
+        r = f()
+        self.restore(v)
+        return r
+
+    def alt(self, *fs) -> bool:
+        v = self.save()
+        for f in fs:
+            if f():
+                return True
+            self.restore(v)
+        return False
+
+    def opt(self, f) -> bool:
+        v = self.save()
+        if not f():
+            self.restore(v)
+        return True
+
+    def k(self) -> bool:                        # [  (backward mode: the slice's right end)
+        self.ket = self.c
+        return True
+
+    def cut(self) -> bool:                      # ] delete
+        self.bra = self.c
+        b, k = self.bra, self.ket
+        self.w = self.w[:b] + self.w[k:]
+        if self.c >= k:
+            self.c -= k - b
+        elif self.c > b:
+            self.c = b
+        return True
+
+    def insert(self, s: str) -> bool:           # <+ at the cursor
+        self.w = self.w[:self.c] + s + self.w[self.c:]
+        self.c += len(s)
+        return True
+
+
+def _by_len(*sufs):
+    return tuple(sorted(sufs, key=len, reverse=True))
+
+
+_TR_POSS = _by_len("mız", "miz", "muz", "müz", "nız", "niz", "nuz", "nüz", "m", "n")
+_TR_YDU = _by_len(*(a + v + e for a in "td" for e in ("m", "n", "k", "") for v in "ıiuü"))
+
+
+class _TrStem(_TrMatcher):
+    # ---- conditions on the letters around a suffix
+    def harmony(self) -> bool:
+        def body():
+            if not self.goto(_TR_V):
+                return False
+            return self.alt(*[(lambda ch=ch, g=g: self.eq(ch) and self.goto(g)) for ch, g in _TR_HARMONY])
+        return self.test(body)
+
+    def opt_consonant(self, ch: str) -> bool:
+        # the suffix's optional consonant ch stands after a vowel; without it, the letter two back is a vowel
+        return self.alt(lambda: self.test(lambda: self.eq(ch)) and self.nxt() and self.test(lambda: self.isin(_TR_V)),
+                        lambda: not self.test(lambda: self.eq(ch)) and
+                        self.test(lambda: self.nxt() and self.test(lambda: self.isin(_TR_V))))
+
+    def opt_u(self) -> bool:
+        return self.alt(lambda: self.test(lambda: self.isin(_TR_U)) and self.nxt() and
+                        self.test(lambda: self.notin(_TR_V)),
+                        lambda: not self.test(lambda: self.isin(_TR_U)) and
+                        self.test(lambda: self.nxt() and self.test(lambda: self.notin(_TR_V))))
+
+    # ---- suffix marks
+    def possessives(self):
+        return self.among(_TR_POSS) and self.opt_u()
+
+    def sU(self):
+        return self.harmony() and self.isin(_TR_U) and self.opt_consonant("s")
+
+    def lArI(self):
+        return self.among(("leri", "ları"))
+
+    def yU(self):
+        return self.harmony() and self.isin(_TR_U) and self.opt_consonant("y")
+
+    def nU(self):
+        return self.harmony() and self.among(("ı", "i", "u", "ü"))
+
+    def nUn(self):
+        return self.harmony() and self.among(("ın", "in", "un", "ün")) and self.opt_consonant("n")
+
+    def yA(self):
+        return self.harmony() and self.among(("a", "e")) and self.opt_consonant("y")
+
+    def nA(self):
+        return self.harmony() and self.among(("na", "ne"))
+
+    def DA(self):
+        return self.harmony() and self.among(("da", "de", "ta", "te"))
+
+    def ndA(self):
+        return self.harmony() and self.among(("nda", "nde"))
+
+    def DAn(self):
+        return self.harmony() and self.among(("dan", "den", "tan", "ten"))
+
+    def ndAn(self):
+        return self.harmony() and self.among(("ndan", "nden"))
+
+    def ylA(self):
+        return self.harmony() and self.among(("la", "le")) and self.opt_consonant("y")
+
+    def ki(self):
+        return self.eq("ki")
+
+    def ncA(self):
+        return self.harmony() and self.among(("ca", "ce")) and self.opt_consonant("n")
+
+    def yUm(self):
+        return self.harmony() and self.among(("ım", "im", "um", "üm")) and self.opt_consonant("y")
+
+    def sUn(self):
+        return self.harmony() and self.among(("sın", "sin", "sun", "sün"))
+
+    def yUz(self):
+        return self.harmony() and self.among(("ız", "iz", "uz", "üz")) and self.opt_consonant("y")
+
+    def sUnUz(self):
+        return self.among(("sınız", "siniz", "sunuz", "sünüz"))
+
+    def lAr(self):
+        return self.harmony() and self.among(("ler", "lar"))
+
+    def nUz(self):
+        return self.harmony() and self.among(("ız", "iz", "uz", "üz"))
+
+    def DUr(self):
+        return self.harmony() and self.among(("tır", "tir", "tur", "tür", "dır", "dir", "dur", "dür"))
+
+    def cAsInA(self):
+        return self.among(("casına", "cesine"))
+
+    def yDU(self):
+        return self.harmony() and self.among(_TR_YDU) and self.opt_consonant("y")
+
+    def ysA(self):                              # does not follow vowel harmony
+        return self.among(("sam", "san", "sak", "sem", "sen", "sek", "sa", "se")) and self.opt_consonant("y")
+
+    def ymUs(self):
+        return self.harmony() and self.among(("mış", "miş", "muş", "müş")) and self.opt_consonant("y")
+
+    def yken(self):
+        return self.eq("ken") and self.opt_consonant("y")
+
+    # ---- suffix chains
+    def nominal_verb(self) -> bool:
+        self.k()
+        self.cont = True
+        person = lambda: self.alt(self.sUnUz, self.lAr, self.yUm, self.sUn, self.yUz, lambda: True)  # noqa: E731
+
+        def after_lar():
+            self.opt(lambda: self.k() and self.alt(self.DUr, self.yDU, self.ysA, self.ymUs))
+            self.cont = False
+            return True
+        ok = self.alt(
+            lambda: self.alt(self.ymUs, self.yDU, self.ysA, self.yken),
+            lambda: self.cAsInA() and person() and self.ymUs(),
+            lambda: self.lAr() and self.cut() and after_lar(),
+            lambda: self.nUz() and self.alt(self.yDU, self.ysA),
+            lambda: self.alt(self.sUnUz, self.yUz, self.sUn, self.yUm) and self.cut() and
+            self.opt(lambda: self.k() and self.ymUs()),
+            lambda: self.DUr() and self.cut() and self.opt(lambda: self.k() and person() and self.ymUs()))
+        return ok and self.cut()
+
+    def lar_ki(self) -> bool:                   # [lAr] delete chain_before_ki
+        return self.k() and self.lAr() and self.cut() and self.chain_ki()
+
+    def poss_or_su(self) -> bool:               # [possessives or sU] delete try([lAr] delete chain_before_ki)
+        return self.k() and self.alt(self.possessives, self.sU) and self.cut() and self.opt(self.lar_ki)
+
+    def chain_ki(self) -> bool:
+        if not (self.k() and self.ki()):
+            return False
+        return self.alt(
+            lambda: self.DA() and self.cut() and self.opt(lambda: self.k() and self.alt(
+                lambda: self.lAr() and self.cut() and self.opt(self.chain_ki),
+                lambda: self.possessives() and self.cut() and self.opt(self.lar_ki))),
+            lambda: self.nUn() and self.cut() and self.opt(lambda: self.k() and self.alt(
+                lambda: self.lArI() and self.cut(),
+                self.poss_or_su,
+                self.chain_ki)),
+            lambda: self.ndA() and self.alt(
+                lambda: self.lArI() and self.cut(),
+                lambda: self.sU() and self.cut() and self.opt(self.lar_ki),
+                self.chain_ki))
+
+    def noun(self) -> bool:
+        return self.alt(
+            lambda: self.k() and self.lAr() and self.cut() and self.opt(self.chain_ki),
+            lambda: self.k() and self.ncA() and self.cut() and self.opt(lambda: self.alt(
+                lambda: self.k() and self.lArI() and self.cut(),
+                self.poss_or_su,
+                self.lar_ki)),
+            lambda: self.k() and self.alt(self.ndA, self.nA) and self.alt(
+                lambda: self.lArI() and self.cut(),
+                lambda: self.sU() and self.cut() and self.opt(self.lar_ki),
+                self.chain_ki),
+            lambda: self.k() and self.alt(self.ndAn, self.nU) and self.alt(
+                lambda: self.sU() and self.cut() and self.opt(self.lar_ki),
+                self.lArI),
+            lambda: self.k() and self.DAn() and self.cut() and self.opt(lambda: self.k() and self.alt(
+                lambda: self.possessives() and self.cut() and self.opt(self.lar_ki),
+                lambda: self.lAr() and self.cut() and self.opt(self.chain_ki),
+                self.chain_ki)),
+            lambda: self.k() and self.alt(self.nUn, self.ylA) and self.cut() and self.opt(lambda: self.alt(
+                self.lar_ki,
+                self.poss_or_su,
+                self.chain_ki)),
+            lambda: self.k() and self.lArI() and self.cut(),
+            self.chain_ki,
+            lambda: self.k() and self.alt(self.DA, self.yU, self.yA) and self.cut() and self.opt(
+                lambda: self.k() and self.alt(
+                    lambda: self.possessives() and self.cut() and self.opt(lambda: self.k() and self.lAr()),
+                    self.lAr) and self.cut() and self.k() and self.chain_ki()),
+            self.poss_or_su)
+
+    # ---- postlude
+    def append_u(self) -> bool:                 # a stem ending in d / g takes the U of its last vowel
+        if not self.test(lambda: self.alt(lambda: self.eq("d"), lambda: self.eq("g"))):
+            return False
+        for vowels, u in (("aı", "ı"), ("ei", "i"), ("ou", "u"), ("öü", "ü")):
+            if self.test(lambda: self.goto(_TR_V) and self.w[self.c - 1] in vowels):
+                return self.insert(u)
+        return False
+
+    def last_consonant(self) -> None:
+        repl = {"b": "p", "c": "ç", "d": "t", "ğ": "k"}.get(self.w[-1:])
+        if repl is not None:
+            self.w = self.w[:-1] + repl
+
+
+def turkish_stem(word: str) -> str:
+    """Snowball Turkish (Çilden's suffix-stripping algorithm): words of one syllable are left alone; the
+    nominal verb suffixes are stripped, then (unless a plural -lAr ended that step) the noun suffix chains,
+    then a d / g stem takes back its U vowel and a final b / c / d / ğ turns into p / ç / t / k (not for the
+    reserved words ad, soyad)."""
+    if sum(ch in _TR_V for ch in word) < 2:
+        return word
+    t = _TrStem(word)
+    v = t.save()
+    t.nominal_verb()
+    t.restore(v)
+    if not t.cont:
+        return t.w
+    v = t.save()
+    t.noun()
+    t.restore(v)
+    if t.w in ("ad", "soyad"):
+        return t.w
+    t.c = len(t.w)
+    t.append_u()
+    t.c = len(t.w)
+    t.last_consonant()
+    return t.w
+
+
+def turkish_lower(text: str) -> str:
+    """TurkishLowerCaseFilter: dotless I -> ı, dotted İ (or I + combining dot above) -> i, then lower case."""
+    return text.replace("İ", "i").replace("İ", "i").replace("I", "ı").lower()

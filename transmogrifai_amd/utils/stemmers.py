@@ -643,11 +643,11 @@ def czech_stem(word: str) -> str:
     return w
 
 
-from .snowball import dutch_stem, finnish_stem, hungarian_stem, romanian_stem, russian_stem  # noqa: E402
+from .snowball import dutch_stem, finnish_stem, hungarian_stem, romanian_stem, russian_stem, turkish_stem  # noqa: E402
 
 STEMMERS: Dict[str, Callable[[str], str]] = {
     "fr": french_light_stem, "de": german_analyze_stem, "es": spanish_light_stem, "it": italian_light_stem,
     "pt": portuguese_light_stem, "no": norwegian_light_stem, "sv": swedish_stem, "da": danish_stem,
     "ru": russian_stem, "nl": dutch_stem, "ro": romanian_stem, "hu": hungarian_stem, "fi": finnish_stem,
-    "ar": arabic_analyze_stem, "hi": hindi_analyze_stem, "bg": bulgarian_stem, "cs": czech_stem,
+    "ar": arabic_analyze_stem, "hi": hindi_analyze_stem, "bg": bulgarian_stem, "cs": czech_stem, "tr": turkish_stem,
 }
