@@ -56,7 +56,7 @@ _HOST_SIGS = {
     "tmog_tok_sizes": [P, P, P],
     "tmog_tok_copy": [P, P, P, P, P],
     "tmog_tok_free": [P],
-    "tmog_clean_ascii": [P, P, I64, P, P, P],
+    "tmog_clean_ascii_lens": [P, P, I64, P, P, P],
     "tmog_first_ids": [P, P, P, I64, P],
 }
 
@@ -135,7 +135,7 @@ _HIP_SIGS = {
 }
 
 
-_RESTYPES = {"tmog_tok_run": C.c_void_p, "tmog_tok_sizes": None, "tmog_tok_copy": None, "tmog_tok_free": None, "tmog_hip_grow_timing": None, "tmog_clean_ascii": None, "tmog_first_ids": I64,
+_RESTYPES = {"tmog_tok_run": C.c_void_p, "tmog_tok_sizes": None, "tmog_tok_copy": None, "tmog_tok_free": None, "tmog_hip_grow_timing": None, "tmog_clean_ascii_lens": None, "tmog_first_ids": I64,
              "tmog_tree_finalize_cpu": C.c_int64, "tmog_shist_new": C.c_void_p, "tmog_shist_free": None, "tmog_shist_update": None,
              "tmog_shist_flush": None, "tmog_shist_merge": None, "tmog_shist_bins": None,
              "tmog_shist_size": C.c_int64, "tmog_shist_sum": C.c_double,

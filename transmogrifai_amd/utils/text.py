@@ -316,15 +316,18 @@ def _clean_batch_impl(strings: Sequence[Optional[str]], clean: bool = True) -> C
     buf, offs = _encode_batch(strings)
     if clean:
         out = np.empty(max(int(offs[-1]), 1), np.uint8)
-        oo = np.empty(n + 1, np.int64)
+        lens = np.empty(max(n, 1), np.int64)
         fb = np.zeros(max(n, 1), np.uint8)
-        lib.tmog_clean_ascii(buf.ctypes.data, offs.ctypes.data, n, out.ctypes.data, oo.ctypes.data, fb.ctypes.data)
-        starts, ends = oo[:-1].copy(), oo[1:].copy()
-        char_len = ends - starts
+        # cleaned string i in place of its input bytes (never longer), in parallel
+        lib.tmog_clean_ascii_lens(buf.ctypes.data, offs.ctypes.data, n, out.ctypes.data, lens.ctypes.data,
+                                  fb.ctypes.data)
+        starts = offs[:-1].copy()
+        ends = starts + lens[:n]
+        char_len = lens[:n].copy()
         bad = np.flatnonzero(fb[:n])
         if bad.size:
             extra = [clean_string(strings[i] or "").encode("utf-8") for i in bad]
-            base = int(oo[-1])
+            base = int(offs[-1])
             lens = np.fromiter((len(e) for e in extra), dtype=np.int64, count=bad.size)
             starts[bad] = base + np.concatenate([[0], np.cumsum(lens)[:-1]])
             ends[bad] = starts[bad] + lens
