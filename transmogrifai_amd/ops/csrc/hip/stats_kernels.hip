@@ -64,17 +64,34 @@ __global__ void col_fold_kernel(const double* __restrict__ part, int chunks, int
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= d) return;
   double na = 0, ma = 0, m2 = 0, nz = 0, mn = DBL_MAX, mx = -DBL_MAX;
-  for (int k = 0; k < chunks; ++k) {
-    const double* p = part + (int64_t)k * 6 * d;
-    const double nb = p[5 * d + c];
-    if (nb <= 0) continue;
-    const double mb = p[c], n = na + nb, delta = mb - ma;
-    ma += delta * (nb / n);
-    m2 += p[d + c] + delta * delta * (na * nb / n);
-    na = n;
-    nz += p[4 * d + c];
-    mn = fmin(mn, p[2 * d + c]);
-    mx = fmax(mx, p[3 * d + c]);
+  // the merge is a serial chain in chunk order (the CPU twin's order); the partials of the next 8 chunks are
+  // loaded together first, so the chain waits on one load round trip per 8 chunks instead of one per chunk
+  constexpr int U = 8;
+  for (int k0 = 0; k0 < chunks; k0 += U) {
+    double pn[U], pm[U], pq[U], pz[U], pl[U], ph[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = min(k0 + u, chunks - 1);
+      const double* p = part + (int64_t)k * 6 * d;
+      pn[u] = k0 + u < chunks ? p[5 * d + c] : 0.0;
+      pm[u] = p[c];
+      pq[u] = p[d + c];
+      pl[u] = p[2 * d + c];
+      ph[u] = p[3 * d + c];
+      pz[u] = p[4 * d + c];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const double nb = pn[u];
+      if (nb <= 0) continue;
+      const double n = na + nb, delta = pm[u] - ma;
+      ma += delta * (nb / n);
+      m2 += pq[u] + delta * delta * (na * nb / n);
+      na = n;
+      nz += pz[u];
+      mn = fmin(mn, pl[u]);
+      mx = fmax(mx, ph[u]);
+    }
   }
   out[c] = ma * na; out[d + c] = m2; out[2 * d + c] = mn; out[3 * d + c] = mx; out[4 * d + c] = nz;
   out[5 * d + c] = ma;
@@ -326,35 +343,65 @@ __global__ void __launch_bounds__(256) col_bf16_exact_kernel(const float* __rest
 // bf16_pack_kernel -- B[r][j] (bf16, row stride ldb) from the fp32 rows of X per output column j:
 //   mode 0 zero, 1 one, 2 X[r][src] as is, 3 / 4 / 5 the high / middle / low bf16 part of (X[r][src] - mu) * sc
 //   (the three parts sum to the fp32 value exactly), 6 (y[r] == src) -- the operand images of gram_bf16_kernel
-// and of the linear learners' bf16 design copy (ops/stats.py, ops/linear.py). Thread = (row, 8 output columns):
-// one 16-byte store.
+// and of the linear learners' bf16 design copy (ops/stats.py, ops/linear.py).
+// Thread = 8 consecutive output columns (one 16-byte store per row); a wave covers 64 column groups of a row and
+// the block's 4 waves walk the rows of its row chunk, so the column descriptors (mode, source, shift, scale) are
+// loaded once into registers per thread instead of once per element. Eight sources that are consecutive X columns
+// (the usual case: design columns in order) are read as two 16-byte loads instead of eight 4-byte gathers.
 __global__ void __launch_bounds__(256) bf16_pack_kernel(const float* __restrict__ X, int64_t n, int64_t ld,
                                                         const int32_t* __restrict__ y, const int32_t* __restrict__ src,
                                                         const int32_t* __restrict__ mode, const float* __restrict__ mu,
                                                         const float* __restrict__ sc, __bf16* __restrict__ B,
-                                                        int64_t ldb) {
-  const int64_t groups = ldb / 8;
-  const int64_t total = n * groups;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / groups;
-    const int j0 = (int)(e - r * groups) * 8;
+                                                        int64_t ldb, int64_t rows_per_blk) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t g = (int64_t)blockIdx.y * 64 + lane;
+  if (g >= ldb / 8) return;                       // whole lanes idle: no barrier below
+  const int j0 = (int)g * 8;
+  int m[8], s[8];
+  float sh[8], sf[8];
+  bool contig = true, need_y = false;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    m[u] = mode[j0 + u];
+    s[u] = src[j0 + u];
+    sh[u] = mu[j0 + u];
+    sf[u] = sc[j0 + u];
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    contig &= m[u] >= 2 && m[u] <= 5 && s[u] == s[0] + u;
+    need_y |= m[u] == 6;
+  }
+  contig &= (s[0] & 3) == 0 && (ld & 3) == 0 && ((uintptr_t)X & 15) == 0;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk, r1 = min(n, r0 + rows_per_blk);
+  for (int64_t r = r0 + wave; r < r1; r += 4) {
+    const float* xr = X + r * ld;
+    float xv[8];
+    if (contig) {
+      const float4 a = *reinterpret_cast<const float4*>(xr + s[0]);
+      const float4 b = *reinterpret_cast<const float4*>(xr + s[0] + 4);
+      xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
+      xv[4] = b.x; xv[5] = b.y; xv[6] = b.z; xv[7] = b.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xv[u] = (m[u] >= 2 && m[u] <= 5) ? xr[s[u]] : 0.f;
+    }
+    const int yr = need_y ? y[r] : 0;
     gbf16x8 out;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int j = j0 + u;
-      const int m = mode[j];
       float v = 0.f;
-      if (m == 1) {
+      if (m[u] == 1) {
         v = 1.f;
-      } else if (m == 2) {
-        v = X[r * ld + src[j]];
-      } else if (m >= 3 && m <= 5) {
-        const float c = (X[r * ld + src[j]] - mu[j]) * sc[j];
+      } else if (m[u] == 2) {
+        v = xv[u];
+      } else if (m[u] >= 3 && m[u] <= 5) {
+        const float c = (xv[u] - sh[u]) * sf[u];
         const float h = (float)(__bf16)c;
         const float mid = (float)(__bf16)(c - h);
-        v = m == 3 ? h : (m == 4 ? mid : c - h - mid);
-      } else if (m == 6) {
-        v = y[r] == src[j] ? 1.f : 0.f;
+        v = m[u] == 3 ? h : (m[u] == 4 ? mid : c - h - mid);
+      } else if (m[u] == 6) {
+        v = yr == s[u] ? 1.f : 0.f;
       }
       out[u] = (__bf16)v;
     }
@@ -779,10 +826,13 @@ int tmog_hip_bf16_pack(const float* X, int64_t n, int64_t ld, const int32_t* y, 
                        const float* mu, const float* sc, void* B, int64_t ldb, hipStream_t stream) {
   if (n <= 0) return 0;
   if (ldb <= 0 || ldb % 8 || (uintptr_t)B % 16) return -2;
-  const int64_t total = n * (ldb / 8);
-  const unsigned nblk = (unsigned)min((total + 255) / 256, (int64_t)16384);
-  hipLaunchKernelGGL(bf16_pack_kernel, dim3(nblk), dim3(256), 0, stream, X, n, ld, y, src, mode, mu, sc, (__bf16*)B,
-                     ldb);
+  const int64_t gy = (ldb / 8 + 63) / 64;         // column tiles of 64 groups (512 columns)
+  if (gy > 65535) return -2;
+  // ~4096 workgroups in all, at least 16 rows each
+  const int64_t gx = max((int64_t)1, min((n + 15) / 16, (int64_t)4096 / gy));
+  const int64_t rpb = (n + gx - 1) / gx;
+  hipLaunchKernelGGL(bf16_pack_kernel, dim3((unsigned)((n + rpb - 1) / rpb), (unsigned)gy), dim3(256), 0, stream, X, n,
+                     ld, y, src, mode, mu, sc, (__bf16*)B, ldb, rpb);
   return (int)hipGetLastError();
 }
 
