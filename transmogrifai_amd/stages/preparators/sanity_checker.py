@@ -21,7 +21,7 @@ import torch
 from ...data.columns import VectorColumn
 from ...data.vector_metadata import OpVectorMetadata
 from ...features import types as T
-from ...ops import stats as ST
+from ...ops import stats as ST, vector as V
 from ..base import BinaryEstimator, BinaryTransformer, register_stage
 from ...tuning.splitters import row_uniform
 
@@ -179,20 +179,25 @@ class SanityChecker(BinaryEstimator):
         frac = self.fraction(n_all)
         if frac <= 0.0 or n_all == 0:
             raise ValueError("Sample size cannot be zero")
+        keep = None
         if frac < 1.0:
             rid = ds.row_ids.to(dev) if ds is not None else torch.arange(n_all, device=dev)
             keep = torch.nonzero(row_uniform(rid, int(p["sample_seed"]), 9) < frac).reshape(-1)
-            X, y = vec_col.take_rows(keep), y.index_select(0, keep.to(y.device))
-        else:
-            X = vec_col.values
         meta: OpVectorMetadata = vec_col.metadata
-        d = X.shape[1]
+        d = vec_col.width
         if d == 0:
             raise ValueError("Feature vector passed in is empty, check your vectorizers")
         if meta is None or meta.size != d:
             raise ValueError(f"Number of columns in vector metadata ({None if meta is None else meta.size}) did not "
                              f"match number of columns in data ({d}), check your vectorizers")
-        Xy = torch.cat([X, y.to(X.dtype)[:, None]], 1).contiguous()
+        # [X | y] gathered from the vector's blocks and the label in one pass (no separate materialisation of X
+        # followed by a concatenating copy); X is its leading column view
+        y_full = y
+        Xy = V.gather_rows_cols(vec_col.blocks + [(y_full.to(vec_col.dtype).to(dev)[:, None].contiguous(), None)],
+                                None if keep is None else keep.to(dev), len(vec_col)).contiguous()
+        if keep is not None:
+            y = y_full.index_select(0, keep.to(y_full.device))
+        X = Xy[:, :d]
         cs = ST.col_stats(Xy)
         count = cs["count"]
         cols = meta.columns
@@ -233,7 +238,7 @@ class SanityChecker(BinaryEstimator):
         # categorical tests
         cat_stats = []
         if want_cat:
-            cat_stats = self._categorical_tests(X, y, cols, pre_cat)
+            cat_stats = self._categorical_tests(X if pre_cat is not None else X.contiguous(), y, cols, pre_cat)
         label_dist = None
         if labels_u.numel() <= 100:
             lu = labels_u
