@@ -232,20 +232,21 @@ def test_aupr_counts_kernel_matches_torch():
     leading empty bins, a set without positives and an empty set."""
     from transmogrifai_amd.evaluators.metrics import _aupr_from_counts_torch, binned_aupr_from_counts
     g = torch.Generator().manual_seed(7)
-    K, bins = 6, 1 << 16
-    h = torch.randint(0, 4, (K, 2, bins), generator=g, dtype=torch.int32)
-    h[:, :, : bins // 3] = 0                                   # leading empty bins
-    h[1, :, ::5] = 0
-    h[2, 1] = 0                                                # no positives
-    h[3] = 0                                                   # empty
-    h[4, :, bins - 7:] = 0                                     # trailing empty bins
-    h[5] = 0
-    h[5, 0, 100] = 3
-    h[5, 1, 101] = 2
-    want = _aupr_from_counts_torch(h.double()).numpy()
-    got = binned_aupr_from_counts(h.cuda()).cpu().numpy()
-    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-14)
-    assert got[2] == 0.0 and got[3] == 0.0
+    for bins in (1 << 16, 4099, 1000):               # 16-byte segment loads, and the scalar path
+        K = 6
+        h = torch.randint(0, 4, (K, 2, bins), generator=g, dtype=torch.int32)
+        h[:, :, : bins // 3] = 0                               # leading empty bins
+        h[1, :, ::5] = 0
+        h[2, 1] = 0                                            # no positives
+        h[3] = 0                                               # empty
+        h[4, :, bins - 7:] = 0                                 # trailing empty bins
+        h[5] = 0
+        h[5, 0, 100] = 3
+        h[5, 1, 101] = 2
+        want = _aupr_from_counts_torch(h.double()).numpy()
+        got = binned_aupr_from_counts(h.cuda()).cpu().numpy()
+        np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-14)
+        assert got[2] == 0.0 and got[3] == 0.0
     assert _native_loaded()
 
 

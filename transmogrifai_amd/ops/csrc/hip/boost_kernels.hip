@@ -286,26 +286,16 @@ __global__ void __launch_bounds__(256) row_uniform_kernel(const int64_t* __restr
 
 // AuPR of K score sets from their (label, score-bin) count tables [K][2][bins] (bins in descending score
 // order; the boosting-round early-stopping metric, evaluators/metrics.py binned_aupr_from_counts): one
-// 1024-thread workgroup per set. Pass 1 reduces the positive total P; pass 2 walks the bins in coalesced
-// 4096-bin chunks (4 consecutive bins per lane), a wave64 shuffle scan + 16 wave totals in LDS give every
-// bin its cumulative (tp, fp), and each bin's trapezoid term is evaluated independently with the torch
-// path's arithmetic (precision tp / cnt, recall tp / P, ((r - r') * (p + p')) * 0.5). The previous bin's
-// precision comes from the cumulative counts before the bin; with none before it (leading empty bins)
-// the torch path uses the first non-empty bin's precision, which is this bin's own whenever the term is
-// non-zero. Replaces a 256-thread version whose per-thread 256-bin segments were uncoalesced (181 us per
-// call at 6 x 65536 bins).
+// 1024-thread workgroup per set, thread t owning the consecutive bins [t seg, (t + 1) seg). The thread sums its
+// segment (16 bins at a time, their loads issued together, 16-byte loads when aligned), one block scan of the segment totals
+// gives every segment its cumulative (tp, fp) before it and the positive total P, and the thread then walks its
+// bins again (L2 hits) evaluating each bin's trapezoid term with the torch path's arithmetic (precision
+// tp / cnt, recall tp / P, ((r - r') * (p + p')) * 0.5). The previous bin's precision comes from the cumulative
+// counts before the bin; with none before it (leading empty bins) the torch path uses the first non-empty bin's
+// precision, which is this bin's own whenever the term is non-zero. Replaces a version that walked the bins in
+// 16 dependent 4096-bin chunks (two barriers and a memory round trip each: ~107 us a call at 65536 bins, one
+// call per boosting round on the round's serial chain).
 constexpr int AUPR_NT = 1024;
-
-// wave64 inclusive prefix sum on DPP (row_shr 1 / 2 / 4 / 8, row_bcast 15 / 31; lanes without a source add 0)
-__device__ __forceinline__ int wave_incl_scan(int v) {
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
-  return v;
-}
 
 __global__ void __launch_bounds__(AUPR_NT) aupr_counts_kernel(const int32_t* __restrict__ counts, int bins,
                                                               double* __restrict__ out) {
@@ -313,56 +303,73 @@ __global__ void __launch_bounds__(AUPR_NT) aupr_counts_kernel(const int32_t* __r
   constexpr int NW = AUPR_NT / 64;
   const int32_t* neg = counts + (int64_t)k * 2 * bins;
   const int32_t* pos = neg + bins;
-  __shared__ long long s_red[NW];
-  __shared__ int s_wp[NW], s_wn[NW];
+  __shared__ long long s_p[NW], s_n[NW];
   __shared__ double s_acc[NW];
-  // pass 1: P
-  long long sp = 0;
-  for (int b = t; b < bins; b += AUPR_NT) sp += pos[b];
-  for (int o = 32; o > 0; o >>= 1) sp += __shfl_xor(sp, o, 64);
-  if (lane == 0) s_red[wv] = sp;
+  const int seg = (bins + AUPR_NT - 1) / AUPR_NT;
+  const int b0 = min(bins, t * seg), b1 = min(bins, b0 + seg);
+  const bool vec = (bins & 3) == 0 && (seg & 3) == 0 && ((uintptr_t)neg & 15) == 0;
+  // 16 bins of the segment at a time, all their loads issued together (bins past the segment read as 0: an
+  // empty bin changes neither the cumulative counts nor the area)
+  auto load16 = [&](int c, int (&pv)[16], int (&nv)[16]) {
+    if (vec && c + 16 <= b1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int4 p4 = *reinterpret_cast<const int4*>(pos + c + 4 * q);
+        const int4 n4 = *reinterpret_cast<const int4*>(neg + c + 4 * q);
+        pv[4 * q] = p4.x; pv[4 * q + 1] = p4.y; pv[4 * q + 2] = p4.z; pv[4 * q + 3] = p4.w;
+        nv[4 * q] = n4.x; nv[4 * q + 1] = n4.y; nv[4 * q + 2] = n4.z; nv[4 * q + 3] = n4.w;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int b = min(c + u, bins - 1);
+        pv[u] = c + u < b1 ? pos[b] : 0;
+        nv[u] = c + u < b1 ? neg[b] : 0;
+      }
+    }
+  };
+  long long lp = 0, ln = 0;
+  for (int c = b0; c < b1; c += 16) {
+    int pv[16], nv[16];
+    load16(c, pv, nv);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      lp += pv[u];
+      ln += nv[u];
+    }
+  }
+  long long ip = lp, in = ln;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long a = __shfl_up(ip, o, 64), c = __shfl_up(in, o, 64);
+    if (lane >= o) {
+      ip += a;
+      in += c;
+    }
+  }
+  if (lane == 63) {
+    s_p[wv] = ip;
+    s_n[wv] = in;
+  }
   __syncthreads();
-  long long Pi = 0;
-  for (int w = 0; w < NW; ++w) Pi += s_red[w];
+  long long ep = ip - lp, en = in - ln, Pi = 0;
+  for (int w = 0; w < NW; ++w) {
+    if (w < wv) {
+      ep += s_p[w];
+      en += s_n[w];
+    }
+    Pi += s_p[w];
+  }
   const double Pt = (double)Pi;
   const double Pm = Pt > 1.0 ? Pt : 1.0;
-  // pass 2: chunked scan + independent per-bin terms
-  int carry_p = 0, carry_n = 0;
-  double acc = 0.0;
-  for (int c0 = 0; c0 < bins; c0 += 4 * AUPR_NT) {
-    const int b0 = c0 + 4 * t;
-    int pv[4], nv[4];
-    int lp = 0, ln = 0;
+  double tp = (double)ep, fp = (double)en, acc = 0.0;
+  for (int c = b0; c < b1; c += 16) {
+    int pv[16], nv[16];
+    load16(c, pv, nv);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int b = b0 + i;
-      pv[i] = b < bins ? pos[b] : 0;
-      nv[i] = b < bins ? neg[b] : 0;
-      lp += pv[i];
-      ln += nv[i];
-    }
-    const int ip = wave_incl_scan(lp), in = wave_incl_scan(ln);
-    __syncthreads();                                   // previous chunk's readers of s_wp / s_wn are done
-    if (lane == 63) {
-      s_wp[wv] = ip;
-      s_wn[wv] = in;
-    }
-    __syncthreads();
-    int ep = carry_p + ip - lp, en = carry_n + in - ln;
-    for (int w = 0; w < NW; ++w) {
-      const int a = s_wp[w], bn = s_wn[w];
-      if (w < wv) {
-        ep += a;
-        en += bn;
-      }
-      carry_p += a;
-      carry_n += bn;
-    }
-    double tp = (double)ep, fp = (double)en;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const double tp1 = tp + (double)pv[i], fp1 = fp + (double)nv[i];
-      if (pv[i] > 0) {
+    for (int u = 0; u < 16; ++u) {
+      const double tp1 = tp + (double)pv[u], fp1 = fp + (double)nv[u];
+      if (pv[u] > 0) {
         const double pr = tp1 / fmax(tp1 + fp1, 1.0);
         const double prev_prec = (tp + fp > 0.0) ? tp / fmax(tp + fp, 1.0) : pr;
         acc += ((tp1 / Pm - tp / Pm) * (pr + prev_prec)) * 0.5;
