@@ -1132,11 +1132,18 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
     const bool lds_fit = plan_lds_ok && lds_attr && cp.cap_nl > 0 &&
                          per_node * (size_t)cp.cap_nl + 64 <= (size_t)148 * 1024;
     P.lds_cap = lds_fit ? cp.cap_nl : 0;
+    // threads of the two single-workgroup kernels (plan, finalisation); TMOG_PLAN_THREADS = 256 / 512 / 1024: a
+    // smaller workgroup finds a CU sooner while the other boosting parts' histogram waves occupy the chip
+    static const int plan_nt = [] {
+      const char* e = std::getenv("TMOG_PLAN_THREADS");
+      const int v = e ? std::atoi(e) : 1024;
+      return (v == 256 || v == 512) ? v : 1024;
+    }();
     const size_t plan_lds = lds_fit ? per_node * (size_t)cp.cap_nl + 64 : 0;
     // plan D + 1 turns the last decisions into leaves
     for (int d = 0; d <= cp.D + 1; ++d) {
       P.d = d;
-      hipLaunchKernelGGL(level_plan_kernel, dim3(1), dim3(1024), plan_lds, st, P);
+      hipLaunchKernelGGL(level_plan_kernel, dim3(1), dim3(plan_nt), plan_lds, st, P);
       kchk((int)hipGetLastError(), "level_plan");
       const int64_t nprev = d > 0 ? cp.nmax[d - 1] : 0;
       const int64_t lbound = (total / std::max<int64_t>(a.chunk_rows, 1) + nprev + 1) +
@@ -1189,7 +1196,7 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
     Fa.gid_tree = io->gid_tree;
     Fa.prune = 0;
     for (int j = 0; j < T; ++j) Fa.prune |= io->job_gamma[j] > 0.0 ? 1 : 0;
-    hipLaunchKernelGGL(tree_finalize_kernel, dim3(1), dim3(1024), 0, st, Fa);
+    hipLaunchKernelGGL(tree_finalize_kernel, dim3(1), dim3(plan_nt), 0, st, Fa);
     kchk((int)hipGetLastError(), "tree_finalize");
     return 0;
   } catch (const std::exception& e) {
