@@ -230,3 +230,22 @@ def test_turkish_snowball_stemmer_and_analyzer():
     assert LG.analyze("Türkiye'nin en büyük şehri İSTANBUL’da kitapları ve okullarında okuyoruz", "Turkish") == [
         "türki", "büyük", "şehri", "istanbul", "kitap", "okul", "okuyor"]
     assert LG.best_language("bu kitap çok güzel ve ben onu okudum ama daha bitirmedim", 0.5) == "tr"
+
+
+def test_indonesian_and_latvian_light_stemmers():
+    """IndonesianAnalyzer (Tala's stemmer with derivational stemming: particles, possessives, first- and
+    second-order prefixes, conditioned suffixes) and LatvianAnalyzer (Kreslins' light stemmer with consonant
+    unpalatalisation); the published algorithms, no reference fixture (parity unpinned)."""
+    from transmogrifai_amd.utils.stemmers import indonesian_stem, latvian_stem
+    ids = {"membaca": "baca", "pembacaan": "baca", "dimakan": "makan", "bukunya": "buku", "bacalah": "baca",
+           "menyapu": "sapu", "bermain": "main", "pelajar": "ajar", "keadilan": "adil", "mempermainkan": "main",
+           "perpustakaan": "pustaka"}
+    assert {w: indonesian_stem(w) for w in ids} == ids
+    lvs = {"grāmatas": "grāmat", "upes": "upe", "brāļiem": "brāl", "lāčiem": "lāc", "kokiem": "kok", "zemes": "zem"}
+    assert {w: latvian_stem(w) for w in lvs} == lvs
+    assert LG.analyze("Para pelajar sedang membaca buku-buku pelajaran di perpustakaan", "Indonesian") == [
+        "ajar", "baca", "buku", "buku", "lajar", "pustaka"]
+    assert LG.analyze("Bērni lasa grāmatas un spēlējas ar kokiem pie upes", "Latvian") == [
+        "bērn", "las", "grāmat", "spēlēj", "kok", "upe"]
+    assert LG.best_language("mereka tidak akan pergi ke pasar karena hujan dan ini adalah hari yang dingin", 0.5) == "id"
+    assert LG.best_language("viņš ir mājās un lasa grāmatu, bet tā nav viņa grāmata", 0.5) == "lv"

@@ -48,6 +48,8 @@ _PROFILE = {
     "tr": "ve bir bu da de için ile çok ama gibi daha olarak olan en ne var",
     "ro": "și în de la cu nu o un care este pe din să se ca mai",
     "cs": "a se na je že to v z do o s k ve jsou ale jak pro po by jako jsem už jeho které který není také",
+    "id": "yang dan di ini itu dengan untuk tidak dari dalam akan pada juga ke karena tersebut bisa ada mereka adalah",
+    "lv": "un ir ar uz no par kas ka bet lai arī vai pie pēc tas to viņš bija tā nav",
 }
 PROFILES: Dict[str, FrozenSet[str]] = {k: frozenset(v.split()) for k, v in _PROFILE.items()}
 
@@ -176,6 +178,41 @@ onların onu onun otuz oysa öyle pek rağmen sadece sanki sekiz seksen sen send
 şeyden şeyi şeyler şöyle şu şuna şunda şundan şunları şunu tarafından trilyon tüm üç üzere var vardı ve veya ya
 yani yapacak yapılan yapılması yapıyor yapmak yaptı yaptığı yaptığını yaptıkları yedi yerine yetmiş yine yirmi
 yoksa yüz zaten""".split())
+# IndonesianAnalyzer's stop set (F. Tala's list; its common entries)
+STOPWORDS["id"] = PROFILES["id"] | frozenset("""
+ada adalah adanya adapun agak agaknya agar akan akankah akhirnya aku akulah amat amatlah anda andalah antar antara
+antaranya apa apaan apabila apakah apalagi apatah atau ataukah ataupun bagai bagaikan bagaimana bagaimanakah
+bagaimanapun bagi bahkan bahwa bahwasanya banyak beberapa begini beginian beginikah beginilah begitu begitukah
+begitulah begitupun belum belumlah berapa berapakah berapalah berapapun bermacam bersama betulkah biasa biasanya
+bila bilakah bisa bisakah boleh bolehkah bolehlah buat bukan bukankah bukanlah bukannya cuma dahulu dalam dan dapat
+dari daripada dekat demi demikian demikianlah dengan depan di dia dialah diantara diantaranya dikarenakan dini diri
+dirinya disini disinilah dong dulu enggak enggaknya entah entahlah hal hampir hanya hanyalah harus haruslah
+harusnya hendak hendaklah hendaknya hingga ia ialah ibarat ingin inginkah inginkan ini inikah inilah itu itukah
+itulah jangan jangankan janganlah jika jikalau juga justru kala kalau kalaulah kalaupun kalian kami kamilah kamu
+kamulah kan kapan kapankah kapanpun karena karenanya ke kecil kemudian kenapa kepada kepadanya ketika khususnya kini
+kinilah kiranya kita kitalah kok lagi lagian lah lain lainnya lalu lama lamanya lebih macam maka makanya makin
+malah malahan mampu mampukah mana manakala manalagi masih masihkah masing mau maupun melainkan melalui memang
+mengapa mereka merekalah merupakan meski meskipun mungkin mungkinkah nah namun nanti nantinya nyaris oleh olehnya
+pada padahal padanya paling pantas para pasti pastilah per percuma pernah pula pun rupanya saat saatnya saja
+sajalah saling sama sambil sampai sana sangat sangatlah saya sayalah se sebab sebabnya sebagai sebagaimana
+sebagainya sebaliknya sebanyak sebegini sebegitu sebelum sebelumnya sebenarnya seberapa sebetulnya sebisanya
+sebuah sedang sedangkan sedemikian sedikit sedikitnya segala segalanya segera seharusnya sehingga sejak sejenak
+sekali sekalian sekaligus sekalipun sekarang seketika sekiranya sekitar sekitarnya sela selagi selain selaku
+selalu selama selamanya seluruh seluruhnya semacam semakin semasih semaunya sementara sempat semua semuanya semula
+sendiri sendirinya seolah seorang sepanjang sepantasnya seperti sepertinya sering seringnya serta serupa sesaat
+sesama sesegera sesuatu sesuatunya sesudah sesudahnya setelah seterusnya setiap setidaknya sewaktu siapa siapakah
+siapapun sini sinilah suatu sudah sudahkah sudahlah supaya tadi tadinya tak tanpa tapi telah tentang tentu
+tentulah tentunya terdiri terhadap terhadapnya terlalu terlebih tersebut tersebutlah tertentu tetapi tiap tidak
+tidakkah tidaklah toh waduh wah wahai walau walaupun wong yaitu yakni yang""".split())
+STOPWORDS["lv"] = PROFILES["lv"] | frozenset("""
+aiz ap ar apakš ārpus augšpus bez caur dēļ gar iekš iz kopš labad lejpus līdz no otrpus pa par pār pēc pie pirms
+pret priekš starp šaipus uz viņpus virs virspus zem apakšpus un bet jo ja ka lai tomēr tikko turpretī arī kaut gan
+tādēļ tā ne tikvien vien kā ir te vai kamēr diezin droši diemžēl nebūt ik it taču nu pat tiklab iekšpus nedz tik
+nevis turpretim jeb iekam iekām iekāms kolīdz līdzko tiklīdz jebšu tālab tāpēc nekā itin jā jau jel nē nezin tad
+tikai vis tak iekams būt biju biji bija bijām bijāt esmu esi esam esat būšu būsi būs būsim būsiet tikt tiku tiki
+tika tikām tikāt tieku tiec tiek tiekam tiekat tikšu tiks tiksim tiksiet tapt tapi tapāt topat tapšu tapsi taps
+tapsim tapsiet kļūt kļuvu kļuvi kļuva kļuvām kļuvāt kļūstu kļūsti kļūst kļūstam kļūstat kļūšu kļūsi kļūs kļūsim
+kļūsiet varēt varēju varējām varēšu varēsim var varēji varējāt varēsi varēsiet varat varēja varēs""".split())
 STOPWORDS["fa"] = frozenset("""
 انان نداشته سراسر خياه ايشان وي تاكنون بيشتري دوم پس ناشي وگو يا داشتند سپس هنگام هرگز پنج نشان امسال ديگر گروهي
 شدند چطور ده و دو نخستين ولي چرا چه وسط ه كدام قابل يك رفت هفت همچنين در هزار بله بلي شايد اما شناسي گرفته دهد
@@ -291,7 +328,7 @@ LANGUAGE_NAMES = {"English": "en", "French": "fr", "German": "de", "Spanish": "e
                   "Hungarian": "hu", "Japanese": "ja", "Korean": "ko", "SimplifiedChinese": "zh-cn",
                   "TraditionalChinese": "zh-tw", "Chinese": "zh", "Arabic": "ar",
                   "Hindi": "hi", "Bulgarian": "bg", "Czech": "cs",
-                  "Persian": "fa"}
+                  "Persian": "fa", "Indonesian": "id", "Latvian": "lv"}
 # Lucene CJKAnalyzer languages (LuceneTextAnalyzer.scala: Korean, SimplifiedChinese, TraditionalChinese)
 CJK_BIGRAM = frozenset({"zh", "zh-cn", "zh-tw", "ko"})
 

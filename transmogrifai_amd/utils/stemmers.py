@@ -5,6 +5,8 @@ Lucene 7.3 ``*Analyzer`` chains):
   Italian / Portuguese ``*LightStemFilter`` and Norwegian (bokmål) ``NorwegianLightStemFilter`` -- J. Savoy's light
   stemmers, which those analyzers use;
 * Swedish and Danish: the Snowball stemmers of ``SwedishAnalyzer`` / ``DanishAnalyzer``.
+* Indonesian ``IndonesianStemFilter`` (F. Tala's algorithm) and Latvian ``LatvianStemFilter`` (K. Kreslins' light
+  stemmer);
 
 Implemented from the published algorithms (Savoy, "Light stemming approaches for the French, Portuguese, German
 and Hungarian languages", SAC 2006; snowballstem.org), not from Lucene's sources; the French one is pinned by the
@@ -643,6 +645,142 @@ def czech_stem(word: str) -> str:
     return w
 
 
+
+# ------------------------------------------------------------------------------------------- Indonesian
+# IndonesianAnalyzer: lower case, stop words, IndonesianStemFilter (Tala's algorithm, derivational stemming on):
+# particles (-kah -lah -pun) and possessive pronouns (-ku -mu -nya) first, then first-order prefixes
+# (meng- / peng- families, di-, ter-, ke-), suffixes (-kan -an -i, conditioned on the prefixes removed) and
+# second-order prefixes (ber-, per-, pe-); every step needs a word of more than two syllables (vowels).
+_ID_V = frozenset("aeiou")
+_ID_KE, _ID_PENG, _ID_DI, _ID_MENG, _ID_TER, _ID_BER, _ID_PE = 1, 2, 4, 8, 16, 32, 64
+
+
+def indonesian_stem(word: str) -> str:
+    w = word
+    syl = sum(c in _ID_V for c in w)
+    flags = 0
+    if syl > 2 and w.endswith(("kah", "lah", "pun")):
+        w, syl = w[:-3], syl - 1
+    if syl > 2:
+        if w.endswith(("ku", "mu")):
+            w, syl = w[:-2], syl - 1
+        elif w.endswith("nya"):
+            w, syl = w[:-3], syl - 1
+
+    def first_order(w, syl, flags):
+        n = len(w)
+        vowel_at = lambda i: n > i and w[i] in _ID_V      # noqa: E731
+        if w.startswith("meng"):
+            return w[4:], syl - 1, flags | _ID_MENG
+        if w.startswith("meny") and vowel_at(4):
+            return "s" + w[4:], syl - 1, flags | _ID_MENG
+        if w.startswith(("men", "mem")):
+            return w[3:], syl - 1, flags | _ID_MENG
+        if w.startswith("me"):
+            return w[2:], syl - 1, flags | _ID_MENG
+        if w.startswith("peng"):
+            return w[4:], syl - 1, flags | _ID_PENG
+        if w.startswith("peny") and vowel_at(4):
+            return "s" + w[4:], syl - 1, flags | _ID_PENG
+        if w.startswith("peny"):
+            return w[4:], syl - 1, flags | _ID_PENG
+        if w.startswith("pen") and vowel_at(3):
+            return "t" + w[3:], syl - 1, flags | _ID_PENG
+        if w.startswith(("pen", "pem")):
+            return w[3:], syl - 1, flags | _ID_PENG
+        if w.startswith("di"):
+            return w[2:], syl - 1, flags | _ID_DI
+        if w.startswith("ter"):
+            return w[3:], syl - 1, flags | _ID_TER
+        if w.startswith("ke"):
+            return w[2:], syl - 1, flags | _ID_KE
+        return w, syl, flags
+
+    def second_order(w, syl, flags):
+        if w.startswith("ber"):
+            return w[3:], syl - 1, flags | _ID_BER
+        if w == "belajar":
+            return w[3:], syl - 1, flags | _ID_BER
+        if w.startswith("be") and len(w) > 4 and w[2] not in _ID_V and w[3] == "e" and w[4] == "r":
+            return w[2:], syl - 1, flags | _ID_BER
+        if w.startswith("per"):
+            return w[3:], syl - 1, flags
+        if w == "pelajar":
+            return w[3:], syl - 1, flags
+        if w.startswith("pe"):
+            return w[2:], syl - 1, flags | _ID_PE
+        return w, syl, flags
+
+    def suffix(w, syl, flags):
+        if w.endswith("kan") and not flags & (_ID_KE | _ID_PENG | _ID_PE):
+            return w[:-3], syl - 1, flags
+        if w.endswith("an") and not flags & (_ID_DI | _ID_MENG | _ID_TER):
+            return w[:-2], syl - 1, flags
+        if w.endswith("i") and not w.endswith("si") and not flags & (_ID_BER | _ID_KE | _ID_PENG):
+            return w[:-1], syl - 1, flags
+        return w, syl, flags
+
+    before = w
+    if syl > 2:
+        w, syl, flags = first_order(w, syl, flags)
+    if w != before:                              # a first-order prefix came off
+        mid = w
+        if syl > 2:
+            w, syl, flags = suffix(w, syl, flags)
+        if w != mid and syl > 2:
+            w, syl, flags = second_order(w, syl, flags)
+    else:
+        if syl > 2:
+            w, syl, flags = second_order(w, syl, flags)
+        if syl > 2:
+            w, syl, flags = suffix(w, syl, flags)
+    return w
+
+
+# ---------------------------------------------------------------------------------------------- Latvian
+# LatvianAnalyzer: lower case, stop words, LatvianStemFilter (Kreslins' light stemmer): the first listed ending
+# whose vowel-count condition holds and that leaves at least three letters is removed; endings marked
+# palatalising undo the consonant alternation the ending caused (kš -> kst, ņņ -> nn after genitive -u, labial
+# + j -> labial, šņ / žņ / šļ / žļ / ļņ / ļļ, č / ļ / ņ -> c / l / n).
+_LV_V = frozenset("aeiouāēīōū")
+_LV_AFFIXES = (("ajiem", 3, False), ("ajai", 3, False), ("ajam", 2, False), ("ajām", 2, False), ("ajos", 2, False),
+               ("ajās", 2, False), ("iem", 2, True), ("ajā", 2, False), ("ais", 2, False), ("ai", 2, False),
+               ("ei", 2, False), ("ām", 1, False), ("am", 1, False), ("ēm", 1, False), ("īm", 1, False),
+               ("im", 1, False), ("um", 1, False), ("us", 1, True), ("as", 1, False), ("ās", 1, False),
+               ("es", 1, False), ("os", 1, True), ("ij", 1, False), ("īs", 1, False), ("ēs", 1, False),
+               ("is", 1, False), ("ie", 1, False), ("u", 1, True), ("a", 1, True), ("i", 1, True), ("e", 1, False),
+               ("ā", 1, False), ("ē", 1, False), ("ī", 1, False), ("ū", 1, False), ("o", 1, False),
+               ("s", 0, False), ("š", 0, False))
+_LV_PAIRS = {"šņ": "sn", "žņ": "zn", "šļ": "sl", "žļ": "zl", "ļņ": "ln", "ļļ": "ll"}
+
+
+def _lv_unpalatalize(w: str, removed: str) -> str:
+    if removed.startswith("u"):                  # genitive plural -u: kš -> kst, ņņ -> nn only here
+        if w.endswith("kš"):
+            return w[:-2] + "kst"
+        if w.endswith("ņņ"):
+            return w[:-2] + "nn"
+    if w.endswith(("pj", "bj", "mj", "vj")):
+        return w[:-1]
+    if w[-2:] in _LV_PAIRS:
+        return w[:-2] + _LV_PAIRS[w[-2:]]
+    if w.endswith("č"):
+        return w[:-1] + "c"
+    if w.endswith("ļ"):
+        return w[:-1] + "l"
+    if w.endswith("ņ"):
+        return w[:-1] + "n"
+    return w
+
+
+def latvian_stem(word: str) -> str:
+    nv = sum(c in _LV_V for c in word)
+    for aff, vc, pal in _LV_AFFIXES:
+        if nv > vc and len(word) >= len(aff) + 3 and word.endswith(aff):
+            w = word[:-len(aff)]
+            return _lv_unpalatalize(w, aff) if pal else w
+    return word
+
 from .snowball import dutch_stem, finnish_stem, hungarian_stem, romanian_stem, russian_stem, turkish_stem  # noqa: E402
 
 STEMMERS: Dict[str, Callable[[str], str]] = {
@@ -650,4 +788,5 @@ STEMMERS: Dict[str, Callable[[str], str]] = {
     "pt": portuguese_light_stem, "no": norwegian_light_stem, "sv": swedish_stem, "da": danish_stem,
     "ru": russian_stem, "nl": dutch_stem, "ro": romanian_stem, "hu": hungarian_stem, "fi": finnish_stem,
     "ar": arabic_analyze_stem, "hi": hindi_analyze_stem, "bg": bulgarian_stem, "cs": czech_stem, "tr": turkish_stem,
+    "id": indonesian_stem, "lv": latvian_stem,
 }
