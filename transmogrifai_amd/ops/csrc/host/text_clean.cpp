@@ -99,8 +99,8 @@ int64_t tmog_first_ids(const uint8_t* buf, const int64_t* starts, const int64_t*
   auto len = [&](int64_t i) { return (size_t)(ends[i] - starts[i]); };
 #pragma omp parallel num_threads(T)
   {
-    const int t = omp_get_thread_num();
-    const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+    const int t = omp_get_thread_num(), TT = omp_get_num_threads();   // the team may be smaller than T
+    const int64_t lo = n * t / TT, hi = n * (t + 1) / TT;
     int64_t* c = cnt.data() + (size_t)t * kShards;
     for (int64_t i = lo; i < hi; ++i) {
       h[i] = hash_bytes(buf + starts[i], len(i));
@@ -112,7 +112,7 @@ int64_t tmog_first_ids(const uint8_t* buf, const int64_t* starts, const int64_t*
       int64_t run = 0;
       for (int sh = 0; sh < kShards; ++sh) {
         shard_off[sh] = run;
-        for (int u = 0; u < T; ++u) {
+        for (int u = 0; u < TT; ++u) {
           const int64_t x = cnt[(size_t)u * kShards + sh];
           cnt[(size_t)u * kShards + sh] = run;   // this thread's first slot in the shard
           run += x;
