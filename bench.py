@@ -73,14 +73,15 @@ def parse():
     ap.add_argument("--max-training-sample", dest="max_training_sample", type=int, default=None,
                     help="the selector splitter's maxTrainingSample (default: the reference's 1M)")
     ap.add_argument("--dtype", default=None, choices=["fp32", "bf16"],
-                    help="linear learners' design-matrix precision (config.linear_dtype): fp32, or bf16 on the "
-                         "bf16 matrix cores (default; BASELINE config '1 MI355X bf16'); tree learners bin their "
-                         "inputs either way")
+                    help="linear learners' design-matrix precision (config.linear_dtype): fp32 (default; the "
+                         "headline's hold-out AuPR must equal the fp32 model's), or lossy bf16 on the bf16 matrix "
+                         "cores (BASELINE config 2, lr-rf-1m '1 MI355X bf16'); tree learners bin their inputs "
+                         "either way")
     a = ap.parse_args()
     if a.config == "lr-rf-1m" and a.models == "default":
         a.models = "OpLogisticRegression,OpRandomForestClassifier"
-    if a.dtype is None:
-        a.dtype = "bf16"
+    if a.dtype is None:         # BASELINE.json names bf16 for config 2 only
+        a.dtype = "bf16" if a.config == "lr-rf-1m" else "fp32"
     if a.rows is None:
         a.rows = CONFIGS[a.config][1]
     return a
@@ -308,7 +309,7 @@ def _timed(args, one_run, expected_configs, use_gpu, dev, torch, D, sim, n_raw, 
             "higher_is_better": False,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": args.dtype,
+            "dtype": args.dtype if use_gpu else "fp32",     # the bf16 design is a device path
             "data": "synthetic (device-generated, seeded), random-init models",
             ("holdout_aupr" if CONFIGS[args.config][3] == "AuPR" else
              "holdout_" + CONFIGS[args.config][3].lower()): auprs[-1],

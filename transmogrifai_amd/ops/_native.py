@@ -156,14 +156,26 @@ def _declare(lib, sigs):
         fn.restype = _RESTYPES.get(name, C.c_int)
 
 
+def _check_loaded_hash(lib, kind: str) -> None:
+    """The mapped library reports the sources it was built from (``build._provenance_source``)."""
+    fn = getattr(lib, f"tmog_{kind}_source_hash")
+    fn.argtypes = []
+    fn.restype = C.c_char_p
+    got = fn().decode()
+    if got != build.source_hash(kind):
+        raise RuntimeError(f"loaded {kind} library reports source hash {got}, the tree has {build.source_hash(kind)}")
+
+
 def host():
     global _host
     if _host is None:
         with _lock:
             if _host is None:
                 path = build.build_host()
+                build.verify(path, "host")
                 lib = C.CDLL(str(path))
                 _declare(lib, _HOST_SIGS)
+                _check_loaded_hash(lib, "host")
                 _host = lib
     return _host
 
@@ -208,9 +220,11 @@ def hip():
                 if os.environ.get("TMOG_DISABLE_HIP") == "1":
                     raise RuntimeError("HIP kernels disabled by TMOG_DISABLE_HIP=1 but a device tensor was passed")
                 path = build.build_hip()
+                build.verify(path, "hip")       # never load a library built from other sources
                 torch.cuda.init()
                 lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
                 _declare(lib, _HIP_SIGS)
+                _check_loaded_hash(lib, "hip")
                 dbg = int(os.environ.get("TMOG_HIST_DEBUG", "0"))
                 if dbg:
                     lib.tmog_hip_debug_flags(dbg)
