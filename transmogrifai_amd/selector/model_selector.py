@@ -188,23 +188,27 @@ class ModelSelector(BinaryEstimator):
         from ..tuning.validators import refit_key
         ready = (ctx.pop("refit_states", None) or {}).get(refit_key(res.best_learner, params))
         ctx.pop("refit_job", None)
-        # the winner's refit uses the same intra-job parallelism over the ranks as its CV fits
-        from ..parallel import dist as D
-        # (projection mode answers collectives locally but cannot emulate the tree grower's RCCL exchange: local refit)
-        if D.world() > 1 and not D.simulated() and learner.parallel in ("rows", "features"):
-            from ..parallel.learner_parallel import LearnerParallel
-            ctx["par"] = LearnerParallel()
-        try:
-            state = ready if ready is not None else learner.fit_batch(X, y, [job], context=ctx)[0]
-        finally:
-            ctx.pop("par", None)
-        # training evaluation on the prepared data
-        Xr = X if rows is None else X[rows]
-        yr = y if rows is None else y[rows]
-        pred, raw, prob = learner.predict(state, Xr)
-        train_eval: Dict = {}
-        for ev in self.evaluators:
-            train_eval.update(ev.evaluate_arrays(yr.to(torch.float64), pred, raw, prob))
+        from ..workflow.workflow import OpStep as _S, step as _step
+        # the winner's refit and its training evaluation are timed as their own phase (not FeatureEngineering)
+        t_refit = time.time()
+        with _step(_S.ModelRefit):
+            # the winner's refit uses the same intra-job parallelism over the ranks as its CV fits
+            from ..parallel import dist as D
+            # (projection mode answers collectives locally but cannot emulate the tree grower's RCCL exchange: local refit)
+            if D.world() > 1 and not D.simulated() and learner.parallel in ("rows", "features"):
+                from ..parallel.learner_parallel import LearnerParallel
+                ctx["par"] = LearnerParallel()
+            try:
+                state = ready if ready is not None else learner.fit_batch(X, y, [job], context=ctx)[0]
+            finally:
+                ctx.pop("par", None)
+            # training evaluation on the prepared data
+            Xr = X if rows is None else X[rows]
+            yr = y if rows is None else y[rows]
+            pred, raw, prob = learner.predict(state, Xr)
+            train_eval: Dict = {}
+            for ev in self.evaluators:
+                train_eval.update(ev.evaluate_arrays(yr.to(torch.float64), pred, raw, prob))
         summary = {
             "validationType": self.validator.validation_type,
             "validationParameters": self.validator.params(),
@@ -220,7 +224,7 @@ class ModelSelector(BinaryEstimator):
             "trainEvaluation": train_eval,
             "holdoutEvaluation": None,
             "failures": res.failures,
-            "timings": dict(res.timings, selector_total=time.time() - t0),
+            "timings": dict(res.timings, refit=time.time() - t_refit, selector_total=time.time() - t0),
         }
         sched = getattr(self.validator, "last_schedule", None)
         if sched:        # multi-rank: per learner (mode, shard s, spread s, ranks per group, hybrid s)

@@ -33,6 +33,10 @@ class OpStep:
     DataReadingAndFiltering = "DataReadingAndFiltering"
     FeatureEngineering = "FeatureEngineering"
     CrossValidation = "CrossValidation"
+    # the selected model's refit on the whole prepared training set and its training evaluation (inside the
+    # selector's fit, after CrossValidation; Spark charges it to FeatureEngineering's job group -- timed apart here so
+    # FeatureEngineering is the feature stages alone)
+    ModelRefit = "ModelRefit"
     ModelIO = "ModelIO"
     Scoring = "Scoring"
     ResultsSaving = "ResultsSaving"
