@@ -118,3 +118,51 @@ def test_run_main_exits_with_device_fault_status(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == EXIT_DEVICE_FAULT, r.stderr
     assert "fatal device fault" in r.stderr
+
+
+_LANES = {}
+
+
+@register_learner
+class _LaneStuckNB(base):
+    """A stuck fit that records the native slot lane it runs on."""
+    name = "_TestLaneStuckNB"
+
+    def fit_batch(self, X, y, jobs, context=None):
+        from transmogrifai_amd.models import tree_engine as TE
+        _LANES["stuck"] = TE.slot_lane()
+        time.sleep(3.0)
+        return super().fit_batch(X, y, jobs, context)
+
+
+@register_learner
+class _LaneNB(base):
+    name = "_TestLaneNB"
+
+    def fit_batch(self, X, y, jobs, context=None):
+        from transmogrifai_amd.models import tree_engine as TE
+        _LANES.setdefault("after", []).append(TE.slot_lane())
+        return super().fit_batch(X, y, jobs, context)
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_abandoned_fit_quarantines_its_slot_lane(monkeypatch, lanes):
+    """an abandoned fit keeps running on its native tree-grower slot lane, so later fits -- of this
+    validate() and of the next -- must run on other lanes until its thread exits."""
+    from transmogrifai_amd.models import tree_engine as TE
+    monkeypatch.setenv("TMOG_CANCEL_GRACE_S", "0.3")
+    _LANES.clear()
+    res = _validate([("OpNaiveBayes", [{"smoothing": 1.0}]), ("_TestLaneStuckNB", [{"smoothing": 1.0}])],
+                    max_wait=0.8, lanes=lanes, monkeypatch=monkeypatch)
+    assert any("_TestLaneStuckNB" in f for f in res.failures)
+    stuck = _LANES["stuck"]
+    assert stuck in TE.quarantined_lanes()
+    assert stuck not in TE.free_lanes()
+    res2 = _validate([("_TestLaneNB", [{"smoothing": 1.0}]), ("OpNaiveBayes", [{"smoothing": 2.0}])],
+                     lanes=lanes, monkeypatch=monkeypatch)
+    assert res2.best_learner in ("_TestLaneNB", "OpNaiveBayes")
+    assert _LANES["after"] and all(b != stuck for b in _LANES["after"])
+    t_end = time.time() + 10
+    while stuck in TE.quarantined_lanes() and time.time() < t_end:
+        time.sleep(0.1)
+    assert stuck not in TE.quarantined_lanes()           # released once the abandoned thread exited

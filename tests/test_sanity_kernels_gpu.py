@@ -122,3 +122,35 @@ def test_class_column_sums_and_naive_bayes_on_device():
     for a, b in zip(sh, sd):
         np.testing.assert_allclose(b["theta"], a["theta"], rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(b["pi"], a["pi"], rtol=1e-12, atol=1e-12)
+
+
+def test_bf16_gramian_fp32_accuracy_vs_fp64():
+    """The default (bf16 three-part) centred Gramian at fp32-accumulation accuracy against the fp64 Gramian of the
+    stored fp32 data, including a column with a large offset and a tiny spread (not bit-identical to the
+    fp32 kernel, so its error is bounded explicitly), and against the fp32 MFMA kernel at the same bound."""
+    X = _data(n=200_003, d=150)
+    g = torch.Generator().manual_seed(5)
+    y = torch.randint(0, 3, (X.shape[0],), generator=g)
+    ref = X.to(torch.float64)
+    mean = ref.mean(0)
+    Xc = ref - mean
+    oh = torch.nn.functional.one_hot(y, 3).double()
+    A = torch.cat([Xc, oh], 1)
+    Gref = A.t() @ A
+    Xd = X.cuda()
+    Gb = ST._gram_centered_bf16(Xd, mean.cuda(), y.cuda(), 3).cpu()
+    Gf = torch.empty_like(Gref).cuda()
+    from transmogrifai_amd.ops import _native as N
+    N.check(N.hip().tmog_hip_gram_aug(N.ptr(Xd), X.shape[0], X.shape[1], Xd.stride(0),
+                                      N.ptr(mean.cuda().to(torch.float32)), N.ptr(y.cuda().to(torch.int32)), 3,
+                                      N.ptr(Gf), N.stream(Xd.device)), "gram_aug")
+    Gf = Gf.cpu()
+    # scale of each entry: sum |a_i| |a_j| (fp32 accumulation error is relative to it)
+    Aa = A.abs()
+    scale = Aa.t() @ Aa
+    eb = ((Gb - Gref).abs() / scale.clamp_min(1e-30))
+    ef = ((Gf - Gref).abs() / scale.clamp_min(1e-30))
+    assert float(eb.max()) < 2e-6, float(eb.max())
+    assert float(ef.max()) < 2e-6, float(ef.max())
+    # the offset column: variance of a 1e6 + 1e-3 N(0, 1) column survives the centring
+    torch.testing.assert_close(Gb[0, 0], Gref[0, 0], rtol=1e-4, atol=0)

@@ -58,15 +58,53 @@ N_SLOTS, SLOT_LANE = 32, 8
 _lane = threading.local()
 
 
+_lane_lock = threading.Lock()
+_quarantined: set = set()       # lane bases held by abandoned fits (maxWait), never handed out until they exit
+
+
 def slot_lane() -> int:
-    """This thread's slot offset (0 unless a lane was set)."""
-    return getattr(_lane, "base", 0)
+    """This thread's slot offset: the lane it was given, else the first lane no abandoned fit holds."""
+    base = getattr(_lane, "base", None)
+    if base is not None:
+        return base
+    free = free_lanes()
+    if not free:
+        raise RuntimeError("every native tree-grower slot lane is held by a fit abandoned at its maxWait deadline")
+    return free[0]
 
 
 def set_slot_lane(base: int) -> None:
     if base < 0 or base + SLOT_LANE > N_SLOTS:
         raise ValueError(f"slot lane {base} outside the {N_SLOTS} native slots")
     _lane.base = int(base)
+
+
+def free_lanes() -> list:
+    """Lane bases not held by an abandoned fit, lowest first."""
+    with _lane_lock:
+        return [b for b in range(0, N_SLOTS, SLOT_LANE) if b not in _quarantined]
+
+
+def quarantine_lane(base: int, thread: threading.Thread, on_exit=None) -> None:
+    """An abandoned fit (tuning/validators.py maxWait) still runs on lane ``base``: its grow-only native buffers
+    must not be shared with another grower, so the lane is withheld until ``thread`` exits (a reaper joins it,
+    then runs ``on_exit``, e.g. returning the fit's leased stream)."""
+    with _lane_lock:
+        _quarantined.add(int(base))
+
+    def reap():
+        thread.join()
+        if on_exit is not None:
+            on_exit()
+        with _lane_lock:
+            _quarantined.discard(int(base))
+
+    threading.Thread(target=reap, name=f"lane-reaper-{base}", daemon=True).start()
+
+
+def quarantined_lanes() -> set:
+    with _lane_lock:
+        return set(_quarantined)
 
 
 @dataclass

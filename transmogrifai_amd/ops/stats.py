@@ -146,12 +146,14 @@ def bf16_pack(X: torch.Tensor, src, mode, mu, sc, ldb: int, rows: Optional[int] 
 
 
 def _gram_centered_bf16(X: torch.Tensor, mean: torch.Tensor, y_codes, L: int) -> torch.Tensor:
-    """``gram_centered`` on the bf16 matrix cores (``stats_kernels.hip`` gram_bf16_kernel), exactly: the Gramian of
-    ``B = [X_E | 1 | C_hi | C_mid | C_lo | onehot(y)]`` where ``E`` are the columns whose values are exact in bf16
-    (kept raw) and ``C = X_R - mean_R`` the other columns centred in fp32 as the fp32 kernel does and split into
-    three bf16 parts that sum to it exactly (one packing pass, ``bf16_pack``). Every product is exact, sums are
-    fp32 over 256 rows then fp64; the centred blocks of the original columns are assembled from ``B^T B`` in fp64
-    (the ones column gives the raw column sums and the row count)."""
+    """``gram_centered`` on the bf16 matrix cores (``stats_kernels.hip`` gram_bf16_kernel) at fp32-accumulation
+    accuracy: the Gramian of ``B = [X_E | 1 | C_hi | C_mid | C_lo | onehot(y)]`` where ``E`` are the columns whose
+    values are exact in bf16 (kept raw) and ``C = X_R - mean_R`` the other columns centred in fp32 as the fp32 kernel
+    does and split into three bf16 parts that sum to it exactly (one packing pass, ``bf16_pack``). Every single
+    product is exact; the products are summed in fp32 over 256-row slices (so the result carries fp32 rounding of
+    those partial sums, like the fp32 kernel, but is not bit-identical to it), then in fp64 across slices; the
+    centred blocks of the original columns are assembled from ``B^T B`` in fp64 (the ones column gives the raw
+    column sums and the row count). ``tests/test_sanity_kernels_gpu.py`` bounds it against the fp64 Gramian."""
     n, d = X.shape
     dev = X.device
     exact = bf16_exact_columns(X)

@@ -489,9 +489,9 @@ class OpValidator:
         # rank) and maxWait is unbounded (a deadline could cancel a collective fit on one rank and not another)
         if world > 1 and (n_collective > 1 or (n_collective and self.max_wait < _UNBOUNDED_WAIT)):
             return 1
-        from ..models.tree_engine import N_SLOTS, SLOT_LANE
+        from ..models.tree_engine import free_lanes
         cap = int(env) if env else 2
-        return max(1, min(cap, n_learners, N_SLOTS // SLOT_LANE))
+        return max(1, min(cap, n_learners, len(free_lanes())))
 
     def _fit_eval_concurrent(self, models, order, jobs, owner, me, X, y, train_rows, val_rows, ctx, t0, lanes, n_tr,
                              pars=None):
@@ -537,6 +537,14 @@ class OpValidator:
         crit = SP.lease(dev, 1, high=True) if gpu and lanes > 1 and os.environ.get("TMOG_LANE_PRIO", "0") == "1" \
             else []
         side = crit + (SP.lease(dev, lanes - 1 - len(crit)) if gpu else [])
+        # native slot lanes no abandoned fit holds (models/tree_engine.py quarantine_lane)
+        bases = TE.free_lanes()
+        if not bases:
+            raise RuntimeError("every native tree-grower slot lane is held by a fit abandoned at its maxWait deadline")
+        lanes = min(lanes, len(bases))
+        if gpu and len(side) > lanes - 1:
+            SP.release(dev, side[lanes - 1:])
+            side = side[:lanes - 1]
         if gpu:
             streams = crit + [cur] + side[len(crit):]
             lanes = len(streams)
@@ -549,7 +557,7 @@ class OpValidator:
             try:
                 if gpu:
                     torch.cuda.set_device(dev)
-                TE.set_slot_lane(w * TE.SLOT_LANE)
+                TE.set_slot_lane(bases[w])
                 with cancel.scope(token), (torch.cuda.stream(streams[w]) if gpu else contextlib.nullcontext()):
                     while True:
                         with lock:
@@ -596,6 +604,12 @@ class OpValidator:
                 # a fit inside a long native call never reaches a check: give it up (the reference abandons
                 # its future) rather than block the selector past maxWait + grace
                 abandoned = [w for w, t in enumerate(th) if t.is_alive()]
+                # an abandoned lane keeps its native slots (and its side stream, returned by the reaper) until its
+                # thread exits: later fits -- this selector's and later validate() calls' -- get other lanes
+                for w in abandoned:
+                    st_w = streams[w] if gpu else None
+                    rel = (lambda s_=st_w: SP.release(dev, [s_])) if (gpu and st_w is not cur) else None
+                    TE.quarantine_lane(bases[w], th[w], rel)
                 if abandoned:
                     log.warning("maxWait: %d learner lane(s) did not stop within %.0fs of cancellation; abandoned",
                                 len(abandoned), _cancel_grace_s())
@@ -607,7 +621,7 @@ class OpValidator:
             if abandoned:
                 for st in live + [cur]:
                     st.synchronize()
-                SP.release(dev, live)           # an abandoned lane keeps its stream leased
+                SP.release(dev, live)           # an abandoned lane's stream is released by its reaper
             else:
                 torch.cuda.synchronize(dev)
                 SP.release(dev, side)
@@ -625,11 +639,14 @@ class OpValidator:
     def _fit_eval_bounded(self, lname, grid, mine, X, y, train_rows, val_rows, ctx, remaining: float):
         """:meth:`_fit_eval` under the ``maxWait`` deadline (``awaitResult(..., maxWait)``, OpValidator.scala:348):
         the learner runs on a worker thread with the caller's device and stream; if it has not returned when
-        the deadline passes, its grid points are reported failed. The reference abandons the future; here the
-        fit is cancelled cooperatively (utils/cancel.py: the learners check between rounds / iterations) and
-        the worker is JOINED before validation goes on, so a timed-out fit never shares the GPU stream, the
-        native tree-grower slots or the binning cache with the learners that follow. Only for learners whose
-        jobs are local to this rank -- a spread learner's collectives must not be left half-way on one rank."""
+        the deadline passes, its grid points are reported failed. The fit is cancelled cooperatively
+        (utils/cancel.py: the learners check between rounds / iterations) and joined for a grace period; a fit
+        stuck inside a long native call is then abandoned, as the reference abandons its future. An abandoned
+        fit keeps running on the caller's stream -- later learners' work is stream-ordered behind it, which is
+        safe -- and on its native tree-grower slot lane, which is quarantined until its thread exits
+        (models/tree_engine.py quarantine_lane) so no later grower shares its grow-only device buffers; it works on
+        its own copy of the context. Only for learners whose jobs are local to this rank -- a spread learner's
+        collectives must not be left half-way on one rank."""
         import threading
         from ..utils import cancel
         box: Dict[str, Any] = {}
@@ -639,9 +656,12 @@ class OpValidator:
         stream = torch.cuda.current_stream(dev) if gpu else None
         ctx.setdefault("refit_states", {})     # shared by the worker's copy: the selector reads the refits
         wctx = dict(ctx)
+        from ..models import tree_engine as TE
+        lane = TE.slot_lane()
 
         def work():
             try:
+                TE.set_slot_lane(lane)
                 if gpu:
                     torch.cuda.set_device(dev)
                 with cancel.scope(token), (torch.cuda.stream(stream) if gpu else contextlib.nullcontext()):
@@ -658,6 +678,7 @@ class OpValidator:
             token.set()
             th.join(_cancel_grace_s())      # returns at the fit's next cancellation check
             if th.is_alive():           # inside a long native call: abandoned, as the reference's future is
+                TE.quarantine_lane(lane, th)
                 log.warning("Model %s did not stop within %.0fs of its maxWait cancellation; abandoned", lname,
                             _cancel_grace_s())
             log.warning("Model %s did not finish within maxWait=%ss; its %d fits are dropped", lname,

@@ -20,7 +20,7 @@ EXIT_DEVICE_FAULT = 70
 
 # message fragments of the sticky HIP / HSA failures (hipGetErrorString texts and the runtime's aborts)
 _STICKY = ("illegal memory access", "illegal address", "hiperrorillegaladdress", "hiperrorlaunchfailure",
-           "unspecified launch failure", "launch failure", "device-side assert", "memory access fault",
+           "unspecified launch failure", "device-side assert", "memory access fault",
            "hsa_status_error", "gpu hang", "hiperrorecc", "ecc error", "hardware exception",
            "an illegal instruction")
 
@@ -31,8 +31,9 @@ class DeviceFault(RuntimeError):
 
 def is_device_fault(err: BaseException, device: Optional[torch.device] = None, probe: bool = True) -> bool:
     """True when ``err`` is (or left behind) a sticky device error. Out-of-memory is not one. With ``probe``
-    and a CUDA ``device``, a synchronisation tells a context that is still healthy from a dead one whatever
-    the message said."""
+    and a CUDA ``device``, a synchronisation of the calling thread's current stream tells a context that is still
+    healthy from a dead one whatever the message said (only that stream: a learner lane must not wait for -- or
+    be blamed for -- the other lanes' queued work; a sticky error fails every synchronisation on the context)."""
     if isinstance(err, DeviceFault):
         return True
     msg = f"{type(err).__name__}: {err}".lower()
@@ -42,7 +43,7 @@ def is_device_fault(err: BaseException, device: Optional[torch.device] = None, p
         return True
     if probe and device is not None and torch.device(device).type == "cuda":
         try:
-            torch.cuda.synchronize(device)
+            torch.cuda.current_stream(device).synchronize()
         except Exception:  # noqa: BLE001 - any failure of a bare synchronise means the context is gone
             return True
     return False
