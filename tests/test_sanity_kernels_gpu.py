@@ -130,6 +130,8 @@ def test_bf16_gramian_fp32_accuracy_vs_fp64():
     fp32 kernel, so its error is bounded explicitly), and against the fp32 MFMA kernel at the same bound."""
     X = _data(n=200_003, d=150)
     g = torch.Generator().manual_seed(5)
+    # large offset, small spread that fp32 still resolves (ulp at 1e4 ~ 1e-3)
+    X[:, 0] = (1e4 + 1e-2 * torch.randn(X.shape[0], generator=g, dtype=torch.float64)).to(torch.float32)
     y = torch.randint(0, 3, (X.shape[0],), generator=g)
     ref = X.to(torch.float64)
     mean = ref.mean(0)
@@ -152,5 +154,6 @@ def test_bf16_gramian_fp32_accuracy_vs_fp64():
     ef = ((Gf - Gref).abs() / scale.clamp_min(1e-30))
     assert float(eb.max()) < 2e-6, float(eb.max())
     assert float(ef.max()) < 2e-6, float(ef.max())
-    # the offset column: variance of a 1e6 + 1e-3 N(0, 1) column survives the centring
+    # the offset column: the variance of a 1e4 + 1e-2 N(0, 1) column survives the centring
+    assert float(Gref[0, 0]) > 0
     torch.testing.assert_close(Gb[0, 0], Gref[0, 0], rtol=1e-4, atol=0)
