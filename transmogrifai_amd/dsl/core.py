@@ -51,6 +51,7 @@ def _replace(self, old, new):
     return ReplaceTransformer(old_value=old, new_value=new).set_input(self).get_output()
 
 
+@register(T.FeatureType, "occurs")         # RichFeature.occurs (RichFeature.scala): the same transformer
 @register(T.FeatureType, "to_occur")
 def _to_occur(self, match_fn: Optional[Callable] = None):
     from ..stages.feature.misc_stages import ToOccurTransformer
@@ -293,11 +294,19 @@ def _vec_text(self, num_terms: int = 512, binary: bool = False, others=(), auto_
               prepend_feature_name: bool = True, top_k: int = 20, min_support: int = 10, clean_text: bool = True,
               track_nulls: bool = True, **kw):
     if self.wtype in (T.Text, T.TextArea):
+        # RichTextFeature.vectorize (RichTextFeature.scala:135-187): tokenize, hash, then the token lists' text
+        # lengths (track_text_len) and null indicators (track_nulls) combined after the hashes
         toks = [TS.TextTokenizer(min_token_length=min_token_length, to_lowercase=to_lowercase)
                 .set_input(f).get_output() for f in _others(self, others)]
-        return V.OPCollectionHashingVectorizer(num_features=num_terms, binary_freq=binary,
-                                               hash_space_strategy=hash_space_strategy,
-                                               prepend_feature_name=prepend_feature_name).set_input(toks).get_output()
+        hashed = V.OPCollectionHashingVectorizer(num_features=num_terms, binary_freq=binary,
+                                                 hash_space_strategy=hash_space_strategy,
+                                                 prepend_feature_name=prepend_feature_name).set_input(toks).get_output()
+        parts = [hashed]
+        if kw.get("track_text_len", False):
+            parts.append(TS.TextLenTransformer().set_input(toks).get_output())
+        if track_nulls:
+            parts.append(TS.TextListNullTransformer().set_input(toks).get_output())
+        return parts[0] if len(parts) == 1 else V.VectorsCombiner().set_input(parts).get_output()
     return _pivot(self, others, top_k, min_support, clean_text, track_nulls)
 
 
@@ -424,6 +433,34 @@ def _auto_bucketize_map(self, label: FeatureLike, track_nulls: bool = True, trac
         track_nulls=track_nulls, track_invalid=track_invalid, min_info_gain=min_info_gain, clean_keys=clean_keys,
         allow_keys=list(allow_list_keys) or None, block_keys=list(block_list_keys) or None
     ).set_input(label, self).get_output()
+
+
+@register([T.TextMap, T.TextAreaMap], "vectorize")
+def _vec_text_map_dispatch(self, *a, **kw):
+    # the converted map types (EmailMap, URLMap, PhoneMap, Base64Map, ...) keep their own RichMapFeature vectorize
+    if self.wtype in (T.TextMap, T.TextAreaMap):
+        return _vec_text_map(self, *a, **kw)
+    return _vec_map(self, *a, **kw)
+
+
+def _vec_text_map(self, clean_text: bool = True, clean_keys: bool = D.CleanKeys,
+                  should_prepend_feature_name: bool = D.PrependFeatureName, allow_list_keys=(), block_list_keys=(),
+                  others=(), track_nulls: bool = D.TrackNulls, track_text_len: bool = D.TrackTextLen,
+                  num_hashes: int = D.DefaultNumOfFeatures, hash_space_strategy: str = D.HashSpaceStrategy, **kw):
+    """``RichTextMapFeature.vectorize`` (RichMapFeature.scala:188-250): text maps are HASHED (every value's tokens of
+    every key into one shared space), with per-key text lengths / null indicators from the raw maps."""
+    from ..stages.feature.maps import TextMapHashingVectorizer, TextMapLenEstimator, TextMapNullEstimator
+    fs = _others(self, others)
+    hashed = TextMapHashingVectorizer(num_features=int(kw.get("num_terms", num_hashes)), clean_keys=clean_keys,
+                                      clean_text=clean_text, prepend_feature_name=should_prepend_feature_name,
+                                      allow_keys=list(allow_list_keys) or None,
+                                      block_keys=list(block_list_keys) or None).set_input(fs).get_output()
+    parts = [hashed]
+    if track_text_len:
+        parts.append(TextMapLenEstimator(clean_keys=clean_keys).set_input(fs).get_output())
+    if track_nulls:
+        parts.append(TextMapNullEstimator(clean_keys=clean_keys).set_input(fs).get_output())
+    return parts[0] if len(parts) == 1 else V.VectorsCombiner().set_input(parts).get_output()
 
 
 @register(T.OPMap, "vectorize")

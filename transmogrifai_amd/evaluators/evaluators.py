@@ -269,6 +269,13 @@ class CustomEvaluator(OpEvaluatorBase):
         return {self.metric: float(self.fn(y, pred, raw, prob))}
 
 
+def _custom(metric_name, is_larger_better, evaluate_fn):
+    """``Evaluators.*.custom`` (Evaluators.scala:126-140): larger is better unless said otherwise."""
+    if evaluate_fn is None:
+        raise ValueError("a custom evaluator needs evaluate_fn")
+    return CustomEvaluator(metric_name, is_larger_better, evaluate_fn)
+
+
 class Evaluators:
     """Factory mirroring ``Evaluators.scala``."""
 
@@ -305,8 +312,8 @@ class Evaluators:
             return OpBinScoreEvaluator("BrierScore")
 
         @staticmethod
-        def custom(metric_name, is_larger_better, evaluate_fn):
-            return CustomEvaluator(metric_name, is_larger_better, evaluate_fn)
+        def custom(metric_name, is_larger_better=True, evaluate_fn=None):
+            return _custom(metric_name, is_larger_better, evaluate_fn)
 
     class MultiClassification:
         def __new__(cls):
@@ -333,8 +340,8 @@ class Evaluators:
             return OpLogLossEvaluator()
 
         @staticmethod
-        def custom(metric_name, is_larger_better, evaluate_fn):
-            return CustomEvaluator(metric_name, is_larger_better, evaluate_fn)
+        def custom(metric_name, is_larger_better=True, evaluate_fn=None):
+            return _custom(metric_name, is_larger_better, evaluate_fn)
 
     class Regression:
         def __new__(cls):
@@ -357,8 +364,8 @@ class Evaluators:
             return OpRegressionEvaluator("R2")
 
         @staticmethod
-        def custom(metric_name, is_larger_better, evaluate_fn):
-            return CustomEvaluator(metric_name, is_larger_better, evaluate_fn)
+        def custom(metric_name, is_larger_better=True, evaluate_fn=None):
+            return _custom(metric_name, is_larger_better, evaluate_fn)
 
     class Forecast:
         def __new__(cls):

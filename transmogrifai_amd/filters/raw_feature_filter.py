@@ -73,6 +73,9 @@ class FeatureDistribution:
     summaryInfo: List[float]
     moments: Optional[Dict[str, float]] = None
     type: str = TRAINING
+    # TextStats of the values (FeatureDistribution.scala cardEstimate): {"valueCounts": {value: n}, "lengthCounts":
+    # {length: n}}, at most MAX_CARDINALITY + 1 distinct values; in memory only (the reference ignores it in JSON)
+    cardEstimate: Optional[Dict[str, Dict]] = None
 
     @property
     def feature_key(self) -> FeatureKey:
@@ -125,18 +128,68 @@ class FeatureDistribution:
         if self.moments and o.moments:
             mom = _combine_moments(self.moments, o.moments)
         return FeatureDistribution(self.name, self.key, self.count + o.count, self.nulls + o.nulls, d, info,
-                                   mom or o.moments, self.type)
+                                   mom or o.moments, self.type, _card_plus(self.cardEstimate, o.cardEstimate))
 
-    def to_json(self) -> Dict:
-        return {"name": self.name, "key": self.key, "count": int(self.count), "nulls": int(self.nulls),
-                "distribution": [float(x) for x in np.asarray(self.distribution).tolist()],
-                "summaryInfo": [float(x) for x in self.summaryInfo], "moments": self.moments, "type": self.type}
+    def to_json(self, with_card: bool = False) -> Dict:
+        out = {"name": self.name, "key": self.key, "count": int(self.count), "nulls": int(self.nulls),
+               "distribution": [float(x) for x in np.asarray(self.distribution).tolist()],
+               "summaryInfo": [float(x) for x in self.summaryInfo], "moments": self.moments, "type": self.type}
+        if with_card:
+            out["cardEstimate"] = self.cardEstimate
+        return out
 
     @staticmethod
     def from_json(d: Dict) -> "FeatureDistribution":
         return FeatureDistribution(d["name"], d.get("key"), int(d["count"]), int(d["nulls"]),
                                    np.asarray(d.get("distribution", []), np.float64), list(d.get("summaryInfo", [])),
                                    d.get("moments"), d.get("type", TRAINING))
+
+
+def _jstr(x: float) -> str:
+    """``Double.toString`` of the JVM (the reference's value keys): plain between 1e-3 and 1e7, else d.dddE+n."""
+    x = float(x)
+    if x != x or x in (math.inf, -math.inf):
+        return "NaN" if x != x else ("Infinity" if x > 0 else "-Infinity")
+    if x == 0 or 1e-3 <= abs(x) < 1e7:
+        r = repr(x)
+        return r if ("." in r or "e" in r) else r + ".0"
+    m, e = f"{x:.17e}".split("e")
+    m = repr(float(m)).rstrip("0")
+    m = m + "0" if m.endswith(".") else m
+    return f"{m}E{int(e)}"
+
+
+def _text_stats(values, weights=None) -> Dict[str, Dict]:
+    """``TextStats`` of a value sequence (strings or numbers; optional integer weight per value) with the reference's
+    MaxCardinality cap: once more than MAX_CARDINALITY distinct values are seen no new value is added
+    (TextStats.monoid)."""
+    vc: Dict[str, int] = {}
+    lc: Dict[int, int] = {}
+    for i, v in enumerate(values):
+        w = 1 if weights is None else int(weights[i])
+        t = v if isinstance(v, str) else _jstr(v)
+        if t in vc:
+            vc[t] += w
+        elif len(vc) <= MAX_CARDINALITY:
+            vc[t] = w
+        lc[len(t)] = lc.get(len(t), 0) + w
+    return {"valueCounts": vc, "lengthCounts": lc}
+
+
+def _card_plus(a, b):
+    if a is None or b is None:
+        return a if b is None else b
+    if len(a["valueCounts"]) > MAX_CARDINALITY:
+        return a
+    if len(b["valueCounts"]) > MAX_CARDINALITY:
+        return b
+    vc = dict(a["valueCounts"])
+    for k, v in b["valueCounts"].items():
+        vc[k] = vc.get(k, 0) + v
+    lc = dict(a["lengthCounts"])
+    for k, v in b["lengthCounts"].items():
+        lc[k] = lc.get(k, 0) + v
+    return {"valueCounts": vc, "lengthCounts": lc}
 
 
 def _combine_moments(a, b):
@@ -238,6 +291,19 @@ class AllFeatureInformation:
     predictor_summaries: "OrderedDict[FeatureKey, Summary]"
     predictor_distributions: List[FeatureDistribution]
     correlation_info: Dict[FeatureKey, Dict[FeatureKey, float]]
+
+
+def _numeric_card(values: torch.Tensor, valid: torch.Tensor) -> Dict[str, Dict]:
+    """TextStats of a numeric column: distinct values and their counts in one device pass (``torch.unique``), the
+    lowest MAX_CARDINALITY + 1 values kept when there are more."""
+    v = values[valid.to(torch.bool)] if valid is not None else values
+    u, c = torch.unique(v.to(torch.float64), return_counts=True)
+    u, c = u[:MAX_CARDINALITY + 1].cpu().tolist(), c[:MAX_CARDINALITY + 1].cpu().tolist()
+    vc = {_jstr(a): int(b) for a, b in zip(u, c)}
+    lc: Dict[int, int] = {}
+    for a, b in vc.items():
+        lc[len(a)] = lc.get(len(a), 0) + b
+    return {"valueCounts": vc, "lengthCounts": lc}
 
 
 # ------------------------------------------------------------------------------------ preparation
@@ -487,7 +553,8 @@ class RawFeatureFilter:
                 else:
                     info_v, hist = [sm.min, sm.max, sm.sum, sm.count], h[:2]
                 dists[k] = FeatureDistribution(k[0], k[1], n, nul, np.asarray(hist, np.float64), info_v,
-                                               _moments_from_sums(*power[k]), dist_type)
+                                               _moments_from_sums(*power[k]), dist_type,
+                                               _numeric_card(*P.numeric_cols[k]))
         for k in P.kind:
             if k in dists or k not in use_sum:
                 continue
@@ -508,8 +575,13 @@ class RawFeatureFilter:
                     for r in rows:
                         if r:
                             np.add.at(hist, hash_terms(r, nb), 1.0)
+                if k in P.text_codes:
+                    pairs = [(x, int(w)) for w, t in zip(cnt, toks) if w for x in (t or ())]
+                    card = _text_stats([x for x, _ in pairs], [w for _, w in pairs])
+                else:
+                    card = _text_stats(x for r in rows if r for x in r)
                 dists[k] = FeatureDistribution(k[0], k[1], n, nulls, hist, [sm.min, sm.max, sm.sum, sm.count],
-                                               _moments_from_sums(*power[k]), dist_type)
+                                               _moments_from_sums(*power[k]), dist_type, card)
             else:
                 rows = P.values[k]
                 nulls = sum(1 for r in rows if r is None)
@@ -526,7 +598,7 @@ class RawFeatureFilter:
                     info_v = [sm.min, sm.max, sm.sum, sm.count]
                     hist = np.array([float((flat == sm.max).sum()), float((flat != sm.max).sum())])
                 dists[k] = FeatureDistribution(k[0], k[1], n, nulls, hist, info_v, _moments_from_sums(*power[k]),
-                                               dist_type)
+                                               dist_type, _text_stats(flat.tolist()))
         # ---- null-indicator / label leakage correlations
         if info is not None:
             corr = info.correlation_info

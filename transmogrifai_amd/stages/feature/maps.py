@@ -577,10 +577,46 @@ GeolocationMapVectorizer = _named("GeolocationMapVectorizer", "vecGeoMap", "geo"
 
 
 @register_stage
-class TextMapHashingVectorizer(MapVectorizer):
-    """Hash every key's tokens (``TextMapHashingVectorizer`` of ``OPMapVectorizer.scala``)."""
+class TextMapHashingVectorizer(VectorizerMixin, SequenceTransformer):
+    """``TextMapHashingVectorizer`` (OPMapVectorizer.scala:411-470): the tokens of every value of every input map
+    (allow / block lists on the cleaned keys) are combined into ONE token list per row and hashed into one space of
+    ``num_features`` columns (``numInputs = 1``), the first input's name prepended to the terms. Null / length
+    tracking is done outside, per key, by :class:`TextMapNullEstimator` / :class:`TextMapLenEstimator`, as
+    ``RichTextMapFeature.vectorize`` wires it."""
     operation_name = "vecHashTextMap"
-    _defaults = dict(MapVectorizer._defaults, kind="smarttext", max_cardinality=-1)
+    _defaults = {"num_features": 512, "clean_keys": False, "clean_text": True, "prepend_feature_name": True,
+                 "allow_keys": None, "block_keys": None}
+
+    def transform_columns(self, *cols, ds=None):
+        from ...ops.text import HashInput, hashed_tf
+        from .vectorizers import col_meta
+        p = self.params
+        tfs = self.get_transient_features()
+        nf = int(p["num_features"])
+        if len(tfs) == 1:
+            cm = [col_meta(tfs[0]) for _ in range(nf)]
+        else:
+            cm = [OpVectorColumnMetadata(tuple(t.name for t in tfs), tuple(t.type_name for t in tfs), None, None,
+                                         None) for _ in range(nf)]
+        self.metadata["vector_metadata"] = self.vector_metadata(cm)
+        dev = default_device()
+        n = len(cols[0]) if cols else 0
+        allow = set(p["allow_keys"]) if p["allow_keys"] else None
+        block = set(p["block_keys"] or ())
+        rows: List[List[str]] = [[] for _ in range(n)]
+        for c in cols:
+            coo = map_coo(c, "pivot", p["clean_keys"], torch.device("cpu"))
+            if not coo.nnz:
+                continue
+            toks = TU.tokenize_batch(coo.vocab).lists() if coo.vocab else []
+            ok = [(allow is None or k in allow) and k not in block for k in coo.keys]
+            for r, k, v in zip(coo.row.tolist(), coo.key.tolist(), coo.vcode.tolist()):
+                if ok[k]:
+                    rows[r].extend(toks[v])
+        prefix = int(TU.hash_terms([tfs[0].name], nf)[0]) if (p["prepend_feature_name"] and tfs) else None
+        out = torch.empty(n, nf, dtype=vector_dtype(dev), device=dev)
+        hashed_tf(out, [HashInput(None, TU.TokenBatch.from_lists(rows), prefix)], nf, True, False)
+        return self._vec(out)
 
 
 def _present_keys(cols, kind: str, clean: bool) -> List[List[str]]:
