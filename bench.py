@@ -163,8 +163,9 @@ def main():
         dev = torch.device("cpu")
     sim = os.environ.get("TMOG_SIM_WORLD")
     if sim:      # projection (scripts/project_schedule.py): this process times rank TMOG_SIM_RANK's share
+        # spread / hybrid learners run too: collectives are answered locally, and the tree grower's split-record
+        # exchange is answered by tiling this rank's records (tree_grow_hip.hip tmog_hip_fp_allgather)
         D.simulate(int(os.environ.get("TMOG_SIM_RANK", "0")), int(sim))
-        os.environ.setdefault("TMOG_PARALLEL_MODE", "shard")    # spread learners would need real peers
     else:
         D.init_from_env(device_id=local_rank if use_gpu else None)
     world = D.world()

@@ -262,3 +262,77 @@ def test_rank_groups_feature_and_row_parallel(tmp_path):
         # same optimum up to the optimizer tolerance (fp32 partial sums in another order), as for the world
         np.testing.assert_allclose(np.asarray(o["lr"]), np.asarray(ref_lr), rtol=0, atol=1.5e-3)
     assert outs[0]["lr"] == outs[1]["lr"] and outs[2]["lr"] == outs[3]["lr"]   # identical inside a group
+
+
+@pytest.mark.gpu
+def test_feature_parallel_resident_loop_on_one_gpu():
+    """Feature-parallel growth on the DEVICE-PLANNED level loop (tree_resident.hip): the split records are
+    all-gathered over the job group's RCCL communicator and merged on the stream between split-find and
+    partition. Forced on a 1-rank world, the trees equal plain device-planned growth bit for bit, and the call
+    really took the resident loop (a ResidentTree comes back, not a host-planned Forest)."""
+    from transmogrifai_amd.models import tree_engine as TE
+    from transmogrifai_amd.models.binning import find_splits, quantize
+    from transmogrifai_amd.parallel.learner_parallel import LearnerParallel
+    dev = torch.device("cuda")
+    X, y = _data(n=6000, d=40)
+    X, y = X.to(dev), y.to(dev)
+    spec = find_splits(X, 32, missing_value=0.0, reserve_missing=True)
+    Xb = quantize(X, spec)
+    N = X.shape[0]
+    g = torch.sigmoid(0.3 * X[:, 0]) - y
+    t1 = torch.stack([g, 0.5 * g]).float()
+    t2 = torch.full_like(t1, 0.25)
+    jobs = [TE.TreeJob(m, TE.TreeParams(max_depth=6, min_child_weight=1.0, reg_lambda=1.0, gamma=0.1, eta=0.3,
+                                        split_eps=1e-6), torch.arange(N, device=dev)) for m in range(2)]
+    kw = dict(mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=t1, t2=t2, B=32, missing_bin=spec.missing_bin,
+              collect_leaves=True, groups=1, resident=True)
+    ref = TE.grow_forest(Xb, spec.n_bins, jobs, csr=TE.onebin_csr(Xb, spec.n_bins), **kw)
+    fp = TE.fp_plan(Xb, spec.n_bins, LearnerParallel(rank=0, world=1), sparse=True, force=True)
+    got = TE.grow_forest(Xb, spec.n_bins, jobs, csr=TE.onebin_csr(Xb, spec.n_bins, cols=fp.one_cols), fp=fp, **kw)
+    assert isinstance(ref, TE.ResidentTree) and isinstance(got, TE.ResidentTree)
+    a, b = TE.resident_forests([ref, got])
+    for k in ("tree_off", "nodes", "default_left", "value"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    assert torch.equal(ref.leaf_assign.rows, got.leaf_assign.rows)
+    assert torch.equal(ref.leaf_assign.value, got.leaf_assign.value)
+
+
+@pytest.mark.gpu
+def test_projected_rank_group_answers_the_exchange_locally():
+    """Projection of a 2-rank feature-parallel group on one GPU (parallel/dist.py simulate): no communicator, the
+    split-record exchange is answered locally (this rank's records tiled), so the device-planned loop runs with
+    the group's shapes -- the projection can time hybrid schedules."""
+    from transmogrifai_amd.models import tree_engine as TE
+    from transmogrifai_amd.models.binning import find_splits, quantize
+    from transmogrifai_amd.parallel import dist as D
+    from transmogrifai_amd.parallel.learner_parallel import LearnerParallel
+    dev = torch.device("cuda")
+    X, y = _data(n=4000, d=40)
+    X, y = X.to(dev), y.to(dev)
+    spec = find_splits(X, 32, missing_value=0.0, reserve_missing=True)
+    Xb = quantize(X, spec)
+    N = X.shape[0]
+    t1 = (torch.sigmoid(0.3 * X[:, 0]) - y).float()[None, :]
+    t2 = torch.full_like(t1, 0.25)
+    jobs = [TE.TreeJob(0, TE.TreeParams(max_depth=5, min_child_weight=1.0, reg_lambda=1.0, split_eps=1e-6),
+                       torch.arange(N, device=dev))]
+    D.simulate(1, 2)
+    try:
+        par = LearnerParallel()
+        assert (par.rank, par.world) == (1, 2)
+        fp = TE.fp_plan(Xb, spec.n_bins, par, sparse=True)
+        rt = TE.grow_forest(Xb, spec.n_bins, jobs, mode=TE.MODE_GH, kind=TE.KIND_NEWTON, t1=t1, t2=t2, B=32,
+                            missing_bin=spec.missing_bin, collect_leaves=True, groups=1, resident=True, fp=fp,
+                            csr=TE.onebin_csr(Xb, spec.n_bins, cols=fp.one_cols))
+        assert isinstance(rt, TE.ResidentTree)
+        (f,) = TE.resident_forests([rt])
+        internal = f.nodes[:, 2] >= 0
+        assert internal.any()
+        mine = set(range(fp.mlo, fp.mhi))       # only this rank's multi-bin slice (and its one-bin columns) split
+        nb = np.asarray(spec.n_bins)
+        multi = np.nonzero(nb != 1)[0]
+        used = set(f.nodes[internal, 0].tolist())
+        allowed = {int(multi[i]) for i in mine} | {int(c) for c in fp.one_cols}
+        assert used <= allowed
+    finally:
+        D.simulate(0, 1)

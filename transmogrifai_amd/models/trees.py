@@ -784,7 +784,9 @@ class XGBoostClassifierLearner(_BoostLearner):
         # GPU path a round is enqueued without any host synchronisation -- the level plans, the tree finalisation
         # and the epilogue all run on the device; the host Forests are built from the node records once, after
         # the last round, and the early-stopping AuPR is read ES_LAG rounds late.
-        resident = fused and par is None and TE.resident_enabled()
+        # a feature-parallel job (fp: the jobs spread over a rank group) grows on the device-planned loop too, as one
+        # job group whose level exchange (RCCL all-gather + merge of the split records) is enqueued on the stream
+        resident = fused and (par is None or fp is not None) and TE.resident_enabled()
         es_lag = max(1, int(os.environ.get("TMOG_ES_LAG", "2"))) if resident else 1
         # Fused round prologue (tree_engine.boost_prologue): the scales, the root copy and the staged (g, h) in
         # one launch; the epilogue's maxima buffer is double-buffered (round it writes tam2[it & 1], which round
@@ -939,7 +941,8 @@ class XGBoostClassifierLearner(_BoostLearner):
             gpp = max(1, int(os.environ.get("TMOG_XGB_PIPE_GROUPS", "1")))
             _run_parts(dev, [(list(range(int(cuts[k]), int(cuts[k + 1]))), k * gpp, gpp) for k in range(parts)], run)
         else:
-            run(list(range(P)))
+            # feature-parallel: all jobs in one group on one stream (one communicator, one collective order)
+            run(list(range(P)), groups=1 if (resident and fp is not None) else None)
         if _XGB_PROF is not None:
             import sys as _sys
             if dev.type == "cuda":

@@ -264,14 +264,20 @@ struct GpuBackend {
     const size_t bytes = rb * (size_t)m;
     grow_plain(sl.fp_recv, sl.fp_recv_cap, bytes * (size_t)g.fp_world, sl.stream);
     ncclComm_t comm = (ncclComm_t)g.fp_comm[group];
-    ncclResult_t r;
-    {
-      // enqueue under a process-wide lock: the job groups' host threads issue their (independent,
-      // per-communicator) collectives concurrently, and RCCL's enqueue path keeps process-global state
-      std::lock_guard<std::mutex> lk(rccl_mutex());
-      r = ncclAllGather(rec, sl.fp_recv, bytes, ncclUint8, comm, sl.stream);
+    if (comm == nullptr) {        // single-GPU projection of a rank group: the exchange answered locally
+      for (int r = 0; r < g.fp_world; ++r)
+        hchk(hipMemcpyAsync(sl.fp_recv + (size_t)r * bytes, rec, bytes, hipMemcpyDeviceToDevice, sl.stream),
+             "fp local exchange");
+    } else {
+      ncclResult_t r;
+      {
+        // enqueue under a process-wide lock: the job groups' host threads issue their (independent,
+        // per-communicator) collectives concurrently, and RCCL's enqueue path keeps process-global state
+        std::lock_guard<std::mutex> lk(rccl_mutex());
+        r = ncclAllGather(rec, sl.fp_recv, bytes, ncclUint8, comm, sl.stream);
+      }
+      if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllGather: ") + ncclGetErrorString(r));
     }
-    if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllGather: ") + ncclGetErrorString(r));
     kchk(tmog_hip_fp_merge(sl.fp_recv, g.fp_world, m, (int64_t)rb, g.S, feat, bin, gain, dl, left, sl.stream),
          "fp_merge");
   }
@@ -475,6 +481,25 @@ void* tmog_hip_rccl_comm_init(const char* id_bytes, int world, int rank) {
   }
   return (void*)comm;
 }
+// All-gather of `bytes` per rank on `stream` for the device-planned feature-parallel levels (tree_resident.hip).
+// comm == nullptr with world > 1 is the single-GPU projection of a rank group (scripts/project_schedule.py): the
+// other ranks' records are answered locally with copies of this rank's, so the level's exchange and merge run
+// with the group's shapes (the trees then only see this rank's feature slice).
+int tmog_hip_fp_allgather(const void* send, void* recv, int64_t bytes, void* comm, int world, hipStream_t stream) {
+  if (bytes <= 0) return 0;
+  if (comm == nullptr) {
+    for (int r = 0; r < world; ++r) {
+      const hipError_t e = hipMemcpyAsync((uint8_t*)recv + (size_t)r * (size_t)bytes, send, (size_t)bytes,
+                                          hipMemcpyDeviceToDevice, stream);
+      if (e != hipSuccess) return (int)e;
+    }
+    return 0;
+  }
+  std::lock_guard<std::mutex> lk(rccl_mutex());
+  const ncclResult_t r = ncclAllGather(send, recv, (size_t)bytes, ncclUint8, (ncclComm_t)comm, stream);
+  return r == ncclSuccess ? 0 : 1000 + (int)r;
+}
+
 int tmog_hip_rccl_comm_destroy(void* comm) {
   return comm ? (int)ncclCommDestroy((ncclComm_t)comm) : 0;
 }

@@ -1420,16 +1420,18 @@ __global__ void __launch_bounds__(64) split_reduce_kernel(ReduceArgs ra) { reduc
 // Feature-parallel merge: node j's decision is the best of the R ranks' records under the split scan's
 // order (gain, then lowest full-list position, dl, bin) -- the candidate a single rank scanning every
 // feature would pick. Host twin: common/tree_grow.hpp fp_merge_host.
+// m_stride: records per rank in recv (the all-gather's count; >= m); dm (device-planned levels): the real node count
+// is read from device memory, the grid covers the host bound m.
 __global__ void fp_merge_kernel(const uint8_t* __restrict__ recv, int R, int m, int64_t rb, int S,
                                 int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin,
                                 float* __restrict__ out_gain, uint8_t* __restrict__ out_dl,
-                                float* __restrict__ out_left) {
+                                float* __restrict__ out_left, int64_t m_stride, const int* __restrict__ dm) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
+  if (j >= m || (dm != nullptr && j >= *dm)) return;
   int w = -1;
   Best best{-INFINITY, 0x7fffffff, 0, 0};
   for (int r = 0; r < R; ++r) {
-    const uint8_t* p = recv + ((int64_t)r * m + j) * rb;
+    const uint8_t* p = recv + ((int64_t)r * m_stride + j) * rb;
     const int32_t* pi = reinterpret_cast<const int32_t*>(p);
     const Best c{*reinterpret_cast<const double*>(p), pi[2], pi[3], pi[4]};
     if (c.f == 0x7fffffff) continue;
@@ -1446,7 +1448,7 @@ __global__ void fp_merge_kernel(const uint8_t* __restrict__ recv, int R, int m, 
     for (int s = 0; s < S; ++s) out_left[(int64_t)j * S + s] = 0.f;
     return;
   }
-  const uint8_t* p = recv + ((int64_t)w * m + j) * rb;
+  const uint8_t* p = recv + ((int64_t)w * m_stride + j) * rb;
   out_feat[j] = reinterpret_cast<const int32_t*>(p)[5];
   out_bin[j] = best.b;
   out_gain[j] = (float)best.gain;
@@ -2009,7 +2011,18 @@ int tmog_hip_fp_merge(const void* recv, int R, int m, int64_t rec_bytes, int S, 
                       float* out_gain, uint8_t* out_dl, float* out_left, hipStream_t stream) {
   if (m == 0) return 0;
   hipLaunchKernelGGL(fp_merge_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, (const uint8_t*)recv, R, m,
-                     rec_bytes, S, out_feat, out_bin, out_gain, out_dl, out_left);
+                     rec_bytes, S, out_feat, out_bin, out_gain, out_dl, out_left, (int64_t)m, (const int*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// Device-planned levels: recv holds m_stride records per rank (the level's host bound), the merged nodes are the
+// first *dm of them.
+int tmog_hip_fp_merge_dev(const void* recv, int R, int m_stride, int64_t rec_bytes, int S, int32_t* out_feat,
+                          int32_t* out_bin, float* out_gain, uint8_t* out_dl, float* out_left, const int* dm,
+                          hipStream_t stream) {
+  if (m_stride == 0) return 0;
+  hipLaunchKernelGGL(fp_merge_kernel, dim3((m_stride + 255) / 256), dim3(256), 0, stream, (const uint8_t*)recv, R,
+                     m_stride, rec_bytes, S, out_feat, out_bin, out_gain, out_dl, out_left, (int64_t)m_stride, dm);
   return (int)hipGetLastError();
 }
 

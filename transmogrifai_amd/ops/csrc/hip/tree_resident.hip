@@ -64,6 +64,10 @@ int tmog_hip_partition_fused(const uint8_t* Xb, int F, const uint32_t* rows_in, 
                              int wide_rows);
 int tmog_hip_leaf_collect(const uint32_t* rows, const void* items, int n_items, uint32_t* out_rows,
                           int32_t* out_gid, hipStream_t stream, const uint32_t* rows_alt, const int* dcount);
+int tmog_hip_fp_allgather(const void* send, void* recv, int64_t bytes, void* comm, int world, hipStream_t stream);
+int tmog_hip_fp_merge_dev(const void* recv, int R, int m_stride, int64_t rec_bytes, int S, int32_t* out_feat,
+                          int32_t* out_bin, float* out_gain, uint8_t* out_dl, float* out_left, const int* dm,
+                          hipStream_t stream);
 }
 
 // plan / finalisation arithmetic with the host twins' IEEE operation sequence (no FMA contraction)
@@ -791,7 +795,7 @@ struct Buf {
 };
 
 struct ResSlot {
-  Buf arena, hist0, hist1, cand, done, res, consts;
+  Buf arena, hist0, hist1, cand, done, res, consts, fp_send, fp_recv;
   uint8_t* pin = nullptr;      // pinned staging of the per-call constants
   size_t pin_cap = 0;
   hipEvent_t copied = nullptr;
@@ -864,12 +868,14 @@ int64_t hist_bound(const tmog::GrowArgs& a, const tmog::GroupLayout& L, int n_sc
 }
 
 // Configurations the device plan covers (everything else stays on the host-planned grower): one job group,
-// no per-node feature subsets, not feature-parallel, subtraction + fused pair scan, narrow split scan with
-// the fused reduction, statistics in one histogram chunk, leaves collected, Newton (MODE 2) or variance
-// (MODE 1) values. Returns an empty string when supported.
+// no per-node feature subsets, subtraction + fused pair scan, narrow split scan with the fused reduction,
+// statistics in one histogram chunk, leaves collected, Newton (MODE 2) or variance (MODE 1) values.
+// Feature-parallel growth is covered: the level's split records are all-gathered and merged on the stream
+// (RCCL, or the local answer of a projected rank group) between split-find and partition, so a spread job's
+// levels need no host round trip either. Returns an empty string when supported.
 std::string unsupported(const tmog::GrowArgs& a) {
   if (a.n_groups != 1) return "more than one job group";
-  if (a.fp_world > 0) return "feature-parallel";
+  if (a.fp_world > 0 && a.fp_comm == nullptr) return "feature-parallel without a communicator array";
   if (!a.collect_leaves) return "leaves not collected";
   if (!a.subtract) return "no subtraction";
   if (a.mode == 0) return "class-count histograms";
@@ -905,7 +911,7 @@ struct ResidentIO {
 int64_t tmog_hip_resident_cap_nodes(const tmog::GrowArgs* args) {
   const tmog::GrowArgs& a = *args;
   if (!unsupported(a).empty()) return -1;
-  const tmog::GroupLayout L = tmog::group_layout<true>(a, false, false);
+  const tmog::GroupLayout L = tmog::group_layout<true>(a, false, a.fp_world > 0);
   return caps_of(a, L, 1).cap_nodes;
 }
 
@@ -952,7 +958,8 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
       sl = ResSlot();
       sl.device = dev;
     }
-    const tmog::GroupLayout L = tmog::group_layout<true>(a, false, false);
+    const bool fp = a.fp_world > 0;
+    const tmog::GroupLayout L = tmog::group_layout<true>(a, false, fp);
     const int n_sc = 1;
     const Caps cp = caps_of(a, L, n_sc);
     if (io->cap_nodes < cp.cap_nodes) throw std::runtime_error("record buffer too small");
@@ -1073,6 +1080,11 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
     sl.hist1.need(sizeof(int64_t) * (size_t)hsz * cp.cap_m, st);
     sl.cand.need(tmog_hip_split_cand_bytes((int)cp.cap_m, F_use, B, S), st);
     sl.done.need(sizeof(unsigned) * (size_t)cp.cap_m, st);
+    const size_t fp_rb = tmog::fp_rec_bytes(S);
+    if (fp) {                                  // split records of this rank / of every rank of the group
+      sl.fp_send.need(fp_rb * (size_t)cp.cap_m, st);
+      sl.fp_recv.need(fp_rb * (size_t)cp.cap_m * (size_t)a.fp_world, st);
+    }
     if (sl.done_zeroed != sl.done.p) {       // ticket counters start (and are left) at zero
       hchk(hipMemsetAsync(sl.done.p, 0, sl.done.cap, st), "memset done");
       sl.done_zeroed = sl.done.p;
@@ -1169,9 +1181,20 @@ int tmog_hip_grow_resident(const tmog::GrowArgs* args, const ResidentIO* io) {
              "pair_scan");
       kchk(tmog_hip_split_find(hist[c], (int)mb, P.nho[c], P.nnf, P.nfo, flist_d, a.n_bins, B, S, a.kind, P.par[c],
                                a.missing_bin, P.nmd[c], a.qinv, F_use, sl.cand.p, r_feat, r_bin, r_gain, r_dl, r_left,
-                               r_tot, r_cur, L.split_n_multi, nullptr, 0, 0, 0, 0, st, (unsigned*)sl.done.p,
+                               r_tot, r_cur, L.split_n_multi, fp ? sl.fp_send.p : nullptr, fp ? (int64_t)fp_rb : 0,
+                               fp ? a.fp_mlo : 0, fp ? L.fp_nml : 0, fp ? L.fp_obase : 0, st, (unsigned*)sl.done.p,
                                cnt + C_M),
            "split_find");
+      if (fp) {
+        // the ranks' best split per node: all-gather the level's records (the host bound mb of them; the
+        // merge reads the device count) and merge them into this level's decisions, all on the stream
+        kchk(tmog_hip_fp_allgather(sl.fp_send.p, sl.fp_recv.p, (int64_t)(fp_rb * (size_t)mb), a.fp_comm[0],
+                                   a.fp_world, st),
+             "fp_allgather");
+        kchk(tmog_hip_fp_merge_dev(sl.fp_recv.p, a.fp_world, (int)mb, (int64_t)fp_rb, S, r_feat, r_bin, r_gain,
+                                   r_dl, r_left, cnt + C_M, st),
+             "fp_merge");
+      }
       kchk(tmog_hip_partition_fused(a.Xb, a.F, rows[c], rows[c ^ 1], P.citems,
                                     (int)std::min<int64_t>(total / tmog::kPartRows + mb + 1, cp.cap_c), P.nb[c],
                                     P.nc[c], r_feat, r_bin, r_dl, P.par[c], r_gain, a.missing_bin, r_cur, a.XbT, a.N,

@@ -59,6 +59,10 @@ class FeatureParallel:
     def comm_array(self, device: torch.device, n_groups: int):
         from ..ops import _native as N
         lib = N.hip()
+        if D.simulated():
+            # single-GPU projection of this rank's share (scripts/project_schedule.py): no peers to talk to -- the
+            # grower answers the split-record exchange locally (tree_grow_hip.hip tmog_hip_fp_allgather)
+            return (C.c_void_p * max(1, n_groups))(*([None] * max(1, n_groups)))
         dev = device.index if device.index is not None else torch.cuda.current_device()
         handles = []
         members = self.group.ranks if self.group is not None else tuple(range(self.world))
