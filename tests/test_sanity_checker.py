@@ -155,3 +155,133 @@ def test_same_statistics_for_same_inputs():
     np.testing.assert_allclose(fs["mean"], X.mean(0))
     np.testing.assert_allclose(fs["variance"], X.var(0, ddof=1))
     assert not any(math.isnan(v) for v in fs["max"])
+
+
+# ------------------------------------------------------------------- text-map fixture (SanityCheckerTest.scala:77-98)
+TEXT_ROWS = [
+    ("0", 1.0, {"color": "red", "fruit": "berry", "beverage": "tea"}),
+    ("1", 1.0, {"color": "orange", "fruit": "berry", "beverage": "coffee"}),
+    ("2", 1.0, {"color": "yello", "fruit": "berry", "beverage": "water"}),
+    ("3", 1.0, {"color": "green", "fruit": "berry"}),
+    ("4", 1.0, {"color": "blue", "fruit": "berry"}),
+    ("5", 1.0, {"color": "indigo", "fruit": "berry"}),
+    ("6", 0.0, {"fruit": "peach"}),
+    ("7", 0.0, {"fruit": "peach"}),
+    ("8", 0.0, {"fruit": "mango"}),
+    ("9", 0.0, {"beverage": "tea"}),
+    ("10", 0.0, {"beverage": "coffee"}),
+    ("11", 0.0, {"beverage": "water"})]
+
+
+def _text_fixture():
+    ds, (ident, target, tm) = TestFeatureBuilder.of(
+        ("id", T.Text, [r[0] for r in TEXT_ROWS]), ("target", T.RealNN, [r[1] for r in TEXT_ROWS]),
+        ("textMap", T.TextMap, [r[2] for r in TEXT_ROWS]), response="target")
+    return ds, ident, target, tm
+
+
+def _train_summary(ds, vec, checked):
+    from transmogrifai_amd.workflow.workflow import OpWorkflow
+    model = OpWorkflow().set_result_features(vec, checked).set_input_dataset(ds).train()
+    return model.get_origin_stage_of(checked).metadata["summary"]
+
+
+def _validate(summ, names, dropped, nan_corr, ignored=(), feature_feature=None):
+    """``SanityCheckerTest.validateTransformerOutput``."""
+    assert sorted(summ["names"][:-1]) == sorted(names)
+    corr = summ["correlationsWLabel"]
+    assert sorted(n for n, v in zip(corr["featuresIn"], corr["values"]) if v is None or v != v) == sorted(nan_corr)
+    assert sorted(corr["featuresIn"]) == sorted([n for n in names if n not in set(ignored)] + [summ["names"][-1]])
+    assert sorted(summ["dropped"]) == sorted(dropped)
+    if feature_feature is not None:
+        assert bool(summ.get("correlationsWFeatures")) == feature_feature
+
+
+def _smart_map(tm, strategy, num_features):
+    from transmogrifai_amd.stages.feature.maps import SmartTextMapVectorizer
+    return SmartTextMapVectorizer(max_cardinality=2, num_features=num_features, min_support=1, top_k=2,
+                                  prepend_feature_name=True, coverage_pct=1.0,
+                                  hash_space_strategy=strategy).set_input(tm).get_output()
+
+
+SHARED_NAMES = [f"textMap_{i}" for i in range(8)] + ["textMap_color_NullIndicatorValue_8",
+                                                       "textMap_fruit_NullIndicatorValue_9",
+                                                       "textMap_beverage_NullIndicatorValue_10"]
+
+
+def test_removes_individual_text_hash_features_independently():
+    """SanityCheckerTest.scala:359-391: shared hash space; protected shared hashes are judged one by one."""
+    ds, _, target, tm = _text_fixture()
+    vec = _smart_map(tm, "shared", 8)
+    checked = SanityChecker(check_sample=1.0, remove_bad_features=True, remove_feature_group=True,
+                            protect_text_shared_hash=True, min_correlation=0.0, max_correlation=0.8,
+                            max_cramers_v=0.8).set_input(target, vec).get_output()
+    summ = _train_summary(ds, vec, checked)
+    _validate(summ, SHARED_NAMES, ["textMap_4", "textMap_7", "textMap_color_NullIndicatorValue_8"], ["textMap_7"])
+
+
+def test_removes_text_hash_features_as_groups():
+    """SanityCheckerTest.scala:393-434: separate hash spaces per key; a bad key's whole hash group goes."""
+    ds, _, target, tm = _text_fixture()
+    vec = _smart_map(tm, "separate", 4)
+    checked = SanityChecker(check_sample=1.0, remove_bad_features=True, remove_feature_group=True,
+                            protect_text_shared_hash=True, min_correlation=0.0, max_correlation=0.8,
+                            max_cramers_v=0.8).set_input(target, vec).get_output()
+    summ = _train_summary(ds, vec, checked)
+    names = ([f"textMap_color_{i}" for i in range(4)] + [f"textMap_fruit_{i}" for i in range(4, 8)] +
+             [f"textMap_beverage_{i}" for i in range(8, 12)] +
+             ["textMap_color_NullIndicatorValue_12", "textMap_fruit_NullIndicatorValue_13",
+              "textMap_beverage_NullIndicatorValue_14"])
+    dropped = ["textMap_color_0", "textMap_color_1", "textMap_color_2", "textMap_color_3", "textMap_fruit_4",
+               "textMap_fruit_5", "textMap_fruit_6", "textMap_fruit_7", "textMap_beverage_8", "textMap_beverage_9",
+               "textMap_color_NullIndicatorValue_12", "textMap_fruit_NullIndicatorValue_13"]
+    nan = ["textMap_color_1", "textMap_color_2", "textMap_fruit_4", "textMap_beverage_8", "textMap_beverage_9"]
+    _validate(summ, names, dropped, nan)
+
+
+def test_no_correlations_on_hashed_text_smart_map():
+    """SanityCheckerTest.scala:436-471: CorrelationExclusion.HashedText leaves the shared hash columns out of the
+    correlations (and so out of the correlation-based removals)."""
+    ds, _, target, tm = _text_fixture()
+    vec = _smart_map(tm, "shared", 8)
+    checked = SanityChecker(check_sample=1.0, remove_bad_features=True, remove_feature_group=True,
+                            protect_text_shared_hash=True, correlation_exclusion="HashedText", min_correlation=0.0,
+                            max_correlation=0.8, max_feature_correlation=1.0, max_cramers_v=0.8).set_input(
+        target, vec).get_output()
+    summ = _train_summary(ds, vec, checked)
+    _validate(summ, SHARED_NAMES, ["textMap_7", "textMap_color_NullIndicatorValue_8"], [],
+              ignored=[f"textMap_{i}" for i in range(8)])
+
+
+def test_no_correlations_on_hashed_text_vectorizer():
+    """SanityCheckerTest.scala:502-533: the same exclusion through ``textMap.vectorize`` (512 shared hashes + per-key
+    null indicators, keys sorted)."""
+    ds, _, target, tm = _text_fixture()
+    vec = tm.vectorize(clean_text=True)
+    checked = SanityChecker(check_sample=1.0, remove_bad_features=True, remove_feature_group=True,
+                            protect_text_shared_hash=True, correlation_exclusion="HashedText", min_variance=-0.1,
+                            min_correlation=0.0, max_correlation=0.8, max_feature_correlation=1.0,
+                            max_cramers_v=0.8).set_input(target, vec).get_output()
+    summ = _train_summary(ds, vec, checked)
+    hashed = [f"textMap_{i}" for i in range(512)]
+    names = hashed + ["textMap_beverage_NullIndicatorValue_512", "textMap_color_NullIndicatorValue_513",
+                      "textMap_fruit_NullIndicatorValue_514"]
+    _validate(summ, names, ["textMap_color_NullIndicatorValue_513"], [], ignored=hashed)
+
+
+def test_maps_with_the_same_keys():
+    """SanityCheckerTest.scala:617-633: two pick-list maps with the same keys and a real map: nothing dropped, one
+    categorical group per (map, key) pivot, 2 labels in every contingency matrix."""
+    from transmogrifai_amd.dsl import transmogrify
+    rng = np.random.default_rng(0)
+    ds, (ident, target, m1, m2, dm) = TestFeatureBuilder.of(
+        ("id", T.Text, [r[0] for r in TEXT_ROWS]), ("target", T.RealNN, [r[1] for r in TEXT_ROWS]),
+        ("textMap1", T.PickListMap, [r[2] for r in TEXT_ROWS]), ("textMap2", T.PickListMap, [r[2] for r in TEXT_ROWS]),
+        ("doubleMap", T.RealMap, [{k: float(rng.random()) for k in r[2]} for r in TEXT_ROWS]))
+    feats = transmogrify([ident, target, m1, m2, dm])          # the target also as a predictor, as the reference
+    checked = target.as_response().sanity_check(feats, categorical_label=True)
+    summ = _train_summary(ds, feats, checked)
+    assert summ["dropped"] == []
+    cats = summ["categoricalStats"]
+    assert len(cats) == 10
+    assert all(len((c.get("contingencyMatrix") or c["contingency"])["0"]) == 2 for c in cats)

@@ -554,6 +554,15 @@ def map_vectorize(t, feats, label, D, **overrides) -> list:
         if k not in _MAP_ARGS:
             raise TypeError(f"map vectorize got an unexpected argument {k!r}")
         params[_MAP_ARGS[k]] = v
+    if kind == "smarttext":         # RichTextMapFeature.smartVectorize (Transmogrifier.scala:214-232)
+        keep = ("clean_keys", "clean_text", "track_nulls", "top_k", "min_support", "max_cardinality", "num_features",
+                "allow_keys", "block_keys")
+        sp = {k: v for k, v in params.items() if k in keep}
+        sp.update(track_text_len=bool(getattr(D, "TrackTextLen", False)),
+                  hash_space_strategy=getattr(D, "HashSpaceStrategy", "auto"),
+                  prepend_feature_name=bool(getattr(D, "PrependFeatureName", True)),
+                  min_length_std_dev=float(getattr(D, "MinLengthStdDev", 0.0)))
+        return [SmartTextMapVectorizer(**sp).set_input(feats).get_output()]
     cls = {"pivot": TextMapPivotVectorizer, "binary": BinaryMapVectorizer}.get(kind, MapVectorizer)
     st = cls(**params) if kind in ("pivot", "binary") and t is not T.OPMap else MapVectorizer(**params)
     return [st.set_input(feats).get_output()]
@@ -571,7 +580,182 @@ IntegralMapVectorizer = _named("IntegralMapVectorizer", "vecIntMap", "integral")
 BinaryMapVectorizer = _named("BinaryMapVectorizer", "vecBinMap", "binary")
 DateMapVectorizer = _named("DateMapVectorizer", "vecDateMap", "date")
 TextMapPivotVectorizer = _named("TextMapPivotVectorizer", "vecPivotTextMap", "pivot")
-SmartTextMapVectorizer = _named("SmartTextMapVectorizer", "smartTxtMapVec", "smarttext")
+
+
+def _first_keys(coo: "MapCOO") -> List[str]:
+    """The map column's keys holding a value, in order of first appearance (row order, then key order)."""
+    if not coo.nnz:
+        return []
+    k = coo.key.cpu().numpy()
+    _, first = np.unique(k, return_index=True)
+    return [coo.keys[int(k[i])] for i in np.sort(first)]
+
+
+@register_stage
+class SmartTextMapVectorizerModel(VectorizerMixin, SequenceTransformer):
+    """Transform of :class:`SmartTextMapVectorizer` (``SmartTextMapVectorizerModel``, SmartTextMapVectorizer.scala:
+    327-420): ``[categorical pivots | hashed text | text lengths | text null indicators]``."""
+    operation_name = "smartTxtMapVec"
+
+    def __init__(self, keys=None, methods=None, tops=None, clean_keys=False, clean_text=True, track_nulls=True,
+                 track_text_len=False, hashing=None, uid=None, **kw):
+        from .vectorizers import HashingParams
+        super().__init__(uid=uid, **kw)
+        self.keys = [list(k) for k in (keys or [])]
+        self.methods = [list(m) for m in (methods or [])]
+        self.tops = [[list(t) for t in tt] for tt in (tops or [])]
+        self.clean_keys, self.clean_text = clean_keys, clean_text
+        self.track_nulls, self.track_text_len = track_nulls, track_text_len
+        self.hashing = hashing if isinstance(hashing, HashingParams) else HashingParams(**(hashing or {}))
+
+    def transform_columns(self, *cols, ds=None):
+        from ...ops.text import HashInput
+        from .vectorizers import _vocab_lut, hash_text_columns
+        dev = default_device()
+        dtype = vector_dtype(dev)
+        n = len(cols[0]) if cols else 0
+        kcols = []
+        for i, c in enumerate(cols):
+            coo = map_coo(c, "pivot", self.clean_keys, dev)
+            kcols.append((coo, _per_key_text_columns(coo, self.keys[i])))
+        piv = [(i, j) for i in range(len(cols)) for j, m in enumerate(self.methods[i]) if m == "pivot"]
+        hsh = [(i, j) for i in range(len(cols)) for j, m in enumerate(self.methods[i]) if m == "hash"]
+        text = [(i, j) for i in range(len(cols)) for j, m in enumerate(self.methods[i]) if m in ("hash", "ignore")]
+        toks = {}
+        for i, _ in text:
+            if i not in toks:
+                voc = kcols[i][0].vocab
+                toks[i] = TU.tokenize_batch(voc) if voc else TU.TokenBatch.from_lists([])
+        blocks = []
+        if piv:
+            blocks.append(pivot_columns([kcols[i][1][j] for i, j in piv], [self.tops[i][j] for i, j in piv],
+                                        self.clean_text, self.track_nulls, dtype))
+        if hsh:
+            hp = self.hashing
+            ins = [HashInput(kcols[i][1][j].codes, toks[i], int(TU.hash_terms([self.keys[i][j]], hp.num_features)[0])
+                             if hp.prepend_feature_name else None) for i, j in hsh]
+            shared = hp.shared(len(hsh))
+            from .vectorizers import HashingParams
+            hp2 = HashingParams(hp.num_features, len(hsh), hp.max_num_features, hp.binary, hp.prepend_feature_name,
+                                "shared" if shared else "separate", hp.hash_with_index)
+            blocks.append(hash_text_columns([kcols[i][1][j] for i, j in hsh], None, hp2, None, dtype, inputs=ins))
+        if text and self.track_text_len:
+            blocks.append(torch.stack([_vocab_lut(kcols[i][1][j], toks[i].char_lengths().astype(np.float64), 0.0,
+                                                  dtype) for i, j in text], 1))
+        if text and self.track_nulls:
+            blocks.append(torch.stack([_vocab_lut(kcols[i][1][j], (toks[i].counts() == 0).astype(np.float64), 1.0,
+                                                  dtype) for i, j in text], 1))
+        out = torch.cat(blocks, 1) if blocks else torch.zeros(n, 0, dtype=dtype, device=dev)
+        return self._vec(out)
+
+    def ctor_args(self):
+        return {"keys": self.keys, "methods": self.methods, "tops": self.tops, "cleanKeys": self.clean_keys,
+                "cleanText": self.clean_text, "trackNulls": self.track_nulls, "trackTextLen": self.track_text_len,
+                "hashingParams": self.hashing.to_json()}
+
+    def load_ctor_args(self, a):
+        from .vectorizers import HashingParams
+        self.keys = [list(k) for k in a["keys"]]
+        self.methods = [list(m) for m in a["methods"]]
+        self.tops = [[list(t) for t in tt] for tt in a["tops"]]
+        self.clean_keys, self.clean_text = a["cleanKeys"], a["cleanText"]
+        self.track_nulls, self.track_text_len = a["trackNulls"], a.get("trackTextLen", False)
+        self.hashing = HashingParams.from_json(a["hashingParams"])
+
+
+@register_stage
+class SmartTextMapVectorizer(VectorizerMixin, SequenceEstimator):
+    """``SmartTextMapVectorizer`` (SmartTextMapVectorizer.scala:58-270): every key of every text map is a text
+    feature of its own, vectorized by the SmartTextVectorizer rule -- pivoted when its cardinality is at most
+    ``max_cardinality`` (or its top-K values with min support cover ``coverage_pct`` of it), ignored when its
+    length spread is below ``min_length_std_dev``, hashed otherwise (all hashed keys in one space of
+    ``num_features`` columns, or one space each: ``hash_space_strategy``, keys' names prepended to their
+    tokens). Keys come in order of first appearance. Output layout: categorical pivots, hashed columns, text
+    lengths (``track_text_len``), null indicators of the hashed / ignored keys."""
+    operation_name = "smartTxtMapVec"
+    _defaults = {"max_cardinality": 30, "top_k": 20, "min_support": 10, "clean_text": True, "clean_keys": False,
+                 "track_nulls": True, "track_text_len": False, "num_features": 512, "hash_space_strategy": "auto",
+                 "prepend_feature_name": True, "binary_freq": False, "coverage_pct": 1.0,
+                 "min_length_std_dev": 0.0, "allow_keys": None, "block_keys": None,
+                 "max_pct_cardinality": 1.0, "unseen_name": OTHER_STRING}
+    dp_aware = True
+
+    def fit_columns(self, *cols, ds=None):
+        from ...parallel import dp
+        from .vectorizers import HashingParams, TextStats, hash_metadata  # noqa: F401
+        p = self.params
+        dev = default_device()
+        max_card = int(p["max_cardinality"])
+        allow = set(p["allow_keys"]) if p["allow_keys"] else None
+        block = set(p["block_keys"] or ())
+        local = []
+        for c in cols:
+            coo = map_coo(c, "pivot", p["clean_keys"], dev)
+            keys = [k for k in _first_keys(coo) if (allow is None or k in allow) and k not in block]
+            kc = _per_key_text_columns(coo, keys)
+            local.append([(k, TextStats.of_column(col, p["clean_text"], False, max_card)) for k, col in zip(keys, kc)])
+        merged: List[Dict[str, "TextStats"]] = [dict() for _ in cols]
+        for part in dp.objects(local):                    # ranks in order: first appearance across the ranks
+            for i, kv in enumerate(part):
+                for k, st in kv:
+                    merged[i][k] = merged[i][k].plus(st, max_card) if k in merged[i] else st
+        keys, methods, tops = [], [], []
+        for i in range(len(cols)):
+            ks, ms, ts = [], [], []
+            for k, st in merged[i].items():
+                vc = st.value_counts
+                total = sum(vc.values())
+                filt = {v: m for v, m in vc.items() if m >= p["min_support"]}
+                sv = sorted(filt.values(), reverse=True)
+                cum = np.cumsum(sv) if sv else np.zeros(0)
+                kk = min(p["top_k"], cum.size)
+                coverage = (cum[kk - 1] / total) if (kk > 0 and total > 0) else 0.0
+                card = len(vc)
+                if card > max_card and card > p["top_k"] and coverage >= p["coverage_pct"]:
+                    m = "pivot"
+                elif card <= max_card:
+                    m = "pivot"
+                elif st.length_std < p["min_length_std_dev"]:
+                    m = "ignore"
+                else:
+                    m = "hash"
+                ks.append(k)
+                ms.append(m)
+                ts.append(top_values(Counter(filt), p["top_k"], 0) if m == "pivot" else [])
+            keys.append(ks)
+            methods.append(ms)
+            tops.append(ts)
+        tfs = self.get_transient_features()
+        hp = HashingParams(p["num_features"], len(cols), 1 << 17, p["binary_freq"], p["prepend_feature_name"],
+                           p["hash_space_strategy"])
+        colsm = []
+        for i, t in enumerate(tfs):                       # categorical keys
+            for k, m, top in zip(keys[i], methods[i], tops[i]):
+                if m != "pivot":
+                    continue
+                vals = list(top) + [p["unseen_name"]] + ([NULL_STRING] if p["track_nulls"] else [])
+                colsm += [OpVectorColumnMetadata((t.name,), (t.type_name,), k, v) for v in vals]
+        n_hash = sum(m == "hash" for ms in methods for m in ms)
+        if n_hash:                                        # hashed keys (MapHashingFun.makeVectorColumnMetadata)
+            if hp.shared(n_hash):
+                hf = [t for i, t in enumerate(tfs) if "hash" in methods[i]]
+                colsm += [OpVectorColumnMetadata(tuple(t.name for t in hf), tuple(t.type_name for t in hf), None, None)
+                          for _ in range(p["num_features"])]
+            else:
+                for i, t in enumerate(tfs):
+                    for k, m in zip(keys[i], methods[i]):
+                        if m == "hash":
+                            colsm += [OpVectorColumnMetadata((t.name,), (t.type_name,), k, None)
+                                      for _ in range(p["num_features"])]
+        text = [(t, k) for i, t in enumerate(tfs) for k, m in zip(keys[i], methods[i]) if m in ("hash", "ignore")]
+        if p["track_text_len"]:
+            colsm += [OpVectorColumnMetadata((t.name,), (t.type_name,), k, None, "TextLen") for t, k in text]
+        if p["track_nulls"]:
+            colsm += [OpVectorColumnMetadata((t.name,), (t.type_name,), k, NULL_STRING) for t, k in text]
+        self.metadata["vector_metadata"] = self.vector_metadata(colsm)
+        return SmartTextMapVectorizerModel(keys, methods, tops, p["clean_keys"], p["clean_text"], p["track_nulls"],
+                                           p["track_text_len"], hp)
+
 MultiPickListMapVectorizer = _named("MultiPickListMapVectorizer", "vecCatMap", "set")
 GeolocationMapVectorizer = _named("GeolocationMapVectorizer", "vecGeoMap", "geo")
 

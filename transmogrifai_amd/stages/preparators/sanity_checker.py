@@ -150,7 +150,9 @@ class SanityChecker(BinaryEstimator):
             v = float(value)
             if not ((v >= lo if lo_incl else v > lo) and v <= hi):
                 raise ValueError(f"SanityChecker param {name} = {value} outside {'[' if lo_incl else '('}{lo}, {hi}]")
-        if name in ("sample_lower_limit", "sample_upper_limit", "min_variance") and float(value) < 0:
+        # (minVariance has no validator in the reference -- DerivedFeatureFilterUtils.scala:65-70 -- and its tests set
+        # it below zero to keep every column)
+        if name in ("sample_lower_limit", "sample_upper_limit") and float(value) < 0:
             raise ValueError(f"SanityChecker param {name} must be >= 0, got {value}")
         return super().set(name, value)
 
