@@ -98,6 +98,8 @@ _HIP_SIGS = {
     "tmog_hip_poisson_pack": [P, I64, P, I32, P, I32, P, P, P, P],
     "tmog_hip_row_uniform": [P, I64, P, I32, P, P],
     "tmog_hip_lr_objective": [P, I64, I32, P, P, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P],
+    "tmog_hip_lr_objective_mixed": [P, I64, I32, P, I32, I32, P, P, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32,
+                                    P],
     "tmog_hip_lr_epilogue_grad": [P, I64, I32, P, P, P, I32, I32, I32, P, I32, P, I32, P, P, P, I32, P],
     "tmog_hip_forest_predict": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P],
     "tmog_hip_forest_predict_multi": [P, I32, I32, P, P, I64, P, P, P, P, P, I32, P, I32, P, P, P, P, P, P],

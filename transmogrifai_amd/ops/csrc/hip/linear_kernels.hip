@@ -60,12 +60,19 @@ __device__ __forceinline__ int kcol(int s, int q) { return 64 * (s >> 4) + (s & 
 // GB = phase-B output blocks per wave, NPF = prefetch float4 slots per thread, TT = rows per tile (64: one
 // 512-thread workgroup per CU; 32: 256-thread workgroups, two per CU -- two tiles' loads in flight per CU).
 // Waves: TT / 16 row blocks x 2 problem halves; phase-B output blocks ob = wave + NW i.
-template <bool GRAD, int GB, int NPF, int DM, int TT>
+// MIX (lossless mixed storage, ops/linear.py MixedDesign): a row of X is cpr 16-byte chunks -- nce chunks of 8 bf16
+// values (the columns whose values are all exact in bf16: one-hot, null indicators, small counts) then chunks of 4
+// fp32 values (every other column). colmap[slot] is the original column of each value slot of a row (-1: padding).
+// The landing step widens the bf16 values (exactly) and scatters every value to its original column of the fp32
+// LDS tile, so the tile -- and everything computed from it -- is bit-identical to the plain fp32 pass, while HBM
+// delivers 2 bytes instead of 4 for the exact columns.
+template <bool GRAD, int GB, int NPF, int DM, int TT, bool MIX>
 __global__ void __launch_bounds__(8 * TT) lr_objective_kernel(
     const float* __restrict__ X, int64_t N, int d, const float* __restrict__ y,
     const float* __restrict__ W, int ldw, int wcol0, int P, const float* __restrict__ V,
     const float* __restrict__ bias, int loss, const float* __restrict__ yscale, double* __restrict__ f_part,
-    double* __restrict__ r_part, float* __restrict__ G_part, int dpad) {
+    double* __restrict__ r_part, float* __restrict__ G_part, int dpad, const int32_t* __restrict__ colmap, int cpr,
+    int nce) {
   constexpr int RB = TT / 16;               // row blocks (waves per problem half)
   constexpr int NW = 2 * RB;                // waves per workgroup
   constexpr int NTT = 64 * NW;              // threads per workgroup
@@ -76,6 +83,9 @@ __global__ void __launch_bounds__(8 * TT) lr_objective_kernel(
   float* Xs = lds;                          // [TT][d] + 64 words of overrun (finite, times V = 0)
   float* Vs = Xs + xs_words;                // [64][VS]: V rows of the ragged last 64-column block, zero beyond d
   float* Rs = Vs + 64 * VS;                 // [TT][PC]
+  int* cm = reinterpret_cast<int*>(Rs + TT * PC);   // MIX: the row's slot -> column map
+  const int n_slots = MIX ? 8 * nce + 4 * (cpr - nce) : 0;
+  const int tile_chunks = MIX ? TT * cpr : 0;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: SGPR, scalar branches
   const int q = lane >> 4, c = lane & 15;
@@ -84,6 +94,8 @@ __global__ void __launch_bounds__(8 * TT) lr_objective_kernel(
   const int nb64 = d >> 6;
 
   for (int i = threadIdx.x; i < xs_words; i += NTT) Xs[i] = 0.f;
+  if (MIX)
+    for (int i = threadIdx.x; i < n_slots; i += NTT) cm[i] = colmap[i];
   for (int i = threadIdx.x; i < 64 * VS; i += NTT) {
     const int k = 64 * nb64 + i / VS, j = i % VS;
     Vs[i] = (k < d && j < PC) ? V[(int64_t)k * PC + j] : 0.f;
@@ -118,6 +130,13 @@ __global__ void __launch_bounds__(8 * TT) lr_objective_kernel(
   int nval4 = 0, ntail = 0;
   auto prefetch = [&](int64_t tile) {
     const int64_t r0 = tile * TT;
+    if constexpr (MIX) {
+      nval4 = (int)(min((int64_t)TT, N - r0) * cpr);      // rows are whole 16-byte chunks: no ragged tail
+      ntail = 0;
+      const f32x4* src = reinterpret_cast<const f32x4*>(reinterpret_cast<const uint8_t*>(X) + r0 * (int64_t)cpr * 16);
+#pragma unroll
+      for (int i = 0; i < NPF; ++i) pf[i] = src[min((int)threadIdx.x + NTT * i, max(nval4 - 1, 0))];
+    } else {
     const int nval = (int)(min((int64_t)TT, N - r0) * d);
     nval4 = nval >> 2;
     ntail = nval & 3;
@@ -127,6 +146,7 @@ __global__ void __launch_bounds__(8 * TT) lr_objective_kernel(
     const float* xt = X + r0 * (int64_t)d;   // every lane reads the same <= 3 words (clamped into the tile)
 #pragma unroll
     for (int k = 0; k < 3; ++k) pt[k] = k < ntail ? xt[min(4 * nval4 + k, nval - 1)] : 0.f;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t gr = min(r0 + 16 * rb + 4 * q + j, N - 1);
@@ -142,12 +162,42 @@ __global__ void __launch_bounds__(8 * TT) lr_objective_kernel(
     const int64_t r0 = tile * TT;
     const int nrows = (int)min((int64_t)TT, N - r0);
     // ---- land the prefetched tile in LDS, then start fetching the next one
+    if constexpr (MIX) {
+#pragma unroll
+      for (int i = 0; i < NPF; ++i) {
+        const int e4 = threadIdx.x + NTT * i;
+        if (e4 < tile_chunks) {
+          const int row = e4 / cpr, off = e4 - row * cpr;
+          const bool live = e4 < nval4;           // rows past N: zeros (finite, and their R is 0)
+          float* xr = Xs + row * d;
+          if (off < nce) {                        // 8 bf16: widened exactly (bf16 = the high half of an fp32)
+            const uint32_t* u = reinterpret_cast<const uint32_t*>(&pf[i]);
+            const int* m = cm + 8 * off;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const uint32_t w = u[k >> 1];
+              const uint32_t bits = (k & 1) ? (w & 0xFFFF0000u) : (w << 16);
+              const int col = m[k];
+              if (col >= 0) xr[col] = live ? __uint_as_float(bits) : 0.f;
+            }
+          } else {                                // 4 fp32
+            const int* m = cm + 8 * nce + 4 * (off - nce);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int col = m[k];
+              if (col >= 0) xr[col] = live ? pf[i][k] : 0.f;
+            }
+          }
+        }
+      }
+    } else {
     f32x4* xs4 = reinterpret_cast<f32x4*>(Xs);
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
       const int e4 = threadIdx.x + NTT * i;
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       if (e4 < tile_f4) xs4[e4] = e4 < nval4 ? pf[i] : (e4 == nval4 && ntail ? pt : z);
+    }
     }
     float cw[4], cy[4];
 #pragma unroll
@@ -528,23 +578,35 @@ static int lr_tile(bool grad) {
 // Workgroups per CU of a tmog_hip_lr_objective pass (ops/linear.py sizes its persistent grid with it).
 int tmog_hip_lr_blocks_per_cu(int grad) { return lr_tile(grad != 0) == 32 ? 2 : 1; }
 
-int tmog_hip_lr_objective(const float* X, int64_t N, int d, const float* y, const float* W, int ldw, int wcol0,
-                          int P, const float* V, const float* bias, int loss, const float* yscale, int grad,
-                          double* f_part, double* r_part, float* G_part, int nblk, hipStream_t stream) {
+static int lr_objective_launch(const float* X, int64_t N, int d, const float* y, const float* W, int ldw, int wcol0,
+                               int P, const float* V, const float* bias, int loss, const float* yscale, int grad,
+                               double* f_part, double* r_part, float* G_part, int nblk, hipStream_t stream,
+                               const int32_t* colmap, int cpr, int nce) {
   if (d > DMAX || d < 1 || P > PC || P < 1 || nblk < 1) return -2;
   if ((reinterpret_cast<uintptr_t>(X) & 15) != 0) return -3;
+  const bool mix = colmap != nullptr;
+  const int dm = d <= 128 ? 128 : d <= 256 ? 256 : 384;
+  // a mixed row must fit the prefetch slots sized for the fp32 row (NPF * NTT >= TT * cpr): cpr <= DM / 4
+  if (mix && (cpr < 1 || nce < 0 || nce > cpr || 4 * cpr > dm)) return -4;
   const int dpad = ((d + 15) / 16) * 16;
   const int tt = lr_tile(grad != 0);
-  const size_t lds = (size_t)(((tt * d + 64 + 3) & ~3) + 64 * VS + tt * PC) * sizeof(float);
+  const int n_slots = mix ? 8 * nce + 4 * (cpr - nce) : 0;
+  const size_t lds = (size_t)(((tt * d + 64 + 3) & ~3) + 64 * VS + tt * PC) * sizeof(float) + sizeof(int) * n_slots;
 #define TM_LR(G, DM, T_)                                                                                          \
-  hipLaunchKernelGGL((lr_objective_kernel<G, (DM / 8 + T_ / 8 - 1) / (T_ / 8), (T_ * DM / 4 + 8 * T_ - 1) / (8 * T_), \
-                                          DM, T_>),                                                               \
-                     dim3(nblk), dim3(8 * T_), lds, stream, X, N, d, y, W, ldw, wcol0, P, V, bias, loss, yscale,     \
-                     f_part, r_part, G_part, dpad)
+  if (mix)                                                                                                        \
+    hipLaunchKernelGGL((lr_objective_kernel<G, (DM / 8 + T_ / 8 - 1) / (T_ / 8), (T_ * DM / 4 + 8 * T_ - 1) / (8 * T_), \
+                                            DM, T_, true>),                                                       \
+                       dim3(nblk), dim3(8 * T_), lds, stream, X, N, d, y, W, ldw, wcol0, P, V, bias, loss, yscale,   \
+                       f_part, r_part, G_part, dpad, colmap, cpr, nce);                                           \
+  else                                                                                                            \
+    hipLaunchKernelGGL((lr_objective_kernel<G, (DM / 8 + T_ / 8 - 1) / (T_ / 8), (T_ * DM / 4 + 8 * T_ - 1) / (8 * T_), \
+                                            DM, T_, false>),                                                      \
+                       dim3(nblk), dim3(8 * T_), lds, stream, X, N, d, y, W, ldw, wcol0, P, V, bias, loss, yscale,   \
+                       f_part, r_part, G_part, dpad, (const int32_t*)nullptr, 0, 0)
 #define TM_LR_D(G, T_)                \
-  if (d <= 128) TM_LR(G, 128, T_);    \
-  else if (d <= 256) TM_LR(G, 256, T_); \
-  else TM_LR(G, 384, T_);
+  if (d <= 128) { TM_LR(G, 128, T_); } \
+  else if (d <= 256) { TM_LR(G, 256, T_); } \
+  else { TM_LR(G, 384, T_); }
   if (grad) {
     if (tt == 32) { TM_LR_D(true, 32) } else { TM_LR_D(true, 64) }
   } else {
@@ -553,6 +615,25 @@ int tmog_hip_lr_objective(const float* X, int64_t N, int d, const float* y, cons
 #undef TM_LR_D
 #undef TM_LR
   return (int)hipGetLastError();
+}
+
+int tmog_hip_lr_objective(const float* X, int64_t N, int d, const float* y, const float* W, int ldw, int wcol0,
+                          int P, const float* V, const float* bias, int loss, const float* yscale, int grad,
+                          double* f_part, double* r_part, float* G_part, int nblk, hipStream_t stream) {
+  return lr_objective_launch(X, N, d, y, W, ldw, wcol0, P, V, bias, loss, yscale, grad, f_part, r_part, G_part, nblk,
+                             stream, nullptr, 0, 0);
+}
+
+// The same pass over the lossless mixed-storage copy of X (Xm: N rows of cpr 16-byte chunks, nce of them bf16;
+// colmap: [8 nce + 4 (cpr - nce)] original column per value slot, -1 = padding). Bit-identical to
+// tmog_hip_lr_objective on the fp32 X. Returns -4 when the mixed row does not fit the pass's prefetch slots.
+int tmog_hip_lr_objective_mixed(const void* Xm, int64_t N, int d, const int32_t* colmap, int cpr, int nce,
+                                const float* y, const float* W, int ldw, int wcol0, int P, const float* V,
+                                const float* bias, int loss, const float* yscale, int grad, double* f_part,
+                                double* r_part, float* G_part, int nblk, hipStream_t stream) {
+  if (colmap == nullptr) return -2;
+  return lr_objective_launch((const float*)Xm, N, d, y, W, ldw, wcol0, P, V, bias, loss, yscale, grad, f_part, r_part,
+                             G_part, nblk, stream, colmap, cpr, nce);
 }
 
 // OWL-QN direction (see owlqn_direction_kernel); all arrays fp64, [d1][P] / [m][d1][P] / [m][P] row-major.

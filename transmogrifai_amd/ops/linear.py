@@ -237,7 +237,14 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
         if yscale is not None:
             ys = torch.ones(_LR_PC, dtype=torch.float32, device=dev)
             ys[:pc] = yscale[c0:c0 + pc]
-        if d <= _LR_DMAX:
+        md = MixedDesign.of(X, grad) if d <= _LR_DMAX else None
+        if md is not None:
+            # lossless mixed storage: bf16 for the bf16-exact columns, fp32 for the others; bit-identical pass
+            N_.check(N_.hip().tmog_hip_lr_objective_mixed(
+                N_.ptr(md.Xm), N, d, N_.ptr(md.colmap), md.cpr, md.nce, N_.ptr(yf), N_.ptr(Wf), P, c0, pc,
+                N_.ptr(Vc), N_.ptr(bc), LOSS_CODES[loss], N_.ptr(ys), int(grad), N_.ptr(fp), N_.ptr(rp),
+                N_.ptr(gp) if grad else None, nblk, N_.stream(dev)), "lr_objective_mixed")
+        elif d <= _LR_DMAX:
             N_.check(N_.hip().tmog_hip_lr_objective(
                 N_.ptr(X), N, d, N_.ptr(yf), N_.ptr(Wf), P, c0, pc, N_.ptr(Vc), N_.ptr(bc), LOSS_CODES[loss],
                 N_.ptr(ys), int(grad), N_.ptr(fp), N_.ptr(rp), N_.ptr(gp) if grad else None, nblk, N_.stream(dev)),
@@ -258,6 +265,62 @@ def fused_objective(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, V: torch.
         if grad:
             G[:, c0:c0 + pc] = gp[:, :d, :pc].sum(0, dtype=torch.float64)
     return f, r, G
+
+
+class MixedDesign:
+    """Lossless mixed-storage copy of an fp32 device design matrix for the fp32 objective pass
+    (``linear_kernels.hip`` ``tmog_hip_lr_objective_mixed``): each row is the columns whose values are all exact in
+    bf16 (one-hot, null indicators, small counts -- most of a transmogrified matrix; ``stats.bf16_exact_columns``)
+    stored as bf16, then the other columns as fp32, in 16-byte chunks. The kernel widens the bf16 values (exactly)
+    and scatters every value back to its own column of the fp32 LDS tile, so the pass -- margins, losses,
+    gradients -- is bit-identical to the plain fp32 pass while HBM moves 2 instead of 4 bytes per exact value.
+
+    ``colmap`` ``int32 [8 nce + 4 (cpr - nce)]``: original column of every value slot of a row (-1 = padding)."""
+
+    def __init__(self, X: torch.Tensor, E: torch.Tensor, R: torch.Tensor):
+        dev = X.device
+        N = int(X.shape[0])
+        nE, nR = int(E.numel()), int(R.numel())
+        dE, dR = (nE + 7) // 8 * 8, (nR + 3) // 4 * 4
+        self.nce = dE // 8
+        self.cpr = self.nce + dR // 4
+        rb = 16 * self.cpr
+        Xm = torch.zeros(N, rb, dtype=torch.uint8, device=dev)
+        if nE:
+            Xm[:, :2 * dE].view(torch.bfloat16)[:, :nE] = X.index_select(1, E).to(torch.bfloat16)
+        if nR:
+            Xm[:, 2 * dE:].view(torch.float32)[:, :nR] = X.index_select(1, R)
+        self.Xm = Xm
+        pad = lambda t, n: torch.cat([t.to(torch.int32), torch.full((n - int(t.numel()),), -1, dtype=torch.int32,
+                                                                      device=dev)])
+        self.colmap = torch.cat([pad(E, dE), pad(R, dR)]).contiguous()
+        self.nE, self.nR = nE, nR
+
+    @staticmethod
+    def of(X: torch.Tensor, grad: bool = False) -> Optional["MixedDesign"]:
+        """The mixed copy of ``X`` (made once per tensor, shared by every pass), or None when it does not pay or
+        fit: fp32 ``linear_dtype`` only, ``TMOG_LR_MIXED=0`` disables, gradient passes keep plain fp32 unless
+        ``TMOG_LR_MIXED=2`` (they are bound by the fp32 MFMA phase, not by HBM)."""
+        from .. import config as _cfg
+        mode = os.environ.get("TMOG_LR_MIXED", "1")
+        if mode == "0" or (grad and mode != "2") or _cfg.linear_dtype() != "fp32":
+            return None
+        if not (isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.float32 and X.dim() == 2
+                and X.is_contiguous() and 1 <= X.shape[1] <= _LR_DMAX and X.shape[0] >= 32):
+            return None
+        D = getattr(X, "_tmog_mixed", None)
+        if D is not None and D[0] == X._version:
+            return D[1]
+        from . import stats as ST
+        exact = ST.bf16_exact_columns(X)
+        E = torch.nonzero(exact).reshape(-1)
+        R = torch.nonzero(~exact).reshape(-1)
+        d = int(X.shape[1])
+        dm = 128 if d <= 128 else 256 if d <= 256 else 384
+        cpr = (int(E.numel()) + 7) // 8 + (int(R.numel()) + 3) // 4
+        md = MixedDesign(X, E, R) if (int(E.numel()) >= 16 and 16 * cpr < 4 * d and 4 * cpr <= dm) else None
+        X._tmog_mixed = (X._version, md)
+        return md
 
 
 _BF16_DMAX = 384        # linear_bf16_kernels.hip: 12 feature blocks of 32 resident in the accumulators
