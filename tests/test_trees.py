@@ -1,0 +1,15 @@
+
+
+def test_budget_chunks_split_a_batch_that_does_not_fit(monkeypatch):
+    """Boosting batches are sized from a device-memory budget up front (models/trees.py _budget_chunks): with a
+    budget of 2.5 jobs, 5 jobs run as 3 consecutive chunks; everything fits -> one chunk; CPU -> one chunk."""
+    import torch
+    from transmogrifai_amd.models import trees as TR
+    dev = torch.device("cuda")
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda d=None: (250, 1000))
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda d=None: 0)
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda d=None: 0)
+    assert TR._budget_chunks([100] * 5, dev, frac=1.0) == [(0, 2), (2, 4), (4, 5)]
+    assert TR._budget_chunks([10] * 5, dev, frac=1.0) == [(0, 5)]
+    assert TR._budget_chunks([400, 10], dev, frac=1.0) == [(0, 1), (1, 2)]
+    assert TR._budget_chunks([100] * 5, torch.device("cpu")) == [(0, 5)]

@@ -17,6 +17,7 @@ learners advance all their models one round per engine call.
 from __future__ import annotations
 
 import json
+import logging
 import math
 import os
 import threading
@@ -33,6 +34,8 @@ from .binning import BinSpec, find_splits, quantize
 from ..stages.base import register_stage
 from ..ops.staging import to_device
 from ..tuning.splitters import row_uniform, row_uniform_multi
+
+log = logging.getLogger(__name__)
 
 
 # --------------------------------------------------------------------------------------- context
@@ -470,6 +473,40 @@ class DecisionTreeRegressorLearner(_ForestLearner):
 
 
 # -------------------------------------------------------------------------------- boosting
+def _boost_job_bytes(job, n_rows: int) -> int:
+    """Device bytes one boosting job holds while its batch runs: its margin row (fp64) and (g, h) rows (fp32) over
+    the batch's rows, and per training entry the grower's ping-pong entries and staged (g, h), the leaf assignment
+    and the root packing (~40 bytes)."""
+    n_train = int(job.rows.numel()) if job.rows is not None else n_rows
+    return 16 * n_rows + 40 * n_train
+
+
+def _budget_chunks(job_bytes: Sequence[int], dev, frac: Optional[float] = None) -> List[tuple]:
+    """Consecutive job ranges whose summed device footprint fits ``frac`` of the memory available now (free device
+    memory plus torch's cached-but-unused blocks) -- a batch is sized from a budget up front instead of hitting
+    out-of-memory and being retried grid point by grid point. One range on the CPU or when everything fits;
+    ``TMOG_TREE_BUDGET_FRAC`` (default 0.6) sets the fraction."""
+    n = len(job_bytes)
+    if n <= 1 or dev.type != "cuda":
+        return [(0, n)]
+    frac = float(os.environ.get("TMOG_TREE_BUDGET_FRAC", "0.6")) if frac is None else frac
+    free, _ = torch.cuda.mem_get_info(dev)
+    cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    budget = max(1, int(frac * (free + max(cached, 0))))
+    if sum(job_bytes) <= budget:
+        return [(0, n)]
+    out, lo, acc = [], 0, 0
+    for i, b in enumerate(job_bytes):
+        if i > lo and acc + b > budget:
+            out.append((lo, i))
+            lo, acc = i, 0
+        acc += b
+    out.append((lo, n))
+    log.info("boosting batch of %d jobs (%.1f GB) split into %d budgeted chunks (budget %.1f GB)", n,
+             sum(job_bytes) / 1e9, len(out), budget / 1e9)
+    return out
+
+
 class _BoostLearner(Learner):
     """Shared boosting loop: all jobs advance one round per engine call."""
     classification = True
@@ -502,7 +539,9 @@ class _BoostLearner(Learner):
                     yd = yd.index_select(0, U)
                     NU = int(U.numel())
                     gjobs = [FitJob(j.params, r, j.weights) for j, r in zip(gjobs, parts)]
-            res = self._boost(Xb, spec, yd, gjobs, NU, F, dev, key[0], par=_par(context))
+            res = []
+            for lo, hi in _budget_chunks([_boost_job_bytes(j, NU) for j in gjobs], dev):
+                res += self._boost(Xb, spec, yd, gjobs[lo:hi], NU, F, dev, key[0], par=_par(context))
             for k, i in enumerate(idxs):
                 out[i] = res[k]
         return out
