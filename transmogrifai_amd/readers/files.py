@@ -7,6 +7,8 @@ columnar dataset (see :mod:`.base`). Avro container files are decoded by :mod:`.
 """
 from __future__ import annotations
 
+import torch
+
 from typing import Callable, List, Optional, Sequence, Tuple
 
 from .base import DataReader
@@ -60,8 +62,15 @@ class CSVReader(DataReader):
             from .columnar import csv_dataset
             text = [n for n, k in self.schema if k in ("string", "text")] \
                 if (self.schema is not None and all(isinstance(s, (tuple, list)) for s in self.schema)) else []
-            ds = csv_dataset(path, raw_features, self.device or default_device(), self._names(), self.has_header,
-                             self.separator, text, self.key_fn)
+            dev = torch.device(self.device or default_device())
+            ds = None
+            if dev.type == "cuda":          # the whole parse on the device (readers/gpu_csv.py)
+                from .gpu_csv import gpu_csv_dataset
+                ds = gpu_csv_dataset(path, raw_features, dev, self._names(), self.has_header, self.separator,
+                                     self.key_fn, text_columns=text)
+            if ds is None:
+                ds = csv_dataset(path, raw_features, dev, self._names(), self.has_header, self.separator, text,
+                                 self.key_fn)
             if ds is not None:
                 return ds
         return super().generate_dataset(raw_features, params)
