@@ -18,7 +18,7 @@ def _write(path, crlf=False, final_newline=True, n=3000, seed=0):
     lines = ['"r1","r2","i1","t1","t2"']
     words = ["alpha", "beta", "c,d", 'e""f', "NA", "", "gamma delta", "x"]
     for k in range(n):
-        r1 = ["%.9g" % np.float32(rng.normal() * 10 ** rng.integers(-8, 8)), "", "nan", "-0.0", "1e-30",
+        r1 = ["%.9g" % np.float32(rng.normal() * 10.0 ** int(rng.integers(-8, 8))), "", "nan", "-0.0", "1e-30",
               "3.14159265358979323846", "12345678901234567890.5", "7", "-2.5E+3", "NULL"][k % 10]
         r2 = repr(float(rng.normal()))
         i1 = ["1", "", "-42", "9007199254740993", "0"][k % 5]

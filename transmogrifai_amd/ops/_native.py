@@ -64,7 +64,7 @@ _HIP_SIGS = {
     "tmog_hip_hist_build": [P, I32, P, P, I32, P, P, P, P, P, I32, I32, I32, P, P, P, I64, P, I32, P, P, I32, I32, I32, P,
                             P, P, I32, P, I32],
     "tmog_hip_hist_stat_chunk": [I32, I32],
-    "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, P],
+    "tmog_hip_hist_subtract": [P, P, P, P, P, P, I32, I64, I64, I32, I32, P],
     "tmog_hip_split_find": [P, I32, P, P, P, P, P, I32, I32, I32, P, I32, P, P, I32, P, P, P, P, P, P, P, P, I32, P,
                             I64, I32, I32, I32, P, P, P],
     "tmog_hip_fp_merge": [P, I32, I32, I64, I32, P, P, P, P, P, P],
@@ -134,6 +134,9 @@ _HIP_SIGS = {
     "tmog_hip_mnl_epilogue": [P, I64, I32, I32, P, P, P, I32, P, I32, P, P, P, I32, P],
     "tmog_hip_mnl_bf16": [P, I64, I64, I32, P, P, I32, P, I32, I32, P, P, I32, P, P, P, I32, P],
     "tmog_hip_lr_bf16": [P, I64, I64, I32, P, P, I32, P, I32, P, P, I32, P, I32, P, P, P, I32, P],
+    "tmog_hip_csv_fields": [P, P, P, I64, I32, I32, P, P, P],
+    "tmog_hip_csv_parse_num": [P, P, P, I64, I32, P, P, I32, P, P, P, P],
+    "tmog_hip_csv_hash_text": [P, P, P, I64, I32, P, I32, P, P, P],
 }
 
 
