@@ -56,6 +56,11 @@ class OpVectorColumnMetadata:
     index: int = 0
 
     def __post_init__(self):
+        # sequences are stored as tuples: the metadata is hashed / grouped by its (name, type) key
+        if not isinstance(self.parent_feature_name, tuple):
+            object.__setattr__(self, "parent_feature_name", tuple(self.parent_feature_name))
+        if not isinstance(self.parent_feature_type, tuple):
+            object.__setattr__(self, "parent_feature_type", tuple(self.parent_feature_type))
         if not self.parent_feature_name:
             raise ValueError("must provide parent feature name")
         if len(self.parent_feature_name) != len(self.parent_feature_type):

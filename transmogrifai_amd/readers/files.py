@@ -14,6 +14,14 @@ from typing import Callable, List, Optional, Sequence, Tuple
 from .base import DataReader
 
 
+def _require_path(path):
+    """The reader's path, the reader params' path overriding it (``DataReader.readPath``: "The path is not
+    set" when neither is)."""
+    if not path:
+        raise ValueError("requirement failed: The path is not set")
+    return path
+
+
 class CSVReader(DataReader):
     """CSV with column names from ``schema`` (``[(name, kind)]`` or names) or the file header."""
 
@@ -35,8 +43,7 @@ class CSVReader(DataReader):
         path = self.path
         if params is not None and getattr(params, "path", None):
             path = params.path
-        if path is None:
-            raise ValueError("CSV reader requires a path")
+        path = _require_path(path)
         names = self._names()
         dtype = None
         if self.schema is not None and all(isinstance(s, (tuple, list)) for s in self.schema):
@@ -49,7 +56,7 @@ class CSVReader(DataReader):
         return df
 
     def _path(self, params):
-        return params.path if (params is not None and getattr(params, "path", None)) else self.path
+        return _require_path(params.path if (params is not None and getattr(params, "path", None)) else self.path)
 
     def generate_dataset(self, raw_features, params=None):
         """Columnar fast path (readers/columnar.py csv_dataset: pyarrow's multi-threaded parser -> Arrow columns ->
@@ -89,7 +96,7 @@ class ParquetReader(DataReader):
         self.path = path
 
     def _path(self, params):
-        return params.path if (params is not None and getattr(params, "path", None)) else self.path
+        return _require_path(params.path if (params is not None and getattr(params, "path", None)) else self.path)
 
     def read_frame(self, params=None):
         import pandas as pd
@@ -117,7 +124,7 @@ class AvroReader(DataReader):
     def read_records(self, params=None):
         from .avro import read_avro
         path = params.path if (params is not None and getattr(params, "path", None)) else self.path
-        return read_avro(path)
+        return read_avro(_require_path(path))
 
 
 class DataReaders:
@@ -156,6 +163,16 @@ class DataReaders:
             return AggregateReader(CSVReader(path, schema, has_header, None, device), key, aggregate_params)
 
         @staticmethod
+        def avro(path=None, key=None, aggregate_params=None, device=None):
+            from .aggregate import AggregateReader
+            return AggregateReader(AvroReader(path, None, device), key, aggregate_params)
+
+        @staticmethod
+        def parquet(path=None, key=None, aggregate_params=None, device=None):
+            from .aggregate import AggregateReader
+            return AggregateReader(ParquetReader(path, None, device), key, aggregate_params)
+
+        @staticmethod
         def custom(data, key=None, aggregate_params=None, device=None):
             from .aggregate import AggregateReader
             from .base import InMemoryReader
@@ -166,6 +183,16 @@ class DataReaders:
         def csv(path=None, schema=None, key=None, conditional_params=None, has_header=False, device=None):
             from .aggregate import ConditionalReader
             return ConditionalReader(CSVReader(path, schema, has_header, None, device), key, conditional_params)
+
+        @staticmethod
+        def avro(path=None, key=None, conditional_params=None, device=None):
+            from .aggregate import ConditionalReader
+            return ConditionalReader(AvroReader(path, None, device), key, conditional_params)
+
+        @staticmethod
+        def parquet(path=None, key=None, conditional_params=None, device=None):
+            from .aggregate import ConditionalReader
+            return ConditionalReader(ParquetReader(path, None, device), key, conditional_params)
 
         @staticmethod
         def custom(data, key=None, conditional_params=None, device=None):

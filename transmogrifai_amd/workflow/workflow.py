@@ -142,6 +142,54 @@ class OpWorkflowCore:
     def get_parameters(self) -> OpParams:
         return self.parameters
 
+    # ``OpWorkflowCore`` getters (OpWorkflowCore.scala:128-214)
+    def get_result_features(self) -> List[FeatureLike]:
+        return list(self.result_features)
+
+    def get_stages(self) -> List[OpPipelineStage]:
+        return list(self.stages)
+
+    def get_raw_features(self) -> List[FeatureLike]:
+        return list(self.raw_features)
+
+    def get_blocklist(self) -> List[FeatureLike]:
+        return list(self.blocklist)
+
+    def get_blocklist_map_keys(self) -> Dict[str, List[str]]:
+        return dict(self.blocklist_map_keys)
+
+    def get_reader(self):
+        return self.reader
+
+    def get_raw_feature_filter_results(self):
+        return self.raw_feature_filter_results
+
+    def get_raw_feature_distributions(self) -> list:
+        r = self.raw_feature_filter_results
+        return list(getattr(r, "rawFeatureDistributions", None) or [])
+
+    def get_raw_training_feature_distributions(self) -> list:
+        return [d for d in self.get_raw_feature_distributions() if getattr(d, "type", "Training") == "Training"]
+
+    def get_raw_scoring_feature_distributions(self) -> list:
+        return [d for d in self.get_raw_feature_distributions() if getattr(d, "type", "Training") == "Scoring"]
+
+    def get_updated_features(self, features: Sequence[FeatureLike]) -> List[FeatureLike]:
+        """The workflow's current version of each feature (by uid): after a blocklist rewired the stages, the
+        caller's old handles map to the rebuilt features (``OpWorkflowCore.getUpdatedFeatures``)."""
+        known = {}
+        for f in self.result_features:
+            for x in f.traverse():
+                known.setdefault(x.uid, x)
+        for f in self.raw_features:
+            known.setdefault(f.uid, f)
+        out = []
+        for f in features:
+            if f.uid not in known:
+                raise ValueError(f"feature {f.name} ({f.uid}) is not part of this workflow")
+            out.append(known[f.uid])
+        return out
+
     def generate_raw_data(self, params: Optional[OpParams] = None) -> Dataset:
         if self.reader is None:
             raise ValueError("Data reader must be set (set_reader or set_input_dataset)")
@@ -247,6 +295,23 @@ class OpWorkflow(OpWorkflowCore):
                        if not any(b.same_origin(f) for b in blocked)]
         self.set_result_features(*new_results)
 
+    def generate_raw_data(self, params: Optional[OpParams] = None) -> Dataset:
+        """The reader's raw data; with a raw feature filter, its cleaned data -- the filter's dropped features are
+        blocklisted (stages rewired) and its results recorded (``OpWorkflow.generateRawData``,
+        ``OpWorkflow.scala:225-262``)."""
+        raw = super().generate_raw_data(params)
+        if getattr(self, "rff", None) is None:
+            return raw
+        rp = None
+        pp = params or self.parameters
+        if pp is not None and pp.reader_params:
+            rp = next(iter(pp.reader_params.values()))
+        raw, to_drop, drop_keys, results = self.rff.generate_filtered_raw(self.raw_features, rp, raw)
+        self.raw_feature_filter_results = results
+        self.set_blocklist(to_drop, results.rawFeatureDistributions)
+        self.blocklist_map_keys = {k: sorted(v) for k, v in drop_keys.items()}
+        return raw
+
     def train(self, params: Optional[OpParams] = None) -> "OpWorkflowModel":
         with _DeferFullGC():
             return self._train(params)
@@ -260,15 +325,6 @@ class OpWorkflow(OpWorkflowCore):
         t0 = time.time()
         with _Timer(timings, OpStep.DataReadingAndFiltering):
             raw = self.generate_raw_data(params or self.parameters)
-            if getattr(self, "rff", None) is not None:
-                rp = None
-                pp = params or self.parameters
-                if pp is not None and pp.reader_params:
-                    rp = next(iter(pp.reader_params.values()))
-                raw, to_drop, drop_keys, results = self.rff.generate_filtered_raw(self.raw_features, rp, raw)
-                self.raw_feature_filter_results = results
-                self.set_blocklist(to_drop, results.rawFeatureDistributions)
-                self.blocklist_map_keys = {k: sorted(v) for k, v in drop_keys.items()}
         box = [raw]
         del raw     # handed over: released once split into train / hold-out
         fitted = self.fit_stages(box, timings)
@@ -311,7 +367,10 @@ class OpWorkflow(OpWorkflowCore):
     def _fit_stages(self, box: list, timings: Dict[str, float]) -> List[OpPipelineStage]:
         with _Timer(timings, "HoldoutSplit"):
             split = list(self._holdout_split(box.pop()))     # handed to the DAG executor below
-        dag = [[(st, d) for st, d in layer if st in self.stages] for layer in compute_dag(self.result_features)]
+        # stages by uid: with_model_stages swaps fitted models in for their estimators
+        by_uid = {s.uid: s for s in self.stages}
+        dag = [[(by_uid[st.uid], d) for st, d in layer if st.uid in by_uid]
+               for layer in compute_dag(self.result_features)]
         dag = [l for l in dag if l]
         stage_t: Dict[str, float] = {}
         if not self.workflow_cv:
@@ -353,9 +412,13 @@ class OpWorkflow(OpWorkflowCore):
         return m
 
     def with_model_stages(self, model: "OpWorkflowModel") -> "OpWorkflow":
-        """Reuse fitted stages of a model (``OpWorkflow.scala:468-472``)."""
-        by_uid = {s.uid: s for s in model.stages}
-        self.stages = [by_uid.get(s.uid, s) for s in self.stages]
+        """Add a fitted model's result features and reuse its fitted stages: training then fits only the stages
+        the model does not hold (``OpWorkflow.withModelStages``, ``OpWorkflow.scala:468-472``)."""
+        fitted = {s.uid: s for s in model.stages}
+        own = list(self.result_features)
+        ids = {f.uid for f in own}
+        results = _copy_with_new_stages(own + [f for f in model.result_features if f.uid not in ids], fitted)
+        self.set_result_features(*results)
         return self
 
 
@@ -385,6 +448,26 @@ class OpWorkflowModel(OpWorkflowCore):
 
     def transform_dataset(self, raw: Dataset, features=None) -> Dataset:
         return apply_transformations_dag(raw, self._fitted_dag(features or self.result_features))
+
+    def compute_data_up_to(self, feature: FeatureLike, params: Optional[OpParams] = None) -> Dataset:
+        """Raw data plus every fitted stage's output up to and including ``feature``
+        (``OpWorkflowModel.computeDataUpTo``, ``OpWorkflowModel.scala:150-170``)."""
+        raw = self.generate_raw_data(params or self.parameters)
+        if feature.is_raw:
+            return raw
+        return self.transform_dataset(raw, [feature])
+
+    def get_metadata(self, *features: FeatureLike) -> Dict[FeatureLike, object]:
+        """Each feature's output metadata (its vector metadata when it has one, else the stage's metadata
+        dict) from the fitted stage that made it (``OpWorkflowModel.getMetadata``)."""
+        by_uid = {s.uid: s for s in self.stages}
+        out = {}
+        for f in features:
+            st = by_uid.get(f.origin_stage.uid) if f.origin_stage is not None else None
+            if st is None:
+                raise ValueError(f"feature {f.name} is not produced by a fitted stage of this model")
+            out[f] = st.metadata.get("vector_metadata", st.metadata)
+        return out
 
     def score(self, data=None, keep_raw_features: bool = False, keep_intermediate_features: bool = False,
               params: Optional[OpParams] = None) -> Dataset:
@@ -467,6 +550,26 @@ class OpWorkflowModel(OpWorkflowCore):
 
     def get_origin_stage_of(self, feature: FeatureLike):
         return next(s for s in self.stages if s.uid == feature.origin_stage.uid)
+
+
+def _copy_with_new_stages(features, stages_by_uid) -> List[FeatureLike]:
+    """``FeatureLike.copyWithNewStages``: the features rebuilt with every origin stage the map holds (by uid)
+    swapped in; one object per feature uid, so a workflow's own features and a loaded model's features of the same
+    DAG merge into one graph (raw features: the first seen -- the workflow's own, with their extract functions)."""
+    memo: Dict[str, FeatureLike] = {}
+
+    def cp(f):
+        if f.uid in memo:
+            return memo[f.uid]
+        if f.is_raw:
+            memo[f.uid] = f
+            return f
+        parents = [cp(p) for p in f.parents]
+        st = stages_by_uid.get(f.origin_stage.uid, f.origin_stage)
+        memo[f.uid] = FeatureLike(f.name, f.wtype, f.is_response, st, parents, uid=f.uid,
+                                  distributions=f.distributions)
+        return memo[f.uid]
+    return [cp(f) for f in features]
 
 
 def _snake(k: str) -> str:
