@@ -116,7 +116,9 @@ def test_empty_insights_without_selector_label_vector_or_model(fx):
     assert ins.features == []
     assert ins.selectedModelInfo is None
     assert ins.trainingParams == fx.params.to_json()
-    assert list(ins.stageInfo)[0] == fx.density.origin_stage.stage_name()
+    # the raw feature filter config always leads (ModelInsightsTest.scala:213 slices keys (1, 2))
+    assert list(ins.stageInfo)[0] == "rawFeatureFilter"
+    assert list(ins.stageInfo)[1] == fx.density.origin_stage.stage_name()
 
 
 def test_only_feature_insights_without_selector_label_or_model(fx):

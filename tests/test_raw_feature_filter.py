@@ -126,7 +126,7 @@ def test_workflow_with_raw_feature_filter_updates_dag(tmp_path):
     model.save(str(tmp_path / "m"))
     m2 = OpWorkflowModel.load(str(tmp_path / "m"))
     assert {f.name for f in m2.blocklist} == {"sparse", "leak"}
-    assert m2.raw_feature_filter_results["exclusionReasons"]
+    assert m2.raw_feature_filter_results.exclusionReasons
 
 
 @pytest.mark.gpu

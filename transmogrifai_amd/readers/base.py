@@ -53,9 +53,24 @@ def column_from_series(ftype, series, device) -> Column:
 class DataReader:
     """Base reader. Subclasses implement :meth:`read_records` or :meth:`read_frame`."""
 
+    # the record type the reader reads (the reference's ``Reader.typeName``): when set, only the OpParams reader
+    # params under that key apply to this reader (``Reader.getReaderParams``, Reader.scala:69); unset, the first
+    # reader params entry does
+    type_name: Optional[str] = None
+
     def __init__(self, key: Optional[Callable] = None, device=None):
         self.key_fn = key
         self.device = torch.device(device) if device is not None else None
+
+    def reader_params_of(self, op_params):
+        """This reader's ``ReaderParams`` from a workflow's ``OpParams`` (None when none apply)."""
+        rps = getattr(op_params, "reader_params", None) or {}
+        if not rps:
+            return None
+        tn = self.type_name or getattr(getattr(self, "source", None), "type_name", None)
+        if tn is not None:
+            return rps.get(tn)
+        return next(iter(rps.values()))
 
     def read_records(self, params=None) -> Optional[List[Any]]:
         return None

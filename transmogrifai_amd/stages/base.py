@@ -50,6 +50,7 @@ _STAGE_MODULES = (
     "transmogrifai_amd.stages.feature.maps", "transmogrifai_amd.stages.feature.math_stages",
     "transmogrifai_amd.stages.feature.misc_stages", "transmogrifai_amd.stages.feature.nlp_stages",
     "transmogrifai_amd.stages.feature.text_stages", "transmogrifai_amd.stages.feature.vector_stages",
+    "transmogrifai_amd.stages.feature.vector_scalers",
     "transmogrifai_amd.stages.insights.record_insights", "transmogrifai_amd.stages.preparators.min_variance",
     "transmogrifai_amd.stages.preparators.sanity_checker", "transmogrifai_amd.models.base",
     "transmogrifai_amd.models.linear", "transmogrifai_amd.models.glm", "transmogrifai_amd.models.mlp",

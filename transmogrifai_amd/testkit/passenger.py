@@ -15,6 +15,7 @@ from ..features.builder import FeatureBuilder
 
 TEST_DATA = os.environ.get("TMOG_REFERENCE_TEST_DATA", "/root/reference/test-data")
 CUTOFF_S = 1471046600
+PASSENGER_TYPE = "com.salesforce.op.test.Passenger"     # the record type name reader params are keyed by
 
 
 def passenger_avro_path() -> str:
@@ -72,14 +73,20 @@ def data_reader(records: Optional[List[dict]] = None):
     from ..readers.files import DataReaders
     params = AggregateParams(lambda r: int(r["recordDate"]), CutOffTime.unix_epoch(CUTOFF_S))
     if records is not None:
-        return DataReaders.Aggregate.custom(records, key=lambda r: str(r["passengerId"]), aggregate_params=params)
-    return DataReaders.Aggregate.avro(passenger_avro_path(), key=lambda r: str(r["passengerId"]),
-                                      aggregate_params=params)
+        r = DataReaders.Aggregate.custom(records, key=lambda r: str(r["passengerId"]), aggregate_params=params)
+    else:
+        r = DataReaders.Aggregate.avro(passenger_avro_path(), key=lambda r: str(r["passengerId"]),
+                                       aggregate_params=params)
+    r.type_name = PASSENGER_TYPE
+    return r
 
 
 def simple_reader(records: Optional[List[dict]] = None):
     """``DataReaders.Simple.avro[Passenger]`` keyed by passenger id."""
     from ..readers.files import DataReaders
     if records is not None:
-        return DataReaders.Simple.custom(records, key=lambda r: str(r["passengerId"]))
-    return DataReaders.Simple.avro(passenger_avro_path(), key=lambda r: str(r["passengerId"]))
+        r = DataReaders.Simple.custom(records, key=lambda r: str(r["passengerId"]))
+    else:
+        r = DataReaders.Simple.avro(passenger_avro_path(), key=lambda r: str(r["passengerId"]))
+    r.type_name = PASSENGER_TYPE
+    return r

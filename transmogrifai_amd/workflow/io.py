@@ -280,8 +280,15 @@ def load_model(path: str, workflow=None):
     # back in allFeatures order (not resultFeaturesUids order)
     res_ids = set(j["resultFeaturesUids"])
     model.result_features = [built[f["uid"]] for f in j["allFeatures"] if f.get("uid") in res_ids and f["uid"] in built]
-    model.raw_features = sorted([f for f in built.values() if f.is_raw and isinstance(f.origin_stage,
-                                                                                      FeatureGeneratorStage)],
+    # the raw features the result features derive from (OpWorkflowModelReader: setResultFeatures recomputes them;
+    # blocklisted raw features stay in the blocklist only)
+    reach = {}
+    for f in model.result_features:
+        for r in f.raw_features():
+            reach[r.uid] = r
+    if not reach:     # no result feature resolved: every raw feature of the checkpoint
+        reach = {f.uid: f for f in built.values() if f.is_raw}
+    model.raw_features = sorted([f for f in reach.values() if isinstance(f.origin_stage, FeatureGeneratorStage)],
                                 key=lambda f: f.name)
     # blocklist (OpWorkflowModelReader.resolveBlocklist): the longer of the new / legacy field lists
     bl_feats: Dict[str, FeatureLike] = dict(wf_feats)
@@ -308,8 +315,12 @@ def load_model(path: str, workflow=None):
             keys[k] = sorted(set(v))
     model.blocklist_map_keys = keys
     rff = j.get("rawFeatureFilterResults")
-    model.raw_feature_filter_results = decode(json.loads(rff)) if isinstance(rff, str) and rff else (rff or
-                                                                                                     _EMPTY_RFF)
+    from ..filters.raw_feature_filter import RawFeatureFilterResults
+    rffj = decode(json.loads(rff)) if isinstance(rff, str) and rff else (rff or _EMPTY_RFF)
+    try:
+        model.raw_feature_filter_results = RawFeatureFilterResults.from_json(rffj or _EMPTY_RFF)
+    except (TypeError, KeyError, ValueError):     # a shape this reader does not model: keep the JSON
+        model.raw_feature_filter_results = rffj
     model.train_timings = decode(j.get("trainTimings", {}))
     if workflow is not None:
         model.reader = workflow.reader

@@ -139,6 +139,14 @@ class OpWorkflowCore:
         self.workflow_cv = True
         return self
 
+    @property
+    def is_workflow_cv(self) -> bool:
+        return self.workflow_cv
+
+    def set_raw_feature_filter_results(self, results) -> "OpWorkflowCore":
+        self.raw_feature_filter_results = results
+        return self
+
     def get_parameters(self) -> OpParams:
         return self.parameters
 
@@ -193,9 +201,7 @@ class OpWorkflowCore:
     def generate_raw_data(self, params: Optional[OpParams] = None) -> Dataset:
         if self.reader is None:
             raise ValueError("Data reader must be set (set_reader or set_input_dataset)")
-        rp = None
-        if params is not None and params.reader_params:
-            rp = next(iter(params.reader_params.values()))
+        rp = self.reader.reader_params_of(params) if hasattr(self.reader, "reader_params_of") else None
         raws = [f for f in self.raw_features if f not in self.blocklist]
         ds = self.reader.generate_dataset(raws, rp)
         return ds
@@ -302,10 +308,9 @@ class OpWorkflow(OpWorkflowCore):
         raw = super().generate_raw_data(params)
         if getattr(self, "rff", None) is None:
             return raw
-        rp = None
         pp = params or self.parameters
-        if pp is not None and pp.reader_params:
-            rp = next(iter(pp.reader_params.values()))
+        tr = getattr(self.rff, "training_reader", None) or self.reader
+        rp = tr.reader_params_of(pp) if hasattr(tr, "reader_params_of") else None
         raw, to_drop, drop_keys, results = self.rff.generate_filtered_raw(self.raw_features, rp, raw)
         self.raw_feature_filter_results = results
         self.set_blocklist(to_drop, results.rawFeatureDistributions)
@@ -334,7 +339,7 @@ class OpWorkflow(OpWorkflowCore):
         model.raw_features = list(self.raw_features)
         model.blocklist = list(self.blocklist)
         model.blocklist_map_keys = dict(self.blocklist_map_keys)
-        model.raw_feature_filter_results = self.raw_feature_filter_results
+        model.raw_feature_filter_results = self.raw_feature_filter_results or _empty_rff_results()
         model.reader = self.reader
         model.train_parameters = self.parameters
         timings["total"] = time.time() - t0
@@ -430,6 +435,38 @@ class OpWorkflowModel(OpWorkflowCore):
         self.parameters = parameters or OpParams()
         self.train_parameters = self.parameters
         self.train_timings: Dict[str, float] = {}
+
+    # ---------------------------------------------------------------------------------- builders
+    def set_stages(self, stages: Sequence[OpPipelineStage]) -> "OpWorkflowModel":
+        self.stages = list(stages)
+        return self
+
+    def set_features(self, features: Sequence[FeatureLike]) -> "OpWorkflowModel":
+        """Result features; the raw features are the ones they derive from (``OpWorkflowModel.setFeatures``)."""
+        self.result_features = list(features)
+        raws = {}
+        for f in self.result_features:
+            for r in f.raw_features():
+                raws[r.uid] = r
+        self.raw_features = sorted(raws.values(), key=lambda f: f.name)
+        return self
+
+    def set_parameters(self, params: OpParams) -> "OpWorkflowModel":
+        self.parameters = params
+        return self
+
+    def copy(self) -> "OpWorkflowModel":
+        """A new model over the same fitted stages and features (``OpWorkflowModel.copy``)."""
+        m = OpWorkflowModel(self.uid, self.parameters)
+        for k in ("stages", "result_features", "raw_features", "blocklist"):
+            setattr(m, k, list(getattr(self, k)))
+        m.blocklist_map_keys = dict(self.blocklist_map_keys)
+        m.train_parameters = self.train_parameters
+        m.raw_feature_filter_results = self.raw_feature_filter_results
+        m.reader = self.reader
+        m.workflow_cv = self.workflow_cv
+        m.train_timings = dict(self.train_timings)
+        return m
 
     # ---------------------------------------------------------------------------------- scoring
     def _fitted_dag(self, features: Sequence[FeatureLike]):
@@ -550,6 +587,13 @@ class OpWorkflowModel(OpWorkflowCore):
 
     def get_origin_stage_of(self, feature: FeatureLike):
         return next(s for s in self.stages if s.uid == feature.origin_stage.uid)
+
+
+def _empty_rff_results():
+    """``RawFeatureFilterResults()`` of a workflow trained without a filter (the default config)."""
+    from ..filters.raw_feature_filter import RawFeatureFilterResults
+    from .io import _EMPTY_RFF
+    return RawFeatureFilterResults.from_json(_EMPTY_RFF)
 
 
 def _copy_with_new_stages(features, stages_by_uid) -> List[FeatureLike]:
