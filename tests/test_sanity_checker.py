@@ -285,3 +285,24 @@ def test_maps_with_the_same_keys():
     cats = summ["categoricalStats"]
     assert len(cats) == 10
     assert all(len((c.get("contingencyMatrix") or c["contingency"])["0"]) == 2 for c in cats)
+
+
+def test_tiny_check_sample_still_fits():
+    """``SanityCheckerTest.scala:237-249``: a 1e-6 check sample on 6 rows is lifted to the sample lower limit; the
+    fit runs through."""
+    ds, label, vec = _fixture()
+    _checker(label, vec, max_correlation=0.99, min_variance=0.0, check_sample=0.000001,
+             remove_bad_features=True).fit(ds)
+
+
+def test_missing_vector_metadata_is_an_error():
+    """``SanityCheckerTest.scala:257-277``: a feature vector without OpVectorMetadata cannot be checked (the
+    column names and groups come from it)."""
+    rows = [(32, [5.0, 1, 1, 0]), (32, [4.0, 0, 0, 1]), (34, [6.0, 1, 1, 0]), (32, [5.5, 1, 1, 0]),
+            (30, [5.4, 0, 0, 1]), (32, [5.4, 0, 0, 1])]
+    ds, (label, vec) = TestFeatureBuilder.of(("label", T.RealNN, [float(r[0]) for r in rows]),
+                                             ("features", T.OPVector, [r[1] for r in rows]), response="label")
+    ds["features"].metadata = None
+    sc = _checker(label, vec, remove_bad_features=True, check_sample=1.0)
+    with pytest.raises(ValueError):
+        sc.fit(ds).transform(ds)
