@@ -7,8 +7,8 @@ mkdir -p gpurun_out/r6b
 export TMPDIR=/tmp
 O=gpurun_out/r6b
 timeout -k 10 600 python3 -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_csv.py tests/test_linear_mixed_gpu.py tests/test_learner_parallel.py tests/test_sanity_kernels_gpu.py \
-  tests/test_tree_resident_gpu.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+  tests/test_dense_gemm_gpu.py tests/test_sanity_kernels_gpu.py tests/test_gpu_csv.py tests/test_linear_mixed_gpu.py \
+  tests/test_learner_parallel.py tests/test_tree_resident_gpu.py tests/test_mlp.py tests/test_linear_bf16_gpu.py tests/test_sparse_linear_gpu.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -3 $O/tests.log
 for m in 1 0; do
   TMOG_LR_MIXED=$m timeout -k 10 400 python3 -u bench.py --steps 5 --warmup 1 --verbose > $O/bench_mixed$m.log 2>&1 || { tail -20 $O/bench_mixed$m.log; exit 1; }

@@ -6,12 +6,14 @@ linear learners do: every job is a column of the parameter matrix ``U [n_params,
 weights ``W [N, P]`` (zero outside its fold), and one batched L-BFGS (``linear.owlqn_batched`` without L1)
 drives all of them. One objective pass is
 
-* forward: the layer products as batched GEMMs (hipBLASLt; the first layer one GEMM of the shared X against
-  all P weight matrices), each followed by the fused bias + sigmoid epilogue (``mlp_kernels.hip``), and the
-  output layer's softmax / weighted cross-entropy / ``W (softmax - onehot)`` in one kernel
-  (``sparse_kernels.hip`` softmax epilogue, shared with the multinomial logistic regression);
-* backward: weight gradients as batched GEMMs, the sigmoid derivative fused with the bias-gradient column sums
-  (``mlp_kernels.hip``), fp64 sums throughout.
+* forward: every layer product on the matrix cores with its bias + sigmoid fused into the GEMM's epilogue
+  (``dense_kernels.hip`` rowgemm; the first layer one launch of the shared X against all P weight matrices as
+  grouped columns, so X is streamed once per 64 output columns), and the output layer's softmax / weighted
+  cross-entropy / ``W (softmax - onehot)`` in one kernel (``sparse_kernels.hip`` softmax epilogue, shared with
+  the multinomial logistic regression);
+* backward: weight gradients as matrix-core ``H^T dZ`` products (``dense_kernels.hip`` xtd: fp32 chunks summed
+  in fp64), ``dZ W^T`` with W read transposed in place, the sigmoid derivative fused with the bias-gradient column
+  sums (``mlp_kernels.hip``).
 
 Spark stacks rows into ``blockSize`` matrices only for BLAS; here all rows of a fold are one batch. The
 objective is the weighted mean cross-entropy (no regularisation, as Spark's MLP). The host path computes the
@@ -114,12 +116,21 @@ class MLPObjective:
         params = self._unpack(U)
         acts = []
         H = None
+        mfma = self.X.is_cuda
+        if mfma:
+            from ..ops import dense as DN
         for i, (Wl, bl) in enumerate(params[:-1]):
-            Z = (torch.matmul(self.X, Wl) if i == 0 else torch.bmm(H, Wl)).contiguous()
-            H = _bias_sigmoid_(Z, bl)
+            if mfma:        # layer product + bias + sigmoid in one matrix-core launch (dense_kernels.hip)
+                H = DN.layer_shared(self.X, Wl, bl, True) if i == 0 else DN.layer_batched(H, Wl, bl, True)
+            else:
+                Z = (torch.matmul(self.X, Wl) if i == 0 else torch.bmm(H, Wl)).contiguous()
+                H = _bias_sigmoid_(Z, bl)
             acts.append(H)
         WL, bL = params[-1]
-        logits = torch.matmul(self.X, WL) if self.nl == 1 else torch.bmm(H, WL)
+        if mfma:
+            logits = DN.layer_shared(self.X, WL, None, False) if self.nl == 1 else DN.layer_batched(H, WL, None, False)
+        else:
+            logits = torch.matmul(self.X, WL) if self.nl == 1 else torch.bmm(H, WL)
         f, R = self._output(logits, bL, grad)
         f = f / self.wsum
         if not grad:
@@ -131,11 +142,15 @@ class MLPObjective:
         for i in range(self.nl - 1, -1, -1):
             o, a, b, ob = self.slices[i]
             Hin = acts[i - 1] if i > 0 else None
-            dW = torch.matmul(self.X.t(), dZ) if i == 0 else torch.bmm(Hin.transpose(1, 2), dZ)     # [P, a, b]
+            if mfma:        # fp32 matrix-core chunks, fp64 across chunks
+                dW = DN.grad_shared(self.X, dZ) if i == 0 else DN.grad_batched(Hin, dZ)                # [P, a, b]
+            else:
+                dW = torch.matmul(self.X.t(), dZ) if i == 0 else torch.bmm(Hin.transpose(1, 2), dZ)
             g[o:o + a * b] = dW.reshape(P, a * b).t().to(U.dtype)
             g[ob:ob + b] = db.t().to(U.dtype)
             if i > 0:
-                dH = torch.bmm(dZ, params[i][0].transpose(1, 2)).contiguous()                       # [P, N, a]
+                dH = DN.backprop_input(dZ, params[i][0]) if mfma else \
+                    torch.bmm(dZ, params[i][0].transpose(1, 2)).contiguous()                        # [P, N, a]
                 db = _sigmoid_backprop_(dH, Hin)
                 dZ = dH
         return f, g

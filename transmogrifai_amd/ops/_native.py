@@ -135,6 +135,10 @@ _HIP_SIGS = {
     "tmog_hip_mnl_bf16": [P, I64, I64, I32, P, P, I32, P, I32, I32, P, P, I32, P, P, P, I32, P],
     "tmog_hip_lr_bf16": [P, I64, I64, I32, P, P, I32, P, I32, P, P, I32, P, I32, P, P, P, I32, P],
     "tmog_hip_csv_fields": [P, P, P, I64, I32, I32, P, P, P],
+    "tmog_hip_rowgemm": [P, I64, I64, P, I64, I64, I32, I32, I64, P, I64, I64, P, I64, I64, I32, I64, I64, I32, I32, I32,
+                         I32, P],
+    "tmog_hip_xtd_chunks": [I64, I32, I32, I32, I32],
+    "tmog_hip_xtd": [P, I64, I64, P, I64, I64, I32, I64, I64, I32, I32, I32, I32, P, P, P],
     "tmog_hip_csv_parse_num": [P, P, P, I64, I32, P, P, I32, P, P, P, P],
     "tmog_hip_csv_hash_text": [P, P, P, I64, I32, P, I32, P, P, P],
 }

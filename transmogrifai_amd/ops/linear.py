@@ -12,17 +12,31 @@ from typing import Optional
 import torch
 
 
+def _dense_mfma(X) -> bool:
+    """A contiguous fp32 device design: its products run on the matrix-core row GEMMs (ops/dense.py)."""
+    return isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and \
+        X.is_contiguous()
+
+
 def gemm(X, V: torch.Tensor) -> torch.Tensor:
-    """``X [N, d] @ V [d, P]`` in X's dtype (a :class:`SparseDesign` multiplies its dense and sparse parts)."""
+    """``X [N, d] @ V [d, P]`` in X's dtype (a :class:`SparseDesign` multiplies its dense and sparse parts; a dense
+    fp32 device design runs ``dense_kernels.hip`` rowgemm)."""
     if isinstance(X, SparseDesign):
         return X.mm(V)
+    if _dense_mfma(X):
+        from . import dense as DN
+        return DN.mm(X, V.to(torch.float32))
     return X @ V.to(X.dtype)
 
 
 def gemm_t(X, R: torch.Tensor) -> torch.Tensor:
-    """``X^T [d, N] @ R [N, P]`` in X's dtype (fp64 for a :class:`SparseDesign`)."""
+    """``X^T [d, N] @ R [N, P]`` in X's dtype (fp64 for a :class:`SparseDesign`, and for a dense fp32 device
+    design: ``dense_kernels.hip`` xtd -- fp32 matrix-core chunks, fp64 across chunks)."""
     if isinstance(X, SparseDesign):
         return X.tmm(R)
+    if _dense_mfma(X):
+        from . import dense as DN
+        return DN.tmm(X, R.to(torch.float32))
     return X.t() @ R.to(X.dtype)
 
 

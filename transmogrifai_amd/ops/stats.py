@@ -153,7 +153,8 @@ def _gram_centered_bf16(X: torch.Tensor, mean: torch.Tensor, y_codes, L: int) ->
     product is exact; the products are summed in fp32 over 256-row slices (so the result carries fp32 rounding of
     those partial sums, like the fp32 kernel, but is not bit-identical to it), then in fp64 across slices; the
     centred blocks of the original columns are assembled from ``B^T B`` in fp64 (the ones column gives the raw
-    column sums and the row count). ``tests/test_sanity_kernels_gpu.py`` bounds it against the fp64 Gramian."""
+    column sums and the row count), re-centred from the fp32-rounded mean the packing used onto the fp64 mean.
+    ``tests/test_sanity_kernels_gpu.py`` bounds it against the fp64 Gramian."""
     n, d = X.shape
     dev = X.device
     exact = bf16_exact_columns(X)
@@ -191,10 +192,15 @@ def _gram_centered_bf16(X: torch.Tensor, mean: torch.Tensor, y_codes, L: int) ->
     sE = GA[io].index_select(0, ie)                     # raw column sums of the exact columns
     cnt = GA[io, io]
     SR = sum(GA[io].index_select(0, p) for p in parts)  # sums of the centred other columns
+    # the other columns were centred on the fp32-rounded mean (C = x - mu32, exact in fp32); re-centre on the fp64
+    # mean in fp64: sum (C_i - dl_i)(C_j - dl_j) with dl = mu64 - mu32 -- for a large-offset, small-spread column
+    # the rounding of the mean is a sizeable fraction of its spread, and the variance would carry n dl^2
+    dl = mu64.index_select(0, R) - muR.to(torch.float64)
     G = torch.empty(d + L, d + L, dtype=torch.float64, device=dev)
     G_EE = blk(ie, ie) - muE[:, None] * sE[None, :] - sE[:, None] * muE[None, :] + cnt * muE[:, None] * muE[None, :]
-    G_ER = sum(blk(ie, p) for p in parts) - muE[:, None] * SR[None, :]
-    G_RR = sum(blk(p, q) for p in parts for q in parts)
+    G_ER = sum(blk(ie, p) for p in parts) - muE[:, None] * SR[None, :] - (sE - cnt * muE)[:, None] * dl[None, :]
+    G_RR = sum(blk(p, q) for p in parts for q in parts) - SR[:, None] * dl[None, :] - dl[:, None] * SR[None, :] + \
+        cnt * dl[:, None] * dl[None, :]
     G[E[:, None], E[None, :]] = G_EE
     G[E[:, None], R[None, :]] = G_ER
     G[R[:, None], E[None, :]] = G_ER.t()
@@ -203,7 +209,7 @@ def _gram_centered_bf16(X: torch.Tensor, mean: torch.Tensor, y_codes, L: int) ->
         ly = torch.arange(d, d + L, device=dev)
         nl = GA[iy, io]
         G_YE = blk(iy, ie) - nl[:, None] * muE[None, :]
-        G_YR = sum(blk(iy, p) for p in parts)
+        G_YR = sum(blk(iy, p) for p in parts) - nl[:, None] * dl[None, :]
         G[ly[:, None], E[None, :]] = G_YE
         G[E[:, None], ly[None, :]] = G_YE.t()
         G[ly[:, None], R[None, :]] = G_YR

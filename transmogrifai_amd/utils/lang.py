@@ -229,10 +229,16 @@ STOPWORDS["fa"] = frozenset("""
 ديده همين گذاري برداري علت گذاشته هم فوق نه ها شوند اباد همواره هر اول خواهند چهار نام امروز مان هاي قبل كنم سعي
 تازه را هستند زير جلوي عنوان بود""".split())
 
+from .stemmers_more import STOPWORDS_MORE as _SW_MORE  # noqa: E402
+
+STOPWORDS.update(_SW_MORE)
+# IrishAnalyzer: its hyphenation prefixes (h-, n-, t-, split off by the tokenizer) are stopped with the stop words
+STOPWORDS["ga"] = STOPWORDS["ga"] | frozenset(("h", "n", "t"))
+
 _ELISIONS = {"fr": ("l", "m", "t", "qu", "n", "s", "j", "d", "c", "jusqu", "quoiqu", "lorsqu", "puisqu"),
              "it": ("c", "l", "all", "dall", "dell", "nell", "sull", "coll", "pell", "gl", "agl", "dagl",
                     "degl", "negl", "sugl", "un", "m", "t", "s", "v", "d"),
-             "ca": ("d", "l", "m", "n", "s", "t")}
+             "ca": ("d", "l", "m", "n", "s", "t"), "ga": ("d", "m", "b")}
 
 
 def _script_counts(text: str) -> Dict[str, int]:
@@ -328,14 +334,17 @@ LANGUAGE_NAMES = {"English": "en", "French": "fr", "German": "de", "Spanish": "e
                   "Hungarian": "hu", "Japanese": "ja", "Korean": "ko", "SimplifiedChinese": "zh-cn",
                   "TraditionalChinese": "zh-tw", "Chinese": "zh", "Arabic": "ar",
                   "Hindi": "hi", "Bulgarian": "bg", "Czech": "cs",
-                  "Persian": "fa", "Indonesian": "id", "Latvian": "lv"}
+                  "Persian": "fa", "Indonesian": "id", "Latvian": "lv", "Greek": "el", "Lithuanian": "lt",
+                  "Galician": "gl", "Basque": "eu", "Irish": "ga", "Bengali": "bn", "Sorani": "ckb", "Thai": "th"}
+LANGUAGE_NAMES["Brazilian"] = "pt-br"
 # Lucene CJKAnalyzer languages (LuceneTextAnalyzer.scala: Korean, SimplifiedChinese, TraditionalChinese)
 CJK_BIGRAM = frozenset({"zh", "zh-cn", "zh-tw", "ko"})
 
 
 def _pre_stop_normalizers():
     from .stemmers import hindi_normalize, persian_normalize
-    return {"hi": hindi_normalize, "fa": persian_normalize}
+    from .stemmers_more import PRE_STOP_MORE
+    return {"hi": hindi_normalize, "fa": persian_normalize, **PRE_STOP_MORE}
 
 
 _PRE_STOP_NORMALIZERS = _pre_stop_normalizers()
@@ -360,6 +369,10 @@ def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_t
         if to_lowercase:
             from .snowball import turkish_lower
             text = turkish_lower(text)
+    if lang == "ga" and to_lowercase:
+        # IrishLowerCaseFilter: an initial n / t before an upper-case vowel is a prefix (nAthair -> n-athair)
+        import re
+        text = re.sub(r"\b([nt])([AEIOU\u00c1\u00c9\u00cd\u00d3\u00da])", r"\1-\2", text)
     toks = TU.tokenize(text, to_lowercase, 1, stopwords=frozenset())
     if lang == "tr":
         toks = [t.partition("'")[0] for t in toks]
@@ -383,7 +396,7 @@ def analyze(text: str, language: str = UNKNOWN, to_lowercase: bool = True, min_t
         return [porter_stem(t) for t in toks if t not in sw and len(t) >= min_token_length]
     from .stemmers import STEMMERS
     stem = STEMMERS.get(language)
-    if language in ("ar", "hi", "fa"):  # DecimalDigitFilter: any Unicode decimal digit -> its ASCII digit
+    if language in ("ar", "hi", "fa", "bn", "ckb"):  # DecimalDigitFilter: any Unicode decimal digit -> its ASCII digit
         toks = ["".join(str(unicodedata.digit(c)) if c.isdecimal() and not c.isascii() else c for c in t)
                 for t in toks]
     # analyzers whose normalisation filters run before their stop filter (HindiAnalyzer, PersianAnalyzer)

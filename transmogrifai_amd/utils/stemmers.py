@@ -790,3 +790,7 @@ STEMMERS: Dict[str, Callable[[str], str]] = {
     "ar": arabic_analyze_stem, "hi": hindi_analyze_stem, "bg": bulgarian_stem, "cs": czech_stem, "tr": turkish_stem,
     "id": indonesian_stem, "lv": latvian_stem,
 }
+
+from .stemmers_more import STEMMERS_MORE  # noqa: E402
+
+STEMMERS.update(STEMMERS_MORE)
