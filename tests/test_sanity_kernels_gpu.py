@@ -157,8 +157,10 @@ def test_bf16_gramian_fp32_accuracy_vs_fp64():
     G32 = A32.t() @ A32
     Gf = torch.empty_like(Gref).cuda()
     from transmogrifai_amd.ops import _native as N
-    N.check(N.hip().tmog_hip_gram_aug(N.ptr(Xd), X.shape[0], X.shape[1], Xd.stride(0), N.ptr(mu32.cuda()),
-                                      N.ptr(y.cuda().to(torch.int32)), 3, N.ptr(Gf), N.stream(Xd.device)), "gram_aug")
+    mu_d, y_d = mu32.cuda(), y.cuda().to(torch.int32)       # (kept alive until the kernel has read them)
+    N.check(N.hip().tmog_hip_gram_aug(N.ptr(Xd), X.shape[0], X.shape[1], Xd.stride(0), N.ptr(mu_d), N.ptr(y_d), 3,
+                                      N.ptr(Gf), N.stream(Xd.device)), "gram_aug")
+    torch.cuda.synchronize()
     Aa = A32.abs()
     ef = (Gf.cpu() - G32).abs() / (Aa.t() @ Aa).clamp_min(1e-30)
     assert float(ef.max()) < 2e-6, float(ef.max())

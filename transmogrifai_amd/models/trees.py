@@ -1025,8 +1025,9 @@ class XGBoostClassifierLearner(_BoostLearner):
         counts = torch.zeros(P, 2, bins, dtype=torch.int32, device=dev) if bins else None
         val = la.value[:, 0].contiguous() if la.value.dim() == 2 else la.value.contiguous()
         tree_job = TE._const_tensor(np.asarray(act, np.int64), dev)
+        tree_c = la.tree.contiguous()       # (bound: a temporary's block could be handed to the next allocation)
         NV.check(NV.hip().tmog_hip_boost_epilogue(
-            NV.ptr(la.rows), NV.ptr(la.gid), int(la.rows.numel()), NV.ptr(val), NV.ptr(la.tree.contiguous()),
+            NV.ptr(la.rows), NV.ptr(la.gid), int(la.rows.numel()), NV.ptr(val), NV.ptr(tree_c),
             NV.ptr(tree_job), int(N), NV.ptr(Fm), NV.ptr(G), NV.ptr(H), NV.ptr(yf), self.objective_code,
             NV.ptr(counts), int(bins), int(val.shape[0]), len(act), int(P), NV.stream(dev), NV.ptr(amax),
             int(getattr(la, "wide", False))),
