@@ -11,3 +11,7 @@ echo "xgb-alone $(grep -a '^{' $O/xgb_alone.log | grep -o '"value": [0-9.]*\|"Fe
 timeout -k 10 900 python3 -u bench.py --config regression-100m --max-training-sample 20000000 --steps 1 --warmup 1 --verbose > $O/reg100m_20m.log 2>&1 || { tail -30 $O/reg100m_20m.log; exit 1; }
 echo "reg100m-20m $(grep -a '^{' $O/reg100m_20m.log | grep -o '"value": [0-9.]*\|"peak_hbm_gb_per_gpu": [0-9.]*' | tr '\n' ' ')"
 grep -a -i "oom\|out of memory" $O/reg100m_20m.log | head -3 || true
+for m in 1 0; do
+  TMOG_DENSE_MFMA=$m timeout -k 10 400 python3 -u bench.py --config multiclass-text --steps 3 --warmup 1 --verbose > $O/mct_dense$m.log 2>&1 || { tail -20 $O/mct_dense$m.log; exit 1; }
+  echo "mct dense=$m $(grep -a '^{' $O/mct_dense$m.log | grep -o '"value": [0-9.]*\|"holdout_error": [0-9.]*\|"OpLogisticRegression": [0-9.]*' | tr '\n' ' ')"
+done

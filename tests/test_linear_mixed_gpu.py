@@ -44,8 +44,9 @@ def test_mixed_pass_is_bit_identical(monkeypatch, n, de, dr, P, loss):
             assert torch.equal(ref[2], got[2])
 
 
-def test_mixed_copy_moves_fewer_bytes():
+def test_mixed_copy_moves_fewer_bytes(monkeypatch):
     from transmogrifai_amd.ops import linear as LK
+    monkeypatch.setenv("TMOG_LR_MIXED", "1")
     X, _ = _design(1000, 200, 129)
     X = X.cuda()
     md = LK.MixedDesign.of(X)

@@ -116,9 +116,8 @@ class MLPObjective:
         params = self._unpack(U)
         acts = []
         H = None
-        mfma = self.X.is_cuda
-        if mfma:
-            from ..ops import dense as DN
+        from ..ops import dense as DN
+        mfma = self.X.is_cuda and DN.enabled()
         for i, (Wl, bl) in enumerate(params[:-1]):
             if mfma:        # layer product + bias + sigmoid in one matrix-core launch (dense_kernels.hip)
                 H = DN.layer_shared(self.X, Wl, bl, True) if i == 0 else DN.layer_batched(H, Wl, bl, True)

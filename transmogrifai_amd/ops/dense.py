@@ -13,11 +13,17 @@ kernel's indexing assumes before it launches; :func:`supported` tells callers wh
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
 
 _TARGET_BLOCKS = 2048
+
+
+def enabled() -> bool:
+    """The matrix-core row GEMMs are the device path; ``TMOG_DENSE_MFMA=0`` selects torch's GEMMs (A/B only)."""
+    return os.environ.get("TMOG_DENSE_MFMA", "1") != "0"
 
 
 def supported(*ts: torch.Tensor) -> bool:

@@ -14,8 +14,9 @@ import torch
 
 def _dense_mfma(X) -> bool:
     """A contiguous fp32 device design: its products run on the matrix-core row GEMMs (ops/dense.py)."""
+    from .dense import enabled
     return isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and \
-        X.is_contiguous()
+        X.is_contiguous() and enabled()
 
 
 def gemm(X, V: torch.Tensor) -> torch.Tensor:
@@ -313,10 +314,12 @@ class MixedDesign:
     @staticmethod
     def of(X: torch.Tensor, grad: bool = False) -> Optional["MixedDesign"]:
         """The mixed copy of ``X`` (made once per tensor, shared by every pass), or None when it does not pay or
-        fit: fp32 ``linear_dtype`` only, ``TMOG_LR_MIXED=0`` disables, gradient passes keep plain fp32 unless
-        ``TMOG_LR_MIXED=2`` (they are bound by the fp32 MFMA phase, not by HBM)."""
+        fit: fp32 ``linear_dtype`` only, opt-in with ``TMOG_LR_MIXED=1`` (value passes) / ``2`` (gradient passes
+        too). Off by default: on the headline it measured slower than the plain fp32 passes -- LR lane 0.634 s vs
+        0.515 s, identical AuPR (profiles/r6b_bench_mixed1.log / r6b_bench_mixed0.log): the landing of the bf16
+        half in LDS costs more than the bytes it saves."""
         from .. import config as _cfg
-        mode = os.environ.get("TMOG_LR_MIXED", "1")
+        mode = os.environ.get("TMOG_LR_MIXED", "0")
         if mode == "0" or (grad and mode != "2") or _cfg.linear_dtype() != "fp32":
             return None
         if not (isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.float32 and X.dim() == 2
