@@ -232,6 +232,10 @@ def main():
                       f"{time.perf_counter() - t_w:.1f} s", file=sys.stderr, flush=True)
             reader = ParquetReader(pq_path[0], device=dev) if args.ingest == "parquet" else \
                 CSVReader(pq_path[0], has_header=True, device=dev)
+            if args.ingest == "csv":
+                # the file holds this table's float32 reals as shortest float32 decimals: stored as float32 they
+                # read back bit-identical to the in-memory table (Parquet keeps the float32 type itself)
+                reader.real_dtype = torch.float32
             del ds
             ds = None
             if use_gpu:

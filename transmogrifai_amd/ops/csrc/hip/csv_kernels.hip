@@ -61,6 +61,8 @@ __device__ __forceinline__ bool is_space(uint8_t c) { return c == ' ' || c == '\
 __device__ bool is_na(const uint8_t* s, int n) {
   if (n == 0) return true;
   if (n > 8) return false;
+  const uint8_t c0 = s[0];              // every NA string starts with one of these
+  if (!(c0 == '#' || c0 == '-' || c0 == '1' || c0 == '<' || c0 == 'N' || c0 == 'n')) return false;
   char t[9];
   for (int i = 0; i < n; ++i) t[i] = (char)s[i];
   t[n] = 0;
@@ -96,8 +98,10 @@ __device__ __forceinline__ void field_range(const uint8_t* buf, const int64_t* f
 __constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                   1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
 
-// One (row, column) per thread. cols[j] = CSV column of output j; kind[j] = 0 float64, 1 int64. out[j * nrows + r]
-// (as double or int64 bits), valid[j * nrows + r]; slow[j * nrows + r] = 1 when the host must parse the field.
+// One (row, column) per thread, row-major: the threads of a wave read one row's consecutive field offsets and bytes.
+// cols[j] = CSV column of output j; kind[j] = 0 float64, 1 int64. out[r * nout + j] (as double or int64 bits),
+// valid[r * nout + j]; slow[r * nout + j] = 1 when the host must parse the field (the host transposes the tile to
+// column-major). A field that does not parse as a number is checked against the NA strings only then.
 __global__ void __launch_bounds__(256) csv_parse_num_kernel(const uint8_t* __restrict__ buf,
                                                             const int64_t* __restrict__ fstart,
                                                             const int32_t* __restrict__ nfields, int64_t nrows,
@@ -107,15 +111,15 @@ __global__ void __launch_bounds__(256) csv_parse_num_kernel(const uint8_t* __res
                                                             uint8_t* __restrict__ slow) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nrows * nout) return;
-  const int j = (int)(i / nrows);
-  const int64_t r = i - (int64_t)j * nrows;
-  const int64_t o = (int64_t)j * nrows + r;
+  const int64_t r = i / nout;
+  const int j = (int)(i - r * nout);
+  const int64_t o = i;
   int64_t a, b;
   field_range(buf, fstart + r * (int64_t)(ncols + 1), nfields[r], cols[j], &a, &b);
   const uint8_t* s = buf + a;
   const int n = (int)(b - a);
   slow[o] = 0;
-  if (is_na(s, n)) {
+  if (n == 0) {
     valid[o] = 0;
     out[o] = 0;
     return;
@@ -161,7 +165,14 @@ __global__ void __launch_bounds__(256) csv_parse_num_kernel(const uint8_t* __res
     bad = bad || !edig;
     e10 += eneg ? -ev : ev;
   }
-  if (!any || k != n) bad = true;       // inf / infinity / hex / stray characters: the host parser decides
+  if (!any || k != n) {                 // not a plain decimal: an NA string is missing, anything else (inf,
+    if (is_na(s, n)) {                  // hex, stray characters) goes to the host parser
+      valid[o] = 0;
+      out[o] = 0;
+      return;
+    }
+    bad = true;
+  }
   if (kind[j] == 1) {                   // int64: an integer literal (a ".0" fraction is accepted)
     if (bad || e10 < 0 || nd + e10 > 18) {
       slow[o] = 1;
@@ -200,9 +211,9 @@ __global__ void __launch_bounds__(256) csv_hash_text_kernel(const uint8_t* __res
                                                             uint64_t* __restrict__ hash, int64_t* __restrict__ span) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nrows * nout) return;
-  const int j = (int)(i / nrows);
-  const int64_t r = i - (int64_t)j * nrows;
-  const int64_t o = (int64_t)j * nrows + r;
+  const int64_t r = i / nout;           // row-major as csv_parse_num: out[r * nout + j]
+  const int j = (int)(i - r * nout);
+  const int64_t o = i;
   int64_t a, b;
   field_range(buf, fstart + r * (int64_t)(ncols + 1), nfields[r], cols[j], &a, &b);
   span[2 * o] = a;

@@ -25,6 +25,10 @@ def _require_path(path):
 class CSVReader(DataReader):
     """CSV with column names from ``schema`` (``[(name, kind)]`` or names) or the file header."""
 
+    # storage type of real-valued columns: float64 (the reference's double) unless a float32 source is declared --
+    # a file written from float32 data (shortest float32 decimals) then reads back bit-identical to it
+    real_dtype = torch.float64
+
     def __init__(self, path: Optional[str] = None, schema: Optional[Sequence] = None, has_header: bool = False,
                  key: Optional[Callable] = None, device=None, separator: str = ","):
         super().__init__(key, device)
@@ -74,13 +78,23 @@ class CSVReader(DataReader):
             if dev.type == "cuda":          # the whole parse on the device (readers/gpu_csv.py)
                 from .gpu_csv import gpu_csv_dataset
                 ds = gpu_csv_dataset(path, raw_features, dev, self._names(), self.has_header, self.separator,
-                                     self.key_fn, text_columns=text)
+                                     self.key_fn, text_columns=text, real_dtype=self.real_dtype)
             if ds is None:
                 ds = csv_dataset(path, raw_features, dev, self._names(), self.has_header, self.separator, text,
                                  self.key_fn)
+                if ds is not None and self.real_dtype != torch.float64:
+                    ds = _cast_reals(ds, self.real_dtype)
             if ds is not None:
                 return ds
         return super().generate_dataset(raw_features, params)
+
+
+def _cast_reals(ds, dtype):
+    from ..data.columns import NumericColumn
+    for name, c in list(ds.columns.items()):
+        if isinstance(c, NumericColumn) and c.values.is_floating_point() and c.values.dtype != dtype:
+            ds.columns[name] = NumericColumn(c.ftype, c.values.to(dtype), c.valid)
+    return ds
 
 
 class CSVAutoReader(CSVReader):

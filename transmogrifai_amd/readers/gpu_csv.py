@@ -51,13 +51,13 @@ def _plan(raw_features, names):
     return plan
 
 
-class _Chunk:
-    def __init__(self, nbytes, dev):
+class _Host:
+    def __init__(self, nbytes):
         self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
         self.np = self.host.numpy()
-        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        self.copied = None
+        self.copied = None          # event: this buffer's last device copy has finished reading it
         self.n = 0
+        self.base = 0               # file offset of byte 0
 
 
 def _pread_into(fd, arr: np.ndarray, off: int, n: int, pool) -> int:
@@ -79,7 +79,11 @@ def _pread_into(fd, arr: np.ndarray, off: int, n: int, pool) -> int:
 
 def gpu_csv_dataset(path: str, raw_features: Sequence, dev, names: Optional[Sequence[str]] = None,
                     has_header: bool = True, separator: str = ",", key_fn=None,
-                    chunk_bytes: int = CHUNK, text_columns: Sequence[str] = ()) -> Optional[Dataset]:
+                    chunk_bytes: int = CHUNK, text_columns: Sequence[str] = (),
+                    real_dtype: torch.dtype = torch.float64) -> Optional[Dataset]:
+    """The CSV file as device columns (None: the generic path decides). ``real_dtype`` is the storage type of the
+    real-valued columns (float64, the reference's double; float32 for a file written from float32 data, whose
+    shortest decimals then read back bit-identically)."""
     dev = torch.device(dev)
     if dev.type != "cuda" or key_fn is not None or len(separator) != 1 or os.environ.get("TMOG_GPU_CSV") == "0":
         return None
@@ -112,7 +116,11 @@ def gpu_csv_dataset(path: str, raw_features: Sequence, dev, names: Optional[Sequ
     tcol_t = torch.tensor([cidx[c] for c in txt_cols], dtype=torch.int32, device=dev)
     size = os.path.getsize(path)
     carry_max = 1 << 20
-    bufs = [_Chunk(chunk_bytes + carry_max, dev) for _ in range(2)]
+    # three pinned host buffers (chunk i is read while chunk i - 1 parses and chunk i - 2's bytes stay readable for
+    # its host fix-ups), two device buffers (chunk i + 1 is copied while chunk i parses)
+    hosts = [_Host(chunk_bytes + carry_max) for _ in range(3)]
+    devs = [torch.empty(chunk_bytes + carry_max, dtype=torch.uint8, device=dev) for _ in range(2)]
+    dev_free = [None, None]             # event: the kernels of the chunk that last used the device buffer are done
     copy_stream = torch.cuda.Stream(device=dev)
     cur = torch.cuda.current_stream(dev)
     pool = cf.ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 4)))
@@ -120,85 +128,110 @@ def gpu_csv_dataset(path: str, raw_features: Sequence, dev, names: Optional[Sequ
     num_vals: List[torch.Tensor] = []
     num_ok: List[torch.Tensor] = []
     txt_hash: List[torch.Tensor] = []
-    vocab: List[Dict[int, str]] = [dict() for _ in txt_cols]
-    prof = {"read_wait": 0.0, "parse": 0.0, "host_fix": 0.0}
+    txt_span: List[torch.Tensor] = []
+    prof = {"read_wait": 0.0, "loop": 0.0, "host_fix": 0.0, "sync": 0.0}
     fd = os.open(path, os.O_RDONLY)
 
     def fill(k, off, carry: bytes):
-        b = bufs[k]
-        if b.copied is not None:
-            b.copied.synchronize()      # its previous chunk's copy to the device has finished
+        h = hosts[k]
+        if h.copied is not None:
+            h.copied.synchronize()      # its previous chunk's copy to the device has finished
         c = len(carry)
         if c:
-            b.np[:c] = np.frombuffer(carry, np.uint8)
-        got = _pread_into(fd, b.np[c:], off, min(chunk_bytes, size - off), pool) if off < size else 0
-        b.n = c + got
+            h.np[:c] = np.frombuffer(carry, np.uint8)
+        got = _pread_into(fd, h.np[c:], off, min(chunk_bytes, size - off), pool) if off < size else 0
+        h.n = c + got
+        h.base = off - c
         return off + got
 
+    pending = None                      # the previous chunk: (host buffer, fstart, flags) awaiting its checks
     try:
+        t_loop = time.perf_counter()
         off = skip
-        k = 0
+        i = 0
         fut = reader.submit(fill, 0, off, b"")
         while True:
             t0 = time.perf_counter()
             off = fut.result()
             prof["read_wait"] += time.perf_counter() - t0
-            b = bufs[k]
-            L = b.n
+            h = hosts[i % 3]
+            L = h.n
             if L == 0:
                 break
             eof = off >= size
             if eof:
-                end = L                     # (the last row may lack its newline: _parse_chunk adds its end)
+                end = L                     # (the last row may lack its newline: its end is added below)
             else:
-                tail = b.np[max(0, L - carry_max):L]
+                tail = h.np[max(0, L - carry_max):L]
                 nl = np.flatnonzero(tail == 10)
                 if nl.size == 0:
                     return None             # a row longer than the carry window: generic path
                 end = max(0, L - carry_max) + int(nl[-1]) + 1
-            carry = b.np[end:L].tobytes() if end < L else b""
-            if not eof:                     # read the next chunk while this one is parsed
-                fut = reader.submit(fill, k ^ 1, off, carry)
-            t1 = time.perf_counter()
-            copy_stream.wait_stream(cur)        # the kernels of the chunk that last used this device buffer
+            carry = h.np[end:L].tobytes() if end < L else b""
+            if not eof:                     # read the next chunk while this one is copied and parsed
+                fut = reader.submit(fill, (i + 1) % 3, off, carry)
+            d = i % 2
             with torch.cuda.stream(copy_stream):
-                b.dev[:end].copy_(b.host[:end], non_blocking=True)
+                if dev_free[d] is not None:
+                    copy_stream.wait_event(dev_free[d])
+                devs[d][:end].copy_(h.host[:end], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(copy_stream)
-            b.copied = ev
+            h.copied = ev
             cur.wait_event(ev)
-            res = _parse_chunk(lib, N, b, end, ncols, separator, ncol_t, kind_t, tcol_t, dev, vocab, prof)
+            final_nl = end > 0 and int(h.np[end - 1]) == 10
+            res = _parse_chunk(lib, N, devs[d], h, end, final_nl, ncols, separator, ncol_t, kind_t, tcol_t, dev,
+                               prof, pending)
             if res is None:
                 return None
-            nv, ok, th = res
+            nv, ok, th, sp, pending = res
+            done = torch.cuda.Event()
+            done.record(cur)
+            dev_free[d] = done
             num_vals.append(nv)
             num_ok.append(ok)
-            txt_hash.append(th)
-            prof["parse"] += time.perf_counter() - t1
+            if th is not None:
+                txt_hash.append(th)
+                txt_span.append(sp)
+            i += 1
             if eof:
                 break
-            k ^= 1
+        if pending is not None and not _check_pending(pending, N, prof):
+            return None
+        prof["loop"] = time.perf_counter() - t_loop
     finally:
         os.close(fd)
         reader.shutdown(wait=True)
         pool.shutdown(wait=False)
-        for b in bufs:
-            if b.copied is not None:
-                b.copied.synchronize()
-    n = sum(int(v.shape[1]) for v in num_vals) if num_vals else sum(int(h.shape[1]) for h in txt_hash)
+        for h in hosts:
+            if h.copied is not None:
+                h.copied.synchronize()
+    t_fin = time.perf_counter()
+    n = sum(int(v.shape[1]) for v in num_vals) if num_vals else sum(int(t.shape[1]) for t in txt_hash)
     cols = OrderedDict()
-    for j, c in enumerate(num_cols):
-        v = torch.cat([x[j] for x in num_vals]) if num_vals else torch.empty(0, dtype=torch.int64, device=dev)
-        ok = torch.cat([x[j] for x in num_ok]).bool() if num_ok else torch.empty(0, dtype=torch.bool, device=dev)
-        vals = v if kind_of[c] == "int" else v.view(torch.float64)
-        cols[c] = (vals, None if bool(ok.all()) else ok)
-    for j, c in enumerate(txt_cols):
-        # a text feature whose cells all look like numbers is read as numbers and rendered back by the generic
-        # path (the Arrow path takes a text column only when Arrow types it as strings)
-        if c not in text_columns and vocab[j] and all(_numeric_literal(v) for v in vocab[j].values()):
-            return None
-        h = torch.cat([x[j] for x in txt_hash])
-        cols[c] = _encode_hashes(h, vocab[j], dev)
+    if num_cols:
+        oks = [torch.cat([x[j] for x in num_ok]).bool() for j in range(len(num_cols))]
+        all_ok = torch.stack([o.all() for o in oks]).cpu().tolist() if n else [True] * len(num_cols)   # one read
+        for j, c in enumerate(num_cols):
+            v = torch.cat([x[j] for x in num_vals])
+            if kind_of[c] == "real":
+                v = v.view(torch.float64)
+                if real_dtype != torch.float64:
+                    v = v.to(real_dtype)
+            cols[c] = (v, None if all_ok[j] else oks[j])
+        del num_vals, num_ok
+    if txt_cols:
+        Hh = torch.cat(txt_hash, 1) if len(txt_hash) > 1 else txt_hash[0]           # [nt, n]
+        Sp = torch.cat(txt_span, 1) if len(txt_span) > 1 else txt_span[0]           # [nt, n, 2] file offsets
+        import mmap
+        with open(path, "rb") as fh, mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ) as mm:
+            for j, c in enumerate(txt_cols):
+                codes, voc = _encode_hashes_spans(Hh[j], Sp[j], mm, dev)
+                # a text feature whose cells all look like numbers is read as numbers and rendered back by the
+                # generic path (the Arrow path takes a text column only when Arrow types it as strings)
+                if c not in text_columns and voc and all(_numeric_literal(v) for v in voc):
+                    return None
+                cols[c] = (codes, voc)
     out = OrderedDict()
     for f, c, k in plan:
         if k == "text":
@@ -211,22 +244,47 @@ def gpu_csv_dataset(path: str, raw_features: Sequence, dev, names: Optional[Sequ
             out[f.name] = NumericColumn(f.wtype, vals, ok)
     if os.environ.get("TMOG_INGEST_PROFILE") == "1":
         import sys
+        torch.cuda.synchronize(dev)
+        prof["finish"] = time.perf_counter() - t_fin
         prof["total"] = time.perf_counter() - t_start
-        sys.stderr.write("[gpu-csv] " + " ".join(f"{a}={b:.3f}" for a, b in prof.items()) + f" rows={n}\n")
+        sys.stderr.write("[gpu-csv] " + " ".join(f"{a}={b:.3f}" for a, b in prof.items()) + f" rows={n} chunks={i}\n")
     return Dataset(OrderedDict((f.name, out[f.name]) for f in raw_features), None, n)
 
 
-def _parse_chunk(lib, N, b: _Chunk, end: int, ncols: int, sep: str, ncol_t, kind_t, tcol_t, dev, vocab, prof):
-    buf = b.dev[:end]
+def _check_pending(pending, N, prof) -> bool:
+    """The previous chunk's checks, read after its kernels have run: ragged rows -> the generic path; cells the
+    device parser left to the host are parsed from the chunk's (still intact) host bytes."""
+    h, fstart, flags, vals, ok, slow, nrows, ncol_t, kind_t = pending
+    t0 = time.perf_counter()
+    f = flags.cpu().tolist()             # [ragged rows, slow cells]: one small read
+    prof["sync"] += time.perf_counter() - t0
+    if f[0]:
+        return False                    # ragged rows: pyarrow / pandas decide
+    if f[1]:
+        idx = torch.nonzero(slow.view(-1)).squeeze(1)
+        t0 = time.perf_counter()
+        if not _host_fix(h, fstart, vals, ok, idx, nrows, ncol_t, kind_t):
+            return False
+        prof["host_fix"] += time.perf_counter() - t0
+    return True
+
+
+def _parse_chunk(lib, N, buf_all, h: _Host, end: int, final_nl: bool, ncols: int, sep: str, ncol_t, kind_t, tcol_t,
+                 dev, prof, pending):
+    buf = buf_all[:end]
     ends = torch.nonzero(buf == 10).squeeze(1)
-    if end and (ends.numel() == 0 or int(ends[-1]) != end - 1):     # a final row without its newline
+    if end and not final_nl:            # a final row without its newline
         ends = torch.cat([ends, torch.tensor([end], dtype=torch.int64, device=dev)])
+    # the nonzero above synchronised with this chunk's copy and the previous chunk's kernels: the previous chunk's
+    # flags are ready -- read them now (no extra wait)
+    if pending is not None and not _check_pending(pending, N, prof):
+        return None
     starts = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), ends[:-1] + 1]) if ends.numel() else ends
     # empty lines are skipped (pyarrow ignore_empty_lines); "\r" alone counts as empty
     length = ends - starts
     blank = (length == 0) | ((length == 1) & (buf[starts.clamp_max(max(end - 1, 0))] == 13))
-    if bool(blank.any()):
-        keep = ~blank
+    keep = torch.nonzero(~blank).squeeze(1)
+    if int(keep.numel()) != int(starts.numel()):
         starts, ends = starts[keep], ends[keep]
     nrows = int(starts.numel())
     fstart = torch.empty(nrows, ncols + 1, dtype=torch.int64, device=dev)
@@ -234,42 +292,33 @@ def _parse_chunk(lib, N, b: _Chunk, end: int, ncols: int, sep: str, ncol_t, kind
     st = N.stream(dev)
     N.check(lib.tmog_hip_csv_fields(N.ptr(buf), N.ptr(starts), N.ptr(ends), nrows, ncols, ord(sep), N.ptr(fstart),
                                     N.ptr(nf), st), "csv_fields")
-    if nrows and bool((nf != ncols).any()):
-        return None                         # ragged rows: pyarrow / pandas decide
     nn, nt = int(ncol_t.numel()), int(tcol_t.numel())
-    vals = torch.empty(nn, nrows, dtype=torch.int64, device=dev)
-    ok = torch.empty(nn, nrows, dtype=torch.uint8, device=dev)
-    slow = torch.empty(nn, nrows, dtype=torch.uint8, device=dev)
+    # the kernels write row-major tiles (a wave reads one row's fields); transposed to column-major here
+    vals_rm = torch.empty(nrows, nn, dtype=torch.int64, device=dev)
+    ok_rm = torch.empty(nrows, nn, dtype=torch.uint8, device=dev)
+    slow_rm = torch.empty(nrows, nn, dtype=torch.uint8, device=dev)
     if nn:
         N.check(lib.tmog_hip_csv_parse_num(N.ptr(buf), N.ptr(fstart), N.ptr(nf), nrows, ncols, N.ptr(ncol_t),
-                                           N.ptr(kind_t), nn, N.ptr(vals), N.ptr(ok), N.ptr(slow), st),
+                                           N.ptr(kind_t), nn, N.ptr(vals_rm), N.ptr(ok_rm), N.ptr(slow_rm), st),
                 "csv_parse_num")
-        idx = torch.nonzero(slow.view(-1)).squeeze(1)
-        if idx.numel():                     # the host parses the rare fields the device fast path leaves
-            t0 = time.perf_counter()
-            if not _host_fix(b, fstart, vals, ok, idx, nrows, ncol_t, kind_t):
-                return None
-            prof["host_fix"] += time.perf_counter() - t0
-    th = torch.empty(nt, nrows, dtype=torch.int64, device=dev)
+    vals, ok, slow = vals_rm.t().contiguous(), ok_rm.t().contiguous(), slow_rm.t().contiguous()
+    del vals_rm, ok_rm, slow_rm
+    th = sp = None
     if nt:
-        span = torch.empty(nt, nrows, 2, dtype=torch.int64, device=dev)
+        th_rm = torch.empty(nrows, nt, dtype=torch.int64, device=dev)
+        sp_rm = torch.empty(nrows, nt, 2, dtype=torch.int64, device=dev)
         N.check(lib.tmog_hip_csv_hash_text(N.ptr(buf), N.ptr(fstart), N.ptr(nf), nrows, ncols, N.ptr(tcol_t), nt,
-                                           N.ptr(th), N.ptr(span), st), "csv_hash_text")
-        for j in range(nt):                 # this chunk's new distinct strings: their first cell's bytes
-            h = th[j]
-            u, inv = torch.unique(h, return_inverse=True)
-            first = torch.full((int(u.numel()),), nrows, dtype=torch.int64, device=dev)
-            first.scatter_reduce_(0, inv, torch.arange(nrows, device=dev), reduce="amin")
-            hs, rows = u.cpu().tolist(), first.cpu()
-            new = [i for i, x in enumerate(hs) if x != 0 and x not in vocab[j]]
-            if new:
-                sp = span[j].index_select(0, rows[new].to(dev)).cpu().numpy()
-                for i, (a, e) in zip(new, sp):
-                    vocab[j][hs[i]] = b.np[a:e].tobytes().decode("utf-8", "replace").replace('""', '"')
-    return vals, ok, th
+                                           N.ptr(th_rm), N.ptr(sp_rm), st), "csv_hash_text")
+        th = th_rm.t().contiguous()
+        sp = sp_rm.transpose(0, 1).contiguous()
+        sp += h.base                    # chunk offsets -> file offsets (the bytes are re-read from the file)
+    ragged = (nf != ncols).sum() if nrows else torch.zeros((), dtype=torch.int64, device=dev)
+    nslow = slow.sum(dtype=torch.int64) if nn and nrows else torch.zeros((), dtype=torch.int64, device=dev)
+    flags = torch.stack([ragged.to(torch.int64), nslow])
+    return vals, ok, th, sp, (h, fstart, flags, vals, ok, slow, nrows, ncol_t, kind_t)
 
 
-def _host_fix(b: _Chunk, fstart, vals, ok, idx, nrows, ncol_t, kind_t) -> bool:
+def _host_fix(h: _Host, fstart, vals, ok, idx, nrows, ncol_t, kind_t) -> bool:
     j = (idx // nrows).cpu().numpy()
     r = (idx % nrows).cpu().numpy()
     cols = ncol_t.cpu().numpy()
@@ -279,7 +328,7 @@ def _host_fix(b: _Chunk, fstart, vals, ok, idx, nrows, ncol_t, kind_t) -> bool:
     out_ok = np.empty(len(idx), np.uint8)
     for t, (jj, rr) in enumerate(zip(j, r)):
         c = int(cols[jj])
-        s = b.np[fs[rr, c]:fs[rr, c + 1] - 1].tobytes().decode("utf-8", "replace").strip()
+        s = h.np[fs[rr, c]:fs[rr, c + 1] - 1].tobytes().decode("utf-8", "replace").strip()
         if len(s) >= 2 and s[0] == '"' and s[-1] == '"':
             s = s[1:-1]
         try:
@@ -306,8 +355,9 @@ def _numeric_literal(s: str) -> bool:
         return False
 
 
-def _encode_hashes(h: torch.Tensor, vocab: Dict[int, str], dev):
-    """``(codes int32, vocab)`` from per-row 64-bit hashes (0 = missing), codes by first appearance."""
+def _encode_hashes_spans(h: torch.Tensor, span: torch.Tensor, mm, dev):
+    """``(codes int32, vocab)`` from per-row 64-bit hashes (0 = missing) and the cells' file byte ranges: codes by
+    first appearance; each distinct string read once from the file (memory-mapped) at its first cell."""
     n = int(h.numel())
     if n == 0:
         return torch.empty(0, dtype=torch.int32, device=dev), []
@@ -320,5 +370,7 @@ def _encode_hashes(h: torch.Tensor, vocab: Dict[int, str], dev):
     rank = torch.empty_like(order)
     rank[order] = torch.arange(int(order.numel()), device=dev)
     codes = torch.where(h == 0, torch.full_like(inv, -1), rank[inv]).to(torch.int32)
-    hs = u[order[:n_used]].cpu().tolist()
-    return codes, [vocab[x] for x in hs]
+    rows = first.index_select(0, order[:n_used])
+    spans = span.index_select(0, rows).cpu().numpy()
+    voc = [mm[a:b].decode("utf-8", "replace").replace('""', '"') for a, b in spans]
+    return codes, voc
