@@ -210,16 +210,32 @@ def gpu_csv_dataset(path: str, raw_features: Sequence, dev, names: Optional[Sequ
     n = sum(int(v.shape[1]) for v in num_vals) if num_vals else sum(int(t.shape[1]) for t in txt_hash)
     cols = OrderedDict()
     if num_cols:
-        oks = [torch.cat([x[j] for x in num_ok]).bool() for j in range(len(num_cols))]
-        all_ok = torch.stack([o.all() for o in oks]).cpu().tolist() if n else [True] * len(num_cols)   # one read
-        for j, c in enumerate(num_cols):
-            v = torch.cat([x[j] for x in num_vals])
-            if kind_of[c] == "real":
-                v = v.view(torch.float64)
-                if real_dtype != torch.float64:
-                    v = v.to(real_dtype)
-            cols[c] = (v, None if all_ok[j] else oks[j])
+        # one block per storage type, filled chunk by chunk (a few large copies instead of one concatenation
+        # and conversion per column); every column is a row of its block
+        ri = [j for j, c in enumerate(num_cols) if kind_of[c] == "real"]
+        ii = [j for j, c in enumerate(num_cols) if kind_of[c] == "int"]
+        R = torch.empty(len(ri), n, dtype=real_dtype, device=dev)
+        I = torch.empty(len(ii), n, dtype=torch.int64, device=dev)
+        OK = torch.empty(len(num_cols), n, dtype=torch.bool, device=dev)
+        ri_t = torch.tensor(ri, dtype=torch.long, device=dev)
+        ii_t = torch.tensor(ii, dtype=torch.long, device=dev)
+        r0 = 0
+        for v, o in zip(num_vals, num_ok):
+            r1 = r0 + int(v.shape[1])
+            if ri:
+                R[:, r0:r1] = v.index_select(0, ri_t).view(torch.float64)
+            if ii:
+                I[:, r0:r1] = v.index_select(0, ii_t)
+            OK[:, r0:r1] = o
+            r0 = r1
         del num_vals, num_ok
+        all_ok = OK.all(1).cpu().tolist() if n else [True] * len(num_cols)      # one read for every column
+        pos = {j: k for k, j in enumerate(ri)}
+        pos.update({j: k for k, j in enumerate(ii)})
+        for j, c in enumerate(num_cols):
+            v = R[pos[j]] if kind_of[c] == "real" else I[pos[j]]
+            cols[c] = (v, None if all_ok[j] else OK[j])
+    prof["finish_num"] = time.perf_counter() - t_fin
     if txt_cols:
         Hh = torch.cat(txt_hash, 1) if len(txt_hash) > 1 else txt_hash[0]           # [nt, n]
         Sp = torch.cat(txt_span, 1) if len(txt_span) > 1 else txt_span[0]           # [nt, n, 2] file offsets
@@ -232,6 +248,7 @@ def gpu_csv_dataset(path: str, raw_features: Sequence, dev, names: Optional[Sequ
                 if c not in text_columns and voc and all(_numeric_literal(v) for v in voc):
                     return None
                 cols[c] = (codes, voc)
+        prof["finish_txt"] = time.perf_counter() - t_fin - prof.get("finish_num", 0.0)
     out = OrderedDict()
     for f, c, k in plan:
         if k == "text":
