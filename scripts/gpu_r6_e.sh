@@ -6,6 +6,8 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r6e
 mkdir -p $O
+timeout -k 10 200 python3 -u scripts/bench_dense.py > $O/bench_dense.log 2>&1 || { tail -20 $O/bench_dense.log; exit 1; }
+cat $O/bench_dense.log
 timeout -k 10 400 python3 -u bench.py --models OpXGBoostClassifier --steps 2 --warmup 1 --verbose > $O/xgb_alone.log 2>&1 || { tail -20 $O/xgb_alone.log; exit 1; }
 echo "xgb-alone $(grep -a '^{' $O/xgb_alone.log | grep -o '"value": [0-9.]*\|"FeatureEngineering": [0-9.]*\|"ModelRefit": [0-9.]*' | tr '\n' ' ')"
 timeout -k 10 900 python3 -u bench.py --config regression-100m --max-training-sample 20000000 --steps 1 --warmup 1 --verbose > $O/reg100m_20m.log 2>&1 || { tail -30 $O/reg100m_20m.log; exit 1; }

@@ -374,19 +374,26 @@ def _numeric_literal(s: str) -> bool:
 
 def _encode_hashes_spans(h: torch.Tensor, span: torch.Tensor, mm, dev):
     """``(codes int32, vocab)`` from per-row 64-bit hashes (0 = missing) and the cells' file byte ranges: codes by
-    first appearance; each distinct string read once from the file (memory-mapped) at its first cell."""
+    first appearance; each distinct string read once from the file (memory-mapped) at its first cell. One stable
+    sort: a group's first sorted position holds its first row (no scatter-min onto the few groups of a pick list,
+    whose atomics would contend on a handful of addresses)."""
     n = int(h.numel())
     if n == 0:
         return torch.empty(0, dtype=torch.int32, device=dev), []
-    u, inv = torch.unique(h, return_inverse=True)
-    first = torch.full((int(u.numel()),), n, dtype=torch.int64, device=dev)
-    first.scatter_reduce_(0, inv, torch.arange(n, device=dev), reduce="amin")
-    present = u != 0
+    hs, idx = torch.sort(h, stable=True)
+    new = torch.ones(n, dtype=torch.bool, device=dev)
+    new[1:] = hs[1:] != hs[:-1]
+    starts = torch.nonzero(new).squeeze(1)                  # first sorted position of every distinct hash
+    gid = torch.cumsum(new.to(torch.int32), 0) - 1          # group of every sorted position
+    first = idx.index_select(0, starts)                     # its first row (the sort is stable)
+    present = hs.index_select(0, starts) != 0
     order = torch.argsort(torch.where(present, first, torch.full_like(first, n + 1)))
     n_used = int(present.sum())
     rank = torch.empty_like(order)
     rank[order] = torch.arange(int(order.numel()), device=dev)
-    codes = torch.where(h == 0, torch.full_like(inv, -1), rank[inv]).to(torch.int32)
+    grank = torch.where(present, rank, torch.full_like(rank, -1)).to(torch.int32)
+    codes = torch.empty(n, dtype=torch.int32, device=dev)
+    codes[idx] = grank.index_select(0, gid.long())
     rows = first.index_select(0, order[:n_used])
     spans = span.index_select(0, rows).cpu().numpy()
     voc = [mm[a:b].decode("utf-8", "replace").replace('""', '"') for a, b in spans]
