@@ -127,9 +127,10 @@ class ConcatText(MonoidAggregator):
         self.separator = separator
 
     def plus(self, a, b):
-        if not a:
-            return b if b else a
-        if not b:
+        # ConcatTextWithSeparator's monoid: only a missing value is the zero -- an empty string is a value
+        if a is None:
+            return b
+        if b is None:
             return a
         return f"{a}{self.separator}{b}"
 

@@ -132,10 +132,14 @@ class _GroupedReader(DataReader):
         for f in raw_features:
             st = f.origin_stage
             agg = st.aggregator or A.default_aggregator(f.wtype)
-            win = st.aggregate_window if st.aggregate_window is not None else windows[1 if f.is_response else 0]
-            mask = _event_mask(ts, cutoff_ev, f.is_response, win) if n else np.zeros(0, bool)
+            # the generator stage's response flag selects the event window (FeatureAggregator.extract: the stage
+            # builds its aggregator with outputIsResponse), so a predictor copy of a response feature aggregates as
+            # the response does
+            resp = bool(getattr(st, "output_is_response", f.is_response))
+            win = st.aggregate_window if st.aggregate_window is not None else windows[1 if resp else 0]
+            mask = _event_mask(ts, cutoff_ev, resp, win) if n else np.zeros(0, bool)
             vals = [st.extract(r) for r in recs_s]
-            out = self._aggregate(agg, vals, mask, seg, len(starts), f.is_response, ts, dev, f.wtype)
+            out = self._aggregate(agg, vals, mask, seg, len(starts), resp, ts, dev, f.wtype)
             if isinstance(out, NumericColumn):          # device-side numeric monoid
                 if len(keep_groups) != len(starts) or np.any(np.asarray(keep_groups) != np.arange(len(starts))):
                     out = out.take(torch.as_tensor(np.asarray(keep_groups, np.int64), device=dev))

@@ -54,6 +54,8 @@ class PassengerFeatures:
             lambda p: None if p.get("survived") is None else p["survived"] == 1).as_response()
         self.boardedTime = FB.Date("boardedTime").extract(
             lambda p: None if p.get("boarded") is None else int(p["boarded"])).as_predictor()
+        self.boardedTimeAsDateTime = FB.DateTime("boardedTimeAsDateTime").extract(
+            lambda p: None if p.get("boarded") is None else int(p["boarded"])).as_predictor()
 
     @property
     def raw_features(self) -> List:
