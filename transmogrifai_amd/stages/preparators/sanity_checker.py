@@ -139,8 +139,9 @@ class SanityChecker(BinaryEstimator):
                  "categorical_label": None, "sample_seed": 42}
 
     # parameter domains (SanityChecker.scala param validators: ParamValidators.inRange / gtEq)
-    _ranges = {"check_sample": (0.0, 1.0, False), "min_correlation": (0.0, 1.0, True),
-               "max_correlation": (0.0, 1.0, True), "max_feature_correlation": (0.0, 1.0, True),
+    # (the correlation thresholds accept [-0.1, 1.1]: 1.1 switches a rule off, SanityChecker.scala:92-116)
+    _ranges = {"check_sample": (0.0, 1.0, False), "min_correlation": (-0.1, 1.1, True),
+               "max_correlation": (-0.1, 1.1, True), "max_feature_correlation": (-0.1, 1.1, True),
                "max_cramers_v": (0.0, 1.0, True), "max_rule_confidence": (0.0, 1.0, True),
                "min_required_rule_support": (0.0, 1.0, True)}
 

@@ -120,12 +120,20 @@ class RandomBinary(RandomData):
 # ------------------------------------------------------------------------------------------------ text
 _ALNUM = string.ascii_letters + string.digits
 _COUNTRIES = ["United States", "Canada", "Mexico", "France", "Germany", "Italy", "Spain", "Japan", "China",
-              "India", "Brazil", "Argentina", "Australia", "Egypt", "Kenya", "Norway", "Sweden", "Poland"]
+              "India", "Brazil", "Argentina", "Australia", "Egypt", "Kenya", "Norway", "Sweden", "Poland",
+              "Portugal", "Ireland", "Netherlands", "Belgium", "Switzerland", "Austria", "Denmark", "Finland",
+              "Greece", "Turkey", "Russia", "Ukraine", "Romania", "Hungary", "Czech Republic", "Chile", "Peru",
+              "Colombia", "Venezuela", "Cuba", "Nigeria", "Ghana", "Morocco", "Algeria", "Ethiopia", "South Africa",
+              "Israel", "Saudi Arabia", "Iran", "Iraq", "Pakistan", "Bangladesh", "Thailand", "Vietnam",
+              "Indonesia", "Philippines", "Malaysia", "Singapore", "South Korea", "New Zealand", "Iceland", "Estonia"]
 _STATES = ["AL", "AK", "AZ", "AR", "CA", "CO", "CT", "DE", "FL", "GA", "HI", "ID", "IL", "IN", "IA", "KS", "KY",
            "LA", "ME", "MD", "MA", "MI", "MN", "MS", "MO", "MT", "NE", "NV", "NH", "NJ", "NM", "NY", "NC", "ND",
            "OH", "OK", "OR", "PA", "RI", "SC", "SD", "TN", "TX", "UT", "VT", "VA", "WA", "WV", "WI", "WY"]
 _CITIES = ["San Jose", "San Francisco", "Los Angeles", "San Diego", "Sacramento", "Oakland", "Fresno",
-           "Palo Alto", "Berkeley", "Santa Clara", "Sunnyvale", "Mountain View", "Cupertino", "Irvine"]
+           "Palo Alto", "Berkeley", "Santa Clara", "Sunnyvale", "Mountain View", "Cupertino", "Irvine", "Seattle",
+           "Portland", "Boston", "New York", "Chicago", "Austin", "Denver", "Phoenix", "Dallas", "Houston",
+           "Atlanta", "Miami", "Detroit", "Minneapolis", "Philadelphia", "Pittsburgh", "Baltimore", "Nashville",
+           "Las Vegas", "Salt Lake City", "Albuquerque", "Tucson", "Omaha", "Kansas City", "St. Louis", "Cleveland"]
 _STREETS = ["Almaden Blvd", "Santa Clara St", "First St", "Market St", "Park Ave", "Story Rd", "Tully Rd",
             "King Rd", "Capitol Expy", "Meridian Ave", "Winchester Blvd", "Bascom Ave"]
 
