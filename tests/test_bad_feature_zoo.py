@@ -117,3 +117,70 @@ def test_null_indicator_leakage_drops_the_parent_features():
                      ("expectedRevenue", T.Currency, rev)])
     assert sum(d.startswith("expectedRevenue") for d in summ["dropped"]) == 2
     assert sum(d.startswith("real") for d in summ["dropped"]) == 2
+
+
+def _summary_feats(ds, label, preds, **sc):
+    from transmogrifai_amd.workflow.workflow import OpWorkflow
+    vec = transmogrify(preds)
+    chk = SanityChecker(check_sample=1.0, remove_bad_features=True, **sc).set_input(label, vec).get_output()
+    model = OpWorkflow().set_result_features(chk).set_input_dataset(ds).train()
+    return model.get_origin_stage_of(chk).metadata["summary"]
+
+
+def test_hashed_text_null_leakage_drops_every_hash_column():
+    """``:401-472``: a label that is "text is present" -- all hashed columns of the text (and its null indicator)
+    go; the same for one key of a text map."""
+    from transmogrifai_amd.stages.feature.transmogrifier import TransmogrifierDefaults as TD
+    city = _take(RandomText.cities(), 0.4, 1)
+    real = _take(RandomReal.uniform(0.0, 1.0), 0.5, 2)
+    text = _take(RandomText.strings(1, 10), 0.4, 3)
+    summ = _summary([1.0 if t is not None else 0.0 for t in text],
+                    [("city", T.City, city), ("real", T.Real, real), ("text", T.Text, text)])
+    assert sum(d.startswith("text") for d in summ["dropped"]) == TD.DefaultNumOfFeatures + 1
+    tmap = _take(RandomMap.of(RandomText.strings(1, 10), 0, 3, ftype=T.TextMap), 0.0, 4)
+    summ2 = _summary([1.0 if "k1" in (m or {}) else 0.0 for m in tmap],
+                     [("city", T.City, city), ("real", T.Real, real), ("textmap", T.TextMap, tmap)])
+    assert sum(d.startswith("textmap_k1") for d in summ2["dropped"]) == TD.DefaultNumOfFeatures + 1
+
+
+def test_pivoted_text_correlation_leakage():
+    """``:474-547``: low-cardinality text is pivoted; the label is "text == alpha" -- all 6 pivoted columns go (4
+    values, other, null); the same for one key of a text map."""
+    city = _take(RandomText.cities(), 0.3, 1)
+    real = _take(RandomReal.uniform(0.0, 1.0), 0.3, 2)
+    dom = ["alpha", "beta", "gamma", "delta"]
+    text = _take(RandomText.text_from_domain(dom), 0.3, 3)
+    summ = _summary([1.0 if t == "alpha" else 0.0 for t in text],
+                    [("city", T.City, city), ("real", T.Real, real), ("text", T.Text, text)])
+    assert sum(d.startswith("text") for d in summ["dropped"]) == 6
+    tmap = _take(RandomMap.of(RandomText.text_from_domain(dom), 0, 2, ftype=T.TextMap), 0.0, 4)
+    summ2 = _summary([1.0 if (m or {}).get("k0") == "alpha" else 0.0 for m in tmap],
+                     [("city", T.City, city), ("real", T.Real, real), ("textmap", T.TextMap, tmap)])
+    assert sum(d.startswith("textmap") for d in summ2["dropped"]) == 6
+
+
+def test_binned_numeric_leakage():
+    """``:549-603``: expected revenue = binary x currency; its 3-bin pick list (null / zero / non-zero) leaks the
+    label -- its 5 columns (3 bins, other, null) go."""
+    from transmogrifai_amd.testkit.random_data import RandomBinary
+    uid.reset(0)
+    b = _take(RandomBinary(0.5), 0.3, 1)
+    cur = _take(RandomReal.log_normal(10.0, 1.0, ftype=T.Currency), 0.0, 2)
+    er = [None if x is None else (1.0 if x else 0.0) * c for x, c in zip(b, cur)]
+    ds, feats = TestFeatureBuilder.of(("label", T.RealNN, [1.0 if x else 0.0 for x in b]), ("binary", T.Binary, b),
+                                      ("currency", T.Currency, cur), ("expectedRevenue", T.Currency, er),
+                                      response="label")
+    label, rb, rc, rer = feats
+    binned = rer.map(lambda v: "null" if v is None else ("nonZero" if v != 0 else "zero"), output_type=T.PickList)
+    summ = _summary_feats(ds, label, [rb, rc, rer, binned])
+    assert sum(d.startswith("expectedRevenue_1-stagesApplied_PickList") for d in summ["dropped"]) == 5
+
+
+def test_no_cramers_v_against_a_numeric_label():
+    """``:628-661``: regression label -- only the pick list's always-empty "other" column goes."""
+    city, country, pick, _ = _base_cols()
+    lab = _take(RandomReal.log_normal(10.0, 1.0, ftype=T.RealNN), 0.0, 9)
+    summ = _summary(lab, [("city", T.City, city), ("country", T.Country, country), ("picklist", T.PickList, pick)],
+                    max_feature_correlation=1.1)
+    assert sum(d.startswith("picklist") for d in summ["dropped"]) == 1
+    assert len(summ["dropped"]) == 1

@@ -144,6 +144,13 @@ def _rand_string(r: np.random.Generator, alphabet: str, lo: int, hi: int) -> str
     return "".join(alphabet[i] for i in idx)
 
 
+def _between(r, lo: int, hi: int) -> int:
+    """The reference's ``RandomStream.randomBetween``: uniform in [lo, hi) (hi exclusive; lo when hi <= lo)."""
+    lo = max(0, lo)
+    hi = max(1, max(lo, hi))
+    return lo if lo == hi else lo + int(r.integers(0, hi - lo))
+
+
 def _select(domain: Sequence[str], dist: Sequence[float] = ()):
     dom = list(domain)
     if dist:
@@ -262,14 +269,14 @@ class RandomList(RandomData):
     @staticmethod
     def of_texts(texts: RandomData, min_len: int = 0, max_len: int = 5):
         def prod(r):
-            n = int(r.integers(min_len, max_len + 1))
+            n = _between(r, min_len, max_len)
             return [v for v in texts.take(n) if v is not None]
         return RandomList(prod, T.TextList)
 
     @staticmethod
     def of_dates(dates: RandomIntegral, min_len: int = 0, max_len: int = 5, ftype=T.DateList):
         def prod(r):
-            n = int(r.integers(min_len, max_len + 1))
+            n = _between(r, min_len, max_len)
             return sorted(v for v in dates.take(n) if v is not None)
         return RandomList(prod, ftype)
 
@@ -288,7 +295,7 @@ class RandomSet(RandomData):
         vals = list(values)
 
         def prod(r):
-            n = int(r.integers(min_len, min(max_len, len(vals)) + 1))
+            n = min(_between(r, min_len, max_len), len(vals))
             return set(vals[i] for i in r.choice(len(vals), n, replace=False))
         return RandomSet(prod, T.MultiPickList)
 
@@ -300,13 +307,13 @@ class RandomMap(RandomData):
     def of(values: RandomData, min_size: int = 0, max_size: int = 5, ftype=T.RealMap,
            key_prefix: str = "k"):
         def prod(r):
-            n = int(r.integers(min_size, max_size + 1))
-            keys = r.choice(max(max_size, 1) * 2, n, replace=False)
+            # keys "k0", "k1", ... by position, as the reference's RandomMap (RandomMap.scala asMap)
+            n = _between(r, min_size, max_size)
             out = {}
-            for k in keys:
+            for k in range(n):
                 v = next(values)
                 if v is not None:
-                    out[f"{key_prefix}{int(k)}"] = v
+                    out[f"{key_prefix}{k}"] = v
             return out
         return RandomMap(prod, ftype)
 
