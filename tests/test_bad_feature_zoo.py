@@ -184,3 +184,68 @@ def test_no_cramers_v_against_a_numeric_label():
                     max_feature_correlation=1.1)
     assert sum(d.startswith("picklist") for d in summ["dropped"]) == 1
     assert len(summ["dropped"]) == 1
+
+
+def test_multipicklist_modified_cramers_v():
+    """``:664-718``: a label set by one multi-pick-list choice -- every multi-pick-list column (topK, other, null)
+    has categorical statistics."""
+    from transmogrifai_amd.stages.feature.transmogrifier import TransmogrifierDefaults as TD
+    rng = np.random.default_rng(5)
+    cur = _take(RandomReal.log_normal(10.0, 1.0, ftype=T.Currency), 0.0, 1)
+    dom = ["Strawberry Milk", "Chocolate Milk", "Soy Milk", "Almond Milk"]
+    plm = _take(RandomMap.of(RandomText.pick_lists(dom), 1, 3, ftype=T.PickListMap), 0.0, 2)
+    mpl = _take(RandomSet.of([str(i) for i in range(20)], 0, 2), 0.0, 3)
+    lab = [3.0 if "3" in (m or ()) else float(rng.integers(0, 3)) for m in mpl]
+    summ = _summary(lab, [("currency", T.Currency, cur), ("multipicklist", T.MultiPickList, mpl),
+                          ("picklistMap", T.PickListMap, plm)])
+    cats = [c for s in summ["categoricalStats"] for c in s["categoricalFeatures"]]
+    assert sum(c.startswith("multipicklist") for c in cats) == TD.TopK + 2
+
+
+def test_sibling_correlations_combined_by_absolute_value():
+    """``:765-805``: label = pick list in {A, B} (random for null); with Cramér's V off (max 1.0) the siblings'
+    correlations are combined by absolute value -- the pick list's 5 columns go, nothing else."""
+    rng = np.random.default_rng(6)
+    pick = _take(RandomText.pick_lists(["A", "B", "C"]), 0.2, 1)
+    cur = _take(RandomReal.log_normal(10.0, 1.0, ftype=T.Currency), 0.2, 2)
+    lab = [1.0 if p in ("A", "B") else 0.0 if p == "C" else float(rng.integers(0, 2)) for p in pick]
+    summ = _summary(lab, [("picklist", T.PickList, pick), ("currency", T.Currency, cur)], max_cramers_v=1.0,
+                    max_correlation=0.6)
+    assert all(d.startswith("picklist") for d in summ["dropped"])
+    assert len(summ["dropped"]) == 5
+
+
+def test_titanic_body_rule_confidence():
+    """``:807-848``: a mostly-empty ID whose presence implies the label (high rule confidence with enough support)
+    -- both columns derived from it go."""
+    rng = np.random.default_rng(7)
+    body = _take(RandomText.ids(), 0.9, 1)
+    boat = _take(RandomText.pick_lists(["A", "B", "C"]), 0.8, 2)
+    cur = _take(RandomReal.log_normal(10.0, 1.0, ftype=T.Currency), 0.8, 3)
+    lab = [1.0 if b is not None else (0.0 if bo is not None else float(rng.integers(0, 2)))
+           for b, bo in zip(body, boat)]
+    summ = _summary(lab, [("body", T.ID, body), ("boat", T.PickList, boat), ("currency", T.Currency, cur)],
+                    max_rule_confidence=0.99, min_required_rule_support=0.05)
+    assert sum(d.startswith("body") for d in summ["dropped"]) == 2
+
+
+@pytest.mark.parametrize("binning", ["bucketize", "auto_bucketize"])
+def test_binned_vector_leakage_drops_the_parent(binning):
+    """``:605-626`` (``expectedRevenueLeakage``): the revenue binned straight to an OPVector (a numeric bucketizer
+    at 0, or a decision-tree bucketizer on the label) leaks the label -- the two raw revenue columns and the bins
+    go (4 columns starting with expectedRevenue)."""
+    from transmogrifai_amd.testkit.random_data import RandomBinary
+    uid.reset(0)
+    b = _take(RandomBinary(0.5), 0.3, 1)
+    cur = _take(RandomReal.log_normal(10.0, 1.0, ftype=T.Currency), 0.0, 2)
+    er = [None if x is None else (1.0 if x else 0.0) * c for x, c in zip(b, cur)]
+    ds, feats = TestFeatureBuilder.of(("label", T.RealNN, [1.0 if x else 0.0 for x in b]), ("binary", T.Binary, b),
+                                      ("currency", T.Currency, cur), ("expectedRevenue", T.Currency, er),
+                                      response="label")
+    label, rb, rc, rer = feats
+    if binning == "bucketize":
+        binned = rer.bucketize(track_nulls=False, splits=[float("-inf"), 0.0, float("inf")], split_inclusion="Right")
+    else:
+        binned = rer.auto_bucketize(label, track_nulls=False)
+    summ = _summary_feats(ds, label, [rb, rc, rer, binned])
+    assert sum(d.startswith("expectedRevenue") for d in summ["dropped"]) == 4
