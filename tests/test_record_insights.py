@@ -162,3 +162,242 @@ def test_loco_100k_rows_on_device():
         assert list(g) == list(e)
         for k in e:
             assert np.allclose([v for _, v in json.loads(g[k])], [v for _, v in json.loads(e[k])], atol=1e-9)
+
+
+# ---------------------------------------------------------------- RecordInsightsLOCOTest.scala scenarios (:99-292)
+def _indexed_meta(name, size):
+    """``addMetaData`` (RecordInsightsLOCOTest.scala:349): column i has parent name / type / grouping /
+    indicator all ``str(i)``, so its column name is ``i_i_i_i``."""
+    from transmogrifai_amd.data.vector_metadata import FeatureHistory, OpVectorColumnMetadata, OpVectorMetadata
+    cols = [OpVectorColumnMetadata((str(i),), (str(i),), str(i), str(i), index=i) for i in range(size)]
+    hist = {str(i): FeatureHistory((f"a_{i}",), (f"b_{i}",)) for i in range(size)}
+    return OpVectorMetadata(name, cols, hist)
+
+
+def _vector_ds(vectors, labels):
+    from transmogrifai_amd.data.columns import VectorColumn
+    ds, (f, l) = TestFeatureBuilder.of(("features", T.OPVector, vectors), ("labels", T.RealNN, labels),
+                                       response="labels")
+    X = ds["features"].values
+    ds = ds.with_column("features", VectorColumn(X, _indexed_meta("features", X.shape[1])))
+    return ds, f, l
+
+
+def _random_sparse(n, d=40):
+    from transmogrifai_amd.testkit.random_data import RandomReal, RandomVector
+    return list(RandomVector.sparse(RandomReal.normal(), d).limit(n))
+
+
+def _insights(loco, ds):
+    return [parse_insights(m) for m in loco.transform(ds)[loco.get_output().name].to_list()]
+
+
+def test_loco_random_features_binary_logistic_regression():
+    """:99 -- 40 dense-filled columns, binary LR: 20 insights per record, each with a non-zero change for
+    both score columns."""
+    from transmogrifai_amd.models.linear import OpLogisticRegression
+    from transmogrifai_amd.testkit.random_data import RandomIntegral
+    labels = [float(v) for v in RandomIntegral.integrals(0, 2).take(1000)]
+    ds, f, l = _vector_ds(_random_sparse(1000), labels)
+    model = OpLogisticRegression().set_input(l, f).fit(ds)
+    parsed = _insights(RecordInsightsLOCO(model).set_input(f), ds)
+    assert len(parsed) == 1000
+    for p in parsed:
+        assert len(p) == 20
+        assert sum(1 for v in p.values() if any(i == 1 for i, _ in v)) == 20
+        assert all(abs(x) > 0 for v in p.values() for _, x in v)
+
+
+def test_loco_random_features_multiclass_random_forest():
+    """:117 -- five classes, top K 2: every record gets 2 insights, each carrying the change of all five
+    class scores and no sixth."""
+    from transmogrifai_amd.models.trees import OpRandomForestClassifier
+    from transmogrifai_amd.testkit.random_data import RandomIntegral
+    labels = [float(v) for v in RandomIntegral.integrals(0, 5).take(1000)]
+    ds, f, l = _vector_ds(_random_sparse(1000), labels)
+    model = OpRandomForestClassifier().set_input(l, f).fit(ds)
+    parsed = _insights(RecordInsightsLOCO(model, top_k=2).set_input(f), ds)
+    for p in parsed:
+        assert len(p) == 2
+        for c in range(5):
+            assert sum(1 for v in p.values() if any(i == c for i, _ in v)) == 2
+        assert not any(i == 5 for v in p.values() for i, _ in v)
+
+
+def test_loco_random_features_linear_regression():
+    """:138 -- a regression model has one score column: 20 insights, all on score index 0, all non-zero."""
+    from transmogrifai_amd.models.linear import OpLinearRegression
+    from transmogrifai_amd.testkit.random_data import RandomReal
+    labels = [float(v) for v in RandomReal.normal().take(1000)]
+    ds, f, l = _vector_ds(_random_sparse(1000), labels)
+    model = OpLinearRegression().set_input(l, f).fit(ds)
+    parsed = _insights(RecordInsightsLOCO(model).set_input(f), ds)
+    for p in parsed:
+        assert len(p) == 20
+        assert all(i == 0 and abs(x) > 0 for v in p.values() for i, x in v)
+
+
+# name, age, height, height_null, isBlueEyed, gender, testFeatNegCor (RecordInsightsLOCOTest.scala:63-89)
+_SANITY_ROWS = [
+    ("a", 32, 5.0, 0, 0.9, 0.5, 0), ("b", 32, 4.0, 1, 0.1, 0, 0.1), ("a", 32, 6.0, 0, 0.8, 0.5, 0),
+    ("a", 32, 5.5, 0, 0.85, 0.5, 0), ("b", 32, 5.4, 1, 0.05, 0, 0.1), ("b", 32, 5.4, 1, 0.2, 0, 0.1),
+    ("a", 32, 5.0, 0, 0.99, 0.5, 0), ("b", 32, 4.0, 0, 0.0, 0, 0.1), ("a", 32, 6.0, 1, 0.7, 0.5, 0),
+    ("a", 32, 5.5, 0, 0.8, 0.5, 0), ("b", 32, 5.4, 1, 0.1, 0, 0.1), ("b", 32, 5.4, 1, 0.05, 0, 0.1),
+    ("a", 32, 5.0, 0, 1, 0.5, 0), ("b", 32, 4.0, 1, 0.1, 0, 0.1), ("a", 32, 6.0, 1, 0.9, 0.5, 0),
+    ("a", 32, 5.5, 0, 1, 0.5, 0), ("b", 32, 5.4, 1, 0.2, 0, 0.1), ("b", 32, 5.4, 1, 0.3, 0, 0.1),
+    ("a", 32, 5.0, 0, 0.6, 0.5, 0), ("b", 32, 4.0, 1, 0.1, 0, 0.1), ("a", 32, 6.0, 0, 0.9, 0.5, 0),
+    ("a", 32, 5.5, 0, 1, 0.5, 0), ("b", 32, 5.4, 1, 0.05, 0, 0.1), ("b", 32, 5.4, 1, 0.3, 0, 0.1),
+    ("b", 32, 5.4, 1, 0.05, 0, 0.1), ("b", 32, 5.4, 1, 0.4, 0, 0.1)]
+
+
+def _sanity_lr():
+    from transmogrifai_amd.models.linear import OpLogisticRegression
+    vecs = [[float(r[1]), float(r[2]), float(r[4]), float(r[5]), float(r[6])] for r in _SANITY_ROWS]
+    ds, f, l = _vector_ds(vecs, [float(r[3]) for r in _SANITY_ROWS])
+    return ds, f, OpLogisticRegression().set_input(l, f).fit(ds)
+
+
+def test_loco_most_predictive_feature():
+    """:156 -- top K 1: the top column is gender (3_3_3_3) or height (1_1_1_1), and for a binary model the
+    two class changes are equal and opposite."""
+    ds, f, model = _sanity_lr()
+    for p in _insights(RecordInsightsLOCO(model, top_k=1).set_input(f), ds):
+        (name, v), = p.items()
+        assert name in ("3_3_3_3", "1_1_1_1"), p
+        assert abs(v[0][1] + v[1][1]) < 1e-5
+
+
+def test_loco_most_predictive_features_positive_negative():
+    """:176 -- top K positives + top K negatives: height leads or gender closes every record's map."""
+    ds, f, model = _sanity_lr()
+    loco = RecordInsightsLOCO(model, top_k_strategy="positive and negative").set_input(f)
+    for p in _insights(loco, ds):
+        names = list(p)
+        assert names[0] == "1_1_1_1" or names[-1] == "3_3_3_3", names
+
+
+@pytest.fixture(scope="module")
+def strongly_related():
+    """:193-226 -- the label is 1 exactly when the picklist is A, B or C; country (30 % empty), picklist (10 %
+    empty) and a log-normal currency (30 % empty) transmogrified, a random forest on top, LOCO top K 10."""
+    from transmogrifai_amd.dsl import transmogrify
+    from transmogrifai_amd.models.trees import OpRandomForestClassifier
+    from transmogrifai_amd.testkit.random_data import RandomReal, RandomText
+    from transmogrifai_amd.workflow.workflow import OpWorkflow
+    n = 1000
+    country = RandomText.countries().with_probability_of_empty(0.3).take(n)
+    pick = RandomText.pick_lists(["A", "B", "C", "D", "E", "F", "G"]).with_probability_of_empty(0.1).take(n)
+    cur = RandomReal.log_normal(10.0, 1.0, T.Currency).with_probability_of_empty(0.3).take(n)
+    label = [1.0 if p in ("A", "B", "C") else 0.0 for p in pick]
+    ds, (fc, fp, fu, fl) = TestFeatureBuilder.of(("country", T.Country, country), ("picklist", T.PickList, pick),
+                                                 ("currency", T.Currency, cur), ("label", T.RealNN, label),
+                                                 response="label")
+    vec = transmogrify([fc, fp, fu])
+    full = OpWorkflow().set_result_features(vec, fl).set_input_dataset(ds).train().score(
+        keep_intermediate_features=True)
+    model = OpRandomForestClassifier().set_input(fl, vec).fit(full)
+    parsed = _insights(RecordInsightsLOCO(model, top_k=10).set_input(vec), full)
+    meta = full[vec.name].metadata
+    return n, parsed, meta, model
+
+
+def _importance_split(parsed, meta):
+    d = meta.size
+    tot, cnt = np.zeros(d), np.zeros(d)
+    idx_of = {c.make_col_name(): c.index for c in meta.columns}
+    for m in parsed:
+        for k, v in m.items():
+            tot[idx_of[k]] += v[-1][1]
+            cnt[idx_of[k]] += 1
+    mean = np.where(cnt > 0, tot / np.maximum(cnt, 1), np.nan)
+    nan = set(np.flatnonzero(np.isnan(mean)).tolist())
+    abc = {c.index for c in meta.columns if c.indicator_value in ("A", "B", "C")} - nan
+    other = set(range(d)) - abc - nan
+    abc_avg = abs(sum(mean[i] for i in abc)) / len(abc)
+    other_avg = abs(sum(mean[i] for i in other)) / len(other)
+    var, vc = np.zeros(d), np.zeros(d)
+    for m in parsed:
+        for k, v in m.items():
+            i = idx_of[k]
+            var[i] += (v[-1][1] - (abc_avg if i in abc else other_avg)) ** 2
+            vc[i] += 1
+    var = np.where(vc > 1, var / np.maximum(vc, 1), np.nan)
+    abc_var = abs(sum(var[i] for i in abc)) / len(abc)
+    other_var = abs(sum(var[i] for i in other)) / len(other)
+    return abc, other, abc_avg, other_avg, abc_var, other_var
+
+
+def test_loco_strongly_related_one_insight_per_record(strongly_related):
+    n, parsed, meta, _ = strongly_related
+    assert len(parsed) == n
+    # country and picklist contribute one non-zero column each; currency its value or its null indicator
+    assert all(1 <= len(p) <= 4 for p in parsed)
+
+
+def test_loco_strongly_related_abc_dominate(strongly_related):
+    n, parsed, meta, _ = strongly_related
+    _, _, abc_avg, other_avg, abc_var, other_var = _importance_split(parsed, meta)
+    assert abc_avg > 3 * other_avg
+    t = abs(abc_avg - other_avg) / math.sqrt((abc_var + other_var) / n)
+    assert t > 10.0
+
+
+def test_loco_strongly_related_agrees_with_forest_importances(strongly_related):
+    """:283 -- the A/B/C-to-other ratio of mean LOCO strengths and of the forest's feature importances differ
+    by less than 0.8 of their mean."""
+    n, parsed, meta, model = strongly_related
+    abc, other, abc_avg, other_avg, _, _ = _importance_split(parsed, meta)
+    imp = np.asarray(model.learner.feature_contributions(model.state, meta.size), np.float64).reshape(-1)
+    abc_rf = sum(imp[i] for i in abc) / len(abc)
+    other_rf = sum(imp[i] for i in other) / len(other)
+    r_ins, r_rf = abs(abc_avg / other_avg), abs(abc_rf / other_rf)
+    assert abs(r_ins - r_rf) * 2 / (r_ins + r_rf) < 0.8
+
+
+@pytest.mark.parametrize("agg", ["Avg", "LeaveOutVector"])
+def test_loco_aggregates_text_and_date_groups_like_manual_loco(agg):
+    """:296-346 + ``assertAggregatedWithPredicate`` (:458) -- for a binary LR over plain, hashed-text and
+    date-circle columns: every map's class changes sum to 0, and each text / date group's insight equals the
+    manual computation (Avg: the mean of the single-column LOCOs of the group; LeaveOutVector: the record
+    re-scored with the whole group zeroed), for every record whose group insight is reported."""
+    from transmogrifai_amd.models.linear import OpLogisticRegression
+    scored, vec, lr = _fit_mixed(OpLogisticRegression, n=300, seed=7)
+    loco = RecordInsightsLOCO(lr, top_k=40, vector_aggregation_strategy=agg).set_input(vec)
+    out = [{k: json.loads(v) for k, v in m.items()} for m in loco.transform(scored)[loco.get_output().name].to_list()]
+    X = scored[vec.name].values.to(torch.float64)
+    hist = scored[vec.name].metadata.column_history()
+    for m in out:
+        for v in m.values():
+            assert abs(sum(x for _, x in v)) < 1e-10
+    w = torch.as_tensor(np.asarray(lr.state["coefficients"]), dtype=torch.float64)
+    b = float(lr.state["intercept"])
+    score = lambda Z: torch.sigmoid(Z @ w + b)
+    groups = {}
+    for h in hist:
+        types = {t.rsplit(".", 1)[-1] for t in h["parentFeatureType"]}
+        if "Text" in types and h["indicatorValue"] is None and h["descriptorValue"] is None:
+            groups.setdefault(("text", h["parentFeatureOrigins"][0]), []).append(h["index"])
+        elif "DateTime" in types and h["descriptorValue"] is not None:
+            groups.setdefault(("date", h["descriptorValue"].split("_")[-1]), []).append(h["index"])
+    assert any(k[0] == "text" for k in groups) and any(k[0] == "date" for k in groups)
+    base = score(X)
+    checked = 0
+    for (_, _), idx in groups.items():
+        ix = torch.as_tensor(idx)
+        if agg == "Avg":
+            locos = []
+            for j in idx:
+                Z = X.clone()
+                Z[:, j] = 0
+                locos.append(base - score(Z))
+            exp1 = torch.stack(locos).sum(0) / len(idx)
+        else:
+            Z = X.clone()
+            Z[:, ix] = 0
+            exp1 = base - score(Z)
+        for i, m in enumerate(out):
+            hit = [v for k, v in m.items() if json.loads(k)["index"] in idx]
+            if hit:
+                assert abs(hit[0][1][1] - float(exp1[i])) < 1e-10
+                checked += 1
+    assert checked > 0

@@ -326,11 +326,14 @@ class RandomVector(RandomData):
         return RandomVector(lambda r: [float(v) if v is not None else 0.0 for v in values.take(length)], T.OPVector)
 
     @staticmethod
-    def sparse(values: RandomReal, length: int, density: float = 0.1):
+    def sparse(values: RandomReal, length: int, density: Optional[float] = None):
+        """``RandomVector.sparse`` (``RandomVector.scala:73``, ``asSparse`` :151): ``length`` draws of ``values``,
+        an empty draw leaving its position zero -- the sparsity comes from ``values.with_probability_of_empty``.
+        ``density`` additionally keeps each position with that probability."""
         def prod(r):
             out = [0.0] * length
             for i in range(length):
-                if r.random() < density:
+                if density is None or r.random() < density:
                     v = next(values)
                     out[i] = float(v) if v is not None else 0.0
             return out
