@@ -98,7 +98,15 @@ class ScalarMathTransformer(UnaryTransformer):
         return self.transform_columns(NumericColumn.from_values(T.Real, [a])).row(0)
 
 
-_UNARY = {"abs": torch.abs, "ceil": torch.ceil, "floor": torch.floor, "round": torch.round, "exp": torch.exp,
+def java_round(x: torch.Tensor) -> torch.Tensor:
+    """``math.round`` (Java ``Math.round``): the nearest integer, halves toward +inf (2.5 -> 3, -2.5 -> -2) --
+    not torch's half-to-even. Written as floor + a compare of the exact fraction ``x - floor(x)``, so
+    0.49999999999999994 rounds to 0 as in Java (``floor(x + 0.5)`` would give 1)."""
+    f = torch.floor(x)
+    return torch.where(x - f >= 0.5, f + 1, f)
+
+
+_UNARY = {"abs": torch.abs, "ceil": torch.ceil, "floor": torch.floor, "round": java_round, "exp": torch.exp,
           "sqrt": torch.sqrt, "log": None, "sigmoid": torch.sigmoid}
 
 
@@ -111,15 +119,17 @@ class UnaryMathTransformer(UnaryTransformer):
         super().__init__(None, uid=uid, operation_name=op, op=op, **kw)
         if op in ("ceil", "floor", "round"):
             self.output_type = T.Integral
+        if op == "log" and not self.params["base"] > 0:
+            raise ValueError("requirement failed: log base must be greater than 0")
 
     def transform_columns(self, a, ds=None):
         x, ok = _f64(a)
         op = self.params["op"]
-        if op == "log":
-            v = torch.log(x) / math.log(self.params["base"])
-        elif op == "roundDigits":
-            f = 10.0 ** self.params["digits"]
-            v = torch.round(x * f) / f
+        if op == "log":       # LogTransformer (MathTransformers.scala:343): log10(v) / log10(base)
+            v = torch.log10(x) / math.log10(self.params["base"])
+        elif op == "roundDigits":   # RoundDigitsTransformer (:388): math.round(v * 10^d) / 10^d
+            f = math.pow(10.0, self.params["digits"])
+            v = java_round(x * f) / f
         else:
             v = _UNARY[op](x)
         ok = ok & _finite(v)

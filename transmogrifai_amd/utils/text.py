@@ -417,26 +417,29 @@ def murmur3(terms: Sequence[str], seed: int = 42) -> np.ndarray:
 
 
 # ------------------------------------------------------------------------------ email / url helpers
-_EMAIL = re.compile(r"^[A-Za-z0-9.!#$%&'*+/=?^_`{|}~-]+@[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?"
-                    r"(?:\.[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?)+$")
+# Email.pattern (features/.../types/Text.scala:87-89): prefix @ domain of zero or more dot-separated labels, so
+# "a@b" is valid; prefix / domain are the two groups of a full match (None otherwise)
+_EMAIL = re.compile(r"^([A-Za-z0-9.!#$%&'*+/=?^_`{|}~-]+)@([A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?"
+                    r"(?:\.[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?)*)$")
+
+
+def _email_parts(s: Optional[str]):
+    m = _EMAIL.match(s) if s is not None else None
+    return (m.group(1), m.group(2)) if m else (None, None)
 
 
 def is_valid_email(s: Optional[str]) -> bool:
-    return s is not None and bool(_EMAIL.match(s))
+    """``ValidEmailTransformer`` (ValidEmailTransformer.scala:43): prefix and domain both parse."""
+    p, d = _email_parts(s)
+    return bool(p) and bool(d)
 
 
 def email_domain(s: Optional[str]) -> Optional[str]:
-    if s is None or s.count("@") != 1:
-        return None
-    d = s.split("@")[1]
-    return d or None
+    return _email_parts(s)[1] or None
 
 
 def email_prefix(s: Optional[str]) -> Optional[str]:
-    if s is None or s.count("@") != 1:
-        return None
-    p = s.split("@")[0]
-    return p or None
+    return _email_parts(s)[0] or None
 
 
 def is_valid_url(s: Optional[str], schemes=("http", "https", "ftp")) -> bool:
