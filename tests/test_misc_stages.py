@@ -69,7 +69,10 @@ def test_label_joiners_and_filter_map():
     tj = M.TopNLabelJoiner(labels=["a", "b", "c"], top_n=2).set_input(lab, p)
     assert check_transformer(tj, ds)[1] == {"a": 0.5, "c": 0.4}
     ds3, (mp,) = TestFeatureBuilder.of(("mp", T.TextMap, [{"k1": "v", "k2": "w"}, {}]))
-    check_transformer(M.FilterMap(block_list_keys=["k2"]).set_input(mp), ds3, expected=[{"k1": "v"}, {}])
+    # cleanText defaults to true (TransmogrifierDefaults.CleanText): "v" -> "V"
+    check_transformer(M.FilterMap(block_list_keys=["k2"]).set_input(mp), ds3, expected=[{"k1": "V"}, {}])
+    check_transformer(M.FilterMap(block_list_keys=["k2"], clean_text=False).set_input(mp), ds3,
+                      expected=[{"k1": "v"}, {}])
 
 
 def test_prediction_descaler_inverts_scaler():

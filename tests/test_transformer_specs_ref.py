@@ -269,3 +269,85 @@ def test_drop_indices_by_on_a_vector_with_metadata():
     out = st.transform(ds)[st.get_output().name]
     assert out.values.tolist() == [[1.0], [0.0], [0.0]]
     assert [c.indicator_value for c in out.metadata.columns] == ["0"]
+
+
+# --------------------------------------------------------------- FilterTextMapTest / FilterIntegralMapTest / ...
+_KNIGHTS_TEXT = [{"Arthur": "King", "Lancelot": "Brave", "Galahad": "Pure"},
+                 {"Lancelot": "Brave", "Galahad": "Pure", "Bedevere": "Wise"}, {"Knight": "Ni"}]
+_KNIGHTS_INT = [{"Arthur": 1, "Lancelot": 2, "Galahad": 3}, {"Lancelot": 2, "Galahad": 3, "Bedevere": 4},
+                {"Knight": 5}]
+_KNIGHTS_MPL = [{"Arthur": {"King", "Briton"}, "Lancelot": {"Brave", "Knight"}, "Galahad": {"Pure", "Knight"}},
+                {"Lancelot": {"Brave", "Knight"}, "Galahad": {"Pure", "Knight"}, "Bedevere": {"Wise", "Knight"}},
+                {"Knight": {"Ni", "Ekke Ekke Ekke Ekke Ptang Zoo Boing"}}]
+
+
+def _norm_maps(rows):
+    return [{k: (set(v) if isinstance(v, (set, frozenset, list, tuple)) else v) for k, v in (r or {}).items()}
+            for r in rows]
+
+
+@pytest.mark.parametrize("ftype,data", [(T.TextMap, _KNIGHTS_TEXT), (T.IntegralMap, _KNIGHTS_INT)])
+def test_filter_map_allow_and_block(ftype, data):
+    from transmogrifai_amd.stages.feature.misc_stages import FilterMap
+    ds, (f1,) = _one(data, ftype)
+    check_transformer(FilterMap().set_input(f1), ds, expected=data)
+    st = FilterMap(allow_list_keys=["Arthur", "Knight"]).set_input(f1)
+    got = _norm_maps(st.transform(ds)[st.get_output().name].to_list())
+    assert got == [{"Arthur": data[0]["Arthur"]}, {}, {"Knight": data[2]["Knight"]}]
+    st = FilterMap(allow_list_keys=[], block_list_keys=["Arthur", "Knight"]).set_input(f1)
+    got = _norm_maps(st.transform(ds)[st.get_output().name].to_list())
+    keep = lambda r: {k: v for k, v in r.items() if k not in ("Arthur", "Knight")}
+    assert got == [keep(data[0]), data[1], {}]
+
+
+def test_filter_multi_pick_list_map_cleaning():
+    """FilterMultiPickListMapTest.scala: clean text is on by default (set values cleaned), and off keeps them."""
+    from transmogrifai_amd.stages.feature.misc_stages import FilterMap
+    ds, (f1,) = _one(_KNIGHTS_MPL, T.MultiPickListMap)
+    cleaned = dict(_KNIGHTS_MPL[2])
+    cleaned["Knight"] = {"Ni", "EkkeEkkeEkkeEkkePtangZooBoing"}
+    st = FilterMap().set_input(f1)
+    assert _norm_maps(st.transform(ds)[st.get_output().name].to_list()) == _norm_maps(_KNIGHTS_MPL[:2] + [cleaned])
+    for clean, knight in ((False, _KNIGHTS_MPL[2]["Knight"]), (True, cleaned["Knight"])):
+        st = FilterMap(allow_list_keys=["Arthur", "Knight"], clean_text=clean, clean_keys=clean).set_input(f1)
+        got = _norm_maps(st.transform(ds)[st.get_output().name].to_list())
+        assert got == [{"Arthur": {"King", "Briton"}}, {}, {"Knight": set(knight)}]
+
+
+def test_filter_map_shortcut():
+    from transmogrifai_amd.stages.feature.misc_stages import FilterMap
+    ds, (f1,) = _one(_KNIGHTS_TEXT, T.TextMap)
+    feat = f1.filter_keys(allow_list_keys=["Arthur", "Knight"])
+    assert isinstance(feat.origin_stage, FilterMap) and list(feat.parents) == [f1]
+    assert feat.name == feat.origin_stage.get_output_feature_name()
+
+
+# ---------------------------------------------------------- TextNGramSimilarityTest / SetNGramSimilarityTest
+_TEXT_PAIRS = [("Hamlet: To be or not to be - that is the question.", "I like like Hamlet"),
+               ("that is the question", "There is no question"), ("Just some random text", "I like like Hamlet"),
+               ("Adobe CreativeSuite 5 Master Collection from cheap 4zp",
+                "Adobe CreativeSuite 5 Master Collection from cheap d1x"),
+               (None, None), ("", ""), ("", None), ("asdf", None), (None, "asdf")]
+
+
+@pytest.mark.parametrize("n,expected", [
+    (3, [0.12666672468185425, 0.6083333492279053, 0.15873020887374878, 0.9629629850387573, 0, 0, 0, 0, 0]),
+    (4, [0.11500000953674316, 0.5666666626930237, 0.1547619104385376, 0.9722222089767456, 0, 0, 0, 0, 0]),
+])
+def test_text_ngram_similarity_exact(n, expected):
+    """Lucene NGramDistance in float32: the reference's printed values bit for bit."""
+    ds, (f1, f2) = _two(_TEXT_PAIRS, T.Text)
+    feat = f1.to_n_gram_similarity(f2, n_gram_size=n, to_lowercase=False)
+    check_transformer(feat.origin_stage, ds, expected=expected, tol=0.0)
+
+
+@pytest.mark.parametrize("n,expected", [
+    (3, [0.3333333134651184, 0.09722214937210083, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0]),
+    (5, [0.3333333432674408, 0.12361115217208862, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0]),
+])
+def test_set_ngram_similarity_exact(n, expected):
+    pairs = [(["Red", "Green"], ["Red"]), (["Red", "Green"], ["Yellow, Blue"]), (["Red", "Yellow"], ["Red", "Yellow"]),
+             ([], ["Red", "Yellow"]), ([], []), ([""], ["asdf"]), ([""], [""]), (["", ""], ["", ""])]
+    ds, (f1, f2) = _two(pairs, T.MultiPickList)
+    feat = f1.to_n_gram_similarity(f2, n_gram_size=n)
+    check_transformer(feat.origin_stage, ds, expected=expected, tol=0.0)

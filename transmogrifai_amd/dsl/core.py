@@ -102,7 +102,7 @@ def _time_period_map(self, period: str):
 
 
 @register(T.OPMap, "filter_keys")
-def _filter_map(self, allow_list_keys=(), block_list_keys=(), clean_keys: bool = False, clean_text: bool = False):
+def _filter_map(self, allow_list_keys=(), block_list_keys=(), clean_keys: bool = False, clean_text: bool = True):
     from ..stages.feature.misc_stages import FilterMap
     return FilterMap(allow_list_keys=list(allow_list_keys), block_list_keys=list(block_list_keys),
                      clean_keys=clean_keys, clean_text=clean_text).set_input(self).get_output()

@@ -307,6 +307,33 @@ class Geolocation(OPList):
         return self.value[2] if self.value else None
 
 
+class OrderedSet(frozenset):
+    """A ``frozenset`` that iterates in a fixed order: the order of the sequence it was built from (Scala's small
+    immutable sets Set1..Set4 iterate in insertion order, which ``SetNGramSimilarity``'s ``mkString(" ")``
+    exposes, NGramSimilarity.scala:53), or sorted when built from an unordered set -- never Python's
+    per-process string-hash order. Equality and hashing are the plain set's."""
+
+    def __new__(cls, items=()):
+        if isinstance(items, OrderedSet):
+            return items
+        if isinstance(items, (set, frozenset)):
+            seq = sorted(items, key=lambda e: (type(e).__name__, str(e)))
+        else:
+            seq = list(dict.fromkeys(items))
+        o = super().__new__(cls, seq)
+        o._order = tuple(seq)
+        return o
+
+    def __iter__(self):
+        return iter(self._order)
+
+    def __reduce__(self):
+        return (OrderedSet, (list(self._order),))
+
+    def __repr__(self):
+        return f"OrderedSet({list(self._order)!r})"
+
+
 class OPSet(OPCollection):
     kind = "set"
     multi_response = True
@@ -315,8 +342,8 @@ class OPSet(OPCollection):
     @classmethod
     def _convert(cls, v):
         if v is None:
-            return frozenset()
-        return frozenset(v)
+            return OrderedSet()
+        return OrderedSet(v)
 
 
 class MultiPickList(OPSet):

@@ -338,9 +338,13 @@ class TopNLabelProbMap(UnaryTransformer):
 
 @register_stage
 class FilterMap(UnaryTransformer):
-    """Keep / drop map keys and optionally clean keys / values (``FilterMap.scala``)."""
+    """Keep / drop map keys and optionally clean keys / values (``FilterMap.scala``; ``filterKeys`` and
+    ``cleanMap``, Transmogrifier.scala:532-625): the map is cleaned first (keys with ``clean_keys``, string values
+    and string-collection values with ``clean_text``; defaults false / true as TransmogrifierDefaults), the
+    allow / block lists are cleaned like the keys, then a non-empty allow list keeps its keys minus the block
+    list, else a non-empty block list drops its keys."""
     operation_name = "filterMap"
-    _defaults = {"allow_list_keys": [], "block_list_keys": [], "clean_keys": False, "clean_text": False}
+    _defaults = {"allow_list_keys": [], "block_list_keys": [], "clean_keys": False, "clean_text": True}
 
     def set_input(self, *features):
         super().set_input(*features)
@@ -349,16 +353,27 @@ class FilterMap(UnaryTransformer):
 
     def transform_fn(self, m):
         p = self.params
-        allow, block = set(p["allow_list_keys"]), set(p["block_list_keys"])
-        out = {}
-        for k, v in (m or {}).items():
-            kk = clean_string(k) if p["clean_keys"] else k
-            if (allow and kk not in allow) or kk in block:
-                continue
-            if p["clean_text"] and isinstance(v, str):
-                v = clean_string(v)
-            out[kk] = v
-        return out
+        ck, cv = bool(p["clean_keys"]), bool(p["clean_text"])
+
+        def clean(x, on):
+            return clean_string(x) if on else x
+
+        def value(v):
+            if isinstance(v, str):
+                return clean(v, cv)
+            if isinstance(v, (set, frozenset, list, tuple)) and v and all(isinstance(e, str) for e in v):
+                out = [clean(e, cv) for e in v]
+                return type(v)(out) if not isinstance(v, frozenset) else frozenset(out)
+            return v
+
+        m = {clean(k, ck): value(v) for k, v in (m or {}).items()}
+        allow = {clean(k, ck) for k in p["allow_list_keys"]}
+        block = {clean(k, ck) for k in p["block_list_keys"]}
+        if allow:
+            return {k: v for k, v in m.items() if k in allow and k not in block}
+        if block:
+            return {k: v for k, v in m.items() if k not in block}
+        return m
 
 
 @register_stage
