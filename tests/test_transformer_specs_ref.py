@@ -351,3 +351,75 @@ def test_set_ngram_similarity_exact(n, expected):
     ds, (f1, f2) = _two(pairs, T.MultiPickList)
     feat = f1.to_n_gram_similarity(f2, n_gram_size=n)
     check_transformer(feat.origin_stage, ds, expected=expected, tol=0.0)
+
+
+# ------------------------------------------------------------------------------------------ EmailParserTest
+def test_email_prefix_and_domain():
+    emails = ["test@example.com", "@example.com", "test@", "@", "", "notanemail", None, "first.last@example.com"]
+    ds, (e,) = _one(emails, T.Email)
+    pre, dom = e.to_email_prefix(), e.to_email_domain()
+    assert pre.origin_stage.transform(ds)[pre.name].to_list() == \
+        ["test", None, None, None, None, None, None, "first.last"]
+    assert dom.origin_stage.transform(ds)[dom.name].to_list() == \
+        ["example.com", None, None, None, None, None, None, "example.com"]
+
+
+# ------------------------------------------------------------------- string indexing (OpStringIndexer*Test)
+def test_string_indexer_no_filter_and_unseen():
+    from transmogrifai_amd.stages.feature.indexers import OpStringIndexerNoFilter
+    from transmogrifai_amd.testkit.spec import check_estimator
+    ds, (t,) = _one(["a", "b", "c", "a", "a", "c"], T.Text)
+    est = OpStringIndexerNoFilter().set_input(t)
+    model, _ = check_estimator(est, ds, expected=[0.0, 2.0, 1.0, 0.0, 0.0, 1.0])
+    ds_new, (t_new,) = _one(["a", "b", "c", "a", "a", "c", "d", "e"], T.Text)
+    out = model.transform(ds_new.with_column(t.name, ds_new[t_new.name]))[model.get_output().name].to_list()
+    assert out == [0.0, 2.0, 1.0, 0.0, 0.0, 1.0, 3.0, 3.0]          # unseen strings -> the extra category
+    idx = t.indexed()
+    assert isinstance(idx.origin_stage, OpStringIndexerNoFilter)
+    # deindexing the indexed column gives the text back (OpStringIndexerNoFilterTest.scala:70-78)
+    from transmogrifai_amd.workflow.workflow import OpWorkflow
+    de = idx.deindexed()
+    scored = OpWorkflow().set_result_features(de).set_input_dataset(ds).train().score()
+    assert scored[de.name].to_list() == ["a", "b", "c", "a", "a", "c"]
+
+
+def test_index_to_string():
+    from transmogrifai_amd.stages.feature.indexers import OpIndexToString, OpIndexToStringNoFilter
+    ds, (i,) = _one([0.0, 2.0, 1.0, 0.0, 0.0, 1.0], T.RealNN)
+    st = OpIndexToString(labels=["a", "c", "b"]).set_input(i)
+    check_transformer(st, ds, expected=["a", "b", "c", "a", "a", "c"])
+    assert st.params["labels"] == ["a", "c", "b"]
+    nf = OpIndexToStringNoFilter(labels=["a", "c"]).set_input(i)   # OpIndexToStringNoFilterTest.scala
+    check_transformer(nf, ds, expected=["a", "UnseenIndex", "c", "a", "a", "c"])
+    short = i.deindexed(["a", "c"])
+    assert isinstance(short.origin_stage, OpIndexToStringNoFilter)
+    assert short.origin_stage.transform(ds)[short.name].to_list() == ["a", "UnseenIndex", "c", "a", "a", "c"]
+
+
+def test_prediction_deindexer():
+    """PredictionDeIndexerTest.scala: a permuted index deindexes through the response's indexer labels; a
+    response without them fails with the reference's message."""
+    from transmogrifai_amd.stages.feature.misc_stages import MapTransformer, PredictionDeIndexer
+    from transmogrifai_amd.workflow.workflow import OpWorkflow
+    ds, (txt, num) = TestFeatureBuilder.of(("txt", T.Text, ["a", "b", "c"]), ("num", T.RealNN, [0.0, 1.0, 2.0]))
+    response = txt.indexed()
+    pred = MapTransformer(lambda v: float((int(v) + 1) % 3), T.RealNN, "modulo").set_input(response).get_output()
+    de = PredictionDeIndexer().set_input(response, pred).get_output()
+    scored = OpWorkflow().set_result_features(de).set_input_dataset(ds).train().score()
+    assert scored[de.name].to_list() == ["b", "c", "a"]
+    bad = PredictionDeIndexer().set_input(num, pred).get_output()
+    with pytest.raises(ValueError, match=f"The feature {num.name} does not contain any label/index mapping"):
+        OpWorkflow().set_result_features(bad).set_input_dataset(ds).train().score()
+
+
+def test_linear_scaler():
+    """LinearScalerTest.scala: a zero slope is refused; scale is slope x + intercept, descale its inverse."""
+    from transmogrifai_amd.stages.feature.math_stages import DescalerTransformer, ScalerTransformer
+    with pytest.raises(ValueError, match="LinearScaler must have a non-zero slope to be invertible"):
+        ScalerTransformer(scaling_type="Linear", slope=0.0, intercept=1.0)
+    xs = [0.0, 1.0, 2.0, 3.0, 4.0]
+    ds, (x,) = _one(xs)
+    sc = ScalerTransformer(scaling_type="Linear", slope=2.0, intercept=1.0).set_input(x)
+    check_transformer(sc, ds, expected=[2.0 * v + 1.0 for v in xs])
+    de = DescalerTransformer().set_input(x, sc.get_output())
+    check_transformer(de, sc.transform(ds), expected=[0.5 * v - 0.5 for v in xs])

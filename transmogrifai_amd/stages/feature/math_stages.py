@@ -243,6 +243,11 @@ def parse_scaler_metadata(meta: dict) -> Optional[dict]:
             "intercept": float(args.get("intercept", 0.0))}
 
 
+def _check_linear(p):
+    if p.get("scaling_type", "Linear") == "Linear" and float(p.get("slope", 1.0)) == 0.0:
+        raise ValueError("requirement failed: LinearScaler must have a non-zero slope to be invertible")
+
+
 @register_stage
 class ScalerTransformer(UnaryTransformer):
     """Linear (``slope * x + intercept``) or log scaling with stored args (``ScalerTransformer.scala``)."""
@@ -252,11 +257,14 @@ class ScalerTransformer(UnaryTransformer):
 
     def __init__(self, *args, **kw):
         super().__init__(*args, **kw)
+        _check_linear(self.params)
         self.metadata.update(scaler_metadata(self.params["scaling_type"], self.params["slope"],
                                              self.params["intercept"]))
 
     def set(self, name, value):
         super().set(name, value)
+        if name in ("scaling_type", "slope", "intercept"):
+            _check_linear(self.params)
         if name in ("scaling_type", "slope", "intercept") and "metadata" in self.__dict__:
             self.metadata.update(scaler_metadata(self.params["scaling_type"], self.params["slope"],
                                                  self.params["intercept"]))

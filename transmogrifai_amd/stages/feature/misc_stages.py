@@ -423,20 +423,34 @@ class PredictionDeIndexer(BinaryTransformer):
     allow_label_as_input = True
     _defaults = {"labels": [], "unseen_name": "UnseenIndex"}
 
-    def set_input(self, *features):
-        super().set_input(*features)
-        st = features[0].origin_stage if features else None
-        labels = getattr(st, "metadata", {}).get("labels") if st is not None else None
+    def _resolve_labels(self):
+        """The response's string-indexer labels (minus its unseen label), read from its origin stage's metadata
+        once that stage has been fitted."""
+        if self.params["labels"] or not self._inputs:
+            return
+        st = self._inputs[0].origin_stage
+        labels = (getattr(st, "metadata", None) or {}).get("labels") if st is not None else None
         if labels:
             self.params["labels"] = [l for l in labels if l != "UnseenLabel"]
+
+    def set_input(self, *features):
+        super().set_input(*features)
+        self._resolve_labels()
         return self
+
+    def transform_columns(self, *cols, ds=None):
+        self._resolve_labels()
+        return super().transform_columns(*cols, ds=ds)
 
     def transform_fn(self, label, pred):
         p = pred.get("prediction") if isinstance(pred, dict) else pred
         if p is None:
             return None
-        i = int(p)
         labels = self.params["labels"]
+        if not labels:      # PredictionDeIndexer.scala:60-66: the response carries no indexer labels
+            name = self._inputs[0].name if self._inputs else "response"
+            raise ValueError(f"The feature {name} does not contain any label/index mapping in its metadata")
+        i = int(p)
         return labels[i] if 0 <= i < len(labels) else self.params["unseen_name"]
 
 
