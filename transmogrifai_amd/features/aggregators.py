@@ -180,27 +180,30 @@ class UnionSet(MonoidAggregator):
 
 
 class GeolocationMidpoint(MonoidAggregator):
-    """Geographic midpoint via unit-sphere averaging (``aggregators/Geolocation.scala``)."""
+    """Geographic midpoint (``aggregators/Geolocation.scala:43-138``; the monoid of :mod:`.geo`: WGS84 point
+    sums, count and the accuracy box, the accuracy presented from the box's widest side)."""
     name = "GeolocationMidpoint"
-    zero = (0.0, 0.0, 0.0, 0, 0.0)
+    zero = (0.0,) * 10
 
     def prepare(self, e):
+        from . import geo
         v = e.value
         if not v:
-            return (0.0, 0.0, 0.0, 0, 0.0)
-        lat, lon = math.radians(v[0]), math.radians(v[1])
-        return (math.cos(lat) * math.cos(lon), math.cos(lat) * math.sin(lon), math.sin(lat), 1, v[2])
+            return (0.0,) * 10
+        import torch
+        return tuple(geo.prepare(torch.tensor([list(v[:3])], dtype=torch.float64))[0].tolist())
 
     def plus(self, a, b):
-        return (a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3], max(a[4], b[4]))
+        if a[3] == 0.0:
+            return b
+        if b[3] == 0.0:
+            return a
+        return (a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3], min(a[4], b[4]), min(a[5], b[5]),
+                min(a[6], b[6]), max(a[7], b[7]), max(a[8], b[8]), max(a[9], b[9]))
 
     def present(self, r):
-        if r[3] == 0:
-            return []
-        x, y, z = r[0] / r[3], r[1] / r[3], r[2] / r[3]
-        lon = math.atan2(y, x)
-        lat = math.atan2(z, math.sqrt(x * x + y * y))
-        return [math.degrees(lat), math.degrees(lon), r[4]]
+        from . import geo
+        return geo.present(r)
 
 
 class UnionMap(MonoidAggregator):
@@ -221,6 +224,26 @@ class UnionMap(MonoidAggregator):
         for k, v in b.items():
             out[k] = self.combine(out[k], v) if k in out else v
         return out
+
+
+class UnionGeolocationMidpointMap(MonoidAggregator):
+    """Per-key geographic midpoint (``UnionGeolocationMidpointMap``): each key folds the full midpoint monoid
+    (sums, count, accuracy box) and is presented once at the end; keys without a location are dropped."""
+    name = "UnionGeolocationMidpointMap"
+    zero = {}
+    _g = GeolocationMidpoint()
+
+    def prepare(self, e):
+        return {k: self._g.prepare(Event(0, v)) for k, v in (e.value or {}).items()}
+
+    def plus(self, a, b):
+        out = dict(a)
+        for k, v in b.items():
+            out[k] = self._g.plus(out[k], v) if k in out else v
+        return out
+
+    def present(self, r):
+        return {k: p for k, p in ((k, self._g.present(v)) for k, v in r.items()) if p}
 
 
 class CombineVector(MonoidAggregator):
@@ -248,9 +271,7 @@ def default_aggregator(t) -> MonoidAggregator:
     if issubclass(t, T.MultiPickListMap):
         return UnionMap(lambda a, b: frozenset(a) | frozenset(b), "UnionMultiPickListMap")
     if issubclass(t, T.GeolocationMap):
-        return UnionMap(lambda a, b: GeolocationMidpoint().present(
-            GeolocationMidpoint().plus(GeolocationMidpoint().prepare(Event(0, a)),
-                                       GeolocationMidpoint().prepare(Event(0, b)))), "UnionGeolocationMidpointMap")
+        return UnionGeolocationMidpointMap()
     if issubclass(t, T.BinaryMap):
         return UnionMap(lambda a, b: a or b, "UnionBinaryMap")
     if issubclass(t, T.DateMap):
@@ -329,13 +350,14 @@ def aggregator_from_json(d) -> Optional[MonoidAggregator]:
     name = (d.get("value") or {}).get("name") or d.get("className")
     simple = {c.name: c for c in (SumNumeric, MaxNumeric, MinNumeric, MeanNumeric, SumRealNN, MaxRealNN, MinRealNN,
                                   MeanRealNN, LogicalOr, ModePickList,
-                                  ConcatList, UnionSet, GeolocationMidpoint, CombineVector)}
+                                  ConcatList, UnionSet, GeolocationMidpoint, CombineVector,
+                                  UnionGeolocationMidpointMap)}
     if name in simple:
         return simple[name]()
     if name == "ConcatText":
         return ConcatText((d.get("value") or {}).get("separator", ","))
     probe = {"UnionMeanPrediction": T.Prediction, "UnionMultiPickListMap": T.MultiPickListMap,
-             "UnionGeolocationMidpointMap": T.GeolocationMap, "UnionBinaryMap": T.BinaryMap,
+             "UnionBinaryMap": T.BinaryMap,
              "UnionMaxDateMap": T.DateMap, "UnionMeanPercentMap": T.PercentMap, "UnionSumMap": T.RealMap,
              "UnionConcatTextMap": T.TextMap}
     if name in probe:

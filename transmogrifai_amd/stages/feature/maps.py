@@ -193,11 +193,6 @@ def _pair_counts(keys_of: torch.Tensor, codes: torch.Tensor, n_codes: int) -> tu
     return u // max(n_codes, 1), u % max(n_codes, 1), c
 
 
-def _geo_fill(S: np.ndarray, A: float):
-    from ...features.aggregators import GeolocationMidpoint
-    return GeolocationMidpoint().present((S[0], S[1], S[2], int(S[3]), float(A)))
-
-
 def _per_key_text_columns(coo: MapCOO, keys: Sequence[str]) -> List[TextColumn]:
     """One dictionary-coded column per model key: row -> value code of (row, key), -1 when absent."""
     last = coo.last_entry(keys)
@@ -416,27 +411,20 @@ class MapVectorizer(VectorizerMixin, SequenceEstimator):
                 fills = [[float(p["fill_value"])] * len(k) for k in all_keys]
         elif kind in ("binary", "date"):
             fills = [[float(p["fill_value"])] * len(k) for k in all_keys]
-        elif kind == "geo":
-            sums, accs = [], []
+        elif kind == "geo":      # per-key geographic midpoint (features/geo.py monoid, reduced over the ranks)
+            from ...features import geo
+            stats = []
             for coo, keys in zip(coos, all_keys):
                 if coo.nnz:
-                    lat, lon = torch.deg2rad(coo.geo[:, 0]), torch.deg2rad(coo.geo[:, 1])
-                    xyz1 = torch.stack([torch.cos(lat) * torch.cos(lon), torch.cos(lat) * torch.sin(lon),
-                                        torch.sin(lat), torch.ones_like(lat)], 1)
-                    sums.append(_key_sums(coo, keys, xyz1))
                     s = coo.slots(keys)[coo.key]
                     sel = s >= 0
-                    a = torch.zeros(len(keys), dtype=torch.float64, device=dev)
-                    a.scatter_reduce_(0, s[sel], coo.geo[sel, 2], reduce="amax", include_self=True)
-                    accs.append(a)
+                    stats.append(geo.reduce_by_key(geo.prepare(coo.geo[sel]), s[sel], len(keys)))
                 else:
-                    sums.append(torch.zeros(len(keys), 4, dtype=torch.float64, device=dev))
-                    accs.append(torch.zeros(len(keys), dtype=torch.float64, device=dev))
-            sums = dp.sum_(sums) if sums else []
-            accs = [dp.max_(a) for a in accs]
+                    stats.append(geo.reduce_by_key(torch.zeros(0, 3, dtype=torch.float64, device=dev),
+                                                   torch.zeros(0, dtype=torch.long, device=dev), len(keys)))
             for i, keys in enumerate(all_keys):
-                S, A = sums[i].cpu().numpy(), accs[i].cpu().numpy()
-                fills[i] = [_geo_fill(S[j], A[j]) for j in range(len(keys))]
+                S = geo.all_reduce(stats[i]).cpu()
+                fills[i] = [geo.present(S[j]) for j in range(len(keys))]
         else:
             counters = []
             for coo in coos:

@@ -819,30 +819,21 @@ class GeolocationVectorizerModel(VectorizerMixin, SequenceTransformer):
 class GeolocationVectorizer(VectorizerMixin, SequenceEstimator):
     operation_name = "vecGeo"
     _defaults = {"fill_with_constant": False, "fill_value": [0.0, 0.0, 0.0], "track_nulls": True}
-    # the geographic midpoint is a monoid of (unit-sphere x, y, z sums, count, max accuracy): partial sums
-    # are all-reduced in one collective, the accuracy max in another (GeolocationVectorizer.scala:87)
+    # the geographic midpoint is a monoid (features/geo.py: WGS84 point sums, count, accuracy box): partial results
+    # reduce over the ranks as one sum, one min and one max (GeolocationVectorizer.scala:80-92)
     dp_aware = True
 
     def fit_columns(self, *cols, ds=None):
-        from ...features.aggregators import GeolocationMidpoint
-        from ...parallel import dp
+        from ...features import geo
         fills = []
-        sums, accs = [], []
-        for c in cols:
-            v = c.values[c.valid].to(torch.float64)
-            lat, lon = torch.deg2rad(v[:, 0]), torch.deg2rad(v[:, 1])
-            xyz = torch.stack([torch.cos(lat) * torch.cos(lon), torch.cos(lat) * torch.sin(lon), torch.sin(lat)], 1)
-            sums.append(torch.cat([xyz.sum(0), torch.tensor([float(v.shape[0])], dtype=torch.float64,
-                                                              device=v.device)]))
-            accs.append(v[:, 2].max() if v.shape[0] else torch.tensor(0.0, dtype=torch.float64, device=v.device))
         if cols:
-            S = dp.sum_([torch.stack(sums)])[0].cpu().numpy()
-            A = dp.max_(torch.stack(accs).clamp_min(0.0)).cpu().numpy()
+            stats = geo.all_reduce(torch.stack([geo.reduce_rows(geo.prepare(c.values[c.valid])) for c in cols]))
+            stats = stats.cpu()
         for i, c in enumerate(cols):
             if self.params["fill_with_constant"]:
                 fills.append(list(self.params["fill_value"]))
                 continue
-            fills.append(GeolocationMidpoint().present((S[i, 0], S[i, 1], S[i, 2], int(S[i, 3]), float(A[i]))))
+            fills.append(geo.present(stats[i]))
         cm = []
         for t in self.get_transient_features():
             cm += [col_meta(t, descriptor=nm) for nm in GEO_NAMES]
