@@ -120,6 +120,40 @@ class LogicalOr(MonoidAggregator):
     plus = staticmethod(_opt(lambda a, b: bool(a) or bool(b)))
 
 
+class LogicalXor(MonoidAggregator):
+    """``LogicalXor`` (Numerics.scala:119, 138-143)."""
+    name = "LogicalXor"
+    plus = staticmethod(_opt(lambda a, b: bool(a) != bool(b)))
+
+
+class LogicalAnd(MonoidAggregator):
+    """``LogicalAnd`` (Numerics.scala:120, 145-150)."""
+    name = "LogicalAnd"
+    plus = staticmethod(_opt(lambda a, b: bool(a) and bool(b)))
+
+
+def clip_percent(p: float) -> float:
+    """``PercentPrepare.prepareFn``: a percent below 0 counts as 0, above 1 as 1."""
+    return 0.0 if p < 0.0 else 1.0 if p > 1.0 else p
+
+
+class MeanPercent(MeanNumeric):
+    """``MeanPercent`` (Numerics.scala:105): the mean of the values clipped to [0, 1]."""
+    name = "MeanPercent"
+
+    def prepare(self, e):
+        return (0.0, 0) if e.value is None else (clip_percent(float(e.value)), 1)
+
+
+def concat_text(a: str, b: str, sep: str) -> str:
+    """``TextUtils.concat``: l if r is empty, r if l is empty, else l + sep + r."""
+    if not a:
+        return b
+    if not b:
+        return a
+    return f"{a}{sep}{b}"
+
+
 class ConcatText(MonoidAggregator):
     name = "ConcatText"
 
@@ -127,12 +161,13 @@ class ConcatText(MonoidAggregator):
         self.separator = separator
 
     def plus(self, a, b):
-        # ConcatTextWithSeparator's monoid: only a missing value is the zero -- an empty string is a value
+        # ConcatTextWithSeparator's monoid (aggregators/Text.scala:50-54): a missing value is the zero, present
+        # values join with TextUtils.concat (an empty side contributes nothing, so ("", "") stays a present "")
         if a is None:
             return b
         if b is None:
             return a
-        return f"{a}{self.separator}{b}"
+        return concat_text(a, b, self.separator)
 
     def to_json(self):
         return {"name": self.name, "separator": self.separator}
@@ -246,6 +281,101 @@ class UnionGeolocationMidpointMap(MonoidAggregator):
         return {k: p for k, p in ((k, self._g.present(v)) for k, v in r.items()) if p}
 
 
+class MinMaxList(MonoidAggregator):
+    """``MinMaxList`` (Lists.scala): the single smallest / largest element of all the lists (``MinDateList``,
+    ``MaxDateList``, ``MinDateTimeList``, ``MaxDateTimeList``)."""
+    zero = ()
+
+    def __init__(self, is_min: bool, name: str):
+        self.is_min, self.name = is_min, name
+
+    def prepare(self, e):
+        v = list(e.value or ())
+        return (min(v) if self.is_min else max(v),) if v else ()
+
+    def plus(self, a, b):
+        v = list(a) + list(b)
+        return (min(v) if self.is_min else max(v),) if v else ()
+
+    def present(self, r):
+        return list(r)
+
+    def to_json(self):
+        return {"name": self.name}
+
+
+class UnionMeanMap(MonoidAggregator):
+    """``UnionMeanDoubleMap`` (Maps.scala:58-74): per-key (sum, count), presented as the mean (0.0 for a key
+    seen without values); ``clip`` is the percent variant."""
+    zero = {}
+
+    def __init__(self, name: str = "UnionMeanRealMap", clip: bool = False):
+        self.name, self.clip = name, clip
+
+    def prepare(self, e):
+        f = clip_percent if self.clip else float
+        return {k: (f(float(v)), 1) for k, v in (e.value or {}).items() if v is not None}
+
+    def plus(self, a, b):
+        out = dict(a)
+        for k, (sv, n) in b.items():
+            s0, n0 = out.get(k, (0.0, 0))
+            out[k] = (s0 + sv, n0 + n)
+        return out
+
+    def present(self, r):
+        return {k: (sv / n if n else 0.0) for k, (sv, n) in r.items()}
+
+    def to_json(self):
+        return {"name": self.name}
+
+
+class UnionMinMaxMap(UnionMap):
+    """``UnionMinMaxNumericMap`` (Maps.scala:106-126): per-key min or max."""
+
+    def __init__(self, is_min: bool, name: str):
+        super().__init__(min if is_min else max, name)
+
+
+class UnionConcatTextMap(UnionMap):
+    """``UnionConcatTextMap`` (Maps.scala:132-153): per-key ``TextUtils.concat`` with the type's separator (a
+    space for TextMap / TextAreaMap, a comma otherwise)."""
+
+    def __init__(self, separator: str = ",", name: str = "UnionConcatTextMap"):
+        self.separator = separator
+        super().__init__(lambda a, b: concat_text(a, b, separator), name)
+
+    def to_json(self):
+        return {"name": self.name, "separator": self.separator}
+
+
+class SumVector(MonoidAggregator):
+    """``SumVector`` (OPVector.scala): element-wise sum; vectors of different lengths are an error."""
+    name = "SumVector"
+
+    def plus(self, a, b):
+        import numpy as np
+        if a is None or len(a) == 0:
+            return b
+        if b is None or len(b) == 0:
+            return a
+        if len(a) != len(b):
+            raise ValueError(f"requirement failed: Vectors must have same length: x.length == y.length "
+                             f"({len(b)} != {len(a)})")
+        return np.asarray(a, np.float64) + np.asarray(b, np.float64)
+
+
+class CustomMonoidAggregator(MonoidAggregator):
+    """``CustomMonoidAggregator``: a user zero and associative function over the raw values."""
+    name = "CustomMonoidAggregator"
+
+    def __init__(self, zero, associative_fn):
+        self.zero, self.fn = zero, associative_fn
+
+    def plus(self, a, b):
+        return self.fn(a, b)
+
+
 class CombineVector(MonoidAggregator):
     name = "CombineVector"
 
@@ -267,7 +397,7 @@ def default_aggregator(t) -> MonoidAggregator:
     if issubclass(t, T.OPList):
         return ConcatList()
     if issubclass(t, T.Prediction):
-        return UnionMap(lambda a, b: (a + b) / 2.0, "UnionMeanPrediction")
+        return UnionMeanMap("UnionMeanPrediction")
     if issubclass(t, T.MultiPickListMap):
         return UnionMap(lambda a, b: frozenset(a) | frozenset(b), "UnionMultiPickListMap")
     if issubclass(t, T.GeolocationMap):
@@ -277,17 +407,18 @@ def default_aggregator(t) -> MonoidAggregator:
     if issubclass(t, T.DateMap):
         return UnionMap(max, "UnionMaxDateMap")
     if issubclass(t, T.PercentMap):
-        return UnionMap(lambda a, b: (a + b) / 2.0, "UnionMeanPercentMap")
+        return UnionMeanMap("UnionMeanPercentMap", clip=True)
     if issubclass(t, T.NumericMap):
         return UnionMap(lambda a, b: a + b, "UnionSumMap")
     if issubclass(t, T.OPMap):
-        return UnionMap(lambda a, b: f"{a},{b}" if a and b else (a or b), "UnionConcatTextMap")
+        sep = " " if t in (T.TextMap, T.TextAreaMap) else ","
+        return UnionConcatTextMap(sep)
     if issubclass(t, T.Binary):
         return LogicalOr()
     if issubclass(t, T.Date):
         return MaxNumeric()
     if issubclass(t, T.Percent):
-        return MeanNumeric()
+        return MeanPercent()
     if issubclass(t, T.RealNN):
         return SumRealNN()
     if issubclass(t, T.OPNumeric):
@@ -349,17 +480,23 @@ def aggregator_from_json(d) -> Optional[MonoidAggregator]:
         return None
     name = (d.get("value") or {}).get("name") or d.get("className")
     simple = {c.name: c for c in (SumNumeric, MaxNumeric, MinNumeric, MeanNumeric, SumRealNN, MaxRealNN, MinRealNN,
-                                  MeanRealNN, LogicalOr, ModePickList,
+                                  MeanRealNN, LogicalOr, LogicalXor, LogicalAnd, MeanPercent, ModePickList, SumVector,
                                   ConcatList, UnionSet, GeolocationMidpoint, CombineVector,
                                   UnionGeolocationMidpointMap)}
     if name in simple:
         return simple[name]()
     if name == "ConcatText":
         return ConcatText((d.get("value") or {}).get("separator", ","))
-    probe = {"UnionMeanPrediction": T.Prediction, "UnionMultiPickListMap": T.MultiPickListMap,
-             "UnionBinaryMap": T.BinaryMap,
-             "UnionMaxDateMap": T.DateMap, "UnionMeanPercentMap": T.PercentMap, "UnionSumMap": T.RealMap,
-             "UnionConcatTextMap": T.TextMap}
+    if name == "UnionConcatTextMap":
+        return UnionConcatTextMap((d.get("value") or {}).get("separator", ","))
+    if name in ("UnionMeanPrediction", "UnionMeanRealMap", "UnionMeanCurrencyMap", "UnionMeanPercentMap"):
+        return UnionMeanMap(name, clip=name == "UnionMeanPercentMap")
+    for pre, is_min in (("UnionMin", True), ("UnionMax", False)):
+        if name.startswith(pre) and name.endswith("Map"):
+            return UnionMinMaxMap(is_min, name)
+    if name in ("MinDateList", "MinDateTimeList", "MaxDateList", "MaxDateTimeList"):
+        return MinMaxList(name.startswith("Min"), name)
+    probe = {"UnionMultiPickListMap": T.MultiPickListMap, "UnionBinaryMap": T.BinaryMap, "UnionSumMap": T.RealMap}
     if name in probe:
         return default_aggregator(probe[name])
     return None
