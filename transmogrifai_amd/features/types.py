@@ -180,18 +180,33 @@ class Text(FeatureType):
 
 
 class Email(Text):
+    """``Email`` (types/Text.scala:60-95): prefix / domain are the groups of ``Email.pattern``, None when the
+    value does not parse."""
+
     def prefix(self):
-        return None if self.value is None or "@" not in self.value else self.value.split("@")[0]
+        from ..utils.text import email_prefix
+        return email_prefix(self.value)
 
     def domain(self):
-        if self.value is None or self.value.count("@") != 1:
-            return None
-        d = self.value.split("@")[1]
-        return d or None
+        from ..utils.text import email_domain
+        return email_domain(self.value)
 
 
 class Base64(Text):
-    pass
+    """``Base64`` (types/Text.scala:100-140): the decoded bytes / UTF-8 string, None when empty."""
+
+    def as_bytes(self) -> Optional[bytes]:
+        import base64
+        return None if self.value is None else base64.b64decode(self.value)
+
+    def as_string(self) -> Optional[str]:
+        b = self.as_bytes()
+        return None if b is None else b.decode("utf-8")
+
+    def map_input_stream(self, fn):
+        import io
+        b = self.as_bytes()
+        return None if b is None else fn(io.BytesIO(b))
 
 
 class Phone(Text):
@@ -203,13 +218,22 @@ class ID(Text):
 
 
 class URL(Text):
-    def is_valid(self) -> bool:
+    """``URL`` (types/Text.scala:160-190): validity per Apache UrlValidator's default schemes (or the given
+    ``protocols``), host and protocol of the parsed URL."""
+
+    def is_valid(self, protocols=None) -> bool:
         from ..utils.text import is_valid_url
-        return self.value is not None and is_valid_url(self.value)
+        if self.value is None:
+            return False
+        return is_valid_url(self.value) if protocols is None else is_valid_url(self.value, tuple(protocols))
 
     def domain(self):
         from ..utils.text import url_domain
         return None if self.value is None else url_domain(self.value)
+
+    def protocol(self):
+        from ..utils.text import url_protocol
+        return None if self.value is None else url_protocol(self.value)
 
 
 class TextArea(Text):
@@ -292,19 +316,31 @@ class Geolocation(OPList):
             lat, lon = v[0], v[1]
             if not (-90.0 <= lat <= 90.0) or not (-180.0 <= lon <= 180.0):
                 raise ValueError(f"Invalid geolocation {v}")
+            if v[2] != int(v[2]) or not 0 <= int(v[2]) <= 10:      # a GeolocationAccuracy value
+                raise ValueError(f"Invalid geolocation accuracy {v[2]}")
         return v
 
     @property
-    def lat(self):
-        return self.value[0] if self.value else None
+    def lat(self) -> float:
+        """Latitude; NaN when empty (``Geolocation.lat``)."""
+        return self.value[0] if self.value else float("nan")
 
     @property
-    def lon(self):
-        return self.value[1] if self.value else None
+    def lon(self) -> float:
+        return self.value[1] if self.value else float("nan")
 
     @property
-    def accuracy(self):
-        return self.value[2] if self.value else None
+    def accuracy(self) -> int:
+        """GeolocationAccuracy value; Unknown (0) when empty."""
+        return int(self.value[2]) if self.value else 0
+
+    def to_geo_point(self):
+        """The spatial3d WGS84 ``GeoPoint`` (x, y, z) of the location; (0, 0, 0) when empty."""
+        if not self.value:
+            return (0.0, 0.0, 0.0)
+        import torch
+        from .geo import prepare
+        return tuple(prepare(torch.tensor([self.value], dtype=torch.float64))[0, :3].tolist())
 
 
 class OrderedSet(frozenset):
@@ -492,7 +528,7 @@ class Prediction(RealMap):
     ProbabilityName = "probability"
 
     def __init__(self, value=None, prediction=None, raw_prediction=None, probability=None):
-        if value is None:
+        if value is None or (isinstance(value, dict) and not value and prediction is not None):
             if prediction is None:
                 raise NonNullableEmptyException("Prediction cannot be empty")
             value = {self.PredictionName: float(prediction)}
@@ -500,9 +536,23 @@ class Prediction(RealMap):
                 value[f"{self.RawPredictionName}_{i}"] = float(r)
             for i, p in enumerate([] if probability is None else list(probability)):
                 value[f"{self.ProbabilityName}_{i}"] = float(p)
-        if self.PredictionName not in value:
-            raise NonNullableEmptyException("Prediction must contain 'prediction' key")
+        if not isinstance(value, dict) or not value:
+            raise NonNullableEmptyException("Prediction cannot be empty")
+        if self.PredictionName not in value:        # Maps.scala:350-362
+            raise NonNullableEmptyException(
+                f"Prediction cannot be empty: value map must contain '{self.PredictionName}' key")
+        bad = [k for k in value if k != self.PredictionName and not k.startswith(self.RawPredictionName)
+               and not k.startswith(self.ProbabilityName)]
+        if bad:
+            raise ValueError(f"requirement failed: value map must only contain valid keys: '{self.PredictionName}' "
+                             f"or starting with '{self.RawPredictionName}' or '{self.ProbabilityName}'")
         FeatureType.__init__(self, value)
+
+    def __str__(self):
+        def arr(v):
+            return "Array(" + ", ".join(repr(float(x)) for x in v) + ")"
+        return (f"Prediction(prediction = {float(self.prediction)!r}, rawPrediction = {arr(self.raw_prediction)}, "
+                f"probability = {arr(self.probability)})")
 
     @property
     def prediction(self) -> float:

@@ -442,14 +442,26 @@ def email_prefix(s: Optional[str]) -> Optional[str]:
     return _email_parts(s)[0] or None
 
 
+_HOST = re.compile(r"^(?:[A-Za-z0-9](?:[A-Za-z0-9-]{0,61}[A-Za-z0-9])?\.)+[A-Za-z]{2,63}$")
+_IPV4 = re.compile(r"^(?:25[0-5]|2[0-4]\d|1?\d?\d)(?:\.(?:25[0-5]|2[0-4]\d|1?\d?\d)){3}$")
+
+
 def is_valid_url(s: Optional[str], schemes=("http", "https", "ftp")) -> bool:
-    if not s:
+    """Apache ``UrlValidator`` (default schemes http / https / ftp): a listed scheme, an authority whose host is
+    a dotted ASCII domain name (labels of letters, digits and inner hyphens, an alphabetic top label) or an
+    IPv4 address, an optional numeric port, and no whitespace."""
+    if not s or any(c.isspace() for c in s):
         return False
     try:
         u = urlparse(s)
+        port = u.port
     except ValueError:
         return False
-    return u.scheme in schemes and bool(u.netloc) and "." in u.netloc and " " not in s
+    if u.scheme.lower() not in schemes or not u.netloc or u.username or u.password:
+        return False
+    host = u.hostname or ""
+    del port
+    return bool(_HOST.match(host) or _IPV4.match(host))
 
 
 def url_domain(s: Optional[str]) -> Optional[str]:
