@@ -92,7 +92,14 @@ class Splitter:
 
     def validation_prepare(self, row_ids: torch.Tensor, y: torch.Tensor, stream: int = 7) -> torch.Tensor:
         """Boolean mask of rows kept for training."""
+        self._check_prepared()
         return torch.ones(row_ids.shape[0], dtype=torch.bool, device=row_ids.device)
+
+    def _check_prepared(self):
+        """``Splitter.checkPreconditions`` (Splitter.scala:87)."""
+        if self.summary is None:
+            raise RuntimeError("requirement failed: Cannot call validationPrepare until preValidationPrepare has "
+                               "been called")
 
     def params(self) -> Dict:
         return {"seed": self.seed, "reserveTestFraction": self.reserve_test_fraction,
@@ -122,6 +129,7 @@ class DataSplitter(Splitter):
         return self.summary
 
     def validation_prepare(self, row_ids, y, stream=7):
+        self._check_prepared()
         if self.down_sample_fraction >= 1.0:
             return torch.ones(row_ids.shape[0], dtype=torch.bool, device=row_ids.device)
         return row_uniform(row_ids, self.seed, stream) < self.down_sample_fraction
@@ -153,15 +161,7 @@ class DataBalancer(Splitter):
             self.up_fraction = 1.0
             reported_up = 0.0        # DataBalancer.scala:233-234 reports 0.0 when already balanced
         else:
-            # getProportions (DataBalancer.scala:84-122)
-            def fits(mult):
-                return mult * small * (1 - f) < f * big and mx * f > small * mult
-            if small < mx * f:
-                up = next((float(m) for m in (100, 50, 10, 5, 4, 3, 2) if fits(m)), 1.0)
-                down = (small * up / f - small * up) / big
-            else:
-                up = (mx * f) / small
-                down = (1 - f) * mx / big
+            down, up = self.get_proportions(small, big, f, mx)
             self.up_fraction, self.down_sample_fraction = up, min(down, 1.0)
             reported_up = self.up_fraction
         self.summary = {"className": "com.salesforce.op.stages.impl.tuning.DataBalancerSummary",
@@ -169,11 +169,27 @@ class DataBalancer(Splitter):
                         "upSamplingFraction": reported_up, "downSamplingFraction": self.down_sample_fraction}
         return self.summary
 
+    @staticmethod
+    def get_proportions(small: float, big: float, f: float, max_training_sample: int) -> Tuple[float, float]:
+        """``getProportions`` (DataBalancer.scala:84-115) -> (down-sample fraction of the big class, up-sample
+        multiplier of the small one): the largest multiplier in (100, 50, 10, 5, 4, 3, 2) that neither overshoots
+        the desired fraction nor the training-size cap, or, when the small class alone exceeds its share of the
+        cap, both classes sampled to the cap."""
+        small, big, mx = float(small), float(big), float(max_training_sample)
+
+        def fits(mult):
+            return mult * small * (1 - f) < f * big and mx * f > small * mult
+        if small < mx * f:
+            up = next((float(m) for m in (100, 50, 10, 5, 4, 3, 2) if fits(m)), 1.0)
+            return (small * up / f - small * up) / big, up
+        return (1 - f) * mx / big, (mx * f) / small
+
     def validation_prepare(self, row_ids, y, stream=7):
         """Boolean keep-mask; up-sampling is expressed as integer weights via :meth:`weights`."""
         return self.weights(row_ids, y, stream) > 0
 
     def weights(self, row_ids, y, stream=7) -> torch.Tensor:
+        self._check_prepared()
         u = row_uniform(row_ids, self.seed, stream)
         if self.already_balanced:
             return (u < self.down_sample_fraction).to(torch.int64)
@@ -206,31 +222,50 @@ class DataBalancer(Splitter):
 
 
 class DataCutter(Splitter):
-    """Multiclass preparation: keep the most frequent labels (<= ``max_label_categories``, each with
-    fraction >= ``min_label_fraction``) and down-sample to ``max_training_sample``."""
+    """Multiclass preparation (``DataCutter.scala:84-245``): keep the most frequent labels (count descending, then
+    label; at most ``max_label_categories``, each with fraction >= ``min_label_fraction``), drop the others'
+    rows, and down-sample to ``max_training_sample`` of the whole data. The summary records the kept labels in
+    that order, the first ``max_names_for_dropped_labels`` dropped labels and the number of dropped label
+    categories; labels estimated once are reused by later prepares."""
 
-    def __init__(self, max_label_categories: int = 100, min_label_fraction: float = 0.0, **kw):
+    def __init__(self, max_label_categories: int = 100, min_label_fraction: float = 0.0,
+                 max_names_for_dropped_labels: int = 10, **kw):
         super().__init__(**kw)
         self.max_label_categories = max_label_categories
         self.min_label_fraction = min_label_fraction
+        self.max_names_for_dropped_labels = max_names_for_dropped_labels
         self.labels_kept = None
+        self.labels_dropped = None
+        self.labels_dropped_total = 0
 
-    def pre_validation_prepare(self, y, n_total=None):
-        cnt = label_counts(y)
+    def _estimate(self, cnt: Dict[float, int]):
         tot = float(sum(cnt.values()))
         order = sorted(cnt.items(), key=lambda vc: (-vc[1], vc[0]))
         kept = [v for v, c in order if c / tot >= self.min_label_fraction][:self.max_label_categories]
-        dropped = [v for v, _ in order if v not in set(kept)]
-        self.labels_kept = sorted(kept)
-        n_kept = sum(c for v, c in order if v in set(kept))
-        self.down_sample_fraction = min(self.max_training_sample / max(n_kept, 1), 1.0)
+        if not kept:
+            raise RuntimeError(f"DataCutter dropped all labels with param settings: minLabelFraction = "
+                               f"{self.min_label_fraction}, maxLabelCategories = {self.max_label_categories}. \n"
+                               f"Label counts were: {order}")
+        ks = set(kept)
+        dropped = [v for v, _ in order if v not in ks]
+        self.labels_kept = kept
+        self.labels_dropped = dropped[:self.max_names_for_dropped_labels]
+        self.labels_dropped_total = len(order) - len(kept)
+
+    def pre_validation_prepare(self, y, n_total=None):
+        cnt = label_counts(y)
+        if self.labels_kept is None:
+            self._estimate(cnt)
+        n = int(sum(cnt.values())) if n_total is None else int(n_total)
+        self.down_sample_fraction = min(self.max_training_sample / max(n, 1), 1.0)
         self.summary = {"className": "com.salesforce.op.stages.impl.tuning.DataCutterSummary",
-                        "preSplitterDataCount": int(tot), "downSamplingFraction": self.down_sample_fraction,
-                        "labelsKept": self.labels_kept, "labelsDropped": sorted(dropped),
-                        "labelsDroppedTotal": int(tot - n_kept)}
+                        "preSplitterDataCount": n, "downSamplingFraction": self.down_sample_fraction,
+                        "labelsKept": list(self.labels_kept), "labelsDropped": list(self.labels_dropped),
+                        "labelsDroppedTotal": int(self.labels_dropped_total)}
         return self.summary
 
     def validation_prepare(self, row_ids, y, stream=7):
+        self._check_prepared()
         keep = torch.isin(y.to(torch.float64), torch.as_tensor(self.labels_kept, dtype=torch.float64, device=y.device))
         if self.down_sample_fraction < 1.0:
             keep &= row_uniform(row_ids, self.seed, stream) < self.down_sample_fraction
