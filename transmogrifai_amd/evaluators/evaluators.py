@@ -134,10 +134,13 @@ class OpBinScoreEvaluator(OpEvaluatorBase):
 
     def __init__(self, metric=None, num_bins: int = 100, **kw):
         super().__init__(metric, **kw)
+        if not num_bins > 0:            # OpBinScoreEvaluator.scala:60
+            raise ValueError("requirement failed: numOfBins must be positive")
         self.num_bins = num_bins
 
     def evaluate_arrays(self, y, pred, raw, prob):
-        return M.bin_score_metrics(_score(None, prob, pred), y, self.num_bins)
+        # the class-1 probability, or the class-1 raw score of a model without probabilities
+        return M.bin_score_metrics(_score(raw, prob, pred), y, self.num_bins)
 
 
 class OpMultiClassificationEvaluator(OpEvaluatorBase):
@@ -249,12 +252,17 @@ class OpForecastEvaluator(OpEvaluatorBase):
 
 
 class OpLogLossEvaluator(OpEvaluatorBase):
+    """``LogLoss`` (OPLogLoss.scala): the mean of -log(probability of the true label); ``binary`` names the
+    metric ``BinarylogLoss``, else ``MultiClasslogLoss``."""
     name = "logLoss"
-    default_metric = "LogLoss"
+    default_metric = "MultiClasslogLoss"
     larger_better = False
 
+    def __init__(self, metric=None, binary: bool = False, **kw):
+        super().__init__(metric or ("BinarylogLoss" if binary else "MultiClasslogLoss"), **kw)
+
     def evaluate_arrays(self, y, pred, raw, prob):
-        return {"LogLoss": M.log_loss(prob, y)}
+        return {self.metric: M.log_loss(prob, y)}
 
 
 class CustomEvaluator(OpEvaluatorBase):

@@ -401,8 +401,11 @@ def forecast_metrics(pred, labels, seasonal_window: int = 1) -> Dict:
 
 
 def log_loss(prob, labels) -> float:
-    """Multiclass log loss (``stages/impl/evaluator/OPLogLoss.scala``)."""
+    """Log loss (``stages/impl/evaluator/OPLogLoss.scala``): mean of -log(probability of the true label), no
+    clipping (a zero probability on the true label gives inf, as the reference)."""
+    if labels.numel() == 0:
+        raise ValueError("requirement failed: Dataset is empty, log loss cannot be calculated")
     pr = prob.to(torch.float64)
     y = labels.to(torch.int64)
-    p = pr.gather(1, y[:, None])[:, 0].clamp(1e-15, 1 - 1e-15)
+    p = pr.gather(1, y[:, None])[:, 0]
     return float(-torch.log(p).mean())
