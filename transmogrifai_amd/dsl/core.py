@@ -493,7 +493,7 @@ def _drop_indices_by(self, match_fn: Callable):
 
 
 @register(T.OPVector, "filter_min_variance")
-def _min_var(self, min_variance: float = 1e-5, remove_bad_features: bool = True):
+def _min_var(self, min_variance: float = 1e-5, remove_bad_features: bool = False):
     from ..stages.preparators.min_variance import MinVarianceFilter
     return MinVarianceFilter(min_variance=min_variance, remove_bad_features=remove_bad_features).set_input(
         self).get_output()

@@ -23,7 +23,7 @@ class MinVarianceFilterModel(OpTransformer):
 
     def transform_columns(self, v, ds=None):
         if not self.remove_bad_features:
-            return VectorColumn(v.values, v.metadata)
+            return VectorColumn(v.values, self.metadata.get("vector_metadata", v.metadata))
         idx = torch.as_tensor(self.indices_to_keep, dtype=torch.long, device=v.values.device)
         return VectorColumn(v.values.index_select(1, idx), self.metadata.get("vector_metadata"))
 
@@ -36,21 +36,37 @@ class MinVarianceFilterModel(OpTransformer):
 
 @register_stage
 class MinVarianceFilter(UnaryEstimator):
+    """Drop vector columns whose variance is at or below ``min_variance`` (``MinVarianceFilter.scala:84-140``):
+    the input needs its vector metadata and at least one row; with ``remove_bad_features`` off nothing is
+    dropped; the summary names every input column, the dropped ones and the column statistics."""
     operation_name = "minVarianceFilter"
     output_type = T.OPVector
-    _defaults = {"min_variance": 1e-5, "remove_bad_features": True}
+    _defaults = {"min_variance": 1e-5, "remove_bad_features": False}     # MinVarianceFilter.MinVariance / ...
 
     def fit_columns(self, v, ds=None):
-        cs = ST.col_stats(v.values.contiguous())
-        var = cs["variance"].cpu().numpy()
-        keep = [i for i in range(len(var)) if var[i] > self.params["min_variance"]]
+        X = v.values
+        if X.shape[0] == 0:
+            raise ValueError("requirement failed: Sample size cannot be zero")
+        if X.shape[1] == 0:
+            raise ValueError("requirement failed: Feature vector passed in is empty, check your vectorizers")
         meta = v.metadata
-        if meta is not None:
-            self.metadata["vector_metadata"] = meta.select(keep if self.params["remove_bad_features"]
-                                                           else range(meta.size), self.get_output_feature_name())
-        self.metadata["summary"] = {"dropped": [meta.columns[i].make_col_name() for i in range(len(var))
-                                                if i not in set(keep)] if meta else [],
+        if meta is None:
+            raise ValueError("Vector input metadata is malformed: no vector metadata on the input feature")
+        if meta.size != X.shape[1]:
+            raise ValueError(f"requirement failed: Number of columns in vector metadata ({meta.size}) did not match "
+                             f"number of columns in data({X.shape[1]}), check your vectorizers")
+        cs = ST.col_stats(X.contiguous())
+        var = cs["variance"].cpu().numpy()
+        remove = bool(self.params["remove_bad_features"])
+        drop = {i for i in range(len(var)) if var[i] <= self.params["min_variance"]} if remove else set()
+        keep = [i for i in range(len(var)) if i not in drop]
+        names = [c.make_col_name() for c in meta.columns]
+        self.metadata["vector_metadata"] = meta.select(keep, self.get_output_feature_name())
+        self.metadata["summary"] = {"dropped": [names[i] for i in sorted(drop)], "names": names,
                                     "featuresStatistics": {"count": cs["count"], "mean": cs["mean"].tolist(),
                                                            "variance": cs["variance"].tolist(),
                                                            "min": cs["min"].tolist(), "max": cs["max"].tolist()}}
-        return MinVarianceFilterModel(keep, self.params["remove_bad_features"])
+        if not keep:
+            raise ValueError("requirement failed: The minimum variance filter has dropped all of your features, "
+                             "check your input data or your threshold")
+        return MinVarianceFilterModel(keep, remove)
