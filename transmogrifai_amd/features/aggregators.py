@@ -281,6 +281,39 @@ class UnionGeolocationMidpointMap(MonoidAggregator):
         return {k: p for k, p in ((k, self._g.present(v)) for k, v in r.items()) if p}
 
 
+class TimeBasedAggregator(MonoidAggregator):
+    """``LastAggregator`` / ``FirstAggregator`` (TimeBasedAggregator.scala:38-75): the value of the latest
+    (earliest) event by date -- ties keep the left value for Last and take the right one for First, as the
+    reference's ``compareFun``; an empty event value is a value like any other."""
+
+    def __init__(self, is_last: bool = True, name: Optional[str] = None):
+        self.is_last = is_last
+        self.name = name or ("LastAggregator" if is_last else "FirstAggregator")
+        self.zero = (0, None) if is_last else ((1 << 63) - 1, None)
+
+    def prepare(self, e):
+        return (int(e.date), e.value)
+
+    def plus(self, a, b):
+        if self.is_last:
+            return b if a[0] < b[0] else a
+        return b if a[0] >= b[0] else a
+
+    def present(self, r):
+        return r[1]
+
+    def to_json(self):
+        return {"name": self.name, "isLast": self.is_last}
+
+
+def LastAggregator(name: Optional[str] = None) -> TimeBasedAggregator:
+    return TimeBasedAggregator(True, name)
+
+
+def FirstAggregator(name: Optional[str] = None) -> TimeBasedAggregator:
+    return TimeBasedAggregator(False, name)
+
+
 class MinMaxList(MonoidAggregator):
     """``MinMaxList`` (Lists.scala): the single smallest / largest element of all the lists (``MinDateList``,
     ``MaxDateList``, ``MinDateTimeList``, ``MaxDateTimeList``)."""
@@ -494,6 +527,8 @@ def aggregator_from_json(d) -> Optional[MonoidAggregator]:
     for pre, is_min in (("UnionMin", True), ("UnionMax", False)):
         if name.startswith(pre) and name.endswith("Map"):
             return UnionMinMaxMap(is_min, name)
+    if name.startswith("Last") or name.startswith("First"):
+        return TimeBasedAggregator(name.startswith("Last"), name)
     if name in ("MinDateList", "MinDateTimeList", "MaxDateList", "MaxDateTimeList"):
         return MinMaxList(name.startswith("Min"), name)
     probe = {"UnionMultiPickListMap": T.MultiPickListMap, "UnionBinaryMap": T.BinaryMap, "UnionSumMap": T.RealMap}

@@ -59,6 +59,25 @@ class FeatureGeneratorStage(OpPipelineStage):
             v = v.value
         return v
 
+    def aggregate_records(self, records, time_fn=None, cutoff=None, response_window: Optional[int] = None,
+                          predictor_window: Optional[int] = None):
+        """``FeatureAggregator.extract`` (FeatureAggregator.scala:48-130): fold one key's records into this
+        feature's value -- each record becomes an event (``time_fn(record)`` ms, 0 without one) and is kept by
+        ``filter_by_date_with_cutoff`` with the response window for a response feature and the predictor
+        window otherwise (the stage's own ``aggregate_window`` when it has one); returns a FeatureType."""
+        from ..features.aggregators import CutOffTime, Event, default_aggregator, filter_by_date_with_cutoff
+        agg = self.aggregator if self.aggregator is not None else default_aggregator(self.output_type)
+        cutoff = cutoff if cutoff is not None else CutOffTime.no_cutoff()
+        resp = bool(self.output_is_response)
+        win = self.aggregate_window if self.aggregate_window is not None else \
+            (response_window if resp else predictor_window)
+        evs = []
+        for r in records:
+            d = int(time_fn(r)) if time_fn is not None else 0
+            if filter_by_date_with_cutoff(d, cutoff, resp, win):
+                evs.append(Event(d, self.extract(r), resp))
+        return self.output_type(agg.aggregate(evs)) if self.output_type.nullable or evs else self.output_type.empty()
+
     def ctor_args(self):
         agg = None
         if self.aggregator is not None:
