@@ -27,10 +27,16 @@ def lookup(wtype, name):
     if name.startswith("__"):
         return None
     _ensure()
+    # the most specific registration wins (Date.vectorize is the date vectorizer even though a Date is an
+    # Integral): the matching type closest to ``wtype`` in its MRO, the first registered among equals
+    best, best_d = None, None
+    mro = wtype.__mro__
     for t, fn in _REGISTRY.get(name, []):
         if issubclass(wtype, t):
-            return fn
-    return None
+            d = mro.index(t) if t in mro else len(mro)
+            if best_d is None or d < best_d:
+                best, best_d = fn, d
+    return best
 
 
 def binary_op(a, b, op, reverse=False):
