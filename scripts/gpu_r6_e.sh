@@ -17,3 +17,11 @@ for m in 1 0; do
   TMOG_DENSE_MFMA=$m timeout -k 10 400 python3 -u bench.py --config multiclass-text --steps 3 --warmup 1 --verbose > $O/mct_dense$m.log 2>&1 || { tail -20 $O/mct_dense$m.log; exit 1; }
   echo "mct dense=$m $(grep -a '^{' $O/mct_dense$m.log | grep -o '"value": [0-9.]*\|"holdout_error": [0-9.]*\|"OpLogisticRegression": [0-9.]*' | tr '\n' ' ')"
 done
+# projection FE outlier check: the rank-0 share of world 2 and 4 over 3 timed steps (r6c showed a 1.4 s pivot
+# transform / 2.2 s selector fit in single-step runs)
+timeout -k 10 400 python3 -u scripts/project_schedule.py --world 2 --ranks 0 --steps 3 --out $O/proj2s3 > $O/proj2s3.out 2>&1 || { tail -20 $O/proj2s3.out; exit 1; }
+tail -1 $O/proj2s3.out
+grep -a -o '"step_s": \[[^]]*\]' $O/proj2s3/rank0.log
+timeout -k 10 400 python3 -u scripts/project_schedule.py --world 4 --ranks 0 --steps 3 --out $O/proj4s3 > $O/proj4s3.out 2>&1 || { tail -20 $O/proj4s3.out; exit 1; }
+tail -1 $O/proj4s3.out
+grep -a -o '"step_s": \[[^]]*\]' $O/proj4s3/rank0.log
