@@ -98,3 +98,55 @@ def test_log_loss():
     assert OpLogLossEvaluator(binary=True).metric == "BinarylogLoss"
     with pytest.raises(ValueError, match="requirement failed: Dataset is empty, log loss cannot be calculated"):
         ev.evaluate_arrays(torch.zeros(0), torch.zeros(0), torch.zeros(0, 3), torch.zeros(0, 3))
+
+
+# ------------------------------------------------------------------------- OpMultiClassificationEvaluatorTest
+def _multi_const(n=1000):
+    y = torch.ones(n, dtype=torch.float64)
+    prob = _t([[0.70, 0.25, 0.05, 0.0, 0.0]] * n)
+    return y, torch.zeros(n, dtype=torch.float64), prob
+
+
+def test_multiclass_threshold_counts_default():
+    from transmogrifai_amd.evaluators.evaluators import OpMultiClassificationEvaluator
+    n = 1000
+    y, pred, prob = _multi_const(n)
+    tm = OpMultiClassificationEvaluator().evaluate_arrays(y, pred, prob, prob)["ThresholdMetrics"]
+    T_ = 101
+    assert tm["topNs"] == [1, 3] and tm["thresholds"] == [i / 100 for i in range(101)]
+    assert tm["correctCounts"] == {"1": [0] * T_, "3": [n] * 26 + [0] * (T_ - 26)}
+    assert tm["incorrectCounts"] == {"1": [n] * 71 + [0] * (T_ - 71), "3": [0] * 26 + [n] * 45 + [0] * (T_ - 71)}
+    assert tm["noPredictionCounts"] == {"1": [0] * 71 + [n] * (T_ - 71), "3": [0] * 71 + [n] * (T_ - 71)}
+
+
+def test_multiclass_settable_thresholds_and_top_ns():
+    from transmogrifai_amd.evaluators.evaluators import OpMultiClassificationEvaluator
+    n = 1000
+    y, pred, prob = _multi_const(n)
+    ev = OpMultiClassificationEvaluator().set_thresholds([0.1, 0.2, 0.5, 0.8, 0.9, 1.0]).set_top_ns([1, 4, 12])
+    tm = ev.evaluate_arrays(y, pred, prob, prob)["ThresholdMetrics"]
+    assert tm["correctCounts"] == {"1": [0] * 6, "4": [n, n, 0, 0, 0, 0], "12": [n, n, 0, 0, 0, 0]}
+    assert tm["incorrectCounts"] == {"1": [n, n, n, 0, 0, 0], "4": [0, 0, n, 0, 0, 0], "12": [0, 0, n, 0, 0, 0]}
+    assert tm["noPredictionCounts"] == {k: [0, 0, 0, n, n, n] for k in ("1", "4", "12")}
+
+
+@pytest.mark.parametrize("ties", [False, True])
+def test_multiclass_random_probabilities(ties):
+    from transmogrifai_amd.evaluators.evaluators import OpMultiClassificationEvaluator
+    g = torch.Generator().manual_seed(3)
+    n, k = 1000, (200 if ties else 100)
+    if ties:
+        raw = torch.full((n, k), 1e-10, dtype=torch.float64)
+        raw[torch.arange(n), torch.randint(0, k, (n,), generator=g)] = 4.0
+    else:
+        raw = torch.rand(n, k, generator=g, dtype=torch.float64)
+    prob = torch.softmax(raw, 1)
+    pred = prob.argmax(1).double()
+    y = torch.where(torch.rand(n, generator=g) < 0.3, pred, torch.ones(n, dtype=torch.float64)) if ties else \
+        torch.randint(0, k, (n,), generator=g).double()
+    m = OpMultiClassificationEvaluator().set_top_ns([1, 3, 5, 10] if ties else [1, 3]).evaluate_arrays(y, pred, raw, prob)
+    tm = m["ThresholdMetrics"]
+    assert tm["correctCounts"]["1"][0] / n + m["Error"] == pytest.approx(1.0)
+    for c, i, z in zip(tm["correctCounts"]["1"], tm["incorrectCounts"]["1"], tm["noPredictionCounts"]["1"]):
+        assert c + i + z == n
+    assert all(v[0] == 0 for v in tm["noPredictionCounts"].values())

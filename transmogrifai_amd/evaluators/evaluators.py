@@ -147,12 +147,24 @@ class OpMultiClassificationEvaluator(OpEvaluatorBase):
     name = "multiEval"
     default_metric = "F1"
 
-    def __init__(self, metric=None, **kw):
+    def __init__(self, metric=None, top_ns=(1, 3), thresholds=None, **kw):
         super().__init__(metric, **kw)
         self.larger_better = self.metric not in ("Error",)
+        self.top_ns = list(top_ns)
+        self.thresholds = None if thresholds is None else list(thresholds)
+
+    def set_top_ns(self, top_ns):
+        """``setTopNs`` (OpMultiClassificationEvaluator.scala): the top-N cut-offs of the threshold metrics."""
+        self.top_ns = list(top_ns)
+        return self
+
+    def set_thresholds(self, thresholds):
+        """``setThresholds``: the probability thresholds of the threshold metrics (default 0.00 .. 1.00)."""
+        self.thresholds = list(thresholds)
+        return self
 
     def evaluate_arrays(self, y, pred, raw, prob):
-        return M.multiclass_metrics(pred, y, prob)
+        return M.multiclass_metrics(pred, y, prob, top_ns=tuple(self.top_ns), thresholds=self.thresholds)
 
     # the selector scores every model of a fold through selection_metric_batch: the selection metric alone (the
     # full evaluation adds threshold curves over the class probabilities, ~10 ms a model on 300K-row folds)
