@@ -150,3 +150,62 @@ def test_multiclass_random_probabilities(ties):
     for c, i, z in zip(tm["correctCounts"]["1"], tm["incorrectCounts"]["1"], tm["noPredictionCounts"]["1"]):
         assert c + i + z == n
     assert all(v[0] == 0 for v in tm["noPredictionCounts"].values())
+
+
+# --------------------------------------------------------------------------------- OpRegressionEvaluatorTest
+_REAL = [(-10.0, -11.0), (-4.0, -8.0), (-2.0, 0.1), (0.0, -0.1), (0.0, 0.0), (0.0, 0.0), (0.0, 0.1), (2.0, 0.0),
+         (4.0, 4.0), (10.0, 100.0)]
+INF = float("inf")
+
+
+def _reg(ev, rows):
+    from transmogrifai_amd.evaluators.evaluators import OpRegressionEvaluator  # noqa: F401
+    y, p = _t([r[0] for r in rows]), _t([r[1] for r in rows])
+    return ev.evaluate_arrays(y, p, None, None)
+
+
+def _reg_ev():
+    from transmogrifai_amd.evaluators.evaluators import OpRegressionEvaluator
+    return OpRegressionEvaluator()
+
+
+def test_regression_param_validation():
+    for bad in ([], [1.0, 0.0, 2.0]):
+        with pytest.raises(ValueError):
+            _reg_ev().set_percentage_error_histogram_bins(bad)
+    with pytest.raises(ValueError):
+        _reg_ev().set_scaled_error_cutoff(-1.0)
+    with pytest.raises(ValueError):
+        _reg_ev().set_smart_cutoff_ratio(-1.0)
+
+
+def test_regression_histogram_cases():
+    fine = [-INF] + [round(-1.0 + 0.1 * i, 10) for i in range(21)] + [INF]
+    m = _reg(_reg_ev().set_percentage_error_histogram_bins(fine), [])
+    assert m["SignedPercentageErrorHistogram"]["counts"] == [0] * (len(fine) - 1)
+    m = _reg(_reg_ev(), _REAL)
+    h = m["SignedPercentageErrorHistogram"]
+    assert sum(h["counts"]) == len(_REAL) and len(h["bins"]) == 23
+    m = _reg(_reg_ev().set_percentage_error_histogram_bins(fine), _REAL)
+    assert m["SignedPercentageErrorHistogram"]["bins"] == fine and len(m["SignedPercentageErrorHistogram"]["counts"]) == 22
+    m = _reg(_reg_ev().set_percentage_error_histogram_bins([-INF, -500.0, -100.0, 0.0, 100.0, 500.0, INF])
+             .set_scaled_error_cutoff(10000.0), _REAL)
+    assert m["SignedPercentageErrorHistogram"]["counts"] == [0, 0, 4, 6, 0, 0]
+    m = _reg(_reg_ev().set_percentage_error_histogram_bins([-10.0, 0.0, 10.0]), _REAL)
+    assert m["SignedPercentageErrorHistogram"]["counts"] == [1, 3]
+    m = _reg(_reg_ev().set_percentage_error_histogram_bins([-INF, -1000.0, -10.0, 0.0, 10.0, 1000.0, INF]), _REAL)
+    assert m["SignedPercentageErrorHistogram"]["counts"] == [1, 2, 1, 3, 2, 1]
+    m = _reg(_reg_ev().set_percentage_error_histogram_bins([-INF, -100.0, 0.0, 100.0, INF]), [(1.0, 1.0)] * 5)
+    assert m["SignedPercentageErrorHistogram"]["counts"] == [0, 0, 5, 0]
+
+
+def test_regression_smart_cutoff_and_nans():
+    ev = _reg_ev().set_smart_cutoff_ratio(0.1)
+    _reg(ev, _REAL)
+    assert ev.scaled_error_cutoff == pytest.approx(0.1 * sum(abs(r[0]) for r in _REAL) / len(_REAL))
+    ev = _reg_ev().set_smart_cutoff_ratio(0.1)
+    _reg(ev, [(0.0, 0.1), (0.0, 0.0), (0.0, 0.1), (0.0, 0.0), (0.0, 0.0)])
+    assert ev.scaled_error_cutoff == 1e-3
+    nan = float("nan")
+    m = _reg(_reg_ev(), [(-2.0, 0.1), (nan, 0.0), (0.0, nan), (2.0, 0.0), (2.0, 0.0)])
+    assert sum(m["SignedPercentageErrorHistogram"]["counts"]) == 3

@@ -214,9 +214,36 @@ class OpRegressionEvaluator(OpEvaluatorBase):
     def __init__(self, metric=None, **kw):
         super().__init__(metric, **kw)
         self.larger_better = self.metric == "R2"
+        self.bins = list(M.DEFAULT_PCT_ERROR_BINS)
+        self.scaled_error_cutoff = 1e-3
+        self.smart_cutoff_ratio = None
+
+    def set_percentage_error_histogram_bins(self, bins):
+        """``setPercentageErrorHistogramBins`` (OpRegressionEvaluator.scala:63-73): non-empty and sorted."""
+        b = [float(x) for x in bins]
+        if not b or b != sorted(b):
+            raise ValueError("signedPercentageErrorHistogramBins must be non-empty and sorted")
+        self.bins = b
+        return self
+
+    def set_scaled_error_cutoff(self, v: float):
+        if not v >= 0.0:
+            raise ValueError("scaledErrorCutoff must be non-negative")
+        self.scaled_error_cutoff = float(v)
+        return self
+
+    def set_smart_cutoff_ratio(self, v: float):
+        if not v >= 0.0:
+            raise ValueError("smartCutoffRatio must be non-negative")
+        self.smart_cutoff_ratio = float(v)
+        return self
 
     def evaluate_arrays(self, y, pred, raw, prob):
-        return M.regression_metrics(pred, y)
+        if self.smart_cutoff_ratio is not None:      # calculateSmartCutoff (:170-174), remembered as the reference
+            yv = y.to(torch.float64).reshape(-1)
+            mean_abs = float(yv.abs().mean()) if yv.numel() else 0.0
+            self.scaled_error_cutoff = max(self.smart_cutoff_ratio * mean_abs, self.scaled_error_cutoff)
+        return M.regression_metrics(pred, y, bins=self.bins, scaled_error_cutoff=self.scaled_error_cutoff)
 
     # the selector scores every model of a fold with this (no percentage-error histogram, one host read
     # for all of them): the full metric set cost ~9 ms per model on 30M-row folds, mostly device syncs

@@ -362,25 +362,40 @@ def multiclass_metrics(pred, labels, prob=None, top_ns=(1, 3), thresholds=None) 
     return out
 
 
-def regression_metrics(pred, labels, bins=(-1e9, -100, -10, 0, 10, 100, 1e9), scaled_error_cutoff=1e-3) -> Dict:
-    """``OpRegressionEvaluator``: RMSE, MSE, MAE, R2 and signed percentage-error histogram."""
+DEFAULT_PCT_ERROR_BINS = tuple([float("-inf")] + [float(v) for v in range(-100, 101, 10)] + [float("inf")])
+
+
+def histogram_counts(x: torch.Tensor, edges) -> list:
+    """Spark ``RDD.histogram(buckets)``: bucket i is [e_i, e_{i+1}) except the last, which also takes its right
+    edge; values outside [e_0, e_last] and NaNs are not counted."""
+    e = torch.as_tensor(list(edges), dtype=torch.float64, device=x.device)
+    nb = e.numel() - 1
+    if nb <= 0:
+        return []
+    v = x[~torch.isnan(x)]
+    v = v[(v >= e[0]) & (v <= e[-1])]
+    idx = torch.clamp(torch.searchsorted(e, v, right=True) - 1, 0, nb - 1)
+    return torch.bincount(idx, minlength=nb)[:nb].tolist()
+
+
+def regression_metrics(pred, labels, bins=DEFAULT_PCT_ERROR_BINS, scaled_error_cutoff=1e-3) -> Dict:
+    """``OpRegressionEvaluator``: RMSE, MSE, MAE, R2 and the signed percentage-error histogram
+    (100 (prediction - label) / max(|label|, scaledErrorCutoff), ``histogram_counts`` over ``bins``)."""
     p = pred.to(torch.float64).reshape(-1)
     y = labels.to(torch.float64).reshape(-1)
     n = y.numel()
     if n == 0:
-        return {"RootMeanSquaredError": 0.0, "MeanSquaredError": 0.0, "R2": 0.0, "MeanAbsoluteError": 0.0}
+        return {"RootMeanSquaredError": 0.0, "MeanSquaredError": 0.0, "R2": 0.0, "MeanAbsoluteError": 0.0,
+                "SignedPercentageErrorHistogram": {"bins": list(bins), "counts": [0] * (len(bins) - 1)}}
     e = p - y
     mse = float((e * e).mean())
     ss_tot = float(((y - y.mean()) ** 2).sum())
     r2 = 1.0 - float((e * e).sum()) / ss_tot if ss_tot > 0 else 0.0
-    den = torch.where(y.abs() > scaled_error_cutoff, y.abs(), torch.full_like(y, scaled_error_cutoff))
+    den = torch.clamp(y.abs(), min=float(scaled_error_cutoff))
     pct = 100.0 * e / den
-    edges = torch.as_tensor(list(bins), dtype=torch.float64, device=y.device)
-    idx = torch.clamp(torch.searchsorted(edges, pct, right=True) - 1, 0, len(bins) - 2)
-    hist = torch.bincount(idx, minlength=len(bins) - 1)
     return {"RootMeanSquaredError": math.sqrt(mse), "MeanSquaredError": mse, "R2": r2,
             "MeanAbsoluteError": float(e.abs().mean()),
-            "SignedPercentageErrorHistogram": {"bins": list(bins), "counts": hist.tolist()}}
+            "SignedPercentageErrorHistogram": {"bins": list(bins), "counts": histogram_counts(pct, bins)}}
 
 
 def forecast_metrics(pred, labels, seasonal_window: int = 1) -> Dict:
