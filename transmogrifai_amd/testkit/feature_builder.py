@@ -37,7 +37,8 @@ class TestFeatureBuilder:
                 raise ValueError("all columns must have the same number of rows")
             cols[name] = column_from_values(ftype, values, device)
             b = FeatureBuilder.of(ftype, name)
-            feats.append(b.as_response() if name == response else b.as_predictor())
+            resp = name in response if isinstance(response, (list, tuple, set)) else name == response
+            feats.append(b.as_response() if resp else b.as_predictor())
         return Dataset(cols, None, n or 0), feats
 
     @staticmethod

@@ -167,8 +167,8 @@ def cut_dag(dag: Sequence[Layer]):
     """Split a DAG around its model selector for workflow-level CV (``FitStagesUtil.cutDAG``)."""
     from ..selector.model_selector import ModelSelector
     sels = [(st, d) for layer in dag for st, d in layer if isinstance(st, ModelSelector)]
-    if not sels:
-        return None, list(dag), [], []
+    if not sels:        # nothing to cut (OpWorkflowCore.cutDAG: CutDAG(None, empty, empty, empty))
+        return None, [], [], []
     if len(sels) > 1:
         raise ValueError(f"OpWorkflow can contain at most 1 Model Selector. Found {len(sels)}")
     ms, dist = sels[0]

@@ -383,6 +383,8 @@ class OpWorkflow(OpWorkflowCore):
                 _, _, fitted = fit_and_transform_dag(dag, split, None, stage_t, keep=set())
         else:
             ms, before, during, after = cut_dag(dag)
+            if ms is None:          # no selector: the whole DAG is fitted as usual
+                before = dag
             later = {f.name for part in (during, after) for layer in part for st, _ in layer
                      for f in st.get_input_features()}
             if ms is not None:
