@@ -69,18 +69,50 @@ class OpParams:
 
     @staticmethod
     def from_string(s: str) -> "OpParams":
+        """JSON, else YAML (``yaml.safe_load``); anything that is not a mapping of params is a ValueError (the
+        reference's ``Failure(IllegalArgumentException)``)."""
         try:
-            return OpParams.from_json(json.loads(s))
+            d = json.loads(s)
         except json.JSONDecodeError:
             import yaml
-            return OpParams.from_json(yaml.safe_load(s) or {})
+            try:
+                d = yaml.safe_load(s)
+            except yaml.YAMLError as e:
+                raise ValueError(f"OpParams: neither JSON nor YAML: {e}") from e
+        if d is None:
+            d = {}
+        if not isinstance(d, dict):
+            raise ValueError(f"OpParams: expected a mapping of parameters, got {type(d).__name__}")
+        return OpParams.from_json(d)
 
     @staticmethod
     def from_file(path: str) -> "OpParams":
         with open(path) as f:
             return OpParams.from_string(f.read())
 
-    def with_values(self, **kw) -> "OpParams":
+    def switch_reader_params(self) -> "OpParams":
+        """``switchReaderParams`` (OpParams.scala:203): the alternate reader params become the main ones."""
+        out = self.with_values()
+        out.reader_params, out.alternate_reader_params = dict(self.alternate_reader_params), dict(self.reader_params)
+        return out
+
+    def with_values(self, read_locations: Optional[Dict[str, str]] = None,
+                    alternate_read_locations: Optional[Dict[str, str]] = None, **kw) -> "OpParams":
+        """``withValues`` (OpParams.scala:116-150): new read paths per reader (added or replacing the reader's
+        path) and any of the location / flag fields."""
+        out = self._with(**kw)
+
+        def upd(rp, locs):
+            rp = dict(rp)
+            for k, path in (locs or {}).items():
+                old = rp.get(k) or ReaderParams()
+                rp[k] = ReaderParams(path, old.partitions, dict(old.custom_params))
+            return rp
+        out.reader_params = upd(self.reader_params, read_locations)
+        out.alternate_reader_params = upd(self.alternate_reader_params, alternate_read_locations)
+        return out
+
+    def _with(self, **kw) -> "OpParams":
         d = asdict(self)
         d.update({k: v for k, v in kw.items() if v is not None})
         out = OpParams(**{k: v for k, v in d.items() if k not in ("reader_params", "alternate_reader_params")})
