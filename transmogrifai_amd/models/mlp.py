@@ -15,6 +15,8 @@ drives all of them. One objective pass is
   in fp64), ``dZ W^T`` with W read transposed in place, the sigmoid derivative fused with the bias-gradient column
   sums (``mlp_kernels.hip``).
 
+The layer products run on hipBLASLt by default (measured faster than the ``dense_kernels.hip`` products on these
+shapes, see ``ops/dense.py enabled``); ``TMOG_DENSE_MFMA=1`` selects the fused matrix-core path described above.
 Spark stacks rows into ``blockSize`` matrices only for BLAS; here all rows of a fold are one batch. The
 objective is the weighted mean cross-entropy (no regularisation, as Spark's MLP). The host path computes the
 same objective with torch ops.

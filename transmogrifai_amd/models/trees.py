@@ -473,12 +473,17 @@ class DecisionTreeRegressorLearner(_ForestLearner):
 
 
 # -------------------------------------------------------------------------------- boosting
-def _boost_job_bytes(job, n_rows: int) -> int:
+def _boost_job_bytes(job, n_rows: int, n_features: int = 0, n_bins: int = 64) -> int:
     """Device bytes one boosting job holds while its batch runs: its margin row (fp64) and (g, h) rows (fp32) over
-    the batch's rows, and per training entry the grower's ping-pong entries and staged (g, h), the leaf assignment
-    and the root packing (~40 bytes)."""
+    the batch's rows; per training entry the grower's ping-pong entries and staged (g, h), the leaf assignment and
+    the root packing (~40 bytes); and the grower's two level histograms -- F x (B + 1) x 2 statistics x 8 bytes
+    for each node of the widest level (2^(max_depth - 1), at most one per training row), the size
+    ``tree_resident.hip`` allocates per job group."""
     n_train = int(job.rows.numel()) if job.rows is not None else n_rows
-    return 16 * n_rows + 40 * n_train
+    depth = int(job.params.get("max_depth", 6)) if getattr(job, "params", None) else 6
+    nodes = min(1 << max(depth - 1, 0), max(n_train, 1))
+    hist = 2 * n_features * (n_bins + 1) * 2 * 8 * nodes
+    return 16 * n_rows + 40 * n_train + hist
 
 
 def _budget_chunks(job_bytes: Sequence[int], dev, frac: Optional[float] = None) -> List[tuple]:
@@ -492,7 +497,9 @@ def _budget_chunks(job_bytes: Sequence[int], dev, frac: Optional[float] = None) 
     frac = float(os.environ.get("TMOG_TREE_BUDGET_FRAC", "0.6")) if frac is None else frac
     free, _ = torch.cuda.mem_get_info(dev)
     cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-    budget = max(1, int(frac * (free + max(cached, 0))))
+    # learner lanes running beside this fit allocate from the same free memory: each lane gets its share
+    from ..ops import streams as SP
+    budget = max(1, int(frac * (free + max(cached, 0)) / SP.active_lanes()))
     if sum(job_bytes) <= budget:
         return [(0, n)]
     out, lo, acc = [], 0, 0
@@ -540,7 +547,7 @@ class _BoostLearner(Learner):
                     NU = int(U.numel())
                     gjobs = [FitJob(j.params, r, j.weights) for j, r in zip(gjobs, parts)]
             res = []
-            for lo, hi in _budget_chunks([_boost_job_bytes(j, NU) for j in gjobs], dev):
+            for lo, hi in _budget_chunks([_boost_job_bytes(j, NU, F, key[0]) for j in gjobs], dev):
                 res += self._boost(Xb, spec, yd, gjobs[lo:hi], NU, F, dev, key[0], par=_par(context))
             for k, i in enumerate(idxs):
                 out[i] = res[k]

@@ -22,8 +22,13 @@ _TARGET_BLOCKS = 2048
 
 
 def enabled() -> bool:
-    """The matrix-core row GEMMs are the device path; ``TMOG_DENSE_MFMA=0`` selects torch's GEMMs (A/B only)."""
-    return os.environ.get("TMOG_DENSE_MFMA", "1") != "0"
+    """``TMOG_DENSE_MFMA=1`` routes the learners' plain dense products through these kernels. Default off: on
+    MI355X hipBLASLt measured faster on every learner shape (``profiles/r6e_bench_dense.log``: X V at
+    1M x 400 0.40 / 0.70 / 1.67 ms vs 1.81 / 3.53 / 7.00 ms here for 8 / 80 / 256 columns, X^T R 1.37 / 2.16 /
+    4.54 vs 1.66 / 3.14 / 6.12 ms, the MLP layer products 3.1 / 2.8 vs 3.6 / 3.1 ms), and the end-to-end
+    multiclass-text step is the same either way (1.128 vs 1.119 s, identical hold-out error). These are plain
+    GEMMs, the library's case; the kernels stay tested (tests/test_dense_gemm_gpu.py) and selectable."""
+    return os.environ.get("TMOG_DENSE_MFMA", "0") == "1"
 
 
 def supported(*ts: torch.Tensor) -> bool:

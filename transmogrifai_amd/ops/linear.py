@@ -13,7 +13,8 @@ import torch
 
 
 def _dense_mfma(X) -> bool:
-    """A contiguous fp32 device design: its products run on the matrix-core row GEMMs (ops/dense.py)."""
+    """A contiguous fp32 device design whose products run on the matrix-core row GEMMs (ops/dense.py) when
+    ``TMOG_DENSE_MFMA=1`` (default: hipBLASLt, measured faster on these shapes)."""
     from .dense import enabled
     return isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and \
         X.is_contiguous() and enabled()

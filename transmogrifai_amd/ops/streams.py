@@ -88,6 +88,19 @@ def leased(dev, n: int, high=None):
         release(dev, got)
 
 
+_LANES = {"n": 1}
+
+
+def set_active_lanes(n: int) -> None:
+    """Learner lanes running at once on this process's GPU (tuning/validators.py sets it around a lanes run):
+    device-memory budgets taken while lanes run are shared between them (models/trees.py _budget_chunks)."""
+    _LANES["n"] = max(1, int(n))
+
+
+def active_lanes() -> int:
+    return _LANES["n"]
+
+
 def in_use(dev) -> int:
     """Streams of ``dev`` currently leased (tests / diagnostics)."""
     i = _index(dev)

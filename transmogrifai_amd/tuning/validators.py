@@ -589,6 +589,7 @@ class OpValidator:
         from ..utils.watchdog import Watchdog
         # a lane returning from a native call must win the GIL back from one running Python promptly; the
         # watchdog dumps every thread's stack if no fit makes progress for TMOG_WATCHDOG_S seconds
+        SP.set_active_lanes(lanes)
         with fast_switch(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))), Watchdog("learner lanes"):
             for t in th:
                 t.start()
@@ -613,6 +614,7 @@ class OpValidator:
                 if abandoned:
                     log.warning("maxWait: %d learner lane(s) did not stop within %.0fs of cancellation; abandoned",
                                 len(abandoned), _cancel_grace_s())
+        SP.set_active_lanes(1)
         if gpu:
             live = [st for w, st in enumerate(streams) if w not in abandoned and st is not cur]
             for st in live:
