@@ -590,31 +590,33 @@ class OpValidator:
         # a lane returning from a native call must win the GIL back from one running Python promptly; the
         # watchdog dumps every thread's stack if no fit makes progress for TMOG_WATCHDOG_S seconds
         SP.set_active_lanes(lanes)
-        with fast_switch(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))), Watchdog("learner lanes"):
-            for t in th:
-                t.start()
-            bounded = self.max_wait < _UNBOUNDED_WAIT
-            for t in th:
-                t.join(max(0.0, self.max_wait - (time.time() - t0)) if bounded else None)
-            abandoned = []
-            if any(t.is_alive() for t in th):
-                token.set()                     # cooperative cancel: running fits stop at their next check
-                grace_end = time.time() + _cancel_grace_s()
+        try:
+            with fast_switch(float(os.environ.get("TMOG_PIPE_SWITCH_S", "5e-5"))), Watchdog("learner lanes"):
                 for t in th:
-                    t.join(max(0.0, grace_end - time.time()))
-                # a fit inside a long native call never reaches a check: give it up (the reference abandons
-                # its future) rather than block the selector past maxWait + grace
-                abandoned = [w for w, t in enumerate(th) if t.is_alive()]
-                # an abandoned lane keeps its native slots (and its side stream, returned by the reaper) until its
-                # thread exits: later fits -- this selector's and later validate() calls' -- get other lanes
-                for w in abandoned:
-                    st_w = streams[w] if gpu else None
-                    rel = (lambda s_=st_w: SP.release(dev, [s_])) if (gpu and st_w is not cur) else None
-                    TE.quarantine_lane(bases[w], th[w], rel)
-                if abandoned:
-                    log.warning("maxWait: %d learner lane(s) did not stop within %.0fs of cancellation; abandoned",
-                                len(abandoned), _cancel_grace_s())
-        SP.set_active_lanes(1)
+                    t.start()
+                bounded = self.max_wait < _UNBOUNDED_WAIT
+                for t in th:
+                    t.join(max(0.0, self.max_wait - (time.time() - t0)) if bounded else None)
+                abandoned = []
+                if any(t.is_alive() for t in th):
+                    token.set()                     # cooperative cancel: running fits stop at their next check
+                    grace_end = time.time() + _cancel_grace_s()
+                    for t in th:
+                        t.join(max(0.0, grace_end - time.time()))
+                    # a fit inside a long native call never reaches a check: give it up (the reference abandons
+                    # its future) rather than block the selector past maxWait + grace
+                    abandoned = [w for w, t in enumerate(th) if t.is_alive()]
+                    # an abandoned lane keeps its native slots (and its side stream, returned by the reaper) until its
+                    # thread exits: later fits -- this selector's and later validate() calls' -- get other lanes
+                    for w in abandoned:
+                        st_w = streams[w] if gpu else None
+                        rel = (lambda s_=st_w: SP.release(dev, [s_])) if (gpu and st_w is not cur) else None
+                        TE.quarantine_lane(bases[w], th[w], rel)
+                    if abandoned:
+                        log.warning("maxWait: %d learner lane(s) did not stop within %.0fs of cancellation; abandoned",
+                                    len(abandoned), _cancel_grace_s())
+        finally:
+            SP.set_active_lanes(1)
         if gpu:
             live = [st for w, st in enumerate(streams) if w not in abandoned and st is not cur]
             for st in live:
