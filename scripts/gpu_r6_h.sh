@@ -14,3 +14,8 @@ timeout -k 10 400 python3 -u bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench
 grep -a '^{' $O/bench.log | cut -c1-400
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 2 --warmup 1 > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
 find $O/prof -name "*kernel_stats.csv" | head -3
+# regression-100m at a 20M training sample with the lane-shared tree budgets (r6e: the GBT batch hit OOM beside
+# the random-forest lane)
+timeout -k 10 900 python3 -u bench.py --config regression-100m --max-training-sample 20000000 --steps 1 --warmup 1 --verbose > $O/reg100m_20m.log 2>&1 || { tail -30 $O/reg100m_20m.log; exit 1; }
+echo "reg100m-20m $(grep -a '^{' $O/reg100m_20m.log | grep -o '"value": [0-9.]*\|"peak_hbm_gb_per_gpu": [0-9.]*' | tr '\n' ' ')"
+grep -a -c "OutOfMemory" $O/reg100m_20m.log || true

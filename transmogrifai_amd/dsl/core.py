@@ -353,6 +353,39 @@ def _mime(self, type_hint: Optional[str] = None):
     return MimeTypeDetector(type_hint=type_hint or "").set_input(self).get_output()
 
 
+# The typed text features vectorize through what they carry, not their raw strings (``RichTextFeature.scala``):
+# an email / URL by its domain (:617-632, :667-682; invalid URLs are empty), base64 content by its detected MIME
+# type (:712-729), each pivoted; a phone number by its validity as a binary (:566-575).
+@register(T.Email, "vectorize")
+def _vec_email(self, top_k: int = 20, clean_text: bool = True, min_support: int = 10, track_nulls: bool = True,
+               others=(), max_pct_cardinality: float = 1.0, **kw):
+    doms = [TS.TextMapTransformer("EmailDomainToPickList", T.PickList).set_input(f).get_output()
+            for f in _others(self, others)]
+    return _pivot(doms[0], doms[1:], top_k, min_support, clean_text, track_nulls, max_pct_cardinality)
+
+
+@register(T.URL, "vectorize")
+def _vec_url(self, top_k: int = 20, clean_text: bool = True, min_support: int = 10, track_nulls: bool = True,
+             others=(), max_pct_cardinality: float = 1.0, **kw):
+    doms = [TS.TextMapTransformer("URLDomainToPickList", T.PickList).set_input(f).get_output()
+            for f in _others(self, others)]
+    return _pivot(doms[0], doms[1:], top_k, min_support, clean_text, track_nulls, max_pct_cardinality)
+
+
+@register(T.Base64, "vectorize")
+def _vec_base64(self, top_k: int = 20, min_support: int = 10, clean_text: bool = True, track_nulls: bool = True,
+                type_hint: Optional[str] = None, others=(), max_pct_cardinality: float = 1.0, **kw):
+    mts = [_mime(f, type_hint) for f in _others(self, others)]
+    return _pivot(mts[0], mts[1:], top_k, min_support, clean_text, track_nulls, max_pct_cardinality)
+
+
+@register(T.Phone, "vectorize")
+def _vec_phone(self, default_region: str = "US", is_strict: bool = False, track_nulls: bool = True,
+               fill_value: bool = False, others=(), **kw):
+    valid = [_phone_valid(f, default_region, is_strict) for f in _others(self, others)]
+    return V.BinaryVectorizer(fill_value=fill_value, track_nulls=track_nulls).set_input(valid).get_output()
+
+
 @register(T.Text, "text_len")
 def _text_len(self, others=()):
     return TS.TextLenTransformer().set_input(_others(self, others)).get_output()

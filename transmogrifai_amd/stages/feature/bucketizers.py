@@ -189,8 +189,11 @@ class DecisionTreeNumericBucketizer(BinaryEstimator):
     dp_aware = True     # global binning sample + one all-reduced (bin, class) table (tree_splits_dp)
 
     def fit_columns(self, label, a, ds=None):
+        from ...parallel import dp
         p = self.params
         ok = a.valid
+        if dp.count(int(ok.shape[0])) == 0:       # DecisionTreeNumericBucketizer.scala:77
+            raise ValueError("requirement failed: Dataset is empty, buckets cannot be computed.")
         x = a.values.to(torch.float64)[ok]
         y = label.values[ok]
         sp = tree_splits_dp(x, y, p["max_depth"], p["max_bins"], p["min_instances_per_node"], p["min_info_gain"],

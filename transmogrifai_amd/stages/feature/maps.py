@@ -230,7 +230,7 @@ class MapVectorizerModel(VectorizerMixin, SequenceTransformer):
         e = last.clamp_min(0)
         if self.kind == "date":
             ms = coo.ival[e] if coo.nnz else torch.zeros(n, K, dtype=torch.int64, device=dev)
-            v = torch.div(int(self.reference_date) - ms, 86400000, rounding_mode="floor").to(torch.float64)
+            v = torch.div(int(self.reference_date) - ms, 86400000, rounding_mode="trunc").to(torch.float64)
         elif self.kind == "integral":
             v = (coo.ival[e] if coo.nnz else torch.zeros(n, K, dtype=torch.int64, device=dev)).to(torch.float64)
         else:
@@ -510,6 +510,7 @@ def map_vectorize(t, feats, label, D, **overrides) -> list:
     """
     kind = _kind_of(t)
     ov = dict(overrides)
+    circular = tuple(ov.pop("circular_date_reps", getattr(D, "CircularDateRepresentations", ())))
     region = ov.pop("default_region", D.DefaultRegion)
     strict = ov.pop("is_strict", False)
     type_hint = ov.pop("type_hint", None)
@@ -553,7 +554,15 @@ def map_vectorize(t, feats, label, D, **overrides) -> list:
         return [SmartTextMapVectorizer(**sp).set_input(feats).get_output()]
     cls = {"pivot": TextMapPivotVectorizer, "binary": BinaryMapVectorizer}.get(kind, MapVectorizer)
     st = cls(**params) if kind in ("pivot", "binary") and t is not T.OPMap else MapVectorizer(**params)
-    return [st.set_input(feats).get_output()]
+    out = st.set_input(feats).get_output()
+    if kind == "date" and circular and t is not T.OPMap:
+        # RichDateMapFeature / RichDateTimeMapFeature.vectorize (RichMapFeature.scala:776-797, :861-882): one
+        # unit-circle vectorizer per circular representation, then the days-since block, combined
+        from .vectorizers import VectorsCombiner
+        circ = [DateMapToUnitCircleVectorizer(time_period=tp, clean_keys=params["clean_keys"]).set_input(feats)
+                .get_output() for tp in circular]
+        out = VectorsCombiner().set_input(circ + [out]).get_output()
+    return [out]
 
 
 # ---------------------------------------------------------------------- named map vectorizers (catalog)

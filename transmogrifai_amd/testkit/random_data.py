@@ -139,7 +139,8 @@ _STREETS = ["Almaden Blvd", "Santa Clara St", "First St", "Market St", "Park Ave
 
 
 def _rand_string(r: np.random.Generator, alphabet: str, lo: int, hi: int) -> str:
-    n = int(r.integers(lo, hi + 1)) if hi > lo else lo
+    """A string of length in [lo, hi) (``RandomText.strings``: minLen inclusive, maxLen exclusive)."""
+    n = int(r.integers(lo, hi)) if hi > lo else lo
     idx = r.integers(0, len(alphabet), n)
     return "".join(alphabet[i] for i in idx)
 
@@ -291,7 +292,22 @@ class RandomSet(RandomData):
     ftype = T.MultiPickList
 
     @staticmethod
-    def of(values: Sequence[str], min_len: int = 0, max_len: int = 3):
+    def of(values, min_len: int = 0, max_len: int = 3):
+        """``RandomSet.of`` (``RandomSet.scala``): ``values`` is a domain sequence or, as in the reference, a
+        generator whose draws fill the set (``max_len`` exclusive; a generator with a small domain gives up
+        after a bounded number of draws rather than looping)."""
+        if isinstance(values, RandomData):
+            def prod_gen(r):
+                n = _between(r, min_len, max_len)
+                out: set = set()
+                for _ in range(max(8 * n, 16)):
+                    if len(out) >= n:
+                        break
+                    v = next(values)
+                    if v is not None:
+                        out.add(v)
+                return out
+            return RandomSet(prod_gen, T.MultiPickList)
         vals = list(values)
 
         def prod(r):
