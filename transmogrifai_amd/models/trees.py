@@ -1041,8 +1041,42 @@ class XGBoostClassifierLearner(_BoostLearner):
             "boost_epilogue")
         return counts
 
+    def fit_batch(self, X, y, jobs, context=None):
+        """Jobs with ``objective="reg:squarederror"`` (xgboost4j's own default, which a bare
+        ``OpXGBoostClassifier`` in the reference trains with -- ``OpXGBoostClassifierTest.scala``; the model
+        selector's grid sets ``binary:logistic``, ``DefaultSelectorParams.scala:72``) boost the label as a
+        regression target and score it as the class-1 probability."""
+        if type(self) is not XGBoostClassifierLearner:
+            return super().fit_batch(X, y, jobs, context)
+        sq = [i for i, j in enumerate(jobs) if j.params.get("objective", "binary:logistic") == "reg:squarederror"]
+        if not sq:
+            return super().fit_batch(X, y, jobs, context)
+        lg = [i for i in range(len(jobs)) if i not in set(sq)]
+        out = [None] * len(jobs)
+        for i, r in zip(lg, super().fit_batch(X, y, [jobs[i] for i in lg], context) if lg else []):
+            out[i] = r
+        for i, r in zip(sq, _SquaredErrorXGBClassifier().fit_batch(X, y, [jobs[i] for i in sq], context)):
+            out[i] = dict(r, objective="reg:squarederror")
+        return out
+
     def _outputs(self, state, m):
+        if state.get("objective") == "reg:squarederror":
+            # xgboost4j's binary model: raw = (-margin, margin), probability = (1 - p, p) with p the booster's
+            # (identity-link) output, prediction from the probability
+            m = m.to(torch.float64)
+            return (m > 0.5).to(torch.float64), torch.stack([-m, m], 1), torch.stack([1 - m, m], 1)
         return probability_outputs(m)
+
+
+class _SquaredErrorXGBClassifier(XGBoostClassifierLearner):
+    """Squared-error boosting of a 0/1 label (see :meth:`XGBoostClassifierLearner.fit_batch`); not registered."""
+    objective_code = 1
+
+    def _grad(self, yy, Fm):
+        return Fm - yy, torch.ones_like(Fm)
+
+    def _base_margin(self, bs):
+        return float(bs)
 
 
 @register_learner
