@@ -219,12 +219,18 @@ def _vec_real(self, fill_value: float = 0.0, fill_with_mean: bool = True, track_
     st = V.RealVectorizer(track_nulls=track_nulls, fill_value=float(fill_value))
     if fill_with_mean:
         st.set_fill_with_mean()
-    out = st.set_input(_others(self, others)).get_output()
+    return _with_buckets(self, st.set_input(_others(self, others)).get_output(), others, label, kw)
+
+
+def _with_buckets(self, out, others, label, kw):
+    """The label-aware buckets a numeric ``vectorize(label = ...)`` appends (RichNumericFeature.scala:329-336,
+    :660-667): ``autoBucketize(label, trackNulls = false, trackInvalid, minInfoGain)`` per feature."""
     if label is None:
         return out
     from ..stages.feature.bucketizers import DecisionTreeNumericBucketizer
-    bs = [DecisionTreeNumericBucketizer(track_nulls=track_nulls).set_input(label, f).get_output()
-          for f in _others(self, others)]
+    bs = [DecisionTreeNumericBucketizer(track_nulls=False, track_invalid=kw.get("track_invalid", D.TrackInvalid),
+                                        min_info_gain=kw.get("min_info_gain", D.MinInfoGain))
+          .set_input(label, f).get_output() for f in _others(self, others)]
     return V.VectorsCombiner().set_input([out] + bs).get_output()
 
 
@@ -239,7 +245,7 @@ def _vec_int(self, fill_value: float = 0.0, fill_with_mode: bool = True, track_n
     st = V.IntegralVectorizer(track_nulls=track_nulls, fill_value=float(fill_value))
     if fill_with_mode:
         st.set_fill_with_mode()
-    return st.set_input(_others(self, others)).get_output()
+    return _with_buckets(self, st.set_input(_others(self, others)).get_output(), others, label, kw)
 
 
 @register(T.Binary, "vectorize")

@@ -73,7 +73,10 @@ def _vectorize_group(t, feats: List[FeatureLike], label, D) -> List[FeatureLike]
         out = [st.set_input(feats).get_output()]
         if label is not None:
             from .bucketizers import DecisionTreeNumericBucketizer
-            out += [DecisionTreeNumericBucketizer(track_nulls=D.TrackNulls, min_info_gain=D.MinInfoGain)
+            # RichRealFeature / RichIntegralFeature.vectorize with a label (RichNumericFeature.scala:329-336,
+            # :660-667): autoBucketize(label, trackNulls = false, trackInvalid, minInfoGain)
+            out += [DecisionTreeNumericBucketizer(track_nulls=False, track_invalid=getattr(D, "TrackInvalid", False),
+                                                  min_info_gain=D.MinInfoGain)
                     .set_input(label, f).get_output() for f in feats]
         return out
     if t is T.Integral:
@@ -83,7 +86,10 @@ def _vectorize_group(t, feats: List[FeatureLike], label, D) -> List[FeatureLike]
         out = [st.set_input(feats).get_output()]
         if label is not None:
             from .bucketizers import DecisionTreeNumericBucketizer
-            out += [DecisionTreeNumericBucketizer(track_nulls=D.TrackNulls, min_info_gain=D.MinInfoGain)
+            # RichRealFeature / RichIntegralFeature.vectorize with a label (RichNumericFeature.scala:329-336,
+            # :660-667): autoBucketize(label, trackNulls = false, trackInvalid, minInfoGain)
+            out += [DecisionTreeNumericBucketizer(track_nulls=False, track_invalid=getattr(D, "TrackInvalid", False),
+                                                  min_info_gain=D.MinInfoGain)
                     .set_input(label, f).get_output() for f in feats]
         return out
     if t is T.Binary:
