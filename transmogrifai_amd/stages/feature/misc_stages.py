@@ -308,7 +308,13 @@ class MultiLabelJoiner(BinaryTransformer):
     _defaults = {"labels": []}
 
     def _labels(self):
-        return list(self.params["labels"])
+        """The given labels, else the class names of the indexed input's string indexer, read from its fitted
+        metadata (``MultiLabelJoiner.scala``: the ``ml_attr`` values of the class-index column)."""
+        if self.params["labels"] or not self._inputs:
+            return list(self.params["labels"])
+        st = self._inputs[0].origin_stage
+        labels = (getattr(st, "metadata", None) or {}).get("labels") if st is not None else None
+        return list(labels or [])
 
     def transform_fn(self, idx, probs):
         p = np.asarray(probs if probs is not None else [], np.float64).reshape(-1)
