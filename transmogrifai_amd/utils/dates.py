@@ -80,3 +80,53 @@ def period_values(ms: torch.Tensor, period: str, raw: bool = False):
     if raw:
         return v, hi
     return (v - 1 if lo == 1 else v), hi
+
+
+# ------------------------------------------------------------------- string helpers (DateTimeUtils.scala:40-142)
+_FORMATS = ("%Y-%m-%d %H:%M:%S.%f", "%Y-%m-%d %H:%M:%S", "%Y/%m/%d", "%m/%d/%Y")
+
+
+def parse(date: str, tz: str = "UTC") -> int:
+    """``DateTimeUtils.parse``: epoch ms of ``yyyy-MM-dd HH:mm:ss.SSS``, ``yyyy-MM-dd HH:mm:ss``, ``yyyy/MM/dd``,
+    ``M/d/yyyy`` or an ISO date-time, read in ``tz`` (UTC by default) unless the string carries an offset."""
+    import datetime as dt
+    from zoneinfo import ZoneInfo
+    zone = dt.timezone.utc if tz in ("UTC", "GMT+0", "GMT") else ZoneInfo(tz)
+    for f in _FORMATS:
+        try:
+            d = dt.datetime.strptime(date, f)
+            break
+        except ValueError:
+            continue
+    else:
+        s = date[:-1] + "+00:00" if date.endswith("Z") else date
+        try:
+            d = dt.datetime.fromisoformat(s)
+        except ValueError:
+            raise ValueError(f"Invalid format: \"{date}\"") from None
+    if d.tzinfo is None:
+        d = d.replace(tzinfo=zone)
+    return int(round(d.timestamp() * 1000))
+
+
+def parse_unix(ms: int) -> str:
+    """``DateTimeUtils.parseUnix``: the UTC ``yyyy/MM/dd`` of an epoch-ms timestamp."""
+    import datetime as dt
+    return dt.datetime.fromtimestamp(ms / 1000.0, dt.timezone.utc).strftime("%Y/%m/%d")
+
+
+def get_standard_days(start_ms: int, end_ms: int) -> int:
+    """``DateTimeUtils.getStandardDays``: whole days of ``end - start``, truncated toward zero."""
+    d = int(end_ms) - int(start_ms)
+    return d // MS_PER_DAY if d >= 0 else -((-d) // MS_PER_DAY)
+
+
+def get_range(start: str, end: str):
+    """``DateTimeUtils.getRange``: every ``yyyy/MM/dd`` from ``start`` to ``end`` inclusive."""
+    s = parse(start)
+    return [parse_unix(s + k * MS_PER_DAY) for k in range(get_standard_days(s, parse(end)) + 1)]
+
+
+def get_date_plus_days(start: str, days: int) -> str:
+    """``DateTimeUtils.getDatePlusDays``: ``start`` plus ``days`` calendar days, as ``yyyy/MM/dd``."""
+    return parse_unix(parse(start) + int(days) * MS_PER_DAY)
