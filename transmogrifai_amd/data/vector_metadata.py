@@ -37,6 +37,16 @@ class FeatureHistory:
     def from_json(d):
         return FeatureHistory(tuple(d.get("originFeatures", [])), tuple(d.get("stages", [])))
 
+    @staticmethod
+    def map_to_json(m: dict) -> dict:
+        """``FeatureHistory.toMetadata(map)`` (FeatureHistory.scala:81-91): one entry per feature name."""
+        return {k: v.to_json() for k, v in m.items()}
+
+    @staticmethod
+    def map_from_json(d: dict) -> dict:
+        """``FeatureHistory.fromMetadataMap`` (FeatureHistory.scala:93-102)."""
+        return {k: FeatureHistory.from_json(v) for k, v in d.items()}
+
 
 @lru_cache(maxsize=4096)
 def _has_subtype(type_names: tuple, t) -> bool:
