@@ -242,11 +242,39 @@ class TransientFeature:
         self.type_name = type_name
         self.origin_features = list(origin_features)
         self.stages = list(stages)
+        self._feature = None        # the live feature, never serialized (TransientFeature.scala:70)
 
     @staticmethod
     def of(f: FeatureLike) -> "TransientFeature":
         h = f.history()
-        return TransientFeature(f.name, f.uid, f.is_response, f.is_raw, f.type_name, h.origin_features, h.stages)
+        t = TransientFeature(f.name, f.uid, f.is_response, f.is_raw, f.type_name, h.origin_features, h.stages)
+        t._feature = f
+        return t
+
+    def get_feature(self) -> FeatureLike:
+        """The feature this was built from (``getFeature``, TransientFeature.scala:92-99); a deserialized or
+        field-built instance has none."""
+        if self._feature is None:
+            raise RuntimeError(f"TransientFeature[{self.name}]: feature is null, possibly because it was "
+                               "deserialized or built without a feature")
+        return self._feature
+
+    as_feature_like = get_feature
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d["_feature"] = None
+        return d
+
+    def __eq__(self, other):                                # TransientFeature.scala:187-200
+        if not isinstance(other, TransientFeature):
+            return NotImplemented
+        return (self.name, self.is_response, self.is_raw, self.uid, self.type_name, list(self.origin_features),
+                list(self.stages)) == (other.name, other.is_response, other.is_raw, other.uid, other.type_name,
+                                       list(other.origin_features), list(other.stages))
+
+    def __hash__(self):
+        return hash(self.uid)
 
     def to_json(self):
         return {"name": self.name, "isResponse": self.is_response, "isRaw": self.is_raw, "uid": self.uid,

@@ -265,7 +265,21 @@ def gpu_csv_dataset(path: str, raw_features: Sequence, dev, names: Optional[Sequ
         prof["finish"] = time.perf_counter() - t_fin
         prof["total"] = time.perf_counter() - t_start
         sys.stderr.write("[gpu-csv] " + " ".join(f"{a}={b:.3f}" for a, b in prof.items()) + f" rows={n} chunks={i}\n")
-    return Dataset(OrderedDict((f.name, out[f.name]) for f in raw_features), None, n)
+    return Dataset(OrderedDict((f.name, out[f.name]) for f in raw_features), _key_column(path, names, has_header,
+                                                                                        separator, n), n)
+
+
+def _key_column(path: str, names: Sequence[str], has_header: bool, separator: str, n: int):
+    """The file's ``key`` column as strings (the columnar / pandas paths' record keys), or None without one."""
+    if "key" not in names:
+        return None
+    import pyarrow as pa
+    import pyarrow.csv as pcsv
+    tab = pcsv.read_csv(path, read_options=pcsv.ReadOptions(column_names=list(names), skip_rows=1 if has_header else 0),
+                        parse_options=pcsv.ParseOptions(delimiter=separator),
+                        convert_options=pcsv.ConvertOptions(include_columns=["key"], column_types={"key": pa.string()}))
+    key = tab.column("key").to_pandas().astype(str).to_numpy(dtype=object)
+    return key if len(key) == n else None
 
 
 def _check_pending(pending, N, prof) -> bool:
